@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""bench.py — residuals+Jacobians/sec of the semantic-BA hot path on MI355X.
+
+A step is one full linearization of the BASELINE.json workload already
+resident in HBM: every reprojection residual block (residual + tangent
+Jacobian, loss-corrected, point blocks V_p/g_p reduced) and every semantic
+sample (residual + 29-point CENTRAL numeric-diff Jacobian, pair blocks
+reduced) — mi_ba_linearize on the context's stream.
+
+value = (reprojection blocks + semantic samples, all ranks) * steps / max-over-
+ranks wall time of the timed steps.  Multi-GPU: points (and image pairs) are
+sharded in contiguous ranges across ranks; the linearization has no
+data-path collective, so the timed region needs none (strong scaling of the
+fixed C5 problem).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C4]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "semantic-bundle-adjustment-colmap_amd")
+sys.path.insert(0, PKG)
+import mi_ba  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+
+OPENCV_EXTRA = (-0.1, 0.01, 1e-4, -1e-4)
+CONFIGS = {
+    "C2": dict(model=mi_ba.SIMPLE_RADIAL, images=200, points=50_000, track=10, extra=(0.05, 0, 0, 0),
+               semantic=None, desc="200 cams / 50k points / 500k obs, SIMPLE_RADIAL, geometric"),
+    "C3": dict(model=mi_ba.SIMPLE_RADIAL, images=200, points=50_000, track=10, extra=(0.05, 0, 0, 0),
+               semantic=dict(step=10, pairs_per_image=2, size=1000),
+               desc="200 cams / 50k points / 500k obs, SIMPLE_RADIAL, geometric + semantic (4.0M samples)"),
+    "C4": dict(model=mi_ba.OPENCV, images=1000, points=1_000_000, track=10, extra=OPENCV_EXTRA,
+               semantic=dict(step=20, pairs_per_image=2, size=1000),
+               desc="1k cams / 1M points / 10M obs, OPENCV, semantic BA (5.0M samples)"),
+}
+# Algorithmic bytes per reprojection block: 24 (obs) + 24/L
+# (point) + 16 (residual) + 16*(9+c) (tangent Jacobian), c = refined intrinsics
+# with the default refine flags: SIMPLE_RADIAL 2, OPENCV 6.
+CAM_TANGENT = {mi_ba.SIMPLE_PINHOLE: 1, mi_ba.PINHOLE: 2, mi_ba.SIMPLE_RADIAL: 2, mi_ba.RADIAL: 3, mi_ba.OPENCV: 6}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def bytes_per_block(model, track):
+    return 24 + 24.0 / track + 16 + 16 * (9 + CAM_TANGENT[model])
+
+
+def build_shard(cfg, rank, world):
+    """Generate the scene (deterministic, seed 0) and keep this rank's shard."""
+    c = mi_ba.synth_config(cfg["model"], cfg["images"], cfg["points"], track_length=cfg["track"],
+                           rotation_range=0.05, extra=cfg["extra"])
+    full = mi_ba.generate_scene(c).gauge()
+    P = full.num_points
+    p0, p1 = P * rank // world, P * (rank + 1) // world
+    m = (full.obs_point >= p0) & (full.obs_point < p1)
+    sc = full
+    if world > 1:
+        sc.obs_xy, sc.obs_image, sc.obs_point = full.obs_xy[m], full.obs_image[m], full.obs_point[m]
+    sem = None
+    if cfg["semantic"]:
+        s = cfg["semantic"]
+        I = cfg["images"]
+        pairs = np.array([(i, (i + d) % I) for i in range(I) for d in range(1, s["pairs_per_image"] + 1)], np.int32)
+        K = len(pairs)
+        pairs = pairs[K * rank // world:K * (rank + 1) // world]
+        H = W = s["size"]
+        need = np.unique(pairs.reshape(-1))
+        depth = np.zeros((I, H, W), np.float32)
+        label = np.zeros((I, H, W), np.float32)
+        sub = mi_ba.Scene(sc.camera_model, sc.camera_params, sc.qvec[need], sc.tvec[need], sc.image_camera[need],
+                          sc.xyz[:1], sc.obs_xy[:0], sc.obs_image[:0], sc.obs_point[:0])
+        d_sub, l_sub = mi_ba.render_semantic(sub, H, W, plane_z=1.0, cell=0.1)
+        depth[need] = d_sub
+        label[need] = l_sub
+        del d_sub, l_sub
+        sem = mi_ba.SemanticInput(depth, label, pairs, pixel_step=s["step"])
+    return sc, sem
+
+
+def cpu_baseline(opts, sc, sem, cfg, nb, ns):
+    """The CPU restatement (oracle, 'port') timed on this host on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = min(threads, 16)
+    geo_blocks = min(nb, 4_000_000)
+    t_geo, done_geo = oracle.reproj_throughput(opts, sc, geo_blocks, 1, threads)
+    rate_geo = done_geo / t_geo
+    sample = f"{done_geo} reprojection blocks"
+    total_time = nb / rate_geo
+    rate_sem = None
+    if sem is not None and ns:
+        t_sem, done_sem = oracle.semantic_throughput(opts, sc, sem, min(ns, 400_000), threads)
+        rate_sem = done_sem / t_sem
+        total_time += ns / rate_sem
+        sample += f" + {done_sem} semantic samples"
+    return {"value": (nb + ns) / total_time, "unit": "residual_blocks/s", "cores": threads, "kind": "port",
+            "sample": sample + " of the same workload, oracle/ CPU restatement (C++/OpenMP, f64), not Ceres",
+            "reproj_blocks_per_s": rate_geo, "semantic_samples_per_s": rate_sem}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C4", choices=sorted(CONFIGS))
+    ap.add_argument("--lm-iters", type=int, default=3, help="LM iterations for the BA-iteration wall time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def allreduce_max(v):
+        if dist is None:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allreduce_sum(v):
+        if dist is None:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    cfg = CONFIGS[args.config]
+    t_setup = time.time()
+    sc, sem = build_shard(cfg, rank, world)
+    opts = mi_ba.default_options(device=local_rank)
+    ctx = mi_ba.Context(opts, sc, sem)
+    nb, W, ns = ctx.dims()
+    setup_s = time.time() - t_setup
+
+    for _ in range(args.warmup):
+        ctx.linearize()
+    ctx.synchronize()
+    ctx.set_timing(True)
+    ctx.reset_kernel_times()
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.linearize()
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    dt = allreduce_max(t1 - t0)
+    j_ms, j_n = ctx.kernel_time("reproj_jacobian")
+    s_ms, s_n = ctx.kernel_time("semantic_jacobian")
+    ctx.set_timing(False)
+    total_blocks = allreduce_sum(float(nb + ns))
+    value = total_blocks * args.steps / dt
+
+    # BA-iteration wall time: a few LM iterations on the same resident context
+    lm = None
+    if args.lm_iters > 0:
+        ctx.options.max_num_iterations = args.lm_iters
+        ctx_lm = mi_ba.Context(mi_ba.default_options(device=local_rank, max_num_iterations=args.lm_iters), sc, sem)
+        s = ctx_lm.solve()
+        its = max(1, s.num_successful_steps + s.num_unsuccessful_steps)
+        lm = {"ba_iteration_ms": 1e3 * s.total_time_in_seconds / its, "iterations": its,
+              "linear_solver_iterations": s.num_linear_solver_iterations,
+              "initial_cost": s.initial_cost, "final_cost": s.final_cost}
+        ctx_lm.close()
+
+    if rank == 0:
+        avg_j = j_ms / max(1, j_n)
+        bpb = bytes_per_block(cfg["model"], cfg["track"])
+        achieved = bpb * nb / (avg_j * 1e-3) / 1e9 if avg_j > 0 else 0.0
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "residual_blocks/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * dt / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong" if world > 1 else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (GenerateReconstruction restated, seed 0; rendered labelled plane)",
+            "config": {"workload": f"{args.config}: {cfg['desc']}", "cameras": cfg["images"],
+                       "points": cfg["points"], "observations": cfg["points"] * cfg["track"],
+                       "reprojection_blocks_rank0": nb, "semantic_samples_rank0": ns,
+                       "camera_model": [k for k, v in mi_ba.MODEL_NAMES.items() if v == cfg["model"]][0],
+                       "parallelism": f"point-sharded x{world}"},
+            "roofline": {"kernel": "reproj_jacobian", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_block": bpb, "blocks_per_launch": nb, "avg_launch_ms": avg_j},
+            "kernels_ms": {"reproj_jacobian": avg_j, "semantic_jacobian": s_ms / max(1, s_n)},
+            "reproj_blocks_per_s": nb * world / (avg_j * 1e-3) if avg_j > 0 else None,
+            "setup_s": setup_s,
+        }
+        if lm:
+            out.update(lm)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(opts, sc, sem, cfg, nb, ns)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,264 @@
+/*
+ * mi_ba.h — C-ABI drop-in boundary of the MI355X-native semantic bundle
+ * adjustment hot path.
+ *
+ * Every entry point here replaces one piece of the reference's C++ interface
+ * (AlainSchoebi/semantic-bundle-adjustment-colmap, a COLMAP 3.8 fork):
+ *
+ *   mi_ba_default_options      <- BundleAdjustmentOptions::BundleAdjustmentOptions()
+ *                                 src/optim/bundle_adjustment.h:49-92
+ *   mi_ba_problem (struct)     <- Reconstruction (cameras/images/points3D/tracks)
+ *                                 + BundleAdjustmentConfig (bundle_adjustment.h:103-167)
+ *                                 flattened the way ParallelBundleAdjuster::SetUp does
+ *                                 (src/optim/bundle_adjustment.cc:665-783)
+ *   mi_ba_setup_stats          <- BundleAdjuster::SetUp + Ceres reduced-program counts
+ *                                 (bundle_adjustment.cc:326-530; summary fields read by
+ *                                 src/optim/bundle_adjustment_test.cc:186-642)
+ *   mi_ba_solve                <- BundleAdjuster::Solve(Reconstruction*) + Summary()
+ *                                 (bundle_adjustment.h:171-203, bundle_adjustment.cc:258-320)
+ *   mi_ba_context_* / mi_ba_linearize / mi_ba_download_*
+ *                              <- the Ceres residual+Jacobian evaluation of every
+ *                                 BundleAdjustmentCostFunction /
+ *                                 BundleAdjustmentConstantPoseCostFunction block
+ *                                 (src/base/cost_functions.h:44-152) and of every
+ *                                 {,ConstantFirstPose,ConstantSecondPose}SemanticBACostFunction
+ *                                 block (src/base/semantic_cost_functions.h:87-404),
+ *                                 reduced into Schur normal equations (Ceres 2.1
+ *                                 SchurEliminator, 3rd party, not vendored)
+ *   mi_ba_semantic (struct)    <- SemanticBundleAdjustmentOptions depth/semantic maps
+ *                                 (src/optim/semantic_bundle_adjustment.h:53-140,
+ *                                 semantic_bundle_adjustment.cc:699-906,1021-1068)
+ *
+ * Conventions: caller owns every host array; arrays marked (in/out) are
+ * updated in place by mi_ba_solve exactly where Ceres would mutate the
+ * Reconstruction through its registered double* parameter blocks
+ * (bundle_adjustment.cc:357-359,393,408-410).  Errors are returned as
+ * mi_ba_status codes (the reference aborts through glog CHECK or throws).
+ * Device buffers are library-owned.  One context per host thread.
+ * All arithmetic is IEEE f64.
+ */
+#ifndef MI_BA_H_
+#define MI_BA_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MI_BA_ABI_VERSION 1
+
+typedef enum mi_ba_status {
+  MI_BA_OK = 0,
+  MI_BA_ERR_INVALID_ARGUMENT = 1, /* reference: glog CHECK abort (bundle_adjustment.cc:165-186,304) */
+  MI_BA_ERR_NO_DEVICE = 2,        /* no MI355X visible: the product never falls back to the CPU */
+  MI_BA_ERR_UNSUPPORTED = 3,      /* reference: std::domain_error / std::runtime_error */
+  MI_BA_ERR_HIP = 4,              /* HIP runtime error */
+  MI_BA_ERR_NO_RESIDUALS = 5,     /* reference: Solve() returns false (bundle_adjustment.cc:267-269) */
+  MI_BA_ERR_STATE = 6,            /* reference: "Cannot use the same BundleAdjuster multiple times" */
+  MI_BA_ERR_OUT_OF_MEMORY = 7
+} mi_ba_status;
+
+/* COLMAP camera model ids (src/base/camera_models.h kModelId). */
+enum {
+  MI_BA_SIMPLE_PINHOLE = 0,
+  MI_BA_PINHOLE = 1,
+  MI_BA_SIMPLE_RADIAL = 2,
+  MI_BA_RADIAL = 3,
+  MI_BA_OPENCV = 4
+};
+
+/* BundleAdjustmentOptions::LossFunctionType (bundle_adjustment.h:51). */
+enum { MI_BA_LOSS_TRIVIAL = 0, MI_BA_LOSS_SOFT_L1 = 1, MI_BA_LOSS_CAUCHY = 2 };
+
+/* Linear solver selection; AUTO reproduces the heuristic of
+ * bundle_adjustment.cc:276-286 (<=50 images dense Schur, else iterative). */
+enum {
+  MI_BA_SOLVER_AUTO = 0,
+  MI_BA_SOLVER_DENSE_SCHUR = 1,
+  MI_BA_SOLVER_ITERATIVE_SCHUR = 2
+};
+
+/* ceres::TerminationType, same numeric order as Ceres 2.1. */
+enum {
+  MI_BA_CONVERGENCE = 0,
+  MI_BA_NO_CONVERGENCE = 1,
+  MI_BA_FAILURE = 2,
+  MI_BA_USER_SUCCESS = 3,
+  MI_BA_USER_FAILURE = 4
+};
+
+/* Semantic sample status (ReprojectionStatus, semantic_cost_functions.h:45). */
+enum { MI_BA_OUT_OF_BOUNDS = -1, MI_BA_INVALID_DEPTH = -2, MI_BA_VALID = 10 };
+
+typedef struct mi_ba_options {
+  int32_t loss_function_type;       /* MI_BA_LOSS_*; default TRIVIAL */
+  double loss_function_scale;       /* default 1.0 */
+  int32_t refine_focal_length;      /* default 1 */
+  int32_t refine_principal_point;   /* default 0 */
+  int32_t refine_extra_params;      /* default 1 */
+  int32_t refine_extrinsics;        /* default 1 */
+  int32_t print_summary;            /* default 0 (library does not print unless asked) */
+  /* ceres::Solver::Options subset set by BundleAdjustmentOptions() */
+  int32_t max_num_iterations;       /* 100 */
+  double function_tolerance;        /* 0 */
+  double gradient_tolerance;        /* 0 */
+  double parameter_tolerance;       /* 0 */
+  int32_t max_linear_solver_iterations;      /* 200 */
+  int32_t max_num_consecutive_invalid_steps; /* 10 */
+  int32_t linear_solver_type;       /* MI_BA_SOLVER_AUTO */
+  double eta;                       /* inexact-Newton forcing, Ceres default 0.1 */
+  double initial_trust_region_radius; /* Ceres default 1e4 */
+  double min_relative_decrease;     /* Ceres default 1e-3 */
+  /* build additions */
+  int32_t device;                   /* HIP device ordinal, default 0 */
+  double semantic_weight;           /* ScaledLoss weight of semantic blocks, default 1 */
+} mi_ba_options;
+
+/* Flattened Reconstruction + BundleAdjustmentConfig.  A single camera model
+ * per problem.  Indices are 0-based positions in these arrays. */
+typedef struct mi_ba_problem {
+  int32_t camera_model;              /* MI_BA_* model id */
+  int32_t num_cameras;
+  double* camera_params;             /* (in/out) [num_cameras][num_params(model)] */
+  const uint8_t* camera_constant;    /* nullable; 1 = config.SetConstantCamera */
+
+  int32_t num_images;
+  double* qvec;                      /* (in/out) [num_images][4] (w,x,y,z), world->camera */
+  double* tvec;                      /* (in/out) [num_images][3] */
+  const int32_t* image_camera;       /* [num_images] camera index */
+  const uint8_t* image_in_config;    /* nullable (= all); 1 = config.AddImage */
+  const uint8_t* image_constant_pose;/* nullable; 1 = config.SetConstantPose */
+  const uint8_t* image_constant_tvec;/* nullable; bit k = tvec[k] constant (config.SetConstantTvec) */
+
+  int64_t num_points;
+  double* xyz;                       /* (in/out) [num_points][3] */
+  const uint8_t* point_config;       /* nullable; 1 = AddVariablePoint, 2 = AddConstantPoint */
+
+  int64_t num_obs;                   /* all track elements of the reconstruction */
+  const double* obs_xy;              /* [num_obs][2] Point2D::XY() */
+  const int32_t* obs_image;          /* [num_obs] */
+  const int32_t* obs_point;          /* [num_obs] */
+} mi_ba_problem;
+
+/* Semantic term (SBA).  Rasters are row-major [image][H][W] float32, i.e. the
+ * Eigen::MatrixXf (row=y, col=x) of matrixFromTiff after its vertical flip
+ * (matrix_vis.h:130-176); every image shares H and W. */
+typedef struct mi_ba_semantic {
+  int32_t height;
+  int32_t width;
+  const float* depth;                /* [num_images][H][W] */
+  const float* label;                /* [num_images][H][W] */
+  int32_t num_pairs;                 /* ordered pairs (i, j); reference uses all i != j */
+  const int32_t* pairs;              /* [num_pairs][2] */
+  int32_t pixel_step;                /* error_computation_pixel_step, default 10 */
+  double depth_error_threshold;      /* default 2 */
+  double numeric_relative_step_size; /* default 1e-3 */
+} mi_ba_semantic;
+
+/* Mirrors the ceres::Solver::Summary fields COLMAP reads
+ * (PrintSolverSummary, bundle_adjustment.cc:1142-1196). */
+typedef struct mi_ba_summary {
+  int64_t num_residuals_reduced;
+  int64_t num_effective_parameters_reduced;
+  int32_t num_successful_steps;
+  int32_t num_unsuccessful_steps;
+  int32_t termination_type;
+  double initial_cost;
+  double final_cost;
+  double fixed_cost;
+  double total_time_in_seconds;
+  double jacobian_evaluation_time_in_seconds;
+  int32_t num_jacobian_evaluations;
+  int32_t num_linear_solver_iterations;
+  int64_t num_semantic_residuals;
+} mi_ba_summary;
+
+/* Structural counts produced by problem assembly (no device needed). */
+typedef struct mi_ba_setup_info {
+  int64_t num_residual_blocks;          /* geometric blocks in the program */
+  int64_t num_residuals_reduced;        /* after dropping all-constant blocks */
+  int64_t num_effective_parameters_reduced;
+  int64_t num_variable_images;
+  int64_t num_variable_cameras;
+  int64_t num_variable_points;
+  int32_t camera_tangent_size;          /* refined intrinsics per camera */
+} mi_ba_setup_info;
+
+typedef struct mi_ba_context mi_ba_context;
+
+/* --- version / device --------------------------------------------------- */
+int32_t mi_ba_abi_version(void);
+const char* mi_ba_status_string(int32_t status);
+int32_t mi_ba_num_params(int32_t camera_model); /* -1 if unknown */
+mi_ba_status mi_ba_device_count(int32_t* count);
+
+/* --- options ------------------------------------------------------------ */
+void mi_ba_default_options(mi_ba_options* options);
+
+/* --- problem assembly (host only) -------------------------------------- */
+mi_ba_status mi_ba_setup_stats(const mi_ba_options* options,
+                               const mi_ba_problem* problem,
+                               mi_ba_setup_info* info);
+
+/* --- one-shot solve: BundleAdjuster::Solve ------------------------------ */
+mi_ba_status mi_ba_solve(const mi_ba_options* options, mi_ba_problem* problem,
+                         const mi_ba_semantic* semantic /* nullable */,
+                         mi_ba_summary* summary);
+
+/* --- resident context (device-resident problem, for throughput/parity) - */
+mi_ba_status mi_ba_context_create(const mi_ba_options* options,
+                                  const mi_ba_problem* problem,
+                                  const mi_ba_semantic* semantic /* nullable */,
+                                  mi_ba_context** ctx);
+void mi_ba_context_destroy(mi_ba_context* ctx);
+
+/* Residual + Jacobian evaluation of every block at the current parameters,
+ * reduced into the Schur normal-equation blocks.  Asynchronous on the
+ * context's stream; call mi_ba_synchronize before reading results. */
+mi_ba_status mi_ba_linearize(mi_ba_context* ctx);
+/* Residual+Jacobian kernel alone (the J-materialising evaluation). */
+mi_ba_status mi_ba_evaluate_jacobian(mi_ba_context* ctx);
+/* Semantic residual+Jacobian kernel alone. */
+mi_ba_status mi_ba_evaluate_semantic(mi_ba_context* ctx);
+mi_ba_status mi_ba_synchronize(mi_ba_context* ctx);
+
+/* Number of geometric residual blocks in the context (rows of the download
+ * arrays below) and the per-block Jacobian width 9 + camera_tangent_size. */
+mi_ba_status mi_ba_context_dims(const mi_ba_context* ctx, int64_t* num_blocks,
+                                int32_t* jacobian_cols, int64_t* num_samples);
+/* Blocks are in the library's point-major order; block_obs[k] = index of
+ * the problem observation evaluated by block k.  Layout:
+ *   residuals [num_blocks][2]
+ *   jacobian  [num_blocks][2][9+c] columns: rot(3 tangent) trans(3) point(3)
+ *             cam(c refined intrinsics); columns of constant parameter blocks
+ *             and constant tvec coordinates are zero. */
+mi_ba_status mi_ba_download_jacobian(mi_ba_context* ctx, int64_t* block_obs,
+                                     double* residuals, double* jacobian);
+/* Semantic samples, ordered by pair then (y, x):
+ *   sample_pixel [n][3] (pair index, x1, y1); status [n]; residual [n];
+ *   jacobian [n][12] = pose1 (rot3, trans3), pose2 (rot3, trans3). */
+mi_ba_status mi_ba_download_semantic(mi_ba_context* ctx, int32_t* sample_pixel,
+                                     int32_t* status, double* residuals,
+                                     double* jacobian);
+/* LM solve on a resident context (single use, like BundleAdjuster::Solve);
+ * parameters stay on the device until mi_ba_context_writeback. */
+mi_ba_status mi_ba_context_solve(mi_ba_context* ctx, mi_ba_summary* summary);
+/* Copy the refined parameters back into the caller's problem arrays. */
+mi_ba_status mi_ba_context_writeback(mi_ba_context* ctx);
+/* Total cost 0.5*sum(rho) at the current parameters (geometric + semantic). */
+mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost);
+
+/* Per-kernel HIP-event timing on the context's stream (enabled with
+ * mi_ba_set_timing).  name: "reproj_jacobian", "semantic_jacobian", ... */
+mi_ba_status mi_ba_set_timing(mi_ba_context* ctx, int32_t enabled);
+mi_ba_status mi_ba_kernel_time(mi_ba_context* ctx, const char* name,
+                               double* total_ms, int64_t* launches);
+mi_ba_status mi_ba_reset_kernel_times(mi_ba_context* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MI_BA_H_ */

@@ -1,0 +1,1010 @@
+// oracle.cc — TEST INFRASTRUCTURE ONLY (the checker, never the product).
+//
+// CPU restatement of the reference hot path, exported as a C ABI for ctypes.
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load
+// liboracle.so.  Every function cites the reference file:line it restates
+// (AlainSchoebi/semantic-bundle-adjustment-colmap, COLMAP 3.8 fork; Ceres 2.1
+// is a third-party dependency that the reference does not vendor — its
+// algorithms are restated from its published behaviour and marked so).
+//
+// Pinning: the known answers of src/base/cost_functions_test.cc:41-99,
+// src/base/projection_test.cc:95-124, src/base/camera_models_test.cc:39-218
+// and the structural counts of src/optim/bundle_adjustment_test.cc:186-642
+// are asserted against this oracle in tests/test_oracle_golden.py.
+// The semantic path has no reference tests or data: "parity unpinned" for
+// that oracle beyond self-consistency.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <ctime>
+#include <map>
+#include <set>
+#include <vector>
+
+#include "../include/mi_ba.h"
+#include "oracle_math.h"
+
+using namespace oracle;
+
+namespace {
+
+constexpr int kJ = 18;  // 4 (q) + 3 (t) + 3 (X) + 8 (max camera params)
+typedef Jet<kJ> J18;
+
+// cost_functions.h:57-81 (BundleAdjustmentCostFunction::operator()) and
+// :116-142 (BundleAdjustmentConstantPoseCostFunction::operator()).
+template <typename T>
+void ReprojResidual(int model, const T q[4], const T t[3], const T X[3], const T* cam,
+                    double ox, double oy, T r[2]) {
+  T projection[3];
+  UnitQuaternionRotatePoint(q, X, projection);
+  projection[0] += t[0];
+  projection[1] += t[1];
+  projection[2] += t[2];
+  projection[0] /= projection[2];
+  projection[1] /= projection[2];
+  WorldToImage(model, cam, projection[0], projection[1], &r[0], &r[1]);
+  r[0] -= T(ox);
+  r[1] -= T(oy);
+}
+
+// Ceres 2.1 loss functions (restated): rho[0..2] at s = |r|^2.
+void LossEvaluate(int type, double scale, double s, double rho[3]) {
+  if (type == MI_BA_LOSS_SOFT_L1) {
+    const double b = scale * scale, c = 1.0 / b;
+    const double sum = 1.0 + s * c;
+    const double tmp = std::sqrt(sum);
+    rho[0] = 2.0 * b * (tmp - 1.0);
+    rho[1] = std::max(std::numeric_limits<double>::min(), 1.0 / tmp);
+    rho[2] = -(c * rho[1]) / (2.0 * sum);
+  } else if (type == MI_BA_LOSS_CAUCHY) {
+    const double b = scale * scale, c = 1.0 / b;
+    const double sum = 1.0 + s * c;
+    const double inv = 1.0 / sum;
+    rho[0] = b * std::log(sum);
+    rho[1] = std::max(std::numeric_limits<double>::min(), inv);
+    rho[2] = -c * (inv * inv);
+  } else {
+    rho[0] = s; rho[1] = 1.0; rho[2] = 0.0;
+  }
+}
+
+// Ceres 2.1 Corrector (corrector.cc, restated): applied to residuals and
+// Jacobian rows of one block.  nres = residual count, ncols = columns.
+void ApplyCorrector(const double rho[3], double sq_norm, int nres, double* r, int ncols, double* J) {
+  const double sqrt_rho1 = std::sqrt(rho[1]);
+  double residual_scaling, alpha_sq_norm;
+  if (sq_norm == 0.0 || rho[2] <= 0.0) {
+    residual_scaling = sqrt_rho1;
+    alpha_sq_norm = 0.0;
+  } else {
+    const double D = 1.0 + 2.0 * sq_norm * rho[2] / rho[1];
+    const double alpha = 1.0 - std::sqrt(D);
+    residual_scaling = sqrt_rho1 / (1 - alpha);
+    alpha_sq_norm = alpha / sq_norm;
+  }
+  if (J) {
+    if (alpha_sq_norm == 0.0) {
+      for (int i = 0; i < nres * ncols; ++i) J[i] *= sqrt_rho1;
+    } else {
+      for (int c = 0; c < ncols; ++c) {
+        double rtJ = 0.0;
+        for (int k = 0; k < nres; ++k) rtJ += r[k] * J[k * ncols + c];
+        for (int k = 0; k < nres; ++k)
+          J[k * ncols + c] = sqrt_rho1 * (J[k * ncols + c] - alpha_sq_norm * r[k] * rtJ);
+      }
+    }
+  }
+  for (int k = 0; k < nres; ++k) r[k] *= residual_scaling;
+}
+
+// ---------------------------------------------------------------------------
+// Problem assembly: BundleAdjuster::SetUp / AddImageToProblem /
+// AddPointToProblem / ParameterizeCameras / ParameterizePoints
+// (src/optim/bundle_adjustment.cc:326-530) + Ceres reduced program.
+// ---------------------------------------------------------------------------
+struct Setup {
+  int np = 0;                          // camera params per camera
+  std::vector<int> cam_tangent;        // refined param indices (SubsetManifold)
+  std::vector<int64_t> block_obs;      // blocks in program order
+  std::vector<uint8_t> block_const_pose;
+  std::vector<double> block_pose;      // [nb][7] baked (q,t) for constant-pose blocks
+  std::vector<uint8_t> block_reduced;  // has >= 1 variable parameter block
+  std::vector<uint8_t> img_var;        // pose is a variable parameter block
+  std::vector<uint8_t> img_tvec_mask;  // constant tvec coords (bitmask)
+  std::vector<uint8_t> cam_var;        // camera block variable with tangent > 0
+  std::vector<uint8_t> pt_var;
+  int64_t num_residuals_reduced = 0;
+  int64_t num_effective_parameters_reduced = 0;
+};
+
+int BuildSetup(const mi_ba_options* o, mi_ba_problem* p, Setup* s) {
+  const int np = NumParams(p->camera_model);
+  if (np < 0) return MI_BA_ERR_UNSUPPORTED;
+  s->np = np;
+  const int I = p->num_images, C = p->num_cameras;
+  const int64_t P = p->num_points, N = p->num_obs;
+  auto in_cfg = [&](int i) { return p->image_in_config ? p->image_in_config[i] != 0 : true; };
+  auto const_pose_cfg = [&](int i) { return p->image_constant_pose && p->image_constant_pose[i]; };
+  auto tvec_mask = [&](int i) { return p->image_constant_tvec ? p->image_constant_tvec[i] : 0; };
+  std::vector<std::vector<int64_t>> obs_of_img(I), obs_of_pt(P);
+  for (int64_t k = 0; k < N; ++k) {
+    obs_of_img[p->obs_image[k]].push_back(k);
+    obs_of_pt[p->obs_point[k]].push_back(k);
+  }
+  std::set<int> cam_ids;
+  std::vector<uint8_t> cam_const_cfg(C, 0);
+  for (int c = 0; c < C; ++c) cam_const_cfg[c] = p->camera_constant ? p->camera_constant[c] : 0;
+  std::map<int64_t, int64_t> pt_nobs;
+  s->img_var.assign(I, 0);
+  s->img_tvec_mask.assign(I, 0);
+  auto add_block = [&](int64_t k, bool cpose, int img) {
+    s->block_obs.push_back(k);
+    s->block_const_pose.push_back(cpose ? 1 : 0);
+    for (int j = 0; j < 4; ++j) s->block_pose.push_back(p->qvec[img * 4 + j]);
+    for (int j = 0; j < 3; ++j) s->block_pose.push_back(p->tvec[img * 3 + j]);
+  };
+  // AddImageToProblem (:348-427)
+  for (int i = 0; i < I; ++i) {
+    if (!in_cfg(i)) continue;
+    // Image::NormalizeQvec -> NormalizeQuaternion (pose.cc:82-91)
+    double* q = &p->qvec[i * 4];
+    const double norm = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    if (norm == 0) { q[0] = 1.0; }
+    else { for (int j = 0; j < 4; ++j) q[j] = q[j] / norm; }
+    const bool cpose = !o->refine_extrinsics || const_pose_cfg(i);
+    int64_t nobs = 0;
+    for (int64_t k : obs_of_img[i]) {
+      nobs += 1;
+      pt_nobs[p->obs_point[k]] += 1;
+      add_block(k, cpose, i);
+    }
+    if (nobs > 0) {
+      cam_ids.insert(p->image_camera[i]);
+      if (!cpose) {
+        s->img_var[i] = 1;
+        s->img_tvec_mask[i] = tvec_mask(i);
+      }
+    }
+  }
+  // AddPointToProblem (:429-478): variable points first, then constant.
+  for (int pass = 1; pass <= 2; ++pass) {
+    for (int64_t pt = 0; pt < P; ++pt) {
+      if (!p->point_config || p->point_config[pt] != pass) continue;
+      const int64_t track_len = (int64_t)obs_of_pt[pt].size();
+      if (pt_nobs[pt] == track_len) continue;
+      for (int64_t k : obs_of_pt[pt]) {
+        const int img = p->obs_image[k];
+        if (in_cfg(img)) continue;
+        pt_nobs[pt] += 1;
+        const int cam = p->image_camera[img];
+        if (!cam_ids.count(cam)) { cam_ids.insert(cam); cam_const_cfg[cam] = 1; }
+        add_block(k, true, img);
+      }
+    }
+  }
+  // ParameterizeCameras (:480-516)
+  int f[2], nf, pp[2], npp, ex[4], nex;
+  ParamGroups(p->camera_model, f, &nf, pp, &npp, ex, &nex);
+  std::vector<int> const_idx;
+  if (!o->refine_focal_length) const_idx.insert(const_idx.end(), f, f + nf);
+  if (!o->refine_principal_point) const_idx.insert(const_idx.end(), pp, pp + npp);
+  if (!o->refine_extra_params) const_idx.insert(const_idx.end(), ex, ex + nex);
+  for (int k = 0; k < np; ++k)
+    if (std::find(const_idx.begin(), const_idx.end(), k) == const_idx.end()) s->cam_tangent.push_back(k);
+  const bool constant_camera = !o->refine_focal_length && !o->refine_principal_point && !o->refine_extra_params;
+  s->cam_var.assign(C, 0);
+  for (int cam : cam_ids) {
+    if (constant_camera || cam_const_cfg[cam]) continue;
+    // Ceres: a SubsetManifold with tangent size 0 makes the block constant.
+    if (!s->cam_tangent.empty()) s->cam_var[cam] = 1;
+  }
+  // ParameterizePoints (:518-530)
+  s->pt_var.assign(P, 0);
+  for (auto& e : pt_nobs) {
+    const int64_t pt = e.first;
+    bool constant = (int64_t)obs_of_pt[pt].size() > e.second;
+    if (p->point_config && p->point_config[pt] == 2) constant = true;
+    s->pt_var[pt] = constant ? 0 : 1;
+  }
+  // Ceres reduced program: drop residual blocks whose parameter blocks are
+  // all constant, then parameter blocks no longer referenced.
+  const int64_t nb = (int64_t)s->block_obs.size();
+  s->block_reduced.assign(nb, 0);
+  std::vector<uint8_t> used_img(I, 0), used_cam(C, 0), used_pt(P, 0);
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t k = s->block_obs[b];
+    const int img = p->obs_image[k];
+    const int cam = p->image_camera[img];
+    const int64_t pt = p->obs_point[k];
+    const bool vpose = !s->block_const_pose[b] && s->img_var[img];
+    const bool any = vpose || s->cam_var[cam] || s->pt_var[pt];
+    if (!any) continue;
+    s->block_reduced[b] = 1;
+    s->num_residuals_reduced += 2;
+    if (vpose) used_img[img] = 1;
+    if (s->cam_var[cam]) used_cam[cam] = 1;
+    if (s->pt_var[pt]) used_pt[pt] = 1;
+  }
+  int64_t ne = 0;
+  for (int i = 0; i < I; ++i)
+    if (used_img[i]) {
+      int masked = 0;
+      for (int k = 0; k < 3; ++k) masked += (s->img_tvec_mask[i] >> k) & 1;
+      ne += 3 + (3 - masked);
+    }
+  for (int c = 0; c < C; ++c)
+    if (used_cam[c]) ne += (int64_t)s->cam_tangent.size();
+  for (int64_t pt = 0; pt < P; ++pt)
+    if (used_pt[pt]) ne += 3;
+  s->num_effective_parameters_reduced = ne;
+  return MI_BA_OK;
+}
+
+// Evaluate one geometric block: residual (2) and tangent Jacobian row-major
+// [2][9+c] with column order rot(3) trans(3) point(3) cam(c), via Jets.
+void EvalBlock(const Setup& s, const mi_ba_problem* p, int64_t b, double r[2], double* Jt) {
+  const int64_t k = s.block_obs[b];
+  const int img = p->obs_image[k];
+  const int cam = p->image_camera[img];
+  const int64_t pt = p->obs_point[k];
+  const int np = s.np;
+  const bool cpose = s.block_const_pose[b] != 0;
+  const double* qv = cpose ? &s.block_pose[b * 7] : &p->qvec[img * 4];
+  const double* tv = cpose ? &s.block_pose[b * 7 + 4] : &p->tvec[img * 3];
+  J18 q[4], t[3], X[3], params[8], res[2];
+  for (int j = 0; j < 4; ++j) q[j] = cpose ? J18(qv[j]) : J18(qv[j], j);
+  for (int j = 0; j < 3; ++j) t[j] = cpose ? J18(tv[j]) : J18(tv[j], 4 + j);
+  for (int j = 0; j < 3; ++j) X[j] = J18(p->xyz[pt * 3 + j], 7 + j);
+  for (int j = 0; j < np; ++j) params[j] = J18(p->camera_params[(int64_t)cam * np + j], 10 + j);
+  ReprojResidual(p->camera_model, q, t, X, params, p->obs_xy[k * 2], p->obs_xy[k * 2 + 1], res);
+  r[0] = res[0].a;
+  r[1] = res[1].a;
+  if (!Jt) return;
+  const int c = (int)s.cam_tangent.size();
+  const int w = 9 + c;
+  double PJ[12];
+  QuaternionPlusJacobian(qv, PJ);
+  const bool vpose = !cpose && s.img_var[img];
+  for (int row = 0; row < 2; ++row) {
+    double* Jr = Jt + row * w;
+    const double* d = res[row].v;
+    for (int col = 0; col < 3; ++col) {
+      double acc = 0.0;
+      for (int m = 0; m < 4; ++m) acc += d[m] * PJ[m * 3 + col];
+      Jr[col] = vpose ? acc : 0.0;
+    }
+    for (int col = 0; col < 3; ++col) {
+      const bool masked = (s.img_tvec_mask[img] >> col) & 1;
+      Jr[3 + col] = (vpose && !masked) ? d[4 + col] : 0.0;
+    }
+    for (int col = 0; col < 3; ++col) Jr[6 + col] = s.pt_var[pt] ? d[7 + col] : 0.0;
+    for (int col = 0; col < c; ++col) Jr[9 + col] = s.cam_var[cam] ? d[10 + s.cam_tangent[col]] : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Semantic residual: BaseSemanticBACostFunction::compute_semantic_error
+// (src/base/semantic_cost_functions.h:87-208), with P_c1 precomputed
+// (:103-118; pose-independent, so evaluating it once is bitwise identical).
+// ---------------------------------------------------------------------------
+struct SemSample {
+  int32_t pair, x, y;
+  double pc1[3];
+  float label1;
+};
+
+struct SemSetup {
+  std::vector<SemSample> samples;
+  std::vector<uint8_t> pair_var1, pair_var2;  // pose i / pose j variable
+};
+
+// semantic_bundle_adjustment.cc:699-906 (AddImagePairToProblem): pixel grid
+// y outer, x inner, step s, skip depth < 1e-4, skip both-constant pairs.
+void BuildSemSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& s,
+                   const mi_ba_semantic* sem, SemSetup* ss) {
+  const int H = sem->height, W = sem->width, step = sem->pixel_step;
+  const int np = NumParams(p->camera_model);
+  ss->pair_var1.assign(sem->num_pairs, 0);
+  ss->pair_var2.assign(sem->num_pairs, 0);
+  for (int k = 0; k < sem->num_pairs; ++k) {
+    const int i = sem->pairs[2 * k], j = sem->pairs[2 * k + 1];
+    if (i == j) continue;
+    const bool c1 = !o->refine_extrinsics || (p->image_constant_pose && p->image_constant_pose[i]);
+    const bool c2 = !o->refine_extrinsics || (p->image_constant_pose && p->image_constant_pose[j]);
+    if (c1 && c2) continue;
+    ss->pair_var1[k] = !c1;
+    ss->pair_var2[k] = !c2;
+    const double* K1 = &p->camera_params[(int64_t)p->image_camera[i] * np];
+    const float* depth1 = sem->depth + (int64_t)i * H * W;
+    const float* label1 = sem->label + (int64_t)i * H * W;
+    for (int y = 0; y < H; y += step) {
+      for (int x = 0; x < W; x += step) {
+        const float depth = depth1[(int64_t)y * W + x];
+        if (depth < 1e-4) continue;
+        SemSample smp;
+        smp.pair = k; smp.x = x; smp.y = y;
+        double u1, v1;
+        ImageToWorld(p->camera_model, K1, (double)x, (double)y, &u1, &v1);
+        smp.pc1[0] = u1 * (double)depth;
+        smp.pc1[1] = v1 * (double)depth;
+        smp.pc1[2] = (double)depth;
+        smp.label1 = label1[(int64_t)y * W + x];
+        ss->samples.push_back(smp);
+      }
+    }
+  }
+  (void)s;
+}
+
+double SemanticError(const mi_ba_problem* p, const mi_ba_semantic* sem, const SemSample& smp,
+                     const double q1[4], const double t1[3], const double q2[4], const double t2[3],
+                     int* status) {
+  const int np = NumParams(p->camera_model);
+  const int j = sem->pairs[2 * smp.pair + 1];
+  const double* K2 = &p->camera_params[(int64_t)p->image_camera[j] * np];
+  double q1i[4], t1i[3];
+  PoseInverse(q1, t1, q1i, t1i);                       // :121-125
+  double pw[3];
+  PoseTransformPoint(q1i, t1i, smp.pc1, pw);           // :127-128
+  double pc2[3];
+  PoseTransformPoint(q2, t2, pw, pc2);                 // :136-138
+  const double u2 = pc2[0] / pc2[2];                   // :141-144
+  const double v2 = pc2[1] / pc2[2];
+  const double measured_depth_2 = pc2[2];
+  double x2, y2;
+  WorldToImage(p->camera_model, K2, u2, v2, &x2, &y2); // :149-151
+  const int px = CastToIntX86(std::round(x2));         // :154-156
+  const int py = CastToIntX86(std::round(y2));
+  const int H = sem->height, W = sem->width;
+  if (px < 0 || px >= W || py < 0 || py >= H) {        // :163-177
+    *status = MI_BA_OUT_OF_BOUNDS;
+    return 0.0;
+  }
+  const int64_t off = (int64_t)j * H * W + (int64_t)py * W + px;
+  const double depth_2 = (double)sem->depth[off];
+  if (std::fabs(depth_2 - measured_depth_2) > sem->depth_error_threshold) {  // :180-196
+    *status = MI_BA_INVALID_DEPTH;
+    return 0.0;
+  }
+  *status = MI_BA_VALID;                               // :199-205
+  return (smp.label1 == sem->label[off]) ? 0.0 : 1.0;
+}
+
+// Ceres 2.1 NumericDiffCostFunction<..., CENTRAL, 1, 4,3[,4,3]> (restated):
+// delta_j = max(sqrt(eps), |x_j| * relative_step_size);
+// J_j = (f(x + delta e_j) - f(x - delta e_j)) * ((1/delta)/2);
+// then QuaternionManifold / SubsetManifold PlusJacobian.
+void EvalSemantic(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, const SemSetup& ss,
+                  int64_t n, int* status, double* r, double* J) {
+  const SemSample& smp = ss.samples[n];
+  const int i = sem->pairs[2 * smp.pair], j = sem->pairs[2 * smp.pair + 1];
+  double x[14];
+  for (int m = 0; m < 4; ++m) x[m] = p->qvec[i * 4 + m];
+  for (int m = 0; m < 3; ++m) x[4 + m] = p->tvec[i * 3 + m];
+  for (int m = 0; m < 4; ++m) x[7 + m] = p->qvec[j * 4 + m];
+  for (int m = 0; m < 3; ++m) x[11 + m] = p->tvec[j * 3 + m];
+  int st;
+  *r = SemanticError(p, sem, smp, &x[0], &x[4], &x[7], &x[11], status);
+  double Jamb[14] = {0};
+  const bool var[2] = {ss.pair_var1[smp.pair] != 0, ss.pair_var2[smp.pair] != 0};
+  const double min_step = std::sqrt(std::numeric_limits<double>::epsilon());
+  for (int blk = 0; blk < 2; ++blk) {
+    if (!var[blk]) continue;
+    for (int m = 0; m < 7; ++m) {
+      const int idx = blk * 7 + m;
+      const double orig = x[idx];
+      const double delta = std::max(min_step, std::fabs(orig) * sem->numeric_relative_step_size);
+      x[idx] = orig + delta;
+      const double fp = SemanticError(p, sem, smp, &x[0], &x[4], &x[7], &x[11], &st);
+      x[idx] = orig - delta;
+      const double fm = SemanticError(p, sem, smp, &x[0], &x[4], &x[7], &x[11], &st);
+      x[idx] = orig;
+      double one_over_delta = 1.0 / delta;
+      one_over_delta /= 2;
+      Jamb[idx] = (fp - fm) * one_over_delta;
+    }
+  }
+  for (int blk = 0; blk < 2; ++blk) {
+    double* Jb = J + blk * 6;
+    const int img = blk == 0 ? i : j;
+    if (!var[blk]) { for (int m = 0; m < 6; ++m) Jb[m] = 0.0; continue; }
+    double PJ[12];
+    QuaternionPlusJacobian(&x[blk * 7], PJ);
+    for (int col = 0; col < 3; ++col) {
+      double acc = 0.0;
+      for (int m = 0; m < 4; ++m) acc += Jamb[blk * 7 + m] * PJ[m * 3 + col];
+      Jb[col] = acc;
+    }
+    for (int col = 0; col < 3; ++col) {
+      const bool masked = (s.img_tvec_mask[img] >> col) & 1;
+      Jb[3 + col] = masked ? 0.0 : Jamb[blk * 7 + 4 + col];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Dense LM + Schur elimination (Ceres 2.1 TrustRegionMinimizer +
+// LevenbergMarquardtStrategy + DENSE_SCHUR, restated; bundle_adjustment.cc:
+// 271-306 selects it for <= 50 images).
+// ---------------------------------------------------------------------------
+struct Layout {
+  // f-block (reduced camera system) coordinates
+  std::vector<int> img_off;   // -1 if not variable; 6 tangent slots (masked coords skipped)
+  std::vector<int> img_cols;  // mapping slot (0..5) -> column or -1
+  std::vector<int> cam_off;
+  int nf = 0;
+  std::vector<int64_t> pt_off;  // -1 if constant
+  int64_t ne = 0;
+};
+
+// Poses of semantic pairs are parameter blocks with the quaternion / tvec
+// manifolds of SetUpManifolds (semantic_bundle_adjustment.cc:670-693).
+void AddSemanticPoses(const mi_ba_problem* p, const mi_ba_semantic* sem, const SemSetup& ss, Setup* s) {
+  for (int k = 0; k < sem->num_pairs; ++k) {
+    for (int side = 0; side < 2; ++side) {
+      if (!(side == 0 ? ss.pair_var1[k] : ss.pair_var2[k])) continue;
+      const int img = sem->pairs[2 * k + side];
+      if (s->img_var[img]) continue;
+      s->img_var[img] = 1;
+      s->img_tvec_mask[img] = p->image_constant_tvec ? p->image_constant_tvec[img] : 0;
+      int masked = 0;
+      for (int b = 0; b < 3; ++b) masked += (s->img_tvec_mask[img] >> b) & 1;
+      s->num_effective_parameters_reduced += 6 - masked;
+    }
+  }
+}
+
+void BuildLayout(const Setup& s, const mi_ba_problem* p, Layout* L, const mi_ba_semantic* sem = nullptr,
+                 const SemSetup* ss = nullptr) {
+  const int I = p->num_images, C = p->num_cameras;
+  L->img_off.assign(I, -1);
+  L->img_cols.assign((size_t)I * 6, -1);
+  std::vector<uint8_t> used_img(I, 0), used_cam(C, 0), used_pt(p->num_points, 0);
+  if (sem && ss)
+    for (int k = 0; k < sem->num_pairs; ++k) {
+      if (ss->pair_var1[k]) used_img[sem->pairs[2 * k]] = 1;
+      if (ss->pair_var2[k]) used_img[sem->pairs[2 * k + 1]] = 1;
+    }
+  for (size_t b = 0; b < s.block_obs.size(); ++b) {
+    if (!s.block_reduced[b]) continue;
+    const int64_t k = s.block_obs[b];
+    const int img = p->obs_image[k];
+    if (!s.block_const_pose[b] && s.img_var[img]) used_img[img] = 1;
+    if (s.cam_var[p->image_camera[img]]) used_cam[p->image_camera[img]] = 1;
+    if (s.pt_var[p->obs_point[k]]) used_pt[p->obs_point[k]] = 1;
+  }
+  int nf = 0;
+  for (int i = 0; i < I; ++i) {
+    if (!used_img[i]) continue;
+    L->img_off[i] = nf;
+    for (int m = 0; m < 6; ++m) {
+      if (m >= 3 && ((s.img_tvec_mask[i] >> (m - 3)) & 1)) continue;
+      L->img_cols[(size_t)i * 6 + m] = nf++;
+    }
+  }
+  L->cam_off.assign(C, -1);
+  for (int c = 0; c < C; ++c) {
+    if (!used_cam[c]) continue;
+    L->cam_off[c] = nf;
+    nf += (int)s.cam_tangent.size();
+  }
+  L->nf = nf;
+  L->pt_off.assign(p->num_points, -1);
+  int64_t ne = 0;
+  for (int64_t pt = 0; pt < p->num_points; ++pt)
+    if (used_pt[pt]) { L->pt_off[pt] = ne; ne += 3; }
+  L->ne = ne;
+}
+
+bool Cholesky(std::vector<double>& A, int n) {  // in place, lower
+  for (int j = 0; j < n; ++j) {
+    double d = A[(size_t)j * n + j];
+    for (int k = 0; k < j; ++k) d -= A[(size_t)j * n + k] * A[(size_t)j * n + k];
+    if (!(d > 0.0)) return false;
+    d = std::sqrt(d);
+    A[(size_t)j * n + j] = d;
+    for (int i = j + 1; i < n; ++i) {
+      double v = A[(size_t)i * n + j];
+      for (int k = 0; k < j; ++k) v -= A[(size_t)i * n + k] * A[(size_t)j * n + k];
+      A[(size_t)i * n + j] = v / d;
+    }
+  }
+  return true;
+}
+void CholSolve(const std::vector<double>& L, int n, std::vector<double>& b) {
+  for (int i = 0; i < n; ++i) {
+    double v = b[i];
+    for (int k = 0; k < i; ++k) v -= L[(size_t)i * n + k] * b[k];
+    b[i] = v / L[(size_t)i * n + i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double v = b[i];
+    for (int k = i + 1; k < n; ++k) v -= L[(size_t)k * n + i] * b[k];
+    b[i] = v / L[(size_t)i * n + i];
+  }
+}
+bool Inv3(const double A[9], double Ai[9]) {
+  const double c00 = A[4] * A[8] - A[5] * A[7], c01 = A[5] * A[6] - A[3] * A[8], c02 = A[3] * A[7] - A[4] * A[6];
+  const double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+  if (!(std::fabs(det) > 0.0)) return false;
+  const double id = 1.0 / det;
+  Ai[0] = c00 * id; Ai[1] = (A[2] * A[7] - A[1] * A[8]) * id; Ai[2] = (A[1] * A[5] - A[2] * A[4]) * id;
+  Ai[3] = c01 * id; Ai[4] = (A[0] * A[8] - A[2] * A[6]) * id; Ai[5] = (A[2] * A[3] - A[0] * A[5]) * id;
+  Ai[6] = c02 * id; Ai[7] = (A[1] * A[6] - A[0] * A[7]) * id; Ai[8] = (A[0] * A[4] - A[1] * A[3]) * id;
+  return true;
+}
+
+// Sparse-row Jacobian of the whole reduced program.
+struct Linearization {
+  std::vector<double> r;          // residuals (corrected)
+  struct Row { std::vector<std::pair<int64_t, double>> f; std::vector<std::pair<int64_t, double>> e; };
+  std::vector<Row> rows;
+  double cost = 0.0;              // 0.5 sum rho (reduced program only)
+};
+
+struct Solver {
+  const mi_ba_options* o;
+  mi_ba_problem* p;
+  const mi_ba_semantic* sem;
+  Setup s;
+  SemSetup ss;
+  Layout L;
+
+  double BlockCost(int64_t b) {
+    double r[2];
+    EvalBlock(s, p, b, r, nullptr);
+    double rho[3];
+    LossEvaluate(o->loss_function_type, o->loss_function_scale, r[0] * r[0] + r[1] * r[1], rho);
+    return 0.5 * rho[0];
+  }
+  double SemCost(int64_t n) {
+    const SemSample& smp = ss.samples[n];
+    const int i = sem->pairs[2 * smp.pair], j = sem->pairs[2 * smp.pair + 1];
+    int st;
+    const double r = SemanticError(p, sem, smp, &p->qvec[i * 4], &p->tvec[i * 3], &p->qvec[j * 4], &p->tvec[j * 3], &st);
+    double rho[3];
+    LossEvaluate(o->loss_function_type, o->loss_function_scale, r * r, rho);
+    return 0.5 * (o->semantic_weight * rho[0]);  // ScaledLoss(w)
+  }
+  // Cost of the reduced program (Ceres adds fixed_cost separately).
+  double Cost() {
+    double c = 0.0;
+    for (size_t b = 0; b < s.block_obs.size(); ++b)
+      if (s.block_reduced[b]) c += BlockCost(b);
+    if (sem)
+      for (size_t n = 0; n < ss.samples.size(); ++n) c += SemCost(n);
+    return c;
+  }
+  void Linearize(Linearization* lin) {
+    lin->r.clear(); lin->rows.clear(); lin->cost = 0.0;
+    const int c = (int)s.cam_tangent.size();
+    std::vector<double> J(2 * (9 + c));
+    for (size_t b = 0; b < s.block_obs.size(); ++b) {
+      if (!s.block_reduced[b]) continue;
+      double r[2];
+      EvalBlock(s, p, b, r, J.data());
+      double rho[3];
+      const double sq = r[0] * r[0] + r[1] * r[1];
+      LossEvaluate(o->loss_function_type, o->loss_function_scale, sq, rho);
+      lin->cost += 0.5 * rho[0];
+      ApplyCorrector(rho, sq, 2, r, 9 + c, J.data());
+      const int64_t k = s.block_obs[b];
+      const int img = p->obs_image[k];
+      const int cam = p->image_camera[img];
+      const int64_t pt = p->obs_point[k];
+      for (int row = 0; row < 2; ++row) {
+        Linearization::Row R;
+        const double* Jr = &J[row * (9 + c)];
+        if (!s.block_const_pose[b] && L.img_off[img] >= 0)
+          for (int m = 0; m < 6; ++m) {
+            const int col = L.img_cols[(size_t)img * 6 + m];
+            if (col >= 0) R.f.push_back({col, Jr[m]});
+          }
+        if (L.cam_off[cam] >= 0)
+          for (int m = 0; m < c; ++m) R.f.push_back({L.cam_off[cam] + m, Jr[9 + m]});
+        if (L.pt_off[pt] >= 0)
+          for (int m = 0; m < 3; ++m) R.e.push_back({L.pt_off[pt] + m, Jr[6 + m]});
+        lin->rows.push_back(R);
+        lin->r.push_back(r[row]);
+      }
+    }
+    if (sem) {
+      for (size_t n = 0; n < ss.samples.size(); ++n) {
+        int st; double r; double Js[12];
+        EvalSemantic(p, s, sem, ss, n, &st, &r, Js);
+        double rho[3];
+        LossEvaluate(o->loss_function_type, o->loss_function_scale, r * r, rho);
+        for (int m = 0; m < 3; ++m) rho[m] *= o->semantic_weight;  // ScaledLoss
+        lin->cost += 0.5 * rho[0];
+        ApplyCorrector(rho, r * r, 1, &r, 12, Js);
+        const SemSample& smp = ss.samples[n];
+        Linearization::Row R;
+        for (int blk = 0; blk < 2; ++blk) {
+          const int img = sem->pairs[2 * smp.pair + blk];
+          if (L.img_off[img] < 0) continue;
+          for (int m = 0; m < 6; ++m) {
+            const int col = L.img_cols[(size_t)img * 6 + m];
+            if (col >= 0) R.f.push_back({col, Js[blk * 6 + m]});
+          }
+        }
+        lin->rows.push_back(R);
+        lin->r.push_back(r);
+      }
+    }
+  }
+  // Apply tangent step delta (f then e coordinates) with manifold Plus.
+  void Plus(const std::vector<double>& delta) {
+    for (int i = 0; i < p->num_images; ++i) {
+      if (L.img_off[i] < 0) continue;
+      double d[6] = {0, 0, 0, 0, 0, 0};
+      for (int m = 0; m < 6; ++m) {
+        const int col = L.img_cols[(size_t)i * 6 + m];
+        if (col >= 0) d[m] = delta[col];
+      }
+      double qn[4];
+      QuaternionPlus(&p->qvec[i * 4], d, qn);
+      for (int m = 0; m < 4; ++m) p->qvec[i * 4 + m] = qn[m];
+      for (int m = 0; m < 3; ++m) p->tvec[i * 3 + m] += d[3 + m];
+    }
+    const int np = s.np;
+    for (int c = 0; c < p->num_cameras; ++c) {
+      if (L.cam_off[c] < 0) continue;
+      for (size_t m = 0; m < s.cam_tangent.size(); ++m)
+        p->camera_params[(int64_t)c * np + s.cam_tangent[m]] += delta[L.cam_off[c] + m];
+    }
+    for (int64_t pt = 0; pt < p->num_points; ++pt) {
+      if (L.pt_off[pt] < 0) continue;
+      for (int m = 0; m < 3; ++m) p->xyz[pt * 3 + m] += delta[L.nf + L.pt_off[pt] + m];
+    }
+  }
+};
+
+}  // namespace
+
+// ===========================================================================
+// C ABI for ctypes
+// ===========================================================================
+extern "C" {
+
+int oracle_num_params(int model) { return NumParams(model); }
+
+// camera_models.h WorldToImage / ImageToWorld for one point.
+void oracle_world_to_image(int model, const double* params, double u, double v, double* x, double* y) {
+  WorldToImage(model, params, u, v, x, y);
+}
+void oracle_image_to_world(int model, const double* params, double x, double y, double* u, double* v) {
+  ImageToWorld(model, params, x, y, u, v);
+}
+
+// BundleAdjustmentCostFunction<M>::Evaluate residuals only (cost_functions.h:57-81).
+void oracle_reproj_residual(int model, const double* q, const double* t, const double* X,
+                            const double* cam, double ox, double oy, double* r) {
+  ReprojResidual<double>(model, q, t, X, cam, ox, oy, r);
+}
+
+// projection.cc:111-131 CalculateSquaredReprojectionError(point2D, point3D, qvec, tvec, camera)
+double oracle_squared_reprojection_error(int model, const double* params, const double* xy,
+                                         const double* X, const double* q, const double* t) {
+  double pc[3];
+  QuaternionRotatePoint(q, X, pc);
+  pc[0] += t[0]; pc[1] += t[1]; pc[2] += t[2];
+  if (pc[2] < std::numeric_limits<double>::epsilon()) return std::numeric_limits<double>::max();
+  double x, y;
+  WorldToImage(model, params, pc[0] / pc[2], pc[1] / pc[2], &x, &y);
+  return (x - xy[0]) * (x - xy[0]) + (y - xy[1]) * (y - xy[1]);
+}
+
+int oracle_setup_stats(const mi_ba_options* o, mi_ba_problem* p, mi_ba_setup_info* info) {
+  Setup s;
+  const int st = BuildSetup(o, p, &s);
+  if (st) return st;
+  info->num_residual_blocks = (int64_t)s.block_obs.size();
+  info->num_residuals_reduced = s.num_residuals_reduced;
+  info->num_effective_parameters_reduced = s.num_effective_parameters_reduced;
+  int64_t vi = 0, vc = 0, vp = 0;
+  for (auto v : s.img_var) vi += v;
+  for (auto v : s.cam_var) vc += v;
+  for (auto v : s.pt_var) vp += v;
+  info->num_variable_images = vi;
+  info->num_variable_cameras = vc;
+  info->num_variable_points = vp;
+  info->camera_tangent_size = (int)s.cam_tangent.size();
+  return MI_BA_OK;
+}
+
+// Residual + tangent Jacobian of every block of the program (program order;
+// block_obs[k] = observation index).  Note: normalises config qvecs in place
+// exactly as SetUp does.  Returns number of blocks or negative status.
+int64_t oracle_reproj_eval(const mi_ba_options* o, mi_ba_problem* p, int64_t* block_obs,
+                           double* residuals, double* jacobian, int64_t capacity) {
+  Setup s;
+  const int st = BuildSetup(o, p, &s);
+  if (st) return -st;
+  const int64_t nb = (int64_t)s.block_obs.size();
+  if (nb > capacity) return nb;
+  const int w = 9 + (int)s.cam_tangent.size();
+#pragma omp parallel for schedule(static)
+  for (int64_t b = 0; b < nb; ++b) {
+    block_obs[b] = s.block_obs[b];
+    EvalBlock(s, p, b, &residuals[2 * b], jacobian ? &jacobian[b * 2 * w] : nullptr);
+  }
+  return nb;
+}
+
+// Throughput baseline: residual+Jacobian of all blocks, `repeats` times,
+// with the given number of OpenMP threads.  Returns wall seconds of the
+// evaluation loop only (setup excluded).
+double oracle_reproj_throughput(const mi_ba_options* o, mi_ba_problem* p, int64_t max_blocks,
+                                int repeats, int threads, int64_t* blocks_done) {
+  Setup s;
+  if (BuildSetup(o, p, &s)) return -1.0;
+  const int64_t nb = std::min<int64_t>((int64_t)s.block_obs.size(), max_blocks);
+  const int w = 9 + (int)s.cam_tangent.size();
+  std::vector<double> r(2 * nb), J(2 * w * nb);
+  double t0 = 0, t1 = 0;
+  {
+    struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); t0 = ts.tv_sec + 1e-9 * ts.tv_nsec;
+  }
+  for (int rep = 0; rep < repeats; ++rep) {
+#pragma omp parallel for schedule(static) num_threads(threads)
+    for (int64_t b = 0; b < nb; ++b) EvalBlock(s, p, b, &r[2 * b], &J[b * 2 * w]);
+  }
+  {
+    struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); t1 = ts.tv_sec + 1e-9 * ts.tv_nsec;
+  }
+  *blocks_done = nb * repeats;
+  return t1 - t0;
+}
+
+// Semantic samples: returns count (or negative status).  Arrays sized by
+// capacity; layout as mi_ba_download_semantic.
+int64_t oracle_semantic_eval(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem,
+                             int32_t* sample_pixel, int32_t* status, double* residuals,
+                             double* jacobian, int64_t capacity) {
+  Setup s;
+  const int st = BuildSetup(o, p, &s);
+  if (st) return -st;
+  SemSetup ss;
+  BuildSemSetup(o, p, s, sem, &ss);
+  const int64_t n = (int64_t)ss.samples.size();
+  if (n > capacity) return n;
+#pragma omp parallel for schedule(dynamic, 256)
+  for (int64_t k = 0; k < n; ++k) {
+    sample_pixel[3 * k] = ss.samples[k].pair;
+    sample_pixel[3 * k + 1] = ss.samples[k].x;
+    sample_pixel[3 * k + 2] = ss.samples[k].y;
+    int stt;
+    EvalSemantic(p, s, sem, ss, k, &stt, &residuals[k], &jacobian[12 * k]);
+    status[k] = stt;
+  }
+  return n;
+}
+
+double oracle_semantic_throughput(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem,
+                                  int64_t max_samples, int threads, int64_t* done) {
+  Setup s;
+  if (BuildSetup(o, p, &s)) return -1.0;
+  SemSetup ss;
+  BuildSemSetup(o, p, s, sem, &ss);
+  const int64_t n = std::min<int64_t>((int64_t)ss.samples.size(), max_samples);
+  std::vector<double> r(n), J(12 * n);
+  struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts);
+  const double t0 = ts.tv_sec + 1e-9 * ts.tv_nsec;
+#pragma omp parallel for schedule(dynamic, 256) num_threads(threads)
+  for (int64_t k = 0; k < n; ++k) {
+    int stt;
+    EvalSemantic(p, s, sem, ss, k, &stt, &r[k], &J[12 * k]);
+  }
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  *done = n;
+  return ts.tv_sec + 1e-9 * ts.tv_nsec - t0;
+}
+
+// Full LM solve, dense Schur (Ceres 2.1 LM semantics, restated).
+int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem, mi_ba_summary* sum) {
+  Solver S;
+  S.o = o; S.p = p; S.sem = sem;
+  std::memset(sum, 0, sizeof(*sum));
+  int st = BuildSetup(o, p, &S.s);
+  if (st) return st;
+  if (sem) {
+    BuildSemSetup(o, p, S.s, sem, &S.ss);
+    AddSemanticPoses(p, sem, S.ss, &S.s);
+  }
+  BuildLayout(S.s, p, &S.L, sem, sem ? &S.ss : nullptr);
+  sum->num_residuals_reduced = S.s.num_residuals_reduced + (int64_t)S.ss.samples.size();
+  sum->num_effective_parameters_reduced = S.s.num_effective_parameters_reduced;
+  sum->num_semantic_residuals = (int64_t)S.ss.samples.size();
+  if (sum->num_residuals_reduced == 0) return MI_BA_ERR_NO_RESIDUALS;
+  // fixed cost of the dropped all-constant blocks
+  double fixed = 0.0;
+  for (size_t b = 0; b < S.s.block_obs.size(); ++b)
+    if (!S.s.block_reduced[b]) fixed += S.BlockCost(b);
+  sum->fixed_cost = fixed;
+  const int nf = S.L.nf;
+  const int64_t ne = S.L.ne;
+  const int64_t n = nf + ne;
+  Linearization lin;
+  S.Linearize(&lin);
+  double x_cost = lin.cost;
+  sum->initial_cost = x_cost + fixed;
+  sum->num_jacobian_evaluations = 1;
+  // Jacobi scaling, computed once at iteration 0.
+  std::vector<double> colnorm(n, 0.0);
+  for (auto& R : lin.rows) {
+    for (auto& e : R.f) colnorm[e.first] += e.second * e.second;
+    for (auto& e : R.e) colnorm[nf + e.first] += e.second * e.second;
+  }
+  std::vector<double> scale(n);
+  for (int64_t i = 0; i < n; ++i) scale[i] = 1.0 / (1.0 + std::sqrt(colnorm[i]));
+  double radius = o->initial_trust_region_radius;
+  double decrease_factor = 2.0;
+  bool reuse_diagonal = false;
+  std::vector<double> diag(n, 0.0);
+  int consecutive_invalid = 0;
+  int iteration = 0;
+  sum->termination_type = MI_BA_NO_CONVERGENCE;
+  const int64_t np3 = ne / 3;
+  while (true) {
+    if (iteration >= o->max_num_iterations) { sum->termination_type = MI_BA_NO_CONVERGENCE; break; }
+    if (radius < 1e-32) { sum->termination_type = MI_BA_CONVERGENCE; break; }
+    ++iteration;
+    // scaled Jacobian column norms -> LM diagonal
+    if (!reuse_diagonal) {
+      std::fill(diag.begin(), diag.end(), 0.0);
+      for (auto& R : lin.rows) {
+        for (auto& e : R.f) { const double v = e.second * scale[e.first]; diag[e.first] += v * v; }
+        for (auto& e : R.e) { const double v = e.second * scale[nf + e.first]; diag[nf + e.first] += v * v; }
+      }
+      for (auto& d : diag) d = std::min(std::max(d, 1e-6), 1e32);
+    }
+    std::vector<double> D2(n);
+    for (int64_t i = 0; i < n; ++i) D2[i] = diag[i] / radius;
+    // Normal equations in scaled coordinates, Schur on points.
+    std::vector<double> U((size_t)nf * nf, 0.0), g(n, 0.0);
+    std::vector<double> V(np3 * 9, 0.0);
+    std::vector<std::vector<double>> W(np3);
+    std::vector<std::vector<int>> Wcols(np3);
+    for (size_t ri = 0; ri < lin.rows.size(); ++ri) {
+      const auto& R = lin.rows[ri];
+      const double rr = lin.r[ri];
+      for (auto& a : R.f) {
+        const double va = a.second * scale[a.first];
+        g[a.first] += va * rr;
+        for (auto& b2 : R.f) U[(size_t)a.first * nf + b2.first] += va * b2.second * scale[b2.first];
+      }
+      if (R.e.empty()) continue;
+      const int64_t pt = R.e[0].first / 3;
+      for (auto& a : R.e) {
+        const double va = a.second * scale[nf + a.first];
+        g[nf + a.first] += va * rr;
+        for (auto& b2 : R.e) V[pt * 9 + (a.first % 3) * 3 + (b2.first % 3)] += va * b2.second * scale[nf + b2.first];
+      }
+      for (auto& a : R.f) {
+        int slot = -1;
+        for (size_t m = 0; m < Wcols[pt].size(); ++m) if (Wcols[pt][m] == a.first) { slot = (int)m; break; }
+        if (slot < 0) { slot = (int)Wcols[pt].size(); Wcols[pt].push_back((int)a.first); W[pt].resize(W[pt].size() + 3, 0.0); }
+        const double va = a.second * scale[a.first];
+        for (auto& e : R.e) W[pt][slot * 3 + (e.first % 3)] += va * e.second * scale[nf + e.first];
+      }
+    }
+    for (int i = 0; i < nf; ++i) U[(size_t)i * nf + i] += D2[i];
+    std::vector<double> Vinv(np3 * 9);
+    bool ok = true;
+    for (int64_t pt = 0; pt < np3; ++pt) {
+      for (int m = 0; m < 3; ++m) V[pt * 9 + m * 4] += D2[nf + pt * 3 + m];
+      if (!Inv3(&V[pt * 9], &Vinv[pt * 9])) ok = false;
+    }
+    // S = U - sum W Vinv W^T ; rhs = g_f - sum W Vinv g_e
+    std::vector<double> Sm = U, rhs(g.begin(), g.begin() + nf);
+    for (int64_t pt = 0; pt < np3 && ok; ++pt) {
+      const auto& cols = Wcols[pt];
+      const size_t m = cols.size();
+      std::vector<double> WV(m * 3, 0.0);
+      for (size_t a = 0; a < m; ++a)
+        for (int c2 = 0; c2 < 3; ++c2) {
+          double acc = 0.0;
+          for (int k = 0; k < 3; ++k) acc += W[pt][a * 3 + k] * Vinv[pt * 9 + k * 3 + c2];
+          WV[a * 3 + c2] = acc;
+        }
+      for (size_t a = 0; a < m; ++a) {
+        for (size_t b2 = 0; b2 < m; ++b2) {
+          double acc = 0.0;
+          for (int k = 0; k < 3; ++k) acc += WV[a * 3 + k] * W[pt][b2 * 3 + k];
+          Sm[(size_t)cols[a] * nf + cols[b2]] -= acc;
+        }
+        double acc = 0.0;
+        for (int k = 0; k < 3; ++k) acc += WV[a * 3 + k] * g[nf + pt * 3 + k];
+        rhs[cols[a]] -= acc;
+      }
+    }
+    std::vector<double> step(n, 0.0);
+    if (ok && nf > 0) ok = Cholesky(Sm, nf);
+    if (ok) {
+      if (nf > 0) CholSolve(Sm, nf, rhs);
+      for (int i = 0; i < nf; ++i) step[i] = rhs[i];
+      for (int64_t pt = 0; pt < np3; ++pt) {
+        double t3[3];
+        for (int k = 0; k < 3; ++k) t3[k] = g[nf + pt * 3 + k];
+        const auto& cols = Wcols[pt];
+        for (size_t a = 0; a < cols.size(); ++a)
+          for (int k = 0; k < 3; ++k) t3[k] -= W[pt][a * 3 + k] * step[cols[a]];
+        for (int k = 0; k < 3; ++k) {
+          double acc = 0.0;
+          for (int m2 = 0; m2 < 3; ++m2) acc += Vinv[pt * 9 + k * 3 + m2] * t3[m2];
+          step[nf + pt * 3 + k] = acc;
+        }
+      }
+      for (auto& v : step) v = -v;  // Ceres solves (J'J+D'D)x = J'f, step = -x
+    }
+    reuse_diagonal = true;
+    double model_cost_change = 0.0;
+    if (ok) {
+      for (size_t ri = 0; ri < lin.rows.size(); ++ri) {
+        const auto& R = lin.rows[ri];
+        double mr = 0.0;
+        for (auto& e : R.f) mr += e.second * scale[e.first] * step[e.first];
+        for (auto& e : R.e) mr += e.second * scale[nf + e.first] * step[nf + e.first];
+        model_cost_change += -(mr * (lin.r[ri] + mr / 2.0));
+      }
+      ok = model_cost_change > 0.0;
+    }
+    if (!ok) {
+      ++consecutive_invalid;
+      ++sum->num_unsuccessful_steps;
+      if (consecutive_invalid > o->max_num_consecutive_invalid_steps) { sum->termination_type = MI_BA_FAILURE; break; }
+      radius = radius / decrease_factor;
+      decrease_factor *= 2.0;
+      continue;
+    }
+    consecutive_invalid = 0;
+    std::vector<double> delta(n);
+    for (int64_t i = 0; i < n; ++i) delta[i] = step[i] * scale[i];
+    // candidate
+    std::vector<double> q0(p->qvec, p->qvec + 4 * p->num_images), t0(p->tvec, p->tvec + 3 * p->num_images);
+    std::vector<double> c0(p->camera_params, p->camera_params + (int64_t)S.s.np * p->num_cameras);
+    std::vector<double> x0(p->xyz, p->xyz + 3 * p->num_points);
+    double x_norm2 = 0.0;
+    for (double v : q0) x_norm2 += v * v;
+    S.Plus(delta);
+    const double candidate_cost = S.Cost();
+    // ParameterToleranceReached / FunctionToleranceReached (tolerance 0 default)
+    double step_norm2 = 0.0;
+    for (int64_t i = 0; i < n; ++i) step_norm2 += delta[i] * delta[i];
+    const double cost_change = x_cost - candidate_cost;
+    const double relative_decrease = cost_change / model_cost_change;
+    const bool success = relative_decrease > o->min_relative_decrease;
+    // ParameterToleranceReached / FunctionToleranceReached return before the
+    // candidate is accepted (x_ stays).
+    if (std::sqrt(step_norm2) <= o->parameter_tolerance * (std::sqrt(x_norm2) + o->parameter_tolerance) ||
+        std::fabs(cost_change) <= o->function_tolerance * x_cost) {
+      std::copy(q0.begin(), q0.end(), p->qvec); std::copy(t0.begin(), t0.end(), p->tvec);
+      std::copy(c0.begin(), c0.end(), p->camera_params); std::copy(x0.begin(), x0.end(), p->xyz);
+      sum->termination_type = MI_BA_CONVERGENCE;
+      ++sum->num_unsuccessful_steps;
+      break;
+    }
+    if (success) {
+      ++sum->num_successful_steps;
+      x_cost = candidate_cost;
+      radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * relative_decrease - 1.0, 3));
+      radius = std::min(1e16, radius);
+      decrease_factor = 2.0;
+      reuse_diagonal = false;
+      S.Linearize(&lin);
+      ++sum->num_jacobian_evaluations;
+    } else {
+      ++sum->num_unsuccessful_steps;
+      std::copy(q0.begin(), q0.end(), p->qvec); std::copy(t0.begin(), t0.end(), p->tvec);
+      std::copy(c0.begin(), c0.end(), p->camera_params); std::copy(x0.begin(), x0.end(), p->xyz);
+      radius = radius / decrease_factor;
+      decrease_factor *= 2.0;
+    }
+  }
+  sum->final_cost = x_cost + fixed;
+  return MI_BA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,173 @@
+"""ctypes binding of liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference hot path (see oracle.cc).  Imported only
+by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, always as
+the checker, never as the thing measured or shipped.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.join(os.path.dirname(_HERE), "semantic-bundle-adjustment-colmap_amd")
+if _PKG not in sys.path:
+    sys.path.insert(0, _PKG)
+import mi_ba  # noqa: E402  (struct layouts of the boundary)
+
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_dp = C.POINTER(C.c_double)
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = C.CDLL(LIB_PATH)
+    lib.oracle_world_to_image.argtypes = [C.c_int, _dp, C.c_double, C.c_double, _dp, _dp]
+    lib.oracle_image_to_world.argtypes = [C.c_int, _dp, C.c_double, C.c_double, _dp, _dp]
+    lib.oracle_reproj_residual.argtypes = [C.c_int, _dp, _dp, _dp, _dp, C.c_double, C.c_double, _dp]
+    lib.oracle_squared_reprojection_error.restype = C.c_double
+    lib.oracle_squared_reprojection_error.argtypes = [C.c_int, _dp, _dp, _dp, _dp, _dp]
+    lib.oracle_setup_stats.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem),
+                                       C.POINTER(mi_ba.SetupInfo)]
+    lib.oracle_reproj_eval.restype = C.c_int64
+    lib.oracle_reproj_eval.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem), _i64p, _dp, _dp,
+                                       C.c_int64]
+    lib.oracle_reproj_throughput.restype = C.c_double
+    lib.oracle_reproj_throughput.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem), C.c_int64,
+                                             C.c_int, C.c_int, _i64p]
+    lib.oracle_semantic_eval.restype = C.c_int64
+    lib.oracle_semantic_eval.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem),
+                                         C.POINTER(mi_ba.Semantic), _i32p, _i32p, _dp, _dp, C.c_int64]
+    lib.oracle_semantic_throughput.restype = C.c_double
+    lib.oracle_semantic_throughput.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem),
+                                               C.POINTER(mi_ba.Semantic), C.c_int64, C.c_int, _i64p]
+    lib.oracle_solve.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem), C.POINTER(mi_ba.Semantic),
+                                 C.POINTER(mi_ba.Summary)]
+    _lib = lib
+    return lib
+
+
+def _a(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return x, x.ctypes.data_as(_dp)
+
+
+def world_to_image(model, params, u, v):
+    p, pp = _a(params)
+    x, y = C.c_double(), C.c_double()
+    load().oracle_world_to_image(model, pp, u, v, C.byref(x), C.byref(y))
+    return x.value, y.value
+
+
+def image_to_world(model, params, x, y):
+    p, pp = _a(params)
+    u, v = C.c_double(), C.c_double()
+    load().oracle_image_to_world(model, pp, x, y, C.byref(u), C.byref(v))
+    return u.value, v.value
+
+
+def reproj_residual(model, q, t, X, cam, obs):
+    arrs = [_a(a) for a in (q, t, X, cam)]
+    r = np.zeros(2)
+    load().oracle_reproj_residual(model, arrs[0][1], arrs[1][1], arrs[2][1], arrs[3][1], float(obs[0]),
+                                  float(obs[1]), r.ctypes.data_as(_dp))
+    return r
+
+
+def squared_reprojection_error(model, params, xy, X, q, t):
+    arrs = [_a(a) for a in (params, xy, X, q, t)]
+    return load().oracle_squared_reprojection_error(model, *[a[1] for a in arrs])
+
+
+def setup_stats(options, scene) -> "mi_ba.SetupInfo":
+    info = mi_ba.SetupInfo()
+    sc = scene.copy()  # SetUp normalises qvecs in place
+    p = sc.problem()
+    st = load().oracle_setup_stats(C.byref(options), C.byref(p), C.byref(info))
+    if st != 0:
+        raise RuntimeError(f"oracle_setup_stats status {st}")
+    return info
+
+
+def reproj_eval(options, scene):
+    """Residual + tangent Jacobian of every program block (program order)."""
+    sc = scene.copy()
+    p = sc.problem()
+    lib = load()
+    n = lib.oracle_reproj_eval(C.byref(options), C.byref(p), None, None, None, 0)
+    if n < 0:
+        raise RuntimeError(f"oracle_reproj_eval status {-n}")
+    info = setup_stats(options, scene)
+    w = 9 + info.camera_tangent_size
+    bo = np.empty(n, np.int64)
+    r = np.empty((n, 2))
+    J = np.empty((n, 2, w))
+    sc = scene.copy()
+    p = sc.problem()
+    lib.oracle_reproj_eval(C.byref(options), C.byref(p), bo.ctypes.data_as(_i64p), r.ctypes.data_as(_dp),
+                           J.ctypes.data_as(_dp), n)
+    return bo, r, J
+
+
+def semantic_eval(options, scene, semantic):
+    sc = scene.copy()
+    p = sc.problem()
+    s = semantic.struct()
+    lib = load()
+    n = lib.oracle_semantic_eval(C.byref(options), C.byref(p), C.byref(s), None, None, None, None, 0)
+    if n < 0:
+        raise RuntimeError(f"oracle_semantic_eval status {-n}")
+    px = np.empty((n, 3), np.int32)
+    st = np.empty(n, np.int32)
+    r = np.empty(n)
+    J = np.empty((n, 12))
+    sc = scene.copy()
+    p = sc.problem()
+    lib.oracle_semantic_eval(C.byref(options), C.byref(p), C.byref(s), px.ctypes.data_as(_i32p),
+                             st.ctypes.data_as(_i32p), r.ctypes.data_as(_dp), J.ctypes.data_as(_dp), n)
+    return px, st, r, J
+
+
+def solve(options, scene, semantic=None):
+    """CPU LM + dense Schur; updates scene arrays in place."""
+    s = mi_ba.Summary()
+    p = scene.problem()
+    sem = semantic.struct() if semantic is not None else None
+    st = load().oracle_solve(C.byref(options), C.byref(p), C.byref(sem) if sem is not None else None, C.byref(s))
+    if st != 0:
+        raise RuntimeError(f"oracle_solve status {st}")
+    return s
+
+
+def reproj_throughput(options, scene, max_blocks, repeats=1, threads=1):
+    sc = scene.copy()
+    p = sc.problem()
+    done = C.c_int64()
+    sec = load().oracle_reproj_throughput(C.byref(options), C.byref(p), max_blocks, repeats, threads,
+                                          C.byref(done))
+    return sec, done.value
+
+
+def semantic_throughput(options, scene, semantic, max_samples, threads=1):
+    sc = scene.copy()
+    p = sc.problem()
+    s = semantic.struct()
+    done = C.c_int64()
+    sec = load().oracle_semantic_throughput(C.byref(options), C.byref(p), C.byref(s), max_samples, threads,
+                                            C.byref(done))
+    return sec, done.value

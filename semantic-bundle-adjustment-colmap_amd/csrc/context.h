@@ -1,0 +1,102 @@
+// context.h — device-resident problem and LM driver (product code).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/mi_ba.h"
+#include "device.h"
+#include "setup.h"
+
+namespace miba {
+
+// RAII device allocation.
+template <typename T>
+struct DevArray {
+  T* ptr = nullptr;
+  size_t n = 0;
+  DevArray() = default;
+  DevArray(const DevArray&) = delete;
+  DevArray& operator=(const DevArray&) = delete;
+  ~DevArray() { release(); }
+  hipError_t alloc(size_t count) {
+    release();
+    n = count;
+    if (count == 0) return hipSuccess;
+    return hipMalloc(&ptr, sizeof(T) * count);
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    n = 0;
+  }
+  size_t bytes() const { return sizeof(T) * n; }
+};
+
+struct SemanticState;  // semantic.h
+
+struct KernelTimer {
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  std::vector<hipEvent_t> pool;
+  std::map<std::string, std::pair<double, int64_t>> totals;
+};
+
+}  // namespace miba
+
+struct mi_ba_context {
+  mi_ba_options options;
+  mi_ba_problem problem;         // host arrays (caller-owned) for write-back
+  miba::HostSetup setup;
+  miba::DevProblem dev;
+  hipStream_t stream = nullptr;
+  int device = 0;
+
+  // geometric blocks (point-major)
+  std::vector<int64_t> block_obs;          // host: observation index per device block
+  miba::DevArray<double2> obs_xy;
+  miba::DevArray<uint32_t> obs_img, obs_pt;
+  miba::DevArray<uint32_t> img_flags, img_cam;
+  miba::DevArray<uint8_t> cam_var, pt_var;
+  miba::DevArray<double> qt, cam, X;       // current parameters
+  miba::DevArray<double> qt_c, cam_c, X_c; // candidate parameters
+  miba::DevArray<uint32_t> cm_perm;
+  miba::DevArray<miba::DevTile> tiles;
+  int ntiles = 0;
+  miba::DevArray<miba::DevPoint> vpoints;
+  int64_t npv = 0;
+
+  // linearization
+  miba::DevArray<double2> r;
+  miba::DevArray<double> J;
+  miba::DevArray<double> Vg;               // [P][9]
+  miba::DevArray<double> partial;          // per-workgroup partial sums
+  int64_t npartial = 0;
+  // LM state
+  miba::DevArray<double> scale_p, diag_p, Vinv;
+  miba::DevArray<double> pose_blk, cam_blk, bvec, udiag;
+  miba::DevArray<double> scale_f, diag_f, lambda_f, prec_pose, prec_cam;
+  miba::DevArray<double> cg_x, cg_r, cg_z, cg_p, cg_q, cg_w, dX;
+  miba::DevArray<double> scalars;          // device scalars
+  double* host_scalars = nullptr;          // pinned
+
+  double fixed_cost = 0.0;
+  miba::SemanticState* sem = nullptr;
+
+  bool timing = false;
+  miba::KernelTimer timer;
+  bool solved = false;
+};
+
+namespace miba {
+mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* p, const mi_ba_semantic* sem,
+                            mi_ba_context** out);
+void context_destroy(mi_ba_context* ctx);
+mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out);
+mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum);
+mi_ba_status context_writeback(mi_ba_context* ctx);
+void timer_begin(mi_ba_context* ctx, const char* name, hipEvent_t* stop_out);
+void timer_end(mi_ba_context* ctx, hipEvent_t stop);
+}  // namespace miba

@@ -1,0 +1,68 @@
+// device.h — device-side data layout of a resident BA problem (product code).
+//
+// HBM layout (all f64 unless noted), chosen for the MI355X path:
+//   blocks (reduced residual blocks, POINT-MAJOR order: all observations of a
+//   point are contiguous, so point-block reductions are wave-local):
+//     obs_xy   double2[nb]     observed pixel (Point2D::XY)
+//     obs_img  u32[nb]         image index
+//     obs_pt   u32[nb]         point index
+//     r        double2[nb]     corrected residual
+//     J        double[nb][2][W] corrected tangent Jacobian, W = 9 + c,
+//                              columns rot(3) trans(3) point(3) cam(c)
+//   images     qt[I][8]        q(4) t(3) pad — one 64-B line per image
+//              img_flags u32[I] bit0 variable pose, bits1..3 constant tvec
+//   cameras    cam[C][8]       params, padded to 8
+//   points     X[P][3]
+// Camera-side reductions run over cm_perm (blocks sorted by image) in tiles
+// that never straddle an image, so each tile folds into one atomic flush.
+#pragma once
+
+#include <cstdint>
+
+namespace miba {
+
+constexpr int kMaxCamTangent = 8;
+constexpr int kBlock = 256;          // threads per workgroup (4 waves)
+constexpr int kTileObs = 1024;       // camera-major tile (4 obs per thread)
+
+struct DevTile {
+  uint32_t image;
+  uint32_t start;  // offset into cm_perm
+  uint32_t count;
+  uint32_t pad;
+};
+
+struct DevPoint {      // variable point with its contiguous block range
+  uint32_t point;
+  uint32_t start;
+  uint32_t count;
+  uint32_t pad;
+};
+
+struct DevProblem {
+  int model;
+  int np;              // camera params per camera
+  int ct;              // refined intrinsics per camera (tangent)
+  int W;               // 9 + ct
+  int cam_tan_idx[kMaxCamTangent];
+  int64_t nb;          // reduced geometric blocks
+  int num_images, num_cameras;
+  int64_t num_points;
+  int64_t nf;          // f-vector length: 6*I + ct*C (fixed slots, masked)
+  int loss_type;
+  double loss_scale;
+  // inputs
+  const double2* obs_xy;
+  const uint32_t* obs_img;
+  const uint32_t* obs_pt;
+  const uint32_t* img_flags;
+  const uint32_t* img_cam;
+  const uint8_t* cam_var;
+  const uint8_t* pt_var;
+  // parameters (current)
+  double* qt;   // [I][8]
+  double* cam;  // [C][8]
+  double* X;    // [P][3]
+};
+
+}  // namespace miba

@@ -1,0 +1,81 @@
+// kernels.h — launch wrappers of the gfx950 kernels (product code).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device.h"
+
+namespace miba {
+
+struct SemDevice;  // defined in semantic.h
+
+// Residual + tangent Jacobian of every reduced block (J-materialising), with
+// the loss Corrector applied, the cost folded into per-workgroup partials and
+// the point blocks V_p = sum Jp'Jp (6) and g_p = sum Jp'r (3) reduced
+// wave-locally into Vg[P][9] (Vg must be zeroed before the launch).
+// write_jacobian = 0 skips the J/r stores (cost + point blocks only).
+void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* Vg,
+                            double* cost_partial, int write_jacobian, hipStream_t s);
+int reproj_grid(int64_t nb);
+
+// Cost 0.5*sum(rho) of every reduced block at parameters (qt, cam, X).
+void launch_reproj_cost(const DevProblem& p, const double* qt, const double* cam, const double* X,
+                        double* cost_partial, hipStream_t s);
+
+// Sum n partials into out[0] (single workgroup).
+void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s);
+
+// Point side: Jacobi scale (first), LM diagonal (when !reuse_diag) and the
+// damped inverse Vinv[P][6] of V_p + Lambda_p.
+void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg,
+                          double* scale_p, double* diag_p, double* Vinv, int first, int reuse_diag,
+                          double radius, hipStream_t s);
+
+// Camera-side tile pass: per image/camera tangent block S_ii = U_ii - sum W V^-1 W',
+// b = g - sum W V^-1 g_p and diag(U) (undamped column norms).
+void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
+                   const double2* r, const double* J, const double* Vg, const double* Vinv,
+                   double* pose_blk, double* cam_blk, double* b, double* udiag, hipStream_t s);
+
+// Finalise: Jacobi scale (first), LM diagonal, damping Lambda_f, block-Jacobi
+// preconditioner (inverse of the damped diagonal blocks), rhs = -b.
+void launch_fblock_finalize(const DevProblem& p, const double* pose_blk, const double* cam_blk,
+                            const double* udiag, double* scale_f, double* diag_f, double* lambda_f,
+                            double* prec_pose, double* prec_cam, double* b, int first, int reuse_diag,
+                            double radius, hipStream_t s);
+
+// Implicit Schur product y = S x (without the semantic pair term).
+void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles,
+                          int ntiles, const uint32_t* cm_perm, const double* J, const double* Vinv,
+                          const double* lambda_f, const double* x, double* w, double* y, hipStream_t s);
+
+// Block-Jacobi preconditioner apply z = M^-1 r.
+void launch_precond(const DevProblem& p, const double* prec_pose, const double* prec_cam,
+                    const double* r, double* z, hipStream_t s);
+
+// Vector ops on the f-vector.
+void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t s);
+void launch_axpy(double* y, const double* x, const double* alpha_num, const double* alpha_den,
+                 double sign, int64_t n, hipStream_t s);
+void launch_xpby(double* p, const double* z, const double* beta_num, const double* beta_den,
+                 int64_t n, hipStream_t s);
+
+// Back substitution dX_p = -Vinv (g_p + sum Jp' Jf df) for variable points.
+void launch_backsub(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* J,
+                    const double* Vg, const double* Vinv, const double* df, double* dX, hipStream_t s);
+
+// Model cost change partials: -(J d).(r + J d / 2) per block.
+void launch_model_cost(const DevProblem& p, const double2* r, const double* J, const double* df,
+                       const double* dX, double* partial, hipStream_t s);
+
+// Candidate parameters: manifold Plus of the tangent step (scaled back).
+void launch_plus(const DevProblem& p, const double* df, const double* dX, const double* qt,
+                 const double* cam, const double* X, double* qt_out, double* cam_out, double* X_out,
+                 hipStream_t s);
+
+// Squared norms of df and dX (for the parameter tolerance test).
+void launch_sqnorm2(const double* a, int64_t na, const double* b, int64_t nb, double* out, hipStream_t s);
+
+}  // namespace miba

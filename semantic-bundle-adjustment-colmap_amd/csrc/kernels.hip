@@ -1,0 +1,1045 @@
+// kernels.hip — gfx950 kernels of the geometric BA hot path (product code).
+//
+// Replaces, on MI355X, the Ceres 2.1 evaluation of every
+// BundleAdjustmentCostFunction / BundleAdjustmentConstantPoseCostFunction
+// residual block (src/base/cost_functions.h:44-152, AutoDiff) and the Ceres
+// ITERATIVE_SCHUR + SCHUR_JACOBI linear algebra that BundleAdjuster::Solve
+// selects (src/optim/bundle_adjustment.cc:276-286).
+//
+// One lane per residual block; blocks are point-major so the point-side
+// normal-equation blocks reduce inside a wavefront (segmented Hillis-Steele
+// scan over 64 lanes, atomics only for the two segments that may straddle a
+// wave boundary).  Camera-side reductions run over image-aligned tiles of a
+// camera-major permutation (one atomic flush per tile and value).
+#include <hip/hip_runtime.h>
+
+#include "ba_math.h"
+#include "device.h"
+#include "kernels.h"
+
+namespace miba {
+
+namespace {
+
+constexpr int kSymPose = 21;  // packed upper triangle of 6x6
+
+__host__ __device__ constexpr int sym_size(int n) { return n * (n + 1) / 2; }
+
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Reduce NV per-thread values over the workgroup; result in sred[0..NV).
+template <int NV>
+__device__ inline void block_reduce(double (&v)[NV], double* sred) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const double s = wave_sum(v[k]);
+    if (lane == 0) sred[wid * NV + k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    const int k = threadIdx.x;
+    sred[k] = sred[k] + sred[NV + k] + sred[2 * NV + k] + sred[3 * NV + k];
+  }
+  __syncthreads();
+}
+
+__device__ inline double block_sum(double v, double* sred) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) sred[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) s = sred[0] + sred[1] + sred[2] + sred[3];
+  __syncthreads();
+  return s;
+}
+
+// Segmented sum over runs of equal key in the wavefront; the run's tail lane
+// stores (interior run) or atomically adds (run touching a wave boundary).
+template <int NV>
+__device__ inline void wave_segmented_store(uint32_t key, bool store, double (&v)[NV], double* dst_base) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t prev = __shfl_up(key, 1, 64);
+  const bool head = (lane == 0) || prev != key;
+  const uint64_t heads = __ballot(head);
+  const uint64_t upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+  const int head_lane = 63 - __clzll(heads & upto);
+  const int idx = lane - head_lane;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const double o = __shfl_up(v[k], off, 64);
+      if (idx >= off) v[k] += o;
+    }
+  }
+  const uint32_t next = __shfl_down(key, 1, 64);
+  const bool tail = (lane == 63) || next != key;
+  if (tail && store) {
+    double* dst = dst_base + (size_t)key * NV;
+    if (head_lane > 0 && lane < 63) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) dst[k] = v[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) atomicAdd(dst + k, v[k]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Residual + Jacobian of one block (analytic, loss-corrected).
+// ---------------------------------------------------------------------------
+template <int M>
+struct BlockEval {
+  double r[2];
+  double jr[2][9];   // rot(3) trans(3) point(3)
+  double jc[2][8];   // refined intrinsics (first ct used)
+  double cost;
+};
+
+template <int M, bool WITH_J>
+__device__ inline void eval_block(const DevProblem& p, const double* __restrict__ qt_all,
+                                  const double* __restrict__ cam_all, const double* __restrict__ X_all,
+                                  int64_t i, BlockEval<M>& e, uint32_t& pt_out, bool& pt_var_out) {
+  constexpr int np = Model<M>::kNumParams;
+  const double2 o = p.obs_xy[i];
+  const uint32_t img = p.obs_img[i];
+  const uint32_t pt = p.obs_pt[i];
+  pt_out = pt;
+  const double* qt = qt_all + 8 * (size_t)img;
+  const double q[4] = {qt[0], qt[1], qt[2], qt[3]};
+  const double t[3] = {qt[4], qt[5], qt[6]};
+  const uint32_t cam_idx = p.img_cam[img];
+  const double* pc = cam_all + 8 * (size_t)cam_idx;
+  double prm[np];
+#pragma unroll
+  for (int k = 0; k < np; ++k) prm[k] = pc[k];
+  const double X[3] = {X_all[3 * (size_t)pt], X_all[3 * (size_t)pt + 1], X_all[3 * (size_t)pt + 2]};
+  double P[3];
+  unit_quat_rotate(q, X, P);
+  P[0] += t[0];
+  P[1] += t[1];
+  P[2] += t[2];
+  const double iz = 1.0 / P[2];
+  const double u = P[0] * iz, v = P[1] * iz;
+  double x, y, A[4], Jp[2 * np];
+  if constexpr (WITH_J) {
+    world_to_image_jac<M>(prm, u, v, &x, &y, A, Jp);
+  } else {
+    world_to_image<M>(prm, u, v, &x, &y);
+  }
+  double r0 = x - o.x, r1 = y - o.y;
+  double rho[3];
+  loss_eval(p.loss_type, p.loss_scale, r0 * r0 + r1 * r1, rho);
+  e.cost = 0.5 * rho[0];
+  // Ceres Corrector, rho'' <= 0 branch (Trivial/SoftL1/Cauchy): scale r, J by sqrt(rho').
+  const double sc = (p.loss_type == kLossTrivial) ? 1.0 : sqrt(rho[1]);
+  e.r[0] = r0 * sc;
+  e.r[1] = r1 * sc;
+  pt_var_out = p.pt_var[pt] != 0;
+  if constexpr (WITH_J) {
+    // B = d(x,y)/dP (2x3) = A * d(u,v)/dP
+    double B[6];
+    B[0] = A[0] * iz; B[1] = A[1] * iz; B[2] = -(A[0] * u + A[1] * v) * iz;
+    B[3] = A[2] * iz; B[4] = A[3] * iz; B[5] = -(A[2] * u + A[3] * v) * iz;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) B[k] *= sc;
+    const uint32_t flags = p.img_flags[img];
+    const bool pose_var = flags & 1u;
+    if (pose_var) {
+      double Dq[12], PJ[12], Mq[9];
+      unit_quat_rotate_dq(q, X, Dq);
+      quat_plus_jacobian(q, PJ);
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+          Mq[a * 3 + b] = Dq[a * 4 + 0] * PJ[0 * 3 + b] + Dq[a * 4 + 1] * PJ[1 * 3 + b] +
+                          Dq[a * 4 + 2] * PJ[2 * 3 + b] + Dq[a * 4 + 3] * PJ[3 * 3 + b];
+#pragma unroll
+      for (int row = 0; row < 2; ++row) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+          e.jr[row][b] = B[row * 3 + 0] * Mq[b] + B[row * 3 + 1] * Mq[3 + b] + B[row * 3 + 2] * Mq[6 + b];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) e.jr[row][3 + b] = ((flags >> (1 + b)) & 1u) ? 0.0 : B[row * 3 + b];
+      }
+    } else {
+#pragma unroll
+      for (int row = 0; row < 2; ++row)
+#pragma unroll
+        for (int b = 0; b < 6; ++b) e.jr[row][b] = 0.0;
+    }
+    if (pt_var_out) {
+      double R[9];
+      unit_quat_matrix(q, R);
+#pragma unroll
+      for (int row = 0; row < 2; ++row)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+          e.jr[row][6 + b] = B[row * 3 + 0] * R[b] + B[row * 3 + 1] * R[3 + b] + B[row * 3 + 2] * R[6 + b];
+    } else {
+#pragma unroll
+      for (int row = 0; row < 2; ++row)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) e.jr[row][6 + b] = 0.0;
+    }
+    const bool cv = p.cam_var[cam_idx] != 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      double c0 = 0.0, c1 = 0.0;
+      if (k < p.ct && cv) {
+        // select refined intrinsic k (SubsetManifold PlusJacobian = selection)
+#pragma unroll
+        for (int m = 0; m < np; ++m) {
+          if (m == p.cam_tan_idx[k]) {
+            c0 = Jp[m] * sc;
+            c1 = Jp[np + m] * sc;
+          }
+        }
+      }
+      e.jc[0][k] = c0;
+      e.jc[1][k] = c1;
+    }
+  }
+}
+
+template <int M>
+__global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
+                                                                  double* __restrict__ J_out,
+                                                                  double* __restrict__ Vg,
+                                                                  double* __restrict__ cost_partial,
+                                                                  int write_jacobian) {
+  __shared__ double sred[4];
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double cost = 0.0;
+  uint32_t key = 0xffffffffu;
+  bool ptv = false;
+  double vg[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) vg[k] = 0.0;
+  if (i < p.nb) {
+    BlockEval<M> e;
+    eval_block<M, true>(p, p.qt, p.cam, p.X, i, e, key, ptv);
+    cost = e.cost;
+    if (write_jacobian) {
+      r_out[i] = make_double2(e.r[0], e.r[1]);
+      double* dst = J_out + (size_t)i * 2 * p.W;
+#pragma unroll
+      for (int row = 0; row < 2; ++row) {
+        double* d = dst + row * p.W;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) d[k] = e.jr[row][k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k < p.ct) d[9 + k] = e.jc[row][k];
+      }
+    }
+    if (ptv) {
+      const double* a = e.jr[0] + 6;
+      const double* b = e.jr[1] + 6;
+      vg[0] = a[0] * a[0] + b[0] * b[0];
+      vg[1] = a[0] * a[1] + b[0] * b[1];
+      vg[2] = a[0] * a[2] + b[0] * b[2];
+      vg[3] = a[1] * a[1] + b[1] * b[1];
+      vg[4] = a[1] * a[2] + b[1] * b[2];
+      vg[5] = a[2] * a[2] + b[2] * b[2];
+      vg[6] = a[0] * e.r[0] + b[0] * e.r[1];
+      vg[7] = a[1] * e.r[0] + b[1] * e.r[1];
+      vg[8] = a[2] * e.r[0] + b[2] * e.r[1];
+    }
+  }
+  wave_segmented_store<9>(key, ptv, vg, Vg);
+  const double s = block_sum(cost, sred);
+  if (threadIdx.x == 0) cost_partial[blockIdx.x] = s;
+}
+
+template <int M>
+__global__ __launch_bounds__(kBlock) void reproj_cost_kernel(DevProblem p, const double* __restrict__ qt,
+                                                              const double* __restrict__ cam,
+                                                              const double* __restrict__ X,
+                                                              double* __restrict__ cost_partial) {
+  __shared__ double sred[4];
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double cost = 0.0;
+  if (i < p.nb) {
+    BlockEval<M> e;
+    uint32_t pt;
+    bool ptv;
+    eval_block<M, false>(p, qt, cam, X, i, e, pt, ptv);
+    cost = e.cost;
+  }
+  const double s = block_sum(cost, sred);
+  if (threadIdx.x == 0) cost_partial[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(1024) void sum_kernel(const double* __restrict__ partial, int64_t n,
+                                                   double* __restrict__ out) {
+  __shared__ double sred[16];
+  double v = 0.0;
+  for (int64_t k = threadIdx.x; k < n; k += 1024) v += partial[k];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int k = 0; k < 16; ++k) s += sred[k];
+    out[0] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Point side
+// ---------------------------------------------------------------------------
+__device__ inline void sym3_inverse(const double a[6], double inv[6]) {
+  // a = [xx xy xz yy yz zz]
+  const double c00 = a[3] * a[5] - a[4] * a[4];
+  const double c01 = a[2] * a[4] - a[1] * a[5];
+  const double c02 = a[1] * a[4] - a[2] * a[3];
+  const double det = a[0] * c00 + a[1] * c01 + a[2] * c02;
+  const double id = 1.0 / det;
+  inv[0] = c00 * id;
+  inv[1] = c01 * id;
+  inv[2] = c02 * id;
+  inv[3] = (a[0] * a[5] - a[2] * a[2]) * id;
+  inv[4] = (a[1] * a[2] - a[0] * a[4]) * id;
+  inv[5] = (a[0] * a[3] - a[1] * a[1]) * id;
+}
+
+__device__ inline void sym3_mul(const double s[6], const double x[3], double y[3]) {
+  y[0] = s[0] * x[0] + s[1] * x[1] + s[2] * x[2];
+  y[1] = s[1] * x[0] + s[3] * x[1] + s[4] * x[2];
+  y[2] = s[2] * x[0] + s[4] * x[1] + s[5] * x[2];
+}
+
+__global__ __launch_bounds__(kBlock) void point_prepare_kernel(const DevPoint* __restrict__ vp, int64_t npv,
+                                                                const double* __restrict__ Vg,
+                                                                double* __restrict__ scale_p,
+                                                                double* __restrict__ diag_p,
+                                                                double* __restrict__ Vinv, int first,
+                                                                int reuse_diag, double radius) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= npv) return;
+  const uint32_t pt = vp[k].point;
+  const double* g = Vg + 9 * (size_t)pt;
+  double V[6] = {g[0], g[1], g[2], g[3], g[4], g[5]};
+  const double dg[3] = {V[0], V[3], V[5]};
+  const int di[3] = {0, 3, 5};
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    double s;
+    if (first) {
+      s = 1.0 / (1.0 + sqrt(dg[m]));
+      scale_p[3 * (size_t)pt + m] = s;
+    } else {
+      s = scale_p[3 * (size_t)pt + m];
+    }
+    double d;
+    if (!reuse_diag) {
+      d = fmin(fmax(s * s * dg[m], 1e-6), 1e32);
+      diag_p[3 * (size_t)pt + m] = d;
+    } else {
+      d = diag_p[3 * (size_t)pt + m];
+    }
+    V[di[m]] += d / (radius * s * s);
+  }
+  double inv[6];
+  sym3_inverse(V, inv);
+#pragma unroll
+  for (int m = 0; m < 6; ++m) Vinv[6 * (size_t)pt + m] = inv[m];
+}
+
+// ---------------------------------------------------------------------------
+// Camera side: tile pass building the Schur-Jacobi diagonal blocks and rhs.
+// ---------------------------------------------------------------------------
+template <int CT>
+__global__ __launch_bounds__(kBlock) void fblock_kernel(DevProblem p, const DevTile* __restrict__ tiles,
+                                                         const uint32_t* __restrict__ cm_perm,
+                                                         const double2* __restrict__ rr,
+                                                         const double* __restrict__ J,
+                                                         const double* __restrict__ Vg,
+                                                         const double* __restrict__ Vinv,
+                                                         double* __restrict__ pose_blk,
+                                                         double* __restrict__ cam_blk,
+                                                         double* __restrict__ bvec,
+                                                         double* __restrict__ udiag) {
+  constexpr int NC = sym_size(CT);
+  constexpr int NV = kSymPose + 6 + 6 + NC + 2 * CT;
+  __shared__ double sred[4 * NV];
+  const DevTile tile = tiles[blockIdx.x];
+  const int W = 9 + CT;
+  double acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+  for (uint32_t k = threadIdx.x; k < tile.count; k += kBlock) {
+    const uint32_t b = cm_perm[tile.start + k];
+    const double* Jb = J + (size_t)b * 2 * W;
+    const double2 r = rr[b];
+    double jf[2][6 + CT], jx[2][3];
+#pragma unroll
+    for (int row = 0; row < 2; ++row) {
+#pragma unroll
+      for (int m = 0; m < 6; ++m) jf[row][m] = Jb[row * W + m];
+#pragma unroll
+      for (int m = 0; m < 3; ++m) jx[row][m] = Jb[row * W + 6 + m];
+#pragma unroll
+      for (int m = 0; m < CT; ++m) jf[row][6 + m] = Jb[row * W + 9 + m];
+    }
+    const double rv[2] = {r.x, r.y};
+    // g, U (diag blocks) contributions
+    double g[6 + CT];
+#pragma unroll
+    for (int m = 0; m < 6 + CT; ++m) g[m] = jf[0][m] * rv[0] + jf[1][m] * rv[1];
+    const uint32_t pt = p.obs_pt[b];
+    double Y[6 + CT][3];
+    double Yg[6 + CT];
+    const bool ptv = p.pt_var[pt] != 0;
+    if (ptv) {
+      double Wm[6 + CT][3];
+#pragma unroll
+      for (int m = 0; m < 6 + CT; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n) Wm[m][n] = jf[0][m] * jx[0][n] + jf[1][m] * jx[1][n];
+      const double* vi = Vinv + 6 * (size_t)pt;
+      const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
+      const double* gp = Vg + 9 * (size_t)pt + 6;
+      const double gpv[3] = {gp[0], gp[1], gp[2]};
+#pragma unroll
+      for (int m = 0; m < 6 + CT; ++m) {
+        sym3_mul(Vi, Wm[m], Y[m]);
+        Yg[m] = Y[m][0] * gpv[0] + Y[m][1] * gpv[1] + Y[m][2] * gpv[2];
+      }
+      // Schur diagonal blocks: U - Y W'
+      int o = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int c = a; c < 6; ++c, ++o)
+          acc[o] += jf[0][a] * jf[0][c] + jf[1][a] * jf[1][c] -
+                    (Y[a][0] * Wm[c][0] + Y[a][1] * Wm[c][1] + Y[a][2] * Wm[c][2]);
+      o = kSymPose + 12;
+#pragma unroll
+      for (int a = 0; a < CT; ++a)
+#pragma unroll
+        for (int c = a; c < CT; ++c, ++o)
+          acc[o] += jf[0][6 + a] * jf[0][6 + c] + jf[1][6 + a] * jf[1][6 + c] -
+                    (Y[6 + a][0] * Wm[6 + c][0] + Y[6 + a][1] * Wm[6 + c][1] + Y[6 + a][2] * Wm[6 + c][2]);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 6 + CT; ++m) Yg[m] = 0.0;
+      int o = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int c = a; c < 6; ++c, ++o) acc[o] += jf[0][a] * jf[0][c] + jf[1][a] * jf[1][c];
+      o = kSymPose + 12;
+#pragma unroll
+      for (int a = 0; a < CT; ++a)
+#pragma unroll
+        for (int c = a; c < CT; ++c, ++o) acc[o] += jf[0][6 + a] * jf[0][6 + c] + jf[1][6 + a] * jf[1][6 + c];
+    }
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+      acc[kSymPose + m] += g[m] - Yg[m];
+      acc[kSymPose + 6 + m] += jf[0][m] * jf[0][m] + jf[1][m] * jf[1][m];
+    }
+#pragma unroll
+    for (int m = 0; m < CT; ++m) {
+      acc[kSymPose + 12 + NC + m] += g[6 + m] - Yg[6 + m];
+      acc[kSymPose + 12 + NC + CT + m] += jf[0][6 + m] * jf[0][6 + m] + jf[1][6 + m] * jf[1][6 + m];
+    }
+  }
+  block_reduce<NV>(acc, sred);
+  const int k = threadIdx.x;
+  if (k < NV) {
+    const uint32_t img = tile.image;
+    const uint32_t cam = p.img_cam[img];
+    const bool pose_var = p.img_flags[img] & 1u;
+    const bool cam_var = p.cam_var[cam] != 0;
+    const double v = sred[k];
+    if (k < kSymPose) {
+      if (pose_var) atomicAdd(pose_blk + (size_t)img * kSymPose + k, v);
+    } else if (k < kSymPose + 6) {
+      if (pose_var) atomicAdd(bvec + 6 * (size_t)img + (k - kSymPose), v);
+    } else if (k < kSymPose + 12) {
+      if (pose_var) atomicAdd(udiag + 6 * (size_t)img + (k - kSymPose - 6), v);
+    } else if (k < kSymPose + 12 + NC) {
+      if (cam_var) atomicAdd(cam_blk + (size_t)cam * NC + (k - kSymPose - 12), v);
+    } else if (k < kSymPose + 12 + NC + CT) {
+      if (cam_var) atomicAdd(bvec + 6 * (size_t)p.num_images + (size_t)CT * cam + (k - kSymPose - 12 - NC), v);
+    } else {
+      if (cam_var)
+        atomicAdd(udiag + 6 * (size_t)p.num_images + (size_t)CT * cam + (k - kSymPose - 12 - NC - CT), v);
+    }
+  }
+}
+
+// Damp, Jacobi-scale and invert the diagonal blocks (one thread per block).
+template <int N>
+__device__ inline void chol_inverse(double (&A)[N][N], double (&Ainv)[N][N]) {
+  // in-place Cholesky (lower), then inverse via L^-1
+  double L[N][N];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) L[i][j] = 0.0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double d = A[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
+    d = sqrt(fmax(d, 1e-300));
+    L[j][j] = d;
+    const double id = 1.0 / d;
+#pragma unroll
+    for (int i = j + 1; i < N; ++i) {
+      double v = A[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k];
+      L[i][j] = v * id;
+    }
+  }
+  // Linv (lower)
+  double Li[N][N];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) Li[i][j] = 0.0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    Li[i][i] = 1.0 / L[i][i];
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int k = j; k < i; ++k) v -= L[i][k] * Li[k][j];
+      Li[i][j] = v * Li[i][i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) v += Li[k][i] * Li[k][j];
+      Ainv[i][j] = v;
+    }
+}
+
+template <int N>
+__device__ void finalize_block(const double* __restrict__ blk, const double* __restrict__ udiag,
+                               double* __restrict__ scale_f, double* __restrict__ diag_f,
+                               double* __restrict__ lambda_f, double* __restrict__ prec, double* __restrict__ b,
+                               bool var, int first, int reuse_diag, double radius) {
+  double A[N][N], Ai[N][N];
+  int o = 0;
+#pragma unroll
+  for (int a = 0; a < N; ++a)
+#pragma unroll
+    for (int c = a; c < N; ++c, ++o) {
+      A[a][c] = var ? blk[o] : 0.0;
+      A[c][a] = A[a][c];
+    }
+#pragma unroll
+  for (int m = 0; m < N; ++m) {
+    if (!var) {
+      scale_f[m] = 1.0;
+      diag_f[m] = 0.0;
+      lambda_f[m] = 0.0;
+      A[m][m] = 1.0;
+      b[m] = 0.0;
+      continue;
+    }
+    double s;
+    if (first) {
+      s = 1.0 / (1.0 + sqrt(udiag[m]));
+      scale_f[m] = s;
+    } else {
+      s = scale_f[m];
+    }
+    double d;
+    if (!reuse_diag) {
+      d = fmin(fmax(s * s * udiag[m], 1e-6), 1e32);
+      diag_f[m] = d;
+    } else {
+      d = diag_f[m];
+    }
+    const double lam = d / (radius * s * s);
+    lambda_f[m] = lam;
+    A[m][m] += lam;
+    b[m] = -b[m];
+  }
+  chol_inverse<N>(A, Ai);
+#pragma unroll
+  for (int a = 0; a < N; ++a)
+#pragma unroll
+    for (int c = 0; c < N; ++c) prec[a * N + c] = var ? Ai[a][c] : (a == c ? 1.0 : 0.0);
+}
+
+template <int CT>
+__global__ __launch_bounds__(64) void fblock_finalize_kernel(DevProblem p, const double* __restrict__ pose_blk,
+                                                              const double* __restrict__ cam_blk,
+                                                              const double* __restrict__ udiag,
+                                                              double* __restrict__ scale_f,
+                                                              double* __restrict__ diag_f,
+                                                              double* __restrict__ lambda_f,
+                                                              double* __restrict__ prec_pose,
+                                                              double* __restrict__ prec_cam,
+                                                              double* __restrict__ b, int first,
+                                                              int reuse_diag, double radius) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  const int I = p.num_images, C = p.num_cameras;
+  if (k < I) {
+    const bool var = p.img_flags[k] & 1u;
+    const size_t o = 6 * (size_t)k;
+    finalize_block<6>(pose_blk + (size_t)k * kSymPose, udiag + o, scale_f + o, diag_f + o, lambda_f + o,
+                      prec_pose + 36 * (size_t)k, b + o, var, first, reuse_diag, radius);
+  } else if (CT > 0 && k < I + C) {
+    const int c = k - I;
+    const bool var = p.cam_var[c] != 0;
+    const size_t o = 6 * (size_t)I + (size_t)CT * c;
+    finalize_block<(CT > 0 ? CT : 1)>(cam_blk + (size_t)c * sym_size(CT), udiag + o, scale_f + o, diag_f + o,
+                                      lambda_f + o, prec_cam + (size_t)CT * CT * c, b + o, var, first,
+                                      reuse_diag, radius);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Implicit Schur product y = (U + Lambda_f) x - W V^-1 W' x
+// ---------------------------------------------------------------------------
+template <int CT>
+__device__ inline void load_jf_x(const DevProblem& p, const double* __restrict__ Jb, uint32_t img,
+                                 const double* __restrict__ x, double e[2]) {
+  const int W = 9 + CT;
+  const double* xi = x + 6 * (size_t)img;
+  const uint32_t cam = p.img_cam[img];
+  const double* xc = x + 6 * (size_t)p.num_images + (size_t)CT * cam;
+  double xv[6 + CT];
+#pragma unroll
+  for (int m = 0; m < 6; ++m) xv[m] = xi[m];
+#pragma unroll
+  for (int m = 0; m < CT; ++m) xv[6 + m] = xc[m];
+#pragma unroll
+  for (int row = 0; row < 2; ++row) {
+    double s = 0.0;
+#pragma unroll
+    for (int m = 0; m < 6; ++m) s += Jb[row * W + m] * xv[m];
+#pragma unroll
+    for (int m = 0; m < CT; ++m) s += Jb[row * W + 9 + m] * xv[6 + m];
+    e[row] = s;
+  }
+}
+
+template <int CT>
+__global__ __launch_bounds__(kBlock) void schur_point_pass(DevProblem p, const DevPoint* __restrict__ vp,
+                                                            int64_t npv, const double* __restrict__ J,
+                                                            const double* __restrict__ Vinv,
+                                                            const double* __restrict__ x,
+                                                            double* __restrict__ w) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= npv) return;
+  const DevPoint d = vp[k];
+  const int W = 9 + CT;
+  double t[3] = {0.0, 0.0, 0.0};
+  for (uint32_t m = 0; m < d.count; ++m) {
+    const uint32_t b = d.start + m;
+    const double* Jb = J + (size_t)b * 2 * W;
+    double e[2];
+    load_jf_x<CT>(p, Jb, p.obs_img[b], x, e);
+#pragma unroll
+    for (int n = 0; n < 3; ++n) t[n] += Jb[6 + n] * e[0] + Jb[W + 6 + n] * e[1];
+  }
+  const double* vi = Vinv + 6 * (size_t)d.point;
+  const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
+  double wv[3];
+  sym3_mul(Vi, t, wv);
+#pragma unroll
+  for (int n = 0; n < 3; ++n) w[3 * (size_t)d.point + n] = wv[n];
+}
+
+template <int CT>
+__global__ __launch_bounds__(kBlock) void schur_f_pass(DevProblem p, const DevTile* __restrict__ tiles,
+                                                        const uint32_t* __restrict__ cm_perm,
+                                                        const double* __restrict__ J,
+                                                        const double* __restrict__ x,
+                                                        const double* __restrict__ w,
+                                                        double* __restrict__ y) {
+  constexpr int NV = 6 + CT;
+  __shared__ double sred[4 * NV];
+  const DevTile tile = tiles[blockIdx.x];
+  const int W = 9 + CT;
+  double acc[NV];
+#pragma unroll
+  for (int m = 0; m < NV; ++m) acc[m] = 0.0;
+  for (uint32_t k = threadIdx.x; k < tile.count; k += kBlock) {
+    const uint32_t b = cm_perm[tile.start + k];
+    const double* Jb = J + (size_t)b * 2 * W;
+    double e[2];
+    load_jf_x<CT>(p, Jb, tile.image, x, e);
+    const uint32_t pt = p.obs_pt[b];
+    if (p.pt_var[pt]) {
+      const double wv[3] = {w[3 * (size_t)pt], w[3 * (size_t)pt + 1], w[3 * (size_t)pt + 2]};
+#pragma unroll
+      for (int row = 0; row < 2; ++row)
+        e[row] -= Jb[row * W + 6] * wv[0] + Jb[row * W + 7] * wv[1] + Jb[row * W + 8] * wv[2];
+    }
+#pragma unroll
+    for (int m = 0; m < 6; ++m) acc[m] += Jb[m] * e[0] + Jb[W + m] * e[1];
+#pragma unroll
+    for (int m = 0; m < CT; ++m) acc[6 + m] += Jb[9 + m] * e[0] + Jb[W + 9 + m] * e[1];
+  }
+  block_reduce<NV>(acc, sred);
+  const int k = threadIdx.x;
+  if (k < NV) {
+    const uint32_t img = tile.image;
+    if (k < 6) {
+      if (p.img_flags[img] & 1u) atomicAdd(y + 6 * (size_t)img + k, sred[k]);
+    } else {
+      const uint32_t cam = p.img_cam[img];
+      if (p.cam_var[cam]) atomicAdd(y + 6 * (size_t)p.num_images + (size_t)CT * cam + (k - 6), sred[k]);
+    }
+  }
+}
+
+__global__ void add_diag_kernel(const double* __restrict__ lambda_f, const double* __restrict__ x,
+                                double* __restrict__ y, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k < n) y[k] += lambda_f[k] * x[k];
+}
+
+template <int CT>
+__global__ void precond_kernel(DevProblem p, const double* __restrict__ prec_pose,
+                               const double* __restrict__ prec_cam, const double* __restrict__ r,
+                               double* __restrict__ z) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  const int I = p.num_images, C = p.num_cameras;
+  if (k < I) {
+    const double* M = prec_pose + 36 * (size_t)k;
+    const double* rv = r + 6 * (size_t)k;
+    double rr[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) rr[m] = rv[m];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) s += M[a * 6 + c] * rr[c];
+      z[6 * (size_t)k + a] = s;
+    }
+  } else if (CT > 0 && k < I + C) {
+    const int c0 = k - I;
+    const double* M = prec_cam + (size_t)CT * CT * c0;
+    const size_t o = 6 * (size_t)I + (size_t)CT * c0;
+    double rr[CT > 0 ? CT : 1];
+#pragma unroll
+    for (int m = 0; m < CT; ++m) rr[m] = r[o + m];
+#pragma unroll
+    for (int a = 0; a < CT; ++a) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) s += M[a * CT + c] * rr[c];
+      z[o + a] = s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void dot_kernel(const double* __restrict__ a, const double* __restrict__ b,
+                                                   int64_t n, double* __restrict__ out) {
+  __shared__ double sred[16];
+  double v = 0.0;
+  for (int64_t k = threadIdx.x; k < n; k += 1024) v += a[k] * b[k];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int k = 0; k < 16; ++k) s += sred[k];
+    out[0] = s;
+  }
+}
+
+__global__ void axpy_kernel(double* __restrict__ y, const double* __restrict__ x, const double* num,
+                            const double* den, double sign, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k < n) y[k] += sign * (num[0] / den[0]) * x[k];
+}
+
+__global__ void xpby_kernel(double* __restrict__ pv, const double* __restrict__ z, const double* num,
+                            const double* den, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k < n) pv[k] = z[k] + (num[0] / den[0]) * pv[k];
+}
+
+template <int CT>
+__global__ __launch_bounds__(kBlock) void backsub_kernel(DevProblem p, const DevPoint* __restrict__ vp,
+                                                          int64_t npv, const double* __restrict__ J,
+                                                          const double* __restrict__ Vg,
+                                                          const double* __restrict__ Vinv,
+                                                          const double* __restrict__ df,
+                                                          double* __restrict__ dX) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= npv) return;
+  const DevPoint d = vp[k];
+  const int W = 9 + CT;
+  const double* g = Vg + 9 * (size_t)d.point + 6;
+  double t[3] = {g[0], g[1], g[2]};
+  for (uint32_t m = 0; m < d.count; ++m) {
+    const uint32_t b = d.start + m;
+    const double* Jb = J + (size_t)b * 2 * W;
+    double e[2];
+    load_jf_x<CT>(p, Jb, p.obs_img[b], df, e);
+#pragma unroll
+    for (int n = 0; n < 3; ++n) t[n] += Jb[6 + n] * e[0] + Jb[W + 6 + n] * e[1];
+  }
+  const double* vi = Vinv + 6 * (size_t)d.point;
+  const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
+  double o[3];
+  sym3_mul(Vi, t, o);
+#pragma unroll
+  for (int n = 0; n < 3; ++n) dX[3 * (size_t)d.point + n] = -o[n];
+}
+
+template <int CT>
+__global__ __launch_bounds__(kBlock) void model_cost_kernel(DevProblem p, const double2* __restrict__ rr,
+                                                             const double* __restrict__ J,
+                                                             const double* __restrict__ df,
+                                                             const double* __restrict__ dX,
+                                                             double* __restrict__ partial) {
+  __shared__ double sred[4];
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double v = 0.0;
+  if (i < p.nb) {
+    const int W = 9 + CT;
+    const double* Jb = J + (size_t)i * 2 * W;
+    double e[2];
+    load_jf_x<CT>(p, Jb, p.obs_img[i], df, e);
+    const uint32_t pt = p.obs_pt[i];
+    if (p.pt_var[pt]) {
+      const double dx[3] = {dX[3 * (size_t)pt], dX[3 * (size_t)pt + 1], dX[3 * (size_t)pt + 2]};
+#pragma unroll
+      for (int row = 0; row < 2; ++row)
+        e[row] += Jb[row * W + 6] * dx[0] + Jb[row * W + 7] * dx[1] + Jb[row * W + 8] * dx[2];
+    }
+    const double2 r = rr[i];
+    v = -(e[0] * (r.x + e[0] / 2.0) + e[1] * (r.y + e[1] / 2.0));
+  }
+  const double s = block_sum(v, sred);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+__global__ void plus_images_kernel(DevProblem p, const double* __restrict__ df, const double* __restrict__ qt,
+                                   double* __restrict__ qt_out) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= p.num_images) return;
+  const double* a = qt + 8 * (size_t)k;
+  double* o = qt_out + 8 * (size_t)k;
+  if (!(p.img_flags[k] & 1u)) {
+    for (int m = 0; m < 8; ++m) o[m] = a[m];
+    return;
+  }
+  const double* d = df + 6 * (size_t)k;
+  const double q[4] = {a[0], a[1], a[2], a[3]};
+  const double dr[3] = {d[0], d[1], d[2]};
+  double qn[4];
+  quat_plus(q, dr, qn);
+  o[0] = qn[0]; o[1] = qn[1]; o[2] = qn[2]; o[3] = qn[3];
+  o[4] = a[4] + d[3];
+  o[5] = a[5] + d[4];
+  o[6] = a[6] + d[5];
+  o[7] = 0.0;
+}
+
+__global__ void plus_cameras_kernel(DevProblem p, const double* __restrict__ df, const double* __restrict__ cam,
+                                    double* __restrict__ cam_out) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= p.num_cameras) return;
+  const double* a = cam + 8 * (size_t)k;
+  double* o = cam_out + 8 * (size_t)k;
+  for (int m = 0; m < 8; ++m) o[m] = a[m];
+  if (!p.cam_var[k]) return;
+  const double* d = df + 6 * (size_t)p.num_images + (size_t)p.ct * k;
+  for (int m = 0; m < p.ct; ++m) o[p.cam_tan_idx[m]] = a[p.cam_tan_idx[m]] + d[m];
+}
+
+__global__ void plus_points_kernel(DevProblem p, const double* __restrict__ dX, const double* __restrict__ X,
+                                   double* __restrict__ X_out) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= p.num_points) return;
+  const bool var = p.pt_var[k] != 0;
+#pragma unroll
+  for (int m = 0; m < 3; ++m) X_out[3 * k + m] = X[3 * k + m] + (var ? dX[3 * k + m] : 0.0);
+}
+
+__global__ __launch_bounds__(1024) void sqnorm2_kernel(const double* __restrict__ a, int64_t na,
+                                                       const double* __restrict__ b, int64_t nb2,
+                                                       double* __restrict__ out) {
+  __shared__ double sred[16];
+  double v = 0.0;
+  for (int64_t k = threadIdx.x; k < na; k += 1024) v += a[k] * a[k];
+  for (int64_t k = threadIdx.x; k < nb2; k += 1024) v += b[k] * b[k];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int k = 0; k < 16; ++k) s += sred[k];
+    out[0] = s;
+  }
+}
+
+template <typename F>
+void dispatch_ct(int ct, F&& f) {
+  switch (ct) {
+    case 0: f(std::integral_constant<int, 0>{}); break;
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    case 6: f(std::integral_constant<int, 6>{}); break;
+    case 7: f(std::integral_constant<int, 7>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    default: break;
+  }
+}
+
+inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+}  // namespace
+
+int reproj_grid(int64_t nb) { return (int)grid_for(nb, kBlock); }
+
+void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* Vg, double* cost_partial,
+                            int write_jacobian, hipStream_t s) {
+  if (p.nb == 0) return;
+  const unsigned g = grid_for(p.nb, kBlock);
+  dispatch_model(p.model, [&](auto m) {
+    constexpr int M = decltype(m)::value;
+    hipLaunchKernelGGL(reproj_jacobian_kernel<M>, dim3(g), dim3(kBlock), 0, s, p, r, J, Vg, cost_partial,
+                       write_jacobian);
+  });
+}
+
+void launch_reproj_cost(const DevProblem& p, const double* qt, const double* cam, const double* X,
+                        double* cost_partial, hipStream_t s) {
+  if (p.nb == 0) return;
+  const unsigned g = grid_for(p.nb, kBlock);
+  dispatch_model(p.model, [&](auto m) {
+    constexpr int M = decltype(m)::value;
+    hipLaunchKernelGGL(reproj_cost_kernel<M>, dim3(g), dim3(kBlock), 0, s, p, qt, cam, X, cost_partial);
+  });
+}
+
+void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, s, partial, n, out);
+}
+
+void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg,
+                          double* scale_p, double* diag_p, double* Vinv, int first, int reuse_diag,
+                          double radius, hipStream_t s) {
+  if (npv == 0) return;
+  hipLaunchKernelGGL(point_prepare_kernel, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, vp, npv, Vg,
+                     scale_p, diag_p, Vinv, first, reuse_diag, radius);
+}
+
+void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
+                   const double2* r, const double* J, const double* Vg, const double* Vinv, double* pose_blk,
+                   double* cam_blk, double* b, double* udiag, hipStream_t s) {
+  if (ntiles == 0) return;
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    hipLaunchKernelGGL(fblock_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, Vg, Vinv,
+                       pose_blk, cam_blk, b, udiag);
+  });
+}
+
+void launch_fblock_finalize(const DevProblem& p, const double* pose_blk, const double* cam_blk,
+                            const double* udiag, double* scale_f, double* diag_f, double* lambda_f,
+                            double* prec_pose, double* prec_cam, double* b, int first, int reuse_diag,
+                            double radius, hipStream_t s) {
+  const int n = p.num_images + p.num_cameras;
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    hipLaunchKernelGGL(fblock_finalize_kernel<CT>, dim3(grid_for(n, 64)), dim3(64), 0, s, p, pose_blk, cam_blk,
+                       udiag, scale_f, diag_f, lambda_f, prec_pose, prec_cam, b, first, reuse_diag, radius);
+  });
+}
+
+void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles,
+                          int ntiles, const uint32_t* cm_perm, const double* J, const double* Vinv,
+                          const double* lambda_f, const double* x, double* w, double* y, hipStream_t s) {
+  (void)hipMemsetAsync(y, 0, sizeof(double) * p.nf, s);
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    if (npv > 0)
+      hipLaunchKernelGGL(schur_point_pass<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, J,
+                         Vinv, x, w);
+    if (ntiles > 0)
+      hipLaunchKernelGGL(schur_f_pass<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, J, x, w, y);
+  });
+  hipLaunchKernelGGL(add_diag_kernel, dim3(grid_for(p.nf, kBlock)), dim3(kBlock), 0, s, lambda_f, x, y, p.nf);
+}
+
+void launch_precond(const DevProblem& p, const double* prec_pose, const double* prec_cam, const double* r,
+                    double* z, hipStream_t s) {
+  const int n = p.num_images + p.num_cameras;
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    hipLaunchKernelGGL(precond_kernel<CT>, dim3(grid_for(n, 64)), dim3(64), 0, s, p, prec_pose, prec_cam, r, z);
+  });
+}
+
+void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(dot_kernel, dim3(1), dim3(1024), 0, s, a, b, n, out);
+}
+
+void launch_axpy(double* y, const double* x, const double* num, const double* den, double sign, int64_t n,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(axpy_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, y, x, num, den, sign, n);
+}
+
+void launch_xpby(double* pv, const double* z, const double* num, const double* den, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(xpby_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, pv, z, num, den, n);
+}
+
+void launch_backsub(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* J, const double* Vg,
+                    const double* Vinv, const double* df, double* dX, hipStream_t s) {
+  if (npv == 0) return;
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    hipLaunchKernelGGL(backsub_kernel<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, J, Vg,
+                       Vinv, df, dX);
+  });
+}
+
+void launch_model_cost(const DevProblem& p, const double2* r, const double* J, const double* df, const double* dX,
+                       double* partial, hipStream_t s) {
+  if (p.nb == 0) return;
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    hipLaunchKernelGGL(model_cost_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, r, J, df, dX,
+                       partial);
+  });
+}
+
+void launch_plus(const DevProblem& p, const double* df, const double* dX, const double* qt, const double* cam,
+                 const double* X, double* qt_out, double* cam_out, double* X_out, hipStream_t s) {
+  hipLaunchKernelGGL(plus_images_kernel, dim3(grid_for(p.num_images, 64)), dim3(64), 0, s, p, df, qt, qt_out);
+  hipLaunchKernelGGL(plus_cameras_kernel, dim3(grid_for(p.num_cameras, 64)), dim3(64), 0, s, p, df, cam, cam_out);
+  if (p.num_points > 0)
+    hipLaunchKernelGGL(plus_points_kernel, dim3(grid_for(p.num_points, kBlock)), dim3(kBlock), 0, s, p, dX, X,
+                       X_out);
+}
+
+void launch_sqnorm2(const double* a, int64_t na, const double* b, int64_t nb2, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(sqnorm2_kernel, dim3(1), dim3(1024), 0, s, a, na, b, nb2, out);
+}
+
+}  // namespace miba

@@ -1,0 +1,786 @@
+// runtime.hip — device-resident problem, LM driver and C-ABI (product code).
+//
+// mi_ba_solve replaces BundleAdjuster::Solve (src/optim/bundle_adjustment.cc:
+// 258-320) including its Ceres 2.1 call: a Levenberg-Marquardt trust-region
+// loop (TrustRegionMinimizer + LevenbergMarquardtStrategy semantics restated:
+// Jacobi scaling fixed at iteration 0, LM diagonal clamped to [1e-6, 1e32],
+// radius update 1/max(1/3, 1-(2q-1)^3), decrease factor doubling, step
+// acceptance at relative decrease > min_relative_decrease) whose linear
+// system is solved by the implicit-Schur PCG of ITERATIVE_SCHUR with the
+// SCHUR_JACOBI preconditioner and Ceres' Nash-Sofer q-termination (eta).
+// No CPU fallback: without an MI355X the entry points return
+// MI_BA_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+
+#include "../../include/mi_ba.h"
+#include "ba_math.h"
+#include "context.h"
+#include "kernels.h"
+#include "semantic.h"
+#include "setup.h"
+
+namespace miba {
+
+namespace {
+
+enum Scalar {
+  kCost = 0, kCandCost = 1, kModelCost = 2, kRho = 3, kRhoPrev = 4, kPQ = 5, kXB = 6, kXR = 7,
+  kStepNorm = 8, kSemCost = 9, kSemCand = 10, kSemModel = 11, kNumScalars = 16
+};
+
+#define MI_HIP(expr)                                     \
+  do {                                                   \
+    hipError_t _e = (expr);                              \
+    if (_e != hipSuccess) {                              \
+      if (_e == hipErrorOutOfMemory) return MI_BA_ERR_OUT_OF_MEMORY; \
+      return MI_BA_ERR_HIP;                              \
+    }                                                    \
+  } while (0)
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Host evaluation of one block's cost (fixed_cost of dropped blocks).
+double host_block_cost(const mi_ba_options& o, const mi_ba_problem* p, int64_t k) {
+  const int img = p->obs_image[k];
+  const int cam = p->image_camera[img];
+  const int64_t pt = p->obs_point[k];
+  const int np = num_params(p->camera_model);
+  const double* q = p->qvec + 4 * (size_t)img;
+  const double* t = p->tvec + 3 * (size_t)img;
+  const double* X = p->xyz + 3 * (size_t)pt;
+  const double* prm = p->camera_params + (size_t)np * cam;
+  double P[3];
+  unit_quat_rotate(q, X, P);
+  P[0] += t[0]; P[1] += t[1]; P[2] += t[2];
+  const double u = P[0] / P[2], v = P[1] / P[2];
+  double x = 0, y = 0;
+  dispatch_model(p->camera_model, [&](auto m) {
+    constexpr int M = decltype(m)::value;
+    world_to_image<M>(prm, u, v, &x, &y);
+  });
+  const double r0 = x - p->obs_xy[2 * k], r1 = y - p->obs_xy[2 * k + 1];
+  double rho[3];
+  loss_eval(o.loss_function_type, o.loss_function_scale, r0 * r0 + r1 * r1, rho);
+  return 0.5 * rho[0];
+}
+
+mi_ba_status read_scalars(mi_ba_context* ctx, int first, int count) {
+  MI_HIP(hipMemcpyAsync(ctx->host_scalars + first, ctx->scalars.ptr + first, sizeof(double) * count,
+                        hipMemcpyDeviceToHost, ctx->stream));
+  MI_HIP(hipStreamSynchronize(ctx->stream));
+  return MI_BA_OK;
+}
+
+}  // namespace
+
+void timer_begin(mi_ba_context* ctx, const char* name, hipEvent_t* stop_out) {
+  *stop_out = nullptr;
+  if (!ctx->timing) return;
+  hipEvent_t a, b;
+  if (ctx->timer.pool.size() >= 2) {
+    a = ctx->timer.pool.back(); ctx->timer.pool.pop_back();
+    b = ctx->timer.pool.back(); ctx->timer.pool.pop_back();
+  } else {
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+  }
+  (void)hipEventRecord(a, ctx->stream);
+  ctx->timer.pending.push_back({name, {a, b}});
+  *stop_out = b;
+}
+
+void timer_end(mi_ba_context* ctx, hipEvent_t stop) {
+  if (!ctx->timing || !stop) return;
+  (void)hipEventRecord(stop, ctx->stream);
+}
+
+static void timer_collect(mi_ba_context* ctx) {
+  if (ctx->timer.pending.empty()) return;
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& e : ctx->timer.pending) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e.second.first, e.second.second);
+    auto& t = ctx->timer.totals[e.first];
+    t.first += ms;
+    t.second += 1;
+    ctx->timer.pool.push_back(e.second.first);
+    ctx->timer.pool.push_back(e.second.second);
+  }
+  ctx->timer.pending.clear();
+}
+
+mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, const mi_ba_semantic* sem,
+                            mi_ba_context** out) {
+  if (!o || !pin || !out) return MI_BA_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MI_BA_ERR_NO_DEVICE;
+  if (o->device < 0 || o->device >= ndev) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_HIP(hipSetDevice(o->device));
+  auto* ctx = new mi_ba_context();
+  ctx->options = *o;
+  ctx->problem = *pin;
+  ctx->device = o->device;
+  mi_ba_problem* p = &ctx->problem;
+  mi_ba_status st = build_setup(*o, p, &ctx->setup);
+  if (st != MI_BA_OK) { delete ctx; return st; }
+  const HostSetup& s = ctx->setup;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { delete ctx; return MI_BA_ERR_HIP; }
+  auto fail = [&](mi_ba_status e) { context_destroy(ctx); return e; };
+
+  const int I = p->num_images, C = p->num_cameras;
+  const int64_t P = p->num_points;
+  // Point-major order of reduced blocks (stable).
+  std::vector<int64_t>& bo = ctx->block_obs;
+  bo = s.reduced_obs;
+  std::stable_sort(bo.begin(), bo.end(),
+                   [&](int64_t a, int64_t b) { return p->obs_point[a] < p->obs_point[b]; });
+  const int64_t nb = (int64_t)bo.size();
+  {
+    std::vector<double2> xy(nb);
+    std::vector<uint32_t> im(nb), pt(nb);
+    for (int64_t b = 0; b < nb; ++b) {
+      const int64_t k = bo[b];
+      xy[b] = make_double2(p->obs_xy[2 * k], p->obs_xy[2 * k + 1]);
+      im[b] = (uint32_t)p->obs_image[k];
+      pt[b] = (uint32_t)p->obs_point[k];
+    }
+    if (ctx->obs_xy.alloc(nb) || ctx->obs_img.alloc(nb) || ctx->obs_pt.alloc(nb)) return fail(MI_BA_ERR_OUT_OF_MEMORY);
+    if (nb) {
+      if (hipMemcpy(ctx->obs_xy.ptr, xy.data(), nb * sizeof(double2), hipMemcpyHostToDevice) ||
+          hipMemcpy(ctx->obs_img.ptr, im.data(), nb * 4, hipMemcpyHostToDevice) ||
+          hipMemcpy(ctx->obs_pt.ptr, pt.data(), nb * 4, hipMemcpyHostToDevice))
+        return fail(MI_BA_ERR_HIP);
+    }
+    // camera-major permutation and image-aligned tiles
+    std::vector<uint32_t> perm(nb);
+    std::iota(perm.begin(), perm.end(), 0u);
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return im[a] < im[b]; });
+    std::vector<DevTile> tl;
+    int64_t a = 0;
+    while (a < nb) {
+      const uint32_t img = im[perm[a]];
+      int64_t e = a;
+      while (e < nb && im[perm[e]] == img) ++e;
+      for (int64_t t0 = a; t0 < e; t0 += kTileObs) {
+        DevTile t;
+        t.image = img;
+        t.start = (uint32_t)t0;
+        t.count = (uint32_t)std::min<int64_t>(kTileObs, e - t0);
+        t.pad = 0;
+        tl.push_back(t);
+      }
+      a = e;
+    }
+    ctx->ntiles = (int)tl.size();
+    if (ctx->cm_perm.alloc(nb) || ctx->tiles.alloc(tl.size())) return fail(MI_BA_ERR_OUT_OF_MEMORY);
+    if (nb && (hipMemcpy(ctx->cm_perm.ptr, perm.data(), nb * 4, hipMemcpyHostToDevice) ||
+               hipMemcpy(ctx->tiles.ptr, tl.data(), tl.size() * sizeof(DevTile), hipMemcpyHostToDevice)))
+      return fail(MI_BA_ERR_HIP);
+    // variable points with their contiguous block ranges
+    std::vector<DevPoint> vp;
+    int64_t b = 0;
+    while (b < nb) {
+      const uint32_t q = pt[b];
+      int64_t e = b;
+      while (e < nb && pt[e] == q) ++e;
+      if (s.pt_var[q]) {
+        DevPoint d;
+        d.point = q;
+        d.start = (uint32_t)b;
+        d.count = (uint32_t)(e - b);
+        d.pad = 0;
+        vp.push_back(d);
+      }
+      b = e;
+    }
+    ctx->npv = (int64_t)vp.size();
+    if (ctx->vpoints.alloc(vp.size())) return fail(MI_BA_ERR_OUT_OF_MEMORY);
+    if (!vp.empty() && hipMemcpy(ctx->vpoints.ptr, vp.data(), vp.size() * sizeof(DevPoint), hipMemcpyHostToDevice))
+      return fail(MI_BA_ERR_HIP);
+  }
+  // parameters
+  const int np = s.np;
+  {
+    std::vector<double> qt(8 * (size_t)I, 0.0), cm(8 * (size_t)C, 0.0);
+    std::vector<uint32_t> fl(I), ic(I);
+    for (int i = 0; i < I; ++i) {
+      for (int m = 0; m < 4; ++m) qt[8 * i + m] = p->qvec[4 * i + m];
+      for (int m = 0; m < 3; ++m) qt[8 * i + 4 + m] = p->tvec[3 * i + m];
+      fl[i] = (s.img_var[i] ? 1u : 0u) | ((uint32_t)s.img_tvec_mask[i] << 1);
+      ic[i] = (uint32_t)p->image_camera[i];
+    }
+    for (int c = 0; c < C; ++c)
+      for (int m = 0; m < np; ++m) cm[8 * c + m] = p->camera_params[(size_t)np * c + m];
+    if (ctx->qt.alloc(8 * I) || ctx->qt_c.alloc(8 * I) || ctx->cam.alloc(8 * C) || ctx->cam_c.alloc(8 * C) ||
+        ctx->X.alloc(3 * P) || ctx->X_c.alloc(3 * P) || ctx->img_flags.alloc(I) || ctx->img_cam.alloc(I) ||
+        ctx->cam_var.alloc(C) || ctx->pt_var.alloc(P))
+      return fail(MI_BA_ERR_OUT_OF_MEMORY);
+    if ((I && (hipMemcpy(ctx->qt.ptr, qt.data(), qt.size() * 8, hipMemcpyHostToDevice) ||
+               hipMemcpy(ctx->img_flags.ptr, fl.data(), I * 4, hipMemcpyHostToDevice) ||
+               hipMemcpy(ctx->img_cam.ptr, ic.data(), I * 4, hipMemcpyHostToDevice))) ||
+        (C && (hipMemcpy(ctx->cam.ptr, cm.data(), cm.size() * 8, hipMemcpyHostToDevice) ||
+               hipMemcpy(ctx->cam_var.ptr, s.cam_var.data(), C, hipMemcpyHostToDevice))) ||
+        (P && (hipMemcpy(ctx->X.ptr, p->xyz, 3 * P * 8, hipMemcpyHostToDevice) ||
+               hipMemcpy(ctx->pt_var.ptr, s.pt_var.data(), P, hipMemcpyHostToDevice))))
+      return fail(MI_BA_ERR_HIP);
+  }
+  DevProblem& d = ctx->dev;
+  d.model = p->camera_model;
+  d.np = np;
+  d.ct = s.ct;
+  d.W = 9 + s.ct;
+  for (int k = 0; k < 8; ++k) d.cam_tan_idx[k] = s.cam_tan_idx[k];
+  d.nb = nb;
+  d.num_images = I;
+  d.num_cameras = C;
+  d.num_points = P;
+  d.nf = 6 * (int64_t)I + (int64_t)s.ct * C;
+  d.loss_type = o->loss_function_type;
+  d.loss_scale = o->loss_function_scale;
+  d.obs_xy = ctx->obs_xy.ptr;
+  d.obs_img = ctx->obs_img.ptr;
+  d.obs_pt = ctx->obs_pt.ptr;
+  d.img_flags = ctx->img_flags.ptr;
+  d.img_cam = ctx->img_cam.ptr;
+  d.cam_var = ctx->cam_var.ptr;
+  d.pt_var = ctx->pt_var.ptr;
+  d.qt = ctx->qt.ptr;
+  d.cam = ctx->cam.ptr;
+  d.X = ctx->X.ptr;
+  // linearization + LM buffers
+  ctx->npartial = std::max<int64_t>(1, reproj_grid(nb));
+  const int64_t nf = d.nf;
+  const int ncs = s.ct * (s.ct + 1) / 2;
+  if (ctx->r.alloc(nb) || ctx->J.alloc((size_t)nb * 2 * d.W) || ctx->Vg.alloc(9 * P) ||
+      ctx->partial.alloc(ctx->npartial) || ctx->scale_p.alloc(3 * P) || ctx->diag_p.alloc(3 * P) ||
+      ctx->Vinv.alloc(6 * P) || ctx->pose_blk.alloc(21 * (size_t)I) || ctx->cam_blk.alloc((size_t)ncs * C + 1) ||
+      ctx->bvec.alloc(nf) || ctx->udiag.alloc(nf) || ctx->scale_f.alloc(nf) || ctx->diag_f.alloc(nf) ||
+      ctx->lambda_f.alloc(nf) || ctx->prec_pose.alloc(36 * (size_t)I) ||
+      ctx->prec_cam.alloc((size_t)s.ct * s.ct * C + 1) || ctx->cg_x.alloc(nf) || ctx->cg_r.alloc(nf) ||
+      ctx->cg_z.alloc(nf) || ctx->cg_p.alloc(nf) || ctx->cg_q.alloc(nf) || ctx->cg_w.alloc(3 * P) ||
+      ctx->dX.alloc(3 * P) || ctx->scalars.alloc(kNumScalars))
+    return fail(MI_BA_ERR_OUT_OF_MEMORY);
+  if (hipHostMalloc(&ctx->host_scalars, sizeof(double) * kNumScalars, hipHostMallocDefault) != hipSuccess)
+    return fail(MI_BA_ERR_OUT_OF_MEMORY);
+  if (hipMemset(ctx->scalars.ptr, 0, sizeof(double) * kNumScalars) != hipSuccess) return fail(MI_BA_ERR_HIP);
+  if (P && (hipMemset(ctx->dX.ptr, 0, 3 * P * 8) || hipMemset(ctx->Vinv.ptr, 0, 6 * P * 8) ||
+            hipMemset(ctx->cg_w.ptr, 0, 3 * P * 8)))
+    return fail(MI_BA_ERR_HIP);
+  // fixed cost of dropped blocks
+  double fixed = 0.0;
+  for (int64_t k : s.fixed_obs) fixed += host_block_cost(*o, p, k);
+  ctx->fixed_cost = fixed;
+  if (sem) {
+    st = semantic_create(ctx, sem);
+    if (st != MI_BA_OK) return fail(st);
+  }
+  *out = ctx;
+  return MI_BA_OK;
+}
+
+void context_destroy(mi_ba_context* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  semantic_destroy(ctx);
+  for (auto& e : ctx->timer.pending) {
+    (void)hipEventDestroy(e.second.first);
+    (void)hipEventDestroy(e.second.second);
+  }
+  for (auto e : ctx->timer.pool) (void)hipEventDestroy(e);
+  if (ctx->host_scalars) (void)hipHostFree(ctx->host_scalars);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+// Residuals + Jacobians + point blocks at the current parameters; cost into
+// scalars[kCost] (geometric) + scalars[kSemCost] (semantic).
+mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
+  hipStream_t s = ctx->stream;
+  const DevProblem& d = ctx->dev;
+  if (d.num_points) MI_HIP(hipMemsetAsync(ctx->Vg.ptr, 0, 9 * d.num_points * sizeof(double), s));
+  MI_HIP(hipMemsetAsync(ctx->scalars.ptr, 0, sizeof(double) * kNumScalars, s));
+  hipEvent_t stop;
+  timer_begin(ctx, "reproj_jacobian", &stop);
+  launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr, ctx->partial.ptr, 1, s);
+  timer_end(ctx, stop);
+  if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s);
+  if (ctx->sem) {
+    mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, true);
+    if (st != MI_BA_OK) return st;
+  }
+  MI_HIP(hipGetLastError());
+  if (cost_out) {
+    mi_ba_status st = read_scalars(ctx, 0, kNumScalars);
+    if (st != MI_BA_OK) return st;
+    *cost_out = ctx->host_scalars[kCost] + ctx->host_scalars[kSemCost];
+  }
+  return MI_BA_OK;
+}
+
+namespace {
+
+// One Schur product y = S x including the semantic pair term.
+void schur_product(mi_ba_context* ctx, const double* x, double* y) {
+  const DevProblem& d = ctx->dev;
+  launch_schur_product(d, ctx->vpoints.ptr, ctx->npv, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr,
+                       ctx->Vinv.ptr, ctx->lambda_f.ptr, x, ctx->cg_w.ptr, y, ctx->stream);
+  if (ctx->sem) semantic_schur_product(ctx, x, y);
+}
+
+// Preconditioned CG on the Schur complement, Ceres ConjugateGradientsSolver
+// semantics (restated): q-termination with tolerance eta, r_tolerance off,
+// residual recomputed every 10 iterations, stop on rho = 0/inf or pq <= 0.
+mi_ba_status pcg(mi_ba_context* ctx, int* iterations) {
+  const DevProblem& d = ctx->dev;
+  hipStream_t s = ctx->stream;
+  const int64_t nf = d.nf;
+  double* sc = ctx->scalars.ptr;
+  double* hs = ctx->host_scalars;
+  MI_HIP(hipMemsetAsync(ctx->cg_x.ptr, 0, nf * 8, s));
+  MI_HIP(hipMemcpyAsync(ctx->cg_r.ptr, ctx->bvec.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
+  launch_dot(ctx->bvec.ptr, ctx->bvec.ptr, nf, sc + kXB, s);
+  mi_ba_status st = read_scalars(ctx, kXB, 1);
+  if (st != MI_BA_OK) return st;
+  *iterations = 0;
+  if (hs[kXB] == 0.0) return MI_BA_OK;
+  double Q0 = 0.0;
+  const int max_it = std::max(1, ctx->options.max_linear_solver_iterations);
+  for (int it = 1; it <= max_it; ++it) {
+    launch_precond(d, ctx->prec_pose.ptr, ctx->prec_cam.ptr, ctx->cg_r.ptr, ctx->cg_z.ptr, s);
+    if (it > 1) MI_HIP(hipMemcpyAsync(sc + kRhoPrev, sc + kRho, 8, hipMemcpyDeviceToDevice, s));
+    launch_dot(ctx->cg_r.ptr, ctx->cg_z.ptr, nf, sc + kRho, s);
+    if (it == 1) {
+      MI_HIP(hipMemcpyAsync(ctx->cg_p.ptr, ctx->cg_z.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
+    } else {
+      launch_xpby(ctx->cg_p.ptr, ctx->cg_z.ptr, sc + kRho, sc + kRhoPrev, nf, s);
+    }
+    schur_product(ctx, ctx->cg_p.ptr, ctx->cg_q.ptr);
+    launch_dot(ctx->cg_p.ptr, ctx->cg_q.ptr, nf, sc + kPQ, s);
+    launch_axpy(ctx->cg_x.ptr, ctx->cg_p.ptr, sc + kRho, sc + kPQ, 1.0, nf, s);
+    if (it % 10 == 0) {
+      // r = b - S x
+      schur_product(ctx, ctx->cg_x.ptr, ctx->cg_q.ptr);
+      MI_HIP(hipMemcpyAsync(ctx->cg_r.ptr, ctx->bvec.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
+      MI_HIP(hipMemcpyAsync(sc + kXR, sc + kPQ, 8, hipMemcpyDeviceToDevice, s));  // keep pq
+      double one = 1.0;
+      MI_HIP(hipMemcpyAsync(sc + kStepNorm, &one, 8, hipMemcpyHostToDevice, s));
+      launch_axpy(ctx->cg_r.ptr, ctx->cg_q.ptr, sc + kStepNorm, sc + kStepNorm, -1.0, nf, s);
+    } else {
+      launch_axpy(ctx->cg_r.ptr, ctx->cg_q.ptr, sc + kRho, sc + kPQ, -1.0, nf, s);
+    }
+    launch_dot(ctx->cg_x.ptr, ctx->bvec.ptr, nf, sc + kXB, s);
+    launch_dot(ctx->cg_x.ptr, ctx->cg_r.ptr, nf, sc + kXR, s);
+    st = read_scalars(ctx, kRho, 5);
+    if (st != MI_BA_OK) return st;
+    *iterations = it;
+    const double rho = hs[kRho], pq = hs[kPQ];
+    if (rho == 0.0 || !std::isfinite(rho)) break;
+    if (!(pq > 0.0) || !std::isfinite(pq)) break;
+    const double Q1 = -1.0 * (hs[kXB] + hs[kXR]) / 2.0;
+    const double zeta = it * (Q1 - Q0) / Q1;
+    if (zeta < ctx->options.eta) break;
+    Q0 = Q1;
+  }
+  return MI_BA_OK;
+}
+
+}  // namespace
+
+mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
+  if (ctx->solved) return MI_BA_ERR_STATE;
+  ctx->solved = true;
+  const double t_start = now_s();
+  const mi_ba_options& o = ctx->options;
+  const DevProblem& d = ctx->dev;
+  hipStream_t s = ctx->stream;
+  double* sc = ctx->scalars.ptr;
+  double* hs = ctx->host_scalars;
+  std::memset(sum, 0, sizeof(*sum));
+  sum->num_residuals_reduced = ctx->setup.num_residuals_reduced + (ctx->sem ? ctx->sem->ns : 0);
+  sum->num_effective_parameters_reduced = ctx->setup.num_effective_parameters_reduced;
+  sum->num_semantic_residuals = ctx->sem ? ctx->sem->ns : 0;
+  sum->fixed_cost = ctx->fixed_cost;
+  if (sum->num_residuals_reduced == 0) return MI_BA_ERR_NO_RESIDUALS;
+  double tj = now_s();
+  double x_cost = 0.0;
+  mi_ba_status st = context_linearize(ctx, &x_cost);
+  if (st != MI_BA_OK) return st;
+  sum->jacobian_evaluation_time_in_seconds += now_s() - tj;
+  sum->num_jacobian_evaluations = 1;
+  sum->initial_cost = x_cost + ctx->fixed_cost;
+  double radius = o.initial_trust_region_radius;
+  double decrease_factor = 2.0;
+  bool reuse_diag = false, first = true;
+  int consecutive_invalid = 0, iteration = 0;
+  sum->termination_type = MI_BA_NO_CONVERGENCE;
+  const int64_t nf = d.nf;
+  while (true) {
+    if (iteration >= o.max_num_iterations) { sum->termination_type = MI_BA_NO_CONVERGENCE; break; }
+    if (radius < 1e-32) { sum->termination_type = MI_BA_CONVERGENCE; break; }
+    ++iteration;
+    // Damped point inverses, Schur-Jacobi blocks, rhs.
+    launch_point_prepare(d, ctx->vpoints.ptr, ctx->npv, ctx->Vg.ptr, ctx->scale_p.ptr, ctx->diag_p.ptr,
+                         ctx->Vinv.ptr, first, reuse_diag, radius, s);
+    MI_HIP(hipMemsetAsync(ctx->pose_blk.ptr, 0, ctx->pose_blk.bytes(), s));
+    MI_HIP(hipMemsetAsync(ctx->cam_blk.ptr, 0, ctx->cam_blk.bytes(), s));
+    MI_HIP(hipMemsetAsync(ctx->bvec.ptr, 0, ctx->bvec.bytes(), s));
+    MI_HIP(hipMemsetAsync(ctx->udiag.ptr, 0, ctx->udiag.bytes(), s));
+    launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr,
+                  ctx->Vinv.ptr, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr, s);
+    if (ctx->sem) semantic_add_fblock(ctx);
+    launch_fblock_finalize(d, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->udiag.ptr, ctx->scale_f.ptr,
+                           ctx->diag_f.ptr, ctx->lambda_f.ptr, ctx->prec_pose.ptr, ctx->prec_cam.ptr,
+                           ctx->bvec.ptr, first, reuse_diag, radius, s);
+    first = false;
+    reuse_diag = true;
+    int cg_it = 0;
+    st = pcg(ctx, &cg_it);
+    if (st != MI_BA_OK) return st;
+    sum->num_linear_solver_iterations += cg_it;
+    // back substitution and model cost change
+    launch_backsub(d, ctx->vpoints.ptr, ctx->npv, ctx->J.ptr, ctx->Vg.ptr, ctx->Vinv.ptr, ctx->cg_x.ptr,
+                   ctx->dX.ptr, s);
+    launch_model_cost(d, ctx->r.ptr, ctx->J.ptr, ctx->cg_x.ptr, ctx->dX.ptr, ctx->partial.ptr, s);
+    MI_HIP(hipMemsetAsync(sc + kModelCost, 0, 8, s));
+    MI_HIP(hipMemsetAsync(sc + kSemModel, 0, 8, s));
+    if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kModelCost, s);
+    if (ctx->sem) semantic_model_cost(ctx, ctx->cg_x.ptr, sc + kSemModel);
+    launch_sqnorm2(ctx->cg_x.ptr, nf, ctx->dX.ptr, 3 * d.num_points, sc + kStepNorm, s);
+    st = read_scalars(ctx, 0, kNumScalars);
+    if (st != MI_BA_OK) return st;
+    const double model_cost_change = hs[kModelCost] + hs[kSemModel];
+    const bool valid = std::isfinite(model_cost_change) && model_cost_change > 0.0;
+    if (!valid) {
+      ++consecutive_invalid;
+      ++sum->num_unsuccessful_steps;
+      if (consecutive_invalid > o.max_num_consecutive_invalid_steps) {
+        sum->termination_type = MI_BA_FAILURE;
+        break;
+      }
+      radius = radius / decrease_factor;
+      decrease_factor *= 2.0;
+      continue;
+    }
+    consecutive_invalid = 0;
+    const double step_norm = std::sqrt(hs[kStepNorm]);
+    // candidate
+    launch_plus(d, ctx->cg_x.ptr, ctx->dX.ptr, ctx->qt.ptr, ctx->cam.ptr, ctx->X.ptr, ctx->qt_c.ptr,
+                ctx->cam_c.ptr, ctx->X_c.ptr, s);
+    MI_HIP(hipMemsetAsync(sc + kCandCost, 0, 8, s));
+    MI_HIP(hipMemsetAsync(sc + kSemCand, 0, 8, s));
+    launch_reproj_cost(d, ctx->qt_c.ptr, ctx->cam_c.ptr, ctx->X_c.ptr, ctx->partial.ptr, s);
+    if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kCandCost, s);
+    if (ctx->sem) semantic_cost(ctx, ctx->qt_c.ptr, sc + kSemCand);
+    st = read_scalars(ctx, 0, kNumScalars);
+    if (st != MI_BA_OK) return st;
+    const double candidate_cost = hs[kCandCost] + hs[kSemCand];
+    const double cost_change = x_cost - candidate_cost;
+    const double relative_decrease = cost_change / model_cost_change;
+    const bool success = std::isfinite(candidate_cost) && relative_decrease > o.min_relative_decrease;
+    // ParameterToleranceReached / FunctionToleranceReached: Ceres returns
+    // before accepting the candidate (x stays at the current point).
+    double x_norm = 0.0;
+    if (o.parameter_tolerance > 0.0) {
+      launch_sqnorm2(ctx->qt.ptr, 8 * (int64_t)d.num_images, ctx->X.ptr, 3 * d.num_points, sc + kStepNorm, s);
+      st = read_scalars(ctx, kStepNorm, 1);
+      if (st != MI_BA_OK) return st;
+      x_norm = std::sqrt(hs[kStepNorm]);
+    }
+    if (step_norm <= o.parameter_tolerance * (x_norm + o.parameter_tolerance) ||
+        std::fabs(cost_change) <= o.function_tolerance * x_cost) {
+      ++sum->num_unsuccessful_steps;
+      sum->termination_type = MI_BA_CONVERGENCE;
+      break;
+    }
+    if (success) {
+      ++sum->num_successful_steps;
+      x_cost = candidate_cost;
+      std::swap(ctx->qt.ptr, ctx->qt_c.ptr);
+      std::swap(ctx->cam.ptr, ctx->cam_c.ptr);
+      std::swap(ctx->X.ptr, ctx->X_c.ptr);
+      ctx->dev.qt = ctx->qt.ptr;
+      ctx->dev.cam = ctx->cam.ptr;
+      ctx->dev.X = ctx->X.ptr;
+      radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * relative_decrease - 1.0, 3));
+      radius = std::min(1e16, radius);
+      decrease_factor = 2.0;
+      reuse_diag = false;
+      tj = now_s();
+      st = context_linearize(ctx, nullptr);
+      if (st != MI_BA_OK) return st;
+      sum->num_jacobian_evaluations += 1;
+      sum->jacobian_evaluation_time_in_seconds += now_s() - tj;
+    } else {
+      ++sum->num_unsuccessful_steps;
+      radius = radius / decrease_factor;
+      decrease_factor *= 2.0;
+    }
+  }
+  sum->final_cost = x_cost + ctx->fixed_cost;
+  MI_HIP(hipStreamSynchronize(s));
+  sum->total_time_in_seconds = now_s() - t_start;
+  return MI_BA_OK;
+}
+
+mi_ba_status context_writeback(mi_ba_context* ctx) {
+  mi_ba_problem* p = &ctx->problem;
+  const HostSetup& s = ctx->setup;
+  const int I = p->num_images, C = p->num_cameras;
+  const int64_t P = p->num_points;
+  std::vector<double> qt(8 * (size_t)I), cm(8 * (size_t)C), X(3 * (size_t)P);
+  MI_HIP(hipStreamSynchronize(ctx->stream));
+  if (I) MI_HIP(hipMemcpy(qt.data(), ctx->qt.ptr, qt.size() * 8, hipMemcpyDeviceToHost));
+  if (C) MI_HIP(hipMemcpy(cm.data(), ctx->cam.ptr, cm.size() * 8, hipMemcpyDeviceToHost));
+  if (P) MI_HIP(hipMemcpy(X.data(), ctx->X.ptr, X.size() * 8, hipMemcpyDeviceToHost));
+  for (int i = 0; i < I; ++i) {
+    if (!s.img_var[i]) continue;
+    for (int m = 0; m < 4; ++m) p->qvec[4 * i + m] = qt[8 * i + m];
+    for (int m = 0; m < 3; ++m) p->tvec[3 * i + m] = qt[8 * i + 4 + m];
+  }
+  for (int c = 0; c < C; ++c) {
+    if (!s.cam_var[c]) continue;
+    for (int m = 0; m < s.np; ++m) p->camera_params[(size_t)s.np * c + m] = cm[8 * c + m];
+  }
+  for (int64_t k = 0; k < P; ++k) {
+    if (!s.pt_var[k]) continue;
+    for (int m = 0; m < 3; ++m) p->xyz[3 * k + m] = X[3 * k + m];
+  }
+  return MI_BA_OK;
+}
+
+}  // namespace miba
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+using namespace miba;
+
+extern "C" {
+
+int32_t mi_ba_abi_version(void) { return MI_BA_ABI_VERSION; }
+
+const char* mi_ba_status_string(int32_t status) {
+  switch (status) {
+    case MI_BA_OK: return "ok";
+    case MI_BA_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case MI_BA_ERR_NO_DEVICE: return "no HIP device (MI355X required; no CPU fallback)";
+    case MI_BA_ERR_UNSUPPORTED: return "unsupported";
+    case MI_BA_ERR_HIP: return "HIP runtime error";
+    case MI_BA_ERR_NO_RESIDUALS: return "problem has no residuals";
+    case MI_BA_ERR_STATE: return "invalid state (single-use solver)";
+    case MI_BA_ERR_OUT_OF_MEMORY: return "out of device memory";
+  }
+  return "unknown status";
+}
+
+int32_t mi_ba_num_params(int32_t camera_model) { return num_params(camera_model); }
+
+mi_ba_status mi_ba_device_count(int32_t* count) {
+  int n = 0;
+  if (!count) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return MI_BA_OK;
+}
+
+// BundleAdjustmentOptions::BundleAdjustmentOptions (bundle_adjustment.h:49-92)
+void mi_ba_default_options(mi_ba_options* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->loss_function_type = MI_BA_LOSS_TRIVIAL;
+  o->loss_function_scale = 1.0;
+  o->refine_focal_length = 1;
+  o->refine_principal_point = 0;
+  o->refine_extra_params = 1;
+  o->refine_extrinsics = 1;
+  o->print_summary = 0;
+  o->max_num_iterations = 100;
+  o->function_tolerance = 0.0;
+  o->gradient_tolerance = 0.0;
+  o->parameter_tolerance = 0.0;
+  o->max_linear_solver_iterations = 200;
+  o->max_num_consecutive_invalid_steps = 10;
+  o->linear_solver_type = MI_BA_SOLVER_AUTO;
+  o->eta = 1e-1;
+  o->initial_trust_region_radius = 1e4;
+  o->min_relative_decrease = 1e-3;
+  o->device = 0;
+  o->semantic_weight = 1.0;
+}
+
+mi_ba_status mi_ba_setup_stats(const mi_ba_options* o, const mi_ba_problem* p, mi_ba_setup_info* info) {
+  if (!o || !p || !info) return MI_BA_ERR_INVALID_ARGUMENT;
+  // SetUp normalises qvecs in place; work on a private copy of the qvecs.
+  mi_ba_problem copy = *p;
+  std::vector<double> q(p->qvec, p->qvec + 4 * (size_t)std::max(0, p->num_images));
+  copy.qvec = q.data();
+  HostSetup s;
+  mi_ba_status st = build_setup(*o, &copy, &s);
+  if (st != MI_BA_OK) return st;
+  info->num_residual_blocks = s.num_residual_blocks;
+  info->num_residuals_reduced = s.num_residuals_reduced;
+  info->num_effective_parameters_reduced = s.num_effective_parameters_reduced;
+  info->num_variable_images = std::accumulate(s.img_var.begin(), s.img_var.end(), (int64_t)0);
+  info->num_variable_cameras = std::accumulate(s.cam_var.begin(), s.cam_var.end(), (int64_t)0);
+  info->num_variable_points = std::accumulate(s.pt_var.begin(), s.pt_var.end(), (int64_t)0);
+  info->camera_tangent_size = s.ct;
+  return MI_BA_OK;
+}
+
+static void print_summary(const mi_ba_summary& s) {
+  // PrintSolverSummary (bundle_adjustment.cc:1142-1196)
+  const char* term = s.termination_type == MI_BA_CONVERGENCE ? "Convergence"
+                     : s.termination_type == MI_BA_NO_CONVERGENCE ? "No convergence"
+                     : s.termination_type == MI_BA_FAILURE ? "Failure" : "Unknown";
+  std::printf("    Residuals : %lld\n   Parameters : %lld\n   Iterations : %d\n         Time : %g [s]\n"
+              " Initial cost : %g [px]\n   Final cost : %g [px]\n  Termination : %s\n\n",
+              (long long)s.num_residuals_reduced, (long long)s.num_effective_parameters_reduced,
+              s.num_successful_steps + s.num_unsuccessful_steps, s.total_time_in_seconds,
+              std::sqrt(s.initial_cost / s.num_residuals_reduced), std::sqrt(s.final_cost / s.num_residuals_reduced),
+              term);
+}
+
+mi_ba_status mi_ba_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem, mi_ba_summary* sum) {
+  if (!o || !p || !sum) return MI_BA_ERR_INVALID_ARGUMENT;
+  const double t0 = now_s();
+  mi_ba_context* ctx = nullptr;
+  mi_ba_status st = context_create(o, p, sem, &ctx);
+  if (st != MI_BA_OK) return st;
+  // SetUp normalised the config qvecs of ctx->problem (== caller arrays).
+  st = context_solve(ctx, sum);
+  if (st == MI_BA_OK) st = context_writeback(ctx);
+  context_destroy(ctx);
+  sum->total_time_in_seconds = now_s() - t0;
+  if (st == MI_BA_OK && o->print_summary) print_summary(*sum);
+  return st;
+}
+
+mi_ba_status mi_ba_context_create(const mi_ba_options* o, const mi_ba_problem* p, const mi_ba_semantic* sem,
+                                  mi_ba_context** ctx) {
+  return context_create(o, p, sem, ctx);
+}
+
+void mi_ba_context_destroy(mi_ba_context* ctx) { context_destroy(ctx); }
+
+mi_ba_status mi_ba_linearize(mi_ba_context* ctx) {
+  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  return context_linearize(ctx, nullptr);
+}
+
+mi_ba_status mi_ba_evaluate_jacobian(mi_ba_context* ctx) {
+  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  const DevProblem& d = ctx->dev;
+  hipEvent_t stop;
+  if (d.num_points) MI_HIP(hipMemsetAsync(ctx->Vg.ptr, 0, 9 * d.num_points * sizeof(double), ctx->stream));
+  timer_begin(ctx, "reproj_jacobian", &stop);
+  launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr, ctx->partial.ptr, 1, ctx->stream);
+  timer_end(ctx, stop);
+  MI_HIP(hipGetLastError());
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_evaluate_semantic(mi_ba_context* ctx) {
+  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (!ctx->sem) return MI_BA_ERR_INVALID_ARGUMENT;
+  return semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, true);
+}
+
+mi_ba_status mi_ba_synchronize(mi_ba_context* ctx) {
+  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_HIP(hipStreamSynchronize(ctx->stream));
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_context_dims(const mi_ba_context* ctx, int64_t* nb, int32_t* cols, int64_t* ns) {
+  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (nb) *nb = ctx->dev.nb;
+  if (cols) *cols = ctx->dev.W;
+  if (ns) *ns = ctx->sem ? ctx->sem->ns : 0;
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_download_jacobian(mi_ba_context* ctx, int64_t* block_obs, double* residuals, double* jacobian) {
+  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  const int64_t nb = ctx->dev.nb;
+  MI_HIP(hipStreamSynchronize(ctx->stream));
+  if (block_obs) std::memcpy(block_obs, ctx->block_obs.data(), nb * sizeof(int64_t));
+  if (residuals && nb) MI_HIP(hipMemcpy(residuals, ctx->r.ptr, nb * sizeof(double2), hipMemcpyDeviceToHost));
+  if (jacobian && nb)
+    MI_HIP(hipMemcpy(jacobian, ctx->J.ptr, (size_t)nb * 2 * ctx->dev.W * sizeof(double), hipMemcpyDeviceToHost));
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_download_semantic(mi_ba_context* ctx, int32_t* sample_pixel, int32_t* status, double* residuals,
+                                     double* jacobian) {
+  if (!ctx || !ctx->sem) return MI_BA_ERR_INVALID_ARGUMENT;
+  SemanticState* S = ctx->sem;
+  MI_HIP(hipStreamSynchronize(ctx->stream));
+  const int64_t n = S->ns;
+  if (sample_pixel) std::memcpy(sample_pixel, S->sample_pixel_host.data(), 3 * n * sizeof(int32_t));
+  if (n == 0) return MI_BA_OK;
+  if (status) MI_HIP(hipMemcpy(status, S->status.ptr, n * 4, hipMemcpyDeviceToHost));
+  if (residuals) MI_HIP(hipMemcpy(residuals, S->r.ptr, n * 8, hipMemcpyDeviceToHost));
+  if (jacobian) MI_HIP(hipMemcpy(jacobian, S->J.ptr, 12 * n * 8, hipMemcpyDeviceToHost));
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_context_solve(mi_ba_context* ctx, mi_ba_summary* summary) {
+  if (!ctx || !summary) return MI_BA_ERR_INVALID_ARGUMENT;
+  return context_solve(ctx, summary);
+}
+
+mi_ba_status mi_ba_context_writeback(mi_ba_context* ctx) {
+  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  return context_writeback(ctx);
+}
+
+mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost) {
+  if (!ctx || !cost) return MI_BA_ERR_INVALID_ARGUMENT;
+  hipStream_t s = ctx->stream;
+  double* sc = ctx->scalars.ptr;
+  MI_HIP(hipMemsetAsync(sc + kCandCost, 0, 8, s));
+  MI_HIP(hipMemsetAsync(sc + kSemCand, 0, 8, s));
+  launch_reproj_cost(ctx->dev, ctx->qt.ptr, ctx->cam.ptr, ctx->X.ptr, ctx->partial.ptr, s);
+  if (ctx->dev.nb) launch_sum(ctx->partial.ptr, reproj_grid(ctx->dev.nb), sc + kCandCost, s);
+  if (ctx->sem) semantic_cost(ctx, ctx->qt.ptr, sc + kSemCand);
+  mi_ba_status st = read_scalars(ctx, 0, kNumScalars);
+  if (st != MI_BA_OK) return st;
+  *cost = ctx->host_scalars[kCandCost] + ctx->host_scalars[kSemCand] + ctx->fixed_cost;
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_set_timing(mi_ba_context* ctx, int32_t enabled) {
+  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  timer_collect(ctx);
+  ctx->timing = enabled != 0;
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_kernel_time(mi_ba_context* ctx, const char* name, double* total_ms, int64_t* launches) {
+  if (!ctx || !name) return MI_BA_ERR_INVALID_ARGUMENT;
+  timer_collect(ctx);
+  auto it = ctx->timer.totals.find(name);
+  if (total_ms) *total_ms = it == ctx->timer.totals.end() ? 0.0 : it->second.first;
+  if (launches) *launches = it == ctx->timer.totals.end() ? 0 : it->second.second;
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_reset_kernel_times(mi_ba_context* ctx) {
+  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  timer_collect(ctx);
+  ctx->timer.totals.clear();
+  return MI_BA_OK;
+}
+
+}  // extern "C"

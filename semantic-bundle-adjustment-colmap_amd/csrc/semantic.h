@@ -1,0 +1,71 @@
+// semantic.h — semantic-label residual term on the GPU (product code).
+//
+// Replaces the Ceres NumericDiff evaluation of the
+// {,ConstantFirstPose,ConstantSecondPose}SemanticBACostFunction blocks
+// (src/base/semantic_cost_functions.h:87-404) that
+// SemanticBundleAdjuster::AddImagePairToProblem creates per sampled pixel
+// (src/optim/semantic_bundle_adjustment.cc:699-906).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/mi_ba.h"
+#include "context.h"
+
+namespace miba {
+
+struct SemSample {      // 32 B, one per sampled pixel
+  double pc1[3];        // P_c1 = (u1*d1, v1*d1, d1) (semantic_cost_functions.h:103-118)
+  float label1;         // semantic_1_
+  uint32_t pair;        // index into the pair table
+};
+
+struct SemTile {       // pair-aligned tile of samples
+  uint32_t pair, start, count, pad;
+};
+
+struct SemPair {
+  uint32_t i, j;        // image indices
+  uint32_t var1, var2;  // pose i / pose j variable
+  uint32_t start, count;
+};
+
+struct SemanticState {
+  int H = 0, W = 0;
+  double depth_threshold = 2.0;
+  double rel_step = 1e-3;
+  int64_t ns = 0;        // samples
+  int npairs = 0;
+  std::vector<SemPair> pairs_host;
+  std::vector<int32_t> sample_pixel_host;  // [ns][3]
+  DevArray<SemSample> samples;
+  DevArray<SemPair> pairs;
+  DevArray<float> depth, label;            // [I][H][W] rasters of images used as j
+  DevArray<uint32_t> raster_slot;          // image -> raster slot
+  DevArray<double> r;                      // [ns]
+  DevArray<int32_t> status;                // [ns]
+  DevArray<double> J;                      // [ns][12]
+  DevArray<double> pair_blk;               // [npairs][12*12 + 12]: M = J'J (full) and g = J'r
+  DevArray<double> partial;
+  int64_t npartial = 0;
+  DevArray<SemTile> tiles;
+  int ntiles = 0;
+};
+
+mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem);
+void semantic_destroy(mi_ba_context* ctx);
+// Evaluate residuals + numeric-diff Jacobians of every sample; store r/J and
+// reduce into per-pair blocks; cost (0.5 * w * sum rho) into *d_cost.
+mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples);
+// Cost only, at parameters qt (candidate evaluation).
+void semantic_cost(mi_ba_context* ctx, const double* qt, double* d_cost);
+// Fold the pair blocks into the Schur-Jacobi pose blocks, b and diag(U).
+void semantic_add_fblock(mi_ba_context* ctx);
+// y += M_pair x (implicit Schur product).
+void semantic_schur_product(mi_ba_context* ctx, const double* x, double* y);
+// Model cost change contribution -(g'd + d'Md/2) into *d_out.
+void semantic_model_cost(mi_ba_context* ctx, const double* df, double* d_out);
+
+}  // namespace miba

@@ -1,0 +1,508 @@
+"""ctypes binding of the mi_ba C-ABI (include/mi_ba.h) and the synthetic
+scene tool (include/mi_ba_synthetic.h).
+
+This is plumbing for tests/ and bench.py: the product is libmi_ba.so (HIP
+kernels + C++ runtime).  Loading the library never falls back to anything:
+if libmi_ba.so is missing, `load()` raises; on a machine without an MI355X
+the compute entry points return MI_BA_ERR_NO_DEVICE.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmi_ba.so")
+SYNTH_PATH = os.path.join(_HERE, "libmi_ba_synth.so")
+
+# status codes / enums (mi_ba.h)
+OK, ERR_INVALID_ARGUMENT, ERR_NO_DEVICE, ERR_UNSUPPORTED, ERR_HIP, ERR_NO_RESIDUALS, ERR_STATE, ERR_OOM = range(8)
+SIMPLE_PINHOLE, PINHOLE, SIMPLE_RADIAL, RADIAL, OPENCV = range(5)
+LOSS_TRIVIAL, LOSS_SOFT_L1, LOSS_CAUCHY = range(3)
+SOLVER_AUTO, SOLVER_DENSE_SCHUR, SOLVER_ITERATIVE_SCHUR = range(3)
+CONVERGENCE, NO_CONVERGENCE, FAILURE = range(3)
+OUT_OF_BOUNDS, INVALID_DEPTH, VALID = -1, -2, 10
+NUM_PARAMS = {SIMPLE_PINHOLE: 3, PINHOLE: 4, SIMPLE_RADIAL: 4, RADIAL: 5, OPENCV: 8}
+MODEL_NAMES = {"SIMPLE_PINHOLE": 0, "PINHOLE": 1, "SIMPLE_RADIAL": 2, "RADIAL": 3, "OPENCV": 4}
+
+_dp = C.POINTER(C.c_double)
+_fp = C.POINTER(C.c_float)
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+_u8p = C.POINTER(C.c_uint8)
+
+
+class Options(C.Structure):
+    _fields_ = [
+        ("loss_function_type", C.c_int32),
+        ("loss_function_scale", C.c_double),
+        ("refine_focal_length", C.c_int32),
+        ("refine_principal_point", C.c_int32),
+        ("refine_extra_params", C.c_int32),
+        ("refine_extrinsics", C.c_int32),
+        ("print_summary", C.c_int32),
+        ("max_num_iterations", C.c_int32),
+        ("function_tolerance", C.c_double),
+        ("gradient_tolerance", C.c_double),
+        ("parameter_tolerance", C.c_double),
+        ("max_linear_solver_iterations", C.c_int32),
+        ("max_num_consecutive_invalid_steps", C.c_int32),
+        ("linear_solver_type", C.c_int32),
+        ("eta", C.c_double),
+        ("initial_trust_region_radius", C.c_double),
+        ("min_relative_decrease", C.c_double),
+        ("device", C.c_int32),
+        ("semantic_weight", C.c_double),
+    ]
+
+
+class Problem(C.Structure):
+    _fields_ = [
+        ("camera_model", C.c_int32),
+        ("num_cameras", C.c_int32),
+        ("camera_params", _dp),
+        ("camera_constant", _u8p),
+        ("num_images", C.c_int32),
+        ("qvec", _dp),
+        ("tvec", _dp),
+        ("image_camera", _i32p),
+        ("image_in_config", _u8p),
+        ("image_constant_pose", _u8p),
+        ("image_constant_tvec", _u8p),
+        ("num_points", C.c_int64),
+        ("xyz", _dp),
+        ("point_config", _u8p),
+        ("num_obs", C.c_int64),
+        ("obs_xy", _dp),
+        ("obs_image", _i32p),
+        ("obs_point", _i32p),
+    ]
+
+
+class Semantic(C.Structure):
+    _fields_ = [
+        ("height", C.c_int32),
+        ("width", C.c_int32),
+        ("depth", _fp),
+        ("label", _fp),
+        ("num_pairs", C.c_int32),
+        ("pairs", _i32p),
+        ("pixel_step", C.c_int32),
+        ("depth_error_threshold", C.c_double),
+        ("numeric_relative_step_size", C.c_double),
+    ]
+
+
+class Summary(C.Structure):
+    _fields_ = [
+        ("num_residuals_reduced", C.c_int64),
+        ("num_effective_parameters_reduced", C.c_int64),
+        ("num_successful_steps", C.c_int32),
+        ("num_unsuccessful_steps", C.c_int32),
+        ("termination_type", C.c_int32),
+        ("initial_cost", C.c_double),
+        ("final_cost", C.c_double),
+        ("fixed_cost", C.c_double),
+        ("total_time_in_seconds", C.c_double),
+        ("jacobian_evaluation_time_in_seconds", C.c_double),
+        ("num_jacobian_evaluations", C.c_int32),
+        ("num_linear_solver_iterations", C.c_int32),
+        ("num_semantic_residuals", C.c_int64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class SetupInfo(C.Structure):
+    _fields_ = [
+        ("num_residual_blocks", C.c_int64),
+        ("num_residuals_reduced", C.c_int64),
+        ("num_effective_parameters_reduced", C.c_int64),
+        ("num_variable_images", C.c_int64),
+        ("num_variable_cameras", C.c_int64),
+        ("num_variable_points", C.c_int64),
+        ("camera_tangent_size", C.c_int32),
+    ]
+
+
+class SynthConfig(C.Structure):
+    _fields_ = [
+        ("camera_model", C.c_int32),
+        ("num_images", C.c_int32),
+        ("num_points", C.c_int64),
+        ("track_length", C.c_int32),
+        ("image_size", C.c_int32),
+        ("focal_factor", C.c_double),
+        ("extra", C.c_double * 4),
+        ("rotation_range", C.c_double),
+        ("noise", C.c_double),
+        ("seed", C.c_uint32),
+    ]
+
+
+def _ptr(a, t):
+    return None if a is None else a.ctypes.data_as(t)
+
+
+_lib = None
+_synth = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libmi_ba.so; raises if the product library is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libmi_ba.so not built at {path} (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    lib.mi_ba_abi_version.restype = C.c_int32
+    lib.mi_ba_status_string.restype = C.c_char_p
+    lib.mi_ba_status_string.argtypes = [C.c_int32]
+    lib.mi_ba_num_params.restype = C.c_int32
+    lib.mi_ba_num_params.argtypes = [C.c_int32]
+    lib.mi_ba_device_count.argtypes = [_i32p]
+    lib.mi_ba_default_options.argtypes = [C.POINTER(Options)]
+    lib.mi_ba_default_options.restype = None
+    lib.mi_ba_setup_stats.argtypes = [C.POINTER(Options), C.POINTER(Problem), C.POINTER(SetupInfo)]
+    lib.mi_ba_solve.argtypes = [C.POINTER(Options), C.POINTER(Problem), C.POINTER(Semantic), C.POINTER(Summary)]
+    lib.mi_ba_context_create.argtypes = [C.POINTER(Options), C.POINTER(Problem), C.POINTER(Semantic),
+                                         C.POINTER(C.c_void_p)]
+    lib.mi_ba_context_destroy.argtypes = [C.c_void_p]
+    lib.mi_ba_context_destroy.restype = None
+    for name in ("mi_ba_linearize", "mi_ba_evaluate_jacobian", "mi_ba_evaluate_semantic", "mi_ba_synchronize",
+                 "mi_ba_reset_kernel_times"):
+        getattr(lib, name).argtypes = [C.c_void_p]
+    lib.mi_ba_context_dims.argtypes = [C.c_void_p, _i64p, _i32p, _i64p]
+    lib.mi_ba_download_jacobian.argtypes = [C.c_void_p, _i64p, _dp, _dp]
+    lib.mi_ba_download_semantic.argtypes = [C.c_void_p, _i32p, _i32p, _dp, _dp]
+    lib.mi_ba_context_cost.argtypes = [C.c_void_p, _dp]
+    lib.mi_ba_context_solve.argtypes = [C.c_void_p, C.POINTER(Summary)]
+    lib.mi_ba_context_writeback.argtypes = [C.c_void_p]
+    lib.mi_ba_set_timing.argtypes = [C.c_void_p, C.c_int32]
+    lib.mi_ba_kernel_time.argtypes = [C.c_void_p, C.c_char_p, _dp, _i64p]
+    _lib = lib
+    return lib
+
+
+def load_synth(path: str = SYNTH_PATH):
+    global _synth
+    if _synth is not None:
+        return _synth
+    lib = C.CDLL(path)
+    lib.mi_ba_synth_num_obs.restype = C.c_int64
+    lib.mi_ba_synth_num_obs.argtypes = [C.POINTER(SynthConfig)]
+    lib.mi_ba_synth_generate.argtypes = [C.POINTER(SynthConfig), _dp, _dp, _dp, _i32p, _dp, _dp, _i32p, _i32p]
+    lib.mi_ba_synth_render.argtypes = [C.c_int32, C.c_int32, _dp, _dp, _dp, _i32p, C.c_int32, C.c_int32,
+                                       C.c_double, C.c_double, _fp, _fp]
+    _synth = lib
+    return lib
+
+
+class MiBaError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = _lib.mi_ba_status_string(status).decode() if _lib else str(status)
+        super().__init__(f"{what}: mi_ba status {status} ({msg})")
+
+
+def check(status: int, what: str = ""):
+    if status != OK:
+        raise MiBaError(status, what)
+
+
+def default_options(**kw) -> Options:
+    o = Options()
+    load().mi_ba_default_options(C.byref(o))
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise AttributeError(k)
+        setattr(o, k, v)
+    return o
+
+
+@dataclass
+class Scene:
+    """Flattened Reconstruction + BundleAdjustmentConfig (numpy-owned)."""
+    camera_model: int
+    camera_params: np.ndarray            # [C][np] f64
+    qvec: np.ndarray                     # [I][4]
+    tvec: np.ndarray                     # [I][3]
+    image_camera: np.ndarray             # [I] i32
+    xyz: np.ndarray                      # [P][3]
+    obs_xy: np.ndarray                   # [N][2]
+    obs_image: np.ndarray                # [N] i32
+    obs_point: np.ndarray                # [N] i32
+    camera_constant: Optional[np.ndarray] = None
+    image_in_config: Optional[np.ndarray] = None
+    image_constant_pose: Optional[np.ndarray] = None
+    image_constant_tvec: Optional[np.ndarray] = None
+    point_config: Optional[np.ndarray] = None
+    _keep: list = field(default_factory=list, repr=False)
+
+    @property
+    def num_images(self):
+        return int(self.qvec.shape[0])
+
+    @property
+    def num_points(self):
+        return int(self.xyz.shape[0])
+
+    @property
+    def num_obs(self):
+        return int(self.obs_image.shape[0])
+
+    def copy(self) -> "Scene":
+        def c(a):
+            return None if a is None else a.copy()
+        return Scene(self.camera_model, c(self.camera_params), c(self.qvec), c(self.tvec), c(self.image_camera),
+                     c(self.xyz), c(self.obs_xy), c(self.obs_image), c(self.obs_point), c(self.camera_constant),
+                     c(self.image_in_config), c(self.image_constant_pose), c(self.image_constant_tvec),
+                     c(self.point_config))
+
+    def gauge(self, const_pose=0, const_tvec_image=1, const_tvec_mask=1):
+        """BundleAdjustmentController gauge (controllers/bundle_adjustment.cc:94-95)."""
+        I = self.num_images
+        self.image_constant_pose = np.zeros(I, np.uint8)
+        self.image_constant_pose[const_pose] = 1
+        self.image_constant_tvec = np.zeros(I, np.uint8)
+        if const_tvec_image is not None and const_tvec_image < I:
+            self.image_constant_tvec[const_tvec_image] = const_tvec_mask
+        return self
+
+    def _normalize(self):
+        for name, dt in (("camera_params", np.float64), ("qvec", np.float64), ("tvec", np.float64),
+                         ("xyz", np.float64), ("obs_xy", np.float64), ("image_camera", np.int32),
+                         ("obs_image", np.int32), ("obs_point", np.int32)):
+            a = getattr(self, name)
+            if a.dtype != dt or not a.flags.c_contiguous:
+                setattr(self, name, np.ascontiguousarray(a, dtype=dt))
+        for name in ("camera_constant", "image_in_config", "image_constant_pose", "image_constant_tvec",
+                     "point_config"):
+            a = getattr(self, name)
+            if a is not None and (a.dtype != np.uint8 or not a.flags.c_contiguous):
+                setattr(self, name, np.ascontiguousarray(a, dtype=np.uint8))
+
+    def problem(self) -> Problem:
+        self._normalize()
+        p = Problem()
+        p.camera_model = self.camera_model
+        p.num_cameras = self.camera_params.shape[0]
+        p.camera_params = _ptr(self.camera_params, _dp)
+        p.camera_constant = _ptr(self.camera_constant, _u8p)
+        p.num_images = self.num_images
+        p.qvec = _ptr(self.qvec, _dp)
+        p.tvec = _ptr(self.tvec, _dp)
+        p.image_camera = _ptr(self.image_camera, _i32p)
+        p.image_in_config = _ptr(self.image_in_config, _u8p)
+        p.image_constant_pose = _ptr(self.image_constant_pose, _u8p)
+        p.image_constant_tvec = _ptr(self.image_constant_tvec, _u8p)
+        p.num_points = self.num_points
+        p.xyz = _ptr(self.xyz, _dp)
+        p.point_config = _ptr(self.point_config, _u8p)
+        p.num_obs = self.num_obs
+        p.obs_xy = _ptr(self.obs_xy, _dp)
+        p.obs_image = _ptr(self.obs_image, _i32p)
+        p.obs_point = _ptr(self.obs_point, _i32p)
+        return p
+
+
+@dataclass
+class SemanticInput:
+    depth: np.ndarray          # [I][H][W] f32
+    label: np.ndarray          # [I][H][W] f32
+    pairs: np.ndarray          # [K][2] i32
+    pixel_step: int = 10
+    depth_error_threshold: float = 2.0
+    numeric_relative_step_size: float = 1e-3
+
+    def struct(self) -> Semantic:
+        self.depth = np.ascontiguousarray(self.depth, np.float32)
+        self.label = np.ascontiguousarray(self.label, np.float32)
+        self.pairs = np.ascontiguousarray(self.pairs, np.int32).reshape(-1, 2)
+        s = Semantic()
+        s.height = self.depth.shape[1]
+        s.width = self.depth.shape[2]
+        s.depth = _ptr(self.depth, _fp)
+        s.label = _ptr(self.label, _fp)
+        s.num_pairs = self.pairs.shape[0]
+        s.pairs = _ptr(self.pairs, _i32p)
+        s.pixel_step = self.pixel_step
+        s.depth_error_threshold = self.depth_error_threshold
+        s.numeric_relative_step_size = self.numeric_relative_step_size
+        return s
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    load().mi_ba_device_count(C.byref(n))
+    return n.value
+
+
+def setup_stats(options: Options, scene: Scene) -> SetupInfo:
+    info = SetupInfo()
+    p = scene.problem()
+    check(load().mi_ba_setup_stats(C.byref(options), C.byref(p), C.byref(info)), "mi_ba_setup_stats")
+    return info
+
+
+def solve(options: Options, scene: Scene, semantic: Optional[SemanticInput] = None) -> Summary:
+    """BundleAdjuster::Solve on the device; updates scene arrays in place."""
+    s = Summary()
+    p = scene.problem()
+    sem = semantic.struct() if semantic is not None else None
+    st = load().mi_ba_solve(C.byref(options), C.byref(p), C.byref(sem) if sem is not None else None, C.byref(s))
+    check(st, "mi_ba_solve")
+    return s
+
+
+class Context:
+    """Device-resident problem (mi_ba_context_*)."""
+
+    def __init__(self, options: Options, scene: Scene, semantic: Optional[SemanticInput] = None):
+        self.lib = load()
+        self.options = options
+        self.scene = scene
+        self.semantic = semantic
+        self._p = scene.problem()
+        self._s = semantic.struct() if semantic is not None else None
+        h = C.c_void_p()
+        check(self.lib.mi_ba_context_create(C.byref(options), C.byref(self._p),
+                                            C.byref(self._s) if self._s is not None else None, C.byref(h)),
+              "mi_ba_context_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.mi_ba_context_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def dims(self):
+        nb, cols, ns = C.c_int64(), C.c_int32(), C.c_int64()
+        check(self.lib.mi_ba_context_dims(self.h, C.byref(nb), C.byref(cols), C.byref(ns)), "dims")
+        return nb.value, cols.value, ns.value
+
+    def linearize(self):
+        check(self.lib.mi_ba_linearize(self.h), "mi_ba_linearize")
+
+    def evaluate_jacobian(self):
+        check(self.lib.mi_ba_evaluate_jacobian(self.h), "mi_ba_evaluate_jacobian")
+
+    def evaluate_semantic(self):
+        check(self.lib.mi_ba_evaluate_semantic(self.h), "mi_ba_evaluate_semantic")
+
+    def synchronize(self):
+        check(self.lib.mi_ba_synchronize(self.h), "mi_ba_synchronize")
+
+    def download_jacobian(self):
+        nb, cols, _ = self.dims()
+        bo = np.empty(nb, np.int64)
+        r = np.empty((nb, 2), np.float64)
+        J = np.empty((nb, 2, cols), np.float64)
+        check(self.lib.mi_ba_download_jacobian(self.h, _ptr(bo, _i64p), _ptr(r, _dp), _ptr(J, _dp)), "download")
+        return bo, r, J
+
+    def download_semantic(self):
+        _, _, ns = self.dims()
+        px = np.empty((ns, 3), np.int32)
+        st = np.empty(ns, np.int32)
+        r = np.empty(ns, np.float64)
+        J = np.empty((ns, 12), np.float64)
+        check(self.lib.mi_ba_download_semantic(self.h, _ptr(px, _i32p), _ptr(st, _i32p), _ptr(r, _dp),
+                                               _ptr(J, _dp)), "download_semantic")
+        return px, st, r, J
+
+    def solve(self) -> Summary:
+        s = Summary()
+        check(self.lib.mi_ba_context_solve(self.h, C.byref(s)), "mi_ba_context_solve")
+        return s
+
+    def writeback(self):
+        check(self.lib.mi_ba_context_writeback(self.h), "mi_ba_context_writeback")
+
+    def cost(self) -> float:
+        c = C.c_double()
+        check(self.lib.mi_ba_context_cost(self.h, C.byref(c)), "cost")
+        return c.value
+
+    def set_timing(self, on: bool):
+        check(self.lib.mi_ba_set_timing(self.h, 1 if on else 0), "timing")
+
+    def kernel_time(self, name: str):
+        ms, n = C.c_double(), C.c_int64()
+        check(self.lib.mi_ba_kernel_time(self.h, name.encode(), C.byref(ms), C.byref(n)), "kernel_time")
+        return ms.value, n.value
+
+    def reset_kernel_times(self):
+        check(self.lib.mi_ba_reset_kernel_times(self.h), "reset")
+
+
+# ---------------------------------------------------------------------------
+# synthetic scenes (include/mi_ba_synthetic.h)
+# ---------------------------------------------------------------------------
+def synth_config(camera_model=SIMPLE_RADIAL, num_images=2, num_points=100, track_length=0, image_size=1000,
+                 focal_factor=1.2, extra=(0.0, 0.0, 0.0, 0.0), rotation_range=0.0, noise=2.0, seed=0):
+    c = SynthConfig()
+    c.camera_model = camera_model
+    c.num_images = num_images
+    c.num_points = num_points
+    c.track_length = track_length
+    c.image_size = image_size
+    c.focal_factor = focal_factor
+    for k in range(4):
+        c.extra[k] = extra[k] if k < len(extra) else 0.0
+    c.rotation_range = rotation_range
+    c.noise = noise
+    c.seed = seed
+    return c
+
+
+def generate_scene(cfg: SynthConfig) -> Scene:
+    lib = load_synth()
+    n = lib.mi_ba_synth_num_obs(C.byref(cfg))
+    I, P = cfg.num_images, cfg.num_points
+    npar = NUM_PARAMS[cfg.camera_model]
+    cam = np.zeros((I, npar))
+    q = np.zeros((I, 4))
+    t = np.zeros((I, 3))
+    ic = np.zeros(I, np.int32)
+    X = np.zeros((P, 3))
+    xy = np.zeros((n, 2))
+    oi = np.zeros(n, np.int32)
+    op = np.zeros(n, np.int32)
+    st = lib.mi_ba_synth_generate(C.byref(cfg), _ptr(cam, _dp), _ptr(q, _dp), _ptr(t, _dp), _ptr(ic, _i32p),
+                                  _ptr(X, _dp), _ptr(xy, _dp), _ptr(oi, _i32p), _ptr(op, _i32p))
+    if st != 0:
+        raise RuntimeError("mi_ba_synth_generate failed")
+    return Scene(cfg.camera_model, cam, q, t, ic, X, xy, oi, op)
+
+
+def render_semantic(scene: Scene, height: int, width: int, plane_z: float = 1.0, cell: float = 0.1):
+    lib = load_synth()
+    I = scene.num_images
+    scene._normalize()
+    depth = np.zeros((I, height, width), np.float32)
+    label = np.zeros((I, height, width), np.float32)
+    st = lib.mi_ba_synth_render(scene.camera_model, I, _ptr(scene.camera_params, _dp), _ptr(scene.qvec, _dp),
+                                _ptr(scene.tvec, _dp), _ptr(scene.image_camera, _i32p), height, width, plane_z,
+                                cell, _ptr(depth, _fp), _ptr(label, _fp))
+    if st != 0:
+        raise RuntimeError("mi_ba_synth_render failed")
+    return depth, label
