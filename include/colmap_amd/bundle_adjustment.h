@@ -1,0 +1,556 @@
+// colmap_amd/bundle_adjustment.h — C++ facade with the reference's API.
+//
+// Keeps the signatures and semantics COLMAP callers use
+// (src/optim/bundle_adjustment.h:49-203, src/optim/semantic_bundle_adjustment.h:
+// 53-272 of AlainSchoebi/semantic-bundle-adjustment-colmap) and routes Solve
+// to the MI355X library through the C-ABI in mi_ba.h.  Header-only; link
+// against libmi_ba.so.
+//
+//   colmap::BundleAdjustmentOptions          -> colmap_amd::BundleAdjustmentOptions
+//   colmap::BundleAdjustmentConfig           -> colmap_amd::BundleAdjustmentConfig
+//   colmap::BundleAdjuster                   -> colmap_amd::BundleAdjuster
+//   colmap::SemanticBundleAdjustmentOptions  -> colmap_amd::SemanticBundleAdjustmentOptions
+//   colmap::SemanticBundleAdjuster           -> colmap_amd::SemanticBundleAdjuster
+//   ceres::Solver::Summary (fields read)     -> colmap_amd::SolverSummary
+//   colmap::Reconstruction (BA subset)       -> colmap_amd::Reconstruction
+//
+// Error convention: the reference aborts through glog CHECK or throws; here
+// invalid configurations throw std::invalid_argument, unknown camera models
+// std::domain_error, reuse of an adjuster std::logic_error, device/runtime
+// failures std::runtime_error; Solve returns false when there are no
+// residuals (bundle_adjustment.cc:267-269).
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <limits>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../mi_ba.h"
+
+namespace colmap_amd {
+
+typedef uint32_t camera_t;
+typedef uint32_t image_t;
+typedef uint64_t point3D_t;
+typedef uint32_t point2D_t;
+const point3D_t kInvalidPoint3DId = std::numeric_limits<point3D_t>::max();
+
+// ---------------------------------------------------------------------------
+// Minimal Reconstruction (the parts BundleAdjuster touches).
+// ---------------------------------------------------------------------------
+struct Camera {
+  camera_t camera_id = 0;
+  int model_id = MI_BA_SIMPLE_RADIAL;
+  std::vector<double> params;
+  double* ParamsData() { return params.data(); }
+  int ModelId() const { return model_id; }
+  camera_t CameraId() const { return camera_id; }
+};
+
+struct Point2D {
+  double xy[2] = {0, 0};
+  point3D_t point3D_id = kInvalidPoint3DId;
+  bool HasPoint3D() const { return point3D_id != kInvalidPoint3DId; }
+};
+
+struct TrackElement {
+  image_t image_id;
+  point2D_t point2D_idx;
+};
+
+struct Image {
+  image_t image_id = 0;
+  camera_t camera_id = 0;
+  std::string name;
+  double qvec[4] = {1, 0, 0, 0};
+  double tvec[3] = {0, 0, 0};
+  std::vector<Point2D> points2D;
+  image_t ImageId() const { return image_id; }
+  camera_t CameraId() const { return camera_id; }
+  const std::string& Name() const { return name; }
+  size_t NumPoints3D() const {
+    return (size_t)std::count_if(points2D.begin(), points2D.end(), [](const Point2D& p) { return p.HasPoint3D(); });
+  }
+};
+
+struct Point3D {
+  double xyz[3] = {0, 0, 0};
+  std::vector<TrackElement> track;
+};
+
+class Reconstruction {
+ public:
+  std::map<camera_t, Camera> cameras;
+  std::map<image_t, Image> images;
+  std::map<point3D_t, Point3D> points3D;
+
+  Camera& GetCamera(camera_t id) { return cameras.at(id); }
+  Image& GetImage(image_t id) { return images.at(id); }
+  Point3D& GetPoint3D(point3D_t id) { return points3D.at(id); }
+  const Image& GetImage(image_t id) const { return images.at(id); }
+  const Point3D& GetPoint3D(point3D_t id) const { return points3D.at(id); }
+
+  void AddCamera(const Camera& c) { cameras[c.camera_id] = c; }
+  void AddImage(const Image& im) { images[im.image_id] = im; }
+  point3D_t AddPoint3D(const double xyz[3]) {
+    const point3D_t id = ++num_added_points3D_;  // 1-based like COLMAP
+    Point3D p;
+    std::copy(xyz, xyz + 3, p.xyz);
+    points3D[id] = p;
+    return id;
+  }
+  void AddObservation(point3D_t point3D_id, const TrackElement& te) {
+    images.at(te.image_id).points2D.at(te.point2D_idx).point3D_id = point3D_id;
+    points3D.at(point3D_id).track.push_back(te);
+  }
+  void DeleteObservation(image_t image_id, point2D_t point2D_idx) {
+    Point2D& p2 = images.at(image_id).points2D.at(point2D_idx);
+    auto& tr = points3D.at(p2.point3D_id).track;
+    tr.erase(std::remove_if(tr.begin(), tr.end(),
+                            [&](const TrackElement& t) { return t.image_id == image_id && t.point2D_idx == point2D_idx; }),
+             tr.end());
+    p2.point3D_id = kInvalidPoint3DId;
+  }
+
+ private:
+  point3D_t num_added_points3D_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+// Options / config (bundle_adjustment.h:49-167)
+// ---------------------------------------------------------------------------
+struct SolverOptions {  // ceres::Solver::Options subset set by COLMAP
+  double function_tolerance = 0.0;
+  double gradient_tolerance = 0.0;
+  double parameter_tolerance = 0.0;
+  bool minimizer_progress_to_stdout = false;
+  int max_num_iterations = 100;
+  int max_linear_solver_iterations = 200;
+  int max_num_consecutive_invalid_steps = 10;
+  int max_consecutive_nonmonotonic_steps = 10;
+  int num_threads = -1;
+};
+
+struct BundleAdjustmentOptions {
+  enum class LossFunctionType { TRIVIAL, SOFT_L1, CAUCHY };
+  LossFunctionType loss_function_type = LossFunctionType::TRIVIAL;
+  double loss_function_scale = 1.0;
+  bool refine_focal_length = true;
+  bool refine_principal_point = false;
+  bool refine_extra_params = true;
+  bool refine_extrinsics = true;
+  bool print_summary = true;
+  int min_num_residuals_for_multi_threading = 50000;  // kept for API parity
+  SolverOptions solver_options;
+  int device = 0;  // build addition: HIP device ordinal
+
+  bool Check() const {
+    if (loss_function_scale < 0) throw std::invalid_argument("loss_function_scale must be >= 0");
+    return true;
+  }
+};
+
+class BundleAdjustmentConfig {
+ public:
+  size_t NumImages() const { return image_ids_.size(); }
+  size_t NumPoints() const { return variable_point3D_ids_.size() + constant_point3D_ids_.size(); }
+  size_t NumConstantCameras() const { return constant_camera_ids_.size(); }
+  size_t NumConstantPoses() const { return constant_poses_.size(); }
+  size_t NumConstantTvecs() const { return constant_tvecs_.size(); }
+  size_t NumVariablePoints() const { return variable_point3D_ids_.size(); }
+  size_t NumConstantPoints() const { return constant_point3D_ids_.size(); }
+
+  // bundle_adjustment.cc:107-138
+  size_t NumResiduals(const Reconstruction& reconstruction) const {
+    size_t n = 0;
+    for (const image_t id : image_ids_) n += reconstruction.GetImage(id).NumPoints3D();
+    auto per_point = [&](point3D_t id) {
+      size_t m = 0;
+      for (const auto& te : reconstruction.GetPoint3D(id).track)
+        if (image_ids_.count(te.image_id) == 0) m += 1;
+      return m;
+    };
+    for (const auto id : variable_point3D_ids_) n += per_point(id);
+    for (const auto id : constant_point3D_ids_) n += per_point(id);
+    return 2 * n;
+  }
+
+  void AddImage(image_t id) { image_ids_.insert(id); }
+  bool HasImage(image_t id) const { return image_ids_.count(id) != 0; }
+  void RemoveImage(image_t id) { image_ids_.erase(id); }
+
+  void SetConstantCamera(camera_t id) { constant_camera_ids_.insert(id); }
+  void SetVariableCamera(camera_t id) { constant_camera_ids_.erase(id); }
+  bool IsConstantCamera(camera_t id) const { return constant_camera_ids_.count(id) != 0; }
+
+  void SetConstantPose(image_t id) {
+    if (!HasImage(id) || HasConstantTvec(id)) throw std::invalid_argument("SetConstantPose");
+    constant_poses_.insert(id);
+  }
+  void SetVariablePose(image_t id) { constant_poses_.erase(id); }
+  bool HasConstantPose(image_t id) const { return constant_poses_.count(id) != 0; }
+
+  void SetConstantTvec(image_t id, const std::vector<int>& idxs) {
+    std::vector<int> s = idxs;
+    std::sort(s.begin(), s.end());
+    if (idxs.empty() || idxs.size() > 3 || !HasImage(id) || HasConstantPose(id) ||
+        std::adjacent_find(s.begin(), s.end()) != s.end() || s.front() < 0 || s.back() > 2)
+      throw std::invalid_argument("SetConstantTvec");
+    constant_tvecs_.emplace(id, idxs);
+  }
+  void RemoveConstantTvec(image_t id) { constant_tvecs_.erase(id); }
+  bool HasConstantTvec(image_t id) const { return constant_tvecs_.count(id) != 0; }
+
+  void AddVariablePoint(point3D_t id) {
+    if (HasConstantPoint(id)) throw std::invalid_argument("AddVariablePoint");
+    variable_point3D_ids_.insert(id);
+  }
+  void AddConstantPoint(point3D_t id) {
+    if (HasVariablePoint(id)) throw std::invalid_argument("AddConstantPoint");
+    constant_point3D_ids_.insert(id);
+  }
+  bool HasPoint(point3D_t id) const { return HasVariablePoint(id) || HasConstantPoint(id); }
+  bool HasVariablePoint(point3D_t id) const { return variable_point3D_ids_.count(id) != 0; }
+  bool HasConstantPoint(point3D_t id) const { return constant_point3D_ids_.count(id) != 0; }
+  void RemoveVariablePoint(point3D_t id) { variable_point3D_ids_.erase(id); }
+  void RemoveConstantPoint(point3D_t id) { constant_point3D_ids_.erase(id); }
+
+  const std::unordered_set<image_t>& Images() const { return image_ids_; }
+  const std::unordered_set<point3D_t>& VariablePoints() const { return variable_point3D_ids_; }
+  const std::unordered_set<point3D_t>& ConstantPoints() const { return constant_point3D_ids_; }
+  const std::vector<int>& ConstantTvec(image_t id) const { return constant_tvecs_.at(id); }
+
+ private:
+  std::unordered_set<camera_t> constant_camera_ids_;
+  std::unordered_set<image_t> image_ids_;
+  std::unordered_set<point3D_t> variable_point3D_ids_;
+  std::unordered_set<point3D_t> constant_point3D_ids_;
+  std::unordered_set<image_t> constant_poses_;
+  std::unordered_map<image_t, std::vector<int>> constant_tvecs_;
+};
+
+// The ceres::Solver::Summary fields COLMAP reads (PrintSolverSummary).
+struct SolverSummary {
+  enum TerminationType { CONVERGENCE = 0, NO_CONVERGENCE = 1, FAILURE = 2, USER_SUCCESS = 3, USER_FAILURE = 4 };
+  int64_t num_residuals_reduced = 0;
+  int64_t num_effective_parameters_reduced = 0;
+  int num_successful_steps = 0;
+  int num_unsuccessful_steps = 0;
+  TerminationType termination_type = FAILURE;
+  double initial_cost = 0, final_cost = 0, fixed_cost = 0;
+  double total_time_in_seconds = 0;
+  double jacobian_evaluation_time_in_seconds = 0;
+  int num_jacobian_evaluations = 0;
+  int num_linear_solver_iterations = 0;
+};
+
+namespace internal {
+
+inline void ThrowStatus(mi_ba_status st, const char* what) {
+  const std::string msg = std::string(what) + ": " + mi_ba_status_string(st);
+  switch (st) {
+    case MI_BA_OK: return;
+    case MI_BA_ERR_INVALID_ARGUMENT: throw std::invalid_argument(msg);
+    case MI_BA_ERR_UNSUPPORTED: throw std::domain_error(msg);
+    case MI_BA_ERR_STATE: throw std::logic_error(msg);
+    default: throw std::runtime_error(msg);
+  }
+}
+
+// Flattened Reconstruction + config (the layout ParallelBundleAdjuster::SetUp
+// builds, bundle_adjustment.cc:665-783) with id <-> index maps for write-back.
+struct Flat {
+  int model = -1;
+  std::vector<camera_t> cam_ids;
+  std::vector<image_t> img_ids;
+  std::vector<point3D_t> pt_ids;
+  std::vector<double> cam_params, qvec, tvec, xyz, obs_xy;
+  std::vector<int32_t> image_camera, obs_image, obs_point;
+  std::vector<uint8_t> cam_const, img_cfg, img_cpose, img_ctvec, pt_cfg;
+  mi_ba_problem problem{};
+
+  void Build(const Reconstruction& rec, const BundleAdjustmentConfig& cfg) {
+    std::unordered_map<camera_t, int32_t> cidx;
+    std::unordered_map<image_t, int32_t> iidx;
+    std::unordered_map<point3D_t, int32_t> pidx;
+    for (const auto& c : rec.cameras) {
+      if (model < 0) model = c.second.model_id;
+      if (c.second.model_id != model) throw std::domain_error("mixed camera models in one problem");
+      cidx[c.first] = (int32_t)cam_ids.size();
+      cam_ids.push_back(c.first);
+      const int np = mi_ba_num_params(model);
+      if (np < 0) throw std::domain_error("Camera model does not exist");
+      if ((int)c.second.params.size() != np) throw std::invalid_argument("camera params size");
+      cam_params.insert(cam_params.end(), c.second.params.begin(), c.second.params.end());
+      cam_const.push_back(cfg.IsConstantCamera(c.first) ? 1 : 0);
+    }
+    for (const auto& p : rec.points3D) {
+      pidx[p.first] = (int32_t)pt_ids.size();
+      pt_ids.push_back(p.first);
+      xyz.insert(xyz.end(), p.second.xyz, p.second.xyz + 3);
+      pt_cfg.push_back(cfg.HasVariablePoint(p.first) ? 1 : cfg.HasConstantPoint(p.first) ? 2 : 0);
+    }
+    for (const auto& im : rec.images) {
+      const int32_t i = (int32_t)img_ids.size();
+      iidx[im.first] = i;
+      img_ids.push_back(im.first);
+      qvec.insert(qvec.end(), im.second.qvec, im.second.qvec + 4);
+      tvec.insert(tvec.end(), im.second.tvec, im.second.tvec + 3);
+      image_camera.push_back(cidx.at(im.second.camera_id));
+      img_cfg.push_back(cfg.HasImage(im.first) ? 1 : 0);
+      img_cpose.push_back(cfg.HasConstantPose(im.first) ? 1 : 0);
+      uint8_t mask = 0;
+      if (cfg.HasConstantTvec(im.first))
+        for (int k : cfg.ConstantTvec(im.first)) mask |= (uint8_t)(1u << k);
+      img_ctvec.push_back(mask);
+    }
+    // observations: every Point2D with a Point3D (the tracks)
+    for (const auto& im : rec.images) {
+      for (const auto& p2 : im.second.points2D) {
+        if (!p2.HasPoint3D()) continue;
+        obs_xy.push_back(p2.xy[0]);
+        obs_xy.push_back(p2.xy[1]);
+        obs_image.push_back(iidx.at(im.first));
+        obs_point.push_back(pidx.at(p2.point3D_id));
+      }
+    }
+    problem.camera_model = model < 0 ? MI_BA_SIMPLE_RADIAL : model;
+    problem.num_cameras = (int32_t)cam_ids.size();
+    problem.camera_params = cam_params.data();
+    problem.camera_constant = cam_const.data();
+    problem.num_images = (int32_t)img_ids.size();
+    problem.qvec = qvec.data();
+    problem.tvec = tvec.data();
+    problem.image_camera = image_camera.data();
+    problem.image_in_config = img_cfg.data();
+    problem.image_constant_pose = img_cpose.data();
+    problem.image_constant_tvec = img_ctvec.data();
+    problem.num_points = (int64_t)pt_ids.size();
+    problem.xyz = xyz.data();
+    problem.point_config = pt_cfg.data();
+    problem.num_obs = (int64_t)obs_image.size();
+    problem.obs_xy = obs_xy.data();
+    problem.obs_image = obs_image.data();
+    problem.obs_point = obs_point.data();
+  }
+
+  void WriteBack(Reconstruction* rec) const {
+    const int np = mi_ba_num_params(problem.camera_model);
+    for (size_t c = 0; c < cam_ids.size(); ++c)
+      std::copy(cam_params.begin() + c * np, cam_params.begin() + (c + 1) * np,
+                rec->cameras.at(cam_ids[c]).params.begin());
+    for (size_t i = 0; i < img_ids.size(); ++i) {
+      Image& im = rec->images.at(img_ids[i]);
+      std::copy(qvec.begin() + 4 * i, qvec.begin() + 4 * i + 4, im.qvec);
+      std::copy(tvec.begin() + 3 * i, tvec.begin() + 3 * i + 3, im.tvec);
+    }
+    for (size_t k = 0; k < pt_ids.size(); ++k)
+      std::copy(xyz.begin() + 3 * k, xyz.begin() + 3 * k + 3, rec->points3D.at(pt_ids[k]).xyz);
+  }
+};
+
+inline mi_ba_options ToOptions(const BundleAdjustmentOptions& o) {
+  mi_ba_options m;
+  mi_ba_default_options(&m);
+  m.loss_function_type = (int32_t)o.loss_function_type;
+  m.loss_function_scale = o.loss_function_scale;
+  m.refine_focal_length = o.refine_focal_length;
+  m.refine_principal_point = o.refine_principal_point;
+  m.refine_extra_params = o.refine_extra_params;
+  m.refine_extrinsics = o.refine_extrinsics;
+  m.print_summary = o.print_summary;
+  m.max_num_iterations = o.solver_options.max_num_iterations;
+  m.function_tolerance = o.solver_options.function_tolerance;
+  m.gradient_tolerance = o.solver_options.gradient_tolerance;
+  m.parameter_tolerance = o.solver_options.parameter_tolerance;
+  m.max_linear_solver_iterations = o.solver_options.max_linear_solver_iterations;
+  m.max_num_consecutive_invalid_steps = o.solver_options.max_num_consecutive_invalid_steps;
+  m.device = o.device;
+  return m;
+}
+
+inline SolverSummary ToSummary(const mi_ba_summary& s) {
+  SolverSummary o;
+  o.num_residuals_reduced = s.num_residuals_reduced;
+  o.num_effective_parameters_reduced = s.num_effective_parameters_reduced;
+  o.num_successful_steps = s.num_successful_steps;
+  o.num_unsuccessful_steps = s.num_unsuccessful_steps;
+  o.termination_type = (SolverSummary::TerminationType)s.termination_type;
+  o.initial_cost = s.initial_cost;
+  o.final_cost = s.final_cost;
+  o.fixed_cost = s.fixed_cost;
+  o.total_time_in_seconds = s.total_time_in_seconds;
+  o.jacobian_evaluation_time_in_seconds = s.jacobian_evaluation_time_in_seconds;
+  o.num_jacobian_evaluations = s.num_jacobian_evaluations;
+  o.num_linear_solver_iterations = s.num_linear_solver_iterations;
+  return o;
+}
+
+}  // namespace internal
+
+// ---------------------------------------------------------------------------
+// BundleAdjuster (bundle_adjustment.h:171-203)
+// ---------------------------------------------------------------------------
+class BundleAdjuster {
+ public:
+  BundleAdjuster(const BundleAdjustmentOptions& options, const BundleAdjustmentConfig& config)
+      : options_(options), config_(config) {
+    options_.Check();
+  }
+
+  bool Solve(Reconstruction* reconstruction) {
+    if (!reconstruction) throw std::invalid_argument("reconstruction is null");
+    if (used_) throw std::logic_error("Cannot use the same BundleAdjuster multiple times");
+    used_ = true;
+    internal::Flat flat;
+    flat.Build(*reconstruction, config_);
+    const mi_ba_options o = internal::ToOptions(options_);
+    mi_ba_summary s;
+    const mi_ba_status st = mi_ba_solve(&o, &flat.problem, nullptr, &s);
+    if (st == MI_BA_ERR_NO_RESIDUALS) return false;
+    internal::ThrowStatus(st, "BundleAdjuster::Solve");
+    summary_ = internal::ToSummary(s);
+    flat.WriteBack(reconstruction);
+    return true;
+  }
+
+  // Problem-assembly counts without solving (host only).
+  mi_ba_setup_info SetUpInfo(const Reconstruction& reconstruction) const {
+    internal::Flat flat;
+    flat.Build(reconstruction, config_);
+    const mi_ba_options o = internal::ToOptions(options_);
+    mi_ba_setup_info info;
+    internal::ThrowStatus(mi_ba_setup_stats(&o, &flat.problem, &info), "SetUpInfo");
+    return info;
+  }
+
+  const SolverSummary& Summary() const { return summary_; }
+
+ private:
+  BundleAdjustmentOptions options_;
+  BundleAdjustmentConfig config_;
+  SolverSummary summary_;
+  bool used_ = false;
+};
+
+// ---------------------------------------------------------------------------
+// Semantic BA (semantic_bundle_adjustment.h:53-272)
+// ---------------------------------------------------------------------------
+struct SemanticBundleAdjustmentOptions : BundleAdjustmentOptions {
+  double depth_error_threshold = 2;
+  int error_computation_pixel_step = 10;
+  double numeric_relative_step_size = 1e-3;
+  double semantic_weight = 1.0;  // build addition (ScaledLoss weight)
+  SemanticBundleAdjustmentOptions() {
+    solver_options.function_tolerance = 1e-8;
+    solver_options.gradient_tolerance = 1e-8;
+    solver_options.parameter_tolerance = 1e-8;
+  }
+};
+typedef BundleAdjustmentConfig SemanticBundleAdjustmentConfig;
+
+// Depth / semantic maps per image name: row-major H x W float32 (the
+// matrixFromTiff matrices after their vertical flip, matrix_vis.h:130-176).
+struct SemanticMaps {
+  int height = 0, width = 0;
+  std::unordered_map<std::string, std::vector<float>> depth, semantic;
+};
+
+class SemanticBundleAdjuster {
+ public:
+  SemanticBundleAdjuster(const SemanticBundleAdjustmentOptions& options, const SemanticBundleAdjustmentConfig& config,
+                         const SemanticMaps& maps)
+      : options_(options), config_(config), maps_(maps) {
+    options_.Check();
+  }
+
+  bool Solve(Reconstruction* reconstruction) {
+    if (!reconstruction) throw std::invalid_argument("reconstruction is null");
+    if (used_) throw std::logic_error("Cannot use the same BundleAdjuster multiple times");
+    used_ = true;
+    // SemanticBundleAdjuster::Assert (semantic_bundle_adjustment.cc:604-644)
+    if (!options_.refine_extrinsics) throw std::runtime_error("the argument 'refine_extrinsics' must be set to true.");
+    for (const image_t id : config_.Images()) {
+      const Image& im = reconstruction->GetImage(id);
+      if (!config_.IsConstantCamera(im.camera_id))
+        throw std::runtime_error("camera intrinsics of image '" + im.name + "' are not set to constant.");
+    }
+    internal::Flat flat;
+    flat.Build(*reconstruction, config_);
+    // The pose-only semantic problem: no reprojection blocks.
+    flat.problem.num_obs = 0;
+    const int H = maps_.height, W = maps_.width;
+    const size_t plane = (size_t)H * W;
+    std::vector<float> depth(plane * flat.img_ids.size(), 0.f), label(plane * flat.img_ids.size(), 0.f);
+    std::vector<int32_t> pairs;
+    for (size_t i = 0; i < flat.img_ids.size(); ++i) {
+      const Image& im = reconstruction->GetImage(flat.img_ids[i]);
+      auto d = maps_.depth.find(im.name), l = maps_.semantic.find(im.name);
+      if (d == maps_.depth.end() || l == maps_.semantic.end()) {
+        if (config_.HasImage(im.image_id)) throw std::runtime_error("missing depth/semantic map for " + im.name);
+        continue;
+      }
+      std::copy(d->second.begin(), d->second.end(), depth.begin() + i * plane);
+      std::copy(l->second.begin(), l->second.end(), label.begin() + i * plane);
+    }
+    // every ordered pair of config images (SetUp, semantic_bundle_adjustment.cc:656-661)
+    for (size_t i = 0; i < flat.img_ids.size(); ++i)
+      for (size_t j = 0; j < flat.img_ids.size(); ++j)
+        if (flat.img_cfg[i] && flat.img_cfg[j]) {
+          pairs.push_back((int32_t)i);
+          pairs.push_back((int32_t)j);
+        }
+    mi_ba_semantic sem;
+    sem.height = H;
+    sem.width = W;
+    sem.depth = depth.data();
+    sem.label = label.data();
+    sem.num_pairs = (int32_t)(pairs.size() / 2);
+    sem.pairs = pairs.data();
+    sem.pixel_step = options_.error_computation_pixel_step;
+    sem.depth_error_threshold = options_.depth_error_threshold;
+    sem.numeric_relative_step_size = options_.numeric_relative_step_size;
+    mi_ba_options o = internal::ToOptions(options_);
+    o.semantic_weight = options_.semantic_weight;
+    mi_ba_summary s;
+    const mi_ba_status st = mi_ba_solve(&o, &flat.problem, &sem, &s);
+    if (st == MI_BA_ERR_NO_RESIDUALS) return false;
+    internal::ThrowStatus(st, "SemanticBundleAdjuster::Solve");
+    summary_ = internal::ToSummary(s);
+    flat.WriteBack(reconstruction);
+    return true;
+  }
+
+  const SolverSummary& Summary() const { return summary_; }
+
+ private:
+  SemanticBundleAdjustmentOptions options_;
+  SemanticBundleAdjustmentConfig config_;
+  SemanticMaps maps_;
+  SolverSummary summary_;
+  bool used_ = false;
+};
+
+// PrintSolverSummary (bundle_adjustment.cc:1142-1196)
+inline void PrintSolverSummary(const SolverSummary& s) {
+  const char* term = s.termination_type == SolverSummary::CONVERGENCE      ? "Convergence"
+                     : s.termination_type == SolverSummary::NO_CONVERGENCE ? "No convergence"
+                     : s.termination_type == SolverSummary::FAILURE        ? "Failure"
+                                                                           : "Unknown";
+  std::printf("    Residuals : %lld\n   Parameters : %lld\n   Iterations : %d\n         Time : %g [s]\n"
+              " Initial cost : %g [px]\n   Final cost : %g [px]\n  Termination : %s\n\n",
+              (long long)s.num_residuals_reduced, (long long)s.num_effective_parameters_reduced,
+              s.num_successful_steps + s.num_unsuccessful_steps, s.total_time_in_seconds,
+              std::sqrt(s.initial_cost / s.num_residuals_reduced), std::sqrt(s.final_cost / s.num_residuals_reduced),
+              term);
+}
+
+}  // namespace colmap_amd

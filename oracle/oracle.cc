@@ -728,7 +728,15 @@ int64_t oracle_reproj_eval(const mi_ba_options* o, mi_ba_problem* p, int64_t* bl
 #pragma omp parallel for schedule(static)
   for (int64_t b = 0; b < nb; ++b) {
     block_obs[b] = s.block_obs[b];
-    EvalBlock(s, p, b, &residuals[2 * b], jacobian ? &jacobian[b * 2 * w] : nullptr);
+    double* r = &residuals[2 * b];
+    double* J = jacobian ? &jacobian[b * 2 * w] : nullptr;
+    EvalBlock(s, p, b, r, J);
+    // Ceres' evaluator applies the loss Corrector before the linear solver
+    // sees r and J; export them in that (corrected) form.
+    double rho[3];
+    const double sq = r[0] * r[0] + r[1] * r[1];
+    LossEvaluate(o->loss_function_type, o->loss_function_scale, sq, rho);
+    ApplyCorrector(rho, sq, 2, r, w, J);
   }
   return nb;
 }

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
 
 #include <map>
 #include <string>
@@ -81,6 +82,12 @@ struct mi_ba_context {
   miba::DevArray<double> cg_x, cg_r, cg_z, cg_p, cg_q, cg_w, dX;
   miba::DevArray<double> scalars;          // device scalars
   double* host_scalars = nullptr;          // pinned
+
+  // explicit reduced camera system (exact Schur solve, rocSOLVER Cholesky)
+  bool dense = false;
+  rocblas_handle blas = nullptr;
+  miba::DevArray<double> S;
+  miba::DevArray<int32_t> info;
 
   double fixed_cost = 0.0;
   miba::SemanticState* sem = nullptr;

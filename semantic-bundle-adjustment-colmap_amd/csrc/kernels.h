@@ -75,6 +75,13 @@ void launch_plus(const DevProblem& p, const double* df, const double* dX, const 
                  const double* cam, const double* X, double* qt_out, double* cam_out, double* X_out,
                  hipStream_t s);
 
+// Explicit reduced camera system (nf x nf, row-major, both triangles):
+// S += U (tile pass) - sum_p W_p V_p^-1 W_p' (point pass); S must be zeroed.
+void launch_dense_schur(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles, int ntiles,
+                        const uint32_t* cm_perm, const double* J, const double* Vinv, double* S, hipStream_t s);
+// S_kk += Lambda_k on parameter slots, S_kk = 1 on non-parameter slots.
+void launch_dense_finalize(const DevProblem& p, const double* lambda_f, double* S, hipStream_t s);
+
 // Squared norms of df and dX (for the parameter tolerance test).
 void launch_sqnorm2(const double* a, int64_t na, const double* b, int64_t nb, double* out, hipStream_t s);
 

@@ -894,6 +894,128 @@ __global__ __launch_bounds__(1024) void sqnorm2_kernel(const double* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Explicit reduced camera system S = U + Lambda - sum_p W_p V_p^-1 W_p'
+// (the system Ceres' DENSE_SCHUR / SPARSE_SCHUR factorise exactly).
+// ---------------------------------------------------------------------------
+__device__ inline int64_t fslot(const DevProblem& p, uint32_t img, uint32_t cam, int m) {
+  return m < 6 ? 6 * (int64_t)img + m : 6 * (int64_t)p.num_images + (int64_t)p.ct * cam + (m - 6);
+}
+
+// U = sum J_f' J_f, reduced per image-aligned tile (one flush per tile).
+template <int CT>
+__global__ __launch_bounds__(kBlock) void dense_u_kernel(DevProblem p, const DevTile* __restrict__ tiles,
+                                                          const uint32_t* __restrict__ cm_perm,
+                                                          const double* __restrict__ J, double* __restrict__ S) {
+  constexpr int F = 6 + CT;
+  constexpr int NV = F * (F + 1) / 2;
+  __shared__ double sred[4 * NV];
+  const DevTile tile = tiles[blockIdx.x];
+  const int W = 9 + CT;
+  double acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+  for (uint32_t k = threadIdx.x; k < tile.count; k += kBlock) {
+    const uint32_t b = cm_perm[tile.start + k];
+    const double* Jb = J + (size_t)b * 2 * W;
+    double jf[2][F];
+#pragma unroll
+    for (int row = 0; row < 2; ++row) {
+#pragma unroll
+      for (int m = 0; m < 6; ++m) jf[row][m] = Jb[row * W + m];
+#pragma unroll
+      for (int m = 0; m < CT; ++m) jf[row][6 + m] = Jb[row * W + 9 + m];
+    }
+    int o = 0;
+#pragma unroll
+    for (int a = 0; a < F; ++a)
+#pragma unroll
+      for (int c = a; c < F; ++c, ++o) acc[o] += jf[0][a] * jf[0][c] + jf[1][a] * jf[1][c];
+  }
+  block_reduce<NV>(acc, sred);
+  const int k = threadIdx.x;
+  if (k < NV) {
+    int a = 0, rem = k;
+    while (rem >= F - a) { rem -= F - a; ++a; }
+    const int c = a + rem;
+    const uint32_t img = tile.image, cam = p.img_cam[img];
+    const bool pv = p.img_flags[img] & 1u, cv = p.cam_var[cam] != 0;
+    const bool va = a < 6 ? pv : cv, vc = c < 6 ? pv : cv;
+    if (va && vc) {
+      const int64_t ra = fslot(p, img, cam, a), rc = fslot(p, img, cam, c);
+      const double v = sred[k];
+      atomicAdd(S + ra * p.nf + rc, v);
+      if (ra != rc) atomicAdd(S + rc * p.nf + ra, v);
+    }
+  }
+}
+
+// Schur correction: per variable point, -Y_a W_b' for every pair of its
+// observations (a, b), Y_a = W_a V^-1, W = J_f' J_p.
+template <int CT>
+__global__ __launch_bounds__(kBlock) void dense_schur_kernel(DevProblem p, const DevPoint* __restrict__ vp,
+                                                              int64_t npv, const double* __restrict__ J,
+                                                              const double* __restrict__ Vinv,
+                                                              double* __restrict__ S) {
+  constexpr int F = 6 + CT;
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= npv) return;
+  const DevPoint d = vp[k];
+  const int W = 9 + CT;
+  const double* vi = Vinv + 6 * (size_t)d.point;
+  const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
+  for (uint32_t ia = 0; ia < d.count; ++ia) {
+    const uint32_t ba = d.start + ia;
+    const double* Ja = J + (size_t)ba * 2 * W;
+    const uint32_t img_a = p.obs_img[ba], cam_a = p.img_cam[img_a];
+    double Y[F][3];
+#pragma unroll
+    for (int m = 0; m < F; ++m) {
+      const int col = m < 6 ? m : 9 + (m - 6);
+      double w3[3];
+#pragma unroll
+      for (int n = 0; n < 3; ++n) w3[n] = Ja[col] * Ja[6 + n] + Ja[W + col] * Ja[W + 6 + n];
+      sym3_mul(Vi, w3, Y[m]);
+    }
+    for (uint32_t ib = 0; ib < d.count; ++ib) {
+      const uint32_t bb = d.start + ib;
+      const double* Jb = J + (size_t)bb * 2 * W;
+      const uint32_t img_b = p.obs_img[bb], cam_b = p.img_cam[img_b];
+      const double jx0[3] = {Jb[6], Jb[7], Jb[8]}, jx1[3] = {Jb[W + 6], Jb[W + 7], Jb[W + 8]};
+#pragma unroll
+      for (int c = 0; c < F; ++c) {
+        const int col = c < 6 ? c : 9 + (c - 6);
+        const double f0 = Jb[col], f1 = Jb[W + col];
+        if (f0 == 0.0 && f1 == 0.0) continue;
+        const double wb[3] = {f0 * jx0[0] + f1 * jx1[0], f0 * jx0[1] + f1 * jx1[1], f0 * jx0[2] + f1 * jx1[2]};
+        const int64_t rc = fslot(p, img_b, cam_b, c);
+#pragma unroll
+        for (int r = 0; r < F; ++r) {
+          const double v = Y[r][0] * wb[0] + Y[r][1] * wb[1] + Y[r][2] * wb[2];
+          if (v != 0.0) atomicAdd(S + fslot(p, img_a, cam_a, r) * p.nf + rc, -v);
+        }
+      }
+    }
+  }
+}
+
+// Damping on the diagonal; identity on slots that are not parameters.
+__global__ void dense_finalize_kernel(DevProblem p, const double* __restrict__ lambda_f, double* __restrict__ S) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= p.nf) return;
+  bool var;
+  if (k < 6 * (int64_t)p.num_images) {
+    var = p.img_flags[k / 6] & 1u;
+  } else {
+    var = p.cam_var[(k - 6 * (int64_t)p.num_images) / (p.ct > 0 ? p.ct : 1)] != 0;
+  }
+  if (var) {
+    S[k * p.nf + k] += lambda_f[k];
+  } else {
+    S[k * p.nf + k] = 1.0;
+  }
+}
+
 template <typename F>
 void dispatch_ct(int ct, F&& f) {
   switch (ct) {
@@ -1036,6 +1158,22 @@ void launch_plus(const DevProblem& p, const double* df, const double* dX, const 
   if (p.num_points > 0)
     hipLaunchKernelGGL(plus_points_kernel, dim3(grid_for(p.num_points, kBlock)), dim3(kBlock), 0, s, p, dX, X,
                        X_out);
+}
+
+void launch_dense_schur(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles, int ntiles,
+                        const uint32_t* cm_perm, const double* J, const double* Vinv, double* S, hipStream_t s) {
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    if (ntiles > 0)
+      hipLaunchKernelGGL(dense_u_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, J, S);
+    if (npv > 0)
+      hipLaunchKernelGGL(dense_schur_kernel<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, J,
+                         Vinv, S);
+  });
+}
+
+void launch_dense_finalize(const DevProblem& p, const double* lambda_f, double* S, hipStream_t s) {
+  hipLaunchKernelGGL(dense_finalize_kernel, dim3(grid_for(p.nf, kBlock)), dim3(kBlock), 0, s, p, lambda_f, S);
 }
 
 void launch_sqnorm2(const double* a, int64_t na, const double* b, int64_t nb2, double* out, hipStream_t s) {

@@ -25,6 +25,7 @@
 #include "kernels.h"
 #include "semantic.h"
 #include "setup.h"
+#include <rocsolver/rocsolver.h>
 
 namespace miba {
 
@@ -276,6 +277,28 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
   if (P && (hipMemset(ctx->dX.ptr, 0, 3 * P * 8) || hipMemset(ctx->Vinv.ptr, 0, 6 * P * 8) ||
             hipMemset(ctx->cg_w.ptr, 0, 3 * P * 8)))
     return fail(MI_BA_ERR_HIP);
+  // Linear solver (bundle_adjustment.cc:276-286): Ceres factorises the
+  // reduced camera system exactly up to 1000 images (DENSE_SCHUR <= 50,
+  // SPARSE_SCHUR <= 1000 with SuiteSparse) and switches to ITERATIVE_SCHUR +
+  // SCHUR_JACOBI above.  Random tracks make S dense, so the exact path builds
+  // S explicitly in HBM and factorises it with rocSOLVER.
+  {
+    int64_t ncfg = 0;
+    for (int i = 0; i < I; ++i) ncfg += p->image_in_config ? (p->image_in_config[i] != 0) : 1;
+    const double s_bytes = 8.0 * (double)d.nf * (double)d.nf;
+    const bool fits = s_bytes <= 24e9 && d.nf < (1 << 30) / 1;
+    if (o->linear_solver_type == MI_BA_SOLVER_DENSE_SCHUR) {
+      if (!fits) return fail(MI_BA_ERR_UNSUPPORTED);
+      ctx->dense = true;
+    } else if (o->linear_solver_type == MI_BA_SOLVER_AUTO) {
+      ctx->dense = ncfg <= 1000 && fits;
+    }
+    if (ctx->dense) {
+      if (ctx->S.alloc((size_t)d.nf * d.nf) || ctx->info.alloc(1)) return fail(MI_BA_ERR_OUT_OF_MEMORY);
+      if (rocblas_create_handle(&ctx->blas) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
+      if (rocblas_set_stream(ctx->blas, ctx->stream) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
+    }
+  }
   // fixed cost of dropped blocks
   double fixed = 0.0;
   for (int64_t k : s.fixed_obs) fixed += host_block_cost(*o, p, k);
@@ -298,6 +321,7 @@ void context_destroy(mi_ba_context* ctx) {
     (void)hipEventDestroy(e.second.second);
   }
   for (auto e : ctx->timer.pool) (void)hipEventDestroy(e);
+  if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas);
   if (ctx->host_scalars) (void)hipHostFree(ctx->host_scalars);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -395,6 +419,41 @@ mi_ba_status pcg(mi_ba_context* ctx, int* iterations) {
   return MI_BA_OK;
 }
 
+// Exact solve of S df = -b with the explicit reduced camera system.
+// *ok = false when S is not positive definite (Ceres: invalid step).
+mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
+  const DevProblem& d = ctx->dev;
+  hipStream_t s = ctx->stream;
+  const int64_t nf = d.nf;
+  *ok = true;
+  MI_HIP(hipMemsetAsync(ctx->S.ptr, 0, ctx->S.bytes(), s));
+  hipEvent_t stop;
+  timer_begin(ctx, "schur_build", &stop);
+  launch_dense_schur(d, ctx->vpoints.ptr, ctx->npv, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr,
+                     ctx->Vinv.ptr, ctx->S.ptr, s);
+  if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
+  launch_dense_finalize(d, ctx->lambda_f.ptr, ctx->S.ptr, s);
+  timer_end(ctx, stop);
+  MI_HIP(hipMemcpyAsync(ctx->cg_x.ptr, ctx->bvec.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
+  timer_begin(ctx, "cholesky", &stop);
+  // S is symmetric and stored with both triangles: row-major == column-major.
+  if (rocsolver_dpotrf(ctx->blas, rocblas_fill_lower, (rocblas_int)nf, ctx->S.ptr, (rocblas_int)nf,
+                       ctx->info.ptr) != rocblas_status_success)
+    return MI_BA_ERR_HIP;
+  timer_end(ctx, stop);
+  int32_t info = 0;
+  MI_HIP(hipMemcpyAsync(&info, ctx->info.ptr, 4, hipMemcpyDeviceToHost, s));
+  MI_HIP(hipStreamSynchronize(s));
+  if (info != 0) {
+    *ok = false;
+    return MI_BA_OK;
+  }
+  if (rocsolver_dpotrs(ctx->blas, rocblas_fill_lower, (rocblas_int)nf, 1, ctx->S.ptr, (rocblas_int)nf, ctx->cg_x.ptr,
+                       (rocblas_int)nf) != rocblas_status_success)
+    return MI_BA_ERR_HIP;
+  return MI_BA_OK;
+}
+
 }  // namespace
 
 mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
@@ -445,9 +504,26 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     first = false;
     reuse_diag = true;
     int cg_it = 0;
-    st = pcg(ctx, &cg_it);
+    bool solved_ok = true;
+    if (ctx->dense) {
+      st = dense_solve(ctx, &solved_ok);
+      cg_it = 1;
+    } else {
+      st = pcg(ctx, &cg_it);
+    }
     if (st != MI_BA_OK) return st;
     sum->num_linear_solver_iterations += cg_it;
+    if (!solved_ok) {
+      ++consecutive_invalid;
+      ++sum->num_unsuccessful_steps;
+      if (consecutive_invalid > o.max_num_consecutive_invalid_steps) {
+        sum->termination_type = MI_BA_FAILURE;
+        break;
+      }
+      radius = radius / decrease_factor;
+      decrease_factor *= 2.0;
+      continue;
+    }
     // back substitution and model cost change
     launch_backsub(d, ctx->vpoints.ptr, ctx->npv, ctx->J.ptr, ctx->Vg.ptr, ctx->Vinv.ptr, ctx->cg_x.ptr,
                    ctx->dX.ptr, s);
@@ -481,7 +557,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     MI_HIP(hipMemsetAsync(sc + kSemCand, 0, 8, s));
     launch_reproj_cost(d, ctx->qt_c.ptr, ctx->cam_c.ptr, ctx->X_c.ptr, ctx->partial.ptr, s);
     if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kCandCost, s);
-    if (ctx->sem) semantic_cost(ctx, ctx->qt_c.ptr, sc + kSemCand);
+    if (ctx->sem) semantic_cost(ctx, ctx->qt_c.ptr, ctx->cam_c.ptr, sc + kSemCand);
     st = read_scalars(ctx, 0, kNumScalars);
     if (st != MI_BA_OK) return st;
     const double candidate_cost = hs[kCandCost] + hs[kSemCand];
@@ -753,7 +829,7 @@ mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost) {
   MI_HIP(hipMemsetAsync(sc + kSemCand, 0, 8, s));
   launch_reproj_cost(ctx->dev, ctx->qt.ptr, ctx->cam.ptr, ctx->X.ptr, ctx->partial.ptr, s);
   if (ctx->dev.nb) launch_sum(ctx->partial.ptr, reproj_grid(ctx->dev.nb), sc + kCandCost, s);
-  if (ctx->sem) semantic_cost(ctx, ctx->qt.ptr, sc + kSemCand);
+  if (ctx->sem) semantic_cost(ctx, ctx->qt.ptr, ctx->cam.ptr, sc + kSemCand);
   mi_ba_status st = read_scalars(ctx, 0, kNumScalars);
   if (st != MI_BA_OK) return st;
   *cost = ctx->host_scalars[kCandCost] + ctx->host_scalars[kSemCand] + ctx->fixed_cost;

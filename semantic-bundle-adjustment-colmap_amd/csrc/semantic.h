@@ -60,11 +60,13 @@ void semantic_destroy(mi_ba_context* ctx);
 // reduce into per-pair blocks; cost (0.5 * w * sum rho) into *d_cost.
 mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples);
 // Cost only, at parameters qt (candidate evaluation).
-void semantic_cost(mi_ba_context* ctx, const double* qt, double* d_cost);
+void semantic_cost(mi_ba_context* ctx, const double* qt, const double* cam, double* d_cost);
 // Fold the pair blocks into the Schur-Jacobi pose blocks, b and diag(U).
 void semantic_add_fblock(mi_ba_context* ctx);
 // y += M_pair x (implicit Schur product).
 void semantic_schur_product(mi_ba_context* ctx, const double* x, double* y);
+// Add the pair blocks M into the explicit reduced camera system S.
+void semantic_add_dense(mi_ba_context* ctx, double* S);
 // Model cost change contribution -(g'd + d'Md/2) into *d_out.
 void semantic_model_cost(mi_ba_context* ctx, const double* df, double* d_out);
 

@@ -324,6 +324,22 @@ __global__ void semantic_product_kernel(const SemPair* __restrict__ pairs, int n
   }
 }
 
+// Pair blocks into the explicit reduced camera system (both triangles).
+__global__ void semantic_dense_kernel(const SemPair* __restrict__ pairs, int npairs,
+                                      const double* __restrict__ pair_blk, int64_t nf, double* __restrict__ S) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)npairs * 144) return;
+  const int k = (int)(t / 144), e = (int)(t % 144);
+  const int a = e / 12, b = e % 12;
+  const SemPair pr = pairs[k];
+  const bool va = a < 6 ? pr.var1 : pr.var2, vb = b < 6 ? pr.var1 : pr.var2;
+  if (!va || !vb) return;
+  const double v = pair_blk[(size_t)k * kPairStride + (a <= b ? sym12(a, b) : sym12(b, a))];
+  const int64_t ra = 6 * (int64_t)(a < 6 ? pr.i : pr.j) + a % 6;
+  const int64_t rb = 6 * (int64_t)(b < 6 ? pr.i : pr.j) + b % 6;
+  atomicAdd(S + ra * nf + rb, v);
+}
+
 __global__ void semantic_model_kernel(const SemPair* __restrict__ pairs, int npairs,
                                       const double* __restrict__ pair_blk, const double* __restrict__ df,
                                       double* __restrict__ out) {
@@ -350,13 +366,13 @@ __global__ void semantic_model_kernel(const SemPair* __restrict__ pairs, int npa
   if ((threadIdx.x & 63) == 0) atomicAdd(out, v);
 }
 
-SemArgs make_args(mi_ba_context* ctx, const double* qt) {
+SemArgs make_args(mi_ba_context* ctx, const double* qt, const double* cam) {
   SemanticState* S = ctx->sem;
   SemArgs a;
   a.samples = S->samples.ptr;
   a.pairs = S->pairs.ptr;
   a.qt = qt;
-  a.cam = ctx->dev.cam;
+  a.cam = cam;
   a.img_cam = ctx->dev.img_cam;
   a.img_flags = ctx->dev.img_flags;
   a.raster_slot = S->raster_slot.ptr;
@@ -517,7 +533,7 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   hipStream_t s = ctx->stream;
   if (S->npairs && hipMemsetAsync(S->pair_blk.ptr, 0, S->pair_blk.bytes(), s) != hipSuccess) return MI_BA_ERR_HIP;
   if (S->ns == 0) return MI_BA_OK;
-  SemArgs a = make_args(ctx, ctx->dev.qt);
+  SemArgs a = make_args(ctx, ctx->dev.qt, ctx->dev.cam);
   hipEvent_t stop;
   timer_begin(ctx, "semantic_jacobian", &stop);
   dispatch_model(ctx->dev.model, [&](auto m) {
@@ -535,10 +551,10 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   return MI_BA_OK;
 }
 
-void semantic_cost(mi_ba_context* ctx, const double* qt, double* d_cost) {
+void semantic_cost(mi_ba_context* ctx, const double* qt, const double* cam, double* d_cost) {
   SemanticState* S = ctx->sem;
   if (S->ns == 0) return;
-  SemArgs a = make_args(ctx, qt);
+  SemArgs a = make_args(ctx, qt, cam);
   const unsigned g = (unsigned)((S->ns + kBlock - 1) / kBlock);
   dispatch_model(ctx->dev.model, [&](auto m) {
     constexpr int M = decltype(m)::value;
@@ -559,6 +575,14 @@ void semantic_schur_product(mi_ba_context* ctx, const double* x, double* y) {
   if (!S->npairs) return;
   hipLaunchKernelGGL(semantic_product_kernel, dim3((S->npairs + 63) / 64), dim3(64), 0, ctx->stream, S->pairs.ptr,
                      S->npairs, S->pair_blk.ptr, x, y);
+}
+
+void semantic_add_dense(mi_ba_context* ctx, double* S) {
+  SemanticState* S_ = ctx->sem;
+  if (!S_->npairs) return;
+  const int64_t n = (int64_t)S_->npairs * 144;
+  hipLaunchKernelGGL(semantic_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
+                     S_->pairs.ptr, S_->npairs, S_->pair_blk.ptr, ctx->dev.nf, S);
 }
 
 void semantic_model_cost(mi_ba_context* ctx, const double* df, double* d_out) {

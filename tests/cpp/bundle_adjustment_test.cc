@@ -1,0 +1,350 @@
+// bundle_adjustment_test.cc — the reference's BundleAdjuster tests
+// (src/optim/bundle_adjustment_test.cc:111-642), rerun through the
+// colmap_amd facade (include/colmap_amd/bundle_adjustment.h) on libmi_ba.so.
+//
+//   ./bundle_adjustment_test counts   structural counts only (host, no GPU)
+//   ./bundle_adjustment_test solve    full Solve on the MI355X + the
+//                                     CheckVariable*/CheckConstant* assertions
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "colmap_amd/bundle_adjustment.h"
+
+using namespace colmap_amd;
+
+static int g_failures = 0;
+#define CHECK_T(cond)                                                        \
+  do {                                                                       \
+    if (!(cond)) {                                                           \
+      std::printf("  FAILED %s:%d: %s\n", __FILE__, __LINE__, #cond);        \
+      ++g_failures;                                                          \
+    }                                                                        \
+  } while (0)
+
+static std::mt19937* g_prng = nullptr;
+static double RandomReal(double a, double b) { return std::uniform_real_distribution<double>(a, b)(*g_prng); }
+
+// GenerateReconstruction (bundle_adjustment_test.cc:123-184), SIMPLE_RADIAL,
+// f = 1.2 * 1000, identity rotations, tvec = (U, U, 10), U(-2, 2) noise.
+static Reconstruction GenerateReconstruction(int num_images, int num_points) {
+  std::mt19937 prng(0);
+  g_prng = &prng;
+  Reconstruction rec;
+  std::vector<point3D_t> ids;
+  for (int i = 0; i < num_points; ++i) {
+    double xyz[3];
+    xyz[0] = RandomReal(-1, 1);
+    xyz[1] = RandomReal(-1, 1);
+    xyz[2] = RandomReal(-1, 1);
+    ids.push_back(rec.AddPoint3D(xyz));
+  }
+  for (int i = 0; i < num_images; ++i) {
+    Camera cam;
+    cam.camera_id = (camera_t)i;
+    cam.model_id = MI_BA_SIMPLE_RADIAL;
+    cam.params = {1.2 * 1000, 500, 500, 0};
+    rec.AddCamera(cam);
+    Image im;
+    im.image_id = (image_t)i;
+    im.camera_id = (camera_t)i;
+    im.name = std::to_string(i);
+    im.tvec[0] = RandomReal(-1.0, 1.0);
+    im.tvec[1] = RandomReal(-1.0, 1.0);
+    im.tvec[2] = 10;
+    for (point3D_t id : ids) {
+      const double* X = rec.GetPoint3D(id).xyz;
+      const double px = X[0] + im.tvec[0], py = X[1] + im.tvec[1], pz = X[2] + im.tvec[2];
+      const double u = px / pz, v = py / pz;  // SIMPLE_RADIAL with k = 0
+      Point2D p2;
+      p2.xy[0] = 1200 * u + 500 + RandomReal(-2.0, 2.0);
+      p2.xy[1] = 1200 * v + 500 + RandomReal(-2.0, 2.0);
+      im.points2D.push_back(p2);
+    }
+    rec.AddImage(im);
+  }
+  for (int i = 0; i < num_images; ++i) {
+    point2D_t idx = 0;
+    for (point3D_t id : ids) rec.AddObservation(id, TrackElement{(image_t)i, idx++});
+  }
+  return rec;
+}
+
+static bool Same(const double* a, const double* b, int n) { return std::memcmp(a, b, sizeof(double) * n) == 0; }
+static void CheckVariableCamera(Reconstruction& r, const Reconstruction& o, camera_t c) {
+  const auto& a = r.GetCamera(c).params;
+  const auto& b = o.cameras.at(c).params;
+  CHECK_T(a[0] != b[0]);  // focal
+  CHECK_T(a[3] != b[3]);  // radial
+}
+static void CheckConstantCamera(Reconstruction& r, const Reconstruction& o, camera_t c) {
+  CHECK_T(r.GetCamera(c).params == o.cameras.at(c).params);
+}
+static void CheckConstantImage(Reconstruction& r, const Reconstruction& o, image_t i) {
+  CHECK_T(Same(r.GetImage(i).qvec, o.GetImage(i).qvec, 4));
+  CHECK_T(Same(r.GetImage(i).tvec, o.GetImage(i).tvec, 3));
+}
+static void CheckVariableImage(Reconstruction& r, const Reconstruction& o, image_t i) {
+  CHECK_T(!Same(r.GetImage(i).qvec, o.GetImage(i).qvec, 4));
+  CHECK_T(!Same(r.GetImage(i).tvec, o.GetImage(i).tvec, 3));
+}
+static void CheckConstantXImage(Reconstruction& r, const Reconstruction& o, image_t i) {
+  CHECK_T(!Same(r.GetImage(i).qvec, o.GetImage(i).qvec, 4));
+  CHECK_T(r.GetImage(i).tvec[0] == o.GetImage(i).tvec[0]);
+}
+static void CheckVariablePoint(Reconstruction& r, const Reconstruction& o, point3D_t p) {
+  CHECK_T(!Same(r.GetPoint3D(p).xyz, o.GetPoint3D(p).xyz, 3));
+}
+static void CheckConstantPoint(Reconstruction& r, const Reconstruction& o, point3D_t p) {
+  CHECK_T(Same(r.GetPoint3D(p).xyz, o.GetPoint3D(p).xyz, 3));
+}
+
+struct Case {
+  std::string name;
+  std::function<void(bool solve)> run;
+};
+
+// Runs counts (always) and, in solve mode, Solve + checks.
+static void Expect(bool solve, BundleAdjuster& ba, Reconstruction& rec, int64_t residuals, int64_t params,
+                   const std::function<void(Reconstruction&, const Reconstruction&)>& checks) {
+  const mi_ba_setup_info info = ba.SetUpInfo(rec);
+  CHECK_T(info.num_residuals_reduced == residuals);
+  CHECK_T(info.num_effective_parameters_reduced == params);
+  if (!solve) return;
+  const Reconstruction orig = rec;
+  CHECK_T(ba.Solve(&rec));
+  CHECK_T(ba.Summary().num_residuals_reduced == residuals);
+  CHECK_T(ba.Summary().num_effective_parameters_reduced == params);
+  CHECK_T(ba.Summary().final_cost <= ba.Summary().initial_cost);
+  checks(rec, orig);
+  bool threw = false;
+  try {
+    ba.Solve(&rec);
+  } catch (const std::logic_error&) {
+    threw = true;
+  }
+  CHECK_T(threw);  // "Cannot use the same BundleAdjuster multiple times"
+}
+
+int main(int argc, char** argv) {
+  const bool solve = argc > 1 && std::string(argv[1]) == "solve";
+  std::vector<Case> cases;
+
+  cases.push_back({"TestConfigNumObservations", [](bool) {
+    Reconstruction rec = GenerateReconstruction(4, 100);
+    BundleAdjustmentConfig config;
+    config.AddImage(0);
+    config.AddImage(1);
+    CHECK_T(config.NumResiduals(rec) == 400);
+    config.AddVariablePoint(1);
+    CHECK_T(config.NumResiduals(rec) == 404);
+    config.AddConstantPoint(2);
+    CHECK_T(config.NumResiduals(rec) == 408);
+    config.AddImage(2);
+    CHECK_T(config.NumResiduals(rec) == 604);
+    config.AddImage(3);
+    CHECK_T(config.NumResiduals(rec) == 800);
+  }});
+
+  cases.push_back({"TestTwoView", [](bool s) {
+    Reconstruction rec = GenerateReconstruction(2, 100);
+    BundleAdjustmentConfig config;
+    config.AddImage(0);
+    config.AddImage(1);
+    config.SetConstantPose(0);
+    config.SetConstantTvec(1, {0});
+    BundleAdjustmentOptions options;
+    options.print_summary = false;
+    BundleAdjuster ba(options, config);
+    Expect(s, ba, rec, 400, 309, [](Reconstruction& r, const Reconstruction& o) {
+      CheckVariableCamera(r, o, 0);
+      CheckConstantImage(r, o, 0);
+      CheckVariableCamera(r, o, 1);
+      CheckConstantXImage(r, o, 1);
+      for (auto& p : r.points3D) CheckVariablePoint(r, o, p.first);
+    });
+  }});
+
+  cases.push_back({"TestTwoViewConstantCamera", [](bool s) {
+    Reconstruction rec = GenerateReconstruction(2, 100);
+    BundleAdjustmentConfig config;
+    config.AddImage(0);
+    config.AddImage(1);
+    config.SetConstantPose(0);
+    config.SetConstantPose(1);
+    config.SetConstantCamera(0);
+    BundleAdjustmentOptions options;
+    options.print_summary = false;
+    BundleAdjuster ba(options, config);
+    Expect(s, ba, rec, 400, 302, [](Reconstruction& r, const Reconstruction& o) {
+      CheckConstantCamera(r, o, 0);
+      CheckConstantImage(r, o, 0);
+      CheckVariableCamera(r, o, 1);
+      CheckConstantImage(r, o, 1);
+      for (auto& p : r.points3D) CheckVariablePoint(r, o, p.first);
+    });
+  }});
+
+  cases.push_back({"TestPartiallyContainedTracks", [](bool s) {
+    Reconstruction rec = GenerateReconstruction(3, 100);
+    const point3D_t variable_id = rec.GetImage(2).points2D[0].point3D_id;
+    rec.DeleteObservation(2, 0);
+    BundleAdjustmentConfig config;
+    config.AddImage(0);
+    config.AddImage(1);
+    config.SetConstantPose(0);
+    config.SetConstantPose(1);
+    BundleAdjustmentOptions options;
+    options.print_summary = false;
+    BundleAdjuster ba(options, config);
+    Expect(s, ba, rec, 400, 7, [variable_id](Reconstruction& r, const Reconstruction& o) {
+      CheckVariableCamera(r, o, 0);
+      CheckConstantImage(r, o, 0);
+      CheckVariableCamera(r, o, 1);
+      CheckConstantImage(r, o, 1);
+      CheckConstantCamera(r, o, 2);
+      CheckConstantImage(r, o, 2);
+      for (auto& p : r.points3D) {
+        if (p.first == variable_id) CheckVariablePoint(r, o, p.first);
+        else CheckConstantPoint(r, o, p.first);
+      }
+    });
+  }});
+
+  cases.push_back({"TestPartiallyContainedTracksForceToOptimizePoint", [](bool s) {
+    Reconstruction rec = GenerateReconstruction(3, 100);
+    const point3D_t variable_id = rec.GetImage(2).points2D[0].point3D_id;
+    const point3D_t add_variable_id = rec.GetImage(2).points2D[1].point3D_id;
+    const point3D_t add_constant_id = rec.GetImage(2).points2D[2].point3D_id;
+    rec.DeleteObservation(2, 0);
+    BundleAdjustmentConfig config;
+    config.AddImage(0);
+    config.AddImage(1);
+    config.SetConstantPose(0);
+    config.SetConstantPose(1);
+    config.AddVariablePoint(add_variable_id);
+    config.AddConstantPoint(add_constant_id);
+    BundleAdjustmentOptions options;
+    options.print_summary = false;
+    BundleAdjuster ba(options, config);
+    Expect(s, ba, rec, 402, 10, [=](Reconstruction& r, const Reconstruction& o) {
+      CheckVariableCamera(r, o, 0);
+      CheckConstantImage(r, o, 0);
+      CheckVariableCamera(r, o, 1);
+      CheckConstantImage(r, o, 1);
+      CheckConstantCamera(r, o, 2);
+      CheckConstantImage(r, o, 2);
+      for (auto& p : r.points3D) {
+        if (p.first == variable_id || p.first == add_variable_id) CheckVariablePoint(r, o, p.first);
+        else CheckConstantPoint(r, o, p.first);
+      }
+    });
+  }});
+
+  cases.push_back({"TestConstantPoints", [](bool s) {
+    Reconstruction rec = GenerateReconstruction(2, 100);
+    BundleAdjustmentConfig config;
+    config.AddImage(0);
+    config.AddImage(1);
+    config.SetConstantPose(0);
+    config.SetConstantPose(1);
+    config.AddConstantPoint(1);
+    config.AddConstantPoint(2);
+    BundleAdjustmentOptions options;
+    options.print_summary = false;
+    BundleAdjuster ba(options, config);
+    Expect(s, ba, rec, 400, 298, [](Reconstruction& r, const Reconstruction& o) {
+      CheckVariableCamera(r, o, 0);
+      CheckConstantImage(r, o, 0);
+      CheckVariableCamera(r, o, 1);
+      CheckConstantImage(r, o, 1);
+      for (auto& p : r.points3D) {
+        if (p.first == 1 || p.first == 2) CheckConstantPoint(r, o, p.first);
+        else CheckVariablePoint(r, o, p.first);
+      }
+    });
+  }});
+
+  cases.push_back({"TestVariableImage", [](bool s) {
+    Reconstruction rec = GenerateReconstruction(3, 100);
+    BundleAdjustmentConfig config;
+    config.AddImage(0);
+    config.AddImage(1);
+    config.AddImage(2);
+    config.SetConstantPose(0);
+    config.SetConstantTvec(1, {0});
+    BundleAdjustmentOptions options;
+    options.print_summary = false;
+    BundleAdjuster ba(options, config);
+    Expect(s, ba, rec, 600, 317, [](Reconstruction& r, const Reconstruction& o) {
+      CheckVariableCamera(r, o, 0);
+      CheckConstantImage(r, o, 0);
+      CheckVariableCamera(r, o, 1);
+      CheckConstantXImage(r, o, 1);
+      CheckVariableCamera(r, o, 2);
+      CheckVariableImage(r, o, 2);
+      for (auto& p : r.points3D) CheckVariablePoint(r, o, p.first);
+    });
+  }});
+
+  auto focal_case = [](const char* flag, int64_t params) {
+    return [flag, params](bool s) {
+      Reconstruction rec = GenerateReconstruction(2, 100);
+      BundleAdjustmentConfig config;
+      config.AddImage(0);
+      config.AddImage(1);
+      config.SetConstantPose(0);
+      config.SetConstantTvec(1, {0});
+      BundleAdjustmentOptions options;
+      options.print_summary = false;
+      const std::string f(flag);
+      if (f == "focal") options.refine_focal_length = false;
+      if (f == "pp") options.refine_principal_point = true;
+      if (f == "extra") options.refine_extra_params = false;
+      BundleAdjuster ba(options, config);
+      Expect(s, ba, rec, 400, params, [f](Reconstruction& r, const Reconstruction& o) {
+        CheckConstantImage(r, o, 0);
+        CheckConstantXImage(r, o, 1);
+        for (camera_t c = 0; c < 2; ++c) {
+          const auto& a = r.GetCamera(c).params;
+          const auto& b = o.cameras.at(c).params;
+          if (f == "focal") { CHECK_T(a[0] == b[0]); CHECK_T(a[3] != b[3]); }
+          if (f == "pp") { CHECK_T(a[0] != b[0]); CHECK_T(a[1] != b[1]); CHECK_T(a[2] != b[2]); CHECK_T(a[3] != b[3]); }
+          if (f == "extra") { CHECK_T(a[0] != b[0]); CHECK_T(a[3] == b[3]); }
+        }
+        for (auto& p : r.points3D) CheckVariablePoint(r, o, p.first);
+      });
+    };
+  };
+  cases.push_back({"TestConstantFocalLength", focal_case("focal", 307)});
+  cases.push_back({"TestVariablePrincipalPoint", focal_case("pp", 313)});
+  cases.push_back({"TestConstantExtraParam", focal_case("extra", 307)});
+
+  cases.push_back({"TestInvalidConfig", [](bool) {
+    BundleAdjustmentConfig config;
+    bool threw = false;
+    try { config.SetConstantPose(7); } catch (const std::invalid_argument&) { threw = true; }
+    CHECK_T(threw);
+    config.AddImage(1);
+    config.SetConstantTvec(1, {0});
+    threw = false;
+    try { config.SetConstantPose(1); } catch (const std::invalid_argument&) { threw = true; }
+    CHECK_T(threw);
+  }});
+
+  for (auto& c : cases) {
+    const int before = g_failures;
+    try {
+      c.run(solve);
+    } catch (const std::exception& e) {
+      std::printf("  EXCEPTION %s\n", e.what());
+      ++g_failures;
+    }
+    std::printf("%s %s\n", g_failures == before ? "PASS" : "FAIL", c.name.c_str());
+  }
+  std::printf("%d failure(s)\n", g_failures);
+  return g_failures == 0 ? 0 : 1;
+}
