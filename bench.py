@@ -178,13 +178,26 @@ def main():
     # BA-iteration wall time: a few LM iterations on the same resident context
     lm = None
     if args.lm_iters > 0:
-        ctx.options.max_num_iterations = args.lm_iters
+        # warm the LM path (lazy code-object loading of every LM kernel and of
+        # rocSOLVER) on a small scene of the same model before timing it
+        wc = mi_ba.synth_config(cfg["model"], 30, 300, track_length=5, rotation_range=0.05, extra=cfg["extra"])
+        wsc = mi_ba.generate_scene(wc).gauge()
+        wsem = None
+        if sem is not None:
+            wd, wl = mi_ba.render_semantic(wsc, 64, 64, cell=0.5)
+            wsem = mi_ba.SemanticInput(wd, wl, np.array([(i, (i + 1) % 30) for i in range(30)], np.int32),
+                                       pixel_step=8)
+        with mi_ba.Context(mi_ba.default_options(device=local_rank, max_num_iterations=2), wsc, wsem) as wctx:
+            wctx.solve()
         ctx_lm = mi_ba.Context(mi_ba.default_options(device=local_rank, max_num_iterations=args.lm_iters), sc, sem)
+        ctx_lm.set_timing(True)
         s = ctx_lm.solve()
         its = max(1, s.num_successful_steps + s.num_unsuccessful_steps)
         lm = {"ba_iteration_ms": 1e3 * s.total_time_in_seconds / its, "iterations": its,
               "linear_solver_iterations": s.num_linear_solver_iterations,
-              "initial_cost": s.initial_cost, "final_cost": s.final_cost}
+              "initial_cost": s.initial_cost, "final_cost": s.final_cost,
+              "lm_phase_ms_total": {k: ctx_lm.kernel_time(k)[0] for k in
+                                    ("reproj_jacobian", "semantic_jacobian", "schur_build", "cholesky", "pcg")}}
         ctx_lm.close()
 
     if rank == 0:

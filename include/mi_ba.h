@@ -250,6 +250,10 @@ mi_ba_status mi_ba_context_writeback(mi_ba_context* ctx);
 /* Total cost 0.5*sum(rho) at the current parameters (geometric + semantic). */
 mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost);
 
+/* Kernel-variant switches for in-process A/B measurement:
+ *   "stage_jacobian" 0/1 — J rows staged through LDS for coalesced stores. */
+mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value);
+
 /* Per-kernel HIP-event timing on the context's stream (enabled with
  * mi_ba_set_timing).  name: "reproj_jacobian", "semantic_jacobian", ... */
 mi_ba_status mi_ba_set_timing(mi_ba_context* ctx, int32_t enabled);

@@ -210,13 +210,14 @@ __device__ inline void eval_block(const DevProblem& p, const double* __restrict_
   }
 }
 
-template <int M>
+template <int M, bool STAGE>
 __global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
                                                                   double* __restrict__ J_out,
                                                                   double* __restrict__ Vg,
                                                                   double* __restrict__ cost_partial,
                                                                   int write_jacobian) {
   __shared__ double sred[4];
+  extern __shared__ double sJ[];  // STAGE: kBlock x (2W+1) doubles
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   double cost = 0.0;
   uint32_t key = 0xffffffffu;
@@ -230,7 +231,9 @@ __global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, d
     cost = e.cost;
     if (write_jacobian) {
       r_out[i] = make_double2(e.r[0], e.r[1]);
-      double* dst = J_out + (size_t)i * 2 * p.W;
+      // STAGE: rows go through LDS (stride 2W+1 doubles: conflict-free
+      // row writes) and leave as one contiguous, fully coalesced stream.
+      double* dst = STAGE ? sJ + threadIdx.x * (2 * p.W + 1) : J_out + (size_t)i * 2 * p.W;
 #pragma unroll
       for (int row = 0; row < 2; ++row) {
         double* d = dst + row * p.W;
@@ -253,6 +256,20 @@ __global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, d
       vg[6] = a[0] * e.r[0] + b[0] * e.r[1];
       vg[7] = a[1] * e.r[0] + b[1] * e.r[1];
       vg[8] = a[2] * e.r[0] + b[2] * e.r[1];
+    }
+  }
+  if constexpr (STAGE) {
+    __syncthreads();
+    if (write_jacobian) {
+      const int64_t b0 = (int64_t)blockIdx.x * kBlock;
+      const int64_t cnt = p.nb - b0 < kBlock ? p.nb - b0 : kBlock;
+      const int w2 = 2 * p.W;
+      const int64_t total = cnt * w2;
+      double* out = J_out + b0 * w2;
+      for (int64_t idx = threadIdx.x; idx < total; idx += kBlock) {
+        const int row = (int)(idx / w2), k = (int)(idx - (int64_t)row * w2);
+        out[idx] = sJ[row * (w2 + 1) + k];
+      }
     }
   }
   wave_segmented_store<9>(key, ptv, vg, Vg);
@@ -1044,8 +1061,14 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
   const unsigned g = grid_for(p.nb, kBlock);
   dispatch_model(p.model, [&](auto m) {
     constexpr int M = decltype(m)::value;
-    hipLaunchKernelGGL(reproj_jacobian_kernel<M>, dim3(g), dim3(kBlock), 0, s, p, r, J, Vg, cost_partial,
-                       write_jacobian);
+    if (p.stage_jacobian) {
+      const size_t lds = sizeof(double) * kBlock * (2 * p.W + 1);
+      hipLaunchKernelGGL((reproj_jacobian_kernel<M, true>), dim3(g), dim3(kBlock), lds, s, p, r, J, Vg,
+                         cost_partial, write_jacobian);
+    } else {
+      hipLaunchKernelGGL((reproj_jacobian_kernel<M, false>), dim3(g), dim3(kBlock), 0, s, p, r, J, Vg,
+                         cost_partial, write_jacobian);
+    }
   });
 }
 

@@ -248,6 +248,7 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
   d.nf = 6 * (int64_t)I + (int64_t)s.ct * C;
   d.loss_type = o->loss_function_type;
   d.loss_scale = o->loss_function_scale;
+  d.stage_jacobian = 1;
   d.obs_xy = ctx->obs_xy.ptr;
   d.obs_img = ctx->obs_img.ptr;
   d.obs_pt = ctx->obs_pt.ptr;
@@ -509,7 +510,10 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       st = dense_solve(ctx, &solved_ok);
       cg_it = 1;
     } else {
+      hipEvent_t pstop;
+      timer_begin(ctx, "pcg", &pstop);
       st = pcg(ctx, &cg_it);
+      timer_end(ctx, pstop);
     }
     if (st != MI_BA_OK) return st;
     sum->num_linear_solver_iterations += cg_it;
@@ -834,6 +838,15 @@ mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost) {
   if (st != MI_BA_OK) return st;
   *cost = ctx->host_scalars[kCandCost] + ctx->host_scalars[kSemCand] + ctx->fixed_cost;
   return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value) {
+  if (!ctx || !key) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (std::strcmp(key, "stage_jacobian") == 0) {
+    ctx->dev.stage_jacobian = value != 0;
+    return MI_BA_OK;
+  }
+  return MI_BA_ERR_INVALID_ARGUMENT;
 }
 
 mi_ba_status mi_ba_set_timing(mi_ba_context* ctx, int32_t enabled) {

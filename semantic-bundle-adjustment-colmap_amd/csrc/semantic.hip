@@ -107,6 +107,94 @@ __device__ inline double semantic_error(const SemArgs& a, const double pc1[3], f
   return (label1 == label2[off]) ? 0.0 : 1.0;
 }
 
+// ---------------------------------------------------------------------------
+// The same evaluation split into its pose-1 / pose-2 stages so the CENTRAL
+// stencil recomputes only what the perturbed parameter feeds.  Each stage is
+// exactly the operation sequence of semantic_error above, so every stencil
+// value is bitwise the one the unsplit evaluation (and the CPU reference)
+// produces.
+// ---------------------------------------------------------------------------
+struct Pose1Stage {   // depends on q1 (and P_c1)
+  double R[9];        // QuaternionToRotation(q_inv)
+  double rot[3];      // QuaternionRotatePoint(q_inv, P_c1)
+};
+
+__device__ inline void pose1_stage(const double* q1, const double pc1[3], Pose1Stage& s) {
+  const double sc = 1.0 / sqrt(q1[0] * q1[0] + q1[1] * q1[1] + q1[2] * q1[2] + q1[3] * q1[3]);
+  const double qi[4] = {sc * q1[0], -(sc * q1[1]), -(sc * q1[2]), -(sc * q1[3])};
+  const double aa = qi[0] * qi[0], ab = qi[0] * qi[1], ac = qi[0] * qi[2], ad = qi[0] * qi[3];
+  const double bb = qi[1] * qi[1], bc = qi[1] * qi[2], bd = qi[1] * qi[3];
+  const double cc = qi[2] * qi[2], cd = qi[2] * qi[3], dd = qi[3] * qi[3];
+  s.R[0] = aa + bb - cc - dd; s.R[1] = 2.0 * (bc - ad);  s.R[2] = 2.0 * (ac + bd);
+  s.R[3] = 2.0 * (ad + bc);  s.R[4] = aa - bb + cc - dd; s.R[5] = 2.0 * (cd - ab);
+  s.R[6] = 2.0 * (bd - ac);  s.R[7] = 2.0 * (ab + cd);  s.R[8] = aa - bb - cc + dd;
+  double nrm = qi[0] * qi[0] + qi[1] * qi[1] + qi[2] * qi[2] + qi[3] * qi[3];
+  nrm = 1.0 / nrm;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) s.R[k] *= nrm;
+  quat_rotate_point(qi, pc1, s.rot);
+}
+
+// P_w = rot + t_inv with t_inv = -(R t1)
+__device__ inline void pose1_world(const Pose1Stage& s, const double* t1, double pw[3]) {
+  const double ti0 = -(s.R[0] * t1[0] + s.R[1] * t1[1] + s.R[2] * t1[2]);
+  const double ti1 = -(s.R[3] * t1[0] + s.R[4] * t1[1] + s.R[5] * t1[2]);
+  const double ti2 = -(s.R[6] * t1[0] + s.R[7] * t1[1] + s.R[8] * t1[2]);
+  pw[0] = s.rot[0] + ti0;
+  pw[1] = s.rot[1] + ti1;
+  pw[2] = s.rot[2] + ti2;
+}
+
+__device__ inline void unit_quat(const double* q, double u[4]) {
+  const double scale = 1.0 / sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  u[0] = scale * q[0];
+  u[1] = scale * q[1];
+  u[2] = scale * q[2];
+  u[3] = scale * q[3];
+}
+
+struct PixelCache {   // the centre evaluation's raster reads
+  int px, py;
+  float depth, label;
+  bool valid;
+};
+
+// Projection into image 2 and the raster tests (semantic_cost_functions.h:141-205).
+template <int M>
+__device__ inline double project_test(const SemArgs& a, const double p2[3], float label1, const double* K2,
+                                      const float* depth2, const float* label2, PixelCache& pc, bool centre,
+                                      int* status) {
+  const double u2 = p2[0] / p2[2];
+  const double v2 = p2[1] / p2[2];
+  const double measured_depth_2 = p2[2];
+  double x2, y2;
+  world_to_image<M>(K2, u2, v2, &x2, &y2);
+  const int px = cast_to_int_x86(round(x2));
+  const int py = cast_to_int_x86(round(y2));
+  if (px < 0 || px >= a.W || py < 0 || py >= a.H) {
+    *status = MI_BA_OUT_OF_BOUNDS;
+    return 0.0;
+  }
+  float d2, l2;
+  if (!centre && pc.valid && px == pc.px && py == pc.py) {
+    d2 = pc.depth;
+    l2 = pc.label;
+  } else {
+    const size_t off = (size_t)py * a.W + px;
+    d2 = depth2[off];
+    l2 = label2[off];
+    if (centre) {
+      pc.px = px; pc.py = py; pc.depth = d2; pc.label = l2; pc.valid = true;
+    }
+  }
+  if (fabs((double)d2 - measured_depth_2) > a.threshold) {
+    *status = MI_BA_INVALID_DEPTH;
+    return 0.0;
+  }
+  *status = MI_BA_VALID;
+  return (label1 == l2) ? 0.0 : 1.0;
+}
+
 template <int M>
 __global__ __launch_bounds__(kBlock) void semantic_jacobian_kernel(SemArgs a, double* __restrict__ r_out,
                                                                     int32_t* __restrict__ status_out,
@@ -117,15 +205,11 @@ __global__ __launch_bounds__(kBlock) void semantic_jacobian_kernel(SemArgs a, do
   const SemPair pr = a.pairs[smp.pair];
   const double* qt1 = a.qt + 8 * (size_t)pr.i;
   const double* qt2 = a.qt + 8 * (size_t)pr.j;
-  double x[14];
+  double q1[4], t1[3], q2[4], t2[3];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) x[m] = qt1[m];
+  for (int m = 0; m < 4; ++m) { q1[m] = qt1[m]; q2[m] = qt2[m]; }
 #pragma unroll
-  for (int m = 0; m < 3; ++m) x[4 + m] = qt1[4 + m];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) x[7 + m] = qt2[m];
-#pragma unroll
-  for (int m = 0; m < 3; ++m) x[11 + m] = qt2[4 + m];
+  for (int m = 0; m < 3; ++m) { t1[m] = qt1[4 + m]; t2[m] = qt2[4 + m]; }
   constexpr int np = Model<M>::kNumParams;
   double K2[np];
   const double* kc = a.cam + 8 * (size_t)a.img_cam[pr.j];
@@ -134,42 +218,121 @@ __global__ __launch_bounds__(kBlock) void semantic_jacobian_kernel(SemArgs a, do
   const size_t slot = a.raster_slot[pr.j];
   const float* depth2 = a.depth + slot * a.H * a.W;
   const float* label2 = a.label + slot * a.H * a.W;
+  PixelCache pc;
+  pc.valid = false;
+  pc.px = pc.py = 0;
+  pc.depth = pc.label = 0.f;
+  // centre
+  Pose1Stage s1;
+  pose1_stage(q1, smp.pc1, s1);
+  double pw[3];
+  pose1_world(s1, t1, pw);
+  double u2[4];
+  unit_quat(q2, u2);
+  double rot2[3];
+  unit_quat_rotate(u2, pw, rot2);
+  double p2[3] = {rot2[0] + t2[0], rot2[1] + t2[1], rot2[2] + t2[2]};
   int st = 0, st2 = 0;
-  const double r = semantic_error<M>(a, smp.pc1, smp.label1, &x[0], &x[4], &x[7], &x[11], K2, depth2, label2, &st);
+  const double r = project_test<M>(a, p2, smp.label1, K2, depth2, label2, pc, true, &st);
   double Jamb[14];
 #pragma unroll
   for (int m = 0; m < 14; ++m) Jamb[m] = 0.0;
-  const bool var[2] = {pr.var1 != 0, pr.var2 != 0};
+  if (pr.var1) {
+    // q1 stencil: pose-1 stage recomputed, normalised q2 reused
 #pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    if (!var[blk]) continue;
-#pragma unroll
-    for (int m = 0; m < 7; ++m) {
-      const int idx = blk * 7 + m;
-      const double orig = x[idx];
+    for (int m = 0; m < 4; ++m) {
+      const double orig = q1[m];
       const double delta = fmax(kMinStep, fabs(orig) * a.rel_step);
-      x[idx] = orig + delta;
-      const double fp = semantic_error<M>(a, smp.pc1, smp.label1, &x[0], &x[4], &x[7], &x[11], K2, depth2, label2, &st2);
-      x[idx] = orig - delta;
-      const double fm = semantic_error<M>(a, smp.pc1, smp.label1, &x[0], &x[4], &x[7], &x[11], K2, depth2, label2, &st2);
-      x[idx] = orig;
+      double f[2];
+#pragma unroll
+      for (int sgn = 0; sgn < 2; ++sgn) {
+        double qq[4] = {q1[0], q1[1], q1[2], q1[3]};
+        qq[m] = sgn == 0 ? orig + delta : orig - delta;
+        Pose1Stage s;
+        pose1_stage(qq, smp.pc1, s);
+        double w[3], rr[3];
+        pose1_world(s, t1, w);
+        unit_quat_rotate(u2, w, rr);
+        const double pp[3] = {rr[0] + t2[0], rr[1] + t2[1], rr[2] + t2[2]};
+        f[sgn] = project_test<M>(a, pp, smp.label1, K2, depth2, label2, pc, false, &st2);
+      }
       double one_over_delta = 1.0 / delta;
       one_over_delta /= 2;
-      Jamb[idx] = (fp - fm) * one_over_delta;
+      Jamb[m] = (f[0] - f[1]) * one_over_delta;
+    }
+    // t1 stencil: rotation stage of pose 1 reused
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const double orig = t1[m];
+      const double delta = fmax(kMinStep, fabs(orig) * a.rel_step);
+      double f[2];
+#pragma unroll
+      for (int sgn = 0; sgn < 2; ++sgn) {
+        double tt[3] = {t1[0], t1[1], t1[2]};
+        tt[m] = sgn == 0 ? orig + delta : orig - delta;
+        double w[3], rr[3];
+        pose1_world(s1, tt, w);
+        unit_quat_rotate(u2, w, rr);
+        const double pp[3] = {rr[0] + t2[0], rr[1] + t2[1], rr[2] + t2[2]};
+        f[sgn] = project_test<M>(a, pp, smp.label1, K2, depth2, label2, pc, false, &st2);
+      }
+      double one_over_delta = 1.0 / delta;
+      one_over_delta /= 2;
+      Jamb[4 + m] = (f[0] - f[1]) * one_over_delta;
+    }
+  }
+  if (pr.var2) {
+    // q2 stencil: world point reused
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const double orig = q2[m];
+      const double delta = fmax(kMinStep, fabs(orig) * a.rel_step);
+      double f[2];
+#pragma unroll
+      for (int sgn = 0; sgn < 2; ++sgn) {
+        double qq[4] = {q2[0], q2[1], q2[2], q2[3]};
+        qq[m] = sgn == 0 ? orig + delta : orig - delta;
+        double uu[4], rr[3];
+        unit_quat(qq, uu);
+        unit_quat_rotate(uu, pw, rr);
+        const double pp[3] = {rr[0] + t2[0], rr[1] + t2[1], rr[2] + t2[2]};
+        f[sgn] = project_test<M>(a, pp, smp.label1, K2, depth2, label2, pc, false, &st2);
+      }
+      double one_over_delta = 1.0 / delta;
+      one_over_delta /= 2;
+      Jamb[7 + m] = (f[0] - f[1]) * one_over_delta;
+    }
+    // t2 stencil: rotated point reused
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const double orig = t2[m];
+      const double delta = fmax(kMinStep, fabs(orig) * a.rel_step);
+      double f[2];
+#pragma unroll
+      for (int sgn = 0; sgn < 2; ++sgn) {
+        double pp[3] = {rot2[0] + t2[0], rot2[1] + t2[1], rot2[2] + t2[2]};
+        pp[m] = rot2[m] + (sgn == 0 ? orig + delta : orig - delta);
+        f[sgn] = project_test<M>(a, pp, smp.label1, K2, depth2, label2, pc, false, &st2);
+      }
+      double one_over_delta = 1.0 / delta;
+      one_over_delta /= 2;
+      Jamb[11 + m] = (f[0] - f[1]) * one_over_delta;
     }
   }
   double Jt[12];
+  const double xq[2][4] = {{q1[0], q1[1], q1[2], q1[3]}, {q2[0], q2[1], q2[2], q2[3]}};
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const uint32_t img = blk == 0 ? pr.i : pr.j;
     const uint32_t mask = (a.img_flags[img] >> 1) & 7u;
-    if (!var[blk]) {
+    const bool var = blk == 0 ? pr.var1 != 0 : pr.var2 != 0;
+    if (!var) {
 #pragma unroll
       for (int m = 0; m < 6; ++m) Jt[blk * 6 + m] = 0.0;
       continue;
     }
     double PJ[12];
-    quat_plus_jacobian(&x[blk * 7], PJ);
+    quat_plus_jacobian(xq[blk], PJ);
 #pragma unroll
     for (int col = 0; col < 3; ++col) {
       double acc = 0.0;
@@ -182,8 +345,9 @@ __global__ __launch_bounds__(kBlock) void semantic_jacobian_kernel(SemArgs a, do
   }
   r_out[n] = r;
   status_out[n] = st;
+  double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
 #pragma unroll
-  for (int m = 0; m < 12; ++m) J_out[12 * n + m] = Jt[m];
+  for (int m = 0; m < 6; ++m) jo[m] = make_double2(Jt[2 * m], Jt[2 * m + 1]);
 }
 
 template <int M>

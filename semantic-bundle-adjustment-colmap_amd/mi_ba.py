@@ -185,6 +185,7 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_context_solve.argtypes = [C.c_void_p, C.POINTER(Summary)]
     lib.mi_ba_context_writeback.argtypes = [C.c_void_p]
     lib.mi_ba_set_timing.argtypes = [C.c_void_p, C.c_int32]
+    lib.mi_ba_set_tuning.argtypes = [C.c_void_p, C.c_char_p, C.c_int32]
     lib.mi_ba_kernel_time.argtypes = [C.c_void_p, C.c_char_p, _dp, _i64p]
     _lib = lib
     return lib
@@ -441,6 +442,9 @@ class Context:
         c = C.c_double()
         check(self.lib.mi_ba_context_cost(self.h, C.byref(c)), "cost")
         return c.value
+
+    def set_tuning(self, key: str, value: int):
+        check(self.lib.mi_ba_set_tuning(self.h, key.encode(), int(value)), "set_tuning")
 
     def set_timing(self, on: bool):
         check(self.lib.mi_ba_set_timing(self.h, 1 if on else 0), "timing")
