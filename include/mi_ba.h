@@ -250,8 +250,8 @@ mi_ba_status mi_ba_context_writeback(mi_ba_context* ctx);
 /* Total cost 0.5*sum(rho) at the current parameters (geometric + semantic). */
 mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost);
 
-/* Kernel-variant switches for in-process A/B measurement:
- *   "stage_jacobian" 0/1 — J rows staged through LDS for coalesced stores. */
+/* Kernel-variant switches for in-process A/B measurement (key, value);
+ * unknown keys return MI_BA_ERR_INVALID_ARGUMENT. */
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value);
 
 /* Per-kernel HIP-event timing on the context's stream (enabled with

@@ -51,7 +51,7 @@ struct DevProblem {
   int64_t nf;          // f-vector length: 6*I + ct*C (fixed slots, masked)
   int loss_type;
   double loss_scale;
-  int stage_jacobian;  // J rows staged through LDS for coalesced stores
+  int refine_mask;     // bit0 focal, bit1 principal point, bit2 extra params
   // inputs
   const double2* obs_xy;
   const uint32_t* obs_img;

@@ -210,14 +210,43 @@ __device__ inline void eval_block(const DevProblem& p, const double* __restrict_
   }
 }
 
-template <int M, bool STAGE>
+// Refined-intrinsics mask per model and refine flags (bit 0 focal, bit 1
+// principal point, bit 2 extra params): camera_models.h *Idxs, and
+// BundleAdjuster::ParameterizeCameras (bundle_adjustment.cc:480-516).
+__host__ __device__ constexpr unsigned cam_tangent_mask(int M, int RF) {
+  unsigned f = 0, pp = 0, ex = 0;
+  if (M == kSimplePinhole) { f = 0x1; pp = 0x6; ex = 0x0; }
+  if (M == kPinhole) { f = 0x3; pp = 0xC; ex = 0x0; }
+  if (M == kSimpleRadial) { f = 0x1; pp = 0x6; ex = 0x8; }
+  if (M == kRadial) { f = 0x1; pp = 0x6; ex = 0x18; }
+  if (M == kOpenCV) { f = 0x3; pp = 0xC; ex = 0xF0; }
+  return ((RF & 1) ? f : 0u) | ((RF & 2) ? pp : 0u) | ((RF & 4) ? ex : 0u);
+}
+__host__ __device__ constexpr int popcount8(unsigned m) {
+  return (int)((m & 1) + ((m >> 1) & 1) + ((m >> 2) & 1) + ((m >> 3) & 1) + ((m >> 4) & 1) + ((m >> 5) & 1) +
+               ((m >> 6) & 1) + ((m >> 7) & 1));
+}
+
+// One lane per reduced block.  Each Jacobian entry is computed straight into
+// the lane's LDS staging row (row stride 2W+1 doubles: conflict-free row
+// writes); the workgroup then streams its 256 rows out as one contiguous,
+// fully coalesced range of J.  The camera-tangent columns are compile-time
+// (template on the refine flags), so W and the read-out index math are
+// constants.
+template <int M, int RF>
 __global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
                                                                   double* __restrict__ J_out,
                                                                   double* __restrict__ Vg,
                                                                   double* __restrict__ cost_partial,
                                                                   int write_jacobian) {
+  constexpr int np = Model<M>::kNumParams;
+  constexpr unsigned CM = cam_tangent_mask(M, RF);
+  constexpr int CT = popcount8(CM);
+  constexpr int W = 9 + CT;
+  constexpr int W2 = 2 * W;
+  constexpr int LS = W2 + 1;
   __shared__ double sred[4];
-  extern __shared__ double sJ[];  // STAGE: kBlock x (2W+1) doubles
+  __shared__ double sJ[kBlock * LS];
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   double cost = 0.0;
   uint32_t key = 0xffffffffu;
@@ -226,50 +255,124 @@ __global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, d
 #pragma unroll
   for (int k = 0; k < 9; ++k) vg[k] = 0.0;
   if (i < p.nb) {
-    BlockEval<M> e;
-    eval_block<M, true>(p, p.qt, p.cam, p.X, i, e, key, ptv);
-    cost = e.cost;
-    if (write_jacobian) {
-      r_out[i] = make_double2(e.r[0], e.r[1]);
-      // STAGE: rows go through LDS (stride 2W+1 doubles: conflict-free
-      // row writes) and leave as one contiguous, fully coalesced stream.
-      double* dst = STAGE ? sJ + threadIdx.x * (2 * p.W + 1) : J_out + (size_t)i * 2 * p.W;
+    const double2 o = p.obs_xy[i];
+    const uint32_t img = p.obs_img[i];
+    const uint32_t pt = p.obs_pt[i];
+    key = pt;
+    const double* qt = p.qt + 8 * (size_t)img;
+    const double q[4] = {qt[0], qt[1], qt[2], qt[3]};
+    const double t[3] = {qt[4], qt[5], qt[6]};
+    const uint32_t flags = p.img_flags[img];
+    const uint32_t cam_idx = p.img_cam[img];
+    const double* pc = p.cam + 8 * (size_t)cam_idx;
+    double prm[np];
 #pragma unroll
-      for (int row = 0; row < 2; ++row) {
-        double* d = dst + row * p.W;
+    for (int k = 0; k < np; ++k) prm[k] = pc[k];
+    const bool cv = p.cam_var[cam_idx] != 0;
+    ptv = p.pt_var[pt] != 0;
+    const double X[3] = {p.X[3 * (size_t)pt], p.X[3 * (size_t)pt + 1], p.X[3 * (size_t)pt + 2]};
+    double P[3];
+    unit_quat_rotate(q, X, P);
+    P[0] += t[0];
+    P[1] += t[1];
+    P[2] += t[2];
+    const double iz = 1.0 / P[2];
+    const double u = P[0] * iz, v = P[1] * iz;
+    double x, y, A[4], Jp[2 * np];
+    world_to_image_jac<M>(prm, u, v, &x, &y, A, Jp);
+    const double r0 = x - o.x, r1 = y - o.y;
+    double rho[3];
+    loss_eval(p.loss_type, p.loss_scale, r0 * r0 + r1 * r1, rho);
+    cost = 0.5 * rho[0];
+    // Ceres Corrector, rho'' <= 0 branch (Trivial/SoftL1/Cauchy): r, J *= sqrt(rho')
+    const double sc = (p.loss_type == kLossTrivial) ? 1.0 : sqrt(rho[1]);
+    const double cr[2] = {r0 * sc, r1 * sc};
+    // B = d(x,y)/dP (2x3) = A * d(u,v)/dP, loss-scaled
+    double B[6];
+    B[0] = A[0] * iz; B[1] = A[1] * iz; B[2] = -(A[0] * u + A[1] * v) * iz;
+    B[3] = A[2] * iz; B[4] = A[3] * iz; B[5] = -(A[2] * u + A[3] * v) * iz;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) d[k] = e.jr[row][k];
+    for (int k = 0; k < 6; ++k) B[k] *= sc;
+    double* row = sJ + threadIdx.x * LS;
+    if (flags & 1u) {
+      double Dq[12], PJ[12], Mq[9];
+      unit_quat_rotate_dq(q, X, Dq);
+      quat_plus_jacobian(q, PJ);
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (k < p.ct) d[9 + k] = e.jc[row][k];
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+          Mq[a * 3 + b] = Dq[a * 4 + 0] * PJ[0 * 3 + b] + Dq[a * 4 + 1] * PJ[1 * 3 + b] +
+                          Dq[a * 4 + 2] * PJ[2 * 3 + b] + Dq[a * 4 + 3] * PJ[3 * 3 + b];
+#pragma unroll
+      for (int rw = 0; rw < 2; ++rw) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+          row[rw * W + b] = B[rw * 3 + 0] * Mq[b] + B[rw * 3 + 1] * Mq[3 + b] + B[rw * 3 + 2] * Mq[6 + b];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) row[rw * W + 3 + b] = ((flags >> (1 + b)) & 1u) ? 0.0 : B[rw * 3 + b];
+      }
+    } else {
+#pragma unroll
+      for (int rw = 0; rw < 2; ++rw)
+#pragma unroll
+        for (int b = 0; b < 6; ++b) row[rw * W + b] = 0.0;
+    }
+    double jx[2][3];
+    if (ptv) {
+      double R[9];
+      unit_quat_matrix(q, R);
+#pragma unroll
+      for (int rw = 0; rw < 2; ++rw)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+          jx[rw][b] = B[rw * 3 + 0] * R[b] + B[rw * 3 + 1] * R[3 + b] + B[rw * 3 + 2] * R[6 + b];
+    } else {
+#pragma unroll
+      for (int rw = 0; rw < 2; ++rw)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) jx[rw][b] = 0.0;
+    }
+#pragma unroll
+    for (int rw = 0; rw < 2; ++rw)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) row[rw * W + 6 + b] = jx[rw][b];
+    // refined intrinsics (SubsetManifold PlusJacobian = column selection)
+    {
+      int c = 0;
+#pragma unroll
+      for (int m = 0; m < np; ++m) {
+        if ((CM >> m) & 1u) {
+          row[9 + c] = cv ? Jp[m] * sc : 0.0;
+          row[W + 9 + c] = cv ? Jp[np + m] * sc : 0.0;
+          ++c;
+        }
       }
     }
+    if (write_jacobian) r_out[i] = make_double2(cr[0], cr[1]);
     if (ptv) {
-      const double* a = e.jr[0] + 6;
-      const double* b = e.jr[1] + 6;
+      const double* a = jx[0];
+      const double* b = jx[1];
       vg[0] = a[0] * a[0] + b[0] * b[0];
       vg[1] = a[0] * a[1] + b[0] * b[1];
       vg[2] = a[0] * a[2] + b[0] * b[2];
       vg[3] = a[1] * a[1] + b[1] * b[1];
       vg[4] = a[1] * a[2] + b[1] * b[2];
       vg[5] = a[2] * a[2] + b[2] * b[2];
-      vg[6] = a[0] * e.r[0] + b[0] * e.r[1];
-      vg[7] = a[1] * e.r[0] + b[1] * e.r[1];
-      vg[8] = a[2] * e.r[0] + b[2] * e.r[1];
+      vg[6] = a[0] * cr[0] + b[0] * cr[1];
+      vg[7] = a[1] * cr[0] + b[1] * cr[1];
+      vg[8] = a[2] * cr[0] + b[2] * cr[1];
     }
   }
-  if constexpr (STAGE) {
-    __syncthreads();
-    if (write_jacobian) {
-      const int64_t b0 = (int64_t)blockIdx.x * kBlock;
-      const int64_t cnt = p.nb - b0 < kBlock ? p.nb - b0 : kBlock;
-      const int w2 = 2 * p.W;
-      const int64_t total = cnt * w2;
-      double* out = J_out + b0 * w2;
-      for (int64_t idx = threadIdx.x; idx < total; idx += kBlock) {
-        const int row = (int)(idx / w2), k = (int)(idx - (int64_t)row * w2);
-        out[idx] = sJ[row * (w2 + 1) + k];
-      }
+  __syncthreads();
+  if (write_jacobian) {
+    const int64_t b0 = (int64_t)blockIdx.x * kBlock;
+    const int cnt = p.nb - b0 < kBlock ? (int)(p.nb - b0) : kBlock;
+    const int total = cnt * W2;
+    double* out = J_out + b0 * W2;
+    for (int idx = threadIdx.x; idx < total; idx += kBlock) {
+      const int rr = idx / W2, k = idx - rr * W2;
+      out[idx] = sJ[rr * LS + k];
     }
   }
   wave_segmented_store<9>(key, ptv, vg, Vg);
@@ -1061,13 +1164,20 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
   const unsigned g = grid_for(p.nb, kBlock);
   dispatch_model(p.model, [&](auto m) {
     constexpr int M = decltype(m)::value;
-    if (p.stage_jacobian) {
-      const size_t lds = sizeof(double) * kBlock * (2 * p.W + 1);
-      hipLaunchKernelGGL((reproj_jacobian_kernel<M, true>), dim3(g), dim3(kBlock), lds, s, p, r, J, Vg,
-                         cost_partial, write_jacobian);
-    } else {
-      hipLaunchKernelGGL((reproj_jacobian_kernel<M, false>), dim3(g), dim3(kBlock), 0, s, p, r, J, Vg,
-                         cost_partial, write_jacobian);
+    auto go = [&](auto rf) {
+      constexpr int RF = decltype(rf)::value;
+      hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF>), dim3(g), dim3(kBlock), 0, s, p, r, J, Vg, cost_partial,
+                         write_jacobian);
+    };
+    switch (p.refine_mask & 7) {
+      case 0: go(std::integral_constant<int, 0>{}); break;
+      case 1: go(std::integral_constant<int, 1>{}); break;
+      case 2: go(std::integral_constant<int, 2>{}); break;
+      case 3: go(std::integral_constant<int, 3>{}); break;
+      case 4: go(std::integral_constant<int, 4>{}); break;
+      case 5: go(std::integral_constant<int, 5>{}); break;
+      case 6: go(std::integral_constant<int, 6>{}); break;
+      default: go(std::integral_constant<int, 7>{}); break;
     }
   });
 }

@@ -248,7 +248,8 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
   d.nf = 6 * (int64_t)I + (int64_t)s.ct * C;
   d.loss_type = o->loss_function_type;
   d.loss_scale = o->loss_function_scale;
-  d.stage_jacobian = 1;
+  d.refine_mask = (o->refine_focal_length ? 1 : 0) | (o->refine_principal_point ? 2 : 0) |
+                  (o->refine_extra_params ? 4 : 0);
   d.obs_xy = ctx->obs_xy.ptr;
   d.obs_img = ctx->obs_img.ptr;
   d.obs_pt = ctx->obs_pt.ptr;
@@ -842,11 +843,9 @@ mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost) {
 
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value) {
   if (!ctx || !key) return MI_BA_ERR_INVALID_ARGUMENT;
-  if (std::strcmp(key, "stage_jacobian") == 0) {
-    ctx->dev.stage_jacobian = value != 0;
-    return MI_BA_OK;
-  }
-  return MI_BA_ERR_INVALID_ARGUMENT;
+  (void)value;
+  (void)ctx;
+  return MI_BA_ERR_INVALID_ARGUMENT;  // no tunable variants in this build
 }
 
 mi_ba_status mi_ba_set_timing(mi_ba_context* ctx, int32_t enabled) {

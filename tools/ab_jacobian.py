@@ -1,5 +1,5 @@
-"""In-process A/B of reproj_jacobian kernel variants (interleaved rounds,
-HIP-event timing on the context stream).  Usage:
+"""Times the reproj_jacobian kernel alone on a BASELINE config (HIP events on
+the context stream, interleaved rounds) and reports GB/s vs the 8 TB/s peak.
     python tools/ab_jacobian.py [--config C4] [--rounds 5] [--reps 5]
 """
 import argparse
@@ -27,32 +27,22 @@ sc = mi_ba.generate_scene(c).gauge()
 ctx = mi_ba.Context(mi_ba.default_options(), sc)
 nb, W, _ = ctx.dims()
 bpb = bench.bytes_per_block(cfg["model"], cfg["track"])
-variants = {"direct": 0, "lds_staged": 1}
-res = {k: [] for k in variants}
-sums = {}
-for name, v in variants.items():
-    ctx.set_tuning("stage_jacobian", v)
-    ctx.evaluate_jacobian()
-    ctx.synchronize()
-    _, r, J = ctx.download_jacobian()
-    sums[name] = (float(np.abs(r).sum()), float(np.abs(J).sum()))
-    del r, J
+ctx.evaluate_jacobian()
+ctx.synchronize()
+_, r, J = ctx.download_jacobian()
+checksum = (float(np.abs(r).sum()), float(np.abs(J).sum()))
+del r, J
+res = []
 for rnd in range(args.rounds):
-    for name, v in variants.items():
-        ctx.set_tuning("stage_jacobian", v)
+    ctx.set_timing(True)
+    ctx.reset_kernel_times()
+    for _ in range(args.reps):
         ctx.evaluate_jacobian()
-        ctx.synchronize()
-        ctx.set_timing(True)
-        ctx.reset_kernel_times()
-        for _ in range(args.reps):
-            ctx.evaluate_jacobian()
-        ms, n = ctx.kernel_time("reproj_jacobian")
-        ctx.set_timing(False)
-        res[name].append(ms / n)
-out = {}
-for name in variants:
-    med = float(np.median(res[name]))
-    out[name] = {"median_ms": med, "min_ms": float(np.min(res[name])), "GBps": bpb * nb / (med * 1e-3) / 1e9,
-                 "frac_of_8TBps": bpb * nb / (med * 1e-3) / 8e12, "checksum": sums[name]}
-print(json.dumps({"config": args.config, "blocks": nb, "bytes_per_block": bpb, "variants": out}))
+    ms, n = ctx.kernel_time("reproj_jacobian")
+    ctx.set_timing(False)
+    res.append(ms / n)
+med = float(np.median(res))
+print(json.dumps({"config": args.config, "blocks": nb, "bytes_per_block": bpb, "median_ms": med,
+                  "min_ms": float(np.min(res)), "GBps": bpb * nb / (med * 1e-3) / 1e9,
+                  "frac_of_8TBps": bpb * nb / (med * 1e-3) / 8e12, "checksum": checksum}))
 ctx.close()
