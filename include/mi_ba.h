@@ -220,7 +220,9 @@ void mi_ba_context_destroy(mi_ba_context* ctx);
 mi_ba_status mi_ba_linearize(mi_ba_context* ctx);
 /* Residual+Jacobian kernel alone (the J-materialising evaluation). */
 mi_ba_status mi_ba_evaluate_jacobian(mi_ba_context* ctx);
-/* Semantic residual+Jacobian kernel alone. */
+/* Semantic residual+Jacobian kernel alone, also storing the per-sample
+ * residual / status / Jacobian for mi_ba_download_semantic (the solver's
+ * linearization reduces them into pair blocks without storing them). */
 mi_ba_status mi_ba_evaluate_semantic(mi_ba_context* ctx);
 mi_ba_status mi_ba_synchronize(mi_ba_context* ctx);
 
@@ -236,7 +238,8 @@ mi_ba_status mi_ba_context_dims(const mi_ba_context* ctx, int64_t* num_blocks,
  *             and constant tvec coordinates are zero. */
 mi_ba_status mi_ba_download_jacobian(mi_ba_context* ctx, int64_t* block_obs,
                                      double* residuals, double* jacobian);
-/* Semantic samples, ordered by pair then (y, x):
+/* Semantic samples of the last mi_ba_evaluate_semantic (MI_BA_ERR_STATE
+ * when the last semantic evaluation did not store them), ordered by pair then (y, x):
  *   sample_pixel [n][3] (pair index, x1, y1); status [n]; residual [n];
  *   jacobian [n][12] = pose1 (rot3, trans3), pose2 (rot3, trans3). */
 mi_ba_status mi_ba_download_semantic(mi_ba_context* ctx, int32_t* sample_pixel,

@@ -52,6 +52,7 @@ struct DevProblem {
   int loss_type;
   double loss_scale;
   int refine_mask;     // bit0 focal, bit1 principal point, bit2 extra params
+  int jvariant;        // Jacobian store path (kernels.hip reproj_jacobian_kernel V)
   // inputs
   const double2* obs_xy;
   const uint32_t* obs_img;

@@ -227,14 +227,56 @@ __host__ __device__ constexpr int popcount8(unsigned m) {
                ((m >> 6) & 1) + ((m >> 7) & 1));
 }
 
-// One lane per reduced block.  Each Jacobian entry is computed straight into
-// the lane's LDS staging row (row stride 2W+1 doubles: conflict-free row
-// writes); the workgroup then streams its 256 rows out as one contiguous,
-// fully coalesced range of J.  The camera-tangent columns are compile-time
-// (template on the refine flags), so W and the read-out index math are
-// constants.
-template <int M, int RF>
-__global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
+// Jacobian entries of one block row (rw = 0: x, 1: y) into dst[0..W).
+// Columns: rotation tangent (3), translation (3), point (3), refined
+// intrinsics (CT, SubsetManifold PlusJacobian = column selection).
+template <int M, unsigned CM>
+__device__ inline void emit_row(int rw, double* dst, const double (&B)[6], const double (&Mq)[9], bool pose_var,
+                                uint32_t flags, const double (&jx)[2][3], const double* Jp, double sc, bool cv) {
+  constexpr int np = Model<M>::kNumParams;
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+    dst[b] = pose_var ? B[rw * 3 + 0] * Mq[b] + B[rw * 3 + 1] * Mq[3 + b] + B[rw * 3 + 2] * Mq[6 + b] : 0.0;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) dst[3 + b] = (pose_var && !((flags >> (1 + b)) & 1u)) ? B[rw * 3 + b] : 0.0;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) dst[6 + b] = jx[rw][b];
+  int c = 0;
+#pragma unroll
+  for (int m = 0; m < np; ++m) {
+    if ((CM >> m) & 1u) {
+      dst[9 + c] = cv ? Jp[rw * np + m] * sc : 0.0;
+      ++c;
+    }
+  }
+}
+
+// Copy NR rows of R doubles (LDS stride LS) into a global range whose rows
+// are G doubles apart, one wavefront, 8 B per lane per step.
+template <int R, int LS, int G>
+__device__ inline void wave_readout(const double* __restrict__ src, double* __restrict__ dst, int nrows) {
+  const int lane = threadIdx.x & 63;
+  const int total = nrows * R;
+  int row = lane / R, col = lane - (lane / R) * R;
+  constexpr int dr = 64 / R, dc = 64 % R;
+#pragma unroll 4
+  for (int e = lane; e < total; e += 64) {
+    dst[row * G + col] = src[row * LS + col];
+    row += dr;
+    col += dc;
+    if (col >= R) { col -= R; ++row; }
+  }
+}
+
+// One lane per reduced block, one wavefront per 64 consecutive blocks.
+// V selects the store path (A/B-tested, tools/ab_jacobian.py):
+//   V = 0  workgroup-shared LDS rows (2W+1 stride), one barrier, 8-B stores;
+//   V = 1  wave-private LDS rows, no workgroup barrier;
+//   V = 2  wave-private half rows (x then y, W stride): half the LDS, twice
+//          the occupancy.
+// The camera-tangent columns are compile-time (template on the refine flags).
+template <int M, int RF, int V>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(V == 2 ? 4 : 1))) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
                                                                   double* __restrict__ J_out,
                                                                   double* __restrict__ Vg,
                                                                   double* __restrict__ cost_partial,
@@ -244,16 +286,25 @@ __global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, d
   constexpr int CT = popcount8(CM);
   constexpr int W = 9 + CT;
   constexpr int W2 = 2 * W;
-  constexpr int LS = W2 + 1;
+  constexpr int LS = (V == 2) ? (W | 1) : (W2 | 1);
   __shared__ double sred[4];
   __shared__ double sJ[kBlock * LS];
+  const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t wb0 = i - lane;  // first block of this wavefront
   double cost = 0.0;
   uint32_t key = 0xffffffffu;
   bool ptv = false;
   double vg[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) vg[k] = 0.0;
+  double B[6] = {0, 0, 0, 0, 0, 0}, Mq[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, jx[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  double Jp[2 * np];
+#pragma unroll
+  for (int k = 0; k < 2 * np; ++k) Jp[k] = 0.0;
+  double sc = 1.0;
+  bool cv = false, pose_var = false;
+  uint32_t flags = 0;
   if (i < p.nb) {
     const double2 o = p.obs_xy[i];
     const uint32_t img = p.obs_img[i];
@@ -262,13 +313,14 @@ __global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, d
     const double* qt = p.qt + 8 * (size_t)img;
     const double q[4] = {qt[0], qt[1], qt[2], qt[3]};
     const double t[3] = {qt[4], qt[5], qt[6]};
-    const uint32_t flags = p.img_flags[img];
+    flags = p.img_flags[img];
+    pose_var = flags & 1u;
     const uint32_t cam_idx = p.img_cam[img];
     const double* pc = p.cam + 8 * (size_t)cam_idx;
     double prm[np];
 #pragma unroll
     for (int k = 0; k < np; ++k) prm[k] = pc[k];
-    const bool cv = p.cam_var[cam_idx] != 0;
+    cv = p.cam_var[cam_idx] != 0;
     ptv = p.pt_var[pt] != 0;
     const double X[3] = {p.X[3 * (size_t)pt], p.X[3 * (size_t)pt + 1], p.X[3 * (size_t)pt + 2]};
     double P[3];
@@ -278,24 +330,22 @@ __global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, d
     P[2] += t[2];
     const double iz = 1.0 / P[2];
     const double u = P[0] * iz, v = P[1] * iz;
-    double x, y, A[4], Jp[2 * np];
+    double x, y, A[4];
     world_to_image_jac<M>(prm, u, v, &x, &y, A, Jp);
     const double r0 = x - o.x, r1 = y - o.y;
     double rho[3];
     loss_eval(p.loss_type, p.loss_scale, r0 * r0 + r1 * r1, rho);
     cost = 0.5 * rho[0];
     // Ceres Corrector, rho'' <= 0 branch (Trivial/SoftL1/Cauchy): r, J *= sqrt(rho')
-    const double sc = (p.loss_type == kLossTrivial) ? 1.0 : sqrt(rho[1]);
+    sc = (p.loss_type == kLossTrivial) ? 1.0 : sqrt(rho[1]);
     const double cr[2] = {r0 * sc, r1 * sc};
     // B = d(x,y)/dP (2x3) = A * d(u,v)/dP, loss-scaled
-    double B[6];
     B[0] = A[0] * iz; B[1] = A[1] * iz; B[2] = -(A[0] * u + A[1] * v) * iz;
     B[3] = A[2] * iz; B[4] = A[3] * iz; B[5] = -(A[2] * u + A[3] * v) * iz;
 #pragma unroll
     for (int k = 0; k < 6; ++k) B[k] *= sc;
-    double* row = sJ + threadIdx.x * LS;
-    if (flags & 1u) {
-      double Dq[12], PJ[12], Mq[9];
+    if (pose_var) {
+      double Dq[12], PJ[12];
       unit_quat_rotate_dq(q, X, Dq);
       quat_plus_jacobian(q, PJ);
 #pragma unroll
@@ -304,21 +354,7 @@ __global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, d
         for (int b = 0; b < 3; ++b)
           Mq[a * 3 + b] = Dq[a * 4 + 0] * PJ[0 * 3 + b] + Dq[a * 4 + 1] * PJ[1 * 3 + b] +
                           Dq[a * 4 + 2] * PJ[2 * 3 + b] + Dq[a * 4 + 3] * PJ[3 * 3 + b];
-#pragma unroll
-      for (int rw = 0; rw < 2; ++rw) {
-#pragma unroll
-        for (int b = 0; b < 3; ++b)
-          row[rw * W + b] = B[rw * 3 + 0] * Mq[b] + B[rw * 3 + 1] * Mq[3 + b] + B[rw * 3 + 2] * Mq[6 + b];
-#pragma unroll
-        for (int b = 0; b < 3; ++b) row[rw * W + 3 + b] = ((flags >> (1 + b)) & 1u) ? 0.0 : B[rw * 3 + b];
-      }
-    } else {
-#pragma unroll
-      for (int rw = 0; rw < 2; ++rw)
-#pragma unroll
-        for (int b = 0; b < 6; ++b) row[rw * W + b] = 0.0;
     }
-    double jx[2][3];
     if (ptv) {
       double R[9];
       unit_quat_matrix(q, R);
@@ -327,52 +363,55 @@ __global__ __launch_bounds__(kBlock) void reproj_jacobian_kernel(DevProblem p, d
 #pragma unroll
         for (int b = 0; b < 3; ++b)
           jx[rw][b] = B[rw * 3 + 0] * R[b] + B[rw * 3 + 1] * R[3 + b] + B[rw * 3 + 2] * R[6 + b];
-    } else {
-#pragma unroll
-      for (int rw = 0; rw < 2; ++rw)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) jx[rw][b] = 0.0;
-    }
-#pragma unroll
-    for (int rw = 0; rw < 2; ++rw)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) row[rw * W + 6 + b] = jx[rw][b];
-    // refined intrinsics (SubsetManifold PlusJacobian = column selection)
-    {
-      int c = 0;
-#pragma unroll
-      for (int m = 0; m < np; ++m) {
-        if ((CM >> m) & 1u) {
-          row[9 + c] = cv ? Jp[m] * sc : 0.0;
-          row[W + 9 + c] = cv ? Jp[np + m] * sc : 0.0;
-          ++c;
-        }
-      }
+      vg[0] = jx[0][0] * jx[0][0] + jx[1][0] * jx[1][0];
+      vg[1] = jx[0][0] * jx[0][1] + jx[1][0] * jx[1][1];
+      vg[2] = jx[0][0] * jx[0][2] + jx[1][0] * jx[1][2];
+      vg[3] = jx[0][1] * jx[0][1] + jx[1][1] * jx[1][1];
+      vg[4] = jx[0][1] * jx[0][2] + jx[1][1] * jx[1][2];
+      vg[5] = jx[0][2] * jx[0][2] + jx[1][2] * jx[1][2];
+      vg[6] = jx[0][0] * cr[0] + jx[1][0] * cr[1];
+      vg[7] = jx[0][1] * cr[0] + jx[1][1] * cr[1];
+      vg[8] = jx[0][2] * cr[0] + jx[1][2] * cr[1];
     }
     if (write_jacobian) r_out[i] = make_double2(cr[0], cr[1]);
-    if (ptv) {
-      const double* a = jx[0];
-      const double* b = jx[1];
-      vg[0] = a[0] * a[0] + b[0] * b[0];
-      vg[1] = a[0] * a[1] + b[0] * b[1];
-      vg[2] = a[0] * a[2] + b[0] * b[2];
-      vg[3] = a[1] * a[1] + b[1] * b[1];
-      vg[4] = a[1] * a[2] + b[1] * b[2];
-      vg[5] = a[2] * a[2] + b[2] * b[2];
-      vg[6] = a[0] * cr[0] + b[0] * cr[1];
-      vg[7] = a[1] * cr[0] + b[1] * cr[1];
-      vg[8] = a[2] * cr[0] + b[2] * cr[1];
-    }
   }
-  __syncthreads();
   if (write_jacobian) {
-    const int64_t b0 = (int64_t)blockIdx.x * kBlock;
-    const int cnt = p.nb - b0 < kBlock ? (int)(p.nb - b0) : kBlock;
-    const int total = cnt * W2;
-    double* out = J_out + b0 * W2;
-    for (int idx = threadIdx.x; idx < total; idx += kBlock) {
-      const int rr = idx / W2, k = idx - rr * W2;
-      out[idx] = sJ[rr * LS + k];
+    const int live = wb0 >= p.nb ? 0 : (p.nb - wb0 < 64 ? (int)(p.nb - wb0) : 64);
+    if constexpr (V == 0) {
+      double* row = sJ + threadIdx.x * LS;
+      if (i < p.nb) {
+        emit_row<M, CM>(0, row, B, Mq, pose_var, flags, jx, Jp, sc, cv);
+        emit_row<M, CM>(1, row + W, B, Mq, pose_var, flags, jx, Jp, sc, cv);
+      }
+      __syncthreads();
+      const int64_t b0 = (int64_t)blockIdx.x * kBlock;
+      const int cnt = p.nb - b0 < kBlock ? (int)(p.nb - b0) : kBlock;
+      const int total = cnt * W2;
+      double* out = J_out + b0 * W2;
+      for (int idx = threadIdx.x; idx < total; idx += kBlock) {
+        const int rr = idx / W2, k = idx - rr * W2;
+        out[idx] = sJ[rr * LS + k];
+      }
+    } else if constexpr (V == 1) {
+      double* wbase = sJ + (threadIdx.x - lane) * LS;
+      if (i < p.nb) {
+        emit_row<M, CM>(0, wbase + lane * LS, B, Mq, pose_var, flags, jx, Jp, sc, cv);
+        emit_row<M, CM>(1, wbase + lane * LS + W, B, Mq, pose_var, flags, jx, Jp, sc, cv);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      wave_readout<W2, LS, W2>(wbase, J_out + wb0 * W2, live);
+    } else {
+      double* wbase = sJ + (threadIdx.x - lane) * LS;
+#pragma unroll
+      for (int rw = 0; rw < 2; ++rw) {
+        if (i < p.nb) emit_row<M, CM>(rw, wbase + lane * LS, B, Mq, pose_var, flags, jx, Jp, sc, cv);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        wave_readout<W, LS, W2>(wbase, J_out + wb0 * W2 + rw * W, live);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      }
     }
   }
   wave_segmented_store<9>(key, ptv, vg, Vg);
@@ -1166,8 +1205,15 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
     constexpr int M = decltype(m)::value;
     auto go = [&](auto rf) {
       constexpr int RF = decltype(rf)::value;
-      hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF>), dim3(g), dim3(kBlock), 0, s, p, r, J, Vg, cost_partial,
-                         write_jacobian);
+      if (p.jvariant == 1)
+        hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 1>), dim3(g), dim3(kBlock), 0, s, p, r, J, Vg,
+                           cost_partial, write_jacobian);
+      else if (p.jvariant == 2)
+        hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 2>), dim3(g), dim3(kBlock), 0, s, p, r, J, Vg,
+                           cost_partial, write_jacobian);
+      else
+        hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0>), dim3(g), dim3(kBlock), 0, s, p, r, J, Vg,
+                           cost_partial, write_jacobian);
     };
     switch (p.refine_mask & 7) {
       case 0: go(std::integral_constant<int, 0>{}); break;

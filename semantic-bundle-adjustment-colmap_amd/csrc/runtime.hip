@@ -248,6 +248,7 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
   d.nf = 6 * (int64_t)I + (int64_t)s.ct * C;
   d.loss_type = o->loss_function_type;
   d.loss_scale = o->loss_function_scale;
+  d.jvariant = 0;
   d.refine_mask = (o->refine_focal_length ? 1 : 0) | (o->refine_principal_point ? 2 : 0) |
                   (o->refine_extra_params ? 4 : 0);
   d.obs_xy = ctx->obs_xy.ptr;
@@ -342,7 +343,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   timer_end(ctx, stop);
   if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s);
   if (ctx->sem) {
-    mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, true);
+    mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
   }
   MI_HIP(hipGetLastError());
@@ -807,6 +808,7 @@ mi_ba_status mi_ba_download_semantic(mi_ba_context* ctx, int32_t* sample_pixel, 
   if (!ctx || !ctx->sem) return MI_BA_ERR_INVALID_ARGUMENT;
   SemanticState* S = ctx->sem;
   MI_HIP(hipStreamSynchronize(ctx->stream));
+  if (!S->samples_valid) return MI_BA_ERR_STATE;  // mi_ba_evaluate_semantic first
   const int64_t n = S->ns;
   if (sample_pixel) std::memcpy(sample_pixel, S->sample_pixel_host.data(), 3 * n * sizeof(int32_t));
   if (n == 0) return MI_BA_OK;
@@ -843,9 +845,11 @@ mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost) {
 
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value) {
   if (!ctx || !key) return MI_BA_ERR_INVALID_ARGUMENT;
-  (void)value;
-  (void)ctx;
-  return MI_BA_ERR_INVALID_ARGUMENT;  // no tunable variants in this build
+  if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 2) {
+    ctx->dev.jvariant = value;
+    return MI_BA_OK;
+  }
+  return MI_BA_ERR_INVALID_ARGUMENT;
 }
 
 mi_ba_status mi_ba_set_timing(mi_ba_context* ctx, int32_t enabled) {

@@ -42,11 +42,13 @@ struct SemanticState {
   std::vector<int32_t> sample_pixel_host;  // [ns][3]
   DevArray<SemSample> samples;
   DevArray<SemPair> pairs;
-  DevArray<float> depth, label;            // [I][H][W] rasters of images used as j
+  DevArray<float2> dl;                     // [slot][H][W] (depth, label) of images used as j
   DevArray<uint32_t> raster_slot;          // image -> raster slot
   DevArray<double> r;                      // [ns]
   DevArray<int32_t> status;                // [ns]
   DevArray<double> J;                      // [ns][12]
+  DevArray<double> pconst;                 // [npairs] PairConst (semantic.hip), per linearization
+  bool samples_valid = false;              // r / status / J hold the last evaluation
   DevArray<double> pair_blk;               // [npairs][12*12 + 12]: M = J'J (full) and g = J'r
   DevArray<double> partial;
   int64_t npartial = 0;

@@ -9,8 +9,9 @@
 // numeric-diff stencil over the ambient pose parameters (1 + 2*7 per
 // variable pose: 29 evaluations for a variable-variable block, 15 with one
 // constant pose), then applies QuaternionManifold / SubsetManifold.
-// Samples are grouped by image pair, so J'J, J'r reduce per pair in
-// pair-aligned tiles (one atomic flush per tile).
+// Samples are grouped by image pair; one workgroup per pair-aligned tile, so
+// the pair's poses are wave-uniform and J'J, J'r reduce in LDS (one atomic
+// flush per tile).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,8 +36,7 @@ struct SemArgs {
   const uint32_t* img_cam;
   const uint32_t* img_flags;
   const uint32_t* raster_slot;
-  const float* depth;
-  const float* label;
+  const float2* dl;   // interleaved (depth, label) rasters [slot][H][W]
   int H, W;
   double threshold;
   double rel_step;
@@ -52,11 +52,12 @@ __device__ inline void quat_rotate_point(const double q[4], const double pt[3], 
   unit_quat_rotate(unit, pt, r);
 }
 
-// compute_semantic_error (semantic_cost_functions.h:87-208).
+// compute_semantic_error (semantic_cost_functions.h:87-208), the reference's
+// operation sequence.
 template <int M>
 __device__ inline double semantic_error(const SemArgs& a, const double pc1[3], float label1, const double* q1,
                                         const double* t1, const double* q2, const double* t2, const double* K2,
-                                        const float* depth2, const float* label2, int* status) {
+                                        const float2* dl2, int* status) {
   // PoseInverse (rotation_extension.h:43-57)
   const double sc = 1.0 / sqrt(q1[0] * q1[0] + q1[1] * q1[1] + q1[2] * q1[2] + q1[3] * q1[3]);
   const double qi[4] = {sc * q1[0], -(sc * q1[1]), -(sc * q1[2]), -(sc * q1[3])};
@@ -97,22 +98,20 @@ __device__ inline double semantic_error(const SemArgs& a, const double pc1[3], f
     *status = MI_BA_OUT_OF_BOUNDS;
     return 0.0;
   }
-  const size_t off = (size_t)py * a.W + px;
-  const double depth_2 = (double)depth2[off];
+  const float2 s = dl2[(size_t)py * a.W + px];
+  const double depth_2 = (double)s.x;
   if (fabs(depth_2 - measured_depth_2) > a.threshold) {
     *status = MI_BA_INVALID_DEPTH;
     return 0.0;
   }
   *status = MI_BA_VALID;
-  return (label1 == label2[off]) ? 0.0 : 1.0;
+  return (label1 == s.y) ? 0.0 : 1.0;
 }
 
 // ---------------------------------------------------------------------------
-// The same evaluation split into its pose-1 / pose-2 stages so the CENTRAL
-// stencil recomputes only what the perturbed parameter feeds.  Each stage is
-// exactly the operation sequence of semantic_error above, so every stencil
-// value is bitwise the one the unsplit evaluation (and the CPU reference)
-// produces.
+// The centre evaluation split into its pose-1 / pose-2 stages (each stage is
+// exactly the operation sequence of semantic_error above, so the centre value
+// is bitwise the reference's).
 // ---------------------------------------------------------------------------
 struct Pose1Stage {   // depends on q1 (and P_c1)
   double R[9];        // QuaternionToRotation(q_inv)
@@ -153,17 +152,17 @@ __device__ inline void unit_quat(const double* q, double u[4]) {
   u[3] = scale * q[3];
 }
 
-struct PixelCache {   // the centre evaluation's raster reads
+struct PixelCache {   // the centre evaluation's raster read
   int px, py;
   float depth, label;
   bool valid;
 };
 
-// Projection into image 2 and the raster tests (semantic_cost_functions.h:141-205).
+// Projection into image 2 and the raster tests (semantic_cost_functions.h:141-205),
+// reference operation order; records the centre pixel.
 template <int M>
-__device__ inline double project_test(const SemArgs& a, const double p2[3], float label1, const double* K2,
-                                      const float* depth2, const float* label2, PixelCache& pc, bool centre,
-                                      int* status) {
+__device__ inline double project_centre(const SemArgs& a, const double p2[3], float label1, const double* K2,
+                                        const float2* dl2, PixelCache& pc, int* status) {
   const double u2 = p2[0] / p2[2];
   const double v2 = p2[1] / p2[2];
   const double measured_depth_2 = p2[2];
@@ -175,179 +174,357 @@ __device__ inline double project_test(const SemArgs& a, const double p2[3], floa
     *status = MI_BA_OUT_OF_BOUNDS;
     return 0.0;
   }
-  float d2, l2;
-  if (!centre && pc.valid && px == pc.px && py == pc.py) {
-    d2 = pc.depth;
-    l2 = pc.label;
-  } else {
-    const size_t off = (size_t)py * a.W + px;
-    d2 = depth2[off];
-    l2 = label2[off];
-    if (centre) {
-      pc.px = px; pc.py = py; pc.depth = d2; pc.label = l2; pc.valid = true;
-    }
-  }
-  if (fabs((double)d2 - measured_depth_2) > a.threshold) {
+  const float2 s = dl2[(size_t)py * a.W + px];
+  pc.px = px; pc.py = py; pc.depth = s.x; pc.label = s.y; pc.valid = true;
+  if (fabs((double)s.x - measured_depth_2) > a.threshold) {
     *status = MI_BA_INVALID_DEPTH;
     return 0.0;
   }
   *status = MI_BA_VALID;
-  return (label1 == l2) ? 0.0 : 1.0;
+  return (label1 == s.y) ? 0.0 : 1.0;
+}
+
+// ---------------------------------------------------------------------------
+// Stencil evaluations.  The residual is a step function: it depends on the
+// perturbed evaluation only through round(x2), round(y2) and the sign of
+// |depth - z| - threshold.  Each perturbed camera-2 point is therefore formed
+// by a cheaper, equally accurate route (unnormalised rotation matrices, one
+// reciprocal, the stage quantities of the centre), and its outcome is taken
+// when every one of those three decisions clears a margin far above the
+// rounding difference between this route and the reference's (both are
+// within ~1e-12 px / ~1e-15 |p| of the exact value; the margins are 1e-6 px
+// and 1e-9 in depth, scaled by the magnitudes involved).  Otherwise the
+// evaluation is redone with the reference operation sequence
+// (semantic_error).  The stencil values, hence J, are the reference's
+// bit for bit.
+// ---------------------------------------------------------------------------
+// Unnormalised rotation matrix: Rot(q) v = Q(q) v / |q|^2 (row-major).
+__device__ inline void quat_matrix_un(const double q[4], double Q[9]) {
+  const double a = q[0], b = q[1], c = q[2], d = q[3];
+  const double aa = a * a, bb = b * b, cc = c * c, dd = d * d;
+  const double ab = a * b, ac = a * c, ad = a * d, bc = b * c, bd = b * d, cd = c * d;
+  Q[0] = aa + bb - cc - dd; Q[1] = 2.0 * (bc - ad);  Q[2] = 2.0 * (ac + bd);
+  Q[3] = 2.0 * (bc + ad);  Q[4] = aa - bb + cc - dd; Q[5] = 2.0 * (cd - ab);
+  Q[6] = 2.0 * (bd - ac);  Q[7] = 2.0 * (ab + cd);  Q[8] = aa - bb - cc + dd;
+}
+
+__device__ inline double rcp_refined(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return r;
 }
 
 template <int M>
-__global__ __launch_bounds__(kBlock) void semantic_jacobian_kernel(SemArgs a, double* __restrict__ r_out,
-                                                                    int32_t* __restrict__ status_out,
-                                                                    double* __restrict__ J_out) {
-  const int64_t n = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (n >= a.ns) return;
-  const SemSample smp = a.samples[n];
-  const SemPair pr = a.pairs[smp.pair];
-  const double* qt1 = a.qt + 8 * (size_t)pr.i;
-  const double* qt2 = a.qt + 8 * (size_t)pr.j;
-  double q1[4], t1[3], q2[4], t2[3];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) { q1[m] = qt1[m]; q2[m] = qt2[m]; }
-#pragma unroll
-  for (int m = 0; m < 3; ++m) { t1[m] = qt1[4 + m]; t2[m] = qt2[4 + m]; }
+__device__ inline double distortion_gain(const double* K, double r2) {
   constexpr int np = Model<M>::kNumParams;
-  double K2[np];
-  const double* kc = a.cam + 8 * (size_t)a.img_cam[pr.j];
+  double s = 0.0;
+  if constexpr (M == kSimpleRadial || M == kRadial) {
 #pragma unroll
-  for (int m = 0; m < np; ++m) K2[m] = kc[m];
-  const size_t slot = a.raster_slot[pr.j];
-  const float* depth2 = a.depth + slot * a.H * a.W;
-  const float* label2 = a.label + slot * a.H * a.W;
-  PixelCache pc;
-  pc.valid = false;
-  pc.px = pc.py = 0;
-  pc.depth = pc.label = 0.f;
-  // centre
-  Pose1Stage s1;
-  pose1_stage(q1, smp.pc1, s1);
-  double pw[3];
-  pose1_world(s1, t1, pw);
-  double u2[4];
-  unit_quat(q2, u2);
-  double rot2[3];
-  unit_quat_rotate(u2, pw, rot2);
-  double p2[3] = {rot2[0] + t2[0], rot2[1] + t2[1], rot2[2] + t2[2]};
-  int st = 0, st2 = 0;
-  const double r = project_test<M>(a, p2, smp.label1, K2, depth2, label2, pc, true, &st);
-  double Jamb[14];
+    for (int k = 3; k < np; ++k) s += fabs(K[k]);
+  } else if constexpr (M == kOpenCV) {
 #pragma unroll
-  for (int m = 0; m < 14; ++m) Jamb[m] = 0.0;
-  if (pr.var1) {
-    // q1 stencil: pose-1 stage recomputed, normalised q2 reused
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const double orig = q1[m];
-      const double delta = fmax(kMinStep, fabs(orig) * a.rel_step);
-      double f[2];
-#pragma unroll
-      for (int sgn = 0; sgn < 2; ++sgn) {
-        double qq[4] = {q1[0], q1[1], q1[2], q1[3]};
-        qq[m] = sgn == 0 ? orig + delta : orig - delta;
-        Pose1Stage s;
-        pose1_stage(qq, smp.pc1, s);
-        double w[3], rr[3];
-        pose1_world(s, t1, w);
-        unit_quat_rotate(u2, w, rr);
-        const double pp[3] = {rr[0] + t2[0], rr[1] + t2[1], rr[2] + t2[2]};
-        f[sgn] = project_test<M>(a, pp, smp.label1, K2, depth2, label2, pc, false, &st2);
-      }
-      double one_over_delta = 1.0 / delta;
-      one_over_delta /= 2;
-      Jamb[m] = (f[0] - f[1]) * one_over_delta;
-    }
-    // t1 stencil: rotation stage of pose 1 reused
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const double orig = t1[m];
-      const double delta = fmax(kMinStep, fabs(orig) * a.rel_step);
-      double f[2];
-#pragma unroll
-      for (int sgn = 0; sgn < 2; ++sgn) {
-        double tt[3] = {t1[0], t1[1], t1[2]};
-        tt[m] = sgn == 0 ? orig + delta : orig - delta;
-        double w[3], rr[3];
-        pose1_world(s1, tt, w);
-        unit_quat_rotate(u2, w, rr);
-        const double pp[3] = {rr[0] + t2[0], rr[1] + t2[1], rr[2] + t2[2]};
-        f[sgn] = project_test<M>(a, pp, smp.label1, K2, depth2, label2, pc, false, &st2);
-      }
-      double one_over_delta = 1.0 / delta;
-      one_over_delta /= 2;
-      Jamb[4 + m] = (f[0] - f[1]) * one_over_delta;
-    }
+    for (int k = 4; k < np; ++k) s += fabs(K[k]);
   }
-  if (pr.var2) {
-    // q2 stencil: world point reused
+  const double g = 1.0 + r2;
+  return 1.0 + s * g * g * g;
+}
+
+// Outcome of one stencil evaluation from its camera-2 point p; false when a
+// decision is inside the margin (caller falls back to semantic_error).
+// mag bounds the magnitudes p was formed from (L1 norms).
+template <int M>
+__device__ inline bool resolve(const SemArgs& a, const double p[3], double mag, float label1, const double* K2,
+                               const float2* dl2, const PixelCache& pc, double& f) {
+  const double iz = rcp_refined(p[2]);
+  const double u = p[0] * iz, v = p[1] * iz;
+  double x, y;
+  world_to_image<M>(K2, u, v, &x, &y);
+  if (!(fabs(x) < 1e8 && fabs(y) < 1e8 && fabs(u) < 1e6 && fabs(v) < 1e6)) return false;
+  const double kscale = (fabs(K2[0]) + fabs(K2[1])) * distortion_gain<M>(K2, u * u + v * v) *
+                        (1.0 + fabs(u) + fabs(v)) * (1.0 + mag * fabs(iz));
+  const double ex = 1e-6 + 1e-11 * (kscale + fabs(x) + fabs(y));
+  const double fx = floor(x), fy = floor(y);
+  const double rx = x - fx, ry = y - fy;
+  if (!(fabs(rx - 0.5) > ex && fabs(ry - 0.5) > ex)) return false;
+  const int px = (int)fx + (rx > 0.5 ? 1 : 0);
+  const int py = (int)fy + (ry > 0.5 ? 1 : 0);
+  if (px < 0 || px >= a.W || py < 0 || py >= a.H) {
+    f = 0.0;
+    return true;
+  }
+  float2 s;
+  if (pc.valid && px == pc.px && py == pc.py) {
+    s = make_float2(pc.depth, pc.label);
+  } else {
+    s = dl2[(size_t)py * a.W + px];
+  }
+  const double dd = fabs((double)s.x - p[2]) - a.threshold;
+  if (!(fabs(dd) > 1e-9 * (1.0 + fabs((double)s.x) + mag))) return false;
+  f = (dd > 0.0) ? 0.0 : ((label1 == s.y) ? 0.0 : 1.0);
+  return true;
+}
+
+// Per-pair constants of one linearization (pose dependent, sample
+// independent), formed with the reference's operation sequence so that the
+// per-sample centre evaluation continues it bit for bit.  Every workgroup
+// works on one pair, so these are wave-uniform (scalar loads/registers).
+struct PairConst {
+  double q1[4], t1[3], q2[4], t2[3];  // raw parameters (stencil base)
+  double uqi[4];                      // normalised q_inv as QuaternionRotatePoint uses it
+  double ti[3];                       // t_inv = -(R t1)
+  double u2[4];                       // normalised q2
+  double R2[9];                       // rotation of u2 (stencil)
+  double C[9];                        // R2 R: d P_2 / d t1 = -C (stencil)
+  double K2[8];                       // camera of image j
+  uint32_t var1, var2, mask1, mask2;  // variable poses, constant-tvec masks
+  uint32_t slot, pad0, pad1, pad2;
+};
+
+__global__ void semantic_pair_prep_kernel(const SemPair* __restrict__ pairs, int npairs, const double* __restrict__ qt,
+                                          const double* __restrict__ cam, const uint32_t* __restrict__ img_cam,
+                                          const uint32_t* __restrict__ img_flags,
+                                          const uint32_t* __restrict__ raster_slot, PairConst* __restrict__ out) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= npairs) return;
+  const SemPair pr = pairs[k];
+  PairConst P;
+  const double* a1 = qt + 8 * (size_t)pr.i;
+  const double* a2 = qt + 8 * (size_t)pr.j;
+  for (int m = 0; m < 4; ++m) { P.q1[m] = a1[m]; P.q2[m] = a2[m]; }
+  for (int m = 0; m < 3; ++m) { P.t1[m] = a1[4 + m]; P.t2[m] = a2[4 + m]; }
+  // PoseInverse + QuaternionToRotation (pose1_stage), t_inv (pose1_world)
+  Pose1Stage s;
+  const double zero[3] = {0.0, 0.0, 0.0};
+  pose1_stage(P.q1, zero, s);
+  {
+    const double* q1 = P.q1;
+    const double sc = 1.0 / sqrt(q1[0] * q1[0] + q1[1] * q1[1] + q1[2] * q1[2] + q1[3] * q1[3]);
+    const double qi[4] = {sc * q1[0], -(sc * q1[1]), -(sc * q1[2]), -(sc * q1[3])};
+    // quat_rotate_point(qi, .) normalisation
+    const double scale = 1.0 / sqrt(qi[0] * qi[0] + qi[1] * qi[1] + qi[2] * qi[2] + qi[3] * qi[3]);
+    for (int m = 0; m < 4; ++m) P.uqi[m] = scale * qi[m];
+  }
+  P.ti[0] = -(s.R[0] * P.t1[0] + s.R[1] * P.t1[1] + s.R[2] * P.t1[2]);
+  P.ti[1] = -(s.R[3] * P.t1[0] + s.R[4] * P.t1[1] + s.R[5] * P.t1[2]);
+  P.ti[2] = -(s.R[6] * P.t1[0] + s.R[7] * P.t1[1] + s.R[8] * P.t1[2]);
+  unit_quat(P.q2, P.u2);
+  unit_quat_matrix(P.u2, P.R2);
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      P.C[3 * r + c] = P.R2[3 * r] * s.R[c] + P.R2[3 * r + 1] * s.R[3 + c] + P.R2[3 * r + 2] * s.R[6 + c];
+  const double* K = cam + 8 * (size_t)img_cam[pr.j];
+  for (int m = 0; m < 8; ++m) P.K2[m] = K[m];
+  P.var1 = pr.var1;
+  P.var2 = pr.var2;
+  P.mask1 = (img_flags[pr.i] >> 1) & 7u;
+  P.mask2 = (img_flags[pr.j] >> 1) & 7u;
+  P.slot = raster_slot[pr.j];
+  P.pad0 = P.pad1 = P.pad2 = 0;
+  out[k] = P;
+}
+
+// Per-pair record: loss-corrected J'J (packed 12x12 upper, 78) and J'r (12).
+constexpr int kPairVals = 78 + 12;
+constexpr int kPairStride = 96;  // padded record per pair
+constexpr int kSemRow = 13;      // LDS row: corrected J (12), corrected r
+
+// One workgroup per pair-aligned tile of <= 256 samples, one lane per sample:
+// centre residual (reference sequence), the CENTRAL stencil over the
+// variable poses' ambient parameters (rolled loop, outcome resolution above),
+// QuaternionManifold / SubsetManifold, the ScaledLoss Corrector, and the
+// tile's J'J / J'r / cost reduced in LDS with one atomic flush per value.
+// Per-sample r / status / J are stored only when requested (parity and
+// download); the solver consumes the pair records.
+template <int M>
+__global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, const SemTile* __restrict__ tiles,
+                                                                     const PairConst* __restrict__ pcs,
+                                                                     double* __restrict__ pair_blk,
+                                                                     double* __restrict__ cost_partial,
+                                                                     double* __restrict__ r_out,
+                                                                     int32_t* __restrict__ status_out,
+                                                                     double* __restrict__ J_out, int write_samples) {
+  __shared__ double sJ[kBlock * kSemRow];
+  __shared__ double spart[2 * kPairVals];
+  __shared__ double sred[4];
+  const SemTile t = tiles[blockIdx.x];
+  const PairConst* __restrict__ P = pcs + t.pair;
+  const int tid = threadIdx.x;
+  const bool active = tid < (int)t.count;
+  const int64_t n = (int64_t)t.start + tid;
+  double cost = 0.0;
+  double* row = sJ + tid * kSemRow;
+  if (active) {
+    const SemSample smp = a.samples[n];
+    const float2* dl2 = a.dl + (size_t)P->slot * a.H * a.W;
+    const double* K2 = P->K2;
+    // centre: QuaternionRotatePoint(q_inv, P_c1) + t_inv, then pose 2
+    double rot[3];
+    unit_quat_rotate(P->uqi, smp.pc1, rot);
+    const double pw[3] = {rot[0] + P->ti[0], rot[1] + P->ti[1], rot[2] + P->ti[2]};
+    double rot2[3];
+    unit_quat_rotate(P->u2, pw, rot2);
+    const double p2[3] = {rot2[0] + P->t2[0], rot2[1] + P->t2[1], rot2[2] + P->t2[2]};
+    PixelCache pc;
+    pc.valid = false;
+    pc.px = pc.py = 0;
+    pc.depth = pc.label = 0.f;
+    int st = 0;
+    const double r = project_centre<M>(a, p2, smp.label1, K2, dl2, pc, &st);
+    const double mag = fabs(smp.pc1[0]) + fabs(smp.pc1[1]) + fabs(smp.pc1[2]) + fabs(P->t1[0]) + fabs(P->t1[1]) +
+                       fabs(P->t1[2]) + fabs(pw[0]) + fabs(pw[1]) + fabs(pw[2]) + fabs(P->t2[0]) +
+                       fabs(P->t2[1]) + fabs(P->t2[2]);
+    // Stencil: parameter m = 0..13 over (q1, t1, q2, t2), + then - (Ceres
+    // CENTRAL order).  Tangent columns accumulate in m order from 0.0
+    // exactly as J_tangent = J_ambient * PlusJacobian does.
+    double Jt[12];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const double orig = q2[m];
+    for (int k = 0; k < 12; ++k) Jt[k] = 0.0;
+    double fplus = 0.0;
+#pragma unroll 1
+    for (int e = 0; e < 28; ++e) {
+      const int m = e >> 1;
+      const bool minus = e & 1;
+      const int grp = m < 4 ? 0 : (m < 7 ? 1 : (m < 11 ? 2 : 3));
+      if (grp < 2 ? !P->var1 : !P->var2) continue;
+      const int k = m - (grp == 0 ? 0 : (grp == 1 ? 4 : (grp == 2 ? 7 : 11)));
+      double orig = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (grp == 0 && c == k) orig = P->q1[c];
+        if (grp == 2 && c == k) orig = P->q2[c];
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        if (grp == 1 && c == k) orig = P->t1[c];
+        if (grp == 3 && c == k) orig = P->t2[c];
+      }
       const double delta = fmax(kMinStep, fabs(orig) * a.rel_step);
-      double f[2];
+      const double pert = minus ? orig - delta : orig + delta;
+      double pp[3];
+      if (grp == 0) {  // q1: P_w' = Q(q1')^T (P_c1 - t1) / |q1'|^2
+        double qq[4];
 #pragma unroll
-      for (int sgn = 0; sgn < 2; ++sgn) {
-        double qq[4] = {q2[0], q2[1], q2[2], q2[3]};
-        qq[m] = sgn == 0 ? orig + delta : orig - delta;
-        double uu[4], rr[3];
-        unit_quat(qq, uu);
-        unit_quat_rotate(uu, pw, rr);
-        const double pp[3] = {rr[0] + t2[0], rr[1] + t2[1], rr[2] + t2[2]};
-        f[sgn] = project_test<M>(a, pp, smp.label1, K2, depth2, label2, pc, false, &st2);
+        for (int c = 0; c < 4; ++c) qq[c] = (c == k) ? pert : P->q1[c];
+        double Q[9];
+        quat_matrix_un(qq, Q);
+        const double in = rcp_refined(qq[0] * qq[0] + qq[1] * qq[1] + qq[2] * qq[2] + qq[3] * qq[3]);
+        const double w[3] = {smp.pc1[0] - P->t1[0], smp.pc1[1] - P->t1[1], smp.pc1[2] - P->t1[2]};
+        double wp[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) wp[c] = (Q[c] * w[0] + Q[3 + c] * w[1] + Q[6 + c] * w[2]) * in;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          pp[c] = P->R2[3 * c] * wp[0] + P->R2[3 * c + 1] * wp[1] + P->R2[3 * c + 2] * wp[2] + P->t2[c];
+      } else if (grp == 1) {  // t1: P_2' = P_2 - C (t1' - t1)
+        const double dt = pert - orig;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          pp[c] = p2[c] - dt * (k == 0 ? P->C[3 * c] : (k == 1 ? P->C[3 * c + 1] : P->C[3 * c + 2]));
+      } else if (grp == 2) {  // q2: P_2' = Q(q2') P_w / |q2'|^2 + t2
+        double qq[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) qq[c] = (c == k) ? pert : P->q2[c];
+        double Q[9];
+        quat_matrix_un(qq, Q);
+        const double in = rcp_refined(qq[0] * qq[0] + qq[1] * qq[1] + qq[2] * qq[2] + qq[3] * qq[3]);
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          pp[c] = (Q[3 * c] * pw[0] + Q[3 * c + 1] * pw[1] + Q[3 * c + 2] * pw[2]) * in + P->t2[c];
+      } else {  // t2: P_2' = P_2 + (t2' - t2)
+        const double dt = pert - orig;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) pp[c] = p2[c] + (c == k ? dt : 0.0);
+      }
+      double f;
+      if (!resolve<M>(a, pp, mag, smp.label1, K2, dl2, pc, f)) {
+        // reference operation sequence for this stencil point
+        double qq1[4], tt1[3], qq2[4], tt2[3];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          qq1[c] = (grp == 0 && c == k) ? pert : P->q1[c];
+          qq2[c] = (grp == 2 && c == k) ? pert : P->q2[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          tt1[c] = (grp == 1 && c == k) ? pert : P->t1[c];
+          tt2[c] = (grp == 3 && c == k) ? pert : P->t2[c];
+        }
+        int st2;
+        f = semantic_error<M>(a, smp.pc1, smp.label1, qq1, tt1, qq2, tt2, K2, dl2, &st2);
+      }
+      if (!minus) {
+        fplus = f;
+        continue;
       }
       double one_over_delta = 1.0 / delta;
       one_over_delta /= 2;
-      Jamb[7 + m] = (f[0] - f[1]) * one_over_delta;
-    }
-    // t2 stencil: rotated point reused
+      const double jm = (fplus - f) * one_over_delta;
+      if (grp == 0 || grp == 2) {
+        const double x0 = grp == 0 ? P->q1[0] : P->q2[0], x1 = grp == 0 ? P->q1[1] : P->q2[1];
+        const double x2 = grp == 0 ? P->q1[2] : P->q2[2], x3 = grp == 0 ? P->q1[3] : P->q2[3];
 #pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const double orig = t2[m];
-      const double delta = fmax(kMinStep, fabs(orig) * a.rel_step);
-      double f[2];
+        for (int c = 0; c < 3; ++c) {
+          // QuaternionManifold PlusJacobian row k, column c (quat_plus_jacobian)
+          double pjc;
+          if (k == 0) pjc = c == 0 ? -x1 : (c == 1 ? -x2 : -x3);
+          else if (k == 1) pjc = c == 0 ? x0 : (c == 1 ? x3 : -x2);
+          else if (k == 2) pjc = c == 0 ? -x3 : (c == 1 ? x0 : x1);
+          else pjc = c == 0 ? x2 : (c == 1 ? -x1 : x0);
+          const double v = (grp == 0 ? Jt[c] : Jt[6 + c]) + jm * pjc;
+          if (grp == 0) Jt[c] = v; else Jt[6 + c] = v;
+        }
+      } else {
+        const uint32_t mask = grp == 1 ? P->mask1 : P->mask2;
+        const double v = ((mask >> k) & 1u) ? 0.0 : jm;
 #pragma unroll
-      for (int sgn = 0; sgn < 2; ++sgn) {
-        double pp[3] = {rot2[0] + t2[0], rot2[1] + t2[1], rot2[2] + t2[2]};
-        pp[m] = rot2[m] + (sgn == 0 ? orig + delta : orig - delta);
-        f[sgn] = project_test<M>(a, pp, smp.label1, K2, depth2, label2, pc, false, &st2);
+        for (int c = 0; c < 3; ++c) {
+          if (c == k) {
+            if (grp == 1) Jt[3 + c] = v; else Jt[9 + c] = v;
+          }
+        }
       }
-      double one_over_delta = 1.0 / delta;
-      one_over_delta /= 2;
-      Jamb[11 + m] = (f[0] - f[1]) * one_over_delta;
     }
+    if (write_samples) {
+      r_out[n] = r;
+      status_out[n] = st;
+      double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
+#pragma unroll
+      for (int m = 0; m < 6; ++m) jo[m] = make_double2(Jt[2 * m], Jt[2 * m + 1]);
+    }
+    // ScaledLoss(w) + loss, Corrector rho'' <= 0 branch: sqrt(w * rho')
+    double rho[3];
+    loss_eval(a.loss_type, a.loss_scale, r * r, rho);
+    cost = 0.5 * (a.weight * rho[0]);
+    const double sc = sqrt(a.weight * rho[1]);
+#pragma unroll
+    for (int m = 0; m < 12; ++m) row[m] = Jt[m] * sc;
+    row[12] = r * sc;
   }
-  double Jt[12];
-  const double xq[2][4] = {{q1[0], q1[1], q1[2], q1[3]}, {q2[0], q2[1], q2[2], q2[3]}};
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const uint32_t img = blk == 0 ? pr.i : pr.j;
-    const uint32_t mask = (a.img_flags[img] >> 1) & 7u;
-    const bool var = blk == 0 ? pr.var1 != 0 : pr.var2 != 0;
-    if (!var) {
-#pragma unroll
-      for (int m = 0; m < 6; ++m) Jt[blk * 6 + m] = 0.0;
-      continue;
+  __syncthreads();
+  // tile J'J (78) and J'r (12): 2 x 90 threads over interleaved samples
+  if (tid < 2 * kPairVals) {
+    const int h = tid / kPairVals, e = tid - h * kPairVals;
+    int ca, cb;
+    if (e < 78) {
+      int a_ = 0, rem = e;
+      while (rem >= 12 - a_) { rem -= 12 - a_; ++a_; }
+      ca = a_;
+      cb = a_ + rem;
+    } else {
+      ca = e - 78;
+      cb = 12;
     }
-    double PJ[12];
-    quat_plus_jacobian(xq[blk], PJ);
-#pragma unroll
-    for (int col = 0; col < 3; ++col) {
-      double acc = 0.0;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) acc += Jamb[blk * 7 + m] * PJ[m * 3 + col];
-      Jt[blk * 6 + col] = acc;
-    }
-#pragma unroll
-    for (int col = 0; col < 3; ++col) Jt[blk * 6 + 3 + col] = ((mask >> col) & 1u) ? 0.0 : Jamb[blk * 7 + 4 + col];
+    double acc = 0.0;
+    for (int s = h; s < (int)t.count; s += 2) acc += sJ[s * kSemRow + ca] * sJ[s * kSemRow + cb];
+    spart[tid] = acc;
   }
-  r_out[n] = r;
-  status_out[n] = st;
-  double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
-#pragma unroll
-  for (int m = 0; m < 6; ++m) jo[m] = make_double2(Jt[2 * m], Jt[2 * m + 1]);
+  double v = cost;
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if ((tid & 63) == 0) sred[tid >> 6] = v;
+  __syncthreads();
+  if (tid < kPairVals) atomicAdd(pair_blk + (size_t)t.pair * kPairStride + tid, spart[tid] + spart[kPairVals + tid]);
+  if (tid == 0) cost_partial[blockIdx.x] = sred[0] + sred[1] + sred[2] + sred[3];
 }
 
 template <int M>
@@ -369,8 +546,7 @@ __global__ __launch_bounds__(kBlock) void semantic_cost_kernel(SemArgs a, double
     for (int m = 0; m < np; ++m) K2[m] = kc[m];
     const size_t slot = a.raster_slot[pr.j];
     int st;
-    const double r = semantic_error<M>(a, smp.pc1, smp.label1, q1, t1, q2, t2, K2, a.depth + slot * a.H * a.W,
-                                       a.label + slot * a.H * a.W, &st);
+    const double r = semantic_error<M>(a, smp.pc1, smp.label1, q1, t1, q2, t2, K2, a.dl + slot * a.H * a.W, &st);
     double rho[3];
     loss_eval(a.loss_type, a.loss_scale, r * r, rho);
     c = 0.5 * (a.weight * rho[0]);
@@ -381,63 +557,6 @@ __global__ __launch_bounds__(kBlock) void semantic_cost_kernel(SemArgs a, double
   if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) partial[blockIdx.x] = sred[0] + sred[1] + sred[2] + sred[3];
-}
-
-// Per-pair tile reduction of the loss-corrected J'J (packed 12x12 upper, 78)
-// and J'r (12), plus the cost.
-constexpr int kPairVals = 78 + 12;
-constexpr int kPairStride = 96;  // padded record per pair
-
-__global__ __launch_bounds__(kBlock) void semantic_reduce_kernel(const SemTile* __restrict__ tiles,
-                                                                  const double* __restrict__ r_in,
-                                                                  const double* __restrict__ J_in, int loss_type,
-                                                                  double loss_scale, double weight,
-                                                                  double* __restrict__ pair_blk,
-                                                                  double* __restrict__ cost_partial) {
-  __shared__ double sred[4 * (kPairVals + 1)];
-  const SemTile t = tiles[blockIdx.x];
-  double acc[kPairVals + 1];
-#pragma unroll
-  for (int k = 0; k < kPairVals + 1; ++k) acc[k] = 0.0;
-  for (uint32_t k = threadIdx.x; k < t.count; k += kBlock) {
-    const int64_t n = (int64_t)t.start + k;
-    double r = r_in[n];
-    double J[12];
-#pragma unroll
-    for (int m = 0; m < 12; ++m) J[m] = J_in[12 * n + m];
-    double rho[3];
-    loss_eval(loss_type, loss_scale, r * r, rho);
-    acc[kPairVals] += 0.5 * (weight * rho[0]);
-    // ScaledLoss(w) Corrector, rho'' <= 0 branch: sqrt(w * rho')
-    const double sc = sqrt(weight * rho[1]);
-    r *= sc;
-#pragma unroll
-    for (int m = 0; m < 12; ++m) J[m] *= sc;
-    int o = 0;
-#pragma unroll
-    for (int a = 0; a < 12; ++a)
-#pragma unroll
-      for (int b = a; b < 12; ++b, ++o) acc[o] += J[a] * J[b];
-#pragma unroll
-    for (int a = 0; a < 12; ++a) acc[78 + a] += J[a] * r;
-  }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < kPairVals + 1; ++k) {
-    double v = acc[k];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (lane == 0) sred[wid * (kPairVals + 1) + k] = v;
-  }
-  __syncthreads();
-  const int k = threadIdx.x;
-  if (k < kPairVals + 1) {
-    const double v = sred[k] + sred[(kPairVals + 1) + k] + sred[2 * (kPairVals + 1) + k] + sred[3 * (kPairVals + 1) + k];
-    if (k < kPairVals) {
-      atomicAdd(pair_blk + (size_t)t.pair * kPairStride + k, v);
-    } else {
-      cost_partial[blockIdx.x] = v;
-    }
-  }
 }
 
 __device__ inline int sym12(int a, int b) {  // a <= b
@@ -540,8 +659,7 @@ SemArgs make_args(mi_ba_context* ctx, const double* qt, const double* cam) {
   a.img_cam = ctx->dev.img_cam;
   a.img_flags = ctx->dev.img_flags;
   a.raster_slot = S->raster_slot.ptr;
-  a.depth = S->depth.ptr;
-  a.label = S->label.ptr;
+  a.dl = S->dl.ptr;
   a.H = S->H;
   a.W = S->W;
   a.threshold = S->depth_threshold;
@@ -616,11 +734,11 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
       }
     }
     pr.count = (uint32_t)(samples.size() - pr.start);
-    for (uint32_t t0 = 0; t0 < pr.count; t0 += kTileObs) {
+    for (uint32_t t0 = 0; t0 < pr.count; t0 += kBlock) {  // one workgroup per tile
       SemTile t;
       t.pair = pair_idx;
       t.start = pr.start + t0;
-      t.count = std::min<uint32_t>(kTileObs, pr.count - t0);
+      t.count = std::min<uint32_t>(kBlock, pr.count - t0);
       t.pad = 0;
       tiles.push_back(t);
     }
@@ -662,10 +780,10 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
   for (int i = 0; i < I; ++i) slot_u[i] = slot[i] < 0 ? 0u : (uint32_t)slot[i];
   S->ntiles = (int)tiles.size();
   if (S->samples.alloc(S->ns) || S->pairs.alloc(S->npairs) || S->raster_slot.alloc(I) ||
-      S->depth.alloc(plane * std::max<size_t>(1, slot_images.size())) ||
-      S->label.alloc(plane * std::max<size_t>(1, slot_images.size())) || S->r.alloc(S->ns) ||
+      S->dl.alloc(plane * std::max<size_t>(1, slot_images.size())) || S->r.alloc(S->ns) ||
       S->status.alloc(S->ns) || S->J.alloc(12 * S->ns) ||
-      S->pair_blk.alloc((size_t)kPairStride * std::max(1, S->npairs)) || S->tiles.alloc(tiles.size()))
+      S->pair_blk.alloc((size_t)kPairStride * std::max(1, S->npairs)) || S->tiles.alloc(tiles.size()) ||
+      S->pconst.alloc(sizeof(PairConst) / sizeof(double) * std::max(1, S->npairs)))
     return MI_BA_ERR_OUT_OF_MEMORY;
   S->npartial = std::max<int64_t>({(int64_t)tiles.size(), (S->ns + kBlock - 1) / kBlock, (int64_t)1});
   if (S->partial.alloc(S->npartial)) return MI_BA_ERR_OUT_OF_MEMORY;
@@ -676,10 +794,14 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
       (!tiles.empty() &&
        hipMemcpy(S->tiles.ptr, tiles.data(), tiles.size() * sizeof(SemTile), hipMemcpyHostToDevice)))
     return MI_BA_ERR_HIP;
+  // rasters interleaved (depth, label): one 8-B gather per pixel test
+  std::vector<float2> buf(plane);
   for (size_t s = 0; s < slot_images.size(); ++s) {
     const int j = slot_images[s];
-    if (hipMemcpy(S->depth.ptr + s * plane, sem->depth + (size_t)j * plane, plane * 4, hipMemcpyHostToDevice) ||
-        hipMemcpy(S->label.ptr + s * plane, sem->label + (size_t)j * plane, plane * 4, hipMemcpyHostToDevice))
+    const float* d = sem->depth + (size_t)j * plane;
+    const float* l = sem->label + (size_t)j * plane;
+    for (size_t k = 0; k < plane; ++k) buf[k] = make_float2(d[k], l[k]);
+    if (hipMemcpy(S->dl.ptr + s * plane, buf.data(), plane * sizeof(float2), hipMemcpyHostToDevice))
       return MI_BA_ERR_HIP;
   }
   return MI_BA_OK;
@@ -692,25 +814,24 @@ void semantic_destroy(mi_ba_context* ctx) {
 }
 
 mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples) {
-  (void)write_samples;
   SemanticState* S = ctx->sem;
   hipStream_t s = ctx->stream;
   if (S->npairs && hipMemsetAsync(S->pair_blk.ptr, 0, S->pair_blk.bytes(), s) != hipSuccess) return MI_BA_ERR_HIP;
+  S->samples_valid = write_samples;
   if (S->ns == 0) return MI_BA_OK;
   SemArgs a = make_args(ctx, ctx->dev.qt, ctx->dev.cam);
+  PairConst* pcs = reinterpret_cast<PairConst*>(S->pconst.ptr);
   hipEvent_t stop;
   timer_begin(ctx, "semantic_jacobian", &stop);
+  hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 63) / 64), dim3(64), 0, s, S->pairs.ptr, S->npairs,
+                     a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, pcs);
   dispatch_model(ctx->dev.model, [&](auto m) {
     constexpr int M = decltype(m)::value;
-    hipLaunchKernelGGL(semantic_jacobian_kernel<M>, dim3((unsigned)((S->ns + kBlock - 1) / kBlock)), dim3(kBlock),
-                       0, s, a, S->r.ptr, S->status.ptr, S->J.ptr);
+    hipLaunchKernelGGL(semantic_linearize_kernel<M>, dim3(S->ntiles), dim3(kBlock), 0, s, a, S->tiles.ptr, pcs,
+                       S->pair_blk.ptr, S->partial.ptr, S->r.ptr, S->status.ptr, S->J.ptr, write_samples ? 1 : 0);
   });
   timer_end(ctx, stop);
-  if (S->ntiles) {
-    hipLaunchKernelGGL(semantic_reduce_kernel, dim3(S->ntiles), dim3(kBlock), 0, s, S->tiles.ptr,
-                       S->r.ptr, S->J.ptr, a.loss_type, a.loss_scale, a.weight, S->pair_blk.ptr, S->partial.ptr);
-    launch_sum(S->partial.ptr, S->ntiles, d_cost, s);
-  }
+  launch_sum(S->partial.ptr, S->ntiles, d_cost, s);
   if (hipGetLastError() != hipSuccess) return MI_BA_ERR_HIP;
   return MI_BA_OK;
 }

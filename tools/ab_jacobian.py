@@ -19,6 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="C4")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--variants", default="0")
 args = ap.parse_args()
 cfg = dict(bench.CONFIGS[args.config])
 c = mi_ba.synth_config(cfg["model"], cfg["images"], cfg["points"], track_length=cfg["track"], rotation_range=0.05,
@@ -27,22 +28,33 @@ sc = mi_ba.generate_scene(c).gauge()
 ctx = mi_ba.Context(mi_ba.default_options(), sc)
 nb, W, _ = ctx.dims()
 bpb = bench.bytes_per_block(cfg["model"], cfg["track"])
-ctx.evaluate_jacobian()
-ctx.synchronize()
-_, r, J = ctx.download_jacobian()
-checksum = (float(np.abs(r).sum()), float(np.abs(J).sum()))
-del r, J
-res = []
+variants = [int(v) for v in args.variants.split(",")]
+ref = None
+ok = {}
+for v in variants:
+    ctx.set_tuning("jacobian_variant", v)
+    ctx.evaluate_jacobian()
+    ctx.synchronize()
+    _, r, J = ctx.download_jacobian()
+    if ref is None:
+        ref = (r.copy(), J.copy())
+    ok[v] = bool(np.array_equal(r, ref[0]) and np.array_equal(J, ref[1]))
+    del r, J
+res = {v: [] for v in variants}
 for rnd in range(args.rounds):
-    ctx.set_timing(True)
-    ctx.reset_kernel_times()
-    for _ in range(args.reps):
+    for v in variants:
+        ctx.set_tuning("jacobian_variant", v)
         ctx.evaluate_jacobian()
-    ms, n = ctx.kernel_time("reproj_jacobian")
-    ctx.set_timing(False)
-    res.append(ms / n)
-med = float(np.median(res))
-print(json.dumps({"config": args.config, "blocks": nb, "bytes_per_block": bpb, "median_ms": med,
-                  "min_ms": float(np.min(res)), "GBps": bpb * nb / (med * 1e-3) / 1e9,
-                  "frac_of_8TBps": bpb * nb / (med * 1e-3) / 8e12, "checksum": checksum}))
+        ctx.set_timing(True)
+        ctx.reset_kernel_times()
+        for _ in range(args.reps):
+            ctx.evaluate_jacobian()
+        ms, n = ctx.kernel_time("reproj_jacobian")
+        ctx.set_timing(False)
+        res[v].append(ms / n)
+for v in variants:
+    med = float(np.median(res[v]))
+    print(json.dumps({"config": args.config, "variant": v, "identical_to_first": ok[v], "blocks": nb,
+                      "bytes_per_block": bpb, "median_ms": med, "min_ms": float(np.min(res[v])),
+                      "GBps": bpb * nb / (med * 1e-3) / 1e9, "frac_of_8TBps": bpb * nb / (med * 1e-3) / 8e12}))
 ctx.close()
