@@ -48,6 +48,20 @@ CAM_TANGENT = {mi_ba.SIMPLE_PINHOLE: 1, mi_ba.PINHOLE: 2, mi_ba.SIMPLE_RADIAL: 2
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+def pmc_traffic(config, kernel_prefix):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary
+    (profiles/<round>_<config>_traffic.json, written by tools/summarize_profile.py
+    from separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config.lower()}_traffic.json")))
+    for f in reversed(files):
+        d = json.load(open(f))
+        for name, v in d.get("kernels", {}).items():
+            if name.startswith(kernel_prefix):
+                return v["hbm_bytes"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def bytes_per_block(model, track):
     return 24 + 24.0 / track + 16 + 16 * (9 + CAM_TANGENT[model])
 
@@ -204,6 +218,7 @@ def main():
         avg_j = j_ms / max(1, j_n)
         bpb = bytes_per_block(cfg["model"], cfg["track"])
         achieved = bpb * nb / (avg_j * 1e-3) / 1e9 if avg_j > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(args.config, "reproj_jacobian_kernel") if world == 1 else (None, None)
         out = {
             "metric": METRIC,
             "value": value,
@@ -223,7 +238,9 @@ def main():
                        "camera_model": [k for k, v in mi_ba.MODEL_NAMES.items() if v == cfg["model"]][0],
                        "parallelism": f"point-sharded x{world}"},
             "roofline": {"kernel": "reproj_jacobian", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": bpb * nb,
                          "bytes_per_block": bpb, "blocks_per_launch": nb, "avg_launch_ms": avg_j},
             "kernels_ms": {"reproj_jacobian": avg_j, "semantic_jacobian": s_ms / max(1, s_n)},
             "reproj_blocks_per_s": nb * world / (avg_j * 1e-3) if avg_j > 0 else None,
