@@ -63,6 +63,7 @@ struct mi_ba_context {
   miba::DevArray<uint8_t> cam_var, pt_var;
   miba::DevArray<double> qt, cam, X;       // current parameters
   miba::DevArray<double> qt_c, cam_c, X_c; // candidate parameters
+  miba::DevArray<double> img_rec;          // [I][16] packed image records
   miba::DevArray<uint32_t> cm_perm;
   miba::DevArray<miba::DevTile> tiles;
   int ntiles = 0;

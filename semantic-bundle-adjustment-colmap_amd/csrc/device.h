@@ -12,6 +12,8 @@
 //   images     qt[I][8]        q(4) t(3) pad — one 64-B line per image
 //              img_flags u32[I] bit0 variable pose, bits1..3 constant tvec
 //   cameras    cam[C][8]       params, padded to 8
+//   img_rec    double[I][16]   q t meta cam: the Jacobian kernel's per-image
+//                              record (one 128-B line), packed per linearization
 //   points     X[P][3]
 // Camera-side reductions run over cm_perm (blocks sorted by image) in tiles
 // that never straddle an image, so each tile folds into one atomic flush.
@@ -65,6 +67,7 @@ struct DevProblem {
   double* qt;   // [I][8]
   double* cam;  // [C][8]
   double* X;    // [P][3]
+  double* img_rec;  // [I][16] q(4) t(3) meta cam(8): packed by launch_pack_images
 };
 
 }  // namespace miba

@@ -12,12 +12,11 @@ namespace miba {
 struct SemDevice;  // defined in semantic.h
 
 // Residual + tangent Jacobian of every reduced block (J-materialising), with
-// the loss Corrector applied, the cost folded into per-workgroup partials and
-// the point blocks V_p = sum Jp'Jp (6) and g_p = sum Jp'r (3) reduced
-// wave-locally into Vg[P][9] (Vg must be zeroed before the launch).
-// write_jacobian = 0 skips the J/r stores (cost + point blocks only).
-void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* Vg,
-                            double* cost_partial, int write_jacobian, hipStream_t s);
+// the loss Corrector applied and the cost folded into per-workgroup partials.
+// p.jvariant selects A/B builds of the C4 shape (0 = production).
+// Rebuild p.img_rec from qt / cam / flags (before every Jacobian launch).
+void launch_pack_images(const DevProblem& p, double* rec, hipStream_t s);
+void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s);
 int reproj_grid(int64_t nb);
 
 // Cost 0.5*sum(rho) of every reduced block at parameters (qt, cam, X).
@@ -29,6 +28,10 @@ void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s);
 
 // Point side: Jacobi scale (first), LM diagonal (when !reuse_diag) and the
 // damped inverse Vinv[P][6] of V_p + Lambda_p.
+// Point blocks Vg[P][9] = (V_p packed upper 6, g_p 3) of the variable points
+// from J and r (the solver's point-side normal equations).
+void launch_point_normal(const DevProblem& p, const DevPoint* vp, int64_t npv, const double2* r, const double* J,
+                         double* Vg, hipStream_t s);
 void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg,
                           double* scale_p, double* diag_p, double* Vinv, int first, int reuse_diag,
                           double radius, hipStream_t s);

@@ -21,6 +21,8 @@ namespace miba {
 
 namespace {
 
+typedef double dvec2 __attribute__((ext_vector_type(2)));  // native 16-B vector (nontemporal builtins)
+
 constexpr int kSymPose = 21;  // packed upper triangle of 6x6
 
 __host__ __device__ constexpr int sym_size(int n) { return n * (n + 1) / 2; }
@@ -253,7 +255,7 @@ __device__ inline void emit_row(int rw, double* dst, const double (&B)[6], const
 
 // Copy NR rows of R doubles (LDS stride LS) into a global range whose rows
 // are G doubles apart, one wavefront, 8 B per lane per step.
-template <int R, int LS, int G>
+template <int R, int LS, int G, bool NT = false>
 __device__ inline void wave_readout(const double* __restrict__ src, double* __restrict__ dst, int nrows) {
   const int lane = threadIdx.x & 63;
   const int total = nrows * R;
@@ -261,43 +263,79 @@ __device__ inline void wave_readout(const double* __restrict__ src, double* __re
   constexpr int dr = 64 / R, dc = 64 % R;
 #pragma unroll 4
   for (int e = lane; e < total; e += 64) {
-    dst[row * G + col] = src[row * LS + col];
+    if constexpr (NT)
+      __builtin_nontemporal_store(src[row * LS + col], dst + row * G + col);
+    else
+      dst[row * G + col] = src[row * LS + col];
     row += dr;
     col += dc;
     if (col >= R) { col -= R; ++row; }
   }
 }
 
-// One lane per reduced block, one wavefront per 64 consecutive blocks.
-// V selects the store path (A/B-tested, tools/ab_jacobian.py):
-//   V = 0  workgroup-shared LDS rows (2W+1 stride), one barrier, 8-B stores;
-//   V = 1  wave-private LDS rows, no workgroup barrier;
-//   V = 2  wave-private half rows (x then y, W stride): half the LDS, twice
-//          the occupancy.
-// The camera-tangent columns are compile-time (template on the refine flags).
-template <int M, int RF, int V>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(V == 2 ? 4 : 1))) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
-                                                                  double* __restrict__ J_out,
-                                                                  double* __restrict__ Vg,
-                                                                  double* __restrict__ cost_partial,
-                                                                  int write_jacobian) {
+// As wave_readout, 16 B per lane: R (even) doubles per row, LDS row stride
+// LS (even), so no pair straddles a row.
+template <int R, int LS, int G, bool NT = false>
+__device__ inline void wave_readout16(const double* __restrict__ src, double* __restrict__ dst, int nrows) {
+  constexpr int R2 = R / 2;
+  const int lane = threadIdx.x & 63;
+  const int total = nrows * R2;
+  int row = lane / R2, col = lane - (lane / R2) * R2;
+  constexpr int dr = 64 / R2, dc = 64 % R2;
+#pragma unroll 4
+  for (int e = lane; e < total; e += 64) {
+    const dvec2 v = *reinterpret_cast<const dvec2*>(src + row * LS + 2 * col);
+    dvec2* d = reinterpret_cast<dvec2*>(dst + row * G + 2 * col);
+    if constexpr (NT)
+      __builtin_nontemporal_store(v, d);
+    else
+      *d = v;
+    row += dr;
+    col += dc;
+    if (col >= R2) { col -= R2; ++row; }
+  }
+}
+
+// One lane per reduced block, one wavefront per 64 consecutive blocks; the
+// kernel writes residuals, tangent Jacobian rows and a per-workgroup cost
+// partial, nothing else (the point/camera normal-equation blocks are reduced
+// by the solver's own passes over J, as Ceres' SchurEliminator does after
+// its Jacobian evaluation).
+//
+// Jacobian rows are 2W doubles per block.  A lane's row is not a coalesced
+// store shape, so rows go through a wave-private LDS slab and leave as
+// 8-B-per-lane stores over contiguous memory (512 B per wave-instruction).
+// The slab holds 64/NP rows and is filled in NP passes: NP = 2 keeps the
+// LDS at 7.9 KB per wave so 5 workgroups (20 waves) share a CU, enough for
+// one wave's f64 arithmetic to hide another's store issue (the kernel sits
+// on the HBM write roof: DESIGN.md §4).  LOSS = 0 compiles the TrivialLoss
+// path without the Corrector.  D: diagnostic builds for the roofline
+// decomposition (1 = no J store, 2 = no arithmetic); never used by the LM.
+// Build options (bits of D): 8 nontemporal J stores, 16 nontemporal obs
+// loads and r stores, 32 16-B J stores; 1 and 2 are the diagnostic builds.
+constexpr int kJacProduction = 8 | 16 | 32;
+template <int M, int RF, int LOSS, int NP, int D = kJacProduction, int WPE = 4>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
+                                                                 double* __restrict__ J_out,
+                                                                 double* __restrict__ cost_partial) {
   constexpr int np = Model<M>::kNumParams;
   constexpr unsigned CM = cam_tangent_mask(M, RF);
   constexpr int CT = popcount8(CM);
   constexpr int W = 9 + CT;
   constexpr int W2 = 2 * W;
-  constexpr int LS = (V == 2) ? (W | 1) : (W2 | 1);
+  // odd row stride: conflict-free row writes; D & 32 (16-B readout) needs an
+  // even stride: W2 + 4 gives 2-way conflicts on the row writes
+  constexpr int LS = (D & 32) ? W2 + 4 : (W2 | 1);
+  constexpr int RP = 64 / NP;
+  constexpr int RS = 18;  // LDS stride of an image record (144 B: conflict-free ds_read_b128)
+  constexpr int SLAB = (RP * LS > 64 * RS) ? RP * LS : 64 * RS;
   __shared__ double sred[4];
-  __shared__ double sJ[kBlock * LS];
+  __shared__ double sJ[(kBlock / 64) * SLAB];
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t wb0 = i - lane;  // first block of this wavefront
+  double* slab = sJ + (threadIdx.x >> 6) * SLAB;
   double cost = 0.0;
-  uint32_t key = 0xffffffffu;
-  bool ptv = false;
-  double vg[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) vg[k] = 0.0;
   double B[6] = {0, 0, 0, 0, 0, 0}, Mq[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, jx[2][3] = {{0, 0, 0}, {0, 0, 0}};
   double Jp[2 * np];
 #pragma unroll
@@ -305,118 +343,145 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(V == 2 ?
   double sc = 1.0;
   bool cv = false, pose_var = false;
   uint32_t flags = 0;
-  if (i < p.nb) {
+  if ((D & 2) && i < p.nb) {
     const double2 o = p.obs_xy[i];
-    const uint32_t img = p.obs_img[i];
-    const uint32_t pt = p.obs_pt[i];
-    key = pt;
-    const double* qt = p.qt + 8 * (size_t)img;
-    const double q[4] = {qt[0], qt[1], qt[2], qt[3]};
-    const double t[3] = {qt[4], qt[5], qt[6]};
-    flags = p.img_flags[img];
-    pose_var = flags & 1u;
-    const uint32_t cam_idx = p.img_cam[img];
-    const double* pc = p.cam + 8 * (size_t)cam_idx;
+    B[0] = o.x; B[1] = o.y; B[2] = o.x + o.y; B[3] = o.x - o.y; B[4] = o.x * 2.0; B[5] = o.y * 2.0;
+    pose_var = true;
+    cv = true;
+    r_out[i] = o;
+  } else if constexpr (!(D & 2)) {
+    // Image records (pose, camera, flags; 128 B each) of the wave's 64 blocks:
+    // consecutive blocks belong to different images (point-major order), so a
+    // per-lane fetch would touch 64 lines per instruction.  Instead 8 lanes
+    // fetch one record with 16-B loads (8 whole lines per instruction) and the
+    // records are handed out through the wave's LDS slab.
+    const bool live = i < p.nb;
+    uint32_t img = 0u;
+    if (live) img = (D & 16) ? __builtin_nontemporal_load(p.obs_img + i) : p.obs_img[i];
+    if constexpr ((D & 4) != 0) img &= 127u;  // diagnostic: L1-resident record working set
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int src = 8 * j + (lane >> 3);
+      const uint32_t is = __shfl(img, src, 64);
+      const double2 v = reinterpret_cast<const double2*>(p.img_rec + 16 * (size_t)is)[lane & 7];
+      reinterpret_cast<double2*>(slab + src * RS)[lane & 7] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const double* rec = slab + lane * RS;
+    const double q[4] = {rec[0], rec[1], rec[2], rec[3]};
+    const double t[3] = {rec[4], rec[5], rec[6]};
+    const uint32_t meta = (uint32_t)__double_as_longlong(rec[7]);
     double prm[np];
 #pragma unroll
-    for (int k = 0; k < np; ++k) prm[k] = pc[k];
-    cv = p.cam_var[cam_idx] != 0;
-    ptv = p.pt_var[pt] != 0;
-    const double X[3] = {p.X[3 * (size_t)pt], p.X[3 * (size_t)pt + 1], p.X[3 * (size_t)pt + 2]};
-    double P[3];
-    unit_quat_rotate(q, X, P);
-    P[0] += t[0];
-    P[1] += t[1];
-    P[2] += t[2];
-    const double iz = 1.0 / P[2];
-    const double u = P[0] * iz, v = P[1] * iz;
-    double x, y, A[4];
-    world_to_image_jac<M>(prm, u, v, &x, &y, A, Jp);
-    const double r0 = x - o.x, r1 = y - o.y;
-    double rho[3];
-    loss_eval(p.loss_type, p.loss_scale, r0 * r0 + r1 * r1, rho);
-    cost = 0.5 * rho[0];
-    // Ceres Corrector, rho'' <= 0 branch (Trivial/SoftL1/Cauchy): r, J *= sqrt(rho')
-    sc = (p.loss_type == kLossTrivial) ? 1.0 : sqrt(rho[1]);
-    const double cr[2] = {r0 * sc, r1 * sc};
-    // B = d(x,y)/dP (2x3) = A * d(u,v)/dP, loss-scaled
-    B[0] = A[0] * iz; B[1] = A[1] * iz; B[2] = -(A[0] * u + A[1] * v) * iz;
-    B[3] = A[2] * iz; B[4] = A[3] * iz; B[5] = -(A[2] * u + A[3] * v) * iz;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) B[k] *= sc;
-    if (pose_var) {
-      double Dq[12], PJ[12];
-      unit_quat_rotate_dq(q, X, Dq);
-      quat_plus_jacobian(q, PJ);
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b)
-          Mq[a * 3 + b] = Dq[a * 4 + 0] * PJ[0 * 3 + b] + Dq[a * 4 + 1] * PJ[1 * 3 + b] +
-                          Dq[a * 4 + 2] * PJ[2 * 3 + b] + Dq[a * 4 + 3] * PJ[3 * 3 + b];
+    for (int k = 0; k < np; ++k) prm[k] = rec[8 + k];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (live) {
+      double2 o;
+      if constexpr ((D & 16) != 0) {
+        const dvec2 ov = __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(p.obs_xy) + i);
+        o = make_double2(ov.x, ov.y);
+      } else {
+        o = p.obs_xy[i];
+      }
+      const uint32_t pt = (D & 16) ? __builtin_nontemporal_load(p.obs_pt + i) : p.obs_pt[i];
+      flags = meta & 0xffu;
+      pose_var = flags & 1u;
+      cv = (meta >> 8) & 1u;
+      const bool ptv = p.pt_var[pt] != 0;
+      const double X[3] = {p.X[3 * (size_t)pt], p.X[3 * (size_t)pt + 1], p.X[3 * (size_t)pt + 2]};
+      double P[3];
+      unit_quat_rotate(q, X, P);
+      P[0] += t[0];
+      P[1] += t[1];
+      P[2] += t[2];
+      const double iz = 1.0 / P[2];
+      const double u = P[0] * iz, v = P[1] * iz;
+      double x, y, A[4];
+      world_to_image_jac<M>(prm, u, v, &x, &y, A, Jp);
+      const double r0 = x - o.x, r1 = y - o.y;
+      if constexpr (LOSS == 0) {
+        cost = 0.5 * (r0 * r0 + r1 * r1);
+      } else {
+        double rho[3];
+        loss_eval(p.loss_type, p.loss_scale, r0 * r0 + r1 * r1, rho);
+        cost = 0.5 * rho[0];
+        // Ceres Corrector, rho'' <= 0 branch (Trivial/SoftL1/Cauchy): r, J *= sqrt(rho')
+        sc = sqrt(rho[1]);
+      }
+      // B = d(x,y)/dP (2x3) = A * d(u,v)/dP, loss-scaled
+      B[0] = A[0] * iz; B[1] = A[1] * iz; B[2] = -(A[0] * u + A[1] * v) * iz;
+      B[3] = A[2] * iz; B[4] = A[3] * iz; B[5] = -(A[2] * u + A[3] * v) * iz;
+      if constexpr (LOSS != 0) {
+  #pragma unroll
+        for (int k = 0; k < 6; ++k) B[k] *= sc;
+      }
+      if (pose_var) {
+        double Dq[12], PJ[12];
+        unit_quat_rotate_dq(q, X, Dq);
+        quat_plus_jacobian(q, PJ);
+  #pragma unroll
+        for (int a = 0; a < 3; ++a)
+  #pragma unroll
+          for (int b = 0; b < 3; ++b)
+            Mq[a * 3 + b] = Dq[a * 4 + 0] * PJ[0 * 3 + b] + Dq[a * 4 + 1] * PJ[1 * 3 + b] +
+                            Dq[a * 4 + 2] * PJ[2 * 3 + b] + Dq[a * 4 + 3] * PJ[3 * 3 + b];
+      }
+      if (ptv) {
+        double R[9];
+        unit_quat_matrix(q, R);
+  #pragma unroll
+        for (int rw = 0; rw < 2; ++rw)
+  #pragma unroll
+          for (int b = 0; b < 3; ++b)
+            jx[rw][b] = B[rw * 3 + 0] * R[b] + B[rw * 3 + 1] * R[3 + b] + B[rw * 3 + 2] * R[6 + b];
+      }
+      if constexpr ((D & 16) != 0)
+        __builtin_nontemporal_store(dvec2{r0 * sc, r1 * sc}, reinterpret_cast<dvec2*>(r_out) + i);
+      else
+        r_out[i] = make_double2(r0 * sc, r1 * sc);
     }
-    if (ptv) {
-      double R[9];
-      unit_quat_matrix(q, R);
-#pragma unroll
-      for (int rw = 0; rw < 2; ++rw)
-#pragma unroll
-        for (int b = 0; b < 3; ++b)
-          jx[rw][b] = B[rw * 3 + 0] * R[b] + B[rw * 3 + 1] * R[3 + b] + B[rw * 3 + 2] * R[6 + b];
-      vg[0] = jx[0][0] * jx[0][0] + jx[1][0] * jx[1][0];
-      vg[1] = jx[0][0] * jx[0][1] + jx[1][0] * jx[1][1];
-      vg[2] = jx[0][0] * jx[0][2] + jx[1][0] * jx[1][2];
-      vg[3] = jx[0][1] * jx[0][1] + jx[1][1] * jx[1][1];
-      vg[4] = jx[0][1] * jx[0][2] + jx[1][1] * jx[1][2];
-      vg[5] = jx[0][2] * jx[0][2] + jx[1][2] * jx[1][2];
-      vg[6] = jx[0][0] * cr[0] + jx[1][0] * cr[1];
-      vg[7] = jx[0][1] * cr[0] + jx[1][1] * cr[1];
-      vg[8] = jx[0][2] * cr[0] + jx[1][2] * cr[1];
-    }
-    if (write_jacobian) r_out[i] = make_double2(cr[0], cr[1]);
   }
-  if (write_jacobian) {
+  if constexpr (!(D & 1)) {
     const int live = wb0 >= p.nb ? 0 : (p.nb - wb0 < 64 ? (int)(p.nb - wb0) : 64);
-    if constexpr (V == 0) {
-      double* row = sJ + threadIdx.x * LS;
-      if (i < p.nb) {
+#pragma unroll
+    for (int h = 0; h < NP; ++h) {
+      if (lane / RP == h && i < p.nb) {
+        double* row = slab + (lane % RP) * LS;
         emit_row<M, CM>(0, row, B, Mq, pose_var, flags, jx, Jp, sc, cv);
         emit_row<M, CM>(1, row + W, B, Mq, pose_var, flags, jx, Jp, sc, cv);
       }
-      __syncthreads();
-      const int64_t b0 = (int64_t)blockIdx.x * kBlock;
-      const int cnt = p.nb - b0 < kBlock ? (int)(p.nb - b0) : kBlock;
-      const int total = cnt * W2;
-      double* out = J_out + b0 * W2;
-      for (int idx = threadIdx.x; idx < total; idx += kBlock) {
-        const int rr = idx / W2, k = idx - rr * W2;
-        out[idx] = sJ[rr * LS + k];
-      }
-    } else if constexpr (V == 1) {
-      double* wbase = sJ + (threadIdx.x - lane) * LS;
-      if (i < p.nb) {
-        emit_row<M, CM>(0, wbase + lane * LS, B, Mq, pose_var, flags, jx, Jp, sc, cv);
-        emit_row<M, CM>(1, wbase + lane * LS + W, B, Mq, pose_var, flags, jx, Jp, sc, cv);
-      }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      wave_readout<W2, LS, W2>(wbase, J_out + wb0 * W2, live);
-    } else {
-      double* wbase = sJ + (threadIdx.x - lane) * LS;
-#pragma unroll
-      for (int rw = 0; rw < 2; ++rw) {
-        if (i < p.nb) emit_row<M, CM>(rw, wbase + lane * LS, B, Mq, pose_var, flags, jx, Jp, sc, cv);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        wave_readout<W, LS, W2>(wbase, J_out + wb0 * W2 + rw * W, live);
+      const int rows = live - h * RP < 0 ? 0 : (live - h * RP > RP ? RP : live - h * RP);
+      if constexpr ((D & 32) != 0)
+        wave_readout16<W2, LS, W2, (D & 8) != 0>(slab, J_out + (wb0 + h * RP) * W2, rows);
+      else
+        wave_readout<W2, LS, W2, (D & 8) != 0>(slab, J_out + (wb0 + h * RP) * W2, rows);
+      if (h + 1 < NP) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       }
     }
   }
-  wave_segmented_store<9>(key, ptv, vg, Vg);
   const double s = block_sum(cost, sred);
   if (threadIdx.x == 0) cost_partial[blockIdx.x] = s;
+}
+
+// Image records img_rec[I][16] = q(4) t(3) meta camera-params(8), meta =
+// img_flags | cam_var << 8 (bit pattern in a double slot): one 128-B line per
+// image, rebuilt whenever poses or intrinsics change.
+__global__ void pack_images_kernel(DevProblem p, double* __restrict__ rec) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= p.num_images) return;
+  const uint32_t cam = p.img_cam[k];
+  double* o = rec + 16 * (size_t)k;
+#pragma unroll
+  for (int m = 0; m < 7; ++m) o[m] = p.qt[8 * (size_t)k + m];
+  o[7] = __longlong_as_double((long long)(p.img_flags[k] | ((p.cam_var[cam] != 0 ? 1u : 0u) << 8)));
+#pragma unroll
+  for (int m = 0; m < 8; ++m) o[8 + m] = p.cam[8 * (size_t)cam + m];
 }
 
 template <int M>
@@ -475,6 +540,39 @@ __device__ inline void sym3_mul(const double s[6], const double x[3], double y[3
   y[0] = s[0] * x[0] + s[1] * x[1] + s[2] * x[2];
   y[1] = s[1] * x[0] + s[3] * x[1] + s[4] * x[2];
   y[2] = s[2] * x[0] + s[4] * x[1] + s[5] * x[2];
+}
+
+// Point blocks V_p = sum J_p'J_p (6, packed upper) and g_p = sum J_p'r (3)
+// of every variable point from its contiguous (point-major) blocks.
+template <int CT>
+__global__ __launch_bounds__(kBlock) void point_normal_kernel(const DevPoint* __restrict__ vp, int64_t npv,
+                                                               const double2* __restrict__ rr,
+                                                               const double* __restrict__ J,
+                                                               double* __restrict__ Vg) {
+  constexpr int W = 9 + CT;
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= npv) return;
+  const DevPoint d = vp[k];
+  double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t n = 0; n < d.count; ++n) {
+    const size_t b = d.start + n;
+    const double* Jb = J + b * 2 * W;
+    const double2 r = rr[b];
+    const double a0 = Jb[6], a1 = Jb[7], a2 = Jb[8];
+    const double c0 = Jb[W + 6], c1 = Jb[W + 7], c2 = Jb[W + 8];
+    v[0] += a0 * a0 + c0 * c0;
+    v[1] += a0 * a1 + c0 * c1;
+    v[2] += a0 * a2 + c0 * c2;
+    v[3] += a1 * a1 + c1 * c1;
+    v[4] += a1 * a2 + c1 * c2;
+    v[5] += a2 * a2 + c2 * c2;
+    v[6] += a0 * r.x + c0 * r.y;
+    v[7] += a1 * r.x + c1 * r.y;
+    v[8] += a2 * r.x + c2 * r.y;
+  }
+  double* out = Vg + 9 * (size_t)d.point;
+#pragma unroll
+  for (int m = 0; m < 9; ++m) out[m] = v[m];
 }
 
 __global__ __launch_bounds__(kBlock) void point_prepare_kernel(const DevPoint* __restrict__ vp, int64_t npv,
@@ -1197,23 +1295,57 @@ inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 
 
 int reproj_grid(int64_t nb) { return (int)grid_for(nb, kBlock); }
 
-void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* Vg, double* cost_partial,
-                            int write_jacobian, hipStream_t s) {
+void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s) {
   if (p.nb == 0) return;
   const unsigned g = grid_for(p.nb, kBlock);
   dispatch_model(p.model, [&](auto m) {
     constexpr int M = decltype(m)::value;
     auto go = [&](auto rf) {
       constexpr int RF = decltype(rf)::value;
-      if (p.jvariant == 1)
-        hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 1>), dim3(g), dim3(kBlock), 0, s, p, r, J, Vg,
-                           cost_partial, write_jacobian);
-      else if (p.jvariant == 2)
-        hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 2>), dim3(g), dim3(kBlock), 0, s, p, r, J, Vg,
-                           cost_partial, write_jacobian);
+      auto launch = [&](auto loss) {
+        constexpr int LOSS = decltype(loss)::value;
+        if constexpr (M == kOpenCV && RF == 5 && LOSS == 0) {
+          // A/B and roofline-decomposition builds of the C4 shape (tools/ab_jacobian.py)
+          switch (p.jvariant) {
+            case 1:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 1, kJacProduction>), dim3(g), dim3(kBlock), 0, s, p, r, J,
+                                 cost_partial);
+              return;
+            case 4:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 4, kJacProduction>), dim3(g), dim3(kBlock), 0, s, p, r, J,
+                                 cost_partial);
+              return;
+            case 20:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, 0>), dim3(g), dim3(kBlock), 0, s, p, r, J,
+                                 cost_partial);
+              return;
+            case 21:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, 24>), dim3(g), dim3(kBlock), 0, s, p, r, J,
+                                 cost_partial);
+              return;
+            case 22:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 4>), dim3(g), dim3(kBlock), 0, s, p, r, J,
+                                 cost_partial);
+              return;
+            case 9:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 1>), dim3(g), dim3(kBlock), 0, s, p, r, J,
+                                 cost_partial);
+              return;
+            case 10:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 2>), dim3(g), dim3(kBlock), 0, s, p, r, J,
+                                 cost_partial);
+              return;
+            default:
+              break;
+          }
+        }
+        hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, LOSS, 2, kJacProduction>), dim3(g), dim3(kBlock), 0, s, p,
+                           r, J, cost_partial);
+      };
+      if (p.loss_type == kLossTrivial)
+        launch(std::integral_constant<int, 0>{});
       else
-        hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0>), dim3(g), dim3(kBlock), 0, s, p, r, J, Vg,
-                           cost_partial, write_jacobian);
+        launch(std::integral_constant<int, 1>{});
     };
     switch (p.refine_mask & 7) {
       case 0: go(std::integral_constant<int, 0>{}); break;
@@ -1228,6 +1360,11 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
   });
 }
 
+void launch_pack_images(const DevProblem& p, double* rec, hipStream_t s) {
+  if (p.num_images == 0) return;
+  hipLaunchKernelGGL(pack_images_kernel, dim3(grid_for(p.num_images, kBlock)), dim3(kBlock), 0, s, p, rec);
+}
+
 void launch_reproj_cost(const DevProblem& p, const double* qt, const double* cam, const double* X,
                         double* cost_partial, hipStream_t s) {
   if (p.nb == 0) return;
@@ -1240,6 +1377,15 @@ void launch_reproj_cost(const DevProblem& p, const double* qt, const double* cam
 
 void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s) {
   hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, s, partial, n, out);
+}
+
+void launch_point_normal(const DevProblem& p, const DevPoint* vp, int64_t npv, const double2* r, const double* J,
+                         double* Vg, hipStream_t s) {
+  if (npv == 0) return;
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    hipLaunchKernelGGL(point_normal_kernel<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, vp, npv, r, J, Vg);
+  });
 }
 
 void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg,

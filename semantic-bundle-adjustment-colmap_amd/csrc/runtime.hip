@@ -224,7 +224,7 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
       for (int m = 0; m < np; ++m) cm[8 * c + m] = p->camera_params[(size_t)np * c + m];
     if (ctx->qt.alloc(8 * I) || ctx->qt_c.alloc(8 * I) || ctx->cam.alloc(8 * C) || ctx->cam_c.alloc(8 * C) ||
         ctx->X.alloc(3 * P) || ctx->X_c.alloc(3 * P) || ctx->img_flags.alloc(I) || ctx->img_cam.alloc(I) ||
-        ctx->cam_var.alloc(C) || ctx->pt_var.alloc(P))
+        ctx->cam_var.alloc(C) || ctx->pt_var.alloc(P) || ctx->img_rec.alloc(16 * I))
       return fail(MI_BA_ERR_OUT_OF_MEMORY);
     if ((I && (hipMemcpy(ctx->qt.ptr, qt.data(), qt.size() * 8, hipMemcpyHostToDevice) ||
                hipMemcpy(ctx->img_flags.ptr, fl.data(), I * 4, hipMemcpyHostToDevice) ||
@@ -261,6 +261,7 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
   d.qt = ctx->qt.ptr;
   d.cam = ctx->cam.ptr;
   d.X = ctx->X.ptr;
+  d.img_rec = ctx->img_rec.ptr;
   // linearization + LM buffers
   ctx->npartial = std::max<int64_t>(1, reproj_grid(nb));
   const int64_t nf = d.nf;
@@ -335,11 +336,11 @@ void context_destroy(mi_ba_context* ctx) {
 mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   hipStream_t s = ctx->stream;
   const DevProblem& d = ctx->dev;
-  if (d.num_points) MI_HIP(hipMemsetAsync(ctx->Vg.ptr, 0, 9 * d.num_points * sizeof(double), s));
   MI_HIP(hipMemsetAsync(ctx->scalars.ptr, 0, sizeof(double) * kNumScalars, s));
   hipEvent_t stop;
+  launch_pack_images(d, ctx->img_rec.ptr, s);
   timer_begin(ctx, "reproj_jacobian", &stop);
-  launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr, ctx->partial.ptr, 1, s);
+  launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->partial.ptr, s);
   timer_end(ctx, stop);
   if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s);
   if (ctx->sem) {
@@ -478,6 +479,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
   double x_cost = 0.0;
   mi_ba_status st = context_linearize(ctx, &x_cost);
   if (st != MI_BA_OK) return st;
+  launch_point_normal(d, ctx->vpoints.ptr, ctx->npv, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr, s);
   sum->jacobian_evaluation_time_in_seconds += now_s() - tj;
   sum->num_jacobian_evaluations = 1;
   sum->initial_cost = x_cost + ctx->fixed_cost;
@@ -601,6 +603,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       tj = now_s();
       st = context_linearize(ctx, nullptr);
       if (st != MI_BA_OK) return st;
+      launch_point_normal(d, ctx->vpoints.ptr, ctx->npv, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr, s);
       sum->num_jacobian_evaluations += 1;
       sum->jacobian_evaluation_time_in_seconds += now_s() - tj;
     } else {
@@ -764,9 +767,9 @@ mi_ba_status mi_ba_evaluate_jacobian(mi_ba_context* ctx) {
   if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
   const DevProblem& d = ctx->dev;
   hipEvent_t stop;
-  if (d.num_points) MI_HIP(hipMemsetAsync(ctx->Vg.ptr, 0, 9 * d.num_points * sizeof(double), ctx->stream));
+  launch_pack_images(d, ctx->img_rec.ptr, ctx->stream);
   timer_begin(ctx, "reproj_jacobian", &stop);
-  launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr, ctx->partial.ptr, 1, ctx->stream);
+  launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->partial.ptr, ctx->stream);
   timer_end(ctx, stop);
   MI_HIP(hipGetLastError());
   return MI_BA_OK;
@@ -845,7 +848,7 @@ mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost) {
 
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value) {
   if (!ctx || !key) return MI_BA_ERR_INVALID_ARGUMENT;
-  if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 2) {
+  if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 31) {
     ctx->dev.jvariant = value;
     return MI_BA_OK;
   }
