@@ -88,6 +88,10 @@ struct mi_ba_context {
   bool dense = false;
   rocblas_handle blas = nullptr;
   miba::DevArray<double> S;
+  miba::DevArray<double> Linv, Z;          // [P][6] inverse point factors, [nb][3F] Schur factors
+  miba::DevArray<miba::DevPairTile> ptiles;
+  miba::DevArray<uint2> pairs;             // (a, b) block pairs bucketed by image pair
+  int nptiles = 0;
   miba::DevArray<int32_t> info;
 
   double fixed_cost = 0.0;

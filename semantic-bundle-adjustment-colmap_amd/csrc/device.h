@@ -41,6 +41,14 @@ struct DevPoint {      // variable point with its contiguous block range
   uint32_t pad;
 };
 
+struct DevPairTile {   // image-pair tile of the explicit Schur build
+  uint32_t ia, ib;     // images of the pairs' first / second block (ia <= ib)
+  uint32_t start;      // offset into the pair list
+  uint32_t count : 31; // pairs (<= kPairTile)
+  uint32_t self : 1;   // pairs (a, a) of one observation
+};
+constexpr int kPairTile = 256;
+
 struct DevProblem {
   int model;
   int np;              // camera params per camera

@@ -33,7 +33,7 @@ void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s);
 void launch_point_normal(const DevProblem& p, const DevPoint* vp, int64_t npv, const double2* r, const double* J,
                          double* Vg, hipStream_t s);
 void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg,
-                          double* scale_p, double* diag_p, double* Vinv, int first, int reuse_diag,
+                          double* scale_p, double* diag_p, double* Vinv, double* Linv, int first, int reuse_diag,
                           double radius, hipStream_t s);
 
 // Camera-side tile pass: per image/camera tangent block S_ii = U_ii - sum W V^-1 W',
@@ -78,10 +78,12 @@ void launch_plus(const DevProblem& p, const double* df, const double* dX, const 
                  const double* cam, const double* X, double* qt_out, double* cam_out, double* X_out,
                  hipStream_t s);
 
-// Explicit reduced camera system (nf x nf, row-major, both triangles):
-// S += U (tile pass) - sum_p W_p V_p^-1 W_p' (point pass); S must be zeroed.
-void launch_dense_schur(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles, int ntiles,
-                        const uint32_t* cm_perm, const double* J, const double* Vinv, double* S, hipStream_t s);
+// Explicit reduced camera system (nf x nf, row-major, upper triangle row <= col,
+// i.e. rocSOLVER's column-major lower): S += U (image tile pass) -
+// sum_p W_p V_p^-1 W_p' (Z factors, then MFMA image-pair tiles); S zeroed.
+void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
+                        const double* J, const double* Linv, double* Z, const DevPairTile* ptiles, int nptiles,
+                        const uint2* pairs, double* S, hipStream_t s);
 // S_kk += Lambda_k on parameter slots, S_kk = 1 on non-parameter slots.
 void launch_dense_finalize(const DevProblem& p, const double* lambda_f, double* S, hipStream_t s);
 

@@ -296,6 +296,23 @@ __device__ inline void wave_readout16(const double* __restrict__ src, double* __
   }
 }
 
+// Coalesced copy of nrows contiguous rows of R doubles from global memory
+// into a wave-private LDS slab with row stride LS (mirror of wave_readout).
+template <int R, int LS>
+__device__ inline void wave_load_rows(const double* __restrict__ src, double* __restrict__ dst, int nrows) {
+  const int lane = threadIdx.x & 63;
+  const int total = nrows * R;
+  int row = lane / R, col = lane - (lane / R) * R;
+  constexpr int dr = 64 / R, dc = 64 % R;
+#pragma unroll 4
+  for (int e = lane; e < total; e += 64) {
+    dst[row * LS + col] = __builtin_nontemporal_load(src + e);
+    row += dr;
+    col += dc;
+    if (col >= R) { col -= R; ++row; }
+  }
+}
+
 // One lane per reduced block, one wavefront per 64 consecutive blocks; the
 // kernel writes residuals, tangent Jacobian rows and a per-workgroup cost
 // partial, nothing else (the point/camera normal-equation blocks are reduced
@@ -579,7 +596,8 @@ __global__ __launch_bounds__(kBlock) void point_prepare_kernel(const DevPoint* _
                                                                 const double* __restrict__ Vg,
                                                                 double* __restrict__ scale_p,
                                                                 double* __restrict__ diag_p,
-                                                                double* __restrict__ Vinv, int first,
+                                                                double* __restrict__ Vinv,
+                                                                double* __restrict__ Linv, int first,
                                                                 int reuse_diag, double radius) {
   const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (k >= npv) return;
@@ -610,6 +628,21 @@ __global__ __launch_bounds__(kBlock) void point_prepare_kernel(const DevPoint* _
   sym3_inverse(V, inv);
 #pragma unroll
   for (int m = 0; m < 6; ++m) Vinv[6 * (size_t)pt + m] = inv[m];
+  if (Linv) {
+    // inverse Cholesky factor of the damped block: V^-1 = Linv' Linv, so the
+    // Schur term W V^-1 W' = Z Z' with Z = W Linv' (schur_z_kernel)
+    const double l00 = sqrt(V[0]);
+    const double l10 = V[1] / l00, l20 = V[2] / l00;
+    const double l11 = sqrt(V[3] - l10 * l10);
+    const double l21 = (V[4] - l20 * l10) / l11;
+    const double l22 = sqrt(V[5] - l20 * l20 - l21 * l21);
+    const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+    const double i10 = -l10 * i00 * i11;
+    const double i21 = -l21 * i11 * i22;
+    const double i20 = -(l20 * i00 + l21 * i10) * i22;
+    double* o = Linv + 6 * (size_t)pt;  // packed lower, row-major
+    o[0] = i00; o[1] = i10; o[2] = i11; o[3] = i20; o[4] = i21; o[5] = i22;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1201,57 +1234,152 @@ __global__ __launch_bounds__(kBlock) void dense_u_kernel(DevProblem p, const Dev
     if (va && vc) {
       const int64_t ra = fslot(p, img, cam, a), rc = fslot(p, img, cam, c);
       const double v = sred[k];
-      atomicAdd(S + ra * p.nf + rc, v);
-      if (ra != rc) atomicAdd(S + rc * p.nf + ra, v);
+      // upper triangle (row <= col) only: rocSOLVER reads the column-major lower
+      if (ra <= rc)
+        atomicAdd(S + ra * p.nf + rc, v);
+      else
+        atomicAdd(S + rc * p.nf + ra, v);
     }
   }
 }
 
-// Schur correction: per variable point, -Y_a W_b' for every pair of its
-// observations (a, b), Y_a = W_a V^-1, W = J_f' J_p.
+// ---------------------------------------------------------------------------
+// Explicit reduced camera system, Schur term.
+//
+// S -= sum_p W_p V_p^-1 W_p' is accumulated per image pair: with the damped
+// point block factored as V^-1 = Linv' Linv, every observation a carries
+// Z_a = W_a Linv' (F x 3, W_a = J_f,a' J_p,a), and the image-pair block is
+// S_ij -= sum over co-observed points of Z_a Z_b'.  That is a GEMM with
+// K = 3 per pair: one v_mfma_f64_16x16x4f64 per pair (F <= 14 padded to 16,
+// K = 3 padded to 4) over a bucketed pair list built once at setup.
+// ---------------------------------------------------------------------------
+
+// Z_a (k-major: Z[b][k*F + m]) of every block of a variable point; zero for
+// blocks of constant points.  J rows are read and Z rows written through the
+// wave's LDS slab (coalesced 8-B-per-lane transfers).
 template <int CT>
-__global__ __launch_bounds__(kBlock) void dense_schur_kernel(DevProblem p, const DevPoint* __restrict__ vp,
-                                                              int64_t npv, const double* __restrict__ J,
-                                                              const double* __restrict__ Vinv,
-                                                              double* __restrict__ S) {
-  constexpr int F = 6 + CT;
-  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (k >= npv) return;
-  const DevPoint d = vp[k];
-  const int W = 9 + CT;
-  const double* vi = Vinv + 6 * (size_t)d.point;
-  const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
-  for (uint32_t ia = 0; ia < d.count; ++ia) {
-    const uint32_t ba = d.start + ia;
-    const double* Ja = J + (size_t)ba * 2 * W;
-    const uint32_t img_a = p.obs_img[ba], cam_a = p.img_cam[img_a];
-    double Y[F][3];
+__global__ __launch_bounds__(kBlock) void schur_z_kernel(DevProblem p, const double* __restrict__ J,
+                                                          const double* __restrict__ Linv, double* __restrict__ Z) {
+  constexpr int F = 6 + CT, W = 9 + CT, W2 = 2 * W, LS = W2 | 1;
+  constexpr int ZN = 3 * F, ZS = ZN | 1;
+  constexpr int SL = (LS > ZS ? LS : ZS) * 64;
+  __shared__ double sl[(kBlock / 64) * SL];
+  double* slab = sl + (threadIdx.x >> 6) * SL;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t wb0 = i - lane;
+  const int live = wb0 >= p.nb ? 0 : (p.nb - wb0 < 64 ? (int)(p.nb - wb0) : 64);
+  wave_load_rows<W2, LS>(J + wb0 * W2, slab, live);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  double jf[2][F], jp[2][3];
+  {
+    const double* row = slab + lane * LS;
 #pragma unroll
-    for (int m = 0; m < F; ++m) {
-      const int col = m < 6 ? m : 9 + (m - 6);
-      double w3[3];
+    for (int rw = 0; rw < 2; ++rw) {
 #pragma unroll
-      for (int n = 0; n < 3; ++n) w3[n] = Ja[col] * Ja[6 + n] + Ja[W + col] * Ja[W + 6 + n];
-      sym3_mul(Vi, w3, Y[m]);
+      for (int m = 0; m < 6; ++m) jf[rw][m] = row[rw * W + m];
+#pragma unroll
+      for (int m = 0; m < 3; ++m) jp[rw][m] = row[rw * W + 6 + m];
+#pragma unroll
+      for (int m = 0; m < CT; ++m) jf[rw][6 + m] = row[rw * W + 9 + m];
     }
-    for (uint32_t ib = 0; ib < d.count; ++ib) {
-      const uint32_t bb = d.start + ib;
-      const double* Jb = J + (size_t)bb * 2 * W;
-      const uint32_t img_b = p.obs_img[bb], cam_b = p.img_cam[img_b];
-      const double jx0[3] = {Jb[6], Jb[7], Jb[8]}, jx1[3] = {Jb[W + 6], Jb[W + 7], Jb[W + 8]};
+  }
+  double L[6] = {0, 0, 0, 0, 0, 0};
+  if (i < p.nb) {
+    const uint32_t pt = p.obs_pt[i];
+    if (p.pt_var[pt]) {
 #pragma unroll
-      for (int c = 0; c < F; ++c) {
-        const int col = c < 6 ? c : 9 + (c - 6);
-        const double f0 = Jb[col], f1 = Jb[W + col];
-        if (f0 == 0.0 && f1 == 0.0) continue;
-        const double wb[3] = {f0 * jx0[0] + f1 * jx1[0], f0 * jx0[1] + f1 * jx1[1], f0 * jx0[2] + f1 * jx1[2]};
-        const int64_t rc = fslot(p, img_b, cam_b, c);
+      for (int m = 0; m < 6; ++m) L[m] = Linv[6 * (size_t)pt + m];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  double* zr = slab + lane * ZS;
 #pragma unroll
-        for (int r = 0; r < F; ++r) {
-          const double v = Y[r][0] * wb[0] + Y[r][1] * wb[1] + Y[r][2] * wb[2];
-          if (v != 0.0) atomicAdd(S + fslot(p, img_a, cam_a, r) * p.nf + rc, -v);
-        }
-      }
+  for (int m = 0; m < F; ++m) {
+    const double w0 = jf[0][m] * jp[0][0] + jf[1][m] * jp[1][0];
+    const double w1 = jf[0][m] * jp[0][1] + jf[1][m] * jp[1][1];
+    const double w2 = jf[0][m] * jp[0][2] + jf[1][m] * jp[1][2];
+    zr[m] = w0 * L[0];
+    zr[F + m] = w0 * L[1] + w1 * L[2];
+    zr[2 * F + m] = w0 * L[3] + w1 * L[4] + w2 * L[5];
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  wave_readout<ZN, ZS, ZN>(slab, Z + wb0 * ZN, live);
+}
+
+// One wavefront per image-pair tile: acc = sum over the tile's pairs of
+// Z_a Z_b' (16x16 f64 MFMA accumulator), then -acc into the upper triangle
+// (row <= col, row-major = rocSOLVER's column-major lower) of S.
+// Cross tiles hold pairs a != b: a mirrored entry lands on the same upper
+// element, a diagonal one counts twice.  Self tiles hold a == b.
+template <int CT>
+__global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const DevPairTile* __restrict__ tiles,
+                                                              int ntiles, const uint2* __restrict__ pairs,
+                                                              const double* __restrict__ Z, double* __restrict__ S) {
+  constexpr int F = 6 + CT, ZN = 3 * F;
+  // XCD-aware order: workgroup b runs on XCD b % 8; give each XCD a
+  // contiguous range of tiles (tiles are sorted by first image, so one
+  // image's Z rows stay in that XCD's L2 while its pairs stream by).
+  const int G = (ntiles + 3) / 4;
+  const int per = (G + 7) / 8;
+  const int b = blockIdx.x;
+  const int lb = (b % 8) * per + b / 8;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = lb * 4 + wv;
+  if (lb >= G || t >= ntiles) return;
+  const DevPairTile tl = tiles[t];
+  const int lane = threadIdx.x & 63;
+  const int m = lane & 15, k = lane >> 4;
+  const bool on = m < F && k < 3;
+  const int off = on ? k * F + m : 0;
+  typedef double dvec4 __attribute__((ext_vector_type(4)));
+  dvec4 acc = {0.0, 0.0, 0.0, 0.0};
+  const uint32_t cnt = tl.count;
+  const uint2* pl = pairs + tl.start;
+  uint32_t n = 0;
+  for (; n + 4 <= cnt; n += 4) {
+    uint2 pr[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pr[u] = pl[n + u];
+    double va[4], vb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      va[u] = on ? Z[(size_t)pr[u].x * ZN + off] : 0.0;
+      vb[u] = on ? Z[(size_t)pr[u].y * ZN + off] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va[u], vb[u], acc, 0, 0, 0);
+  }
+  for (; n < cnt; ++n) {
+    const uint2 pr = pl[n];
+    const double va = on ? Z[(size_t)pr.x * ZN + off] : 0.0;
+    const double vb = on ? Z[(size_t)pr.y * ZN + off] : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, acc, 0, 0, 0);
+  }
+  const uint32_t ia = tl.ia, ib = tl.ib;
+  const uint32_t ca = p.img_cam[ia], cb = p.img_cam[ib];
+  const bool pa = p.img_flags[ia] & 1u, pb = p.img_flags[ib] & 1u;
+  const bool cva = p.cam_var[ca] != 0, cvb = p.cam_var[cb] != 0;
+  const int ncol = lane & 15;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int mrow = 4 * r + (lane >> 4);  // v_mfma_f64_16x16x4f64 D layout (measured): D[4r + l/16][l%16]
+    if (mrow >= F || ncol >= F) continue;
+    const bool va = mrow < 6 ? pa : cva, vb = ncol < 6 ? pb : cvb;
+    if (!va || !vb) continue;
+    const int64_t ra = fslot(p, ia, ca, mrow), rb = fslot(p, ib, cb, ncol);
+    const double v = acc[r];
+    if (tl.self) {
+      if (ra <= rb) atomicAdd(S + ra * p.nf + rb, -v);
+    } else if (ra < rb) {
+      atomicAdd(S + ra * p.nf + rb, -v);
+    } else if (ra > rb) {
+      atomicAdd(S + rb * p.nf + ra, -v);
+    } else {
+      atomicAdd(S + ra * p.nf + ra, -2.0 * v);
     }
   }
 }
@@ -1389,11 +1517,11 @@ void launch_point_normal(const DevProblem& p, const DevPoint* vp, int64_t npv, c
 }
 
 void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg,
-                          double* scale_p, double* diag_p, double* Vinv, int first, int reuse_diag,
+                          double* scale_p, double* diag_p, double* Vinv, double* Linv, int first, int reuse_diag,
                           double radius, hipStream_t s) {
   if (npv == 0) return;
   hipLaunchKernelGGL(point_prepare_kernel, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, vp, npv, Vg,
-                     scale_p, diag_p, Vinv, first, reuse_diag, radius);
+                     scale_p, diag_p, Vinv, Linv, first, reuse_diag, radius);
 }
 
 void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
@@ -1485,15 +1613,19 @@ void launch_plus(const DevProblem& p, const double* df, const double* dX, const 
                        X_out);
 }
 
-void launch_dense_schur(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles, int ntiles,
-                        const uint32_t* cm_perm, const double* J, const double* Vinv, double* S, hipStream_t s) {
+void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
+                        const double* J, const double* Linv, double* Z, const DevPairTile* ptiles, int nptiles,
+                        const uint2* pairs, double* S, hipStream_t s) {
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
     if (ntiles > 0)
       hipLaunchKernelGGL(dense_u_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, J, S);
-    if (npv > 0)
-      hipLaunchKernelGGL(dense_schur_kernel<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, J,
-                         Vinv, S);
+    if (nptiles > 0 && p.nb > 0) {
+      hipLaunchKernelGGL(schur_z_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z);
+      const int G = (nptiles + 3) / 4;
+      const int grid = ((G + 7) / 8) * 8;  // whole XCD stripes (extra workgroups exit)
+      hipLaunchKernelGGL(schur_pairs_kernel<CT>, dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs, Z, S);
+    }
   });
 }
 

@@ -119,6 +119,84 @@ static void timer_collect(mi_ba_context* ctx) {
   ctx->timer.pending.clear();
 }
 
+// Pair list of the explicit Schur build: every unordered pair {a, b} of
+// blocks of one variable point (a == b included), bucketed by image pair
+// (ia <= ib) and cut into tiles of <= kPairTile pairs; self pairs (a == b)
+// get tiles of their own.  Built once per problem (structure only).
+mi_ba_status build_pair_tiles(mi_ba_context* ctx) {
+  const DevProblem& d = ctx->dev;
+  const int I = d.num_images;
+  const int64_t nb = d.nb;
+  std::vector<DevPoint> vp(ctx->npv);
+  std::vector<uint32_t> im(nb);
+  if (ctx->npv && hipMemcpy(vp.data(), ctx->vpoints.ptr, ctx->npv * sizeof(DevPoint), hipMemcpyDeviceToHost))
+    return MI_BA_ERR_HIP;
+  if (nb && hipMemcpy(im.data(), ctx->obs_img.ptr, nb * 4, hipMemcpyDeviceToHost)) return MI_BA_ERR_HIP;
+  // bucket key: first image ia (ia <= ib), self pairs in bucket I + ia
+  std::vector<int64_t> cnt(2 * (size_t)I + 1, 0);
+  auto visit = [&](auto&& f) {
+    for (const DevPoint& q : vp)
+      for (uint32_t x = 0; x < q.count; ++x)
+        for (uint32_t y = x; y < q.count; ++y) {
+          uint32_t a = q.start + x, b = q.start + y;
+          if (im[a] > im[b]) std::swap(a, b);
+          f(a, b, a == b ? (size_t)I + im[a] : (size_t)im[a]);
+        }
+  };
+  visit([&](uint32_t, uint32_t, size_t key) { ++cnt[key + 1]; });
+  for (size_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
+  const int64_t npairs = cnt.back();
+  std::vector<uint2> pr(npairs);
+  {
+    std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+    visit([&](uint32_t a, uint32_t b, size_t key) { pr[pos[key]++] = make_uint2(a, b); });
+  }
+  // within a first-image bucket, order by second image (counting sort, stable)
+  {
+    std::vector<int64_t> c2(I + 1);
+    std::vector<uint2> tmp;
+    for (int k = 0; k < 2 * I; ++k) {
+      const int64_t b0 = cnt[k], b1 = cnt[k + 1];
+      if (b1 - b0 < 2) continue;
+      std::fill(c2.begin(), c2.end(), 0);
+      for (int64_t e = b0; e < b1; ++e) ++c2[im[pr[e].y] + 1];
+      for (int j = 1; j <= I; ++j) c2[j] += c2[j - 1];
+      tmp.resize(b1 - b0);
+      for (int64_t e = b0; e < b1; ++e) tmp[c2[im[pr[e].y]]++] = pr[e];
+      std::copy(tmp.begin(), tmp.end(), pr.begin() + b0);
+    }
+  }
+  std::vector<DevPairTile> tl;
+  for (int k = 0; k < 2 * I; ++k) {
+    int64_t a = cnt[k];
+    while (a < cnt[k + 1]) {
+      const uint32_t ib = im[pr[a].y];
+      int64_t e = a;
+      while (e < cnt[k + 1] && im[pr[e].y] == ib) ++e;
+      for (int64_t t0 = a; t0 < e; t0 += kPairTile) {
+        DevPairTile t;
+        t.ia = im[pr[a].x];
+        t.ib = ib;
+        t.start = (uint32_t)t0;
+        t.count = (uint32_t)std::min<int64_t>(kPairTile, e - t0);
+        t.self = k >= I ? 1u : 0u;
+        tl.push_back(t);
+      }
+      a = e;
+    }
+  }
+  if (npairs >= (int64_t)UINT32_MAX || tl.size() >= (size_t)INT32_MAX) return MI_BA_ERR_UNSUPPORTED;
+  ctx->nptiles = (int)tl.size();
+  if (ctx->pairs.alloc(npairs) || ctx->ptiles.alloc(tl.size()) || ctx->Linv.alloc(6 * (size_t)d.num_points) ||
+      ctx->Z.alloc((size_t)nb * 3 * (6 + d.ct)))
+    return MI_BA_ERR_OUT_OF_MEMORY;
+  if ((npairs && hipMemcpy(ctx->pairs.ptr, pr.data(), npairs * sizeof(uint2), hipMemcpyHostToDevice)) ||
+      (!tl.empty() && hipMemcpy(ctx->ptiles.ptr, tl.data(), tl.size() * sizeof(DevPairTile), hipMemcpyHostToDevice)))
+    return MI_BA_ERR_HIP;
+  if (d.num_points && hipMemset(ctx->Linv.ptr, 0, 6 * (size_t)d.num_points * 8)) return MI_BA_ERR_HIP;
+  return MI_BA_OK;
+}
+
 mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, const mi_ba_semantic* sem,
                             mi_ba_context** out) {
   if (!o || !pin || !out) return MI_BA_ERR_INVALID_ARGUMENT;
@@ -299,6 +377,8 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
     }
     if (ctx->dense) {
       if (ctx->S.alloc((size_t)d.nf * d.nf) || ctx->info.alloc(1)) return fail(MI_BA_ERR_OUT_OF_MEMORY);
+      st = build_pair_tiles(ctx);
+      if (st != MI_BA_OK) return fail(st);
       if (rocblas_create_handle(&ctx->blas) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
       if (rocblas_set_stream(ctx->blas, ctx->stream) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
     }
@@ -433,8 +513,8 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   MI_HIP(hipMemsetAsync(ctx->S.ptr, 0, ctx->S.bytes(), s));
   hipEvent_t stop;
   timer_begin(ctx, "schur_build", &stop);
-  launch_dense_schur(d, ctx->vpoints.ptr, ctx->npv, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr,
-                     ctx->Vinv.ptr, ctx->S.ptr, s);
+  launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
+                     ctx->ptiles.ptr, ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, s);
   if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
   launch_dense_finalize(d, ctx->lambda_f.ptr, ctx->S.ptr, s);
   timer_end(ctx, stop);
@@ -495,7 +575,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     ++iteration;
     // Damped point inverses, Schur-Jacobi blocks, rhs.
     launch_point_prepare(d, ctx->vpoints.ptr, ctx->npv, ctx->Vg.ptr, ctx->scale_p.ptr, ctx->diag_p.ptr,
-                         ctx->Vinv.ptr, first, reuse_diag, radius, s);
+                         ctx->Vinv.ptr, ctx->dense ? ctx->Linv.ptr : nullptr, first, reuse_diag, radius, s);
     MI_HIP(hipMemsetAsync(ctx->pose_blk.ptr, 0, ctx->pose_blk.bytes(), s));
     MI_HIP(hipMemsetAsync(ctx->cam_blk.ptr, 0, ctx->cam_blk.bytes(), s));
     MI_HIP(hipMemsetAsync(ctx->bvec.ptr, 0, ctx->bvec.bytes(), s));

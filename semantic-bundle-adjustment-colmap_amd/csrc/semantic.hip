@@ -607,7 +607,7 @@ __global__ void semantic_product_kernel(const SemPair* __restrict__ pairs, int n
   }
 }
 
-// Pair blocks into the explicit reduced camera system (both triangles).
+// Pair blocks into the explicit reduced camera system (upper triangle).
 __global__ void semantic_dense_kernel(const SemPair* __restrict__ pairs, int npairs,
                                       const double* __restrict__ pair_blk, int64_t nf, double* __restrict__ S) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -620,7 +620,7 @@ __global__ void semantic_dense_kernel(const SemPair* __restrict__ pairs, int npa
   const double v = pair_blk[(size_t)k * kPairStride + (a <= b ? sym12(a, b) : sym12(b, a))];
   const int64_t ra = 6 * (int64_t)(a < 6 ? pr.i : pr.j) + a % 6;
   const int64_t rb = 6 * (int64_t)(b < 6 ? pr.i : pr.j) + b % 6;
-  atomicAdd(S + ra * nf + rb, v);
+  if (ra <= rb) atomicAdd(S + ra * nf + rb, v);
 }
 
 __global__ void semantic_model_kernel(const SemPair* __restrict__ pairs, int npairs,
