@@ -211,7 +211,9 @@ def main():
               "linear_solver_iterations": s.num_linear_solver_iterations,
               "initial_cost": s.initial_cost, "final_cost": s.final_cost,
               "lm_phase_ms_total": {k: ctx_lm.kernel_time(k)[0] for k in
-                                    ("reproj_jacobian", "semantic_jacobian", "schur_build", "cholesky", "pcg")}}
+                                    ("reproj_jacobian", "semantic_jacobian", "point_prepare", "fblock", "s_zero",
+                                     "schur_build", "cholesky", "cholesky_solve", "pcg", "backsub",
+                                     "trial_cost")}}
         ctx_lm.close()
 
     if rank == 0:

@@ -21,6 +21,7 @@
 
 #include "../../include/mi_ba.h"
 #include "ba_math.h"
+#include "cholesky.h"
 #include "context.h"
 #include "kernels.h"
 #include "semantic.h"
@@ -103,6 +104,14 @@ void timer_end(mi_ba_context* ctx, hipEvent_t stop) {
   if (!ctx->timing || !stop) return;
   (void)hipEventRecord(stop, ctx->stream);
 }
+
+// Scoped phase timer (HIP events on the context stream; no-op unless timing).
+struct Phase {
+  mi_ba_context* ctx;
+  hipEvent_t stop;
+  Phase(mi_ba_context* c, const char* name) : ctx(c) { timer_begin(c, name, &stop); }
+  ~Phase() { timer_end(ctx, stop); }
+};
 
 static void timer_collect(mi_ba_context* ctx) {
   if (ctx->timer.pending.empty()) return;
@@ -376,7 +385,8 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
       ctx->dense = ncfg <= 1000 && fits;
     }
     if (ctx->dense) {
-      if (ctx->S.alloc((size_t)d.nf * d.nf) || ctx->info.alloc(1)) return fail(MI_BA_ERR_OUT_OF_MEMORY);
+      if (ctx->S.alloc((size_t)d.nf * d.nf) || ctx->info.alloc(chol_leaf_count((int)d.nf)))
+        return fail(MI_BA_ERR_OUT_OF_MEMORY);
       st = build_pair_tiles(ctx);
       if (st != MI_BA_OK) return fail(st);
       if (rocblas_create_handle(&ctx->blas) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
@@ -510,7 +520,10 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   hipStream_t s = ctx->stream;
   const int64_t nf = d.nf;
   *ok = true;
-  MI_HIP(hipMemsetAsync(ctx->S.ptr, 0, ctx->S.bytes(), s));
+  {
+    Phase ph_(ctx, "s_zero");
+    MI_HIP(hipMemsetAsync(ctx->S.ptr, 0, ctx->S.bytes(), s));
+  }
   hipEvent_t stop;
   timer_begin(ctx, "schur_build", &stop);
   launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
@@ -520,21 +533,25 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   timer_end(ctx, stop);
   MI_HIP(hipMemcpyAsync(ctx->cg_x.ptr, ctx->bvec.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
   timer_begin(ctx, "cholesky", &stop);
-  // S is symmetric and stored with both triangles: row-major == column-major.
-  if (rocsolver_dpotrf(ctx->blas, rocblas_fill_lower, (rocblas_int)nf, ctx->S.ptr, (rocblas_int)nf,
-                       ctx->info.ptr) != rocblas_status_success)
+  // S holds the upper triangle row-major == the lower triangle column-major.
+  const int leaves = chol_leaf_count((int)nf);
+  if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr) != rocblas_status_success)
     return MI_BA_ERR_HIP;
   timer_end(ctx, stop);
-  int32_t info = 0;
-  MI_HIP(hipMemcpyAsync(&info, ctx->info.ptr, 4, hipMemcpyDeviceToHost, s));
+  std::vector<int32_t> info(leaves, 0);
+  MI_HIP(hipMemcpyAsync(info.data(), ctx->info.ptr, 4 * (size_t)leaves, hipMemcpyDeviceToHost, s));
   MI_HIP(hipStreamSynchronize(s));
-  if (info != 0) {
-    *ok = false;
-    return MI_BA_OK;
+  for (int32_t v : info) {
+    if (v != 0) {
+      *ok = false;
+      return MI_BA_OK;
+    }
   }
-  if (rocsolver_dpotrs(ctx->blas, rocblas_fill_lower, (rocblas_int)nf, 1, ctx->S.ptr, (rocblas_int)nf, ctx->cg_x.ptr,
-                       (rocblas_int)nf) != rocblas_status_success)
-    return MI_BA_ERR_HIP;
+  {
+    Phase ph_(ctx, "cholesky_solve");
+    if (chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr) != rocblas_status_success)
+      return MI_BA_ERR_HIP;
+  }
   return MI_BA_OK;
 }
 
@@ -574,15 +591,21 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     if (radius < 1e-32) { sum->termination_type = MI_BA_CONVERGENCE; break; }
     ++iteration;
     // Damped point inverses, Schur-Jacobi blocks, rhs.
-    launch_point_prepare(d, ctx->vpoints.ptr, ctx->npv, ctx->Vg.ptr, ctx->scale_p.ptr, ctx->diag_p.ptr,
-                         ctx->Vinv.ptr, ctx->dense ? ctx->Linv.ptr : nullptr, first, reuse_diag, radius, s);
+    {
+      Phase ph_(ctx, "point_prepare");
+      launch_point_prepare(d, ctx->vpoints.ptr, ctx->npv, ctx->Vg.ptr, ctx->scale_p.ptr, ctx->diag_p.ptr,
+                           ctx->Vinv.ptr, ctx->dense ? ctx->Linv.ptr : nullptr, first, reuse_diag, radius, s);
+    }
     MI_HIP(hipMemsetAsync(ctx->pose_blk.ptr, 0, ctx->pose_blk.bytes(), s));
     MI_HIP(hipMemsetAsync(ctx->cam_blk.ptr, 0, ctx->cam_blk.bytes(), s));
     MI_HIP(hipMemsetAsync(ctx->bvec.ptr, 0, ctx->bvec.bytes(), s));
     MI_HIP(hipMemsetAsync(ctx->udiag.ptr, 0, ctx->udiag.bytes(), s));
-    launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr,
-                  ctx->Vinv.ptr, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr, s);
-    if (ctx->sem) semantic_add_fblock(ctx);
+    {
+      Phase ph_(ctx, "fblock");
+      launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr,
+                    ctx->Vinv.ptr, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr, s);
+      if (ctx->sem) semantic_add_fblock(ctx);
+    }
     launch_fblock_finalize(d, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->udiag.ptr, ctx->scale_f.ptr,
                            ctx->diag_f.ptr, ctx->lambda_f.ptr, ctx->prec_pose.ptr, ctx->prec_cam.ptr,
                            ctx->bvec.ptr, first, reuse_diag, radius, s);
@@ -613,8 +636,11 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       continue;
     }
     // back substitution and model cost change
-    launch_backsub(d, ctx->vpoints.ptr, ctx->npv, ctx->J.ptr, ctx->Vg.ptr, ctx->Vinv.ptr, ctx->cg_x.ptr,
-                   ctx->dX.ptr, s);
+    {
+      Phase ph_(ctx, "backsub");
+      launch_backsub(d, ctx->vpoints.ptr, ctx->npv, ctx->J.ptr, ctx->Vg.ptr, ctx->Vinv.ptr, ctx->cg_x.ptr,
+                     ctx->dX.ptr, s);
+    }
     launch_model_cost(d, ctx->r.ptr, ctx->J.ptr, ctx->cg_x.ptr, ctx->dX.ptr, ctx->partial.ptr, s);
     MI_HIP(hipMemsetAsync(sc + kModelCost, 0, 8, s));
     MI_HIP(hipMemsetAsync(sc + kSemModel, 0, 8, s));
@@ -643,7 +669,10 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
                 ctx->cam_c.ptr, ctx->X_c.ptr, s);
     MI_HIP(hipMemsetAsync(sc + kCandCost, 0, 8, s));
     MI_HIP(hipMemsetAsync(sc + kSemCand, 0, 8, s));
-    launch_reproj_cost(d, ctx->qt_c.ptr, ctx->cam_c.ptr, ctx->X_c.ptr, ctx->partial.ptr, s);
+    {
+      Phase ph_(ctx, "trial_cost");
+      launch_reproj_cost(d, ctx->qt_c.ptr, ctx->cam_c.ptr, ctx->X_c.ptr, ctx->partial.ptr, s);
+    }
     if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kCandCost, s);
     if (ctx->sem) semantic_cost(ctx, ctx->qt_c.ptr, ctx->cam_c.ptr, sc + kSemCand);
     st = read_scalars(ctx, 0, kNumScalars);
