@@ -210,7 +210,7 @@ def main():
         lm = {"ba_iteration_ms": 1e3 * s.total_time_in_seconds / its, "iterations": its,
               "linear_solver_iterations": s.num_linear_solver_iterations,
               "initial_cost": s.initial_cost, "final_cost": s.final_cost,
-              "lm_phase_ms_total": {k: ctx_lm.kernel_time(k)[0] for k in
+              "lm_phase_ms_calls": {k: list(ctx_lm.kernel_time(k)) for k in
                                     ("reproj_jacobian", "semantic_jacobian", "point_prepare", "fblock", "s_zero",
                                      "schur_build", "cholesky", "cholesky_solve", "pcg", "backsub",
                                      "trial_cost")}}

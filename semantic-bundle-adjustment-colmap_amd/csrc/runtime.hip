@@ -75,6 +75,11 @@ double host_block_cost(const mi_ba_options& o, const mi_ba_problem* p, int64_t k
   return 0.5 * rho[0];
 }
 
+__global__ void identity_kernel(double* __restrict__ S, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) S[k * n + k] = 1.0;
+}
+
 mi_ba_status read_scalars(mi_ba_context* ctx, int first, int count) {
   MI_HIP(hipMemcpyAsync(ctx->host_scalars + first, ctx->scalars.ptr + first, sizeof(double) * count,
                         hipMemcpyDeviceToHost, ctx->stream));
@@ -391,6 +396,19 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
       if (st != MI_BA_OK) return fail(st);
       if (rocblas_create_handle(&ctx->blas) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
       if (rocblas_set_stream(ctx->blas, ctx->stream) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
+      // Warm the factorisation at this size once: rocBLAS / rocSOLVER load the
+      // code objects of every (shape, kernel) pair on first use, hundreds of ms
+      // that would otherwise land inside the first LM iterations.
+      const int64_t nf = d.nf;
+      if (hipMemsetAsync(ctx->S.ptr, 0, ctx->S.bytes(), ctx->stream) != hipSuccess ||
+          hipMemsetAsync(ctx->cg_x.ptr, 0, nf * 8, ctx->stream) != hipSuccess)
+        return fail(MI_BA_ERR_HIP);
+      hipLaunchKernelGGL(identity_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, ctx->stream, ctx->S.ptr,
+                         nf);
+      if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr) != rocblas_status_success ||
+          chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr) != rocblas_status_success ||
+          hipStreamSynchronize(ctx->stream) != hipSuccess)
+        return fail(MI_BA_ERR_HIP);
     }
   }
   // fixed cost of dropped blocks

@@ -279,16 +279,76 @@ struct PairConst {
   double K2[8];                       // camera of image j
   uint32_t var1, var2, mask1, mask2;  // variable poses, constant-tvec masks
   uint32_t slot, pad0, pad1, pad2;
+  // stencil tables, e = 2 m + minus over the 14 ambient parameters
+  double pert[28];                    // perturbed parameter value
+  double ood[14];                     // (1 / delta) / 2, Ceres CENTRAL
+  double A[16][9];                    // q1 points (e 0..7): R2 Q(q1')^T / |q1'|^2; q2 (e 14..21): Q(q2') / |q2'|^2
+  double pj[8][3];                    // PlusJacobian rows of q1 (0..3) and q2 (4..7)
 };
 
+// Stencil entries of one pair: one lane per stencil point (perturbed value,
+// the Ceres step 1/(2 delta) with the lane-side operation sequence of the
+// reference, the perturbed rotation map).
+__device__ inline void stencil_prep(const double* q1, const double* t1, const double* q2, const double* t2,
+                                    double rel_step, int e, PairConst* __restrict__ P) {
+  const int m = e >> 1;
+  const bool minus = e & 1;
+  const int grp = m < 4 ? 0 : (m < 7 ? 1 : (m < 11 ? 2 : 3));
+  const int k = m - (grp == 0 ? 0 : (grp == 1 ? 4 : (grp == 2 ? 7 : 11)));
+  const double orig = grp == 0 ? q1[k] : (grp == 1 ? t1[k] : (grp == 2 ? q2[k] : t2[k]));
+  const double delta = fmax(kMinStep, fabs(orig) * rel_step);
+  const double pert = minus ? orig - delta : orig + delta;
+  P->pert[e] = pert;
+  if (minus) {
+    double one_over_delta = 1.0 / delta;
+    one_over_delta /= 2;
+    P->ood[m] = one_over_delta;
+  }
+  if (grp == 1 || grp == 3) return;
+  const double* q = grp == 0 ? q1 : q2;
+  double qq[4] = {q[0], q[1], q[2], q[3]};
+  qq[k] = pert;
+  double Q[9];
+  quat_matrix_un(qq, Q);
+  const double in = 1.0 / (qq[0] * qq[0] + qq[1] * qq[1] + qq[2] * qq[2] + qq[3] * qq[3]);
+  double* A = P->A[grp == 0 ? e : e - 6];
+  if (grp == 0) {
+    double u2[4], R2[9];
+    unit_quat(q2, u2);
+    unit_quat_matrix(u2, R2);
+    for (int r = 0; r < 3; ++r)
+      for (int j = 0; j < 3; ++j)
+        A[3 * r + j] = (R2[3 * r] * Q[3 * j] + R2[3 * r + 1] * Q[3 * j + 1] + R2[3 * r + 2] * Q[3 * j + 2]) * in;
+  } else {
+    for (int c = 0; c < 9; ++c) A[c] = Q[c] * in;
+  }
+  if (minus) {
+    double PJ[12];
+    quat_plus_jacobian(q, PJ);
+    for (int c = 0; c < 3; ++c) P->pj[(grp == 0 ? 0 : 4) + k][c] = PJ[3 * k + c];
+  }
+}
+
+// Two pairs per 64-lane workgroup: lanes 0..27 of each half fill the stencil
+// tables, lane 28 the pair's base constants.
 __global__ void semantic_pair_prep_kernel(const SemPair* __restrict__ pairs, int npairs, const double* __restrict__ qt,
                                           const double* __restrict__ cam, const uint32_t* __restrict__ img_cam,
                                           const uint32_t* __restrict__ img_flags,
-                                          const uint32_t* __restrict__ raster_slot, PairConst* __restrict__ out) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= npairs) return;
+                                          const uint32_t* __restrict__ raster_slot, double rel_step,
+                                          PairConst* __restrict__ out) {
+  const int k = blockIdx.x * 2 + (threadIdx.x >> 5);
+  const int lane = threadIdx.x & 31;
+  if (k >= npairs || lane > 28) return;
   const SemPair pr = pairs[k];
-  PairConst P;
+  if (lane < 28) {
+    const double* a1 = qt + 8 * (size_t)pr.i;
+    const double* a2 = qt + 8 * (size_t)pr.j;
+    const double q1[4] = {a1[0], a1[1], a1[2], a1[3]}, t1[3] = {a1[4], a1[5], a1[6]};
+    const double q2[4] = {a2[0], a2[1], a2[2], a2[3]}, t2[3] = {a2[4], a2[5], a2[6]};
+    stencil_prep(q1, t1, q2, t2, rel_step, lane, out + k);
+    return;
+  }
+  PairConst& P = out[k];
   const double* a1 = qt + 8 * (size_t)pr.i;
   const double* a2 = qt + 8 * (size_t)pr.j;
   for (int m = 0; m < 4; ++m) { P.q1[m] = a1[m]; P.q2[m] = a2[m]; }
@@ -321,7 +381,6 @@ __global__ void semantic_pair_prep_kernel(const SemPair* __restrict__ pairs, int
   P.mask2 = (img_flags[pr.j] >> 1) & 7u;
   P.slot = raster_slot[pr.j];
   P.pad0 = P.pad1 = P.pad2 = 0;
-  out[k] = P;
 }
 
 // Per-pair record: loss-corrected J'J (packed 12x12 upper, 78) and J'r (12).
@@ -375,11 +434,15 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
                        fabs(P->t1[2]) + fabs(pw[0]) + fabs(pw[1]) + fabs(pw[2]) + fabs(P->t2[0]) +
                        fabs(P->t2[1]) + fabs(P->t2[2]);
     // Stencil: parameter m = 0..13 over (q1, t1, q2, t2), + then - (Ceres
-    // CENTRAL order).  Tangent columns accumulate in m order from 0.0
+    // CENTRAL order).  Everything that depends only on the pair and the
+    // stencil point (perturbed value, 1/(2 delta), the perturbed rotation
+    // folded into one 3x3 map, PlusJacobian rows) comes from the per-pair
+    // table as wave-uniform scalar loads; a lane forms one mat-vec per point.
+    // Tangent columns accumulate in the lane's LDS row in m order from 0.0,
     // exactly as J_tangent = J_ambient * PlusJacobian does.
-    double Jt[12];
+    const double w[3] = {smp.pc1[0] - P->t1[0], smp.pc1[1] - P->t1[1], smp.pc1[2] - P->t1[2]};
 #pragma unroll
-    for (int k = 0; k < 12; ++k) Jt[k] = 0.0;
+    for (int k = 0; k < 12; ++k) row[k] = 0.0;
     double fplus = 0.0;
 #pragma unroll 1
     for (int e = 0; e < 28; ++e) {
@@ -388,51 +451,20 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
       const int grp = m < 4 ? 0 : (m < 7 ? 1 : (m < 11 ? 2 : 3));
       if (grp < 2 ? !P->var1 : !P->var2) continue;
       const int k = m - (grp == 0 ? 0 : (grp == 1 ? 4 : (grp == 2 ? 7 : 11)));
-      double orig = 0.0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (grp == 0 && c == k) orig = P->q1[c];
-        if (grp == 2 && c == k) orig = P->q2[c];
-      }
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        if (grp == 1 && c == k) orig = P->t1[c];
-        if (grp == 3 && c == k) orig = P->t2[c];
-      }
-      const double delta = fmax(kMinStep, fabs(orig) * a.rel_step);
-      const double pert = minus ? orig - delta : orig + delta;
+      const double pert = P->pert[e];
       double pp[3];
-      if (grp == 0) {  // q1: P_w' = Q(q1')^T (P_c1 - t1) / |q1'|^2
-        double qq[4];
+      if (grp == 0 || grp == 2) {
+        // q1: P_2' = R2 Q(q1')^T (P_c1 - t1) / |q1'|^2 + t2;  q2: P_2' = Q(q2') P_w / |q2'|^2 + t2
+        const double* A = P->A[grp == 0 ? e : e - 6];
+        const double v0 = grp == 0 ? w[0] : pw[0], v1 = grp == 0 ? w[1] : pw[1], v2 = grp == 0 ? w[2] : pw[2];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) qq[c] = (c == k) ? pert : P->q1[c];
-        double Q[9];
-        quat_matrix_un(qq, Q);
-        const double in = rcp_refined(qq[0] * qq[0] + qq[1] * qq[1] + qq[2] * qq[2] + qq[3] * qq[3]);
-        const double w[3] = {smp.pc1[0] - P->t1[0], smp.pc1[1] - P->t1[1], smp.pc1[2] - P->t1[2]};
-        double wp[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) wp[c] = (Q[c] * w[0] + Q[3 + c] * w[1] + Q[6 + c] * w[2]) * in;
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          pp[c] = P->R2[3 * c] * wp[0] + P->R2[3 * c + 1] * wp[1] + P->R2[3 * c + 2] * wp[2] + P->t2[c];
+        for (int c = 0; c < 3; ++c) pp[c] = A[3 * c] * v0 + A[3 * c + 1] * v1 + A[3 * c + 2] * v2 + P->t2[c];
       } else if (grp == 1) {  // t1: P_2' = P_2 - C (t1' - t1)
-        const double dt = pert - orig;
+        const double dt = pert - P->t1[k];
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-          pp[c] = p2[c] - dt * (k == 0 ? P->C[3 * c] : (k == 1 ? P->C[3 * c + 1] : P->C[3 * c + 2]));
-      } else if (grp == 2) {  // q2: P_2' = Q(q2') P_w / |q2'|^2 + t2
-        double qq[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) qq[c] = (c == k) ? pert : P->q2[c];
-        double Q[9];
-        quat_matrix_un(qq, Q);
-        const double in = rcp_refined(qq[0] * qq[0] + qq[1] * qq[1] + qq[2] * qq[2] + qq[3] * qq[3]);
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          pp[c] = (Q[3 * c] * pw[0] + Q[3 * c + 1] * pw[1] + Q[3 * c + 2] * pw[2]) * in + P->t2[c];
+        for (int c = 0; c < 3; ++c) pp[c] = p2[c] - dt * P->C[3 * c + k];
       } else {  // t2: P_2' = P_2 + (t2' - t2)
-        const double dt = pert - orig;
+        const double dt = pert - P->t2[k];
 #pragma unroll
         for (int c = 0; c < 3; ++c) pp[c] = p2[c] + (c == k ? dt : 0.0);
       }
@@ -457,34 +489,20 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
         fplus = f;
         continue;
       }
-      double one_over_delta = 1.0 / delta;
-      one_over_delta /= 2;
-      const double jm = (fplus - f) * one_over_delta;
+      const double jm = (fplus - f) * P->ood[m];
       if (grp == 0 || grp == 2) {
-        const double x0 = grp == 0 ? P->q1[0] : P->q2[0], x1 = grp == 0 ? P->q1[1] : P->q2[1];
-        const double x2 = grp == 0 ? P->q1[2] : P->q2[2], x3 = grp == 0 ? P->q1[3] : P->q2[3];
+        double* jr = row + (grp == 0 ? 0 : 6);
+        const double* pj = P->pj[(grp == 0 ? 0 : 4) + k];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          // QuaternionManifold PlusJacobian row k, column c (quat_plus_jacobian)
-          double pjc;
-          if (k == 0) pjc = c == 0 ? -x1 : (c == 1 ? -x2 : -x3);
-          else if (k == 1) pjc = c == 0 ? x0 : (c == 1 ? x3 : -x2);
-          else if (k == 2) pjc = c == 0 ? -x3 : (c == 1 ? x0 : x1);
-          else pjc = c == 0 ? x2 : (c == 1 ? -x1 : x0);
-          const double v = (grp == 0 ? Jt[c] : Jt[6 + c]) + jm * pjc;
-          if (grp == 0) Jt[c] = v; else Jt[6 + c] = v;
-        }
+        for (int c = 0; c < 3; ++c) jr[c] = jr[c] + jm * pj[c];
       } else {
         const uint32_t mask = grp == 1 ? P->mask1 : P->mask2;
-        const double v = ((mask >> k) & 1u) ? 0.0 : jm;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          if (c == k) {
-            if (grp == 1) Jt[3 + c] = v; else Jt[9 + c] = v;
-          }
-        }
+        row[(grp == 1 ? 3 : 9) + k] = ((mask >> k) & 1u) ? 0.0 : jm;
       }
     }
+    double Jt[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) Jt[k] = row[k];
     if (write_samples) {
       r_out[n] = r;
       status_out[n] = st;
@@ -823,8 +841,8 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   PairConst* pcs = reinterpret_cast<PairConst*>(S->pconst.ptr);
   hipEvent_t stop;
   timer_begin(ctx, "semantic_jacobian", &stop);
-  hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 63) / 64), dim3(64), 0, s, S->pairs.ptr, S->npairs,
-                     a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, pcs);
+  hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 1) / 2), dim3(64), 0, s, S->pairs.ptr, S->npairs,
+                     a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs);
   dispatch_model(ctx->dev.model, [&](auto m) {
     constexpr int M = decltype(m)::value;
     hipLaunchKernelGGL(semantic_linearize_kernel<M>, dim3(S->ntiles), dim3(kBlock), 0, s, a, S->tiles.ptr, pcs,
