@@ -8,10 +8,10 @@ sample (residual + 29-point CENTRAL numeric-diff Jacobian, pair blocks
 reduced) — mi_ba_linearize on the context's stream.
 
 value = (reprojection blocks + semantic samples, all ranks) * steps / max-over-
-ranks wall time of the timed steps.  Multi-GPU: points (and image pairs) are
-sharded in contiguous ranges across ranks; the linearization has no
-data-path collective, so the timed region needs none (strong scaling of the
-fixed C5 problem).
+ranks wall time of the timed steps.  Multi-GPU: the linearization shards by
+point blocks (with all their observations) and image pairs and has no
+data-path collective, so the timed region needs none.  Default --scaling weak:
+every rank owns a C4-sized shard; --scaling strong splits the one C5 problem.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C4]
 """
@@ -66,11 +66,17 @@ def bytes_per_block(model, track):
     return 24 + 24.0 / track + 16 + 16 * (9 + CAM_TANGENT[model])
 
 
-def build_shard(cfg, rank, world):
-    """Generate the scene (deterministic, seed 0) and keep this rank's shard."""
+def build_shard(cfg, rank, world, scaling="weak"):
+    """This rank's shard.  weak: every rank owns a full config-sized block of
+    points (synthetic scene seeded with the rank; the per-GPU work is fixed as
+    ranks are added).  strong: one scene (seed 0) whose points, with all their
+    observations, and image pairs are split into contiguous rank ranges."""
+    weak = scaling == "weak"
     c = mi_ba.synth_config(cfg["model"], cfg["images"], cfg["points"], track_length=cfg["track"],
-                           rotation_range=0.05, extra=cfg["extra"])
+                           rotation_range=0.05, extra=cfg["extra"], seed=rank if weak else 0)
     full = mi_ba.generate_scene(c).gauge()
+    if weak:
+        rank, world = 0, 1
     P = full.num_points
     p0, p1 = P * rank // world, P * (rank + 1) // world
     m = (full.obs_point >= p0) & (full.obs_point < p1)
@@ -128,17 +134,22 @@ def main():
     ap.add_argument("--config", default="C4", choices=sorted(CONFIGS))
     ap.add_argument("--lm-iters", type=int, default=3, help="LM iterations for the BA-iteration wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: a config-sized shard per rank (default); strong: the config split across ranks")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    ap_backend = os.environ.get("MI_BA_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm; gloo for 1-GPU rehearsals
     dist = None
+    device = local_rank
     if world > 1:
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
+        device = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        tdist.init_process_group(ap_backend)
         dist = tdist
 
     def barrier():
@@ -149,7 +160,7 @@ def main():
         if dist is None:
             return v
         import torch
-        t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{device}" if ap_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -157,14 +168,14 @@ def main():
         if dist is None:
             return v
         import torch
-        t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{device}" if ap_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
     cfg = CONFIGS[args.config]
     t_setup = time.time()
-    sc, sem = build_shard(cfg, rank, world)
-    opts = mi_ba.default_options(device=local_rank)
+    sc, sem = build_shard(cfg, rank, world, args.scaling)
+    opts = mi_ba.default_options(device=device)
     ctx = mi_ba.Context(opts, sc, sem)
     nb, W, ns = ctx.dims()
     setup_s = time.time() - t_setup
@@ -201,9 +212,9 @@ def main():
             wd, wl = mi_ba.render_semantic(wsc, 64, 64, cell=0.5)
             wsem = mi_ba.SemanticInput(wd, wl, np.array([(i, (i + 1) % 30) for i in range(30)], np.int32),
                                        pixel_step=8)
-        with mi_ba.Context(mi_ba.default_options(device=local_rank, max_num_iterations=2), wsc, wsem) as wctx:
+        with mi_ba.Context(mi_ba.default_options(device=device, max_num_iterations=2), wsc, wsem) as wctx:
             wctx.solve()
-        ctx_lm = mi_ba.Context(mi_ba.default_options(device=local_rank, max_num_iterations=args.lm_iters), sc, sem)
+        ctx_lm = mi_ba.Context(mi_ba.default_options(device=device, max_num_iterations=args.lm_iters), sc, sem)
         ctx_lm.set_timing(True)
         s = ctx_lm.solve()
         its = max(1, s.num_successful_steps + s.num_unsuccessful_steps)
@@ -230,15 +241,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * dt / args.steps,
             "higher_is_better": True,
-            "scaling": "strong" if world > 1 else "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (GenerateReconstruction restated, seed 0; rendered labelled plane)",
-            "config": {"workload": f"{args.config}: {cfg['desc']}", "cameras": cfg["images"],
+            "data": "synthetic (GenerateReconstruction restated, seed = rank for weak shards, 0 otherwise; rendered labelled plane)",
+            "config": {"workload": (f"{args.config}: {cfg['desc']}" if world == 1 else
+                                    f"{args.config} x{world} ({args.scaling} scaling): {cfg['desc']}"
+                                    + (" per rank" if args.scaling == "weak" else " split across ranks")),
+                       "cameras": cfg["images"],
                        "points": cfg["points"], "observations": cfg["points"] * cfg["track"],
                        "reprojection_blocks_rank0": nb, "semantic_samples_rank0": ns,
                        "camera_model": [k for k, v in mi_ba.MODEL_NAMES.items() if v == cfg["model"]][0],
-                       "parallelism": f"point-sharded x{world}"},
+                       "parallelism": f"point-sharded x{world}", "scaling": args.scaling},
             "roofline": {"kernel": "reproj_jacobian", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic_src,

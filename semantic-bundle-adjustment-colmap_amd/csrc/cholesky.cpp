@@ -3,6 +3,8 @@
 
 #include <rocsolver/rocsolver.h>
 
+#include <algorithm>
+
 namespace miba {
 
 namespace {
@@ -63,12 +65,49 @@ rocblas_status backward(rocblas_handle h, int n, const double* A, int lda, doubl
   return backward(h, n1, A, lda, x);
 }
 
+// Right-looking blocked factorisation: per panel, dpotrf of the diagonal
+// block, dtrsm of the panel below it, then the trailing lower triangle
+// updated by dsyrk (or by dgemm per block column of width `panel`).
+rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg) {
+  const double one = 1.0, minus_one = -1.0;
+  const int nb = cfg.panel;
+  for (int k = 0; k < n; k += nb) {
+    const int kb = std::min(nb, n - k);
+    double* Akk = A + k + (size_t)k * lda;
+    rocblas_status st = rocsolver_dpotrf(h, rocblas_fill_lower, kb, Akk, lda, info++);
+    if (st != rocblas_status_success) return st;
+    const int m = n - k - kb;
+    if (m == 0) break;
+    double* Aik = Akk + kb;  // panel below the diagonal block
+    st = rocblas_dtrsm(h, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                       rocblas_diagonal_non_unit, m, kb, &one, Akk, lda, Aik, lda);
+    if (st != rocblas_status_success) return st;
+    double* T = Aik + (size_t)kb * lda;  // trailing matrix, lower triangle
+    if (!cfg.gemm_update) {
+      st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, m, kb, &minus_one, Aik, lda, &one, T, lda);
+      if (st != rocblas_status_success) return st;
+    } else {
+      for (int j = 0; j < m; j += nb) {
+        const int jb = std::min(nb, m - j);
+        st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m - j, jb, kb, &minus_one, Aik + j,
+                           lda, Aik + j, lda, &one, T + j + (size_t)j * lda, lda);
+        if (st != rocblas_status_success) return st;
+      }
+    }
+  }
+  return rocblas_status_success;
+}
+
 }  // namespace
 
-int chol_leaf_count(int n) { return n <= 0 ? 1 : leaves(n); }
+int chol_leaf_count(int n, const CholConfig& cfg) {
+  if (n <= 0) return 1;
+  return cfg.panel > 0 ? (n + cfg.panel - 1) / cfg.panel : leaves(n);
+}
 
-rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info) {
+rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg) {
   if (n <= 0) return rocblas_status_success;
+  if (cfg.panel > 0) return factor_blocked(h, n, A, lda, info, cfg);
   return factor(h, n, A, lda, info);
 }
 

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/mi_ba.h"
+#include "cholesky.h"
 #include "device.h"
 #include "setup.h"
 
@@ -93,6 +94,7 @@ struct mi_ba_context {
   miba::DevArray<uint2> pairs;             // (a, b) block pairs bucketed by image pair
   int nptiles = 0;
   miba::DevArray<int32_t> info;
+  miba::CholConfig chol;                   // factorisation variant (mi_ba_set_tuning)
 
   double fixed_cost = 0.0;
   miba::SemanticState* sem = nullptr;

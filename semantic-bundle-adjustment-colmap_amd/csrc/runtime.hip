@@ -390,7 +390,8 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
       ctx->dense = ncfg <= 1000 && fits;
     }
     if (ctx->dense) {
-      if (ctx->S.alloc((size_t)d.nf * d.nf) || ctx->info.alloc(chol_leaf_count((int)d.nf)))
+      if (ctx->S.alloc((size_t)d.nf * d.nf) ||
+          ctx->info.alloc(std::max<int64_t>(chol_leaf_count((int)d.nf), d.nf / 64 + 1)))
         return fail(MI_BA_ERR_OUT_OF_MEMORY);
       st = build_pair_tiles(ctx);
       if (st != MI_BA_OK) return fail(st);
@@ -405,7 +406,7 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
         return fail(MI_BA_ERR_HIP);
       hipLaunchKernelGGL(identity_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, ctx->stream, ctx->S.ptr,
                          nf);
-      if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr) != rocblas_status_success ||
+      if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr, ctx->chol) != rocblas_status_success ||
           chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr) != rocblas_status_success ||
           hipStreamSynchronize(ctx->stream) != hipSuccess)
         return fail(MI_BA_ERR_HIP);
@@ -552,8 +553,8 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   MI_HIP(hipMemcpyAsync(ctx->cg_x.ptr, ctx->bvec.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
   timer_begin(ctx, "cholesky", &stop);
   // S holds the upper triangle row-major == the lower triangle column-major.
-  const int leaves = chol_leaf_count((int)nf);
-  if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr) != rocblas_status_success)
+  const int leaves = chol_leaf_count((int)nf, ctx->chol);
+  if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr, ctx->chol) != rocblas_status_success)
     return MI_BA_ERR_HIP;
   timer_end(ctx, stop);
   std::vector<int32_t> info(leaves, 0);
@@ -977,6 +978,14 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   if (!ctx || !key) return MI_BA_ERR_INVALID_ARGUMENT;
   if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 31) {
     ctx->dev.jvariant = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_panel") == 0 && (value == 0 || (value >= 64 && value <= 4096))) {
+    ctx->chol.panel = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_gemm_update") == 0 && (value == 0 || value == 1)) {
+    ctx->chol.gemm_update = value != 0;
     return MI_BA_OK;
   }
   return MI_BA_ERR_INVALID_ARGUMENT;
