@@ -253,6 +253,30 @@ mi_ba_status mi_ba_context_writeback(mi_ba_context* ctx);
 /* Total cost 0.5*sum(rho) at the current parameters (geometric + semantic). */
 mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost);
 
+/* --- multi-GPU LM (one process per GPU) ---------------------------------
+ * Replaces the single-process Ceres solve with a point-sharded one (SURVEY
+ * 8e): each rank creates its context from its own shard — all cameras and
+ * images, the observations of its own points (point-major ranges) and its
+ * own semantic image pairs — and joins a communicator before
+ * mi_ba_context_solve.  Per LM iteration the camera-side normal-equation
+ * blocks, the explicit reduced camera system S and the cost scalars are
+ * summed over ranks; every rank then factors the same S and back-substitutes
+ * its own points.  Exact (dense Schur) solver only.
+ *
+ * mi_ba_comm_unique_id: RCCL unique id (ncclGetUniqueId) to be created on
+ * rank 0 and broadcast by the caller (e.g. torch.distributed). */
+#define MI_BA_COMM_ID_BYTES 128
+mi_ba_status mi_ba_comm_unique_id(char id[MI_BA_COMM_ID_BYTES]);
+/* Join rank `rank` of `world` over RCCL (xGMI on one node). */
+mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t world,
+                                    const char id[MI_BA_COMM_ID_BYTES]);
+/* Alternative reducer for hosts without one GPU per rank: sums `n` doubles of
+ * a host buffer in place across ranks (returns 0 on success).  Used by the
+ * 1-GPU multi-rank rehearsal (gloo). */
+typedef int32_t (*mi_ba_host_allreduce_fn)(double* data, int64_t n, void* user);
+mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, int32_t world,
+                                            mi_ba_host_allreduce_fn fn, void* user);
+
 /* Kernel-variant switches for in-process A/B measurement (key, value);
  * unknown keys return MI_BA_ERR_INVALID_ARGUMENT. */
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value);

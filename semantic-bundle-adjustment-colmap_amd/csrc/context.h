@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
+#include <rccl/rccl.h>
 
 #include <map>
 #include <string>
@@ -102,6 +103,13 @@ struct mi_ba_context {
   bool timing = false;
   miba::KernelTimer timer;
   bool solved = false;
+
+  // multi-rank LM (mi_ba_context_set_comm / _set_host_reducer)
+  int rank = 0, world = 1;
+  ncclComm_t comm = nullptr;
+  mi_ba_host_allreduce_fn host_reduce = nullptr;
+  void* host_reduce_user = nullptr;
+  std::vector<double> reduce_buf;
 };
 
 namespace miba {

@@ -89,6 +89,25 @@ mi_ba_status read_scalars(mi_ba_context* ctx, int first, int count) {
 
 }  // namespace
 
+// Sum n doubles of a device buffer over the ranks of a multi-rank solve (RCCL
+// all-reduce on the context stream, or the host reducer); no-op on one rank.
+mi_ba_status allreduce(mi_ba_context* ctx, double* d, int64_t n) {
+  if (ctx->world <= 1 || n <= 0) return MI_BA_OK;
+  if (ctx->comm) {
+    if (ncclAllReduce(d, d, (size_t)n, ncclDouble, ncclSum, ctx->comm, ctx->stream) != ncclSuccess)
+      return MI_BA_ERR_HIP;
+    return MI_BA_OK;
+  }
+  if (!ctx->host_reduce) return MI_BA_ERR_STATE;
+  ctx->reduce_buf.resize(n);
+  MI_HIP(hipMemcpyAsync(ctx->reduce_buf.data(), d, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  MI_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->host_reduce(ctx->reduce_buf.data(), n, ctx->host_reduce_user) != 0) return MI_BA_ERR_HIP;
+  MI_HIP(hipMemcpyAsync(d, ctx->reduce_buf.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
+  MI_HIP(hipStreamSynchronize(ctx->stream));
+  return MI_BA_OK;
+}
+
 void timer_begin(mi_ba_context* ctx, const char* name, hipEvent_t* stop_out) {
   *stop_out = nullptr;
   if (!ctx->timing) return;
@@ -435,6 +454,7 @@ void context_destroy(mi_ba_context* ctx) {
   }
   for (auto e : ctx->timer.pool) (void)hipEventDestroy(e);
   if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas);
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   if (ctx->host_scalars) (void)hipHostFree(ctx->host_scalars);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -457,6 +477,11 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     if (st != MI_BA_OK) return st;
   }
   MI_HIP(hipGetLastError());
+  if (ctx->world > 1 && cost_out) {
+    mi_ba_status st = allreduce(ctx, ctx->scalars.ptr + kCost, 1);
+    if (st == MI_BA_OK) st = allreduce(ctx, ctx->scalars.ptr + kSemCost, 1);
+    if (st != MI_BA_OK) return st;
+  }
   if (cost_out) {
     mi_ba_status st = read_scalars(ctx, 0, kNumScalars);
     if (st != MI_BA_OK) return st;
@@ -548,6 +573,14 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
                      ctx->ptiles.ptr, ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, s);
   if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
+  timer_end(ctx, stop);
+  if (ctx->world > 1) {
+    // every rank holds the Schur contribution of its own points
+    Phase ph_(ctx, "s_allreduce");
+    mi_ba_status st = allreduce(ctx, ctx->S.ptr, nf * nf);
+    if (st != MI_BA_OK) return st;
+  }
+  timer_begin(ctx, "schur_build", &stop);
   launch_dense_finalize(d, ctx->lambda_f.ptr, ctx->S.ptr, s);
   timer_end(ctx, stop);
   MI_HIP(hipMemcpyAsync(ctx->cg_x.ptr, ctx->bvec.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
@@ -590,7 +623,8 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
   sum->num_effective_parameters_reduced = ctx->setup.num_effective_parameters_reduced;
   sum->num_semantic_residuals = ctx->sem ? ctx->sem->ns : 0;
   sum->fixed_cost = ctx->fixed_cost;
-  if (sum->num_residuals_reduced == 0) return MI_BA_ERR_NO_RESIDUALS;
+  if (ctx->world > 1 && !ctx->dense) return MI_BA_ERR_UNSUPPORTED;  // multi-rank: exact Schur solver only
+  if (sum->num_residuals_reduced == 0 && ctx->world == 1) return MI_BA_ERR_NO_RESIDUALS;
   double tj = now_s();
   double x_cost = 0.0;
   mi_ba_status st = context_linearize(ctx, &x_cost);
@@ -624,6 +658,14 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr,
                     ctx->Vinv.ptr, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr, s);
       if (ctx->sem) semantic_add_fblock(ctx);
+    }
+    if (ctx->world > 1) {
+      Phase ph_(ctx, "f_allreduce");
+      st = allreduce(ctx, ctx->pose_blk.ptr, (int64_t)ctx->pose_blk.n);
+      if (st == MI_BA_OK) st = allreduce(ctx, ctx->cam_blk.ptr, (int64_t)ctx->cam_blk.n);
+      if (st == MI_BA_OK) st = allreduce(ctx, ctx->bvec.ptr, (int64_t)ctx->bvec.n);
+      if (st == MI_BA_OK) st = allreduce(ctx, ctx->udiag.ptr, (int64_t)ctx->udiag.n);
+      if (st != MI_BA_OK) return st;
     }
     launch_fblock_finalize(d, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->udiag.ptr, ctx->scale_f.ptr,
                            ctx->diag_f.ptr, ctx->lambda_f.ptr, ctx->prec_pose.ptr, ctx->prec_cam.ptr,
@@ -665,7 +707,14 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     MI_HIP(hipMemsetAsync(sc + kSemModel, 0, 8, s));
     if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kModelCost, s);
     if (ctx->sem) semantic_model_cost(ctx, ctx->cg_x.ptr, sc + kSemModel);
-    launch_sqnorm2(ctx->cg_x.ptr, nf, ctx->dX.ptr, 3 * d.num_points, sc + kStepNorm, s);
+    // camera step counted once (rank 0), point steps on their own ranks
+    launch_sqnorm2(ctx->cg_x.ptr, ctx->rank == 0 ? nf : 0, ctx->dX.ptr, 3 * d.num_points, sc + kStepNorm, s);
+    if (ctx->world > 1) {
+      st = allreduce(ctx, sc + kModelCost, 1);
+      if (st == MI_BA_OK) st = allreduce(ctx, sc + kSemModel, 1);
+      if (st == MI_BA_OK) st = allreduce(ctx, sc + kStepNorm, 1);
+      if (st != MI_BA_OK) return st;
+    }
     st = read_scalars(ctx, 0, kNumScalars);
     if (st != MI_BA_OK) return st;
     const double model_cost_change = hs[kModelCost] + hs[kSemModel];
@@ -694,6 +743,11 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     }
     if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kCandCost, s);
     if (ctx->sem) semantic_cost(ctx, ctx->qt_c.ptr, ctx->cam_c.ptr, sc + kSemCand);
+    if (ctx->world > 1) {
+      st = allreduce(ctx, sc + kCandCost, 1);
+      if (st == MI_BA_OK) st = allreduce(ctx, sc + kSemCand, 1);
+      if (st != MI_BA_OK) return st;
+    }
     st = read_scalars(ctx, 0, kNumScalars);
     if (st != MI_BA_OK) return st;
     const double candidate_cost = hs[kCandCost] + hs[kSemCand];
@@ -704,7 +758,10 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     // before accepting the candidate (x stays at the current point).
     double x_norm = 0.0;
     if (o.parameter_tolerance > 0.0) {
-      launch_sqnorm2(ctx->qt.ptr, 8 * (int64_t)d.num_images, ctx->X.ptr, 3 * d.num_points, sc + kStepNorm, s);
+      launch_sqnorm2(ctx->qt.ptr, ctx->rank == 0 ? 8 * (int64_t)d.num_images : 0, ctx->X.ptr, 3 * d.num_points,
+                     sc + kStepNorm, s);
+      st = allreduce(ctx, sc + kStepNorm, 1);
+      if (st != MI_BA_OK) return st;
       st = read_scalars(ctx, kStepNorm, 1);
       if (st != MI_BA_OK) return st;
       x_norm = std::sqrt(hs[kStepNorm]);
@@ -968,10 +1025,61 @@ mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost) {
   launch_reproj_cost(ctx->dev, ctx->qt.ptr, ctx->cam.ptr, ctx->X.ptr, ctx->partial.ptr, s);
   if (ctx->dev.nb) launch_sum(ctx->partial.ptr, reproj_grid(ctx->dev.nb), sc + kCandCost, s);
   if (ctx->sem) semantic_cost(ctx, ctx->qt.ptr, ctx->cam.ptr, sc + kSemCand);
-  mi_ba_status st = read_scalars(ctx, 0, kNumScalars);
+  mi_ba_status st = allreduce(ctx, sc + kCandCost, 1);
+  if (st == MI_BA_OK) st = allreduce(ctx, sc + kSemCand, 1);
+  if (st != MI_BA_OK) return st;
+  st = read_scalars(ctx, 0, kNumScalars);
   if (st != MI_BA_OK) return st;
   *cost = ctx->host_scalars[kCandCost] + ctx->host_scalars[kSemCand] + ctx->fixed_cost;
   return MI_BA_OK;
+}
+
+// Fixed cost of the dropped all-constant blocks, summed over the ranks' shards.
+static mi_ba_status reduce_fixed_cost(mi_ba_context* ctx) {
+  double* slot = ctx->scalars.ptr + kXR;
+  MI_HIP(hipMemcpyAsync(slot, &ctx->fixed_cost, 8, hipMemcpyHostToDevice, ctx->stream));
+  mi_ba_status st = allreduce(ctx, slot, 1);
+  if (st != MI_BA_OK) return st;
+  MI_HIP(hipMemcpyAsync(&ctx->fixed_cost, slot, 8, hipMemcpyDeviceToHost, ctx->stream));
+  MI_HIP(hipStreamSynchronize(ctx->stream));
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_comm_unique_id(char id[MI_BA_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) <= MI_BA_COMM_ID_BYTES, "RCCL unique id size");
+  if (!id) return MI_BA_ERR_INVALID_ARGUMENT;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return MI_BA_ERR_HIP;
+  std::memset(id, 0, MI_BA_COMM_ID_BYTES);
+  std::memcpy(id, &u, sizeof(u));
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t world,
+                                    const char id[MI_BA_COMM_ID_BYTES]) {
+  if (!ctx || !id || world < 1 || rank < 0 || rank >= world) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (ctx->comm || ctx->host_reduce || ctx->solved) return MI_BA_ERR_STATE;
+  MI_HIP(hipSetDevice(ctx->device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  if (ncclCommInitRank(&ctx->comm, world, u, rank) != ncclSuccess) {
+    ctx->comm = nullptr;
+    return MI_BA_ERR_HIP;
+  }
+  ctx->rank = rank;
+  ctx->world = world;
+  return reduce_fixed_cost(ctx);
+}
+
+mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, int32_t world,
+                                            mi_ba_host_allreduce_fn fn, void* user) {
+  if (!ctx || !fn || world < 1 || rank < 0 || rank >= world) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (ctx->comm || ctx->host_reduce || ctx->solved) return MI_BA_ERR_STATE;
+  ctx->host_reduce = fn;
+  ctx->host_reduce_user = user;
+  ctx->rank = rank;
+  ctx->world = world;
+  return reduce_fixed_cost(ctx);
 }
 
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value) {

@@ -151,6 +151,9 @@ def _ptr(a, t):
 
 _lib = None
 _synth = None
+# mi_ba_host_allreduce_fn: int32 (double* data, int64 n, void* user)
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int32, _dp, C.c_int64, C.c_void_p)
+COMM_ID_BYTES = 128
 
 
 def load(path: str = LIB_PATH):
@@ -187,6 +190,9 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_set_timing.argtypes = [C.c_void_p, C.c_int32]
     lib.mi_ba_set_tuning.argtypes = [C.c_void_p, C.c_char_p, C.c_int32]
     lib.mi_ba_kernel_time.argtypes = [C.c_void_p, C.c_char_p, _dp, _i64p]
+    lib.mi_ba_comm_unique_id.argtypes = [C.c_char_p]
+    lib.mi_ba_context_set_comm.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
+    lib.mi_ba_context_set_host_reducer.argtypes = [C.c_void_p, C.c_int32, C.c_int32, HOST_ALLREDUCE_FN, C.c_void_p]
     _lib = lib
     return lib
 
@@ -339,6 +345,30 @@ class SemanticInput:
         return s
 
 
+def comm_unique_id() -> bytes:
+    """RCCL unique id for mi_ba_context_set_comm (create on rank 0, broadcast)."""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    check(load().mi_ba_comm_unique_id(buf), "mi_ba_comm_unique_id")
+    return buf.raw
+
+
+def shard_scene(scene: "Scene", rank: int, world: int, semantic: Optional["SemanticInput"] = None):
+    """Rank `rank`'s shard for the multi-rank LM: every camera and image, the
+    observations of the points in the rank's contiguous point range, and the
+    rank's contiguous range of semantic image pairs."""
+    P = scene.num_points
+    p0, p1 = P * rank // world, P * (rank + 1) // world
+    m = (scene.obs_point >= p0) & (scene.obs_point < p1)
+    sh = scene.copy()
+    sh.obs_xy, sh.obs_image, sh.obs_point = scene.obs_xy[m].copy(), scene.obs_image[m].copy(), scene.obs_point[m].copy()
+    sem = None
+    if semantic is not None:
+        K = len(semantic.pairs)
+        sem = SemanticInput(semantic.depth, semantic.label, np.asarray(semantic.pairs)[K * rank // world:K * (rank + 1) // world],
+                            semantic.pixel_step, semantic.depth_error_threshold, semantic.numeric_relative_step_size)
+    return sh, sem
+
+
 def device_count() -> int:
     n = C.c_int32(0)
     load().mi_ba_device_count(C.byref(n))
@@ -456,6 +486,25 @@ class Context:
 
     def reset_kernel_times(self):
         check(self.lib.mi_ba_reset_kernel_times(self.h), "reset")
+
+    # multi-rank LM ------------------------------------------------------
+    def set_comm(self, rank: int, world: int, unique_id: bytes):
+        """Join an RCCL communicator (one process per GPU)."""
+        check(self.lib.mi_ba_context_set_comm(self.h, rank, world, bytes(unique_id).ljust(COMM_ID_BYTES, b"\0")),
+              "mi_ba_context_set_comm")
+
+    def set_host_reducer(self, rank: int, world: int, reduce_inplace):
+        """Join a multi-rank solve whose sums go through `reduce_inplace(np.ndarray)`
+        (e.g. a torch.distributed gloo all-reduce); for ranks sharing a GPU."""
+        def _cb(ptr, n, _user):
+            try:
+                reduce_inplace(np.ctypeslib.as_array(ptr, shape=(n,)))
+                return 0
+            except Exception:  # noqa: BLE001 — reported to the library as a failed reduction
+                return 1
+        self._reducer = HOST_ALLREDUCE_FN(_cb)  # keep the thunk alive
+        check(self.lib.mi_ba_context_set_host_reducer(self.h, rank, world, self._reducer, None),
+              "mi_ba_context_set_host_reducer")
 
 
 # ---------------------------------------------------------------------------

@@ -1,0 +1,103 @@
+"""Multi-rank LM (point-sharded).
+
+CPU (gloo, world 2): the shard partition and the host reducer.
+GPU: two ranks on the one visible MI355X, sums through gloo
+(mi_ba_context_set_host_reducer), against the single-process solve of the
+same scene — final cost within 1e-6 relative (north-star tolerance; the two
+runs sum in different orders), cameras/poses bitwise equal across ranks,
+points within 1e-5.  The RCCL path (mi_ba_context_set_comm) needs one GPU per
+rank and runs on multi-GPU nodes only.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import multirank_cases as mc  # noqa: E402
+
+mi_ba = mc.mi_ba
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gloo_sum_worker(rank, world, port, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    a = np.arange(5, dtype=np.float64) * (rank + 1)
+    mc.gloo_reducer()(a)
+    q.put((rank, a.tolist()))
+    dist.destroy_process_group()
+
+
+def test_gloo_host_reducer_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gloo_sum_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(2):
+        assert out[r] == (np.arange(5) * 3.0).tolist()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_partition(world):
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 5, 101, track_length=3))
+    depth = np.zeros((5, 8, 8), np.float32)
+    sem = mi_ba.SemanticInput(depth, depth, np.array([(i, (i + 1) % 5) for i in range(5)], np.int32))
+    seen = np.zeros(sc.num_obs, np.int64)
+    pairs = []
+    for r in range(world):
+        sh, ss = mi_ba.shard_scene(sc, r, world, sem)
+        assert sh.num_images == sc.num_images and np.array_equal(sh.camera_params, sc.camera_params)
+        P = sc.num_points
+        assert np.all((sh.obs_point >= P * r // world) & (sh.obs_point < P * (r + 1) // world))
+        key = {(int(p), int(i)): k for k, (p, i) in enumerate(zip(sc.obs_point, sc.obs_image))}
+        for p, i in zip(sh.obs_point, sh.obs_image):
+            seen[key[(int(p), int(i))]] += 1
+        pairs += [tuple(x) for x in ss.pairs]
+    assert np.all(seen == 1)
+    assert sorted(pairs) == sorted(tuple(x) for x in sem.pairs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["geo", "sem"])
+def test_two_rank_solve_matches_single(gpu, case, tmp_path):
+    world = 2
+    port = _free_port()
+    outs = [tmp_path / f"r{r}.json" for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "multirank_worker.py"), "--rank", str(r),
+                               "--world", str(world), "--port", str(port), "--case", case, "--out", str(outs[r])])
+             for r in range(world)]
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    res = [json.load(open(o)) for o in outs]
+    sc, sem, opts = mc.make_case(case)
+    full = sc.copy()
+    s1 = mi_ba.solve(opts, full, sem)
+    for r in res:
+        assert abs(r["initial_cost"] - s1.initial_cost) <= 1e-12 * s1.initial_cost
+        assert abs(r["final_cost"] - s1.final_cost) <= 1e-6 * s1.final_cost, (r["final_cost"], s1.final_cost)
+    # every rank factors the same summed system: identical camera-side results
+    for key in ("qvec", "tvec", "camera_params"):
+        assert res[0][key] == res[1][key]
+    dq = np.abs(np.array(res[0]["qvec"]) - full.qvec).max()
+    assert dq <= 1e-6, dq
+    for r in res:
+        p0, p1 = r["points"]
+        dx = np.abs(np.array(r["xyz"]).reshape(-1, 3) - full.xyz[p0:p1]).max() if p1 > p0 else 0.0
+        assert dx <= 1e-5, dx
