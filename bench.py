@@ -214,15 +214,32 @@ def main():
                                        pixel_step=8)
         with mi_ba.Context(mi_ba.default_options(device=device, max_num_iterations=2), wsc, wsem) as wctx:
             wctx.solve()
-        ctx_lm = mi_ba.Context(mi_ba.default_options(device=device, max_num_iterations=args.lm_iters), sc, sem)
+        lm_sc, lm_sem = sc, sem
+        if world > 1:
+            # C5: the one C4 problem point-sharded across the ranks, reduced camera
+            # system summed over RCCL (xGMI) every LM iteration
+            lm_sc, lm_sem = build_shard(cfg, rank, world, "strong")
+        ctx_lm = mi_ba.Context(mi_ba.default_options(device=device, max_num_iterations=args.lm_iters), lm_sc, lm_sem)
+        if world > 1:
+            if ap_backend == "nccl":
+                obj = [mi_ba.comm_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0)
+                ctx_lm.set_comm(rank, world, obj[0])
+            else:
+                sys.path.insert(0, os.path.join(ROOT, "tests"))
+                import multirank_cases
+                ctx_lm.set_host_reducer(rank, world, multirank_cases.gloo_reducer())
         ctx_lm.set_timing(True)
+        barrier()
         s = ctx_lm.solve()
         its = max(1, s.num_successful_steps + s.num_unsuccessful_steps)
-        lm = {"ba_iteration_ms": 1e3 * s.total_time_in_seconds / its, "iterations": its,
+        lm = {"ba_iteration_ms": allreduce_max(1e3 * s.total_time_in_seconds / its), "iterations": its,
+              "ba_iteration_workload": ((f"C5: {args.config} point-sharded across {world} ranks, S summed by " + ("RCCL all-reduce" if ap_backend == "nccl" else "gloo host reducer")) if world > 1
+                                        else f"{args.config} on one GPU"),
               "linear_solver_iterations": s.num_linear_solver_iterations,
               "initial_cost": s.initial_cost, "final_cost": s.final_cost,
               "lm_phase_ms_calls": {k: list(ctx_lm.kernel_time(k)) for k in
-                                    ("reproj_jacobian", "semantic_jacobian", "point_prepare", "fblock", "s_zero",
+                                    ("reproj_jacobian", "semantic_jacobian", "point_prepare", "fblock", "f_allreduce", "s_zero", "s_allreduce",
                                      "schur_build", "cholesky", "cholesky_solve", "pcg", "backsub",
                                      "trial_cost")}}
         ctx_lm.close()
