@@ -1,6 +1,7 @@
 // cholesky.cpp — recursive blocked Cholesky over rocBLAS/rocSOLVER (see cholesky.h).
 #include "cholesky.h"
 
+#include <hip/hip_runtime.h>
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
@@ -8,6 +9,153 @@
 namespace miba {
 
 namespace {
+
+
+// ---------------------------------------------------------------------------
+// Diagonal-block factor (replaces rocsolver_dpotrf on the panel's diagonal
+// block: 1.2 ms per 512-block there, 29 of the 48 ms of an nf = 12 000
+// factorisation — profiles/r1/chol_breakdown.txt).  Right-looking over
+// 64-wide sub-panels, two launches per sub-panel:
+//   diag_panel_kernel:  every workgroup (one wave) factors the 64x64 tile in
+//     LDS (lane = row, column-major tile, the pivot column broadcast from a
+//     separate LDS vector), workgroup 0
+//     writes it back, workgroups 1.. solve 64 rows each of the sub-panel
+//     below it (x L' = a, lane = row, L read as LDS broadcasts);
+//   diag_update_kernel: the trailing lower triangle of the block, A22 -= P P',
+//     one 64x64 tile per 256-thread workgroup, K staged through LDS.
+// Widths below 64 are padded with an identity (pivots 1, zero couplings).
+constexpr int kSub = 64;
+
+__global__ __launch_bounds__(64) void diag_panel_kernel(double* __restrict__ A, int lda, int w, int mrows,
+                                                        int* __restrict__ info) {
+  // Column-major tiles in LDS, element (r, c) at [c * 64 + r]: lane r's
+  // accesses are consecutive across the wave, L[c][j] reads are broadcasts.
+  __shared__ double L[kSub * kSub], P[kSub * kSub], col[kSub];
+  const int lane = threadIdx.x;
+  // Loads are unconditional at clamped (in-range) addresses and selected
+  // afterwards, so the unrolled loops issue them back to back instead of
+  // paying one global-memory latency per column.
+  const double* tile_row = A + std::min(lane, w - 1);
+#pragma unroll 16
+  for (int c = 0; c < kSub; ++c) {
+    const double v = tile_row[(size_t)std::min(c, w - 1) * lda];
+    L[c * kSub + lane] = (lane < w && c < w) ? (lane >= c ? v : 0.0) : (lane == c ? 1.0 : 0.0);
+  }
+  const int r = (blockIdx.x - 1) * kSub + lane;  // row of the sub-panel below the tile (blocks >= 1)
+  const bool solve = blockIdx.x > 0 && r < mrows;
+  double* row = A + w + r;  // A points at the tile; the sub-panel rows start w below it
+  if (blockIdx.x > 0) {
+    const double* src = A + w + std::min(r, mrows - 1);
+#pragma unroll 16
+    for (int c = 0; c < kSub; ++c) {
+      const double v = src[(size_t)std::min(c, w - 1) * lda];
+      P[c * kSub + lane] = (solve && c < w) ? v : 0.0;
+    }
+  }
+  __syncthreads();
+  int bad = 0;
+  for (int j = 0; j < kSub; ++j) {
+    const double d = L[j * kSub + j];
+    if (!(d > 0.0) && bad == 0) bad = j + 1;
+    const double sd = sqrt(d);
+    const double l = lane > j ? L[j * kSub + lane] / sd : (lane == j ? sd : 0.0);
+    __syncthreads();
+    if (lane >= j) L[j * kSub + lane] = l;
+    col[lane] = l;  // separate array: the update's broadcast loads cannot alias its stores
+    __syncthreads();
+    // branch-free: entries above the diagonal (c > lane) take garbage, never read
+#pragma unroll 8
+    for (int c = j + 1; c < kSub; ++c) L[c * kSub + lane] -= l * col[c];
+    __syncthreads();
+  }
+  if (blockIdx.x == 0) {
+#pragma unroll 16
+    for (int c = 0; c < kSub; ++c)
+      if (lane < w && c < w && lane >= c) A[lane + (size_t)c * lda] = L[c * kSub + lane];
+    if (lane == 0 && bad != 0 && bad <= w) info[0] = bad;
+    return;
+  }
+  // x L' = a, right-looking over the columns of the lane's row
+  for (int c = 0; c < kSub; ++c) {
+    const double x = P[c * kSub + lane] / L[c * kSub + c];
+    P[c * kSub + lane] = x;
+#pragma unroll 8
+    for (int t = c + 1; t < kSub; ++t) P[t * kSub + lane] -= x * L[c * kSub + t];
+  }
+  if (solve)
+#pragma unroll 16
+    for (int c = 0; c < kSub; ++c)
+      if (c < w) row[(size_t)c * lda] = P[c * kSub + lane];
+}
+
+// A22 (m x m, lower) -= P P', P = the m x w sub-panel left of A22 (column-
+// major, P[r + t*lda] = A22[r - w*lda ...]); tile (bi >= bj) per workgroup.
+__global__ __launch_bounds__(256) void diag_update_kernel(double* __restrict__ A22, const double* __restrict__ P,
+                                                          int lda, int m, int w) {
+  __shared__ double sr[kSub * 33], sc[kSub * 33];
+  // lower-triangle tile index -> (bi, bj), bi >= bj
+  int t = blockIdx.x, bi = 0;
+  while (t > bi) { t -= bi + 1; ++bi; }
+  const int bj = t;
+  const int r0 = bi * kSub, c0 = bj * kSub;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  double acc[4][4] = {};
+  for (int k0 = 0; k0 < w; k0 += 32) {
+#pragma unroll
+    for (int e = threadIdx.x; e < kSub * 32; e += 256) {
+      const int rr = e & 63, kk = e >> 6;
+      const int k = k0 + kk;
+      const size_t kc = (size_t)std::min(k, w - 1) * lda;  // clamped: loads issue back to back
+      const double vr = P[std::min(r0 + rr, m - 1) + kc], vc = P[std::min(c0 + rr, m - 1) + kc];
+      sr[rr * 33 + kk] = (r0 + rr < m && k < w) ? vr : 0.0;
+      sc[rr * 33 + kk] = (c0 + rr < m && k < w) ? vc : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < 32; ++kk) {
+      double x[4], y[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = sr[(ty + 16 * i) * 33 + kk];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = sc[(tx + 16 * j) * 33 + kk];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += x[i] * y[j];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = r0 + ty + 16 * i, c = c0 + tx + 16 * j;
+      if (r < m && c < m && r >= c) A22[r + (size_t)c * lda] -= acc[i][j];
+    }
+}
+
+rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info) {
+  hipStream_t s;
+  if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
+  if (hipMemsetAsync(info, 0, sizeof(int), s) != hipSuccess) return rocblas_status_internal_error;
+  for (int k = 0; k < n; k += kSub) {
+    const int w = std::min(kSub, n - k);
+    const int m = n - k - w;  // rows (and columns) of the block after this sub-panel
+    double* Akk = A + k + (size_t)k * lda;
+    hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(kSub), 0, s, Akk, lda, w, m, info);
+    if (m > 0) {
+      const int T = (m + kSub - 1) / kSub;
+      hipLaunchKernelGGL(diag_update_kernel, dim3(T * (T + 1) / 2), dim3(256), 0, s, Akk + w + (size_t)w * lda,
+                         Akk + w, lda, m, w);
+    }
+  }
+  return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
+}
+
+rocblas_status potrf_leaf(rocblas_handle h, int n, double* A, int lda, int* info, bool own) {
+  if (own) return potrf_diag(h, n, A, lda, info);
+  return rocsolver_dpotrf(h, rocblas_fill_lower, n, A, lda, info);
+}
 
 constexpr int kLeaf = 768;  // diagonal leaves factored by rocSOLVER
 
@@ -17,13 +165,13 @@ int split(int n) {
   return n1 < n ? n1 : n / 2;
 }
 
-rocblas_status factor(rocblas_handle h, int n, double* A, int lda, int*& info) {
-  if (n <= kLeaf) return rocsolver_dpotrf(h, rocblas_fill_lower, n, A, lda, info++);
+rocblas_status factor(rocblas_handle h, int n, double* A, int lda, int*& info, bool own) {
+  if (n <= kLeaf) return potrf_leaf(h, n, A, lda, info++, own);
   const int n1 = split(n), n2 = n - n1;
   double* A11 = A;
   double* A21 = A + n1;
   double* A22 = A + n1 + (size_t)n1 * lda;
-  rocblas_status st = factor(h, n1, A11, lda, info);
+  rocblas_status st = factor(h, n1, A11, lda, info, own);
   if (st != rocblas_status_success) return st;
   const double one = 1.0, minus_one = -1.0;
   // A21 := A21 L11^-T
@@ -33,7 +181,7 @@ rocblas_status factor(rocblas_handle h, int n, double* A, int lda, int*& info) {
   // A22 := A22 - A21 A21'
   st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, n2, n1, &minus_one, A21, lda, &one, A22, lda);
   if (st != rocblas_status_success) return st;
-  return factor(h, n2, A22, lda, info);
+  return factor(h, n2, A22, lda, info, own);
 }
 
 int leaves(int n) { return n <= kLeaf ? 1 : leaves(split(n)) + leaves(n - split(n)); }
@@ -74,7 +222,7 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
   for (int k = 0; k < n; k += nb) {
     const int kb = std::min(nb, n - k);
     double* Akk = A + k + (size_t)k * lda;
-    rocblas_status st = rocsolver_dpotrf(h, rocblas_fill_lower, kb, Akk, lda, info++);
+    rocblas_status st = potrf_leaf(h, kb, Akk, lda, info++, cfg.own_diag);
     if (st != rocblas_status_success) return st;
     const int m = n - k - kb;
     if (m == 0) break;
@@ -108,7 +256,7 @@ int chol_leaf_count(int n, const CholConfig& cfg) {
 rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg) {
   if (n <= 0) return rocblas_status_success;
   if (cfg.panel > 0) return factor_blocked(h, n, A, lda, info, cfg);
-  return factor(h, n, A, lda, info);
+  return factor(h, n, A, lda, info, cfg.own_diag);
 }
 
 rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x) {

@@ -22,6 +22,7 @@ namespace miba {
 struct CholConfig {
   int panel = 512;        // 0: recursive split; > 0: right-looking panel width
   bool gemm_update = true;
+  bool own_diag = true;   // diagonal blocks by the hand-written 64-wide factor, else rocsolver_dpotrf
 };
 
 // In-place lower Cholesky of the n x n column-major matrix A (leading

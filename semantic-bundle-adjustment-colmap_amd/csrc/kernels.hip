@@ -345,7 +345,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   constexpr int LS = (D & 32) ? W2 + 4 : (W2 | 1);
   constexpr int RP = 64 / NP;
   constexpr int RS = 18;  // LDS stride of an image record (144 B: conflict-free ds_read_b128)
-  constexpr int SLAB = (RP * LS > 64 * RS) ? RP * LS : 64 * RS;
+  // D & 64: image records fetched per lane (no LDS staging), slab = J rows only
+  constexpr int SLAB = ((D & 64) || RP * LS > 64 * RS) ? RP * LS : 64 * RS;
   __shared__ double sred[4];
   __shared__ double sJ[(kBlock / 64) * SLAB];
   const int lane = threadIdx.x & 63;
@@ -376,24 +377,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     uint32_t img = 0u;
     if (live) img = (D & 16) ? __builtin_nontemporal_load(p.obs_img + i) : p.obs_img[i];
     if constexpr ((D & 4) != 0) img &= 127u;  // diagnostic: L1-resident record working set
+    double q[4], t[3], prm[np];
+    uint32_t meta;
+    if constexpr ((D & 64) != 0) {
+      // per-lane record fetch: 16-B loads of the lane's own 128-B line (L1/L2
+      // resident, 1000 images = 128 KB), no LDS and no wave barrier
+      const double2* rv = reinterpret_cast<const double2*>(p.img_rec + 16 * (size_t)img);
+      const double2 a0 = rv[0], a1 = rv[1], a2 = rv[2], a3 = rv[3];
+      q[0] = a0.x; q[1] = a0.y; q[2] = a1.x; q[3] = a1.y;
+      t[0] = a2.x; t[1] = a2.y; t[2] = a3.x;
+      meta = (uint32_t)__double_as_longlong(a3.y);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int src = 8 * j + (lane >> 3);
-      const uint32_t is = __shfl(img, src, 64);
-      const double2 v = reinterpret_cast<const double2*>(p.img_rec + 16 * (size_t)is)[lane & 7];
-      reinterpret_cast<double2*>(slab + src * RS)[lane & 7] = v;
+      for (int k = 0; k < (np + 1) / 2; ++k) {
+        const double2 c = rv[4 + k];
+        prm[2 * k] = c.x;
+        if (2 * k + 1 < np) prm[2 * k + 1] = c.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int src = 8 * j + (lane >> 3);
+        const uint32_t is = __shfl(img, src, 64);
+        const double2 v = reinterpret_cast<const double2*>(p.img_rec + 16 * (size_t)is)[lane & 7];
+        reinterpret_cast<double2*>(slab + src * RS)[lane & 7] = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      const double* rec = slab + lane * RS;
+      q[0] = rec[0]; q[1] = rec[1]; q[2] = rec[2]; q[3] = rec[3];
+      t[0] = rec[4]; t[1] = rec[5]; t[2] = rec[6];
+      meta = (uint32_t)__double_as_longlong(rec[7]);
+#pragma unroll
+      for (int k = 0; k < np; ++k) prm[k] = rec[8 + k];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const double* rec = slab + lane * RS;
-    const double q[4] = {rec[0], rec[1], rec[2], rec[3]};
-    const double t[3] = {rec[4], rec[5], rec[6]};
-    const uint32_t meta = (uint32_t)__double_as_longlong(rec[7]);
-    double prm[np];
-#pragma unroll
-    for (int k = 0; k < np; ++k) prm[k] = rec[8 + k];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (live) {
       double2 o;
       if constexpr ((D & 16) != 0) {
@@ -1454,6 +1472,31 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
             case 22:
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 4>), dim3(g), dim3(kBlock), 0, s, p, r, J,
                                  cost_partial);
+              return;
+            // occupancy study: per-lane records (64), J slab in NP passes, WPE waves/SIMD
+            case 30:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction, 5>), dim3(g), dim3(kBlock), 0, s, p, r, J,
+                                 cost_partial);
+              return;
+            case 31:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 64, 4>), dim3(g), dim3(kBlock), 0, s, p, r,
+                                 J, cost_partial);
+              return;
+            case 32:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 4, kJacProduction | 64, 5>), dim3(g), dim3(kBlock), 0, s, p, r,
+                                 J, cost_partial);
+              return;
+            case 33:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 4, kJacProduction | 64, 6>), dim3(g), dim3(kBlock), 0, s, p, r,
+                                 J, cost_partial);
+              return;
+            case 34:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 4, kJacProduction | 64, 8>), dim3(g), dim3(kBlock), 0, s, p, r,
+                                 J, cost_partial);
+              return;
+            case 35:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 64, 6>), dim3(g), dim3(kBlock), 0, s, p, r,
+                                 J, cost_partial);
               return;
             case 9:
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 1>), dim3(g), dim3(kBlock), 0, s, p, r, J,

@@ -1084,12 +1084,16 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
 
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value) {
   if (!ctx || !key) return MI_BA_ERR_INVALID_ARGUMENT;
-  if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 31) {
+  if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 63) {
     ctx->dev.jvariant = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_panel") == 0 && (value == 0 || (value >= 64 && value <= 4096))) {
     ctx->chol.panel = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_own_diag") == 0 && (value == 0 || value == 1)) {
+    ctx->chol.own_diag = value != 0;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_gemm_update") == 0 && (value == 0 || value == 1)) {
