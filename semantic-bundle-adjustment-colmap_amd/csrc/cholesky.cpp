@@ -16,7 +16,7 @@ namespace {
 // block: 1.2 ms per 512-block there, 29 of the 48 ms of an nf = 12 000
 // factorisation — profiles/r1/chol_breakdown.txt).  Right-looking over
 // 64-wide sub-panels, two launches per sub-panel:
-//   diag_panel_kernel:  every workgroup (one wave) factors the 64x64 tile in
+//   diag_panel_kernel:  every workgroup (four waves) factors the 64x64 tile in
 //     LDS (lane = row, column-major tile, the pivot column broadcast from a
 //     separate LDS vector), workgroup 0
 //     writes it back, workgroups 1.. solve 64 rows each of the sub-panel
@@ -26,18 +26,19 @@ namespace {
 // Widths below 64 are padded with an identity (pivots 1, zero couplings).
 constexpr int kSub = 64;
 
-__global__ __launch_bounds__(64) void diag_panel_kernel(double* __restrict__ A, int lda, int w, int mrows,
-                                                        int* __restrict__ info) {
+__global__ __launch_bounds__(256) void diag_panel_kernel(double* __restrict__ A, int lda, int w, int mrows,
+                                                         int* __restrict__ info) {
   // Column-major tiles in LDS, element (r, c) at [c * 64 + r]: lane r's
-  // accesses are consecutive across the wave, L[c][j] reads are broadcasts.
+  // accesses are consecutive across a wave, L[c][j] reads are broadcasts.
+  // Four waves share the 64 rows: each takes every fourth column of the
+  // rank-1 updates (factor) and of the right-looking updates (solve).
   __shared__ double L[kSub * kSub], P[kSub * kSub], col[kSub];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // Loads are unconditional at clamped (in-range) addresses and selected
-  // afterwards, so the unrolled loops issue them back to back instead of
-  // paying one global-memory latency per column.
+  // afterwards, so the unrolled loops issue them back to back.
   const double* tile_row = A + std::min(lane, w - 1);
-#pragma unroll 16
-  for (int c = 0; c < kSub; ++c) {
+#pragma unroll
+  for (int c = wv; c < kSub; c += 4) {
     const double v = tile_row[(size_t)std::min(c, w - 1) * lda];
     L[c * kSub + lane] = (lane < w && c < w) ? (lane >= c ? v : 0.0) : (lane == c ? 1.0 : 0.0);
   }
@@ -46,8 +47,8 @@ __global__ __launch_bounds__(64) void diag_panel_kernel(double* __restrict__ A, 
   double* row = A + w + r;  // A points at the tile; the sub-panel rows start w below it
   if (blockIdx.x > 0) {
     const double* src = A + w + std::min(r, mrows - 1);
-#pragma unroll 16
-    for (int c = 0; c < kSub; ++c) {
+#pragma unroll
+    for (int c = wv; c < kSub; c += 4) {
       const double v = src[(size_t)std::min(c, w - 1) * lda];
       P[c * kSub + lane] = (solve && c < w) ? v : 0.0;
     }
@@ -60,32 +61,32 @@ __global__ __launch_bounds__(64) void diag_panel_kernel(double* __restrict__ A, 
     const double sd = sqrt(d);
     const double l = lane > j ? L[j * kSub + lane] / sd : (lane == j ? sd : 0.0);
     __syncthreads();
-    if (lane >= j) L[j * kSub + lane] = l;
-    col[lane] = l;  // separate array: the update's broadcast loads cannot alias its stores
+    if (wv == 0) {
+      if (lane >= j) L[j * kSub + lane] = l;
+      col[lane] = l;  // separate array: the update's broadcast loads cannot alias its stores
+    }
     __syncthreads();
     // branch-free: entries above the diagonal (c > lane) take garbage, never read
-#pragma unroll 8
-    for (int c = j + 1; c < kSub; ++c) L[c * kSub + lane] -= l * col[c];
+#pragma unroll 4
+    for (int c = j + 1 + wv; c < kSub; c += 4) L[c * kSub + lane] -= l * col[c];
     __syncthreads();
   }
   if (blockIdx.x == 0) {
-#pragma unroll 16
-    for (int c = 0; c < kSub; ++c)
+#pragma unroll
+    for (int c = wv; c < kSub; c += 4)
       if (lane < w && c < w && lane >= c) A[lane + (size_t)c * lda] = L[c * kSub + lane];
-    if (lane == 0 && bad != 0 && bad <= w) info[0] = bad;
+    if (threadIdx.x == 0 && bad != 0 && bad <= w) info[0] = bad;
     return;
   }
-  // x L' = a, right-looking over the columns of the lane's row
+  // x L' = a, right-looking over the columns of the lane's row; column c's
+  // result leaves from the wave that owns it (P[c] is never written again)
   for (int c = 0; c < kSub; ++c) {
     const double x = P[c * kSub + lane] / L[c * kSub + c];
-    P[c * kSub + lane] = x;
-#pragma unroll 8
-    for (int t = c + 1; t < kSub; ++t) P[t * kSub + lane] -= x * L[c * kSub + t];
+    if (solve && c < w && (c & 3) == wv) row[(size_t)c * lda] = x;
+#pragma unroll 4
+    for (int t = c + 1 + wv; t < kSub; t += 4) P[t * kSub + lane] -= x * L[c * kSub + t];
+    __syncthreads();
   }
-  if (solve)
-#pragma unroll 16
-    for (int c = 0; c < kSub; ++c)
-      if (c < w) row[(size_t)c * lda] = P[c * kSub + lane];
 }
 
 // A22 (m x m, lower) -= P P', P = the m x w sub-panel left of A22 (column-
@@ -142,7 +143,7 @@ rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info
     const int w = std::min(kSub, n - k);
     const int m = n - k - w;  // rows (and columns) of the block after this sub-panel
     double* Akk = A + k + (size_t)k * lda;
-    hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(kSub), 0, s, Akk, lda, w, m, info);
+    hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(256), 0, s, Akk, lda, w, m, info);
     if (m > 0) {
       const int T = (m + kSub - 1) / kSub;
       hipLaunchKernelGGL(diag_update_kernel, dim3(T * (T + 1) / 2), dim3(256), 0, s, Akk + w + (size_t)w * lda,
