@@ -16,7 +16,7 @@ namespace {
 // block: 1.2 ms per 512-block there, 29 of the 48 ms of an nf = 12 000
 // factorisation — profiles/r1/chol_breakdown.txt).  Right-looking over
 // 64-wide sub-panels, two launches per sub-panel:
-//   diag_panel_kernel:  every workgroup (four waves) factors the 64x64 tile in
+//   diag_panel_kernel:  every workgroup (kPanelWaves waves) factors the 64x64 tile in
 //     LDS (lane = row, column-major tile, the pivot column broadcast from a
 //     separate LDS vector), workgroup 0
 //     writes it back, workgroups 1.. solve 64 rows each of the sub-panel
@@ -25,20 +25,22 @@ namespace {
 //     one 64x64 tile per 256-thread workgroup, K staged through LDS.
 // Widths below 64 are padded with an identity (pivots 1, zero couplings).
 constexpr int kSub = 64;
+constexpr int kPanelWaves = 8;  // waves per diag_panel_kernel workgroup
 
-__global__ __launch_bounds__(256) void diag_panel_kernel(double* __restrict__ A, int lda, int w, int mrows,
+__global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_kernel(double* __restrict__ A, int lda, int w, int mrows,
                                                          int* __restrict__ info) {
   // Column-major tiles in LDS, element (r, c) at [c * 64 + r]: lane r's
   // accesses are consecutive across a wave, L[c][j] reads are broadcasts.
-  // Four waves share the 64 rows: each takes every fourth column of the
-  // rank-1 updates (factor) and of the right-looking updates (solve).
+  // kPanelWaves waves share the 64 rows: each takes every kPanelWaves-th
+  // column of the rank-1 updates (factor) and of the right-looking updates
+  // (solve).
   __shared__ double L[kSub * kSub], P[kSub * kSub], col[kSub];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // Loads are unconditional at clamped (in-range) addresses and selected
   // afterwards, so the unrolled loops issue them back to back.
   const double* tile_row = A + std::min(lane, w - 1);
 #pragma unroll
-  for (int c = wv; c < kSub; c += 4) {
+  for (int c = wv; c < kSub; c += kPanelWaves) {
     const double v = tile_row[(size_t)std::min(c, w - 1) * lda];
     L[c * kSub + lane] = (lane < w && c < w) ? (lane >= c ? v : 0.0) : (lane == c ? 1.0 : 0.0);
   }
@@ -48,7 +50,7 @@ __global__ __launch_bounds__(256) void diag_panel_kernel(double* __restrict__ A,
   if (blockIdx.x > 0) {
     const double* src = A + w + std::min(r, mrows - 1);
 #pragma unroll
-    for (int c = wv; c < kSub; c += 4) {
+    for (int c = wv; c < kSub; c += kPanelWaves) {
       const double v = src[(size_t)std::min(c, w - 1) * lda];
       P[c * kSub + lane] = (solve && c < w) ? v : 0.0;
     }
@@ -60,20 +62,18 @@ __global__ __launch_bounds__(256) void diag_panel_kernel(double* __restrict__ A,
     if (!(d > 0.0) && bad == 0) bad = j + 1;
     const double sd = sqrt(d);
     const double l = lane > j ? L[j * kSub + lane] / sd : (lane == j ? sd : 0.0);
+    if (wv == 0) col[lane] = l;  // separate array: the update's broadcast loads cannot alias its stores
     __syncthreads();
-    if (wv == 0) {
-      if (lane >= j) L[j * kSub + lane] = l;
-      col[lane] = l;  // separate array: the update's broadcast loads cannot alias its stores
-    }
-    __syncthreads();
+    // column j in place only after every wave has read it (before the barrier)
+    if (wv == 0 && lane >= j) L[j * kSub + lane] = l;
     // branch-free: entries above the diagonal (c > lane) take garbage, never read
-#pragma unroll 4
-    for (int c = j + 1 + wv; c < kSub; c += 4) L[c * kSub + lane] -= l * col[c];
+#pragma unroll 2
+    for (int c = j + 1 + wv; c < kSub; c += kPanelWaves) L[c * kSub + lane] -= l * col[c];
     __syncthreads();
   }
   if (blockIdx.x == 0) {
 #pragma unroll
-    for (int c = wv; c < kSub; c += 4)
+    for (int c = wv; c < kSub; c += kPanelWaves)
       if (lane < w && c < w && lane >= c) A[lane + (size_t)c * lda] = L[c * kSub + lane];
     if (threadIdx.x == 0 && bad != 0 && bad <= w) info[0] = bad;
     return;
@@ -82,9 +82,9 @@ __global__ __launch_bounds__(256) void diag_panel_kernel(double* __restrict__ A,
   // result leaves from the wave that owns it (P[c] is never written again)
   for (int c = 0; c < kSub; ++c) {
     const double x = P[c * kSub + lane] / L[c * kSub + c];
-    if (solve && c < w && (c & 3) == wv) row[(size_t)c * lda] = x;
-#pragma unroll 4
-    for (int t = c + 1 + wv; t < kSub; t += 4) P[t * kSub + lane] -= x * L[c * kSub + t];
+    if (solve && c < w && c % kPanelWaves == wv) row[(size_t)c * lda] = x;
+#pragma unroll 2
+    for (int t = c + 1 + wv; t < kSub; t += kPanelWaves) P[t * kSub + lane] -= x * L[c * kSub + t];
     __syncthreads();
   }
 }
@@ -143,7 +143,7 @@ rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info
     const int w = std::min(kSub, n - k);
     const int m = n - k - w;  // rows (and columns) of the block after this sub-panel
     double* Akk = A + k + (size_t)k * lda;
-    hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(256), 0, s, Akk, lda, w, m, info);
+    hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s, Akk, lda, w, m, info);
     if (m > 0) {
       const int T = (m + kSub - 1) / kSub;
       hipLaunchKernelGGL(diag_update_kernel, dim3(T * (T + 1) / 2), dim3(256), 0, s, Akk + w + (size_t)w * lda,
