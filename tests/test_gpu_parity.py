@@ -259,3 +259,25 @@ def test_large_scene_properties(gpu, cfg):
     assert np.abs(r[sel] - r_o).max() <= 1e-9
     scale = np.maximum(1.0, np.abs(J_o).reshape(len(sel), -1).max(axis=1))
     assert (np.abs(J[sel] - J_o).reshape(len(sel), -1).max(axis=1) / scale).max() <= 1e-10
+
+
+@pytest.mark.parametrize("images", [70, 121])
+def test_own_diagonal_cholesky_matches_rocsolver(gpu, images):
+    """The hand-written diagonal-block factor (cholesky.cpp diag_panel_kernel /
+    diag_update_kernel) against rocsolver_dpotrf inside the same LM run, on
+    reduced camera systems spanning several 64-wide sub-panels and (121
+    images) two 512-wide panels, with ragged last sub-panels (SIMPLE_RADIAL
+    with the gauge: nf = 8 * images - 7).  Tolerance: final cost within 1e-9
+    relative, same step counts."""
+    sc = scene(mi_ba.SIMPLE_RADIAL, images=images, points=2000, track=6, seed=3)
+    opts = mi_ba.default_options(max_num_iterations=8)
+    out = []
+    for own in (1, 0):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            ctx.set_tuning("cholesky_own_diag", own)
+            out.append(ctx.solve())
+    a, b = out
+    assert a.num_successful_steps == b.num_successful_steps
+    assert a.num_unsuccessful_steps == b.num_unsuccessful_steps
+    assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost, (a.final_cost, b.final_cost)
+    assert a.final_cost < a.initial_cost
