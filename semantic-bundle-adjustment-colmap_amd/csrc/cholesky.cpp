@@ -158,7 +158,11 @@ rocblas_status potrf_leaf(rocblas_handle h, int n, double* A, int lda, int* info
   return rocsolver_dpotrf(h, rocblas_fill_lower, n, A, lda, info);
 }
 
-constexpr int kLeaf = 768;  // diagonal leaves factored by rocSOLVER
+constexpr int kLeaf = 768;  // diagonal leaves of the recursive factor
+// dtrsv leaves of the solve (rocBLAS dtrsv, 135 us at 768); 384-wide leaves
+// measured slower (5.9 -> 8.7 ms per solve at nf = 12 000: the extra dgemv
+// calls cost more than the shorter column sweeps save)
+constexpr int kSolveLeaf = 768;
 
 int split(int n) {
   int n1 = n / 2;
@@ -189,7 +193,7 @@ int leaves(int n) { return n <= kLeaf ? 1 : leaves(split(n)) + leaves(n - split(
 
 // L y = b (forward) and L' x = y (backward), recursively.
 rocblas_status forward(rocblas_handle h, int n, const double* A, int lda, double* x) {
-  if (n <= kLeaf)
+  if (n <= kSolveLeaf)
     return rocblas_dtrsv(h, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit, n, A, lda, x, 1);
   const int n1 = split(n), n2 = n - n1;
   rocblas_status st = forward(h, n1, A, lda, x);
@@ -201,7 +205,7 @@ rocblas_status forward(rocblas_handle h, int n, const double* A, int lda, double
 }
 
 rocblas_status backward(rocblas_handle h, int n, const double* A, int lda, double* x) {
-  if (n <= kLeaf)
+  if (n <= kSolveLeaf)
     return rocblas_dtrsv(h, rocblas_fill_lower, rocblas_operation_transpose, rocblas_diagonal_non_unit, n, A, lda, x,
                          1);
   const int n1 = split(n), n2 = n - n1;
