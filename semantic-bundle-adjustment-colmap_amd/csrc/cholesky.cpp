@@ -251,6 +251,82 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
   return rocblas_status_success;
 }
 
+// Look-ahead variant of factor_blocked (gemm update): as soon as panel k's
+// dgemm has updated block column k+1, the diagonal factor and dtrsm of panel
+// k+1 run on a side stream (own rocBLAS handle) while the rest of panel k's
+// trailing dgemm runs on the caller's stream; the next iteration's dgemm waits
+// on the side stream's event.  Hides the latency-bound diagonal factor behind
+// the MFMA update.  Side resources are created once per device.
+struct SideStream {
+  rocblas_handle h = nullptr;
+  hipStream_t s = nullptr;
+  hipEvent_t upd = nullptr, pan = nullptr;
+};
+
+SideStream* side_for_device() {
+  static SideStream sides[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SideStream& ss = sides[dev];
+  if (!ss.h) {
+    if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&ss.upd, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&ss.pan, hipEventDisableTiming) != hipSuccess) return nullptr;
+    rocblas_handle h2;
+    if (rocblas_create_handle(&h2) != rocblas_status_success) return nullptr;
+    if (rocblas_set_stream(h2, ss.s) != rocblas_status_success) return nullptr;
+    ss.h = h2;
+  }
+  return &ss;
+}
+
+rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, bool own) {
+  double* Akk = A + k + (size_t)k * lda;
+  rocblas_status st = potrf_leaf(h, kb, Akk, lda, info, own);
+  if (st != rocblas_status_success) return st;
+  const int m = n - k - kb;
+  if (m == 0) return st;
+  const double one = 1.0;
+  return rocblas_dtrsm(h, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                       rocblas_diagonal_non_unit, m, kb, &one, Akk, lda, Akk + kb, lda);
+}
+
+rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
+                                SideStream& ss) {
+  const double minus_one = -1.0, one = 1.0;
+  const int nb = cfg.panel;
+  hipStream_t s1;
+  if (rocblas_get_stream(h, &s1) != rocblas_status_success) return rocblas_status_internal_error;
+  rocblas_status st = panel_factor(h, n, A, lda, 0, std::min(nb, n), info, cfg.own_diag);
+  if (st != rocblas_status_success) return st;
+  for (int k = 0, kk = 0; k < n; k += nb, ++kk) {
+    const int kb = std::min(nb, n - k);
+    const int m = n - k - kb;
+    if (m == 0) break;
+    double* Aik = A + k + kb + (size_t)k * lda;  // panel k below its diagonal block
+    double* T = Aik + (size_t)kb * lda;          // trailing matrix, lower triangle
+    // block column k+1 first
+    const int jb0 = std::min(nb, m);
+    st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, jb0, kb, &minus_one, Aik, lda, Aik,
+                       lda, &one, T, lda);
+    if (st != rocblas_status_success) return st;
+    if (hipEventRecord(ss.upd, s1) != hipSuccess || hipStreamWaitEvent(ss.s, ss.upd, 0) != hipSuccess)
+      return rocblas_status_internal_error;
+    st = panel_factor(ss.h, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag);
+    if (st != rocblas_status_success) return st;
+    if (hipEventRecord(ss.pan, ss.s) != hipSuccess) return rocblas_status_internal_error;
+    for (int j = jb0; j < m; j += nb) {
+      const int jb = std::min(nb, m - j);
+      st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m - j, jb, kb, &minus_one, Aik + j,
+                         lda, Aik + j, lda, &one, T + j + (size_t)j * lda, lda);
+      if (st != rocblas_status_success) return st;
+    }
+    // panel k+1 is read by the next iteration's updates (and by the solve)
+    if (hipStreamWaitEvent(s1, ss.pan, 0) != hipSuccess) return rocblas_status_internal_error;
+  }
+  return rocblas_status_success;
+}
+
 }  // namespace
 
 int chol_leaf_count(int n, const CholConfig& cfg) {
@@ -260,6 +336,10 @@ int chol_leaf_count(int n, const CholConfig& cfg) {
 
 rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg) {
   if (n <= 0) return rocblas_status_success;
+  if (cfg.panel > 0 && cfg.gemm_update && cfg.lookahead) {
+    SideStream* ss = side_for_device();
+    if (ss) return factor_lookahead(h, n, A, lda, info, cfg, *ss);
+  }
   if (cfg.panel > 0) return factor_blocked(h, n, A, lda, info, cfg);
   return factor(h, n, A, lda, info, cfg.own_diag);
 }

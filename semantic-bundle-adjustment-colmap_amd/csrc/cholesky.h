@@ -22,6 +22,11 @@ namespace miba {
 struct CholConfig {
   int panel = 512;        // 0: recursive split; > 0: right-looking panel width
   bool gemm_update = true;
+  // panel k+1's diagonal factor + dtrsm on a side stream under panel k's dgemm:
+  // 34.6 -> 30.4 ms at nf = 12 000, but the C4 LM run diverged from the
+  // serial factor (one factorisation reported non-SPD) — off until the race is
+  // found (tuning key cholesky_lookahead)
+  bool lookahead = false;
   bool own_diag = true;   // diagonal blocks by the hand-written 64-wide factor, else rocsolver_dpotrf
 };
 

@@ -1092,6 +1092,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.panel = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "cholesky_lookahead") == 0 && (value == 0 || value == 1)) {
+    ctx->chol.lookahead = value != 0;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_own_diag") == 0 && (value == 0 || value == 1)) {
     ctx->chol.own_diag = value != 0;
     return MI_BA_OK;
