@@ -278,7 +278,14 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
                                             mi_ba_host_allreduce_fn fn, void* user);
 
 /* Kernel-variant switches for in-process A/B measurement (key, value);
- * unknown keys return MI_BA_ERR_INVALID_ARGUMENT. */
+ * unknown keys return MI_BA_ERR_INVALID_ARGUMENT.  Keys:
+ *   "jacobian_variant"      0 production; 1/4 row-staging passes, 9/10 no-store /
+ *                           no-arithmetic roofline builds, 20-22 store variants,
+ *                           30-35 occupancy study (tools/ab_jacobian.py)
+ *   "cholesky_panel"        0 recursive split, 64..4096 right-looking panel width
+ *   "cholesky_gemm_update"  0 dsyrk / 1 dgemm trailing update
+ *   "cholesky_own_diag"     1 hand-written diagonal-block factor / 0 rocsolver_dpotrf
+ *   "cholesky_lookahead"    1 side-stream look-ahead (experimental) / 0 serial */
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value);
 
 /* Per-kernel HIP-event timing on the context's stream (enabled with
