@@ -5,6 +5,7 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <vector>
 
 namespace miba {
 
@@ -261,6 +262,7 @@ struct SideStream {
   rocblas_handle h = nullptr;
   hipStream_t s = nullptr;
   hipEvent_t upd = nullptr, pan = nullptr;
+  std::vector<hipEvent_t> ev;  // one pair per panel: no event is re-recorded within a factorisation
 };
 
 SideStream* side_for_device() {
@@ -297,6 +299,12 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
   const int nb = cfg.panel;
   hipStream_t s1;
   if (rocblas_get_stream(h, &s1) != rocblas_status_success) return rocblas_status_internal_error;
+  const size_t need = 2 * (size_t)((n + nb - 1) / nb);
+  while (ss.ev.size() < need) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return rocblas_status_internal_error;
+    ss.ev.push_back(e);
+  }
   rocblas_status st = panel_factor(h, n, A, lda, 0, std::min(nb, n), info, cfg.own_diag);
   if (st != rocblas_status_success) return st;
   for (int k = 0, kk = 0; k < n; k += nb, ++kk) {
@@ -310,11 +318,12 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, jb0, kb, &minus_one, Aik, lda, Aik,
                        lda, &one, T, lda);
     if (st != rocblas_status_success) return st;
-    if (hipEventRecord(ss.upd, s1) != hipSuccess || hipStreamWaitEvent(ss.s, ss.upd, 0) != hipSuccess)
+    hipEvent_t upd = ss.ev[2 * kk], pan = ss.ev[2 * kk + 1];
+    if (hipEventRecord(upd, s1) != hipSuccess || hipStreamWaitEvent(ss.s, upd, 0) != hipSuccess)
       return rocblas_status_internal_error;
     st = panel_factor(ss.h, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag);
     if (st != rocblas_status_success) return st;
-    if (hipEventRecord(ss.pan, ss.s) != hipSuccess) return rocblas_status_internal_error;
+    if (hipEventRecord(pan, ss.s) != hipSuccess) return rocblas_status_internal_error;
     for (int j = jb0; j < m; j += nb) {
       const int jb = std::min(nb, m - j);
       st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m - j, jb, kb, &minus_one, Aik + j,
@@ -322,7 +331,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       if (st != rocblas_status_success) return st;
     }
     // panel k+1 is read by the next iteration's updates (and by the solve)
-    if (hipStreamWaitEvent(s1, ss.pan, 0) != hipSuccess) return rocblas_status_internal_error;
+    if (hipStreamWaitEvent(s1, pan, 0) != hipSuccess) return rocblas_status_internal_error;
   }
   return rocblas_status_success;
 }

@@ -22,11 +22,10 @@ namespace miba {
 struct CholConfig {
   int panel = 512;        // 0: recursive split; > 0: right-looking panel width
   bool gemm_update = true;
-  // panel k+1's diagonal factor + dtrsm on a side stream under panel k's dgemm:
-  // 34.6 -> 30.4 ms at nf = 12 000, but the C4 LM run diverged from the
-  // serial factor (one factorisation reported non-SPD) — off until the race is
-  // found (tuning key cholesky_lookahead)
-  bool lookahead = false;
+  // panel k+1's diagonal factor + dtrsm on a side stream under panel k's dgemm
+  // (34.6 -> 30.4 ms at nf = 12 000); one event pair per panel — re-recording one
+  // event per iteration let a wait slip past its producer (a diverged C4 run)
+  bool lookahead = true;
   bool own_diag = true;   // diagonal blocks by the hand-written 64-wide factor, else rocsolver_dpotrf
 };
 
