@@ -288,6 +288,22 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *   "cholesky_lookahead"    1 side-stream look-ahead (default) / 0 serial */
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value);
 
+/* Dense Cholesky of a symmetric positive-definite n x n matrix with the
+ * factorisation the exact Schur solver applies to the reduced camera system
+ * (the replacement of the DENSE_SCHUR / SPARSE_SCHUR factorisation Ceres runs
+ * inside BundleAdjuster::Solve, bundle_adjustment.cc:276-306), exposed for
+ * parity tests and for callers that assemble their own S.  A: host, column-
+ * major, lda = n; its lower triangle is read and overwritten with L (the
+ * strict upper triangle is left as given).  b (nullable, host, n): on return
+ * the solution of A x = b.  panel / lookahead / own_diag as the cholesky_*
+ * tuning keys (panel 0 = recursive split).  *info = 0, or (panel > 0) the
+ * 1-based column of the first pivot found not positive definite, (panel = 0)
+ * a positive value (A unspecified in both cases).
+ * Every call owns its stream, handles and workspace: concurrent calls from
+ * several host threads share nothing. */
+mi_ba_status mi_ba_dense_cholesky(int32_t device, int32_t n, double* A, double* b, int32_t panel, int32_t lookahead,
+                                  int32_t own_diag, int32_t* info);
+
 /* Per-kernel HIP-event timing on the context's stream (enabled with
  * mi_ba_set_timing).  name: "reproj_jacobian", "semantic_jacobian", ... */
 mi_ba_status mi_ba_set_timing(mi_ba_context* ctx, int32_t enabled);

@@ -810,6 +810,28 @@ double oracle_semantic_throughput(const mi_ba_options* o, mi_ba_problem* p, cons
   return ts.tv_sec + 1e-9 * ts.tv_nsec - t0;
 }
 
+// The oracle's dense Cholesky (the factorisation its LM applies to the
+// reduced camera system, DENSE_SCHUR restated): A row-major n x n, lower
+// triangle overwritten with L.  Returns 0, or the 1-based column of the first
+// pivot that is not positive.  Rows of L are independent given the columns
+// to their left, so the i-loop runs in parallel with unchanged arithmetic.
+int oracle_cholesky(double* A, int n) {
+  for (int j = 0; j < n; ++j) {
+    double d = A[(size_t)j * n + j];
+    for (int k = 0; k < j; ++k) d -= A[(size_t)j * n + k] * A[(size_t)j * n + k];
+    if (!(d > 0.0)) return j + 1;
+    d = std::sqrt(d);
+    A[(size_t)j * n + j] = d;
+#pragma omp parallel for schedule(static) if (n - j > 256)
+    for (int i = j + 1; i < n; ++i) {
+      double v = A[(size_t)i * n + j];
+      for (int k = 0; k < j; ++k) v -= A[(size_t)i * n + k] * A[(size_t)j * n + k];
+      A[(size_t)i * n + j] = v / d;
+    }
+  }
+  return 0;
+}
+
 // Full LM solve, dense Schur (Ceres 2.1 LM semantics, restated).
 int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem, mi_ba_summary* sum) {
   Solver S;

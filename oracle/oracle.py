@@ -58,6 +58,8 @@ def load():
                                                C.POINTER(mi_ba.Semantic), C.c_int64, C.c_int, _i64p]
     lib.oracle_solve.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem), C.POINTER(mi_ba.Semantic),
                                  C.POINTER(mi_ba.Summary)]
+    lib.oracle_cholesky.restype = C.c_int
+    lib.oracle_cholesky.argtypes = [_dp, C.c_int]
     _lib = lib
     return lib
 
@@ -141,6 +143,14 @@ def semantic_eval(options, scene, semantic):
     lib.oracle_semantic_eval(C.byref(options), C.byref(p), C.byref(s), px.ctypes.data_as(_i32p),
                              st.ctypes.data_as(_i32p), r.ctypes.data_as(_dp), J.ctypes.data_as(_dp), n)
     return px, st, r, J
+
+
+def cholesky(A):
+    """Lower Cholesky factor of a symmetric matrix (the oracle's DENSE_SCHUR
+    factorisation).  Returns (L, info)."""
+    M = np.ascontiguousarray(A, dtype=np.float64).copy()
+    info = load().oracle_cholesky(M.ctypes.data_as(_dp), M.shape[0])
+    return np.tril(M), info
 
 
 def solve(options, scene, semantic=None):

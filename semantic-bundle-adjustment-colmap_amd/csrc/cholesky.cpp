@@ -29,7 +29,8 @@ constexpr int kSub = 64;
 constexpr int kPanelWaves = 8;  // waves per diag_panel_kernel workgroup
 
 __global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_kernel(double* __restrict__ A, int lda, int w, int mrows,
-                                                         int* __restrict__ info) {
+                                                         int* __restrict__ info, double* __restrict__ scratch,
+                                                         int koff) {
   // Column-major tiles in LDS, element (r, c) at [c * 64 + r]: lane r's
   // accesses are consecutive across a wave, L[c][j] reads are broadcasts.
   // kPanelWaves waves share the 64 rows: each takes every kPanelWaves-th
@@ -73,10 +74,14 @@ __global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_kernel(double* __
     __syncthreads();
   }
   if (blockIdx.x == 0) {
+    // the factored tile goes to scratch, not over A: the other workgroups of
+    // this launch may not have loaded the tile yet (diag_update_kernel's last
+    // workgroup copies it back)
 #pragma unroll
-    for (int c = wv; c < kSub; c += kPanelWaves)
-      if (lane < w && c < w && lane >= c) A[lane + (size_t)c * lda] = L[c * kSub + lane];
-    if (threadIdx.x == 0 && bad != 0 && bad <= w) info[0] = bad;
+    for (int c = wv; c < kSub; c += kPanelWaves) scratch[c * kSub + lane] = L[c * kSub + lane];
+    // first failing pivot of the block, 1-based (earlier sub-panels' launches
+    // have completed; later ones see it set and keep it)
+    if (threadIdx.x == 0 && bad != 0 && bad <= w && info[0] == 0) info[0] = koff + bad;
     return;
   }
   // x L' = a, right-looking over the columns of the lane's row; column c's
@@ -92,9 +97,21 @@ __global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_kernel(double* __
 
 // A22 (m x m, lower) -= P P', P = the m x w sub-panel left of A22 (column-
 // major, P[r + t*lda] = A22[r - w*lda ...]); tile (bi >= bj) per workgroup.
+// The workgroup after the last tile copies the factored w x w diagonal tile
+// from the scratch diag_panel_kernel parked it in back to `tile` (nothing in
+// this launch reads the tile).
 __global__ __launch_bounds__(256) void diag_update_kernel(double* __restrict__ A22, const double* __restrict__ P,
-                                                          int lda, int m, int w) {
+                                                          int lda, int m, int w, const double* __restrict__ scratch,
+                                                          double* __restrict__ tile) {
   __shared__ double sr[kSub * 33], sc[kSub * 33];
+  const int ntiles = ((m + kSub - 1) / kSub) * ((m + kSub - 1) / kSub + 1) / 2;
+  if ((int)blockIdx.x == ntiles) {
+    for (int e = threadIdx.x; e < kSub * kSub; e += 256) {
+      const int r = e & (kSub - 1), c = e / kSub;
+      if (r < w && c < w && r >= c) tile[r + (size_t)c * lda] = scratch[e];
+    }
+    return;
+  }
   // lower-triangle tile index -> (bi, bj), bi >= bj
   int t = blockIdx.x, bi = 0;
   while (t > bi) { t -= bi + 1; ++bi; }
@@ -136,26 +153,27 @@ __global__ __launch_bounds__(256) void diag_update_kernel(double* __restrict__ A
     }
 }
 
-rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info) {
+rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info, double* scratch) {
   hipStream_t s;
+  if (!scratch) return rocblas_status_invalid_pointer;
   if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
   if (hipMemsetAsync(info, 0, sizeof(int), s) != hipSuccess) return rocblas_status_internal_error;
   for (int k = 0; k < n; k += kSub) {
     const int w = std::min(kSub, n - k);
     const int m = n - k - w;  // rows (and columns) of the block after this sub-panel
     double* Akk = A + k + (size_t)k * lda;
-    hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s, Akk, lda, w, m, info);
-    if (m > 0) {
-      const int T = (m + kSub - 1) / kSub;
-      hipLaunchKernelGGL(diag_update_kernel, dim3(T * (T + 1) / 2), dim3(256), 0, s, Akk + w + (size_t)w * lda,
-                         Akk + w, lda, m, w);
-    }
+    hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s, Akk, lda, w, m,
+                       info, scratch, k);
+    // trailing tiles of the block + one workgroup writing the tile back
+    const int T = (m + kSub - 1) / kSub;
+    hipLaunchKernelGGL(diag_update_kernel, dim3(T * (T + 1) / 2 + 1), dim3(256), 0, s, Akk + w + (size_t)w * lda,
+                       Akk + w, lda, m, w, scratch, Akk);
   }
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
 
-rocblas_status potrf_leaf(rocblas_handle h, int n, double* A, int lda, int* info, bool own) {
-  if (own) return potrf_diag(h, n, A, lda, info);
+rocblas_status potrf_leaf(rocblas_handle h, int n, double* A, int lda, int* info, bool own, double* scratch) {
+  if (own) return potrf_diag(h, n, A, lda, info, scratch);
   return rocsolver_dpotrf(h, rocblas_fill_lower, n, A, lda, info);
 }
 
@@ -171,13 +189,13 @@ int split(int n) {
   return n1 < n ? n1 : n / 2;
 }
 
-rocblas_status factor(rocblas_handle h, int n, double* A, int lda, int*& info, bool own) {
-  if (n <= kLeaf) return potrf_leaf(h, n, A, lda, info++, own);
+rocblas_status factor(rocblas_handle h, int n, double* A, int lda, int*& info, bool own, double* scratch) {
+  if (n <= kLeaf) return potrf_leaf(h, n, A, lda, info++, own, scratch);
   const int n1 = split(n), n2 = n - n1;
   double* A11 = A;
   double* A21 = A + n1;
   double* A22 = A + n1 + (size_t)n1 * lda;
-  rocblas_status st = factor(h, n1, A11, lda, info, own);
+  rocblas_status st = factor(h, n1, A11, lda, info, own, scratch);
   if (st != rocblas_status_success) return st;
   const double one = 1.0, minus_one = -1.0;
   // A21 := A21 L11^-T
@@ -187,7 +205,7 @@ rocblas_status factor(rocblas_handle h, int n, double* A, int lda, int*& info, b
   // A22 := A22 - A21 A21'
   st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, n2, n1, &minus_one, A21, lda, &one, A22, lda);
   if (st != rocblas_status_success) return st;
-  return factor(h, n2, A22, lda, info, own);
+  return factor(h, n2, A22, lda, info, own, scratch);
 }
 
 int leaves(int n) { return n <= kLeaf ? 1 : leaves(split(n)) + leaves(n - split(n)); }
@@ -222,13 +240,14 @@ rocblas_status backward(rocblas_handle h, int n, const double* A, int lda, doubl
 // Right-looking blocked factorisation: per panel, dpotrf of the diagonal
 // block, dtrsm of the panel below it, then the trailing lower triangle
 // updated by dsyrk (or by dgemm per block column of width `panel`).
-rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg) {
+rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
+                              double* scratch) {
   const double one = 1.0, minus_one = -1.0;
   const int nb = cfg.panel;
   for (int k = 0; k < n; k += nb) {
     const int kb = std::min(nb, n - k);
     double* Akk = A + k + (size_t)k * lda;
-    rocblas_status st = potrf_leaf(h, kb, Akk, lda, info++, cfg.own_diag);
+    rocblas_status st = potrf_leaf(h, kb, Akk, lda, info++, cfg.own_diag, scratch);
     if (st != rocblas_status_success) return st;
     const int m = n - k - kb;
     if (m == 0) break;
@@ -254,37 +273,14 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
 
 // Look-ahead variant of factor_blocked (gemm update): as soon as panel k's
 // dgemm has updated block column k+1, the diagonal factor and dtrsm of panel
-// k+1 run on a side stream (own rocBLAS handle) while the rest of panel k's
-// trailing dgemm runs on the caller's stream; the next iteration's dgemm waits
-// on the side stream's event.  Hides the latency-bound diagonal factor behind
-// the MFMA update.  Side resources are created once per device.
-struct SideStream {
-  rocblas_handle h = nullptr;
-  hipStream_t s = nullptr;
-  hipEvent_t upd = nullptr, pan = nullptr;
-  std::vector<hipEvent_t> ev;  // one pair per panel: no event is re-recorded within a factorisation
-};
-
-SideStream* side_for_device() {
-  static SideStream sides[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  SideStream& ss = sides[dev];
-  if (!ss.h) {
-    if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&ss.upd, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&ss.pan, hipEventDisableTiming) != hipSuccess) return nullptr;
-    rocblas_handle h2;
-    if (rocblas_create_handle(&h2) != rocblas_status_success) return nullptr;
-    if (rocblas_set_stream(h2, ss.s) != rocblas_status_success) return nullptr;
-    ss.h = h2;
-  }
-  return &ss;
-}
-
-rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, bool own) {
+// k+1 run on the workspace's side stream (own rocBLAS handle) while the rest
+// of panel k's trailing dgemm runs on the caller's stream; the next
+// iteration's dgemm waits on the side stream's event.  Hides the latency-bound
+// diagonal factor behind the MFMA update.
+rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, bool own,
+                            double* scratch) {
   double* Akk = A + k + (size_t)k * lda;
-  rocblas_status st = potrf_leaf(h, kb, Akk, lda, info, own);
+  rocblas_status st = potrf_leaf(h, kb, Akk, lda, info, own, scratch);
   if (st != rocblas_status_success) return st;
   const int m = n - k - kb;
   if (m == 0) return st;
@@ -294,19 +290,24 @@ rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, 
 }
 
 rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
-                                SideStream& ss) {
+                                CholWorkspace& ws) {
   const double minus_one = -1.0, one = 1.0;
   const int nb = cfg.panel;
   hipStream_t s1;
   if (rocblas_get_stream(h, &s1) != rocblas_status_success) return rocblas_status_internal_error;
-  const size_t need = 2 * (size_t)((n + nb - 1) / nb);
-  while (ss.ev.size() < need) {
-    hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return rocblas_status_internal_error;
-    ss.ev.push_back(e);
-  }
-  rocblas_status st = panel_factor(h, n, A, lda, 0, std::min(nb, n), info, cfg.own_diag);
+  if (ws.ev.size() < 2 * (size_t)((n + nb - 1) / nb)) return rocblas_status_invalid_size;
+  double* scratch_main = ws.scratch;
+  double* scratch_side = ws.scratch + kSub * kSub;
+  rocblas_status st = panel_factor(h, n, A, lda, 0, std::min(nb, n), info, cfg.own_diag, scratch_main);
   if (st != rocblas_status_success) return st;
+  // On a failure after the side stream got work, the caller's stream waits
+  // for it (the caller may free A / info once its own stream is drained).
+  auto fail = [&](rocblas_status e) {
+    hipEvent_t last = ws.ev.back();
+    if (hipEventRecord(last, ws.side) != hipSuccess || hipStreamWaitEvent(s1, last, 0) != hipSuccess)
+      (void)hipStreamSynchronize(ws.side);
+    return e;
+  };
   for (int k = 0, kk = 0; k < n; k += nb, ++kk) {
     const int kb = std::min(nb, n - k);
     const int m = n - k - kb;
@@ -317,21 +318,21 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     const int jb0 = std::min(nb, m);
     st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, jb0, kb, &minus_one, Aik, lda, Aik,
                        lda, &one, T, lda);
-    if (st != rocblas_status_success) return st;
-    hipEvent_t upd = ss.ev[2 * kk], pan = ss.ev[2 * kk + 1];
-    if (hipEventRecord(upd, s1) != hipSuccess || hipStreamWaitEvent(ss.s, upd, 0) != hipSuccess)
-      return rocblas_status_internal_error;
-    st = panel_factor(ss.h, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag);
-    if (st != rocblas_status_success) return st;
-    if (hipEventRecord(pan, ss.s) != hipSuccess) return rocblas_status_internal_error;
+    if (st != rocblas_status_success) return fail(st);
+    hipEvent_t upd = ws.ev[2 * kk], pan = ws.ev[2 * kk + 1];
+    if (hipEventRecord(upd, s1) != hipSuccess || hipStreamWaitEvent(ws.side, upd, 0) != hipSuccess)
+      return fail(rocblas_status_internal_error);
+    st = panel_factor(ws.side_h, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag, scratch_side);
+    if (st != rocblas_status_success) return fail(st);
+    if (hipEventRecord(pan, ws.side) != hipSuccess) return fail(rocblas_status_internal_error);
     for (int j = jb0; j < m; j += nb) {
       const int jb = std::min(nb, m - j);
       st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m - j, jb, kb, &minus_one, Aik + j,
                          lda, Aik + j, lda, &one, T + j + (size_t)j * lda, lda);
-      if (st != rocblas_status_success) return st;
+      if (st != rocblas_status_success) return fail(st);
     }
     // panel k+1 is read by the next iteration's updates (and by the solve)
-    if (hipStreamWaitEvent(s1, pan, 0) != hipSuccess) return rocblas_status_internal_error;
+    if (hipStreamWaitEvent(s1, pan, 0) != hipSuccess) return fail(rocblas_status_internal_error);
   }
   return rocblas_status_success;
 }
@@ -343,14 +344,44 @@ int chol_leaf_count(int n, const CholConfig& cfg) {
   return cfg.panel > 0 ? (n + cfg.panel - 1) / cfg.panel : leaves(n);
 }
 
-rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg) {
-  if (n <= 0) return rocblas_status_success;
-  if (cfg.panel > 0 && cfg.gemm_update && cfg.lookahead) {
-    SideStream* ss = side_for_device();
-    if (ss) return factor_lookahead(h, n, A, lda, info, cfg, *ss);
+bool CholWorkspace::create(int dev, int max_panels) {
+  destroy();
+  device = dev;
+  if (hipSetDevice(dev) != hipSuccess) return false;
+  if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) { side = nullptr; return false; }
+  if (rocblas_create_handle(&side_h) != rocblas_status_success) { side_h = nullptr; return false; }
+  if (rocblas_set_stream(side_h, side) != rocblas_status_success) return false;
+  for (int k = 0; k < 2 * std::max(1, max_panels); ++k) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+    ev.push_back(e);
   }
-  if (cfg.panel > 0) return factor_blocked(h, n, A, lda, info, cfg);
-  return factor(h, n, A, lda, info, cfg.own_diag);
+  if (hipMalloc(&scratch, 2 * sizeof(double) * kSub * kSub) != hipSuccess) { scratch = nullptr; return false; }
+  return true;
+}
+
+void CholWorkspace::destroy() {
+  if (device >= 0) (void)hipSetDevice(device);
+  if (side) (void)hipStreamSynchronize(side);
+  for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  ev.clear();
+  if (side_h) (void)rocblas_destroy_handle(side_h);
+  side_h = nullptr;
+  if (side) (void)hipStreamDestroy(side);
+  side = nullptr;
+  if (scratch) (void)hipFree(scratch);
+  scratch = nullptr;
+}
+
+rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
+                           CholWorkspace* ws) {
+  if (n <= 0) return rocblas_status_success;
+  if (cfg.own_diag && (!ws || !ws->scratch)) return rocblas_status_invalid_pointer;
+  double* scratch = ws ? ws->scratch : nullptr;
+  if (cfg.panel > 0 && cfg.gemm_update && cfg.lookahead && ws && ws->side)
+    return factor_lookahead(h, n, A, lda, info, cfg, *ws);
+  if (cfg.panel > 0) return factor_blocked(h, n, A, lda, info, cfg, scratch);
+  return factor(h, n, A, lda, info, cfg.own_diag, scratch);
 }
 
 rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x) {

@@ -12,7 +12,10 @@
 // The solve recurses the same way (dtrsv leaves + dgemv).
 #pragma once
 
+#include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
+
+#include <vector>
 
 namespace miba {
 
@@ -22,17 +25,40 @@ namespace miba {
 struct CholConfig {
   int panel = 512;        // 0: recursive split; > 0: right-looking panel width
   bool gemm_update = true;
-  // panel k+1's diagonal factor + dtrsm on a side stream under panel k's dgemm
-  // (34.6 -> 30.4 ms at nf = 12 000); one event pair per panel — re-recording one
-  // event per iteration let a wait slip past its producer (a diverged C4 run)
+  // panel k+1's diagonal factor + dtrsm on the workspace's side stream under
+  // panel k's dgemm (34.6 -> 30.4 ms at nf = 12 000)
   bool lookahead = true;
   bool own_diag = true;   // diagonal blocks by the hand-written 64-wide factor, else rocsolver_dpotrf
 };
 
+// Device resources of one factorisation owner (one per mi_ba_context, created
+// on the context's device): the look-ahead side stream with its own rocBLAS
+// handle, one event pair per panel (no event is re-recorded within a
+// factorisation), and a scratch tile per stream for the hand-written diagonal
+// factor (the factored 64x64 tile is parked there and copied back by the next
+// launch, so no workgroup reads a tile another workgroup is overwriting).
+struct CholWorkspace {
+  int device = -1;
+  hipStream_t side = nullptr;
+  rocblas_handle side_h = nullptr;
+  std::vector<hipEvent_t> ev;
+  double* scratch = nullptr;  // [2][64*64]: [0] caller's stream, [1] side stream
+
+  // Creates the resources on `device` with events for up to `max_panels`
+  // panels; false on any HIP/rocBLAS failure (partially created resources are
+  // released by destroy()).
+  bool create(int device, int max_panels);
+  void destroy();
+};
+
 // In-place lower Cholesky of the n x n column-major matrix A (leading
-// dimension lda).  info[k] (device, one int per diagonal block, count from
-// chol_leaf_count) is 0 for every block of a positive-definite A.
-rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg = {});
+// dimension lda) on h's stream.  info[k] (device, one int per diagonal block,
+// count from chol_leaf_count) is 0 for every block of a positive-definite A.
+// ws is required for own_diag and for look-ahead; every exit path leaves no
+// work of this call pending on the side stream that h's stream does not wait
+// for.
+rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
+                           CholWorkspace* ws);
 int chol_leaf_count(int n, const CholConfig& cfg = {});
 // x := (L L')^-1 x with the factor chol_factor left in A.
 rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x);

@@ -96,6 +96,7 @@ struct mi_ba_context {
   int nptiles = 0;
   miba::DevArray<int32_t> info;
   miba::CholConfig chol;                   // factorisation variant (mi_ba_set_tuning)
+  miba::CholWorkspace cholws;              // side stream / handle / events / scratch of this context
 
   double fixed_cost = 0.0;
   miba::SemanticState* sem = nullptr;

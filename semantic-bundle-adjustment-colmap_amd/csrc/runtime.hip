@@ -416,6 +416,9 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
       if (st != MI_BA_OK) return fail(st);
       if (rocblas_create_handle(&ctx->blas) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
       if (rocblas_set_stream(ctx->blas, ctx->stream) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
+      // per-context look-ahead resources on this context's device (panel
+      // widths down to 64 allowed by mi_ba_set_tuning)
+      if (!ctx->cholws.create(ctx->device, (int)((d.nf + 63) / 64))) return fail(MI_BA_ERR_HIP);
       // Warm the factorisation at this size once: rocBLAS / rocSOLVER load the
       // code objects of every (shape, kernel) pair on first use, hundreds of ms
       // that would otherwise land inside the first LM iterations.
@@ -425,7 +428,8 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
         return fail(MI_BA_ERR_HIP);
       hipLaunchKernelGGL(identity_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, ctx->stream, ctx->S.ptr,
                          nf);
-      if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr, ctx->chol) != rocblas_status_success ||
+      if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr, ctx->chol, &ctx->cholws) !=
+              rocblas_status_success ||
           chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr) != rocblas_status_success ||
           hipStreamSynchronize(ctx->stream) != hipSuccess)
         return fail(MI_BA_ERR_HIP);
@@ -453,6 +457,7 @@ void context_destroy(mi_ba_context* ctx) {
     (void)hipEventDestroy(e.second.second);
   }
   for (auto e : ctx->timer.pool) (void)hipEventDestroy(e);
+  ctx->cholws.destroy();
   if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   if (ctx->host_scalars) (void)hipHostFree(ctx->host_scalars);
@@ -587,7 +592,8 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   timer_begin(ctx, "cholesky", &stop);
   // S holds the upper triangle row-major == the lower triangle column-major.
   const int leaves = chol_leaf_count((int)nf, ctx->chol);
-  if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr, ctx->chol) != rocblas_status_success)
+  if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr, ctx->chol, &ctx->cholws) !=
+      rocblas_status_success)
     return MI_BA_ERR_HIP;
   timer_end(ctx, stop);
   std::vector<int32_t> info(leaves, 0);
@@ -836,6 +842,15 @@ mi_ba_status context_writeback(mi_ba_context* ctx) {
 // ===========================================================================
 using namespace miba;
 
+// Every entry point that works on a context makes the context's device current
+// on the calling thread first (contexts on several devices may be driven from
+// one host thread).
+#define MI_BIND(ctx)                                               \
+  do {                                                             \
+    if (!(ctx)) return MI_BA_ERR_INVALID_ARGUMENT;                 \
+    if (hipSetDevice((ctx)->device) != hipSuccess) return MI_BA_ERR_HIP; \
+  } while (0)
+
 extern "C" {
 
 int32_t mi_ba_abi_version(void) { return MI_BA_ABI_VERSION; }
@@ -944,12 +959,12 @@ mi_ba_status mi_ba_context_create(const mi_ba_options* o, const mi_ba_problem* p
 void mi_ba_context_destroy(mi_ba_context* ctx) { context_destroy(ctx); }
 
 mi_ba_status mi_ba_linearize(mi_ba_context* ctx) {
-  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_BIND(ctx);
   return context_linearize(ctx, nullptr);
 }
 
 mi_ba_status mi_ba_evaluate_jacobian(mi_ba_context* ctx) {
-  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_BIND(ctx);
   const DevProblem& d = ctx->dev;
   hipEvent_t stop;
   launch_pack_images(d, ctx->img_rec.ptr, ctx->stream);
@@ -961,13 +976,13 @@ mi_ba_status mi_ba_evaluate_jacobian(mi_ba_context* ctx) {
 }
 
 mi_ba_status mi_ba_evaluate_semantic(mi_ba_context* ctx) {
-  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_BIND(ctx);
   if (!ctx->sem) return MI_BA_ERR_INVALID_ARGUMENT;
   return semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, true);
 }
 
 mi_ba_status mi_ba_synchronize(mi_ba_context* ctx) {
-  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_BIND(ctx);
   MI_HIP(hipStreamSynchronize(ctx->stream));
   return MI_BA_OK;
 }
@@ -981,7 +996,7 @@ mi_ba_status mi_ba_context_dims(const mi_ba_context* ctx, int64_t* nb, int32_t* 
 }
 
 mi_ba_status mi_ba_download_jacobian(mi_ba_context* ctx, int64_t* block_obs, double* residuals, double* jacobian) {
-  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_BIND(ctx);
   const int64_t nb = ctx->dev.nb;
   MI_HIP(hipStreamSynchronize(ctx->stream));
   if (block_obs) std::memcpy(block_obs, ctx->block_obs.data(), nb * sizeof(int64_t));
@@ -993,7 +1008,8 @@ mi_ba_status mi_ba_download_jacobian(mi_ba_context* ctx, int64_t* block_obs, dou
 
 mi_ba_status mi_ba_download_semantic(mi_ba_context* ctx, int32_t* sample_pixel, int32_t* status, double* residuals,
                                      double* jacobian) {
-  if (!ctx || !ctx->sem) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_BIND(ctx);
+  if (!ctx->sem) return MI_BA_ERR_INVALID_ARGUMENT;
   SemanticState* S = ctx->sem;
   MI_HIP(hipStreamSynchronize(ctx->stream));
   if (!S->samples_valid) return MI_BA_ERR_STATE;  // mi_ba_evaluate_semantic first
@@ -1007,17 +1023,19 @@ mi_ba_status mi_ba_download_semantic(mi_ba_context* ctx, int32_t* sample_pixel, 
 }
 
 mi_ba_status mi_ba_context_solve(mi_ba_context* ctx, mi_ba_summary* summary) {
-  if (!ctx || !summary) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (!summary) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_BIND(ctx);
   return context_solve(ctx, summary);
 }
 
 mi_ba_status mi_ba_context_writeback(mi_ba_context* ctx) {
-  if (!ctx) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_BIND(ctx);
   return context_writeback(ctx);
 }
 
 mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost) {
-  if (!ctx || !cost) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (!cost) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_BIND(ctx);
   hipStream_t s = ctx->stream;
   double* sc = ctx->scalars.ptr;
   MI_HIP(hipMemsetAsync(sc + kCandCost, 0, 8, s));
@@ -1105,6 +1123,75 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     return MI_BA_OK;
   }
   return MI_BA_ERR_INVALID_ARGUMENT;
+}
+
+mi_ba_status mi_ba_dense_cholesky(int32_t device, int32_t n, double* A, double* b, int32_t panel, int32_t lookahead,
+                                  int32_t own_diag, int32_t* info) {
+  if (n < 0 || !A || !info || (panel != 0 && (panel < 64 || panel > 4096)) || (lookahead != 0 && lookahead != 1) ||
+      (own_diag != 0 && own_diag != 1))
+    return MI_BA_ERR_INVALID_ARGUMENT;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MI_BA_ERR_NO_DEVICE;
+  if (device < 0 || device >= ndev) return MI_BA_ERR_INVALID_ARGUMENT;
+  MI_HIP(hipSetDevice(device));
+  *info = 0;
+  if (n == 0) return MI_BA_OK;
+  CholConfig cfg;
+  cfg.panel = panel;
+  cfg.lookahead = lookahead != 0;
+  cfg.own_diag = own_diag != 0;
+  // all resources are owned by this call: concurrent calls share nothing
+  hipStream_t s = nullptr;
+  rocblas_handle h = nullptr;
+  CholWorkspace ws;
+  DevArray<double> dA, dx;
+  DevArray<int32_t> dinfo;
+  const int nleaf = chol_leaf_count(n, cfg);
+  mi_ba_status st = MI_BA_OK;
+  std::vector<int32_t> hinfo(nleaf, 0);
+  do {
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { s = nullptr; st = MI_BA_ERR_HIP; break; }
+    if (rocblas_create_handle(&h) != rocblas_status_success) { h = nullptr; st = MI_BA_ERR_HIP; break; }
+    if (rocblas_set_stream(h, s) != rocblas_status_success || !ws.create(device, (n + 63) / 64)) {
+      st = MI_BA_ERR_HIP;
+      break;
+    }
+    if (dA.alloc((size_t)n * n) || dx.alloc(n) || dinfo.alloc(nleaf)) { st = MI_BA_ERR_OUT_OF_MEMORY; break; }
+    if (hipMemcpyAsync(dA.ptr, A, dA.bytes(), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(dinfo.ptr, 0, dinfo.bytes(), s) != hipSuccess ||
+        (b && hipMemcpyAsync(dx.ptr, b, dx.bytes(), hipMemcpyHostToDevice, s) != hipSuccess)) {
+      st = MI_BA_ERR_HIP;
+      break;
+    }
+    if (chol_factor(h, n, dA.ptr, n, dinfo.ptr, cfg, &ws) != rocblas_status_success) { st = MI_BA_ERR_HIP; break; }
+    if (hipMemcpyAsync(hinfo.data(), dinfo.ptr, dinfo.bytes(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      st = MI_BA_ERR_HIP;
+      break;
+    }
+    // first failing block: report its first column (1-based) like potrf
+    int64_t col0 = 0;
+    for (int k = 0; k < nleaf && *info == 0; ++k) {
+      const int width = cfg.panel > 0 ? std::min(cfg.panel, n - (int)col0) : 0;
+      if (hinfo[k] != 0) *info = (int32_t)(col0 + hinfo[k]);
+      col0 += width;
+    }
+    if (b && *info == 0 && chol_solve(h, n, dA.ptr, n, dx.ptr) != rocblas_status_success) { st = MI_BA_ERR_HIP; break; }
+    if (hipMemcpyAsync(A, dA.ptr, dA.bytes(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (b && hipMemcpyAsync(b, dx.ptr, dx.bytes(), hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      st = MI_BA_ERR_HIP;
+      break;
+    }
+  } while (false);
+  if (s) (void)hipStreamSynchronize(s);
+  ws.destroy();
+  if (h) (void)rocblas_destroy_handle(h);
+  dA.release();
+  dx.release();
+  dinfo.release();
+  if (s) (void)hipStreamDestroy(s);
+  return st;
 }
 
 mi_ba_status mi_ba_set_timing(mi_ba_context* ctx, int32_t enabled) {

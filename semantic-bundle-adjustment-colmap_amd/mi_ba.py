@@ -193,6 +193,7 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_comm_unique_id.argtypes = [C.c_char_p]
     lib.mi_ba_context_set_comm.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
     lib.mi_ba_context_set_host_reducer.argtypes = [C.c_void_p, C.c_int32, C.c_int32, HOST_ALLREDUCE_FN, C.c_void_p]
+    lib.mi_ba_dense_cholesky.argtypes = [C.c_int32, C.c_int32, _dp, _dp, C.c_int32, C.c_int32, C.c_int32, _i32p]
     _lib = lib
     return lib
 
@@ -367,6 +368,20 @@ def shard_scene(scene: "Scene", rank: int, world: int, semantic: Optional["Seman
         sem = SemanticInput(semantic.depth, semantic.label, np.asarray(semantic.pairs)[K * rank // world:K * (rank + 1) // world],
                             semantic.pixel_step, semantic.depth_error_threshold, semantic.numeric_relative_step_size)
     return sh, sem
+
+
+def dense_cholesky(A: np.ndarray, b: Optional[np.ndarray] = None, device: int = 0, panel: int = 512,
+                   lookahead: int = 1, own_diag: int = 1):
+    """mi_ba_dense_cholesky: the reduced-camera-system factorisation on a
+    caller-supplied SPD matrix.  Returns (L, x, info): L lower triangular
+    (strict upper zeroed), x the solution of A x = b (None without b)."""
+    n = A.shape[0]
+    F = np.asfortranarray(A, dtype=np.float64).copy(order="F")
+    x = None if b is None else np.ascontiguousarray(b, dtype=np.float64).copy()
+    info = C.c_int32(0)
+    check(load().mi_ba_dense_cholesky(device, n, F.ctypes.data_as(_dp), _ptr(x, _dp), panel, lookahead, own_diag,
+                                      C.byref(info)), "mi_ba_dense_cholesky")
+    return np.tril(F), x, info.value
 
 
 def device_count() -> int:

@@ -1,0 +1,142 @@
+"""The reduced-camera-system factorisation (csrc/cholesky.cpp) through
+mi_ba_dense_cholesky, against the oracle's dense Cholesky and LAPACK.
+
+Replaces the DENSE_SCHUR / SPARSE_SCHUR factorisation Ceres runs inside
+BundleAdjuster::Solve (src/optim/bundle_adjustment.cc:276-306; Ceres 2.1 is
+not vendored, so the oracle restates a plain column Cholesky).
+
+Tolerances (f64):
+  * look-ahead on vs off: bitwise identical L and info (same rocBLAS dgemm /
+    dtrsm shapes in the same order; only the stream a panel runs on differs)
+  * hand-written diagonal factor vs rocsolver_dpotrf, and vs the oracle /
+    LAPACK: max|dL| <= 1e-12 * max|L| (different summation orders)
+  * solve: max|dx| <= 1e-10 * max|x|
+  * concurrent factorisations from two host threads: bitwise equal to the
+    serial results (every call owns its stream, handles and workspace)
+Sizes span several 512-wide panels with a ragged last panel and ragged
+64-wide sub-panels (n = 1700 = 3 * 512 + 164, 2100).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import mi_ba
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def spd(n, seed=0):
+    rng = np.random.default_rng(seed)
+    G = rng.standard_normal((n, n // 2))
+    return G @ G.T / n + np.diag(rng.uniform(0.5, 2.0, n))
+
+
+@pytest.mark.parametrize("n", [1700, 2100])
+def test_lookahead_bitwise_equal(gpu, n):
+    A = spd(n, seed=n)
+    L0, _, i0 = mi_ba.dense_cholesky(A, lookahead=0)
+    L1, _, i1 = mi_ba.dense_cholesky(A, lookahead=1)
+    assert i0 == 0 and i1 == 0
+    assert np.array_equal(L0, L1)
+    # repeatable
+    L2, _, _ = mi_ba.dense_cholesky(A, lookahead=1)
+    assert np.array_equal(L1, L2)
+
+
+@pytest.mark.parametrize("n", [1700, 2100])
+def test_factor_matches_oracle_and_lapack(gpu, n):
+    A = spd(n, seed=7 + n)
+    b = np.random.default_rng(n).standard_normal(n)
+    L_o, info_o = oracle.cholesky(A)
+    assert info_o == 0
+    L_np = np.linalg.cholesky(A)
+    x_ref = np.linalg.solve(A, b)
+    scale = np.abs(L_o).max()
+    for own in (1, 0):
+        for panel in (512, 0):
+            L, x, info = mi_ba.dense_cholesky(A, b, panel=panel, own_diag=own)
+            assert info == 0
+            assert np.abs(L - L_o).max() <= 1e-12 * scale, (own, panel)
+            assert np.abs(L - L_np).max() <= 1e-12 * scale, (own, panel)
+            assert np.abs(x - x_ref).max() <= 1e-10 * np.abs(x_ref).max(), (own, panel)
+
+
+@pytest.mark.parametrize("col", [5, 700, 1663])
+def test_not_positive_definite_reports_column(gpu, col):
+    n = 1700
+    A = spd(n, seed=3)
+    A[col, col] = -1.0
+    _, info_o = oracle.cholesky(A)
+    assert info_o == col + 1
+    for own in (1, 0):
+        for la in (0, 1):
+            _, _, info = mi_ba.dense_cholesky(A, panel=512, lookahead=la, own_diag=own)
+            assert info == col + 1, (own, la, info)
+
+
+def test_concurrent_factorisations_share_nothing(gpu):
+    mats = [spd(1700, seed=s) for s in (11, 12, 13, 14)]
+    serial = [mi_ba.dense_cholesky(A, np.ones(1700)) for A in mats]
+    out = [None] * len(mats)
+
+    def run(k):
+        out[k] = mi_ba.dense_cholesky(mats[k], np.ones(1700))
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(len(mats))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    for k in range(len(mats)):
+        assert np.array_equal(out[k][0], serial[k][0]) and np.array_equal(out[k][1], serial[k][1])
+
+
+def test_two_contexts_two_threads(gpu):
+    """Two resident contexts solving at once on one device (each owns its
+    look-ahead side stream, rocBLAS handles and events) reach the results of
+    the same solves run one after the other."""
+    scenes = [mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 120, 3000, track_length=6,
+                                                      rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=s)).gauge()
+              for s in (21, 22)]
+    opts = mi_ba.default_options(max_num_iterations=6)
+
+    def solve(sc):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            return ctx.solve()
+
+    serial = [solve(sc) for sc in scenes]
+    out = [None, None]
+
+    def run(k):
+        out[k] = solve(scenes[k])
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    for a, b in zip(out, serial):
+        assert a.num_successful_steps == b.num_successful_steps
+        assert a.num_unsuccessful_steps == b.num_unsuccessful_steps
+        assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
+
+
+@pytest.mark.parametrize("images", [200])
+def test_lm_lookahead_on_off(gpu, images):
+    """LM at nf = 1593 (C2 shape, 4 panels): look-ahead on/off give the same
+    steps and final cost (within the run-to-run spread of the atomics-based
+    normal-equation build)."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, images, 20000, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=4)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for la in (0, 1):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            ctx.set_tuning("cholesky_lookahead", la)
+            res.append(ctx.solve())
+    a, b = res
+    assert a.num_successful_steps == b.num_successful_steps
+    assert a.num_unsuccessful_steps == b.num_unsuccessful_steps
+    assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
