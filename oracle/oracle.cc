@@ -15,8 +15,11 @@
 // that oracle beyond self-consistency.
 #include <algorithm>
 #include <cmath>
+#include <omp.h>
 #include <cstdint>
 #include <cstring>
+#include <cstdio>
+#include <cstdlib>
 #include <ctime>
 #include <map>
 #include <set>
@@ -505,6 +508,7 @@ bool Cholesky(std::vector<double>& A, int n) {  // in place, lower
     if (!(d > 0.0)) return false;
     d = std::sqrt(d);
     A[(size_t)j * n + j] = d;
+#pragma omp parallel for schedule(static) if (n - j > 256)
     for (int i = j + 1; i < n; ++i) {
       double v = A[(size_t)i * n + j];
       for (int k = 0; k < j; ++k) v -= A[(size_t)i * n + k] * A[(size_t)j * n + k];
@@ -536,12 +540,29 @@ bool Inv3(const double A[9], double Ai[9]) {
   return true;
 }
 
-// Sparse-row Jacobian of the whole reduced program.
+// Sparse-row Jacobian of the whole reduced program, flat: row k has fn[k]
+// f-block entries (column, value) at [k * kF, ...) and en[k] e-block
+// (point) entries at [k * 3, ...).
 struct Linearization {
+  static constexpr int kF = 16;
   std::vector<double> r;          // residuals (corrected)
-  struct Row { std::vector<std::pair<int64_t, double>> f; std::vector<std::pair<int64_t, double>> e; };
-  std::vector<Row> rows;
+  std::vector<int32_t> fcol;
+  std::vector<double> fval;
+  std::vector<uint8_t> fn;
+  std::vector<int64_t> ecol;
+  std::vector<double> eval;
+  std::vector<uint8_t> en;
   double cost = 0.0;              // 0.5 sum rho (reduced program only)
+  size_t rows() const { return r.size(); }
+  void resize(size_t n) {
+    r.assign(n, 0.0);
+    fcol.assign(n * kF, 0);
+    fval.assign(n * kF, 0.0);
+    fn.assign(n, 0);
+    ecol.assign(n * 3, 0);
+    eval.assign(n * 3, 0.0);
+    en.assign(n, 0);
+  }
 };
 
 struct Solver {
@@ -551,6 +572,7 @@ struct Solver {
   Setup s;
   SemSetup ss;
   Layout L;
+  std::vector<int64_t> reduced;   // reduced program blocks, program order
 
   double BlockCost(int64_t b) {
     double r[2];
@@ -568,71 +590,93 @@ struct Solver {
     LossEvaluate(o->loss_function_type, o->loss_function_scale, r * r, rho);
     return 0.5 * (o->semantic_weight * rho[0]);  // ScaledLoss(w)
   }
-  // Cost of the reduced program (Ceres adds fixed_cost separately).
+  // Cost of the reduced program (Ceres adds fixed_cost separately).  Terms
+  // are evaluated in parallel and summed in program order.
   double Cost() {
+    const int64_t nr = (int64_t)reduced.size(), ns = (int64_t)ss.samples.size();
+    std::vector<double> t(nr + (sem ? ns : 0));
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < nr; ++k) t[k] = BlockCost(reduced[k]);
+    if (sem) {
+#pragma omp parallel for schedule(dynamic, 1024)
+      for (int64_t n = 0; n < ns; ++n) t[nr + n] = SemCost(n);
+    }
     double c = 0.0;
-    for (size_t b = 0; b < s.block_obs.size(); ++b)
-      if (s.block_reduced[b]) c += BlockCost(b);
-    if (sem)
-      for (size_t n = 0; n < ss.samples.size(); ++n) c += SemCost(n);
+    for (double v : t) c += v;
     return c;
   }
   void Linearize(Linearization* lin) {
-    lin->r.clear(); lin->rows.clear(); lin->cost = 0.0;
     const int c = (int)s.cam_tangent.size();
-    std::vector<double> J(2 * (9 + c));
-    for (size_t b = 0; b < s.block_obs.size(); ++b) {
-      if (!s.block_reduced[b]) continue;
-      double r[2];
-      EvalBlock(s, p, b, r, J.data());
-      double rho[3];
-      const double sq = r[0] * r[0] + r[1] * r[1];
-      LossEvaluate(o->loss_function_type, o->loss_function_scale, sq, rho);
-      lin->cost += 0.5 * rho[0];
-      ApplyCorrector(rho, sq, 2, r, 9 + c, J.data());
-      const int64_t k = s.block_obs[b];
-      const int img = p->obs_image[k];
-      const int cam = p->image_camera[img];
-      const int64_t pt = p->obs_point[k];
-      for (int row = 0; row < 2; ++row) {
-        Linearization::Row R;
-        const double* Jr = &J[row * (9 + c)];
-        if (!s.block_const_pose[b] && L.img_off[img] >= 0)
-          for (int m = 0; m < 6; ++m) {
-            const int col = L.img_cols[(size_t)img * 6 + m];
-            if (col >= 0) R.f.push_back({col, Jr[m]});
-          }
-        if (L.cam_off[cam] >= 0)
-          for (int m = 0; m < c; ++m) R.f.push_back({L.cam_off[cam] + m, Jr[9 + m]});
-        if (L.pt_off[pt] >= 0)
-          for (int m = 0; m < 3; ++m) R.e.push_back({L.pt_off[pt] + m, Jr[6 + m]});
-        lin->rows.push_back(R);
-        lin->r.push_back(r[row]);
-      }
-    }
-    if (sem) {
-      for (size_t n = 0; n < ss.samples.size(); ++n) {
-        int st; double r; double Js[12];
-        EvalSemantic(p, s, sem, ss, n, &st, &r, Js);
+    const int64_t nr = (int64_t)reduced.size(), ns = sem ? (int64_t)ss.samples.size() : 0;
+    lin->resize(2 * nr + ns);
+    std::vector<double> cost(nr + ns);
+#pragma omp parallel
+    {
+      std::vector<double> J(2 * (9 + c));
+#pragma omp for schedule(static)
+      for (int64_t k = 0; k < nr; ++k) {
+        const int64_t b = reduced[k];
+        double r[2];
+        EvalBlock(s, p, b, r, J.data());
         double rho[3];
-        LossEvaluate(o->loss_function_type, o->loss_function_scale, r * r, rho);
-        for (int m = 0; m < 3; ++m) rho[m] *= o->semantic_weight;  // ScaledLoss
-        lin->cost += 0.5 * rho[0];
-        ApplyCorrector(rho, r * r, 1, &r, 12, Js);
-        const SemSample& smp = ss.samples[n];
-        Linearization::Row R;
-        for (int blk = 0; blk < 2; ++blk) {
-          const int img = sem->pairs[2 * smp.pair + blk];
-          if (L.img_off[img] < 0) continue;
-          for (int m = 0; m < 6; ++m) {
-            const int col = L.img_cols[(size_t)img * 6 + m];
-            if (col >= 0) R.f.push_back({col, Js[blk * 6 + m]});
+        const double sq = r[0] * r[0] + r[1] * r[1];
+        LossEvaluate(o->loss_function_type, o->loss_function_scale, sq, rho);
+        cost[k] = 0.5 * rho[0];
+        ApplyCorrector(rho, sq, 2, r, 9 + c, J.data());
+        const int64_t ob = s.block_obs[b];
+        const int img = p->obs_image[ob];
+        const int cam = p->image_camera[img];
+        const int64_t pt = p->obs_point[ob];
+        for (int row = 0; row < 2; ++row) {
+          const size_t R = 2 * (size_t)k + row;
+          const double* Jr = &J[row * (9 + c)];
+          int nf = 0;
+          if (!s.block_const_pose[b] && L.img_off[img] >= 0)
+            for (int m = 0; m < 6; ++m) {
+              const int col = L.img_cols[(size_t)img * 6 + m];
+              if (col >= 0) { lin->fcol[R * Linearization::kF + nf] = col; lin->fval[R * Linearization::kF + nf++] = Jr[m]; }
+            }
+          if (L.cam_off[cam] >= 0)
+            for (int m = 0; m < c; ++m) {
+              lin->fcol[R * Linearization::kF + nf] = L.cam_off[cam] + m;
+              lin->fval[R * Linearization::kF + nf++] = Jr[9 + m];
+            }
+          lin->fn[R] = (uint8_t)nf;
+          if (L.pt_off[pt] >= 0) {
+            for (int m = 0; m < 3; ++m) { lin->ecol[R * 3 + m] = L.pt_off[pt] + m; lin->eval[R * 3 + m] = Jr[6 + m]; }
+            lin->en[R] = 3;
           }
+          lin->r[R] = r[row];
         }
-        lin->rows.push_back(R);
-        lin->r.push_back(r);
+      }
+      if (sem) {
+#pragma omp for schedule(dynamic, 1024)
+        for (int64_t n = 0; n < ns; ++n) {
+          int st; double r; double Js[12];
+          EvalSemantic(p, s, sem, ss, n, &st, &r, Js);
+          double rho[3];
+          LossEvaluate(o->loss_function_type, o->loss_function_scale, r * r, rho);
+          for (int m = 0; m < 3; ++m) rho[m] *= o->semantic_weight;  // ScaledLoss
+          cost[nr + n] = 0.5 * rho[0];
+          ApplyCorrector(rho, r * r, 1, &r, 12, Js);
+          const SemSample& smp = ss.samples[n];
+          const size_t R = 2 * (size_t)nr + n;
+          int nf = 0;
+          for (int blk = 0; blk < 2; ++blk) {
+            const int img = sem->pairs[2 * smp.pair + blk];
+            if (L.img_off[img] < 0) continue;
+            for (int m = 0; m < 6; ++m) {
+              const int col = L.img_cols[(size_t)img * 6 + m];
+              if (col >= 0) { lin->fcol[R * Linearization::kF + nf] = col; lin->fval[R * Linearization::kF + nf++] = Js[blk * 6 + m]; }
+            }
+          }
+          lin->fn[R] = (uint8_t)nf;
+          lin->r[R] = r;
+        }
       }
     }
+    lin->cost = 0.0;
+    for (double v : cost) lin->cost += v;
   }
   // Apply tangent step delta (f then e coordinates) with manifold Plus.
   void Plus(const std::vector<double>& delta) {
@@ -776,6 +820,9 @@ int64_t oracle_semantic_eval(const mi_ba_options* o, mi_ba_problem* p, const mi_
   if (st) return -st;
   SemSetup ss;
   BuildSemSetup(o, p, s, sem, &ss);
+  // poses of semantic pairs carry their manifolds even without reprojection
+  // blocks (SetUpManifolds, semantic_bundle_adjustment.cc:670-693)
+  AddSemanticPoses(p, sem, ss, &s);
   const int64_t n = (int64_t)ss.samples.size();
   if (n > capacity) return n;
 #pragma omp parallel for schedule(dynamic, 256)
@@ -796,6 +843,7 @@ double oracle_semantic_throughput(const mi_ba_options* o, mi_ba_problem* p, cons
   if (BuildSetup(o, p, &s)) return -1.0;
   SemSetup ss;
   BuildSemSetup(o, p, s, sem, &ss);
+  AddSemanticPoses(p, sem, ss, &s);
   const int64_t n = std::min<int64_t>((int64_t)ss.samples.size(), max_samples);
   std::vector<double> r(n), J(12 * n);
   struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -844,6 +892,8 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
     AddSemanticPoses(p, sem, S.ss, &S.s);
   }
   BuildLayout(S.s, p, &S.L, sem, sem ? &S.ss : nullptr);
+  for (size_t b = 0; b < S.s.block_obs.size(); ++b)
+    if (S.s.block_reduced[b]) S.reduced.push_back((int64_t)b);
   sum->num_residuals_reduced = S.s.num_residuals_reduced + (int64_t)S.ss.samples.size();
   sum->num_effective_parameters_reduced = S.s.num_effective_parameters_reduced;
   sum->num_semantic_residuals = (int64_t)S.ss.samples.size();
@@ -863,9 +913,11 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
   sum->num_jacobian_evaluations = 1;
   // Jacobi scaling, computed once at iteration 0.
   std::vector<double> colnorm(n, 0.0);
-  for (auto& R : lin.rows) {
-    for (auto& e : R.f) colnorm[e.first] += e.second * e.second;
-    for (auto& e : R.e) colnorm[nf + e.first] += e.second * e.second;
+  constexpr int kF = Linearization::kF;
+  const size_t nrows = lin.rows();
+  for (size_t R = 0; R < nrows; ++R) {
+    for (int m = 0; m < lin.fn[R]; ++m) colnorm[lin.fcol[R * kF + m]] += lin.fval[R * kF + m] * lin.fval[R * kF + m];
+    for (int m = 0; m < lin.en[R]; ++m) colnorm[nf + lin.ecol[R * 3 + m]] += lin.eval[R * 3 + m] * lin.eval[R * 3 + m];
   }
   std::vector<double> scale(n);
   for (int64_t i = 0; i < n; ++i) scale[i] = 1.0 / (1.0 + std::sqrt(colnorm[i]));
@@ -877,6 +929,9 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
   int iteration = 0;
   sum->termination_type = MI_BA_NO_CONVERGENCE;
   const int64_t np3 = ne / 3;
+  std::vector<std::vector<double>> W(np3);
+  std::vector<std::vector<int>> Wcols(np3);
+  std::vector<int> wslot;  // [row][kF] slot of f entry in its point's W
   while (true) {
     if (iteration >= o->max_num_iterations) { sum->termination_type = MI_BA_NO_CONVERGENCE; break; }
     if (radius < 1e-32) { sum->termination_type = MI_BA_CONVERGENCE; break; }
@@ -884,9 +939,17 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
     // scaled Jacobian column norms -> LM diagonal
     if (!reuse_diagonal) {
       std::fill(diag.begin(), diag.end(), 0.0);
-      for (auto& R : lin.rows) {
-        for (auto& e : R.f) { const double v = e.second * scale[e.first]; diag[e.first] += v * v; }
-        for (auto& e : R.e) { const double v = e.second * scale[nf + e.first]; diag[nf + e.first] += v * v; }
+      for (size_t R = 0; R < nrows; ++R) {
+        for (int m = 0; m < lin.fn[R]; ++m) {
+          const int64_t col = lin.fcol[R * kF + m];
+          const double v = lin.fval[R * kF + m] * scale[col];
+          diag[col] += v * v;
+        }
+        for (int m = 0; m < lin.en[R]; ++m) {
+          const int64_t col = nf + lin.ecol[R * 3 + m];
+          const double v = lin.eval[R * 3 + m] * scale[col];
+          diag[col] += v * v;
+        }
       }
       for (auto& d : diag) d = std::min(std::max(d, 1e-6), 1e32);
     }
@@ -895,29 +958,67 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
     // Normal equations in scaled coordinates, Schur on points.
     std::vector<double> U((size_t)nf * nf, 0.0), g(n, 0.0);
     std::vector<double> V(np3 * 9, 0.0);
-    std::vector<std::vector<double>> W(np3);
-    std::vector<std::vector<int>> Wcols(np3);
-    for (size_t ri = 0; ri < lin.rows.size(); ++ri) {
-      const auto& R = lin.rows[ri];
-      const double rr = lin.r[ri];
-      for (auto& a : R.f) {
-        const double va = a.second * scale[a.first];
-        g[a.first] += va * rr;
-        for (auto& b2 : R.f) U[(size_t)a.first * nf + b2.first] += va * b2.second * scale[b2.first];
+    // U and g_f: threads own contiguous row ranges of U (row order of the
+    // serial loop per element)
+#pragma omp parallel
+    {
+      const int nt = omp_get_num_threads(), tid = omp_get_thread_num();
+      const int r0 = (int)((int64_t)nf * tid / nt), r1 = (int)((int64_t)nf * (tid + 1) / nt);
+      for (size_t R = 0; R < nrows; ++R) {
+        const double rr = lin.r[R];
+        const int32_t* fc = &lin.fcol[R * kF];
+        const double* fv = &lin.fval[R * kF];
+        const int nfr = lin.fn[R];
+        for (int x = 0; x < nfr; ++x) {
+          if (fc[x] < r0 || fc[x] >= r1) continue;
+          const double va = fv[x] * scale[fc[x]];
+          g[fc[x]] += va * rr;
+          for (int y = 0; y < nfr; ++y) U[(size_t)fc[x] * nf + fc[y]] += va * fv[y] * scale[fc[y]];
+        }
       }
-      if (R.e.empty()) continue;
-      const int64_t pt = R.e[0].first / 3;
-      for (auto& a : R.e) {
-        const double va = a.second * scale[nf + a.first];
-        g[nf + a.first] += va * rr;
-        for (auto& b2 : R.e) V[pt * 9 + (a.first % 3) * 3 + (b2.first % 3)] += va * b2.second * scale[nf + b2.first];
+    }
+    // e side (V, g_e, W): the row -> W-slot map depends on the structure
+    // only, built once; threads own contiguous point ranges (serial row
+    // order per element)
+    if (wslot.empty()) {
+      wslot.assign(nrows * kF, -1);
+      for (size_t R = 0; R < nrows; ++R) {
+        if (lin.en[R] == 0) continue;
+        const int64_t pt = lin.ecol[R * 3] / 3;
+        for (int x = 0; x < lin.fn[R]; ++x) {
+          const int32_t c = lin.fcol[R * kF + x];
+          int slot = -1;
+          for (size_t m = 0; m < Wcols[pt].size(); ++m) if (Wcols[pt][m] == c) { slot = (int)m; break; }
+          if (slot < 0) { slot = (int)Wcols[pt].size(); Wcols[pt].push_back((int)c); }
+          wslot[R * kF + x] = slot;
+        }
       }
-      for (auto& a : R.f) {
-        int slot = -1;
-        for (size_t m = 0; m < Wcols[pt].size(); ++m) if (Wcols[pt][m] == a.first) { slot = (int)m; break; }
-        if (slot < 0) { slot = (int)Wcols[pt].size(); Wcols[pt].push_back((int)a.first); W[pt].resize(W[pt].size() + 3, 0.0); }
-        const double va = a.second * scale[a.first];
-        for (auto& e : R.e) W[pt][slot * 3 + (e.first % 3)] += va * e.second * scale[nf + e.first];
+    }
+    for (int64_t pt = 0; pt < np3; ++pt) W[pt].assign(3 * Wcols[pt].size(), 0.0);
+#pragma omp parallel
+    {
+      const int nt = omp_get_num_threads(), tid = omp_get_thread_num();
+      const int64_t p0 = np3 * tid / nt, p1 = np3 * (tid + 1) / nt;
+      for (size_t R = 0; R < nrows; ++R) {
+        if (lin.en[R] == 0) continue;
+        const int64_t* ec = &lin.ecol[R * 3];
+        const int64_t pt = ec[0] / 3;
+        if (pt < p0 || pt >= p1) continue;
+        const double rr = lin.r[R];
+        const int32_t* fc = &lin.fcol[R * kF];
+        const double* fv = &lin.fval[R * kF];
+        const int nfr = lin.fn[R];
+        const double* ev = &lin.eval[R * 3];
+        for (int x = 0; x < 3; ++x) {
+          const double va = ev[x] * scale[nf + ec[x]];
+          g[nf + ec[x]] += va * rr;
+          for (int y = 0; y < 3; ++y) V[pt * 9 + (ec[x] % 3) * 3 + (ec[y] % 3)] += va * ev[y] * scale[nf + ec[y]];
+        }
+        for (int x = 0; x < nfr; ++x) {
+          const int slot = wslot[R * kF + x];
+          const double va = fv[x] * scale[fc[x]];
+          for (int y = 0; y < 3; ++y) W[pt][slot * 3 + (ec[y] % 3)] += va * ev[y] * scale[nf + ec[y]];
+        }
       }
     }
     for (int i = 0; i < nf; ++i) U[(size_t)i * nf + i] += D2[i];
@@ -927,27 +1028,47 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
       for (int m = 0; m < 3; ++m) V[pt * 9 + m * 4] += D2[nf + pt * 3 + m];
       if (!Inv3(&V[pt * 9], &Vinv[pt * 9])) ok = false;
     }
-    // S = U - sum W Vinv W^T ; rhs = g_f - sum W Vinv g_e
+    // S = U - sum W Vinv W^T ; rhs = g_f - sum W Vinv g_e.  Every element
+    // of S is updated in point order; threads own contiguous row ranges of S,
+    // so the arithmetic is that of the serial loop.
     std::vector<double> Sm = U, rhs(g.begin(), g.begin() + nf);
-    for (int64_t pt = 0; pt < np3 && ok; ++pt) {
-      const auto& cols = Wcols[pt];
-      const size_t m = cols.size();
-      std::vector<double> WV(m * 3, 0.0);
-      for (size_t a = 0; a < m; ++a)
-        for (int c2 = 0; c2 < 3; ++c2) {
-          double acc = 0.0;
-          for (int k = 0; k < 3; ++k) acc += W[pt][a * 3 + k] * Vinv[pt * 9 + k * 3 + c2];
-          WV[a * 3 + c2] = acc;
+    std::vector<std::vector<double>> WV(np3);
+    if (ok) {
+#pragma omp parallel for schedule(static)
+      for (int64_t pt = 0; pt < np3; ++pt) {
+        const size_t m = Wcols[pt].size();
+        WV[pt].assign(m * 3, 0.0);
+        for (size_t a = 0; a < m; ++a)
+          for (int c2 = 0; c2 < 3; ++c2) {
+            double acc = 0.0;
+            for (int k = 0; k < 3; ++k) acc += W[pt][a * 3 + k] * Vinv[pt * 9 + k * 3 + c2];
+            WV[pt][a * 3 + c2] = acc;
+          }
+      }
+#pragma omp parallel
+      {
+        const int nt = omp_get_num_threads(), tid = omp_get_thread_num();
+        const int r0 = (int)((int64_t)nf * tid / nt), r1 = (int)((int64_t)nf * (tid + 1) / nt);
+        for (int64_t pt = 0; pt < np3; ++pt) {
+          const auto& cols = Wcols[pt];
+          const size_t m = cols.size();
+          for (size_t a = 0; a < m; ++a) {
+            if (cols[a] < r0 || cols[a] >= r1) continue;
+            for (size_t b2 = 0; b2 < m; ++b2) {
+              double acc = 0.0;
+              for (int k = 0; k < 3; ++k) acc += WV[pt][a * 3 + k] * W[pt][b2 * 3 + k];
+              Sm[(size_t)cols[a] * nf + cols[b2]] -= acc;
+            }
+          }
         }
-      for (size_t a = 0; a < m; ++a) {
-        for (size_t b2 = 0; b2 < m; ++b2) {
+      }
+      for (int64_t pt = 0; pt < np3; ++pt) {
+        const auto& cols = Wcols[pt];
+        for (size_t a = 0; a < cols.size(); ++a) {
           double acc = 0.0;
-          for (int k = 0; k < 3; ++k) acc += WV[a * 3 + k] * W[pt][b2 * 3 + k];
-          Sm[(size_t)cols[a] * nf + cols[b2]] -= acc;
+          for (int k = 0; k < 3; ++k) acc += WV[pt][a * 3 + k] * g[nf + pt * 3 + k];
+          rhs[cols[a]] -= acc;
         }
-        double acc = 0.0;
-        for (int k = 0; k < 3; ++k) acc += WV[a * 3 + k] * g[nf + pt * 3 + k];
-        rhs[cols[a]] -= acc;
       }
     }
     std::vector<double> step(n, 0.0);
@@ -955,6 +1076,7 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
     if (ok) {
       if (nf > 0) CholSolve(Sm, nf, rhs);
       for (int i = 0; i < nf; ++i) step[i] = rhs[i];
+#pragma omp parallel for schedule(static)
       for (int64_t pt = 0; pt < np3; ++pt) {
         double t3[3];
         for (int k = 0; k < 3; ++k) t3[k] = g[nf + pt * 3 + k];
@@ -972,13 +1094,16 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
     reuse_diagonal = true;
     double model_cost_change = 0.0;
     if (ok) {
-      for (size_t ri = 0; ri < lin.rows.size(); ++ri) {
-        const auto& R = lin.rows[ri];
+      std::vector<double> mc(nrows);
+#pragma omp parallel for schedule(static)
+      for (size_t R = 0; R < nrows; ++R) {
         double mr = 0.0;
-        for (auto& e : R.f) mr += e.second * scale[e.first] * step[e.first];
-        for (auto& e : R.e) mr += e.second * scale[nf + e.first] * step[nf + e.first];
-        model_cost_change += -(mr * (lin.r[ri] + mr / 2.0));
+        for (int m = 0; m < lin.fn[R]; ++m) mr += lin.fval[R * kF + m] * scale[lin.fcol[R * kF + m]] * step[lin.fcol[R * kF + m]];
+        for (int m = 0; m < lin.en[R]; ++m)
+          mr += lin.eval[R * 3 + m] * scale[nf + lin.ecol[R * 3 + m]] * step[nf + lin.ecol[R * 3 + m]];
+        mc[R] = -(mr * (lin.r[R] + mr / 2.0));
       }
+      for (double v : mc) model_cost_change += v;
       ok = model_cost_change > 0.0;
     }
     if (!ok) {
