@@ -2,10 +2,12 @@
 """bench.py — residuals+Jacobians/sec of the semantic-BA hot path on MI355X.
 
 A step is one full linearization of the BASELINE.json workload already
-resident in HBM: every reprojection residual block (residual + tangent
-Jacobian, loss-corrected, point blocks V_p/g_p reduced) and every semantic
-sample (residual + 29-point CENTRAL numeric-diff Jacobian, pair blocks
-reduced) — mi_ba_linearize on the context's stream.
+resident in HBM: every reprojection residual block (residual + loss-corrected
+tangent Jacobian, written to HBM) and every semantic sample (residual +
+29-point CENTRAL numeric-diff Jacobian, reduced into the per-pair J'J / J'r
+blocks) — mi_ba_linearize on the context's stream.  The point and camera
+normal-equation blocks are reduced by the LM's own passes (timed in the
+BA-iteration figures), not inside the step.
 
 value = (reprojection blocks + semantic samples, all ranks) * steps / max-over-
 ranks wall time of the timed steps.  Multi-GPU: the linearization shards by
@@ -104,26 +106,79 @@ def build_shard(cfg, rank, world, scaling="weak"):
     return sc, sem
 
 
+def host_cpu():
+    """CPU model, logical CPUs of the machine and of this process's affinity mask."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, affinity
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: the CPUs this process may use.  On the
+    GPU boxes the job's CPU share is exported as OMP_NUM_THREADS (16 per GPU)
+    while nproc reports the whole host; the share is what the baseline gets."""
+    _, nproc, affinity = host_cpu()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(affinity, share) if share > 0 else affinity
+
+
+def cpu_ba_iteration(iters=3):
+    """CPU BA-iteration wall time of the oracle's LM (dense Schur, 'port',
+    not Ceres) on C2, and the GPU's on the same problem."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    c = CONFIGS["C2"]
+    sc = mi_ba.generate_scene(mi_ba.synth_config(c["model"], c["images"], c["points"], track_length=c["track"],
+                                                 rotation_range=0.05, extra=c["extra"])).gauge()
+    opts = mi_ba.default_options(max_num_iterations=iters)
+    t0 = time.perf_counter()
+    s0 = oracle.solve(mi_ba.default_options(max_num_iterations=0), sc.copy())
+    t_setup = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    s = oracle.solve(opts, sc.copy())
+    wall = time.perf_counter() - t0 - t_setup
+    its = max(1, s.num_successful_steps + s.num_unsuccessful_steps)
+    with mi_ba.Context(opts, sc.copy()) as ctx:  # solve time only (context setup excluded, as for the CPU)
+        g = ctx.solve()
+    g_its = max(1, g.num_successful_steps + g.num_unsuccessful_steps)
+    return {"workload": "C2: 200 cams / 50k points / 500k obs, SIMPLE_RADIAL, exact Schur LM",
+            "cpu_ms": 1e3 * wall / its, "cpu_kind": "port (oracle/ C++/OpenMP dense-Schur LM, not Ceres)",
+            "gpu_ms": 1e3 * g.total_time_in_seconds / g_its, "iterations": its,
+            "cpu_final_cost": s.final_cost, "gpu_final_cost": g.final_cost}
+
+
 def cpu_baseline(opts, sc, sem, cfg, nb, ns):
     """The CPU restatement (oracle, 'port') timed on this host on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = min(threads, 16)
-    geo_blocks = min(nb, 4_000_000)
+    threads = cpu_threads()
+    geo_blocks = nb  # the whole workload: ~1.5 s wall x 16 threads
     t_geo, done_geo = oracle.reproj_throughput(opts, sc, geo_blocks, 1, threads)
     rate_geo = done_geo / t_geo
     sample = f"{done_geo} reprojection blocks"
     total_time = nb / rate_geo
     rate_sem = None
     if sem is not None and ns:
-        t_sem, done_sem = oracle.semantic_throughput(opts, sc, sem, min(ns, 400_000), threads)
+        t_sem, done_sem = oracle.semantic_throughput(opts, sc, sem, ns, threads)
         rate_sem = done_sem / t_sem
         total_time += ns / rate_sem
         sample += f" + {done_sem} semantic samples"
+    model, nproc, affinity = host_cpu()
     return {"value": (nb + ns) / total_time, "unit": "residual_blocks/s", "cores": threads, "kind": "port",
             "sample": sample + " of the same workload, oracle/ CPU restatement (C++/OpenMP, f64), not Ceres",
-            "reproj_blocks_per_s": rate_geo, "semantic_samples_per_s": rate_sem}
+            "reproj_blocks_per_s": rate_geo, "semantic_samples_per_s": rate_sem,
+            "cpu_model": model, "host_nproc": nproc, "affinity_cpus": affinity,
+            "threads_note": "threads = the job's CPU share (OMP_NUM_THREADS on the GPU box), capped by the affinity mask"}
 
 
 def main():
@@ -234,8 +289,10 @@ def main():
         s = ctx_lm.solve()
         its = max(1, s.num_successful_steps + s.num_unsuccessful_steps)
         lm = {"ba_iteration_ms": allreduce_max(1e3 * s.total_time_in_seconds / its), "iterations": its,
-              "ba_iteration_workload": ((f"C5: {args.config} point-sharded across {world} ranks, S summed by " + ("RCCL all-reduce" if ap_backend == "nccl" else "gloo host reducer")) if world > 1
-                                        else f"{args.config} on one GPU"),
+              "ba_iteration_workload": (((("C5 = " if args.config == "C4" else "") +
+                                          f"{args.config} point-sharded across {world} ranks, S summed by ") +
+                                         ("RCCL all-reduce" if ap_backend == "nccl" else "gloo host reducer"))
+                                        if world > 1 else f"{args.config} on one GPU"),
               "linear_solver_iterations": s.num_linear_solver_iterations,
               "initial_cost": s.initial_cost, "final_cost": s.final_cost,
               "lm_phase_ms_calls": {k: list(ctx_lm.kernel_time(k)) for k in
@@ -283,6 +340,7 @@ def main():
             out.update(lm)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(opts, sc, sem, cfg, nb, ns)
+            out["ba_iteration_c2"] = cpu_ba_iteration()
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
