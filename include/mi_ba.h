@@ -284,7 +284,7 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *                           30-35 occupancy study (tools/ab_jacobian.py)
  *   "cholesky_panel"        0 recursive split, 64..4096 right-looking panel width
  *   "cholesky_gemm_update"  0 dsyrk / 1 dgemm trailing update
- *   "cholesky_own_diag"     1 hand-written diagonal-block factor / 0 rocsolver_dpotrf
+ *   "cholesky_own_diag"     1 hand-written diagonal-block factor (default) / 0 rocsolver_dpotrf
  *   "cholesky_lookahead"    1 side-stream look-ahead (default) / 0 serial */
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value);
 

@@ -162,8 +162,8 @@ rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info
     const int w = std::min(kSub, n - k);
     const int m = n - k - w;  // rows (and columns) of the block after this sub-panel
     double* Akk = A + k + (size_t)k * lda;
-    hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s, Akk, lda, w, m,
-                       info, scratch, k);
+    hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s, Akk, lda, w,
+                       m, info, scratch, k);
     // trailing tiles of the block + one workgroup writing the tile back
     const int T = (m + kSub - 1) / kSub;
     hipLaunchKernelGGL(diag_update_kernel, dim3(T * (T + 1) / 2 + 1), dim3(256), 0, s, Akk + w + (size_t)w * lda,
@@ -172,7 +172,7 @@ rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
 
-rocblas_status potrf_leaf(rocblas_handle h, int n, double* A, int lda, int* info, bool own, double* scratch) {
+rocblas_status potrf_leaf(rocblas_handle h, int n, double* A, int lda, int* info, int own, double* scratch) {
   if (own) return potrf_diag(h, n, A, lda, info, scratch);
   return rocsolver_dpotrf(h, rocblas_fill_lower, n, A, lda, info);
 }
@@ -189,7 +189,7 @@ int split(int n) {
   return n1 < n ? n1 : n / 2;
 }
 
-rocblas_status factor(rocblas_handle h, int n, double* A, int lda, int*& info, bool own, double* scratch) {
+rocblas_status factor(rocblas_handle h, int n, double* A, int lda, int*& info, int own, double* scratch) {
   if (n <= kLeaf) return potrf_leaf(h, n, A, lda, info++, own, scratch);
   const int n1 = split(n), n2 = n - n1;
   double* A11 = A;
@@ -277,7 +277,7 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
 // of panel k's trailing dgemm runs on the caller's stream; the next
 // iteration's dgemm waits on the side stream's event.  Hides the latency-bound
 // diagonal factor behind the MFMA update.
-rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, bool own,
+rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, int own,
                             double* scratch) {
   double* Akk = A + k + (size_t)k * lda;
   rocblas_status st = potrf_leaf(h, kb, Akk, lda, info, own, scratch);

@@ -28,7 +28,12 @@ struct CholConfig {
   // panel k+1's diagonal factor + dtrsm on the workspace's side stream under
   // panel k's dgemm (34.6 -> 30.4 ms at nf = 12 000)
   bool lookahead = true;
-  bool own_diag = true;   // diagonal blocks by the hand-written 64-wide factor, else rocsolver_dpotrf
+  // diagonal blocks: 1 hand-written 64-wide sub-panels (eight-wave LDS tile
+  // factor, diag_panel_kernel), 0 rocsolver_dpotrf.  (Measured dead ends,
+  // a four-wave register-resident tile factor with one barrier
+  // per pivot ran 80 us per sub-panel vs 69; a fully unrolled one-wave
+  // register factor ~300 us, instruction-fetch bound.)
+  int own_diag = 1;
 };
 
 // Device resources of one factorisation owner (one per mi_ba_context, created

@@ -1115,7 +1115,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_own_diag") == 0 && (value == 0 || value == 1)) {
-    ctx->chol.own_diag = value != 0;
+    ctx->chol.own_diag = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_gemm_update") == 0 && (value == 0 || value == 1)) {
@@ -1139,7 +1139,7 @@ mi_ba_status mi_ba_dense_cholesky(int32_t device, int32_t n, double* A, double* 
   CholConfig cfg;
   cfg.panel = panel;
   cfg.lookahead = lookahead != 0;
-  cfg.own_diag = own_diag != 0;
+  cfg.own_diag = own_diag;
   // all resources are owned by this call: concurrent calls share nothing
   hipStream_t s = nullptr;
   rocblas_handle h = nullptr;
