@@ -34,6 +34,7 @@ struct CholConfig {
   // per pivot ran 80 us per sub-panel vs 69; a fully unrolled one-wave
   // register factor ~300 us, instruction-fetch bound.)
   int own_diag = 1;
+  int solve = 1;          // chol_solve variant: 1 blocked sweeps, 0 recursive rocBLAS dtrsv / dgemv
 };
 
 // Device resources of one factorisation owner (one per mi_ba_context, created
@@ -48,11 +49,15 @@ struct CholWorkspace {
   rocblas_handle side_h = nullptr;
   std::vector<hipEvent_t> ev;
   double* scratch = nullptr;  // [2][64*64]: [0] caller's stream, [1] side stream
+  double* linv = nullptr;     // [n/64][64*64] inverses of the factor's 64x64 diagonal blocks (chol_solve)
+  double* ybuf = nullptr;     // [n] intermediate vector of chol_solve (L y = b)
+  int linv_rows = 0;
 
   // Creates the resources on `device` with events for up to `max_panels`
-  // panels; false on any HIP/rocBLAS failure (partially created resources are
-  // released by destroy()).
-  bool create(int device, int max_panels);
+  // panels and diagonal-block inverses for matrices up to max_n; false on any
+  // HIP/rocBLAS failure (partially created resources are released by
+  // destroy()).
+  bool create(int device, int max_panels, int max_n);
   void destroy();
 };
 
@@ -65,7 +70,11 @@ struct CholWorkspace {
 rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
                            CholWorkspace* ws);
 int chol_leaf_count(int n, const CholConfig& cfg = {});
-// x := (L L')^-1 x with the factor chol_factor left in A.
-rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x);
+// x := (L L')^-1 x with the factor chol_factor left in A, on h's stream.
+// variant 1 (default): the hand-written blocked forward / backward sweeps
+// (one launch per 64-wide block column, diagonal blocks by their inverses in
+// ws); 0: recursive rocBLAS dtrsv + dgemv (ws unused).
+rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x, int variant,
+                          CholWorkspace* ws);
 
 }  // namespace miba

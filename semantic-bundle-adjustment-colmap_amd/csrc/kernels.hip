@@ -329,8 +329,10 @@ __device__ inline void wave_load_rows(const double* __restrict__ src, double* __
 // path without the Corrector.  D: diagnostic builds for the roofline
 // decomposition (1 = no J store, 2 = no arithmetic); never used by the LM.
 // Build options (bits of D): 8 nontemporal J stores, 16 nontemporal obs
-// loads and r stores, 32 16-B J stores; 1 and 2 are the diagnostic builds.
-constexpr int kJacProduction = 8 | 16 | 32;
+// loads and r stores, 32 16-B J stores, 128 per-block loads issued up front;
+// 1 and 2 are the diagnostic builds.
+constexpr int kJacProduction = 8 | 16 | 32 | 128;
+constexpr int kJacR1 = 8 | 16 | 32;  // round-1 production (three serial round trips), A/B variant 23
 template <int M, int RF, int LOSS, int NP, int D = kJacProduction, int WPE = 4>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
                                                                  double* __restrict__ J_out,
@@ -375,7 +377,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // records are handed out through the wave's LDS slab.
     const bool live = i < p.nb;
     uint32_t img = 0u;
+    // D & 128: every per-block input is requested up front (image, point,
+    // observation), the point gathers as soon as the point index lands, so
+    // they overlap the image-record fetch: two dependent memory round trips
+    // before the arithmetic instead of three.
+    uint32_t pt_e = 0u;
+    double2 o_e = make_double2(0.0, 0.0);
+    double X_e[3] = {0.0, 0.0, 0.0};
+    bool ptv_e = false;
     if (live) img = (D & 16) ? __builtin_nontemporal_load(p.obs_img + i) : p.obs_img[i];
+    if constexpr ((D & 128) != 0) {
+      if (live) {
+        pt_e = __builtin_nontemporal_load(p.obs_pt + i);
+        const dvec2 ov = __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(p.obs_xy) + i);
+        o_e = make_double2(ov.x, ov.y);
+        X_e[0] = p.X[3 * (size_t)pt_e];
+        X_e[1] = p.X[3 * (size_t)pt_e + 1];
+        X_e[2] = p.X[3 * (size_t)pt_e + 2];
+        ptv_e = p.pt_var[pt_e] != 0;
+      }
+    }
     if constexpr ((D & 4) != 0) img &= 127u;  // diagnostic: L1-resident record working set
     double q[4], t[3], prm[np];
     uint32_t meta;
@@ -414,18 +435,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     }
     if (live) {
       double2 o;
-      if constexpr ((D & 16) != 0) {
-        const dvec2 ov = __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(p.obs_xy) + i);
-        o = make_double2(ov.x, ov.y);
+      uint32_t pt;
+      bool ptv;
+      double X[3];
+      if constexpr ((D & 128) != 0) {
+        o = o_e;
+        pt = pt_e;
+        ptv = ptv_e;
+        X[0] = X_e[0]; X[1] = X_e[1]; X[2] = X_e[2];
       } else {
-        o = p.obs_xy[i];
+        if constexpr ((D & 16) != 0) {
+          const dvec2 ov = __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(p.obs_xy) + i);
+          o = make_double2(ov.x, ov.y);
+        } else {
+          o = p.obs_xy[i];
+        }
+        pt = (D & 16) ? __builtin_nontemporal_load(p.obs_pt + i) : p.obs_pt[i];
+        ptv = p.pt_var[pt] != 0;
+        X[0] = p.X[3 * (size_t)pt]; X[1] = p.X[3 * (size_t)pt + 1]; X[2] = p.X[3 * (size_t)pt + 2];
       }
-      const uint32_t pt = (D & 16) ? __builtin_nontemporal_load(p.obs_pt + i) : p.obs_pt[i];
+      (void)pt;
       flags = meta & 0xffu;
       pose_var = flags & 1u;
       cv = (meta >> 8) & 1u;
-      const bool ptv = p.pt_var[pt] != 0;
-      const double X[3] = {p.X[3 * (size_t)pt], p.X[3 * (size_t)pt + 1], p.X[3 * (size_t)pt + 2]};
       double P[3];
       unit_quat_rotate(q, X, P);
       P[0] += t[0];
@@ -1467,6 +1499,10 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
               return;
             case 21:
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, 24>), dim3(g), dim3(kBlock), 0, s, p, r, J,
+                                 cost_partial);
+              return;
+            case 23:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacR1>), dim3(g), dim3(kBlock), 0, s, p, r, J,
                                  cost_partial);
               return;
             case 22:

@@ -418,7 +418,7 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
       if (rocblas_set_stream(ctx->blas, ctx->stream) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
       // per-context look-ahead resources on this context's device (panel
       // widths down to 64 allowed by mi_ba_set_tuning)
-      if (!ctx->cholws.create(ctx->device, (int)((d.nf + 63) / 64))) return fail(MI_BA_ERR_HIP);
+      if (!ctx->cholws.create(ctx->device, (int)((d.nf + 63) / 64), (int)d.nf)) return fail(MI_BA_ERR_HIP);
       // Warm the factorisation at this size once: rocBLAS / rocSOLVER load the
       // code objects of every (shape, kernel) pair on first use, hundreds of ms
       // that would otherwise land inside the first LM iterations.
@@ -430,7 +430,7 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
                          nf);
       if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr, ctx->chol, &ctx->cholws) !=
               rocblas_status_success ||
-          chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr) != rocblas_status_success ||
+          chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr, ctx->chol.solve, &ctx->cholws) != rocblas_status_success ||
           hipStreamSynchronize(ctx->stream) != hipSuccess)
         return fail(MI_BA_ERR_HIP);
     }
@@ -607,7 +607,7 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   }
   {
     Phase ph_(ctx, "cholesky_solve");
-    if (chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr) != rocblas_status_success)
+    if (chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr, ctx->chol.solve, &ctx->cholws) != rocblas_status_success)
       return MI_BA_ERR_HIP;
   }
   return MI_BA_OK;
@@ -1118,6 +1118,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.own_diag = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "cholesky_solve") == 0 && (value == 0 || value == 1)) {
+    ctx->chol.solve = value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_gemm_update") == 0 && (value == 0 || value == 1)) {
     ctx->chol.gemm_update = value != 0;
     return MI_BA_OK;
@@ -1152,7 +1156,7 @@ mi_ba_status mi_ba_dense_cholesky(int32_t device, int32_t n, double* A, double* 
   do {
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { s = nullptr; st = MI_BA_ERR_HIP; break; }
     if (rocblas_create_handle(&h) != rocblas_status_success) { h = nullptr; st = MI_BA_ERR_HIP; break; }
-    if (rocblas_set_stream(h, s) != rocblas_status_success || !ws.create(device, (n + 63) / 64)) {
+    if (rocblas_set_stream(h, s) != rocblas_status_success || !ws.create(device, (n + 63) / 64, n)) {
       st = MI_BA_ERR_HIP;
       break;
     }
@@ -1176,7 +1180,10 @@ mi_ba_status mi_ba_dense_cholesky(int32_t device, int32_t n, double* A, double* 
       if (hinfo[k] != 0) *info = (int32_t)(col0 + hinfo[k]);
       col0 += width;
     }
-    if (b && *info == 0 && chol_solve(h, n, dA.ptr, n, dx.ptr) != rocblas_status_success) { st = MI_BA_ERR_HIP; break; }
+    if (b && *info == 0 && chol_solve(h, n, dA.ptr, n, dx.ptr, cfg.solve, &ws) != rocblas_status_success) {
+      st = MI_BA_ERR_HIP;
+      break;
+    }
     if (hipMemcpyAsync(A, dA.ptr, dA.bytes(), hipMemcpyDeviceToHost, s) != hipSuccess ||
         (b && hipMemcpyAsync(b, dx.ptr, dx.bytes(), hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipStreamSynchronize(s) != hipSuccess) {

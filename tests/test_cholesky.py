@@ -123,6 +123,22 @@ def test_two_contexts_two_threads(gpu):
         assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
 
 
+def test_lm_solve_variants(gpu):
+    """The blocked triangular sweeps (default) and the recursive rocBLAS
+    dtrsv / dgemv solve drive the same LM (nf = 1593, ragged last block)."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=5)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for v in (0, 1):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            ctx.set_tuning("cholesky_solve", v)
+            res.append(ctx.solve())
+    a, b = res
+    assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
+    assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
+
+
 @pytest.mark.parametrize("images", [200])
 def test_lm_lookahead_on_off(gpu, images):
     """LM at nf = 1593 (C2 shape, 4 panels): look-ahead on/off give the same

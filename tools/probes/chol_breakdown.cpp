@@ -79,7 +79,7 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(fill_spd, dim3((unsigned)(((size_t)n * n + 255) / 256)), dim3(256), 0, st, S, n);
     miba::CholConfig cfg;
     hipEventRecord(ev[0], st);
-    { static miba::CholWorkspace ws; if (ws.device < 0) ws.create(0, (n + 63) / 64); miba::chol_factor(h, n, S, n, info, cfg, &ws); }
+    { static miba::CholWorkspace ws; if (ws.device < 0) ws.create(0, (n + 63) / 64, n); miba::chol_factor(h, n, S, n, info, cfg, &ws); }
     hipEventRecord(ev[1], st);
     hipEventSynchronize(ev[1]);
     float ms;

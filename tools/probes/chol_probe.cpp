@@ -21,7 +21,7 @@ int main() {
     hipLaunchKernelGGL(fill_spd, dim3((n*(size_t)n+255)/256), dim3(256), 0, st, S, n);
     hipMemcpyAsync(x, hx.data(), 8*n, hipMemcpyHostToDevice, st);
     hipEventRecord(e0, st);
-    { static miba::CholWorkspace ws; if (ws.device < 0) ws.create(0, (n + 63) / 64); miba::chol_factor(h, n, S, n, info, {}, &ws); }
+    { static miba::CholWorkspace ws; if (ws.device < 0) ws.create(0, (n + 63) / 64, n); miba::chol_factor(h, n, S, n, info, {}, &ws); }
     hipEventRecord(e1, st); hipEventSynchronize(e1); hipEventElapsedTime(&ms, e0, e1);
     printf("chol_factor n=%d: %.3f ms (%.1f TF)\n", n, ms, (double)n*n*n/3.0/(ms*1e-3)/1e12);
     hipEventRecord(e0, st);

@@ -47,7 +47,7 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL(fill_spd, dim3((unsigned)(((size_t)n * n + 255) / 256)), dim3(256), 0, st, S, n);
       hipMemcpyAsync(x, hx.data(), 8 * n, hipMemcpyHostToDevice, st);
       hipEventRecord(e0, st);
-      { static miba::CholWorkspace ws; if (ws.device < 0) ws.create(0, (n + 63) / 64); miba::chol_factor(h, n, S, n, info, cfg, &ws); }
+      { static miba::CholWorkspace ws; if (ws.device < 0) ws.create(0, (n + 63) / 64, n); miba::chol_factor(h, n, S, n, info, cfg, &ws); }
       hipEventRecord(e1, st);
       hipEventSynchronize(e1);
       float ms;
