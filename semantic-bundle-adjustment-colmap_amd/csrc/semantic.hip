@@ -134,16 +134,6 @@ __device__ inline void pose1_stage(const double* q1, const double pc1[3], Pose1S
   quat_rotate_point(qi, pc1, s.rot);
 }
 
-// P_w = rot + t_inv with t_inv = -(R t1)
-__device__ inline void pose1_world(const Pose1Stage& s, const double* t1, double pw[3]) {
-  const double ti0 = -(s.R[0] * t1[0] + s.R[1] * t1[1] + s.R[2] * t1[2]);
-  const double ti1 = -(s.R[3] * t1[0] + s.R[4] * t1[1] + s.R[5] * t1[2]);
-  const double ti2 = -(s.R[6] * t1[0] + s.R[7] * t1[1] + s.R[8] * t1[2]);
-  pw[0] = s.rot[0] + ti0;
-  pw[1] = s.rot[1] + ti1;
-  pw[2] = s.rot[2] + ti2;
-}
-
 __device__ inline void unit_quat(const double* q, double u[4]) {
   const double scale = 1.0 / sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
   u[0] = scale * q[0];

@@ -1,0 +1,40 @@
+"""Times the semantic linearization kernel alone at C4 (5.0M samples, HIP
+events on the context stream) and checks its samples against a reference
+download.    python tools/ab_semantic.py [--rounds 5]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "semantic-bundle-adjustment-colmap_amd"))
+sys.path.insert(0, ROOT)
+import mi_ba  # noqa: E402
+import bench  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--reps", type=int, default=5)
+args = ap.parse_args()
+cfg = bench.CONFIGS["C4"]
+sc, sem = bench.build_shard(cfg, 0, 1)
+sc.obs_xy, sc.obs_image, sc.obs_point = sc.obs_xy[:0], sc.obs_image[:0], sc.obs_point[:0]
+ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
+_, _, ns = ctx.dims()
+ctx.evaluate_semantic()
+px, st, r, J = ctx.download_semantic()
+ts = []
+for rnd in range(args.rounds):
+    ctx.set_timing(True)
+    ctx.reset_kernel_times()
+    for _ in range(args.reps):
+        ctx.linearize()
+    ms, n = ctx.kernel_time("semantic_jacobian")
+    ctx.set_timing(False)
+    ts.append(ms / n)
+print(json.dumps({"samples": ns, "median_ms": float(np.median(ts)), "min_ms": float(np.min(ts)),
+                  "valid": int((st == mi_ba.VALID).sum()), "nonzero_J_rows": int((np.abs(J).sum(1) > 0).sum()),
+                  "checksum_J": float(np.abs(J).sum()), "checksum_r": float(r.sum())}))
+ctx.close()
