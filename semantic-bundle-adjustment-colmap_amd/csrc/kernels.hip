@@ -50,16 +50,6 @@ __device__ inline void block_reduce(double (&v)[NV], double* sred) {
   __syncthreads();
 }
 
-__device__ inline double block_sum(double v, double* sred) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  v = wave_sum(v);
-  if (lane == 0) sred[wid] = v;
-  __syncthreads();
-  double s = 0.0;
-  if (threadIdx.x == 0) s = sred[0] + sred[1] + sred[2] + sred[3];
-  __syncthreads();
-  return s;
-}
 
 // Segmented sum over runs of equal key in the wavefront; the run's tail lane
 // stores (interior run) or atomically adds (run touching a wave boundary).
@@ -333,8 +323,10 @@ __device__ inline void wave_load_rows(const double* __restrict__ src, double* __
 // 1 and 2 are the diagnostic builds.
 constexpr int kJacProduction = 8 | 16 | 32 | 128;
 constexpr int kJacR1 = 8 | 16 | 32;  // round-1 production (three serial round trips), A/B variant 23
-template <int M, int RF, int LOSS, int NP, int D = kJacProduction, int WPE = 4>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
+// TB: threads per workgroup.  The cost partial is per wave (no workgroup
+// barrier), cost_partial[i / 64].
+template <int M, int RF, int LOSS, int NP, int D = kJacProduction, int WPE = 4, int TB = kBlock>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
                                                                  double* __restrict__ J_out,
                                                                  double* __restrict__ cost_partial) {
   constexpr int np = Model<M>::kNumParams;
@@ -349,10 +341,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   constexpr int RS = 18;  // LDS stride of an image record (144 B: conflict-free ds_read_b128)
   // D & 64: image records fetched per lane (no LDS staging), slab = J rows only
   constexpr int SLAB = ((D & 64) || RP * LS > 64 * RS) ? RP * LS : 64 * RS;
-  __shared__ double sred[4];
-  __shared__ double sJ[(kBlock / 64) * SLAB];
+  __shared__ double sJ[(TB / 64) * SLAB];
   const int lane = threadIdx.x & 63;
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
   const int64_t wb0 = i - lane;  // first block of this wavefront
   double* slab = sJ + (threadIdx.x >> 6) * SLAB;
   double cost = 0.0;
@@ -522,18 +513,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       const int rows = live - h * RP < 0 ? 0 : (live - h * RP > RP ? RP : live - h * RP);
+      // D & 256: the store bursts issue at raised priority (the arithmetic of
+      // the SIMD's other waves fills around them)
+      if constexpr ((D & 256) != 0) __builtin_amdgcn_s_setprio(2);
       if constexpr ((D & 32) != 0)
         wave_readout16<W2, LS, W2, (D & 8) != 0>(slab, J_out + (wb0 + h * RP) * W2, rows);
       else
         wave_readout<W2, LS, W2, (D & 8) != 0>(slab, J_out + (wb0 + h * RP) * W2, rows);
+      if constexpr ((D & 256) != 0) __builtin_amdgcn_s_setprio(0);
       if (h + 1 < NP) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       }
     }
   }
-  const double s = block_sum(cost, sred);
-  if (threadIdx.x == 0) cost_partial[blockIdx.x] = s;
+  const double s = wave_sum(cost);
+  if (lane == 0 && wb0 < p.nb) cost_partial[wb0 >> 6] = s;
 }
 
 // Image records img_rec[I][16] = q(4) t(3) meta camera-params(8), meta =
@@ -556,7 +551,6 @@ __global__ __launch_bounds__(kBlock) void reproj_cost_kernel(DevProblem p, const
                                                               const double* __restrict__ cam,
                                                               const double* __restrict__ X,
                                                               double* __restrict__ cost_partial) {
-  __shared__ double sred[4];
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   double cost = 0.0;
   if (i < p.nb) {
@@ -566,8 +560,8 @@ __global__ __launch_bounds__(kBlock) void reproj_cost_kernel(DevProblem p, const
     eval_block<M, false>(p, qt, cam, X, i, e, pt, ptv);
     cost = e.cost;
   }
-  const double s = block_sum(cost, sred);
-  if (threadIdx.x == 0) cost_partial[blockIdx.x] = s;
+  const double s = wave_sum(cost);  // per-wave partial (reproj_grid)
+  if ((threadIdx.x & 63) == 0 && i < p.nb) cost_partial[i >> 6] = s;
 }
 
 __global__ __launch_bounds__(1024) void sum_kernel(const double* __restrict__ partial, int64_t n,
@@ -1152,7 +1146,6 @@ __global__ __launch_bounds__(kBlock) void model_cost_kernel(DevProblem p, const 
                                                              const double* __restrict__ df,
                                                              const double* __restrict__ dX,
                                                              double* __restrict__ partial) {
-  __shared__ double sred[4];
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   double v = 0.0;
   if (i < p.nb) {
@@ -1170,8 +1163,8 @@ __global__ __launch_bounds__(kBlock) void model_cost_kernel(DevProblem p, const 
     const double2 r = rr[i];
     v = -(e[0] * (r.x + e[0] / 2.0) + e[1] * (r.y + e[1] / 2.0));
   }
-  const double s = block_sum(v, sred);
-  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+  const double s = wave_sum(v);  // per-wave partial (reproj_grid)
+  if ((threadIdx.x & 63) == 0 && i < p.nb) partial[i >> 6] = s;
 }
 
 __global__ void plus_images_kernel(DevProblem p, const double* __restrict__ df, const double* __restrict__ qt,
@@ -1471,7 +1464,8 @@ inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 
 
 }  // namespace
 
-int reproj_grid(int64_t nb) { return (int)grid_for(nb, kBlock); }
+// cost partials of the reprojection kernels: one per 64 blocks
+int reproj_grid(int64_t nb) { return (int)grid_for(nb, 64); }
 
 void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s) {
   if (p.nb == 0) return;
@@ -1500,6 +1494,22 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
             case 21:
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, 24>), dim3(g), dim3(kBlock), 0, s, p, r, J,
                                  cost_partial);
+              return;
+            case 26:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 256>), dim3(g), dim3(kBlock), 0, s, p,
+                                 r, J, cost_partial);
+              return;
+            case 27:  // plain (temporal) 16-B J stores
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction & ~8>), dim3(g), dim3(kBlock), 0, s,
+                                 p, r, J, cost_partial);
+              return;
+            case 24:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction, 4, 64>), dim3(grid_for(p.nb, 64)),
+                                 dim3(64), 0, s, p, r, J, cost_partial);
+              return;
+            case 25:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction, 4, 128>),
+                                 dim3(grid_for(p.nb, 128)), dim3(128), 0, s, p, r, J, cost_partial);
               return;
             case 23:
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacR1>), dim3(g), dim3(kBlock), 0, s, p, r, J,
