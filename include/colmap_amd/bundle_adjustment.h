@@ -273,7 +273,8 @@ struct Flat {
   std::vector<image_t> img_ids;
   std::vector<point3D_t> pt_ids;
   std::vector<double> cam_params, qvec, tvec, xyz, obs_xy;
-  std::vector<int32_t> image_camera, obs_image, obs_point;
+  std::vector<int32_t> image_camera, obs_image, obs_point, cam_models;
+  std::vector<size_t> cam_offsets;  // params of camera c at [cam_offsets[c], cam_offsets[c + 1])
   std::vector<uint8_t> cam_const, img_cfg, img_cpose, img_ctvec, pt_cfg;
   mi_ba_problem problem{};
 
@@ -281,15 +282,18 @@ struct Flat {
     std::unordered_map<camera_t, int32_t> cidx;
     std::unordered_map<image_t, int32_t> iidx;
     std::unordered_map<point3D_t, int32_t> pidx;
+    // per-camera models (camera_models.h:117-141), params back to back
+    cam_offsets.push_back(0);
     for (const auto& c : rec.cameras) {
       if (model < 0) model = c.second.model_id;
-      if (c.second.model_id != model) throw std::domain_error("mixed camera models in one problem");
       cidx[c.first] = (int32_t)cam_ids.size();
       cam_ids.push_back(c.first);
-      const int np = mi_ba_num_params(model);
+      const int np = mi_ba_num_params(c.second.model_id);
       if (np < 0) throw std::domain_error("Camera model does not exist");
       if ((int)c.second.params.size() != np) throw std::invalid_argument("camera params size");
       cam_params.insert(cam_params.end(), c.second.params.begin(), c.second.params.end());
+      cam_offsets.push_back(cam_params.size());
+      cam_models.push_back(c.second.model_id);
       cam_const.push_back(cfg.IsConstantCamera(c.first) ? 1 : 0);
     }
     for (const auto& p : rec.points3D) {
@@ -340,12 +344,12 @@ struct Flat {
     problem.obs_xy = obs_xy.data();
     problem.obs_image = obs_image.data();
     problem.obs_point = obs_point.data();
+    problem.camera_model_ids = cam_models.data();
   }
 
   void WriteBack(Reconstruction* rec) const {
-    const int np = mi_ba_num_params(problem.camera_model);
     for (size_t c = 0; c < cam_ids.size(); ++c)
-      std::copy(cam_params.begin() + c * np, cam_params.begin() + (c + 1) * np,
+      std::copy(cam_params.begin() + cam_offsets[c], cam_params.begin() + cam_offsets[c + 1],
                 rec->cameras.at(cam_ids[c]).params.begin());
     for (size_t i = 0; i < img_ids.size(); ++i) {
       Image& im = rec->images.at(img_ids[i]);

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MI_BA_ABI_VERSION 1
+#define MI_BA_ABI_VERSION 2
 
 typedef enum mi_ba_status {
   MI_BA_OK = 0,
@@ -116,12 +116,17 @@ typedef struct mi_ba_options {
   double semantic_weight;           /* ScaledLoss weight of semantic blocks, default 1 */
 } mi_ba_options;
 
-/* Flattened Reconstruction + BundleAdjustmentConfig.  A single camera model
- * per problem.  Indices are 0-based positions in these arrays. */
+/* Flattened Reconstruction + BundleAdjustmentConfig.  Indices are 0-based
+ * positions in these arrays.  Camera models: camera_model_ids[c] per camera
+ * (Camera::ModelId, dispatched per camera like camera_models.h:117-141), or,
+ * when camera_model_ids is NULL, camera_model for every camera.
+ * camera_params holds each camera's Camera::Params() back to back in camera
+ * order (num_params(model of camera c) doubles each; with one model this is
+ * [num_cameras][num_params(model)]). */
 typedef struct mi_ba_problem {
-  int32_t camera_model;              /* MI_BA_* model id */
+  int32_t camera_model;              /* MI_BA_* model id of every camera when camera_model_ids is NULL */
   int32_t num_cameras;
-  double* camera_params;             /* (in/out) [num_cameras][num_params(model)] */
+  double* camera_params;             /* (in/out) per-camera params, back to back */
   const uint8_t* camera_constant;    /* nullable; 1 = config.SetConstantCamera */
 
   int32_t num_images;
@@ -140,6 +145,7 @@ typedef struct mi_ba_problem {
   const double* obs_xy;              /* [num_obs][2] Point2D::XY() */
   const int32_t* obs_image;          /* [num_obs] */
   const int32_t* obs_point;          /* [num_obs] */
+  const int32_t* camera_model_ids;   /* nullable; [num_cameras] MI_BA_* model id per camera (ABI 2) */
 } mi_ba_problem;
 
 /* Semantic term (SBA).  Rasters are row-major [image][H][W] float32, i.e. the

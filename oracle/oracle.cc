@@ -108,8 +108,10 @@ void ApplyCorrector(const double rho[3], double sq_norm, int nres, double* r, in
 // (src/optim/bundle_adjustment.cc:326-530) + Ceres reduced program.
 // ---------------------------------------------------------------------------
 struct Setup {
-  int np = 0;                          // camera params per camera
-  std::vector<int> cam_tangent;        // refined param indices (SubsetManifold)
+  int ct = 0;                          // widest camera tangent (Jacobian rows are 9 + ct wide)
+  std::vector<int> cam_model;          // model id per camera (camera_models.h:117-141)
+  std::vector<int64_t> cam_poff;       // offset of the camera's params in camera_params
+  std::vector<std::vector<int>> cam_tangent;  // per camera: refined param indices (SubsetManifold)
   std::vector<int64_t> block_obs;      // blocks in program order
   std::vector<uint8_t> block_const_pose;
   std::vector<double> block_pose;      // [nb][7] baked (q,t) for constant-pose blocks
@@ -123,10 +125,15 @@ struct Setup {
 };
 
 int BuildSetup(const mi_ba_options* o, mi_ba_problem* p, Setup* s) {
-  const int np = NumParams(p->camera_model);
-  if (np < 0) return MI_BA_ERR_UNSUPPORTED;
-  s->np = np;
   const int I = p->num_images, C = p->num_cameras;
+  if (!p->camera_model_ids && NumParams(p->camera_model) < 0) return MI_BA_ERR_UNSUPPORTED;
+  s->cam_model.assign(C, 0);
+  s->cam_poff.assign(C + 1, 0);
+  for (int c = 0; c < C; ++c) {
+    s->cam_model[c] = p->camera_model_ids ? p->camera_model_ids[c] : p->camera_model;
+    if (NumParams(s->cam_model[c]) < 0) return MI_BA_ERR_UNSUPPORTED;
+    s->cam_poff[c + 1] = s->cam_poff[c] + NumParams(s->cam_model[c]);
+  }
   const int64_t P = p->num_points, N = p->num_obs;
   auto in_cfg = [&](int i) { return p->image_in_config ? p->image_in_config[i] != 0 : true; };
   auto const_pose_cfg = [&](int i) { return p->image_constant_pose && p->image_constant_pose[i]; };
@@ -187,21 +194,26 @@ int BuildSetup(const mi_ba_options* o, mi_ba_problem* p, Setup* s) {
       }
     }
   }
-  // ParameterizeCameras (:480-516)
-  int f[2], nf, pp[2], npp, ex[4], nex;
-  ParamGroups(p->camera_model, f, &nf, pp, &npp, ex, &nex);
-  std::vector<int> const_idx;
-  if (!o->refine_focal_length) const_idx.insert(const_idx.end(), f, f + nf);
-  if (!o->refine_principal_point) const_idx.insert(const_idx.end(), pp, pp + npp);
-  if (!o->refine_extra_params) const_idx.insert(const_idx.end(), ex, ex + nex);
-  for (int k = 0; k < np; ++k)
-    if (std::find(const_idx.begin(), const_idx.end(), k) == const_idx.end()) s->cam_tangent.push_back(k);
+  // ParameterizeCameras (:480-516), per camera model
+  s->cam_tangent.assign(C, {});
+  s->ct = 0;
+  for (int c = 0; c < C; ++c) {
+    int f[2], nf, pp[2], npp, ex[4], nex;
+    ParamGroups(s->cam_model[c], f, &nf, pp, &npp, ex, &nex);
+    std::vector<int> const_idx;
+    if (!o->refine_focal_length) const_idx.insert(const_idx.end(), f, f + nf);
+    if (!o->refine_principal_point) const_idx.insert(const_idx.end(), pp, pp + npp);
+    if (!o->refine_extra_params) const_idx.insert(const_idx.end(), ex, ex + nex);
+    for (int k = 0; k < NumParams(s->cam_model[c]); ++k)
+      if (std::find(const_idx.begin(), const_idx.end(), k) == const_idx.end()) s->cam_tangent[c].push_back(k);
+    s->ct = std::max(s->ct, (int)s->cam_tangent[c].size());
+  }
   const bool constant_camera = !o->refine_focal_length && !o->refine_principal_point && !o->refine_extra_params;
   s->cam_var.assign(C, 0);
   for (int cam : cam_ids) {
     if (constant_camera || cam_const_cfg[cam]) continue;
     // Ceres: a SubsetManifold with tangent size 0 makes the block constant.
-    if (!s->cam_tangent.empty()) s->cam_var[cam] = 1;
+    if (!s->cam_tangent[cam].empty()) s->cam_var[cam] = 1;
   }
   // ParameterizePoints (:518-530)
   s->pt_var.assign(P, 0);
@@ -238,7 +250,7 @@ int BuildSetup(const mi_ba_options* o, mi_ba_problem* p, Setup* s) {
       ne += 3 + (3 - masked);
     }
   for (int c = 0; c < C; ++c)
-    if (used_cam[c]) ne += (int64_t)s->cam_tangent.size();
+    if (used_cam[c]) ne += (int64_t)s->cam_tangent[c].size();
   for (int64_t pt = 0; pt < P; ++pt)
     if (used_pt[pt]) ne += 3;
   s->num_effective_parameters_reduced = ne;
@@ -252,7 +264,7 @@ void EvalBlock(const Setup& s, const mi_ba_problem* p, int64_t b, double r[2], d
   const int img = p->obs_image[k];
   const int cam = p->image_camera[img];
   const int64_t pt = p->obs_point[k];
-  const int np = s.np;
+  const int np = NumParams(s.cam_model[cam]);
   const bool cpose = s.block_const_pose[b] != 0;
   const double* qv = cpose ? &s.block_pose[b * 7] : &p->qvec[img * 4];
   const double* tv = cpose ? &s.block_pose[b * 7 + 4] : &p->tvec[img * 3];
@@ -260,13 +272,15 @@ void EvalBlock(const Setup& s, const mi_ba_problem* p, int64_t b, double r[2], d
   for (int j = 0; j < 4; ++j) q[j] = cpose ? J18(qv[j]) : J18(qv[j], j);
   for (int j = 0; j < 3; ++j) t[j] = cpose ? J18(tv[j]) : J18(tv[j], 4 + j);
   for (int j = 0; j < 3; ++j) X[j] = J18(p->xyz[pt * 3 + j], 7 + j);
-  for (int j = 0; j < np; ++j) params[j] = J18(p->camera_params[(int64_t)cam * np + j], 10 + j);
-  ReprojResidual(p->camera_model, q, t, X, params, p->obs_xy[k * 2], p->obs_xy[k * 2 + 1], res);
+  for (int j = 0; j < np; ++j) params[j] = J18(p->camera_params[s.cam_poff[cam] + j], 10 + j);
+  ReprojResidual(s.cam_model[cam], q, t, X, params, p->obs_xy[k * 2], p->obs_xy[k * 2 + 1], res);
   r[0] = res[0].a;
   r[1] = res[1].a;
   if (!Jt) return;
-  const int c = (int)s.cam_tangent.size();
-  const int w = 9 + c;
+  // rows are 9 + s.ct wide; a camera with fewer refined intrinsics leaves
+  // the rest of its columns zero
+  const int c = (int)s.cam_tangent[cam].size();
+  const int w = 9 + s.ct;
   double PJ[12];
   QuaternionPlusJacobian(qv, PJ);
   const bool vpose = !cpose && s.img_var[img];
@@ -283,7 +297,7 @@ void EvalBlock(const Setup& s, const mi_ba_problem* p, int64_t b, double r[2], d
       Jr[3 + col] = (vpose && !masked) ? d[4 + col] : 0.0;
     }
     for (int col = 0; col < 3; ++col) Jr[6 + col] = s.pt_var[pt] ? d[7 + col] : 0.0;
-    for (int col = 0; col < c; ++col) Jr[9 + col] = s.cam_var[cam] ? d[10 + s.cam_tangent[col]] : 0.0;
+    for (int col = 0; col < s.ct; ++col) Jr[9 + col] = (col < c && s.cam_var[cam]) ? d[10 + s.cam_tangent[cam][col]] : 0.0;
   }
 }
 
@@ -308,7 +322,6 @@ struct SemSetup {
 void BuildSemSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& s,
                    const mi_ba_semantic* sem, SemSetup* ss) {
   const int H = sem->height, W = sem->width, step = sem->pixel_step;
-  const int np = NumParams(p->camera_model);
   ss->pair_var1.assign(sem->num_pairs, 0);
   ss->pair_var2.assign(sem->num_pairs, 0);
   for (int k = 0; k < sem->num_pairs; ++k) {
@@ -319,7 +332,8 @@ void BuildSemSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& 
     if (c1 && c2) continue;
     ss->pair_var1[k] = !c1;
     ss->pair_var2[k] = !c2;
-    const double* K1 = &p->camera_params[(int64_t)p->image_camera[i] * np];
+    const int cam1 = p->image_camera[i];
+    const double* K1 = &p->camera_params[s.cam_poff[cam1]];
     const float* depth1 = sem->depth + (int64_t)i * H * W;
     const float* label1 = sem->label + (int64_t)i * H * W;
     for (int y = 0; y < H; y += step) {
@@ -329,7 +343,7 @@ void BuildSemSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& 
         SemSample smp;
         smp.pair = k; smp.x = x; smp.y = y;
         double u1, v1;
-        ImageToWorld(p->camera_model, K1, (double)x, (double)y, &u1, &v1);
+        ImageToWorld(s.cam_model[cam1], K1, (double)x, (double)y, &u1, &v1);
         smp.pc1[0] = u1 * (double)depth;
         smp.pc1[1] = v1 * (double)depth;
         smp.pc1[2] = (double)depth;
@@ -338,15 +352,14 @@ void BuildSemSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& 
       }
     }
   }
-  (void)s;
 }
 
-double SemanticError(const mi_ba_problem* p, const mi_ba_semantic* sem, const SemSample& smp,
+double SemanticError(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, const SemSample& smp,
                      const double q1[4], const double t1[3], const double q2[4], const double t2[3],
                      int* status) {
-  const int np = NumParams(p->camera_model);
   const int j = sem->pairs[2 * smp.pair + 1];
-  const double* K2 = &p->camera_params[(int64_t)p->image_camera[j] * np];
+  const int cam2 = p->image_camera[j];
+  const double* K2 = &p->camera_params[s.cam_poff[cam2]];
   double q1i[4], t1i[3];
   PoseInverse(q1, t1, q1i, t1i);                       // :121-125
   double pw[3];
@@ -357,7 +370,7 @@ double SemanticError(const mi_ba_problem* p, const mi_ba_semantic* sem, const Se
   const double v2 = pc2[1] / pc2[2];
   const double measured_depth_2 = pc2[2];
   double x2, y2;
-  WorldToImage(p->camera_model, K2, u2, v2, &x2, &y2); // :149-151
+  WorldToImage(s.cam_model[cam2], K2, u2, v2, &x2, &y2); // :149-151
   const int px = CastToIntX86(std::round(x2));         // :154-156
   const int py = CastToIntX86(std::round(y2));
   const int H = sem->height, W = sem->width;
@@ -389,7 +402,7 @@ void EvalSemantic(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* 
   for (int m = 0; m < 4; ++m) x[7 + m] = p->qvec[j * 4 + m];
   for (int m = 0; m < 3; ++m) x[11 + m] = p->tvec[j * 3 + m];
   int st;
-  *r = SemanticError(p, sem, smp, &x[0], &x[4], &x[7], &x[11], status);
+  *r = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], status);
   double Jamb[14] = {0};
   const bool var[2] = {ss.pair_var1[smp.pair] != 0, ss.pair_var2[smp.pair] != 0};
   const double min_step = std::sqrt(std::numeric_limits<double>::epsilon());
@@ -400,9 +413,9 @@ void EvalSemantic(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* 
       const double orig = x[idx];
       const double delta = std::max(min_step, std::fabs(orig) * sem->numeric_relative_step_size);
       x[idx] = orig + delta;
-      const double fp = SemanticError(p, sem, smp, &x[0], &x[4], &x[7], &x[11], &st);
+      const double fp = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], &st);
       x[idx] = orig - delta;
-      const double fm = SemanticError(p, sem, smp, &x[0], &x[4], &x[7], &x[11], &st);
+      const double fm = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], &st);
       x[idx] = orig;
       double one_over_delta = 1.0 / delta;
       one_over_delta /= 2;
@@ -491,7 +504,7 @@ void BuildLayout(const Setup& s, const mi_ba_problem* p, Layout* L, const mi_ba_
   for (int c = 0; c < C; ++c) {
     if (!used_cam[c]) continue;
     L->cam_off[c] = nf;
-    nf += (int)s.cam_tangent.size();
+    nf += (int)s.cam_tangent[c].size();
   }
   L->nf = nf;
   L->pt_off.assign(p->num_points, -1);
@@ -585,7 +598,7 @@ struct Solver {
     const SemSample& smp = ss.samples[n];
     const int i = sem->pairs[2 * smp.pair], j = sem->pairs[2 * smp.pair + 1];
     int st;
-    const double r = SemanticError(p, sem, smp, &p->qvec[i * 4], &p->tvec[i * 3], &p->qvec[j * 4], &p->tvec[j * 3], &st);
+    const double r = SemanticError(p, s, sem, smp, &p->qvec[i * 4], &p->tvec[i * 3], &p->qvec[j * 4], &p->tvec[j * 3], &st);
     double rho[3];
     LossEvaluate(o->loss_function_type, o->loss_function_scale, r * r, rho);
     return 0.5 * (o->semantic_weight * rho[0]);  // ScaledLoss(w)
@@ -606,7 +619,7 @@ struct Solver {
     return c;
   }
   void Linearize(Linearization* lin) {
-    const int c = (int)s.cam_tangent.size();
+    const int c = s.ct;
     const int64_t nr = (int64_t)reduced.size(), ns = sem ? (int64_t)ss.samples.size() : 0;
     lin->resize(2 * nr + ns);
     std::vector<double> cost(nr + ns);
@@ -637,7 +650,7 @@ struct Solver {
               if (col >= 0) { lin->fcol[R * Linearization::kF + nf] = col; lin->fval[R * Linearization::kF + nf++] = Jr[m]; }
             }
           if (L.cam_off[cam] >= 0)
-            for (int m = 0; m < c; ++m) {
+            for (int m = 0; m < (int)s.cam_tangent[cam].size(); ++m) {
               lin->fcol[R * Linearization::kF + nf] = L.cam_off[cam] + m;
               lin->fval[R * Linearization::kF + nf++] = Jr[9 + m];
             }
@@ -692,11 +705,10 @@ struct Solver {
       for (int m = 0; m < 4; ++m) p->qvec[i * 4 + m] = qn[m];
       for (int m = 0; m < 3; ++m) p->tvec[i * 3 + m] += d[3 + m];
     }
-    const int np = s.np;
     for (int c = 0; c < p->num_cameras; ++c) {
       if (L.cam_off[c] < 0) continue;
-      for (size_t m = 0; m < s.cam_tangent.size(); ++m)
-        p->camera_params[(int64_t)c * np + s.cam_tangent[m]] += delta[L.cam_off[c] + m];
+      for (size_t m = 0; m < s.cam_tangent[c].size(); ++m)
+        p->camera_params[s.cam_poff[c] + s.cam_tangent[c][m]] += delta[L.cam_off[c] + m];
     }
     for (int64_t pt = 0; pt < p->num_points; ++pt) {
       if (L.pt_off[pt] < 0) continue;
@@ -754,7 +766,7 @@ int oracle_setup_stats(const mi_ba_options* o, mi_ba_problem* p, mi_ba_setup_inf
   info->num_variable_images = vi;
   info->num_variable_cameras = vc;
   info->num_variable_points = vp;
-  info->camera_tangent_size = (int)s.cam_tangent.size();
+  info->camera_tangent_size = s.ct;
   return MI_BA_OK;
 }
 
@@ -768,7 +780,7 @@ int64_t oracle_reproj_eval(const mi_ba_options* o, mi_ba_problem* p, int64_t* bl
   if (st) return -st;
   const int64_t nb = (int64_t)s.block_obs.size();
   if (nb > capacity) return nb;
-  const int w = 9 + (int)s.cam_tangent.size();
+  const int w = 9 + s.ct;
 #pragma omp parallel for schedule(static)
   for (int64_t b = 0; b < nb; ++b) {
     block_obs[b] = s.block_obs[b];
@@ -793,7 +805,7 @@ double oracle_reproj_throughput(const mi_ba_options* o, mi_ba_problem* p, int64_
   Setup s;
   if (BuildSetup(o, p, &s)) return -1.0;
   const int64_t nb = std::min<int64_t>((int64_t)s.block_obs.size(), max_blocks);
-  const int w = 9 + (int)s.cam_tangent.size();
+  const int w = 9 + s.ct;
   std::vector<double> r(2 * nb), J(2 * w * nb);
   double t0 = 0, t1 = 0;
   {
@@ -1119,7 +1131,7 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
     for (int64_t i = 0; i < n; ++i) delta[i] = step[i] * scale[i];
     // candidate
     std::vector<double> q0(p->qvec, p->qvec + 4 * p->num_images), t0(p->tvec, p->tvec + 3 * p->num_images);
-    std::vector<double> c0(p->camera_params, p->camera_params + (int64_t)S.s.np * p->num_cameras);
+    std::vector<double> c0(p->camera_params, p->camera_params + S.s.cam_poff[p->num_cameras]);
     std::vector<double> x0(p->xyz, p->xyz + 3 * p->num_points);
     double x_norm2 = 0.0;
     for (double v : q0) x_norm2 += v * v;

@@ -25,6 +25,7 @@
 namespace miba {
 
 enum CameraModelId { kSimplePinhole = 0, kPinhole = 1, kSimpleRadial = 2, kRadial = 3, kOpenCV = 4 };
+constexpr int kNumModels = 5;
 
 MI_HD int num_params(int model) {
   return model == kSimplePinhole ? 3 : model == kPinhole ? 4 : model == kSimpleRadial ? 4
@@ -37,6 +38,11 @@ template <> struct Model<kPinhole> { static constexpr int kNumParams = 4; };
 template <> struct Model<kSimpleRadial> { static constexpr int kNumParams = 4; };
 template <> struct Model<kRadial> { static constexpr int kNumParams = 5; };
 template <> struct Model<kOpenCV> { static constexpr int kNumParams = 8; };
+// Kernel instantiation for problems whose cameras use different models
+// (camera_models.h:117-141 dispatches per camera): the model is read per
+// camera at run time, parameters are held in 8-wide slots.
+constexpr int kMixedModels = 15;
+template <> struct Model<kMixedModels> { static constexpr int kNumParams = 8; };
 
 // ---------------------------------------------------------------------------
 // Rotations (Ceres 2.1 rotation.h, restated)
@@ -276,6 +282,38 @@ MI_HD void image_to_world(const double* prm, double x, double y, double* u, doub
     *v = (y - prm[3]) / prm[1];
     iterative_undistortion<M>(prm + 4, u, v);
   }
+}
+
+// Run-time dispatch on a per-camera model id (host and device).
+template <typename F>
+MI_HD void switch_model(int model, F&& f) {
+  switch (model) {
+    case kSimplePinhole: f(std::integral_constant<int, kSimplePinhole>{}); break;
+    case kPinhole: f(std::integral_constant<int, kPinhole>{}); break;
+    case kSimpleRadial: f(std::integral_constant<int, kSimpleRadial>{}); break;
+    case kRadial: f(std::integral_constant<int, kRadial>{}); break;
+    default: f(std::integral_constant<int, kOpenCV>{}); break;
+  }
+}
+
+// Projection of a camera whose model is known only at run time; Jp8 is
+// d(x,y)/dparams in 8-wide rows (2 x 8, unused columns zero).
+MI_HD void world_to_image_any(int model, const double* prm, double u, double v, double* x, double* y) {
+  switch_model(model, [&](auto m) { world_to_image<decltype(m)::value>(prm, u, v, x, y); });
+}
+MI_HD void world_to_image_jac_any(int model, const double* prm, double u, double v, double* x, double* y,
+                                  double A[4], double Jp8[16]) {
+  switch_model(model, [&](auto m) {
+    constexpr int M = decltype(m)::value;
+    constexpr int np = Model<M>::kNumParams;
+    double Jp[2 * np];
+    world_to_image_jac<M>(prm, u, v, x, y, A, Jp);
+    for (int rw = 0; rw < 2; ++rw)
+      for (int k = 0; k < 8; ++k) Jp8[rw * 8 + k] = k < np ? Jp[rw * np + k] : 0.0;
+  });
+}
+MI_HD void image_to_world_any(int model, const double* prm, double x, double y, double* u, double* v) {
+  switch_model(model, [&](auto m) { image_to_world<decltype(m)::value>(prm, x, y, u, v); });
 }
 
 // Runtime dispatch helpers for host code.

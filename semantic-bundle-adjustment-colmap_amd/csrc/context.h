@@ -62,7 +62,7 @@ struct mi_ba_context {
   miba::DevArray<double2> obs_xy;
   miba::DevArray<uint32_t> obs_img, obs_pt;
   miba::DevArray<uint32_t> img_flags, img_cam;
-  miba::DevArray<uint8_t> cam_var, pt_var;
+  miba::DevArray<uint8_t> cam_var, cam_model, pt_var;
   miba::DevArray<double> qt, cam, X;       // current parameters
   miba::DevArray<double> qt_c, cam_c, X_c; // candidate parameters
   miba::DevArray<double> img_rec;          // [I][16] packed image records

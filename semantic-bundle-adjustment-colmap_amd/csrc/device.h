@@ -13,7 +13,8 @@
 //              img_flags u32[I] bit0 variable pose, bits1..3 constant tvec
 //   cameras    cam[C][8]       params, padded to 8
 //   img_rec    double[I][16]   q t meta cam: the Jacobian kernel's per-image
-//                              record (one 128-B line), packed per linearization
+//                              record (one 128-B line), packed per linearization;
+//                              meta = img_flags | cam_var << 8 | model << 16
 //   points     X[P][3]
 // Camera-side reductions run over cm_perm (blocks sorted by image) in tiles
 // that never straddle an image, so each tile folds into one atomic flush.
@@ -50,9 +51,10 @@ struct DevPairTile {   // image-pair tile of the explicit Schur build
 constexpr int kPairTile = 256;
 
 struct DevProblem {
-  int model;
-  int np;              // camera params per camera
-  int ct;              // refined intrinsics per camera (tangent)
+  int model;           // camera model of every camera, or kMixedModels (per-camera cam_model)
+  int np;              // camera params per camera (largest)
+  int ct;              // refined intrinsics slots per camera (largest; a camera with fewer
+                       // refined intrinsics has zero Jacobian columns in the rest)
   int W;               // 9 + ct
   int cam_tan_idx[kMaxCamTangent];
   int64_t nb;          // reduced geometric blocks
@@ -70,6 +72,7 @@ struct DevProblem {
   const uint32_t* img_flags;
   const uint32_t* img_cam;
   const uint8_t* cam_var;
+  const uint8_t* cam_model;  // [C] model id per camera
   const uint8_t* pt_var;
   // parameters (current)
   double* qt;   // [I][8]

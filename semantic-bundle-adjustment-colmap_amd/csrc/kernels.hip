@@ -85,25 +85,16 @@ __device__ inline void wave_segmented_store(uint32_t key, bool store, double (&v
 }
 
 // ---------------------------------------------------------------------------
-// Residual + Jacobian of one block (analytic, loss-corrected).
+// Cost of one block at trial parameters (the LM's candidate evaluation).
 // ---------------------------------------------------------------------------
 template <int M>
-struct BlockEval {
-  double r[2];
-  double jr[2][9];   // rot(3) trans(3) point(3)
-  double jc[2][8];   // refined intrinsics (first ct used)
-  double cost;
-};
-
-template <int M, bool WITH_J>
-__device__ inline void eval_block(const DevProblem& p, const double* __restrict__ qt_all,
-                                  const double* __restrict__ cam_all, const double* __restrict__ X_all,
-                                  int64_t i, BlockEval<M>& e, uint32_t& pt_out, bool& pt_var_out) {
+__device__ inline double block_cost(const DevProblem& p, const double* __restrict__ qt_all,
+                                    const double* __restrict__ cam_all, const double* __restrict__ X_all,
+                                    int64_t i) {
   constexpr int np = Model<M>::kNumParams;
   const double2 o = p.obs_xy[i];
   const uint32_t img = p.obs_img[i];
   const uint32_t pt = p.obs_pt[i];
-  pt_out = pt;
   const double* qt = qt_all + 8 * (size_t)img;
   const double q[4] = {qt[0], qt[1], qt[2], qt[3]};
   const double t[3] = {qt[4], qt[5], qt[6]};
@@ -120,86 +111,15 @@ __device__ inline void eval_block(const DevProblem& p, const double* __restrict_
   P[2] += t[2];
   const double iz = 1.0 / P[2];
   const double u = P[0] * iz, v = P[1] * iz;
-  double x, y, A[4], Jp[2 * np];
-  if constexpr (WITH_J) {
-    world_to_image_jac<M>(prm, u, v, &x, &y, A, Jp);
-  } else {
+  double x, y;
+  if constexpr (M == kMixedModels)
+    world_to_image_any(p.cam_model[cam_idx], prm, u, v, &x, &y);
+  else
     world_to_image<M>(prm, u, v, &x, &y);
-  }
-  double r0 = x - o.x, r1 = y - o.y;
+  const double r0 = x - o.x, r1 = y - o.y;
   double rho[3];
   loss_eval(p.loss_type, p.loss_scale, r0 * r0 + r1 * r1, rho);
-  e.cost = 0.5 * rho[0];
-  // Ceres Corrector, rho'' <= 0 branch (Trivial/SoftL1/Cauchy): scale r, J by sqrt(rho').
-  const double sc = (p.loss_type == kLossTrivial) ? 1.0 : sqrt(rho[1]);
-  e.r[0] = r0 * sc;
-  e.r[1] = r1 * sc;
-  pt_var_out = p.pt_var[pt] != 0;
-  if constexpr (WITH_J) {
-    // B = d(x,y)/dP (2x3) = A * d(u,v)/dP
-    double B[6];
-    B[0] = A[0] * iz; B[1] = A[1] * iz; B[2] = -(A[0] * u + A[1] * v) * iz;
-    B[3] = A[2] * iz; B[4] = A[3] * iz; B[5] = -(A[2] * u + A[3] * v) * iz;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) B[k] *= sc;
-    const uint32_t flags = p.img_flags[img];
-    const bool pose_var = flags & 1u;
-    if (pose_var) {
-      double Dq[12], PJ[12], Mq[9];
-      unit_quat_rotate_dq(q, X, Dq);
-      quat_plus_jacobian(q, PJ);
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b)
-          Mq[a * 3 + b] = Dq[a * 4 + 0] * PJ[0 * 3 + b] + Dq[a * 4 + 1] * PJ[1 * 3 + b] +
-                          Dq[a * 4 + 2] * PJ[2 * 3 + b] + Dq[a * 4 + 3] * PJ[3 * 3 + b];
-#pragma unroll
-      for (int row = 0; row < 2; ++row) {
-#pragma unroll
-        for (int b = 0; b < 3; ++b)
-          e.jr[row][b] = B[row * 3 + 0] * Mq[b] + B[row * 3 + 1] * Mq[3 + b] + B[row * 3 + 2] * Mq[6 + b];
-#pragma unroll
-        for (int b = 0; b < 3; ++b) e.jr[row][3 + b] = ((flags >> (1 + b)) & 1u) ? 0.0 : B[row * 3 + b];
-      }
-    } else {
-#pragma unroll
-      for (int row = 0; row < 2; ++row)
-#pragma unroll
-        for (int b = 0; b < 6; ++b) e.jr[row][b] = 0.0;
-    }
-    if (pt_var_out) {
-      double R[9];
-      unit_quat_matrix(q, R);
-#pragma unroll
-      for (int row = 0; row < 2; ++row)
-#pragma unroll
-        for (int b = 0; b < 3; ++b)
-          e.jr[row][6 + b] = B[row * 3 + 0] * R[b] + B[row * 3 + 1] * R[3 + b] + B[row * 3 + 2] * R[6 + b];
-    } else {
-#pragma unroll
-      for (int row = 0; row < 2; ++row)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) e.jr[row][6 + b] = 0.0;
-    }
-    const bool cv = p.cam_var[cam_idx] != 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      double c0 = 0.0, c1 = 0.0;
-      if (k < p.ct && cv) {
-        // select refined intrinsic k (SubsetManifold PlusJacobian = selection)
-#pragma unroll
-        for (int m = 0; m < np; ++m) {
-          if (m == p.cam_tan_idx[k]) {
-            c0 = Jp[m] * sc;
-            c1 = Jp[np + m] * sc;
-          }
-        }
-      }
-      e.jc[0][k] = c0;
-      e.jc[1][k] = c1;
-    }
-  }
+  return 0.5 * rho[0];
 }
 
 // Refined-intrinsics mask per model and refine flags (bit 0 focal, bit 1
@@ -222,10 +142,8 @@ __host__ __device__ constexpr int popcount8(unsigned m) {
 // Jacobian entries of one block row (rw = 0: x, 1: y) into dst[0..W).
 // Columns: rotation tangent (3), translation (3), point (3), refined
 // intrinsics (CT, SubsetManifold PlusJacobian = column selection).
-template <int M, unsigned CM>
-__device__ inline void emit_row(int rw, double* dst, const double (&B)[6], const double (&Mq)[9], bool pose_var,
-                                uint32_t flags, const double (&jx)[2][3], const double* Jp, double sc, bool cv) {
-  constexpr int np = Model<M>::kNumParams;
+__device__ inline void emit_row_pose_point(int rw, double* dst, const double (&B)[6], const double (&Mq)[9],
+                                           bool pose_var, uint32_t flags, const double (&jx)[2][3]) {
 #pragma unroll
   for (int b = 0; b < 3; ++b)
     dst[b] = pose_var ? B[rw * 3 + 0] * Mq[b] + B[rw * 3 + 1] * Mq[3 + b] + B[rw * 3 + 2] * Mq[6 + b] : 0.0;
@@ -233,6 +151,13 @@ __device__ inline void emit_row(int rw, double* dst, const double (&B)[6], const
   for (int b = 0; b < 3; ++b) dst[3 + b] = (pose_var && !((flags >> (1 + b)) & 1u)) ? B[rw * 3 + b] : 0.0;
 #pragma unroll
   for (int b = 0; b < 3; ++b) dst[6 + b] = jx[rw][b];
+}
+
+template <int M, unsigned CM>
+__device__ inline void emit_row(int rw, double* dst, const double (&B)[6], const double (&Mq)[9], bool pose_var,
+                                uint32_t flags, const double (&jx)[2][3], const double* Jp, double sc, bool cv) {
+  constexpr int np = Model<M>::kNumParams;
+  emit_row_pose_point(rw, dst, B, Mq, pose_var, flags, jx);
   int c = 0;
 #pragma unroll
   for (int m = 0; m < np; ++m) {
@@ -241,6 +166,25 @@ __device__ inline void emit_row(int rw, double* dst, const double (&B)[6], const
       ++c;
     }
   }
+}
+
+// Mixed camera models: the camera's refined intrinsics (run-time mask cmask,
+// parameter order) fill the first of CT slots, the rest are zero.  Jp8 holds
+// d(x,y)/dparams in 8-wide rows.
+template <int CT>
+__device__ inline void emit_row_mixed(int rw, double* dst, const double (&B)[6], const double (&Mq)[9],
+                                      bool pose_var, uint32_t flags, const double (&jx)[2][3], const double* Jp8,
+                                      double sc, bool cv, unsigned cmask) {
+  emit_row_pose_point(rw, dst, B, Mq, pose_var, flags, jx);
+  int c = 0;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    if ((cmask >> m) & 1u) {
+      if (c < CT) dst[9 + c] = cv ? Jp8[rw * 8 + m] * sc : 0.0;
+      ++c;
+    }
+  }
+  for (; c < CT; ++c) dst[9 + c] = 0.0;
 }
 
 // Copy NR rows of R doubles (LDS stride LS) into a global range whose rows
@@ -325,15 +269,18 @@ constexpr int kJacProduction = 8 | 16 | 32 | 128;
 constexpr int kJacR1 = 8 | 16 | 32;  // round-1 production (three serial round trips), A/B variant 23
 // TB: threads per workgroup.  The cost partial is per wave (no workgroup
 // barrier), cost_partial[i / 64].
-template <int M, int RF, int LOSS, int NP, int D = kJacProduction, int WPE = 4, int TB = kBlock>
+// CTX: the camera-slot width of a mixed-model build (M == kMixedModels, RF
+// then unused: the refine flags are applied per camera at run time).
+template <int M, int RF, int LOSS, int NP, int D = kJacProduction, int WPE = 4, int TB = kBlock, int CTX = 0>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void reproj_jacobian_kernel(DevProblem p, double2* __restrict__ r_out,
                                                                  double* __restrict__ J_out,
                                                                  double* __restrict__ cost_partial) {
   constexpr int np = Model<M>::kNumParams;
   constexpr unsigned CM = cam_tangent_mask(M, RF);
-  constexpr int CT = popcount8(CM);
+  constexpr int CT = M == kMixedModels ? CTX : popcount8(CM);
   constexpr int W = 9 + CT;
   constexpr int W2 = 2 * W;
+  unsigned cmask = 0;  // mixed models: the lane's camera's refined-intrinsics mask
   // odd row stride: conflict-free row writes; D & 32 (16-B readout) needs an
   // even stride: W2 + 4 gives 2-way conflicts on the row writes
   constexpr int LS = (D & 32) ? W2 + 4 : (W2 | 1);
@@ -457,7 +404,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const double iz = 1.0 / P[2];
       const double u = P[0] * iz, v = P[1] * iz;
       double x, y, A[4];
-      world_to_image_jac<M>(prm, u, v, &x, &y, A, Jp);
+      if constexpr (M == kMixedModels) {
+        const int model = (int)((meta >> 16) & 0xffu);
+        world_to_image_jac_any(model, prm, u, v, &x, &y, A, Jp);
+        cmask = cam_tangent_mask(model, p.refine_mask);
+      } else {
+        world_to_image_jac<M>(prm, u, v, &x, &y, A, Jp);
+      }
       const double r0 = x - o.x, r1 = y - o.y;
       if constexpr (LOSS == 0) {
         cost = 0.5 * (r0 * r0 + r1 * r1);
@@ -507,8 +460,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     for (int h = 0; h < NP; ++h) {
       if (lane / RP == h && i < p.nb) {
         double* row = slab + (lane % RP) * LS;
-        emit_row<M, CM>(0, row, B, Mq, pose_var, flags, jx, Jp, sc, cv);
-        emit_row<M, CM>(1, row + W, B, Mq, pose_var, flags, jx, Jp, sc, cv);
+        if constexpr (M == kMixedModels) {
+          emit_row_mixed<CT>(0, row, B, Mq, pose_var, flags, jx, Jp, sc, cv, cmask);
+          emit_row_mixed<CT>(1, row + W, B, Mq, pose_var, flags, jx, Jp, sc, cv, cmask);
+        } else {
+          emit_row<M, CM>(0, row, B, Mq, pose_var, flags, jx, Jp, sc, cv);
+          emit_row<M, CM>(1, row + W, B, Mq, pose_var, flags, jx, Jp, sc, cv);
+        }
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -541,7 +499,8 @@ __global__ void pack_images_kernel(DevProblem p, double* __restrict__ rec) {
   double* o = rec + 16 * (size_t)k;
 #pragma unroll
   for (int m = 0; m < 7; ++m) o[m] = p.qt[8 * (size_t)k + m];
-  o[7] = __longlong_as_double((long long)(p.img_flags[k] | ((p.cam_var[cam] != 0 ? 1u : 0u) << 8)));
+  o[7] = __longlong_as_double(
+      (long long)(p.img_flags[k] | ((p.cam_var[cam] != 0 ? 1u : 0u) << 8) | ((uint32_t)p.cam_model[cam] << 16)));
 #pragma unroll
   for (int m = 0; m < 8; ++m) o[8 + m] = p.cam[8 * (size_t)cam + m];
 }
@@ -553,13 +512,7 @@ __global__ __launch_bounds__(kBlock) void reproj_cost_kernel(DevProblem p, const
                                                               double* __restrict__ cost_partial) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   double cost = 0.0;
-  if (i < p.nb) {
-    BlockEval<M> e;
-    uint32_t pt;
-    bool ptv;
-    eval_block<M, false>(p, qt, cam, X, i, e, pt, ptv);
-    cost = e.cost;
-  }
+  if (i < p.nb) cost = block_cost<M>(p, qt, cam, X, i);
   const double s = wave_sum(cost);  // per-wave partial (reproj_grid)
   if ((threadIdx.x & 63) == 0 && i < p.nb) cost_partial[i >> 6] = s;
 }
@@ -1197,8 +1150,16 @@ __global__ void plus_cameras_kernel(DevProblem p, const double* __restrict__ df,
   double* o = cam_out + 8 * (size_t)k;
   for (int m = 0; m < 8; ++m) o[m] = a[m];
   if (!p.cam_var[k]) return;
+  // the camera's refined intrinsics, in parameter order, occupy the first
+  // slots of its p.ct-wide block (SubsetManifold::Plus)
   const double* d = df + 6 * (size_t)p.num_images + (size_t)p.ct * k;
-  for (int m = 0; m < p.ct; ++m) o[p.cam_tan_idx[m]] = a[p.cam_tan_idx[m]] + d[m];
+  const unsigned cm = cam_tangent_mask(p.cam_model[k], p.refine_mask);
+  int c = 0;
+  for (int m = 0; m < 8; ++m)
+    if ((cm >> m) & 1u) {
+      o[m] = a[m] + d[c];
+      ++c;
+    }
 }
 
 __global__ void plus_points_kernel(DevProblem p, const double* __restrict__ dX, const double* __restrict__ X,
@@ -1470,6 +1431,18 @@ int reproj_grid(int64_t nb) { return (int)grid_for(nb, 64); }
 void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s) {
   if (p.nb == 0) return;
   const unsigned g = grid_for(p.nb, kBlock);
+  if (p.model == kMixedModels) {
+    dispatch_ct(p.ct, [&](auto c) {
+      constexpr int CT = decltype(c)::value;
+      if (p.loss_type == kLossTrivial)
+        hipLaunchKernelGGL((reproj_jacobian_kernel<kMixedModels, 0, 0, 2, kJacProduction, 4, kBlock, CT>), dim3(g),
+                           dim3(kBlock), 0, s, p, r, J, cost_partial);
+      else
+        hipLaunchKernelGGL((reproj_jacobian_kernel<kMixedModels, 0, 1, 2, kJacProduction, 4, kBlock, CT>), dim3(g),
+                           dim3(kBlock), 0, s, p, r, J, cost_partial);
+    });
+    return;
+  }
   dispatch_model(p.model, [&](auto m) {
     constexpr int M = decltype(m)::value;
     auto go = [&](auto rf) {
@@ -1586,6 +1559,10 @@ void launch_reproj_cost(const DevProblem& p, const double* qt, const double* cam
                         double* cost_partial, hipStream_t s) {
   if (p.nb == 0) return;
   const unsigned g = grid_for(p.nb, kBlock);
+  if (p.model == kMixedModels) {
+    hipLaunchKernelGGL(reproj_cost_kernel<kMixedModels>, dim3(g), dim3(kBlock), 0, s, p, qt, cam, X, cost_partial);
+    return;
+  }
   dispatch_model(p.model, [&](auto m) {
     constexpr int M = decltype(m)::value;
     hipLaunchKernelGGL(reproj_cost_kernel<M>, dim3(g), dim3(kBlock), 0, s, p, qt, cam, X, cost_partial);

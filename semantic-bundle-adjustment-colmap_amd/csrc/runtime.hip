@@ -51,24 +51,20 @@ double now_s() {
 }
 
 // Host evaluation of one block's cost (fixed_cost of dropped blocks).
-double host_block_cost(const mi_ba_options& o, const mi_ba_problem* p, int64_t k) {
+double host_block_cost(const mi_ba_options& o, const mi_ba_problem* p, const HostSetup& s, int64_t k) {
   const int img = p->obs_image[k];
   const int cam = p->image_camera[img];
   const int64_t pt = p->obs_point[k];
-  const int np = num_params(p->camera_model);
   const double* q = p->qvec + 4 * (size_t)img;
   const double* t = p->tvec + 3 * (size_t)img;
   const double* X = p->xyz + 3 * (size_t)pt;
-  const double* prm = p->camera_params + (size_t)np * cam;
+  const double* prm = p->camera_params + s.cam_off[cam];
   double P[3];
   unit_quat_rotate(q, X, P);
   P[0] += t[0]; P[1] += t[1]; P[2] += t[2];
   const double u = P[0] / P[2], v = P[1] / P[2];
   double x = 0, y = 0;
-  dispatch_model(p->camera_model, [&](auto m) {
-    constexpr int M = decltype(m)::value;
-    world_to_image<M>(prm, u, v, &x, &y);
-  });
+  world_to_image_any(s.cam_model[cam], prm, u, v, &x, &y);
   const double r0 = x - p->obs_xy[2 * k], r1 = y - p->obs_xy[2 * k + 1];
   double rho[3];
   loss_eval(o.loss_function_type, o.loss_function_scale, r0 * r0 + r1 * r1, rho);
@@ -321,9 +317,9 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
       return fail(MI_BA_ERR_HIP);
   }
   // parameters
-  const int np = s.np;
   {
     std::vector<double> qt(8 * (size_t)I, 0.0), cm(8 * (size_t)C, 0.0);
+    std::vector<uint8_t> cmod(C);
     std::vector<uint32_t> fl(I), ic(I);
     for (int i = 0; i < I; ++i) {
       for (int m = 0; m < 4; ++m) qt[8 * i + m] = p->qvec[4 * i + m];
@@ -331,24 +327,27 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
       fl[i] = (s.img_var[i] ? 1u : 0u) | ((uint32_t)s.img_tvec_mask[i] << 1);
       ic[i] = (uint32_t)p->image_camera[i];
     }
-    for (int c = 0; c < C; ++c)
-      for (int m = 0; m < np; ++m) cm[8 * c + m] = p->camera_params[(size_t)np * c + m];
+    for (int c = 0; c < C; ++c) {
+      cmod[c] = (uint8_t)s.cam_model[c];
+      for (int64_t m = s.cam_off[c]; m < s.cam_off[c + 1]; ++m) cm[8 * c + (m - s.cam_off[c])] = p->camera_params[m];
+    }
     if (ctx->qt.alloc(8 * I) || ctx->qt_c.alloc(8 * I) || ctx->cam.alloc(8 * C) || ctx->cam_c.alloc(8 * C) ||
         ctx->X.alloc(3 * P) || ctx->X_c.alloc(3 * P) || ctx->img_flags.alloc(I) || ctx->img_cam.alloc(I) ||
-        ctx->cam_var.alloc(C) || ctx->pt_var.alloc(P) || ctx->img_rec.alloc(16 * I))
+        ctx->cam_var.alloc(C) || ctx->cam_model.alloc(C) || ctx->pt_var.alloc(P) || ctx->img_rec.alloc(16 * I))
       return fail(MI_BA_ERR_OUT_OF_MEMORY);
     if ((I && (hipMemcpy(ctx->qt.ptr, qt.data(), qt.size() * 8, hipMemcpyHostToDevice) ||
                hipMemcpy(ctx->img_flags.ptr, fl.data(), I * 4, hipMemcpyHostToDevice) ||
                hipMemcpy(ctx->img_cam.ptr, ic.data(), I * 4, hipMemcpyHostToDevice))) ||
         (C && (hipMemcpy(ctx->cam.ptr, cm.data(), cm.size() * 8, hipMemcpyHostToDevice) ||
-               hipMemcpy(ctx->cam_var.ptr, s.cam_var.data(), C, hipMemcpyHostToDevice))) ||
+               hipMemcpy(ctx->cam_var.ptr, s.cam_var.data(), C, hipMemcpyHostToDevice) ||
+               hipMemcpy(ctx->cam_model.ptr, cmod.data(), C, hipMemcpyHostToDevice))) ||
         (P && (hipMemcpy(ctx->X.ptr, p->xyz, 3 * P * 8, hipMemcpyHostToDevice) ||
                hipMemcpy(ctx->pt_var.ptr, s.pt_var.data(), P, hipMemcpyHostToDevice))))
       return fail(MI_BA_ERR_HIP);
   }
   DevProblem& d = ctx->dev;
-  d.model = p->camera_model;
-  d.np = np;
+  d.model = s.model;
+  d.np = s.np;
   d.ct = s.ct;
   d.W = 9 + s.ct;
   for (int k = 0; k < 8; ++k) d.cam_tan_idx[k] = s.cam_tan_idx[k];
@@ -368,6 +367,7 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
   d.img_flags = ctx->img_flags.ptr;
   d.img_cam = ctx->img_cam.ptr;
   d.cam_var = ctx->cam_var.ptr;
+  d.cam_model = ctx->cam_model.ptr;
   d.pt_var = ctx->pt_var.ptr;
   d.qt = ctx->qt.ptr;
   d.cam = ctx->cam.ptr;
@@ -437,7 +437,7 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
   }
   // fixed cost of dropped blocks
   double fixed = 0.0;
-  for (int64_t k : s.fixed_obs) fixed += host_block_cost(*o, p, k);
+  for (int64_t k : s.fixed_obs) fixed += host_block_cost(*o, p, s, k);
   ctx->fixed_cost = fixed;
   if (sem) {
     st = semantic_create(ctx, sem);
@@ -826,7 +826,7 @@ mi_ba_status context_writeback(mi_ba_context* ctx) {
   }
   for (int c = 0; c < C; ++c) {
     if (!s.cam_var[c]) continue;
-    for (int m = 0; m < s.np; ++m) p->camera_params[(size_t)s.np * c + m] = cm[8 * c + m];
+    for (int64_t m = s.cam_off[c]; m < s.cam_off[c + 1]; ++m) p->camera_params[m] = cm[8 * c + (m - s.cam_off[c])];
   }
   for (int64_t k = 0; k < P; ++k) {
     if (!s.pt_var[k]) continue;

@@ -12,6 +12,7 @@
 #include <cstdint>
 
 #include "../../include/mi_ba.h"
+#include "ba_math.h"
 #include "context.h"
 
 namespace miba {
@@ -52,8 +53,9 @@ struct SemanticState {
   DevArray<double> pair_blk;               // [npairs][12*12 + 12]: M = J'J (full) and g = J'r
   DevArray<double> partial;
   int64_t npartial = 0;
-  DevArray<SemTile> tiles;
+  DevArray<SemTile> tiles;                 // grouped by the model of the pair's second camera
   int ntiles = 0;
+  int model_tiles[kNumModels + 1] = {};    // tile range of each camera model
 };
 
 mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem);

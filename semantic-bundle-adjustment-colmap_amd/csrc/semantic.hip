@@ -34,6 +34,7 @@ struct SemArgs {
   const double* qt;
   const double* cam;
   const uint32_t* img_cam;
+  const uint8_t* cam_model;  // [C] model id per camera (mixed-model cost kernel)
   const uint32_t* img_flags;
   const uint32_t* raster_slot;
   const float2* dl;   // interleaved (depth, label) rasters [slot][H][W]
@@ -549,12 +550,21 @@ __global__ __launch_bounds__(kBlock) void semantic_cost_kernel(SemArgs a, double
     const double q2[4] = {qt2[0], qt2[1], qt2[2], qt2[3]}, t2[3] = {qt2[4], qt2[5], qt2[6]};
     constexpr int np = Model<M>::kNumParams;
     double K2[np];
-    const double* kc = a.cam + 8 * (size_t)a.img_cam[pr.j];
+    const uint32_t cam2 = a.img_cam[pr.j];
+    const double* kc = a.cam + 8 * (size_t)cam2;
 #pragma unroll
     for (int m = 0; m < np; ++m) K2[m] = kc[m];
     const size_t slot = a.raster_slot[pr.j];
     int st;
-    const double r = semantic_error<M>(a, smp.pc1, smp.label1, q1, t1, q2, t2, K2, a.dl + slot * a.H * a.W, &st);
+    double r;
+    if constexpr (M == kMixedModels) {
+      switch_model(a.cam_model[cam2], [&](auto m) {
+        r = semantic_error<decltype(m)::value>(a, smp.pc1, smp.label1, q1, t1, q2, t2, K2, a.dl + slot * a.H * a.W,
+                                               &st);
+      });
+    } else {
+      r = semantic_error<M>(a, smp.pc1, smp.label1, q1, t1, q2, t2, K2, a.dl + slot * a.H * a.W, &st);
+    }
     double rho[3];
     loss_eval(a.loss_type, a.loss_scale, r * r, rho);
     c = 0.5 * (a.weight * rho[0]);
@@ -665,6 +675,7 @@ SemArgs make_args(mi_ba_context* ctx, const double* qt, const double* cam) {
   a.qt = qt;
   a.cam = cam;
   a.img_cam = ctx->dev.img_cam;
+  a.cam_model = ctx->dev.cam_model;
   a.img_flags = ctx->dev.img_flags;
   a.raster_slot = S->raster_slot.ptr;
   a.dl = S->dl.ptr;
@@ -694,7 +705,7 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
   S->depth_threshold = sem->depth_error_threshold;
   S->rel_step = sem->numeric_relative_step_size;
   const int H = S->H, W = S->W, I = p->num_images;
-  const int np = num_params(p->camera_model);
+  const HostSetup& hs = ctx->setup;
   auto const_pose = [&](int i) {
     return !o.refine_extrinsics || (p->image_constant_pose && p->image_constant_pose[i]);
   };
@@ -715,7 +726,8 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
     pr.var1 = !c1;
     pr.var2 = !c2;
     pr.start = (uint32_t)samples.size();
-    const double* K1 = p->camera_params + (size_t)np * p->image_camera[i];
+    const double* K1 = p->camera_params + hs.cam_off[p->image_camera[i]];
+    const int model1 = hs.cam_model[p->image_camera[i]];
     const float* d1 = sem->depth + (size_t)i * H * W;
     const float* l1 = sem->label + (size_t)i * H * W;
     const uint32_t pair_idx = (uint32_t)S->pairs_host.size();
@@ -725,10 +737,7 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
         const float depth = d1[(size_t)y * W + x];
         if (depth < 1e-4) continue;
         double u1 = 0, v1 = 0;
-        dispatch_model(p->camera_model, [&](auto m) {
-          constexpr int M = decltype(m)::value;
-          image_to_world<M>(K1, (double)x, (double)y, &u1, &v1);
-        });
+        image_to_world_any(model1, K1, (double)x, (double)y, &u1, &v1);
         SemSample smp;
         smp.pc1[0] = u1 * (double)depth;
         smp.pc1[1] = v1 * (double)depth;
@@ -786,6 +795,16 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
   const size_t plane = (size_t)H * W;
   std::vector<uint32_t> slot_u(I, 0);
   for (int i = 0; i < I; ++i) slot_u[i] = slot[i] < 0 ? 0u : (uint32_t)slot[i];
+  // tiles grouped by the model of the pair's second camera (one launch per
+  // model present; order within a model unchanged)
+  {
+    auto tile_model = [&](const SemTile& t) { return hs.cam_model[p->image_camera[S->pairs_host[t.pair].j]]; };
+    std::stable_sort(tiles.begin(), tiles.end(),
+                     [&](const SemTile& x, const SemTile& y) { return tile_model(x) < tile_model(y); });
+    for (int m = 0; m <= kNumModels; ++m) S->model_tiles[m] = 0;
+    for (const SemTile& t : tiles) S->model_tiles[tile_model(t) + 1]++;
+    for (int m = 0; m < kNumModels; ++m) S->model_tiles[m + 1] += S->model_tiles[m];
+  }
   S->ntiles = (int)tiles.size();
   if (S->samples.alloc(S->ns) || S->pairs.alloc(S->npairs) || S->raster_slot.alloc(I) ||
       S->dl.alloc(plane * std::max<size_t>(1, slot_images.size())) || S->r.alloc(S->ns) ||
@@ -833,11 +852,16 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   timer_begin(ctx, "semantic_jacobian", &stop);
   hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 1) / 2), dim3(64), 0, s, S->pairs.ptr, S->npairs,
                      a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs);
-  dispatch_model(ctx->dev.model, [&](auto m) {
-    constexpr int M = decltype(m)::value;
-    hipLaunchKernelGGL(semantic_linearize_kernel<M>, dim3(S->ntiles), dim3(kBlock), 0, s, a, S->tiles.ptr, pcs,
-                       S->pair_blk.ptr, S->partial.ptr, S->r.ptr, S->status.ptr, S->J.ptr, write_samples ? 1 : 0);
-  });
+  for (int model = 0; model < kNumModels; ++model) {
+    const int t0 = S->model_tiles[model], nt = S->model_tiles[model + 1] - t0;
+    if (nt == 0) continue;
+    dispatch_model(model, [&](auto m) {
+      constexpr int M = decltype(m)::value;
+      hipLaunchKernelGGL(semantic_linearize_kernel<M>, dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0, pcs,
+                         S->pair_blk.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr,
+                         write_samples ? 1 : 0);
+    });
+  }
   timer_end(ctx, stop);
   launch_sum(S->partial.ptr, S->ntiles, d_cost, s);
   if (hipGetLastError() != hipSuccess) return MI_BA_ERR_HIP;
@@ -849,10 +873,14 @@ void semantic_cost(mi_ba_context* ctx, const double* qt, const double* cam, doub
   if (S->ns == 0) return;
   SemArgs a = make_args(ctx, qt, cam);
   const unsigned g = (unsigned)((S->ns + kBlock - 1) / kBlock);
-  dispatch_model(ctx->dev.model, [&](auto m) {
-    constexpr int M = decltype(m)::value;
-    hipLaunchKernelGGL(semantic_cost_kernel<M>, dim3(g), dim3(kBlock), 0, ctx->stream, a, S->partial.ptr);
-  });
+  if (ctx->dev.model == kMixedModels) {
+    hipLaunchKernelGGL(semantic_cost_kernel<kMixedModels>, dim3(g), dim3(kBlock), 0, ctx->stream, a, S->partial.ptr);
+  } else {
+    dispatch_model(ctx->dev.model, [&](auto m) {
+      constexpr int M = decltype(m)::value;
+      hipLaunchKernelGGL(semantic_cost_kernel<M>, dim3(g), dim3(kBlock), 0, ctx->stream, a, S->partial.ptr);
+    });
+  }
   launch_sum(S->partial.ptr, g, d_cost, ctx->stream);
 }
 

@@ -1,6 +1,7 @@
 // setup.cpp — host-side problem assembly (product code); see setup.h.
 #include "setup.h"
 
+#include <algorithm>
 #include <cmath>
 
 #include "ba_math.h"
@@ -35,8 +36,6 @@ void csr(const int32_t* key, int64_t n, int64_t nkeys, std::vector<int64_t>* off
 
 mi_ba_status build_setup(const mi_ba_options& o, mi_ba_problem* p, HostSetup* s) {
   if (!p) return MI_BA_ERR_INVALID_ARGUMENT;
-  const int np = num_params(p->camera_model);
-  if (np < 0) return MI_BA_ERR_UNSUPPORTED;  // std::domain_error (camera_models.h:140-141)
   if (p->num_images < 0 || p->num_cameras < 0 || p->num_points < 0 || p->num_obs < 0)
     return MI_BA_ERR_INVALID_ARGUMENT;
   if (p->num_obs > 0 && (!p->obs_xy || !p->obs_image || !p->obs_point)) return MI_BA_ERR_INVALID_ARGUMENT;
@@ -61,6 +60,23 @@ mi_ba_status build_setup(const mi_ba_options& o, mi_ba_problem* p, HostSetup* s)
     if ((tm & ~7u) != 0) return MI_BA_ERR_INVALID_ARGUMENT;
     if (cp && tm) return MI_BA_ERR_INVALID_ARGUMENT;
   }
+  // per-camera models (camera_models.h:117-141: unknown ids throw
+  // std::domain_error, :140-141)
+  if (!p->camera_model_ids && num_params(p->camera_model) < 0) return MI_BA_ERR_UNSUPPORTED;
+  s->cam_model.assign(C, 0);
+  s->cam_off.assign(C + 1, 0);
+  bool mixed = false;
+  int np = num_params(p->camera_model);
+  for (int c = 0; c < C; ++c) {
+    const int m = problem_camera_model(p, c);
+    if (num_params(m) < 0) return MI_BA_ERR_UNSUPPORTED;
+    s->cam_model[c] = m;
+    s->cam_off[c + 1] = s->cam_off[c] + num_params(m);
+    if (c == 0) np = num_params(m);
+    if (m != s->cam_model[0]) mixed = true;
+    np = std::max(np, num_params(m));
+  }
+  s->model = mixed ? kMixedModels : (C > 0 ? s->cam_model[0] : p->camera_model);
   s->np = np;
 
   std::vector<int64_t> img_off, img_items, pt_off, pt_items;
@@ -122,20 +138,39 @@ mi_ba_status build_setup(const mi_ba_options& o, mi_ba_problem* p, HostSetup* s)
       }
     }
   }
-  // ParameterizeCameras (:480-516)
-  std::vector<int> f, pp, ex, cidx;
-  param_groups(p->camera_model, &f, &pp, &ex);
-  std::vector<uint8_t> is_const(np, 0);
-  if (!o.refine_focal_length) for (int k : f) is_const[k] = 1;
-  if (!o.refine_principal_point) for (int k : pp) is_const[k] = 1;
-  if (!o.refine_extra_params) for (int k : ex) is_const[k] = 1;
-  s->ct = 0;
-  for (int k = 0; k < np; ++k)
-    if (!is_const[k]) s->cam_tan_idx[s->ct++] = k;
+  // ParameterizeCameras (:480-516): SubsetManifold over the params the
+  // refine flags hold constant, per camera model.
+  auto tangent = [&](int model, int* idx) {
+    std::vector<int> f, pp, ex;
+    param_groups(model, &f, &pp, &ex);
+    const int n = num_params(model);
+    std::vector<uint8_t> is_const(n, 0);
+    if (!o.refine_focal_length) for (int k : f) is_const[k] = 1;
+    if (!o.refine_principal_point) for (int k : pp) is_const[k] = 1;
+    if (!o.refine_extra_params) for (int k : ex) is_const[k] = 1;
+    int ct = 0;
+    for (int k = 0; k < n; ++k)
+      if (!is_const[k]) {
+        if (idx) idx[ct] = k;
+        ++ct;
+      }
+    return ct;
+  };
+  s->ct = tangent(s->model == kMixedModels ? kOpenCV : s->model, s->cam_tan_idx);
+  s->cam_ct.assign(C, 0);
+  if (s->model == kMixedModels) {
+    s->ct = 0;
+    for (int c = 0; c < C; ++c) {
+      s->cam_ct[c] = (uint8_t)tangent(s->cam_model[c], nullptr);
+      s->ct = std::max<int>(s->ct, s->cam_ct[c]);
+    }
+  } else {
+    for (int c = 0; c < C; ++c) s->cam_ct[c] = (uint8_t)s->ct;
+  }
   const bool constant_camera = !o.refine_focal_length && !o.refine_principal_point && !o.refine_extra_params;
   s->cam_var.assign(C, 0);
   for (int c = 0; c < C; ++c)
-    s->cam_var[c] = cam_in[c] && !constant_camera && !cam_const[c] && s->ct > 0;
+    s->cam_var[c] = cam_in[c] && !constant_camera && !cam_const[c] && s->cam_ct[c] > 0;
   // ParameterizePoints (:518-530)
   s->pt_var.assign(P, 0);
   for (int64_t pt = 0; pt < P; ++pt) {
@@ -174,7 +209,7 @@ mi_ba_status build_setup(const mi_ba_options& o, mi_ba_problem* p, HostSetup* s)
       ne += 6 - masked;
     }
   for (int c = 0; c < C; ++c)
-    if (used_cam[c]) ne += s->ct;
+    if (used_cam[c]) ne += s->cam_ct[c];
   s->num_effective_parameters_reduced = ne;
   return MI_BA_OK;
 }

@@ -16,9 +16,15 @@
 namespace miba {
 
 struct HostSetup {
-  int np = 0;
-  int ct = 0;
-  int cam_tan_idx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int model = 0;       // the problem's camera model, or kMixedModels
+  int np = 0;          // params per camera (the largest, mixed models)
+  int ct = 0;          // refined intrinsics slots per camera (the largest, mixed models)
+  int cam_tan_idx[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // single-model problems
+  // per camera: model id, offset of its params in mi_ba_problem::camera_params,
+  // refined intrinsics (its slots ct_c..ct-1 are padding: zero Jacobian columns)
+  std::vector<int32_t> cam_model;
+  std::vector<int64_t> cam_off;
+  std::vector<uint8_t> cam_ct;
   std::vector<int64_t> reduced_obs;   // observation index of each reduced block (program order)
   std::vector<int64_t> fixed_obs;     // blocks dropped from the reduced program
   std::vector<uint8_t> img_var;       // pose is a variable parameter block
@@ -29,6 +35,11 @@ struct HostSetup {
   int64_t num_residuals_reduced = 0;
   int64_t num_effective_parameters_reduced = 0;
 };
+
+// Model id of camera c (camera_model_ids, else camera_model).
+inline int problem_camera_model(const mi_ba_problem* p, int c) {
+  return p->camera_model_ids ? p->camera_model_ids[c] : p->camera_model;
+}
 
 // Validates the problem, normalises config qvecs in place (Image::NormalizeQvec
 // at bundle_adjustment.cc:355) and fills `s`.

@@ -80,6 +80,7 @@ class Problem(C.Structure):
         ("obs_xy", _dp),
         ("obs_image", _i32p),
         ("obs_point", _i32p),
+        ("camera_model_ids", _i32p),
     ]
 
 
@@ -238,7 +239,7 @@ def default_options(**kw) -> Options:
 class Scene:
     """Flattened Reconstruction + BundleAdjustmentConfig (numpy-owned)."""
     camera_model: int
-    camera_params: np.ndarray            # [C][np] f64
+    camera_params: np.ndarray            # [C][np] f64 (one model), or packed per camera (camera_models)
     qvec: np.ndarray                     # [I][4]
     tvec: np.ndarray                     # [I][3]
     image_camera: np.ndarray             # [I] i32
@@ -251,7 +252,19 @@ class Scene:
     image_constant_pose: Optional[np.ndarray] = None
     image_constant_tvec: Optional[np.ndarray] = None
     point_config: Optional[np.ndarray] = None
+    camera_models: Optional[np.ndarray] = None  # [C] i32 model id per camera (mixed models)
     _keep: list = field(default_factory=list, repr=False)
+
+    @property
+    def num_cameras(self):
+        return int(len(self.camera_models)) if self.camera_models is not None else int(self.camera_params.shape[0])
+
+    def camera_param_offsets(self):
+        """Offset of each camera's params in the flattened camera_params (+ total)."""
+        if self.camera_models is None:
+            n = NUM_PARAMS[self.camera_model]
+            return np.arange(self.num_cameras + 1, dtype=np.int64) * n
+        return np.concatenate([[0], np.cumsum([NUM_PARAMS[int(m)] for m in self.camera_models])]).astype(np.int64)
 
     @property
     def num_images(self):
@@ -271,7 +284,7 @@ class Scene:
         return Scene(self.camera_model, c(self.camera_params), c(self.qvec), c(self.tvec), c(self.image_camera),
                      c(self.xyz), c(self.obs_xy), c(self.obs_image), c(self.obs_point), c(self.camera_constant),
                      c(self.image_in_config), c(self.image_constant_pose), c(self.image_constant_tvec),
-                     c(self.point_config))
+                     c(self.point_config), c(self.camera_models))
 
     def gauge(self, const_pose=0, const_tvec_image=1, const_tvec_mask=1):
         """BundleAdjustmentController gauge (controllers/bundle_adjustment.cc:94-95)."""
@@ -290,6 +303,9 @@ class Scene:
             a = getattr(self, name)
             if a.dtype != dt or not a.flags.c_contiguous:
                 setattr(self, name, np.ascontiguousarray(a, dtype=dt))
+        if self.camera_models is not None and (self.camera_models.dtype != np.int32
+                                               or not self.camera_models.flags.c_contiguous):
+            self.camera_models = np.ascontiguousarray(self.camera_models, dtype=np.int32)
         for name in ("camera_constant", "image_in_config", "image_constant_pose", "image_constant_tvec",
                      "point_config"):
             a = getattr(self, name)
@@ -300,8 +316,9 @@ class Scene:
         self._normalize()
         p = Problem()
         p.camera_model = self.camera_model
-        p.num_cameras = self.camera_params.shape[0]
+        p.num_cameras = self.num_cameras
         p.camera_params = _ptr(self.camera_params, _dp)
+        p.camera_model_ids = _ptr(self.camera_models, _i32p)
         p.camera_constant = _ptr(self.camera_constant, _u8p)
         p.num_images = self.num_images
         p.qvec = _ptr(self.qvec, _dp)
@@ -542,6 +559,25 @@ def synth_config(camera_model=SIMPLE_RADIAL, num_images=2, num_points=100, track
     return c
 
 
+def convert_cameras(scene: Scene, models) -> Scene:
+    """Give camera c the model models[c % len(models)] (a mixed-model
+    reconstruction): the SIMPLE_RADIAL parameters (f, cx, cy, k) of a
+    generated scene are carried over to the other models' layouts
+    (camera_models.h *Idxs), with small second-order distortion terms."""
+    assert scene.camera_model == SIMPLE_RADIAL and scene.camera_models is None
+    ids, params = [], []
+    for c in range(scene.num_cameras):
+        f, cx, cy, k = scene.camera_params[c]
+        m = int(models[c % len(models)])
+        ids.append(m)
+        params.extend({SIMPLE_PINHOLE: [f, cx, cy], PINHOLE: [f, f * 1.01, cx, cy], SIMPLE_RADIAL: [f, cx, cy, k],
+                       RADIAL: [f, cx, cy, k, -0.01], OPENCV: [f, f * 0.99, cx, cy, k, 0.01, 1e-4, -1e-4]}[m])
+    out = scene.copy()
+    out.camera_models = np.array(ids, np.int32)
+    out.camera_params = np.array(params, np.float64)
+    return out
+
+
 def generate_scene(cfg: SynthConfig) -> Scene:
     lib = load_synth()
     n = lib.mi_ba_synth_num_obs(C.byref(cfg))
@@ -568,6 +604,16 @@ def render_semantic(scene: Scene, height: int, width: int, plane_z: float = 1.0,
     scene._normalize()
     depth = np.zeros((I, height, width), np.float32)
     label = np.zeros((I, height, width), np.float32)
+    if scene.camera_models is not None:  # mixed models: one image at a time with its camera's model
+        off = scene.camera_param_offsets()
+        for i in range(I):
+            c = int(scene.image_camera[i])
+            one = Scene(int(scene.camera_models[c]), scene.camera_params[off[c]:off[c + 1]][None, :].copy(),
+                        scene.qvec[i:i + 1].copy(), scene.tvec[i:i + 1].copy(), np.zeros(1, np.int32),
+                        scene.xyz[:0], scene.obs_xy[:0], scene.obs_image[:0], scene.obs_point[:0])
+            d, l_ = render_semantic(one, height, width, plane_z, cell)
+            depth[i], label[i] = d[0], l_[0]
+        return depth, label
     st = lib.mi_ba_synth_render(scene.camera_model, I, _ptr(scene.camera_params, _dp), _ptr(scene.qvec, _dp),
                                 _ptr(scene.tvec, _dp), _ptr(scene.image_camera, _i32p), height, width, plane_z,
                                 cell, _ptr(depth, _fp), _ptr(label, _fp))

@@ -5,6 +5,7 @@
 //   ./bundle_adjustment_test counts   structural counts only (host, no GPU)
 //   ./bundle_adjustment_test solve    full Solve on the MI355X + the
 //                                     CheckVariable*/CheckConstant* assertions
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -322,6 +323,92 @@ int main(int argc, char** argv) {
   cases.push_back({"TestConstantFocalLength", focal_case("focal", 307)});
   cases.push_back({"TestVariablePrincipalPoint", focal_case("pp", 313)});
   cases.push_back({"TestConstantExtraParam", focal_case("extra", 307)});
+
+  // Build addition: cameras of different models in one problem (the
+  // reference dispatches the model per camera, camera_models.h:117-141,
+  // bundle_adjustment.cc:396-406).  Counts: SIMPLE_RADIAL f,k + PINHOLE
+  // fx,fy + OPENCV fx,fy,k1,k2,p1,p2 = 10; poses 0 + 5 + 6; points 300.
+  cases.push_back({"TestMixedCameraModels", [](bool s) {
+    Reconstruction rec = GenerateReconstruction(3, 100);
+    rec.GetCamera(1).model_id = MI_BA_PINHOLE;
+    rec.GetCamera(1).params = {1200, 1200, 500, 500};
+    rec.GetCamera(2).model_id = MI_BA_OPENCV;
+    rec.GetCamera(2).params = {1200, 1200, 500, 500, 0, 0, 0, 0};
+    BundleAdjustmentConfig config;
+    config.AddImage(0);
+    config.AddImage(1);
+    config.AddImage(2);
+    config.SetConstantPose(0);
+    config.SetConstantTvec(1, {0});
+    BundleAdjustmentOptions options;
+    options.print_summary = false;
+    BundleAdjuster ba(options, config);
+    Expect(s, ba, rec, 600, 321, [](Reconstruction& r, const Reconstruction& o) {
+      CheckVariableCamera(r, o, 0);
+      const auto& p1 = r.GetCamera(1).params;
+      const auto& q1 = o.cameras.at(1).params;
+      CHECK_T(p1[0] != q1[0] && p1[1] != q1[1] && p1[2] == q1[2] && p1[3] == q1[3]);
+      const auto& p2 = r.GetCamera(2).params;
+      const auto& q2 = o.cameras.at(2).params;
+      CHECK_T(p2[0] != q2[0] && p2[1] != q2[1] && p2[2] == q2[2] && p2[3] == q2[3]);
+      for (int k = 4; k < 8; ++k) CHECK_T(p2[k] != q2[k]);
+      CheckConstantImage(r, o, 0);
+      CheckConstantXImage(r, o, 1);
+      CheckVariableImage(r, o, 2);
+      for (auto& p : r.points3D) CheckVariablePoint(r, o, p.first);
+    });
+  }});
+
+  // SemanticBundleAdjuster through the facade (semantic_bundle_adjustment.h:
+  // 217-225): Assert (cc:604-644) on the host, then a pose-only semantic
+  // solve over every ordered pair of three images looking at a labelled plane.
+  cases.push_back({"TestSemanticBundleAdjuster", [](bool s) {
+    Reconstruction rec = GenerateReconstruction(3, 10);
+    const int H = 60, W = 60;
+    SemanticMaps maps;
+    maps.height = H;
+    maps.width = W;
+    for (auto& e : rec.images) {
+      Image& im = e.second;
+      std::vector<float> depth((size_t)H * W), label((size_t)H * W);
+      // the plane z = 0 at camera depth tvec[2] = 10; labels: 0.5-wide checkerboard
+      for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+          const double d = im.tvec[2];
+          const double X = (x - 500.0 + 470.0) / 1200.0 * d - im.tvec[0];
+          const double Y = (y - 500.0 + 470.0) / 1200.0 * d - im.tvec[1];
+          depth[(size_t)y * W + x] = (float)d;
+          label[(size_t)y * W + x] = (float)((((int)std::floor(X / 0.05) + (int)std::floor(Y / 0.05)) % 2 + 2) % 2);
+        }
+      maps.depth[im.name] = depth;
+      maps.semantic[im.name] = label;
+      // a principal point near the raster so the pairs overlap inside it
+      rec.GetCamera(im.camera_id).params = {1200, 30, 30, 0};
+      im.tvec[0] += 0.002 * (double)im.image_id;  // pose error for the semantic term to pull on
+    }
+    SemanticBundleAdjustmentOptions options;
+    options.print_summary = false;
+    options.error_computation_pixel_step = 3;
+    SemanticBundleAdjustmentConfig config;
+    for (image_t i = 0; i < 3; ++i) config.AddImage(i);
+    config.SetConstantPose(0);
+    {
+      SemanticBundleAdjuster bad(options, config, maps);  // cameras not constant: Assert throws
+      bool threw = false;
+      try { bad.Solve(&rec); } catch (const std::runtime_error&) { threw = true; }
+      CHECK_T(threw);
+    }
+    for (camera_t c = 0; c < 3; ++c) config.SetConstantCamera(c);
+    if (!s) return;
+    const Reconstruction orig = rec;
+    SemanticBundleAdjuster sba(options, config, maps);
+    CHECK_T(sba.Solve(&rec));
+    CHECK_T(sba.Summary().num_residuals_reduced > 0);
+    CHECK_T(sba.Summary().final_cost <= sba.Summary().initial_cost);
+    CheckConstantImage(rec, orig, 0);
+    for (camera_t c = 0; c < 3; ++c) CheckConstantCamera(rec, orig, c);
+    for (auto& p : rec.points3D) CheckConstantPoint(rec, orig, p.first);
+  }});
 
   cases.push_back({"TestInvalidConfig", [](bool) {
     BundleAdjustmentConfig config;
