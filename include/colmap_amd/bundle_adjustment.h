@@ -83,6 +83,7 @@ struct Image {
 
 struct Point3D {
   double xyz[3] = {0, 0, 0};
+  double error = -1.0;
   std::vector<TrackElement> track;
 };
 
@@ -119,6 +120,20 @@ class Reconstruction {
              tr.end());
     p2.point3D_id = kInvalidPoint3DId;
   }
+  void DeletePoint3D(point3D_t id) {
+    for (const TrackElement& te : points3D.at(id).track)
+      images.at(te.image_id).points2D.at(te.point2D_idx).point3D_id = kInvalidPoint3DId;
+    points3D.erase(id);
+  }
+
+  // Reconstruction::FilterPoints3DWithLargeReprojectionError
+  // (reconstruction.cc:1472-1525) on the GPU (mi_ba_filter_points3d): the
+  // given points' track elements are flattened in Track order, their errors
+  // evaluated and the decisions applied here.  Returns the number of
+  // observations filtered.
+  size_t FilterPoints3DWithLargeReprojectionError(double max_reproj_error,
+                                                  const std::unordered_set<point3D_t>& point3D_ids,
+                                                  int device = 0);
 
  private:
   point3D_t num_added_points3D_ = 0;
@@ -399,6 +414,75 @@ inline SolverSummary ToSummary(const mi_ba_summary& s) {
 }
 
 }  // namespace internal
+
+inline size_t Reconstruction::FilterPoints3DWithLargeReprojectionError(
+    double max_reproj_error, const std::unordered_set<point3D_t>& point3D_ids, int device) {
+  std::unordered_map<camera_t, int32_t> cidx;
+  std::unordered_map<image_t, int32_t> iidx;
+  std::vector<camera_t> cam_ids;
+  std::vector<image_t> img_ids;
+  std::vector<point3D_t> pt_ids;
+  std::vector<double> params, qv, tv, xyz, obs_xy;
+  std::vector<int32_t> models, image_camera, obs_image, obs_point;
+  std::vector<TrackElement> obs_te;
+  for (const auto& c : cameras) {
+    cidx[c.first] = (int32_t)cam_ids.size();
+    cam_ids.push_back(c.first);
+    models.push_back(c.second.model_id);
+    params.insert(params.end(), c.second.params.begin(), c.second.params.end());
+  }
+  for (const auto& im : images) {
+    iidx[im.first] = (int32_t)img_ids.size();
+    img_ids.push_back(im.first);
+    qv.insert(qv.end(), im.second.qvec, im.second.qvec + 4);
+    tv.insert(tv.end(), im.second.tvec, im.second.tvec + 3);
+    image_camera.push_back(cidx.at(im.second.camera_id));
+  }
+  for (const point3D_t id : point3D_ids) {
+    auto it = points3D.find(id);
+    if (it == points3D.end()) continue;  // ExistsPoint3D (:1481-1483)
+    const int32_t p = (int32_t)pt_ids.size();
+    pt_ids.push_back(id);
+    xyz.insert(xyz.end(), it->second.xyz, it->second.xyz + 3);
+    for (const TrackElement& te : it->second.track) {
+      const Point2D& p2 = images.at(te.image_id).points2D.at(te.point2D_idx);
+      obs_xy.push_back(p2.xy[0]);
+      obs_xy.push_back(p2.xy[1]);
+      obs_image.push_back(iidx.at(te.image_id));
+      obs_point.push_back(p);
+      obs_te.push_back(te);
+    }
+  }
+  mi_ba_problem pr{};
+  pr.camera_model = models.empty() ? MI_BA_SIMPLE_RADIAL : models[0];
+  pr.camera_model_ids = models.data();
+  pr.num_cameras = (int32_t)cam_ids.size();
+  pr.camera_params = params.data();
+  pr.num_images = (int32_t)img_ids.size();
+  pr.qvec = qv.data();
+  pr.tvec = tv.data();
+  pr.image_camera = image_camera.data();
+  pr.num_points = (int64_t)pt_ids.size();
+  pr.xyz = xyz.data();
+  pr.num_obs = (int64_t)obs_image.size();
+  pr.obs_xy = obs_xy.data();
+  pr.obs_image = obs_image.data();
+  pr.obs_point = obs_point.data();
+  std::vector<uint8_t> obs_keep(obs_image.size()), point_keep(pt_ids.size());
+  std::vector<double> err(pt_ids.size());
+  for (size_t p = 0; p < pt_ids.size(); ++p) err[p] = points3D.at(pt_ids[p]).error;
+  int64_t num_filtered = 0;
+  internal::ThrowStatus(mi_ba_filter_points3d(&pr, max_reproj_error, nullptr, device, obs_keep.data(),
+                                              point_keep.data(), err.data(), &num_filtered),
+                        "FilterPoints3DWithLargeReprojectionError");
+  for (size_t k = 0; k < obs_te.size(); ++k)
+    if (point_keep[obs_point[k]] && !obs_keep[k]) DeleteObservation(obs_te[k].image_id, obs_te[k].point2D_idx);
+  for (size_t p = 0; p < pt_ids.size(); ++p) {
+    if (!point_keep[p]) DeletePoint3D(pt_ids[p]);
+    else points3D.at(pt_ids[p]).error = err[p];
+  }
+  return (size_t)num_filtered;
+}
 
 // ---------------------------------------------------------------------------
 // BundleAdjuster (bundle_adjustment.h:171-203)

@@ -25,6 +25,10 @@
  *                                 block (src/base/semantic_cost_functions.h:87-404),
  *                                 reduced into Schur normal equations (Ceres 2.1
  *                                 SchurEliminator, 3rd party, not vendored)
+ *   mi_ba_squared_reprojection_errors / mi_ba_filter_points3d
+ *                              <- CalculateSquaredReprojectionError (src/base/projection.cc:111-128),
+ *                                 Reconstruction::FilterPoints3DWithLargeReprojectionError
+ *                                 (src/base/reconstruction.cc:1472-1525)
  *   mi_ba_semantic (struct)    <- SemanticBundleAdjustmentOptions depth/semantic maps
  *                                 (src/optim/semantic_bundle_adjustment.h:53-140,
  *                                 semantic_bundle_adjustment.cc:699-906,1021-1068)
@@ -212,6 +216,29 @@ mi_ba_status mi_ba_setup_stats(const mi_ba_options* options,
 mi_ba_status mi_ba_solve(const mi_ba_options* options, mi_ba_problem* problem,
                          const mi_ba_semantic* semantic /* nullable */,
                          mi_ba_summary* summary);
+
+/* --- reprojection errors and track filtering (host buffers in and out) --
+ * mi_ba_squared_reprojection_errors: CalculateSquaredReprojectionError
+ * (src/base/projection.cc:111-128) of every observation at the problem's
+ * current parameters; DBL_MAX where the point is behind the camera
+ * (z < DBL_EPSILON).  qvec need not be normalised (QuaternionRotatePoint
+ * normalises).
+ * mi_ba_filter_points3d: Reconstruction::FilterPoints3DWithLargeReprojectionError
+ * (src/base/reconstruction.cc:1472-1525) over the points with point_mask[p]
+ * != 0 (NULL = every point): a point's observations with squared error above
+ * max_reproj_error^2 are dropped (obs_keep[k] = 0); a point left with fewer
+ * than two (or with a track shorter than two) is deleted (point_keep[p] = 0,
+ * all its observations dropped); otherwise point_error[p] = mean
+ * reprojection error of the kept observations (unmasked and deleted points
+ * keep the caller's value).  *num_filtered = observations dropped, as the
+ * reference's return value.  A point's observations are visited in problem
+ * order (the flatteners emit them in Track order). */
+mi_ba_status mi_ba_squared_reprojection_errors(const mi_ba_problem* problem, int32_t device,
+                                               double* sq_errors);
+mi_ba_status mi_ba_filter_points3d(const mi_ba_problem* problem, double max_reproj_error,
+                                   const uint8_t* point_mask /* nullable */, int32_t device,
+                                   uint8_t* obs_keep, uint8_t* point_keep, double* point_error,
+                                   int64_t* num_filtered);
 
 /* --- resident context (device-resident problem, for throughput/parity) - */
 mi_ba_status mi_ba_context_create(const mi_ba_options* options,

@@ -96,6 +96,59 @@ def squared_reprojection_error(model, params, xy, X, q, t):
     return load().oracle_squared_reprojection_error(model, *[a[1] for a in arrs])
 
 
+def scene_squared_reprojection_errors(scene):
+    """CalculateSquaredReprojectionError (projection.cc:111-128) of every
+    observation of a flattened scene (per-camera models)."""
+    off = scene.camera_param_offsets()
+    out = np.zeros(scene.num_obs)
+    for k in range(scene.num_obs):
+        i, p = int(scene.obs_image[k]), int(scene.obs_point[k])
+        c = int(scene.image_camera[i])
+        model = int(scene.camera_models[c]) if scene.camera_models is not None else scene.camera_model
+        out[k] = squared_reprojection_error(model, scene.camera_params.reshape(-1)[off[c]:off[c + 1]],
+                                            scene.obs_xy[k], scene.xyz[p], scene.qvec[i], scene.tvec[i])
+    return out
+
+
+def filter_points3d(scene, max_reproj_error, point_mask=None, point_error=None, sq=None):
+    """Reconstruction::FilterPoints3DWithLargeReprojectionError
+    (reconstruction.cc:1472-1525) over every point with point_mask[p] != 0;
+    a point's track elements in observation order.  Returns (obs_keep,
+    point_keep, point_error, num_filtered)."""
+    sq = scene_squared_reprojection_errors(scene) if sq is None else sq
+    max_sq = max_reproj_error * max_reproj_error
+    P = scene.num_points
+    obs_keep = np.ones(scene.num_obs, bool)
+    point_keep = np.ones(P, bool)
+    err = np.zeros(P) if point_error is None else np.array(point_error, np.float64)
+    order = np.argsort(scene.obs_point, kind="stable")
+    bounds = np.searchsorted(scene.obs_point[order], np.arange(P + 1))
+    num_filtered = 0
+    for p in range(P):
+        if point_mask is not None and not point_mask[p]:
+            continue
+        track = order[bounds[p]:bounds[p + 1]]
+        if len(track) < 2:                                   # :1486-1490
+            num_filtered += len(track)
+            point_keep[p] = False
+            obs_keep[track] = False
+            continue
+        bad = [k for k in track if sq[k] > max_sq]           # :1496-1504
+        s = 0.0
+        for k in track:
+            if not sq[k] > max_sq:
+                s += float(np.sqrt(sq[k]))
+        if len(bad) >= len(track) - 1:                       # :1507-1509
+            num_filtered += len(track)
+            point_keep[p] = False
+            obs_keep[track] = False
+        else:                                                # :1510-1516
+            num_filtered += len(bad)
+            obs_keep[bad] = False
+            err[p] = s / (len(track) - len(bad))
+    return obs_keep, point_keep, err, num_filtered
+
+
 def setup_stats(options, scene) -> "mi_ba.SetupInfo":
     info = mi_ba.SetupInfo()
     sc = scene.copy()  # SetUp normalises qvecs in place

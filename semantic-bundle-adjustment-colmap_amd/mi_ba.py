@@ -195,6 +195,9 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_context_set_comm.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
     lib.mi_ba_context_set_host_reducer.argtypes = [C.c_void_p, C.c_int32, C.c_int32, HOST_ALLREDUCE_FN, C.c_void_p]
     lib.mi_ba_dense_cholesky.argtypes = [C.c_int32, C.c_int32, _dp, _dp, C.c_int32, C.c_int32, C.c_int32, _i32p]
+    lib.mi_ba_squared_reprojection_errors.argtypes = [C.c_void_p, C.c_int32, _dp]
+    lib.mi_ba_filter_points3d.argtypes = [C.c_void_p, C.c_double, _u8p, C.c_int32, _u8p, _u8p, _dp,
+                                          C.POINTER(C.c_int64)]
     _lib = lib
     return lib
 
@@ -399,6 +402,31 @@ def dense_cholesky(A: np.ndarray, b: Optional[np.ndarray] = None, device: int = 
     check(load().mi_ba_dense_cholesky(device, n, F.ctypes.data_as(_dp), _ptr(x, _dp), panel, lookahead, own_diag,
                                       C.byref(info)), "mi_ba_dense_cholesky")
     return np.tril(F), x, info.value
+
+
+def squared_reprojection_errors(scene: Scene, device: int = 0) -> np.ndarray:
+    """CalculateSquaredReprojectionError of every observation (projection.cc:111-128)."""
+    p = scene.problem()
+    out = np.zeros(scene.num_obs)
+    check(load().mi_ba_squared_reprojection_errors(C.byref(p), device, out.ctypes.data_as(_dp)),
+          "mi_ba_squared_reprojection_errors")
+    return out
+
+
+def filter_points3d(scene: Scene, max_reproj_error: float, point_mask: Optional[np.ndarray] = None,
+                    point_error: Optional[np.ndarray] = None, device: int = 0):
+    """FilterPoints3DWithLargeReprojectionError (reconstruction.cc:1472-1525).
+    Returns (obs_keep, point_keep, point_error, num_filtered)."""
+    p = scene.problem()
+    obs_keep = np.zeros(scene.num_obs, np.uint8)
+    point_keep = np.zeros(scene.num_points, np.uint8)
+    err = np.zeros(scene.num_points) if point_error is None else np.array(point_error, np.float64)
+    mask = None if point_mask is None else np.ascontiguousarray(point_mask, dtype=np.uint8)
+    nf = C.c_int64(0)
+    check(load().mi_ba_filter_points3d(C.byref(p), max_reproj_error, _ptr(mask, _u8p), device,
+                                       obs_keep.ctypes.data_as(_u8p), point_keep.ctypes.data_as(_u8p),
+                                       err.ctypes.data_as(_dp), C.byref(nf)), "mi_ba_filter_points3d")
+    return obs_keep.astype(bool), point_keep.astype(bool), err, nf.value
 
 
 def device_count() -> int:

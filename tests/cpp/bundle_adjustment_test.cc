@@ -410,6 +410,51 @@ int main(int argc, char** argv) {
     for (auto& p : rec.points3D) CheckConstantPoint(rec, orig, p.first);
   }});
 
+  // Reconstruction::FilterPoints3DWithLargeReprojectionError
+  // (reconstruction.cc:1472-1525) on the GPU against its rule restated here.
+  cases.push_back({"TestFilterPoints3D", [](bool s) {
+    if (!s) return;
+    Reconstruction rec = GenerateReconstruction(3, 100);
+    // outliers: point p gets p % 4 of its observations moved by 30 px
+    for (auto& e : rec.points3D) {
+      int n = 0;
+      for (const TrackElement& te : e.second.track)
+        if (n++ < (int)(e.first % 4)) rec.GetImage(te.image_id).points2D[te.point2D_idx].xy[0] += 30.0;
+    }
+    const Reconstruction orig = rec;
+    std::unordered_set<point3D_t> ids;
+    for (auto& e : rec.points3D) ids.insert(e.first);
+    const double max_err = 5.0;
+    // expected: squared error of each element (SIMPLE_RADIAL, k = 0, identity rotations)
+    size_t expect = 0;
+    std::vector<point3D_t> expect_deleted;
+    for (auto& e : orig.points3D) {
+      size_t bad = 0;
+      for (const TrackElement& te : e.second.track) {
+        const Image& im = orig.GetImage(te.image_id);
+        const double* X = e.second.xyz;
+        const double pz = X[2] + im.tvec[2];
+        const double x = 1200 * (X[0] + im.tvec[0]) / pz + 500, y = 1200 * (X[1] + im.tvec[1]) / pz + 500;
+        const double* o = im.points2D[te.point2D_idx].xy;
+        if ((x - o[0]) * (x - o[0]) + (y - o[1]) * (y - o[1]) > max_err * max_err) ++bad;
+      }
+      if (bad >= e.second.track.size() - 1) {
+        expect += e.second.track.size();
+        expect_deleted.push_back(e.first);
+      } else {
+        expect += bad;
+      }
+    }
+    const size_t n = rec.FilterPoints3DWithLargeReprojectionError(max_err, ids);
+    CHECK_T(n == expect);
+    CHECK_T(rec.points3D.size() == orig.points3D.size() - expect_deleted.size());
+    for (point3D_t id : expect_deleted) CHECK_T(rec.points3D.count(id) == 0);
+    for (auto& e : rec.points3D) {
+      CHECK_T(e.second.track.size() == 3 - e.first % 4);
+      CHECK_T(e.second.error >= 0.0 && e.second.error < max_err);
+    }
+  }});
+
   cases.push_back({"TestInvalidConfig", [](bool) {
     BundleAdjustmentConfig config;
     bool threw = false;
