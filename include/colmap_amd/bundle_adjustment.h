@@ -49,6 +49,7 @@ const point3D_t kInvalidPoint3DId = std::numeric_limits<point3D_t>::max();
 struct Camera {
   camera_t camera_id = 0;
   int model_id = MI_BA_SIMPLE_RADIAL;
+  uint64_t width = 0, height = 0;
   std::vector<double> params;
   double* ParamsData() { return params.data(); }
   int ModelId() const { return model_id; }
@@ -73,6 +74,8 @@ struct Image {
   double qvec[4] = {1, 0, 0, 0};
   double tvec[3] = {0, 0, 0};
   std::vector<Point2D> points2D;
+  bool registered = true;
+  bool IsRegistered() const { return registered; }
   image_t ImageId() const { return image_id; }
   camera_t CameraId() const { return camera_id; }
   const std::string& Name() const { return name; }
@@ -83,6 +86,7 @@ struct Image {
 
 struct Point3D {
   double xyz[3] = {0, 0, 0};
+  uint8_t color[3] = {0, 0, 0};
   double error = -1.0;
   std::vector<TrackElement> track;
 };
@@ -107,6 +111,11 @@ class Reconstruction {
     std::copy(xyz, xyz + 3, p.xyz);
     points3D[id] = p;
     return id;
+  }
+  // A point with a given id (model readers); later AddPoint3D ids continue after it.
+  void SetPoint3D(point3D_t id, const Point3D& p) {
+    points3D[id] = p;
+    num_added_points3D_ = std::max(num_added_points3D_, id);
   }
   void AddObservation(point3D_t point3D_id, const TrackElement& te) {
     images.at(te.image_id).points2D.at(te.point2D_idx).point3D_id = point3D_id;
@@ -623,6 +632,131 @@ class SemanticBundleAdjuster {
   SemanticBundleAdjustmentOptions options_;
   SemanticBundleAdjustmentConfig config_;
   SemanticMaps maps_;
+  SolverSummary summary_;
+  bool used_ = false;
+};
+
+// ---------------------------------------------------------------------------
+// ParallelBundleAdjuster (bundle_adjustment.h:208-268, bundle_adjustment.cc:
+// 536-783): the PBA entry point COLMAP's mapper takes for global BA when
+// ba_global_use_pba is set (controllers/incremental_mapper.cc:66-71,
+// sfm/incremental_mapper.cc:716-747).  Same Options, construction CHECKs,
+// IsSupported rule and problem: every config image (SIMPLE_RADIAL, no shared
+// intrinsics), the measurements of config images only, every point they see
+// variable, per-image camera state (constant pose + intrinsics / fixed
+// intrinsics / variable).  PBA's own float LM is replaced by the MI355X
+// solver in f64 with Ceres' LM semantics (max_num_iterations from Options);
+// Summary() reports that solve's counts and costs.
+// ---------------------------------------------------------------------------
+class ParallelBundleAdjuster {
+ public:
+  struct Options {
+    bool print_summary = true;
+    int max_num_iterations = 50;
+    int gpu_index = -1;  // -1: device 0
+    int num_threads = -1;
+    int min_num_residuals_for_multi_threading = 50000;
+    bool Check() const {
+      if (max_num_iterations < 0) throw std::invalid_argument("max_num_iterations must be >= 0");
+      return true;
+    }
+  };
+
+  ParallelBundleAdjuster(const Options& options, const BundleAdjustmentOptions& ba_options,
+                         const BundleAdjustmentConfig& config)
+      : options_(options), ba_options_(ba_options), config_(config) {
+    options_.Check();
+    ba_options_.Check();
+    if (config_.NumConstantCameras() != 0)
+      throw std::invalid_argument("PBA does not allow to set individual cameras constant");
+    if (config_.NumConstantPoses() != 0)
+      throw std::invalid_argument("PBA does not allow to set individual translational elements constant");
+    if (config_.NumConstantTvecs() != 0)
+      throw std::invalid_argument("PBA does not allow to set individual translational elements constant");
+    if (config_.NumVariablePoints() != 0 || config_.NumConstantPoints() != 0)
+      throw std::invalid_argument("PBA does not allow to parameterize individual 3D points");
+  }
+
+  static bool IsSupported(const BundleAdjustmentOptions& options, const Reconstruction& reconstruction) {
+    if (options.refine_principal_point || options.refine_focal_length != options.refine_extra_params) return false;
+    std::unordered_set<camera_t> camera_ids;
+    for (const auto& im : reconstruction.images) {
+      if (!im.second.IsRegistered()) continue;
+      const auto cam = reconstruction.cameras.find(im.second.camera_id);
+      if (camera_ids.count(im.second.camera_id) != 0 || cam == reconstruction.cameras.end() ||
+          cam->second.model_id != MI_BA_SIMPLE_RADIAL)
+        return false;
+      camera_ids.insert(im.second.camera_id);
+    }
+    return true;
+  }
+
+  bool Solve(Reconstruction* reconstruction) {
+    if (!reconstruction) throw std::invalid_argument("reconstruction is null");
+    if (used_) throw std::logic_error("Cannot use the same ParallelBundleAdjuster multiple times");
+    used_ = true;
+    if (ba_options_.refine_principal_point) throw std::invalid_argument("PBA: refine_principal_point");
+    if (ba_options_.refine_focal_length != ba_options_.refine_extra_params)
+      throw std::invalid_argument("PBA: refine_focal_length != refine_extra_params");
+    // AddImagesToProblem (bundle_adjustment.cc:680-728)
+    std::unordered_set<camera_t> cams;
+    for (const image_t id : config_.Images()) {
+      const Image& im = reconstruction->GetImage(id);
+      if (!cams.insert(im.camera_id).second) throw std::invalid_argument("PBA does not support shared intrinsics");
+      if (reconstruction->GetCamera(im.camera_id).model_id != MI_BA_SIMPLE_RADIAL)
+        throw std::domain_error("PBA only supports the SIMPLE_RADIAL camera model");
+    }
+    // The PBA problem: config images only (their measurements); every point
+    // they observe is variable because no other image's observation enters.
+    Reconstruction sub;
+    for (const image_t id : config_.Images()) {
+      const Image& im = reconstruction->GetImage(id);
+      sub.AddCamera(reconstruction->GetCamera(im.camera_id));
+      Image copy = im;
+      for (Point2D& p2 : copy.points2D) p2.point3D_id = kInvalidPoint3DId;
+      sub.AddImage(copy);
+    }
+    std::unordered_map<point3D_t, point3D_t> sub_id;
+    for (const image_t id : config_.Images()) {
+      const Image& im = reconstruction->GetImage(id);
+      for (point2D_t k = 0; k < (point2D_t)im.points2D.size(); ++k) {
+        const point3D_t pid = im.points2D[k].point3D_id;
+        if (pid == kInvalidPoint3DId) continue;
+        auto it = sub_id.find(pid);
+        if (it == sub_id.end()) it = sub_id.emplace(pid, sub.AddPoint3D(reconstruction->GetPoint3D(pid).xyz)).first;
+        sub.AddObservation(it->second, TrackElement{id, k});
+      }
+    }
+    BundleAdjustmentConfig cfg;
+    for (const image_t id : config_.Images()) cfg.AddImage(id);
+    BundleAdjustmentOptions o = ba_options_;
+    o.solver_options.max_num_iterations = options_.max_num_iterations;
+    o.print_summary = options_.print_summary;
+    o.device = options_.gpu_index < 0 ? 0 : options_.gpu_index;
+    BundleAdjuster ba(o, cfg);
+    if (!ba.Solve(&sub)) return false;
+    summary_ = ba.Summary();
+    // TearDown (:742-766): poses, focal length + distortion, points
+    for (const image_t id : config_.Images()) {
+      Image& im = reconstruction->GetImage(id);
+      const Image& s = sub.GetImage(id);
+      std::copy(s.qvec, s.qvec + 4, im.qvec);
+      std::copy(s.tvec, s.tvec + 3, im.tvec);
+      reconstruction->GetCamera(im.camera_id).params = sub.GetCamera(im.camera_id).params;
+    }
+    for (const auto& e : sub_id) {
+      const double* x = sub.GetPoint3D(e.second).xyz;
+      std::copy(x, x + 3, reconstruction->GetPoint3D(e.first).xyz);
+    }
+    return true;
+  }
+
+  const SolverSummary& Summary() const { return summary_; }
+
+ private:
+  Options options_;
+  BundleAdjustmentOptions ba_options_;
+  BundleAdjustmentConfig config_;
   SolverSummary summary_;
   bool used_ = false;
 };

@@ -455,6 +455,66 @@ int main(int argc, char** argv) {
     }
   }});
 
+  // ParallelBundleAdjuster (bundle_adjustment.cc:536-783) routed to the GPU
+  // solver: the PBA problem has the config images' measurements only, so
+  // every point they see is variable (here: images 0 and 1 of 3, 400
+  // residuals, 2 * (6 + 2) + 300 parameters).
+  cases.push_back({"TestParallelBundleAdjuster", [](bool s) {
+    Reconstruction rec = GenerateReconstruction(3, 100);
+    BundleAdjustmentOptions options;
+    options.print_summary = false;
+    CHECK_T(ParallelBundleAdjuster::IsSupported(options, rec));
+    BundleAdjustmentOptions pp = options;
+    pp.refine_principal_point = true;
+    CHECK_T(!ParallelBundleAdjuster::IsSupported(pp, rec));
+    BundleAdjustmentOptions ex = options;
+    ex.refine_extra_params = false;
+    CHECK_T(!ParallelBundleAdjuster::IsSupported(ex, rec));
+    Reconstruction shared = rec;
+    shared.GetImage(1).camera_id = 0;
+    CHECK_T(!ParallelBundleAdjuster::IsSupported(options, shared));
+    Reconstruction pinhole = rec;
+    pinhole.GetCamera(2).model_id = MI_BA_PINHOLE;
+    pinhole.GetCamera(2).params = {1200, 1200, 500, 500};
+    CHECK_T(!ParallelBundleAdjuster::IsSupported(options, pinhole));
+    ParallelBundleAdjuster::Options po;
+    po.print_summary = false;
+    {
+      BundleAdjustmentConfig bad;
+      bad.AddImage(0);
+      bad.SetConstantCamera(0);
+      bool threw = false;
+      try { ParallelBundleAdjuster pba(po, options, bad); } catch (const std::invalid_argument&) { threw = true; }
+      CHECK_T(threw);
+      bad = BundleAdjustmentConfig();
+      bad.AddImage(0);
+      bad.AddVariablePoint(1);
+      threw = false;
+      try { ParallelBundleAdjuster pba(po, options, bad); } catch (const std::invalid_argument&) { threw = true; }
+      CHECK_T(threw);
+    }
+    if (!s) return;
+    BundleAdjustmentConfig config;
+    config.AddImage(0);
+    config.AddImage(1);
+    const Reconstruction orig = rec;
+    ParallelBundleAdjuster pba(po, options, config);
+    CHECK_T(pba.Solve(&rec));
+    CHECK_T(pba.Summary().num_residuals_reduced == 400);
+    CHECK_T(pba.Summary().num_effective_parameters_reduced == 2 * (6 + 2) + 300);
+    CHECK_T(pba.Summary().final_cost <= pba.Summary().initial_cost);
+    CheckVariableImage(rec, orig, 0);
+    CheckVariableImage(rec, orig, 1);
+    CheckVariableCamera(rec, orig, 0);
+    CheckVariableCamera(rec, orig, 1);
+    CheckConstantImage(rec, orig, 2);
+    CheckConstantCamera(rec, orig, 2);
+    for (auto& p : rec.points3D) CheckVariablePoint(rec, orig, p.first);
+    bool threw = false;
+    try { pba.Solve(&rec); } catch (const std::logic_error&) { threw = true; }
+    CHECK_T(threw);
+  }});
+
   cases.push_back({"TestInvalidConfig", [](bool) {
     BundleAdjustmentConfig config;
     bool threw = false;

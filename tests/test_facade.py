@@ -26,10 +26,10 @@ def run(mode):
 
 def test_facade_counts_cpu():
     out = run("counts")
-    assert out.count("PASS") == 14
+    assert out.count("PASS") == 15
 
 
 @pytest.mark.gpu
 def test_facade_solve_gpu(gpu):
     out = run("solve")
-    assert out.count("PASS") == 14
+    assert out.count("PASS") == 15
