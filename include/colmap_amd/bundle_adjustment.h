@@ -493,6 +493,20 @@ inline size_t Reconstruction::FilterPoints3DWithLargeReprojectionError(
   return (size_t)num_filtered;
 }
 
+// Device resources reused by consecutive solves of one host thread (the
+// mapper's repeated local BAs): pass the same arena to every Solve.
+class SolverArena {
+ public:
+  SolverArena() = default;
+  SolverArena(const SolverArena&) = delete;
+  SolverArena& operator=(const SolverArena&) = delete;
+  ~SolverArena() { mi_ba_context_destroy(ctx_); }
+  mi_ba_context** get() { return &ctx_; }
+
+ private:
+  mi_ba_context* ctx_ = nullptr;
+};
+
 // ---------------------------------------------------------------------------
 // BundleAdjuster (bundle_adjustment.h:171-203)
 // ---------------------------------------------------------------------------
@@ -503,7 +517,8 @@ class BundleAdjuster {
     options_.Check();
   }
 
-  bool Solve(Reconstruction* reconstruction) {
+  // arena (optional): device resources kept across solves (SolverArena)
+  bool Solve(Reconstruction* reconstruction, SolverArena* arena = nullptr) {
     if (!reconstruction) throw std::invalid_argument("reconstruction is null");
     if (used_) throw std::logic_error("Cannot use the same BundleAdjuster multiple times");
     used_ = true;
@@ -511,7 +526,8 @@ class BundleAdjuster {
     flat.Build(*reconstruction, config_);
     const mi_ba_options o = internal::ToOptions(options_);
     mi_ba_summary s;
-    const mi_ba_status st = mi_ba_solve(&o, &flat.problem, nullptr, &s);
+    const mi_ba_status st = arena ? mi_ba_solve_in(arena->get(), &o, &flat.problem, nullptr, &s)
+                                  : mi_ba_solve(&o, &flat.problem, nullptr, &s);
     if (st == MI_BA_ERR_NO_RESIDUALS) return false;
     internal::ThrowStatus(st, "BundleAdjuster::Solve");
     summary_ = internal::ToSummary(s);

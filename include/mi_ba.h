@@ -217,6 +217,26 @@ mi_ba_status mi_ba_solve(const mi_ba_options* options, mi_ba_problem* problem,
                          const mi_ba_semantic* semantic /* nullable */,
                          mi_ba_summary* summary);
 
+/* --- repeated solves (the incremental mapper's local / global BAs) -------
+ * As mi_ba_solve, on the context in *arena (NULL: one is created) whose
+ * device resources — stream, rocBLAS handles, Cholesky workspace, device
+ * arrays large enough for the new problem — are reused; the context stays
+ * in *arena for the next call (NULL after a failed call).  Release it with
+ * mi_ba_context_destroy.  One arena per host thread. */
+mi_ba_status mi_ba_solve_in(mi_ba_context** arena, const mi_ba_options* options, mi_ba_problem* problem,
+                            const mi_ba_semantic* semantic /* nullable */, mi_ba_summary* summary);
+
+/* --- many independent problems (incremental-mapper local BAs, submodels) -
+ * Solves problems[k] with options[k] (and semantics[k] when semantics is not
+ * NULL) for k < n, as mi_ba_solve would one after the other, with up to
+ * max_concurrent (<= 0: 8) solves in flight on their own contexts and HIP
+ * streams.  statuses[k] / summaries[k] are mi_ba_solve's per problem; the
+ * call itself fails only on invalid arguments.  Problems must not share
+ * arrays they write (parameters). */
+mi_ba_status mi_ba_solve_batch(const mi_ba_options* options, mi_ba_problem* problems,
+                               const mi_ba_semantic* const* semantics /* nullable */, int32_t n,
+                               int32_t max_concurrent, mi_ba_summary* summaries, int32_t* statuses);
+
 /* --- reprojection errors and track filtering (host buffers in and out) --
  * mi_ba_squared_reprojection_errors: CalculateSquaredReprojectionError
  * (src/base/projection.cc:111-128) of every observation at the problem's

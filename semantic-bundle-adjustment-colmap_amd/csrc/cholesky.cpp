@@ -481,6 +481,12 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
   return true;
 }
 
+bool CholWorkspace::ensure(int dev, int max_panels, int max_n) {
+  const int nblk = (std::max(0, max_n) + kTB - 1) / kTB;
+  if (side && device == dev && (int)ev.size() >= 2 * std::max(1, max_panels) && linv_rows >= nblk * kTB) return true;
+  return create(dev, max_panels, max_n);
+}
+
 void CholWorkspace::destroy() {
   if (device >= 0) (void)hipSetDevice(device);
   if (side) (void)hipStreamSynchronize(side);

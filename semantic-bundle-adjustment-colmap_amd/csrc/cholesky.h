@@ -58,6 +58,8 @@ struct CholWorkspace {
   // HIP/rocBLAS failure (partially created resources are released by
   // destroy()).
   bool create(int device, int max_panels, int max_n);
+  // create() unless the existing resources already cover (device, max_panels, max_n)
+  bool ensure(int device, int max_panels, int max_n);
   void destroy();
 };
 

@@ -16,25 +16,36 @@
 
 namespace miba {
 
-// RAII device allocation.
+// RAII device allocation.  alloc() keeps an allocation that is large
+// enough (a recycled context re-sizes without hipMalloc / hipFree, which
+// synchronise the device), so n is the live size and cap the allocated one.
 template <typename T>
 struct DevArray {
   T* ptr = nullptr;
   size_t n = 0;
+  size_t cap = 0;
   DevArray() = default;
   DevArray(const DevArray&) = delete;
   DevArray& operator=(const DevArray&) = delete;
   ~DevArray() { release(); }
   hipError_t alloc(size_t count) {
+    if (ptr && count <= cap) {
+      n = count;
+      return hipSuccess;
+    }
     release();
     n = count;
     if (count == 0) return hipSuccess;
-    return hipMalloc(&ptr, sizeof(T) * count);
+    const hipError_t e = hipMalloc(&ptr, sizeof(T) * count);
+    if (e == hipSuccess) cap = count;
+    else ptr = nullptr;
+    return e;
   }
   void release() {
     if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
     n = 0;
+    cap = 0;
   }
   size_t bytes() const { return sizeof(T) * n; }
 };
@@ -116,6 +127,12 @@ struct mi_ba_context {
 namespace miba {
 mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* p, const mi_ba_semantic* sem,
                             mi_ba_context** out);
+// As context_create, reusing `old` (may be null) when it lives on the same
+// device: its stream, rocBLAS handles, Cholesky workspace, pinned scalars and
+// device arrays (re-sized in place when large enough) carry over, the problem
+// state is replaced.  On failure `old` is destroyed and *out is null.
+mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const mi_ba_problem* p,
+                             const mi_ba_semantic* sem, mi_ba_context** out);
 void context_destroy(mi_ba_context* ctx);
 mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out);
 mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum);

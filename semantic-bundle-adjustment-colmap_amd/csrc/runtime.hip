@@ -13,7 +13,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -228,22 +230,67 @@ mi_ba_status build_pair_tiles(mi_ba_context* ctx) {
 
 mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, const mi_ba_semantic* sem,
                             mi_ba_context** out) {
-  if (!o || !pin || !out) return MI_BA_ERR_INVALID_ARGUMENT;
+  return context_recycle(nullptr, o, pin, sem, out);
+}
+
+namespace {
+// Drops the problem state of a solved context, keeping its device resources.
+void reset_problem_state(mi_ba_context* ctx) {
+  semantic_destroy(ctx);
+  ctx->timer.totals.clear();
+  ctx->timing = false;
+  ctx->solved = false;
+  ctx->dense = false;
+  ctx->nptiles = 0;
+  ctx->chol = CholConfig{};
+  ctx->fixed_cost = 0.0;
+  ctx->block_obs.clear();
+  ctx->setup = HostSetup{};
+  ctx->dev = DevProblem{};
+}
+}  // namespace
+
+mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const mi_ba_problem* pin,
+                             const mi_ba_semantic* sem, mi_ba_context** out) {
+  if (!o || !pin || !out) {
+    context_destroy(old);
+    return MI_BA_ERR_INVALID_ARGUMENT;
+  }
   *out = nullptr;
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MI_BA_ERR_NO_DEVICE;
-  if (o->device < 0 || o->device >= ndev) return MI_BA_ERR_INVALID_ARGUMENT;
-  MI_HIP(hipSetDevice(o->device));
-  auto* ctx = new mi_ba_context();
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    context_destroy(old);
+    return MI_BA_ERR_NO_DEVICE;
+  }
+  if (o->device < 0 || o->device >= ndev) {
+    context_destroy(old);
+    return MI_BA_ERR_INVALID_ARGUMENT;
+  }
+  if (hipSetDevice(o->device) != hipSuccess) {
+    context_destroy(old);
+    return MI_BA_ERR_HIP;
+  }
+  mi_ba_context* ctx = nullptr;
+  const bool recycled = old && old->device == o->device && old->world <= 1 && old->timer.pending.empty();
+  if (recycled) {
+    ctx = old;
+    reset_problem_state(ctx);
+  } else {
+    context_destroy(old);
+    ctx = new mi_ba_context();
+  }
   ctx->options = *o;
   ctx->problem = *pin;
   ctx->device = o->device;
+  auto fail = [&](mi_ba_status e) { context_destroy(ctx); return e; };
   mi_ba_problem* p = &ctx->problem;
   mi_ba_status st = build_setup(*o, p, &ctx->setup);
-  if (st != MI_BA_OK) { delete ctx; return st; }
+  if (st != MI_BA_OK) return fail(st);
   const HostSetup& s = ctx->setup;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { delete ctx; return MI_BA_ERR_HIP; }
-  auto fail = [&](mi_ba_status e) { context_destroy(ctx); return e; };
+  if (!ctx->stream && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    ctx->stream = nullptr;
+    return fail(MI_BA_ERR_HIP);
+  }
 
   const int I = p->num_images, C = p->num_cameras;
   const int64_t P = p->num_points;
@@ -386,8 +433,11 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
       ctx->cg_z.alloc(nf) || ctx->cg_p.alloc(nf) || ctx->cg_q.alloc(nf) || ctx->cg_w.alloc(3 * P) ||
       ctx->dX.alloc(3 * P) || ctx->scalars.alloc(kNumScalars))
     return fail(MI_BA_ERR_OUT_OF_MEMORY);
-  if (hipHostMalloc(&ctx->host_scalars, sizeof(double) * kNumScalars, hipHostMallocDefault) != hipSuccess)
+  if (!ctx->host_scalars &&
+      hipHostMalloc(&ctx->host_scalars, sizeof(double) * kNumScalars, hipHostMallocDefault) != hipSuccess) {
+    ctx->host_scalars = nullptr;
     return fail(MI_BA_ERR_OUT_OF_MEMORY);
+  }
   if (hipMemset(ctx->scalars.ptr, 0, sizeof(double) * kNumScalars) != hipSuccess) return fail(MI_BA_ERR_HIP);
   if (P && (hipMemset(ctx->dX.ptr, 0, 3 * P * 8) || hipMemset(ctx->Vinv.ptr, 0, 6 * P * 8) ||
             hipMemset(ctx->cg_w.ptr, 0, 3 * P * 8)))
@@ -414,11 +464,19 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* pin, co
         return fail(MI_BA_ERR_OUT_OF_MEMORY);
       st = build_pair_tiles(ctx);
       if (st != MI_BA_OK) return fail(st);
-      if (rocblas_create_handle(&ctx->blas) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
-      if (rocblas_set_stream(ctx->blas, ctx->stream) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
+      if (!ctx->blas) {
+        if (rocblas_create_handle(&ctx->blas) != rocblas_status_success) {
+          ctx->blas = nullptr;
+          return fail(MI_BA_ERR_HIP);
+        }
+        if (rocblas_set_stream(ctx->blas, ctx->stream) != rocblas_status_success) return fail(MI_BA_ERR_HIP);
+      }
       // per-context look-ahead resources on this context's device (panel
       // widths down to 64 allowed by mi_ba_set_tuning)
-      if (!ctx->cholws.create(ctx->device, (int)((d.nf + 63) / 64), (int)d.nf)) return fail(MI_BA_ERR_HIP);
+      if (!ctx->cholws.ensure(ctx->device, (int)((d.nf + 63) / 64), (int)d.nf)) return fail(MI_BA_ERR_HIP);
+      // (a recycled context has run factorisations already: no warm-up)
+    }
+    if (ctx->dense && !recycled) {
       // Warm the factorisation at this size once: rocBLAS / rocSOLVER load the
       // code objects of every (shape, kernel) pair on first use, hundreds of ms
       // that would otherwise land inside the first LM iterations.
@@ -936,19 +994,69 @@ static void print_summary(const mi_ba_summary& s) {
               term);
 }
 
-mi_ba_status mi_ba_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem, mi_ba_summary* sum) {
+namespace {
+// One BundleAdjuster::Solve on *arena (recycled, or created when null); the
+// context is kept in *arena for the next solve, or destroyed on failure.
+mi_ba_status solve_on(mi_ba_context** arena, const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem,
+                      mi_ba_summary* sum) {
   if (!o || !p || !sum) return MI_BA_ERR_INVALID_ARGUMENT;
   const double t0 = now_s();
   mi_ba_context* ctx = nullptr;
-  mi_ba_status st = context_create(o, p, sem, &ctx);
+  mi_ba_status st = context_recycle(*arena, o, p, sem, &ctx);
+  *arena = ctx;
   if (st != MI_BA_OK) return st;
   // SetUp normalised the config qvecs of ctx->problem (== caller arrays).
   st = context_solve(ctx, sum);
   if (st == MI_BA_OK) st = context_writeback(ctx);
-  context_destroy(ctx);
+  if (st != MI_BA_OK) {
+    context_destroy(ctx);
+    *arena = nullptr;
+  }
   sum->total_time_in_seconds = now_s() - t0;
   if (st == MI_BA_OK && o->print_summary) print_summary(*sum);
   return st;
+}
+}  // namespace
+
+mi_ba_status mi_ba_solve_in(mi_ba_context** arena, const mi_ba_options* o, mi_ba_problem* p,
+                            const mi_ba_semantic* sem, mi_ba_summary* sum) {
+  if (!arena) return MI_BA_ERR_INVALID_ARGUMENT;
+  return solve_on(arena, o, p, sem, sum);
+}
+
+mi_ba_status mi_ba_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem, mi_ba_summary* sum) {
+  mi_ba_context* ctx = nullptr;
+  const mi_ba_status st = solve_on(&ctx, o, p, sem, sum);
+  context_destroy(ctx);
+  return st;
+}
+
+// Independent problems solved concurrently: up to max_concurrent host
+// threads, each running whole solves on a context of its own (own HIP
+// stream, rocBLAS handles, workspaces), so the small, latency-bound kernels
+// and host round trips of one local problem overlap those of the others.
+mi_ba_status mi_ba_solve_batch(const mi_ba_options* options, mi_ba_problem* problems,
+                               const mi_ba_semantic* const* semantics, int32_t n, int32_t max_concurrent,
+                               mi_ba_summary* summaries, int32_t* statuses) {
+  if (n < 0 || (n > 0 && (!options || !problems || !summaries || !statuses))) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (n == 0) return MI_BA_OK;
+  const int workers = std::max(1, std::min<int>(max_concurrent > 0 ? max_concurrent : 8, n));
+  std::atomic<int> next{0};
+  auto run = [&]() {
+    // each worker recycles one context across its problems (device arrays,
+    // stream, rocBLAS handles and workspaces are allocated once)
+    mi_ba_context* arena = nullptr;
+    for (int k = next.fetch_add(1); k < n; k = next.fetch_add(1)) {
+      summaries[k] = mi_ba_summary{};
+      statuses[k] = solve_on(&arena, &options[k], &problems[k], semantics ? semantics[k] : nullptr, &summaries[k]);
+    }
+    context_destroy(arena);
+  };
+  std::vector<std::thread> pool;
+  for (int w = 1; w < workers; ++w) pool.emplace_back(run);
+  run();
+  for (auto& t : pool) t.join();
+  return MI_BA_OK;
 }
 
 mi_ba_status mi_ba_context_create(const mi_ba_options* o, const mi_ba_problem* p, const mi_ba_semantic* sem,

@@ -195,6 +195,9 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_context_set_comm.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
     lib.mi_ba_context_set_host_reducer.argtypes = [C.c_void_p, C.c_int32, C.c_int32, HOST_ALLREDUCE_FN, C.c_void_p]
     lib.mi_ba_dense_cholesky.argtypes = [C.c_int32, C.c_int32, _dp, _dp, C.c_int32, C.c_int32, C.c_int32, _i32p]
+    lib.mi_ba_solve_in.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.mi_ba_solve_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
+                                      C.c_void_p]
     lib.mi_ba_squared_reprojection_errors.argtypes = [C.c_void_p, C.c_int32, _dp]
     lib.mi_ba_filter_points3d.argtypes = [C.c_void_p, C.c_double, _u8p, C.c_int32, _u8p, _u8p, _dp,
                                           C.POINTER(C.c_int64)]
@@ -402,6 +405,57 @@ def dense_cholesky(A: np.ndarray, b: Optional[np.ndarray] = None, device: int = 
     check(load().mi_ba_dense_cholesky(device, n, F.ctypes.data_as(_dp), _ptr(x, _dp), panel, lookahead, own_diag,
                                       C.byref(info)), "mi_ba_dense_cholesky")
     return np.tril(F), x, info.value
+
+
+class Arena:
+    """mi_ba_solve_in: consecutive solves on one recycled context."""
+
+    def __init__(self):
+        self.h = C.c_void_p(None)
+
+    def solve(self, options: Options, scene: Scene, semantic: Optional[SemanticInput] = None) -> Summary:
+        s = Summary()
+        p = scene.problem()
+        sem = semantic.struct() if semantic is not None else None
+        check(load().mi_ba_solve_in(C.byref(self.h), C.cast(C.pointer(options), C.c_void_p),
+                                    C.cast(C.pointer(p), C.c_void_p),
+                                    None if sem is None else C.cast(C.pointer(sem), C.c_void_p),
+                                    C.cast(C.pointer(s), C.c_void_p)), "mi_ba_solve_in")
+        return s
+
+    def close(self):
+        if self.h.value:
+            load().mi_ba_context_destroy(self.h)
+            self.h = C.c_void_p(None)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def solve_batch(options, scenes, semantics=None, max_concurrent: int = 8):
+    """mi_ba_solve_batch: independent problems solved concurrently; updates
+    each scene in place.  options: one Options or one per scene.  Returns
+    (statuses, summaries)."""
+    n = len(scenes)
+    opts = options if isinstance(options, (list, tuple)) else [options] * n
+    O = (Options * n)(*opts)
+    P = (Problem * n)(*[s.problem() for s in scenes])
+    S = None
+    keep = []
+    if semantics is not None:
+        structs = [None if x is None else x.struct() for x in semantics]
+        keep = structs
+        S = (C.c_void_p * n)(*[None if x is None else C.cast(C.pointer(x), C.c_void_p) for x in structs])
+    sums = (Summary * n)()
+    st = (C.c_int32 * n)()
+    check(load().mi_ba_solve_batch(C.cast(O, C.c_void_p), C.cast(P, C.c_void_p), S and C.cast(S, C.c_void_p), n,
+                                   max_concurrent, C.cast(sums, C.c_void_p), C.cast(st, C.c_void_p)),
+          "mi_ba_solve_batch")
+    del keep
+    return list(st), list(sums)
 
 
 def squared_reprojection_errors(scene: Scene, device: int = 0) -> np.ndarray:
