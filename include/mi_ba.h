@@ -167,6 +167,37 @@ typedef struct mi_ba_semantic {
   double numeric_relative_step_size; /* default 1e-3 */
 } mi_ba_semantic;
 
+/* Geometric-semantic BA (GSBA): one cylinder IoU residual per (config image,
+ * cylinder) (GeometricSemanticBundleAdjuster<Cylinder>,
+ * src/optim/geometric_semantic_bundle_adjustment.{h,cc}; residual 1 - IoU of
+ * the cylinder's projected quadrilateral against the image's trunk mask,
+ * Cylinder::ComputeSemanticIoU src/util/cylinder.h:496-540; CENTRAL numeric
+ * derivatives, geometric_semantic_cost_functions.h:33-165), ScaledLoss(1 /
+ * number of config images).  Requirements as GeometricSemanticBundleAdjuster::
+ * Assert (:664-712): config cameras constant and SIMPLE_PINHOLE, TRIVIAL loss
+ * (else MI_BA_ERR_UNSUPPORTED).  Cylinders: QuaternionManifold on qvec,
+ * radius bounded below by 0 (the reference sets the "height" bound on the
+ * radius block, :1180). */
+typedef struct mi_ba_cylinder {
+  double qvec[4];                    /* (w,x,y,z) cylinder -> world rotation (Cylinder::Qvec) */
+  double tvec[3];                    /* lower circle centre in the world */
+  double radius;
+  double height;
+} mi_ba_cylinder;
+
+typedef struct mi_ba_gsba {
+  int32_t height;                    /* trunk mask size, every image */
+  int32_t width;
+  const uint8_t* trunk_mask;         /* [num_images][H][W] row-major, 1 where the semantic map
+                                        == trunk_semantic_class (:1328-1333), images in problem order */
+  int32_t num_cylinders;
+  mi_ba_cylinder* cylinders;         /* (in/out) */
+  int32_t refine_geometry;           /* default 1 */
+  double numeric_relative_step_size; /* default 1e-3 */
+  int32_t include_landmark_error;    /* default 0: the problem's observations are not used */
+  double landmark_error_weight;      /* default 1: reprojection blocks get ScaledLoss(w / #config 2D features) */
+} mi_ba_gsba;
+
 /* Mirrors the ceres::Solver::Summary fields COLMAP reads
  * (PrintSolverSummary, bundle_adjustment.cc:1142-1196). */
 typedef struct mi_ba_summary {
@@ -216,6 +247,25 @@ mi_ba_status mi_ba_setup_stats(const mi_ba_options* options,
 mi_ba_status mi_ba_solve(const mi_ba_options* options, mi_ba_problem* problem,
                          const mi_ba_semantic* semantic /* nullable */,
                          mi_ba_summary* summary);
+
+/* --- geometric-semantic BA (GSBA) ----------------------------------------
+ * mi_ba_default_gsba: GeometricSemanticBundleAdjustmentOptions defaults.
+ * mi_ba_gsba_solve: GeometricSemanticBundleAdjuster<Cylinder>::Solve on the
+ * GPU: poses (and cylinders when refine_geometry) refined; with
+ * include_landmark_error also the problem's points (SIMPLE_PINHOLE
+ * reprojection blocks, ScaledLoss).  Blocks are ordered by config image
+ * (problem order) then cylinder.
+ * mi_ba_gsba_evaluate: residual 1 - IoU and the ambient CENTRAL Jacobian
+ * [n][16] (camera q(4) t(3), cylinder q(4) t(3) radius height; columns of
+ * constant blocks zero) of every block, before the ScaledLoss; block_ids
+ * [n][2] = (image, cylinder).  *num_blocks receives the count; nothing is
+ * written when it exceeds capacity. */
+void mi_ba_default_gsba(mi_ba_gsba* gsba);
+mi_ba_status mi_ba_gsba_solve(const mi_ba_options* options, mi_ba_problem* problem, mi_ba_gsba* gsba,
+                              mi_ba_summary* summary);
+mi_ba_status mi_ba_gsba_evaluate(const mi_ba_options* options, mi_ba_problem* problem, const mi_ba_gsba* gsba,
+                                 int64_t capacity, int64_t* num_blocks, int32_t* block_ids,
+                                 double* residuals, double* jacobians);
 
 /* --- repeated solves (the incremental mapper's local / global BAs) -------
  * As mi_ba_solve, on the context in *arena (NULL: one is created) whose

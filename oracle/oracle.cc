@@ -27,6 +27,7 @@
 
 #include "../include/mi_ba.h"
 #include "oracle_math.h"
+#include "oracle_gsba.h"
 
 using namespace oracle;
 
@@ -52,6 +53,8 @@ void ReprojResidual(int model, const T q[4], const T t[3], const T X[3], const T
   r[1] -= T(oy);
 }
 
+constexpr int kLossScaled = 3;  // internal: ceres::ScaledLoss(nullptr, scale)
+
 // Ceres 2.1 loss functions (restated): rho[0..2] at s = |r|^2.
 void LossEvaluate(int type, double scale, double s, double rho[3]) {
   if (type == MI_BA_LOSS_SOFT_L1) {
@@ -68,6 +71,8 @@ void LossEvaluate(int type, double scale, double s, double rho[3]) {
     rho[0] = b * std::log(sum);
     rho[1] = std::max(std::numeric_limits<double>::min(), inv);
     rho[2] = -c * (inv * inv);
+  } else if (type == kLossScaled) {  // ScaledLoss(nullptr, a): the GSBA weights
+    rho[0] = scale * s; rho[1] = scale; rho[2] = 0.0;
   } else {
     rho[0] = s; rho[1] = 1.0; rho[2] = 0.0;
   }
@@ -445,11 +450,84 @@ void EvalSemantic(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* 
 // LevenbergMarquardtStrategy + DENSE_SCHUR, restated; bundle_adjustment.cc:
 // 271-306 selects it for <= 50 images).
 // ---------------------------------------------------------------------------
+// GSBA term (geometric_semantic_bundle_adjustment.cc:714-909): one block per
+// (config image, cylinder) in config-image then cylinder order.
+struct GsbaBlock {
+  int img, cyl, variant;
+};
+struct GsbaSetup {
+  const mi_ba_gsba* g = nullptr;
+  std::vector<GsbaBlock> blocks;
+  std::vector<int64_t> sem_total;  // per image: count of the trunk mask
+  double weight = 1.0;             // ScaledLoss(1 / #config images), :721-722
+};
+
+// GeometricSemanticBundleAdjuster::Assert (:664-712) + AddImageToProblem
+// (:835-909).
+int BuildGsbaSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& s, const mi_ba_gsba* g,
+                   GsbaSetup* gs) {
+  gs->g = g;
+  const int I = p->num_images;
+  auto in_cfg = [&](int i) { return p->image_in_config ? p->image_in_config[i] != 0 : true; };
+  int64_t ncfg = 0;
+  for (int i = 0; i < I; ++i) {
+    if (!in_cfg(i)) continue;
+    ++ncfg;
+    const int cam = p->image_camera[i];
+    if (!(p->camera_constant && p->camera_constant[cam])) return MI_BA_ERR_UNSUPPORTED;
+    if (s.cam_model[cam] != MI_BA_SIMPLE_PINHOLE) return MI_BA_ERR_UNSUPPORTED;
+  }
+  gs->weight = ncfg > 0 ? 1. / (double)ncfg : 1.0;
+  const int64_t plane = (int64_t)g->height * g->width;
+  gs->sem_total.assign(I, 0);
+  for (int i = 0; i < I; ++i) {
+    int64_t c = 0;
+    for (int64_t k = 0; k < plane; ++k) c += g->trunk_mask[i * plane + k] != 0;
+    gs->sem_total[i] = c;
+  }
+  for (int i = 0; i < I; ++i) {
+    if (!in_cfg(i)) continue;
+    const bool constant_pose = !o->refine_extrinsics || (p->image_constant_pose && p->image_constant_pose[i]);
+    if (constant_pose && !g->refine_geometry) continue;
+    for (int c = 0; c < g->num_cylinders; ++c) {
+      const int v = constant_pose ? kGsbaConstantPose : g->refine_geometry ? kGsbaFull : kGsbaConstantCylinder;
+      gs->blocks.push_back(GsbaBlock{i, c, v});
+    }
+  }
+  return MI_BA_OK;
+}
+
+// Poses of GSBA blocks are variable parameter blocks (SetUpManifolds,
+// :1205-1232).
+void AddGsbaPoses(const mi_ba_problem* p, const GsbaSetup& gs, Setup* s) {
+  for (const GsbaBlock& b : gs.blocks) {
+    if (b.variant == kGsbaConstantPose || s->img_var[b.img]) continue;
+    s->img_var[b.img] = 1;
+    s->img_tvec_mask[b.img] = p->image_constant_tvec ? p->image_constant_tvec[b.img] : 0;
+    int masked = 0;
+    for (int k = 0; k < 3; ++k) masked += (s->img_tvec_mask[b.img] >> k) & 1;
+    s->num_effective_parameters_reduced += 6 - masked;
+  }
+}
+
+// Residual (1 - IoU) and ambient Jacobian of GSBA block b at the current
+// parameters.
+double GsbaResidual(const mi_ba_problem* p, const Setup& s, const GsbaSetup& gs, const GsbaBlock& b, double* J16) {
+  const mi_ba_gsba* g = gs.g;
+  const mi_ba_cylinder& y = g->cylinders[b.cyl];
+  const double* K = &p->camera_params[s.cam_poff[p->image_camera[b.img]]];
+  const int64_t plane = (int64_t)g->height * g->width;
+  return GsbaEvalBlock(b.variant, &p->qvec[b.img * 4], &p->tvec[b.img * 3], K, y.qvec, y.tvec, y.radius, y.height,
+                       g->trunk_mask + b.img * plane, g->height, g->width, gs.sem_total[b.img],
+                       g->numeric_relative_step_size, J16);
+}
+
 struct Layout {
   // f-block (reduced camera system) coordinates
   std::vector<int> img_off;   // -1 if not variable; 6 tangent slots (masked coords skipped)
   std::vector<int> img_cols;  // mapping slot (0..5) -> column or -1
   std::vector<int> cam_off;
+  std::vector<int> cyl_off;   // GSBA cylinders: 8 tangent slots (q 3, t 3, radius, height) or -1
   int nf = 0;
   std::vector<int64_t> pt_off;  // -1 if constant
   int64_t ne = 0;
@@ -473,7 +551,7 @@ void AddSemanticPoses(const mi_ba_problem* p, const mi_ba_semantic* sem, const S
 }
 
 void BuildLayout(const Setup& s, const mi_ba_problem* p, Layout* L, const mi_ba_semantic* sem = nullptr,
-                 const SemSetup* ss = nullptr) {
+                 const SemSetup* ss = nullptr, const GsbaSetup* gs = nullptr) {
   const int I = p->num_images, C = p->num_cameras;
   L->img_off.assign(I, -1);
   L->img_cols.assign((size_t)I * 6, -1);
@@ -482,6 +560,12 @@ void BuildLayout(const Setup& s, const mi_ba_problem* p, Layout* L, const mi_ba_
     for (int k = 0; k < sem->num_pairs; ++k) {
       if (ss->pair_var1[k]) used_img[sem->pairs[2 * k]] = 1;
       if (ss->pair_var2[k]) used_img[sem->pairs[2 * k + 1]] = 1;
+    }
+  std::vector<uint8_t> used_cyl(gs && gs->g ? gs->g->num_cylinders : 0, 0);
+  if (gs)
+    for (const GsbaBlock& b : gs->blocks) {
+      if (b.variant != kGsbaConstantPose) used_img[b.img] = 1;
+      if (b.variant != kGsbaConstantCylinder) used_cyl[b.cyl] = 1;
     }
   for (size_t b = 0; b < s.block_obs.size(); ++b) {
     if (!s.block_reduced[b]) continue;
@@ -505,6 +589,12 @@ void BuildLayout(const Setup& s, const mi_ba_problem* p, Layout* L, const mi_ba_
     if (!used_cam[c]) continue;
     L->cam_off[c] = nf;
     nf += (int)s.cam_tangent[c].size();
+  }
+  L->cyl_off.assign(used_cyl.size(), -1);
+  for (size_t c = 0; c < used_cyl.size(); ++c) {
+    if (!used_cyl[c]) continue;
+    L->cyl_off[c] = nf;
+    nf += 8;
   }
   L->nf = nf;
   L->pt_off.assign(p->num_points, -1);
@@ -584,8 +674,16 @@ struct Solver {
   const mi_ba_semantic* sem;
   Setup s;
   SemSetup ss;
+  GsbaSetup gs;                   // GSBA blocks (empty without a GSBA term)
   Layout L;
   std::vector<int64_t> reduced;   // reduced program blocks, program order
+
+  double GsbaCost(size_t k) {
+    const double r = GsbaResidual(p, s, gs, gs.blocks[k], nullptr);
+    double rho[3];
+    LossEvaluate(kLossScaled, gs.weight, r * r, rho);
+    return 0.5 * rho[0];
+  }
 
   double BlockCost(int64_t b) {
     double r[2];
@@ -607,13 +705,17 @@ struct Solver {
   // are evaluated in parallel and summed in program order.
   double Cost() {
     const int64_t nr = (int64_t)reduced.size(), ns = (int64_t)ss.samples.size();
-    std::vector<double> t(nr + (sem ? ns : 0));
+    const int64_t ng = (int64_t)gs.blocks.size();
+    std::vector<double> t(nr + (sem ? ns : 0) + ng);
 #pragma omp parallel for schedule(static)
     for (int64_t k = 0; k < nr; ++k) t[k] = BlockCost(reduced[k]);
     if (sem) {
 #pragma omp parallel for schedule(dynamic, 1024)
       for (int64_t n = 0; n < ns; ++n) t[nr + n] = SemCost(n);
     }
+    const int64_t g0 = nr + (sem ? ns : 0);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t k = 0; k < ng; ++k) t[g0 + k] = GsbaCost((size_t)k);
     double c = 0.0;
     for (double v : t) c += v;
     return c;
@@ -621,8 +723,9 @@ struct Solver {
   void Linearize(Linearization* lin) {
     const int c = s.ct;
     const int64_t nr = (int64_t)reduced.size(), ns = sem ? (int64_t)ss.samples.size() : 0;
-    lin->resize(2 * nr + ns);
-    std::vector<double> cost(nr + ns);
+    const int64_t ng = (int64_t)gs.blocks.size();
+    lin->resize(2 * nr + ns + ng);
+    std::vector<double> cost(nr + ns + ng);
 #pragma omp parallel
     {
       std::vector<double> J(2 * (9 + c));
@@ -687,6 +790,47 @@ struct Solver {
           lin->r[R] = r;
         }
       }
+      // GSBA rows: tangent columns camera pose (6) + cylinder (8)
+#pragma omp for schedule(dynamic, 1)
+      for (int64_t k = 0; k < ng; ++k) {
+        const GsbaBlock& b = gs.blocks[k];
+        double J16[16];
+        double r = GsbaResidual(p, s, gs, b, J16);
+        double Jt[14];
+        double PJ[12];
+        QuaternionPlusJacobian(&p->qvec[b.img * 4], PJ);
+        for (int col = 0; col < 3; ++col) {
+          double acc = 0.0;
+          for (int m = 0; m < 4; ++m) acc += J16[m] * PJ[m * 3 + col];
+          Jt[col] = acc;
+        }
+        for (int col = 0; col < 3; ++col) Jt[3 + col] = J16[4 + col];
+        QuaternionPlusJacobian(gs.g->cylinders[b.cyl].qvec, PJ);
+        for (int col = 0; col < 3; ++col) {
+          double acc = 0.0;
+          for (int m = 0; m < 4; ++m) acc += J16[7 + m] * PJ[m * 3 + col];
+          Jt[6 + col] = acc;
+        }
+        for (int col = 0; col < 5; ++col) Jt[9 + col] = J16[11 + col];
+        double rho[3];
+        LossEvaluate(kLossScaled, gs.weight, r * r, rho);
+        cost[nr + ns + k] = 0.5 * rho[0];
+        ApplyCorrector(rho, r * r, 1, &r, 14, Jt);
+        const size_t R = 2 * (size_t)nr + ns + k;
+        int nf = 0;
+        if (b.variant != kGsbaConstantPose && L.img_off[b.img] >= 0)
+          for (int m = 0; m < 6; ++m) {
+            const int col = L.img_cols[(size_t)b.img * 6 + m];
+            if (col >= 0) { lin->fcol[R * Linearization::kF + nf] = col; lin->fval[R * Linearization::kF + nf++] = Jt[m]; }
+          }
+        if (b.variant != kGsbaConstantCylinder && L.cyl_off[b.cyl] >= 0)
+          for (int m = 0; m < 8; ++m) {
+            lin->fcol[R * Linearization::kF + nf] = L.cyl_off[b.cyl] + m;
+            lin->fval[R * Linearization::kF + nf++] = Jt[6 + m];
+          }
+        lin->fn[R] = (uint8_t)nf;
+        lin->r[R] = r;
+      }
     }
     lin->cost = 0.0;
     for (double v : cost) lin->cost += v;
@@ -713,6 +857,19 @@ struct Solver {
     for (int64_t pt = 0; pt < p->num_points; ++pt) {
       if (L.pt_off[pt] < 0) continue;
       for (int m = 0; m < 3; ++m) p->xyz[pt * 3 + m] += delta[L.nf + L.pt_off[pt] + m];
+    }
+    // cylinders: QuaternionManifold on qvec; radius clamped to its lower
+    // bound 0 (ParameterBlock::Plus projects onto the bounds)
+    for (size_t c = 0; c < L.cyl_off.size(); ++c) {
+      if (L.cyl_off[c] < 0) continue;
+      mi_ba_cylinder& y = gs.g->cylinders[c];
+      const double* d = &delta[L.cyl_off[c]];
+      double qn[4];
+      QuaternionPlus(y.qvec, d, qn);
+      for (int m = 0; m < 4; ++m) y.qvec[m] = qn[m];
+      for (int m = 0; m < 3; ++m) y.tvec[m] += d[3 + m];
+      y.radius = std::max(y.radius + d[6], 0.0);
+      y.height += d[7];
     }
   }
 };
@@ -892,8 +1049,13 @@ int oracle_cholesky(double* A, int n) {
   return 0;
 }
 
-// Full LM solve, dense Schur (Ceres 2.1 LM semantics, restated).
-int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem, mi_ba_summary* sum) {
+}  // extern "C"
+
+namespace {
+// Full LM solve, dense Schur (Ceres 2.1 LM semantics, restated), with the
+// optional semantic (SBA) and GSBA terms.
+int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem, const mi_ba_gsba* gsba,
+              mi_ba_summary* sum) {
   Solver S;
   S.o = o; S.p = p; S.sem = sem;
   std::memset(sum, 0, sizeof(*sum));
@@ -903,11 +1065,19 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
     BuildSemSetup(o, p, S.s, sem, &S.ss);
     AddSemanticPoses(p, sem, S.ss, &S.s);
   }
-  BuildLayout(S.s, p, &S.L, sem, sem ? &S.ss : nullptr);
+  if (gsba) {
+    st = BuildGsbaSetup(o, p, S.s, gsba, &S.gs);
+    if (st) return st;
+    AddGsbaPoses(p, S.gs, &S.s);
+  }
+  BuildLayout(S.s, p, &S.L, sem, sem ? &S.ss : nullptr, gsba ? &S.gs : nullptr);
   for (size_t b = 0; b < S.s.block_obs.size(); ++b)
     if (S.s.block_reduced[b]) S.reduced.push_back((int64_t)b);
-  sum->num_residuals_reduced = S.s.num_residuals_reduced + (int64_t)S.ss.samples.size();
-  sum->num_effective_parameters_reduced = S.s.num_effective_parameters_reduced;
+  int64_t ncyl_var = 0;
+  for (int c : S.L.cyl_off) ncyl_var += c >= 0 ? 1 : 0;
+  sum->num_residuals_reduced =
+      S.s.num_residuals_reduced + (int64_t)S.ss.samples.size() + (int64_t)S.gs.blocks.size();
+  sum->num_effective_parameters_reduced = S.s.num_effective_parameters_reduced + 8 * ncyl_var;
   sum->num_semantic_residuals = (int64_t)S.ss.samples.size();
   if (sum->num_residuals_reduced == 0) return MI_BA_ERR_NO_RESIDUALS;
   // fixed cost of the dropped all-constant blocks
@@ -1133,6 +1303,13 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
     std::vector<double> q0(p->qvec, p->qvec + 4 * p->num_images), t0(p->tvec, p->tvec + 3 * p->num_images);
     std::vector<double> c0(p->camera_params, p->camera_params + S.s.cam_poff[p->num_cameras]);
     std::vector<double> x0(p->xyz, p->xyz + 3 * p->num_points);
+    std::vector<mi_ba_cylinder> y0;
+    if (gsba) y0.assign(gsba->cylinders, gsba->cylinders + gsba->num_cylinders);
+    auto restore = [&]() {
+      std::copy(q0.begin(), q0.end(), p->qvec); std::copy(t0.begin(), t0.end(), p->tvec);
+      std::copy(c0.begin(), c0.end(), p->camera_params); std::copy(x0.begin(), x0.end(), p->xyz);
+      if (gsba) std::copy(y0.begin(), y0.end(), gsba->cylinders);
+    };
     double x_norm2 = 0.0;
     for (double v : q0) x_norm2 += v * v;
     S.Plus(delta);
@@ -1147,8 +1324,7 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
     // candidate is accepted (x_ stays).
     if (std::sqrt(step_norm2) <= o->parameter_tolerance * (std::sqrt(x_norm2) + o->parameter_tolerance) ||
         std::fabs(cost_change) <= o->function_tolerance * x_cost) {
-      std::copy(q0.begin(), q0.end(), p->qvec); std::copy(t0.begin(), t0.end(), p->tvec);
-      std::copy(c0.begin(), c0.end(), p->camera_params); std::copy(x0.begin(), x0.end(), p->xyz);
+      restore();
       sum->termination_type = MI_BA_CONVERGENCE;
       ++sum->num_unsuccessful_steps;
       break;
@@ -1164,14 +1340,107 @@ int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic*
       ++sum->num_jacobian_evaluations;
     } else {
       ++sum->num_unsuccessful_steps;
-      std::copy(q0.begin(), q0.end(), p->qvec); std::copy(t0.begin(), t0.end(), p->tvec);
-      std::copy(c0.begin(), c0.end(), p->camera_params); std::copy(x0.begin(), x0.end(), p->xyz);
+      restore();
       radius = radius / decrease_factor;
       decrease_factor *= 2.0;
     }
   }
   sum->final_cost = x_cost + fixed;
   return MI_BA_OK;
+}
+
+// The GSBA problem: the reprojection blocks only with include_landmark_error,
+// then with ScaledLoss(landmark_error_weight / #2D features of the config
+// images) (:729-762); GeometricSemanticBundleAdjuster::Assert (:664-712).
+int GsbaProblem(const mi_ba_options* o, const mi_ba_problem* p, const mi_ba_gsba* g, mi_ba_options* oo,
+                mi_ba_problem* pp) {
+  if (!o || !p || !g) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (o->loss_function_type != MI_BA_LOSS_TRIVIAL) return MI_BA_ERR_UNSUPPORTED;
+  *oo = *o;
+  *pp = *p;
+  if (!g->include_landmark_error) {
+    pp->num_obs = 0;
+  } else {
+    int64_t total = 0;
+    for (int64_t k = 0; k < p->num_obs; ++k) {
+      const int i = p->obs_image[k];
+      total += p->image_in_config ? (p->image_in_config[i] != 0) : 1;
+    }
+    oo->loss_function_type = kLossScaled;
+    oo->loss_function_scale = g->landmark_error_weight / (double)std::max<int64_t>(1, total);
+  }
+  return MI_BA_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int oracle_solve(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem, mi_ba_summary* sum) {
+  return SolveImpl(o, p, sem, nullptr, sum);
+}
+
+int oracle_gsba_solve(const mi_ba_options* o, mi_ba_problem* p, mi_ba_gsba* g, mi_ba_summary* sum) {
+  mi_ba_options oo;
+  mi_ba_problem pp;
+  int st = GsbaProblem(o, p, g, &oo, &pp);
+  if (st) return st;
+  return SolveImpl(&oo, &pp, nullptr, g, sum);
+}
+
+// Every GSBA block's residual (1 - IoU) and ambient Jacobian [16]; returns
+// the block count (nothing written beyond capacity), or -status.
+int64_t oracle_gsba_evaluate(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_gsba* g, int64_t capacity,
+                             int32_t* ids, double* residuals, double* jacobians) {
+  mi_ba_options oo;
+  mi_ba_problem pp;
+  int st = GsbaProblem(o, p, g, &oo, &pp);
+  if (st) return -st;
+  Setup s;
+  if ((st = BuildSetup(&oo, &pp, &s))) return -st;
+  GsbaSetup gs;
+  if ((st = BuildGsbaSetup(&oo, &pp, s, g, &gs))) return -st;
+  const int64_t n = (int64_t)gs.blocks.size();
+  if (n > capacity) return n;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t k = 0; k < n; ++k) {
+    ids[2 * k] = gs.blocks[k].img;
+    ids[2 * k + 1] = gs.blocks[k].cyl;
+    residuals[k] = GsbaResidual(&pp, s, gs, gs.blocks[k], &jacobians[16 * k]);
+  }
+  return n;
+}
+
+// Trunk masks for tests: the union over `cylinders` of their projected
+// quadrilaterals (drawQuadrilateral), per image of the problem.
+int oracle_gsba_render(const mi_ba_problem* p, const mi_ba_cylinder* cyl, int ncyl, int H, int W, uint8_t* out) {
+  Setup s;
+  s.cam_poff.assign(p->num_cameras + 1, 0);
+  for (int c = 0; c < p->num_cameras; ++c) s.cam_poff[c + 1] = s.cam_poff[c] + 3;  // SIMPLE_PINHOLE
+  for (int i = 0; i < p->num_images; ++i) {
+    uint8_t* m = out + (int64_t)i * H * W;
+    std::fill(m, m + (int64_t)H * W, 0);
+    const double* K = &p->camera_params[s.cam_poff[p->image_camera[i]]];
+    for (int c = 0; c < ncyl; ++c) {
+      double q[4][2];
+      if (!GsbaQuad(&p->qvec[i * 4], &p->tvec[i * 3], K, cyl[c].qvec, cyl[c].tvec, cyl[c].radius, cyl[c].height, q))
+        continue;
+      GsbaBox box;
+      std::vector<uint8_t> mask;
+      GsbaDraw(q, W, H, &box, &mask);
+      for (int y = 0; y < box.h; ++y)
+        for (int x = 0; x < box.w; ++x)
+          if (mask[(size_t)y * box.w + x]) m[(int64_t)(box.y + y) * W + box.x + x] = 1;
+    }
+  }
+  return 0;
+}
+
+// Cylinder::ComputeSemanticIoU for one configuration (tests).
+double oracle_gsba_iou(const double* cq, const double* ct, const double* K, const mi_ba_cylinder* y,
+                       const uint8_t* mask, int H, int W) {
+  int64_t total = 0;
+  for (int64_t k = 0; k < (int64_t)H * W; ++k) total += mask[k] != 0;
+  return GsbaIoU(cq, ct, K, y->qvec, y->tvec, y->radius, y->height, mask, H, W, total);
 }
 
 }  // extern "C"

@@ -58,6 +58,13 @@ def load():
                                                C.POINTER(mi_ba.Semantic), C.c_int64, C.c_int, _i64p]
     lib.oracle_solve.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem), C.POINTER(mi_ba.Semantic),
                                  C.POINTER(mi_ba.Summary)]
+    lib.oracle_gsba_render.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    lib.oracle_gsba_evaluate.restype = C.c_int64
+    lib.oracle_gsba_evaluate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                         C.c_void_p]
+    lib.oracle_gsba_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.oracle_gsba_iou.restype = C.c_double
+    lib.oracle_gsba_iou.argtypes = [_dp, _dp, _dp, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
     lib.oracle_cholesky.restype = C.c_int
     lib.oracle_cholesky.argtypes = [_dp, C.c_int]
     _lib = lib
@@ -147,6 +154,62 @@ def filter_points3d(scene, max_reproj_error, point_mask=None, point_error=None, 
             obs_keep[bad] = False
             err[p] = s / (len(track) - len(bad))
     return obs_keep, point_keep, err, num_filtered
+
+
+def gsba_render(scene, cylinders, height, width):
+    """Trunk masks [I][H][W] uint8: the union of the cylinders' projected
+    quadrilaterals (drawQuadrilateral) per image."""
+    lib = load()
+    n = len(cylinders)
+    arr = (mi_ba.Cylinder * max(1, n))()
+    for k in range(n):
+        arr[k].qvec[:] = list(cylinders[k][:4])
+        arr[k].tvec[:] = list(cylinders[k][4:7])
+        arr[k].radius = float(cylinders[k][7])
+        arr[k].height = float(cylinders[k][8])
+    out = np.zeros((scene.num_images, height, width), np.uint8)
+    p = scene.problem()
+    lib.oracle_gsba_render(C.byref(p), arr, n, height, width, out.ctypes.data_as(C.c_void_p))
+    return out
+
+
+def gsba_evaluate(options, scene, gsba):
+    lib = load()
+    p = scene.problem()
+    g, arr = gsba.struct()
+    n = lib.oracle_gsba_evaluate(C.byref(options), C.byref(p), C.byref(g), 0, None, None, None)
+    if n < 0:
+        raise RuntimeError("oracle_gsba_evaluate status %d" % -n)
+    ids = np.zeros((n, 2), np.int32)
+    r = np.zeros(n)
+    J = np.zeros((n, 16))
+    lib.oracle_gsba_evaluate(C.byref(options), C.byref(p), C.byref(g), n, ids.ctypes.data_as(C.c_void_p),
+                             r.ctypes.data_as(C.c_void_p), J.ctypes.data_as(C.c_void_p))
+    return ids, r, J
+
+
+def gsba_solve(options, scene, gsba):
+    lib = load()
+    s = mi_ba.Summary()
+    p = scene.problem()
+    g, arr = gsba.struct()
+    st = lib.oracle_gsba_solve(C.byref(options), C.byref(p), C.byref(g), C.byref(s))
+    if st != 0:
+        raise RuntimeError("oracle_gsba_solve status %d" % st)
+    gsba.read_back(arr)
+    return s
+
+
+def gsba_iou(cq, ct, K, cylinder, mask):
+    lib = load()
+    y = mi_ba.Cylinder()
+    y.qvec[:] = list(cylinder[:4])
+    y.tvec[:] = list(cylinder[4:7])
+    y.radius = float(cylinder[7])
+    y.height = float(cylinder[8])
+    m = np.ascontiguousarray(mask, np.uint8)
+    return lib.oracle_gsba_iou(_a(cq)[1], _a(ct)[1], _a(K)[1], C.byref(y), m.ctypes.data_as(C.c_void_p),
+                               m.shape[0], m.shape[1])
 
 
 def setup_stats(options, scene) -> "mi_ba.SetupInfo":

@@ -334,10 +334,16 @@ inline void dispatch_model(int model, F&& f) {
 // and the Corrector's residual/Jacobian scale for the rho'' <= 0 branch
 // (every loss used here: Trivial rho''=0, SoftL1/Cauchy rho''<0).
 // ---------------------------------------------------------------------------
-enum LossType { kLossTrivial = 0, kLossSoftL1 = 1, kLossCauchy = 2 };
+// kLossScaled: ceres::ScaledLoss(nullptr, scale), internal (the GSBA
+// landmark term, geometric_semantic_bundle_adjustment.cc:758-762).
+enum LossType { kLossTrivial = 0, kLossSoftL1 = 1, kLossCauchy = 2, kLossScaled = 3 };
 
 MI_HD void loss_eval(int type, double scale, double s, double rho[3]) {
-  if (type == kLossSoftL1) {
+  if (type == kLossScaled) {
+    rho[0] = scale * s;
+    rho[1] = scale;
+    rho[2] = 0.0;
+  } else if (type == kLossSoftL1) {
     const double b = scale * scale, c = 1.0 / b;
     const double sum = 1.0 + s * c;
     const double tmp = sqrt(sum);

@@ -51,6 +51,7 @@ struct DevArray {
 };
 
 struct SemanticState;  // semantic.h
+struct GsbaState;      // gsba.h
 
 struct KernelTimer {
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -111,6 +112,7 @@ struct mi_ba_context {
 
   double fixed_cost = 0.0;
   miba::SemanticState* sem = nullptr;
+  miba::GsbaState* gsba = nullptr;        // geometric-semantic (cylinder IoU) term
 
   bool timing = false;
   miba::KernelTimer timer;
@@ -132,7 +134,7 @@ mi_ba_status context_create(const mi_ba_options* o, const mi_ba_problem* p, cons
 // device arrays (re-sized in place when large enough) carry over, the problem
 // state is replaced.  On failure `old` is destroyed and *out is null.
 mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const mi_ba_problem* p,
-                             const mi_ba_semantic* sem, mi_ba_context** out);
+                             const mi_ba_semantic* sem, mi_ba_context** out, const mi_ba_gsba* gsba = nullptr);
 void context_destroy(mi_ba_context* ctx);
 mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out);
 mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum);

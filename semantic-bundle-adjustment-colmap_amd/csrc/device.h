@@ -60,7 +60,9 @@ struct DevProblem {
   int64_t nb;          // reduced geometric blocks
   int num_images, num_cameras;
   int64_t num_points;
-  int64_t nf;          // f-vector length: 6*I + ct*C (fixed slots, masked)
+  int64_t nf;          // f-vector length: 6*I + ct*C (+ 8 per GSBA cylinder: fixed slots, masked)
+  int64_t cyl0;        // first GSBA cylinder slot (= 6*I + ct*C)
+  int cyl_var;         // GSBA cylinders are parameters (refine_geometry)
   int loss_type;
   double loss_scale;
   int refine_mask;     // bit0 focal, bit1 principal point, bit2 extra params

@@ -1,0 +1,783 @@
+// gsba.hip — geometric-semantic BA (GSBA) cylinder IoU term (product code;
+// see gsba.h).
+//
+// Restates for gfx950:
+//   Cylinder::ComputeSemanticIoU / ProjectToMask / ProjectToQuadrilateral /
+//   GetEdgePoints       src/util/cylinder.h:270-540
+//   drawQuadrilateral   src/util/cylinder.h:21-117 (as a per-pixel predicate)
+//   XYWH                src/util/xywh.h
+//   simplePinholeProject src/util/utils.h:22-54
+//   GSBA cost functions src/base/geometric_semantic_cost_functions.h:33-165
+//   Ceres 2.1 AngleAxisRotatePoint, NumericDiffCostFunction CENTRAL,
+//   QuaternionManifold (3rd party, restated)
+// Built with -ffp-contract=off: the pixel predicates compare products of
+// doubles against 0 exactly as the reference's x86-64 (no FMA) build does.
+//
+// Layout and roofline: one workgroup (4 waves) per IoU evaluation; waves take
+// rows of the quadrilateral's bounding box, lanes consecutive pixels (1-byte
+// trunk mask loads, coalesced along x).  Per pixel: <= 4 edge tests (2 FP64
+// multiplies) and <= 4 rectangle tests; the 33 evaluations of a block scan
+// nearly the same box, so the mask stays in L2 — the kernel is bound by FP64
+// VALU issue, not HBM.
+#include "gsba.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+#include "ba_math.h"
+#include "kernels.h"
+
+namespace miba {
+
+namespace {
+
+constexpr int kGsbaFull = 0, kGsbaConstantPose = 1, kGsbaConstantCylinder = 2;
+constexpr int kTB = 256;
+
+struct Box {
+  int x, y, w, h;
+  __device__ int x_end() const { return x + w - 1; }
+  __device__ int y_end() const { return y + h - 1; }
+};
+
+__device__ inline Box bound2(double ax, double ay, double bx, double by) {
+  const double min_x = fmin(ax, bx), max_x = fmax(ax, bx);
+  const double min_y = fmin(ay, by), max_y = fmax(ay, by);
+  Box b;
+  b.x = cast_to_int_x86(floor(min_x));
+  b.y = cast_to_int_x86(floor(min_y));
+  b.w = cast_to_int_x86(ceil(max_x)) - b.x + 1;
+  b.h = cast_to_int_x86(ceil(max_y)) - b.y + 1;
+  return b;
+}
+
+// XYWH::shrinkToFitInToFitIn(XYWH(0, 0, W, H)); the empty box is (0,0,0,0)
+__device__ inline Box shrink(Box b, int W, int H) {
+  const int x0 = max(b.x, 0), y0 = max(b.y, 0);
+  const int x1 = min(b.x_end(), W - 1), y1 = min(b.y_end(), H - 1);
+  Box o{0, 0, 0, 0};
+  if (x1 < x0 || y1 < y0) return o;
+  o.x = x0;
+  o.y = y0;
+  o.w = x1 - x0 + 1;
+  o.h = y1 - y0 + 1;
+  return o;
+}
+
+// QuaternionRotatePoint (normalising) + t
+__device__ inline void pose_transform(const double q[4], const double t[3], const double pt[3], double r[3]) {
+  const double scale = 1.0 / sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const double u[4] = {scale * q[0], scale * q[1], scale * q[2], scale * q[3]};
+  unit_quat_rotate(u, pt, r);
+  r[0] += t[0];
+  r[1] += t[1];
+  r[2] += t[2];
+}
+
+// PoseInverse (rotation_extension.h:43-79): QuaternionInverseRotation, then
+// t_inv = -R(q_inv) t with QuaternionToRotation's 1 / |q|^2 normaliser.
+__device__ inline void pose_inverse(const double q[4], const double t[3], double qi[4], double ti[3]) {
+  const double scale = 1.0 / sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  qi[0] = scale * q[0];
+  qi[1] = -(scale * q[1]);
+  qi[2] = -(scale * q[2]);
+  qi[3] = -(scale * q[3]);
+  const double a = qi[0], b = qi[1], c = qi[2], d = qi[3];
+  const double aa = a * a, ab = a * b, ac = a * c, ad = a * d;
+  const double bb = b * b, bc = b * c, bd = b * d;
+  const double cc = c * c, cd = c * d, dd = d * d;
+  double R[9] = {aa + bb - cc - dd, 2.0 * (bc - ad), 2.0 * (ac + bd),
+                 2.0 * (ad + bc),  aa - bb + cc - dd, 2.0 * (cd - ab),
+                 2.0 * (bd - ac),  2.0 * (ab + cd),  aa - bb - cc + dd};
+  double normalizer = a * a + b * b + c * c + d * d;
+  normalizer = 1.0 / normalizer;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] *= normalizer;
+  ti[0] = -(R[0] * t[0] + R[1] * t[1] + R[2] * t[2]);
+  ti[1] = -(R[3] * t[0] + R[4] * t[1] + R[5] * t[2]);
+  ti[2] = -(R[6] * t[0] + R[7] * t[1] + R[8] * t[2]);
+}
+
+// Ceres 2.1 AngleAxisRotatePoint
+__device__ inline void angle_axis_rotate(const double aa[3], const double pt[3], double r[3]) {
+  const double theta2 = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
+  if (theta2 > DBL_EPSILON) {
+    const double theta = sqrt(theta2);
+    const double costheta = cos(theta);
+    const double sintheta = sin(theta);
+    const double theta_inverse = 1.0 / theta;
+    const double w[3] = {aa[0] * theta_inverse, aa[1] * theta_inverse, aa[2] * theta_inverse};
+    const double wx[3] = {w[1] * pt[2] - w[2] * pt[1], w[2] * pt[0] - w[0] * pt[2], w[0] * pt[1] - w[1] * pt[0]};
+    const double tmp = (w[0] * pt[0] + w[1] * pt[1] + w[2] * pt[2]) * (1.0 - costheta);
+    r[0] = pt[0] * costheta + wx[0] * sintheta + w[0] * tmp;
+    r[1] = pt[1] * costheta + wx[1] * sintheta + w[1] * tmp;
+    r[2] = pt[2] * costheta + wx[2] * sintheta + w[2] * tmp;
+  } else {
+    const double wx[3] = {aa[1] * pt[2] - aa[2] * pt[1], aa[2] * pt[0] - aa[0] * pt[2], aa[0] * pt[1] - aa[1] * pt[0]};
+    r[0] = pt[0] + wx[0];
+    r[1] = pt[1] + wx[1];
+    r[2] = pt[2] + wx[2];
+  }
+}
+
+// ProjectToQuadrilateral + GetEdgePoints; false where the reference throws
+// (ComputeSemanticIoU then returns 0).
+__device__ inline bool project_quad(const double* x, const double K[3], double p[4][2]) {
+  const double* cq = x;
+  const double* ct = x + 4;
+  const double* yq = x + 7;
+  const double* yt = x + 11;
+  double radius = x[14], height = x[15];
+  if (radius <= 0) radius = 1e-4;  // Cylinder::Check on the evaluated copy
+  if (height <= 0) height = 1e-4;
+  double cwq[4], cwt[3];
+  pose_inverse(cq, ct, cwq, cwt);
+  double qi[4], ti[3];
+  pose_inverse(yq, yt, qi, ti);
+  double c[3];
+  pose_transform(qi, ti, cwt, c);
+  c[2] = 0;
+  const double dist = sqrt(c[0] * c[0] + c[1] * c[1]);
+  if (dist <= radius) return false;
+  const double dir[3] = {c[0] / dist * radius, c[1] / dist * radius, 0};
+  const double beta = acos(radius / dist);
+  const double aap[3] = {0, 0, beta}, aan[3] = {0, 0, -beta};
+  double e[4][3];
+  angle_axis_rotate(aap, dir, e[0]);
+  angle_axis_rotate(aan, dir, e[1]);
+  e[2][0] = e[1][0]; e[2][1] = e[1][1]; e[2][2] = e[1][2] + height;
+  e[3][0] = e[0][0]; e[3][1] = e[0][1]; e[3][2] = e[0][2] + height;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double w[3], pc[3];
+    pose_transform(yq, yt, e[k], w);
+    pose_transform(cq, ct, w, pc);
+    if (pc[2] <= 0) return false;
+    pc[0] /= pc[2];
+    pc[1] /= pc[2];
+    p[k][0] = K[0] * pc[0] + K[1];
+    p[k][1] = K[0] * pc[1] + K[2];
+  }
+  const double v0x = p[1][0] - p[0][0], v0y = p[1][1] - p[0][1];
+  const double v1x = p[2][0] - p[0][0], v1y = p[2][1] - p[0][1];
+  if (v0x * v1y - v0y * v1x < 0) {
+    double t0 = p[1][0], t1 = p[1][1];
+    p[1][0] = p[3][0]; p[1][1] = p[3][1];
+    p[3][0] = t0; p[3][1] = t1;
+  }
+  return true;
+}
+
+struct GsbaArgs {
+  const GsbaBlock* blocks;
+  const double* qt;        // [I][8] poses (current or candidate)
+  const double* cam;       // [C][8]
+  const uint32_t* img_cam;
+  const double* cyl;       // [ncyl][9]
+  const uint8_t* masks;    // [slot][H][W]
+  const int64_t* sem_total;
+  int H, W;
+  double rel_step;
+};
+
+// Ambient parameter vector of a block: camera q(4) t(3), cylinder q(4) t(3), r, h.
+__device__ inline void load_params(const GsbaArgs& a, const GsbaBlock& b, double x[16]) {
+  const double* qt = a.qt + 8 * (size_t)b.img;
+#pragma unroll
+  for (int m = 0; m < 7; ++m) x[m] = qt[m];
+  const double* y = a.cyl + 9 * (size_t)b.cyl;
+#pragma unroll
+  for (int m = 0; m < 9; ++m) x[7 + m] = y[m];
+}
+
+// numeric_diff.h: delta = max(sqrt(eps), |x| * relative_step_size)
+__device__ inline double step_of(double xj, double rel) {
+  return fmax(sqrt(DBL_EPSILON), fabs(xj) * rel);
+}
+
+// One IoU evaluation per workgroup.
+__global__ __launch_bounds__(kTB) void gsba_iou_kernel(GsbaArgs a, const GsbaEval* __restrict__ evals,
+                                                       double* __restrict__ iou_out) {
+  __shared__ int64_t red[2][kTB / 64];
+  const GsbaEval ev = evals[blockIdx.x];
+  const GsbaBlock b = a.blocks[ev.block];
+  double x[16];
+  load_params(a, b, x);
+  if (ev.param >= 0) {
+    const double orig = x[ev.param];
+    const double delta = step_of(orig, a.rel_step);
+    x[ev.param] = ev.sign > 0 ? orig + delta : orig - delta;
+  }
+  const double* kc = a.cam + 8 * (size_t)a.img_cam[b.img];
+  const double K[3] = {kc[0], kc[1], kc[2]};
+  double p[4][2];
+  const bool ok = project_quad(x, K, p);
+  const int H = a.H, W = a.W;
+  int64_t tp = 0, fp = 0;
+  if (ok) {
+    // drawQuadrilateral as a predicate over the shrunk bounding box
+    double min_x = p[0][0], min_y = p[0][1], max_x = p[0][0], max_y = p[0][1];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      min_x = fmin(min_x, p[k][0]);
+      max_x = fmax(max_x, p[k][0]);
+      min_y = fmin(min_y, p[k][1]);
+      max_y = fmax(max_y, p[k][1]);
+    }
+    Box box;
+    box.x = cast_to_int_x86(floor(min_x));
+    box.y = cast_to_int_x86(floor(min_y));
+    box.w = cast_to_int_x86(ceil(max_x)) - box.x + 1;
+    box.h = cast_to_int_x86(ceil(max_y)) - box.y + 1;
+    box = shrink(box, W, H);
+    Box eb[4];
+    double dy[4], dx[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = (e + 1) & 3;
+      eb[e] = shrink(bound2(p[e][0], p[e][1], p[n][0], p[n][1]), W, H);
+      dy[e] = p[n][1] - p[e][1];
+      dx[e] = p[n][0] - p[e][0];
+    }
+    Box rb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      rb[k] = Box{0, 0, 0, 0};
+      const double qx = p[k][0], qy = p[k][1];
+      if (qx - box.x < 1 || box.x_end() - qx < 1 || qy - box.y < 1 || box.y_end() - qy < 1) continue;
+      const int cx[4] = {box.x, box.x_end(), box.x_end(), box.x};
+      const int cy[4] = {box.y, box.y, box.y_end(), box.y_end()};
+      int best = 0;
+      double bd = 0.0;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const double ddx = qx - (double)cx[m], ddy = qy - (double)cy[m];
+        const double d = sqrt(ddx * ddx + ddy * ddy);
+        if (m == 0 || d < bd) { best = m; bd = d; }
+      }
+      rb[k] = shrink(bound2((double)cx[best], (double)cy[best], qx, qy), W, H);
+    }
+    const uint8_t* sem = a.masks + (size_t)b.slot * H * W;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int y = box.y + wave; y <= box.y_end(); y += kTB / 64) {
+      const uint8_t* srow = sem + (size_t)y * W;
+      for (int xx = box.x + lane; xx <= box.x_end(); xx += 64) {
+        bool m = true;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (xx >= eb[e].x && xx <= eb[e].x_end() && y >= eb[e].y && y <= eb[e].y_end()) {
+            const double cross = ((double)xx - p[e][0]) * dy[e] - ((double)y - p[e][1]) * dx[e];
+            if (cross > 0) m = false;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (xx >= rb[k].x && xx <= rb[k].x_end() && y >= rb[k].y && y <= rb[k].y_end()) m = false;
+        if (m) {
+          if (srow[xx]) ++tp;
+          else ++fp;
+        }
+      }
+    }
+  }
+  // workgroup sums
+  for (int off = 32; off > 0; off >>= 1) {
+    tp += __shfl_xor(tp, off, 64);
+    fp += __shfl_xor(fp, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = tp;
+    red[1][threadIdx.x >> 6] = fp;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double iou = 0.0;
+    if (ok) {
+      int64_t T = 0, F = 0;
+#pragma unroll
+      for (int w = 0; w < kTB / 64; ++w) {
+        T += red[0][w];
+        F += red[1][w];
+      }
+      const int64_t fn = a.sem_total[b.slot] - T;
+      double den = (double)T * 1.;
+      den = den + (double)F;
+      den = den + (double)fn;
+      iou = (double)T / den;
+    }
+    iou_out[blockIdx.x] = iou;
+  }
+}
+
+// Ceres 2.1 QuaternionManifold::PlusJacobian (4 x 3 row-major)
+__device__ inline void quat_plus_jac(const double q[4], double J[12]) {
+  J[0] = -q[1]; J[1] = -q[2];  J[2] = -q[3];
+  J[3] = q[0];  J[4] = q[3];   J[5] = -q[2];
+  J[6] = -q[3]; J[7] = q[0];   J[8] = q[1];
+  J[9] = q[2];  J[10] = -q[1]; J[11] = q[0];
+}
+
+// Per block: residual, ambient CENTRAL Jacobian, tangent rows with the
+// manifolds (camera / cylinder quaternions, constant tvec coordinates) and
+// the ScaledLoss(weight) Corrector (r, J *= sqrt(weight)).
+__global__ void gsba_block_kernel(GsbaArgs a, int nblocks, const uint32_t* __restrict__ img_flags,
+                                  const double* __restrict__ iou, double weight, double* __restrict__ r_out,
+                                  double* __restrict__ J_out, double* __restrict__ J16_out,
+                                  double* __restrict__ r_raw_out, double* __restrict__ cost) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= nblocks) return;
+  const GsbaBlock b = a.blocks[k];
+  double x[16];
+  load_params(a, b, x);
+  const double* f = iou + b.eval0;
+  double r = 1.0 - f[0];
+  const int lo = b.variant == kGsbaConstantPose ? 7 : 0;
+  const int hi = b.variant == kGsbaConstantCylinder ? 7 : 16;
+  double J16[16];
+  int e = 1;
+  for (int j = 0; j < 16; ++j) {
+    J16[j] = 0.0;
+    if (j < lo || j >= hi) continue;
+    const double delta = step_of(x[j], a.rel_step);
+    const double fp = 1.0 - f[e], fm = 1.0 - f[e + 1];
+    e += 2;
+    double one_over_delta = 1.0 / delta;
+    one_over_delta /= 2;
+    J16[j] = (fp - fm) * one_over_delta;
+  }
+  if (J16_out) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) J16_out[16 * (size_t)k + j] = J16[j];
+    r_raw_out[k] = r;
+  }
+  double Jt[14], PJ[12];
+  quat_plus_jac(x, PJ);
+  for (int col = 0; col < 3; ++col) {
+    double acc = 0.0;
+    for (int m = 0; m < 4; ++m) acc += J16[m] * PJ[m * 3 + col];
+    Jt[col] = acc;
+  }
+  const uint32_t flags = img_flags[b.img];
+  for (int col = 0; col < 3; ++col) Jt[3 + col] = ((flags >> (1 + col)) & 1u) ? 0.0 : J16[4 + col];
+  quat_plus_jac(x + 7, PJ);
+  for (int col = 0; col < 3; ++col) {
+    double acc = 0.0;
+    for (int m = 0; m < 4; ++m) acc += J16[7 + m] * PJ[m * 3 + col];
+    Jt[6 + col] = acc;
+  }
+  for (int col = 0; col < 5; ++col) Jt[9 + col] = J16[11 + col];
+  // ScaledLoss corrector: rho = (w s, w, 0)
+  cost[k] = 0.5 * (weight * (r * r));
+  const double sqrt_rho1 = sqrt(weight);
+  for (int col = 0; col < 14; ++col) J_out[14 * (size_t)k + col] = Jt[col] * sqrt_rho1;
+  r_out[k] = r * sqrt_rho1;
+}
+
+__global__ void gsba_cost_kernel(const GsbaBlock* __restrict__ blocks, int nblocks, const double* __restrict__ iou,
+                                 double weight, double* __restrict__ cost) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= nblocks) return;
+  const double r = 1.0 - iou[k];
+  (void)blocks;
+  cost[k] = 0.5 * (weight * (r * r));
+}
+
+// Slots of a block's tangent columns: pose 6 (or -1), cylinder 8 (or -1).
+__device__ inline int64_t gsba_slot(const GsbaBlock& b, int m, int64_t cyl0, int cyl_var, uint32_t pose_var) {
+  if (m < 6) return (b.variant != kGsbaConstantPose && pose_var) ? 6 * (int64_t)b.img + m : -1;
+  return (b.variant != kGsbaConstantCylinder && cyl_var) ? cyl0 + 8 * (int64_t)b.cyl + (m - 6) : -1;
+}
+
+__device__ inline int sym6(int a, int c) { return a * 6 - (a * (a - 1)) / 2 + (c - a); }   // a <= c < 6
+__device__ inline int sym8(int a, int c) { return a * 8 - (a * (a - 1)) / 2 + (c - a); }   // a <= c < 8
+
+__global__ void gsba_fblock_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
+                                   const uint32_t* __restrict__ img_flags, const double* __restrict__ r,
+                                   const double* __restrict__ J, int64_t cyl0, int cyl_var,
+                                   double* __restrict__ pose_blk, double* __restrict__ cyl_blk,
+                                   double* __restrict__ bvec, double* __restrict__ udiag) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= nblocks) return;
+  const GsbaBlock b = blocks[k];
+  const double* Jr = J + 14 * (size_t)k;
+  const double rr = r[k];
+  const uint32_t pv = img_flags[b.img] & 1u;
+  if (gsba_slot(b, 0, cyl0, cyl_var, pv) >= 0) {
+    for (int a = 0; a < 6; ++a) {
+      for (int c = a; c < 6; ++c) atomicAdd(pose_blk + 21 * (size_t)b.img + sym6(a, c), Jr[a] * Jr[c]);
+      atomicAdd(bvec + 6 * (size_t)b.img + a, Jr[a] * rr);
+      atomicAdd(udiag + 6 * (size_t)b.img + a, Jr[a] * Jr[a]);
+    }
+  }
+  if (gsba_slot(b, 6, cyl0, cyl_var, pv) >= 0) {
+    const int64_t o = cyl0 + 8 * (int64_t)b.cyl;
+    for (int a = 0; a < 8; ++a) {
+      for (int c = a; c < 8; ++c) atomicAdd(cyl_blk + 36 * (size_t)b.cyl + sym8(a, c), Jr[6 + a] * Jr[6 + c]);
+      atomicAdd(bvec + o + a, Jr[6 + a] * rr);
+      atomicAdd(udiag + o + a, Jr[6 + a] * Jr[6 + a]);
+    }
+  }
+}
+
+// y += J'(J x) over the block's slots.
+__global__ void gsba_product_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
+                                    const uint32_t* __restrict__ img_flags, const double* __restrict__ J,
+                                    int64_t cyl0, int cyl_var, const double* __restrict__ x, double* __restrict__ y) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= nblocks) return;
+  const GsbaBlock b = blocks[k];
+  const double* Jr = J + 14 * (size_t)k;
+  const uint32_t pv = img_flags[b.img] & 1u;
+  double e = 0.0;
+  for (int m = 0; m < 14; ++m) {
+    const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv);
+    if (s >= 0) e += Jr[m] * x[s];
+  }
+  for (int m = 0; m < 14; ++m) {
+    const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv);
+    if (s >= 0) atomicAdd(y + s, Jr[m] * e);
+  }
+}
+
+// S += J'J (upper triangle, row-major nf x nf).
+__global__ void gsba_dense_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
+                                  const uint32_t* __restrict__ img_flags, const double* __restrict__ J, int64_t cyl0,
+                                  int cyl_var, int64_t nf, double* __restrict__ S) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)nblocks * 196) return;
+  const int k = (int)(t / 196), e = (int)(t % 196);
+  const int a = e / 14, c = e % 14;
+  const GsbaBlock b = blocks[k];
+  const uint32_t pv = img_flags[b.img] & 1u;
+  const int64_t ra = gsba_slot(b, a, cyl0, cyl_var, pv), rc = gsba_slot(b, c, cyl0, cyl_var, pv);
+  if (ra < 0 || rc < 0 || ra > rc) return;
+  const double* Jr = J + 14 * (size_t)k;
+  atomicAdd(S + ra * nf + rc, Jr[a] * Jr[c]);
+}
+
+// model cost change contribution -(e (r + e / 2)), e = J df
+__global__ void gsba_model_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
+                                  const uint32_t* __restrict__ img_flags, const double* __restrict__ r,
+                                  const double* __restrict__ J, int64_t cyl0, int cyl_var,
+                                  const double* __restrict__ df, double* __restrict__ out) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  double v = 0.0;
+  if (k < nblocks) {
+    const GsbaBlock b = blocks[k];
+    const double* Jr = J + 14 * (size_t)k;
+    const uint32_t pv = img_flags[b.img] & 1u;
+    double e = 0.0;
+    for (int m = 0; m < 14; ++m) {
+      const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv);
+      if (s >= 0) e += Jr[m] * df[s];
+    }
+    v = -(e * (r[k] + e / 2.0));
+  }
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, v);
+}
+
+// Ceres 2.1 QuaternionManifold::Plus on the cylinder qvec, Euclidean t, r,
+// h; the radius is projected onto its lower bound 0 (ParameterBlock::Plus).
+__global__ void gsba_plus_kernel(int ncyl, const double* __restrict__ cyl, const double* __restrict__ df,
+                                 double* __restrict__ out) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= ncyl) return;
+  const double* y = cyl + 9 * (size_t)k;
+  const double* d = df + 8 * (size_t)k;
+  double* o = out + 9 * (size_t)k;
+  const double q[4] = {y[0], y[1], y[2], y[3]};
+  const double dr[3] = {d[0], d[1], d[2]};
+  double qn[4];
+  quat_plus(q, dr, qn);
+  o[0] = qn[0]; o[1] = qn[1]; o[2] = qn[2]; o[3] = qn[3];
+  o[4] = y[4] + d[3];
+  o[5] = y[5] + d[4];
+  o[6] = y[6] + d[5];
+  o[7] = fmax(y[7] + d[6], 0.0);
+  o[8] = y[8] + d[7];
+}
+
+GsbaArgs make_args(mi_ba_context* ctx, const double* qt, const double* cyl) {
+  GsbaState* G = ctx->gsba;
+  GsbaArgs a;
+  a.blocks = G->blocks.ptr;
+  a.qt = qt;
+  a.cam = ctx->dev.cam;
+  a.img_cam = ctx->dev.img_cam;
+  a.cyl = cyl;
+  a.masks = G->masks.ptr;
+  a.sem_total = G->sem_total.ptr;
+  a.H = G->H;
+  a.W = G->W;
+  a.rel_step = G->rel_step;
+  return a;
+}
+
+unsigned grid64(int64_t n) { return (unsigned)((n + 63) / 64); }
+
+}  // namespace
+
+int gsba_cylinder_slots(const mi_ba_options& o, const mi_ba_problem* p, const mi_ba_gsba* g) {
+  (void)o;
+  if (!g || !g->refine_geometry || g->num_cylinders <= 0) return 0;
+  int ncfg = 0;
+  for (int i = 0; i < p->num_images; ++i) ncfg += p->image_in_config ? (p->image_in_config[i] != 0) : 1;
+  return ncfg > 0 ? 8 * g->num_cylinders : 0;
+}
+
+mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
+  const mi_ba_problem* p = &ctx->problem;
+  const mi_ba_options& o = ctx->options;
+  if (g->height <= 0 || g->width <= 0 || !g->trunk_mask || g->num_cylinders < 0 ||
+      (g->num_cylinders > 0 && !g->cylinders) || !(g->numeric_relative_step_size > 0))
+    return MI_BA_ERR_INVALID_ARGUMENT;
+  HostSetup& s = ctx->setup;
+  const int I = p->num_images;
+  auto in_cfg = [&](int i) { return p->image_in_config ? p->image_in_config[i] != 0 : true; };
+  // GeometricSemanticBundleAdjuster::Assert (:664-712)
+  int ncfg = 0;
+  for (int i = 0; i < I; ++i) {
+    if (!in_cfg(i)) continue;
+    ++ncfg;
+    const int cam = p->image_camera[i];
+    if (!(p->camera_constant && p->camera_constant[cam])) return MI_BA_ERR_UNSUPPORTED;
+    if (s.cam_model[cam] != kSimplePinhole) return MI_BA_ERR_UNSUPPORTED;
+  }
+  auto* G = new GsbaState();
+  ctx->gsba = G;
+  G->host = g;
+  G->H = g->height;
+  G->W = g->width;
+  G->ncyl = g->num_cylinders;
+  G->rel_step = g->numeric_relative_step_size;
+  G->weight = ncfg > 0 ? 1. / (double)ncfg : 1.0;
+  // blocks (AddImageToProblem, :835-909): config images in problem order
+  std::vector<int32_t> slot(I, -1);
+  std::vector<int> slot_images;
+  std::vector<GsbaEval> evals, centres;
+  for (int i = 0; i < I; ++i) {
+    if (!in_cfg(i)) continue;
+    const bool constant_pose = !o.refine_extrinsics || (p->image_constant_pose && p->image_constant_pose[i]);
+    if (constant_pose && !g->refine_geometry) continue;
+    for (int c = 0; c < g->num_cylinders; ++c) {
+      GsbaBlock b{};
+      b.img = i;
+      b.cyl = c;
+      b.variant = constant_pose ? kGsbaConstantPose : g->refine_geometry ? kGsbaFull : kGsbaConstantCylinder;
+      if (slot[i] < 0) {
+        slot[i] = (int32_t)slot_images.size();
+        slot_images.push_back(i);
+      }
+      b.slot = slot[i];
+      b.eval0 = (int32_t)evals.size();
+      const int32_t kb = (int32_t)G->blocks_host.size();
+      evals.push_back(GsbaEval{kb, -1, 1});
+      centres.push_back(GsbaEval{kb, -1, 1});
+      const int lo = b.variant == kGsbaConstantPose ? 7 : 0;
+      const int hi = b.variant == kGsbaConstantCylinder ? 7 : 16;
+      for (int j = lo; j < hi; ++j) {
+        evals.push_back(GsbaEval{kb, (int16_t)j, 1});
+        evals.push_back(GsbaEval{kb, (int16_t)j, -1});
+      }
+      b.nevals = (int32_t)evals.size() - b.eval0;
+      G->blocks_host.push_back(b);
+      // poses of GSBA blocks are variable parameter blocks (SetUpManifolds)
+      if (b.variant != kGsbaConstantPose && !s.img_var[i]) {
+        s.img_var[i] = 1;
+        s.img_tvec_mask[i] = p->image_constant_tvec ? p->image_constant_tvec[i] : 0;
+        int masked = 0;
+        for (int m = 0; m < 3; ++m) masked += (s.img_tvec_mask[i] >> m) & 1;
+        s.num_effective_parameters_reduced += 6 - masked;
+      }
+    }
+  }
+  G->nblocks = (int)G->blocks_host.size();
+  G->nevals = (int64_t)evals.size();
+  if (ctx->dev.cyl_var) s.num_effective_parameters_reduced += 8 * (int64_t)G->ncyl;
+  const size_t plane = (size_t)G->H * G->W;
+  std::vector<int64_t> totals(slot_images.size(), 0);
+  for (size_t k = 0; k < slot_images.size(); ++k) {
+    const uint8_t* m = g->trunk_mask + (size_t)slot_images[k] * plane;
+    int64_t t = 0;
+    for (size_t q = 0; q < plane; ++q) t += m[q] != 0;
+    totals[k] = t;
+  }
+  std::vector<double> cyl(9 * (size_t)std::max(1, G->ncyl), 0.0);
+  for (int c = 0; c < G->ncyl; ++c) {
+    const mi_ba_cylinder& y = g->cylinders[c];
+    for (int m = 0; m < 4; ++m) cyl[9 * c + m] = y.qvec[m];
+    for (int m = 0; m < 3; ++m) cyl[9 * c + 4 + m] = y.tvec[m];
+    cyl[9 * c + 7] = y.radius;
+    cyl[9 * c + 8] = y.height;
+  }
+  const int nb = std::max(1, G->nblocks);
+  if (G->blocks.alloc(nb) || G->evals.alloc(std::max<int64_t>(1, G->nevals)) || G->centres.alloc(nb) ||
+      G->masks.alloc(plane * std::max<size_t>(1, slot_images.size())) ||
+      G->sem_total.alloc(std::max<size_t>(1, slot_images.size())) || G->cyl.alloc(cyl.size()) ||
+      G->cyl_c.alloc(cyl.size()) || G->iou.alloc(std::max<int64_t>(1, G->nevals)) || G->r.alloc(nb) ||
+      G->J.alloc(14 * (size_t)nb) || G->cyl_blk.alloc(36 * (size_t)std::max(1, G->ncyl)) ||
+      G->prec_cyl.alloc(64 * (size_t)std::max(1, G->ncyl)) || G->partial.alloc(nb))
+    return MI_BA_ERR_OUT_OF_MEMORY;
+  if ((G->nblocks &&
+       (hipMemcpy(G->blocks.ptr, G->blocks_host.data(), G->nblocks * sizeof(GsbaBlock), hipMemcpyHostToDevice) ||
+        hipMemcpy(G->evals.ptr, evals.data(), evals.size() * sizeof(GsbaEval), hipMemcpyHostToDevice) ||
+        hipMemcpy(G->centres.ptr, centres.data(), centres.size() * sizeof(GsbaEval), hipMemcpyHostToDevice))) ||
+      hipMemcpy(G->cyl.ptr, cyl.data(), cyl.size() * 8, hipMemcpyHostToDevice) ||
+      (!slot_images.empty() &&
+       hipMemcpy(G->sem_total.ptr, totals.data(), totals.size() * 8, hipMemcpyHostToDevice)))
+    return MI_BA_ERR_HIP;
+  for (size_t k = 0; k < slot_images.size(); ++k)
+    if (hipMemcpy(G->masks.ptr + k * plane, g->trunk_mask + (size_t)slot_images[k] * plane, plane,
+                  hipMemcpyHostToDevice))
+      return MI_BA_ERR_HIP;
+  // refresh image flags (poses made variable by the GSBA term)
+  std::vector<uint32_t> fl(I);
+  for (int i = 0; i < I; ++i) fl[i] = (s.img_var[i] ? 1u : 0u) | ((uint32_t)s.img_tvec_mask[i] << 1);
+  if (I && hipMemcpy(ctx->img_flags.ptr, fl.data(), I * 4, hipMemcpyHostToDevice) != hipSuccess) return MI_BA_ERR_HIP;
+  return MI_BA_OK;
+}
+
+void gsba_destroy(mi_ba_context* ctx) {
+  if (!ctx->gsba) return;
+  delete ctx->gsba;
+  ctx->gsba = nullptr;
+}
+
+namespace {
+mi_ba_status eval_blocks(mi_ba_context* ctx, double* d_cost, double* J16, double* r_raw) {
+  GsbaState* G = ctx->gsba;
+  if (!G->nblocks) return MI_BA_OK;
+  hipStream_t s = ctx->stream;
+  GsbaArgs a = make_args(ctx, ctx->dev.qt, G->cyl.ptr);
+  hipEvent_t stop;
+  timer_begin(ctx, "gsba_iou", &stop);
+  hipLaunchKernelGGL(gsba_iou_kernel, dim3((unsigned)G->nevals), dim3(kTB), 0, s, a, G->evals.ptr, G->iou.ptr);
+  timer_end(ctx, stop);
+  hipLaunchKernelGGL(gsba_block_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, s, a, G->nblocks, ctx->dev.img_flags,
+                     G->iou.ptr, G->weight, G->r.ptr, G->J.ptr, J16, r_raw, G->partial.ptr);
+  launch_sum(G->partial.ptr, G->nblocks, d_cost, s);
+  return hipGetLastError() == hipSuccess ? MI_BA_OK : MI_BA_ERR_HIP;
+}
+}  // namespace
+
+mi_ba_status gsba_linearize(mi_ba_context* ctx, double* d_cost) { return eval_blocks(ctx, d_cost, nullptr, nullptr); }
+
+void gsba_cost(mi_ba_context* ctx, const double* qt, const double* cyl, double* d_cost) {
+  GsbaState* G = ctx->gsba;
+  if (!G->nblocks) return;
+  hipStream_t s = ctx->stream;
+  GsbaArgs a = make_args(ctx, qt, cyl);
+  hipLaunchKernelGGL(gsba_iou_kernel, dim3((unsigned)G->nblocks), dim3(kTB), 0, s, a, G->centres.ptr, G->iou.ptr);
+  hipLaunchKernelGGL(gsba_cost_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, s, G->blocks.ptr, G->nblocks,
+                     G->iou.ptr, G->weight, G->partial.ptr);
+  launch_sum(G->partial.ptr, G->nblocks, d_cost, s);
+}
+
+void gsba_add_fblock(mi_ba_context* ctx) {
+  GsbaState* G = ctx->gsba;
+  hipStream_t s = ctx->stream;
+  (void)hipMemsetAsync(G->cyl_blk.ptr, 0, G->cyl_blk.bytes(), s);
+  if (!G->nblocks) return;
+  hipLaunchKernelGGL(gsba_fblock_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, s, G->blocks.ptr, G->nblocks,
+                     ctx->dev.img_flags, G->r.ptr, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, ctx->pose_blk.ptr,
+                     G->cyl_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr);
+}
+
+void gsba_finalize(mi_ba_context* ctx, int first, int reuse_diag, double radius) {
+  GsbaState* G = ctx->gsba;
+  if (!ctx->dev.cyl_var || G->ncyl == 0) return;
+  const int64_t o = ctx->dev.cyl0;
+  launch_finalize8(G->ncyl, G->cyl_blk.ptr, ctx->udiag.ptr + o, ctx->scale_f.ptr + o, ctx->diag_f.ptr + o,
+                   ctx->lambda_f.ptr + o, G->prec_cyl.ptr, ctx->bvec.ptr + o, 1, first, reuse_diag, radius,
+                   ctx->stream);
+}
+
+void gsba_schur_product(mi_ba_context* ctx, const double* x, double* y) {
+  GsbaState* G = ctx->gsba;
+  if (!G->nblocks) return;
+  hipLaunchKernelGGL(gsba_product_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, ctx->stream, G->blocks.ptr,
+                     G->nblocks, ctx->dev.img_flags, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, x, y);
+}
+
+void gsba_precond(mi_ba_context* ctx, const double* r, double* z) {
+  GsbaState* G = ctx->gsba;
+  if (!ctx->dev.cyl_var || G->ncyl == 0) return;
+  const int64_t o = ctx->dev.cyl0;
+  launch_precond8(G->ncyl, G->prec_cyl.ptr, r + o, z + o, ctx->stream);
+}
+
+void gsba_add_dense(mi_ba_context* ctx, double* S) {
+  GsbaState* G = ctx->gsba;
+  if (!G->nblocks) return;
+  const int64_t n = (int64_t)G->nblocks * 196;
+  hipLaunchKernelGGL(gsba_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, G->blocks.ptr,
+                     G->nblocks, ctx->dev.img_flags, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, ctx->dev.nf, S);
+}
+
+void gsba_model_cost(mi_ba_context* ctx, const double* df, double* d_out) {
+  GsbaState* G = ctx->gsba;
+  if (!G->nblocks) return;
+  hipLaunchKernelGGL(gsba_model_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, ctx->stream, G->blocks.ptr,
+                     G->nblocks, ctx->dev.img_flags, G->r.ptr, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, df, d_out);
+}
+
+void gsba_plus(mi_ba_context* ctx, const double* df) {
+  GsbaState* G = ctx->gsba;
+  if (G->ncyl == 0) return;
+  if (!ctx->dev.cyl_var) {
+    (void)hipMemcpyAsync(G->cyl_c.ptr, G->cyl.ptr, G->cyl.bytes(), hipMemcpyDeviceToDevice, ctx->stream);
+    return;
+  }
+  hipLaunchKernelGGL(gsba_plus_kernel, dim3(grid64(G->ncyl)), dim3(64), 0, ctx->stream, G->ncyl, G->cyl.ptr,
+                     df + ctx->dev.cyl0, G->cyl_c.ptr);
+}
+
+void gsba_accept(mi_ba_context* ctx) {
+  GsbaState* G = ctx->gsba;
+  std::swap(G->cyl.ptr, G->cyl_c.ptr);
+}
+
+mi_ba_status gsba_writeback(mi_ba_context* ctx) {
+  GsbaState* G = ctx->gsba;
+  if (!G->ncyl) return MI_BA_OK;
+  std::vector<double> cyl(9 * (size_t)G->ncyl);
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+      hipMemcpy(cyl.data(), G->cyl.ptr, cyl.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return MI_BA_ERR_HIP;
+  if (!ctx->dev.cyl_var) return MI_BA_OK;
+  for (int c = 0; c < G->ncyl; ++c) {
+    mi_ba_cylinder& y = G->host->cylinders[c];
+    for (int m = 0; m < 4; ++m) y.qvec[m] = cyl[9 * c + m];
+    for (int m = 0; m < 3; ++m) y.tvec[m] = cyl[9 * c + 4 + m];
+    y.radius = cyl[9 * c + 7];
+    y.height = cyl[9 * c + 8];
+  }
+  return MI_BA_OK;
+}
+
+mi_ba_status gsba_download(mi_ba_context* ctx, int32_t* ids, double* residuals, double* jacobians) {
+  GsbaState* G = ctx->gsba;
+  const int nb = G->nblocks;
+  if (!nb) return MI_BA_OK;
+  DevArray<double> J16, rr;
+  DevArray<double> cost;
+  if (J16.alloc(16 * (size_t)nb) || rr.alloc(nb) || cost.alloc(1)) return MI_BA_ERR_OUT_OF_MEMORY;
+  if (hipMemsetAsync(cost.ptr, 0, 8, ctx->stream) != hipSuccess) return MI_BA_ERR_HIP;
+  mi_ba_status st = eval_blocks(ctx, cost.ptr, J16.ptr, rr.ptr);
+  if (st != MI_BA_OK) return st;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+      hipMemcpy(jacobians, J16.ptr, 16 * (size_t)nb * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(residuals, rr.ptr, (size_t)nb * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return MI_BA_ERR_HIP;
+  for (int k = 0; k < nb; ++k) {
+    ids[2 * k] = G->blocks_host[k].img;
+    ids[2 * k + 1] = G->blocks_host[k].cyl;
+  }
+  return MI_BA_OK;
+}
+
+}  // namespace miba

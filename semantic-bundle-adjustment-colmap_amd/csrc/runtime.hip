@@ -26,6 +26,7 @@
 #include "cholesky.h"
 #include "context.h"
 #include "kernels.h"
+#include "gsba.h"
 #include "semantic.h"
 #include "setup.h"
 #include <rocsolver/rocsolver.h>
@@ -36,7 +37,8 @@ namespace {
 
 enum Scalar {
   kCost = 0, kCandCost = 1, kModelCost = 2, kRho = 3, kRhoPrev = 4, kPQ = 5, kXB = 6, kXR = 7,
-  kStepNorm = 8, kSemCost = 9, kSemCand = 10, kSemModel = 11, kNumScalars = 16
+  kStepNorm = 8, kSemCost = 9, kSemCand = 10, kSemModel = 11, kGsCost = 12, kGsCand = 13, kGsModel = 14,
+  kNumScalars = 16
 };
 
 #define MI_HIP(expr)                                     \
@@ -237,6 +239,7 @@ namespace {
 // Drops the problem state of a solved context, keeping its device resources.
 void reset_problem_state(mi_ba_context* ctx) {
   semantic_destroy(ctx);
+  gsba_destroy(ctx);
   ctx->timer.totals.clear();
   ctx->timing = false;
   ctx->solved = false;
@@ -251,7 +254,7 @@ void reset_problem_state(mi_ba_context* ctx) {
 }  // namespace
 
 mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const mi_ba_problem* pin,
-                             const mi_ba_semantic* sem, mi_ba_context** out) {
+                             const mi_ba_semantic* sem, mi_ba_context** out, const mi_ba_gsba* gsba) {
   if (!o || !pin || !out) {
     context_destroy(old);
     return MI_BA_ERR_INVALID_ARGUMENT;
@@ -402,7 +405,12 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
   d.num_images = I;
   d.num_cameras = C;
   d.num_points = P;
-  d.nf = 6 * (int64_t)I + (int64_t)s.ct * C;
+  d.cyl0 = 6 * (int64_t)I + (int64_t)s.ct * C;
+  {
+    const int slots = gsba ? gsba_cylinder_slots(*o, p, gsba) : 0;
+    d.nf = d.cyl0 + slots;
+    d.cyl_var = slots > 0;
+  }
   d.loss_type = o->loss_function_type;
   d.loss_scale = o->loss_function_scale;
   d.jvariant = 0;
@@ -501,6 +509,10 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
     st = semantic_create(ctx, sem);
     if (st != MI_BA_OK) return fail(st);
   }
+  if (gsba) {
+    st = gsba_create(ctx, gsba);
+    if (st != MI_BA_OK) return fail(st);
+  }
   *out = ctx;
   return MI_BA_OK;
 }
@@ -510,6 +522,7 @@ void context_destroy(mi_ba_context* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   semantic_destroy(ctx);
+  gsba_destroy(ctx);
   for (auto& e : ctx->timer.pending) {
     (void)hipEventDestroy(e.second.first);
     (void)hipEventDestroy(e.second.second);
@@ -539,6 +552,10 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
   }
+  if (ctx->gsba) {
+    mi_ba_status st = gsba_linearize(ctx, ctx->scalars.ptr + kGsCost);
+    if (st != MI_BA_OK) return st;
+  }
   MI_HIP(hipGetLastError());
   if (ctx->world > 1 && cost_out) {
     mi_ba_status st = allreduce(ctx, ctx->scalars.ptr + kCost, 1);
@@ -548,7 +565,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   if (cost_out) {
     mi_ba_status st = read_scalars(ctx, 0, kNumScalars);
     if (st != MI_BA_OK) return st;
-    *cost_out = ctx->host_scalars[kCost] + ctx->host_scalars[kSemCost];
+    *cost_out = ctx->host_scalars[kCost] + ctx->host_scalars[kSemCost] + ctx->host_scalars[kGsCost];
   }
   return MI_BA_OK;
 }
@@ -561,6 +578,7 @@ void schur_product(mi_ba_context* ctx, const double* x, double* y) {
   launch_schur_product(d, ctx->vpoints.ptr, ctx->npv, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr,
                        ctx->Vinv.ptr, ctx->lambda_f.ptr, x, ctx->cg_w.ptr, y, ctx->stream);
   if (ctx->sem) semantic_schur_product(ctx, x, y);
+  if (ctx->gsba) gsba_schur_product(ctx, x, y);
 }
 
 // Preconditioned CG on the Schur complement, Ceres ConjugateGradientsSolver
@@ -583,6 +601,7 @@ mi_ba_status pcg(mi_ba_context* ctx, int* iterations) {
   const int max_it = std::max(1, ctx->options.max_linear_solver_iterations);
   for (int it = 1; it <= max_it; ++it) {
     launch_precond(d, ctx->prec_pose.ptr, ctx->prec_cam.ptr, ctx->cg_r.ptr, ctx->cg_z.ptr, s);
+    if (ctx->gsba) gsba_precond(ctx, ctx->cg_r.ptr, ctx->cg_z.ptr);
     if (it > 1) MI_HIP(hipMemcpyAsync(sc + kRhoPrev, sc + kRho, 8, hipMemcpyDeviceToDevice, s));
     launch_dot(ctx->cg_r.ptr, ctx->cg_z.ptr, nf, sc + kRho, s);
     if (it == 1) {
@@ -636,6 +655,7 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
                      ctx->ptiles.ptr, ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, s);
   if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
+  if (ctx->gsba) gsba_add_dense(ctx, ctx->S.ptr);
   timer_end(ctx, stop);
   if (ctx->world > 1) {
     // every rank holds the Schur contribution of its own points
@@ -683,7 +703,8 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
   double* sc = ctx->scalars.ptr;
   double* hs = ctx->host_scalars;
   std::memset(sum, 0, sizeof(*sum));
-  sum->num_residuals_reduced = ctx->setup.num_residuals_reduced + (ctx->sem ? ctx->sem->ns : 0);
+  sum->num_residuals_reduced =
+      ctx->setup.num_residuals_reduced + (ctx->sem ? ctx->sem->ns : 0) + (ctx->gsba ? ctx->gsba->nblocks : 0);
   sum->num_effective_parameters_reduced = ctx->setup.num_effective_parameters_reduced;
   sum->num_semantic_residuals = ctx->sem ? ctx->sem->ns : 0;
   sum->fixed_cost = ctx->fixed_cost;
@@ -722,6 +743,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr,
                     ctx->Vinv.ptr, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr, s);
       if (ctx->sem) semantic_add_fblock(ctx);
+      if (ctx->gsba) gsba_add_fblock(ctx);
     }
     if (ctx->world > 1) {
       Phase ph_(ctx, "f_allreduce");
@@ -734,6 +756,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     launch_fblock_finalize(d, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->udiag.ptr, ctx->scale_f.ptr,
                            ctx->diag_f.ptr, ctx->lambda_f.ptr, ctx->prec_pose.ptr, ctx->prec_cam.ptr,
                            ctx->bvec.ptr, first, reuse_diag, radius, s);
+    if (ctx->gsba) gsba_finalize(ctx, first, reuse_diag, radius);
     first = false;
     reuse_diag = true;
     int cg_it = 0;
@@ -769,8 +792,10 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     launch_model_cost(d, ctx->r.ptr, ctx->J.ptr, ctx->cg_x.ptr, ctx->dX.ptr, ctx->partial.ptr, s);
     MI_HIP(hipMemsetAsync(sc + kModelCost, 0, 8, s));
     MI_HIP(hipMemsetAsync(sc + kSemModel, 0, 8, s));
+    MI_HIP(hipMemsetAsync(sc + kGsModel, 0, 8, s));
     if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kModelCost, s);
     if (ctx->sem) semantic_model_cost(ctx, ctx->cg_x.ptr, sc + kSemModel);
+    if (ctx->gsba) gsba_model_cost(ctx, ctx->cg_x.ptr, sc + kGsModel);
     // camera step counted once (rank 0), point steps on their own ranks
     launch_sqnorm2(ctx->cg_x.ptr, ctx->rank == 0 ? nf : 0, ctx->dX.ptr, 3 * d.num_points, sc + kStepNorm, s);
     if (ctx->world > 1) {
@@ -781,7 +806,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     }
     st = read_scalars(ctx, 0, kNumScalars);
     if (st != MI_BA_OK) return st;
-    const double model_cost_change = hs[kModelCost] + hs[kSemModel];
+    const double model_cost_change = hs[kModelCost] + hs[kSemModel] + hs[kGsModel];
     const bool valid = std::isfinite(model_cost_change) && model_cost_change > 0.0;
     if (!valid) {
       ++consecutive_invalid;
@@ -799,14 +824,17 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     // candidate
     launch_plus(d, ctx->cg_x.ptr, ctx->dX.ptr, ctx->qt.ptr, ctx->cam.ptr, ctx->X.ptr, ctx->qt_c.ptr,
                 ctx->cam_c.ptr, ctx->X_c.ptr, s);
+    if (ctx->gsba) gsba_plus(ctx, ctx->cg_x.ptr);
     MI_HIP(hipMemsetAsync(sc + kCandCost, 0, 8, s));
     MI_HIP(hipMemsetAsync(sc + kSemCand, 0, 8, s));
+    MI_HIP(hipMemsetAsync(sc + kGsCand, 0, 8, s));
     {
       Phase ph_(ctx, "trial_cost");
       launch_reproj_cost(d, ctx->qt_c.ptr, ctx->cam_c.ptr, ctx->X_c.ptr, ctx->partial.ptr, s);
     }
     if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kCandCost, s);
     if (ctx->sem) semantic_cost(ctx, ctx->qt_c.ptr, ctx->cam_c.ptr, sc + kSemCand);
+    if (ctx->gsba) gsba_cost(ctx, ctx->qt_c.ptr, ctx->gsba->cyl_c.ptr, sc + kGsCand);
     if (ctx->world > 1) {
       st = allreduce(ctx, sc + kCandCost, 1);
       if (st == MI_BA_OK) st = allreduce(ctx, sc + kSemCand, 1);
@@ -814,7 +842,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     }
     st = read_scalars(ctx, 0, kNumScalars);
     if (st != MI_BA_OK) return st;
-    const double candidate_cost = hs[kCandCost] + hs[kSemCand];
+    const double candidate_cost = hs[kCandCost] + hs[kSemCand] + hs[kGsCand];
     const double cost_change = x_cost - candidate_cost;
     const double relative_decrease = cost_change / model_cost_change;
     const bool success = std::isfinite(candidate_cost) && relative_decrease > o.min_relative_decrease;
@@ -845,6 +873,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       ctx->dev.qt = ctx->qt.ptr;
       ctx->dev.cam = ctx->cam.ptr;
       ctx->dev.X = ctx->X.ptr;
+      if (ctx->gsba) gsba_accept(ctx);
       radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * relative_decrease - 1.0, 3));
       radius = std::min(1e16, radius);
       decrease_factor = 2.0;
@@ -890,6 +919,7 @@ mi_ba_status context_writeback(mi_ba_context* ctx) {
     if (!s.pt_var[k]) continue;
     for (int m = 0; m < 3; ++m) p->xyz[3 * k + m] = X[3 * k + m];
   }
+  if (ctx->gsba) return gsba_writeback(ctx);
   return MI_BA_OK;
 }
 
@@ -1017,6 +1047,77 @@ mi_ba_status solve_on(mi_ba_context** arena, const mi_ba_options* o, mi_ba_probl
   return st;
 }
 }  // namespace
+
+void mi_ba_default_gsba(mi_ba_gsba* g) {
+  if (!g) return;
+  std::memset(g, 0, sizeof(*g));
+  g->refine_geometry = 1;
+  g->numeric_relative_step_size = 1e-3;
+  g->include_landmark_error = 0;
+  g->landmark_error_weight = 1.0;
+}
+
+// The GSBA problem (geometric_semantic_bundle_adjustment.cc:714-800): TRIVIAL
+// loss required (Assert); the reprojection blocks only with
+// include_landmark_error, under ScaledLoss(landmark_error_weight / #2D
+// features of the config images).
+static mi_ba_status gsba_problem(const mi_ba_options* o, const mi_ba_problem* p, const mi_ba_gsba* g,
+                                 mi_ba_options* oo, mi_ba_problem* pp) {
+  if (!o || !p || !g) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (o->loss_function_type != MI_BA_LOSS_TRIVIAL) return MI_BA_ERR_UNSUPPORTED;
+  *oo = *o;
+  *pp = *p;
+  if (!g->include_landmark_error) {
+    pp->num_obs = 0;
+  } else {
+    int64_t total = 0;
+    for (int64_t k = 0; k < p->num_obs; ++k) {
+      const int32_t i = p->obs_image[k];
+      if (i < 0 || i >= p->num_images) return MI_BA_ERR_INVALID_ARGUMENT;
+      total += p->image_in_config ? (p->image_in_config[i] != 0) : 1;
+    }
+    oo->loss_function_type = kLossScaled;
+    oo->loss_function_scale = g->landmark_error_weight / (double)std::max<int64_t>(1, total);
+  }
+  return MI_BA_OK;
+}
+
+mi_ba_status mi_ba_gsba_solve(const mi_ba_options* o, mi_ba_problem* p, mi_ba_gsba* g, mi_ba_summary* sum) {
+  if (!sum) return MI_BA_ERR_INVALID_ARGUMENT;
+  mi_ba_options oo;
+  mi_ba_problem pp;
+  mi_ba_status st = gsba_problem(o, p, g, &oo, &pp);
+  if (st != MI_BA_OK) return st;
+  const double t0 = now_s();
+  mi_ba_context* ctx = nullptr;
+  st = context_recycle(nullptr, &oo, &pp, nullptr, &ctx, g);
+  if (st != MI_BA_OK) return st;
+  st = context_solve(ctx, sum);
+  if (st == MI_BA_OK) st = context_writeback(ctx);
+  context_destroy(ctx);
+  sum->total_time_in_seconds = now_s() - t0;
+  if (st == MI_BA_OK && o->print_summary) print_summary(*sum);
+  return st;
+}
+
+mi_ba_status mi_ba_gsba_evaluate(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_gsba* g, int64_t capacity,
+                                 int64_t* num_blocks, int32_t* ids, double* residuals, double* jacobians) {
+  if (!num_blocks) return MI_BA_ERR_INVALID_ARGUMENT;
+  mi_ba_options oo;
+  mi_ba_problem pp;
+  mi_ba_status st = gsba_problem(o, p, g, &oo, &pp);
+  if (st != MI_BA_OK) return st;
+  mi_ba_context* ctx = nullptr;
+  st = context_recycle(nullptr, &oo, &pp, nullptr, &ctx, g);
+  if (st != MI_BA_OK) return st;
+  *num_blocks = ctx->gsba->nblocks;
+  if (*num_blocks <= capacity && *num_blocks > 0) {
+    if (!ids || !residuals || !jacobians) st = MI_BA_ERR_INVALID_ARGUMENT;
+    else st = gsba_download(ctx, ids, residuals, jacobians);
+  }
+  context_destroy(ctx);
+  return st;
+}
 
 mi_ba_status mi_ba_solve_in(mi_ba_context** arena, const mi_ba_options* o, mi_ba_problem* p,
                             const mi_ba_semantic* sem, mi_ba_summary* sum) {
@@ -1151,12 +1252,15 @@ mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost) {
   launch_reproj_cost(ctx->dev, ctx->qt.ptr, ctx->cam.ptr, ctx->X.ptr, ctx->partial.ptr, s);
   if (ctx->dev.nb) launch_sum(ctx->partial.ptr, reproj_grid(ctx->dev.nb), sc + kCandCost, s);
   if (ctx->sem) semantic_cost(ctx, ctx->qt.ptr, ctx->cam.ptr, sc + kSemCand);
+  MI_HIP(hipMemsetAsync(sc + kGsCand, 0, 8, s));
+  if (ctx->gsba) gsba_cost(ctx, ctx->qt.ptr, ctx->gsba->cyl.ptr, sc + kGsCand);
   mi_ba_status st = allreduce(ctx, sc + kCandCost, 1);
   if (st == MI_BA_OK) st = allreduce(ctx, sc + kSemCand, 1);
   if (st != MI_BA_OK) return st;
   st = read_scalars(ctx, 0, kNumScalars);
   if (st != MI_BA_OK) return st;
-  *cost = ctx->host_scalars[kCandCost] + ctx->host_scalars[kSemCand] + ctx->fixed_cost;
+  *cost = ctx->host_scalars[kCandCost] + ctx->host_scalars[kSemCand] + ctx->host_scalars[kGsCand] +
+          ctx->fixed_cost;
   return MI_BA_OK;
 }
 

@@ -84,6 +84,24 @@ class Problem(C.Structure):
     ]
 
 
+class Cylinder(C.Structure):
+    _fields_ = [("qvec", C.c_double * 4), ("tvec", C.c_double * 3), ("radius", C.c_double), ("height", C.c_double)]
+
+
+class Gsba(C.Structure):
+    _fields_ = [
+        ("height", C.c_int32),
+        ("width", C.c_int32),
+        ("trunk_mask", _u8p),
+        ("num_cylinders", C.c_int32),
+        ("cylinders", C.POINTER(Cylinder)),
+        ("refine_geometry", C.c_int32),
+        ("numeric_relative_step_size", C.c_double),
+        ("include_landmark_error", C.c_int32),
+        ("landmark_error_weight", C.c_double),
+    ]
+
+
 class Semantic(C.Structure):
     _fields_ = [
         ("height", C.c_int32),
@@ -195,6 +213,9 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_context_set_comm.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
     lib.mi_ba_context_set_host_reducer.argtypes = [C.c_void_p, C.c_int32, C.c_int32, HOST_ALLREDUCE_FN, C.c_void_p]
     lib.mi_ba_dense_cholesky.argtypes = [C.c_int32, C.c_int32, _dp, _dp, C.c_int32, C.c_int32, C.c_int32, _i32p]
+    lib.mi_ba_gsba_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.mi_ba_gsba_evaluate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64),
+                                        C.c_void_p, C.c_void_p, C.c_void_p]
     lib.mi_ba_solve_in.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.mi_ba_solve_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
                                       C.c_void_p]
@@ -405,6 +426,149 @@ def dense_cholesky(A: np.ndarray, b: Optional[np.ndarray] = None, device: int = 
     check(load().mi_ba_dense_cholesky(device, n, F.ctypes.data_as(_dp), _ptr(x, _dp), panel, lookahead, own_diag,
                                       C.byref(info)), "mi_ba_dense_cholesky")
     return np.tril(F), x, info.value
+
+
+@dataclass
+class GsbaInput:
+    """mi_ba_gsba: trunk masks [I][H][W] (uint8, 1 = trunk class) and
+    cylinders [N][9] = q(4) t(3) radius height (updated in place by solves)."""
+    masks: np.ndarray
+    cylinders: np.ndarray
+    refine_geometry: int = 1
+    numeric_relative_step_size: float = 1e-3
+    include_landmark_error: int = 0
+    landmark_error_weight: float = 1.0
+
+    def copy(self) -> "GsbaInput":
+        return GsbaInput(self.masks, self.cylinders.copy(), self.refine_geometry, self.numeric_relative_step_size,
+                         self.include_landmark_error, self.landmark_error_weight)
+
+    def struct(self):
+        self.masks = np.ascontiguousarray(self.masks, np.uint8)
+        n = len(self.cylinders)
+        arr = (Cylinder * max(1, n))()
+        for k in range(n):
+            c = self.cylinders[k]
+            arr[k].qvec[:] = list(c[:4])
+            arr[k].tvec[:] = list(c[4:7])
+            arr[k].radius = float(c[7])
+            arr[k].height = float(c[8])
+        g = Gsba()
+        g.height, g.width = int(self.masks.shape[1]), int(self.masks.shape[2])
+        g.trunk_mask = _ptr(self.masks, _u8p)
+        g.num_cylinders = n
+        g.cylinders = C.cast(arr, C.POINTER(Cylinder))
+        g.refine_geometry = self.refine_geometry
+        g.numeric_relative_step_size = self.numeric_relative_step_size
+        g.include_landmark_error = self.include_landmark_error
+        g.landmark_error_weight = self.landmark_error_weight
+        return g, arr
+
+    def read_back(self, arr):
+        for k in range(len(self.cylinders)):
+            self.cylinders[k, :4] = list(arr[k].qvec)
+            self.cylinders[k, 4:7] = list(arr[k].tvec)
+            self.cylinders[k, 7] = arr[k].radius
+            self.cylinders[k, 8] = arr[k].height
+
+
+def gsba_solve(options: Options, scene: Scene, gsba: GsbaInput) -> Summary:
+    """GeometricSemanticBundleAdjuster<Cylinder>::Solve on the device."""
+    s = Summary()
+    p = scene.problem()
+    g, arr = gsba.struct()
+    check(load().mi_ba_gsba_solve(C.byref(options), C.byref(p), C.byref(g), C.byref(s)), "mi_ba_gsba_solve")
+    gsba.read_back(arr)
+    return s
+
+
+def gsba_evaluate(options: Options, scene: Scene, gsba: GsbaInput):
+    """Every GSBA block: (ids [n][2], residual 1 - IoU [n], ambient J [n][16])."""
+    p = scene.problem()
+    g, arr = gsba.struct()
+    n = C.c_int64(0)
+    lib = load()
+    check(lib.mi_ba_gsba_evaluate(C.byref(options), C.byref(p), C.byref(g), 0, C.byref(n), None, None, None),
+          "mi_ba_gsba_evaluate")
+    ids = np.zeros((n.value, 2), np.int32)
+    r = np.zeros(n.value)
+    J = np.zeros((n.value, 16))
+    check(lib.mi_ba_gsba_evaluate(C.byref(options), C.byref(p), C.byref(g), n.value, C.byref(n),
+                                  ids.ctypes.data_as(C.c_void_p), r.ctypes.data_as(C.c_void_p),
+                                  J.ctypes.data_as(C.c_void_p)), "mi_ba_gsba_evaluate")
+    return ids, r, J
+
+
+def look_at_qvec(center, target):
+    """World->camera (qvec, tvec) of a camera at `center` looking at `target`
+    (image x right, y down, z forward; world z up)."""
+    z = np.asarray(target, float) - np.asarray(center, float)
+    z /= np.linalg.norm(z)
+    x = np.cross(z, [0.0, 0.0, 1.0])
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x)
+    R = np.stack([x, y, z])
+    t = -R @ np.asarray(center, float)
+    # rotation matrix -> (w, x, y, z)
+    w = np.sqrt(max(0.0, 1.0 + R[0, 0] + R[1, 1] + R[2, 2])) / 2.0
+    if w > 1e-6:
+        q = np.array([w, (R[2, 1] - R[1, 2]) / (4 * w), (R[0, 2] - R[2, 0]) / (4 * w), (R[1, 0] - R[0, 1]) / (4 * w)])
+    else:
+        i = int(np.argmax(np.diag(R)))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = np.sqrt(1.0 + R[i, i] - R[j, j] - R[k, k]) * 2.0
+        q = np.zeros(4)
+        q[0] = (R[k, j] - R[j, k]) / s
+        q[1 + i] = 0.25 * s
+        q[1 + j] = (R[j, i] + R[i, j]) / s
+        q[1 + k] = (R[k, i] + R[i, k]) / s
+    return q / np.linalg.norm(q), t
+
+
+def gsba_scene(num_images=10, num_cylinders=5, height=240, width=320, seed=0, points=0):
+    """Synthetic GSBA workload: SIMPLE_PINHOLE cameras (constant) on a circle
+    looking at vertical cylinders (tree trunks) around the origin; returns the
+    scene (poses = ground truth) and the ground-truth cylinders [N][9]."""
+    rng = np.random.default_rng(seed)
+    f, cx, cy = 0.8 * width, width / 2.0, height / 2.0
+    cams = np.tile([f, cx, cy], (num_images, 1))
+    q = np.zeros((num_images, 4))
+    t = np.zeros((num_images, 3))
+    for i in range(num_images):
+        a = 2 * np.pi * i / num_images + rng.uniform(-0.1, 0.1)
+        centre = [9.0 * np.cos(a), 9.0 * np.sin(a), 1.5 + rng.uniform(-0.2, 0.2)]
+        q[i], t[i] = look_at_qvec(centre, [rng.uniform(-0.5, 0.5), rng.uniform(-0.5, 0.5), 2.0])
+    cyl = np.zeros((num_cylinders, 9))
+    for c in range(num_cylinders):
+        a = 2 * np.pi * c / num_cylinders
+        cyl[c, :4] = [1, 0, 0, 0]
+        cyl[c, 4:7] = [2.2 * np.cos(a), 2.2 * np.sin(a), 0.0]
+        cyl[c, 7] = rng.uniform(0.2, 0.4)
+        cyl[c, 8] = rng.uniform(3.0, 4.5)
+    X = rng.uniform(-3, 3, (points, 3)) + [0, 0, 2.0] if points else np.zeros((0, 3))
+    xy, oi, op = [], [], []
+    for p in range(points):
+        for i in range(num_images):
+            R = quat_to_rot(q[i])
+            pc = R @ X[p] + t[i]
+            if pc[2] <= 0.1:
+                continue
+            u, v = f * pc[0] / pc[2] + cx, f * pc[1] / pc[2] + cy
+            if 0 <= u < width and 0 <= v < height:
+                xy.append([u + rng.uniform(-1, 1), v + rng.uniform(-1, 1)])
+                oi.append(i)
+                op.append(p)
+    sc = Scene(SIMPLE_PINHOLE, cams, q, t, np.arange(num_images, dtype=np.int32), np.asarray(X, float).reshape(-1, 3),
+               np.asarray(xy, float).reshape(-1, 2), np.asarray(oi, np.int32), np.asarray(op, np.int32))
+    sc.camera_constant = np.ones(num_images, np.uint8)
+    return sc, cyl
+
+
+def quat_to_rot(q):
+    w, x, y, z = np.asarray(q, float) / np.linalg.norm(q)
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
 
 
 class Arena:
