@@ -10,11 +10,15 @@
 //       controllers/bundle_adjustment.cc:69-101): read, every registered image
 //       in the config, pose of the first constant, tvec x of the second
 //       constant, Solve on the GPU, write binary
+//   model_io_test gsba <model dir> <data dir> <cylinders in> <cylinders out> [iters]
+//       GeometricSemanticBundleAdjuster: every registered image, first pose
+//       constant, cameras constant, maps from <data dir>, cylinders file I/O
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
 #include <string>
 
+#include "colmap_amd/geometric_semantic_bundle_adjustment.h"
 #include "colmap_amd/model_io.h"
 #include "colmap_amd/tiff.h"
 
@@ -120,6 +124,27 @@ int main(int argc, char** argv) {
       WriteModelBinary(argv[3], r);
       std::printf("%.17g %.17g %d %d\n", ba.Summary().initial_cost, ba.Summary().final_cost,
                   ba.Summary().num_successful_steps, ba.Summary().num_unsuccessful_steps);
+    } else if (mode == "gsba" && argc >= 6) {
+      Reconstruction r;
+      ReadModel(argv[2], &r);
+      BundleAdjustmentConfig cfg;
+      bool first = true;
+      for (const auto& e : r.images) {
+        cfg.AddImage(e.first);
+        if (first) cfg.SetConstantPose(e.first);
+        first = false;
+      }
+      for (const auto& c : r.cameras) cfg.SetConstantCamera(c.first);
+      GeometricSemanticBundleAdjustmentOptions o;
+      o.print_summary = false;
+      o.data_path = argv[3];
+      o.input_geometry = argv[4];
+      if (argc >= 7) o.solver_options.max_num_iterations = std::atoi(argv[6]);
+      GeometricSemanticBundleAdjuster gsba(o, cfg);
+      if (!gsba.Solve(&r)) return 4;
+      WriteCylindersText(argv[5], gsba.Cylinders());
+      std::printf("%.17g %.17g %d %d\n", gsba.Summary().initial_cost, gsba.Summary().final_cost,
+                  gsba.Summary().num_successful_steps, gsba.Summary().num_unsuccessful_steps);
     } else {
       return 2;
     }

@@ -122,3 +122,44 @@ def test_gsba_solve_parity(gpu, case):
     assert abs(s_g.final_cost - s_o.final_cost) <= 1e-6 * s_o.final_cost
     assert np.abs(b.cylinders - a.cylinders).max() <= 1e-6
     assert s_g.final_cost < s_g.initial_cost
+
+
+@pytest.mark.gpu
+def test_gsba_facade_workflow_from_files(gpu, tmp_path):
+    """The GeometricSemanticBundleAdjuster workflow through the C++ facade
+    (colmap_amd/geometric_semantic_bundle_adjustment.h): COLMAP text model,
+    depth_tiff / semantic_tiff float32 maps (trunk class 250), cylinder text
+    file in and out; same result as mi_ba.gsba_solve on the arrays."""
+    import os
+    import subprocess
+    from PIL import Image
+    from test_model_io import write_text_model
+    sc, g, _ = workload(seed=6)
+    sc.image_constant_tvec = None  # the workflow fixes the first pose only
+    write_text_model(sc, str(tmp_path / "model"))
+    (tmp_path / "data" / "depth_tiff").mkdir(parents=True)
+    (tmp_path / "data" / "semantic_tiff").mkdir()
+    for i in range(sc.num_images):
+        Image.fromarray(np.full((H, W), 5.0, np.float32), mode="F").save(
+            tmp_path / "data" / "depth_tiff" / ("img%d_depth.tiff" % i))
+        Image.fromarray(np.where(g.masks[i] > 0, 250.0, 3.0).astype(np.float32), mode="F").save(
+            tmp_path / "data" / "semantic_tiff" / ("img%d_semantic.tiff" % i), compression="tiff_lzw")
+    with open(tmp_path / "cyl.txt", "w") as f:
+        for c in g.cylinders:
+            f.write("q %r %r %r %r t %r %r %r r %r h %r\n" % tuple(float(v) for v in c))
+    exe = os.path.join(os.path.dirname(__file__), "cpp", "model_io_test")
+    subprocess.run(["make", "-s", "-C", os.path.dirname(exe), "model_io_test"], check=True)
+    r = subprocess.run([exe, "gsba", str(tmp_path / "model"), str(tmp_path / "data"), str(tmp_path / "cyl.txt"),
+                        str(tmp_path / "out.txt"), "8"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    c0, c1, ns, nu = r.stdout.split()
+    ref = g.copy()
+    s = mi_ba.gsba_solve(mi_ba.default_options(max_num_iterations=8), sc.copy(), ref)
+    assert abs(float(c0) - s.initial_cost) <= 1e-12 * s.initial_cost
+    assert abs(float(c1) - s.final_cost) <= 1e-6 * s.final_cost
+    assert (int(ns), int(nu)) == (s.num_successful_steps, s.num_unsuccessful_steps)
+    out = []
+    for line in open(tmp_path / "out.txt"):
+        t = line.split()
+        out.append([float(v) for v in t[1:5] + t[6:9] + [t[10], t[12]]])
+    assert np.abs(np.array(out) - ref.cylinders).max() <= 1e-6
