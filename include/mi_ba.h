@@ -387,7 +387,8 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *                           30-35 occupancy study (tools/ab_jacobian.py)
  *   "cholesky_panel"        0 recursive split, 64..4096 right-looking panel width
  *   "cholesky_gemm_update"  0 dsyrk / 1 dgemm trailing update
- *   "cholesky_own_diag"     1 hand-written diagonal-block factor (default) / 0 rocsolver_dpotrf
+ *   "cholesky_own_diag"     1 hand-written diagonal-block factor (one column per step), 2 the
+ *                           same blocked by 4 (3: by 8) columns per step, 0 rocsolver_dpotrf
  *   "cholesky_lookahead"    1 side-stream look-ahead (default) / 0 serial
  *   "cholesky_solve"        1 hand-written blocked triangular sweeps (default) /
  *                           0 recursive rocBLAS dtrsv + dgemv */

@@ -95,6 +95,126 @@ __global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_kernel(double* __
   }
 }
 
+// As diag_panel_kernel, blocked by kStep columns: per step the kStep x kStep
+// diagonal block is factored redundantly by every lane (registers), each lane
+// forms its row's kStep new entries, and the trailing columns take one
+// rank-kStep update — two barriers per kStep columns instead of two per
+// column.  The sub-panel solve (x L' = a) steps the same way: each lane forms
+// its row's kStep unknowns from the diagonal block, one barrier per step.
+template <int kStep>
+__global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_blocked_kernel(double* __restrict__ A, int lda, int w,
+                                                                 int mrows, int* __restrict__ info,
+                                                                 double* __restrict__ scratch, int koff) {
+  __shared__ double L[kSub * kSub], P[kSub * kSub], nb[kStep * kSub];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const double* tile_row = A + std::min(lane, w - 1);
+#pragma unroll
+  for (int c = wv; c < kSub; c += kPanelWaves) {
+    const double v = tile_row[(size_t)std::min(c, w - 1) * lda];
+    L[c * kSub + lane] = (lane < w && c < w) ? (lane >= c ? v : 0.0) : (lane == c ? 1.0 : 0.0);
+  }
+  const int r = (blockIdx.x - 1) * kSub + lane;
+  const bool solve = blockIdx.x > 0 && r < mrows;
+  double* row = A + w + r;
+  if (blockIdx.x > 0) {
+    const double* src = A + w + std::min(r, mrows - 1);
+#pragma unroll
+    for (int c = wv; c < kSub; c += kPanelWaves) {
+      const double v = src[(size_t)std::min(c, w - 1) * lda];
+      P[c * kSub + lane] = (solve && c < w) ? v : 0.0;
+    }
+  }
+  __syncthreads();
+  int bad = 0;
+  for (int jb = 0; jb < kSub; jb += kStep) {
+    // kStep x kStep diagonal block (lower), factored in registers by every lane
+    double d[kStep][kStep];
+#pragma unroll
+    for (int i = 0; i < kStep; ++i)
+#pragma unroll
+      for (int k = 0; k <= i; ++k) d[i][k] = L[(jb + k) * kSub + jb + i];
+#pragma unroll
+    for (int k = 0; k < kStep; ++k) {
+      const double piv = d[k][k];
+      if (!(piv > 0.0) && bad == 0) bad = jb + k + 1;
+      d[k][k] = sqrt(piv);
+#pragma unroll
+      for (int i = k + 1; i < kStep; ++i) d[i][k] /= d[k][k];
+#pragma unroll
+      for (int i = k + 1; i < kStep; ++i)
+#pragma unroll
+        for (int m = k + 1; m <= i; ++m) d[i][m] -= d[i][k] * d[m][k];
+    }
+    // this lane's row of the kStep new columns
+    double y[kStep];
+    if (lane >= jb + kStep) {
+#pragma unroll
+      for (int k = 0; k < kStep; ++k) {
+        double v = L[(jb + k) * kSub + lane];
+#pragma unroll
+        for (int m = 0; m < k; ++m) v -= y[m] * d[k][m];
+        y[k] = v / d[k][k];
+      }
+    } else {
+      const int i = lane - jb;
+#pragma unroll
+      for (int k = 0; k < kStep; ++k) {
+        double v = 0.0;
+#pragma unroll
+        for (int ii = k; ii < kStep; ++ii) v = (i == ii) ? d[ii][k] : v;
+        y[k] = v;
+      }
+    }
+    if (wv == 0) {
+#pragma unroll
+      for (int k = 0; k < kStep; ++k) nb[k * kSub + lane] = y[k];
+    }
+    __syncthreads();
+    // every wave has read the block's old columns: store them final, and the
+    // trailing columns take the rank-kStep update
+    if (wv == 0) {
+#pragma unroll
+      for (int k = 0; k < kStep; ++k)
+        if (lane >= jb + k) L[(jb + k) * kSub + lane] = y[k];
+    }
+    for (int c = jb + kStep + wv; c < kSub; c += kPanelWaves) {
+      double v = L[c * kSub + lane];
+#pragma unroll
+      for (int k = 0; k < kStep; ++k) v -= y[k] * nb[k * kSub + c];
+      L[c * kSub + lane] = v;
+    }
+    __syncthreads();
+  }
+  if (blockIdx.x == 0) {
+#pragma unroll
+    for (int c = wv; c < kSub; c += kPanelWaves) scratch[c * kSub + lane] = L[c * kSub + lane];
+    if (threadIdx.x == 0 && bad != 0 && bad <= w && info[0] == 0) info[0] = koff + bad;
+    return;
+  }
+  // x L' = a, kStep unknowns per step: the lane's row from the diagonal block
+  // (broadcast reads), then the trailing columns of the row (waves by column)
+  for (int cb = 0; cb < kSub; cb += kStep) {
+    double x[kStep];
+#pragma unroll
+    for (int k = 0; k < kStep; ++k) {
+      double v = P[(cb + k) * kSub + lane];
+#pragma unroll
+      for (int m = 0; m < k; ++m) v -= x[m] * L[(cb + m) * kSub + cb + k];
+      x[k] = v / L[(cb + k) * kSub + cb + k];
+    }
+#pragma unroll
+    for (int k = 0; k < kStep; ++k)
+      if (solve && cb + k < w && (cb + k) % kPanelWaves == wv) row[(size_t)(cb + k) * lda] = x[k];
+    for (int t = cb + kStep + wv; t < kSub; t += kPanelWaves) {
+      double v = P[t * kSub + lane];
+#pragma unroll
+      for (int k = 0; k < kStep; ++k) v -= x[k] * L[(cb + k) * kSub + t];
+      P[t * kSub + lane] = v;
+    }
+    __syncthreads();
+  }
+}
+
 // A22 (m x m, lower) -= P P', P = the m x w sub-panel left of A22 (column-
 // major, P[r + t*lda] = A22[r - w*lda ...]); tile (bi >= bj) per workgroup.
 // The workgroup after the last tile copies the factored w x w diagonal tile
@@ -267,7 +387,7 @@ __global__ __launch_bounds__(kTB) void trsv_bwd_step_kernel(const double* __rest
   }
 }
 
-rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info, double* scratch) {
+rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info, double* scratch, int variant) {
   hipStream_t s;
   if (!scratch) return rocblas_status_invalid_pointer;
   if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
@@ -276,8 +396,15 @@ rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info
     const int w = std::min(kSub, n - k);
     const int m = n - k - w;  // rows (and columns) of the block after this sub-panel
     double* Akk = A + k + (size_t)k * lda;
-    hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s, Akk, lda, w,
-                       m, info, scratch, k);
+    if (variant == 2)
+      hipLaunchKernelGGL(diag_panel_blocked_kernel<4>, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s,
+                         Akk, lda, w, m, info, scratch, k);
+    else if (variant == 3)
+      hipLaunchKernelGGL(diag_panel_blocked_kernel<8>, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s,
+                         Akk, lda, w, m, info, scratch, k);
+    else
+      hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s, Akk, lda,
+                         w, m, info, scratch, k);
     // trailing tiles of the block + one workgroup writing the tile back
     const int T = (m + kSub - 1) / kSub;
     hipLaunchKernelGGL(diag_update_kernel, dim3(T * (T + 1) / 2 + 1), dim3(256), 0, s, Akk + w + (size_t)w * lda,
@@ -287,7 +414,7 @@ rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info
 }
 
 rocblas_status potrf_leaf(rocblas_handle h, int n, double* A, int lda, int* info, int own, double* scratch) {
-  if (own) return potrf_diag(h, n, A, lda, info, scratch);
+  if (own) return potrf_diag(h, n, A, lda, info, scratch, own);
   return rocsolver_dpotrf(h, rocblas_fill_lower, n, A, lda, info);
 }
 

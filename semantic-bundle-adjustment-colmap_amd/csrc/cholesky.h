@@ -28,12 +28,15 @@ struct CholConfig {
   // panel k+1's diagonal factor + dtrsm on the workspace's side stream under
   // panel k's dgemm (34.6 -> 30.4 ms at nf = 12 000)
   bool lookahead = true;
-  // diagonal blocks: 1 hand-written 64-wide sub-panels (eight-wave LDS tile
-  // factor, diag_panel_kernel), 0 rocsolver_dpotrf.  (Measured dead ends,
-  // a four-wave register-resident tile factor with one barrier
-  // per pivot ran 80 us per sub-panel vs 69; a fully unrolled one-wave
-  // register factor ~300 us, instruction-fetch bound.)
-  int own_diag = 1;
+  // diagonal blocks: hand-written 64-wide sub-panels (eight-wave LDS tile
+  // factor + sub-panel solve), 2 blocked by 4 columns per step
+  // (diag_panel_blocked_kernel<4>: two barriers per 4 columns; Cholesky 30.7 ->
+  // 25.5 ms at nf = 12 000), 3 blocked by 8 (26.7 ms), 1 one column per step
+  // (diag_panel_kernel), 0 rocsolver_dpotrf.  (Measured dead ends, DESIGN.md:
+  // a four-wave register-resident tile factor with one barrier per pivot ran
+  // 80 us per sub-panel vs 69; a fully unrolled one-wave register factor
+  // ~300 us, instruction-fetch bound.)
+  int own_diag = 2;
   int solve = 1;          // chol_solve variant: 1 blocked sweeps, 0 recursive rocBLAS dtrsv / dgemv
 };
 

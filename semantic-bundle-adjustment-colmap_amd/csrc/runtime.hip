@@ -1326,7 +1326,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.lookahead = value != 0;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_own_diag") == 0 && (value == 0 || value == 1)) {
+  if (std::strcmp(key, "cholesky_own_diag") == 0 && value >= 0 && value <= 3) {
     ctx->chol.own_diag = value;
     return MI_BA_OK;
   }
@@ -1344,7 +1344,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
 mi_ba_status mi_ba_dense_cholesky(int32_t device, int32_t n, double* A, double* b, int32_t panel, int32_t lookahead,
                                   int32_t own_diag, int32_t* info) {
   if (n < 0 || !A || !info || (panel != 0 && (panel < 64 || panel > 4096)) || (lookahead != 0 && lookahead != 1) ||
-      (own_diag != 0 && own_diag != 1))
+      (own_diag < 0 || own_diag > 3))
     return MI_BA_ERR_INVALID_ARGUMENT;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MI_BA_ERR_NO_DEVICE;

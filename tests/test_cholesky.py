@@ -54,7 +54,7 @@ def test_factor_matches_oracle_and_lapack(gpu, n):
     L_np = np.linalg.cholesky(A)
     x_ref = np.linalg.solve(A, b)
     scale = np.abs(L_o).max()
-    for own in (1, 0):
+    for own in (2, 1, 0):
         for panel in (512, 0):
             L, x, info = mi_ba.dense_cholesky(A, b, panel=panel, own_diag=own)
             assert info == 0
@@ -70,7 +70,7 @@ def test_not_positive_definite_reports_column(gpu, col):
     A[col, col] = -1.0
     _, info_o = oracle.cholesky(A)
     assert info_o == col + 1
-    for own in (1, 0):
+    for own in (2, 1, 0):
         for la in (0, 1):
             _, _, info = mi_ba.dense_cholesky(A, panel=512, lookahead=la, own_diag=own)
             assert info == col + 1, (own, la, info)

@@ -9,7 +9,9 @@ sc = mi_ba.generate_scene(c).gauge()
 w = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.OPENCV, 30, 300, track_length=5, rotation_range=0.05, extra=(-0.1, 0.01, 1e-4, -1e-4))).gauge()
 with mi_ba.Context(mi_ba.default_options(max_num_iterations=2), w) as x: x.solve()
 import os
-variants = [dict(own=1, la=1, panel=512, solve=1), dict(own=0, la=1, panel=512, solve=1),
+variants = [dict(own=1, la=1, panel=512, solve=1), dict(own=2, la=1, panel=512, solve=1),
+            dict(own=2, la=1, panel=1024, solve=1), dict(own=3, la=1, panel=512, solve=1),
+            dict(own=0, la=1, panel=512, solve=1),
             dict(own=1, la=0, panel=512, solve=1), dict(own=1, la=1, panel=1024, solve=1),
             dict(own=1, la=1, panel=256, solve=1)]
 if len(sys.argv) > 1:
