@@ -101,15 +101,15 @@ __global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_kernel(double* __
 // rank-kStep update — two barriers per kStep columns instead of two per
 // column.  The sub-panel solve (x L' = a) steps the same way: each lane forms
 // its row's kStep unknowns from the diagonal block, one barrier per step.
-template <int kStep>
-__global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_blocked_kernel(double* __restrict__ A, int lda, int w,
+template <int kStep, int NW = kPanelWaves>
+__global__ __launch_bounds__(64 * NW) void diag_panel_blocked_kernel(double* __restrict__ A, int lda, int w,
                                                                  int mrows, int* __restrict__ info,
                                                                  double* __restrict__ scratch, int koff) {
   __shared__ double L[kSub * kSub], P[kSub * kSub], nb[kStep * kSub];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const double* tile_row = A + std::min(lane, w - 1);
 #pragma unroll
-  for (int c = wv; c < kSub; c += kPanelWaves) {
+  for (int c = wv; c < kSub; c += NW) {
     const double v = tile_row[(size_t)std::min(c, w - 1) * lda];
     L[c * kSub + lane] = (lane < w && c < w) ? (lane >= c ? v : 0.0) : (lane == c ? 1.0 : 0.0);
   }
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_blocked_kernel(do
   if (blockIdx.x > 0) {
     const double* src = A + w + std::min(r, mrows - 1);
 #pragma unroll
-    for (int c = wv; c < kSub; c += kPanelWaves) {
+    for (int c = wv; c < kSub; c += NW) {
       const double v = src[(size_t)std::min(c, w - 1) * lda];
       P[c * kSub + lane] = (solve && c < w) ? v : 0.0;
     }
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_blocked_kernel(do
       for (int k = 0; k < kStep; ++k)
         if (lane >= jb + k) L[(jb + k) * kSub + lane] = y[k];
     }
-    for (int c = jb + kStep + wv; c < kSub; c += kPanelWaves) {
+    for (int c = jb + kStep + wv; c < kSub; c += NW) {
       double v = L[c * kSub + lane];
 #pragma unroll
       for (int k = 0; k < kStep; ++k) v -= y[k] * nb[k * kSub + c];
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_blocked_kernel(do
   }
   if (blockIdx.x == 0) {
 #pragma unroll
-    for (int c = wv; c < kSub; c += kPanelWaves) scratch[c * kSub + lane] = L[c * kSub + lane];
+    for (int c = wv; c < kSub; c += NW) scratch[c * kSub + lane] = L[c * kSub + lane];
     if (threadIdx.x == 0 && bad != 0 && bad <= w && info[0] == 0) info[0] = koff + bad;
     return;
   }
@@ -204,8 +204,8 @@ __global__ __launch_bounds__(64 * kPanelWaves) void diag_panel_blocked_kernel(do
     }
 #pragma unroll
     for (int k = 0; k < kStep; ++k)
-      if (solve && cb + k < w && (cb + k) % kPanelWaves == wv) row[(size_t)(cb + k) * lda] = x[k];
-    for (int t = cb + kStep + wv; t < kSub; t += kPanelWaves) {
+      if (solve && cb + k < w && (cb + k) % NW == wv) row[(size_t)(cb + k) * lda] = x[k];
+    for (int t = cb + kStep + wv; t < kSub; t += NW) {
       double v = P[t * kSub + lane];
 #pragma unroll
       for (int k = 0; k < kStep; ++k) v -= x[k] * L[(cb + k) * kSub + t];
@@ -402,6 +402,12 @@ rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info
     else if (variant == 3)
       hipLaunchKernelGGL(diag_panel_blocked_kernel<8>, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s,
                          Akk, lda, w, m, info, scratch, k);
+    else if (variant == 4)
+      hipLaunchKernelGGL((diag_panel_blocked_kernel<4, 4>), dim3(1 + (m + kSub - 1) / kSub), dim3(64 * 4), 0, s, Akk,
+                         lda, w, m, info, scratch, k);
+    else if (variant == 5)
+      hipLaunchKernelGGL((diag_panel_blocked_kernel<4, 2>), dim3(1 + (m + kSub - 1) / kSub), dim3(64 * 2), 0, s, Akk,
+                         lda, w, m, info, scratch, k);
     else
       hipLaunchKernelGGL(diag_panel_kernel, dim3(1 + (m + kSub - 1) / kSub), dim3(64 * kPanelWaves), 0, s, Akk, lda,
                          w, m, info, scratch, k);

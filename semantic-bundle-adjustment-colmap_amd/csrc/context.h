@@ -96,6 +96,7 @@ struct mi_ba_context {
   miba::DevArray<double> scale_f, diag_f, lambda_f, prec_pose, prec_cam;
   miba::DevArray<double> cg_x, cg_r, cg_z, cg_p, cg_q, cg_w, dX;
   miba::DevArray<double> scalars;          // device scalars
+  miba::DevArray<double> red;              // per-workgroup partials of the multi-workgroup reductions
   double* host_scalars = nullptr;          // pinned
 
   // explicit reduced camera system (exact Schur solve, rocSOLVER Cholesky)

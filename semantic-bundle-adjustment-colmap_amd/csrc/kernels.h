@@ -95,6 +95,10 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
 void launch_dense_finalize(const DevProblem& p, const double* lambda_f, double* S, hipStream_t s);
 
 // Squared norms of df and dX (for the parameter tolerance test).
-void launch_sqnorm2(const double* a, int64_t na, const double* b, int64_t nb, double* out, hipStream_t s);
+// |a|^2 + |b|^2 into out[0]; scratch (kReduceBlocks doubles, or null for a
+// one-workgroup reduction) holds per-workgroup partials
+constexpr int kReduceBlocks = 256;
+void launch_sqnorm2(const double* a, int64_t na, const double* b, int64_t nb, double* out, double* scratch,
+                    hipStream_t s);
 
 }  // namespace miba

@@ -439,7 +439,7 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
       ctx->lambda_f.alloc(nf) || ctx->prec_pose.alloc(36 * (size_t)I) ||
       ctx->prec_cam.alloc((size_t)s.ct * s.ct * C + 1) || ctx->cg_x.alloc(nf) || ctx->cg_r.alloc(nf) ||
       ctx->cg_z.alloc(nf) || ctx->cg_p.alloc(nf) || ctx->cg_q.alloc(nf) || ctx->cg_w.alloc(3 * P) ||
-      ctx->dX.alloc(3 * P) || ctx->scalars.alloc(kNumScalars))
+      ctx->dX.alloc(3 * P) || ctx->scalars.alloc(kNumScalars) || ctx->red.alloc(kReduceBlocks))
     return fail(MI_BA_ERR_OUT_OF_MEMORY);
   if (!ctx->host_scalars &&
       hipHostMalloc(&ctx->host_scalars, sizeof(double) * kNumScalars, hipHostMallocDefault) != hipSuccess) {
@@ -797,7 +797,8 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     if (ctx->sem) semantic_model_cost(ctx, ctx->cg_x.ptr, sc + kSemModel);
     if (ctx->gsba) gsba_model_cost(ctx, ctx->cg_x.ptr, sc + kGsModel);
     // camera step counted once (rank 0), point steps on their own ranks
-    launch_sqnorm2(ctx->cg_x.ptr, ctx->rank == 0 ? nf : 0, ctx->dX.ptr, 3 * d.num_points, sc + kStepNorm, s);
+    launch_sqnorm2(ctx->cg_x.ptr, ctx->rank == 0 ? nf : 0, ctx->dX.ptr, 3 * d.num_points, sc + kStepNorm,
+                   ctx->red.ptr, s);
     if (ctx->world > 1) {
       st = allreduce(ctx, sc + kModelCost, 1);
       if (st == MI_BA_OK) st = allreduce(ctx, sc + kSemModel, 1);
@@ -851,7 +852,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     double x_norm = 0.0;
     if (o.parameter_tolerance > 0.0) {
       launch_sqnorm2(ctx->qt.ptr, ctx->rank == 0 ? 8 * (int64_t)d.num_images : 0, ctx->X.ptr, 3 * d.num_points,
-                     sc + kStepNorm, s);
+                     sc + kStepNorm, ctx->red.ptr, s);
       st = allreduce(ctx, sc + kStepNorm, 1);
       if (st != MI_BA_OK) return st;
       st = read_scalars(ctx, kStepNorm, 1);
@@ -1326,7 +1327,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.lookahead = value != 0;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_own_diag") == 0 && value >= 0 && value <= 3) {
+  if (std::strcmp(key, "cholesky_own_diag") == 0 && value >= 0 && value <= 5) {
     ctx->chol.own_diag = value;
     return MI_BA_OK;
   }
@@ -1344,7 +1345,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
 mi_ba_status mi_ba_dense_cholesky(int32_t device, int32_t n, double* A, double* b, int32_t panel, int32_t lookahead,
                                   int32_t own_diag, int32_t* info) {
   if (n < 0 || !A || !info || (panel != 0 && (panel < 64 || panel > 4096)) || (lookahead != 0 && lookahead != 1) ||
-      (own_diag < 0 || own_diag > 3))
+      (own_diag < 0 || own_diag > 5))
     return MI_BA_ERR_INVALID_ARGUMENT;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MI_BA_ERR_NO_DEVICE;

@@ -11,7 +11,8 @@ with mi_ba.Context(mi_ba.default_options(max_num_iterations=2), w) as x: x.solve
 import os
 variants = [dict(own=1, la=1, panel=512, solve=1), dict(own=2, la=1, panel=512, solve=1),
             dict(own=2, la=1, panel=1024, solve=1), dict(own=3, la=1, panel=512, solve=1),
-            dict(own=0, la=1, panel=512, solve=1),
+            dict(own=0, la=1, panel=512, solve=1), dict(own=4, la=1, panel=512, solve=1),
+            dict(own=5, la=1, panel=512, solve=1),
             dict(own=1, la=0, panel=512, solve=1), dict(own=1, la=1, panel=1024, solve=1),
             dict(own=1, la=1, panel=256, solve=1)]
 if len(sys.argv) > 1:
