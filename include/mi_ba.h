@@ -390,7 +390,8 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *   "cholesky_own_diag"     1 hand-written diagonal-block factor (one column per step), 2 the
  *                           same blocked by 4 (3: by 8) columns per step, 0 rocsolver_dpotrf
  *   "cholesky_lookahead"    1 side-stream look-ahead (default) / 0 serial
- *   "cholesky_solve"        1 hand-written blocked triangular sweeps (default) /
+ *   "cholesky_solve"        2 sync-free triangular sweeps, one launch per direction
+ *                           (default) / 1 hand-written blocked triangular sweeps /
  *                           0 recursive rocBLAS dtrsv + dgemv */
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value);
 
@@ -409,6 +410,11 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
  * several host threads share nothing. */
 mi_ba_status mi_ba_dense_cholesky(int32_t device, int32_t n, double* A, double* b, int32_t panel, int32_t lookahead,
                                   int32_t own_diag, int32_t* info);
+/* As mi_ba_dense_cholesky with the triangular-solve variant of the
+ * "cholesky_solve" tuning key (2 sync-free sweeps = the default of
+ * mi_ba_dense_cholesky, 1 per-block-column sweeps, 0 rocBLAS dtrsv/dgemv). */
+mi_ba_status mi_ba_dense_cholesky_ex(int32_t device, int32_t n, double* A, double* b, int32_t panel,
+                                     int32_t lookahead, int32_t own_diag, int32_t solve, int32_t* info);
 
 /* Per-kernel HIP-event timing on the context's stream (enabled with
  * mi_ba_set_timing).  name: "reproj_jacobian", "semantic_jacobian", ... */

@@ -387,6 +387,130 @@ __global__ __launch_bounds__(kTB) void trsv_bwd_step_kernel(const double* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// Sync-free triangular sweeps (chol_solve variant 2): ONE launch per
+// direction instead of one per 64-wide block column.  Workgroup t takes row
+// block ib (forward: ib = t, backward: ib = nblk-1-t; t from an atomic
+// ticket, so a block's producers always started before it and the spin-waits
+// below cannot deadlock whatever the dispatch order).  Its waves stream the
+// blocks it depends on round-robin — each wave first loads its 64x64 block of
+// L into registers, then waits for that block's solution flag, then folds the
+// block in — so L is read once per direction, off the critical path.  Wave 0
+// then solves the diagonal block by a 64-step register sweep (pivots as
+// precomputed reciprocals, the solved entry broadcast with readlane), writes
+// the block's solution in place, and publishes it (release fence, flag =
+// epoch).  The critical path per block is one flag hand-off + one 64x64
+// register solve, with no kernel boundary and no diagonal-block inverses.
+//   forward  L y = b: lane = row of the block, dependency blocks L[ib][jb < ib]
+//   backward L'x = y: lane = column of the block, dependency blocks L[jb > ib][ib]
+// ctrl = {forward ticket, backward ticket, flag[nblk]}.
+constexpr int kSweepWaves = 4;
+typedef double sweep_dvec2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+template <bool FWD>
+__global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const double* __restrict__ L, int lda, int n,
+                                                                      double* x, unsigned* ctrl, unsigned epoch) {
+  __shared__ int s_blk;
+  __shared__ double part[kSweepWaves][kTB];
+  __shared__ double xs[kSweepWaves][kTB];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nblk = (n + kTB - 1) / kTB;
+  if (threadIdx.x == 0) s_blk = (int)atomicAdd(ctrl + (FWD ? 0 : 1), 1u);
+  __syncthreads();
+  const int t = s_blk;
+  const int ib = FWD ? t : nblk - 1 - t;
+  const int r0 = ib * kTB, w = min(kTB, n - r0);
+  unsigned* flag = ctrl + 2;
+  const int me = r0 + min(lane, w - 1);  // the lane's row (forward) / column (backward), clamped
+  // wave 0: the diagonal block, the pivot reciprocal and the right-hand side
+  // are loaded before any waiting (nothing else writes them)
+  double u[kTB];
+  double dinv = 0.0, z = 0.0;
+  if (wv == 0) {
+    if (FWD) {
+      const double* src = L + me + (size_t)r0 * lda;
+#pragma unroll
+      for (int c = 0; c < kTB; ++c) u[c] = src[(size_t)min(c, w - 1) * lda];
+    } else {
+      const double* src = L + r0 + (size_t)me * lda;
+#pragma unroll
+      for (int r = 0; r < kTB; ++r) u[r] = src[min(r, w - 1)];
+    }
+    dinv = 1.0 / L[(size_t)me * (lda + 1)];
+    z = lane < w ? x[r0 + lane] : 0.0;
+  }
+  double acc = 0.0;
+  const int ndep = FWD ? ib : nblk - 1 - ib;
+  for (int q = wv; q < ndep; q += kSweepWaves) {
+    const int jb = FWD ? q : nblk - 1 - q;
+    const int c0 = jb * kTB, wj = min(kTB, n - c0);
+    double v[kTB];
+    if (FWD) {
+      // row me, columns c0 .. c0+63 (a block left of ib is full width)
+      const double* src = L + me + (size_t)c0 * lda;
+#pragma unroll
+      for (int c = 0; c < kTB; ++c) v[c] = __builtin_nontemporal_load(src + (size_t)c * lda);
+    } else {
+      // column me, rows c0 .. c0+wj-1 (contiguous)
+      const double* src = L + c0 + (size_t)me * lda;
+      if (wj == kTB && ((c0 | lda) & 1) == 0) {
+        const sweep_dvec2* s2 = reinterpret_cast<const sweep_dvec2*>(src);
+#pragma unroll
+        for (int r = 0; r < kTB / 2; ++r) {
+          const sweep_dvec2 p = __builtin_nontemporal_load(s2 + r);
+          v[2 * r] = p.x;
+          v[2 * r + 1] = p.y;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < kTB; ++r) v[r] = src[min(r, wj - 1)];
+      }
+    }
+    while (__hip_atomic_load(flag + jb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch)
+      __builtin_amdgcn_s_sleep(1);
+    xs[wv][lane] = lane < wj ? x[c0 + lane] : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+    for (int c = 0; c < kTB; ++c) acc += v[c] * xs[wv][c];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  part[wv][lane] = acc;
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int k = 0; k < kSweepWaves; ++k) z -= part[k][lane];
+  if (lane >= w) z = 0.0;
+  // straight-line: past a ragged block's width z is 0 and u, dinv are finite
+  // (clamped loads), so those steps leave every live lane unchanged
+  if (FWD) {
+#pragma unroll
+    for (int c = 0; c < kTB; ++c) {
+      const double xc = readlane_f64(z, c) * readlane_f64(dinv, c);
+      const double zu = z - u[c] * xc;
+      z = lane == c ? xc : (lane > c ? zu : z);
+    }
+  } else {
+#pragma unroll
+    for (int r = kTB - 1; r >= 0; --r) {
+      const double xr = readlane_f64(z, r) * readlane_f64(dinv, r);
+      const double zu = z - u[r] * xr;
+      z = lane == r ? xr : (lane < r ? zu : z);
+    }
+  }
+  if (lane < w) x[r0 + lane] = z;
+  __threadfence();
+  if (lane == 0) __hip_atomic_store(flag + ib, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info, double* scratch, int variant) {
   hipStream_t s;
   if (!scratch) return rocblas_status_invalid_pointer;
@@ -572,11 +696,25 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     st = panel_factor(ws.side_h, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag, scratch_side);
     if (st != rocblas_status_success) return fail(st);
     if (hipEventRecord(pan, ws.side) != hipSuccess) return fail(rocblas_status_internal_error);
-    for (int j = jb0; j < m; j += nb) {
-      const int jb = std::min(nb, m - j);
-      st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m - j, jb, kb, &minus_one, Aik + j,
-                         lda, Aik + j, lda, &one, T + j + (size_t)j * lda, lda);
+    // the rest of the trailing lower triangle (columns jb0 .. m)
+    const int mr = m - jb0;
+    if (mr > 0 && cfg.rest_update == 1) {
+      st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, mr, kb, &minus_one, Aik + jb0, lda, &one,
+                         T + jb0 + (size_t)jb0 * lda, lda);
       if (st != rocblas_status_success) return fail(st);
+    } else if (mr > 0 && cfg.rest_update == 2) {
+      st = rocblas_dgemmt(h, rocblas_fill_lower, rocblas_operation_none, rocblas_operation_transpose, mr, kb,
+                          &minus_one, Aik + jb0, lda, Aik + jb0, lda, &one, T + jb0 + (size_t)jb0 * lda, lda);
+      if (st != rocblas_status_success) return fail(st);
+    } else {
+      // block columns of width nb (rest_update 0) or 2 nb (3)
+      const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
+      for (int j = jb0; j < m; j += cw) {
+        const int jb = std::min(cw, m - j);
+        st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m - j, jb, kb, &minus_one,
+                           Aik + j, lda, Aik + j, lda, &one, T + j + (size_t)j * lda, lda);
+        if (st != rocblas_status_success) return fail(st);
+      }
     }
     // panel k+1 is read by the next iteration's updates (and by the solve)
     if (hipStreamWaitEvent(s1, pan, 0) != hipSuccess) return fail(rocblas_status_internal_error);
@@ -620,6 +758,9 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
     if (hipMalloc(&linv, sizeof(double) * kTB * kTB * (size_t)nblk) != hipSuccess) { linv = nullptr; return false; }
     if (hipMalloc(&ybuf, sizeof(double) * kTB * (size_t)nblk) != hipSuccess) { ybuf = nullptr; return false; }
     if (hipMemset(linv, 0, sizeof(double) * kTB * kTB * (size_t)nblk) != hipSuccess) return false;
+    if (hipMalloc(&ctrl, sizeof(unsigned) * (2 + (size_t)nblk)) != hipSuccess) { ctrl = nullptr; return false; }
+    if (hipMemset(ctrl, 0, sizeof(unsigned) * (2 + (size_t)nblk)) != hipSuccess) return false;
+    epoch = 0;
     linv_rows = nblk * kTB;
   }
   return true;
@@ -646,6 +787,8 @@ void CholWorkspace::destroy() {
   linv = nullptr;
   if (ybuf) (void)hipFree(ybuf);
   ybuf = nullptr;
+  if (ctrl) (void)hipFree(ctrl);
+  ctrl = nullptr;
   linv_rows = 0;
 }
 
@@ -671,6 +814,22 @@ rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, dou
   if (!ws || !ws->linv || !ws->ybuf || n > ws->linv_rows) return rocblas_status_invalid_pointer;
   hipStream_t s;
   if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
+  if (variant == 2) {
+    if (!ws->ctrl) return rocblas_status_invalid_pointer;
+    // tickets reset; the flags carry the sweep's epoch (no reset needed)
+    if (ws->epoch > 0xfffffff0u) {
+      if (hipMemsetAsync(ws->ctrl, 0, sizeof(unsigned) * (2 + (size_t)ws->linv_rows / kTB), s) != hipSuccess)
+        return rocblas_status_internal_error;
+      ws->epoch = 0;
+    }
+    if (hipMemsetAsync(ws->ctrl, 0, 2 * sizeof(unsigned), s) != hipSuccess) return rocblas_status_internal_error;
+    const unsigned e = ++ws->epoch;
+    const unsigned e2 = ++ws->epoch;
+    const int nblk = (n + kTB - 1) / kTB;
+    hipLaunchKernelGGL(trsv_sweep_kernel<true>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e);
+    hipLaunchKernelGGL(trsv_sweep_kernel<false>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e2);
+    return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
+  }
   // inverses of the diagonal blocks (full blocks in one batched call, the
   // ragged last block on its own)
   const int nfull = n / kTB, tail = n - nfull * kTB;

@@ -25,6 +25,11 @@ namespace miba {
 struct CholConfig {
   int panel = 512;        // 0: recursive split; > 0: right-looking panel width
   bool gemm_update = true;
+  // look-ahead: the trailing update after the next panel's block column,
+  // 0 one dgemm per 512-wide block column, 1 one dsyrk, 2 one dgemmt,
+  // 3 one dgemm per 1024-wide block column (default: 25.7 -> 25.2 ms at nf =
+  // 12 000; dsyrk 38.6 ms, dgemmt 519 ms — profiles/r2_ab_rest_update.jsonl)
+  int rest_update = 3;
   // panel k+1's diagonal factor + dtrsm on the workspace's side stream under
   // panel k's dgemm (34.6 -> 30.4 ms at nf = 12 000)
   bool lookahead = true;
@@ -37,7 +42,10 @@ struct CholConfig {
   // 80 us per sub-panel vs 69; a fully unrolled one-wave register factor
   // ~300 us, instruction-fetch bound.)
   int own_diag = 2;
-  int solve = 1;          // chol_solve variant: 1 blocked sweeps, 0 recursive rocBLAS dtrsv / dgemv
+  // chol_solve variant: 2 sync-free sweeps (one launch per direction), 1 one
+  // launch per 64-wide block column with diagonal-block inverses, 0 recursive
+  // rocBLAS dtrsv / dgemv
+  int solve = 2;
 };
 
 // Device resources of one factorisation owner (one per mi_ba_context, created
@@ -54,6 +62,8 @@ struct CholWorkspace {
   double* scratch = nullptr;  // [2][64*64]: [0] caller's stream, [1] side stream
   double* linv = nullptr;     // [n/64][64*64] inverses of the factor's 64x64 diagonal blocks (chol_solve)
   double* ybuf = nullptr;     // [n] intermediate vector of chol_solve (L y = b)
+  unsigned* ctrl = nullptr;   // [2 + n/64] sync-free sweeps: two tickets + per-block solution flags
+  unsigned epoch = 0;         // last flag value published (two per chol_solve)
   int linv_rows = 0;
 
   // Creates the resources on `device` with events for up to `max_panels`
@@ -76,9 +86,10 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
                            CholWorkspace* ws);
 int chol_leaf_count(int n, const CholConfig& cfg = {});
 // x := (L L')^-1 x with the factor chol_factor left in A, on h's stream.
-// variant 1 (default): the hand-written blocked forward / backward sweeps
-// (one launch per 64-wide block column, diagonal blocks by their inverses in
-// ws); 0: recursive rocBLAS dtrsv + dgemv (ws unused).
+// variant 2 (default): sync-free forward / backward sweeps, one launch each
+// (per-block solution flags in ws); 1: one launch per 64-wide block column,
+// diagonal blocks by their inverses in ws; 0: recursive rocBLAS dtrsv + dgemv
+// (ws unused).
 rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x, int variant,
                           CholWorkspace* ws);
 

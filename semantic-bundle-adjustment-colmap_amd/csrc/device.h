@@ -67,6 +67,7 @@ struct DevProblem {
   double loss_scale;
   int refine_mask;     // bit0 focal, bit1 principal point, bit2 extra params
   int jvariant;        // Jacobian store path (kernels.hip reproj_jacobian_kernel V)
+  int svariant;        // explicit Schur pair kernel (kernels.hip launch_dense_schur)
   // inputs
   const double2* obs_xy;
   const uint32_t* obs_img;

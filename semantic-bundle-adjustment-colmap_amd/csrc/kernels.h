@@ -33,14 +33,22 @@ void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s);
 void launch_point_normal(const DevProblem& p, const DevPoint* vp, int64_t npv, const double2* r, const double* J,
                          double* Vg, hipStream_t s);
 void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg,
-                          double* scale_p, double* diag_p, double* Vinv, double* Linv, int first, int reuse_diag,
-                          double radius, hipStream_t s);
+                          double* scale_p, double* diag_p, double* Vinv, double* Linv, double* q, int first,
+                          int reuse_diag, double radius, hipStream_t s);
+// (q, nullable: q_p = V_p^-1 g_p [P][3] for launch_fblock_dense)
 
 // Camera-side tile pass: per image/camera tangent block S_ii = U_ii - sum W V^-1 W',
 // b = g - sum W V^-1 g_p and diag(U) (undamped column norms).
 void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
                    const double2* r, const double* J, const double* Vg, const double* Vinv,
                    double* pose_blk, double* cam_blk, double* b, double* udiag, hipStream_t s);
+
+// Exact-solver variant of launch_fblock: U = sum J_f'J_f added into S's image
+// blocks, b = g - sum W V^-1 g_p and diag(U), in one pass (no Schur-Jacobi
+// blocks, which only the PCG preconditioner uses).
+void launch_fblock_dense(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
+                         const double2* r, const double* J, const double* q, double* b, double* udiag, double* S,
+                         hipStream_t s);
 
 // Finalise: Jacobi scale (first), LM diagonal, damping Lambda_f, block-Jacobi
 // preconditioner (inverse of the damped diagonal blocks), rhs = -b.
@@ -86,11 +94,12 @@ void launch_plus(const DevProblem& p, const double* df, const double* dX, const 
                  hipStream_t s);
 
 // Explicit reduced camera system (nf x nf, row-major, upper triangle row <= col,
-// i.e. rocSOLVER's column-major lower): S += U (image tile pass) -
-// sum_p W_p V_p^-1 W_p' (Z factors, then MFMA image-pair tiles); S zeroed.
+// i.e. rocSOLVER's column-major lower): S += U (image tile pass, with_u; else
+// launch_fblock_dense added it) - sum_p W_p V_p^-1 W_p' (Z factors, then MFMA
+// image-pair tiles).
 void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
                         const double* J, const double* Linv, double* Z, const DevPairTile* ptiles, int nptiles,
-                        const uint2* pairs, double* S, hipStream_t s);
+                        const uint2* pairs, double* S, bool with_u, hipStream_t s);
 // S_kk += Lambda_k on parameter slots, S_kk = 1 on non-parameter slots.
 void launch_dense_finalize(const DevProblem& p, const double* lambda_f, double* S, hipStream_t s);
 

@@ -594,7 +594,8 @@ __global__ __launch_bounds__(kBlock) void point_prepare_kernel(const DevPoint* _
                                                                 double* __restrict__ scale_p,
                                                                 double* __restrict__ diag_p,
                                                                 double* __restrict__ Vinv,
-                                                                double* __restrict__ Linv, int first,
+                                                                double* __restrict__ Linv,
+                                                                double* __restrict__ q, int first,
                                                                 int reuse_diag, double radius) {
   const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (k >= npv) return;
@@ -625,6 +626,13 @@ __global__ __launch_bounds__(kBlock) void point_prepare_kernel(const DevPoint* _
   sym3_inverse(V, inv);
 #pragma unroll
   for (int m = 0; m < 6; ++m) Vinv[6 * (size_t)pt + m] = inv[m];
+  if (q) {
+    // q_p = V_p^-1 g_p: the point term of the reduced rhs (fblock_dense_kernel)
+    double o[3];
+    sym3_mul(inv, g + 6, o);
+#pragma unroll
+    for (int m = 0; m < 3; ++m) q[3 * (size_t)pt + m] = o[m];
+  }
   if (Linv) {
     // inverse Cholesky factor of the damped block: V^-1 = Linv' Linv, so the
     // Schur term W V^-1 W' = Z Z' with Z = W Linv' (schur_z_kernel)
@@ -764,6 +772,87 @@ __global__ __launch_bounds__(kBlock) void fblock_kernel(DevProblem p, const DevT
       if (cam_var)
         atomicAdd(udiag + 6 * (size_t)p.num_images + (size_t)CT * cam + (k - kSymPose - 12 - NC - CT), v);
     }
+  }
+}
+
+// f-vector slot of tangent column m (pose 0..5, camera 6..) of an image's block
+__device__ inline int64_t fslot(const DevProblem& p, uint32_t img, uint32_t cam, int m) {
+  return m < 6 ? 6 * (int64_t)img + m : 6 * (int64_t)p.num_images + (int64_t)p.ct * cam + (m - 6);
+}
+
+// Exact (explicit S) path: one pass over an image tile's J rows giving
+//   U = sum J_f'J_f into S's image block (upper triangle, as dense_u_kernel),
+//   b = g - sum W V^-1 g_p = sum J_f'(r - J_p q_p), q_p = V_p^-1 g_p (point_prepare),
+//   diag(U) (the LM damping's column norms).
+// Replaces fblock_kernel + dense_u_kernel there: the Schur-Jacobi blocks
+// fblock_kernel also forms are only the PCG preconditioner's.
+template <int CT>
+__global__ __launch_bounds__(kBlock) void fblock_dense_kernel(DevProblem p, const DevTile* __restrict__ tiles,
+                                                               const uint32_t* __restrict__ cm_perm,
+                                                               const double2* __restrict__ rr,
+                                                               const double* __restrict__ J,
+                                                               const double* __restrict__ q,
+                                                               double* __restrict__ bvec,
+                                                               double* __restrict__ udiag, double* __restrict__ S) {
+  constexpr int F = 6 + CT, W = 9 + CT;
+  constexpr int NU = F * (F + 1) / 2, NV = NU + F;
+  __shared__ double sred[4 * NV];
+  const DevTile tile = tiles[blockIdx.x];
+  double acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+  for (uint32_t k = threadIdx.x; k < tile.count; k += kBlock) {
+    const uint32_t b = cm_perm[tile.start + k];
+    const double* Jb = J + (size_t)b * 2 * W;
+    const uint32_t pt = p.obs_pt[b];
+    const double2 r = rr[b];
+    const bool ptv = p.pt_var[pt] != 0;
+    double qp[3] = {0.0, 0.0, 0.0};
+    if (ptv) {
+      qp[0] = q[3 * (size_t)pt];
+      qp[1] = q[3 * (size_t)pt + 1];
+      qp[2] = q[3 * (size_t)pt + 2];
+    }
+    double jf[2][F];
+    double e[2];
+#pragma unroll
+    for (int row = 0; row < 2; ++row) {
+#pragma unroll
+      for (int m = 0; m < 6; ++m) jf[row][m] = Jb[row * W + m];
+#pragma unroll
+      for (int m = 0; m < CT; ++m) jf[row][6 + m] = Jb[row * W + 9 + m];
+      e[row] = (row == 0 ? r.x : r.y) -
+               (Jb[row * W + 6] * qp[0] + Jb[row * W + 7] * qp[1] + Jb[row * W + 8] * qp[2]);
+    }
+    int o = 0;
+#pragma unroll
+    for (int a = 0; a < F; ++a)
+#pragma unroll
+      for (int c = a; c < F; ++c, ++o) acc[o] += jf[0][a] * jf[0][c] + jf[1][a] * jf[1][c];
+#pragma unroll
+    for (int m = 0; m < F; ++m) acc[NU + m] += jf[0][m] * e[0] + jf[1][m] * e[1];
+  }
+  block_reduce<NV>(acc, sred);
+  const int k = threadIdx.x;
+  if (k >= NV) return;
+  const uint32_t img = tile.image, cam = p.img_cam[img];
+  const bool pv = p.img_flags[img] & 1u, cv = p.cam_var[cam] != 0;
+  const double v = sred[k];
+  if (k < NU) {
+    int a = 0, rem = k;
+    while (rem >= F - a) { rem -= F - a; ++a; }
+    const int c = a + rem;
+    const bool va = a < 6 ? pv : cv, vc = c < 6 ? pv : cv;
+    if (!(va && vc)) return;
+    const int64_t ra = fslot(p, img, cam, a), rc = fslot(p, img, cam, c);
+    if (ra <= rc)
+      atomicAdd(S + ra * p.nf + rc, v);
+    else
+      atomicAdd(S + rc * p.nf + ra, v);
+    if (a == c) atomicAdd(udiag + ra, v);
+  } else {
+    const int m = k - NU;
+    if (m < 6 ? pv : cv) atomicAdd(bvec + fslot(p, img, cam, m), v);
   }
 }
 
@@ -1227,9 +1316,6 @@ __global__ __launch_bounds__(1024) void sqnorm2_kernel(const double* __restrict_
 // Explicit reduced camera system S = U + Lambda - sum_p W_p V_p^-1 W_p'
 // (the system Ceres' DENSE_SCHUR / SPARSE_SCHUR factorise exactly).
 // ---------------------------------------------------------------------------
-__device__ inline int64_t fslot(const DevProblem& p, uint32_t img, uint32_t cam, int m) {
-  return m < 6 ? 6 * (int64_t)img + m : 6 * (int64_t)p.num_images + (int64_t)p.ct * cam + (m - 6);
-}
 
 // U = sum J_f' J_f, reduced per image-aligned tile (one flush per tile).
 template <int CT>
@@ -1409,6 +1495,89 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
     if (mrow >= F || ncol >= F) continue;
     const bool va = mrow < 6 ? pa : cva, vb = ncol < 6 ? pb : cvb;
     if (!va || !vb) continue;
+    const int64_t ra = fslot(p, ia, ca, mrow), rb = fslot(p, ib, cb, ncol);
+    const double v = acc[r];
+    if (tl.self) {
+      if (ra <= rb) atomicAdd(S + ra * p.nf + rb, -v);
+    } else if (ra < rb) {
+      atomicAdd(S + ra * p.nf + rb, -v);
+    } else if (ra > rb) {
+      atomicAdd(S + rb * p.nf + ra, -v);
+    } else {
+      atomicAdd(S + ra * p.nf + ra, -2.0 * v);
+    }
+  }
+}
+
+// As schur_pairs_kernel, latency-hidden: the tile's pair list is staged once
+// in the wave's LDS slot (read back as broadcasts, no dependent global load
+// per pair), and the Z rows of U pairs are requested one step ahead, so the
+// next step's 2U gathers are in flight while this step's MFMAs run.
+template <int CT, int U>
+__global__ __launch_bounds__(kBlock) void schur_pairs_pipelined_kernel(DevProblem p, const DevPairTile* __restrict__ tiles,
+                                                                       int ntiles, const uint2* __restrict__ pairs,
+                                                                       const double* __restrict__ Z,
+                                                                       double* __restrict__ S) {
+  constexpr int F = 6 + CT, ZN = 3 * F;
+  __shared__ uint2 spl[kBlock / 64][kPairTile];
+  const int G = (ntiles + 3) / 4;
+  const int per = (G + 7) / 8;
+  const int b = blockIdx.x;
+  const int lb = (b % 8) * per + b / 8;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = lb * 4 + wv;
+  if (lb >= G || t >= ntiles) return;
+  const DevPairTile tl = tiles[t];
+  const int lane = threadIdx.x & 63;
+  const int m = lane & 15, k = lane >> 4;
+  const bool on = m < F && k < 3;
+  const int off = on ? k * F + m : 0;
+  const int cnt = (int)tl.count;
+  const uint2* pl = pairs + tl.start;
+  uint2* sp = spl[wv];
+  for (int n = lane; n < cnt; n += 64) sp[n] = pl[n];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  typedef double dvec4 __attribute__((ext_vector_type(4)));
+  dvec4 acc = {0.0, 0.0, 0.0, 0.0};
+  double va[U], vb[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint2 pr = sp[u < cnt ? u : 0];
+    const bool ld = on && u < cnt;
+    va[u] = ld ? Z[(size_t)pr.x * ZN + off] : 0.0;
+    vb[u] = ld ? Z[(size_t)pr.y * ZN + off] : 0.0;
+  }
+  for (int n0 = 0; n0 < cnt; n0 += U) {
+    double na[U], nb[U];
+    const int n1 = n0 + U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int n = n1 + u;
+      const uint2 pr = sp[n < cnt ? n : 0];
+      const bool ld = on && n < cnt;
+      na[u] = ld ? Z[(size_t)pr.x * ZN + off] : 0.0;
+      nb[u] = ld ? Z[(size_t)pr.y * ZN + off] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va[u], vb[u], acc, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      va[u] = na[u];
+      vb[u] = nb[u];
+    }
+  }
+  const uint32_t ia = tl.ia, ib = tl.ib;
+  const uint32_t ca = p.img_cam[ia], cb = p.img_cam[ib];
+  const bool pa = p.img_flags[ia] & 1u, pb = p.img_flags[ib] & 1u;
+  const bool cva = p.cam_var[ca] != 0, cvb = p.cam_var[cb] != 0;
+  const int ncol = lane & 15;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int mrow = 4 * r + (lane >> 4);
+    if (mrow >= F || ncol >= F) continue;
+    const bool xa = mrow < 6 ? pa : cva, xb = ncol < 6 ? pb : cvb;
+    if (!xa || !xb) continue;
     const int64_t ra = fslot(p, ia, ca, mrow), rb = fslot(p, ib, cb, ncol);
     const double v = acc[r];
     if (tl.self) {
@@ -1620,11 +1789,22 @@ void launch_point_normal(const DevProblem& p, const DevPoint* vp, int64_t npv, c
 }
 
 void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg,
-                          double* scale_p, double* diag_p, double* Vinv, double* Linv, int first, int reuse_diag,
-                          double radius, hipStream_t s) {
+                          double* scale_p, double* diag_p, double* Vinv, double* Linv, double* q, int first,
+                          int reuse_diag, double radius, hipStream_t s) {
   if (npv == 0) return;
   hipLaunchKernelGGL(point_prepare_kernel, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, vp, npv, Vg,
-                     scale_p, diag_p, Vinv, Linv, first, reuse_diag, radius);
+                     scale_p, diag_p, Vinv, Linv, q, first, reuse_diag, radius);
+}
+
+void launch_fblock_dense(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
+                         const double2* r, const double* J, const double* q, double* b, double* udiag, double* S,
+                         hipStream_t s) {
+  if (ntiles == 0) return;
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    hipLaunchKernelGGL(fblock_dense_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, q, b,
+                       udiag, S);
+  });
 }
 
 void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
@@ -1731,16 +1911,26 @@ void launch_plus(const DevProblem& p, const double* df, const double* dX, const 
 
 void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
                         const double* J, const double* Linv, double* Z, const DevPairTile* ptiles, int nptiles,
-                        const uint2* pairs, double* S, hipStream_t s) {
+                        const uint2* pairs, double* S, bool with_u, hipStream_t s) {
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
-    if (ntiles > 0)
+    if (with_u && ntiles > 0)
       hipLaunchKernelGGL(dense_u_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, J, S);
     if (nptiles > 0 && p.nb > 0) {
       hipLaunchKernelGGL(schur_z_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z);
       const int G = (nptiles + 3) / 4;
       const int grid = ((G + 7) / 8) * 8;  // whole XCD stripes (extra workgroups exit)
-      hipLaunchKernelGGL(schur_pairs_kernel<CT>, dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs, Z, S);
+      if (p.svariant == 1)
+        hipLaunchKernelGGL((schur_pairs_pipelined_kernel<CT, 8>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles,
+                           pairs, Z, S);
+      else if (p.svariant == 2)
+        hipLaunchKernelGGL((schur_pairs_pipelined_kernel<CT, 4>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles,
+                           pairs, Z, S);
+      else if (p.svariant == 3)
+        hipLaunchKernelGGL((schur_pairs_pipelined_kernel<CT, 16>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles,
+                           pairs, Z, S);
+      else
+        hipLaunchKernelGGL(schur_pairs_kernel<CT>, dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs, Z, S);
     }
   });
 }

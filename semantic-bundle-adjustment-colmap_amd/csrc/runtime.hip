@@ -414,6 +414,7 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
   d.loss_type = o->loss_function_type;
   d.loss_scale = o->loss_function_scale;
   d.jvariant = 0;
+  d.svariant = 0;
   d.refine_mask = (o->refine_focal_length ? 1 : 0) | (o->refine_principal_point ? 2 : 0) |
                   (o->refine_extra_params ? 4 : 0);
   d.obs_xy = ctx->obs_xy.ptr;
@@ -646,14 +647,11 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   hipStream_t s = ctx->stream;
   const int64_t nf = d.nf;
   *ok = true;
-  {
-    Phase ph_(ctx, "s_zero");
-    MI_HIP(hipMemsetAsync(ctx->S.ptr, 0, ctx->S.bytes(), s));
-  }
+  // S was zeroed and took U from launch_fblock_dense (context_solve)
   hipEvent_t stop;
   timer_begin(ctx, "schur_build", &stop);
   launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
-                     ctx->ptiles.ptr, ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, s);
+                     ctx->ptiles.ptr, ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, false, s);
   if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
   if (ctx->gsba) gsba_add_dense(ctx, ctx->S.ptr);
   timer_end(ctx, stop);
@@ -732,16 +730,26 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     {
       Phase ph_(ctx, "point_prepare");
       launch_point_prepare(d, ctx->vpoints.ptr, ctx->npv, ctx->Vg.ptr, ctx->scale_p.ptr, ctx->diag_p.ptr,
-                           ctx->Vinv.ptr, ctx->dense ? ctx->Linv.ptr : nullptr, first, reuse_diag, radius, s);
+                           ctx->Vinv.ptr, ctx->dense ? ctx->Linv.ptr : nullptr,
+                           ctx->dense ? ctx->cg_w.ptr : nullptr,  // q_p: the PCG's point vector is free here
+                           first, reuse_diag, radius, s);
     }
     MI_HIP(hipMemsetAsync(ctx->pose_blk.ptr, 0, ctx->pose_blk.bytes(), s));
     MI_HIP(hipMemsetAsync(ctx->cam_blk.ptr, 0, ctx->cam_blk.bytes(), s));
     MI_HIP(hipMemsetAsync(ctx->bvec.ptr, 0, ctx->bvec.bytes(), s));
     MI_HIP(hipMemsetAsync(ctx->udiag.ptr, 0, ctx->udiag.bytes(), s));
+    if (ctx->dense) {
+      Phase ph_(ctx, "s_zero");
+      MI_HIP(hipMemsetAsync(ctx->S.ptr, 0, ctx->S.bytes(), s));
+    }
     {
       Phase ph_(ctx, "fblock");
-      launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr,
-                    ctx->Vinv.ptr, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr, s);
+      if (ctx->dense)
+        launch_fblock_dense(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->cg_w.ptr,
+                            ctx->bvec.ptr, ctx->udiag.ptr, ctx->S.ptr, s);
+      else
+        launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr,
+                      ctx->Vinv.ptr, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr, s);
       if (ctx->sem) semantic_add_fblock(ctx);
       if (ctx->gsba) gsba_add_fblock(ctx);
     }
@@ -1319,6 +1327,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->dev.jvariant = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 3) {
+    ctx->dev.svariant = value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_panel") == 0 && (value == 0 || (value >= 64 && value <= 4096))) {
     ctx->chol.panel = value;
     return MI_BA_OK;
@@ -1331,8 +1343,12 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.own_diag = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_solve") == 0 && (value == 0 || value == 1)) {
+  if (std::strcmp(key, "cholesky_solve") == 0 && value >= 0 && value <= 2) {
     ctx->chol.solve = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 3) {
+    ctx->chol.rest_update = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_gemm_update") == 0 && (value == 0 || value == 1)) {
@@ -1344,8 +1360,13 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
 
 mi_ba_status mi_ba_dense_cholesky(int32_t device, int32_t n, double* A, double* b, int32_t panel, int32_t lookahead,
                                   int32_t own_diag, int32_t* info) {
+  return mi_ba_dense_cholesky_ex(device, n, A, b, panel, lookahead, own_diag, CholConfig{}.solve, info);
+}
+
+mi_ba_status mi_ba_dense_cholesky_ex(int32_t device, int32_t n, double* A, double* b, int32_t panel,
+                                     int32_t lookahead, int32_t own_diag, int32_t solve, int32_t* info) {
   if (n < 0 || !A || !info || (panel != 0 && (panel < 64 || panel > 4096)) || (lookahead != 0 && lookahead != 1) ||
-      (own_diag < 0 || own_diag > 5))
+      (own_diag < 0 || own_diag > 5) || solve < 0 || solve > 2)
     return MI_BA_ERR_INVALID_ARGUMENT;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MI_BA_ERR_NO_DEVICE;
@@ -1357,6 +1378,7 @@ mi_ba_status mi_ba_dense_cholesky(int32_t device, int32_t n, double* A, double* 
   cfg.panel = panel;
   cfg.lookahead = lookahead != 0;
   cfg.own_diag = own_diag;
+  cfg.solve = solve;
   // all resources are owned by this call: concurrent calls share nothing
   hipStream_t s = nullptr;
   rocblas_handle h = nullptr;

@@ -213,6 +213,8 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_context_set_comm.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
     lib.mi_ba_context_set_host_reducer.argtypes = [C.c_void_p, C.c_int32, C.c_int32, HOST_ALLREDUCE_FN, C.c_void_p]
     lib.mi_ba_dense_cholesky.argtypes = [C.c_int32, C.c_int32, _dp, _dp, C.c_int32, C.c_int32, C.c_int32, _i32p]
+    lib.mi_ba_dense_cholesky_ex.argtypes = [C.c_int32, C.c_int32, _dp, _dp, C.c_int32, C.c_int32, C.c_int32,
+                                            C.c_int32, _i32p]
     lib.mi_ba_gsba_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.mi_ba_gsba_evaluate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64),
                                         C.c_void_p, C.c_void_p, C.c_void_p]
@@ -415,7 +417,7 @@ def shard_scene(scene: "Scene", rank: int, world: int, semantic: Optional["Seman
 
 
 def dense_cholesky(A: np.ndarray, b: Optional[np.ndarray] = None, device: int = 0, panel: int = 512,
-                   lookahead: int = 1, own_diag: int = 2):
+                   lookahead: int = 1, own_diag: int = 2, solve: int = 2):
     """mi_ba_dense_cholesky: the reduced-camera-system factorisation on a
     caller-supplied SPD matrix.  Returns (L, x, info): L lower triangular
     (strict upper zeroed), x the solution of A x = b (None without b)."""
@@ -423,8 +425,8 @@ def dense_cholesky(A: np.ndarray, b: Optional[np.ndarray] = None, device: int = 
     F = np.asfortranarray(A, dtype=np.float64).copy(order="F")
     x = None if b is None else np.ascontiguousarray(b, dtype=np.float64).copy()
     info = C.c_int32(0)
-    check(load().mi_ba_dense_cholesky(device, n, F.ctypes.data_as(_dp), _ptr(x, _dp), panel, lookahead, own_diag,
-                                      C.byref(info)), "mi_ba_dense_cholesky")
+    check(load().mi_ba_dense_cholesky_ex(device, n, F.ctypes.data_as(_dp), _ptr(x, _dp), panel, lookahead, own_diag,
+                                         solve, C.byref(info)), "mi_ba_dense_cholesky_ex")
     return np.tril(F), x, info.value
 
 

@@ -20,6 +20,7 @@ import threading
 
 import numpy as np
 import pytest
+from scipy.linalg import solve_triangular
 
 import mi_ba
 import oracle
@@ -61,6 +62,28 @@ def test_factor_matches_oracle_and_lapack(gpu, n):
             assert np.abs(L - L_o).max() <= 1e-12 * scale, (own, panel)
             assert np.abs(L - L_np).max() <= 1e-12 * scale, (own, panel)
             assert np.abs(x - x_ref).max() <= 1e-10 * np.abs(x_ref).max(), (own, panel)
+    # the three triangular-solve variants on the default factor
+    for solve in (0, 1, 2):
+        L, x, info = mi_ba.dense_cholesky(A, b, solve=solve)
+        assert info == 0
+        assert np.abs(x - x_ref).max() <= 1e-10 * np.abs(x_ref).max(), solve
+
+
+@pytest.mark.parametrize("n", [64, 65, 130, 12000])
+def test_sync_free_solve_sizes(gpu, n):
+    """Sync-free sweeps (one launch per direction) at one block, a ragged
+    second block, and the C4 reduced-camera size (188 blocks, ragged last):
+    against LAPACK on the same factor, and repeated solves (flag epochs) stay
+    equal."""
+    A = spd(n, seed=n + 3) if n <= 4096 else np.diag(np.linspace(1.0, 3.0, n)) + 1e-3
+    b = np.random.default_rng(n).standard_normal(n)
+    L, x, info = mi_ba.dense_cholesky(A, b, solve=2)
+    assert info == 0
+    y = solve_triangular(L, b, lower=True)
+    x_ref = solve_triangular(L, y, lower=True, trans="T")
+    assert np.abs(x - x_ref).max() <= 1e-10 * np.abs(x_ref).max()
+    _, x1, _ = mi_ba.dense_cholesky(A, b, solve=1)
+    assert np.abs(x - x1).max() <= 1e-12 * np.abs(x_ref).max()
 
 
 @pytest.mark.parametrize("col", [5, 700, 1663])
@@ -124,19 +147,21 @@ def test_two_contexts_two_threads(gpu):
 
 
 def test_lm_solve_variants(gpu):
-    """The blocked triangular sweeps (default) and the recursive rocBLAS
-    dtrsv / dgemv solve drive the same LM (nf = 1593, ragged last block)."""
+    """The sync-free sweeps (default), the per-block-column sweeps and the
+    recursive rocBLAS dtrsv / dgemv solve drive the same LM (nf = 1593,
+    ragged last block)."""
     sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=5)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
     res = []
-    for v in (0, 1):
+    for v in (0, 1, 2):
         with mi_ba.Context(opts, sc.copy()) as ctx:
             ctx.set_tuning("cholesky_solve", v)
             res.append(ctx.solve())
-    a, b = res
-    assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
-    assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
+    b = res[-1]
+    for a in res[:-1]:
+        assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
+        assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
 
 
 @pytest.mark.parametrize("images", [200])
