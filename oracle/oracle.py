@@ -297,3 +297,54 @@ def semantic_throughput(options, scene, semantic, max_samples, threads=1):
     sec = load().oracle_semantic_throughput(C.byref(options), C.byref(p), C.byref(s), max_samples, threads,
                                             C.byref(done))
     return sec, done.value
+
+
+# ---------------------------------------------------------------------------
+# oracle/_ref: the reference's own PBA CPU double solver (built from the
+# reference's lib/PBA sources by oracle/Makefile.ref when /root/reference is
+# present; the built .so travels with the tree).  Cross-check of converged
+# geometric BA for SIMPLE_RADIAL (ParallelBundleAdjuster, bundle_adjustment.cc:559-663).
+REF_LIB_PATH = os.path.join(_HERE, "_ref", "libpba_ref.so")
+_ref_lib = None
+
+
+def ref_available():
+    return os.path.exists(REF_LIB_PATH)
+
+
+def load_ref():
+    global _ref_lib
+    if _ref_lib is None:
+        lib = C.CDLL(REF_LIB_PATH)
+        lib.pba_ref_solve.argtypes = [C.c_int, _dp, _dp, _dp, C.c_int, _dp, C.c_int, _dp, _i32p, _i32p, C.c_int,
+                                      C.c_int, C.c_int, _dp, _dp, _i32p]
+        _ref_lib = lib
+    return _ref_lib
+
+
+def pba_ref_solve(scene, max_iterations=50, refine_intrinsics=True, threads=1):
+    """Runs the reference PBA (CPU, double) on a SIMPLE_RADIAL scene with one
+    camera per image; updates the scene in place; returns (initial_cost,
+    final_cost, lm_iterations) as ParallelBundleAdjuster reports them."""
+    assert scene.camera_model == mi_ba.SIMPLE_RADIAL
+    order = np.argsort(scene.obs_point, kind="stable")
+    cam_of_img = np.asarray(scene.image_camera)
+    assert len(np.unique(cam_of_img)) == scene.num_images, "PBA: one camera per image"
+    params = np.ascontiguousarray(scene.camera_params[cam_of_img], dtype=np.float64).copy()
+    q = np.ascontiguousarray(scene.qvec, dtype=np.float64).copy()
+    t = np.ascontiguousarray(scene.tvec, dtype=np.float64).copy()
+    X = np.ascontiguousarray(scene.xyz, dtype=np.float64).copy()
+    xy = np.ascontiguousarray(scene.obs_xy[order], dtype=np.float64)
+    oc = np.ascontiguousarray(scene.obs_image[order], dtype=np.int32)
+    op = np.ascontiguousarray(scene.obs_point[order], dtype=np.int32)
+    ic, fc, it = C.c_double(0), C.c_double(0), C.c_int32(0)
+    rc = load_ref().pba_ref_solve(scene.num_images, params.ctypes.data_as(_dp), q.ctypes.data_as(_dp),
+                                  t.ctypes.data_as(_dp), scene.num_points, X.ctypes.data_as(_dp), len(op),
+                                  xy.ctypes.data_as(_dp), oc.ctypes.data_as(_i32p), op.ctypes.data_as(_i32p),
+                                  max_iterations, int(refine_intrinsics), threads, C.byref(ic), C.byref(fc),
+                                  C.byref(it))
+    if rc != 0:
+        raise RuntimeError(f"pba_ref_solve failed: {rc}")
+    scene.camera_params[cam_of_img] = params
+    scene.qvec[:], scene.tvec[:], scene.xyz[:] = q, t, X
+    return ic.value, fc.value, it.value

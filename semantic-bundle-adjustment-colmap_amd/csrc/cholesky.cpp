@@ -473,8 +473,10 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
         for (int r = 0; r < kTB; ++r) v[r] = src[min(r, wj - 1)];
       }
     }
-    while (__hip_atomic_load(flag + jb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch)
+    for (int spin = 0; spin < (1 << 24); ++spin) {  // bounded, as pf_wait
+      if (__hip_atomic_load(flag + jb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
       __builtin_amdgcn_s_sleep(1);
+    }
     xs[wv][lane] = lane < wj ? x[c0 + lane] : 0.0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -509,6 +511,247 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
   if (lane < w) x[r0 + lane] = z;
   __threadfence();
   if (lane == 0) __hip_atomic_store(flag + ib, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------
+// Panel factor in ONE launch (own_diag 6): the diagonal block's Cholesky AND
+// the panel's triangular solve below it (replaces potrf_diag's 16 launches
+// per 512-wide block plus rocBLAS dtrsm — together the look-ahead's critical
+// path: 19.7 ms of side-stream work per nf = 12 000 factorisation against
+// 15.4 ms of trailing dgemm, profiles/r2_chol_timeline.txt).
+// Tiles are 64 x 64: column tile c (nc <= 8 of them, the last ragged), row
+// tile r: r < nc the diagonal block's rows (tile height = that column tile's
+// width), r >= nc 64-row blocks below it.  One 256-thread workgroup per row
+// tile (atomic ticket = dispatch order), left-looking over its row:
+//   T = A_rc - sum_{k<c} L_rk L_ck'         (MFMA f64 16x16x4 tile GEMMs)
+//   c < r:  L_rc = T Linv_cc'                (Linv_cc from workgroup c)
+//   c == r: L_rr = chol(T) in LDS, Linv_rr = L_rr^-1, published with L_rr
+// A diagonal-block workgroup also keeps its diagonal tile's accumulator
+// across its steps (A_rr -= L_rc L_rc' as soon as L_rc exists), so the step
+// after a flag is one TRSM-GEMM + one SYRK-GEMM + the 64x64 factor.
+// Workgroups only ever wait for lower-numbered ones (flag = epoch of this
+// launch, release/acquire at agent scope, as the sweeps above).
+typedef double pf_dvec4 __attribute__((ext_vector_type(4)));
+constexpr int kPfMaxTiles = 8;  // column tiles per panel (panel <= 512)
+
+__device__ __forceinline__ int pf_row0(int r, int kb, int nc) { return r < nc ? 64 * r : kb + 64 * (r - nc); }
+__device__ __forceinline__ int pf_rows(int r, int kb, int nc, int mrows) {
+  return r < nc ? min(64, kb - 64 * r) : min(64, mrows - kb - 64 * (r - nc));
+}
+
+__device__ __forceinline__ void pf_wait(const unsigned* f, unsigned epoch) {
+  // bounded (~seconds): a lost flag ends the launch with a wrong factor
+  // instead of a wave that never finishes
+  for (int spin = 0; spin < (1 << 24); ++spin) {
+    if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// acc (wave w: rows 16w..16w+15 of the 64x64 tile, column tiles t = 0..3,
+// v_mfma_f64_16x16x4f64 D layout D[4q + l/16][l%16]) += sign * X Y' over
+// K = 64; ldx(i, k) / ldy(j, k) return X[i][k], Y[j][k] (zero-padded).
+template <typename LX, typename LY>
+__device__ __forceinline__ void pf_gemm_nt(pf_dvec4 (&acc)[4], double sign, LX ldx, LY ldy, int w, int lane) {
+  const int m = lane & 15, k = lane >> 4;
+#pragma unroll 4
+  for (int s = 0; s < 16; ++s) {
+    const double a = sign * ldx(16 * w + m, 4 * s + k);
+    double b[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) b[t] = ldy(16 * t + m, 4 * s + k);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[t], acc[t], 0, 0, 0);
+  }
+}
+
+// accumulator <-> column-major 64x64 LDS tile
+__device__ __forceinline__ void pf_acc_to_lds(const pf_dvec4 (&acc)[4], double* T, int w, int lane) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) T[(16 * t + (lane & 15)) * 64 + 16 * w + 4 * q + (lane >> 4)] = acc[t][q];
+}
+
+// In-LDS Cholesky of a 64x64 column-major tile (lower), blocked by kStep
+// columns (diag_panel_blocked_kernel's factor loop); returns the first
+// non-positive pivot (1-based) or 0.
+template <int kStep, int NW>
+__device__ int tile_chol_lds(double* L, double* nb, int lane, int wv) {
+  int bad = 0;
+  for (int jb = 0; jb < 64; jb += kStep) {
+    double d[kStep][kStep];
+#pragma unroll
+    for (int i = 0; i < kStep; ++i)
+#pragma unroll
+      for (int k = 0; k <= i; ++k) d[i][k] = L[(jb + k) * 64 + jb + i];
+#pragma unroll
+    for (int k = 0; k < kStep; ++k) {
+      const double piv = d[k][k];
+      if (!(piv > 0.0) && bad == 0) bad = jb + k + 1;
+      d[k][k] = sqrt(piv);
+#pragma unroll
+      for (int i = k + 1; i < kStep; ++i) d[i][k] /= d[k][k];
+#pragma unroll
+      for (int i = k + 1; i < kStep; ++i)
+#pragma unroll
+        for (int m = k + 1; m <= i; ++m) d[i][m] -= d[i][k] * d[m][k];
+    }
+    double y[kStep];
+    if (lane >= jb + kStep) {
+#pragma unroll
+      for (int k = 0; k < kStep; ++k) {
+        double v = L[(jb + k) * 64 + lane];
+#pragma unroll
+        for (int m = 0; m < k; ++m) v -= y[m] * d[k][m];
+        y[k] = v / d[k][k];
+      }
+    } else {
+      const int i = lane - jb;
+#pragma unroll
+      for (int k = 0; k < kStep; ++k) {
+        double v = 0.0;
+#pragma unroll
+        for (int ii = k; ii < kStep; ++ii) v = (i == ii) ? d[ii][k] : v;
+        y[k] = v;
+      }
+    }
+    if (wv == 0) {
+#pragma unroll
+      for (int k = 0; k < kStep; ++k) nb[k * 64 + lane] = y[k];
+    }
+    __syncthreads();
+    if (wv == 0) {
+#pragma unroll
+      for (int k = 0; k < kStep; ++k)
+        if (lane >= jb + k) L[(jb + k) * 64 + lane] = y[k];
+    }
+    for (int c = jb + kStep + wv; c < 64; c += NW) {
+      double v = L[c * 64 + lane];
+#pragma unroll
+      for (int k = 0; k < kStep; ++k) v -= y[k] * nb[k * 64 + c];
+      L[c * 64 + lane] = v;
+    }
+    __syncthreads();
+  }
+  return bad;
+}
+
+__global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ A, int lda, int kb, int mrows,
+                                                           int* __restrict__ info, double* __restrict__ linv,
+                                                           unsigned* ctrl, unsigned base, unsigned epoch) {
+  __shared__ double T[64 * 64];   // column-major staging / factor tile
+  __shared__ double Li[64 * 64];  // diagonal tile inverse
+  __shared__ double nbuf[4 * 64];
+  __shared__ int s_r;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_r = (int)(atomicAdd(ctrl, 1u) - base);
+  __syncthreads();
+  const int r = s_r;
+  const int nc = (kb + 63) / 64;
+  unsigned* flag = ctrl + 1;  // [8][8]: tile (r, c) of the diagonal block rows final in A
+  const int r0 = pf_row0(r, kb, nc), hr = pf_rows(r, kb, nc, mrows);
+  const int cmax = min(r, nc - 1);
+  const bool diag_row = r < nc;
+  const int m = lane & 15, kq = lane >> 4;
+  // tile loaders (clamped addresses, zero padding)
+  auto gtile = [&](int row0, int h, int col0, int w) {
+    return [=](int i, int j) {
+      const double v = A[(size_t)(col0 + min(j, w - 1)) * lda + row0 + min(i, h - 1)];
+      return (i < h && j < w) ? v : 0.0;
+    };
+  };
+  auto ltile = [&](const double* S) { return [=](int i, int j) { return S[j * 64 + i]; }; };
+  // the diagonal tile's running accumulator (diagonal-block rows)
+  pf_dvec4 dacc[4];
+  if (diag_row) {
+    const int w = hr;  // = the width of column tile r
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 16 * wv + 4 * q + kq, j = 16 * t + m;
+        const double v = A[(size_t)(r0 + min(j, w - 1)) * lda + r0 + min(i, w - 1)];
+        dacc[t][q] = (i < w && j < w) ? v : (i == j ? 1.0 : 0.0);
+      }
+  }
+  for (int c = 0; c <= cmax; ++c) {
+    const int c0 = 64 * c, wc = min(64, kb - c0);
+    if (c < r) {
+      pf_dvec4 acc[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = 16 * wv + 4 * q + kq, j = 16 * t + m;
+          const double v = A[(size_t)(c0 + min(j, wc - 1)) * lda + r0 + min(i, hr - 1)];
+          acc[t][q] = (i < hr && j < wc) ? v : 0.0;
+        }
+      for (int k = 0; k < c; ++k) {
+        pf_wait(flag + c * kPfMaxTiles + k, epoch);
+        pf_gemm_nt(acc, -1.0, gtile(r0, hr, 64 * k, 64), gtile(c0, wc, 64 * k, 64), wv, lane);
+      }
+      pf_wait(flag + c * kPfMaxTiles + c, epoch);
+      // L_rc = T Linv_cc'
+      pf_acc_to_lds(acc, T, wv, lane);
+      __syncthreads();
+      pf_dvec4 out[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) out[t] = pf_dvec4{0.0, 0.0, 0.0, 0.0};
+      const double* lc = linv + (size_t)c * 64 * 64;
+      pf_gemm_nt(out, 1.0, ltile(T), [=](int i, int j) { return lc[j * 64 + i]; }, wv, lane);
+      __syncthreads();  // every wave is done reading T
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = 16 * wv + 4 * q + kq, j = 16 * t + m;
+          if (i < hr && j < wc) A[(size_t)(c0 + j) * lda + r0 + i] = out[t][q];
+        }
+      if (diag_row) {
+        // publish L_rc, and fold it into the diagonal tile: A_rr -= L_rc L_rc'
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0)
+          __hip_atomic_store(flag + r * kPfMaxTiles + c, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        pf_acc_to_lds(out, T, wv, lane);
+        __syncthreads();
+        pf_gemm_nt(dacc, -1.0, ltile(T), ltile(T), wv, lane);
+        __syncthreads();
+      }
+      continue;
+    }
+    // c == r: factor the diagonal tile, invert it, publish both
+    pf_acc_to_lds(dacc, T, wv, lane);
+    __syncthreads();
+    const int bad = tile_chol_lds<4, 4>(T, nbuf, lane, wv);
+    if (wv == 0) {
+      // Li = L^-1 (lower): lane = column, forward substitution over rows
+      const double dinv = 1.0 / T[lane * 64 + lane];
+      double x[64];
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        double s = (i == lane) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < i; ++k) s -= T[k * 64 + i] * x[k];
+        x[i] = s * readlane_f64(dinv, i);
+      }
+#pragma unroll
+      for (int i = 0; i < 64; ++i) Li[lane * 64 + i] = x[i];
+    }
+    __syncthreads();
+    double* lo = linv + (size_t)c * 64 * 64;
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+      lo[e] = Li[e];
+      const int i = e & 63, j = e >> 6;
+      if (i < wc && j < wc && i >= j) A[(size_t)(c0 + j) * lda + c0 + i] = T[e];
+    }
+    if (threadIdx.x == 0 && bad != 0 && bad <= wc) atomicCAS(info, 0, c0 + bad);
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(flag + r * kPfMaxTiles + r, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 rocblas_status potrf_diag(rocblas_handle h, int n, double* A, int lda, int* info, double* scratch, int variant) {
@@ -611,21 +854,21 @@ rocblas_status backward(rocblas_handle h, int n, const double* A, int lda, doubl
 // Right-looking blocked factorisation: per panel, dpotrf of the diagonal
 // block, dtrsm of the panel below it, then the trailing lower triangle
 // updated by dsyrk (or by dgemm per block column of width `panel`).
+rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, int own,
+                            double* scratch, CholWorkspace* ws);
+
 rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
-                              double* scratch) {
+                              double* scratch, CholWorkspace* ws) {
   const double one = 1.0, minus_one = -1.0;
   const int nb = cfg.panel;
   for (int k = 0; k < n; k += nb) {
     const int kb = std::min(nb, n - k);
     double* Akk = A + k + (size_t)k * lda;
-    rocblas_status st = potrf_leaf(h, kb, Akk, lda, info++, cfg.own_diag, scratch);
+    rocblas_status st = panel_factor(h, n, A, lda, k, kb, info++, cfg.own_diag, scratch, ws);
     if (st != rocblas_status_success) return st;
     const int m = n - k - kb;
     if (m == 0) break;
     double* Aik = Akk + kb;  // panel below the diagonal block
-    st = rocblas_dtrsm(h, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
-                       rocblas_diagonal_non_unit, m, kb, &one, Akk, lda, Aik, lda);
-    if (st != rocblas_status_success) return st;
     double* T = Aik + (size_t)kb * lda;  // trailing matrix, lower triangle
     if (!cfg.gemm_update) {
       st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, m, kb, &minus_one, Aik, lda, &one, T, lda);
@@ -648,8 +891,32 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
 // of panel k's trailing dgemm runs on the caller's stream; the next
 // iteration's dgemm waits on the side stream's event.  Hides the latency-bound
 // diagonal factor behind the MFMA update.
+// own_diag 6: diagonal factor + panel solve in one panel_factor_kernel launch
+rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info,
+                                  CholWorkspace* ws) {
+  if (!ws || !ws->pf_ctrl || !ws->pf_linv || kb > 64 * kPfMaxTiles) return rocblas_status_invalid_pointer;
+  hipStream_t s;
+  if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
+  if (hipMemsetAsync(info, 0, sizeof(int), s) != hipSuccess) return rocblas_status_internal_error;
+  const int mrows = n - k;
+  const int nc = (kb + 63) / 64;
+  const int nr = nc + (mrows - kb + 63) / 64;
+  if (ws->pf_base > 0x7fffffffu || ws->pf_epoch > 0xfffffff0u) {
+    if (hipMemsetAsync(ws->pf_ctrl, 0, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles), s) != hipSuccess)
+      return rocblas_status_internal_error;
+    ws->pf_base = 0;
+    ws->pf_epoch = 0;
+  }
+  const unsigned epoch = ++ws->pf_epoch;
+  hipLaunchKernelGGL(panel_factor_kernel, dim3(nr), dim3(256), 0, s, A + k + (size_t)k * lda, lda, kb, mrows, info,
+                     ws->pf_linv, ws->pf_ctrl, ws->pf_base, epoch);
+  ws->pf_base += (unsigned)nr;
+  return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
+}
+
 rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, int own,
-                            double* scratch) {
+                            double* scratch, CholWorkspace* ws) {
+  if (own == 6) return panel_factor_fused(h, n, A, lda, k, kb, info, ws);
   double* Akk = A + k + (size_t)k * lda;
   rocblas_status st = potrf_leaf(h, kb, Akk, lda, info, own, scratch);
   if (st != rocblas_status_success) return st;
@@ -669,7 +936,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
   if (ws.ev.size() < 2 * (size_t)((n + nb - 1) / nb)) return rocblas_status_invalid_size;
   double* scratch_main = ws.scratch;
   double* scratch_side = ws.scratch + kSub * kSub;
-  rocblas_status st = panel_factor(h, n, A, lda, 0, std::min(nb, n), info, cfg.own_diag, scratch_main);
+  rocblas_status st = panel_factor(h, n, A, lda, 0, std::min(nb, n), info, cfg.own_diag, scratch_main, &ws);
   if (st != rocblas_status_success) return st;
   // On a failure after the side stream got work, the caller's stream waits
   // for it (the caller may free A / info once its own stream is drained).
@@ -693,7 +960,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     hipEvent_t upd = ws.ev[2 * kk], pan = ws.ev[2 * kk + 1];
     if (hipEventRecord(upd, s1) != hipSuccess || hipStreamWaitEvent(ws.side, upd, 0) != hipSuccess)
       return fail(rocblas_status_internal_error);
-    st = panel_factor(ws.side_h, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag, scratch_side);
+    st = panel_factor(ws.side_h, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag, scratch_side, &ws);
     if (st != rocblas_status_success) return fail(st);
     if (hipEventRecord(pan, ws.side) != hipSuccess) return fail(rocblas_status_internal_error);
     // the rest of the trailing lower triangle (columns jb0 .. m)
@@ -759,6 +1026,14 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
     if (hipMalloc(&ybuf, sizeof(double) * kTB * (size_t)nblk) != hipSuccess) { ybuf = nullptr; return false; }
     if (hipMemset(linv, 0, sizeof(double) * kTB * kTB * (size_t)nblk) != hipSuccess) return false;
     if (hipMalloc(&ctrl, sizeof(unsigned) * (2 + (size_t)nblk)) != hipSuccess) { ctrl = nullptr; return false; }
+    if (hipMalloc(&pf_ctrl, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles)) != hipSuccess) {
+      pf_ctrl = nullptr;
+      return false;
+    }
+    if (hipMemset(pf_ctrl, 0, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles)) != hipSuccess) return false;
+    if (hipMalloc(&pf_linv, sizeof(double) * 64 * 64 * kPfMaxTiles) != hipSuccess) { pf_linv = nullptr; return false; }
+    pf_base = 0;
+    pf_epoch = 0;
     if (hipMemset(ctrl, 0, sizeof(unsigned) * (2 + (size_t)nblk)) != hipSuccess) return false;
     epoch = 0;
     linv_rows = nblk * kTB;
@@ -789,6 +1064,10 @@ void CholWorkspace::destroy() {
   ybuf = nullptr;
   if (ctrl) (void)hipFree(ctrl);
   ctrl = nullptr;
+  if (pf_ctrl) (void)hipFree(pf_ctrl);
+  pf_ctrl = nullptr;
+  if (pf_linv) (void)hipFree(pf_linv);
+  pf_linv = nullptr;
   linv_rows = 0;
 }
 
@@ -796,10 +1075,12 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
                            CholWorkspace* ws) {
   if (n <= 0) return rocblas_status_success;
   if (cfg.own_diag && (!ws || !ws->scratch)) return rocblas_status_invalid_pointer;
+  // the one-launch panel factor needs panels of at most 8 tiles
+  if (cfg.own_diag == 6 && (cfg.panel <= 0 || cfg.panel > 64 * kPfMaxTiles)) return rocblas_status_invalid_size;
   double* scratch = ws ? ws->scratch : nullptr;
   if (cfg.panel > 0 && cfg.gemm_update && cfg.lookahead && ws && ws->side)
     return factor_lookahead(h, n, A, lda, info, cfg, *ws);
-  if (cfg.panel > 0) return factor_blocked(h, n, A, lda, info, cfg, scratch);
+  if (cfg.panel > 0) return factor_blocked(h, n, A, lda, info, cfg, scratch, ws);
   return factor(h, n, A, lda, info, cfg.own_diag, scratch);
 }
 

@@ -41,6 +41,8 @@ struct CholConfig {
   // a four-wave register-resident tile factor with one barrier per pivot ran
   // 80 us per sub-panel vs 69; a fully unrolled one-wave register factor
   // ~300 us, instruction-fetch bound.)
+  // 6: one panel_factor_kernel launch per panel for the diagonal block AND the
+  // panel's solve below it (no dtrsm; panel <= 512)
   int own_diag = 2;
   // chol_solve variant: 2 sync-free sweeps (one launch per direction), 1 one
   // launch per 64-wide block column with diagonal-block inverses, 0 recursive
@@ -64,6 +66,10 @@ struct CholWorkspace {
   double* ybuf = nullptr;     // [n] intermediate vector of chol_solve (L y = b)
   unsigned* ctrl = nullptr;   // [2 + n/64] sync-free sweeps: two tickets + per-block solution flags
   unsigned epoch = 0;         // last flag value published (two per chol_solve)
+  unsigned* pf_ctrl = nullptr;  // one-launch panel factor: ticket + [8][8] tile flags
+  double* pf_linv = nullptr;    // [8][64*64] inverses of the panel's diagonal tiles
+  unsigned pf_base = 0;         // tickets handed out so far
+  unsigned pf_epoch = 0;        // flag value of the last panel launch
   int linv_rows = 0;
 
   // Creates the resources on `device` with events for up to `max_panels`

@@ -83,6 +83,8 @@ struct mi_ba_context {
   int ntiles = 0;
   miba::DevArray<miba::DevPoint> vpoints;
   int64_t npv = 0;
+  int64_t nb_const = 0;  // reduced blocks of constant points
+  int sem_variant = 0;   // semantic linearization kernel (tuning key "semantic_variant")
 
   // linearization
   miba::DevArray<double2> r;

@@ -57,7 +57,8 @@ void launch_fblock_finalize(const DevProblem& p, const double* pose_blk, const d
                             double* prec_pose, double* prec_cam, double* b, int first, int reuse_diag,
                             double radius, hipStream_t s);
 
-// Implicit Schur product y = S x (without the semantic pair term).
+// Implicit Schur product y = S x (without the semantic pair term); lambda_f
+// null leaves out the damping diagonal (multi-rank: added by rank 0 only).
 void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles,
                           int ntiles, const uint32_t* cm_perm, const double* J, const double* Vinv,
                           const double* lambda_f, const double* x, double* w, double* y, hipStream_t s);
@@ -83,6 +84,13 @@ void launch_xpby(double* p, const double* z, const double* beta_num, const doubl
 // Back substitution dX_p = -Vinv (g_p + sum Jp' Jf df) for variable points.
 void launch_backsub(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* J,
                     const double* Vg, const double* Vinv, const double* df, double* dX, hipStream_t s);
+
+// Back substitution + model cost change in one pass over the variable
+// points' blocks (per-wave partials into partial, count returned; the
+// blocks of constant points, const_blocks, atomically into partial[0]).
+int64_t launch_backsub_cost(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* J, const double2* r,
+                            const double* Vg, const double* Vinv, const double* df, double* dX, double* partial,
+                            bool const_blocks, hipStream_t s);
 
 // Model cost change partials: -(J d).(r + J d / 2) per block.
 void launch_model_cost(const DevProblem& p, const double2* r, const double* J, const double* df,

@@ -1213,6 +1213,83 @@ __global__ __launch_bounds__(kBlock) void backsub_kernel(DevProblem p, const Dev
   for (int n = 0; n < 3; ++n) dX[3 * (size_t)d.point + n] = -o[n];
 }
 
+// Back substitution fused with the model cost change: one pass over a
+// variable point's blocks gives e_a = J_f,a df, dX_p = -V_p^-1 (g_p + sum
+// J_p,a' e_a), and the point's share of the model cost change
+//   -sum_a [(J_a d).r_a + |J_a d|^2 / 2],  J_a d = e_a + J_p,a dX_p
+//   = -(sum e.r + dX.g_p + sum |e|^2 / 2 + dX.sum J_p'e + dX' V_p dX / 2)
+// (V_p, g_p undamped from point_normal), so J is read once instead of twice.
+// Per-wave partials into partial[k / 64]; blocks of constant points are
+// added by model_cost_const_kernel.
+template <int CT>
+__global__ __launch_bounds__(kBlock) void backsub_cost_kernel(DevProblem p, const DevPoint* __restrict__ vp,
+                                                               int64_t npv, const double* __restrict__ J,
+                                                               const double2* __restrict__ rr,
+                                                               const double* __restrict__ Vg,
+                                                               const double* __restrict__ Vinv,
+                                                               const double* __restrict__ df,
+                                                               double* __restrict__ dX,
+                                                               double* __restrict__ partial) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double model = 0.0;
+  if (k < npv) {
+    const DevPoint d = vp[k];
+    const int W = 9 + CT;
+    const double* g = Vg + 9 * (size_t)d.point;
+    double te[3] = {0.0, 0.0, 0.0};
+    double see = 0.0, ser = 0.0;
+    for (uint32_t m = 0; m < d.count; ++m) {
+      const uint32_t b = d.start + m;
+      const double* Jb = J + (size_t)b * 2 * W;
+      double e[2];
+      load_jf_x<CT>(p, Jb, p.obs_img[b], df, e);
+      const double2 r = rr[b];
+#pragma unroll
+      for (int n = 0; n < 3; ++n) te[n] += Jb[6 + n] * e[0] + Jb[W + 6 + n] * e[1];
+      see += e[0] * e[0] + e[1] * e[1];
+      ser += e[0] * r.x + e[1] * r.y;
+    }
+    const double t[3] = {g[6] + te[0], g[7] + te[1], g[8] + te[2]};
+    const double* vi = Vinv + 6 * (size_t)d.point;
+    const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
+    double o[3];
+    sym3_mul(Vi, t, o);
+    const double x[3] = {-o[0], -o[1], -o[2]};
+#pragma unroll
+    for (int n = 0; n < 3; ++n) dX[3 * (size_t)d.point + n] = x[n];
+    double Vx[3];
+    sym3_mul(g, x, Vx);  // g[0..5] = V_p packed
+    const double xg = x[0] * g[6] + x[1] * g[7] + x[2] * g[8];
+    const double xte = x[0] * te[0] + x[1] * te[1] + x[2] * te[2];
+    const double xVx = x[0] * Vx[0] + x[1] * Vx[1] + x[2] * Vx[2];
+    model = -(ser + xg + see / 2.0 + xte + xVx / 2.0);
+  }
+  const double s = wave_sum(model);
+  if ((threadIdx.x & 63) == 0 && k < npv) partial[k >> 6] = s;
+}
+
+// Model cost change of the blocks of constant points (no point step).
+template <int CT>
+__global__ __launch_bounds__(kBlock) void model_cost_const_kernel(DevProblem p, const double2* __restrict__ rr,
+                                                                   const double* __restrict__ J,
+                                                                   const double* __restrict__ df,
+                                                                   double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double v = 0.0;
+  bool any = false;
+  if (i < p.nb && !p.pt_var[p.obs_pt[i]]) {
+    const double* Jb = J + (size_t)i * 2 * (9 + CT);
+    double e[2];
+    load_jf_x<CT>(p, Jb, p.obs_img[i], df, e);
+    const double2 r = rr[i];
+    v = -(e[0] * (r.x + e[0] / 2.0) + e[1] * (r.y + e[1] / 2.0));
+    any = true;
+  }
+  const double s = wave_sum(v);
+  const bool wave_any = __any(any);  // voted with every lane active
+  if ((threadIdx.x & 63) == 0 && wave_any) atomicAdd(out, s);
+}
+
 template <int CT>
 __global__ __launch_bounds__(kBlock) void model_cost_kernel(DevProblem p, const double2* __restrict__ rr,
                                                              const double* __restrict__ J,
@@ -1842,7 +1919,8 @@ void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, 
     if (ntiles > 0)
       hipLaunchKernelGGL(schur_f_pass<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, J, x, w, y);
   });
-  hipLaunchKernelGGL(add_diag_kernel, dim3(grid_for(p.nf, kBlock)), dim3(kBlock), 0, s, lambda_f, x, y, p.nf);
+  if (lambda_f)
+    hipLaunchKernelGGL(add_diag_kernel, dim3(grid_for(p.nf, kBlock)), dim3(kBlock), 0, s, lambda_f, x, y, p.nf);
 }
 
 void launch_precond(const DevProblem& p, const double* prec_pose, const double* prec_cam, const double* r,
@@ -1888,6 +1966,22 @@ void launch_backsub(const DevProblem& p, const DevPoint* vp, int64_t npv, const 
     hipLaunchKernelGGL(backsub_kernel<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, J, Vg,
                        Vinv, df, dX);
   });
+}
+
+int64_t launch_backsub_cost(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* J, const double2* r,
+                            const double* Vg, const double* Vinv, const double* df, double* dX, double* partial,
+                            bool const_blocks, hipStream_t s) {
+  (void)hipMemsetAsync(partial, 0, sizeof(double), s);
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    if (npv > 0)
+      hipLaunchKernelGGL(backsub_cost_kernel<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, J,
+                         r, Vg, Vinv, df, dX, partial);
+    if (p.nb > 0 && const_blocks)
+      hipLaunchKernelGGL(model_cost_const_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, r, J,
+                         df, partial);
+  });
+  return std::max<int64_t>(1, (npv + 63) / 64);
 }
 
 void launch_model_cost(const DevProblem& p, const double2* r, const double* J, const double* df, const double* dX,

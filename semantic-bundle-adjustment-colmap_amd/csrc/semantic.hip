@@ -221,16 +221,58 @@ __device__ inline double distortion_gain(const double* K, double r2) {
   return 1.0 + s * g * g * g;
 }
 
+// The camera models with FMA contraction, for resolve's fast route only (an
+// outcome is taken only when it clears resolve's margins, which are orders of
+// magnitude above the rounding difference contraction makes; the reference
+// operation sequence, semantic_error, stays uncontracted).
+template <int M>
+__device__ inline void world_to_image_fma(const double* K, double u, double v, double* x, double* y) {
+#pragma clang fp contract(fast)
+  if constexpr (M == kSimplePinhole) {
+    *x = K[0] * u + K[1];
+    *y = K[0] * v + K[2];
+  } else if constexpr (M == kPinhole) {
+    *x = K[0] * u + K[2];
+    *y = K[1] * v + K[3];
+  } else if constexpr (M == kSimpleRadial || M == kRadial) {
+    const double r2 = u * u + v * v;
+    double rad = K[3] * r2;
+    if constexpr (M == kRadial) rad = rad + K[4] * r2 * r2;
+    *x = K[0] * (u + u * rad) + K[1];
+    *y = K[0] * (v + v * rad) + K[2];
+  } else {
+    const double k1 = K[4], k2 = K[5], p1 = K[6], p2 = K[7];
+    const double u2 = u * u, uv = u * v, v2 = v * v, r2 = u2 + v2;
+    const double rad = k1 * r2 + k2 * r2 * r2;
+    const double du = u * rad + 2.0 * p1 * uv + p2 * (r2 + 2.0 * u2);
+    const double dv = v * rad + 2.0 * p2 * uv + p1 * (r2 + 2.0 * v2);
+    *x = K[0] * (u + du) + K[2];
+    *y = K[1] * (v + dv) + K[3];
+  }
+}
+
+// A p + t, contracted (fast route's perturbed camera-2 point)
+__device__ inline void matvec3_t_fma(const double* A, double v0, double v1, double v2, const double* t,
+                                     double pp[3]) {
+#pragma clang fp contract(fast)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) pp[c] = A[3 * c] * v0 + A[3 * c + 1] * v1 + A[3 * c + 2] * v2 + t[c];
+}
+
 // Outcome of one stencil evaluation from its camera-2 point p; false when a
 // decision is inside the margin (caller falls back to semantic_error).
-// mag bounds the magnitudes p was formed from (L1 norms).
-template <int M>
+// mag bounds the magnitudes p was formed from (L1 norms).  FAST: the
+// projection with FMA contraction (world_to_image_fma).
+template <int M, bool FAST = false>
 __device__ inline bool resolve(const SemArgs& a, const double p[3], double mag, float label1, const double* K2,
                                const float2* dl2, const PixelCache& pc, double& f) {
   const double iz = rcp_refined(p[2]);
   const double u = p[0] * iz, v = p[1] * iz;
   double x, y;
-  world_to_image<M>(K2, u, v, &x, &y);
+  if constexpr (FAST)
+    world_to_image_fma<M>(K2, u, v, &x, &y);
+  else
+    world_to_image<M>(K2, u, v, &x, &y);
   if (!(fabs(x) < 1e8 && fabs(y) < 1e8 && fabs(u) < 1e6 && fabs(v) < 1e6)) return false;
   const double kscale = (fabs(K2[0]) + fabs(K2[1])) * distortion_gain<M>(K2, u * u + v * v) *
                         (1.0 + fabs(u) + fabs(v)) * (1.0 + mag * fabs(iz));
@@ -386,7 +428,7 @@ constexpr int kSemRow = 13;      // LDS row: corrected J (12), corrected r
 // tile's J'J / J'r / cost reduced in LDS with one atomic flush per value.
 // Per-sample r / status / J are stored only when requested (parity and
 // download); the solver consumes the pair records.
-template <int M>
+template <int M, bool FAST = false>
 __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, const SemTile* __restrict__ tiles,
                                                                      const PairConst* __restrict__ pcs,
                                                                      double* __restrict__ pair_blk,
@@ -448,8 +490,12 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
         // q1: P_2' = R2 Q(q1')^T (P_c1 - t1) / |q1'|^2 + t2;  q2: P_2' = Q(q2') P_w / |q2'|^2 + t2
         const double* A = P->A[grp == 0 ? e : e - 6];
         const double v0 = grp == 0 ? w[0] : pw[0], v1 = grp == 0 ? w[1] : pw[1], v2 = grp == 0 ? w[2] : pw[2];
+        if constexpr (FAST) {
+          matvec3_t_fma(A, v0, v1, v2, P->t2, pp);
+        } else {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) pp[c] = A[3 * c] * v0 + A[3 * c + 1] * v1 + A[3 * c + 2] * v2 + P->t2[c];
+          for (int c = 0; c < 3; ++c) pp[c] = A[3 * c] * v0 + A[3 * c + 1] * v1 + A[3 * c + 2] * v2 + P->t2[c];
+        }
       } else if (grp == 1) {  // t1: P_2' = P_2 - C (t1' - t1)
         const double dt = pert - P->t1[k];
 #pragma unroll
@@ -460,7 +506,7 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
         for (int c = 0; c < 3; ++c) pp[c] = p2[c] + (c == k ? dt : 0.0);
       }
       double f;
-      if (!resolve<M>(a, pp, mag, smp.label1, K2, dl2, pc, f)) {
+      if (!resolve<M, FAST>(a, pp, mag, smp.label1, K2, dl2, pc, f)) {
         // reference operation sequence for this stencil point
         double qq1[4], tt1[3], qq2[4], tt2[3];
 #pragma unroll
@@ -857,9 +903,14 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
     if (nt == 0) continue;
     dispatch_model(model, [&](auto m) {
       constexpr int M = decltype(m)::value;
-      hipLaunchKernelGGL(semantic_linearize_kernel<M>, dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0, pcs,
-                         S->pair_blk.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr,
-                         write_samples ? 1 : 0);
+      if (ctx->sem_variant == 1)
+        hipLaunchKernelGGL((semantic_linearize_kernel<M, true>), dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0,
+                           pcs, S->pair_blk.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr,
+                           write_samples ? 1 : 0);
+      else
+        hipLaunchKernelGGL((semantic_linearize_kernel<M, false>), dim3(nt), dim3(kBlock), 0, s, a,
+                           S->tiles.ptr + t0, pcs, S->pair_blk.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr,
+                           S->J.ptr, write_samples ? 1 : 0);
     });
   }
   timer_end(ctx, stop);

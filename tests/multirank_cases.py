@@ -31,6 +31,14 @@ def make_case(name):
         rng = np.random.default_rng(2)
         sc.tvec[2:] += rng.uniform(-0.02, 0.02, sc.tvec[2:].shape)
         return sc, sem, mi_ba.default_options(max_num_iterations=10, semantic_weight=0.01, eta=1e-12)
+    if name in ("geo_pcg", "sem_pcg"):
+        # ITERATIVE_SCHUR: one nf-vector all-reduce per Schur product; eta small
+        # so the linear solves are exact to rounding
+        sc, sem, opts = make_case(name[:3])
+        opts.linear_solver_type = mi_ba.SOLVER_ITERATIVE_SCHUR
+        opts.eta = 1e-12
+        opts.max_linear_solver_iterations = 500
+        return sc, sem, opts
     raise KeyError(name)
 
 

@@ -34,16 +34,28 @@ def spd(n, seed=0):
     return G @ G.T / n + np.diag(rng.uniform(0.5, 2.0, n))
 
 
+@pytest.mark.parametrize("own", [2, 6])
 @pytest.mark.parametrize("n", [1700, 2100])
-def test_lookahead_bitwise_equal(gpu, n):
+def test_lookahead_bitwise_equal(gpu, n, own):
     A = spd(n, seed=n)
-    L0, _, i0 = mi_ba.dense_cholesky(A, lookahead=0)
-    L1, _, i1 = mi_ba.dense_cholesky(A, lookahead=1)
+    L0, _, i0 = mi_ba.dense_cholesky(A, lookahead=0, own_diag=own)
+    L1, _, i1 = mi_ba.dense_cholesky(A, lookahead=1, own_diag=own)
     assert i0 == 0 and i1 == 0
     assert np.array_equal(L0, L1)
     # repeatable
-    L2, _, _ = mi_ba.dense_cholesky(A, lookahead=1)
+    L2, _, _ = mi_ba.dense_cholesky(A, lookahead=1, own_diag=own)
     assert np.array_equal(L1, L2)
+
+
+@pytest.mark.parametrize("n", [64, 100, 512, 513, 1000])
+def test_panel_kernel_small_and_ragged(gpu, n):
+    """One-launch panel factor (own_diag 6) at one tile, a ragged tile, one
+    full panel, one panel + 1 row, and a ragged last panel, against LAPACK."""
+    A = spd(n, seed=n + 11)
+    L, _, info = mi_ba.dense_cholesky(A, own_diag=6)
+    assert info == 0
+    L_np = np.linalg.cholesky(A)
+    assert np.abs(L - L_np).max() <= 1e-12 * np.abs(L_np).max()
 
 
 @pytest.mark.parametrize("n", [1700, 2100])
@@ -55,8 +67,8 @@ def test_factor_matches_oracle_and_lapack(gpu, n):
     L_np = np.linalg.cholesky(A)
     x_ref = np.linalg.solve(A, b)
     scale = np.abs(L_o).max()
-    for own in (2, 1, 0):
-        for panel in (512, 0):
+    for own in (6, 2, 1, 0):
+        for panel in ((512, 256) if own == 6 else (512, 0)):
             L, x, info = mi_ba.dense_cholesky(A, b, panel=panel, own_diag=own)
             assert info == 0
             assert np.abs(L - L_o).max() <= 1e-12 * scale, (own, panel)
@@ -93,7 +105,7 @@ def test_not_positive_definite_reports_column(gpu, col):
     A[col, col] = -1.0
     _, info_o = oracle.cholesky(A)
     assert info_o == col + 1
-    for own in (2, 1, 0):
+    for own in (6, 2, 1, 0):
         for la in (0, 1):
             _, _, info = mi_ba.dense_cholesky(A, panel=512, lookahead=la, own_diag=own)
             assert info == col + 1, (own, la, info)

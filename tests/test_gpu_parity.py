@@ -115,6 +115,20 @@ def test_solve_parity(gpu, model):
     assert dk <= 1e-6, dk
 
 
+def test_solve_parity_constant_points(gpu):
+    """Points the config holds constant (AddConstantPoint) next to variable
+    ones: the back substitution / model-cost pass covers the variable points,
+    the blocks of constant points enter the model cost without a point step."""
+    sc = scene(mi_ba.SIMPLE_RADIAL, images=8, points=400, track=4)
+    rng = np.random.default_rng(3)
+    sc.point_config = np.where(rng.uniform(size=sc.num_points) < 0.3, 2, 1).astype(np.uint8)
+    opts = mi_ba.default_options(max_num_iterations=50)
+    s_o, s_g, a, b = assert_solve_parity(opts, sc)
+    const = sc.point_config == 2
+    assert np.array_equal(b.xyz[const], sc.xyz[const])
+    assert np.abs(b.xyz - a.xyz).max() <= 1e-5
+
+
 def test_solve_parity_c1_reference_generator(gpu):
     """Config C1 shape: 20-image SIMPLE_PINHOLE scene, every point in every image."""
     sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_PINHOLE, 20, 200)).gauge()

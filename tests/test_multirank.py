@@ -2,6 +2,8 @@
 
 CPU (gloo, world 2): the shard partition and the host reducer.
 GPU: two ranks on the one visible MI355X, sums through gloo
+(exact Schur: S summed in 512-row bands of its upper triangle; ITERATIVE_SCHUR:
+one nf-vector sum per Schur product)
 (mi_ba_context_set_host_reducer), against the single-process solve of the
 same scene — final cost within 1e-6 relative (north-star tolerance; the two
 runs sum in different orders), cameras/poses bitwise equal across ranks,
@@ -75,7 +77,7 @@ def test_shard_partition(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["geo", "sem"])
+@pytest.mark.parametrize("case", ["geo", "sem", "geo_pcg", "sem_pcg"])
 def test_two_rank_solve_matches_single(gpu, case, tmp_path):
     world = 2
     port = _free_port()

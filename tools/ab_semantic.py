@@ -17,6 +17,7 @@ import bench  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--variants", default="0,1", help="semantic_variant values (0 reference-order fast route, 1 FMA)")
 args = ap.parse_args()
 cfg = bench.CONFIGS["C4"]
 sc, sem = bench.build_shard(cfg, 0, 1)
@@ -25,16 +26,22 @@ ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
 _, _, ns = ctx.dims()
 ctx.evaluate_semantic()
 px, st, r, J = ctx.download_semantic()
-ts = []
-for rnd in range(args.rounds):
-    ctx.set_timing(True)
-    ctx.reset_kernel_times()
-    for _ in range(args.reps):
-        ctx.linearize()
-    ms, n = ctx.kernel_time("semantic_jacobian")
-    ctx.set_timing(False)
-    ts.append(ms / n)
-print(json.dumps({"samples": ns, "median_ms": float(np.median(ts)), "min_ms": float(np.min(ts)),
-                  "valid": int((st == mi_ba.VALID).sum()), "nonzero_J_rows": int((np.abs(J).sum(1) > 0).sum()),
-                  "checksum_J": float(np.abs(J).sum()), "checksum_r": float(r.sum())}))
+for v in [int(x) for x in args.variants.split(",")]:
+    ctx.set_tuning("semantic_variant", v)
+    ctx.evaluate_semantic()
+    _, st_v, r_v, J_v = ctx.download_semantic()
+    same = bool(np.array_equal(st, st_v) and np.array_equal(r, r_v) and np.array_equal(J, J_v))
+    ts = []
+    for rnd in range(args.rounds):
+        ctx.set_timing(True)
+        ctx.reset_kernel_times()
+        for _ in range(args.reps):
+            ctx.linearize()
+        ms, n = ctx.kernel_time("semantic_jacobian")
+        ctx.set_timing(False)
+        ts.append(ms / n)
+    print(json.dumps({"variant": v, "samples": ns, "median_ms": float(np.median(ts)), "min_ms": float(np.min(ts)),
+                      "bitwise_equal_to_variant0": same,
+                      "valid": int((st_v == mi_ba.VALID).sum()), "nonzero_J_rows": int((np.abs(J_v).sum(1) > 0).sum()),
+                      "checksum_J": float(np.abs(J_v).sum()), "checksum_r": float(r_v.sum())}), flush=True)
 ctx.close()
