@@ -64,6 +64,21 @@ def pmc_traffic(config, kernel_prefix):
     return None, None
 
 
+FP64_PEAK_TFS = 78.6  # MI355X vector FP64 (MI355X_MICROARCH.md)
+
+
+def semantic_pmc(config):
+    """FP64 operations and HBM bytes per launch of the semantic kernel from the
+    newest committed PMC summary (profiles/<round>_<config>_semantic_pmc.json,
+    tools/pmc_semantic.sh + tools/summarize_pmc_semantic.py)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config.lower()}_semantic_pmc.json")))
+    if not files:
+        return None, None, None
+    d = json.load(open(files[-1]))
+    return d.get("fp64_ops_per_launch"), d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def bytes_per_block(model, track):
     return 24 + 24.0 / track + 16 + 16 * (9 + CAM_TANGENT[model])
 
@@ -179,6 +194,28 @@ def cpu_baseline(opts, sc, sem, cfg, nb, ns):
             "reproj_blocks_per_s": rate_geo, "semantic_samples_per_s": rate_sem,
             "cpu_model": model, "host_nproc": nproc, "affinity_cpus": affinity,
             "threads_note": "threads = the job's CPU share (OMP_NUM_THREADS on the GPU box), capped by the affinity mask"}
+
+
+def roofline_semantic(config, ns, avg_ms):
+    """The semantic kernel against both roofs (FP64-bound by
+    construction): FP64 from PMC operation counts, HBM from PMC traffic, per
+    launch, over the launch time measured here (HIP events on the context
+    stream).  Algorithmic bytes: 32 (sample record) + 8 (compulsory raster
+    gather) per sample; the per-pair records are negligible."""
+    flops, hbm, src = semantic_pmc(config)
+    if avg_ms <= 0:
+        return None
+    t = avg_ms * 1e-3
+    alg = 40.0 * ns
+    out = {"kernel": "semantic_linearize", "bound": "fp64", "unit": "TFLOP/s", "peak": FP64_PEAK_TFS,
+           "achieved": flops / t / 1e12 if flops else None,
+           "frac": flops / t / 1e12 / FP64_PEAK_TFS if flops else None,
+           "fp64_ops_per_launch": flops, "traffic": hbm, "traffic_unit": "bytes/launch",
+           "hbm_achieved_GBs": hbm / t / 1e9 if hbm else None,
+           "hbm_frac": hbm / t / 1e9 / HBM_PEAK_GBS if hbm else None,
+           "algorithmic_bytes_per_launch": alg, "samples_per_launch": ns, "avg_launch_ms": avg_ms,
+           "pmc_source": src}
+    return out
 
 
 def main():
@@ -333,6 +370,7 @@ def main():
                          "algorithmic_bytes_per_launch": bpb * nb,
                          "bytes_per_block": bpb, "blocks_per_launch": nb, "avg_launch_ms": avg_j},
             "kernels_ms": {"reproj_jacobian": avg_j, "semantic_jacobian": s_ms / max(1, s_n)},
+            "roofline_semantic": roofline_semantic(args.config, ns, s_ms / max(1, s_n)) if ns and world == 1 else None,
             "reproj_blocks_per_s": nb * world / (avg_j * 1e-3) if avg_j > 0 else None,
             "setup_s": setup_s,
         }

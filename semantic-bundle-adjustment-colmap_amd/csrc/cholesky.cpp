@@ -565,26 +565,63 @@ __device__ __forceinline__ void pf_gemm_nt(pf_dvec4 (&acc)[4], double sign, LX l
   }
 }
 
-// accumulator <-> column-major 64x64 LDS tile
+// LDS tiles are row-major with a padded stride (MFMA operand reads of 16
+// consecutive rows then fall in distinct banks)
+constexpr int kPfLd = 65;
+
+// accumulator -> LDS tile T[i * kPfLd + j]
 __device__ __forceinline__ void pf_acc_to_lds(const pf_dvec4 (&acc)[4], double* T, int w, int lane) {
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) T[(16 * t + (lane & 15)) * 64 + 16 * w + 4 * q + (lane >> 4)] = acc[t][q];
+    for (int q = 0; q < 4; ++q) T[(16 * w + 4 * q + (lane >> 4)) * kPfLd + 16 * t + (lane & 15)] = acc[t][q];
+}
+
+
+// accumulator -> LDS tile transposed, T[j * kPfLd + i] = D[i][j]: the
+// column-major view of T is D (the diagonal step factors D's lower triangle,
+// the only half of S the caller filled)
+__device__ __forceinline__ void pf_acc_to_lds_t(const pf_dvec4 (&acc)[4], double* T, int w, int lane) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) T[(16 * t + (lane & 15)) * kPfLd + 16 * w + 4 * q + (lane >> 4)] = acc[t][q];
+}
+
+// One wave, lane = column j: Li = L^-1 (row-major padded) from L in T
+// (row-major padded, unit-free) and the pivot reciprocals dinv: forward
+// substitution over rows, the solved rows kept in Li itself (lane-contiguous
+// reads), L's row read as contiguous broadcasts, four partial sums per row.
+__device__ void pf_inv_wave(const double* L, int ldl, const double* dinv, double* Li, int lane) {
+  for (int i = 0; i < 64; ++i) {
+    const double* Lrow = L + i * ldl;
+    double s0 = (i == lane) ? 1.0 : 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int k = 0;
+    for (; k + 3 < i; k += 4) {
+      s0 -= Lrow[k] * Li[k * kPfLd + lane];
+      s1 -= Lrow[k + 1] * Li[(k + 1) * kPfLd + lane];
+      s2 -= Lrow[k + 2] * Li[(k + 2) * kPfLd + lane];
+      s3 -= Lrow[k + 3] * Li[(k + 3) * kPfLd + lane];
+    }
+    for (; k < i; ++k) s0 -= Lrow[k] * Li[k * kPfLd + lane];
+    Li[i * kPfLd + lane] = ((s0 + s1) + (s2 + s3)) * dinv[i];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  }
 }
 
 // In-LDS Cholesky of a 64x64 column-major tile (lower), blocked by kStep
 // columns (diag_panel_blocked_kernel's factor loop); returns the first
 // non-positive pivot (1-based) or 0.
 template <int kStep, int NW>
-__device__ int tile_chol_lds(double* L, double* nb, int lane, int wv) {
+__device__ int tile_chol_lds(double* L, double* nb, int lane, int wv, int ld = 64) {
   int bad = 0;
   for (int jb = 0; jb < 64; jb += kStep) {
     double d[kStep][kStep];
 #pragma unroll
     for (int i = 0; i < kStep; ++i)
 #pragma unroll
-      for (int k = 0; k <= i; ++k) d[i][k] = L[(jb + k) * 64 + jb + i];
+      for (int k = 0; k <= i; ++k) d[i][k] = L[(jb + k) * ld + jb + i];
 #pragma unroll
     for (int k = 0; k < kStep; ++k) {
       const double piv = d[k][k];
@@ -601,7 +638,7 @@ __device__ int tile_chol_lds(double* L, double* nb, int lane, int wv) {
     if (lane >= jb + kStep) {
 #pragma unroll
       for (int k = 0; k < kStep; ++k) {
-        double v = L[(jb + k) * 64 + lane];
+        double v = L[(jb + k) * ld + lane];
 #pragma unroll
         for (int m = 0; m < k; ++m) v -= y[m] * d[k][m];
         y[k] = v / d[k][k];
@@ -624,25 +661,32 @@ __device__ int tile_chol_lds(double* L, double* nb, int lane, int wv) {
     if (wv == 0) {
 #pragma unroll
       for (int k = 0; k < kStep; ++k)
-        if (lane >= jb + k) L[(jb + k) * 64 + lane] = y[k];
+        if (lane >= jb + k) L[(jb + k) * ld + lane] = y[k];
     }
     for (int c = jb + kStep + wv; c < 64; c += NW) {
-      double v = L[c * 64 + lane];
+      double v = L[c * ld + lane];
 #pragma unroll
       for (int k = 0; k < kStep; ++k) v -= y[k] * nb[k * 64 + c];
-      L[c * 64 + lane] = v;
+      L[c * ld + lane] = v;
     }
     __syncthreads();
   }
   return bad;
 }
 
+// dbg (nullable, probes only): wall_clock64() stamps [row tile][20]: 0 start,
+// 1 + 2c after step c's waits (diagonal step: after the factor), 2 + 2c at
+// step c's end.
+constexpr int kPfDbgSlots = 20;
+
 __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ A, int lda, int kb, int mrows,
                                                            int* __restrict__ info, double* __restrict__ linv,
-                                                           unsigned* ctrl, unsigned base, unsigned epoch) {
-  __shared__ double T[64 * 64];   // column-major staging / factor tile
-  __shared__ double Li[64 * 64];  // diagonal tile inverse
-  __shared__ double nbuf[4 * 64];
+                                                           unsigned* ctrl, unsigned base, unsigned epoch,
+                                                           unsigned long long* dbg = nullptr) {
+  __shared__ double T[64 * kPfLd];   // staging / factor tile (row-major padded)
+  __shared__ double Li[64 * kPfLd];  // a diagonal tile's inverse (own, or workgroup c's)
+  __shared__ double Lc[64 * 64];     // the factor's columns (pf_chol_inv_wave)
+  __shared__ double dinv[64];
   __shared__ int s_r;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_r = (int)(atomicAdd(ctrl, 1u) - base);
@@ -650,6 +694,13 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
   const int r = s_r;
   const int nc = (kb + 63) / 64;
   unsigned* flag = ctrl + 1;  // [8][8]: tile (r, c) of the diagonal block rows final in A
+  auto stamp = [&](int slot) {
+    if (dbg && threadIdx.x == 0) dbg[(size_t)r * kPfDbgSlots + slot] = wall_clock64();
+  };
+  stamp(0);
+  // the panel's info starts at 0 (row tile 0 clears it before its first
+  // release; every other write follows one of its flags)
+  if (r == 0 && threadIdx.x == 0) *info = 0;
   const int r0 = pf_row0(r, kb, nc), hr = pf_rows(r, kb, nc, mrows);
   const int cmax = min(r, nc - 1);
   const bool diag_row = r < nc;
@@ -661,7 +712,7 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
       return (i < h && j < w) ? v : 0.0;
     };
   };
-  auto ltile = [&](const double* S) { return [=](int i, int j) { return S[j * 64 + i]; }; };
+  auto ltile = [&](const double* S) { return [=](int i, int j) { return S[i * kPfLd + j]; }; };
   // the diagonal tile's running accumulator (diagonal-block rows)
   pf_dvec4 dacc[4];
   if (diag_row) {
@@ -692,14 +743,17 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
         pf_gemm_nt(acc, -1.0, gtile(r0, hr, 64 * k, 64), gtile(c0, wc, 64 * k, 64), wv, lane);
       }
       pf_wait(flag + c * kPfMaxTiles + c, epoch);
-      // L_rc = T Linv_cc'
+      stamp(1 + 2 * c);
+      // L_rc = T Linv_cc' (Linv_cc row-major in linv, staged in LDS)
       pf_acc_to_lds(acc, T, wv, lane);
+      const double* lc = linv + (size_t)c * 64 * 64;
+#pragma unroll
+      for (int e = threadIdx.x; e < 64 * 64; e += 256) Li[(e >> 6) * kPfLd + (e & 63)] = lc[e];
       __syncthreads();
       pf_dvec4 out[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) out[t] = pf_dvec4{0.0, 0.0, 0.0, 0.0};
-      const double* lc = linv + (size_t)c * 64 * 64;
-      pf_gemm_nt(out, 1.0, ltile(T), [=](int i, int j) { return lc[j * 64 + i]; }, wv, lane);
+      pf_gemm_nt(out, 1.0, ltile(T), ltile(Li), wv, lane);
       __syncthreads();  // every wave is done reading T
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -719,38 +773,42 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
         pf_gemm_nt(dacc, -1.0, ltile(T), ltile(T), wv, lane);
         __syncthreads();
       }
+      stamp(2 + 2 * c);
       continue;
     }
     // c == r: factor the diagonal tile, invert it, publish both
-    pf_acc_to_lds(dacc, T, wv, lane);
+    pf_acc_to_lds_t(dacc, T, wv, lane);
     __syncthreads();
-    const int bad = tile_chol_lds<4, 4>(T, nbuf, lane, wv);
+    __shared__ int s_bad;
+    // factor in LDS (4 waves, tile_chol_lds on the column-major view), then
+    // the inverse by wave 0
+    const int bad = tile_chol_lds<4, 4>(T, Lc, lane, wv, kPfLd);
     if (wv == 0) {
-      // Li = L^-1 (lower): lane = column, forward substitution over rows
-      const double dinv = 1.0 / T[lane * 64 + lane];
-      double x[64];
-#pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        double s = (i == lane) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < i; ++k) s -= T[k * 64 + i] * x[k];
-        x[i] = s * readlane_f64(dinv, i);
-      }
-#pragma unroll
-      for (int i = 0; i < 64; ++i) Li[lane * 64 + i] = x[i];
+      dinv[lane] = 1.0 / T[lane * kPfLd + lane];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      // L[i][k] = T[k * kPfLd + i] (column-major view): transpose into Lc rows
+      // for the contiguous row reads of pf_inv_wave
+      for (int i = 0; i < 64; ++i) Lc[i * 64 + lane] = lane <= i ? T[lane * kPfLd + i] : 0.0;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      pf_inv_wave(Lc, 64, dinv, Li, lane);
+      if (lane == 0) s_bad = bad;
     }
     __syncthreads();
+    stamp(1 + 2 * c);
     double* lo = linv + (size_t)c * 64 * 64;
     for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-      lo[e] = Li[e];
+      lo[e] = Li[(e >> 6) * kPfLd + (e & 63)];  // row-major, ld 64
       const int i = e & 63, j = e >> 6;
-      if (i < wc && j < wc && i >= j) A[(size_t)(c0 + j) * lda + c0 + i] = T[e];
+      if (i < wc && j < wc && i >= j) A[(size_t)(c0 + j) * lda + c0 + i] = T[j * kPfLd + i];  // column-major view
     }
-    if (threadIdx.x == 0 && bad != 0 && bad <= wc) atomicCAS(info, 0, c0 + bad);
+    if (threadIdx.x == 0 && s_bad != 0 && s_bad <= wc) atomicCAS(info, 0, c0 + s_bad);
     __threadfence();
     __syncthreads();
     if (threadIdx.x == 0)
       __hip_atomic_store(flag + r * kPfMaxTiles + r, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    stamp(2 + 2 * c);
   }
 }
 
@@ -897,7 +955,6 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   if (!ws || !ws->pf_ctrl || !ws->pf_linv || kb > 64 * kPfMaxTiles) return rocblas_status_invalid_pointer;
   hipStream_t s;
   if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
-  if (hipMemsetAsync(info, 0, sizeof(int), s) != hipSuccess) return rocblas_status_internal_error;
   const int mrows = n - k;
   const int nc = (kb + 63) / 64;
   const int nr = nc + (mrows - kb + 63) / 64;

@@ -43,7 +43,7 @@ struct CholConfig {
   // ~300 us, instruction-fetch bound.)
   // 6: one panel_factor_kernel launch per panel for the diagonal block AND the
   // panel's solve below it (no dtrsm; panel <= 512)
-  int own_diag = 2;
+  int own_diag = 2;  // 6 measured slower at nf = 12 000 (26.0 vs 25.0 ms; profiles/r2_panel_probe_v2.txt: 64x64 factor + inverse ~95 us per step)
   // chol_solve variant: 2 sync-free sweeps (one launch per direction), 1 one
   // launch per 64-wide block column with diagonal-block inverses, 0 recursive
   // rocBLAS dtrsv / dgemv

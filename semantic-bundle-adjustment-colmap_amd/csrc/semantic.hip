@@ -428,6 +428,71 @@ constexpr int kSemRow = 13;      // LDS row: corrected J (12), corrected r
 // tile's J'J / J'r / cost reduced in LDS with one atomic flush per value.
 // Per-sample r / status / J are stored only when requested (parity and
 // download); the solver consumes the pair records.
+// Reference-order evaluation of one stencil point (the fallback when
+// resolve's margins are not cleared), out of line: four group loops share it.
+template <int M>
+__device__ __forceinline__ double stencil_reference(const SemArgs& a, const PairConst* __restrict__ P, int grp, int k,
+                                                 double pert, const double pc1[3], float label1, const double* K2,
+                                                 const float2* dl2) {
+  double qq1[4], tt1[3], qq2[4], tt2[3];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    qq1[c] = (grp == 0 && c == k) ? pert : P->q1[c];
+    qq2[c] = (grp == 2 && c == k) ? pert : P->q2[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    tt1[c] = (grp == 1 && c == k) ? pert : P->t1[c];
+    tt2[c] = (grp == 3 && c == k) ? pert : P->t2[c];
+  }
+  int st2;
+  return semantic_error<M>(a, pc1, label1, qq1, tt1, qq2, tt2, K2, dl2, &st2);
+}
+
+// One stencil point e (ambient coordinate k of group GRP: 0 q1, 1 t1, 2 q2,
+// 3 t2): the perturbed camera-2 point from the pair table, its outcome by
+// resolve, or the reference sequence inside the margins.
+template <int M, bool FAST, int GRP>
+__device__ __forceinline__ double stencil_point(const SemArgs& a, const PairConst* __restrict__ P, int e, int k,
+                                                const double w[3], const double pw[3], const double p2[3],
+                                                double mag, const double pc1[3], float label1, const double* K2,
+                                                const float2* dl2, const PixelCache& pc) {
+  const double pert = P->pert[e];
+  double pp[3];
+  if constexpr (GRP == 0 || GRP == 2) {
+    // q1: P_2' = R2 Q(q1')^T (P_c1 - t1) / |q1'|^2 + t2;  q2: P_2' = Q(q2') P_w / |q2'|^2 + t2
+    const double* A = P->A[GRP == 0 ? e : e - 6];
+    const double* v = GRP == 0 ? w : pw;
+    if constexpr (FAST) {
+      matvec3_t_fma(A, v[0], v[1], v[2], P->t2, pp);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pp[c] = A[3 * c] * v[0] + A[3 * c + 1] * v[1] + A[3 * c + 2] * v[2] + P->t2[c];
+    }
+  } else if constexpr (GRP == 1) {  // t1: P_2' = P_2 - C (t1' - t1)
+    const double dt = pert - P->t1[k];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) pp[c] = p2[c] - dt * P->C[3 * c + k];
+  } else {  // t2: P_2' = P_2 + (t2' - t2)
+    const double dt = pert - P->t2[k];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) pp[c] = p2[c] + (c == k ? dt : 0.0);
+  }
+  double f;
+  if (!resolve<M, FAST>(a, pp, mag, label1, K2, dl2, pc, f))
+    f = stencil_reference<M>(a, P, GRP, k, pert, pc1, label1, K2, dl2);
+  return f;
+}
+
+// One workgroup per pair-aligned tile of <= 256 samples, one lane per sample:
+// centre residual (reference sequence), the CENTRAL stencil over the
+// variable poses' ambient parameters (one rolled loop per parameter group, so
+// the tangent row stays in registers), QuaternionManifold / SubsetManifold,
+// the ScaledLoss Corrector, and the tile's J'J / J'r / cost reduced through
+// LDS in two 128-row halves (13 KB of LDS per workgroup: occupancy is set by
+// registers, not LDS) with one atomic flush per value.  Per-sample r /
+// status / J are stored only when requested (parity and download); the
+// solver consumes the pair records.
 template <int M, bool FAST = false>
 __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, const SemTile* __restrict__ tiles,
                                                                      const PairConst* __restrict__ pcs,
@@ -436,7 +501,8 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
                                                                      double* __restrict__ r_out,
                                                                      int32_t* __restrict__ status_out,
                                                                      double* __restrict__ J_out, int write_samples) {
-  __shared__ double sJ[kBlock * kSemRow];
+  constexpr int kHalf = kBlock / 2;
+  __shared__ double sJ[kHalf * kSemRow];
   __shared__ double spart[2 * kPairVals];
   __shared__ double sred[4];
   const SemTile t = tiles[blockIdx.x];
@@ -445,7 +511,9 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
   const bool active = tid < (int)t.count;
   const int64_t n = (int64_t)t.start + tid;
   double cost = 0.0;
-  double* row = sJ + tid * kSemRow;
+  double rowv[kSemRow];
+#pragma unroll
+  for (int k = 0; k < kSemRow; ++k) rowv[k] = 0.0;
   if (active) {
     const SemSample smp = a.samples[n];
     const float2* dl2 = a.dl + (size_t)P->slot * a.H * a.W;
@@ -467,79 +535,79 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
                        fabs(P->t1[2]) + fabs(pw[0]) + fabs(pw[1]) + fabs(pw[2]) + fabs(P->t2[0]) +
                        fabs(P->t2[1]) + fabs(P->t2[2]);
     // Stencil: parameter m = 0..13 over (q1, t1, q2, t2), + then - (Ceres
-    // CENTRAL order).  Everything that depends only on the pair and the
-    // stencil point (perturbed value, 1/(2 delta), the perturbed rotation
-    // folded into one 3x3 map, PlusJacobian rows) comes from the per-pair
-    // table as wave-uniform scalar loads; a lane forms one mat-vec per point.
-    // Tangent columns accumulate in the lane's LDS row in m order from 0.0,
+    // CENTRAL order), e = 2 m + minus.  Everything that depends only on the
+    // pair and the stencil point (perturbed value, 1/(2 delta), the
+    // perturbed rotation folded into one 3x3 map, PlusJacobian rows) comes
+    // from the per-pair table as wave-uniform scalar loads; a lane forms one
+    // mat-vec per point.  Tangent columns accumulate from 0.0 in m order,
     // exactly as J_tangent = J_ambient * PlusJacobian does.
     const double w[3] = {smp.pc1[0] - P->t1[0], smp.pc1[1] - P->t1[1], smp.pc1[2] - P->t1[2]};
-#pragma unroll
-    for (int k = 0; k < 12; ++k) row[k] = 0.0;
-    double fplus = 0.0;
+    double jq1[3] = {0.0, 0.0, 0.0}, jt1[3] = {0.0, 0.0, 0.0}, jq2[3] = {0.0, 0.0, 0.0}, jt2[3] = {0.0, 0.0, 0.0};
+    if (P->var1) {
 #pragma unroll 1
-    for (int e = 0; e < 28; ++e) {
-      const int m = e >> 1;
-      const bool minus = e & 1;
-      const int grp = m < 4 ? 0 : (m < 7 ? 1 : (m < 11 ? 2 : 3));
-      if (grp < 2 ? !P->var1 : !P->var2) continue;
-      const int k = m - (grp == 0 ? 0 : (grp == 1 ? 4 : (grp == 2 ? 7 : 11)));
-      const double pert = P->pert[e];
-      double pp[3];
-      if (grp == 0 || grp == 2) {
-        // q1: P_2' = R2 Q(q1')^T (P_c1 - t1) / |q1'|^2 + t2;  q2: P_2' = Q(q2') P_w / |q2'|^2 + t2
-        const double* A = P->A[grp == 0 ? e : e - 6];
-        const double v0 = grp == 0 ? w[0] : pw[0], v1 = grp == 0 ? w[1] : pw[1], v2 = grp == 0 ? w[2] : pw[2];
-        if constexpr (FAST) {
-          matvec3_t_fma(A, v0, v1, v2, P->t2, pp);
-        } else {
-#pragma unroll
-          for (int c = 0; c < 3; ++c) pp[c] = A[3 * c] * v0 + A[3 * c + 1] * v1 + A[3 * c + 2] * v2 + P->t2[c];
+      for (int m = 0; m < 4; ++m) {
+        double fp = 0.0, fm = 0.0;
+#pragma unroll 1
+        for (int sg = 0; sg < 2; ++sg) {
+          const double f = stencil_point<M, FAST, 0>(a, P, 2 * m + sg, m, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc);
+          fp = sg == 0 ? f : fp;
+          fm = sg == 1 ? f : fm;
         }
-      } else if (grp == 1) {  // t1: P_2' = P_2 - C (t1' - t1)
-        const double dt = pert - P->t1[k];
+        const double jm = (fp - fm) * P->ood[m];
+        const double* pj = P->pj[m];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) pp[c] = p2[c] - dt * P->C[3 * c + k];
-      } else {  // t2: P_2' = P_2 + (t2' - t2)
-        const double dt = pert - P->t2[k];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) pp[c] = p2[c] + (c == k ? dt : 0.0);
+        for (int c = 0; c < 3; ++c) jq1[c] = jq1[c] + jm * pj[c];
       }
-      double f;
-      if (!resolve<M, FAST>(a, pp, mag, smp.label1, K2, dl2, pc, f)) {
-        // reference operation sequence for this stencil point
-        double qq1[4], tt1[3], qq2[4], tt2[3];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          qq1[c] = (grp == 0 && c == k) ? pert : P->q1[c];
-          qq2[c] = (grp == 2 && c == k) ? pert : P->q2[c];
+#pragma unroll 1
+      for (int k = 0; k < 3; ++k) {
+        const int m = 4 + k;
+        double fp = 0.0, fm = 0.0;
+#pragma unroll 1
+        for (int sg = 0; sg < 2; ++sg) {
+          const double f = stencil_point<M, FAST, 1>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc);
+          fp = sg == 0 ? f : fp;
+          fm = sg == 1 ? f : fm;
         }
+        const double jm = (fp - fm) * P->ood[m];
+        const double v = ((P->mask1 >> k) & 1u) ? 0.0 : jm;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          tt1[c] = (grp == 1 && c == k) ? pert : P->t1[c];
-          tt2[c] = (grp == 3 && c == k) ? pert : P->t2[c];
-        }
-        int st2;
-        f = semantic_error<M>(a, smp.pc1, smp.label1, qq1, tt1, qq2, tt2, K2, dl2, &st2);
-      }
-      if (!minus) {
-        fplus = f;
-        continue;
-      }
-      const double jm = (fplus - f) * P->ood[m];
-      if (grp == 0 || grp == 2) {
-        double* jr = row + (grp == 0 ? 0 : 6);
-        const double* pj = P->pj[(grp == 0 ? 0 : 4) + k];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) jr[c] = jr[c] + jm * pj[c];
-      } else {
-        const uint32_t mask = grp == 1 ? P->mask1 : P->mask2;
-        row[(grp == 1 ? 3 : 9) + k] = ((mask >> k) & 1u) ? 0.0 : jm;
+        for (int c = 0; c < 3; ++c) jt1[c] = c == k ? v : jt1[c];
       }
     }
-    double Jt[12];
+    if (P->var2) {
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) {
+        const int m = 7 + k;
+        double fp = 0.0, fm = 0.0;
+#pragma unroll 1
+        for (int sg = 0; sg < 2; ++sg) {
+          const double f = stencil_point<M, FAST, 2>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc);
+          fp = sg == 0 ? f : fp;
+          fm = sg == 1 ? f : fm;
+        }
+        const double jm = (fp - fm) * P->ood[m];
+        const double* pj = P->pj[4 + k];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) Jt[k] = row[k];
+        for (int c = 0; c < 3; ++c) jq2[c] = jq2[c] + jm * pj[c];
+      }
+#pragma unroll 1
+      for (int k = 0; k < 3; ++k) {
+        const int m = 11 + k;
+        double fp = 0.0, fm = 0.0;
+#pragma unroll 1
+        for (int sg = 0; sg < 2; ++sg) {
+          const double f = stencil_point<M, FAST, 3>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc);
+          fp = sg == 0 ? f : fp;
+          fm = sg == 1 ? f : fm;
+        }
+        const double jm = (fp - fm) * P->ood[m];
+        const double v = ((P->mask2 >> k) & 1u) ? 0.0 : jm;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) jt2[c] = c == k ? v : jt2[c];
+      }
+    }
+    const double Jt[12] = {jq1[0], jq1[1], jq1[2], jt1[0], jt1[1], jt1[2],
+                           jq2[0], jq2[1], jq2[2], jt2[0], jt2[1], jt2[2]};
     if (write_samples) {
       r_out[n] = r;
       status_out[n] = st;
@@ -553,14 +621,14 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
     cost = 0.5 * (a.weight * rho[0]);
     const double sc = sqrt(a.weight * rho[1]);
 #pragma unroll
-    for (int m = 0; m < 12; ++m) row[m] = Jt[m] * sc;
-    row[12] = r * sc;
+    for (int m = 0; m < 12; ++m) rowv[m] = Jt[m] * sc;
+    rowv[12] = r * sc;
   }
-  __syncthreads();
-  // tile J'J (78) and J'r (12): 2 x 90 threads over interleaved samples
+  // tile J'J (78) and J'r (12): the rows pass through LDS in two halves
+  // (threads 0..127, then 128..255); 2 x 90 threads over interleaved rows
+  int ca = 0, cb = 0;
+  const int h = tid / kPairVals, e = tid - h * kPairVals;
   if (tid < 2 * kPairVals) {
-    const int h = tid / kPairVals, e = tid - h * kPairVals;
-    int ca, cb;
     if (e < 78) {
       int a_ = 0, rem = e;
       while (rem >= 12 - a_) { rem -= 12 - a_; ++a_; }
@@ -570,10 +638,22 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
       ca = e - 78;
       cb = 12;
     }
-    double acc = 0.0;
-    for (int s = h; s < (int)t.count; s += 2) acc += sJ[s * kSemRow + ca] * sJ[s * kSemRow + cb];
-    spart[tid] = acc;
   }
+  double acc = 0.0;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (tid / kHalf == half) {
+      double* row = sJ + (tid - half * kHalf) * kSemRow;
+#pragma unroll
+      for (int k = 0; k < kSemRow; ++k) row[k] = rowv[k];
+    }
+    __syncthreads();
+    const int cnt = min(kHalf, (int)t.count - half * kHalf);
+    if (tid < 2 * kPairVals)
+      for (int q = h; q < cnt; q += 2) acc += sJ[q * kSemRow + ca] * sJ[q * kSemRow + cb];
+    __syncthreads();
+  }
+  if (tid < 2 * kPairVals) spart[tid] = acc;
   double v = cost;
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   if ((tid & 63) == 0) sred[tid >> 6] = v;

@@ -47,6 +47,20 @@ def test_lookahead_bitwise_equal(gpu, n, own):
     assert np.array_equal(L1, L2)
 
 
+@pytest.mark.parametrize("own", [2, 6, 0])
+def test_factor_reads_lower_triangle_only(gpu, own):
+    """The LM fills only S's column-major lower triangle (its row-major upper
+    half, csrc/kernels.hip dense_u / schur_pairs): the strict upper
+    triangle of A holds junk and must not be read."""
+    n = 1300
+    A = spd(n, seed=21)
+    junk = np.triu(np.random.default_rng(5).uniform(-1e6, 1e6, (n, n)), 1)
+    L, _, info = mi_ba.dense_cholesky(np.tril(A) + junk, own_diag=own)
+    assert info == 0
+    L_np = np.linalg.cholesky(A)
+    assert np.abs(L - L_np).max() <= 1e-12 * np.abs(L_np).max()
+
+
 @pytest.mark.parametrize("n", [64, 100, 512, 513, 1000])
 def test_panel_kernel_small_and_ragged(gpu, n):
     """One-launch panel factor (own_diag 6) at one tile, a ragged tile, one

@@ -1,0 +1,64 @@
+// Phase timeline of one panel_factor_kernel launch (csrc/cholesky.cpp,
+// own_diag 6) on the first 512-wide panel of an nf = 12 000 SPD matrix:
+// wall_clock64() stamps per row tile (kernel's dbg buffer).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/panel_probe.cpp -lrocsolver -lrocblas -o tools/panel_probe.bin
+#include "../../semantic-bundle-adjustment-colmap_amd/csrc/cholesky.cpp"
+
+#include <cstdio>
+
+__global__ void fill_spd(double* A, int n) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= (size_t)n * n) return;
+  int r = i % n, c = i / n;
+  A[i] = (r == c) ? n * 0.02 + 1.0 : 0.01 * sin(0.37 * (r + c)) + 0.005 * cos(0.011 * (double)r * c);
+}
+
+int main(int argc, char** argv) {
+  using namespace miba;
+  const int n = argc > 1 ? atoi(argv[1]) : 12000;
+  const int kb = 512;
+  double* A;
+  int* info;
+  unsigned long long* dbg;
+  hipMalloc(&A, 8ull * n * n);
+  hipMalloc(&info, 64);
+  const int nr = 8 + (n - kb + 63) / 64;
+  hipMalloc(&dbg, 8ull * nr * kPfDbgSlots);
+  CholWorkspace ws;
+  ws.create(0, (n + 511) / 512, n);
+  for (int rep = 0; rep < 3; ++rep) {
+    hipLaunchKernelGGL(fill_spd, dim3((unsigned)(((size_t)n * n + 255) / 256)), dim3(256), 0, 0, A, n);
+    hipMemset(dbg, 0, 8ull * nr * kPfDbgSlots);
+    hipMemset(info, 0, 4);
+    hipDeviceSynchronize();
+    const unsigned epoch = ++ws.pf_epoch;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0, 0);
+    hipLaunchKernelGGL(panel_factor_kernel, dim3(nr), dim3(256), 0, 0, A, n, kb, n, info, ws.pf_linv, ws.pf_ctrl,
+                       ws.pf_base, epoch, dbg);
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    ws.pf_base += nr;
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    std::vector<unsigned long long> h((size_t)nr * kPfDbgSlots);
+    hipMemcpy(h.data(), dbg, 8ull * h.size(), hipMemcpyDeviceToHost);
+    unsigned long long t0 = ~0ull;
+    for (int r = 0; r < nr; ++r) t0 = std::min(t0, h[(size_t)r * kPfDbgSlots]);
+    int hinfo = 0;
+    hipMemcpy(&hinfo, info, 4, hipMemcpyDeviceToHost);
+    printf("rep %d: kernel %.1f us, info %d (stamps in us from the first start, 100 MHz clock)\n", rep, ms * 1e3, hinfo);
+    for (int r = 0; r < nr; ++r) {
+      if (r > 9 && r != nr - 1) continue;
+      printf("  row %3d:", r);
+      for (int k = 0; k < kPfDbgSlots; ++k) {
+        const unsigned long long v = h[(size_t)r * kPfDbgSlots + k];
+        if (v) printf(" %d:%.1f", k, (v - t0) / 100.0);
+      }
+      printf("\n");
+    }
+  }
+  return 0;
+}
