@@ -84,6 +84,9 @@ struct mi_ba_context {
   miba::DevArray<miba::DevPoint> vpoints;
   int64_t npv = 0;
   int64_t nb_const = 0;  // reduced blocks of constant points
+  bool lin_overlap = false;            // semantic kernel on lin_side beside the reprojection kernel
+  hipStream_t lin_side = nullptr;
+  hipEvent_t lin_ev[2] = {nullptr, nullptr};
   int sem_variant = 1;   // semantic kernel: 1 FMA-contracted fast route (bitwise-equal outputs, 0.90 vs 0.93 ms at C4), 0 uncontracted ("semantic_variant")
 
   // linearization

@@ -535,6 +535,12 @@ void context_destroy(mi_ba_context* ctx) {
   if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   if (ctx->host_scalars) (void)hipHostFree(ctx->host_scalars);
+  if (ctx->lin_side) {
+    (void)hipStreamSynchronize(ctx->lin_side);
+    (void)hipStreamDestroy(ctx->lin_side);
+  }
+  if (ctx->lin_ev[0]) (void)hipEventDestroy(ctx->lin_ev[0]);
+  if (ctx->lin_ev[1]) (void)hipEventDestroy(ctx->lin_ev[1]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -547,11 +553,33 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   MI_HIP(hipMemsetAsync(ctx->scalars.ptr, 0, sizeof(double) * kNumScalars, s));
   hipEvent_t stop;
   launch_pack_images(d, ctx->img_rec.ptr, s);
+  // linearize_overlap: the semantic kernel (FP64/latency-bound) on a second
+  // stream beside the reprojection kernel (HBM-write-bound); joined below
+  const bool overlap = ctx->sem && ctx->lin_overlap;
+  if (overlap) {
+    if (!ctx->lin_side) {
+      if (hipStreamCreateWithFlags(&ctx->lin_side, hipStreamNonBlocking) != hipSuccess) {
+        ctx->lin_side = nullptr;
+        return MI_BA_ERR_HIP;
+      }
+      MI_HIP(hipEventCreateWithFlags(&ctx->lin_ev[0], hipEventDisableTiming));
+      MI_HIP(hipEventCreateWithFlags(&ctx->lin_ev[1], hipEventDisableTiming));
+    }
+    MI_HIP(hipEventRecord(ctx->lin_ev[0], s));
+    MI_HIP(hipStreamWaitEvent(ctx->lin_side, ctx->lin_ev[0], 0));
+    ctx->stream = ctx->lin_side;  // semantic_linearize launches (and times) on ctx->stream
+    mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
+    ctx->stream = s;
+    if (st != MI_BA_OK) return st;
+    MI_HIP(hipEventRecord(ctx->lin_ev[1], ctx->lin_side));
+  }
   timer_begin(ctx, "reproj_jacobian", &stop);
   launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->partial.ptr, s);
   timer_end(ctx, stop);
   if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s);
-  if (ctx->sem) {
+  if (overlap) {
+    MI_HIP(hipStreamWaitEvent(s, ctx->lin_ev[1], 0));
+  } else if (ctx->sem) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
   }
@@ -1341,6 +1369,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   if (!ctx || !key) return MI_BA_ERR_INVALID_ARGUMENT;
   if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 63) {
     ctx->dev.jvariant = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "linearize_overlap") == 0 && (value == 0 || value == 1)) {
+    ctx->lin_overlap = value != 0;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "semantic_variant") == 0 && (value == 0 || value == 1)) {

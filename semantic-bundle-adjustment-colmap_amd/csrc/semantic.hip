@@ -263,10 +263,31 @@ __device__ inline void matvec3_t_fma(const double* A, double v0, double v1, doub
 // decision is inside the margin (caller falls back to semantic_error).
 // mag bounds the magnitudes p was formed from (L1 norms).  FAST: the
 // projection with FMA contraction (world_to_image_fma).
+// FAST also takes the pixel margin's model term from the sample's centre
+// (exk = 2e-11 * kscale at the centre, margin_model_term): a stencil point's
+// u, v, 1/z differ from the centre's by ~1e-3 relative, so twice the centre's
+// bound covers every point of the stencil; and one Newton step of the
+// reciprocal (2^-44 relative, ~1e-10 px at 1000 px, far inside the 1e-6 px
+// margin).
+template <int M>
+__device__ inline double margin_model_term(const double* K2, const double p[3], double mag) {
+  const double iz = 1.0 / p[2];
+  const double u = p[0] * iz, v = p[1] * iz;
+  return 2e-11 * (fabs(K2[0]) + fabs(K2[1])) * distortion_gain<M>(K2, u * u + v * v) * (1.0 + fabs(u) + fabs(v)) *
+         (1.0 + mag * fabs(iz));
+}
+
 template <int M, bool FAST = false>
 __device__ inline bool resolve(const SemArgs& a, const double p[3], double mag, float label1, const double* K2,
-                               const float2* dl2, const PixelCache& pc, double& f) {
-  const double iz = rcp_refined(p[2]);
+                               const float2* dl2, const PixelCache& pc, double& f, double exk = 0.0) {
+  double iz;
+  if constexpr (FAST) {
+    const double x0 = p[2];
+    double r = __builtin_amdgcn_rcp(x0);
+    iz = fma(r, fma(-x0, r, 1.0), r);
+  } else {
+    iz = rcp_refined(p[2]);
+  }
   const double u = p[0] * iz, v = p[1] * iz;
   double x, y;
   if constexpr (FAST)
@@ -274,9 +295,14 @@ __device__ inline bool resolve(const SemArgs& a, const double p[3], double mag, 
   else
     world_to_image<M>(K2, u, v, &x, &y);
   if (!(fabs(x) < 1e8 && fabs(y) < 1e8 && fabs(u) < 1e6 && fabs(v) < 1e6)) return false;
-  const double kscale = (fabs(K2[0]) + fabs(K2[1])) * distortion_gain<M>(K2, u * u + v * v) *
-                        (1.0 + fabs(u) + fabs(v)) * (1.0 + mag * fabs(iz));
-  const double ex = 1e-6 + 1e-11 * (kscale + fabs(x) + fabs(y));
+  double ex;
+  if constexpr (FAST) {
+    ex = 1e-6 + exk + 1e-11 * (fabs(x) + fabs(y));
+  } else {
+    const double kscale = (fabs(K2[0]) + fabs(K2[1])) * distortion_gain<M>(K2, u * u + v * v) *
+                          (1.0 + fabs(u) + fabs(v)) * (1.0 + mag * fabs(iz));
+    ex = 1e-6 + 1e-11 * (kscale + fabs(x) + fabs(y));
+  }
   const double fx = floor(x), fy = floor(y);
   const double rx = x - fx, ry = y - fy;
   if (!(fabs(rx - 0.5) > ex && fabs(ry - 0.5) > ex)) return false;
@@ -456,7 +482,7 @@ template <int M, bool FAST, int GRP>
 __device__ __forceinline__ double stencil_point(const SemArgs& a, const PairConst* __restrict__ P, int e, int k,
                                                 const double w[3], const double pw[3], const double p2[3],
                                                 double mag, const double pc1[3], float label1, const double* K2,
-                                                const float2* dl2, const PixelCache& pc) {
+                                                const float2* dl2, const PixelCache& pc, double exk) {
   const double pert = P->pert[e];
   double pp[3];
   if constexpr (GRP == 0 || GRP == 2) {
@@ -479,7 +505,7 @@ __device__ __forceinline__ double stencil_point(const SemArgs& a, const PairCons
     for (int c = 0; c < 3; ++c) pp[c] = p2[c] + (c == k ? dt : 0.0);
   }
   double f;
-  if (!resolve<M, FAST>(a, pp, mag, label1, K2, dl2, pc, f))
+  if (!resolve<M, FAST>(a, pp, mag, label1, K2, dl2, pc, f, exk))
     f = stencil_reference<M>(a, P, GRP, k, pert, pc1, label1, K2, dl2);
   return f;
 }
@@ -542,6 +568,7 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
     // mat-vec per point.  Tangent columns accumulate from 0.0 in m order,
     // exactly as J_tangent = J_ambient * PlusJacobian does.
     const double w[3] = {smp.pc1[0] - P->t1[0], smp.pc1[1] - P->t1[1], smp.pc1[2] - P->t1[2]};
+    const double exk = FAST ? margin_model_term<M>(K2, p2, mag) : 0.0;
     double jq1[3] = {0.0, 0.0, 0.0}, jt1[3] = {0.0, 0.0, 0.0}, jq2[3] = {0.0, 0.0, 0.0}, jt2[3] = {0.0, 0.0, 0.0};
     if (P->var1) {
 #pragma unroll 1
@@ -549,7 +576,7 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
         double fp = 0.0, fm = 0.0;
 #pragma unroll 1
         for (int sg = 0; sg < 2; ++sg) {
-          const double f = stencil_point<M, FAST, 0>(a, P, 2 * m + sg, m, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc);
+          const double f = stencil_point<M, FAST, 0>(a, P, 2 * m + sg, m, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc, exk);
           fp = sg == 0 ? f : fp;
           fm = sg == 1 ? f : fm;
         }
@@ -564,7 +591,7 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
         double fp = 0.0, fm = 0.0;
 #pragma unroll 1
         for (int sg = 0; sg < 2; ++sg) {
-          const double f = stencil_point<M, FAST, 1>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc);
+          const double f = stencil_point<M, FAST, 1>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc, exk);
           fp = sg == 0 ? f : fp;
           fm = sg == 1 ? f : fm;
         }
@@ -581,7 +608,7 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
         double fp = 0.0, fm = 0.0;
 #pragma unroll 1
         for (int sg = 0; sg < 2; ++sg) {
-          const double f = stencil_point<M, FAST, 2>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc);
+          const double f = stencil_point<M, FAST, 2>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc, exk);
           fp = sg == 0 ? f : fp;
           fm = sg == 1 ? f : fm;
         }
@@ -596,7 +623,7 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
         double fp = 0.0, fm = 0.0;
 #pragma unroll 1
         for (int sg = 0; sg < 2; ++sg) {
-          const double f = stencil_point<M, FAST, 3>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc);
+          const double f = stencil_point<M, FAST, 3>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc, exk);
           fp = sg == 0 ? f : fp;
           fm = sg == 1 ? f : fm;
         }
