@@ -387,8 +387,16 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *                           30-35 occupancy study (tools/ab_jacobian.py)
  *   "cholesky_panel"        0 recursive split, 64..4096 right-looking panel width
  *   "cholesky_gemm_update"  0 dsyrk / 1 dgemm trailing update
- *   "cholesky_own_diag"     1 hand-written diagonal-block factor (one column per step), 2 the
+ *   "cholesky_own_diag"     6 one launch per panel for the diagonal block and the panel
+ *                           solve (default; panels <= 512, else 2), 1 hand-written
+ *                           diagonal-block factor (one column per step) + dtrsm, 2 the
  *                           same blocked by 4 (3: by 8) columns per step, 0 rocsolver_dpotrf
+ *   "cholesky_rest_update"  trailing update after the look-ahead column: 3 dgemm per
+ *                           1024-wide block column (default), 0 per 512, 1 dsyrk, 2 dgemmt
+ *   "schur_pairs_variant"   0 explicit Schur pair kernel (default), 1-3 pipelined variants
+ *   "semantic_variant"      1 FMA-contracted fast route (default), 0 uncontracted
+ *   "linearize_overlap"     1 semantic kernel on a second stream beside the reprojection
+ *                           kernel, 0 one stream (default)
  *   "cholesky_lookahead"    1 side-stream look-ahead (default) / 0 serial
  *   "cholesky_solve"        2 sync-free triangular sweeps, one launch per direction
  *                           (default) / 1 hand-written blocked triangular sweeps /

@@ -674,6 +674,139 @@ __device__ int tile_chol_lds(double* L, double* nb, int lane, int wv, int ld = 6
   return bad;
 }
 
+// ---- 64x64 factor + inverse in LDS by 16x16 blocks (4 waves, MFMA) --------
+// M: row-major padded (ld kPfLd) 64x64, lower triangle valid.  Right-looking
+// over four 16-wide block columns: the 16x16 diagonal block by one wave in
+// registers (lane = row), the 16-column solve below it by one lane per row
+// (registers), the trailing lower blocks by v_mfma_f64_16x16x4f64.  Then
+// X = L^-1: the four diagonal blocks by one wave (lane = block x column), the
+// off-diagonal blocks by block diagonals, X_ik = -X_ii sum_m L_im X_mk (MFMA).
+// Returns the first non-positive pivot (1-based) or 0 (every thread).
+
+// acc (16x16, MFMA D layout) += sign * A(16x16) * op(B); A, B row-major with
+// leading dimensions lda, ldb; op(B) = B' when TB.
+template <bool TB>
+__device__ __forceinline__ void blk16_mma(pf_dvec4& acc, double sign, const double* A, int lda, const double* B,
+                                          int ldb, int lane) {
+  const int m = lane & 15, k = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const double a = sign * A[m * lda + 4 * s + k];
+    const double b = TB ? B[m * ldb + 4 * s + k] : B[(4 * s + k) * ldb + m];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void blk16_load(pf_dvec4& acc, const double* C, int ldc, int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = C[(4 * q + (lane >> 4)) * ldc + (lane & 15)];
+}
+__device__ __forceinline__ void blk16_store(const pf_dvec4& acc, double* C, int ldc, int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) C[(4 * q + (lane >> 4)) * ldc + (lane & 15)] = acc[q];
+}
+
+__device__ int pf_chol_inv_blocked(double* M, double* X, double* scr, double* dinv, int lane, int wv) {
+  int bad = 0;
+  double* col = scr;  // [16][16] pivot columns of the current diagonal block
+  for (int kb = 0; kb < 4; ++kb) {
+    const int o = 16 * kb;
+    // 1. diagonal block, wave 0 (lanes 16.. repeat lanes 0..15)
+    if (wv == 0) {
+      const int i = lane & 15;
+      double a[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a[j] = M[(o + i) * kPfLd + o + j];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const double dk = readlane_f64(a[k], k);
+        if (!(dk > 0.0) && bad == 0) bad = o + k + 1;
+        const double sk = sqrt(dk);
+        const double isk = 1.0 / sk;
+        const double lik = i > k ? a[k] * isk : (i == k ? sk : 0.0);
+        a[k] = lik;
+        if (lane < 16) col[k * 16 + i] = lik;
+        if (lane == 0) dinv[o + k] = isk;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+#pragma unroll
+        for (int j = k + 1; j < 16; ++j) a[j] -= lik * col[k * 16 + j];
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) M[(o + i) * kPfLd + o + j] = j <= i ? a[j] : 0.0;
+      }
+    }
+    __syncthreads();
+    // 2. rows below: x D' = a, lane = row (wave 0, up to 48 rows)
+    const int nbelow = 48 - o;
+    if (wv == 0 && lane < nbelow) {
+      const int r = o + 16 + lane;
+      double x[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        double v = M[r * kPfLd + o + k];
+#pragma unroll
+        for (int m2 = 0; m2 < k; ++m2) v -= x[m2] * M[(o + k) * kPfLd + o + m2];
+        x[k] = v * dinv[o + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) M[r * kPfLd + o + k] = x[k];
+    }
+    __syncthreads();
+    // 3. trailing lower blocks (ib >= jb > kb): A_ib,jb -= L_ib,kb L_jb,kb'
+    int t = 0;
+    for (int ib = kb + 1; ib < 4; ++ib)
+      for (int jb = kb + 1; jb <= ib; ++jb, ++t) {
+        if (t % 4 != wv) continue;
+        pf_dvec4 acc;
+        double* C = M + 16 * ib * kPfLd + 16 * jb;
+        blk16_load(acc, C, kPfLd, lane);
+        blk16_mma<true>(acc, -1.0, M + 16 * ib * kPfLd + o, kPfLd, M + 16 * jb * kPfLd + o, kPfLd, lane);
+        blk16_store(acc, C, kPfLd, lane);
+      }
+    __syncthreads();
+  }
+  // X = L^-1.  Diagonal blocks: wave 0, lane = (block b, column j)
+  if (wv == 0) {
+    const int b = lane >> 4, j = lane & 15, o = 16 * b;
+    double x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      double v = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+      for (int m2 = 0; m2 < i; ++m2) v -= M[(o + i) * kPfLd + o + m2] * x[m2];
+      x[i] = v * dinv[o + i];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) X[(o + i) * kPfLd + o + j] = x[i];
+  }
+  // strict upper blocks of X are zero
+  for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
+    const int i = e >> 6, j = e & 63;
+    if ((j >> 4) > (i >> 4)) X[i * kPfLd + j] = 0.0;
+  }
+  __syncthreads();
+  // off-diagonal blocks by block diagonals d: X_ik = -X_ii (sum_{m=k}^{i-1} L_im X_mk)
+  double* T = scr + wv * 16 * 17;  // per-wave 16x16 scratch (ld 17)
+  for (int d = 1; d < 4; ++d) {
+    const int k = wv;
+    const int i = k + d;
+    if (i < 4) {
+      pf_dvec4 acc = {0.0, 0.0, 0.0, 0.0};
+      for (int m2 = k; m2 < i; ++m2)
+        blk16_mma<false>(acc, 1.0, M + 16 * i * kPfLd + 16 * m2, kPfLd, X + 16 * m2 * kPfLd + 16 * k, kPfLd, lane);
+      blk16_store(acc, T, 17, lane);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      pf_dvec4 out = {0.0, 0.0, 0.0, 0.0};
+      blk16_mma<false>(out, -1.0, X + 16 * i * kPfLd + 16 * i, kPfLd, T, 17, lane);
+      blk16_store(out, X + 16 * i * kPfLd + 16 * k, kPfLd, lane);
+    }
+    __syncthreads();
+  }
+  return bad;
+}
+
 // dbg (nullable, probes only): wall_clock64() stamps [row tile][20]: 0 start,
 // 1 + 2c after step c's waits (diagonal step: after the factor), 2 + 2c at
 // step c's end.
@@ -777,33 +910,18 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
       continue;
     }
     // c == r: factor the diagonal tile, invert it, publish both
-    pf_acc_to_lds_t(dacc, T, wv, lane);
+    pf_acc_to_lds(dacc, T, wv, lane);
     __syncthreads();
-    __shared__ int s_bad;
-    // factor in LDS (4 waves, tile_chol_lds on the column-major view), then
-    // the inverse by wave 0
-    const int bad = tile_chol_lds<4, 4>(T, Lc, lane, wv, kPfLd);
-    if (wv == 0) {
-      dinv[lane] = 1.0 / T[lane * kPfLd + lane];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-      // L[i][k] = T[k * kPfLd + i] (column-major view): transpose into Lc rows
-      // for the contiguous row reads of pf_inv_wave
-      for (int i = 0; i < 64; ++i) Lc[i * 64 + lane] = lane <= i ? T[lane * kPfLd + i] : 0.0;
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-      pf_inv_wave(Lc, 64, dinv, Li, lane);
-      if (lane == 0) s_bad = bad;
-    }
-    __syncthreads();
+    // factor + inverse by 16x16 blocks (Lc: pivot columns + per-wave scratch)
+    const int bad = pf_chol_inv_blocked(T, Li, Lc, dinv, lane, wv);
     stamp(1 + 2 * c);
     double* lo = linv + (size_t)c * 64 * 64;
     for (int e = threadIdx.x; e < 64 * 64; e += 256) {
       lo[e] = Li[(e >> 6) * kPfLd + (e & 63)];  // row-major, ld 64
       const int i = e & 63, j = e >> 6;
-      if (i < wc && j < wc && i >= j) A[(size_t)(c0 + j) * lda + c0 + i] = T[j * kPfLd + i];  // column-major view
+      if (i < wc && j < wc && i >= j) A[(size_t)(c0 + j) * lda + c0 + i] = T[i * kPfLd + j];
     }
-    if (threadIdx.x == 0 && s_bad != 0 && s_bad <= wc) atomicCAS(info, 0, c0 + s_bad);
+    if (threadIdx.x == 0 && bad != 0 && bad <= wc) atomicCAS(info, 0, c0 + bad);
     __threadfence();
     __syncthreads();
     if (threadIdx.x == 0)
@@ -1132,13 +1250,15 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
                            CholWorkspace* ws) {
   if (n <= 0) return rocblas_status_success;
   if (cfg.own_diag && (!ws || !ws->scratch)) return rocblas_status_invalid_pointer;
-  // the one-launch panel factor needs panels of at most 8 tiles
-  if (cfg.own_diag == 6 && (cfg.panel <= 0 || cfg.panel > 64 * kPfMaxTiles)) return rocblas_status_invalid_size;
+  // the one-launch panel factor needs panels of at most 8 tiles: other panel
+  // widths (and the recursive split) take the two-kernel diagonal factor
+  CholConfig c = cfg;
+  if (c.own_diag == 6 && (c.panel <= 0 || c.panel > 64 * kPfMaxTiles)) c.own_diag = 2;
   double* scratch = ws ? ws->scratch : nullptr;
-  if (cfg.panel > 0 && cfg.gemm_update && cfg.lookahead && ws && ws->side)
-    return factor_lookahead(h, n, A, lda, info, cfg, *ws);
-  if (cfg.panel > 0) return factor_blocked(h, n, A, lda, info, cfg, scratch, ws);
-  return factor(h, n, A, lda, info, cfg.own_diag, scratch);
+  if (c.panel > 0 && c.gemm_update && c.lookahead && ws && ws->side)
+    return factor_lookahead(h, n, A, lda, info, c, *ws);
+  if (c.panel > 0) return factor_blocked(h, n, A, lda, info, c, scratch, ws);
+  return factor(h, n, A, lda, info, c.own_diag, scratch);
 }
 
 rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x, int variant,

@@ -43,7 +43,9 @@ struct CholConfig {
   // ~300 us, instruction-fetch bound.)
   // 6: one panel_factor_kernel launch per panel for the diagonal block AND the
   // panel's solve below it (no dtrsm; panel <= 512)
-  int own_diag = 2;  // 6 measured slower at nf = 12 000 (26.0 vs 25.0 ms; profiles/r2_panel_probe_v2.txt: 64x64 factor + inverse ~95 us per step)
+  // default 6: 21.5 vs 25.0 ms at nf = 12 000 (profiles/r2_ab_own_diag.jsonl; 16x16-blocked
+  // MFMA factor + inverse per diagonal tile, profiles/r2_panel_probe_v3.txt)
+  int own_diag = 6;
   // chol_solve variant: 2 sync-free sweeps (one launch per direction), 1 one
   // launch per 64-wide block column with diagonal-block inverses, 0 recursive
   // rocBLAS dtrsv / dgemv

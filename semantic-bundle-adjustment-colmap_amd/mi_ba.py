@@ -417,7 +417,7 @@ def shard_scene(scene: "Scene", rank: int, world: int, semantic: Optional["Seman
 
 
 def dense_cholesky(A: np.ndarray, b: Optional[np.ndarray] = None, device: int = 0, panel: int = 512,
-                   lookahead: int = 1, own_diag: int = 2, solve: int = 2):
+                   lookahead: int = 1, own_diag: int = 6, solve: int = 2):
     """mi_ba_dense_cholesky: the reduced-camera-system factorisation on a
     caller-supplied SPD matrix.  Returns (L, x, info): L lower triangular
     (strict upper zeroed), x the solution of A x = b (None without b)."""
