@@ -533,6 +533,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
 // launch, release/acquire at agent scope, as the sweeps above).
 typedef double pf_dvec4 __attribute__((ext_vector_type(4)));
 constexpr int kPfMaxTiles = 8;  // column tiles per panel (panel <= 512)
+constexpr int kPfRows = 4;      // row tiles per below-diagonal workgroup
 
 __device__ __forceinline__ int pf_row0(int r, int kb, int nc) { return r < nc ? 64 * r : kb + 64 * (r - nc); }
 __device__ __forceinline__ int pf_rows(int r, int kb, int nc, int mrows) {
@@ -815,7 +816,7 @@ constexpr int kPfDbgSlots = 20;
 __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ A, int lda, int kb, int mrows,
                                                            int* __restrict__ info, double* __restrict__ linv,
                                                            unsigned* ctrl, unsigned base, unsigned epoch,
-                                                           unsigned long long* dbg = nullptr) {
+                                                           int nbw, unsigned long long* dbg = nullptr) {
   __shared__ double T[64 * kPfLd];   // staging / factor tile (row-major padded)
   __shared__ double Li[64 * kPfLd];  // a diagonal tile's inverse (own, or workgroup c's)
   __shared__ double Lc[64 * 64];     // the factor's columns (pf_chol_inv_wave)
@@ -858,6 +859,76 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
         const double v = A[(size_t)(r0 + min(j, w - 1)) * lda + r0 + min(i, w - 1)];
         dacc[t][q] = (i < w && j < w) ? v : (i == j ? 1.0 : 0.0);
       }
+  }
+  if (!diag_row) {
+    // below the diagonal block: this workgroup owns up to kPfRows row tiles
+    // (r, r + nbw, ...), so the launch occupies few CUs beside the
+    // look-ahead's trailing dgemm; each L_ck and Linv_cc is staged in LDS once
+    // for all of them
+    const int nr = nc + (mrows - kb + 63) / 64;
+    int rr[kPfRows], h[kPfRows];
+#pragma unroll
+    for (int j = 0; j < kPfRows; ++j) {
+      rr[j] = r + j * nbw;
+      h[j] = (rr[j] < nr && j * nbw < nr - nc) ? pf_rows(rr[j], kb, nc, mrows) : 0;
+    }
+    for (int c = 0; c < nc; ++c) {
+      const int c0 = 64 * c, wc = min(64, kb - c0);
+      pf_dvec4 acc[kPfRows][4];
+#pragma unroll
+      for (int j = 0; j < kPfRows; ++j) {
+        const int row0 = pf_row0(rr[j], kb, nc), hj = max(h[j], 1);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int i = 16 * wv + 4 * q + kq, jj = 16 * t + m;
+            const double v = h[j] > 0 ? A[(size_t)(c0 + min(jj, wc - 1)) * lda + row0 + min(i, hj - 1)] : 0.0;
+            acc[j][t][q] = (i < h[j] && jj < wc) ? v : 0.0;
+          }
+      }
+      for (int k = 0; k < c; ++k) {
+        pf_wait(flag + c * kPfMaxTiles + k, epoch);
+        // L_ck (rows of column tile c, columns of tile k) staged once
+        for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+          const int i = e & 63, kk = e >> 6;
+          const double v = A[(size_t)(64 * k + kk) * lda + c0 + min(i, wc - 1)];
+          Li[i * kPfLd + kk] = i < wc ? v : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kPfRows; ++j)
+          if (h[j] > 0)
+            pf_gemm_nt(acc[j], -1.0, gtile(pf_row0(rr[j], kb, nc), h[j], 64 * k, 64), ltile(Li), wv, lane);
+        __syncthreads();
+      }
+      pf_wait(flag + c * kPfMaxTiles + c, epoch);
+      stamp(1 + 2 * c);
+      const double* lc = linv + (size_t)c * 64 * 64;
+      for (int e = threadIdx.x; e < 64 * 64; e += 256) Li[(e >> 6) * kPfLd + (e & 63)] = lc[e];
+#pragma unroll
+      for (int j = 0; j < kPfRows; ++j) {
+        if (h[j] <= 0) continue;
+        pf_acc_to_lds(acc[j], T, wv, lane);
+        __syncthreads();
+        pf_dvec4 out[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) out[t] = pf_dvec4{0.0, 0.0, 0.0, 0.0};
+        pf_gemm_nt(out, 1.0, ltile(T), ltile(Li), wv, lane);
+        __syncthreads();
+        const int row0 = pf_row0(rr[j], kb, nc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int i = 16 * wv + 4 * q + kq, jj = 16 * t + m;
+            if (i < h[j] && jj < wc) A[(size_t)(c0 + jj) * lda + row0 + i] = out[t][q];
+          }
+      }
+      stamp(2 + 2 * c);
+      __syncthreads();  // Li is restaged next step
+    }
+    return;
   }
   for (int c = 0; c <= cmax; ++c) {
     const int c0 = 64 * c, wc = min(64, kb - c0);
@@ -1075,7 +1146,10 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
   const int mrows = n - k;
   const int nc = (kb + 63) / 64;
-  const int nr = nc + (mrows - kb + 63) / 64;
+  const int nbelow = (mrows - kb + 63) / 64;
+  const int rows = std::max(1, std::min(kPfRows, ws->pf_rows));
+  const int nbw = (nbelow + rows - 1) / rows;  // below-diagonal workgroups
+  const int nr = nc + nbw;                           // workgroups (tickets) of the launch
   if (ws->pf_base > 0x7fffffffu || ws->pf_epoch > 0xfffffff0u) {
     if (hipMemsetAsync(ws->pf_ctrl, 0, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles), s) != hipSuccess)
       return rocblas_status_internal_error;
@@ -1084,7 +1158,7 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   }
   const unsigned epoch = ++ws->pf_epoch;
   hipLaunchKernelGGL(panel_factor_kernel, dim3(nr), dim3(256), 0, s, A + k + (size_t)k * lda, lda, kb, mrows, info,
-                     ws->pf_linv, ws->pf_ctrl, ws->pf_base, epoch);
+                     ws->pf_linv, ws->pf_ctrl, ws->pf_base, epoch, nbw, nullptr);
   ws->pf_base += (unsigned)nr;
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
@@ -1254,6 +1328,7 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   // widths (and the recursive split) take the two-kernel diagonal factor
   CholConfig c = cfg;
   if (c.own_diag == 6 && (c.panel <= 0 || c.panel > 64 * kPfMaxTiles)) c.own_diag = 2;
+  if (ws) ws->pf_rows = c.panel_rows;
   double* scratch = ws ? ws->scratch : nullptr;
   if (c.panel > 0 && c.gemm_update && c.lookahead && ws && ws->side)
     return factor_lookahead(h, n, A, lda, info, c, *ws);

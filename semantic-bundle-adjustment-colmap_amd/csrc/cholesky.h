@@ -46,6 +46,9 @@ struct CholConfig {
   // default 6: 21.5 vs 25.0 ms at nf = 12 000 (profiles/r2_ab_own_diag.jsonl; 16x16-blocked
   // MFMA factor + inverse per diagonal tile, profiles/r2_panel_probe_v3.txt)
   int own_diag = 6;
+  // own_diag 6: row tiles per below-diagonal workgroup (1..4; fewer CUs held
+  // beside the trailing dgemm vs a longer left-looking update per workgroup)
+  int panel_rows = 1;
   // chol_solve variant: 2 sync-free sweeps (one launch per direction), 1 one
   // launch per 64-wide block column with diagonal-block inverses, 0 recursive
   // rocBLAS dtrsv / dgemv
@@ -72,6 +75,7 @@ struct CholWorkspace {
   double* pf_linv = nullptr;    // [8][64*64] inverses of the panel's diagonal tiles
   unsigned pf_base = 0;         // tickets handed out so far
   unsigned pf_epoch = 0;        // flag value of the last panel launch
+  int pf_rows = 1;              // row tiles per below-diagonal workgroup (CholConfig::panel_rows)
   int linv_rows = 0;
 
   // Creates the resources on `device` with events for up to `max_panels`

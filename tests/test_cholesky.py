@@ -207,3 +207,21 @@ def test_lm_lookahead_on_off(gpu, images):
     assert a.num_successful_steps == b.num_successful_steps
     assert a.num_unsuccessful_steps == b.num_unsuccessful_steps
     assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
+
+
+def test_lm_panel_rows(gpu):
+    """The one-launch panel factor with 1, 2 and 4 row tiles per
+    below-diagonal workgroup drives the same LM (nf = 1593: 4 panels, ragged
+    row counts per workgroup)."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for rows in (1, 2, 4):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            ctx.set_tuning("cholesky_panel_rows", rows)
+            res.append(ctx.solve())
+    b = res[0]
+    for a in res[1:]:
+        assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
+        assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost

@@ -22,7 +22,9 @@ int main(int argc, char** argv) {
   unsigned long long* dbg;
   hipMalloc(&A, 8ull * n * n);
   hipMalloc(&info, 64);
-  const int nr = 8 + (n - kb + 63) / 64;
+  const int prow = argc > 2 ? atoi(argv[2]) : 1;
+  const int nbw = ((n - kb + 63) / 64 + prow - 1) / prow;
+  const int nr = 8 + nbw;
   hipMalloc(&dbg, 8ull * nr * kPfDbgSlots);
   CholWorkspace ws;
   ws.create(0, (n + 511) / 512, n);
@@ -37,7 +39,7 @@ int main(int argc, char** argv) {
     hipEventCreate(&e1);
     hipEventRecord(e0, 0);
     hipLaunchKernelGGL(panel_factor_kernel, dim3(nr), dim3(256), 0, 0, A, n, kb, n, info, ws.pf_linv, ws.pf_ctrl,
-                       ws.pf_base, epoch, dbg);
+                       ws.pf_base, epoch, nbw, dbg);
     hipEventRecord(e1, 0);
     hipEventSynchronize(e1);
     ws.pf_base += nr;
