@@ -394,7 +394,14 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *   "cholesky_rest_update"  trailing update after the look-ahead column: 3 dgemm per
  *                           1024-wide block column (default), 0 per 512, 1 dsyrk, 2 dgemmt
  *   "schur_pairs_variant"   0 explicit Schur pair kernel (default), 1-3 pipelined variants
- *   "semantic_variant"      1 FMA-contracted fast route (default), 0 uncontracted
+ *   "semantic_variant"      6 flat pass (samples whose stencil provably stays on
+ *                           the centre's outcome: J = 0) + deferred-sample pass
+ *                           (default); 5 flat test + in-tile gather; 4, 3, 2
+ *                           batched stencil with 4 / 2 / 1 parameters per step;
+ *                           1 per-point FMA route; 0 per-point uncontracted
+ *                           (all bitwise equal)
+ *   "semantic_diag"         1: downloaded status carries 0x100 for samples the
+ *                           flat test deferred (variants 5, 6; diagnostic)
  *   "linearize_overlap"     1 semantic kernel on a second stream beside the reprojection
  *                           kernel, 0 one stream (default)
  *   "cholesky_lookahead"    1 side-stream look-ahead (default) / 0 serial

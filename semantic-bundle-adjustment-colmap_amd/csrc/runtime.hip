@@ -1375,7 +1375,11 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->lin_overlap = value != 0;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "semantic_variant") == 0 && (value == 0 || value == 1)) {
+  if (std::strcmp(key, "semantic_diag") == 0 && (value == 0 || value == 1)) {
+    ctx->sem_diag = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "semantic_variant") == 0 && value >= 0 && value <= 6) {
     ctx->sem_variant = value;
     return MI_BA_OK;
   }

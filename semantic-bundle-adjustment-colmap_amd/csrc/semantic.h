@@ -56,6 +56,11 @@ struct SemanticState {
   DevArray<SemTile> tiles;                 // grouped by the model of the pair's second camera
   int ntiles = 0;
   int model_tiles[kNumModels + 1] = {};    // tile range of each camera model
+  // two-pass linearization (semantic_variant 6): per-pair deferred lists
+  DevArray<uint32_t> pair_cnt;             // [npairs] deferred samples of the pair
+  DevArray<uint32_t> dlist;                // [ns] deferred samples (offset in pair), pair regions
+  DevArray<uint2> chunks;                  // (pair, first entry): 64-entry chunks of every pair region
+  int model_chunks[kNumModels + 1] = {};   // chunk range of each camera model
 };
 
 mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem);

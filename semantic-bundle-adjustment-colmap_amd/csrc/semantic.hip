@@ -343,7 +343,34 @@ struct PairConst {
   double ood[14];                     // (1 / delta) / 2, Ceres CENTRAL
   double A[16][9];                    // q1 points (e 0..7): R2 Q(q1')^T / |q1'|^2; q2 (e 14..21): Q(q2') / |q2'|^2
   double pj[8][3];                    // PlusJacobian rows of q1 (0..3) and q2 (4..7)
+  // displacement bounds of the camera-2 point over the stencil (flat test):
+  // |P_2' - P_2| <= rho1 |P_c1 - t1| (q1 points), rho2 |P_w| (q2 points);
+  // t1 point k moves it by dt1[k] C[:, k], t2 point k by dt2[k] e_k
+  double rho1, rho2, dt1[3], dt2[3];
 };
+
+// Bounds of one pose's stencil (the flat test): a perturbed quaternion q' =
+// q + d e_k rotates by ||R(q') - R(q)|| = 2 sin(angle(q, q')) <= 2 d_perp /
+// (|q| - d), d_perp = d sqrt(1 - q_k^2 / |q|^2) the step's component normal
+// to q; a translation step moves the point by d.  d is the stencil's actual
+// |q_k' - q_k| (Ceres' delta, as stencil_prep forms it).
+__device__ inline void stencil_bounds(const double* q, const double* t, double rel_step, double* rho, double dt[3]) {
+  const double nq2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
+  const double nq = sqrt(nq2);
+  double r = 0.0;
+  for (int k = 0; k < 4; ++k) {
+    const double delta = fmax(kMinStep, fabs(q[k]) * rel_step);
+    const double d = fmax(fabs((q[k] + delta) - q[k]), fabs(q[k] - (q[k] - delta)));
+    const double perp = d * sqrt(fmax(0.0, 1.0 - q[k] * q[k] / nq2));
+    const double den = nq - d;
+    r = fmax(r, den > 0.0 ? 2.0 * perp / den : INFINITY);
+  }
+  *rho = r * 1.001;
+  for (int k = 0; k < 3; ++k) {
+    const double delta = fmax(kMinStep, fabs(t[k]) * rel_step);
+    dt[k] = fmax(fabs((t[k] + delta) - t[k]), fabs(t[k] - (t[k] - delta))) * 1.001;
+  }
+}
 
 // Stencil entries of one pair: one lane per stencil point (perturbed value,
 // the Ceres step 1/(2 delta) with the lane-side operation sequence of the
@@ -440,6 +467,8 @@ __global__ void semantic_pair_prep_kernel(const SemPair* __restrict__ pairs, int
   P.mask2 = (img_flags[pr.j] >> 1) & 7u;
   P.slot = raster_slot[pr.j];
   P.pad0 = P.pad1 = P.pad2 = 0;
+  stencil_bounds(P.q1, P.t1, rel_step, &P.rho1, P.dt1);
+  stencil_bounds(P.q2, P.t2, rel_step, &P.rho2, P.dt2);
 }
 
 // Per-pair record: loss-corrected J'J (packed 12x12 upper, 78) and J'r (12).
@@ -478,13 +507,9 @@ __device__ __forceinline__ double stencil_reference(const SemArgs& a, const Pair
 // One stencil point e (ambient coordinate k of group GRP: 0 q1, 1 t1, 2 q2,
 // 3 t2): the perturbed camera-2 point from the pair table, its outcome by
 // resolve, or the reference sequence inside the margins.
-template <int M, bool FAST, int GRP>
-__device__ __forceinline__ double stencil_point(const SemArgs& a, const PairConst* __restrict__ P, int e, int k,
-                                                const double w[3], const double pw[3], const double p2[3],
-                                                double mag, const double pc1[3], float label1, const double* K2,
-                                                const float2* dl2, const PixelCache& pc, double exk) {
-  const double pert = P->pert[e];
-  double pp[3];
+template <bool FAST, int GRP>
+__device__ __forceinline__ void stencil_pp(const PairConst* __restrict__ P, int e, int k, const double w[3],
+                                           const double pw[3], const double p2[3], double pp[3]) {
   if constexpr (GRP == 0 || GRP == 2) {
     // q1: P_2' = R2 Q(q1')^T (P_c1 - t1) / |q1'|^2 + t2;  q2: P_2' = Q(q2') P_w / |q2'|^2 + t2
     const double* A = P->A[GRP == 0 ? e : e - 6];
@@ -496,18 +521,288 @@ __device__ __forceinline__ double stencil_point(const SemArgs& a, const PairCons
       for (int c = 0; c < 3; ++c) pp[c] = A[3 * c] * v[0] + A[3 * c + 1] * v[1] + A[3 * c + 2] * v[2] + P->t2[c];
     }
   } else if constexpr (GRP == 1) {  // t1: P_2' = P_2 - C (t1' - t1)
-    const double dt = pert - P->t1[k];
+    const double dt = P->pert[e] - P->t1[k];
 #pragma unroll
     for (int c = 0; c < 3; ++c) pp[c] = p2[c] - dt * P->C[3 * c + k];
   } else {  // t2: P_2' = P_2 + (t2' - t2)
-    const double dt = pert - P->t2[k];
+    const double dt = P->pert[e] - P->t2[k];
 #pragma unroll
     for (int c = 0; c < 3; ++c) pp[c] = p2[c] + (c == k ? dt : 0.0);
   }
+}
+
+template <int M, bool FAST, int GRP>
+__device__ __forceinline__ double stencil_point(const SemArgs& a, const PairConst* __restrict__ P, int e, int k,
+                                                const double w[3], const double pw[3], const double p2[3],
+                                                double mag, const double pc1[3], float label1, const double* K2,
+                                                const float2* dl2, const PixelCache& pc, double exk) {
+  const double pert = P->pert[e];
+  double pp[3];
+  stencil_pp<FAST, GRP>(P, e, k, w, pw, p2, pp);
   double f;
   if (!resolve<M, FAST>(a, pp, mag, label1, K2, dl2, pc, f, exk))
     f = stencil_reference<M>(a, P, GRP, k, pert, pc1, label1, K2, dl2);
   return f;
+}
+
+// The per-point route over every variable pose (one rolled loop per parameter
+// group, so the tangent row stays in registers): tangent columns accumulate
+// from 0.0 in m order, exactly as J_tangent = J_ambient * PlusJacobian does.
+template <int M, bool FAST>
+__device__ __forceinline__ void stencil_rolled(const SemArgs& a, const PairConst* __restrict__ P, const double w[3],
+                                               const double pw[3], const double p2[3], double mag, const double pc1[3],
+                                               float label1, const double* K2, const float2* dl2, const PixelCache& pc,
+                                               double exk, double Jt[12]) {
+  double jq1[3] = {0.0, 0.0, 0.0}, jt1[3] = {0.0, 0.0, 0.0}, jq2[3] = {0.0, 0.0, 0.0}, jt2[3] = {0.0, 0.0, 0.0};
+  if (P->var1) {
+#pragma unroll 1
+    for (int m = 0; m < 4; ++m) {
+      double fp = 0.0, fm = 0.0;
+#pragma unroll 1
+      for (int sg = 0; sg < 2; ++sg) {
+        const double f = stencil_point<M, FAST, 0>(a, P, 2 * m + sg, m, w, pw, p2, mag, pc1, label1, K2, dl2, pc, exk);
+        fp = sg == 0 ? f : fp;
+        fm = sg == 1 ? f : fm;
+      }
+      const double jm = (fp - fm) * P->ood[m];
+      const double* pj = P->pj[m];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) jq1[c] = jq1[c] + jm * pj[c];
+    }
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) {
+      const int m = 4 + k;
+      double fp = 0.0, fm = 0.0;
+#pragma unroll 1
+      for (int sg = 0; sg < 2; ++sg) {
+        const double f = stencil_point<M, FAST, 1>(a, P, 2 * m + sg, k, w, pw, p2, mag, pc1, label1, K2, dl2, pc, exk);
+        fp = sg == 0 ? f : fp;
+        fm = sg == 1 ? f : fm;
+      }
+      const double jm = (fp - fm) * P->ood[m];
+      const double v = ((P->mask1 >> k) & 1u) ? 0.0 : jm;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) jt1[c] = c == k ? v : jt1[c];
+    }
+  }
+  if (P->var2) {
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+      const int m = 7 + k;
+      double fp = 0.0, fm = 0.0;
+#pragma unroll 1
+      for (int sg = 0; sg < 2; ++sg) {
+        const double f = stencil_point<M, FAST, 2>(a, P, 2 * m + sg, k, w, pw, p2, mag, pc1, label1, K2, dl2, pc, exk);
+        fp = sg == 0 ? f : fp;
+        fm = sg == 1 ? f : fm;
+      }
+      const double jm = (fp - fm) * P->ood[m];
+      const double* pj = P->pj[4 + k];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) jq2[c] = jq2[c] + jm * pj[c];
+    }
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) {
+      const int m = 11 + k;
+      double fp = 0.0, fm = 0.0;
+#pragma unroll 1
+      for (int sg = 0; sg < 2; ++sg) {
+        const double f = stencil_point<M, FAST, 3>(a, P, 2 * m + sg, k, w, pw, p2, mag, pc1, label1, K2, dl2, pc, exk);
+        fp = sg == 0 ? f : fp;
+        fm = sg == 1 ? f : fm;
+      }
+      const double jm = (fp - fm) * P->ood[m];
+      const double v = ((P->mask2 >> k) & 1u) ? 0.0 : jm;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) jt2[c] = c == k ? v : jt2[c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    Jt[c] = jq1[c];
+    Jt[3 + c] = jt1[c];
+    Jt[6 + c] = jq2[c];
+    Jt[9 + c] = jt2[c];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Batched stencil.  The per-point route waits on one raster read per stencil
+// point (a dependent gather inside a rolled loop: ~29 serial memory round
+// trips per wave).  Here a step of NB parameters (2 NB points) forms every
+// perturbed pixel first, issues the step's raster reads together and then
+// takes the decisions — the same decisions with the same margins as resolve.
+// A point whose decision falls inside a margin does not fall back on its own:
+// it marks the sample, and the sample is redone by the per-point route
+// (stencil_rolled, which falls back to the reference sequence), so the
+// values stay the reference's bit for bit.
+// ---------------------------------------------------------------------------
+// First half of resolve: 0 = inside a pixel margin (redo), 1 = out of bounds
+// (f = 0), 2 = raster test at *idx needed.
+template <int M, bool FAST>
+__device__ __forceinline__ int probe_pixel(const SemArgs& a, const double p[3], double mag, const double* K2,
+                                           double exk, int* idx) {
+  double iz;
+  if constexpr (FAST) {
+    const double x0 = p[2];
+    double r = __builtin_amdgcn_rcp(x0);
+    iz = fma(r, fma(-x0, r, 1.0), r);
+  } else {
+    iz = rcp_refined(p[2]);
+  }
+  const double u = p[0] * iz, v = p[1] * iz;
+  double x, y;
+  if constexpr (FAST)
+    world_to_image_fma<M>(K2, u, v, &x, &y);
+  else
+    world_to_image<M>(K2, u, v, &x, &y);
+  if (!(fabs(x) < 1e8 && fabs(y) < 1e8 && fabs(u) < 1e6 && fabs(v) < 1e6)) return 0;
+  double ex;
+  if constexpr (FAST) {
+    ex = 1e-6 + exk + 1e-11 * (fabs(x) + fabs(y));
+  } else {
+    const double kscale = (fabs(K2[0]) + fabs(K2[1])) * distortion_gain<M>(K2, u * u + v * v) *
+                          (1.0 + fabs(u) + fabs(v)) * (1.0 + mag * fabs(iz));
+    ex = 1e-6 + 1e-11 * (kscale + fabs(x) + fabs(y));
+  }
+  const double fx = floor(x), fy = floor(y);
+  const double rx = x - fx, ry = y - fy;
+  if (!(fabs(rx - 0.5) > ex && fabs(ry - 0.5) > ex)) return 0;
+  const int px = (int)fx + (rx > 0.5 ? 1 : 0);
+  const int py = (int)fy + (ry > 0.5 ? 1 : 0);
+  if (px < 0 || px >= a.W || py < 0 || py >= a.H) return 1;
+  *idx = py * a.W + px;
+  return 2;
+}
+
+// Second half of resolve: the depth decision (false = inside its margin).
+__device__ __forceinline__ bool probe_depth(const SemArgs& a, float2 s, double z, double mag, float label1,
+                                            double* f) {
+  const double dd = fabs((double)s.x - z) - a.threshold;
+  if (!(fabs(dd) > 1e-9 * (1.0 + fabs((double)s.x) + mag))) return false;
+  *f = (dd > 0.0) ? 0.0 : ((label1 == s.y) ? 0.0 : 1.0);
+  return true;
+}
+
+// One step: parameters k0 .. k0 + NB - 1 (< n) of group GRP, global index
+// m0 + j for parameter k0 + j; fp / fm the + / - values.  cidx: a pixel the
+// lane has read already (the centre's), read again by points with no raster
+// test so that every read of the step issues unconditionally.
+template <int M, bool FAST, int GRP, int NB>
+__device__ __forceinline__ bool stencil_step(const SemArgs& a, const PairConst* __restrict__ P, int m0, int k0, int n,
+                                             const double w[3], const double pw[3], const double p2[3], double mag,
+                                             float label1, const double* K2, const float2* __restrict__ dl2, int cidx,
+                                             double exk, double fp[NB], double fm[NB]) {
+  int code[2 * NB], idx[2 * NB];
+  double z[2 * NB];
+#pragma unroll
+  for (int j = 0; j < 2 * NB; ++j) {
+    code[j] = 1;
+    idx[j] = cidx;
+    z[j] = 0.0;
+    if (k0 + j / 2 < n) {
+      double pp[3];
+      stencil_pp<FAST, GRP>(P, 2 * (m0 + j / 2) + (j & 1), k0 + j / 2, w, pw, p2, pp);
+      z[j] = pp[2];
+      int ix = cidx;
+      code[j] = probe_pixel<M, FAST>(a, pp, mag, K2, exk, &ix);
+      idx[j] = code[j] == 2 ? ix : cidx;
+    }
+  }
+  float2 s[2 * NB];
+#pragma unroll
+  for (int j = 0; j < 2 * NB; ++j) s[j] = dl2[idx[j]];
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 2 * NB; ++j) {
+    double f = 0.0;
+    if (code[j] == 0 || (code[j] == 2 && !probe_depth(a, s[j], z[j], mag, label1, &f))) ok = false;
+    if (j & 1)
+      fm[j / 2] = f;
+    else
+      fp[j / 2] = f;
+  }
+  return ok;
+}
+
+// The stencil in steps of NB parameters; false when some point's decision was
+// inside a margin (Jt is then not the reference's: redo with stencil_rolled).
+// Accumulation order as stencil_rolled.
+template <int M, bool FAST, int NB>
+__device__ __forceinline__ bool stencil_batched(const SemArgs& a, const PairConst* __restrict__ P, const double w[3],
+                                                const double pw[3], const double p2[3], double mag, float label1,
+                                                const double* K2, const float2* dl2, int cidx, double exk,
+                                                double Jt[12]) {
+  double jq1[3] = {0.0, 0.0, 0.0}, jt1[3] = {0.0, 0.0, 0.0}, jq2[3] = {0.0, 0.0, 0.0}, jt2[3] = {0.0, 0.0, 0.0};
+  bool ok = true;
+  if (P->var1) {
+#pragma unroll 1
+    for (int k = 0; k < 4; k += NB) {
+      double fp[NB], fm[NB];
+      ok &= stencil_step<M, FAST, 0, NB>(a, P, k, k, 4, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if (k + j < 4) {
+          const double jm = (fp[j] - fm[j]) * P->ood[k + j];
+          const double* pj = P->pj[k + j];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) jq1[c] = jq1[c] + jm * pj[c];
+        }
+      }
+    }
+#pragma unroll 1
+    for (int k = 0; k < 3; k += NB) {
+      double fp[NB], fm[NB];
+      ok &= stencil_step<M, FAST, 1, NB>(a, P, 4 + k, k, 3, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if (k + j < 3) {
+          const double jm = (fp[j] - fm[j]) * P->ood[4 + k + j];
+          const double v = ((P->mask1 >> (k + j)) & 1u) ? 0.0 : jm;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) jt1[c] = c == k + j ? v : jt1[c];
+        }
+      }
+    }
+  }
+  if (P->var2) {
+#pragma unroll 1
+    for (int k = 0; k < 4; k += NB) {
+      double fp[NB], fm[NB];
+      ok &= stencil_step<M, FAST, 2, NB>(a, P, 7 + k, k, 4, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if (k + j < 4) {
+          const double jm = (fp[j] - fm[j]) * P->ood[7 + k + j];
+          const double* pj = P->pj[4 + k + j];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) jq2[c] = jq2[c] + jm * pj[c];
+        }
+      }
+    }
+#pragma unroll 1
+    for (int k = 0; k < 3; k += NB) {
+      double fp[NB], fm[NB];
+      ok &= stencil_step<M, FAST, 3, NB>(a, P, 11 + k, k, 3, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if (k + j < 3) {
+          const double jm = (fp[j] - fm[j]) * P->ood[11 + k + j];
+          const double v = ((P->mask2 >> (k + j)) & 1u) ? 0.0 : jm;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) jt2[c] = c == k + j ? v : jt2[c];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    Jt[c] = jq1[c];
+    Jt[3 + c] = jt1[c];
+    Jt[6 + c] = jq2[c];
+    Jt[9 + c] = jt2[c];
+  }
+  return ok;
 }
 
 // One workgroup per pair-aligned tile of <= 256 samples, one lane per sample:
@@ -519,7 +814,164 @@ __device__ __forceinline__ double stencil_point(const SemArgs& a, const PairCons
 // registers, not LDS) with one atomic flush per value.  Per-sample r /
 // status / J are stored only when requested (parity and download); the
 // solver consumes the pair records.
-template <int M, bool FAST = false>
+// ---------------------------------------------------------------------------
+// Centre evaluation of one sample (reference operation sequence) and the
+// quantities its stencil starts from.
+// ---------------------------------------------------------------------------
+struct Centre {
+  double pw[3], p2[3], w[3];
+  double r, mag, exk;
+  PixelCache pc;
+  int st;
+};
+
+template <int M, bool FAST>
+__device__ __forceinline__ void centre_eval(const SemArgs& a, const PairConst* __restrict__ P, const SemSample& smp,
+                                            const double* K2, const float2* dl2, Centre& c) {
+  // QuaternionRotatePoint(q_inv, P_c1) + t_inv, then pose 2
+  double rot[3];
+  unit_quat_rotate(P->uqi, smp.pc1, rot);
+  c.pw[0] = rot[0] + P->ti[0];
+  c.pw[1] = rot[1] + P->ti[1];
+  c.pw[2] = rot[2] + P->ti[2];
+  double rot2[3];
+  unit_quat_rotate(P->u2, c.pw, rot2);
+  c.p2[0] = rot2[0] + P->t2[0];
+  c.p2[1] = rot2[1] + P->t2[1];
+  c.p2[2] = rot2[2] + P->t2[2];
+  c.pc.valid = false;
+  c.pc.px = c.pc.py = 0;
+  c.pc.depth = c.pc.label = 0.f;
+  c.st = 0;
+  c.r = project_centre<M>(a, c.p2, smp.label1, K2, dl2, c.pc, &c.st);
+  c.mag = fabs(smp.pc1[0]) + fabs(smp.pc1[1]) + fabs(smp.pc1[2]) + fabs(P->t1[0]) + fabs(P->t1[1]) +
+          fabs(P->t1[2]) + fabs(c.pw[0]) + fabs(c.pw[1]) + fabs(c.pw[2]) + fabs(P->t2[0]) + fabs(P->t2[1]) +
+          fabs(P->t2[2]);
+  c.w[0] = smp.pc1[0] - P->t1[0];
+  c.w[1] = smp.pc1[1] - P->t1[1];
+  c.w[2] = smp.pc1[2] - P->t1[2];
+  c.exk = FAST ? margin_model_term<M>(K2, c.p2, c.mag) : 0.0;
+}
+
+// Stencil: parameter m = 0..13 over (q1, t1, q2, t2), + then - (Ceres
+// CENTRAL order), e = 2 m + minus.  Everything that depends only on the pair
+// and the stencil point (perturbed value, 1/(2 delta), the perturbed rotation
+// folded into one 3x3 map, PlusJacobian rows) comes from the per-pair table
+// as wave-uniform scalar loads; a lane forms one mat-vec per point.
+template <int M, bool FAST, int NB>
+__device__ __forceinline__ void stencil_full(const SemArgs& a, const PairConst* __restrict__ P, const Centre& c,
+                                             const SemSample& smp, const double* K2, const float2* dl2,
+                                             double Jt[12]) {
+  if constexpr (NB > 0) {
+    const int cidx = c.pc.valid ? c.pc.py * a.W + c.pc.px : 0;
+    if (!stencil_batched<M, FAST, NB>(a, P, c.w, c.pw, c.p2, c.mag, smp.label1, K2, dl2, cidx, c.exk, Jt))
+      stencil_rolled<M, FAST>(a, P, c.w, c.pw, c.p2, c.mag, smp.pc1, smp.label1, K2, dl2, c.pc, c.exk, Jt);
+  } else {
+    stencil_rolled<M, FAST>(a, P, c.w, c.pw, c.p2, c.mag, smp.pc1, smp.label1, K2, dl2, c.pc, c.exk, Jt);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Flat test.  Most samples have a zero Jacobian: every stencil point lands on
+// a pixel with the centre's outcome.  This proves it without evaluating the
+// stencil: every stencil point's camera-2 point lies within d of the
+// centre's (PairConst bounds), so |du| <= d (1 + |u|) / (z - d) (same for v)
+// exactly, the pixel moves by at most 1.1 (|A00| du + |A01| dv) (A = d(x,y) /
+// d(u,v) at the centre; the camera model's second derivatives are bounded by
+// ~20 x distortion_gain of the first, so with gain * |d(u,v)| (1 + |u| + |v|)
+// <= 2e-3 (guarded below) A changes by <= 4 % over the displacement) plus
+// resolve's rounding margin, and the depth compared by at most d.  When every
+// pixel the rounded projection can reach gives the centre's outcome for every
+// depth within d (outside the margin), every stencil value equals the
+// centre's residual: all CENTRAL differences are +0.0, J = +0.0 exactly as
+// the reference's accumulation yields.  Otherwise (or on any doubt: depth
+// near zero, huge coordinates, a wide pixel box) the sample takes the full
+// stencil.
+// ---------------------------------------------------------------------------
+template <int M>
+__device__ __forceinline__ bool stencil_flat(const SemArgs& a, const PairConst* __restrict__ P, const Centre& c,
+                                             float label1, const double* K2, const float2* __restrict__ dl2) {
+  const double z = c.p2[2];
+  if (!(z > 0.0)) return false;  // NaN-safe
+  const double iz = 1.0 / z;
+  const double u = c.p2[0] * iz, v = c.p2[1] * iz;
+  constexpr int np = Model<M>::kNumParams;
+  double x, y, A[4], Jp[2 * np];
+  world_to_image_jac<M>(K2, u, v, &x, &y, A, Jp);
+  if (!(fabs(x) < 1e8 && fabs(y) < 1e8 && fabs(u) < 1e6 && fabs(v) < 1e6)) return false;
+  // per class of stencil points, componentwise bounds (ax, ay, az) of the
+  // camera-2 point's displacement: du <= (ax + |u| az) / (z - az), dv alike
+  double bxm = 0.0, bym = 0.0, dz = 0.0, gm = 0.0;
+  bool ok = true;
+  auto cls = [&](double ax, double ay, double az) {
+    const double den = z - az;
+    ok = ok && den > 0.5 * z;
+    const double du = (ax + fabs(u) * az) / den, dv = (ay + fabs(v) * az) / den;
+    bxm = fmax(bxm, fabs(A[0]) * du + fabs(A[1]) * dv);
+    bym = fmax(bym, fabs(A[2]) * du + fabs(A[3]) * dv);
+    dz = fmax(dz, az);
+    gm = fmax(gm, fmax(du, dv));
+  };
+  if (P->var1) {
+    const double dq = P->rho1 * sqrt(c.w[0] * c.w[0] + c.w[1] * c.w[1] + c.w[2] * c.w[2]) * (1.0 + 1e-12);
+    cls(dq, dq, dq);
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      cls(P->dt1[k] * fabs(P->C[k]), P->dt1[k] * fabs(P->C[3 + k]), P->dt1[k] * fabs(P->C[6 + k]));
+  }
+  if (P->var2) {
+    const double dq = P->rho2 * sqrt(c.pw[0] * c.pw[0] + c.pw[1] * c.pw[1] + c.pw[2] * c.pw[2]) * (1.0 + 1e-12);
+    cls(dq, dq, dq);
+    cls(P->dt2[0], 0.0, 0.0);
+    cls(0.0, P->dt2[1], 0.0);
+    cls(0.0, 0.0, P->dt2[2]);
+  }
+  if (!ok) return false;
+  const double gain = distortion_gain<M>(K2, u * u + v * v);
+  if (!(gain * gm * (1.0 + fabs(u) + fabs(v)) <= 2e-3)) return false;
+  const double d = dz;
+  const double kscale = (fabs(K2[0]) + fabs(K2[1])) * gain * (1.0 + fabs(u) + fabs(v)) * (1.0 + c.mag * fabs(iz));
+  const double ex = 1e-6 + 1e-11 * (kscale + fabs(x) + fabs(y));
+  const double bx = 1.1 * bxm + ex;
+  const double by = 1.1 * bym + ex;
+  // round() is monotone: the reachable pixels are round(x - bx) .. round(x + bx)
+  const int x0 = (int)round(x - bx), x1 = (int)round(x + bx);
+  const int y0 = (int)round(y - by), y1 = (int)round(y + by);
+  if (x1 - x0 > 3 || y1 - y0 > 3) return false;
+  // the box's raster reads (at most 4 x 4) issue together; pixels outside
+  // the box or the raster re-read pixel 0 and are ignored
+  const int ncol = x1 - x0 + 1, nrow = y1 - y0 + 1;
+  float2 s[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int px = x0 + (q & 3), py = y0 + (q >> 2);
+    const bool in = (q & 3) < ncol && (q >> 2) < nrow && px >= 0 && px < a.W && py >= 0 && py < a.H;
+    s[q] = dl2[in ? py * a.W + px : 0];
+  }
+  const double r = c.r;
+  bool flat = true;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int px = x0 + (q & 3), py = y0 + (q >> 2);
+    if ((q & 3) < ncol && (q >> 2) < nrow) {
+      double f = 0.0;
+      if (px >= 0 && px < a.W && py >= 0 && py < a.H) {
+        const double dz = fabs((double)s[q].x - z) - a.threshold;
+        if (!(fabs(dz) > d + 1e-9 * (1.0 + fabs((double)s[q].x) + c.mag))) flat = false;
+        f = dz > 0.0 ? 0.0 : (label1 == s[q].y ? 0.0 : 1.0);
+      }
+      if (f != r) flat = false;
+    }
+  }
+  return flat;
+}
+
+// NB > 0: the batched stencil (NB parameters per step), the per-point route
+// only for samples with a decision inside a margin.  FLAT: the flat test
+// first; the samples it cannot clear are gathered into the workgroup's first
+// lanes (one sample per lane) and only those evaluate the stencil, so a
+// workgroup with few of them keeps most of its waves free.
+template <int M, bool FAST = false, int NB = 0, bool FLAT = false>
 __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, const SemTile* __restrict__ tiles,
                                                                      const PairConst* __restrict__ pcs,
                                                                      double* __restrict__ pair_blk,
@@ -528,116 +980,78 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
                                                                      int32_t* __restrict__ status_out,
                                                                      double* __restrict__ J_out, int write_samples) {
   constexpr int kHalf = kBlock / 2;
-  __shared__ double sJ[kHalf * kSemRow];
+  // sbuf: the tile's rows for the J'J reduction (kHalf x kSemRow), earlier
+  // (FLAT) the stencil results of the gathered samples (kBlock x 12)
+  constexpr int kBuf = FLAT ? kBlock * 12 : kHalf * kSemRow;
+  __shared__ double sbuf[kBuf];
   __shared__ double spart[2 * kPairVals];
   __shared__ double sred[4];
+  __shared__ int slist[FLAT ? kBlock : 1];
+  __shared__ int scnt[kBlock / 64];
+  double* sJ = sbuf;
   const SemTile t = tiles[blockIdx.x];
   const PairConst* __restrict__ P = pcs + t.pair;
   const int tid = threadIdx.x;
   const bool active = tid < (int)t.count;
   const int64_t n = (int64_t)t.start + tid;
+  const float2* dl2 = a.dl + (size_t)P->slot * a.H * a.W;
+  const double* K2 = P->K2;
   double cost = 0.0;
   double rowv[kSemRow];
 #pragma unroll
   for (int k = 0; k < kSemRow; ++k) rowv[k] = 0.0;
+  double r = 0.0;
+  int st = 0;
+  double Jt[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) Jt[k] = 0.0;
+  bool deferred = false;  // FLAT: stencil evaluated by a gathered lane
   if (active) {
     const SemSample smp = a.samples[n];
-    const float2* dl2 = a.dl + (size_t)P->slot * a.H * a.W;
-    const double* K2 = P->K2;
-    // centre: QuaternionRotatePoint(q_inv, P_c1) + t_inv, then pose 2
-    double rot[3];
-    unit_quat_rotate(P->uqi, smp.pc1, rot);
-    const double pw[3] = {rot[0] + P->ti[0], rot[1] + P->ti[1], rot[2] + P->ti[2]};
-    double rot2[3];
-    unit_quat_rotate(P->u2, pw, rot2);
-    const double p2[3] = {rot2[0] + P->t2[0], rot2[1] + P->t2[1], rot2[2] + P->t2[2]};
-    PixelCache pc;
-    pc.valid = false;
-    pc.px = pc.py = 0;
-    pc.depth = pc.label = 0.f;
-    int st = 0;
-    const double r = project_centre<M>(a, p2, smp.label1, K2, dl2, pc, &st);
-    const double mag = fabs(smp.pc1[0]) + fabs(smp.pc1[1]) + fabs(smp.pc1[2]) + fabs(P->t1[0]) + fabs(P->t1[1]) +
-                       fabs(P->t1[2]) + fabs(pw[0]) + fabs(pw[1]) + fabs(pw[2]) + fabs(P->t2[0]) +
-                       fabs(P->t2[1]) + fabs(P->t2[2]);
-    // Stencil: parameter m = 0..13 over (q1, t1, q2, t2), + then - (Ceres
-    // CENTRAL order), e = 2 m + minus.  Everything that depends only on the
-    // pair and the stencil point (perturbed value, 1/(2 delta), the
-    // perturbed rotation folded into one 3x3 map, PlusJacobian rows) comes
-    // from the per-pair table as wave-uniform scalar loads; a lane forms one
-    // mat-vec per point.  Tangent columns accumulate from 0.0 in m order,
-    // exactly as J_tangent = J_ambient * PlusJacobian does.
-    const double w[3] = {smp.pc1[0] - P->t1[0], smp.pc1[1] - P->t1[1], smp.pc1[2] - P->t1[2]};
-    const double exk = FAST ? margin_model_term<M>(K2, p2, mag) : 0.0;
-    double jq1[3] = {0.0, 0.0, 0.0}, jt1[3] = {0.0, 0.0, 0.0}, jq2[3] = {0.0, 0.0, 0.0}, jt2[3] = {0.0, 0.0, 0.0};
-    if (P->var1) {
-#pragma unroll 1
-      for (int m = 0; m < 4; ++m) {
-        double fp = 0.0, fm = 0.0;
-#pragma unroll 1
-        for (int sg = 0; sg < 2; ++sg) {
-          const double f = stencil_point<M, FAST, 0>(a, P, 2 * m + sg, m, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc, exk);
-          fp = sg == 0 ? f : fp;
-          fm = sg == 1 ? f : fm;
-        }
-        const double jm = (fp - fm) * P->ood[m];
-        const double* pj = P->pj[m];
+    Centre c;
+    centre_eval<M, FAST>(a, P, smp, K2, dl2, c);
+    r = c.r;
+    st = c.st;
+    if constexpr (FLAT)
+      deferred = !stencil_flat<M>(a, P, c, smp.label1, K2, dl2);  // flat: Jt stays +0.0
+    else
+      stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt);
+  }
+  if constexpr (FLAT) {
+    // gather the deferred samples into lanes 0 .. nd-1 (workgroup order)
+    const int lane = tid & 63;
+    const unsigned long long bal = __ballot(deferred);
+    if (lane == 0) scnt[tid >> 6] = __popcll(bal);
+    __syncthreads();
+    int base = 0, nd = 0;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) jq1[c] = jq1[c] + jm * pj[c];
-      }
-#pragma unroll 1
-      for (int k = 0; k < 3; ++k) {
-        const int m = 4 + k;
-        double fp = 0.0, fm = 0.0;
-#pragma unroll 1
-        for (int sg = 0; sg < 2; ++sg) {
-          const double f = stencil_point<M, FAST, 1>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc, exk);
-          fp = sg == 0 ? f : fp;
-          fm = sg == 1 ? f : fm;
-        }
-        const double jm = (fp - fm) * P->ood[m];
-        const double v = ((P->mask1 >> k) & 1u) ? 0.0 : jm;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) jt1[c] = c == k ? v : jt1[c];
-      }
+    for (int wv = 0; wv < kBlock / 64; ++wv) {
+      base += wv < (tid >> 6) ? scnt[wv] : 0;
+      nd += scnt[wv];
     }
-    if (P->var2) {
-#pragma unroll 1
-      for (int k = 0; k < 4; ++k) {
-        const int m = 7 + k;
-        double fp = 0.0, fm = 0.0;
-#pragma unroll 1
-        for (int sg = 0; sg < 2; ++sg) {
-          const double f = stencil_point<M, FAST, 2>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc, exk);
-          fp = sg == 0 ? f : fp;
-          fm = sg == 1 ? f : fm;
-        }
-        const double jm = (fp - fm) * P->ood[m];
-        const double* pj = P->pj[4 + k];
+    const int slot = base + __popcll(bal & ((1ull << lane) - 1ull));
+    if (deferred) slist[slot] = tid;
+    __syncthreads();
+    if (tid < nd) {
+      const SemSample smp = a.samples[(int64_t)t.start + slist[tid]];
+      Centre c;
+      centre_eval<M, FAST>(a, P, smp, K2, dl2, c);
+      double Jd[12];
+      stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jd);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) jq2[c] = jq2[c] + jm * pj[c];
-      }
-#pragma unroll 1
-      for (int k = 0; k < 3; ++k) {
-        const int m = 11 + k;
-        double fp = 0.0, fm = 0.0;
-#pragma unroll 1
-        for (int sg = 0; sg < 2; ++sg) {
-          const double f = stencil_point<M, FAST, 3>(a, P, 2 * m + sg, k, w, pw, p2, mag, smp.pc1, smp.label1, K2, dl2, pc, exk);
-          fp = sg == 0 ? f : fp;
-          fm = sg == 1 ? f : fm;
-        }
-        const double jm = (fp - fm) * P->ood[m];
-        const double v = ((P->mask2 >> k) & 1u) ? 0.0 : jm;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) jt2[c] = c == k ? v : jt2[c];
-      }
+      for (int k = 0; k < 12; ++k) sbuf[tid * 12 + k] = Jd[k];
     }
-    const double Jt[12] = {jq1[0], jq1[1], jq1[2], jt1[0], jt1[1], jt1[2],
-                           jq2[0], jq2[1], jq2[2], jt2[0], jt2[1], jt2[2]};
+    __syncthreads();
+    if (deferred) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) Jt[k] = sbuf[slot * 12 + k];
+    }
+    __syncthreads();  // sbuf is reused by the reduction below
+  }
+  if (active) {
     if (write_samples) {
       r_out[n] = r;
-      status_out[n] = st;
+      status_out[n] = st | ((write_samples & 2) && deferred ? 0x100 : 0);  // 2: mark deferred samples (diagnostic)
       double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
 #pragma unroll
       for (int m = 0; m < 6; ++m) jo[m] = make_double2(Jt[2 * m], Jt[2 * m + 1]);
@@ -687,6 +1101,142 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
   __syncthreads();
   if (tid < kPairVals) atomicAdd(pair_blk + (size_t)t.pair * kPairStride + tid, spart[tid] + spart[kPairVals + tid]);
   if (tid == 0) cost_partial[blockIdx.x] = sred[0] + sred[1] + sred[2] + sred[3];
+}
+
+// ---------------------------------------------------------------------------
+// Two-pass linearization (semantic_variant 6).  A sample the flat test clears
+// has J = +0.0: its row adds nothing to J'J or J'r, only its cost.  Pass 1
+// (one workgroup per tile) evaluates every sample's centre, cost and flat
+// test and appends the samples it cannot clear to their pair's region of a
+// deferred list (one atomic per wave).  Pass 2 runs the full stencil on the
+// deferred samples only, 64 per workgroup and all of one pair (wave-uniform
+// pair table), and reduces their J'J / J'r into the pair block — dense
+// waves, unlike in-tile compaction, which leaves most waves of a tile idle.
+// ---------------------------------------------------------------------------
+template <int M, bool FAST>
+__global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const SemTile* __restrict__ tiles,
+                                                               const PairConst* __restrict__ pcs,
+                                                               uint32_t* __restrict__ pair_cnt,
+                                                               uint32_t* __restrict__ dlist,
+                                                               double* __restrict__ cost_partial,
+                                                               double* __restrict__ r_out,
+                                                               int32_t* __restrict__ status_out,
+                                                               double* __restrict__ J_out, int write_samples) {
+  __shared__ double sred[kBlock / 64];
+  const SemTile t = tiles[blockIdx.x];
+  const PairConst* __restrict__ P = pcs + t.pair;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool active = tid < (int)t.count;
+  const int64_t n = (int64_t)t.start + tid;
+  const float2* dl2 = a.dl + (size_t)P->slot * a.H * a.W;
+  const double* K2 = P->K2;
+  double cost = 0.0;
+  bool deferred = false;
+  if (active) {
+    const SemSample smp = a.samples[n];
+    Centre c;
+    centre_eval<M, FAST>(a, P, smp, K2, dl2, c);
+    deferred = !stencil_flat<M>(a, P, c, smp.label1, K2, dl2);
+    double rho[3];
+    loss_eval(a.loss_type, a.loss_scale, c.r * c.r, rho);
+    cost = 0.5 * (a.weight * rho[0]);
+    if (write_samples) {
+      r_out[n] = c.r;
+      status_out[n] = c.st | ((write_samples & 2) && deferred ? 0x100 : 0);
+      if (!deferred) {
+        double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
+#pragma unroll
+        for (int m = 0; m < 6; ++m) jo[m] = make_double2(0.0, 0.0);
+      }
+    }
+  }
+  // append the wave's deferred samples to the pair's region
+  const unsigned long long bal = __ballot(deferred);
+  if (bal) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(pair_cnt + t.pair, (uint32_t)__popcll(bal));
+    base = __shfl(base, 0, 64);
+    if (deferred) {
+      const uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+      dlist[a.pairs[t.pair].start + slot] = (uint32_t)(n - a.pairs[t.pair].start);
+    }
+  }
+  double v = cost;
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if (lane == 0) sred[tid >> 6] = v;
+  __syncthreads();
+  if (tid == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) s += sred[w];
+    cost_partial[blockIdx.x] = s;
+  }
+}
+
+// Pass 2: chunk = 64 consecutive entries of one pair's deferred region
+// (chunks past the pair's count exit at once).
+template <int M, bool FAST, int NB>
+__global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const uint2* __restrict__ chunks,
+                                                              const PairConst* __restrict__ pcs,
+                                                              const uint32_t* __restrict__ pair_cnt,
+                                                              const uint32_t* __restrict__ dlist,
+                                                              double* __restrict__ pair_blk,
+                                                              double* __restrict__ J_out, int write_samples) {
+  __shared__ double sJ[64 * kSemRow];
+  const uint2 ch = chunks[blockIdx.x];  // (pair, first entry)
+  const uint32_t cnt = pair_cnt[ch.x];
+  if (ch.y >= cnt) return;
+  const PairConst* __restrict__ P = pcs + ch.x;
+  const int lane = threadIdx.x;
+  const uint32_t k = ch.y + lane;
+  const uint32_t pstart = a.pairs[ch.x].start;
+  const float2* dl2 = a.dl + (size_t)P->slot * a.H * a.W;
+  const double* K2 = P->K2;
+  double rowv[kSemRow];
+#pragma unroll
+  for (int q = 0; q < kSemRow; ++q) rowv[q] = 0.0;
+  if (k < cnt) {
+    const int64_t n = (int64_t)pstart + dlist[pstart + k];
+    const SemSample smp = a.samples[n];
+    Centre c;
+    centre_eval<M, FAST>(a, P, smp, K2, dl2, c);
+    double Jt[12];
+    stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt);
+    if (write_samples) {
+      double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
+#pragma unroll
+      for (int m = 0; m < 6; ++m) jo[m] = make_double2(Jt[2 * m], Jt[2 * m + 1]);
+    }
+    double rho[3];
+    loss_eval(a.loss_type, a.loss_scale, c.r * c.r, rho);
+    const double sc = sqrt(a.weight * rho[1]);
+#pragma unroll
+    for (int m = 0; m < 12; ++m) rowv[m] = Jt[m] * sc;
+    rowv[12] = c.r * sc;
+  }
+#pragma unroll
+  for (int q = 0; q < kSemRow; ++q) sJ[lane * kSemRow + q] = rowv[q];
+  __syncthreads();
+  const int rows = min(64, (int)(cnt - ch.y));
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int e = lane + 64 * h;
+    if (e < kPairVals) {
+      int ca, cb;
+      if (e < 78) {
+        int a_ = 0, rem = e;
+        while (rem >= 12 - a_) { rem -= 12 - a_; ++a_; }
+        ca = a_;
+        cb = a_ + rem;
+      } else {
+        ca = e - 78;
+        cb = 12;
+      }
+      double acc = 0.0;
+      for (int q = 0; q < rows; ++q) acc += sJ[q * kSemRow + ca] * sJ[q * kSemRow + cb];
+      atomicAdd(pair_blk + (size_t)ch.x * kPairStride + e, acc);
+    }
+  }
 }
 
 template <int M>
@@ -959,6 +1509,26 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
     for (int m = 0; m < kNumModels; ++m) S->model_tiles[m + 1] += S->model_tiles[m];
   }
   S->ntiles = (int)tiles.size();
+  // 64-entry chunks of every pair's deferred region, grouped by model like the tiles
+  std::vector<uint2> chunks;
+  {
+    std::vector<std::vector<uint2>> per(kNumModels);
+    for (int k = 0; k < S->npairs; ++k) {
+      const SemPair& pr = S->pairs_host[k];
+      const int m = hs.cam_model[p->image_camera[pr.j]];
+      for (uint32_t off = 0; off < pr.count; off += 64) per[m].push_back(make_uint2((uint32_t)k, off));
+    }
+    S->model_chunks[0] = 0;
+    for (int m = 0; m < kNumModels; ++m) {
+      chunks.insert(chunks.end(), per[m].begin(), per[m].end());
+      S->model_chunks[m + 1] = (int)chunks.size();
+    }
+  }
+  if (S->pair_cnt.alloc(std::max(1, S->npairs)) || S->dlist.alloc(std::max<int64_t>(1, S->ns)) ||
+      S->chunks.alloc(std::max<size_t>(1, chunks.size())))
+    return MI_BA_ERR_OUT_OF_MEMORY;
+  if (!chunks.empty() && hipMemcpy(S->chunks.ptr, chunks.data(), chunks.size() * sizeof(uint2), hipMemcpyHostToDevice))
+    return MI_BA_ERR_HIP;
   if (S->samples.alloc(S->ns) || S->pairs.alloc(S->npairs) || S->raster_slot.alloc(I) ||
       S->dl.alloc(plane * std::max<size_t>(1, slot_images.size())) || S->r.alloc(S->ns) ||
       S->status.alloc(S->ns) || S->J.alloc(12 * S->ns) ||
@@ -1005,19 +1575,42 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   timer_begin(ctx, "semantic_jacobian", &stop);
   hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 1) / 2), dim3(64), 0, s, S->pairs.ptr, S->npairs,
                      a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs);
-  for (int model = 0; model < kNumModels; ++model) {
+  if (ctx->sem_variant == 6) {
+    if (hipMemsetAsync(S->pair_cnt.ptr, 0, sizeof(uint32_t) * S->npairs, s) != hipSuccess) return MI_BA_ERR_HIP;
+    const int ws = write_samples ? 1 | (ctx->sem_diag ? 2 : 0) : 0;
+    for (int model = 0; model < kNumModels; ++model) {
+      const int t0 = S->model_tiles[model], nt = S->model_tiles[model + 1] - t0;
+      const int c0 = S->model_chunks[model], nc = S->model_chunks[model + 1] - c0;
+      if (nt == 0) continue;
+      dispatch_model(model, [&](auto m) {
+        constexpr int M = decltype(m)::value;
+        hipLaunchKernelGGL((semantic_flat_kernel<M, true>), dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0, pcs,
+                           S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr,
+                           ws);
+        if (nc > 0)
+          hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4>), dim3(nc), dim3(64), 0, s, a, S->chunks.ptr + c0,
+                             pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
+      });
+    }
+  }
+  for (int model = 0; model < kNumModels && ctx->sem_variant != 6; ++model) {
     const int t0 = S->model_tiles[model], nt = S->model_tiles[model + 1] - t0;
     if (nt == 0) continue;
     dispatch_model(model, [&](auto m) {
       constexpr int M = decltype(m)::value;
-      if (ctx->sem_variant == 1)
-        hipLaunchKernelGGL((semantic_linearize_kernel<M, true>), dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0,
-                           pcs, S->pair_blk.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr,
-                           write_samples ? 1 : 0);
-      else
-        hipLaunchKernelGGL((semantic_linearize_kernel<M, false>), dim3(nt), dim3(kBlock), 0, s, a,
-                           S->tiles.ptr + t0, pcs, S->pair_blk.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr,
-                           S->J.ptr, write_samples ? 1 : 0);
+      auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0, pcs, S->pair_blk.ptr,
+                           S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr,
+                           write_samples ? 1 | (ctx->sem_diag ? 2 : 0) : 0);
+      };
+      switch (ctx->sem_variant) {
+        case 0: launch(semantic_linearize_kernel<M, false>); break;
+        case 1: launch(semantic_linearize_kernel<M, true>); break;
+        case 2: launch(semantic_linearize_kernel<M, true, 1>); break;
+        case 3: launch(semantic_linearize_kernel<M, true, 2>); break;
+        case 4: launch(semantic_linearize_kernel<M, true, 4>); break;
+        default: launch(semantic_linearize_kernel<M, true, 4, true>); break;
+      }
     });
   }
   timer_end(ctx, stop);

@@ -220,6 +220,28 @@ def test_semantic_parity_bitwise(gpu, model):
     assert (st_o == mi_ba.VALID).sum() > 0 and (np.abs(J_o).sum(axis=1) > 0).sum() > 0
 
 
+@pytest.mark.parametrize("model", [mi_ba.SIMPLE_PINHOLE, mi_ba.SIMPLE_RADIAL, mi_ba.OPENCV])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+def test_semantic_kernel_variants_bitwise(gpu, model, variant):
+    """Every semantic kernel variant (0 uncontracted per-point route, 1 FMA
+    per-point route, 2-4 batched stencil with 1/2/4 parameters per step,
+    5 flat test + batched stencil on the gathered samples, 6 flat pass +
+    deferred-sample pass)
+    reproduces the oracle's samples bit for bit, constant first/second poses
+    and a constant tvec component included (gauge)."""
+    sc, sem = semantic_scene(model, images=4, size=160, step=3, seed=5)
+    opts = mi_ba.default_options()
+    px_o, st_o, r_o, J_o = oracle.semantic_eval(opts, sc, sem)
+    with mi_ba.Context(opts, sc.copy(), sem) as ctx:
+        ctx.set_tuning("semantic_variant", variant)
+        ctx.evaluate_semantic()
+        px_g, st_g, r_g, J_g = ctx.download_semantic()
+    assert np.array_equal(px_g, px_o)
+    same = (st_g == st_o) & (r_g == r_o) & np.all(J_g == J_o, axis=1)
+    assert same.mean() >= 0.9999, (len(st_o), int((~same).sum()))
+    assert (np.abs(J_o).sum(axis=1) > 0).sum() > 0
+
+
 def test_semantic_solve_parity(gpu):
     """Semantic BA (pose-only, constant intrinsics) through both LMs."""
     sc, sem = semantic_scene(mi_ba.SIMPLE_PINHOLE, images=3, size=120, step=4)

@@ -40,7 +40,14 @@ for v in [int(x) for x in args.variants.split(",")]:
         ms, n = ctx.kernel_time("semantic_jacobian")
         ctx.set_timing(False)
         ts.append(ms / n)
-    print(json.dumps({"variant": v, "samples": ns, "median_ms": float(np.median(ts)), "min_ms": float(np.min(ts)),
+    deferred = None
+    if v in (5, 6):
+        ctx.set_tuning("semantic_diag", 1)
+        ctx.evaluate_semantic()
+        _, st_d, _, _ = ctx.download_semantic()
+        deferred = int(((st_d & 0x100) != 0).sum())
+        ctx.set_tuning("semantic_diag", 0)
+    print(json.dumps({"variant": v, "deferred": deferred, "samples": ns, "median_ms": float(np.median(ts)), "min_ms": float(np.min(ts)),
                       "bitwise_equal_to_variant0": same,
                       "valid": int((st_v == mi_ba.VALID).sum()), "nonzero_J_rows": int((np.abs(J_v).sum(1) > 0).sum()),
                       "checksum_J": float(np.abs(J_v).sum()), "checksum_r": float(r_v.sum())}), flush=True)

@@ -14,18 +14,22 @@ import sys
 from collections import defaultdict
 
 src, dst = sys.argv[1], sys.argv[2]
-vals = defaultdict(list)
-dur = []
+# one linearization = one launch of each semantic kernel family present
+# (semantic_linearize_kernel, or semantic_flat_kernel + semantic_deferred_kernel):
+# per-family averages per launch, summed over the families
+fams = ("semantic_linearize", "semantic_flat", "semantic_deferred")
+vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        if "semantic_linearize" not in r["Kernel_Name"]:
+        fam = next((x for x in fams if x in r["Kernel_Name"]), None)
+        if fam is None:
             continue
-        vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-        dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-avg = {k: sum(v) / len(v) for k, v in vals.items()}
+        vals[r["Counter_Name"]][fam].append(float(r["Counter_Value"]))
+avg = {k: sum(sum(v) / len(v) for v in per.values()) for k, per in vals.items()}
 f64 = 64 * (avg.get("SQ_INSTS_VALU_ADD_F64", 0) + avg.get("SQ_INSTS_VALU_MUL_F64", 0) +
             avg.get("SQ_INSTS_VALU_TRANS_F64", 0) + 2 * avg.get("SQ_INSTS_VALU_FMA_F64", 0))
-out = {"kernel": "semantic_linearize_kernel", "launches_sampled": {k: len(v) for k, v in vals.items()},
+out = {"kernel": "+".join(sorted({f for per in vals.values() for f in per})),
+       "launches_sampled": {k: {f: len(v) for f, v in per.items()} for k, per in vals.items()},
        "counters_avg_per_launch": avg,
        "fp64_ops_per_launch": f64,
        "hbm_bytes_per_launch": 1024 * (2 * avg.get("FETCH_SIZE", 0) + avg.get("WRITE_SIZE", 0))
