@@ -888,9 +888,16 @@ __device__ __forceinline__ void stencil_full(const SemArgs& a, const PairConst* 
 // near zero, huge coordinates, a wide pixel box) the sample takes the full
 // stencil.
 // ---------------------------------------------------------------------------
+struct FlatBox {
+  int x0, y0, ncol, nrow;  // reachable pixels (x0 .. x0 + ncol - 1, y0 .. y0 + nrow - 1)
+  double d;                // bound of the depth change
+};
+
+// Geometry half of the flat test: false when the sample cannot be cleared
+// whatever the raster holds.  c needs p2, pw, w, mag (not the raster).
 template <int M>
-__device__ __forceinline__ bool stencil_flat(const SemArgs& a, const PairConst* __restrict__ P, const Centre& c,
-                                             float label1, const double* K2, const float2* __restrict__ dl2) {
+__device__ __forceinline__ bool flat_box(const PairConst* __restrict__ P, const Centre& c, const double* K2,
+                                         FlatBox& fb) {
   const double z = c.p2[2];
   if (!(z > 0.0)) return false;  // NaN-safe
   const double iz = 1.0 / z;
@@ -901,69 +908,87 @@ __device__ __forceinline__ bool stencil_flat(const SemArgs& a, const PairConst* 
   if (!(fabs(x) < 1e8 && fabs(y) < 1e8 && fabs(u) < 1e6 && fabs(v) < 1e6)) return false;
   // per class of stencil points, componentwise bounds (ax, ay, az) of the
   // camera-2 point's displacement: du <= (ax + |u| az) / (z - az), dv alike
-  double bxm = 0.0, bym = 0.0, dz = 0.0, gm = 0.0;
-  bool ok = true;
+  // (one reciprocal for every class: 1 / (z - az_max) bounds each 1 / (z - az))
+  const double dq1 = P->var1 ? P->rho1 * sqrt(c.w[0] * c.w[0] + c.w[1] * c.w[1] + c.w[2] * c.w[2]) * (1.0 + 1e-12) : 0.0;
+  const double dq2 = P->var2 ? P->rho2 * sqrt(c.pw[0] * c.pw[0] + c.pw[1] * c.pw[1] + c.pw[2] * c.pw[2]) * (1.0 + 1e-12) : 0.0;
+  double az_max = fmax(dq1, dq2);
+  if (P->var1)
+    az_max = fmax(az_max, fmax(P->dt1[0] * fabs(P->C[6]), fmax(P->dt1[1] * fabs(P->C[7]), P->dt1[2] * fabs(P->C[8]))));
+  if (P->var2) az_max = fmax(az_max, P->dt2[2]);
+  if (!(z - az_max > 0.5 * z)) return false;
+  const double iden = 1.0 / (z - az_max) * (1.0 + 1e-12);
+  double bxm = 0.0, bym = 0.0, gm = 0.0;
   auto cls = [&](double ax, double ay, double az) {
-    const double den = z - az;
-    ok = ok && den > 0.5 * z;
-    const double du = (ax + fabs(u) * az) / den, dv = (ay + fabs(v) * az) / den;
+    const double du = (ax + fabs(u) * az) * iden, dv = (ay + fabs(v) * az) * iden;
     bxm = fmax(bxm, fabs(A[0]) * du + fabs(A[1]) * dv);
     bym = fmax(bym, fabs(A[2]) * du + fabs(A[3]) * dv);
-    dz = fmax(dz, az);
     gm = fmax(gm, fmax(du, dv));
   };
   if (P->var1) {
-    const double dq = P->rho1 * sqrt(c.w[0] * c.w[0] + c.w[1] * c.w[1] + c.w[2] * c.w[2]) * (1.0 + 1e-12);
-    cls(dq, dq, dq);
+    cls(dq1, dq1, dq1);
 #pragma unroll
     for (int k = 0; k < 3; ++k)
       cls(P->dt1[k] * fabs(P->C[k]), P->dt1[k] * fabs(P->C[3 + k]), P->dt1[k] * fabs(P->C[6 + k]));
   }
   if (P->var2) {
-    const double dq = P->rho2 * sqrt(c.pw[0] * c.pw[0] + c.pw[1] * c.pw[1] + c.pw[2] * c.pw[2]) * (1.0 + 1e-12);
-    cls(dq, dq, dq);
+    cls(dq2, dq2, dq2);
     cls(P->dt2[0], 0.0, 0.0);
     cls(0.0, P->dt2[1], 0.0);
     cls(0.0, 0.0, P->dt2[2]);
   }
-  if (!ok) return false;
   const double gain = distortion_gain<M>(K2, u * u + v * v);
   if (!(gain * gm * (1.0 + fabs(u) + fabs(v)) <= 2e-3)) return false;
-  const double d = dz;
   const double kscale = (fabs(K2[0]) + fabs(K2[1])) * gain * (1.0 + fabs(u) + fabs(v)) * (1.0 + c.mag * fabs(iz));
   const double ex = 1e-6 + 1e-11 * (kscale + fabs(x) + fabs(y));
   const double bx = 1.1 * bxm + ex;
   const double by = 1.1 * bym + ex;
   // round() is monotone: the reachable pixels are round(x - bx) .. round(x + bx)
-  const int x0 = (int)round(x - bx), x1 = (int)round(x + bx);
-  const int y0 = (int)round(y - by), y1 = (int)round(y + by);
-  if (x1 - x0 > 3 || y1 - y0 > 3) return false;
-  // the box's raster reads (at most 4 x 4) issue together; pixels outside
-  // the box or the raster re-read pixel 0 and are ignored
-  const int ncol = x1 - x0 + 1, nrow = y1 - y0 + 1;
-  float2 s[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int px = x0 + (q & 3), py = y0 + (q >> 2);
-    const bool in = (q & 3) < ncol && (q >> 2) < nrow && px >= 0 && px < a.W && py >= 0 && py < a.H;
-    s[q] = dl2[in ? py * a.W + px : 0];
-  }
-  const double r = c.r;
+  fb.x0 = (int)round(x - bx);
+  fb.y0 = (int)round(y - by);
+  fb.ncol = (int)round(x + bx) - fb.x0 + 1;
+  fb.nrow = (int)round(y + by) - fb.y0 + 1;
+  fb.d = az_max;
+  return fb.ncol <= 3 && fb.nrow <= 3;
+}
+
+// Box entry q (of 3 x 3): raster index to read (pixel 0 when q is outside the
+// box or the raster — read and ignored, so every read issues unconditionally).
+__device__ __forceinline__ int flat_index(const SemArgs& a, const FlatBox& fb, bool cand, int q) {
+  const int px = fb.x0 + q % 3, py = fb.y0 + q / 3;
+  const bool in = cand && q % 3 < fb.ncol && q / 3 < fb.nrow && px >= 0 && px < a.W && py >= 0 && py < a.H;
+  return in ? py * a.W + px : 0;
+}
+
+// Raster half: every box pixel gives the centre's outcome r for every depth
+// within d of z (outside the margin).
+__device__ __forceinline__ bool flat_check(const SemArgs& a, const FlatBox& fb, const float2 s[9], double z,
+                                           double mag, float label1, double r) {
   bool flat = true;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int px = x0 + (q & 3), py = y0 + (q >> 2);
-    if ((q & 3) < ncol && (q >> 2) < nrow) {
+  for (int q = 0; q < 9; ++q) {
+    const int px = fb.x0 + q % 3, py = fb.y0 + q / 3;
+    if (q % 3 < fb.ncol && q / 3 < fb.nrow) {
       double f = 0.0;
       if (px >= 0 && px < a.W && py >= 0 && py < a.H) {
         const double dz = fabs((double)s[q].x - z) - a.threshold;
-        if (!(fabs(dz) > d + 1e-9 * (1.0 + fabs((double)s[q].x) + c.mag))) flat = false;
+        if (!(fabs(dz) > fb.d + 1e-9 * (1.0 + fabs((double)s[q].x) + mag))) flat = false;
         f = dz > 0.0 ? 0.0 : (label1 == s[q].y ? 0.0 : 1.0);
       }
       if (f != r) flat = false;
     }
   }
   return flat;
+}
+
+template <int M>
+__device__ __forceinline__ bool stencil_flat(const SemArgs& a, const PairConst* __restrict__ P, const Centre& c,
+                                             float label1, const double* K2, const float2* __restrict__ dl2) {
+  FlatBox fb;
+  if (!flat_box<M>(P, c, K2, fb)) return false;
+  float2 s[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) s[q] = dl2[flat_index(a, fb, true, q)];
+  return flat_check(a, fb, s, c.p2[2], c.mag, label1, c.r);
 }
 
 // NB > 0: the batched stencil (NB parameters per step), the per-point route
@@ -1134,9 +1159,50 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
   bool deferred = false;
   if (active) {
     const SemSample smp = a.samples[n];
+    // centre geometry (reference sequence, as centre_eval / project_centre)
     Centre c;
-    centre_eval<M, FAST>(a, P, smp, K2, dl2, c);
-    deferred = !stencil_flat<M>(a, P, c, smp.label1, K2, dl2);
+    double rot[3];
+    unit_quat_rotate(P->uqi, smp.pc1, rot);
+    c.pw[0] = rot[0] + P->ti[0];
+    c.pw[1] = rot[1] + P->ti[1];
+    c.pw[2] = rot[2] + P->ti[2];
+    double rot2[3];
+    unit_quat_rotate(P->u2, c.pw, rot2);
+    c.p2[0] = rot2[0] + P->t2[0];
+    c.p2[1] = rot2[1] + P->t2[1];
+    c.p2[2] = rot2[2] + P->t2[2];
+    c.mag = fabs(smp.pc1[0]) + fabs(smp.pc1[1]) + fabs(smp.pc1[2]) + fabs(P->t1[0]) + fabs(P->t1[1]) +
+            fabs(P->t1[2]) + fabs(c.pw[0]) + fabs(c.pw[1]) + fabs(c.pw[2]) + fabs(P->t2[0]) + fabs(P->t2[1]) +
+            fabs(P->t2[2]);
+    c.w[0] = smp.pc1[0] - P->t1[0];
+    c.w[1] = smp.pc1[1] - P->t1[1];
+    c.w[2] = smp.pc1[2] - P->t1[2];
+    const double u2 = c.p2[0] / c.p2[2];
+    const double v2 = c.p2[1] / c.p2[2];
+    double x2, y2;
+    world_to_image<M>(K2, u2, v2, &x2, &y2);
+    const int cpx = cast_to_int_x86(round(x2));
+    const int cpy = cast_to_int_x86(round(y2));
+    const bool cin = !(cpx < 0 || cpx >= a.W || cpy < 0 || cpy >= a.H);
+    FlatBox fb;
+    const bool cand = flat_box<M>(P, c, K2, fb);
+    // every raster read of the sample in one round trip: the centre pixel and the box
+    const float2 sc = dl2[cin ? cpy * a.W + cpx : 0];
+    float2 s[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) s[q] = dl2[flat_index(a, fb, cand, q)];
+    // centre outcome (semantic_cost_functions.h:141-205)
+    if (!cin) {
+      c.st = MI_BA_OUT_OF_BOUNDS;
+      c.r = 0.0;
+    } else if (fabs((double)sc.x - c.p2[2]) > a.threshold) {
+      c.st = MI_BA_INVALID_DEPTH;
+      c.r = 0.0;
+    } else {
+      c.st = MI_BA_VALID;
+      c.r = (smp.label1 == sc.y) ? 0.0 : 1.0;
+    }
+    deferred = !(cand && flat_check(a, fb, s, c.p2[2], c.mag, smp.label1, c.r));
     double rho[3];
     loss_eval(a.loss_type, a.loss_scale, c.r * c.r, rho);
     cost = 0.5 * (a.weight * rho[0]);
