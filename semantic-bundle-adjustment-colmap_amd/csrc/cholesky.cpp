@@ -1273,17 +1273,21 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
   if (nblk > 0) {
     if (hipMalloc(&linv, sizeof(double) * kTB * kTB * (size_t)nblk) != hipSuccess) { linv = nullptr; return false; }
     if (hipMalloc(&ybuf, sizeof(double) * kTB * (size_t)nblk) != hipSuccess) { ybuf = nullptr; return false; }
-    if (hipMemset(linv, 0, sizeof(double) * kTB * kTB * (size_t)nblk) != hipSuccess) return false;
+    // stream-ordered zero fills, complete before the workspace is used (a
+    // null-stream memset is not ordered against the non-blocking streams)
+    if (hipMemsetAsync(linv, 0, sizeof(double) * kTB * kTB * (size_t)nblk, side) != hipSuccess) return false;
     if (hipMalloc(&ctrl, sizeof(unsigned) * (2 + (size_t)nblk)) != hipSuccess) { ctrl = nullptr; return false; }
     if (hipMalloc(&pf_ctrl, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles)) != hipSuccess) {
       pf_ctrl = nullptr;
       return false;
     }
-    if (hipMemset(pf_ctrl, 0, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles)) != hipSuccess) return false;
+    if (hipMemsetAsync(pf_ctrl, 0, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles), side) != hipSuccess)
+      return false;
     if (hipMalloc(&pf_linv, sizeof(double) * 64 * 64 * kPfMaxTiles) != hipSuccess) { pf_linv = nullptr; return false; }
     pf_base = 0;
     pf_epoch = 0;
-    if (hipMemset(ctrl, 0, sizeof(unsigned) * (2 + (size_t)nblk)) != hipSuccess) return false;
+    if (hipMemsetAsync(ctrl, 0, sizeof(unsigned) * (2 + (size_t)nblk), side) != hipSuccess) return false;
+    if (hipStreamSynchronize(side) != hipSuccess) return false;
     epoch = 0;
     linv_rows = nblk * kTB;
   }

@@ -264,8 +264,9 @@ __device__ inline void wave_load_rows(const double* __restrict__ src, double* __
 // decomposition (1 = no J store, 2 = no arithmetic); never used by the LM.
 // Build options (bits of D): 8 nontemporal J stores, 16 nontemporal obs
 // loads and r stores, 32 16-B J stores, 128 per-block loads issued up front;
-// 1 and 2 are the diagnostic builds.
-constexpr int kJacProduction = 8 | 16 | 32 | 128;
+// 1 and 2 are the diagnostic builds; 512 closed-form rotation columns, 1024
+// R X through the rotation matrix.
+constexpr int kJacProduction = 8 | 16 | 32 | 128 | 512 | 1024;  // 0.583 -> 0.543 ms at C4 with 512 | 1024
 constexpr int kJacR1 = 8 | 16 | 32;  // round-1 production (three serial round trips), A/B variant 23
 // TB: threads per workgroup.  The cost partial is per wave (no workgroup
 // barrier), cost_partial[i / 64].
@@ -397,7 +398,16 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       pose_var = flags & 1u;
       cv = (meta >> 8) & 1u;
       double P[3];
-      unit_quat_rotate(q, X, P);
+      double Rm[9];
+      if constexpr ((D & 1024) != 0) {
+        // R X from the rotation matrix the point columns need anyway
+        unit_quat_matrix(q, Rm);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) P[c] = Rm[3 * c] * X[0] + Rm[3 * c + 1] * X[1] + Rm[3 * c + 2] * X[2];
+      } else {
+        unit_quat_rotate(q, X, P);
+      }
+      const double a0 = P[0], a1 = P[1], a2 = P[2];  // R X
       P[0] += t[0];
       P[1] += t[1];
       P[2] += t[2];
@@ -428,7 +438,14 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   #pragma unroll
         for (int k = 0; k < 6; ++k) B[k] *= sc;
       }
-      if (pose_var) {
+      if (pose_var && (D & 512)) {
+        // d(R X)/d(tangent) of QuaternionManifold (plus = q_delta * q, rotation
+        // angle 2|delta|) = -2 [R X]x, the product Dq * PlusJacobian below in
+        // closed form (equal up to rounding for a unit q)
+        Mq[0] = 0.0;       Mq[1] = 2.0 * a2;  Mq[2] = -2.0 * a1;
+        Mq[3] = -2.0 * a2; Mq[4] = 0.0;       Mq[5] = 2.0 * a0;
+        Mq[6] = 2.0 * a1;  Mq[7] = -2.0 * a0; Mq[8] = 0.0;
+      } else if (pose_var) {
         double Dq[12], PJ[12];
         unit_quat_rotate_dq(q, X, Dq);
         quat_plus_jacobian(q, PJ);
@@ -441,7 +458,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
       if (ptv) {
         double R[9];
-        unit_quat_matrix(q, R);
+        if constexpr ((D & 1024) != 0) {
+#pragma unroll
+          for (int c = 0; c < 9; ++c) R[c] = Rm[c];
+        } else {
+          unit_quat_matrix(q, R);
+        }
   #pragma unroll
         for (int rw = 0; rw < 2; ++rw)
   #pragma unroll
@@ -1799,6 +1821,22 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
             case 35:
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 64, 6>), dim3(g), dim3(kBlock), 0, s, p, r,
                                  J, cost_partial);
+              return;
+            case 36:  // closed-form rotation columns
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 512>), dim3(g), dim3(kBlock), 0, s,
+                                 p, r, J, cost_partial);
+              return;
+            case 37:  // closed-form rotation columns, R X through the rotation matrix
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 512 | 1024>), dim3(g), dim3(kBlock),
+                                 0, s, p, r, J, cost_partial);
+              return;
+            case 38:  // closed-form rotation columns, raised-priority store bursts
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 512 | 256>), dim3(g), dim3(kBlock),
+                                 0, s, p, r, J, cost_partial);
+              return;
+            case 39:  // closed-form rotation columns, 5 waves per SIMD
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 512, 5>), dim3(g), dim3(kBlock),
+                                 0, s, p, r, J, cost_partial);
               return;
             case 9:
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 1>), dim3(g), dim3(kBlock), 0, s, p, r, J,

@@ -226,7 +226,9 @@ mi_ba_status build_pair_tiles(mi_ba_context* ctx) {
   if ((npairs && hipMemcpy(ctx->pairs.ptr, pr.data(), npairs * sizeof(uint2), hipMemcpyHostToDevice)) ||
       (!tl.empty() && hipMemcpy(ctx->ptiles.ptr, tl.data(), tl.size() * sizeof(DevPairTile), hipMemcpyHostToDevice)))
     return MI_BA_ERR_HIP;
-  if (d.num_points && hipMemset(ctx->Linv.ptr, 0, 6 * (size_t)d.num_points * 8)) return MI_BA_ERR_HIP;
+  // stream-ordered: a null-stream memset is not ordered against the context's
+  // non-blocking stream (the LM's kernels could overtake it)
+  if (d.num_points && hipMemsetAsync(ctx->Linv.ptr, 0, 6 * (size_t)d.num_points * 8, ctx->stream)) return MI_BA_ERR_HIP;
   return MI_BA_OK;
 }
 
@@ -449,9 +451,12 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
     ctx->host_scalars = nullptr;
     return fail(MI_BA_ERR_OUT_OF_MEMORY);
   }
-  if (hipMemset(ctx->scalars.ptr, 0, sizeof(double) * kNumScalars) != hipSuccess) return fail(MI_BA_ERR_HIP);
-  if (P && (hipMemset(ctx->dX.ptr, 0, 3 * P * 8) || hipMemset(ctx->Vinv.ptr, 0, 6 * P * 8) ||
-            hipMemset(ctx->cg_w.ptr, 0, 3 * P * 8)))
+  // stream-ordered (see build_pair_tiles)
+  if (hipMemsetAsync(ctx->scalars.ptr, 0, sizeof(double) * kNumScalars, ctx->stream) != hipSuccess)
+    return fail(MI_BA_ERR_HIP);
+  if (P && (hipMemsetAsync(ctx->dX.ptr, 0, 3 * P * 8, ctx->stream) ||
+            hipMemsetAsync(ctx->Vinv.ptr, 0, 6 * P * 8, ctx->stream) ||
+            hipMemsetAsync(ctx->cg_w.ptr, 0, 3 * P * 8, ctx->stream)))
     return fail(MI_BA_ERR_HIP);
   // Linear solver (bundle_adjustment.cc:276-286): Ceres factorises the
   // reduced camera system exactly up to 1000 images (DENSE_SCHUR <= 50,

@@ -39,6 +39,7 @@ for v in variants:
     if ref is None:
         ref = (r.copy(), J.copy())
     ok[v] = bool(np.array_equal(r, ref[0]) and np.array_equal(J, ref[1]))
+    ok[v] = (ok[v], float(np.abs(J - ref[1]).max() / max(1.0, float(np.abs(ref[1]).max()))))
     del r, J
 res = {v: [] for v in variants}
 for rnd in range(args.rounds):
@@ -54,7 +55,7 @@ for rnd in range(args.rounds):
         res[v].append(ms / n)
 for v in variants:
     med = float(np.median(res[v]))
-    print(json.dumps({"config": args.config, "variant": v, "identical_to_first": ok[v], "blocks": nb,
+    print(json.dumps({"config": args.config, "variant": v, "identical_to_first": ok[v][0], "max_rel_dJ_vs_first": ok[v][1], "blocks": nb,
                       "bytes_per_block": bpb, "median_ms": med, "min_ms": float(np.min(res[v])),
                       "GBps": bpb * nb / (med * 1e-3) / 1e9, "frac_of_8TBps": bpb * nb / (med * 1e-3) / 8e12}))
 ctx.close()
