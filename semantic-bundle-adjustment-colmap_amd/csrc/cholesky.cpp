@@ -533,6 +533,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
 // launch, release/acquire at agent scope, as the sweeps above).
 typedef double pf_dvec4 __attribute__((ext_vector_type(4)));
 constexpr int kPfMaxTiles = 8;  // column tiles per panel (panel <= 512)
+constexpr int kTinv = 512;  // own_diag 7: widest panel
 constexpr int kPfRows = 4;      // row tiles per below-diagonal workgroup
 
 __device__ __forceinline__ int pf_row0(int r, int kb, int nc) { return r < nc ? 64 * r : kb + 64 * (r - nc); }
@@ -1163,9 +1164,35 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
 
+// own_diag 7: the two-kernel diagonal factor, then the panel solve
+// A_ik <- A_ik L_kk^-T as one dgemm against the explicit inverse of the
+// diagonal block (rocBLAS dtrtri) instead of a dtrsm: the panel solve runs at
+// dgemm rate off a copy of the panel.
+rocblas_status panel_factor_inv(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info,
+                                double* scratch, CholWorkspace* ws) {
+  if (!ws || !ws->tinv || !ws->tbuf || kb > kTinv || n - k - kb > ws->tbuf_rows) return rocblas_status_invalid_pointer;
+  double* Akk = A + k + (size_t)k * lda;
+  rocblas_status st = potrf_leaf(h, kb, Akk, lda, info, 2, scratch);
+  if (st != rocblas_status_success) return st;
+  const int m = n - k - kb;
+  if (m == 0) return st;
+  hipStream_t s;
+  if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
+  if (hipMemsetAsync(ws->tinv, 0, sizeof(double) * kb * kb, s) != hipSuccess) return rocblas_status_internal_error;
+  st = rocblas_dtrtri(h, rocblas_fill_lower, rocblas_diagonal_non_unit, kb, Akk, lda, ws->tinv, kb);
+  if (st != rocblas_status_success) return st;
+  if (hipMemcpy2DAsync(ws->tbuf, sizeof(double) * m, Akk + kb, sizeof(double) * lda, sizeof(double) * m, kb,
+                       hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return rocblas_status_internal_error;
+  const double one = 1.0, zero = 0.0;
+  return rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, kb, kb, &one, ws->tbuf, m, ws->tinv,
+                       kb, &zero, Akk + kb, lda);
+}
+
 rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, int own,
                             double* scratch, CholWorkspace* ws) {
   if (own == 6) return panel_factor_fused(h, n, A, lda, k, kb, info, ws);
+  if (own == 7) return panel_factor_inv(h, n, A, lda, k, kb, info, scratch, ws);
   double* Akk = A + k + (size_t)k * lda;
   rocblas_status st = potrf_leaf(h, kb, Akk, lda, info, own, scratch);
   if (st != rocblas_status_success) return st;
@@ -1287,6 +1314,9 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
     pf_base = 0;
     pf_epoch = 0;
     if (hipMemsetAsync(ctrl, 0, sizeof(unsigned) * (2 + (size_t)nblk), side) != hipSuccess) return false;
+    if (hipMalloc(&tinv, sizeof(double) * kTinv * kTinv) != hipSuccess) { tinv = nullptr; return false; }
+    if (hipMalloc(&tbuf, sizeof(double) * kTinv * (size_t)nblk * kTB) != hipSuccess) { tbuf = nullptr; return false; }
+    tbuf_rows = nblk * kTB;
     if (hipStreamSynchronize(side) != hipSuccess) return false;
     epoch = 0;
     linv_rows = nblk * kTB;
@@ -1321,6 +1351,11 @@ void CholWorkspace::destroy() {
   pf_ctrl = nullptr;
   if (pf_linv) (void)hipFree(pf_linv);
   pf_linv = nullptr;
+  if (tinv) (void)hipFree(tinv);
+  tinv = nullptr;
+  if (tbuf) (void)hipFree(tbuf);
+  tbuf = nullptr;
+  tbuf_rows = 0;
   linv_rows = 0;
 }
 
@@ -1332,6 +1367,7 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   // widths (and the recursive split) take the two-kernel diagonal factor
   CholConfig c = cfg;
   if (c.own_diag == 6 && (c.panel <= 0 || c.panel > 64 * kPfMaxTiles)) c.own_diag = 2;
+  if (c.own_diag == 7 && (c.panel <= 0 || c.panel > kTinv)) c.own_diag = 2;
   if (ws) ws->pf_rows = c.panel_rows;
   double* scratch = ws ? ws->scratch : nullptr;
   if (c.panel > 0 && c.gemm_update && c.lookahead && ws && ws->side)

@@ -77,6 +77,9 @@ struct CholWorkspace {
   unsigned pf_epoch = 0;        // flag value of the last panel launch
   int pf_rows = 1;              // row tiles per below-diagonal workgroup (CholConfig::panel_rows)
   int linv_rows = 0;
+  double* tinv = nullptr;       // own_diag 7: [512*512] inverse of the panel's diagonal block
+  double* tbuf = nullptr;       // own_diag 7: [max_n * 512] copy of the panel below it
+  int tbuf_rows = 0;
 
   // Creates the resources on `device` with events for up to `max_panels`
   // panels and diagonal-block inverses for matrices up to max_n; false on any

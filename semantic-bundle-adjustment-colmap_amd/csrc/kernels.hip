@@ -267,6 +267,10 @@ __device__ inline void wave_load_rows(const double* __restrict__ src, double* __
 // 1 and 2 are the diagnostic builds; 512 closed-form rotation columns, 1024
 // R X through the rotation matrix.
 constexpr int kJacProduction = 8 | 16 | 32 | 128 | 512 | 1024;  // 0.583 -> 0.543 ms at C4 with 512 | 1024
+// J rows staged in one slab pass (64 rows, 17 KB of LDS per wave at OPENCV: 2
+// waves per SIMD, each store burst 15 KB): 0.554 (2 passes) -> 0.454 ms at C4
+// once the arithmetic was cut by the closed-form rotation columns
+constexpr int kJacPasses = 1;
 constexpr int kJacR1 = 8 | 16 | 32;  // round-1 production (three serial round trips), A/B variant 23
 // TB: threads per workgroup.  The cost partial is per wave (no workgroup
 // barrier), cost_partial[i / 64].
@@ -1740,10 +1744,10 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
     dispatch_ct(p.ct, [&](auto c) {
       constexpr int CT = decltype(c)::value;
       if (p.loss_type == kLossTrivial)
-        hipLaunchKernelGGL((reproj_jacobian_kernel<kMixedModels, 0, 0, 2, kJacProduction, 4, kBlock, CT>), dim3(g),
+        hipLaunchKernelGGL((reproj_jacobian_kernel<kMixedModels, 0, 0, kJacPasses, kJacProduction, 4, kBlock, CT>), dim3(g),
                            dim3(kBlock), 0, s, p, r, J, cost_partial);
       else
-        hipLaunchKernelGGL((reproj_jacobian_kernel<kMixedModels, 0, 1, 2, kJacProduction, 4, kBlock, CT>), dim3(g),
+        hipLaunchKernelGGL((reproj_jacobian_kernel<kMixedModels, 0, 1, kJacPasses, kJacProduction, 4, kBlock, CT>), dim3(g),
                            dim3(kBlock), 0, s, p, r, J, cost_partial);
     });
     return;
@@ -1759,6 +1763,10 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
           switch (p.jvariant) {
             case 1:
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 1, kJacProduction>), dim3(g), dim3(kBlock), 0, s, p, r, J,
+                                 cost_partial);
+              return;
+            case 2:  // two slab passes (production before the closed-form rotation columns)
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction>), dim3(g), dim3(kBlock), 0, s, p, r, J,
                                  cost_partial);
               return;
             case 4:
@@ -1850,8 +1858,8 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
               break;
           }
         }
-        hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, LOSS, 2, kJacProduction>), dim3(g), dim3(kBlock), 0, s, p,
-                           r, J, cost_partial);
+        hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, LOSS, kJacPasses, kJacProduction>), dim3(g), dim3(kBlock), 0,
+                           s, p, r, J, cost_partial);
       };
       if (p.loss_type == kLossTrivial)
         launch(std::integral_constant<int, 0>{});

@@ -1400,7 +1400,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.lookahead = value != 0;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_own_diag") == 0 && value >= 0 && value <= 6) {
+  if (std::strcmp(key, "cholesky_own_diag") == 0 && value >= 0 && value <= 7) {
     ctx->chol.own_diag = value;
     return MI_BA_OK;
   }
