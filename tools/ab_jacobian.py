@@ -20,12 +20,18 @@ ap.add_argument("--config", default="C4")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--variants", default="0")
+ap.add_argument("--step", action="store_true",
+                help="time the kernel inside the full C4 linearization step (after the semantic pass, as bench.py)")
 args = ap.parse_args()
 cfg = dict(bench.CONFIGS[args.config])
 c = mi_ba.synth_config(cfg["model"], cfg["images"], cfg["points"], track_length=cfg["track"], rotation_range=0.05,
                        extra=cfg["extra"])
-sc = mi_ba.generate_scene(c).gauge()
-ctx = mi_ba.Context(mi_ba.default_options(), sc)
+if args.step:
+    sc, sem = bench.build_shard(cfg, 0, 1)
+    ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
+else:
+    sc = mi_ba.generate_scene(c).gauge()
+    ctx = mi_ba.Context(mi_ba.default_options(), sc)
 nb, W, _ = ctx.dims()
 bpb = bench.bytes_per_block(cfg["model"], cfg["track"])
 variants = [int(v) for v in args.variants.split(",")]
@@ -49,7 +55,7 @@ for rnd in range(args.rounds):
         ctx.set_timing(True)
         ctx.reset_kernel_times()
         for _ in range(args.reps):
-            ctx.evaluate_jacobian()
+            ctx.linearize() if args.step else ctx.evaluate_jacobian()
         ms, n = ctx.kernel_time("reproj_jacobian")
         ctx.set_timing(False)
         res[v].append(ms / n)

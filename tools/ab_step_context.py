@@ -36,6 +36,23 @@ with mi_ba.Context(mi_ba.default_options(), sc.copy(), sem) as ctx:
         j, s = timed(ctx, ctx.linearize)
         print(json.dumps({"context": "semantic ctx", "mode": "linearize x10", "reproj_ms": j, "semantic_ms": s}),
               flush=True)
+    # the step with an idle gap after the semantic pass (clocks / power vs cache / TLB state)
+    import time
+
+    def lin_gap():
+        ctx.linearize()
+        ctx.synchronize()
+        time.sleep(0.002)
+    j, s = timed(ctx, lin_gap)
+    print(json.dumps({"context": "semantic ctx", "mode": "linearize + sync + 2 ms idle x10", "reproj_ms": j,
+                      "semantic_ms": s}), flush=True)
+
+    def sem_then_jac():
+        ctx.evaluate_semantic()
+        ctx.evaluate_jacobian()
+    j, s = timed(ctx, sem_then_jac)
+    print(json.dumps({"context": "semantic ctx", "mode": "evaluate_semantic(write) + evaluate_jacobian x10",
+                      "reproj_ms": j, "semantic_ms": s}), flush=True)
 with mi_ba.Context(mi_ba.default_options(), sc.copy()) as ctx:
     for rnd in range(2):
         j, _ = timed(ctx, ctx.linearize)
