@@ -400,8 +400,8 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *                           batched stencil with 4 / 2 / 1 parameters per step;
  *                           1 per-point FMA route; 0 per-point uncontracted
  *                           (all bitwise equal)
- *   "semantic_diag"         1: downloaded status carries 0x100 for samples the
- *                           flat test deferred (variants 5, 6; diagnostic)
+ *   "semantic_diag"         1: downloaded status is offset by +0x1000 for samples
+ *                           the flat test deferred (variants 5, 6; diagnostic)
  *   "linearize_overlap"     1 semantic kernel on a second stream beside the reprojection
  *                           kernel, 0 one stream (default)
  *   "cholesky_lookahead"    1 side-stream look-ahead (default) / 0 serial

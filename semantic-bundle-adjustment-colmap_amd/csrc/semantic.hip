@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
   if (active) {
     if (write_samples) {
       r_out[n] = r;
-      status_out[n] = st | ((write_samples & 2) && deferred ? 0x100 : 0);  // 2: mark deferred samples (diagnostic)
+      status_out[n] = st + ((write_samples & 2) && deferred ? 0x1000 : 0);  // 2: mark deferred samples (diagnostic)
       double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
 #pragma unroll
       for (int m = 0; m < 6; ++m) jo[m] = make_double2(Jt[2 * m], Jt[2 * m + 1]);
@@ -1208,7 +1208,7 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
     cost = 0.5 * (a.weight * rho[0]);
     if (write_samples) {
       r_out[n] = c.r;
-      status_out[n] = c.st | ((write_samples & 2) && deferred ? 0x100 : 0);
+      status_out[n] = c.st + ((write_samples & 2) && deferred ? 0x1000 : 0);
       if (!deferred) {
         double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
 #pragma unroll

@@ -33,7 +33,7 @@ with mi_ba.Context(mi_ba.default_options(), sc.copy(), sem) as ctx:
     for rnd in range(2):
         print(json.dumps({"context": "semantic ctx", "mode": "evaluate_jacobian x10",
                           "reproj_ms": timed(ctx, ctx.evaluate_jacobian)[0]}), flush=True)
-        for v in (6, 7):
+        for v in (6,):
             ctx.set_tuning("semantic_variant", v)
             j, s = timed(ctx, ctx.linearize)
             print(json.dumps({"context": "semantic ctx", "mode": "linearize x10", "semantic_variant": v,
