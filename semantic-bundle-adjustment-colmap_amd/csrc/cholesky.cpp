@@ -474,9 +474,10 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
       }
     }
     for (int spin = 0; spin < (1 << 24); ++spin) {  // bounded, as pf_wait
-      if (__hip_atomic_load(flag + jb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
+      if (__hip_atomic_load(flag + jb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
       __builtin_amdgcn_s_sleep(1);
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // once, after the flag (see pf_wait)
     xs[wv][lane] = lane < wj ? x[c0 + lane] : 0.0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -543,11 +544,16 @@ __device__ __forceinline__ int pf_rows(int r, int kb, int nc, int mrows) {
 
 __device__ __forceinline__ void pf_wait(const unsigned* f, unsigned epoch) {
   // bounded (~seconds): a lost flag ends the launch with a wrong factor
-  // instead of a wave that never finishes
+  // instead of a wave that never finishes.  The poll is a relaxed (coherent,
+  // sc1) load and the acquire fence runs once after the flag is seen: an
+  // acquire load in the loop would issue an agent-scope cache invalidate
+  // (buffer_inv sc1) per poll, from every waiting workgroup, flushing the
+  // XCD's cached tiles under the concurrent trailing dgemm.
   for (int spin = 0; spin < (1 << 24); ++spin) {
-    if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch) return;
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
     __builtin_amdgcn_s_sleep(1);
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 // acc (wave w: rows 16w..16w+15 of the 64x64 tile, column tiles t = 0..3,
