@@ -442,10 +442,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   #pragma unroll
         for (int k = 0; k < 6; ++k) B[k] *= sc;
       }
-      if (pose_var && (D & 512)) {
-        // d(R X)/d(tangent) of QuaternionManifold (plus = q_delta * q, rotation
-        // angle 2|delta|) = -2 [R X]x, the product Dq * PlusJacobian below in
-        // closed form (equal up to rounding for a unit q)
+      // d(R X)/d(tangent) of QuaternionManifold (plus = q_delta * q, rotation
+      // angle 2|delta|) = -2 [R X]x: the product Dq * PlusJacobian below in
+      // closed form, equal up to rounding for a unit q (the general product
+      // serves a quaternion that is not normalised, as AutoDiff would)
+      const bool unit_q =
+          (D & 512) && ((D & 4096) || fabs(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3] - 1.0) <= 1e-12);
+      if (pose_var && unit_q) {
         Mq[0] = 0.0;       Mq[1] = 2.0 * a2;  Mq[2] = -2.0 * a1;
         Mq[3] = -2.0 * a2; Mq[4] = 0.0;       Mq[5] = 2.0 * a0;
         Mq[6] = 2.0 * a1;  Mq[7] = -2.0 * a0; Mq[8] = 0.0;
@@ -1833,6 +1836,10 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
             case 36:  // closed-form rotation columns
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 512>), dim3(g), dim3(kBlock), 0, s,
                                  p, r, J, cost_partial);
+              return;
+            case 42:  // A/B: closed form without the unit-quaternion check
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 1, kJacProduction | 4096>), dim3(g), dim3(kBlock), 0,
+                                 s, p, r, J, cost_partial);
               return;
             case 37:  // closed-form rotation columns, R X through the rotation matrix
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 512 | 1024>), dim3(g), dim3(kBlock),

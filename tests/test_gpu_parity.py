@@ -59,6 +59,17 @@ def test_reproj_jacobian_parity_models(gpu, model):
     compare_jacobians(mi_ba.default_options(refine_principal_point=1), sc)
 
 
+@pytest.mark.parametrize("model", [mi_ba.SIMPLE_RADIAL, mi_ba.OPENCV])
+def test_reproj_jacobian_non_unit_quaternions(gpu, model):
+    """Poses whose quaternion is not normalised (|q| = 0.98 .. 1.03): the
+    rotation columns take the general Dq * PlusJacobian product there (the
+    closed form -2[RX]x holds for unit quaternions only), as AutoDiff does."""
+    sc = scene(model, images=6, points=300, track=4, seed=4)
+    scale = np.array([1.0, 1.0, 1.03, 0.98, 1.0 + 1e-9, 1.01])
+    sc.qvec = sc.qvec * scale[:, None]
+    compare_jacobians(mi_ba.default_options(), sc)
+
+
 def test_reproj_jacobian_parity_flags(gpu):
     rng = np.random.default_rng(3)
     for trial in range(6):
