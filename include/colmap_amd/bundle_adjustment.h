@@ -22,9 +22,11 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <functional>
 #include <limits>
 #include <map>
 #include <stdexcept>
@@ -121,9 +123,15 @@ class Reconstruction {
     images.at(te.image_id).points2D.at(te.point2D_idx).point3D_id = point3D_id;
     points3D.at(point3D_id).track.push_back(te);
   }
+  // Reconstruction::DeleteObservation (reconstruction.cc:257-277): a track
+  // of length <= 2 takes its point with it.
   void DeleteObservation(image_t image_id, point2D_t point2D_idx) {
     Point2D& p2 = images.at(image_id).points2D.at(point2D_idx);
     auto& tr = points3D.at(p2.point3D_id).track;
+    if (tr.size() <= 2) {
+      DeletePoint3D(p2.point3D_id);
+      return;
+    }
     tr.erase(std::remove_if(tr.begin(), tr.end(),
                             [&](const TrackElement& t) { return t.image_id == image_id && t.point2D_idx == point2D_idx; }),
              tr.end());
@@ -144,6 +152,13 @@ class Reconstruction {
                                                   const std::unordered_set<point3D_t>& point3D_ids,
                                                   int device = 0);
 
+  // Reconstruction::FilterObservationsWithNegativeDepth (reconstruction.cc:
+  // 647-665): the depth test of every observation of the registered images
+  // on the GPU (mi_ba_positive_depth), then the reference's deletions in
+  // image / point2D order (registered images in image-id order).  Returns the
+  // number of observations deleted.
+  size_t FilterObservationsWithNegativeDepth(int device = 0);
+
  private:
   point3D_t num_added_points3D_ = 0;
 };
@@ -151,6 +166,21 @@ class Reconstruction {
 // ---------------------------------------------------------------------------
 // Options / config (bundle_adjustment.h:49-167)
 // ---------------------------------------------------------------------------
+// ceres::CallbackReturnType / IterationSummary / IterationCallback
+// (the solver_options.callbacks interface COLMAP's controllers use,
+// controllers/bundle_adjustment.cc:43-61,87-88).
+enum CallbackReturnType {
+  SOLVER_CONTINUE = MI_BA_SOLVER_CONTINUE,
+  SOLVER_ABORT = MI_BA_SOLVER_ABORT,
+  SOLVER_TERMINATE_SUCCESSFULLY = MI_BA_SOLVER_TERMINATE_SUCCESSFULLY
+};
+typedef mi_ba_iteration_summary IterationSummary;
+class IterationCallback {
+ public:
+  virtual ~IterationCallback() {}
+  virtual CallbackReturnType operator()(const IterationSummary& summary) = 0;
+};
+
 struct SolverOptions {  // ceres::Solver::Options subset set by COLMAP
   double function_tolerance = 0.0;
   double gradient_tolerance = 0.0;
@@ -161,6 +191,11 @@ struct SolverOptions {  // ceres::Solver::Options subset set by COLMAP
   int max_num_consecutive_invalid_steps = 10;
   int max_consecutive_nonmonotonic_steps = 10;
   int num_threads = -1;
+  // run in order after every iteration; the first one that does not return
+  // SOLVER_CONTINUE decides (Ceres RunCallbacks).  Not owned.
+  std::vector<IterationCallback*> callbacks;
+  // the Reconstruction holds the current point whenever a callback runs
+  bool update_state_every_iteration = false;
 };
 
 struct BundleAdjustmentOptions {
@@ -175,6 +210,10 @@ struct BundleAdjustmentOptions {
   int min_num_residuals_for_multi_threading = 50000;  // kept for API parity
   SolverOptions solver_options;
   int device = 0;  // build addition: HIP device ordinal
+  // build addition: a flag another thread may set to MI_BA_SOLVER_TERMINATE_
+  // SUCCESSFULLY / MI_BA_SOLVER_ABORT to stop the solve at the next
+  // iteration boundary (Thread::Stop without a callback); not owned
+  const std::atomic<int32_t>* stop_flag = nullptr;
 
   bool Check() const {
     if (loss_function_scale < 0) throw std::invalid_argument("loss_function_scale must be >= 0");
@@ -405,6 +444,39 @@ inline mi_ba_options ToOptions(const BundleAdjustmentOptions& o) {
   return m;
 }
 
+static_assert(sizeof(std::atomic<int32_t>) == sizeof(int32_t) && alignof(std::atomic<int32_t>) == alignof(int32_t),
+              "the stop flag is read as an int32_t");
+
+// solver_options.callbacks through the C-ABI's single callback: the bridge
+// runs the caller's callbacks in order; `sync` (set when
+// update_state_every_iteration) copies the point the library has just
+// written into the flattened arrays back into the caller's objects first.
+struct CallbackBridge {
+  const std::vector<IterationCallback*>* callbacks = nullptr;
+  std::function<void()> sync;
+  static int32_t Call(void* user, const mi_ba_iteration_summary* summary) {
+    CallbackBridge* b = static_cast<CallbackBridge*>(user);
+    if (b->sync) b->sync();
+    for (IterationCallback* cb : *b->callbacks) {
+      const CallbackReturnType r = (*cb)(*summary);
+      if (r != SOLVER_CONTINUE) return r;
+    }
+    return SOLVER_CONTINUE;
+  }
+};
+
+// Installs the options' callbacks / stop flag into o (bridge must outlive the solve).
+inline void InstallCallbacks(const BundleAdjustmentOptions& options, CallbackBridge* bridge,
+                             std::function<void()> sync, mi_ba_options* o) {
+  o->stop_flag = reinterpret_cast<const int32_t*>(options.stop_flag);
+  o->update_state_every_iteration = options.solver_options.update_state_every_iteration ? 1 : 0;
+  if (options.solver_options.callbacks.empty()) return;
+  bridge->callbacks = &options.solver_options.callbacks;
+  if (o->update_state_every_iteration) bridge->sync = std::move(sync);
+  o->iteration_callback = &CallbackBridge::Call;
+  o->callback_user = bridge;
+}
+
 inline SolverSummary ToSummary(const mi_ba_summary& s) {
   SolverSummary o;
   o.num_residuals_reduced = s.num_residuals_reduced;
@@ -493,6 +565,71 @@ inline size_t Reconstruction::FilterPoints3DWithLargeReprojectionError(
   return (size_t)num_filtered;
 }
 
+inline size_t Reconstruction::FilterObservationsWithNegativeDepth(int device) {
+  std::unordered_map<camera_t, int32_t> cidx;
+  std::vector<double> params, qv, tv, xyz, obs_xy;
+  std::vector<int32_t> models, image_camera, obs_image, obs_point;
+  std::vector<uint8_t> reg;
+  std::vector<std::pair<image_t, point2D_t>> obs_ref;
+  std::unordered_map<point3D_t, int32_t> pidx;
+  for (const auto& c : cameras) {
+    cidx[c.first] = (int32_t)models.size();
+    models.push_back(c.second.model_id);
+    params.insert(params.end(), c.second.params.begin(), c.second.params.end());
+  }
+  for (const auto& p : points3D) {
+    pidx[p.first] = (int32_t)(xyz.size() / 3);
+    xyz.insert(xyz.end(), p.second.xyz, p.second.xyz + 3);
+  }
+  for (const auto& im : images) {
+    const int32_t i = (int32_t)image_camera.size();
+    qv.insert(qv.end(), im.second.qvec, im.second.qvec + 4);
+    tv.insert(tv.end(), im.second.tvec, im.second.tvec + 3);
+    image_camera.push_back(cidx.at(im.second.camera_id));
+    reg.push_back(im.second.IsRegistered() ? 1 : 0);
+    if (!im.second.IsRegistered()) continue;
+    for (point2D_t k = 0; k < (point2D_t)im.second.points2D.size(); ++k) {
+      const Point2D& p2 = im.second.points2D[k];
+      if (!p2.HasPoint3D()) continue;
+      obs_xy.push_back(p2.xy[0]);
+      obs_xy.push_back(p2.xy[1]);
+      obs_image.push_back(i);
+      obs_point.push_back(pidx.at(p2.point3D_id));
+      obs_ref.emplace_back(im.first, k);
+    }
+  }
+  if (obs_ref.empty()) return 0;
+  mi_ba_problem pr{};
+  pr.camera_model = models.empty() ? MI_BA_SIMPLE_RADIAL : models[0];
+  pr.camera_model_ids = models.data();
+  pr.num_cameras = (int32_t)models.size();
+  pr.camera_params = params.data();
+  pr.num_images = (int32_t)image_camera.size();
+  pr.qvec = qv.data();
+  pr.tvec = tv.data();
+  pr.image_camera = image_camera.data();
+  pr.num_points = (int64_t)(xyz.size() / 3);
+  pr.xyz = xyz.data();
+  pr.num_obs = (int64_t)obs_image.size();
+  pr.obs_xy = obs_xy.data();
+  pr.obs_image = obs_image.data();
+  pr.obs_point = obs_point.data();
+  std::vector<uint8_t> keep(obs_ref.size());
+  int64_t negative = 0;
+  internal::ThrowStatus(mi_ba_positive_depth(&pr, reg.data(), device, keep.data(), &negative),
+                        "FilterObservationsWithNegativeDepth");
+  // the reference's deletions, in order: an observation whose point an
+  // earlier deletion already removed is no longer counted (HasPoint3D)
+  size_t num_filtered = 0;
+  for (size_t k = 0; k < obs_ref.size(); ++k) {
+    if (keep[k]) continue;
+    if (!images.at(obs_ref[k].first).points2D.at(obs_ref[k].second).HasPoint3D()) continue;
+    DeleteObservation(obs_ref[k].first, obs_ref[k].second);
+    ++num_filtered;
+  }
+  return num_filtered;
+}
+
 // Device resources reused by consecutive solves of one host thread (the
 // mapper's repeated local BAs): pass the same arena to every Solve.
 class SolverArena {
@@ -524,7 +661,9 @@ class BundleAdjuster {
     used_ = true;
     internal::Flat flat;
     flat.Build(*reconstruction, config_);
-    const mi_ba_options o = internal::ToOptions(options_);
+    mi_ba_options o = internal::ToOptions(options_);
+    internal::CallbackBridge bridge;
+    internal::InstallCallbacks(options_, &bridge, [&] { flat.WriteBack(reconstruction); }, &o);
     mi_ba_summary s;
     const mi_ba_status st = arena ? mi_ba_solve_in(arena->get(), &o, &flat.problem, nullptr, &s)
                                   : mi_ba_solve(&o, &flat.problem, nullptr, &s);
@@ -633,6 +772,8 @@ class SemanticBundleAdjuster {
     sem.numeric_relative_step_size = options_.numeric_relative_step_size;
     mi_ba_options o = internal::ToOptions(options_);
     o.semantic_weight = options_.semantic_weight;
+    internal::CallbackBridge bridge;
+    internal::InstallCallbacks(options_, &bridge, [&] { flat.WriteBack(reconstruction); }, &o);
     mi_ba_summary s;
     const mi_ba_status st = mi_ba_solve(&o, &flat.problem, &sem, &s);
     if (st == MI_BA_ERR_NO_RESIDUALS) return false;
@@ -782,6 +923,8 @@ inline void PrintSolverSummary(const SolverSummary& s) {
   const char* term = s.termination_type == SolverSummary::CONVERGENCE      ? "Convergence"
                      : s.termination_type == SolverSummary::NO_CONVERGENCE ? "No convergence"
                      : s.termination_type == SolverSummary::FAILURE        ? "Failure"
+                     : s.termination_type == SolverSummary::USER_SUCCESS   ? "User success"
+                     : s.termination_type == SolverSummary::USER_FAILURE   ? "User failure"
                                                                            : "Unknown";
   std::printf("    Residuals : %lld\n   Parameters : %lld\n   Iterations : %d\n         Time : %g [s]\n"
               " Initial cost : %g [px]\n   Final cost : %g [px]\n  Termination : %s\n\n",

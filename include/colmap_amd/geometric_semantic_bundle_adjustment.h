@@ -151,20 +151,19 @@ class GeometricSemanticBundleAdjuster {
     g.numeric_relative_step_size = options_.numeric_relative_step_size;
     g.include_landmark_error = options_.include_landmark_error;
     g.landmark_error_weight = options_.landmark_error_weight;
-    const mi_ba_options o = internal::ToOptions(options_);
+    mi_ba_options o = internal::ToOptions(options_);
+    internal::CallbackBridge bridge;
+    internal::InstallCallbacks(options_, &bridge, [&] {
+      flat.WriteBack(reconstruction);
+      CopyCylinders(cyl, cylinders);
+    }, &o);
     mi_ba_summary s;
     const mi_ba_status st = mi_ba_gsba_solve(&o, &flat.problem, &g, &s);
     if (st == MI_BA_ERR_NO_RESIDUALS) return false;
     internal::ThrowStatus(st, "GeometricSemanticBundleAdjuster::Solve");
     summary_ = internal::ToSummary(s);
     flat.WriteBack(reconstruction);
-    for (size_t c = 0; c < cyl.size(); ++c) {
-      Cylinder& y = (*cylinders)[c];
-      std::copy(cyl[c].qvec, cyl[c].qvec + 4, y.qvec);
-      std::copy(cyl[c].tvec, cyl[c].tvec + 3, y.tvec);
-      y.radius = cyl[c].radius;
-      y.height = cyl[c].height;
-    }
+    CopyCylinders(cyl, cylinders);
     return true;
   }
 
@@ -172,6 +171,16 @@ class GeometricSemanticBundleAdjuster {
   const std::vector<Cylinder>& Cylinders() const { return cylinders_; }
 
  private:
+  static void CopyCylinders(const std::vector<mi_ba_cylinder>& cyl, std::vector<Cylinder>* cylinders) {
+    for (size_t c = 0; c < cyl.size(); ++c) {
+      Cylinder& y = (*cylinders)[c];
+      std::copy(cyl[c].qvec, cyl[c].qvec + 4, y.qvec);
+      std::copy(cyl[c].tvec, cyl[c].tvec + 3, y.tvec);
+      y.radius = cyl[c].radius;
+      y.height = cyl[c].height;
+    }
+  }
+
   GeometricSemanticBundleAdjustmentOptions options_;
   BundleAdjustmentConfig config_;
   SolverSummary summary_;

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define MI_BA_ABI_VERSION 2
+#define MI_BA_ABI_VERSION 3
 
 typedef enum mi_ba_status {
   MI_BA_OK = 0,
@@ -93,6 +93,44 @@ enum {
   MI_BA_USER_FAILURE = 4
 };
 
+/* ceres::CallbackReturnType, same numeric order as Ceres 2.1: what an
+ * iteration callback (or the stop flag) asks of the solver. */
+enum {
+  MI_BA_SOLVER_CONTINUE = 0,
+  MI_BA_SOLVER_ABORT = 1,                  /* -> termination_type MI_BA_USER_FAILURE; the
+                                              problem arrays are not updated (Ceres) */
+  MI_BA_SOLVER_TERMINATE_SUCCESSFULLY = 2  /* -> termination_type MI_BA_USER_SUCCESS */
+};
+
+/* ceres::IterationSummary fields, handed to the iteration callback at the end
+ * of every LM iteration (TrustRegionMinimizer::
+ * FinalizeIterationAndCheckIfMinimizerCanContinue): iteration 0 is the
+ * initial state (after the first residual + Jacobian evaluation), then one
+ * per iteration, successful, unsuccessful or invalid.  Iterations that end
+ * the solve on a tolerance or on too many invalid steps run no callback
+ * (Ceres returns from those before the callbacks). */
+typedef struct mi_ba_iteration_summary {
+  int32_t iteration;
+  int32_t step_is_valid;
+  int32_t step_is_successful;
+  int32_t linear_solver_iterations;
+  double cost;                        /* at the current (accepted) point, fixed cost included */
+  double cost_change;                 /* decrease of this iteration's step (0 when not successful) */
+  double relative_decrease;
+  double trust_region_radius;         /* after this iteration's update */
+  double step_norm;
+  double iteration_time_in_seconds;
+  double cumulative_time_in_seconds;
+} mi_ba_iteration_summary;
+
+/* ceres::IterationCallback::operator(): returns MI_BA_SOLVER_*.  Runs on the
+ * thread that called the solve.  With options.update_state_every_iteration
+ * the problem's parameter arrays (qvec, tvec, xyz, camera_params, cylinders)
+ * hold the current point when it runs (Ceres' update_state_every_iteration,
+ * which the reference's SBA / GSBA snapshot callbacks rely on,
+ * semantic_bundle_adjustment.h:129, semantic_bundle_adjustment.cc:1086-1123). */
+typedef int32_t (*mi_ba_iteration_callback_fn)(void* user, const mi_ba_iteration_summary* summary);
+
 /* Semantic sample status (ReprojectionStatus, semantic_cost_functions.h:45). */
 enum { MI_BA_OUT_OF_BOUNDS = -1, MI_BA_INVALID_DEPTH = -2, MI_BA_VALID = 10 };
 
@@ -118,6 +156,19 @@ typedef struct mi_ba_options {
   /* build additions */
   int32_t device;                   /* HIP device ordinal, default 0 */
   double semantic_weight;           /* ScaledLoss weight of semantic blocks, default 1 */
+  /* solver_options.callbacks / update_state_every_iteration (ABI 3): the
+   * reference's controllers install an IterationCallback that blocks while
+   * the thread is paused and returns SOLVER_TERMINATE_SUCCESSFULLY once it is
+   * stopped (controllers/bundle_adjustment.cc:43-61,87-88). */
+  mi_ba_iteration_callback_fn iteration_callback; /* nullable, default NULL */
+  void* callback_user;
+  int32_t update_state_every_iteration;           /* default 0 */
+  /* Stop flag, nullable: read (atomically, relaxed) where the callback runs;
+   * a nonzero value is taken as that callback return (MI_BA_SOLVER_*), so
+   * another thread stops the solve at the next iteration boundary by
+   * storing MI_BA_SOLVER_TERMINATE_SUCCESSFULLY (Thread::Stop) or
+   * MI_BA_SOLVER_ABORT. */
+  const int32_t* stop_flag;
 } mi_ba_options;
 
 /* Flattened Reconstruction + BundleAdjustmentConfig.  Indices are 0-based
@@ -243,7 +294,12 @@ mi_ba_status mi_ba_setup_stats(const mi_ba_options* options,
                                const mi_ba_problem* problem,
                                mi_ba_setup_info* info);
 
-/* --- one-shot solve: BundleAdjuster::Solve ------------------------------ */
+/* --- one-shot solve: BundleAdjuster::Solve ------------------------------
+ * The refined parameters are written into the problem arrays unless the
+ * solve ends in MI_BA_FAILURE or MI_BA_USER_FAILURE, where Ceres leaves the
+ * user's parameter blocks untouched (Solver::Solve copies the state back only
+ * for a usable solution); with update_state_every_iteration they then hold
+ * the point of the last callback. */
 mi_ba_status mi_ba_solve(const mi_ba_options* options, mi_ba_problem* problem,
                          const mi_ba_semantic* semantic /* nullable */,
                          mi_ba_summary* summary);
@@ -309,6 +365,24 @@ mi_ba_status mi_ba_filter_points3d(const mi_ba_problem* problem, double max_repr
                                    const uint8_t* point_mask /* nullable */, int32_t device,
                                    uint8_t* obs_keep, uint8_t* point_keep, double* point_error,
                                    int64_t* num_filtered);
+
+/* mi_ba_positive_depth: the test of Reconstruction::
+ * FilterObservationsWithNegativeDepth (src/base/reconstruction.cc:647-665),
+ * the pre-step every BA controller runs before Solve
+ * (controllers/bundle_adjustment.cc:82, semantic_bundle_adjustment.cc:86,
+ * geometric_semantic_bundle_adjustment.cc:89): obs_keep[k] = 1 when
+ * HasPointPositiveDepth(ProjectionMatrix of the observation's image, its
+ * point) (projection.cc:191-195: third row of [R(normalised qvec) | t] dotted
+ * with (X, 1) >= DBL_EPSILON), 0 otherwise; observations of images with
+ * image_mask[i] == 0 (NULL = every image; the reference visits the registered
+ * images) are kept.  *num_negative = observations with obs_keep 0.  The
+ * reference then deletes those observations one by one in image / point2D
+ * order, a track of length <= 2 taking its point with it
+ * (Reconstruction::DeleteObservation, reconstruction.cc:257-277); the facade
+ * (colmap_amd::Reconstruction::FilterObservationsWithNegativeDepth) applies
+ * the mask that way. */
+mi_ba_status mi_ba_positive_depth(const mi_ba_problem* problem, const uint8_t* image_mask /* nullable */,
+                                  int32_t device, uint8_t* obs_keep, int64_t* num_negative);
 
 /* --- resident context (device-resident problem, for throughput/parity) - */
 mi_ba_status mi_ba_context_create(const mi_ba_options* options,
@@ -407,7 +481,12 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *   "cholesky_lookahead"    1 side-stream look-ahead (default) / 0 serial
  *   "cholesky_solve"        2 sync-free triangular sweeps, one launch per direction
  *                           (default) / 1 hand-written blocked triangular sweeps /
- *                           0 recursive rocBLAS dtrsv + dgemv */
+ *                           0 recursive rocBLAS dtrsv + dgemv
+ *   "cholesky_spin_log2"    bound of the in-launch flag waits, 2^value polls (default
+ *                           24; 0: no polling, so a wait on a flag not already set runs
+ *                           out at once — the hook of the timeout test).  A wait that
+ *                           runs out makes the solve return MI_BA_ERR_HIP (never a
+ *                           silently wrong factor) */
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value);
 
 /* Dense Cholesky of a symmetric positive-definite n x n matrix with the

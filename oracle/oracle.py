@@ -67,8 +67,37 @@ def load():
     lib.oracle_gsba_iou.argtypes = [_dp, _dp, _dp, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
     lib.oracle_cholesky.restype = C.c_int
     lib.oracle_cholesky.argtypes = [_dp, C.c_int]
+    lib.oracle_set_dense_factor.argtypes = [DENSE_FACTOR_FN]
+    lib.oracle_set_dense_factor.restype = None
     _lib = lib
     return lib
+
+
+# int (*)(double* A, int n): row-major lower factor in place, 0 or failing column
+DENSE_FACTOR_FN = C.CFUNCTYPE(C.c_int, _dp, C.c_int)
+
+
+def _lapack_factor(ptr, n):
+    """LAPACK dpotrf on the oracle's row-major lower triangle: the same bytes
+    read column-major are the upper triangle, and dpotrf(lower=0) leaves U
+    with U'U = A there, i.e. L = U' row-major."""
+    from scipy.linalg import lapack
+    A = np.ctypeslib.as_array(ptr, shape=(n, n))
+    F = A.T  # column-major view, no copy
+    c, info = lapack.dpotrf(F, lower=0, clean=0, overwrite_a=1)
+    if not np.shares_memory(c, A):
+        F[...] = c
+    return int(info)
+
+
+_lapack_thunk = DENSE_FACTOR_FN(_lapack_factor)
+
+
+def use_lapack_factor(enable: bool = True):
+    """Route the oracle LM's reduced-camera-system factorisation through
+    LAPACK dpotrf (multi-threaded; for C4-sized systems, nf ~ 12 000) instead
+    of the oracle's own blocked Cholesky.  Test infrastructure only."""
+    load().oracle_set_dense_factor(_lapack_thunk if enable else DENSE_FACTOR_FN())
 
 
 def _a(x):

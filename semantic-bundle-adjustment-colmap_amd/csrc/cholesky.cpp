@@ -404,6 +404,29 @@ __global__ __launch_bounds__(kTB) void trsv_bwd_step_kernel(const double* __rest
 //   forward  L y = b: lane = row of the block, dependency blocks L[ib][jb < ib]
 //   backward L'x = y: lane = column of the block, dependency blocks L[jb > ib][ib]
 // ctrl = {forward ticket, backward ticket, flag[nblk]}.
+// Bounded in-launch flag wait (sync-free sweeps, one-launch panel factor).
+// The poll is a relaxed (coherent, sc1) load and the acquire fence runs once
+// after the flag is seen: an acquire load in the loop would issue an
+// agent-scope cache invalidate (buffer_inv sc1) per poll, from every waiting
+// workgroup, flushing the XCD's cached tiles under the concurrent trailing
+// dgemm.  Bounded by `limit` polls: a lost flag must not leave waves that
+// never finish.  A wait that runs out — or that sees (every 256 polls) that
+// another wait of the call already ran out, so a broken chain drains fast —
+// sets kCholErrWait in the error word and returns; the host reads the word
+// (chol_error) and reports the factor / solution invalid instead of using it.
+__device__ __forceinline__ void flag_wait(const unsigned* f, unsigned epoch, unsigned* err, unsigned limit) {
+  for (unsigned spin = 0;; ++spin) {
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
+    if (spin >= limit ||
+        ((spin & 255u) == 255u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+      __hip_atomic_fetch_or(err, kCholErrWait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 constexpr int kSweepWaves = 4;
 typedef double sweep_dvec2 __attribute__((ext_vector_type(2)));
 
@@ -416,7 +439,8 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 
 template <bool FWD>
 __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const double* __restrict__ L, int lda, int n,
-                                                                      double* x, unsigned* ctrl, unsigned epoch) {
+                                                                      double* x, unsigned* ctrl, unsigned epoch,
+                                                                      unsigned* err, unsigned limit) {
   __shared__ int s_blk;
   __shared__ double part[kSweepWaves][kTB];
   __shared__ double xs[kSweepWaves][kTB];
@@ -473,11 +497,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
         for (int r = 0; r < kTB; ++r) v[r] = src[min(r, wj - 1)];
       }
     }
-    for (int spin = 0; spin < (1 << 24); ++spin) {  // bounded, as pf_wait
-      if (__hip_atomic_load(flag + jb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // once, after the flag (see pf_wait)
+    flag_wait(flag + jb, epoch, err, limit);
     xs[wv][lane] = lane < wj ? x[c0 + lane] : 0.0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -542,18 +562,8 @@ __device__ __forceinline__ int pf_rows(int r, int kb, int nc, int mrows) {
   return r < nc ? min(64, kb - 64 * r) : min(64, mrows - kb - 64 * (r - nc));
 }
 
-__device__ __forceinline__ void pf_wait(const unsigned* f, unsigned epoch) {
-  // bounded (~seconds): a lost flag ends the launch with a wrong factor
-  // instead of a wave that never finishes.  The poll is a relaxed (coherent,
-  // sc1) load and the acquire fence runs once after the flag is seen: an
-  // acquire load in the loop would issue an agent-scope cache invalidate
-  // (buffer_inv sc1) per poll, from every waiting workgroup, flushing the
-  // XCD's cached tiles under the concurrent trailing dgemm.
-  for (int spin = 0; spin < (1 << 24); ++spin) {
-    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+__device__ __forceinline__ void pf_wait(const unsigned* f, unsigned epoch, unsigned* err, unsigned limit) {
+  flag_wait(f, epoch, err, limit);
 }
 
 // acc (wave w: rows 16w..16w+15 of the 64x64 tile, column tiles t = 0..3,
@@ -823,7 +833,8 @@ constexpr int kPfDbgSlots = 20;
 __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ A, int lda, int kb, int mrows,
                                                            int* __restrict__ info, double* __restrict__ linv,
                                                            unsigned* ctrl, unsigned base, unsigned epoch,
-                                                           int nbw, unsigned long long* dbg = nullptr) {
+                                                           int nbw, unsigned* err, unsigned limit,
+                                                           unsigned long long* dbg = nullptr) {
   __shared__ double T[64 * kPfLd];   // staging / factor tile (row-major padded)
   __shared__ double Li[64 * kPfLd];  // a diagonal tile's inverse (own, or workgroup c's)
   __shared__ double Lc[64 * 64];     // the factor's columns (pf_chol_inv_wave)
@@ -895,7 +906,7 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
           }
       }
       for (int k = 0; k < c; ++k) {
-        pf_wait(flag + c * kPfMaxTiles + k, epoch);
+        pf_wait(flag + c * kPfMaxTiles + k, epoch, err, limit);
         // L_ck (rows of column tile c, columns of tile k) staged once
         for (int e = threadIdx.x; e < 64 * 64; e += 256) {
           const int i = e & 63, kk = e >> 6;
@@ -909,7 +920,7 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
             pf_gemm_nt(acc[j], -1.0, gtile(pf_row0(rr[j], kb, nc), h[j], 64 * k, 64), ltile(Li), wv, lane);
         __syncthreads();
       }
-      pf_wait(flag + c * kPfMaxTiles + c, epoch);
+      pf_wait(flag + c * kPfMaxTiles + c, epoch, err, limit);
       stamp(1 + 2 * c);
       const double* lc = linv + (size_t)c * 64 * 64;
       for (int e = threadIdx.x; e < 64 * 64; e += 256) Li[(e >> 6) * kPfLd + (e & 63)] = lc[e];
@@ -950,10 +961,10 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
           acc[t][q] = (i < hr && j < wc) ? v : 0.0;
         }
       for (int k = 0; k < c; ++k) {
-        pf_wait(flag + c * kPfMaxTiles + k, epoch);
+        pf_wait(flag + c * kPfMaxTiles + k, epoch, err, limit);
         pf_gemm_nt(acc, -1.0, gtile(r0, hr, 64 * k, 64), gtile(c0, wc, 64 * k, 64), wv, lane);
       }
-      pf_wait(flag + c * kPfMaxTiles + c, epoch);
+      pf_wait(flag + c * kPfMaxTiles + c, epoch, err, limit);
       stamp(1 + 2 * c);
       // L_rc = T Linv_cc' (Linv_cc row-major in linv, staged in LDS)
       pf_acc_to_lds(acc, T, wv, lane);
@@ -1148,7 +1159,7 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
 // own_diag 6: diagonal factor + panel solve in one panel_factor_kernel launch
 rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info,
                                   CholWorkspace* ws) {
-  if (!ws || !ws->pf_ctrl || !ws->pf_linv || kb > 64 * kPfMaxTiles) return rocblas_status_invalid_pointer;
+  if (!ws || !ws->pf_ctrl || !ws->pf_linv || !ws->err || kb > 64 * kPfMaxTiles) return rocblas_status_invalid_pointer;
   hipStream_t s;
   if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
   const int mrows = n - k;
@@ -1165,7 +1176,7 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   }
   const unsigned epoch = ++ws->pf_epoch;
   hipLaunchKernelGGL(panel_factor_kernel, dim3(nr), dim3(256), 0, s, A + k + (size_t)k * lda, lda, kb, mrows, info,
-                     ws->pf_linv, ws->pf_ctrl, ws->pf_base, epoch, nbw, nullptr);
+                     ws->pf_linv, ws->pf_ctrl, ws->pf_base, epoch, nbw, ws->err, ws->spin_limit, nullptr);
   ws->pf_base += (unsigned)nr;
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
@@ -1320,6 +1331,8 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
     pf_base = 0;
     pf_epoch = 0;
     if (hipMemsetAsync(ctrl, 0, sizeof(unsigned) * (2 + (size_t)nblk), side) != hipSuccess) return false;
+    if (hipMalloc(&err, 4 * sizeof(unsigned)) != hipSuccess) { err = nullptr; return false; }
+    if (hipMemsetAsync(err, 0, 4 * sizeof(unsigned), side) != hipSuccess) return false;
     if (hipMalloc(&tinv, sizeof(double) * kTinv * kTinv) != hipSuccess) { tinv = nullptr; return false; }
     if (hipMalloc(&tbuf, sizeof(double) * kTinv * (size_t)nblk * kTB) != hipSuccess) { tbuf = nullptr; return false; }
     tbuf_rows = nblk * kTB;
@@ -1361,6 +1374,8 @@ void CholWorkspace::destroy() {
   tinv = nullptr;
   if (tbuf) (void)hipFree(tbuf);
   tbuf = nullptr;
+  if (err) (void)hipFree(err);
+  err = nullptr;
   tbuf_rows = 0;
   linv_rows = 0;
 }
@@ -1374,12 +1389,26 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   CholConfig c = cfg;
   if (c.own_diag == 6 && (c.panel <= 0 || c.panel > 64 * kPfMaxTiles)) c.own_diag = 2;
   if (c.own_diag == 7 && (c.panel <= 0 || c.panel > kTinv)) c.own_diag = 2;
-  if (ws) ws->pf_rows = c.panel_rows;
+  if (ws) {
+    ws->pf_rows = c.panel_rows;
+    ws->spin_limit = c.spin_log2 <= 0 ? 0u : (1u << std::min(c.spin_log2, 30));
+  }
   double* scratch = ws ? ws->scratch : nullptr;
   if (c.panel > 0 && c.gemm_update && c.lookahead && ws && ws->side)
     return factor_lookahead(h, n, A, lda, info, c, *ws);
   if (c.panel > 0) return factor_blocked(h, n, A, lda, info, c, scratch, ws);
   return factor(h, n, A, lda, info, c.own_diag, scratch);
+}
+
+hipError_t chol_error(CholWorkspace* ws, hipStream_t s, unsigned* word) {
+  *word = 0;
+  if (!ws || !ws->err) return hipSuccess;
+  unsigned h = 0;
+  hipError_t e = hipMemcpyAsync(&h, ws->err, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess && h != 0) e = hipMemsetAsync(ws->err, 0, sizeof(unsigned), s);
+  if (e == hipSuccess) *word = h;
+  return e;
 }
 
 rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x, int variant,
@@ -1394,7 +1423,7 @@ rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, dou
   hipStream_t s;
   if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
   if (variant == 2) {
-    if (!ws->ctrl) return rocblas_status_invalid_pointer;
+    if (!ws->ctrl || !ws->err) return rocblas_status_invalid_pointer;
     // tickets reset; the flags carry the sweep's epoch (no reset needed)
     if (ws->epoch > 0xfffffff0u) {
       if (hipMemsetAsync(ws->ctrl, 0, sizeof(unsigned) * (2 + (size_t)ws->linv_rows / kTB), s) != hipSuccess)
@@ -1405,8 +1434,10 @@ rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, dou
     const unsigned e = ++ws->epoch;
     const unsigned e2 = ++ws->epoch;
     const int nblk = (n + kTB - 1) / kTB;
-    hipLaunchKernelGGL(trsv_sweep_kernel<true>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e);
-    hipLaunchKernelGGL(trsv_sweep_kernel<false>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e2);
+    hipLaunchKernelGGL(trsv_sweep_kernel<true>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e,
+                       ws->err, ws->spin_limit);
+    hipLaunchKernelGGL(trsv_sweep_kernel<false>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e2,
+                       ws->err, ws->spin_limit);
     return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
   }
   // inverses of the diagonal blocks (full blocks in one batched call, the

@@ -53,7 +53,16 @@ struct CholConfig {
   // launch per 64-wide block column with diagonal-block inverses, 0 recursive
   // rocBLAS dtrsv / dgemv
   int solve = 2;
+  // bound of every in-launch flag wait (panel factor, sync-free sweeps):
+  // 2^spin_log2 polls (~64 cycles each), 0 = no polling at all (a wait whose
+  // flag is not already set times out at once: the timeout test's hook).
+  // A wait that runs out records kCholErrWait in the workspace's error word
+  // (chol_error) instead of returning a silently wrong factor or solution.
+  int spin_log2 = 24;
 };
+
+// Error word bits (CholWorkspace::err, read by chol_error).
+constexpr unsigned kCholErrWait = 1u;  // a flag wait ran out: the factor / solution is invalid
 
 // Device resources of one factorisation owner (one per mi_ba_context, created
 // on the context's device): the look-ahead side stream with its own rocBLAS
@@ -80,6 +89,8 @@ struct CholWorkspace {
   double* tinv = nullptr;       // own_diag 7: [512*512] inverse of the panel's diagonal block
   double* tbuf = nullptr;       // own_diag 7: [max_n * 512] copy of the panel below it
   int tbuf_rows = 0;
+  unsigned* err = nullptr;      // [4] error word (kCholErr* bits) of the in-launch flag waits
+  unsigned spin_limit = 1u << 24;  // polls per flag wait (CholConfig::spin_log2)
 
   // Creates the resources on `device` with events for up to `max_panels`
   // panels and diagonal-block inverses for matrices up to max_n; false on any
@@ -107,5 +118,10 @@ int chol_leaf_count(int n, const CholConfig& cfg = {});
 // (ws unused).
 rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x, int variant,
                           CholWorkspace* ws);
+// Error word of the factorisations / solves issued on stream s since the last
+// call (synchronises s, then clears the word): 0, or kCholErr* bits.  A
+// nonzero word means a result of those calls is invalid; callers report it
+// as MI_BA_ERR_HIP.  *word = 0 without a workspace.
+hipError_t chol_error(CholWorkspace* ws, hipStream_t s, unsigned* word);
 
 }  // namespace miba

@@ -6,6 +6,9 @@
 //   mi_ba_filter_points3d              <- Reconstruction::
 //                                         FilterPoints3DWithLargeReprojectionError
 //                                         (src/base/reconstruction.cc:1470-1525)
+//   mi_ba_positive_depth               <- the HasPointPositiveDepth test of
+//                                         Reconstruction::FilterObservationsWithNegativeDepth
+//                                         (src/base/reconstruction.cc:647-665)
 //
 // One lane per observation (error) and one lane per point (filter decision
 // over its track, CSR by point built on the host in track order).  Both are
@@ -71,6 +74,44 @@ __global__ __launch_bounds__(kTB) void sq_reproj_error_kernel(ProjArgs a, double
   world_to_image_any(a.cam_model[cam], prm, P[0] / P[2], P[1] / P[2], &x, &y);
   const double2 o = a.xy[k];
   out[k] = (x - o.x) * (x - o.x) + (y - o.y) * (y - o.y);
+}
+
+// HasPointPositiveDepth(image.ProjectionMatrix(), X) (projection.cc:191-195)
+// for every observation: the third row of [R | t] with R =
+// Eigen::Quaterniond(qvec).normalized().toRotationMatrix() (pose.cc
+// QuaternionToRotationMatrix), dotted with (X, 1), >= DBL_EPSILON.  The
+// products are kept unfused and in Eigen's order (SSE2 squaredNorm pairs
+// (x, z) and (y, w); the strided row dot sums left to right), as the
+// reference's x86-64 build evaluates them.  Observations of images outside
+// image_mask are kept.
+__global__ __launch_bounds__(kTB) void positive_depth_kernel(ProjArgs a, const uint8_t* __restrict__ image_mask,
+                                                              uint8_t* __restrict__ keep) {
+#pragma clang fp contract(off)
+  const int64_t k = (int64_t)blockIdx.x * kTB + threadIdx.x;
+  if (k >= a.n) return;
+  const int img = a.obs_image[k];
+  if (image_mask && !image_mask[img]) {
+    keep[k] = 1;
+    return;
+  }
+  const int64_t pt = a.obs_point[k];
+  const double* qt = a.qt + 8 * (size_t)img;
+  const double w = qt[0], x = qt[1], y = qt[2], z = qt[3];
+  const double sq = (x * x + z * z) + (y * y + w * w);
+  double nw = w, nx = x, ny = y, nz = z;
+  if (sq > 0.0) {
+    const double n = sqrt(sq);
+    nw = w / n;
+    nx = x / n;
+    ny = y / n;
+    nz = z / n;
+  }
+  const double tx = 2.0 * nx, ty = 2.0 * ny, tz = 2.0 * nz;
+  const double twx = tx * nw, twy = ty * nw;
+  const double txx = tx * nx, txz = tz * nx, tyy = ty * ny, tyz = tz * ny;
+  const double r20 = txz - twy, r21 = tyz + twx, r22 = 1.0 - (txx + tyy);
+  const double depth = ((r20 * a.X[3 * pt] + r21 * a.X[3 * pt + 1]) + r22 * a.X[3 * pt + 2]) + qt[6] * 1.0;
+  keep[k] = depth >= DBL_EPSILON ? 1 : 0;
 }
 
 // reconstruction.cc:1480-1521 for one point: track elements with squared
@@ -282,5 +323,32 @@ extern "C" mi_ba_status mi_ba_filter_points3d(const mi_ba_problem* problem, doub
   int64_t total = 0;
   for (int64_t v : nf) total += v;
   *num_filtered = total;
+  return MI_BA_OK;
+}
+
+extern "C" mi_ba_status mi_ba_positive_depth(const mi_ba_problem* problem, const uint8_t* image_mask, int32_t device,
+                                            uint8_t* obs_keep, int64_t* num_negative) {
+  HostSetup s;
+  mi_ba_status st = check(problem, &s);
+  if (st != MI_BA_OK) return st;
+  const int64_t N = problem->num_obs;
+  if ((N > 0 && !obs_keep) || !num_negative) return MI_BA_ERR_INVALID_ARGUMENT;
+  if ((st = set_device(device)) != MI_BA_OK) return st;
+  *num_negative = 0;
+  if (N == 0) return MI_BA_OK;
+  Buf b[11];
+  ProjArgs a;
+  if ((st = upload(problem, s, b, &a)) != MI_BA_OK) return st;
+  const int I = problem->num_images;
+  uint8_t* d_mask = image_mask ? b[8].alloc<uint8_t>(I) : nullptr;
+  uint8_t* d_keep = b[9].alloc<uint8_t>(N);
+  if ((image_mask && !d_mask) || !d_keep) return MI_BA_ERR_OUT_OF_MEMORY;
+  if (image_mask && I && hipMemcpy(d_mask, image_mask, I, hipMemcpyHostToDevice) != hipSuccess) return MI_BA_ERR_HIP;
+  hipLaunchKernelGGL(positive_depth_kernel, dim3((unsigned)((N + kTB - 1) / kTB)), dim3(kTB), 0, 0, a, d_mask, d_keep);
+  if (hipGetLastError() != hipSuccess) return MI_BA_ERR_HIP;
+  if (hipMemcpy(obs_keep, d_keep, N, hipMemcpyDeviceToHost) != hipSuccess) return MI_BA_ERR_HIP;
+  int64_t neg = 0;
+  for (int64_t k = 0; k < N; ++k) neg += obs_keep[k] == 0;
+  *num_negative = neg;
   return MI_BA_OK;
 }

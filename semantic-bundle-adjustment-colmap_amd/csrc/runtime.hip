@@ -502,10 +502,11 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
         return fail(MI_BA_ERR_HIP);
       hipLaunchKernelGGL(identity_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, ctx->stream, ctx->S.ptr,
                          nf);
+      unsigned werr = 0;
       if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr, ctx->chol, &ctx->cholws) !=
               rocblas_status_success ||
           chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr, ctx->chol.solve, &ctx->cholws) != rocblas_status_success ||
-          hipStreamSynchronize(ctx->stream) != hipSuccess)
+          chol_error(&ctx->cholws, ctx->stream, &werr) != hipSuccess || werr != 0)
         return fail(MI_BA_ERR_HIP);
     }
   }
@@ -682,6 +683,21 @@ mi_ba_status pcg(mi_ba_context* ctx, int* iterations) {
   return MI_BA_OK;
 }
 
+// A device-side failure seen by this rank (a Cholesky flag wait that ran
+// out) ends the solve with MI_BA_ERR_HIP on every rank: one 8-byte sum over
+// the ranks, so no rank stays behind in a later collective.
+mi_ba_status agree_on_error(mi_ba_context* ctx, bool failed) {
+  if (ctx->world <= 1) return failed ? MI_BA_ERR_HIP : MI_BA_OK;
+  double* slot = ctx->scalars.ptr + kXR;
+  const double v = failed ? 1.0 : 0.0;
+  MI_HIP(hipMemcpyAsync(slot, &v, 8, hipMemcpyHostToDevice, ctx->stream));
+  mi_ba_status st = allreduce(ctx, slot, 1);
+  if (st != MI_BA_OK) return st;
+  st = read_scalars(ctx, kXR, 1);
+  if (st != MI_BA_OK) return st;
+  return ctx->host_scalars[kXR] != 0.0 ? MI_BA_ERR_HIP : MI_BA_OK;
+}
+
 // Exact solve of S df = -b with the explicit reduced camera system.
 // *ok = false when S is not positive definite (Ceres: invalid step).
 mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
@@ -724,7 +740,12 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   timer_end(ctx, stop);
   std::vector<int32_t> info(leaves, 0);
   MI_HIP(hipMemcpyAsync(info.data(), ctx->info.ptr, 4 * (size_t)leaves, hipMemcpyDeviceToHost, s));
-  MI_HIP(hipStreamSynchronize(s));
+  unsigned werr = 0;
+  MI_HIP(chol_error(&ctx->cholws, s, &werr));  // synchronises s
+  // a flag wait of the factorisation ran out: the factor is invalid (every
+  // rank learns it, so no rank takes a step the others do not)
+  mi_ba_status st = agree_on_error(ctx, werr != 0);
+  if (st != MI_BA_OK) return st;
   for (int32_t v : info) {
     if (v != 0) {
       *ok = false;
@@ -736,6 +757,43 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
     if (chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr, ctx->chol.solve, &ctx->cholws) != rocblas_status_success)
       return MI_BA_ERR_HIP;
   }
+  MI_HIP(chol_error(&ctx->cholws, s, &werr));
+  return agree_on_error(ctx, werr != 0);
+}
+
+// Ceres RunCallbacks for one finished iteration: the stop flag, then the
+// caller's IterationCallback (after writing the current point back into the
+// problem arrays when update_state_every_iteration is set).  Multi-rank: the
+// ranks' requests are summed so every rank takes the same decision (abort
+// before terminate before continue).  Returns the MI_BA_SOLVER_* decision.
+mi_ba_status run_callbacks(mi_ba_context* ctx, const mi_ba_iteration_summary& it, int32_t* decision) {
+  const mi_ba_options& o = ctx->options;
+  int32_t d = MI_BA_SOLVER_CONTINUE;
+  if (o.stop_flag) {
+    const int32_t v = __atomic_load_n(o.stop_flag, __ATOMIC_RELAXED);
+    if (v == MI_BA_SOLVER_TERMINATE_SUCCESSFULLY || v == MI_BA_SOLVER_ABORT) d = v;
+  }
+  if (d == MI_BA_SOLVER_CONTINUE && o.iteration_callback) {
+    if (o.update_state_every_iteration) {
+      mi_ba_status st = context_writeback(ctx);
+      if (st != MI_BA_OK) return st;
+    }
+    const int32_t v = o.iteration_callback(o.callback_user, &it);
+    if (v == MI_BA_SOLVER_TERMINATE_SUCCESSFULLY || v == MI_BA_SOLVER_ABORT) d = v;
+  }
+  if (ctx->world > 1) {
+    double* slot = ctx->scalars.ptr + kXB;  // kXB, kXR: PCG scratch, free between solves
+    const double v[2] = {d == MI_BA_SOLVER_TERMINATE_SUCCESSFULLY ? 1.0 : 0.0, d == MI_BA_SOLVER_ABORT ? 1.0 : 0.0};
+    MI_HIP(hipMemcpyAsync(slot, v, 16, hipMemcpyHostToDevice, ctx->stream));
+    mi_ba_status st = allreduce(ctx, slot, 2);
+    if (st != MI_BA_OK) return st;
+    st = read_scalars(ctx, kXB, 2);
+    if (st != MI_BA_OK) return st;
+    d = ctx->host_scalars[kXR] != 0.0   ? MI_BA_SOLVER_ABORT
+        : ctx->host_scalars[kXB] != 0.0 ? MI_BA_SOLVER_TERMINATE_SUCCESSFULLY
+                                        : MI_BA_SOLVER_CONTINUE;
+  }
+  *decision = d;
   return MI_BA_OK;
 }
 
@@ -771,10 +829,31 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
   int consecutive_invalid = 0, iteration = 0;
   sum->termination_type = MI_BA_NO_CONVERGENCE;
   const int64_t nf = d.nf;
+  // the finished iteration handed to the callbacks (iteration 0: the initial
+  // evaluation, valid and successful as in Ceres' IterationZero)
+  mi_ba_iteration_summary its{};
+  its.step_is_valid = 1;
+  its.step_is_successful = 1;
+  double t_iter = t_start;
+  const bool callbacks = o.iteration_callback || o.stop_flag || ctx->world > 1;
   while (true) {
+    if (callbacks) {
+      its.iteration = iteration;
+      its.cost = x_cost + ctx->fixed_cost;
+      its.trust_region_radius = radius;
+      its.iteration_time_in_seconds = now_s() - t_iter;
+      its.cumulative_time_in_seconds = now_s() - t_start;
+      int32_t decision = MI_BA_SOLVER_CONTINUE;
+      st = run_callbacks(ctx, its, &decision);
+      if (st != MI_BA_OK) return st;
+      if (decision == MI_BA_SOLVER_TERMINATE_SUCCESSFULLY) { sum->termination_type = MI_BA_USER_SUCCESS; break; }
+      if (decision == MI_BA_SOLVER_ABORT) { sum->termination_type = MI_BA_USER_FAILURE; break; }
+    }
     if (iteration >= o.max_num_iterations) { sum->termination_type = MI_BA_NO_CONVERGENCE; break; }
     if (radius < 1e-32) { sum->termination_type = MI_BA_CONVERGENCE; break; }
     ++iteration;
+    t_iter = now_s();
+    its = mi_ba_iteration_summary{};
     // Damped point inverses, Schur-Jacobi blocks, rhs.
     {
       Phase ph_(ctx, "point_prepare");
@@ -829,6 +908,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     }
     if (st != MI_BA_OK) return st;
     sum->num_linear_solver_iterations += cg_it;
+    its.linear_solver_iterations = cg_it;
     if (!solved_ok) {
       ++consecutive_invalid;
       ++sum->num_unsuccessful_steps;
@@ -879,6 +959,8 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     }
     consecutive_invalid = 0;
     const double step_norm = std::sqrt(hs[kStepNorm]);
+    its.step_is_valid = 1;
+    its.step_norm = step_norm;
     // candidate
     launch_plus(d, ctx->cg_x.ptr, ctx->dX.ptr, ctx->qt.ptr, ctx->cam.ptr, ctx->X.ptr, ctx->qt_c.ptr,
                 ctx->cam_c.ptr, ctx->X_c.ptr, s);
@@ -922,8 +1004,11 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       sum->termination_type = MI_BA_CONVERGENCE;
       break;
     }
+    its.relative_decrease = relative_decrease;
     if (success) {
       ++sum->num_successful_steps;
+      its.step_is_successful = 1;
+      its.cost_change = cost_change;
       x_cost = candidate_cost;
       std::swap(ctx->qt.ptr, ctx->qt_c.ptr);
       std::swap(ctx->cam.ptr, ctx->cam_c.ptr);
@@ -1048,6 +1133,10 @@ void mi_ba_default_options(mi_ba_options* o) {
   o->min_relative_decrease = 1e-3;
   o->device = 0;
   o->semantic_weight = 1.0;
+  o->iteration_callback = nullptr;
+  o->callback_user = nullptr;
+  o->update_state_every_iteration = 0;
+  o->stop_flag = nullptr;
 }
 
 mi_ba_status mi_ba_setup_stats(const mi_ba_options* o, const mi_ba_problem* p, mi_ba_setup_info* info) {
@@ -1073,7 +1162,9 @@ static void print_summary(const mi_ba_summary& s) {
   // PrintSolverSummary (bundle_adjustment.cc:1142-1196)
   const char* term = s.termination_type == MI_BA_CONVERGENCE ? "Convergence"
                      : s.termination_type == MI_BA_NO_CONVERGENCE ? "No convergence"
-                     : s.termination_type == MI_BA_FAILURE ? "Failure" : "Unknown";
+                     : s.termination_type == MI_BA_FAILURE ? "Failure"
+                     : s.termination_type == MI_BA_USER_SUCCESS ? "User success"
+                     : s.termination_type == MI_BA_USER_FAILURE ? "User failure" : "Unknown";
   std::printf("    Residuals : %lld\n   Parameters : %lld\n   Iterations : %d\n         Time : %g [s]\n"
               " Initial cost : %g [px]\n   Final cost : %g [px]\n  Termination : %s\n\n",
               (long long)s.num_residuals_reduced, (long long)s.num_effective_parameters_reduced,
@@ -1083,6 +1174,12 @@ static void print_summary(const mi_ba_summary& s) {
 }
 
 namespace {
+// Ceres copies the solver state back into the user's parameter blocks only
+// for a usable solution: not after FAILURE or USER_FAILURE (Solver::Solve).
+bool solution_usable(const mi_ba_summary& s) {
+  return s.termination_type != MI_BA_FAILURE && s.termination_type != MI_BA_USER_FAILURE;
+}
+
 // One BundleAdjuster::Solve on *arena (recycled, or created when null); the
 // context is kept in *arena for the next solve, or destroyed on failure.
 mi_ba_status solve_on(mi_ba_context** arena, const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem,
@@ -1095,7 +1192,7 @@ mi_ba_status solve_on(mi_ba_context** arena, const mi_ba_options* o, mi_ba_probl
   if (st != MI_BA_OK) return st;
   // SetUp normalised the config qvecs of ctx->problem (== caller arrays).
   st = context_solve(ctx, sum);
-  if (st == MI_BA_OK) st = context_writeback(ctx);
+  if (st == MI_BA_OK && solution_usable(*sum)) st = context_writeback(ctx);
   if (st != MI_BA_OK) {
     context_destroy(ctx);
     *arena = nullptr;
@@ -1151,7 +1248,7 @@ mi_ba_status mi_ba_gsba_solve(const mi_ba_options* o, mi_ba_problem* p, mi_ba_gs
   st = context_recycle(nullptr, &oo, &pp, nullptr, &ctx, g);
   if (st != MI_BA_OK) return st;
   st = context_solve(ctx, sum);
-  if (st == MI_BA_OK) st = context_writeback(ctx);
+  if (st == MI_BA_OK && solution_usable(*sum)) st = context_writeback(ctx);
   context_destroy(ctx);
   sum->total_time_in_seconds = now_s() - t0;
   if (st == MI_BA_OK && o->print_summary) print_summary(*sum);
@@ -1416,6 +1513,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.rest_update = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "cholesky_spin_log2") == 0 && value >= 0 && value <= 30) {
+    ctx->chol.spin_log2 = value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_gemm_update") == 0 && (value == 0 || value == 1)) {
     ctx->chol.gemm_update = value != 0;
     return MI_BA_OK;
@@ -1468,8 +1569,9 @@ mi_ba_status mi_ba_dense_cholesky_ex(int32_t device, int32_t n, double* A, doubl
       break;
     }
     if (chol_factor(h, n, dA.ptr, n, dinfo.ptr, cfg, &ws) != rocblas_status_success) { st = MI_BA_ERR_HIP; break; }
+    unsigned werr = 0;
     if (hipMemcpyAsync(hinfo.data(), dinfo.ptr, dinfo.bytes(), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
+        chol_error(&ws, s, &werr) != hipSuccess || werr != 0) {
       st = MI_BA_ERR_HIP;
       break;
     }
@@ -1480,7 +1582,9 @@ mi_ba_status mi_ba_dense_cholesky_ex(int32_t device, int32_t n, double* A, doubl
       if (hinfo[k] != 0) *info = (int32_t)(col0 + hinfo[k]);
       col0 += width;
     }
-    if (b && *info == 0 && chol_solve(h, n, dA.ptr, n, dx.ptr, cfg.solve, &ws) != rocblas_status_success) {
+    if (b && *info == 0 &&
+        (chol_solve(h, n, dA.ptr, n, dx.ptr, cfg.solve, &ws) != rocblas_status_success ||
+         chol_error(&ws, s, &werr) != hipSuccess || werr != 0)) {
       st = MI_BA_ERR_HIP;
       break;
     }

@@ -24,7 +24,8 @@ OK, ERR_INVALID_ARGUMENT, ERR_NO_DEVICE, ERR_UNSUPPORTED, ERR_HIP, ERR_NO_RESIDU
 SIMPLE_PINHOLE, PINHOLE, SIMPLE_RADIAL, RADIAL, OPENCV = range(5)
 LOSS_TRIVIAL, LOSS_SOFT_L1, LOSS_CAUCHY = range(3)
 SOLVER_AUTO, SOLVER_DENSE_SCHUR, SOLVER_ITERATIVE_SCHUR = range(3)
-CONVERGENCE, NO_CONVERGENCE, FAILURE = range(3)
+CONVERGENCE, NO_CONVERGENCE, FAILURE, USER_SUCCESS, USER_FAILURE = range(5)
+SOLVER_CONTINUE, SOLVER_ABORT, SOLVER_TERMINATE_SUCCESSFULLY = range(3)
 OUT_OF_BOUNDS, INVALID_DEPTH, VALID = -1, -2, 10
 NUM_PARAMS = {SIMPLE_PINHOLE: 3, PINHOLE: 4, SIMPLE_RADIAL: 4, RADIAL: 5, OPENCV: 8}
 MODEL_NAMES = {"SIMPLE_PINHOLE": 0, "PINHOLE": 1, "SIMPLE_RADIAL": 2, "RADIAL": 3, "OPENCV": 4}
@@ -34,6 +35,30 @@ _fp = C.POINTER(C.c_float)
 _i32p = C.POINTER(C.c_int32)
 _i64p = C.POINTER(C.c_int64)
 _u8p = C.POINTER(C.c_uint8)
+
+
+class IterationSummary(C.Structure):
+    """mi_ba_iteration_summary (ceres::IterationSummary fields)."""
+    _fields_ = [
+        ("iteration", C.c_int32),
+        ("step_is_valid", C.c_int32),
+        ("step_is_successful", C.c_int32),
+        ("linear_solver_iterations", C.c_int32),
+        ("cost", C.c_double),
+        ("cost_change", C.c_double),
+        ("relative_decrease", C.c_double),
+        ("trust_region_radius", C.c_double),
+        ("step_norm", C.c_double),
+        ("iteration_time_in_seconds", C.c_double),
+        ("cumulative_time_in_seconds", C.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# mi_ba_iteration_callback_fn: int32 (void* user, const mi_ba_iteration_summary*)
+ITERATION_CALLBACK_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.POINTER(IterationSummary))
 
 
 class Options(C.Structure):
@@ -57,7 +82,34 @@ class Options(C.Structure):
         ("min_relative_decrease", C.c_double),
         ("device", C.c_int32),
         ("semantic_weight", C.c_double),
+        ("iteration_callback", ITERATION_CALLBACK_FN),
+        ("callback_user", C.c_void_p),
+        ("update_state_every_iteration", C.c_int32),
+        ("stop_flag", _i32p),
     ]
+
+    def set_callback(self, fn, update_state_every_iteration: bool = False):
+        """Install `fn(IterationSummary) -> MI_BA_SOLVER_*` (None / a falsy
+        return continues) as the solver's iteration callback; the thunk is
+        kept alive on the options object."""
+        def _cb(_user, summary):
+            try:
+                r = fn(summary.contents)
+                return int(r) if r else SOLVER_CONTINUE
+            except Exception:  # noqa: BLE001 — an exception in the callback aborts the solve
+                return SOLVER_ABORT
+        self._thunk = ITERATION_CALLBACK_FN(_cb)
+        self.iteration_callback = self._thunk
+        self.update_state_every_iteration = 1 if update_state_every_iteration else 0
+        return self
+
+    def set_stop_flag(self, flag: "np.ndarray"):
+        """Point the solver's stop flag at flag[0] (an int32 numpy array the
+        caller keeps alive and may set from another thread)."""
+        assert flag.dtype == np.int32 and flag.flags.c_contiguous
+        self._stop = flag
+        self.stop_flag = flag.ctypes.data_as(_i32p)
+        return self
 
 
 class Problem(C.Structure):
@@ -224,6 +276,7 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_squared_reprojection_errors.argtypes = [C.c_void_p, C.c_int32, _dp]
     lib.mi_ba_filter_points3d.argtypes = [C.c_void_p, C.c_double, _u8p, C.c_int32, _u8p, _u8p, _dp,
                                           C.POINTER(C.c_int64)]
+    lib.mi_ba_positive_depth.argtypes = [C.c_void_p, _u8p, C.c_int32, _u8p, C.POINTER(C.c_int64)]
     _lib = lib
     return lib
 
@@ -647,6 +700,18 @@ def filter_points3d(scene: Scene, max_reproj_error: float, point_mask: Optional[
                                        obs_keep.ctypes.data_as(_u8p), point_keep.ctypes.data_as(_u8p),
                                        err.ctypes.data_as(_dp), C.byref(nf)), "mi_ba_filter_points3d")
     return obs_keep.astype(bool), point_keep.astype(bool), err, nf.value
+
+
+def positive_depth(scene: Scene, image_mask: Optional[np.ndarray] = None, device: int = 0):
+    """mi_ba_positive_depth: (keep [N] bool, number of negative-depth
+    observations) — FilterObservationsWithNegativeDepth's test."""
+    p = scene.problem()
+    keep = np.zeros(scene.num_obs, np.uint8)
+    mask = None if image_mask is None else np.ascontiguousarray(image_mask, dtype=np.uint8)
+    n = C.c_int64(0)
+    check(load().mi_ba_positive_depth(C.byref(p), _ptr(mask, _u8p), device, keep.ctypes.data_as(_u8p), C.byref(n)),
+          "mi_ba_positive_depth")
+    return keep.astype(bool), n.value
 
 
 def device_count() -> int:

@@ -225,3 +225,25 @@ def test_lm_panel_rows(gpu):
     for a in res[1:]:
         assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
         assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
+
+
+def test_factor_at_c4_size_matches_lapack(gpu):
+    """nf = 11 993, the C4 reduced camera system (998 * 6 + 5 + 1000 * 6): the
+    default factorisation the bench times (24 panels of 512, one-launch panel
+    factor, look-ahead, sync-free sweeps) on a random DENSE SPD matrix against
+    LAPACK dpotrf: max|dL| <= 1e-12 * max|L|, solve within 1e-10 of LAPACK's."""
+    from scipy.linalg import cho_factor, cho_solve
+    n = 11993
+    rng = np.random.default_rng(n)
+    G = rng.standard_normal((n, 1024))
+    A = G @ G.T / 1024.0 + np.diag(rng.uniform(0.5, 2.0, n))
+    del G
+    b = rng.standard_normal(n)
+    L, x, info = mi_ba.dense_cholesky(A, b)
+    assert info == 0
+    c, low = cho_factor(A, lower=True, check_finite=False)
+    L_ref = np.tril(c)
+    scale = np.abs(L_ref).max()
+    assert np.abs(L - L_ref).max() <= 1e-12 * scale
+    x_ref = cho_solve((c, low), b, check_finite=False)
+    assert np.abs(x - x_ref).max() <= 1e-10 * np.abs(x_ref).max()

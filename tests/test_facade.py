@@ -1,6 +1,9 @@
 """The reference's BundleAdjuster tests (src/optim/bundle_adjustment_test.cc)
 rerun in C++ through the colmap_amd facade (include/colmap_amd/) on
-libmi_ba.so: structural counts on the host, full Solve on the MI355X."""
+libmi_ba.so: structural counts on the host, full Solve on the MI355X.  Also
+the controllers / iteration callbacks / Reconstruction filters
+(tests/cpp/controllers_test.cc: reconstruction_test.cc:415-434,510-531 known
+answers, controllers/bundle_adjustment.cc:43-103 callback semantics)."""
 import os
 import subprocess
 
@@ -10,13 +13,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CPP = os.path.join(HERE, "cpp")
 
 
-def build():
+def build(name="bundle_adjustment_test"):
     subprocess.run(["make", "-s", "-C", CPP], check=True)
-    return os.path.join(CPP, "bundle_adjustment_test")
+    return os.path.join(CPP, name)
 
 
-def run(mode):
-    exe = build()
+def run(mode, name="bundle_adjustment_test"):
+    exe = build(name)
     out = subprocess.run([exe, mode], capture_output=True, text=True, timeout=600)
     print(out.stdout)
     assert out.returncode == 0, out.stdout + out.stderr
@@ -33,3 +36,14 @@ def test_facade_counts_cpu():
 def test_facade_solve_gpu(gpu):
     out = run("solve")
     assert out.count("PASS") == 15
+
+
+def test_controllers_host():
+    out = run("host", "controllers_test")
+    assert out.count("PASS") == 2
+
+
+@pytest.mark.gpu
+def test_controllers_gpu(gpu):
+    out = run("gpu", "controllers_test")
+    assert out.count("PASS") == 9

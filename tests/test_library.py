@@ -64,7 +64,7 @@ def test_default_options_match_reference():
 
 def test_abi_version_and_params():
     lib = mi_ba.load()
-    assert lib.mi_ba_abi_version() == 2
+    assert lib.mi_ba_abi_version() == 3
     for m, n in mi_ba.NUM_PARAMS.items():
         assert lib.mi_ba_num_params(m) == n
     assert lib.mi_ba_num_params(99) == -1
