@@ -4,6 +4,8 @@
 //   colmap::Cylinder (q, t, radius, height; text I/O)      src/util/cylinder.h:153-631
 //   colmap::GeometricSemanticBundleAdjustmentOptions        src/optim/geometric_semantic_bundle_adjustment.h:51-150
 //   colmap::GeometricSemanticBundleAdjuster<Cylinder>        ...bundle_adjustment.cc:481-1338
+//   colmap::GeometricSemanticBundleAdjuster<CylinderBy2Points> (cylinder_parametrization
+//     "by_2_points"; src/util/cylinder_by_2_points.h, ...bundle_adjustment.cc:917-1010,1185-1213)
 //
 // Solve(reconstruction, cylinders): reads <data_path>/depth_tiff and
 // semantic_tiff maps of the config images (ReadDepthAndSemanticMaps,
@@ -78,6 +80,8 @@ inline void WriteCylindersText(const std::string& path, const std::vector<Cylind
   for (const Cylinder& c : cylinders) f << c.ToString() << "\n";
 }
 
+enum class CylinderParametrization { DEFAULT, BY2POINTS };
+
 struct GeometricSemanticBundleAdjustmentOptions : BundleAdjustmentOptions {
   std::string data_path;               // folder with depth_tiff/ and semantic_tiff/
   std::string input_geometry;          // cylinder text file (Solve(reconstruction) reads it)
@@ -86,6 +90,15 @@ struct GeometricSemanticBundleAdjustmentOptions : BundleAdjustmentOptions {
   bool include_landmark_error = false;
   double landmark_error_weight = 1;
   double numeric_relative_step_size = 1e-3;
+  // "default" (GeometricSemanticBundleAdjuster<Cylinder>) or "by_2_points"
+  // (<CylinderBy2Points>): geometric_semantic_bundle_adjustment.h:49-95
+  std::string cylinder_parametrization = "default";
+
+  CylinderParametrization GetCylinderParametrization() const {
+    if (cylinder_parametrization == "default") return CylinderParametrization::DEFAULT;
+    if (cylinder_parametrization == "by_2_points") return CylinderParametrization::BY2POINTS;
+    throw std::runtime_error("ERROR: '" + cylinder_parametrization + "' is not a valid cylinder parametrization.");
+  }
 };
 
 class GeometricSemanticBundleAdjuster {
@@ -151,6 +164,9 @@ class GeometricSemanticBundleAdjuster {
     g.numeric_relative_step_size = options_.numeric_relative_step_size;
     g.include_landmark_error = options_.include_landmark_error;
     g.landmark_error_weight = options_.landmark_error_weight;
+    g.cylinder_parametrization = options_.GetCylinderParametrization() == CylinderParametrization::BY2POINTS
+                                     ? MI_BA_CYLINDER_BY_2_POINTS
+                                     : MI_BA_CYLINDER_DEFAULT;
     mi_ba_options o = internal::ToOptions(options_);
     internal::CallbackBridge bridge;
     internal::InstallCallbacks(options_, &bridge, [&] {

@@ -236,6 +236,16 @@ typedef struct mi_ba_cylinder {
   double height;
 } mi_ba_cylinder;
 
+/* GeometricSemanticBundleAdjustmentOptions::cylinder_parametrization
+ * (geometric_semantic_bundle_adjustment.h:49-95): "default" optimises each
+ * cylinder as (qvec 4 on the QuaternionManifold, tvec 3, radius, height);
+ * "by_2_points" as CylinderBy2Points (src/util/cylinder_by_2_points.h:26-155):
+ * the centres of its two circles and its radius, Euclidean, radius bounded
+ * below by 0 (:1185-1213), evaluated through CylinderBy2Points::ToCylinder.
+ * The cylinders are read and written as (qvec, tvec, radius, height) in both
+ * (pushBackCylindersReadFromText / exportCylindersToText). */
+enum { MI_BA_CYLINDER_DEFAULT = 0, MI_BA_CYLINDER_BY_2_POINTS = 1 };
+
 typedef struct mi_ba_gsba {
   int32_t height;                    /* trunk mask size, every image */
   int32_t width;
@@ -247,6 +257,7 @@ typedef struct mi_ba_gsba {
   double numeric_relative_step_size; /* default 1e-3 */
   int32_t include_landmark_error;    /* default 0: the problem's observations are not used */
   double landmark_error_weight;      /* default 1: reprojection blocks get ScaledLoss(w / #config 2D features) */
+  int32_t cylinder_parametrization;  /* MI_BA_CYLINDER_*, default MI_BA_CYLINDER_DEFAULT (ABI 3) */
 } mi_ba_gsba;
 
 /* Mirrors the ceres::Solver::Summary fields COLMAP reads
@@ -306,13 +317,15 @@ mi_ba_status mi_ba_solve(const mi_ba_options* options, mi_ba_problem* problem,
 
 /* --- geometric-semantic BA (GSBA) ----------------------------------------
  * mi_ba_default_gsba: GeometricSemanticBundleAdjustmentOptions defaults.
- * mi_ba_gsba_solve: GeometricSemanticBundleAdjuster<Cylinder>::Solve on the
+ * mi_ba_gsba_solve: GeometricSemanticBundleAdjuster<Cylinder> (or
+ * <CylinderBy2Points>, gsba.cylinder_parametrization)::Solve on the
  * GPU: poses (and cylinders when refine_geometry) refined; with
  * include_landmark_error also the problem's points (SIMPLE_PINHOLE
  * reprojection blocks, ScaledLoss).  Blocks are ordered by config image
  * (problem order) then cylinder.
  * mi_ba_gsba_evaluate: residual 1 - IoU and the ambient CENTRAL Jacobian
- * [n][16] (camera q(4) t(3), cylinder q(4) t(3) radius height; columns of
+ * [n][16] (camera q(4) t(3), cylinder q(4) t(3) radius height — by_2_points:
+ * cylinder tvec_1(3) tvec_2(3) radius and two zero columns; columns of
  * constant blocks zero) of every block, before the ScaledLoss; block_ids
  * [n][2] = (image, cylinder).  *num_blocks receives the count; nothing is
  * written when it exceeds capacity. */

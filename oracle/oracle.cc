@@ -460,6 +460,9 @@ struct GsbaSetup {
   std::vector<GsbaBlock> blocks;
   std::vector<int64_t> sem_total;  // per image: count of the trunk mask
   double weight = 1.0;             // ScaledLoss(1 / #config images), :721-722
+  bool by2 = false;                // MI_BA_CYLINDER_BY_2_POINTS
+  std::vector<double> by2p;        // by2: [ncyl][7] tvec_1, tvec_2, radius (the LM's parameters)
+  int cw() const { return by2 ? 7 : 8; }
 };
 
 // GeometricSemanticBundleAdjuster::Assert (:664-712) + AddImageToProblem
@@ -478,6 +481,17 @@ int BuildGsbaSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& 
     if (s.cam_model[cam] != MI_BA_SIMPLE_PINHOLE) return MI_BA_ERR_UNSUPPORTED;
   }
   gs->weight = ncfg > 0 ? 1. / (double)ncfg : 1.0;
+  if (g->cylinder_parametrization != MI_BA_CYLINDER_DEFAULT && g->cylinder_parametrization != MI_BA_CYLINDER_BY_2_POINTS)
+    return MI_BA_ERR_INVALID_ARGUMENT;
+  gs->by2 = g->cylinder_parametrization == MI_BA_CYLINDER_BY_2_POINTS;
+  if (gs->by2) {
+    // pushBackCylindersReadFromText: every Cylinder converted (cylinder_by_2_points.h:145-153)
+    gs->by2p.assign(7 * (size_t)g->num_cylinders, 0.0);
+    for (int c = 0; c < g->num_cylinders; ++c) {
+      const mi_ba_cylinder& y = g->cylinders[c];
+      GsbaCylinderToBy2(y.qvec, y.tvec, y.radius, y.height, &gs->by2p[7 * (size_t)c]);
+    }
+  }
   const int64_t plane = (int64_t)g->height * g->width;
   gs->sem_total.assign(I, 0);
   for (int i = 0; i < I; ++i) {
@@ -517,6 +531,10 @@ double GsbaResidual(const mi_ba_problem* p, const Setup& s, const GsbaSetup& gs,
   const mi_ba_cylinder& y = g->cylinders[b.cyl];
   const double* K = &p->camera_params[s.cam_poff[p->image_camera[b.img]]];
   const int64_t plane = (int64_t)g->height * g->width;
+  if (gs.by2)
+    return GsbaEvalBlock(b.variant, &p->qvec[b.img * 4], &p->tvec[b.img * 3], K, nullptr, &gs.by2p[7 * (size_t)b.cyl],
+                         0.0, 0.0, g->trunk_mask + b.img * plane, g->height, g->width, gs.sem_total[b.img],
+                         g->numeric_relative_step_size, J16);
   return GsbaEvalBlock(b.variant, &p->qvec[b.img * 4], &p->tvec[b.img * 3], K, y.qvec, y.tvec, y.radius, y.height,
                        g->trunk_mask + b.img * plane, g->height, g->width, gs.sem_total[b.img],
                        g->numeric_relative_step_size, J16);
@@ -527,7 +545,8 @@ struct Layout {
   std::vector<int> img_off;   // -1 if not variable; 6 tangent slots (masked coords skipped)
   std::vector<int> img_cols;  // mapping slot (0..5) -> column or -1
   std::vector<int> cam_off;
-  std::vector<int> cyl_off;   // GSBA cylinders: 8 tangent slots (q 3, t 3, radius, height) or -1
+  std::vector<int> cyl_off;   // GSBA cylinders: 8 tangent slots (q 3, t 3, radius, height), by 2 points 7
+                              // (tvec_1 3, tvec_2 3, radius), or -1
   int nf = 0;
   std::vector<int64_t> pt_off;  // -1 if constant
   int64_t ne = 0;
@@ -594,7 +613,7 @@ void BuildLayout(const Setup& s, const mi_ba_problem* p, Layout* L, const mi_ba_
   for (size_t c = 0; c < used_cyl.size(); ++c) {
     if (!used_cyl[c]) continue;
     L->cyl_off[c] = nf;
-    nf += 8;
+    nf += gs && gs->by2 ? 7 : 8;
   }
   L->nf = nf;
   L->pt_off.assign(p->num_points, -1);
@@ -855,13 +874,18 @@ struct Solver {
           Jt[col] = acc;
         }
         for (int col = 0; col < 3; ++col) Jt[3 + col] = J16[4 + col];
-        QuaternionPlusJacobian(gs.g->cylinders[b.cyl].qvec, PJ);
-        for (int col = 0; col < 3; ++col) {
-          double acc = 0.0;
-          for (int m = 0; m < 4; ++m) acc += J16[7 + m] * PJ[m * 3 + col];
-          Jt[6 + col] = acc;
+        if (gs.by2) {
+          for (int col = 0; col < 7; ++col) Jt[6 + col] = J16[7 + col];  // Euclidean
+          Jt[13] = 0.0;
+        } else {
+          QuaternionPlusJacobian(gs.g->cylinders[b.cyl].qvec, PJ);
+          for (int col = 0; col < 3; ++col) {
+            double acc = 0.0;
+            for (int m = 0; m < 4; ++m) acc += J16[7 + m] * PJ[m * 3 + col];
+            Jt[6 + col] = acc;
+          }
+          for (int col = 0; col < 5; ++col) Jt[9 + col] = J16[11 + col];
         }
-        for (int col = 0; col < 5; ++col) Jt[9 + col] = J16[11 + col];
         double rho[3];
         LossEvaluate(kLossScaled, gs.weight, r * r, rho);
         cost[nr + ns + k] = 0.5 * rho[0];
@@ -874,7 +898,7 @@ struct Solver {
             if (col >= 0) { lin->fcol[R * Linearization::kF + nf] = col; lin->fval[R * Linearization::kF + nf++] = Jt[m]; }
           }
         if (b.variant != kGsbaConstantCylinder && L.cyl_off[b.cyl] >= 0)
-          for (int m = 0; m < 8; ++m) {
+          for (int m = 0; m < gs.cw(); ++m) {
             lin->fcol[R * Linearization::kF + nf] = L.cyl_off[b.cyl] + m;
             lin->fval[R * Linearization::kF + nf++] = Jt[6 + m];
           }
@@ -912,6 +936,13 @@ struct Solver {
     // bound 0 (ParameterBlock::Plus projects onto the bounds)
     for (size_t c = 0; c < L.cyl_off.size(); ++c) {
       if (L.cyl_off[c] < 0) continue;
+      if (gs.by2) {  // Euclidean; radius bounded below by 0 (:1185-1213)
+        double* y = &gs.by2p[7 * c];
+        const double* d = &delta[L.cyl_off[c]];
+        for (int m = 0; m < 6; ++m) y[m] += d[m];
+        y[6] = std::max(y[6] + d[6], 0.0);
+        continue;
+      }
       mi_ba_cylinder& y = gs.g->cylinders[c];
       const double* d = &delta[L.cyl_off[c]];
       double qn[4];
@@ -1116,7 +1147,7 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
   for (int c : S.L.cyl_off) ncyl_var += c >= 0 ? 1 : 0;
   sum->num_residuals_reduced =
       S.s.num_residuals_reduced + (int64_t)S.ss.samples.size() + (int64_t)S.gs.blocks.size();
-  sum->num_effective_parameters_reduced = S.s.num_effective_parameters_reduced + 8 * ncyl_var;
+  sum->num_effective_parameters_reduced = S.s.num_effective_parameters_reduced + S.gs.cw() * ncyl_var;
   sum->num_semantic_residuals = (int64_t)S.ss.samples.size();
   if (sum->num_residuals_reduced == 0) return MI_BA_ERR_NO_RESIDUALS;
   // fixed cost of the dropped all-constant blocks
@@ -1344,10 +1375,12 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
     std::vector<double> x0(p->xyz, p->xyz + 3 * p->num_points);
     std::vector<mi_ba_cylinder> y0;
     if (gsba) y0.assign(gsba->cylinders, gsba->cylinders + gsba->num_cylinders);
+    const std::vector<double> by2_0 = S.gs.by2p;
     auto restore = [&]() {
       std::copy(q0.begin(), q0.end(), p->qvec); std::copy(t0.begin(), t0.end(), p->tvec);
       std::copy(c0.begin(), c0.end(), p->camera_params); std::copy(x0.begin(), x0.end(), p->xyz);
       if (gsba) std::copy(y0.begin(), y0.end(), gsba->cylinders);
+      S.gs.by2p = by2_0;
     };
     double x_norm2 = 0.0;
     for (double v : q0) x_norm2 += v * v;
@@ -1389,6 +1422,13 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
     }
   }
   sum->final_cost = x_cost + fixed;
+  // by 2 points: the cylinders leave as ToCylinder() (exportCylindersToText)
+  if (gsba && S.gs.by2 && gsba->refine_geometry)
+    for (int c = 0; c < gsba->num_cylinders; ++c) {
+      if (S.L.cyl_off[c] < 0) continue;
+      mi_ba_cylinder& y = gsba->cylinders[c];
+      GsbaBy2ToCylinder(&S.gs.by2p[7 * (size_t)c], y.qvec, y.tvec, &y.radius, &y.height);
+    }
   return MI_BA_OK;
 }
 

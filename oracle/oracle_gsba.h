@@ -205,6 +205,64 @@ inline double GsbaIoU(const double cq[4], const double ct[3], const double K[3],
   return (double)tp / den;
 }
 
+// CylinderBy2Points::ToCylinder (src/util/cylinder_by_2_points.h:95-117) on
+// y = tvec_1(3) tvec_2(3) radius, through the constructor's Check (radius
+// <= 0 -> 1e-4, :38-42) and Cylinder's (height <= 0 -> 1e-4): d = (t2 - t1)
+// / |t2 - t1| (Eigen: norms and dot products of 3-vectors summed left to
+// right, division per element), axis = z x d normalised ((1, 0, 0) when its
+// norm < 1e-10), angle = acos(z . d), Ceres 2.1 AngleAxisToQuaternion(angle *
+// axis); tvec = t1, height = |t1 - t2|.
+inline void GsbaBy2ToCylinder(const double* y, double q[4], double t[3], double* radius, double* height) {
+  *radius = y[6] <= 0 ? 1e-4 : y[6];
+  double d[3] = {y[3] - y[0], y[4] - y[1], y[5] - y[2]};
+  const double dn = std::sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+  for (double& v : d) v /= dn;
+  double axis[3] = {0.0 * d[2] - 1.0 * d[1], 1.0 * d[0] - 0.0 * d[2], 0.0 * d[1] - 0.0 * d[0]};
+  const double an = std::sqrt((axis[0] * axis[0] + axis[1] * axis[1]) + axis[2] * axis[2]);
+  if (std::fabs(an) < 1e-10) {
+    axis[0] = 1.0;
+    axis[1] = 0.0;
+    axis[2] = 0.0;
+  } else {
+    for (double& v : axis) v /= an;
+  }
+  const double angle = std::acos((0.0 * d[0] + 0.0 * d[1]) + 1.0 * d[2]);
+  const double aa[3] = {angle * axis[0], angle * axis[1], angle * axis[2]};
+  const double theta2 = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
+  if (theta2 > 0.0) {
+    const double theta = std::sqrt(theta2);
+    const double half = theta * 0.5;
+    const double k = std::sin(half) / theta;
+    q[0] = std::cos(half);
+    q[1] = aa[0] * k;
+    q[2] = aa[1] * k;
+    q[3] = aa[2] * k;
+  } else {
+    q[0] = 1.0;
+    q[1] = aa[0] * 0.5;
+    q[2] = aa[1] * 0.5;
+    q[3] = aa[2] * 0.5;
+  }
+  for (int m = 0; m < 3; ++m) t[m] = y[m];
+  const double e0 = y[0] - y[3], e1 = y[1] - y[4], e2 = y[2] - y[5];
+  const double h = std::sqrt((e0 * e0 + e1 * e1) + e2 * e2);
+  *height = h <= 0 ? 1e-4 : h;
+}
+
+// CylinderBy2Points(const Cylinder&) (:44-48): tvec_1 = tvec, tvec_2 =
+// GetEigUpperTvec() = PoseTransformPoint(q, t, (0, 0, height)) (cylinder.h:
+// 567-577), radius.
+inline void GsbaCylinderToBy2(const double q[4], const double t[3], double radius, double height, double y[7]) {
+  const double top[3] = {0, 0, height};
+  double u[3];
+  PoseTransformPoint(q, t, top, u);
+  for (int m = 0; m < 3; ++m) {
+    y[m] = t[m];
+    y[3 + m] = u[m];
+  }
+  y[6] = radius;
+}
+
 // GSBA residual block variants (geometric_semantic_bundle_adjustment.cc:853-909).
 enum { kGsbaFull = 0, kGsbaConstantPose = 1, kGsbaConstantCylinder = 2 };
 
@@ -213,21 +271,37 @@ enum { kGsbaFull = 0, kGsbaConstantPose = 1, kGsbaConstantCylinder = 2 };
 // height] (columns of constant blocks zero), Ceres 2.1 numeric_diff.h:
 // delta_j = max(sqrt(eps), |x_j| * relative_step_size),
 // J_j = (f(x + delta e_j) - f(x - delta e_j)) * ((1 / delta) / 2).
+//
+// by2 (CylinderBy2Points, GSBACostFunctionBy2Points and its constant-pose /
+// constant-cylinder variants, geometric_semantic_cost_functions.h:167-348):
+// yq = nullptr and yt = the 7 parameters tvec_1, tvec_2, radius; the
+// cylinder columns are then [tvec_1, tvec_2, radius, 0, 0].
 inline double GsbaEvalBlock(int variant, const double cq[4], const double ct[3], const double K[3],
                             const double yq[4], const double yt[3], double radius, double height,
                             const uint8_t* sem, int H, int W, int64_t sem_total, double rel_step, double* J16) {
+  const bool by2 = yq == nullptr;
   double x[16];
   for (int m = 0; m < 4; ++m) x[m] = cq[m];
   for (int m = 0; m < 3; ++m) x[4 + m] = ct[m];
-  for (int m = 0; m < 4; ++m) x[7 + m] = yq[m];
-  for (int m = 0; m < 3; ++m) x[11 + m] = yt[m];
-  x[14] = radius;
-  x[15] = height;
-  auto f = [&]() { return 1.0 - GsbaIoU(&x[0], &x[4], K, &x[7], &x[11], x[14], x[15], sem, H, W, sem_total); };
+  if (by2) {
+    for (int m = 0; m < 7; ++m) x[7 + m] = yt[m];
+    x[14] = x[15] = 0.0;
+  } else {
+    for (int m = 0; m < 4; ++m) x[7 + m] = yq[m];
+    for (int m = 0; m < 3; ++m) x[11 + m] = yt[m];
+    x[14] = radius;
+    x[15] = height;
+  }
+  auto f = [&]() {
+    if (!by2) return 1.0 - GsbaIoU(&x[0], &x[4], K, &x[7], &x[11], x[14], x[15], sem, H, W, sem_total);
+    double q[4], t[3], r, h;
+    GsbaBy2ToCylinder(&x[7], q, t, &r, &h);
+    return 1.0 - GsbaIoU(&x[0], &x[4], K, q, t, r, h, sem, H, W, sem_total);
+  };
   const double r = f();
   if (!J16) return r;
   const int lo = variant == kGsbaConstantPose ? 7 : 0;
-  const int hi = variant == kGsbaConstantCylinder ? 7 : 16;
+  const int hi = variant == kGsbaConstantCylinder ? 7 : (by2 ? 14 : 16);
   const double min_step = std::sqrt(std::numeric_limits<double>::epsilon());
   for (int j = 0; j < 16; ++j) {
     J16[j] = 0.0;

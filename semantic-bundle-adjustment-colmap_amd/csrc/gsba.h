@@ -35,23 +35,26 @@ struct GsbaState {
   int64_t nevals = 0;
   double rel_step = 1e-3;
   double weight = 1.0;               // ScaledLoss(1 / #config images)
+  bool by2 = false;                  // MI_BA_CYLINDER_BY_2_POINTS (CylinderBy2Points)
+  int cw = 8;                        // cylinder tangent width: 8, or 7 by 2 points
   std::vector<GsbaBlock> blocks_host;
   DevArray<GsbaBlock> blocks;
   DevArray<GsbaEval> evals;          // linearization: every evaluation
   DevArray<GsbaEval> centres;        // cost: one per block
   DevArray<uint8_t> masks;           // [slot][H][W]
   DevArray<int64_t> sem_total;       // [slot]
-  DevArray<double> cyl, cyl_c;       // [ncyl][9] q(4) t(3) radius height: current, candidate
+  DevArray<double> cyl, cyl_c;       // [ncyl][9] q(4) t(3) radius height (by 2 points: t1(3) t2(3) radius 0 0):
+                                     // current, candidate
   DevArray<double> iou;              // [nevals]
   DevArray<double> r;                // [nblocks] corrected residual
-  DevArray<double> J;                // [nblocks][14] corrected tangent rows: pose(6) cylinder(8)
-  DevArray<double> cyl_blk;          // [ncyl][36] cylinder Schur-Jacobi blocks (packed upper)
+  DevArray<double> J;                // [nblocks][14] corrected tangent rows: pose(6) cylinder(cw)
+  DevArray<double> cyl_blk;          // [ncyl][cw (cw + 1) / 2] cylinder Schur-Jacobi blocks (packed upper)
   DevArray<double> prec_cyl;         // [ncyl][64]
   DevArray<double> partial;          // per-block cost
 };
 
 // Number of cylinder parameter slots the context must reserve (8 per
-// cylinder when they are refined).
+// cylinder when they are refined, 7 by 2 points).
 int gsba_cylinder_slots(const mi_ba_options& o, const mi_ba_problem* p, const mi_ba_gsba* g);
 // Validates (GeometricSemanticBundleAdjuster::Assert), builds blocks, uploads
 // masks and cylinders, marks GSBA poses variable.  Called at the end of

@@ -123,6 +123,78 @@ __device__ inline void angle_axis_rotate(const double aa[3], const double pt[3],
   }
 }
 
+// CylinderBy2Points (src/util/cylinder_by_2_points.h:26-155).  The
+// parameters y = tvec_1(3) tvec_2(3) radius; ToCylinder (:95-117) gives the
+// evaluated Cylinder (qvec, tvec_1, radius, |tvec_1 - tvec_2|): the axis
+// direction d = (t2 - t1) / |t2 - t1|, rotation z -> d as the angle-axis
+// acos(z . d) * (z x d) / |z x d| ((1, 0, 0) when |z x d| < 1e-10) through
+// Ceres 2.1 AngleAxisToQuaternion.  Eigen's fixed-size-3 norms and dot
+// products sum left to right; the constructor's Check clamps a radius <= 0 to
+// 1e-4 (and Cylinder's a height <= 0).  out = q(4) t(3) r h.
+MI_HD void by2_to_cylinder(const double* y, double out[9]) {
+  const double radius = y[6] <= 0 ? 1e-4 : y[6];
+  double d[3] = {y[3] - y[0], y[4] - y[1], y[5] - y[2]};
+  const double dn = sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+  d[0] /= dn;
+  d[1] /= dn;
+  d[2] /= dn;
+  double axis[3] = {0.0 * d[2] - 1.0 * d[1], 1.0 * d[0] - 0.0 * d[2], 0.0 * d[1] - 0.0 * d[0]};
+  const double an = sqrt((axis[0] * axis[0] + axis[1] * axis[1]) + axis[2] * axis[2]);
+  if (fabs(an) < 1e-10) {
+    axis[0] = 1.0;
+    axis[1] = 0.0;
+    axis[2] = 0.0;
+  } else {
+    axis[0] /= an;
+    axis[1] /= an;
+    axis[2] /= an;
+  }
+  const double angle = acos((0.0 * d[0] + 0.0 * d[1]) + 1.0 * d[2]);
+  const double aa[3] = {angle * axis[0], angle * axis[1], angle * axis[2]};
+  // Ceres 2.1 AngleAxisToQuaternion
+  const double theta2 = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
+  if (theta2 > 0.0) {
+    const double theta = sqrt(theta2);
+    const double half = theta * 0.5;
+    const double k = sin(half) / theta;
+    out[0] = cos(half);
+    out[1] = aa[0] * k;
+    out[2] = aa[1] * k;
+    out[3] = aa[2] * k;
+  } else {
+    out[0] = 1.0;
+    out[1] = aa[0] * 0.5;
+    out[2] = aa[1] * 0.5;
+    out[3] = aa[2] * 0.5;
+  }
+  out[4] = y[0];
+  out[5] = y[1];
+  out[6] = y[2];
+  const double e0 = y[0] - y[3], e1 = y[1] - y[4], e2 = y[2] - y[5];
+  const double height = sqrt((e0 * e0 + e1 * e1) + e2 * e2);
+  out[7] = radius;
+  out[8] = height <= 0 ? 1e-4 : height;
+}
+
+// CylinderBy2Points(const Cylinder&) (cylinder_by_2_points.h:44-48): tvec_1 =
+// the lower circle centre, tvec_2 = GetEigUpperTvec() (PoseTransformPoint of
+// (0, 0, height), cylinder.h:567-577), the radius; y = t1(3) t2(3) r, 0, 0.
+inline void cylinder_to_by2(const mi_ba_cylinder& c, double y[9]) {
+  const double* q = c.qvec;
+  const double scale = 1.0 / sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const double u[4] = {scale * q[0], scale * q[1], scale * q[2], scale * q[3]};
+  const double top[3] = {0, 0, c.height};
+  double r[3];
+  unit_quat_rotate(u, top, r);
+  for (int m = 0; m < 3; ++m) {
+    y[m] = c.tvec[m];
+    y[3 + m] = r[m] + c.tvec[m];
+  }
+  y[6] = c.radius;
+  y[7] = 0.0;
+  y[8] = 0.0;
+}
+
 // ProjectToQuadrilateral + GetEdgePoints; false where the reference throws
 // (ComputeSemanticIoU then returns 0).
 __device__ inline bool project_quad(const double* x, const double K[3], double p[4][2]) {
@@ -181,9 +253,11 @@ struct GsbaArgs {
   const int64_t* sem_total;
   int H, W;
   double rel_step;
+  int by2;                 // MI_BA_CYLINDER_BY_2_POINTS: cyl rows are t1(3) t2(3) r, 0, 0
 };
 
-// Ambient parameter vector of a block: camera q(4) t(3), cylinder q(4) t(3), r, h.
+// Ambient parameter vector of a block: camera q(4) t(3), then the cylinder's
+// 9 stored values — q(4) t(3) r h, or by_2_points t1(3) t2(3) r (+ 2 unused).
 __device__ inline void load_params(const GsbaArgs& a, const GsbaBlock& b, double x[16]) {
   const double* qt = a.qt + 8 * (size_t)b.img;
 #pragma unroll
@@ -213,6 +287,12 @@ __global__ __launch_bounds__(kTB) void gsba_iou_kernel(GsbaArgs a, const GsbaEva
   }
   const double* kc = a.cam + 8 * (size_t)a.img_cam[b.img];
   const double K[3] = {kc[0], kc[1], kc[2]};
+  if (a.by2) {
+    double cyl[9];
+    by2_to_cylinder(x + 7, cyl);
+#pragma unroll
+    for (int m = 0; m < 9; ++m) x[7 + m] = cyl[m];
+  }
   double p[4][2];
   const bool ok = project_quad(x, K, p);
   const int H = a.H, W = a.W;
@@ -335,7 +415,7 @@ __global__ void gsba_block_kernel(GsbaArgs a, int nblocks, const uint32_t* __res
   const double* f = iou + b.eval0;
   double r = 1.0 - f[0];
   const int lo = b.variant == kGsbaConstantPose ? 7 : 0;
-  const int hi = b.variant == kGsbaConstantCylinder ? 7 : 16;
+  const int hi = b.variant == kGsbaConstantCylinder ? 7 : (a.by2 ? 14 : 16);
   double J16[16];
   int e = 1;
   for (int j = 0; j < 16; ++j) {
@@ -362,13 +442,19 @@ __global__ void gsba_block_kernel(GsbaArgs a, int nblocks, const uint32_t* __res
   }
   const uint32_t flags = img_flags[b.img];
   for (int col = 0; col < 3; ++col) Jt[3 + col] = ((flags >> (1 + col)) & 1u) ? 0.0 : J16[4 + col];
-  quat_plus_jac(x + 7, PJ);
-  for (int col = 0; col < 3; ++col) {
-    double acc = 0.0;
-    for (int m = 0; m < 4; ++m) acc += J16[7 + m] * PJ[m * 3 + col];
-    Jt[6 + col] = acc;
+  if (a.by2) {
+    // by_2_points: Euclidean t1, t2, radius (no manifold); column 13 unused
+    for (int col = 0; col < 7; ++col) Jt[6 + col] = J16[7 + col];
+    Jt[13] = 0.0;
+  } else {
+    quat_plus_jac(x + 7, PJ);
+    for (int col = 0; col < 3; ++col) {
+      double acc = 0.0;
+      for (int m = 0; m < 4; ++m) acc += J16[7 + m] * PJ[m * 3 + col];
+      Jt[6 + col] = acc;
+    }
+    for (int col = 0; col < 5; ++col) Jt[9 + col] = J16[11 + col];
   }
-  for (int col = 0; col < 5; ++col) Jt[9 + col] = J16[11 + col];
   // ScaledLoss corrector: rho = (w s, w, 0)
   cost[k] = 0.5 * (weight * (r * r));
   const double sqrt_rho1 = sqrt(weight);
@@ -385,18 +471,21 @@ __global__ void gsba_cost_kernel(const GsbaBlock* __restrict__ blocks, int nbloc
   cost[k] = 0.5 * (weight * (r * r));
 }
 
-// Slots of a block's tangent columns: pose 6 (or -1), cylinder 8 (or -1).
-__device__ inline int64_t gsba_slot(const GsbaBlock& b, int m, int64_t cyl0, int cyl_var, uint32_t pose_var) {
+// Slots of a block's tangent columns: pose 6 (or -1), cylinder cw (or -1):
+// cw = 8 (q 3, t 3, radius, height) or 7 (by_2_points: t1 3, t2 3, radius).
+__device__ inline int64_t gsba_slot(const GsbaBlock& b, int m, int64_t cyl0, int cyl_var, uint32_t pose_var,
+                                    int cw) {
   if (m < 6) return (b.variant != kGsbaConstantPose && pose_var) ? 6 * (int64_t)b.img + m : -1;
-  return (b.variant != kGsbaConstantCylinder && cyl_var) ? cyl0 + 8 * (int64_t)b.cyl + (m - 6) : -1;
+  return (b.variant != kGsbaConstantCylinder && cyl_var && m - 6 < cw) ? cyl0 + cw * (int64_t)b.cyl + (m - 6) : -1;
 }
 
 __device__ inline int sym6(int a, int c) { return a * 6 - (a * (a - 1)) / 2 + (c - a); }   // a <= c < 6
-__device__ inline int sym8(int a, int c) { return a * 8 - (a * (a - 1)) / 2 + (c - a); }   // a <= c < 8
+// packed upper index of (a, c), a <= c < n
+__device__ inline int symn(int n, int a, int c) { return a * n - (a * (a - 1)) / 2 + (c - a); }
 
 __global__ void gsba_fblock_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
                                    const uint32_t* __restrict__ img_flags, const double* __restrict__ r,
-                                   const double* __restrict__ J, int64_t cyl0, int cyl_var,
+                                   const double* __restrict__ J, int64_t cyl0, int cyl_var, int cw,
                                    double* __restrict__ pose_blk, double* __restrict__ cyl_blk,
                                    double* __restrict__ bvec, double* __restrict__ udiag) {
   const int k = blockIdx.x * 64 + threadIdx.x;
@@ -405,17 +494,18 @@ __global__ void gsba_fblock_kernel(const GsbaBlock* __restrict__ blocks, int nbl
   const double* Jr = J + 14 * (size_t)k;
   const double rr = r[k];
   const uint32_t pv = img_flags[b.img] & 1u;
-  if (gsba_slot(b, 0, cyl0, cyl_var, pv) >= 0) {
+  if (gsba_slot(b, 0, cyl0, cyl_var, pv, cw) >= 0) {
     for (int a = 0; a < 6; ++a) {
       for (int c = a; c < 6; ++c) atomicAdd(pose_blk + 21 * (size_t)b.img + sym6(a, c), Jr[a] * Jr[c]);
       atomicAdd(bvec + 6 * (size_t)b.img + a, Jr[a] * rr);
       atomicAdd(udiag + 6 * (size_t)b.img + a, Jr[a] * Jr[a]);
     }
   }
-  if (gsba_slot(b, 6, cyl0, cyl_var, pv) >= 0) {
-    const int64_t o = cyl0 + 8 * (int64_t)b.cyl;
-    for (int a = 0; a < 8; ++a) {
-      for (int c = a; c < 8; ++c) atomicAdd(cyl_blk + 36 * (size_t)b.cyl + sym8(a, c), Jr[6 + a] * Jr[6 + c]);
+  if (gsba_slot(b, 6, cyl0, cyl_var, pv, cw) >= 0) {
+    const int64_t o = cyl0 + cw * (int64_t)b.cyl;
+    const int ps = cw * (cw + 1) / 2;
+    for (int a = 0; a < cw; ++a) {
+      for (int c = a; c < cw; ++c) atomicAdd(cyl_blk + ps * (size_t)b.cyl + symn(cw, a, c), Jr[6 + a] * Jr[6 + c]);
       atomicAdd(bvec + o + a, Jr[6 + a] * rr);
       atomicAdd(udiag + o + a, Jr[6 + a] * Jr[6 + a]);
     }
@@ -425,7 +515,8 @@ __global__ void gsba_fblock_kernel(const GsbaBlock* __restrict__ blocks, int nbl
 // y += J'(J x) over the block's slots.
 __global__ void gsba_product_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
                                     const uint32_t* __restrict__ img_flags, const double* __restrict__ J,
-                                    int64_t cyl0, int cyl_var, const double* __restrict__ x, double* __restrict__ y) {
+                                    int64_t cyl0, int cyl_var, int cw, const double* __restrict__ x,
+                                    double* __restrict__ y) {
   const int k = blockIdx.x * 64 + threadIdx.x;
   if (k >= nblocks) return;
   const GsbaBlock b = blocks[k];
@@ -433,11 +524,11 @@ __global__ void gsba_product_kernel(const GsbaBlock* __restrict__ blocks, int nb
   const uint32_t pv = img_flags[b.img] & 1u;
   double e = 0.0;
   for (int m = 0; m < 14; ++m) {
-    const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv);
+    const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv, cw);
     if (s >= 0) e += Jr[m] * x[s];
   }
   for (int m = 0; m < 14; ++m) {
-    const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv);
+    const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv, cw);
     if (s >= 0) atomicAdd(y + s, Jr[m] * e);
   }
 }
@@ -445,14 +536,14 @@ __global__ void gsba_product_kernel(const GsbaBlock* __restrict__ blocks, int nb
 // S += J'J (upper triangle, row-major nf x nf).
 __global__ void gsba_dense_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
                                   const uint32_t* __restrict__ img_flags, const double* __restrict__ J, int64_t cyl0,
-                                  int cyl_var, int64_t nf, double* __restrict__ S) {
+                                  int cyl_var, int cw, int64_t nf, double* __restrict__ S) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)nblocks * 196) return;
   const int k = (int)(t / 196), e = (int)(t % 196);
   const int a = e / 14, c = e % 14;
   const GsbaBlock b = blocks[k];
   const uint32_t pv = img_flags[b.img] & 1u;
-  const int64_t ra = gsba_slot(b, a, cyl0, cyl_var, pv), rc = gsba_slot(b, c, cyl0, cyl_var, pv);
+  const int64_t ra = gsba_slot(b, a, cyl0, cyl_var, pv, cw), rc = gsba_slot(b, c, cyl0, cyl_var, pv, cw);
   if (ra < 0 || rc < 0 || ra > rc) return;
   const double* Jr = J + 14 * (size_t)k;
   atomicAdd(S + ra * nf + rc, Jr[a] * Jr[c]);
@@ -461,7 +552,7 @@ __global__ void gsba_dense_kernel(const GsbaBlock* __restrict__ blocks, int nblo
 // model cost change contribution -(e (r + e / 2)), e = J df
 __global__ void gsba_model_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
                                   const uint32_t* __restrict__ img_flags, const double* __restrict__ r,
-                                  const double* __restrict__ J, int64_t cyl0, int cyl_var,
+                                  const double* __restrict__ J, int64_t cyl0, int cyl_var, int cw,
                                   const double* __restrict__ df, double* __restrict__ out) {
   const int k = blockIdx.x * 64 + threadIdx.x;
   double v = 0.0;
@@ -471,7 +562,7 @@ __global__ void gsba_model_kernel(const GsbaBlock* __restrict__ blocks, int nblo
     const uint32_t pv = img_flags[b.img] & 1u;
     double e = 0.0;
     for (int m = 0; m < 14; ++m) {
-      const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv);
+      const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv, cw);
       if (s >= 0) e += Jr[m] * df[s];
     }
     v = -(e * (r[k] + e / 2.0));
@@ -501,6 +592,22 @@ __global__ void gsba_plus_kernel(int ncyl, const double* __restrict__ cyl, const
   o[8] = y[8] + d[7];
 }
 
+// by_2_points: Euclidean t1, t2; the radius projected onto its lower bound 0
+// (SetUpCylinderManifolds, :1185-1213; ParameterBlock::Plus).
+__global__ void gsba_plus_by2_kernel(int ncyl, const double* __restrict__ cyl, const double* __restrict__ df,
+                                     double* __restrict__ out) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= ncyl) return;
+  const double* y = cyl + 9 * (size_t)k;
+  const double* d = df + 7 * (size_t)k;
+  double* o = out + 9 * (size_t)k;
+#pragma unroll
+  for (int m = 0; m < 6; ++m) o[m] = y[m] + d[m];
+  o[6] = fmax(y[6] + d[6], 0.0);
+  o[7] = 0.0;
+  o[8] = 0.0;
+}
+
 GsbaArgs make_args(mi_ba_context* ctx, const double* qt, const double* cyl) {
   GsbaState* G = ctx->gsba;
   GsbaArgs a;
@@ -514,6 +621,7 @@ GsbaArgs make_args(mi_ba_context* ctx, const double* qt, const double* cyl) {
   a.H = G->H;
   a.W = G->W;
   a.rel_step = G->rel_step;
+  a.by2 = G->by2 ? 1 : 0;
   return a;
 }
 
@@ -526,14 +634,17 @@ int gsba_cylinder_slots(const mi_ba_options& o, const mi_ba_problem* p, const mi
   if (!g || !g->refine_geometry || g->num_cylinders <= 0) return 0;
   int ncfg = 0;
   for (int i = 0; i < p->num_images; ++i) ncfg += p->image_in_config ? (p->image_in_config[i] != 0) : 1;
-  return ncfg > 0 ? 8 * g->num_cylinders : 0;
+  const int cw = g->cylinder_parametrization == MI_BA_CYLINDER_BY_2_POINTS ? 7 : 8;
+  return ncfg > 0 ? cw * g->num_cylinders : 0;
 }
 
 mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
   const mi_ba_problem* p = &ctx->problem;
   const mi_ba_options& o = ctx->options;
   if (g->height <= 0 || g->width <= 0 || !g->trunk_mask || g->num_cylinders < 0 ||
-      (g->num_cylinders > 0 && !g->cylinders) || !(g->numeric_relative_step_size > 0))
+      (g->num_cylinders > 0 && !g->cylinders) || !(g->numeric_relative_step_size > 0) ||
+      (g->cylinder_parametrization != MI_BA_CYLINDER_DEFAULT &&
+       g->cylinder_parametrization != MI_BA_CYLINDER_BY_2_POINTS))
     return MI_BA_ERR_INVALID_ARGUMENT;
   HostSetup& s = ctx->setup;
   const int I = p->num_images;
@@ -555,6 +666,8 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
   G->ncyl = g->num_cylinders;
   G->rel_step = g->numeric_relative_step_size;
   G->weight = ncfg > 0 ? 1. / (double)ncfg : 1.0;
+  G->by2 = g->cylinder_parametrization == MI_BA_CYLINDER_BY_2_POINTS;
+  G->cw = G->by2 ? 7 : 8;
   // blocks (AddImageToProblem, :835-909): config images in problem order
   std::vector<int32_t> slot(I, -1);
   std::vector<int> slot_images;
@@ -578,7 +691,7 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
       evals.push_back(GsbaEval{kb, -1, 1});
       centres.push_back(GsbaEval{kb, -1, 1});
       const int lo = b.variant == kGsbaConstantPose ? 7 : 0;
-      const int hi = b.variant == kGsbaConstantCylinder ? 7 : 16;
+      const int hi = b.variant == kGsbaConstantCylinder ? 7 : (G->by2 ? 14 : 16);
       for (int j = lo; j < hi; ++j) {
         evals.push_back(GsbaEval{kb, (int16_t)j, 1});
         evals.push_back(GsbaEval{kb, (int16_t)j, -1});
@@ -597,7 +710,7 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
   }
   G->nblocks = (int)G->blocks_host.size();
   G->nevals = (int64_t)evals.size();
-  if (ctx->dev.cyl_var) s.num_effective_parameters_reduced += 8 * (int64_t)G->ncyl;
+  if (ctx->dev.cyl_var) s.num_effective_parameters_reduced += G->cw * (int64_t)G->ncyl;
   const size_t plane = (size_t)G->H * G->W;
   std::vector<int64_t> totals(slot_images.size(), 0);
   for (size_t k = 0; k < slot_images.size(); ++k) {
@@ -609,6 +722,10 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
   std::vector<double> cyl(9 * (size_t)std::max(1, G->ncyl), 0.0);
   for (int c = 0; c < G->ncyl; ++c) {
     const mi_ba_cylinder& y = g->cylinders[c];
+    if (G->by2) {
+      cylinder_to_by2(y, &cyl[9 * c]);
+      continue;
+    }
     for (int m = 0; m < 4; ++m) cyl[9 * c + m] = y.qvec[m];
     for (int m = 0; m < 3; ++m) cyl[9 * c + 4 + m] = y.tvec[m];
     cyl[9 * c + 7] = y.radius;
@@ -683,31 +800,31 @@ void gsba_add_fblock(mi_ba_context* ctx) {
   (void)hipMemsetAsync(G->cyl_blk.ptr, 0, G->cyl_blk.bytes(), s);
   if (!G->nblocks) return;
   hipLaunchKernelGGL(gsba_fblock_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, s, G->blocks.ptr, G->nblocks,
-                     ctx->dev.img_flags, G->r.ptr, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, ctx->pose_blk.ptr,
-                     G->cyl_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr);
+                     ctx->dev.img_flags, G->r.ptr, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw,
+                     ctx->pose_blk.ptr, G->cyl_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr);
 }
 
 void gsba_finalize(mi_ba_context* ctx, int first, int reuse_diag, double radius) {
   GsbaState* G = ctx->gsba;
   if (!ctx->dev.cyl_var || G->ncyl == 0) return;
   const int64_t o = ctx->dev.cyl0;
-  launch_finalize8(G->ncyl, G->cyl_blk.ptr, ctx->udiag.ptr + o, ctx->scale_f.ptr + o, ctx->diag_f.ptr + o,
-                   ctx->lambda_f.ptr + o, G->prec_cyl.ptr, ctx->bvec.ptr + o, 1, first, reuse_diag, radius,
-                   ctx->stream);
+  launch_finalize_n(G->cw, G->ncyl, G->cyl_blk.ptr, ctx->udiag.ptr + o, ctx->scale_f.ptr + o, ctx->diag_f.ptr + o,
+                    ctx->lambda_f.ptr + o, G->prec_cyl.ptr, ctx->bvec.ptr + o, 1, first, reuse_diag, radius,
+                    ctx->stream);
 }
 
 void gsba_schur_product(mi_ba_context* ctx, const double* x, double* y) {
   GsbaState* G = ctx->gsba;
   if (!G->nblocks) return;
   hipLaunchKernelGGL(gsba_product_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, ctx->stream, G->blocks.ptr,
-                     G->nblocks, ctx->dev.img_flags, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, x, y);
+                     G->nblocks, ctx->dev.img_flags, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw, x, y);
 }
 
 void gsba_precond(mi_ba_context* ctx, const double* r, double* z) {
   GsbaState* G = ctx->gsba;
   if (!ctx->dev.cyl_var || G->ncyl == 0) return;
   const int64_t o = ctx->dev.cyl0;
-  launch_precond8(G->ncyl, G->prec_cyl.ptr, r + o, z + o, ctx->stream);
+  launch_precond_n(G->cw, G->ncyl, G->prec_cyl.ptr, r + o, z + o, ctx->stream);
 }
 
 void gsba_add_dense(mi_ba_context* ctx, double* S) {
@@ -715,14 +832,15 @@ void gsba_add_dense(mi_ba_context* ctx, double* S) {
   if (!G->nblocks) return;
   const int64_t n = (int64_t)G->nblocks * 196;
   hipLaunchKernelGGL(gsba_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, G->blocks.ptr,
-                     G->nblocks, ctx->dev.img_flags, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, ctx->dev.nf, S);
+                     G->nblocks, ctx->dev.img_flags, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw, ctx->dev.nf, S);
 }
 
 void gsba_model_cost(mi_ba_context* ctx, const double* df, double* d_out) {
   GsbaState* G = ctx->gsba;
   if (!G->nblocks) return;
   hipLaunchKernelGGL(gsba_model_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, ctx->stream, G->blocks.ptr,
-                     G->nblocks, ctx->dev.img_flags, G->r.ptr, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, df, d_out);
+                     G->nblocks, ctx->dev.img_flags, G->r.ptr, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw, df,
+                     d_out);
 }
 
 void gsba_plus(mi_ba_context* ctx, const double* df) {
@@ -732,8 +850,12 @@ void gsba_plus(mi_ba_context* ctx, const double* df) {
     (void)hipMemcpyAsync(G->cyl_c.ptr, G->cyl.ptr, G->cyl.bytes(), hipMemcpyDeviceToDevice, ctx->stream);
     return;
   }
-  hipLaunchKernelGGL(gsba_plus_kernel, dim3(grid64(G->ncyl)), dim3(64), 0, ctx->stream, G->ncyl, G->cyl.ptr,
-                     df + ctx->dev.cyl0, G->cyl_c.ptr);
+  if (G->by2)
+    hipLaunchKernelGGL(gsba_plus_by2_kernel, dim3(grid64(G->ncyl)), dim3(64), 0, ctx->stream, G->ncyl, G->cyl.ptr,
+                       df + ctx->dev.cyl0, G->cyl_c.ptr);
+  else
+    hipLaunchKernelGGL(gsba_plus_kernel, dim3(grid64(G->ncyl)), dim3(64), 0, ctx->stream, G->ncyl, G->cyl.ptr,
+                       df + ctx->dev.cyl0, G->cyl_c.ptr);
 }
 
 void gsba_accept(mi_ba_context* ctx) {
@@ -751,6 +873,16 @@ mi_ba_status gsba_writeback(mi_ba_context* ctx) {
   if (!ctx->dev.cyl_var) return MI_BA_OK;
   for (int c = 0; c < G->ncyl; ++c) {
     mi_ba_cylinder& y = G->host->cylinders[c];
+    if (G->by2) {
+      // exportCylindersToText writes ToCylinder() (cylinder_by_2_points.h:134-143)
+      double e[9];
+      by2_to_cylinder(&cyl[9 * c], e);
+      for (int m = 0; m < 4; ++m) y.qvec[m] = e[m];
+      for (int m = 0; m < 3; ++m) y.tvec[m] = e[4 + m];
+      y.radius = e[7];
+      y.height = e[8];
+      continue;
+    }
     for (int m = 0; m < 4; ++m) y.qvec[m] = cyl[9 * c + m];
     for (int m = 0; m < 3; ++m) y.tvec[m] = cyl[9 * c + 4 + m];
     y.radius = cyl[9 * c + 7];

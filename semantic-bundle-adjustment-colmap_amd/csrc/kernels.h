@@ -68,13 +68,14 @@ void launch_precond(const DevProblem& p, const double* prec_pose, const double* 
                     const double* r, double* z, hipStream_t s);
 
 // Vector ops on the f-vector.
-// n 8x8 parameter blocks (GSBA cylinders): Jacobi scaling, LM damping,
+// n 8xNxN parameter blocks (GSBA cylinders): Jacobi scaling, LM damping,
 // Schur-Jacobi preconditioner blocks, rhs sign (as the pose / camera blocks);
 // pointers offset to the first block's f-vector slots.
-void launch_finalize8(int n, const double* blk, const double* udiag, double* scale_f, double* diag_f,
-                      double* lambda_f, double* prec, double* b, int var, int first, int reuse_diag, double radius,
-                      hipStream_t s);
-void launch_precond8(int n, const double* prec, const double* r, double* z, hipStream_t s);
+// width 8 (Cylinder: q 3, t 3, radius, height) or 7 (CylinderBy2Points).
+void launch_finalize_n(int width, int n, const double* blk, const double* udiag, double* scale_f, double* diag_f,
+                       double* lambda_f, double* prec, double* b, int var, int first, int reuse_diag, double radius,
+                       hipStream_t s);
+void launch_precond_n(int width, int n, const double* prec, const double* r, double* z, hipStream_t s);
 void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t s);
 void launch_axpy(double* y, const double* x, const double* alpha_num, const double* alpha_den,
                  double sign, int64_t n, hipStream_t s);

@@ -1016,34 +1016,36 @@ __global__ __launch_bounds__(64) void fblock_finalize_kernel(DevProblem p, const
   }
 }
 
-// n generic 8x8 blocks (GSBA cylinders): blk [n][36] packed upper, f-vector
-// arrays already offset to the first block's slots.
-__global__ __launch_bounds__(64) void finalize8_kernel(int n, const double* __restrict__ blk,
-                                                       const double* __restrict__ udiag, double* __restrict__ scale_f,
-                                                       double* __restrict__ diag_f, double* __restrict__ lambda_f,
-                                                       double* __restrict__ prec, double* __restrict__ b, int var,
-                                                       int first, int reuse_diag, double radius) {
+// n generic NxN blocks (GSBA cylinders, N = 8 or 7): blk [n][N (N + 1) / 2]
+// packed upper, f-vector arrays already offset to the first block's slots.
+template <int N>
+__global__ __launch_bounds__(64) void finalize_n_kernel(int n, const double* __restrict__ blk,
+                                                        const double* __restrict__ udiag, double* __restrict__ scale_f,
+                                                        double* __restrict__ diag_f, double* __restrict__ lambda_f,
+                                                        double* __restrict__ prec, double* __restrict__ b, int var,
+                                                        int first, int reuse_diag, double radius) {
   const int k = blockIdx.x * 64 + threadIdx.x;
   if (k >= n) return;
-  const size_t o = 8 * (size_t)k;
-  finalize_block<8>(blk + 36 * (size_t)k, udiag + o, scale_f + o, diag_f + o, lambda_f + o, prec + 64 * (size_t)k,
-                    b + o, var != 0, first, reuse_diag, radius);
+  const size_t o = N * (size_t)k;
+  finalize_block<N>(blk + (N * (N + 1) / 2) * (size_t)k, udiag + o, scale_f + o, diag_f + o, lambda_f + o,
+                    prec + N * N * (size_t)k, b + o, var != 0, first, reuse_diag, radius);
 }
 
-__global__ __launch_bounds__(64) void precond8_kernel(int n, const double* __restrict__ prec,
-                                                      const double* __restrict__ r, double* __restrict__ z) {
+template <int N>
+__global__ __launch_bounds__(64) void precond_n_kernel(int n, const double* __restrict__ prec,
+                                                       const double* __restrict__ r, double* __restrict__ z) {
   const int k = blockIdx.x * 64 + threadIdx.x;
   if (k >= n) return;
-  const double* M = prec + 64 * (size_t)k;
-  double rr[8];
+  const double* M = prec + N * N * (size_t)k;
+  double rr[N];
 #pragma unroll
-  for (int m = 0; m < 8; ++m) rr[m] = r[8 * (size_t)k + m];
+  for (int m = 0; m < N; ++m) rr[m] = r[N * (size_t)k + m];
 #pragma unroll
-  for (int a = 0; a < 8; ++a) {
+  for (int a = 0; a < N; ++a) {
     double s = 0.0;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) s += M[a * 8 + c] * rr[c];
-    z[8 * (size_t)k + a] = s;
+    for (int c = 0; c < N; ++c) s += M[a * N + c] * rr[c];
+    z[N * (size_t)k + a] = s;
   }
 }
 
@@ -1985,17 +1987,24 @@ void launch_precond(const DevProblem& p, const double* prec_pose, const double* 
   });
 }
 
-void launch_finalize8(int n, const double* blk, const double* udiag, double* scale_f, double* diag_f,
-                      double* lambda_f, double* prec, double* b, int var, int first, int reuse_diag, double radius,
-                      hipStream_t s) {
+void launch_finalize_n(int width, int n, const double* blk, const double* udiag, double* scale_f, double* diag_f,
+                       double* lambda_f, double* prec, double* b, int var, int first, int reuse_diag, double radius,
+                       hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(finalize8_kernel, dim3(grid_for(n, 64)), dim3(64), 0, s, n, blk, udiag, scale_f, diag_f,
-                     lambda_f, prec, b, var, first, reuse_diag, radius);
+  if (width == 7)
+    hipLaunchKernelGGL(finalize_n_kernel<7>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, blk, udiag, scale_f, diag_f,
+                       lambda_f, prec, b, var, first, reuse_diag, radius);
+  else
+    hipLaunchKernelGGL(finalize_n_kernel<8>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, blk, udiag, scale_f, diag_f,
+                       lambda_f, prec, b, var, first, reuse_diag, radius);
 }
 
-void launch_precond8(int n, const double* prec, const double* r, double* z, hipStream_t s) {
+void launch_precond_n(int width, int n, const double* prec, const double* r, double* z, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(precond8_kernel, dim3(grid_for(n, 64)), dim3(64), 0, s, n, prec, r, z);
+  if (width == 7)
+    hipLaunchKernelGGL(precond_n_kernel<7>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, prec, r, z);
+  else
+    hipLaunchKernelGGL(precond_n_kernel<8>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, prec, r, z);
 }
 
 void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t s) {

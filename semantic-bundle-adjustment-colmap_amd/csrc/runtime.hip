@@ -1210,6 +1210,7 @@ void mi_ba_default_gsba(mi_ba_gsba* g) {
   g->numeric_relative_step_size = 1e-3;
   g->include_landmark_error = 0;
   g->landmark_error_weight = 1.0;
+  g->cylinder_parametrization = MI_BA_CYLINDER_DEFAULT;
 }
 
 // The GSBA problem (geometric_semantic_bundle_adjustment.cc:714-800): TRIVIAL

@@ -26,6 +26,7 @@ LOSS_TRIVIAL, LOSS_SOFT_L1, LOSS_CAUCHY = range(3)
 SOLVER_AUTO, SOLVER_DENSE_SCHUR, SOLVER_ITERATIVE_SCHUR = range(3)
 CONVERGENCE, NO_CONVERGENCE, FAILURE, USER_SUCCESS, USER_FAILURE = range(5)
 SOLVER_CONTINUE, SOLVER_ABORT, SOLVER_TERMINATE_SUCCESSFULLY = range(3)
+CYLINDER_DEFAULT, CYLINDER_BY_2_POINTS = range(2)
 OUT_OF_BOUNDS, INVALID_DEPTH, VALID = -1, -2, 10
 NUM_PARAMS = {SIMPLE_PINHOLE: 3, PINHOLE: 4, SIMPLE_RADIAL: 4, RADIAL: 5, OPENCV: 8}
 MODEL_NAMES = {"SIMPLE_PINHOLE": 0, "PINHOLE": 1, "SIMPLE_RADIAL": 2, "RADIAL": 3, "OPENCV": 4}
@@ -151,6 +152,7 @@ class Gsba(C.Structure):
         ("numeric_relative_step_size", C.c_double),
         ("include_landmark_error", C.c_int32),
         ("landmark_error_weight", C.c_double),
+        ("cylinder_parametrization", C.c_int32),
     ]
 
 
@@ -493,10 +495,11 @@ class GsbaInput:
     numeric_relative_step_size: float = 1e-3
     include_landmark_error: int = 0
     landmark_error_weight: float = 1.0
+    cylinder_parametrization: int = CYLINDER_DEFAULT
 
     def copy(self) -> "GsbaInput":
         return GsbaInput(self.masks, self.cylinders.copy(), self.refine_geometry, self.numeric_relative_step_size,
-                         self.include_landmark_error, self.landmark_error_weight)
+                         self.include_landmark_error, self.landmark_error_weight, self.cylinder_parametrization)
 
     def struct(self):
         self.masks = np.ascontiguousarray(self.masks, np.uint8)
@@ -517,6 +520,7 @@ class GsbaInput:
         g.numeric_relative_step_size = self.numeric_relative_step_size
         g.include_landmark_error = self.include_landmark_error
         g.landmark_error_weight = self.landmark_error_weight
+        g.cylinder_parametrization = self.cylinder_parametrization
         return g, arr
 
     def read_back(self, arr):

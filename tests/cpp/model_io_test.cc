@@ -10,7 +10,7 @@
 //       controllers/bundle_adjustment.cc:69-101): read, every registered image
 //       in the config, pose of the first constant, tvec x of the second
 //       constant, Solve on the GPU, write binary
-//   model_io_test gsba <model dir> <data dir> <cylinders in> <cylinders out> [iters]
+//   model_io_test gsba <model dir> <data dir> <cylinders in> <cylinders out> [iters] [parametrization]
 //       GeometricSemanticBundleAdjuster: every registered image, first pose
 //       constant, cameras constant, maps from <data dir>, cylinders file I/O
 #include <cstdio>
@@ -140,6 +140,7 @@ int main(int argc, char** argv) {
       o.data_path = argv[3];
       o.input_geometry = argv[4];
       if (argc >= 7) o.solver_options.max_num_iterations = std::atoi(argv[6]);
+      if (argc >= 8) o.cylinder_parametrization = argv[7];
       GeometricSemanticBundleAdjuster gsba(o, cfg);
       if (!gsba.Solve(&r)) return 4;
       WriteCylindersText(argv[5], gsba.Cylinders());

@@ -1,7 +1,9 @@
 """Geometric-semantic BA (GSBA): cylinder IoU residuals.
 
-Reference: GeometricSemanticBundleAdjuster<Cylinder>
-(src/optim/geometric_semantic_bundle_adjustment.cc:481-909,1160-1232),
+Reference: GeometricSemanticBundleAdjuster<Cylinder> and
+<CylinderBy2Points> (src/optim/geometric_semantic_bundle_adjustment.cc:
+481-1010,1160-1232; src/util/cylinder_by_2_points.h:26-155; functors
+geometric_semantic_cost_functions.h:167-348),
 Cylinder::ComputeSemanticIoU (src/util/cylinder.h:270-540), drawQuadrilateral
 (:21-117), the GSBA cost functions (src/base/geometric_semantic_cost_functions.h:
 33-165).  The reference has no GSBA tests or data: parity unpinned beyond
@@ -26,7 +28,10 @@ import oracle
 H, W = 240, 320
 
 
-def workload(seed=0, images=10, cylinders=5, points=0, shift=0.08):
+BY2 = mi_ba.CYLINDER_BY_2_POINTS
+
+
+def workload(seed=0, images=10, cylinders=5, points=0, shift=0.08, tilt=0.0):
     sc, cyl = mi_ba.gsba_scene(images, cylinders, H, W, seed=seed, points=points)
     masks = oracle.gsba_render(sc, cyl, H, W)
     rng = np.random.default_rng(seed + 100)
@@ -34,6 +39,12 @@ def workload(seed=0, images=10, cylinders=5, points=0, shift=0.08):
     init[:, 4:6] += rng.uniform(-shift, shift, (cylinders, 2))
     init[:, 7] *= rng.uniform(0.85, 1.15, cylinders)
     init[:, 8] *= rng.uniform(0.9, 1.1, cylinders)
+    if tilt:
+        # lean the initial cylinders (by 2 points: tvec_2 leaves the vertical)
+        for c in range(cylinders):
+            a = rng.uniform(-tilt, tilt, 2)
+            q = np.array([1.0, a[0] / 2, a[1] / 2, 0.0])
+            init[c, :4] = q / np.linalg.norm(q)
     sc = sc.gauge()
     sc.tvec[2:] += rng.uniform(-0.02, 0.02, sc.tvec[2:].shape)  # pose noise on the free images
     return sc, mi_ba.GsbaInput(masks, init), cyl
@@ -163,3 +174,127 @@ def test_gsba_facade_workflow_from_files(gpu, tmp_path):
         t = line.split()
         out.append([float(v) for v in t[1:5] + t[6:9] + [t[10], t[12]]])
     assert np.abs(np.array(out) - ref.cylinders).max() <= 1e-6
+
+
+# ---------------------------------------------------------------------------
+# CylinderBy2Points (cylinder_parametrization = "by_2_points")
+# ---------------------------------------------------------------------------
+def test_by2_block_variants_and_oracle_descent():
+    """Blocks as for Cylinder; the cylinder columns are tvec_1, tvec_2, radius
+    (GSBACostFunctionBy2Points / ConstantPose..., 7 parameters, no manifold);
+    7 effective parameters per refined cylinder; the oracle LM descends."""
+    sc, g, _ = workload(seed=12, tilt=0.1)
+    g.cylinder_parametrization = BY2
+    ids, r, J = oracle.gsba_evaluate(mi_ba.default_options(), sc, g)
+    assert len(ids) == sc.num_images * 5
+    assert np.all(J[:, 14:] == 0) and np.abs(J[:, 7:14]).sum() > 0
+    const = ids[:, 0] == 0
+    assert np.all(J[const][:, :7] == 0)
+    a = g.copy()
+    s = oracle.gsba_solve(mi_ba.default_options(max_num_iterations=10), sc.copy(), a)
+    assert s.final_cost < s.initial_cost
+    b = g.copy()
+    b.cylinder_parametrization = mi_ba.CYLINDER_DEFAULT
+    s8 = oracle.gsba_solve(mi_ba.default_options(max_num_iterations=0), sc.copy(), b)
+    assert s.num_effective_parameters_reduced == s8.num_effective_parameters_reduced - 5  # 7 vs 8 per cylinder
+    # the cylinders leave as ToCylinder(): unit quaternions, radius >= 0
+    assert np.allclose(np.linalg.norm(a.cylinders[:, :4], axis=1), 1.0, atol=1e-12)
+    assert np.all(a.cylinders[:, 7] >= 0)
+
+
+def test_by2_round_trip_keeps_the_cylinder():
+    """CylinderBy2Points(Cylinder) -> ToCylinder keeps the lower centre, the
+    radius, the height and the axis (a rotation about the axis is not kept:
+    the reference writes the canonical z -> axis rotation); a vertical
+    cylinder comes back exactly.  Checked through a zero-iteration oracle
+    solve (the cylinders are written back through ToCylinder)."""
+    sc, g, gt = workload(seed=13, tilt=0.3)
+    g.cylinder_parametrization = BY2
+    out = g.copy()
+    oracle.gsba_solve(mi_ba.default_options(max_num_iterations=0), sc.copy(), out)
+    assert np.allclose(out.cylinders[:, 4:9], g.cylinders[:, 4:9], rtol=0, atol=1e-12)
+    for c in range(len(g.cylinders)):
+        axis_in = mi_ba.quat_to_rot(g.cylinders[c, :4])[:, 2]
+        axis_out = mi_ba.quat_to_rot(out.cylinders[c, :4])[:, 2]
+        assert np.abs(axis_in - axis_out).max() <= 1e-12
+    vert = g.copy()
+    vert.cylinders = gt.copy()
+    o2 = vert.copy()
+    oracle.gsba_solve(mi_ba.default_options(max_num_iterations=0), sc.copy(), o2)
+    assert np.array_equal(o2.cylinders, gt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("refine_geometry", [1, 0])
+def test_by2_evaluate_bitwise(gpu, refine_geometry):
+    sc, g, _ = workload(seed=14, tilt=0.1)
+    g.cylinder_parametrization = BY2
+    g.refine_geometry = refine_geometry
+    o = mi_ba.default_options()
+    ids_o, r_o, J_o = oracle.gsba_evaluate(o, sc, g)
+    ids_g, r_g, J_g = mi_ba.gsba_evaluate(o, sc, g)
+    assert np.array_equal(ids_g, ids_o)
+    same = np.concatenate([(r_g == r_o)[:, None], J_g == J_o], axis=1)
+    assert same.mean() >= 0.999, int((~same).sum())
+    assert np.abs(J_o).sum() > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["full", "constant_geometry", "landmarks"])
+def test_by2_solve_parity(gpu, case):
+    sc, g, _ = workload(seed=15, points=200 if case == "landmarks" else 0, tilt=0.1)
+    g.cylinder_parametrization = BY2
+    if case == "constant_geometry":
+        g.refine_geometry = 0
+    if case == "landmarks":
+        g.include_landmark_error = 1
+        g.landmark_error_weight = 0.5
+    o = mi_ba.default_options(max_num_iterations=8)
+    a, b = g.copy(), g.copy()
+    s_o = oracle.gsba_solve(o, sc.copy(), a)
+    s_g = mi_ba.gsba_solve(o, sc.copy(), b)
+    assert s_g.num_residuals_reduced == s_o.num_residuals_reduced
+    assert s_g.num_effective_parameters_reduced == s_o.num_effective_parameters_reduced
+    assert abs(s_g.initial_cost - s_o.initial_cost) <= 1e-12 * s_o.initial_cost
+    assert (s_g.num_successful_steps, s_g.num_unsuccessful_steps) == \
+        (s_o.num_successful_steps, s_o.num_unsuccessful_steps)
+    assert abs(s_g.final_cost - s_o.final_cost) <= 1e-6 * s_o.final_cost
+    assert np.abs(b.cylinders - a.cylinders).max() <= 1e-6
+    assert s_g.final_cost <= s_g.initial_cost
+
+
+@pytest.mark.gpu
+def test_by2_facade_option(gpu, tmp_path):
+    """cylinder_parametrization = "by_2_points" through the facade equals the
+    array solve; an unknown name throws (GetCylinderParametrization)."""
+    import os
+    import subprocess
+    from PIL import Image
+    from test_model_io import write_text_model
+    sc, g, _ = workload(seed=16, tilt=0.1)
+    sc.image_constant_tvec = None
+    write_text_model(sc, str(tmp_path / "model"))
+    (tmp_path / "data" / "depth_tiff").mkdir(parents=True)
+    (tmp_path / "data" / "semantic_tiff").mkdir()
+    for i in range(sc.num_images):
+        Image.fromarray(np.full((H, W), 5.0, np.float32), mode="F").save(
+            tmp_path / "data" / "depth_tiff" / ("img%d_depth.tiff" % i))
+        Image.fromarray(np.where(g.masks[i] > 0, 250.0, 3.0).astype(np.float32), mode="F").save(
+            tmp_path / "data" / "semantic_tiff" / ("img%d_semantic.tiff" % i))
+    with open(tmp_path / "cyl.txt", "w") as f:
+        for c in g.cylinders:
+            f.write("q %r %r %r %r t %r %r %r r %r h %r\n" % tuple(float(v) for v in c))
+    exe = os.path.join(os.path.dirname(__file__), "cpp", "model_io_test")
+    subprocess.run(["make", "-s", "-C", os.path.dirname(exe), "model_io_test"], check=True)
+    args = [exe, "gsba", str(tmp_path / "model"), str(tmp_path / "data"), str(tmp_path / "cyl.txt"),
+            str(tmp_path / "out.txt"), "6"]
+    r = subprocess.run(args + ["by_2_points"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    c0, c1, ns, nu = r.stdout.split()
+    ref = g.copy()
+    ref.cylinder_parametrization = BY2
+    s = mi_ba.gsba_solve(mi_ba.default_options(max_num_iterations=6), sc.copy(), ref)
+    assert abs(float(c1) - s.final_cost) <= 1e-6 * s.final_cost
+    assert (int(ns), int(nu)) == (s.num_successful_steps, s.num_unsuccessful_steps)
+    bad = subprocess.run(args + ["by_3_points"], capture_output=True, text=True)
+    assert bad.returncode == 3 and "not a valid cylinder parametrization" in bad.stdout
