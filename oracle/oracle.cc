@@ -14,6 +14,7 @@
 // The semantic path has no reference tests or data: "parity unpinned" for
 // that oracle beyond self-consistency.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <omp.h>
 #include <cstdint>
@@ -443,6 +444,149 @@ void EvalSemantic(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* 
       Jb[3 + col] = masked ? 0.0 : Jamb[blk * 7 + 4 + col];
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// The product's semantic flat test (csrc/semantic.hip flat_box / flat_check
+// and stencil_bounds; derivation in DESIGN.md §4), restated with the
+// oracle's own arithmetic for the property test
+// (tests/test_semantic_flat_property.py): a sample it clears must have every
+// CENTRAL stencil value equal to its centre residual.
+// ---------------------------------------------------------------------------
+// Negative control of the property test (oracle_set_flat_bound_scale): the
+// pixel bound bx, by is multiplied by this factor (1 = the product's test).
+double g_flat_bound_scale = 1.0;
+
+struct FlatBounds {
+  double rho1 = 0, rho2 = 0, dt1[3] = {0, 0, 0}, dt2[3] = {0, 0, 0}, C[9] = {0};
+};
+
+// |R(q') - R(q)| <= 2 d_perp / (|q| - d) per quaternion step, translation
+// steps d; padded by 1.001.
+void FlatStencilBounds(const double* q, const double* t, double rel, double* rho, double dt[3]) {
+  const double min_step = std::sqrt(std::numeric_limits<double>::epsilon());
+  const double nq2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
+  const double nq = std::sqrt(nq2);
+  double r = 0.0;
+  for (int k = 0; k < 4; ++k) {
+    const double delta = std::max(min_step, std::fabs(q[k]) * rel);
+    const double d = std::max(std::fabs((q[k] + delta) - q[k]), std::fabs(q[k] - (q[k] - delta)));
+    const double perp = d * std::sqrt(std::max(0.0, 1.0 - q[k] * q[k] / nq2));
+    const double den = nq - d;
+    r = std::max(r, den > 0.0 ? 2.0 * perp / den : std::numeric_limits<double>::infinity());
+  }
+  *rho = r * 1.001;
+  for (int k = 0; k < 3; ++k) {
+    const double delta = std::max(min_step, std::fabs(t[k]) * rel);
+    dt[k] = std::max(std::fabs((t[k] + delta) - t[k]), std::fabs(t[k] - (t[k] - delta))) * 1.001;
+  }
+}
+
+double FlatDistortionGain(int model, const double* K, double r2) {
+  double s = 0.0;
+  if (model == MI_BA_SIMPLE_RADIAL || model == MI_BA_RADIAL)
+    for (int k = 3; k < NumParams(model); ++k) s += std::fabs(K[k]);
+  else if (model == MI_BA_OPENCV)
+    for (int k = 4; k < 8; ++k) s += std::fabs(K[k]);
+  const double g = 1.0 + r2;
+  return 1.0 + s * g * g * g;
+}
+
+// every second derivative of (u, v) -> u + Du over |(u, v)| <= rho
+double FlatSecondDerivativeBound(int model, const double* K, double rho) {
+  if (model == MI_BA_SIMPLE_RADIAL) return 6.0 * std::fabs(K[3]) * rho;
+  if (model == MI_BA_RADIAL) return 6.0 * std::fabs(K[3]) * rho + 20.0 * std::fabs(K[4]) * rho * rho * rho;
+  if (model == MI_BA_OPENCV)
+    return 6.0 * std::fabs(K[4]) * rho + 20.0 * std::fabs(K[5]) * rho * rho * rho +
+           6.0 * (std::fabs(K[6]) + std::fabs(K[7]));
+  return 0.0;
+}
+
+bool FlatClears(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, const SemSample& smp,
+                const FlatBounds& B, bool var1, bool var2, double r_centre) {
+  const int i = sem->pairs[2 * smp.pair], j = sem->pairs[2 * smp.pair + 1];
+  const double* q1 = &p->qvec[i * 4];
+  const double* t1 = &p->tvec[i * 3];
+  const double* q2 = &p->qvec[j * 4];
+  const double* t2 = &p->tvec[j * 3];
+  const int model = s.cam_model[p->image_camera[j]];
+  const double* K = &p->camera_params[s.cam_poff[p->image_camera[j]]];
+  double q1i[4], t1i[3], pw[3], p2[3];
+  PoseInverse(q1, t1, q1i, t1i);
+  PoseTransformPoint(q1i, t1i, smp.pc1, pw);
+  PoseTransformPoint(q2, t2, pw, p2);
+  const double w[3] = {smp.pc1[0] - t1[0], smp.pc1[1] - t1[1], smp.pc1[2] - t1[2]};
+  double mag = 0.0;
+  for (int m = 0; m < 3; ++m) mag += std::fabs(smp.pc1[m]) + std::fabs(t1[m]) + std::fabs(pw[m]) + std::fabs(t2[m]);
+  const double z = p2[2];
+  if (!(z > 0.0)) return false;
+  const double iz = 1.0 / z;
+  const double u = p2[0] * iz, v = p2[1] * iz;
+  // x, y and A = d(x, y) / d(u, v) by dual numbers
+  Jet<2> Kj[8], uj(u, 0), vj(v, 1), xj, yj;
+  for (int m = 0; m < NumParams(model); ++m) Kj[m] = Jet<2>(K[m]);
+  WorldToImage(model, Kj, uj, vj, &xj, &yj);
+  const double x = xj.a, y = yj.a;
+  const double A[4] = {xj.v[0], xj.v[1], yj.v[0], yj.v[1]};
+  if (!(std::fabs(x) < 1e8 && std::fabs(y) < 1e8 && std::fabs(u) < 1e6 && std::fabs(v) < 1e6)) return false;
+  const double dq1 = var1 ? B.rho1 * std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]) * (1.0 + 1e-12) : 0.0;
+  const double dq2 = var2 ? B.rho2 * std::sqrt(pw[0] * pw[0] + pw[1] * pw[1] + pw[2] * pw[2]) * (1.0 + 1e-12) : 0.0;
+  std::vector<std::array<double, 3>> cls;
+  if (var1) {
+    cls.push_back({dq1, dq1, dq1});
+    for (int k = 0; k < 3; ++k)
+      cls.push_back({B.dt1[k] * std::fabs(B.C[k]), B.dt1[k] * std::fabs(B.C[3 + k]), B.dt1[k] * std::fabs(B.C[6 + k])});
+  }
+  if (var2) {
+    cls.push_back({dq2, dq2, dq2});
+    cls.push_back({B.dt2[0], 0.0, 0.0});
+    cls.push_back({0.0, B.dt2[1], 0.0});
+    cls.push_back({0.0, 0.0, B.dt2[2]});
+  }
+  double az = 0.0;
+  for (const auto& c : cls) az = std::max(az, c[2]);
+  if (!(z - az > 0.5 * z)) return false;
+  const double iden = 1.0 / (z - az) * (1.0 + 1e-12);
+  double gm = 0.0;
+  std::vector<std::array<double, 2>> d;
+  for (const auto& c : cls) {
+    d.push_back({(c[0] + std::fabs(u) * c[2]) * iden, (c[1] + std::fabs(v) * c[2]) * iden});
+    gm = std::max(gm, std::max(d.back()[0], d.back()[1]));
+  }
+  if (!(gm < 0.1)) return false;
+  const double ru = std::fabs(u) + gm, rv = std::fabs(v) + gm;
+  const double H = FlatSecondDerivativeBound(model, K, std::sqrt(ru * ru + rv * rv) * (1.0 + 1e-12));
+  const double fx = std::fabs(K[0]);
+  const double fy = (model == MI_BA_PINHOLE || model == MI_BA_OPENCV) ? std::fabs(K[1]) : std::fabs(K[0]);
+  double bxm = 0.0, bym = 0.0;
+  for (const auto& e : d) {
+    const double sk = e[0] + e[1];
+    bxm = std::max(bxm, (std::fabs(A[0]) + fx * H * sk) * e[0] + (std::fabs(A[1]) + fx * H * sk) * e[1]);
+    bym = std::max(bym, (std::fabs(A[2]) + fy * H * sk) * e[0] + (std::fabs(A[3]) + fy * H * sk) * e[1]);
+  }
+  const double gain = FlatDistortionGain(model, K, u * u + v * v);
+  const double kscale =
+      (std::fabs(K[0]) + std::fabs(K[1])) * gain * (1.0 + std::fabs(u) + std::fabs(v)) * (1.0 + mag * std::fabs(iz));
+  const double ex = 1e-6 + 1e-11 * (kscale + std::fabs(x) + std::fabs(y));
+  const double bx = (bxm * (1.0 + 1e-12) + ex) * g_flat_bound_scale;
+  const double by = (bym * (1.0 + 1e-12) + ex) * g_flat_bound_scale;
+  const int x0 = (int)std::round(x - bx), y0 = (int)std::round(y - by);
+  const int ncol = (int)std::round(x + bx) - x0 + 1, nrow = (int)std::round(y + by) - y0 + 1;
+  if (ncol > 3 || nrow > 3) return false;
+  const int H_ = sem->height, W_ = sem->width;
+  for (int py = y0; py < y0 + nrow; ++py)
+    for (int px = x0; px < x0 + ncol; ++px) {
+      double f = 0.0;
+      if (px >= 0 && px < W_ && py >= 0 && py < H_) {
+        const int64_t off = (int64_t)j * H_ * W_ + (int64_t)py * W_ + px;
+        const double sd = (double)sem->depth[off];
+        const double dz = std::fabs(sd - z) - sem->depth_error_threshold;
+        if (!(std::fabs(dz) > az + 1e-9 * (1.0 + std::fabs(sd) + mag))) return false;
+        f = dz > 0.0 ? 0.0 : (smp.label1 == sem->label[off] ? 0.0 : 1.0);
+      }
+      if (f != r_centre) return false;
+    }
+  return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -1114,6 +1258,78 @@ double oracle_semantic_throughput(const mi_ba_options* o, mi_ba_problem* p, cons
 // pivot that is not positive.  Rows of L are independent given the columns
 // to their left, so the i-loop runs in parallel with unchanged arithmetic.
 int oracle_cholesky(double* A, int n) { return CholeskyBlocked(A, n); }
+
+// Property test of the flat test (restated above) against the full CENTRAL
+// stencil over every sample of the problem: counts[0] samples, [1] cleared
+// by the flat test, [2] cleared samples with a stencil value different from
+// the centre residual (the test is sound iff 0), [3] samples with a nonzero
+// Jacobian, [4] samples not cleared whose stencil was flat anyway.
+int oracle_semantic_flat_property(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem,
+                                  int64_t* counts) {
+  Setup s;
+  const int st = BuildSetup(o, p, &s);
+  if (st) return st;
+  SemSetup ss;
+  BuildSemSetup(o, p, s, sem, &ss);
+  std::vector<FlatBounds> pb(sem->num_pairs);
+  for (int k = 0; k < sem->num_pairs; ++k) {
+    const int i = sem->pairs[2 * k], j = sem->pairs[2 * k + 1];
+    FlatStencilBounds(&p->qvec[i * 4], &p->tvec[i * 3], sem->numeric_relative_step_size, &pb[k].rho1, pb[k].dt1);
+    FlatStencilBounds(&p->qvec[j * 4], &p->tvec[j * 3], sem->numeric_relative_step_size, &pb[k].rho2, pb[k].dt2);
+    double qi[4], ti[3], Ri[9], R2[9];
+    PoseInverse(&p->qvec[i * 4], &p->tvec[i * 3], qi, ti);
+    QuaternionToRotation(qi, Ri);
+    QuaternionToRotation(&p->qvec[j * 4], R2);
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c)
+        pb[k].C[3 * r + c] = R2[3 * r] * Ri[c] + R2[3 * r + 1] * Ri[3 + c] + R2[3 * r + 2] * Ri[6 + c];
+  }
+  const int64_t n = (int64_t)ss.samples.size();
+  int64_t cleared = 0, bad = 0, nonzero = 0, flat_deferred = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : cleared, bad, nonzero, flat_deferred)
+  for (int64_t k = 0; k < n; ++k) {
+    const SemSample& smp = ss.samples[k];
+    const int i = sem->pairs[2 * smp.pair], j = sem->pairs[2 * smp.pair + 1];
+    double x[14];
+    for (int m = 0; m < 4; ++m) x[m] = p->qvec[i * 4 + m];
+    for (int m = 0; m < 3; ++m) x[4 + m] = p->tvec[i * 3 + m];
+    for (int m = 0; m < 4; ++m) x[7 + m] = p->qvec[j * 4 + m];
+    for (int m = 0; m < 3; ++m) x[11 + m] = p->tvec[j * 3 + m];
+    int stt;
+    const double r = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], &stt);
+    const bool var[2] = {ss.pair_var1[smp.pair] != 0, ss.pair_var2[smp.pair] != 0};
+    const double min_step = std::sqrt(std::numeric_limits<double>::epsilon());
+    bool flat = true, jz = true;
+    for (int blk = 0; blk < 2; ++blk) {
+      if (!var[blk]) continue;
+      for (int m = 0; m < 7; ++m) {
+        const int idx = blk * 7 + m;
+        const double orig = x[idx];
+        const double delta = std::max(min_step, std::fabs(orig) * sem->numeric_relative_step_size);
+        x[idx] = orig + delta;
+        const double fp = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], &stt);
+        x[idx] = orig - delta;
+        const double fm = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], &stt);
+        x[idx] = orig;
+        if (fp != r || fm != r) flat = false;
+        if (fp != fm) jz = false;
+      }
+    }
+    const bool clears = FlatClears(p, s, sem, smp, pb[smp.pair], var[0], var[1], r);
+    cleared += clears;
+    bad += clears && !flat;
+    nonzero += !jz;
+    flat_deferred += !clears && flat;
+  }
+  counts[0] = n;
+  counts[1] = cleared;
+  counts[2] = bad;
+  counts[3] = nonzero;
+  counts[4] = flat_deferred;
+  return 0;
+}
+
+void oracle_set_flat_bound_scale(double scale) { g_flat_bound_scale = scale; }
 
 // Registers (or clears, NULL) the dense factor the LM uses for its reduced
 // camera system.

@@ -67,6 +67,10 @@ def load():
     lib.oracle_gsba_iou.argtypes = [_dp, _dp, _dp, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
     lib.oracle_cholesky.restype = C.c_int
     lib.oracle_cholesky.argtypes = [_dp, C.c_int]
+    lib.oracle_semantic_flat_property.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem),
+                                                  C.POINTER(mi_ba.Semantic), _i64p]
+    lib.oracle_set_flat_bound_scale.argtypes = [C.c_double]
+    lib.oracle_set_flat_bound_scale.restype = None
     lib.oracle_set_dense_factor.argtypes = [DENSE_FACTOR_FN]
     lib.oracle_set_dense_factor.restype = None
     _lib = lib
@@ -288,6 +292,27 @@ def semantic_eval(options, scene, semantic):
     lib.oracle_semantic_eval(C.byref(options), C.byref(p), C.byref(s), px.ctypes.data_as(_i32p),
                              st.ctypes.data_as(_i32p), r.ctypes.data_as(_dp), J.ctypes.data_as(_dp), n)
     return px, st, r, J
+
+
+def semantic_flat_property(options, scene, semantic, bound_scale=1.0):
+    """The product's semantic flat test (restated) vs the full CENTRAL
+    stencil over every sample: dict(samples, cleared, cleared_not_flat,
+    nonzero_jacobian, flat_deferred).  cleared_not_flat must be 0.
+    bound_scale < 1 shrinks the pixel bound (negative control)."""
+    sc = scene.copy()
+    p = sc.problem()
+    s = semantic.struct()
+    counts = np.zeros(5, np.int64)
+    lib = load()
+    lib.oracle_set_flat_bound_scale(bound_scale)
+    try:
+        st = lib.oracle_semantic_flat_property(C.byref(options), C.byref(p), C.byref(s), counts.ctypes.data_as(_i64p))
+    finally:
+        lib.oracle_set_flat_bound_scale(1.0)
+    if st != 0:
+        raise RuntimeError(f"oracle_semantic_flat_property status {st}")
+    return dict(zip(("samples", "cleared", "cleared_not_flat", "nonzero_jacobian", "flat_deferred"),
+                    (int(v) for v in counts)))
 
 
 def cholesky(A):

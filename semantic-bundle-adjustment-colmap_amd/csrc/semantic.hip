@@ -874,24 +874,50 @@ __device__ __forceinline__ void stencil_full(const SemArgs& a, const PairConst* 
 // ---------------------------------------------------------------------------
 // Flat test.  Most samples have a zero Jacobian: every stencil point lands on
 // a pixel with the centre's outcome.  This proves it without evaluating the
-// stencil: every stencil point's camera-2 point lies within d of the
-// centre's (PairConst bounds), so |du| <= d (1 + |u|) / (z - d) (same for v)
-// exactly, the pixel moves by at most 1.1 (|A00| du + |A01| dv) (A = d(x,y) /
-// d(u,v) at the centre; the camera model's second derivatives are bounded by
-// ~20 x distortion_gain of the first, so with gain * |d(u,v)| (1 + |u| + |v|)
-// <= 2e-3 (guarded below) A changes by <= 4 % over the displacement) plus
-// resolve's rounding margin, and the depth compared by at most d.  When every
-// pixel the rounded projection can reach gives the centre's outcome for every
-// depth within d (outside the margin), every stencil value equals the
-// centre's residual: all CENTRAL differences are +0.0, J = +0.0 exactly as
-// the reference's accumulation yields.  Otherwise (or on any doubt: depth
-// near zero, huge coordinates, a wide pixel box) the sample takes the full
-// stencil.
+// stencil (DESIGN.md §4 has the derivation):
+//  (1) every stencil point's camera-2 point P' lies within a componentwise
+//      bound (ax, ay, az) of the centre's P (per class of stencil points:
+//      PairConst bounds), so with z' >= z - az > 0, u' - u = (dPx - u dPz) /
+//      (z + dPz) gives |du| <= (ax + |u| az) / (z - az) exactly (v alike);
+//  (2) the pixel x(u, v) = f (u + D(u, v)) + c moves by the mean value
+//      theorem by |dx| <= (|A00| + Hx s) du + (|A01| + Hx s) dv, s = du + dv,
+//      A = d(x, y) / d(u, v) at the centre and Hx = |fx| H(rho) a bound of
+//      every second derivative of x over the box |(u, v)| <= rho
+//      (second_derivative_bound: the radial terms u r^2 / u r^4 give 6 rho /
+//      20 rho^3, the tangential ones 6 (|p1| + |p2|); 0 for the pinholes);
+//  (3) the reference's computed pixel differs from the exact one by rounding
+//      far below resolve's margin ex, so round() can only reach the pixels
+//      round(x - bx) .. round(x + bx), bx = bound + ex; the depth compared
+//      moves by at most az.
+// When every pixel of that box gives the centre's outcome for every depth
+// within az (outside the margin), every stencil value equals the centre's
+// residual: all CENTRAL differences are +0.0 and J = +0.0 exactly as the
+// reference's accumulation yields.  Otherwise (or on any doubt: depth near
+// zero, huge coordinates, a box wider than 3 x 3) the sample takes the full
+// stencil.  tests/test_semantic_flat_property.py checks the oracle's
+// restatement of this test against the full stencil on >= 1e7 samples.
 // ---------------------------------------------------------------------------
 struct FlatBox {
   int x0, y0, ncol, nrow;  // reachable pixels (x0 .. x0 + ncol - 1, y0 .. y0 + nrow - 1)
   double d;                // bound of the depth change
 };
+
+// Bound H(rho) of every second derivative of the distortion map (u, v) ->
+// u + Du(u, v) (and v + Dv) over |(u, v)| <= rho, per unit focal length:
+//   d2(u r^2) <= 6 rho, d2(u r^4) <= 20 rho^3 (all of d2/du2, d2/dudv,
+//   d2/dv2; v alike), d2 of the OPENCV tangential terms <= 6 (|p1| + |p2|).
+template <int M>
+__device__ __forceinline__ double second_derivative_bound(const double* K, double rho) {
+  if constexpr (M == kSimpleRadial) {
+    return 6.0 * fabs(K[3]) * rho;
+  } else if constexpr (M == kRadial) {
+    return 6.0 * fabs(K[3]) * rho + 20.0 * fabs(K[4]) * rho * rho * rho;
+  } else if constexpr (M == kOpenCV) {
+    return 6.0 * fabs(K[4]) * rho + 20.0 * fabs(K[5]) * rho * rho * rho + 6.0 * (fabs(K[6]) + fabs(K[7]));
+  } else {
+    return 0.0;
+  }
+}
 
 // Geometry half of the flat test: false when the sample cannot be cleared
 // whatever the raster holds.  c needs p2, pw, w, mag (not the raster).
@@ -917,12 +943,13 @@ __device__ __forceinline__ bool flat_box(const PairConst* __restrict__ P, const 
   if (P->var2) az_max = fmax(az_max, P->dt2[2]);
   if (!(z - az_max > 0.5 * z)) return false;
   const double iden = 1.0 / (z - az_max) * (1.0 + 1e-12);
-  double bxm = 0.0, bym = 0.0, gm = 0.0;
+  // the classes' (du, dv): q1, t1 x3, q2, t2 x3
+  double cu[8], cv[8];
+  int nc = 0;
   auto cls = [&](double ax, double ay, double az) {
-    const double du = (ax + fabs(u) * az) * iden, dv = (ay + fabs(v) * az) * iden;
-    bxm = fmax(bxm, fabs(A[0]) * du + fabs(A[1]) * dv);
-    bym = fmax(bym, fabs(A[2]) * du + fabs(A[3]) * dv);
-    gm = fmax(gm, fmax(du, dv));
+    cu[nc] = (ax + fabs(u) * az) * iden;
+    cv[nc] = (ay + fabs(v) * az) * iden;
+    ++nc;
   };
   if (P->var1) {
     cls(dq1, dq1, dq1);
@@ -936,12 +963,24 @@ __device__ __forceinline__ bool flat_box(const PairConst* __restrict__ P, const 
     cls(0.0, P->dt2[1], 0.0);
     cls(0.0, 0.0, P->dt2[2]);
   }
+  double gm = 0.0;
+  for (int k = 0; k < nc; ++k) gm = fmax(gm, fmax(cu[k], cv[k]));
+  if (!(gm < 0.1)) return false;  // a stencil this wide is never cleared (and keeps rho finite)
+  const double ru = fabs(u) + gm, rv = fabs(v) + gm;
+  const double H = second_derivative_bound<M>(K2, sqrt(ru * ru + rv * rv) * (1.0 + 1e-12));
+  const double fx = fabs(K2[0]);
+  const double fy = (M == kPinhole || M == kOpenCV) ? fabs(K2[1]) : fabs(K2[0]);
+  double bxm = 0.0, bym = 0.0;
+  for (int k = 0; k < nc; ++k) {
+    const double sk = cu[k] + cv[k];
+    bxm = fmax(bxm, (fabs(A[0]) + fx * H * sk) * cu[k] + (fabs(A[1]) + fx * H * sk) * cv[k]);
+    bym = fmax(bym, (fabs(A[2]) + fy * H * sk) * cu[k] + (fabs(A[3]) + fy * H * sk) * cv[k]);
+  }
   const double gain = distortion_gain<M>(K2, u * u + v * v);
-  if (!(gain * gm * (1.0 + fabs(u) + fabs(v)) <= 2e-3)) return false;
   const double kscale = (fabs(K2[0]) + fabs(K2[1])) * gain * (1.0 + fabs(u) + fabs(v)) * (1.0 + c.mag * fabs(iz));
   const double ex = 1e-6 + 1e-11 * (kscale + fabs(x) + fabs(y));
-  const double bx = 1.1 * bxm + ex;
-  const double by = 1.1 * bym + ex;
+  const double bx = bxm * (1.0 + 1e-12) + ex;
+  const double by = bym * (1.0 + 1e-12) + ex;
   // round() is monotone: the reachable pixels are round(x - bx) .. round(x + bx)
   fb.x0 = (int)round(x - bx);
   fb.y0 = (int)round(y - by);
