@@ -15,8 +15,9 @@ BA-iteration figures), not inside the step.
 value = (reprojection blocks + semantic samples, all ranks) * steps / max-over-
 ranks wall time of the timed steps.  Multi-GPU: the linearization shards by
 point blocks (with all their observations) and image pairs and has no
-data-path collective, so the timed region needs none.  Default --scaling weak:
-every rank owns a C4-sized shard; --scaling strong splits the one C5 problem.
+data-path collective, so the timed region needs none.  Default at N > 1:
+--scaling strong, the one C4 problem split across the ranks (BASELINE's C5);
+--scaling weak gives every rank a C4-sized shard of its own (labelled).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C4]
 """
@@ -176,25 +177,45 @@ def cpu_ba_iteration(iters=3):
 
 
 def cpu_baseline(opts, sc, sem, cfg, nb, ns):
-    """The CPU restatement (oracle, 'port') timed on this host on a bounded sample."""
+    """The CPU restatement (oracle, 'port') timed on this host on a bounded
+    sample of the same workload, at 1 thread and at the job's CPU share
+    (OMP_NUM_THREADS = 16 on the GPU boxes; `value`).  The host has more
+    CPUs (affinity_cpus) than the share this job may load — the pool's rule is
+    to size worker pools to the share — so the whole-host figure is the
+    share's rate scaled linearly by affinity_cpus / cores (an upper bound:
+    memory bandwidth does not scale with threads), reported as an
+    extrapolation, not a measurement."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     threads = cpu_threads()
-    geo_blocks = nb  # the whole workload: ~1.5 s wall x 16 threads
-    t_geo, done_geo = oracle.reproj_throughput(opts, sc, geo_blocks, 1, threads)
-    rate_geo = done_geo / t_geo
-    sample = f"{done_geo} reprojection blocks"
-    total_time = nb / rate_geo
-    rate_sem = None
-    if sem is not None and ns:
-        t_sem, done_sem = oracle.semantic_throughput(opts, sc, sem, ns, threads)
-        rate_sem = done_sem / t_sem
-        total_time += ns / rate_sem
-        sample += f" + {done_sem} semantic samples"
+
+    def rates(nthreads, geo_blocks, sem_samples):
+        t_geo, done_geo = oracle.reproj_throughput(opts, sc, geo_blocks, 1, nthreads)
+        r_geo = done_geo / t_geo
+        r_sem, done_sem = None, 0
+        if sem is not None and ns:
+            t_sem, done_sem = oracle.semantic_throughput(opts, sc, sem, sem_samples, nthreads)
+            r_sem = done_sem / t_sem
+        total = nb / r_geo + (ns / r_sem if r_sem else 0.0)
+        return (nb + ns) / total, r_geo, r_sem, done_geo, done_sem
+
+    # the whole workload at the share (~1.5 s wall x 16 threads); a bounded
+    # sample single-threaded
+    value, rate_geo, rate_sem, done_geo, done_sem = rates(threads, nb, ns)
+    one, one_geo, one_sem, d1g, d1s = rates(1, min(nb, 500_000), min(ns, 100_000))
     model, nproc, affinity = host_cpu()
-    return {"value": (nb + ns) / total_time, "unit": "residual_blocks/s", "cores": threads, "kind": "port",
-            "sample": sample + " of the same workload, oracle/ CPU restatement (C++/OpenMP, f64), not Ceres",
+    sample = f"{done_geo} reprojection blocks" + (f" + {done_sem} semantic samples" if done_sem else "")
+    return {"value": value, "unit": "residual_blocks/s", "cores": threads, "kind": "port",
+            "sample": sample + " of the same workload at `cores` threads (1 thread: " +
+                      f"{d1g} blocks" + (f" + {d1s} samples" if d1s else "") +
+                      "), oracle/ CPU restatement (C++/OpenMP, f64), not Ceres",
             "reproj_blocks_per_s": rate_geo, "semantic_samples_per_s": rate_sem,
+            "single_thread_value": one, "single_thread_reproj_blocks_per_s": one_geo,
+            "single_thread_semantic_samples_per_s": one_sem,
+            "parallel_efficiency": value / (one * threads) if one else None,
+            "whole_host_extrapolated_value": value * affinity / max(1, threads),
+            "whole_host_note": "linear extrapolation of the share's rate to affinity_cpus threads (not measured: "
+                               "the job's CPU share is `cores`); an upper bound",
             "cpu_model": model, "host_nproc": nproc, "affinity_cpus": affinity,
             "threads_note": "threads = the job's CPU share (OMP_NUM_THREADS on the GPU box), capped by the affinity mask"}
 
@@ -205,25 +226,33 @@ def roofline_semantic(config, ns, avg_ms):
     HBM from PMC traffic, per linearization, over the time measured here (HIP
     events on the context stream).  SURVEY 8d expected it FP64-bound; since
     the flat test skips the stencil of most samples the raster gathers bind
-    it, so `bound` names the roof with the larger fraction.  Algorithmic
-    bytes: 32 (sample record) + 8 (compulsory raster gather) per sample; the
-    per-pair records are negligible."""
+    it.  `bound` names the roof with the larger fraction and `achieved` /
+    `peak` / `unit` / `frac` are that roof's.
+    Algorithmic bytes: SURVEY 8d's 128 B per sample (16 sample in, 8
+    compulsory raster gather, 8 residual + 96 tangent-Jacobian row out) is the
+    J-materialising definition; the product reduces the rows into the per-pair
+    J'J / J'r blocks instead of writing them, so its own algorithmic traffic is
+    32 (sample record) + 8 (raster gather) = 40 B per sample.  Both are
+    reported; the HBM fraction uses the measured (PMC) traffic."""
     flops, hbm, src = semantic_pmc(config)
     if avg_ms <= 0:
         return None
     t = avg_ms * 1e-3
-    alg = 40.0 * ns
     f_fp64 = flops / t / 1e12 / FP64_PEAK_TFS if flops else 0.0
     f_hbm = hbm / t / 1e9 / HBM_PEAK_GBS if hbm else 0.0
-    out = {"kernel": "semantic_flat+semantic_deferred", "bound": "hbm" if f_hbm > f_fp64 else "fp64",
-           "unit": "TFLOP/s", "peak": FP64_PEAK_TFS,
-           "achieved": flops / t / 1e12 if flops else None,
-           "frac": flops / t / 1e12 / FP64_PEAK_TFS if flops else None,
-           "fp64_ops_per_launch": flops, "traffic": hbm, "traffic_unit": "bytes/launch",
-           "hbm_achieved_GBs": hbm / t / 1e9 if hbm else None,
-           "hbm_frac": hbm / t / 1e9 / HBM_PEAK_GBS if hbm else None,
-           "algorithmic_bytes_per_launch": alg, "samples_per_launch": ns, "avg_launch_ms": avg_ms,
-           "pmc_source": src}
+    hbm_bound = f_hbm > f_fp64
+    out = {"kernel": "semantic_flat+semantic_deferred", "bound": "hbm" if hbm_bound else "fp64",
+           "unit": "GB/s" if hbm_bound else "TFLOP/s",
+           "peak": HBM_PEAK_GBS if hbm_bound else FP64_PEAK_TFS,
+           "achieved": (hbm / t / 1e9 if hbm_bound else flops / t / 1e12) if (hbm or flops) else None,
+           "frac": (f_hbm if hbm_bound else f_fp64) if (hbm or flops) else None,
+           "fp64_achieved_TFs": flops / t / 1e12 if flops else None, "fp64_frac": f_fp64 if flops else None,
+           "fp64_ops_per_launch": flops,
+           "hbm_achieved_GBs": hbm / t / 1e9 if hbm else None, "hbm_frac": f_hbm if hbm else None,
+           "traffic": hbm, "traffic_unit": "bytes/launch",
+           "algorithmic_bytes_per_sample_survey": 128, "algorithmic_bytes_per_sample_fused": 40,
+           "algorithmic_GBs_survey": 128.0 * ns / t / 1e9, "algorithmic_GBs_fused": 40.0 * ns / t / 1e9,
+           "samples_per_launch": ns, "avg_launch_ms": avg_ms, "pmc_source": src}
     return out
 
 
@@ -235,12 +264,15 @@ def main():
     ap.add_argument("--config", default="C4", choices=sorted(CONFIGS))
     ap.add_argument("--lm-iters", type=int, default=3, help="LM iterations for the BA-iteration wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: a config-sized shard per rank (default); strong: the config split across ranks")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="strong (default at N > 1): the one config problem split across the ranks (C4 split "
+                         "this way is BASELINE's C5); weak: a config-sized shard per rank")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.scaling is None:
+        args.scaling = "strong" if world > 1 else "weak"  # N = 1: both are the whole config
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     ap_backend = os.environ.get("MI_BA_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm; gloo for 1-GPU rehearsals
     dist = None
