@@ -555,7 +555,6 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
 typedef double pf_dvec4 __attribute__((ext_vector_type(4)));
 constexpr int kPfMaxTiles = 8;  // column tiles per panel (panel <= 512)
 constexpr int kTinv = 512;  // own_diag 7: widest panel
-constexpr int kPfRows = 4;      // row tiles per below-diagonal workgroup
 
 __device__ __forceinline__ int pf_row0(int r, int kb, int nc) { return r < nc ? 64 * r : kb + 64 * (r - nc); }
 __device__ __forceinline__ int pf_rows(int r, int kb, int nc, int mrows) {
@@ -583,6 +582,21 @@ __device__ __forceinline__ void pf_gemm_nt(pf_dvec4 (&acc)[4], double sign, LX l
   }
 }
 
+// pf_gemm_nt with Y lower triangular by 16x16 blocks (Y[j][k] read only for
+// k-block <= j-block, the rest taken as zero: the published inverses'
+// strict upper blocks are not stored): 40 of 64 MFMA steps.
+template <typename LX, typename LY>
+__device__ __forceinline__ void pf_gemm_nt_lt(pf_dvec4 (&acc)[4], double sign, LX ldx, LY ldy, int w, int lane) {
+  const int m = lane & 15, k = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const double a = sign * ldx(16 * w + m, 4 * s + k);
+#pragma unroll
+    for (int t = s / 4; t < 4; ++t)
+      acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, ldy(16 * t + m, 4 * s + k), acc[t], 0, 0, 0);
+  }
+}
+
 // LDS tiles are row-major with a padded stride (MFMA operand reads of 16
 // consecutive rows then fall in distinct banks)
 constexpr int kPfLd = 65;
@@ -606,101 +620,7 @@ __device__ __forceinline__ void pf_acc_to_lds_t(const pf_dvec4 (&acc)[4], double
     for (int q = 0; q < 4; ++q) T[(16 * t + (lane & 15)) * kPfLd + 16 * w + 4 * q + (lane >> 4)] = acc[t][q];
 }
 
-// One wave, lane = column j: Li = L^-1 (row-major padded) from L in T
-// (row-major padded, unit-free) and the pivot reciprocals dinv: forward
-// substitution over rows, the solved rows kept in Li itself (lane-contiguous
-// reads), L's row read as contiguous broadcasts, four partial sums per row.
-__device__ void pf_inv_wave(const double* L, int ldl, const double* dinv, double* Li, int lane) {
-  for (int i = 0; i < 64; ++i) {
-    const double* Lrow = L + i * ldl;
-    double s0 = (i == lane) ? 1.0 : 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    int k = 0;
-    for (; k + 3 < i; k += 4) {
-      s0 -= Lrow[k] * Li[k * kPfLd + lane];
-      s1 -= Lrow[k + 1] * Li[(k + 1) * kPfLd + lane];
-      s2 -= Lrow[k + 2] * Li[(k + 2) * kPfLd + lane];
-      s3 -= Lrow[k + 3] * Li[(k + 3) * kPfLd + lane];
-    }
-    for (; k < i; ++k) s0 -= Lrow[k] * Li[k * kPfLd + lane];
-    Li[i * kPfLd + lane] = ((s0 + s1) + (s2 + s3)) * dinv[i];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-  }
-}
-
-// In-LDS Cholesky of a 64x64 column-major tile (lower), blocked by kStep
-// columns (diag_panel_blocked_kernel's factor loop); returns the first
-// non-positive pivot (1-based) or 0.
-template <int kStep, int NW>
-__device__ int tile_chol_lds(double* L, double* nb, int lane, int wv, int ld = 64) {
-  int bad = 0;
-  for (int jb = 0; jb < 64; jb += kStep) {
-    double d[kStep][kStep];
-#pragma unroll
-    for (int i = 0; i < kStep; ++i)
-#pragma unroll
-      for (int k = 0; k <= i; ++k) d[i][k] = L[(jb + k) * ld + jb + i];
-#pragma unroll
-    for (int k = 0; k < kStep; ++k) {
-      const double piv = d[k][k];
-      if (!(piv > 0.0) && bad == 0) bad = jb + k + 1;
-      d[k][k] = sqrt(piv);
-#pragma unroll
-      for (int i = k + 1; i < kStep; ++i) d[i][k] /= d[k][k];
-#pragma unroll
-      for (int i = k + 1; i < kStep; ++i)
-#pragma unroll
-        for (int m = k + 1; m <= i; ++m) d[i][m] -= d[i][k] * d[m][k];
-    }
-    double y[kStep];
-    if (lane >= jb + kStep) {
-#pragma unroll
-      for (int k = 0; k < kStep; ++k) {
-        double v = L[(jb + k) * ld + lane];
-#pragma unroll
-        for (int m = 0; m < k; ++m) v -= y[m] * d[k][m];
-        y[k] = v / d[k][k];
-      }
-    } else {
-      const int i = lane - jb;
-#pragma unroll
-      for (int k = 0; k < kStep; ++k) {
-        double v = 0.0;
-#pragma unroll
-        for (int ii = k; ii < kStep; ++ii) v = (i == ii) ? d[ii][k] : v;
-        y[k] = v;
-      }
-    }
-    if (wv == 0) {
-#pragma unroll
-      for (int k = 0; k < kStep; ++k) nb[k * 64 + lane] = y[k];
-    }
-    __syncthreads();
-    if (wv == 0) {
-#pragma unroll
-      for (int k = 0; k < kStep; ++k)
-        if (lane >= jb + k) L[(jb + k) * ld + lane] = y[k];
-    }
-    for (int c = jb + kStep + wv; c < 64; c += NW) {
-      double v = L[c * ld + lane];
-#pragma unroll
-      for (int k = 0; k < kStep; ++k) v -= y[k] * nb[k * 64 + c];
-      L[c * ld + lane] = v;
-    }
-    __syncthreads();
-  }
-  return bad;
-}
-
-// ---- 64x64 factor + inverse in LDS by 16x16 blocks (4 waves, MFMA) --------
-// M: row-major padded (ld kPfLd) 64x64, lower triangle valid.  Right-looking
-// over four 16-wide block columns: the 16x16 diagonal block by one wave in
-// registers (lane = row), the 16-column solve below it by one lane per row
-// (registers), the trailing lower blocks by v_mfma_f64_16x16x4f64.  Then
-// X = L^-1: the four diagonal blocks by one wave (lane = block x column), the
-// off-diagonal blocks by block diagonals, X_ik = -X_ii sum_m L_im X_mk (MFMA).
-// Returns the first non-positive pivot (1-based) or 0 (every thread).
-
+// ---- 16x16 MFMA block helpers of the tile factor --------------------------
 // acc (16x16, MFMA D layout) += sign * A(16x16) * op(B); A, B row-major with
 // leading dimensions lda, ldb; op(B) = B' when TB.
 template <bool TB>
@@ -723,55 +643,119 @@ __device__ __forceinline__ void blk16_store(const pf_dvec4& acc, double* C, int 
   for (int q = 0; q < 4; ++q) C[(4 * q + (lane >> 4)) * ldc + (lane & 15)] = acc[q];
 }
 
-__device__ int pf_chol_inv_blocked(double* M, double* X, double* scr, double* dinv, int lane, int wv) {
+
+// ---- 64x64 factor + inverse, block columns by register sweeps -------------
+// M: row-major padded (ld kPfLd) 64x64, lower triangle valid; on return L in
+// M's lower triangle, X = L^-1 (lower blocks), dinv[i] = 1 / L_ii, and the
+// first non-positive pivot (1-based) or 0 (every thread).  Block column kb
+// (16 wide) by wave 0 with lane = tile row: the 16 pivots of the diagonal
+// block AND the solve of every row below it in one register sweep (x D' = a
+// is the same elimination applied to the rows below the block), each pivot
+// and multiplier broadcast by readlane — no LDS round trip or wave barrier
+// per pivot (the previous per-pivot LDS exchange + lane-per-row substitution
+// took 36 us per tile vs 15.6, profiles/r3_tile_probe.txt).  Trailing lower
+// blocks by v_mfma_f64_16x16x4f64; X's off-diagonal blocks by block
+// diagonals, X_ik = -X_ii sum_m L_im X_mk (MFMA).
+// 1/sqrt(d) and sqrt(d) for a pivot: RSQ, v_rsq_f64 (~2^-23 relative) and
+// two Goldschmidt steps (~1 ulp; six dependent ops on the pivot chain instead
+// of the correctly rounded sqrt + divide expansions' ~25); else sqrt and 1/x.
+template <bool RSQ>
+__device__ __forceinline__ void pf_pivot(double d, double& sd, double& isd) {
+  if (RSQ) {
+    const double y = __builtin_amdgcn_rsq(d);
+    double g = d * y, h = 0.5 * y;
+    double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    sd = g;
+    isd = h + h;
+  } else {
+    sd = sqrt(d);
+    isd = 1.0 / sd;
+  }
+}
+
+template <bool RSQ>
+__device__ __forceinline__ int pf_col16(double* M, double* dinv, int o, int lane) {
+  double a[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) a[c] = M[lane * kPfLd + o + c];
   int bad = 0;
-  double* col = scr;  // [16][16] pivot columns of the current diagonal block
+  double my_isd = 0.0;  // lane o + k keeps pivot k's reciprocal
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const double d = readlane_f64(a[k], o + k);
+    if (!(d > 0.0) && bad == 0) bad = o + k + 1;
+    double sd, isd;
+    pf_pivot<RSQ>(d, sd, isd);
+    const bool piv = lane == o + k;
+    const double l = piv ? sd : a[k] * isd;
+    my_isd = piv ? isd : my_isd;
+    a[k] = l;
+#pragma unroll
+    for (int c = k + 1; c < 16; ++c) a[c] -= l * readlane_f64(l, o + c);
+  }
+  // rows above the block computed garbage and are left alone; the block's
+  // strict upper triangle is written as zero
+  if (lane >= o) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) M[lane * kPfLd + o + c] = lane >= o + c ? a[c] : 0.0;
+    if (lane < o + 16) dinv[lane] = my_isd;
+  }
+  return bad;
+}
+
+// Diagonal block b's inverse X_bb = L_bb^-1 by one wave: lane = column j
+// (lanes 16.. repeat lanes 0..15 and store nothing), forward substitution
+// over the block's rows with L broadcast from LDS.
+__device__ __forceinline__ void pf_diag_inv16(const double* M, const double* dinv, double* X, int b, int lane) {
+  const int j = lane & 15, o = 16 * b;
+  double x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    double v = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+    for (int m2 = 0; m2 < i; ++m2) v -= M[(o + i) * kPfLd + o + m2] * x[m2];
+    x[i] = v * dinv[o + i];
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) X[(o + i) * kPfLd + o + j] = x[i];
+  }
+}
+
+// Factor + inverse of the 64x64 tile M (row-major padded, lower valid): the
+// four block-column sweeps by wave 0 (pf_col16), the trailing lower blocks
+// by all waves (MFMA); while wave 0 sweeps block column kb, wave
+// 1 + (kb - 1) % 3 inverts diagonal block kb - 1 (final since sweep kb - 1).
+// scr: [0, 1088) per-wave 16x16 scratch, [1088] the pivot status.
+// X = L^-1 in its lower blocks only (the strict upper blocks are left as they
+// are: every consumer reads X as lower triangular, pf_gemm_nt_lt).
+// stamps (nullable, probes only): clock64() by thread 0 after each block
+// column's sweep and trailing update (8), the last diagonal inverse, the end.
+template <bool RSQ>
+__device__ __forceinline__ int pf_chol_inv_fast(double* M, double* X, double* scr, double* dinv, int lane, int wv,
+                                                long long* stamps = nullptr) {
+  int bad = 0;
+  auto stamp = [&](int k) {
+    if (stamps && threadIdx.x == 0) stamps[k] = clock64();
+  };
   for (int kb = 0; kb < 4; ++kb) {
     const int o = 16 * kb;
-    // 1. diagonal block, wave 0 (lanes 16.. repeat lanes 0..15)
     if (wv == 0) {
-      const int i = lane & 15;
-      double a[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) a[j] = M[(o + i) * kPfLd + o + j];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const double dk = readlane_f64(a[k], k);
-        if (!(dk > 0.0) && bad == 0) bad = o + k + 1;
-        const double sk = sqrt(dk);
-        const double isk = 1.0 / sk;
-        const double lik = i > k ? a[k] * isk : (i == k ? sk : 0.0);
-        a[k] = lik;
-        if (lane < 16) col[k * 16 + i] = lik;
-        if (lane == 0) dinv[o + k] = isk;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-#pragma unroll
-        for (int j = k + 1; j < 16; ++j) a[j] -= lik * col[k * 16 + j];
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) M[(o + i) * kPfLd + o + j] = j <= i ? a[j] : 0.0;
-      }
+      const int b = pf_col16<RSQ>(M, dinv, o, lane);
+      if (bad == 0) bad = b;
+      // bad lives in wave 0; every thread returns it
+      if (kb == 3 && lane == 0) reinterpret_cast<int*>(scr)[4 * 16 * 17 * 2] = bad;
+    } else if (kb >= 1 && wv == 1 + (kb - 1) % 3) {
+      pf_diag_inv16(M, dinv, X, kb - 1, lane);
     }
     __syncthreads();
-    // 2. rows below: x D' = a, lane = row (wave 0, up to 48 rows)
-    const int nbelow = 48 - o;
-    if (wv == 0 && lane < nbelow) {
-      const int r = o + 16 + lane;
-      double x[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        double v = M[r * kPfLd + o + k];
-#pragma unroll
-        for (int m2 = 0; m2 < k; ++m2) v -= x[m2] * M[(o + k) * kPfLd + o + m2];
-        x[k] = v * dinv[o + k];
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) M[r * kPfLd + o + k] = x[k];
-    }
-    __syncthreads();
-    // 3. trailing lower blocks (ib >= jb > kb): A_ib,jb -= L_ib,kb L_jb,kb'
+    stamp(2 * kb);
+    // trailing lower blocks (ib >= jb > kb): A_ib,jb -= L_ib,kb L_jb,kb'
     int t = 0;
     for (int ib = kb + 1; ib < 4; ++ib)
       for (int jb = kb + 1; jb <= ib; ++jb, ++t) {
@@ -782,30 +766,15 @@ __device__ int pf_chol_inv_blocked(double* M, double* X, double* scr, double* di
         blk16_mma<true>(acc, -1.0, M + 16 * ib * kPfLd + o, kPfLd, M + 16 * jb * kPfLd + o, kPfLd, lane);
         blk16_store(acc, C, kPfLd, lane);
       }
-    __syncthreads();
+    if (kb < 3) __syncthreads();
+    stamp(2 * kb + 1);
   }
-  // X = L^-1.  Diagonal blocks: wave 0, lane = (block b, column j)
-  if (wv == 0) {
-    const int b = lane >> 4, j = lane & 15, o = 16 * b;
-    double x[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      double v = (i == j) ? 1.0 : 0.0;
-#pragma unroll
-      for (int m2 = 0; m2 < i; ++m2) v -= M[(o + i) * kPfLd + o + m2] * x[m2];
-      x[i] = v * dinv[o + i];
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) X[(o + i) * kPfLd + o + j] = x[i];
-  }
-  // strict upper blocks of X are zero
-  for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
-    const int i = e >> 6, j = e & 63;
-    if ((j >> 4) > (i >> 4)) X[i * kPfLd + j] = 0.0;
-  }
+  if (wv == 3) pf_diag_inv16(M, dinv, X, 3, lane);
   __syncthreads();
+  stamp(8);
+  bad = reinterpret_cast<const int*>(scr)[4 * 16 * 17 * 2];
   // off-diagonal blocks by block diagonals d: X_ik = -X_ii (sum_{m=k}^{i-1} L_im X_mk)
-  double* T = scr + wv * 16 * 17;  // per-wave 16x16 scratch (ld 17)
+  double* T = scr + wv * 16 * 17;
   for (int d = 1; d < 4; ++d) {
     const int k = wv;
     const int i = k + d;
@@ -822,18 +791,79 @@ __device__ int pf_chol_inv_blocked(double* M, double* X, double* scr, double* di
     }
     __syncthreads();
   }
+  stamp(9);
   return bad;
 }
 
 // dbg (nullable, probes only): wall_clock64() stamps [row tile][20]: 0 start,
 // 1 + 2c after step c's waits (diagonal step: after the factor), 2 + 2c at
-// step c's end.
+// step c's end; diagonal rows' last solve step (c = r - 1): 17 inverse staged,
+// 18 solve GEMM done, 19 SYRK done and published.
 constexpr int kPfDbgSlots = 20;
 
+// Tile staging global -> LDS S[i * kPfLd + j] with every load of the tile
+// in flight before the first LDS store (16 per thread, 256 threads): a
+// load-then-store loop waits one memory round trip per element (32 KB: 3.9
+// vs 0.4 us hot, profiles/r3_tile_probe.txt).  Column-major source: element
+// (i, j) at src[j * ld + i], rows clamped to h and columns to w, zero outside.
+struct PfStage {
+  double v[16];
+  __device__ __forceinline__ void load_cm(const double* __restrict__ src, size_t ld, int h, int w) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = threadIdx.x + 256 * q, i = e & 63, j = e >> 6;
+      v[q] = src[(size_t)min(j, w - 1) * ld + min(i, h - 1)];
+    }
+  }
+  __device__ __forceinline__ void store_cm(double* S, int h, int w) const {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = threadIdx.x + 256 * q, i = e & 63, j = e >> 6;
+      S[i * kPfLd + j] = (i < h && j < w) ? v[q] : 0.0;
+    }
+  }
+  // row-major source with leading dimension 64 (the published inverses)
+  __device__ __forceinline__ void load_rm(const double* __restrict__ src) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = src[threadIdx.x + 256 * q];
+  }
+  __device__ __forceinline__ void store_rm(double* S) const {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = threadIdx.x + 256 * q;
+      S[(e >> 6) * kPfLd + (e & 63)] = v[q];
+    }
+  }
+};
+
+// Hand-off store of the panel's published tiles: WT (write-through) = a
+// relaxed agent-scope 8-byte atomic store (global_store sc1), drained by
+// s_waitcnt vmcnt(0) before the flag, no release fence (the publish costs
+// 0.84 vs 2.84 us per 32 KB, profiles/r3_tile_probe.txt); else a plain store
+// behind __threadfence().
+template <bool WT>
+__device__ __forceinline__ void pf_st(double* p, double v) {
+  if (WT)
+    __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)p,
+                       (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+template <bool WT>
+__device__ __forceinline__ void pf_drain() {
+  if (WT)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else
+    __threadfence();
+}
+
+// FV: 64x64 tile factor pf_chol_inv_fast, 1 sqrt + divide pivots, 2 rsq
+// pivots; WT: pf_st
+template <int FV, bool WT>
 __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ A, int lda, int kb, int mrows,
                                                            int* __restrict__ info, double* __restrict__ linv,
                                                            unsigned* ctrl, unsigned base, unsigned epoch,
-                                                           int nbw, unsigned* err, unsigned limit,
+                                                           unsigned* err, unsigned limit,
                                                            unsigned long long* dbg = nullptr) {
   __shared__ double T[64 * kPfLd];   // staging / factor tile (row-major padded)
   __shared__ double Li[64 * kPfLd];  // a diagonal tile's inverse (own, or workgroup c's)
@@ -851,8 +881,10 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
   };
   stamp(0);
   // the panel's info starts at 0 (row tile 0 clears it before its first
-  // release; every other write follows one of its flags)
-  if (r == 0 && threadIdx.x == 0) *info = 0;
+  // publish; every other write follows one of its flags).  An agent-scope
+  // store: with write-through publishes no release fence writes back a plain
+  // store's dirty line, which could then land after another workgroup's CAS
+  if (r == 0 && threadIdx.x == 0) __hip_atomic_store(info, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int r0 = pf_row0(r, kb, nc), hr = pf_rows(r, kb, nc, mrows);
   const int cmax = min(r, nc - 1);
   const bool diag_row = r < nc;
@@ -879,72 +911,55 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
       }
   }
   if (!diag_row) {
-    // below the diagonal block: this workgroup owns up to kPfRows row tiles
-    // (r, r + nbw, ...), so the launch occupies few CUs beside the
-    // look-ahead's trailing dgemm; each L_ck and Linv_cc is staged in LDS once
-    // for all of them
-    const int nr = nc + (mrows - kb + 63) / 64;
-    int rr[kPfRows], h[kPfRows];
-#pragma unroll
-    for (int j = 0; j < kPfRows; ++j) {
-      rr[j] = r + j * nbw;
-      h[j] = (rr[j] < nr && j * nbw < nr - nc) ? pf_rows(rr[j], kb, nc, mrows) : 0;
-    }
+    // below the diagonal block: one 64-row tile per workgroup, left-looking
+    // over the panel's column tiles (L_ck staged with L_rk per update)
     for (int c = 0; c < nc; ++c) {
       const int c0 = 64 * c, wc = min(64, kb - c0);
-      pf_dvec4 acc[kPfRows][4];
+      pf_dvec4 acc[4];
 #pragma unroll
-      for (int j = 0; j < kPfRows; ++j) {
-        const int row0 = pf_row0(rr[j], kb, nc), hj = max(h[j], 1);
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int i = 16 * wv + 4 * q + kq, jj = 16 * t + m;
-            const double v = h[j] > 0 ? A[(size_t)(c0 + min(jj, wc - 1)) * lda + row0 + min(i, hj - 1)] : 0.0;
-            acc[j][t][q] = (i < h[j] && jj < wc) ? v : 0.0;
-          }
-      }
+        for (int q = 0; q < 4; ++q) {
+          const int i = 16 * wv + 4 * q + kq, jj = 16 * t + m;
+          const double v = A[(size_t)(c0 + min(jj, wc - 1)) * lda + r0 + min(i, hr - 1)];
+          acc[t][q] = (i < hr && jj < wc) ? v : 0.0;
+        }
       for (int k = 0; k < c; ++k) {
         pf_wait(flag + c * kPfMaxTiles + k, epoch, err, limit);
-        // L_ck (rows of column tile c, columns of tile k) staged once
-        for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-          const int i = e & 63, kk = e >> 6;
-          const double v = A[(size_t)(64 * k + kk) * lda + c0 + min(i, wc - 1)];
-          Li[i * kPfLd + kk] = i < wc ? v : 0.0;
+        {
+          PfStage sc, sr;
+          sc.load_cm(A + (size_t)64 * k * lda + c0, lda, wc, 64);
+          sr.load_cm(A + (size_t)64 * k * lda + r0, lda, hr, 64);
+          sc.store_cm(Li, wc, 64);
+          sr.store_cm(T, hr, 64);
         }
         __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kPfRows; ++j)
-          if (h[j] > 0)
-            pf_gemm_nt(acc[j], -1.0, gtile(pf_row0(rr[j], kb, nc), h[j], 64 * k, 64), ltile(Li), wv, lane);
+        pf_gemm_nt(acc, -1.0, ltile(T), ltile(Li), wv, lane);
         __syncthreads();
       }
       pf_wait(flag + c * kPfMaxTiles + c, epoch, err, limit);
       stamp(1 + 2 * c);
-      const double* lc = linv + (size_t)c * 64 * 64;
-      for (int e = threadIdx.x; e < 64 * 64; e += 256) Li[(e >> 6) * kPfLd + (e & 63)] = lc[e];
+      {
+        PfStage sl;
+        sl.load_rm(linv + (size_t)c * 64 * 64);
+        sl.store_rm(Li);
+      }
+      pf_acc_to_lds(acc, T, wv, lane);
+      __syncthreads();
+      pf_dvec4 out[4];
 #pragma unroll
-      for (int j = 0; j < kPfRows; ++j) {
-        if (h[j] <= 0) continue;
-        pf_acc_to_lds(acc[j], T, wv, lane);
-        __syncthreads();
-        pf_dvec4 out[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) out[t] = pf_dvec4{0.0, 0.0, 0.0, 0.0};
-        pf_gemm_nt(out, 1.0, ltile(T), ltile(Li), wv, lane);
-        __syncthreads();
-        const int row0 = pf_row0(rr[j], kb, nc);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int i = 16 * wv + 4 * q + kq, jj = 16 * t + m;
-            if (i < h[j] && jj < wc) A[(size_t)(c0 + jj) * lda + row0 + i] = out[t][q];
-          }
+      for (int t = 0; t < 4; ++t) out[t] = pf_dvec4{0.0, 0.0, 0.0, 0.0};
+      pf_gemm_nt_lt(out, 1.0, ltile(T), ltile(Li), wv, lane);
+      __syncthreads();
+      // through T: each wave stores whole 512-byte column segments
+      pf_acc_to_lds(out, T, wv, lane);
+      __syncthreads();
+      for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+        const int i = e & 63, jj = e >> 6;
+        if (i < hr && jj < wc) A[(size_t)(c0 + jj) * lda + r0 + i] = T[i * kPfLd + jj];
       }
       stamp(2 + 2 * c);
-      __syncthreads();  // Li is restaged next step
+      __syncthreads();  // T and Li are restaged next step
     }
     return;
   }
@@ -962,39 +977,51 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
         }
       for (int k = 0; k < c; ++k) {
         pf_wait(flag + c * kPfMaxTiles + k, epoch, err, limit);
-        pf_gemm_nt(acc, -1.0, gtile(r0, hr, 64 * k, 64), gtile(c0, wc, 64 * k, 64), wv, lane);
+        // L_rk and L_ck staged together (all loads in flight), LDS GEMM
+        {
+          PfStage sr, sc;
+          sr.load_cm(A + (size_t)64 * k * lda + r0, lda, hr, 64);
+          sc.load_cm(A + (size_t)64 * k * lda + c0, lda, wc, 64);
+          sr.store_cm(T, hr, 64);
+          sc.store_cm(Li, wc, 64);
+        }
+        __syncthreads();
+        pf_gemm_nt(acc, -1.0, ltile(T), ltile(Li), wv, lane);
+        __syncthreads();
       }
       pf_wait(flag + c * kPfMaxTiles + c, epoch, err, limit);
       stamp(1 + 2 * c);
       // L_rc = T Linv_cc' (Linv_cc row-major in linv, staged in LDS)
       pf_acc_to_lds(acc, T, wv, lane);
-      const double* lc = linv + (size_t)c * 64 * 64;
-#pragma unroll
-      for (int e = threadIdx.x; e < 64 * 64; e += 256) Li[(e >> 6) * kPfLd + (e & 63)] = lc[e];
+      {
+        PfStage sl;
+        sl.load_rm(linv + (size_t)c * 64 * 64);
+        sl.store_rm(Li);
+      }
       __syncthreads();
+      if (c == r - 1) stamp(17);
       pf_dvec4 out[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) out[t] = pf_dvec4{0.0, 0.0, 0.0, 0.0};
-      pf_gemm_nt(out, 1.0, ltile(T), ltile(Li), wv, lane);
+      pf_gemm_nt_lt(out, 1.0, ltile(T), ltile(Li), wv, lane);
       __syncthreads();  // every wave is done reading T
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = 16 * wv + 4 * q + kq, j = 16 * t + m;
-          if (i < hr && j < wc) A[(size_t)(c0 + j) * lda + r0 + i] = out[t][q];
-        }
-      if (diag_row) {
-        // publish L_rc, and fold it into the diagonal tile: A_rr -= L_rc L_rc'
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0)
-          __hip_atomic_store(flag + r * kPfMaxTiles + c, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        pf_acc_to_lds(out, T, wv, lane);
-        __syncthreads();
-        pf_gemm_nt(dacc, -1.0, ltile(T), ltile(T), wv, lane);
-        __syncthreads();
+      // L_rc through T (whole column segments per store): its stores are
+      // issued, folded into the diagonal tile (A_rr -= L_rc L_rc') while they
+      // drain, then published (its consumers first need this row's factor)
+      pf_acc_to_lds(out, T, wv, lane);
+      __syncthreads();
+      if (c == r - 1) stamp(18);
+      for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+        const int i = e & 63, j = e >> 6;
+        if (i < hr && j < wc) pf_st<WT>(A + (size_t)(c0 + j) * lda + r0 + i, T[i * kPfLd + j]);
       }
+      pf_gemm_nt(dacc, -1.0, ltile(T), ltile(T), wv, lane);
+      pf_drain<WT>();
+      __syncthreads();
+      if (threadIdx.x == 0)
+        __hip_atomic_store(flag + r * kPfMaxTiles + c, epoch, WT ? __ATOMIC_RELAXED : __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      if (c == r - 1) stamp(19);
       stamp(2 + 2 * c);
       continue;
     }
@@ -1002,19 +1029,25 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
     pf_acc_to_lds(dacc, T, wv, lane);
     __syncthreads();
     // factor + inverse by 16x16 blocks (Lc: pivot columns + per-wave scratch)
-    const int bad = pf_chol_inv_blocked(T, Li, Lc, dinv, lane, wv);
+    const int bad = FV == 2 ? pf_chol_inv_fast<true>(T, Li, Lc, dinv, lane, wv)
+                            : pf_chol_inv_fast<false>(T, Li, Lc, dinv, lane, wv);
     stamp(1 + 2 * c);
+    // publish the inverse's lower blocks (row-major, ld 64: the only part
+    // its consumers read); the factor tile itself is read by no workgroup of
+    // this launch and is stored after the flag
     double* lo = linv + (size_t)c * 64 * 64;
+    for (int e = threadIdx.x; e < 64 * 64; e += 256)
+      if (((e & 63) >> 4) <= (e >> 10)) pf_st<WT>(lo + e, Li[(e >> 6) * kPfLd + (e & 63)]);
+    if (threadIdx.x == 0 && bad != 0 && bad <= wc) atomicCAS(info, 0, c0 + bad);
+    pf_drain<WT>();
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(flag + r * kPfMaxTiles + r, epoch, WT ? __ATOMIC_RELAXED : __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
     for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-      lo[e] = Li[(e >> 6) * kPfLd + (e & 63)];  // row-major, ld 64
       const int i = e & 63, j = e >> 6;
       if (i < wc && j < wc && i >= j) A[(size_t)(c0 + j) * lda + c0 + i] = T[i * kPfLd + j];
     }
-    if (threadIdx.x == 0 && bad != 0 && bad <= wc) atomicCAS(info, 0, c0 + bad);
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store(flag + r * kPfMaxTiles + r, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     stamp(2 + 2 * c);
   }
 }
@@ -1165,9 +1198,7 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   const int mrows = n - k;
   const int nc = (kb + 63) / 64;
   const int nbelow = (mrows - kb + 63) / 64;
-  const int rows = std::max(1, std::min(kPfRows, ws->pf_rows));
-  const int nbw = (nbelow + rows - 1) / rows;  // below-diagonal workgroups
-  const int nr = nc + nbw;                           // workgroups (tickets) of the launch
+  const int nr = nc + nbelow;  // workgroups (tickets) of the launch: one per row tile
   if (ws->pf_base > 0x7fffffffu || ws->pf_epoch > 0xfffffff0u) {
     if (hipMemsetAsync(ws->pf_ctrl, 0, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles), s) != hipSuccess)
       return rocblas_status_internal_error;
@@ -1175,8 +1206,10 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
     ws->pf_epoch = 0;
   }
   const unsigned epoch = ++ws->pf_epoch;
-  hipLaunchKernelGGL(panel_factor_kernel, dim3(nr), dim3(256), 0, s, A + k + (size_t)k * lda, lda, kb, mrows, info,
-                     ws->pf_linv, ws->pf_ctrl, ws->pf_base, epoch, nbw, ws->err, ws->spin_limit, nullptr);
+  auto kern = ws->tile_factor == 2 ? (ws->write_through ? panel_factor_kernel<2, true> : panel_factor_kernel<2, false>)
+                                   : (ws->write_through ? panel_factor_kernel<1, true> : panel_factor_kernel<1, false>);
+  hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, s, A + k + (size_t)k * lda, lda, kb, mrows, info, ws->pf_linv,
+                     ws->pf_ctrl, ws->pf_base, epoch, ws->err, ws->spin_limit, nullptr);
   ws->pf_base += (unsigned)nr;
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
@@ -1390,7 +1423,8 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   if (c.own_diag == 6 && (c.panel <= 0 || c.panel > 64 * kPfMaxTiles)) c.own_diag = 2;
   if (c.own_diag == 7 && (c.panel <= 0 || c.panel > kTinv)) c.own_diag = 2;
   if (ws) {
-    ws->pf_rows = c.panel_rows;
+    ws->tile_factor = c.tile_factor;
+    ws->write_through = c.write_through;
     ws->spin_limit = c.spin_log2 <= 0 ? 0u : (1u << std::min(c.spin_log2, 30));
   }
   double* scratch = ws ? ws->scratch : nullptr;

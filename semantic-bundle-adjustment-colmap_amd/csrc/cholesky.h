@@ -46,9 +46,15 @@ struct CholConfig {
   // default 6: 21.5 vs 25.0 ms at nf = 12 000 (profiles/r2_ab_own_diag.jsonl; 16x16-blocked
   // MFMA factor + inverse per diagonal tile, profiles/r2_panel_probe_v3.txt)
   int own_diag = 6;
-  // own_diag 6: row tiles per below-diagonal workgroup (1..4; fewer CUs held
-  // beside the trailing dgemm vs a longer left-looking update per workgroup)
-  int panel_rows = 1;
+  // own_diag 6: the diagonal tiles' 64x64 factor + inverse (block columns by
+  // register sweeps, pf_chol_inv_fast): 2 pivots by rsq + two Goldschmidt
+  // steps (~1 ulp), 1 correctly rounded sqrt + divide.  2 (default): Cholesky
+  // 17.3 vs 17.7 ms at nf = 12 000; the previous per-pivot LDS-exchange
+  // factor (36 us per tile, 22 ms) is gone (profiles/r3_tile_probe.txt).
+  int tile_factor = 2;
+  // own_diag 6: published tiles stored write-through (sc1) and drained before
+  // the flag, instead of plain stores + __threadfence()
+  bool write_through = true;
   // chol_solve variant: 2 sync-free sweeps (one launch per direction), 1 one
   // launch per 64-wide block column with diagonal-block inverses, 0 recursive
   // rocBLAS dtrsv / dgemv
@@ -84,7 +90,8 @@ struct CholWorkspace {
   double* pf_linv = nullptr;    // [8][64*64] inverses of the panel's diagonal tiles
   unsigned pf_base = 0;         // tickets handed out so far
   unsigned pf_epoch = 0;        // flag value of the last panel launch
-  int pf_rows = 1;              // row tiles per below-diagonal workgroup (CholConfig::panel_rows)
+  int tile_factor = 2;          // CholConfig::tile_factor
+  bool write_through = false;   // CholConfig::write_through
   int linv_rows = 0;
   double* tinv = nullptr;       // own_diag 7: [512*512] inverse of the panel's diagonal block
   double* tbuf = nullptr;       // own_diag 7: [max_n * 512] copy of the panel below it

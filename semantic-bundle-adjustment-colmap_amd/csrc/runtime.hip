@@ -1506,12 +1506,16 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.solve = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_panel_rows") == 0 && value >= 1 && value <= 4) {
-    ctx->chol.panel_rows = value;
-    return MI_BA_OK;
-  }
   if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 3) {
     ctx->chol.rest_update = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_tile_factor") == 0 && (value == 1 || value == 2)) {
+    ctx->chol.tile_factor = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_write_through") == 0 && (value == 0 || value == 1)) {
+    ctx->chol.write_through = value != 0;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_spin_log2") == 0 && value >= 0 && value <= 30) {

@@ -209,24 +209,6 @@ def test_lm_lookahead_on_off(gpu, images):
     assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
 
 
-def test_lm_panel_rows(gpu):
-    """The one-launch panel factor with 1, 2 and 4 row tiles per
-    below-diagonal workgroup drives the same LM (nf = 1593: 4 panels, ragged
-    row counts per workgroup)."""
-    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
-                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
-    opts = mi_ba.default_options(max_num_iterations=10)
-    res = []
-    for rows in (1, 2, 4):
-        with mi_ba.Context(opts, sc.copy()) as ctx:
-            ctx.set_tuning("cholesky_panel_rows", rows)
-            res.append(ctx.solve())
-    b = res[0]
-    for a in res[1:]:
-        assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
-        assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
-
-
 def test_factor_at_c4_size_matches_lapack(gpu):
     """nf = 11 993, the C4 reduced camera system (998 * 6 + 5 + 1000 * 6): the
     default factorisation the bench times (24 panels of 512, one-launch panel
@@ -247,3 +229,25 @@ def test_factor_at_c4_size_matches_lapack(gpu):
     assert np.abs(L - L_ref).max() <= 1e-12 * scale
     x_ref = cho_solve((c, low), b, check_finite=False)
     assert np.abs(x - x_ref).max() <= 1e-10 * np.abs(x_ref).max()
+
+
+def test_lm_tile_factor_and_publish(gpu):
+    """The panel factor's 64x64 tile factor (block-column register sweeps
+    with rsq (2) or sqrt + divide (1) pivots) and its publish (write-through
+    sc1 stores drained before the flag vs plain stores + __threadfence())
+    drive the same LM (nf = 1593: 4 panels), all four combinations."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for tf in (2, 1):
+        for wt in (1, 0):
+            with mi_ba.Context(opts, sc.copy()) as ctx:
+                ctx.set_tuning("cholesky_tile_factor", tf)
+                ctx.set_tuning("cholesky_write_through", wt)
+                res.append(ctx.solve())
+    b = res[0]
+    for a in res[1:]:
+        assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
+        assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
+

@@ -31,6 +31,11 @@ def analyze(path):
         a[1] += 1
     for (k, q), (t, c) in sorted(fam.items(), key=lambda x: -x[1][0]):
         print(f"  q{q} {t:8.3f} ms {c:5d}  {k}")
+    # sequence: every kernel (start, duration) relative to t0, grouped by queue
+    if "--seq" in sys.argv:
+        for s_, e_, n_, q_ in ts:
+            k = "dgemm" if n_.startswith("Cijk") else n_.split("(")[0].replace("void ", "")[-32:]
+            print(f"  q{q_} {(s_ - t0) / 1e3:9.1f} us +{(e_ - s_) / 1e3:8.1f} us  {k}")
     # busy union per queue
     for q in sorted(set(t[3] for t in ts)):
         iv = sorted((s, e) for s, e, n, qq in ts if qq == q)

@@ -1,7 +1,8 @@
 // Phase timeline of one panel_factor_kernel launch (csrc/cholesky.cpp,
 // own_diag 6) on the first 512-wide panel of an nf = 12 000 SPD matrix:
 // wall_clock64() stamps per row tile (kernel's dbg buffer).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/panel_probe.cpp -lrocsolver -lrocblas -o tools/panel_probe.bin
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/panel_probe.cpp -lrocsolver -lrocblas -o tools/probes/panel_probe.bin
+//   tools/probes/panel_probe.bin [n] [tile_factor] [write_through]
 #include "../../semantic-bundle-adjustment-colmap_amd/csrc/cholesky.cpp"
 
 #include <cstdio>
@@ -22,9 +23,10 @@ int main(int argc, char** argv) {
   unsigned long long* dbg;
   hipMalloc(&A, 8ull * n * n);
   hipMalloc(&info, 64);
-  const int prow = argc > 2 ? atoi(argv[2]) : 1;
-  const int nbw = ((n - kb + 63) / 64 + prow - 1) / prow;
-  const int nr = 8 + nbw;
+  const int fv = argc > 2 ? atoi(argv[2]) : 2;  // tile factor: 2 rsq, 1 sqrt pivots
+  const int wt = argc > 3 ? atoi(argv[3]) : 1;  // write-through publish
+  printf("n %d, tile_factor %d, write_through %d\n", n, fv, wt);
+  const int nr = 8 + (n - kb + 63) / 64;
   hipMalloc(&dbg, 8ull * nr * kPfDbgSlots);
   CholWorkspace ws;
   ws.create(0, (n + 511) / 512, n);
@@ -38,8 +40,10 @@ int main(int argc, char** argv) {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     hipEventRecord(e0, 0);
-    hipLaunchKernelGGL(panel_factor_kernel, dim3(nr), dim3(256), 0, 0, A, n, kb, n, info, ws.pf_linv, ws.pf_ctrl,
-                       ws.pf_base, epoch, nbw, dbg);
+    auto kern = fv == 2 ? (wt ? panel_factor_kernel<2, true> : panel_factor_kernel<2, false>)
+                        : (wt ? panel_factor_kernel<1, true> : panel_factor_kernel<1, false>);
+    hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, 0, A, n, kb, n, info, ws.pf_linv, ws.pf_ctrl, ws.pf_base, epoch,
+                       ws.err, ws.spin_limit, dbg);
     hipEventRecord(e1, 0);
     hipEventSynchronize(e1);
     ws.pf_base += nr;

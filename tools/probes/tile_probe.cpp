@@ -1,6 +1,7 @@
 // Phase costs inside one 256-thread workgroup for the panel factor's
 // building blocks (csrc/cholesky.cpp): 64x64 tile load global -> LDS, the
-// in-LDS factor + inverse (pf_chol_inv_blocked), a 64x64x64 MFMA GEMM with
+// in-LDS factor + inverse (pf_chol_inv_fast, sqrt / rsq pivots, with phase
+// stamps), a 64x64x64 MFMA GEMM with
 // LDS operands and with global operands (gtile-style loads), and the publish
 // of a 32 KB tile by plain stores + __threadfence() vs sc1 (write-through)
 // stores + vmcnt(0).  Stamps: wall_clock64 (100 MHz) and clock64 (cycles).
@@ -13,10 +14,11 @@
 using namespace miba;
 
 constexpr int kReps = 8;
-constexpr int kPhases = 7;
+constexpr int kPhases = 10;
 
+template <int V>
 __global__ __launch_bounds__(256) void tile_probe_kernel(double* __restrict__ A, int lda, double* __restrict__ out,
-                                                         unsigned long long* __restrict__ st) {
+                                                         unsigned long long* __restrict__ st, double* __restrict__ res) {
   __shared__ double T[64 * kPfLd];
   __shared__ double Li[64 * kPfLd];
   __shared__ double Lc[64 * 64];
@@ -45,8 +47,15 @@ __global__ __launch_bounds__(256) void tile_probe_kernel(double* __restrict__ A,
     __syncthreads();
     w[1] = wall_clock64(); c[1] = clock64();
     // 1: factor + inverse in LDS
-    const int bad = pf_chol_inv_blocked(T, Li, Lc, dinv, lane, wv);
+    long long* sub = (long long*)(st + (size_t)kReps * kPhases * 2) + rep * 10;
+    const int bad = V == 1 ? pf_chol_inv_fast<false>(T, Li, Lc, dinv, lane, wv, blockIdx.x == 0 ? sub : nullptr)
+                           : pf_chol_inv_fast<true>(T, Li, Lc, dinv, lane, wv, blockIdx.x == 0 ? sub : nullptr);
     __syncthreads();
+    if (rep == kReps - 1 && blockIdx.x == 0)
+      for (int e = threadIdx.x; e < 4096; e += 256) {
+        res[e] = T[(e >> 6) * kPfLd + (e & 63)];
+        res[4096 + e] = Li[(e >> 6) * kPfLd + (e & 63)];
+      }
     w[2] = wall_clock64(); c[2] = clock64();
     // 2: GEMM with LDS operands: out = T Li'
     pf_dvec4 o[4];
@@ -79,6 +88,51 @@ __global__ __launch_bounds__(256) void tile_probe_kernel(double* __restrict__ A,
     for (int e = threadIdx.x; e < 4096; e += 256) Li[(e >> 6) * kPfLd + (e & 63)] = src[e];
     __syncthreads();
     w[7] = wall_clock64(); c[7] = clock64();
+    // 7: the same staging with 16-byte loads, all eight per thread in flight
+    {
+      const sweep_dvec2* src2 = reinterpret_cast<const sweep_dvec2*>(src);
+      sweep_dvec2 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = src2[threadIdx.x + 256 * j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = 2 * (threadIdx.x + 256 * j);
+        Li[(e >> 6) * kPfLd + (e & 63)] = v[j].x;
+        Li[(e >> 6) * kPfLd + (e & 63) + 1] = v[j].y;
+      }
+    }
+    __syncthreads();
+    w[8] = wall_clock64(); c[8] = clock64();
+    // 8: GEMM with global operands on cold tiles (a different pair per rep, per workgroup)
+    {
+      const int cc = 64 * (1 + rep + kReps * blockIdx.x);
+      pf_gemm_nt(o, -1.0, gtile(cc, 0), gtile(cc + 64 * kReps * 8, 0), wv, lane);
+    }
+    __syncthreads();
+    w[9] = wall_clock64(); c[9] = clock64();
+    // 9: stage two cold 64x64 column-major tiles (16-byte loads in flight) + LDS GEMM
+    {
+      const int cc = 64 * (1 + rep + kReps * blockIdx.x) + 64 * kReps * 16;
+      sweep_dvec2 v[16];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = 2 * (threadIdx.x + 256 * j);  // column e >> 6, rows e & 63, e & 63 + 1
+        v[j] = *reinterpret_cast<const sweep_dvec2*>(A + (size_t)(e >> 6) * lda + cc + (e & 63));
+        v[8 + j] = *reinterpret_cast<const sweep_dvec2*>(A + (size_t)(e >> 6) * lda + cc + 64 * kReps * 8 + (e & 63));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = 2 * (threadIdx.x + 256 * j);
+        T[(e & 63) * kPfLd + (e >> 6)] = v[j].x;
+        T[((e & 63) + 1) * kPfLd + (e >> 6)] = v[j].y;
+        Li[(e & 63) * kPfLd + (e >> 6)] = v[8 + j].x;
+        Li[((e & 63) + 1) * kPfLd + (e >> 6)] = v[8 + j].y;
+      }
+      __syncthreads();
+      pf_gemm_nt(o, -1.0, ltile(T), ltile(Li), wv, lane);
+    }
+    __syncthreads();
+    w[10] = wall_clock64(); c[10] = clock64();
     sink += (double)bad + o[0][0] + Li[lane];
     if (threadIdx.x == 0 && blockIdx.x == 0)
       for (int k = 0; k < kPhases; ++k) {
@@ -90,7 +144,7 @@ __global__ __launch_bounds__(256) void tile_probe_kernel(double* __restrict__ A,
 }
 
 int main() {
-  const int n = 512;
+  const int n = 64 * (1 + kReps * 8) + 64 * kReps * 24;
   std::vector<double> h((size_t)n * n);
   for (int j = 0; j < n; ++j)
     for (int i = 0; i < n; ++i) h[(size_t)j * n + i] = (i == j) ? 64.0 : 0.01 * sin(0.37 * (i + j));
@@ -98,17 +152,26 @@ int main() {
   unsigned long long* st;
   hipMalloc(&A, 8ull * n * n);
   hipMalloc(&out, 8ull * 2 * 4096 * 64);
-  hipMalloc(&st, 8ull * kReps * kPhases * 2);
+  hipMalloc(&st, 8ull * kReps * kPhases * 2 + 8ull * kReps * 10);
+  double* res;
+  hipMalloc(&res, 8ull * 4 * 2 * 4096);
   hipMemcpy(A, h.data(), 8ull * n * n, hipMemcpyHostToDevice);
-  const char* names[kPhases] = {"load tile -> LDS", "chol+inv (pf_chol_inv_blocked)", "gemm LDS operands",
+  const char* names[kPhases] = {"load tile -> LDS", "chol+inv", "gemm LDS operands",
                                 "gemm global operands", "publish 32KB plain + threadfence",
-                                "publish 32KB sc1 + vmcnt", "stage 32KB global -> LDS"};
-  for (int grid : {1, 8}) {
-    hipLaunchKernelGGL(tile_probe_kernel, dim3(grid), dim3(256), 0, 0, A, n, out, st);
+                                "publish 32KB sc1 + vmcnt", "stage 32KB global -> LDS",
+                                "stage 32KB 16B loads in flight", "gemm global operands, cold tiles",
+                                "stage 2 cold tiles (16B) + LDS gemm"};
+  for (int cfg = 2; cfg < 6; ++cfg) {
+    const int grid = cfg & 1 ? 8 : 1, V = cfg >> 1;
+    if (V == 1)
+      hipLaunchKernelGGL(tile_probe_kernel<1>, dim3(grid), dim3(256), 0, 0, A, n, out, st, res + 8192);
+    else
+      hipLaunchKernelGGL(tile_probe_kernel<2>, dim3(grid), dim3(256), 0, 0, A, n, out, st, res + 16384);
     hipDeviceSynchronize();
     std::vector<unsigned long long> s((size_t)kReps * kPhases * 2);
     hipMemcpy(s.data(), st, 8 * s.size(), hipMemcpyDeviceToHost);
-    printf("grid %d (workgroup 0), per phase: min / median over %d reps  [us, cycles]\n", grid, kReps);
+    printf("%s, grid %d (workgroup 0), per phase: min / median over %d reps  [us, cycles]\n",
+           V == 1 ? "pf_chol_inv_fast<sqrt>" : "pf_chol_inv_fast<rsq>", grid, kReps);
     for (int k = 0; k < kPhases; ++k) {
       std::vector<double> us, cy;
       for (int r = 1; r < kReps; ++r) {
@@ -120,6 +183,40 @@ int main() {
       printf("  %-36s %8.2f / %8.2f us   %9.0f / %9.0f cyc\n", names[k], us[0], us[us.size() / 2], cy[0],
              cy[cy.size() / 2]);
     }
+    {
+      std::vector<long long> sub(kReps * 10);
+      hipMemcpy(sub.data(), st + (size_t)kReps * kPhases * 2, 8 * sub.size(), hipMemcpyDeviceToHost);
+      const long long* q = sub.data() + (kReps - 1) * 10;
+      printf("  factor sub-phases (last rep, cycles from the first stamp): ");
+      for (int k = 1; k < 10; ++k) printf(" %lld", q[k] - q[0]);
+      printf("\n    (sweep kb0 | upd0 sweep1 upd1 sweep2 upd2 sweep3 upd3 last diag-inv, inverse)\n");
+    }
+  }
+  // L and X of both variants vs a host Cholesky of the same tile
+  std::vector<double> r(8 * 4096);
+  hipMemcpy(r.data(), res, 8ull * r.size(), hipMemcpyDeviceToHost);
+  std::vector<double> L(4096, 0.0);
+  for (int j = 0; j < 64; ++j) {
+    double s = h[(size_t)j * n + j];
+    for (int k = 0; k < j; ++k) s -= L[j * 64 + k] * L[j * 64 + k];
+    L[j * 64 + j] = sqrt(s);
+    for (int i = j + 1; i < 64; ++i) {
+      double v = h[(size_t)j * n + i];
+      for (int k = 0; k < j; ++k) v -= L[i * 64 + k] * L[j * 64 + k];
+      L[i * 64 + j] = v / L[j * 64 + j];
+    }
+  }
+  for (int V = 1; V < 3; ++V) {
+    double el = 0.0, ex = 0.0;
+    for (int i = 0; i < 64; ++i)
+      for (int j = 0; j < 64; ++j) {
+        if (j <= i) el = std::max(el, fabs(r[V * 8192 + i * 64 + j] - L[i * 64 + j]));
+        double lx = 0.0;  // (L X)_ij - I
+        for (int k = 0; k < 64; ++k)  // X's strict upper blocks are not stored
+          if ((j >> 4) <= (k >> 4)) lx += L[i * 64 + k] * r[V * 8192 + 4096 + k * 64 + j];
+        ex = std::max(ex, fabs(lx - (i == j ? 1.0 : 0.0)));
+      }
+    printf("variant %d: max |L - L_host| %.3e, max |L X - I| %.3e\n", V, el, ex);
   }
   return 0;
 }
