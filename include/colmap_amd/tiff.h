@@ -66,6 +66,8 @@ inline std::vector<uint32_t> EntryValues(const File& f, size_t e) {
   const size_t size = type == 3 ? 2 : type == 4 ? 4 : 0;
   if (size == 0) return {};
   const size_t base = (size * count <= 4) ? e + 8 : f.U32(e + 8);
+  // bounds first: a hostile count must not size the allocation
+  if ((uint64_t)base + (uint64_t)size * count > f.d.size()) Fail("truncated");
   std::vector<uint32_t> v(count);
   for (uint32_t k = 0; k < count; ++k) v[k] = size == 2 ? f.U16(base + 2 * k) : f.U32(base + 4 * k);
   return v;
@@ -96,6 +98,7 @@ inline std::vector<uint8_t> Lzw(const uint8_t* in, size_t n, size_t expect) {
       continue;
     }
     std::vector<uint8_t> entry;
+    if (prev >= 0 && dict.size() >= 4096) Fail("bad LZW code");  // 12-bit table full without a Clear
     if (code < dict.size()) {
       entry = dict[code];
       if (prev >= 0) {
@@ -111,6 +114,7 @@ inline std::vector<uint8_t> Lzw(const uint8_t* in, size_t n, size_t expect) {
       Fail("bad LZW code");
     }
     out.insert(out.end(), entry.begin(), entry.end());
+    if (out.size() >= expect) break;  // the block's bytes are complete: no unbounded output
     prev = (int)code;
     if (dict.size() + 1 >= (1u << width) && width < 12) ++width;
   }
@@ -241,6 +245,7 @@ inline std::vector<float> MatrixFromTiff(const std::string& path, int* height, i
     std::memcpy(&x, &v, 4);
     return x;
   };
+  if ((uint64_t)W * H > (1ull << 28)) Fail("size");  // 1 GB of float32 at most
   std::vector<float> out((size_t)W * H);
   if (tag.count(322)) {  // tiles
     const uint32_t tw = one(322, 0), th = one(323, 0);
@@ -260,6 +265,7 @@ inline std::vector<float> MatrixFromTiff(const std::string& path, int* height, i
       }
   } else {  // strips
     const uint32_t rps = std::min<uint32_t>(one(278, H), H);
+    if (rps == 0) Fail("RowsPerStrip");
     const auto& offs = tag[273];
     const auto& lens = tag[279];
     const uint32_t nstrips = (H + rps - 1) / rps;

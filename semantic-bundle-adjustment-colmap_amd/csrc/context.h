@@ -85,6 +85,7 @@ struct mi_ba_context {
   int64_t npv = 0;
   int64_t nb_const = 0;  // reduced blocks of constant points
   bool lin_overlap = false;            // semantic kernel on lin_side beside the reprojection kernel
+  int lin_order = 0;                   // 0 reprojection kernel first, 1 semantic pass first
   hipStream_t lin_side = nullptr;
   hipEvent_t lin_ev[2] = {nullptr, nullptr};
   int sem_diag = 0;      // "semantic_diag" 1: downloaded status is offset by +0x1000 for samples the flat test deferred

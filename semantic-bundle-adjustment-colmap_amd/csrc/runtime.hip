@@ -579,13 +579,20 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     if (st != MI_BA_OK) return st;
     MI_HIP(hipEventRecord(ctx->lin_ev[1], ctx->lin_side));
   }
+  // lin_order: 0 reprojection then semantic, 1 semantic first (A/B of the
+  // reprojection kernel's in-step time after the semantic gathers)
+  const bool sem_first = ctx->sem && !overlap && ctx->lin_order == 1;
+  if (sem_first) {
+    mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
+    if (st != MI_BA_OK) return st;
+  }
   timer_begin(ctx, "reproj_jacobian", &stop);
   launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->partial.ptr, s);
   timer_end(ctx, stop);
   if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s);
   if (overlap) {
     MI_HIP(hipStreamWaitEvent(s, ctx->lin_ev[1], 0));
-  } else if (ctx->sem) {
+  } else if (ctx->sem && !sem_first) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
   }
@@ -1472,6 +1479,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   if (!ctx || !key) return MI_BA_ERR_INVALID_ARGUMENT;
   if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 63) {
     ctx->dev.jvariant = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "linearize_order") == 0 && (value == 0 || value == 1)) {
+    ctx->lin_order = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "linearize_overlap") == 0 && (value == 0 || value == 1)) {

@@ -116,6 +116,60 @@ def test_tiff_rejects_non_float32(exe, tmp_path):
     assert got is None and "Error loading depth map" in msg
 
 
+def patch_ifd(src, dst, tag, count=None, value=None):
+    """Copy a little-endian classic TIFF, overwriting one IFD entry's count
+    and / or value field (malformed-input fixtures made from valid ones)."""
+    import struct
+    d = bytearray(open(src, "rb").read())
+    assert d[:2] == b"II"
+    ifd = struct.unpack_from("<I", d, 4)[0]
+    n = struct.unpack_from("<H", d, ifd)[0]
+    for k in range(n):
+        e = ifd + 2 + 12 * k
+        if struct.unpack_from("<H", d, e)[0] == tag:
+            if count is not None:
+                struct.pack_into("<I", d, e + 4, count)
+            if value is not None:
+                typ = struct.unpack_from("<H", d, e + 2)[0]
+                struct.pack_into("<H" if typ == 3 else "<I", d, e + 8, value)
+            open(dst, "wb").write(bytes(d))
+            return
+    raise AssertionError("tag %d not found" % tag)
+
+
+@pytest.mark.parametrize("case", ["rows_per_strip_0", "huge_entry_count", "huge_size", "lzw_short_expect"])
+def test_tiff_malformed_inputs_fail_cleanly(exe, tmp_path, case):
+    """Hostile headers end in the loader's error, never a crash or an
+    unbounded allocation: RowsPerStrip = 0 (was an integer divide by zero),
+    an entry count of 2^30 pointing past the file (was allocated before any
+    bounds check), a 2^20 x 2^20 image; and an LZW strip decoded against a
+    smaller expected size stops at that size (no unbounded output)."""
+    src = os.path.join(GOLD, "tiff", "depth_none.tiff")
+    bad = str(tmp_path / "bad.tiff")
+    if case == "rows_per_strip_0":
+        patch_ifd(src, bad, 278, value=0)
+    elif case == "huge_entry_count":
+        patch_ifd(src, bad, 273, count=1 << 30)
+    elif case == "huge_size":
+        patch_ifd(src, bad, 256, value=1 << 20)
+        patch_ifd(bad, bad, 257, value=1 << 20)
+    else:
+        # one LZW strip holding the whole image, the height cut to one row:
+        # the strip decodes to more bytes than one row needs
+        src = os.path.join(GOLD, "tiff", "depth_lzw.tiff")
+        patch_ifd(src, bad, 257, value=1)
+        patch_ifd(bad, bad, 278, value=1)
+    r = subprocess.run([exe, "tiff", bad, str(tmp_path / "r.f32")], capture_output=True, text=True, timeout=60)
+    assert r.returncode >= 0, "crashed with signal %d" % -r.returncode
+    if case == "lzw_short_expect":
+        exp = np.load(os.path.join(GOLD, "tiff", "expected_depth.npy"))
+        got, msg = read_tiff(exe, bad, tmp_path)
+        assert got is not None, msg
+        assert got.shape == (1, exp.shape[1]) and np.array_equal(got[0].view(np.uint32), exp[0].view(np.uint32))
+    else:
+        assert r.returncode != 0 and "Error loading depth map" in r.stdout, r.stdout
+
+
 def test_semantic_maps_layout(exe, tmp_path):
     data = tmp_path / "data"
     (data / "depth_tiff").mkdir(parents=True)
