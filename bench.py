@@ -264,6 +264,11 @@ def main():
     ap.add_argument("--config", default="C4", choices=sorted(CONFIGS))
     ap.add_argument("--lm-iters", type=int, default=3, help="LM iterations for the BA-iteration wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lm-solver", default=None, choices=["exact", "iterative"],
+                    help="reduced camera system of the BA-iteration figure: exact (dense Schur + Cholesky, "
+                         "the 1-GPU default) or iterative (ITERATIVE_SCHUR + SCHUR_JACOBI: one nf-vector "
+                         "all-reduce per CG product, the default at N > 1, where an exact solve would have "
+                         "every rank factor the same summed S)")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="strong (default at N > 1): the one config problem split across the ranks (C4 split "
                          "this way is BASELINE's C5); weak: a config-sized shard per rank")
@@ -352,7 +357,11 @@ def main():
             # C5: the one C4 problem point-sharded across the ranks, reduced camera
             # system summed over RCCL (xGMI) every LM iteration
             lm_sc, lm_sem = build_shard(cfg, rank, world, "strong")
-        ctx_lm = mi_ba.Context(mi_ba.default_options(device=device, max_num_iterations=args.lm_iters), lm_sc, lm_sem)
+        lm_solver = args.lm_solver or ("iterative" if world > 1 else "exact")
+        ctx_lm = mi_ba.Context(mi_ba.default_options(
+            device=device, max_num_iterations=args.lm_iters,
+            linear_solver_type=mi_ba.SOLVER_ITERATIVE_SCHUR if lm_solver == "iterative" else mi_ba.SOLVER_DENSE_SCHUR),
+            lm_sc, lm_sem)
         if world > 1:
             if ap_backend == "nccl":
                 obj = [mi_ba.comm_unique_id() if rank == 0 else None]
@@ -371,6 +380,8 @@ def main():
                                           f"{args.config} point-sharded across {world} ranks, S summed by ") +
                                          ("RCCL all-reduce" if ap_backend == "nccl" else "gloo host reducer"))
                                         if world > 1 else f"{args.config} on one GPU"),
+              "lm_solver": ("ITERATIVE_SCHUR + SCHUR_JACOBI (nf-vector all-reduce per CG product)"
+                            if lm_solver == "iterative" else "exact dense Schur + Cholesky"),
               "linear_solver_iterations": s.num_linear_solver_iterations,
               "initial_cost": s.initial_cost, "final_cost": s.final_cost,
               "lm_phase_ms_calls": {k: list(ctx_lm.kernel_time(k)) for k in

@@ -1,5 +1,6 @@
 // cholesky.cpp — recursive blocked Cholesky over rocBLAS/rocSOLVER (see cholesky.h).
 #include "cholesky.h"
+#include "dgemm_nt.h"
 
 #include <hip/hip_runtime.h>
 #include <rocsolver/rocsolver.h>
@@ -1280,9 +1281,15 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     double* T = Aik + (size_t)kb * lda;          // trailing matrix, lower triangle
     // block column k+1 first
     const int jb0 = std::min(nb, m);
-    st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, jb0, kb, &minus_one, Aik, lda, Aik,
-                       lda, &one, T, lda);
-    if (st != rocblas_status_success) return fail(st);
+    const bool own_gemm = cfg.rest_update == 4 && kb % 16 == 0;
+    if (own_gemm) {
+      if (dgemm_nt_sub(m, jb0, kb, Aik, lda, Aik, lda, T, lda, true, s1) != hipSuccess)
+        return fail(rocblas_status_internal_error);
+    } else {
+      st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, jb0, kb, &minus_one, Aik, lda, Aik,
+                         lda, &one, T, lda);
+      if (st != rocblas_status_success) return fail(st);
+    }
     hipEvent_t upd = ws.ev[2 * kk], pan = ws.ev[2 * kk + 1];
     if (hipEventRecord(upd, s1) != hipSuccess || hipStreamWaitEvent(ws.side, upd, 0) != hipSuccess)
       return fail(rocblas_status_internal_error);
@@ -1291,7 +1298,13 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     if (hipEventRecord(pan, ws.side) != hipSuccess) return fail(rocblas_status_internal_error);
     // the rest of the trailing lower triangle (columns jb0 .. m)
     const int mr = m - jb0;
-    if (mr > 0 && cfg.rest_update == 1) {
+    if (mr > 0 && own_gemm) {
+      // the whole trailing lower triangle in one launch of the hand-written
+      // MFMA GEMM (tiles above the diagonal skipped)
+      if (dgemm_nt_sub(mr, mr, kb, Aik + jb0, lda, Aik + jb0, lda, T + jb0 + (size_t)jb0 * lda, lda, true, s1) !=
+          hipSuccess)
+        return fail(rocblas_status_internal_error);
+    } else if (mr > 0 && cfg.rest_update == 1) {
       st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, mr, kb, &minus_one, Aik + jb0, lda, &one,
                          T + jb0 + (size_t)jb0 * lda, lda);
       if (st != rocblas_status_success) return fail(st);

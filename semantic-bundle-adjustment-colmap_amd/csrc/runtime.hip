@@ -1517,7 +1517,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.solve = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 3) {
+  if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 4) {
     ctx->chol.rest_update = value;
     return MI_BA_OK;
   }
