@@ -1,6 +1,5 @@
 // cholesky.cpp — recursive blocked Cholesky over rocBLAS/rocSOLVER (see cholesky.h).
 #include "cholesky.h"
-#include "dgemm_nt.h"
 
 #include <hip/hip_runtime.h>
 #include <rocsolver/rocsolver.h>
@@ -868,7 +867,7 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
                                                            unsigned long long* dbg = nullptr) {
   __shared__ double T[64 * kPfLd];   // staging / factor tile (row-major padded)
   __shared__ double Li[64 * kPfLd];  // a diagonal tile's inverse (own, or workgroup c's)
-  __shared__ double Lc[64 * 64];     // the factor's columns (pf_chol_inv_wave)
+  __shared__ double Lc[1152];        // pf_chol_inv_fast scratch: per-wave 16x16 tiles + the pivot status
   __shared__ double dinv[64];
   __shared__ int s_r;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1254,6 +1253,23 @@ rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, 
                        rocblas_diagonal_non_unit, m, kb, &one, Akk, lda, Akk + kb, lda);
 }
 
+// C -= P P' for the trailing update (P: m rows of the panel, its first n
+// rows' block column of C): rocBLAS dgemm, or rocblas_gemm_ex with an
+// explicit Tensile solution index (CholConfig::gemm_solution); an index the
+// library does not accept for the shape falls back to the default solution.
+rocblas_status gemm_nt(rocblas_handle h, int m, int n, int k, const double* P, int ldp, double* C, int ldc, int sol) {
+  const double minus_one = -1.0, one = 1.0;
+  if (sol != 0) {
+    const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_transpose, m, n, k,
+                                              &minus_one, P, rocblas_datatype_f64_r, ldp, P, rocblas_datatype_f64_r, ldp,
+                                              &one, C, rocblas_datatype_f64_r, ldc, C, rocblas_datatype_f64_r, ldc,
+                                              rocblas_datatype_f64_r, rocblas_gemm_algo_solution_index, sol, 0);
+    if (st == rocblas_status_success) return st;
+  }
+  return rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, n, k, &minus_one, P, ldp, P, ldp,
+                       &one, C, ldc);
+}
+
 rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
                                 CholWorkspace& ws) {
   const double minus_one = -1.0, one = 1.0;
@@ -1281,15 +1297,8 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     double* T = Aik + (size_t)kb * lda;          // trailing matrix, lower triangle
     // block column k+1 first
     const int jb0 = std::min(nb, m);
-    const bool own_gemm = cfg.rest_update == 4 && kb % 16 == 0;
-    if (own_gemm) {
-      if (dgemm_nt_sub(m, jb0, kb, Aik, lda, Aik, lda, T, lda, true, s1) != hipSuccess)
-        return fail(rocblas_status_internal_error);
-    } else {
-      st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, jb0, kb, &minus_one, Aik, lda, Aik,
-                         lda, &one, T, lda);
-      if (st != rocblas_status_success) return fail(st);
-    }
+    st = gemm_nt(h, m, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
+    if (st != rocblas_status_success) return fail(st);
     hipEvent_t upd = ws.ev[2 * kk], pan = ws.ev[2 * kk + 1];
     if (hipEventRecord(upd, s1) != hipSuccess || hipStreamWaitEvent(ws.side, upd, 0) != hipSuccess)
       return fail(rocblas_status_internal_error);
@@ -1298,13 +1307,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     if (hipEventRecord(pan, ws.side) != hipSuccess) return fail(rocblas_status_internal_error);
     // the rest of the trailing lower triangle (columns jb0 .. m)
     const int mr = m - jb0;
-    if (mr > 0 && own_gemm) {
-      // the whole trailing lower triangle in one launch of the hand-written
-      // MFMA GEMM (tiles above the diagonal skipped)
-      if (dgemm_nt_sub(mr, mr, kb, Aik + jb0, lda, Aik + jb0, lda, T + jb0 + (size_t)jb0 * lda, lda, true, s1) !=
-          hipSuccess)
-        return fail(rocblas_status_internal_error);
-    } else if (mr > 0 && cfg.rest_update == 1) {
+    if (mr > 0 && cfg.rest_update == 1) {
       st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, mr, kb, &minus_one, Aik + jb0, lda, &one,
                          T + jb0 + (size_t)jb0 * lda, lda);
       if (st != rocblas_status_success) return fail(st);
@@ -1317,8 +1320,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
       for (int j = jb0; j < m; j += cw) {
         const int jb = std::min(cw, m - j);
-        st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m - j, jb, kb, &minus_one,
-                           Aik + j, lda, Aik + j, lda, &one, T + j + (size_t)j * lda, lda);
+        st = gemm_nt(h, m - j, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
         if (st != rocblas_status_success) return fail(st);
       }
     }

@@ -30,6 +30,14 @@ struct CholConfig {
   // 3 one dgemm per 1024-wide block column (default: 25.7 -> 25.2 ms at nf =
   // 12 000; dsyrk 38.6 ms, dgemmt 519 ms — profiles/r2_ab_rest_update.jsonl)
   int rest_update = 3;
+  // trailing-update dgemm: 0 rocBLAS's default solution, else a Tensile
+  // solution index for rocblas_gemm_ex (rocblas_gemm_ex_get_solutions; an
+  // index the shape does not accept falls back to the default).  Default: the
+  // fastest of the sweep over all 267 solutions of the update's shapes
+  // (tools/probes/dgemm_solutions.cpp, profiles/r3_dgemm_solutions.txt: 65-72
+  // vs 46-49 TF at M ~ 11 000, N = 512 / 1024, K = 512): Cholesky 17.5 ->
+  // 15.8 ms at nf = 12 000 (profiles/r3_ab_gemm_solution.jsonl).
+  int gemm_solution = -624952224;
   // panel k+1's diagonal factor + dtrsm on the workspace's side stream under
   // panel k's dgemm (34.6 -> 30.4 ms at nf = 12 000)
   bool lookahead = true;

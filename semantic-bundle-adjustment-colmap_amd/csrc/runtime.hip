@@ -1517,7 +1517,11 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.solve = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 4) {
+  if (std::strcmp(key, "cholesky_gemm_solution") == 0) {
+    ctx->chol.gemm_solution = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 3) {
     ctx->chol.rest_update = value;
     return MI_BA_OK;
   }

@@ -251,3 +251,22 @@ def test_lm_tile_factor_and_publish(gpu):
         assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
         assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
 
+
+
+def test_lm_gemm_solution(gpu):
+    """The trailing update through rocblas_gemm_ex with an explicit Tensile
+    solution index (cholesky_gemm_solution; an index the shape does not accept
+    falls back to the default) drives the same LM as rocBLAS's default
+    dgemm (nf = 1593)."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for sol in (0, -624952238, -624952224, 12345):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            ctx.set_tuning("cholesky_gemm_solution", sol)
+            res.append(ctx.solve())
+    b = res[0]
+    for a in res[1:]:
+        assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
+        assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost

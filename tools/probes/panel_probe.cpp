@@ -2,7 +2,7 @@
 // own_diag 6) on the first 512-wide panel of an nf = 12 000 SPD matrix:
 // wall_clock64() stamps per row tile (kernel's dbg buffer).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/panel_probe.cpp -lrocsolver -lrocblas -o tools/probes/panel_probe.bin
-//   tools/probes/panel_probe.bin [n] [tile_factor] [write_through]
+//   tools/probes/panel_probe.bin [n] [tile_factor] [write_through] [concurrent dgemms]
 #include "../../semantic-bundle-adjustment-colmap_amd/csrc/cholesky.cpp"
 
 #include <cstdio>
@@ -25,7 +25,8 @@ int main(int argc, char** argv) {
   hipMalloc(&info, 64);
   const int fv = argc > 2 ? atoi(argv[2]) : 2;  // tile factor: 2 rsq, 1 sqrt pivots
   const int wt = argc > 3 ? atoi(argv[3]) : 1;  // write-through publish
-  printf("n %d, tile_factor %d, write_through %d\n", n, fv, wt);
+  const int busy = argc > 4 ? atoi(argv[4]) : 0;  // 1: trailing-update dgemms on a second stream meanwhile
+  printf("n %d, tile_factor %d, write_through %d, concurrent dgemms %d\n", n, fv, wt, busy);
   const int nr = 8 + (n - kb + 63) / 64;
   hipMalloc(&dbg, 8ull * nr * kPfDbgSlots);
   CholWorkspace ws;
@@ -39,13 +40,33 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    hipEventRecord(e0, 0);
+    hipStream_t bs = nullptr;
+    rocblas_handle bh = nullptr;
+    if (busy) {
+      // the look-ahead's rest update beside the panel: 1024-wide block columns
+      // of the trailing matrix, C -= P P' with K = 512 (default solution index)
+      hipStreamCreateWithFlags(&bs, hipStreamNonBlocking);
+      rocblas_create_handle(&bh);
+      rocblas_set_stream(bh, bs);
+      const double m1 = -1.0, p1 = 1.0;
+      for (int j = 2 * kb; j + 1024 <= n; j += 1024)
+        rocblas_gemm_ex(bh, rocblas_operation_none, rocblas_operation_transpose, n - j, 1024, kb, &m1, A + j, rocblas_datatype_f64_r,
+                        n, A + j, rocblas_datatype_f64_r, n, &p1, A + j + (size_t)j * n, rocblas_datatype_f64_r, n,
+                        A + j + (size_t)j * n, rocblas_datatype_f64_r, n, rocblas_datatype_f64_r,
+                        rocblas_gemm_algo_solution_index, CholConfig{}.gemm_solution, 0);
+    }
+    hipEventRecord(e0, ws.side);
     auto kern = fv == 2 ? (wt ? panel_factor_kernel<2, true> : panel_factor_kernel<2, false>)
                         : (wt ? panel_factor_kernel<1, true> : panel_factor_kernel<1, false>);
-    hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, 0, A, n, kb, n, info, ws.pf_linv, ws.pf_ctrl, ws.pf_base, epoch,
+    hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, ws.side, A, n, kb, n, info, ws.pf_linv, ws.pf_ctrl, ws.pf_base, epoch,
                        ws.err, ws.spin_limit, dbg);
-    hipEventRecord(e1, 0);
+    hipEventRecord(e1, ws.side);
     hipEventSynchronize(e1);
+    if (busy) {
+      hipStreamSynchronize(bs);
+      rocblas_destroy_handle(bh);
+      hipStreamDestroy(bs);
+    }
     ws.pf_base += nr;
     float ms;
     hipEventElapsedTime(&ms, e0, e1);
