@@ -112,6 +112,8 @@ struct mi_ba_context {
   miba::DevArray<double> S;
   miba::DevArray<double> Linv, Z;          // [P][6] inverse point factors, [nb][3F] Schur factors
   miba::DevArray<miba::DevPairTile> ptiles;
+  miba::DevArray<miba::DevPairTile> ptiles_blk;  // the same tiles in image-block order (schur_pairs_variant 4)
+  int schur_block = 32;                           // images per block edge of ptiles_blk
   miba::DevArray<uint2> pairs;             // (a, b) block pairs bucketed by image pair
   int nptiles = 0;
   miba::DevArray<int32_t> info;

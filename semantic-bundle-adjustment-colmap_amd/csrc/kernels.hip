@@ -1548,18 +1548,19 @@ __global__ __launch_bounds__(kBlock) void schur_z_kernel(DevProblem p, const dou
 // (row <= col, row-major = rocSOLVER's column-major lower) of S.
 // Cross tiles hold pairs a != b: a mirrored entry lands on the same upper
 // element, a diagonal one counts twice.  Self tiles hold a == b.
-template <int CT>
+// XMAP: XCD-aware order — workgroup b runs on XCD b % 8; each XCD gets a
+// contiguous range of tiles (tiles sorted by first image, so one image's Z
+// rows stay in that XCD's L2 while its pairs stream by).  Else dispatch order
+// (image-block-ordered tiles: every XCD sweeps the same image block at once).
+template <int CT, bool XMAP = true>
 __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const DevPairTile* __restrict__ tiles,
                                                               int ntiles, const uint2* __restrict__ pairs,
                                                               const double* __restrict__ Z, double* __restrict__ S) {
   constexpr int F = 6 + CT, ZN = 3 * F;
-  // XCD-aware order: workgroup b runs on XCD b % 8; give each XCD a
-  // contiguous range of tiles (tiles are sorted by first image, so one
-  // image's Z rows stay in that XCD's L2 while its pairs stream by).
   const int G = (ntiles + 3) / 4;
   const int per = (G + 7) / 8;
   const int b = blockIdx.x;
-  const int lb = (b % 8) * per + b / 8;
+  const int lb = XMAP ? (b % 8) * per + b / 8 : b;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t = lb * 4 + wv;
   if (lb >= G || t >= ntiles) return;
@@ -2085,6 +2086,9 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
       else if (p.svariant == 3)
         hipLaunchKernelGGL((schur_pairs_pipelined_kernel<CT, 16>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles,
                            pairs, Z, S);
+      else if (p.svariant == 4)
+        hipLaunchKernelGGL((schur_pairs_kernel<CT, false>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs,
+                           Z, S);
       else
         hipLaunchKernelGGL(schur_pairs_kernel<CT>, dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs, Z, S);
     }

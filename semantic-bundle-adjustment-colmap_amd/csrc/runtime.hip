@@ -220,11 +220,25 @@ mi_ba_status build_pair_tiles(mi_ba_context* ctx) {
   }
   if (npairs >= (int64_t)UINT32_MAX || tl.size() >= (size_t)INT32_MAX) return MI_BA_ERR_UNSUPPORTED;
   ctx->nptiles = (int)tl.size();
-  if (ctx->pairs.alloc(npairs) || ctx->ptiles.alloc(tl.size()) || ctx->Linv.alloc(6 * (size_t)d.num_points) ||
-      ctx->Z.alloc((size_t)nb * 3 * (6 + d.ct)))
+  // the same tiles in image-block order (svariant 4): blocks of B x B image
+  // pairs, so the workgroups in flight at any time (dispatch order) gather
+  // the Z rows of ~2B images only — a working set the 256 MB MALL holds
+  // (2.9 MB of Z per image at C4), where the first-image order scatters the
+  // second image's rows over every image
+  std::vector<DevPairTile> tb(tl);
+  {
+    const uint32_t B = (uint32_t)std::max(1, ctx->schur_block);
+    std::stable_sort(tb.begin(), tb.end(), [B](const DevPairTile& x, const DevPairTile& y) {
+      const uint32_t xa = x.ia / B, xb = x.ib / B, ya = y.ia / B, yb = y.ib / B;
+      return xa != ya ? xa < ya : xb < yb;
+    });
+  }
+  if (ctx->pairs.alloc(npairs) || ctx->ptiles.alloc(tl.size()) || ctx->ptiles_blk.alloc(tb.size()) ||
+      ctx->Linv.alloc(6 * (size_t)d.num_points) || ctx->Z.alloc((size_t)nb * 3 * (6 + d.ct)))
     return MI_BA_ERR_OUT_OF_MEMORY;
   if ((npairs && hipMemcpy(ctx->pairs.ptr, pr.data(), npairs * sizeof(uint2), hipMemcpyHostToDevice)) ||
-      (!tl.empty() && hipMemcpy(ctx->ptiles.ptr, tl.data(), tl.size() * sizeof(DevPairTile), hipMemcpyHostToDevice)))
+      (!tl.empty() && hipMemcpy(ctx->ptiles.ptr, tl.data(), tl.size() * sizeof(DevPairTile), hipMemcpyHostToDevice)) ||
+      (!tb.empty() && hipMemcpy(ctx->ptiles_blk.ptr, tb.data(), tb.size() * sizeof(DevPairTile), hipMemcpyHostToDevice)))
     return MI_BA_ERR_HIP;
   // stream-ordered: a null-stream memset is not ordered against the context's
   // non-blocking stream (the LM's kernels could overtake it)
@@ -716,7 +730,8 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   hipEvent_t stop;
   timer_begin(ctx, "schur_build", &stop);
   launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
-                     ctx->ptiles.ptr, ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, false, s);
+                     d.svariant == 4 ? ctx->ptiles_blk.ptr : ctx->ptiles.ptr, ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr,
+                     false, s);
   if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
   if (ctx->gsba) gsba_add_dense(ctx, ctx->S.ptr);
   timer_end(ctx, stop);
@@ -1497,8 +1512,13 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->sem_variant = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 3) {
+  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 4) {
     ctx->dev.svariant = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "schur_block_images") == 0 && value >= 1) {
+    // takes effect when the pair tiles are built (before the first solve)
+    ctx->schur_block = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_panel") == 0 && (value == 0 || (value >= 64 && value <= 4096))) {

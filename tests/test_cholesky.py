@@ -270,3 +270,23 @@ def test_lm_gemm_solution(gpu):
     for a in res[1:]:
         assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
         assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
+
+
+def test_lm_schur_pair_orders(gpu):
+    """The explicit Schur build's pair tiles in first-image order with the
+    XCD-striped mapping (schur_pairs_variant 0) and in image-block order with
+    dispatch-order mapping (4, blocks of 8 and 64 images) drive the same LM:
+    the same S up to the order of the float atomics (nf = 1593)."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for var, blk in ((0, 32), (4, 8), (4, 64)):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            ctx.set_tuning("schur_pairs_variant", var)
+            ctx.set_tuning("schur_block_images", blk)
+            res.append(ctx.solve())
+    b = res[0]
+    for a in res[1:]:
+        assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
+        assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
