@@ -554,7 +554,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
 // launch, release/acquire at agent scope, as the sweeps above).
 typedef double pf_dvec4 __attribute__((ext_vector_type(4)));
 constexpr int kPfMaxTiles = 8;  // column tiles per panel (panel <= 512)
-constexpr int kTinv = 512;  // own_diag 7: widest panel
+[[maybe_unused]] constexpr int kTinv = 512;  // own_diag 7: widest panel
 
 __device__ __forceinline__ int pf_row0(int r, int kb, int nc) { return r < nc ? 64 * r : kb + 64 * (r - nc); }
 __device__ __forceinline__ int pf_rows(int r, int kb, int nc, int mrows) {
@@ -609,16 +609,6 @@ __device__ __forceinline__ void pf_acc_to_lds(const pf_dvec4 (&acc)[4], double* 
     for (int q = 0; q < 4; ++q) T[(16 * w + 4 * q + (lane >> 4)) * kPfLd + 16 * t + (lane & 15)] = acc[t][q];
 }
 
-
-// accumulator -> LDS tile transposed, T[j * kPfLd + i] = D[i][j]: the
-// column-major view of T is D (the diagonal step factors D's lower triangle,
-// the only half of S the caller filled)
-__device__ __forceinline__ void pf_acc_to_lds_t(const pf_dvec4 (&acc)[4], double* T, int w, int lane) {
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) T[(16 * t + (lane & 15)) * kPfLd + 16 * w + 4 * q + (lane >> 4)] = acc[t][q];
-}
 
 // ---- 16x16 MFMA block helpers of the tile factor --------------------------
 // acc (16x16, MFMA D layout) += sign * A(16x16) * op(B); A, B row-major with
@@ -890,12 +880,6 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
   const bool diag_row = r < nc;
   const int m = lane & 15, kq = lane >> 4;
   // tile loaders (clamped addresses, zero padding)
-  auto gtile = [&](int row0, int h, int col0, int w) {
-    return [=](int i, int j) {
-      const double v = A[(size_t)(col0 + min(j, w - 1)) * lda + row0 + min(i, h - 1)];
-      return (i < h && j < w) ? v : 0.0;
-    };
-  };
   auto ltile = [&](const double* S) { return [=](int i, int j) { return S[i * kPfLd + j]; }; };
   // the diagonal tile's running accumulator (diagonal-block rows)
   pf_dvec4 dacc[4];
@@ -1154,6 +1138,7 @@ rocblas_status backward(rocblas_handle h, int n, const double* A, int lda, doubl
 // updated by dsyrk (or by dgemm per block column of width `panel`).
 rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, int own,
                             double* scratch, CholWorkspace* ws);
+rocblas_status gemm_nt(rocblas_handle h, int m, int n, int k, const double* P, int ldp, double* C, int ldc, int sol);
 
 rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
                               double* scratch, CholWorkspace* ws) {
@@ -1172,10 +1157,14 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
       st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, m, kb, &minus_one, Aik, lda, &one, T, lda);
       if (st != rocblas_status_success) return st;
     } else {
-      for (int j = 0; j < m; j += nb) {
-        const int jb = std::min(nb, m - j);
-        st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m - j, jb, kb, &minus_one, Aik + j,
-                           lda, Aik + j, lda, &one, T + j + (size_t)j * lda, lda);
+      // the look-ahead's partition and GEMM solution (block column k+1, then
+      // columns of width nb or 2 nb): both orders run the same GEMMs on the
+      // same shapes, so their factors are bitwise equal
+      const int jb0 = std::min(nb, m);
+      const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
+      for (int j = 0; j < m; j = j == 0 ? jb0 : j + cw) {
+        const int jb = std::min(j == 0 ? jb0 : cw, m - j);
+        st = gemm_nt(h, m - j, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
         if (st != rocblas_status_success) return st;
       }
     }
@@ -1206,15 +1195,20 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
     ws->pf_epoch = 0;
   }
   const unsigned epoch = ++ws->pf_epoch;
+#ifdef MI_BA_AB_VARIANTS
   auto kern = ws->tile_factor == 2 ? (ws->write_through ? panel_factor_kernel<2, true> : panel_factor_kernel<2, false>)
                                    : (ws->write_through ? panel_factor_kernel<1, true> : panel_factor_kernel<1, false>);
+#else
+  auto kern = panel_factor_kernel<2, true>;  // the tools build keeps tile_factor 1 / plain stores for A/B
+#endif
   hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, s, A + k + (size_t)k * lda, lda, kb, mrows, info, ws->pf_linv,
                      ws->pf_ctrl, ws->pf_base, epoch, ws->err, ws->spin_limit, nullptr);
   ws->pf_base += (unsigned)nr;
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
 
-// own_diag 7: the two-kernel diagonal factor, then the panel solve
+#ifdef MI_BA_AB_VARIANTS
+// own_diag 7 (tools build only): the two-kernel diagonal factor, then the panel solve
 // A_ik <- A_ik L_kk^-T as one dgemm against the explicit inverse of the
 // diagonal block (rocBLAS dtrtri) instead of a dtrsm: the panel solve runs at
 // dgemm rate off a copy of the panel.
@@ -1238,11 +1232,14 @@ rocblas_status panel_factor_inv(rocblas_handle h, int n, double* A, int lda, int
   return rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, kb, kb, &one, ws->tbuf, m, ws->tinv,
                        kb, &zero, Akk + kb, lda);
 }
+#endif
 
 rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, int own,
                             double* scratch, CholWorkspace* ws) {
   if (own == 6) return panel_factor_fused(h, n, A, lda, k, kb, info, ws);
+#ifdef MI_BA_AB_VARIANTS
   if (own == 7) return panel_factor_inv(h, n, A, lda, k, kb, info, scratch, ws);
+#endif
   double* Akk = A + k + (size_t)k * lda;
   rocblas_status st = potrf_leaf(h, kb, Akk, lda, info, own, scratch);
   if (st != rocblas_status_success) return st;
@@ -1272,7 +1269,7 @@ rocblas_status gemm_nt(rocblas_handle h, int m, int n, int k, const double* P, i
 
 rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
                                 CholWorkspace& ws) {
-  const double minus_one = -1.0, one = 1.0;
+  [[maybe_unused]] const double minus_one = -1.0, one = 1.0;  // rest_update 1 / 2 (tools build)
   const int nb = cfg.panel;
   hipStream_t s1;
   if (rocblas_get_stream(h, &s1) != rocblas_status_success) return rocblas_status_internal_error;
@@ -1306,7 +1303,8 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     if (st != rocblas_status_success) return fail(st);
     if (hipEventRecord(pan, ws.side) != hipSuccess) return fail(rocblas_status_internal_error);
     // the rest of the trailing lower triangle (columns jb0 .. m)
-    const int mr = m - jb0;
+    [[maybe_unused]] const int mr = m - jb0;
+#ifdef MI_BA_AB_VARIANTS
     if (mr > 0 && cfg.rest_update == 1) {
       st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, mr, kb, &minus_one, Aik + jb0, lda, &one,
                          T + jb0 + (size_t)jb0 * lda, lda);
@@ -1315,7 +1313,9 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       st = rocblas_dgemmt(h, rocblas_fill_lower, rocblas_operation_none, rocblas_operation_transpose, mr, kb,
                           &minus_one, Aik + jb0, lda, Aik + jb0, lda, &one, T + jb0 + (size_t)jb0 * lda, lda);
       if (st != rocblas_status_success) return fail(st);
-    } else {
+    } else
+#endif
+    {
       // block columns of width nb (rest_update 0) or 2 nb (3)
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
       for (int j = jb0; j < m; j += cw) {
@@ -1381,9 +1381,11 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
     if (hipMemsetAsync(ctrl, 0, sizeof(unsigned) * (2 + (size_t)nblk), side) != hipSuccess) return false;
     if (hipMalloc(&err, 4 * sizeof(unsigned)) != hipSuccess) { err = nullptr; return false; }
     if (hipMemsetAsync(err, 0, 4 * sizeof(unsigned), side) != hipSuccess) return false;
+#ifdef MI_BA_AB_VARIANTS
     if (hipMalloc(&tinv, sizeof(double) * kTinv * kTinv) != hipSuccess) { tinv = nullptr; return false; }
     if (hipMalloc(&tbuf, sizeof(double) * kTinv * (size_t)nblk * kTB) != hipSuccess) { tbuf = nullptr; return false; }
     tbuf_rows = nblk * kTB;
+#endif
     if (hipStreamSynchronize(side) != hipSuccess) return false;
     epoch = 0;
     linv_rows = nblk * kTB;
@@ -1436,7 +1438,11 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   // widths (and the recursive split) take the two-kernel diagonal factor
   CholConfig c = cfg;
   if (c.own_diag == 6 && (c.panel <= 0 || c.panel > 64 * kPfMaxTiles)) c.own_diag = 2;
+#ifdef MI_BA_AB_VARIANTS
   if (c.own_diag == 7 && (c.panel <= 0 || c.panel > kTinv)) c.own_diag = 2;
+#else
+  if (c.own_diag == 7) c.own_diag = 2;  // own_diag 7 is in the tools build only
+#endif
   if (ws) {
     ws->tile_factor = c.tile_factor;
     ws->write_through = c.write_through;

@@ -112,7 +112,8 @@ struct mi_ba_context {
   miba::DevArray<double> S;
   miba::DevArray<double> Linv, Z;          // [P][6] inverse point factors, [nb][3F] Schur factors
   miba::DevArray<miba::DevPairTile> ptiles;
-  miba::DevArray<miba::DevPairTile> ptiles_blk;  // the same tiles in image-block order (schur_pairs_variant 4)
+  miba::DevArray<miba::DevPairTile> ptiles_blk;  // the same tiles in image-block order (schur_pairs_variant 4, default)
+  std::vector<miba::DevPairTile> ptiles_host;    // first-image order, kept to re-order on "schur_block_images"
   int schur_block = 32;                           // images per block edge of ptiles_blk
   miba::DevArray<uint2> pairs;             // (a, b) block pairs bucketed by image pair
   int nptiles = 0;

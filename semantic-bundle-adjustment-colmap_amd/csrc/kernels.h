@@ -15,7 +15,8 @@ struct SemDevice;  // defined in semantic.h
 // the loss Corrector applied and the cost folded into per-workgroup partials.
 // p.jvariant selects A/B builds of the C4 shape (0 = production).
 // Rebuild p.img_rec from qt / cam / flags (before every Jacobian launch).
-void launch_pack_images(const DevProblem& p, double* rec, hipStream_t s);
+// also zeroes zero[0..nzero) when zero is given
+void launch_pack_images(const DevProblem& p, double* rec, hipStream_t s, double* zero = nullptr, int nzero = 0);
 void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s);
 int reproj_grid(int64_t nb);
 

@@ -271,7 +271,7 @@ constexpr int kJacProduction = 8 | 16 | 32 | 128 | 512 | 1024;  // 0.583 -> 0.54
 // waves per SIMD, each store burst 15 KB): 0.554 (2 passes) -> 0.454 ms at C4
 // once the arithmetic was cut by the closed-form rotation columns
 constexpr int kJacPasses = 1;
-constexpr int kJacR1 = 8 | 16 | 32;  // round-1 production (three serial round trips), A/B variant 23
+[[maybe_unused]] constexpr int kJacR1 = 8 | 16 | 32;  // round-1 production (three serial round trips), A/B variant 23
 // TB: threads per workgroup.  The cost partial is per wave (no workgroup
 // barrier), cost_partial[i / 64].
 // CTX: the camera-slot width of a mixed-model build (M == kMixedModels, RF
@@ -521,8 +521,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 // Image records img_rec[I][16] = q(4) t(3) meta camera-params(8), meta =
 // img_flags | cam_var << 8 (bit pattern in a double slot): one 128-B line per
 // image, rebuilt whenever poses or intrinsics change.
-__global__ void pack_images_kernel(DevProblem p, double* __restrict__ rec) {
+// zero[0..nzero) is cleared too (the step's scalar slots: one launch fewer
+// than a separate memset ahead of it).
+__global__ void pack_images_kernel(DevProblem p, double* __restrict__ rec, double* __restrict__ zero, int nzero) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nzero) zero[k] = 0.0;
   if (k >= p.num_images) return;
   const uint32_t cam = p.img_cam[k];
   double* o = rec + 16 * (size_t)k;
@@ -546,11 +549,23 @@ __global__ __launch_bounds__(kBlock) void reproj_cost_kernel(DevProblem p, const
   if ((threadIdx.x & 63) == 0 && i < p.nb) cost_partial[i >> 6] = s;
 }
 
+// One workgroup; each thread sums its strided share with kSumIlp loads in
+// flight (a serial load-add chain ran 40 us over the 156k partials of C4's
+// reprojection pass).  The order is fixed: results are deterministic.
+constexpr int kSumIlp = 16;
 __global__ __launch_bounds__(1024) void sum_kernel(const double* __restrict__ partial, int64_t n,
                                                    double* __restrict__ out) {
   __shared__ double sred[16];
   double v = 0.0;
-  for (int64_t k = threadIdx.x; k < n; k += 1024) v += partial[k];
+  int64_t k = threadIdx.x;
+  for (; k + (kSumIlp - 1) * 1024 < n; k += kSumIlp * 1024) {
+    double x[kSumIlp];
+#pragma unroll
+    for (int u = 0; u < kSumIlp; ++u) x[u] = partial[k + u * 1024];
+#pragma unroll
+    for (int u = 0; u < kSumIlp; ++u) v += x[u];
+  }
+  for (; k < n; k += 1024) v += partial[k];
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -1764,6 +1779,7 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
       constexpr int RF = decltype(rf)::value;
       auto launch = [&](auto loss) {
         constexpr int LOSS = decltype(loss)::value;
+#ifdef MI_BA_AB_VARIANTS
         if constexpr (M == kOpenCV && RF == 5 && LOSS == 0) {
           // A/B and roofline-decomposition builds of the C4 shape (tools/ab_jacobian.py)
           switch (p.jvariant) {
@@ -1868,6 +1884,7 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
               break;
           }
         }
+#endif
         hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, LOSS, kJacPasses, kJacProduction>), dim3(g), dim3(kBlock), 0,
                            s, p, r, J, cost_partial);
       };
@@ -1889,9 +1906,11 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
   });
 }
 
-void launch_pack_images(const DevProblem& p, double* rec, hipStream_t s) {
-  if (p.num_images == 0) return;
-  hipLaunchKernelGGL(pack_images_kernel, dim3(grid_for(p.num_images, kBlock)), dim3(kBlock), 0, s, p, rec);
+void launch_pack_images(const DevProblem& p, double* rec, hipStream_t s, double* zero, int nzero) {
+  const int64_t n = std::max<int64_t>(p.num_images, zero ? nzero : 0);
+  if (n == 0) return;
+  hipLaunchKernelGGL(pack_images_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, p, rec, zero,
+                     zero ? nzero : 0);
 }
 
 void launch_reproj_cost(const DevProblem& p, const double* qt, const double* cam, const double* X,
@@ -2077,6 +2096,7 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
       hipLaunchKernelGGL(schur_z_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z);
       const int G = (nptiles + 3) / 4;
       const int grid = ((G + 7) / 8) * 8;  // whole XCD stripes (extra workgroups exit)
+#ifdef MI_BA_AB_VARIANTS
       if (p.svariant == 1)
         hipLaunchKernelGGL((schur_pairs_pipelined_kernel<CT, 8>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles,
                            pairs, Z, S);
@@ -2086,7 +2106,9 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
       else if (p.svariant == 3)
         hipLaunchKernelGGL((schur_pairs_pipelined_kernel<CT, 16>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles,
                            pairs, Z, S);
-      else if (p.svariant == 4)
+      else
+#endif
+      if (p.svariant == 4)
         hipLaunchKernelGGL((schur_pairs_kernel<CT, false>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs,
                            Z, S);
       else

@@ -156,6 +156,26 @@ static void timer_collect(mi_ba_context* ctx) {
 // blocks of one variable point (a == b included), bucketed by image pair
 // (ia <= ib) and cut into tiles of <= kPairTile pairs; self pairs (a == b)
 // get tiles of their own.  Built once per problem (structure only).
+// The pair tiles in image-block order (schur_pairs_variant 4): blocks of
+// B x B image pairs, so the workgroups in flight at any time (dispatch order)
+// gather the Z rows of ~2B images only — a working set the 256 MB MALL holds
+// (2.9 MB of Z per image at C4), where the first-image order scatters the
+// second image's rows over every image.
+mi_ba_status order_block_tiles(mi_ba_context* ctx) {
+  std::vector<DevPairTile> tb(ctx->ptiles_host);
+  const uint32_t B = (uint32_t)std::max(1, ctx->schur_block);
+  std::stable_sort(tb.begin(), tb.end(), [B](const DevPairTile& x, const DevPairTile& y) {
+    const uint32_t xa = x.ia / B, xb = x.ib / B, ya = y.ia / B, yb = y.ib / B;
+    return xa != ya ? xa < ya : xb < yb;
+  });
+  if (tb.empty()) return MI_BA_OK;
+  // kernels of an earlier solve may still read the old order
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+      hipMemcpy(ctx->ptiles_blk.ptr, tb.data(), tb.size() * sizeof(DevPairTile), hipMemcpyHostToDevice) != hipSuccess)
+    return MI_BA_ERR_HIP;
+  return MI_BA_OK;
+}
+
 mi_ba_status build_pair_tiles(mi_ba_context* ctx) {
   const DevProblem& d = ctx->dev;
   const int I = d.num_images;
@@ -225,21 +245,15 @@ mi_ba_status build_pair_tiles(mi_ba_context* ctx) {
   // the Z rows of ~2B images only — a working set the 256 MB MALL holds
   // (2.9 MB of Z per image at C4), where the first-image order scatters the
   // second image's rows over every image
-  std::vector<DevPairTile> tb(tl);
-  {
-    const uint32_t B = (uint32_t)std::max(1, ctx->schur_block);
-    std::stable_sort(tb.begin(), tb.end(), [B](const DevPairTile& x, const DevPairTile& y) {
-      const uint32_t xa = x.ia / B, xb = x.ib / B, ya = y.ia / B, yb = y.ib / B;
-      return xa != ya ? xa < ya : xb < yb;
-    });
-  }
-  if (ctx->pairs.alloc(npairs) || ctx->ptiles.alloc(tl.size()) || ctx->ptiles_blk.alloc(tb.size()) ||
+  if (ctx->pairs.alloc(npairs) || ctx->ptiles.alloc(tl.size()) || ctx->ptiles_blk.alloc(tl.size()) ||
       ctx->Linv.alloc(6 * (size_t)d.num_points) || ctx->Z.alloc((size_t)nb * 3 * (6 + d.ct)))
     return MI_BA_ERR_OUT_OF_MEMORY;
   if ((npairs && hipMemcpy(ctx->pairs.ptr, pr.data(), npairs * sizeof(uint2), hipMemcpyHostToDevice)) ||
-      (!tl.empty() && hipMemcpy(ctx->ptiles.ptr, tl.data(), tl.size() * sizeof(DevPairTile), hipMemcpyHostToDevice)) ||
-      (!tb.empty() && hipMemcpy(ctx->ptiles_blk.ptr, tb.data(), tb.size() * sizeof(DevPairTile), hipMemcpyHostToDevice)))
+      (!tl.empty() && hipMemcpy(ctx->ptiles.ptr, tl.data(), tl.size() * sizeof(DevPairTile), hipMemcpyHostToDevice)))
     return MI_BA_ERR_HIP;
+  ctx->ptiles_host = std::move(tl);
+  mi_ba_status st = order_block_tiles(ctx);
+  if (st != MI_BA_OK) return st;
   // stream-ordered: a null-stream memset is not ordered against the context's
   // non-blocking stream (the LM's kernels could overtake it)
   if (d.num_points && hipMemsetAsync(ctx->Linv.ptr, 0, 6 * (size_t)d.num_points * 8, ctx->stream)) return MI_BA_ERR_HIP;
@@ -432,7 +446,9 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
   d.loss_type = o->loss_function_type;
   d.loss_scale = o->loss_function_scale;
   d.jvariant = 0;
-  d.svariant = 0;
+  // image-block tile order, dispatch-order mapping: schur_build 4.9 -> 3.4 ms
+  // at C4 (profiles/r3_ab_schur_order.jsonl)
+  d.svariant = 4;
   d.refine_mask = (o->refine_focal_length ? 1 : 0) | (o->refine_principal_point ? 2 : 0) |
                   (o->refine_extra_params ? 4 : 0);
   d.obs_xy = ctx->obs_xy.ptr;
@@ -570,9 +586,9 @@ void context_destroy(mi_ba_context* ctx) {
 mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   hipStream_t s = ctx->stream;
   const DevProblem& d = ctx->dev;
-  MI_HIP(hipMemsetAsync(ctx->scalars.ptr, 0, sizeof(double) * kNumScalars, s));
   hipEvent_t stop;
-  launch_pack_images(d, ctx->img_rec.ptr, s);
+  // image records + the scalar slots zeroed in one launch
+  launch_pack_images(d, ctx->img_rec.ptr, s, ctx->scalars.ptr, kNumScalars);
   // linearize_overlap: the semantic kernel (FP64/latency-bound) on a second
   // stream beside the reprojection kernel (HBM-write-bound); joined below
   const bool overlap = ctx->sem && ctx->lin_overlap;
@@ -1490,9 +1506,18 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
   return reduce_fixed_cost(ctx);
 }
 
+// A/B variants measured slower than the defaults are compiled into the tools
+// build only (make ab -> libmi_ba_ab.so, MI_BA_AB_VARIANTS); the product
+// library accepts their keys with the default value alone.
+#ifdef MI_BA_AB_VARIANTS
+static bool ab_value(int, int) { return true; }
+#else
+static bool ab_value(int value, int product) { return value == product; }
+#endif
+
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value) {
   if (!ctx || !key) return MI_BA_ERR_INVALID_ARGUMENT;
-  if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 63) {
+  if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 63 && ab_value(value, 0)) {
     ctx->dev.jvariant = value;
     return MI_BA_OK;
   }
@@ -1508,18 +1533,18 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->sem_diag = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "semantic_variant") == 0 && value >= 0 && value <= 6) {
+  if (std::strcmp(key, "semantic_variant") == 0 && value >= 0 && value <= 6 && ab_value(value, 6)) {
     ctx->sem_variant = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 4) {
+  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 4 &&
+      (value == 0 || value == 4 || ab_value(value, 0))) {
     ctx->dev.svariant = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "schur_block_images") == 0 && value >= 1) {
-    // takes effect when the pair tiles are built (before the first solve)
     ctx->schur_block = value;
-    return MI_BA_OK;
+    return ctx->ptiles_host.empty() ? MI_BA_OK : order_block_tiles(ctx);
   }
   if (std::strcmp(key, "cholesky_panel") == 0 && (value == 0 || (value >= 64 && value <= 4096))) {
     ctx->chol.panel = value;
@@ -1529,7 +1554,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.lookahead = value != 0;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_own_diag") == 0 && value >= 0 && value <= 7) {
+  if (std::strcmp(key, "cholesky_own_diag") == 0 && value >= 0 && value <= 7 && (value != 7 || ab_value(value, 6))) {
     ctx->chol.own_diag = value;
     return MI_BA_OK;
   }
@@ -1541,15 +1566,16 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.gemm_solution = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 3) {
+  if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 3 &&
+      (value == 0 || value == 3 || ab_value(value, 3))) {
     ctx->chol.rest_update = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_tile_factor") == 0 && (value == 1 || value == 2)) {
+  if (std::strcmp(key, "cholesky_tile_factor") == 0 && (value == 1 || value == 2) && ab_value(value, 2)) {
     ctx->chol.tile_factor = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_write_through") == 0 && (value == 0 || value == 1)) {
+  if (std::strcmp(key, "cholesky_write_through") == 0 && (value == 0 || value == 1) && ab_value(value, 1)) {
     ctx->chol.write_through = value != 0;
     return MI_BA_OK;
   }

@@ -199,7 +199,7 @@ __device__ inline void quat_matrix_un(const double q[4], double Q[9]) {
   Q[6] = 2.0 * (bd - ac);  Q[7] = 2.0 * (ab + cd);  Q[8] = aa - bb - cc + dd;
 }
 
-__device__ inline double rcp_refined(double x) {
+[[maybe_unused]] __device__ inline double rcp_refined(double x) {
   double r = __builtin_amdgcn_rcp(x);
   r = fma(r, fma(-x, r, 1.0), r);
   r = fma(r, fma(-x, r, 1.0), r);
@@ -416,15 +416,21 @@ __device__ inline void stencil_prep(const double* q1, const double* t1, const do
 }
 
 // Two pairs per 64-lane workgroup: lanes 0..27 of each half fill the stencil
-// tables, lane 28 the pair's base constants.
+// tables, lane 28 the pair's base constants.  The pair's accumulator record
+// (blk_stride doubles of pair_blk) and deferred-sample count are cleared here
+// too (two launches fewer than separate memsets).
 __global__ void semantic_pair_prep_kernel(const SemPair* __restrict__ pairs, int npairs, const double* __restrict__ qt,
                                           const double* __restrict__ cam, const uint32_t* __restrict__ img_cam,
                                           const uint32_t* __restrict__ img_flags,
                                           const uint32_t* __restrict__ raster_slot, double rel_step,
-                                          PairConst* __restrict__ out) {
+                                          PairConst* __restrict__ out, double* __restrict__ pair_blk, int blk_stride,
+                                          uint32_t* __restrict__ pair_cnt) {
   const int k = blockIdx.x * 2 + (threadIdx.x >> 5);
   const int lane = threadIdx.x & 31;
-  if (k >= npairs || lane > 28) return;
+  if (k >= npairs) return;
+  for (int e = lane; e < blk_stride; e += 32) pair_blk[(size_t)k * blk_stride + e] = 0.0;
+  if (pair_cnt && lane == 31) pair_cnt[k] = 0u;
+  if (lane > 28) return;
   const SemPair pr = pairs[k];
   if (lane < 28) {
     const double* a1 = qt + 8 * (size_t)pr.i;
@@ -1671,17 +1677,19 @@ void semantic_destroy(mi_ba_context* ctx) {
 mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples) {
   SemanticState* S = ctx->sem;
   hipStream_t s = ctx->stream;
-  if (S->npairs && hipMemsetAsync(S->pair_blk.ptr, 0, S->pair_blk.bytes(), s) != hipSuccess) return MI_BA_ERR_HIP;
   S->samples_valid = write_samples;
-  if (S->ns == 0) return MI_BA_OK;
+  if (S->ns == 0) {
+    if (S->npairs && hipMemsetAsync(S->pair_blk.ptr, 0, S->pair_blk.bytes(), s) != hipSuccess) return MI_BA_ERR_HIP;
+    return MI_BA_OK;
+  }
   SemArgs a = make_args(ctx, ctx->dev.qt, ctx->dev.cam);
   PairConst* pcs = reinterpret_cast<PairConst*>(S->pconst.ptr);
   hipEvent_t stop;
   timer_begin(ctx, "semantic_jacobian", &stop);
   hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 1) / 2), dim3(64), 0, s, S->pairs.ptr, S->npairs,
-                     a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs);
+                     a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs, S->pair_blk.ptr, kPairStride,
+                     ctx->sem_variant == 6 ? S->pair_cnt.ptr : nullptr);
   if (ctx->sem_variant == 6) {
-    if (hipMemsetAsync(S->pair_cnt.ptr, 0, sizeof(uint32_t) * S->npairs, s) != hipSuccess) return MI_BA_ERR_HIP;
     const int ws = write_samples ? 1 | (ctx->sem_diag ? 2 : 0) : 0;
     for (int model = 0; model < kNumModels; ++model) {
       const int t0 = S->model_tiles[model], nt = S->model_tiles[model + 1] - t0;
@@ -1698,6 +1706,8 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
       });
     }
   }
+#ifdef MI_BA_AB_VARIANTS
+  // the one-kernel routes (variants 0-5), kept for A/B in the tools build
   for (int model = 0; model < kNumModels && ctx->sem_variant != 6; ++model) {
     const int t0 = S->model_tiles[model], nt = S->model_tiles[model + 1] - t0;
     if (nt == 0) continue;
@@ -1718,6 +1728,7 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
       }
     });
   }
+#endif
   timer_end(ctx, stop);
   launch_sum(S->partial.ptr, S->ntiles, d_cost, s);
   if (hipGetLastError() != hipSuccess) return MI_BA_ERR_HIP;

@@ -16,7 +16,11 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmi_ba.so")
+# MI_BA_LIB=ab selects the tools-only A/B build (libmi_ba_ab.so: `make ab`,
+# the measured-slower kernel variants compiled in) for tools/ab_*.py; tests,
+# smoke() and bench.py load the product library.
+AB_LIB_PATH = os.path.join(_HERE, "libmi_ba_ab.so")
+LIB_PATH = AB_LIB_PATH if os.environ.get("MI_BA_LIB") == "ab" else os.path.join(_HERE, "libmi_ba.so")
 SYNTH_PATH = os.path.join(_HERE, "libmi_ba_synth.so")
 
 # status codes / enums (mi_ba.h)
@@ -235,7 +239,8 @@ def load(path: str = LIB_PATH):
     if _lib is not None:
         return _lib
     if not os.path.exists(path):
-        raise RuntimeError(f"libmi_ba.so not built at {path} (run __graft_entry__.build())")
+        raise RuntimeError(f"{os.path.basename(path)} not built at {path} "
+                           "(run __graft_entry__.build(); the A/B build: make -C semantic-bundle-adjustment-colmap_amd ab)")
     lib = C.CDLL(path)
     lib.mi_ba_abi_version.restype = C.c_int32
     lib.mi_ba_status_string.restype = C.c_char_p
@@ -281,6 +286,12 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_positive_depth.argtypes = [C.c_void_p, _u8p, C.c_int32, _u8p, C.POINTER(C.c_int64)]
     _lib = lib
     return lib
+
+
+def ab_build() -> bool:
+    """True when the loaded library is the tools-only A/B build."""
+    load()
+    return LIB_PATH == AB_LIB_PATH
 
 
 def load_synth(path: str = SYNTH_PATH):

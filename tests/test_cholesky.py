@@ -235,7 +235,10 @@ def test_lm_tile_factor_and_publish(gpu):
     """The panel factor's 64x64 tile factor (block-column register sweeps
     with rsq (2) or sqrt + divide (1) pivots) and its publish (write-through
     sc1 stores drained before the flag vs plain stores + __threadfence())
-    drive the same LM (nf = 1593: 4 panels), all four combinations."""
+    drive the same LM (nf = 1593: 4 panels), all four combinations (the
+    non-default ones are in the tools-only A/B build)."""
+    if not mi_ba.ab_build():
+        pytest.skip("tile factor 1 / plain-store publish: tools build only (MI_BA_LIB=ab)")
     sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)

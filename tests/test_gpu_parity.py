@@ -240,6 +240,8 @@ def test_semantic_kernel_variants_bitwise(gpu, model, variant):
     deferred-sample pass)
     reproduces the oracle's samples bit for bit, constant first/second poses
     and a constant tvec component included (gauge)."""
+    if variant != 6 and not mi_ba.ab_build():
+        pytest.skip("one-kernel A/B route: tools build only (MI_BA_LIB=ab)")
     sc, sem = semantic_scene(model, images=4, size=160, step=3, seed=5)
     opts = mi_ba.default_options()
     px_o, st_o, r_o, J_o = oracle.semantic_eval(opts, sc, sem)

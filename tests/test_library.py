@@ -51,6 +51,17 @@ def test_library_is_gfx950_code_object():
     assert b"amdgcn-amd-amdhsa--gfx950" in data
 
 
+def test_product_library_ships_no_ab_variants():
+    """The measured-slower A/B kernel variants are compiled into the
+    tools-only build (make ab -> libmi_ba_ab.so) and not into the product
+    library: its code object holds none of their kernels."""
+    prod = os.path.join(os.path.dirname(mi_ba.__file__), "libmi_ba.so")
+    data = open(prod, "rb").read()
+    for name in (b"schur_pairs_pipelined_kernel", b"semantic_linearize_kernel", b"panel_factor_kernelILi1E"):
+        assert name not in data, name
+    assert b"semantic_flat_kernel" in data and b"schur_pairs_kernel" in data
+
+
 def test_default_options_match_reference():
     # BundleAdjustmentOptions() (bundle_adjustment.h:49-92) + Ceres 2.1 defaults
     o = mi_ba.default_options()

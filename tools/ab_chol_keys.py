@@ -7,6 +7,8 @@ import json
 import sys
 
 sys.path.insert(0, 'semantic-bundle-adjustment-colmap_amd')
+import os as _os
+_os.environ.setdefault("MI_BA_LIB", "ab")  # A/B variants: the tools-only build (make ab)
 import mi_ba  # noqa: E402
 
 c = mi_ba.synth_config(mi_ba.OPENCV, 1000, 1_000_000, track_length=10, rotation_range=0.05,

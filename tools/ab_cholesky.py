@@ -1,6 +1,8 @@
 """A/B of the LM-phase timings at C4 over Cholesky tuning keys (own_diag, lookahead, panel, solve).
     python tools/ab_cholesky.py"""
 import sys, time, json
+import os as _os
+_os.environ.setdefault("MI_BA_LIB", "ab")  # A/B variants: the tools-only build (make ab)
 sys.path.insert(0,'semantic-bundle-adjustment-colmap_amd')
 import numpy as np, mi_ba
 c = mi_ba.synth_config(mi_ba.OPENCV, 1000, 1_000_000, track_length=10, rotation_range=0.05, extra=(-0.1, 0.01, 1e-4, -1e-4))

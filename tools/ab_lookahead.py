@@ -2,6 +2,8 @@
 final cost and wall time with the side-stream factor on and off.   python tools/ab_lookahead.py
 """
 import sys, json, time
+import os as _os
+_os.environ.setdefault("MI_BA_LIB", "ab")  # A/B variants: the tools-only build (make ab)
 sys.path.insert(0, "semantic-bundle-adjustment-colmap_amd"); sys.path.insert(0, ".")
 import mi_ba, bench
 cfg = dict(bench.CONFIGS["C4"])

@@ -4,6 +4,8 @@ LM per combination of the given keys.
 import json
 import sys
 
+import os as _os
+_os.environ.setdefault("MI_BA_LIB", "ab")  # A/B variants: the tools-only build (make ab)
 sys.path.insert(0, 'semantic-bundle-adjustment-colmap_amd')
 import mi_ba  # noqa: E402
 
