@@ -1137,17 +1137,17 @@ rocblas_status backward(rocblas_handle h, int n, const double* A, int lda, doubl
 // block, dtrsm of the panel below it, then the trailing lower triangle
 // updated by dsyrk (or by dgemm per block column of width `panel`).
 rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, int own,
-                            double* scratch, CholWorkspace* ws);
+                            double* scratch, CholWorkspace* ws, int ex);
 rocblas_status gemm_nt(rocblas_handle h, int m, int n, int k, const double* P, int ldp, double* C, int ldc, int sol);
 
 rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
-                              double* scratch, CholWorkspace* ws) {
+                              double* scratch, CholWorkspace* ws, int ex) {
   const double one = 1.0, minus_one = -1.0;
   const int nb = cfg.panel;
   for (int k = 0; k < n; k += nb) {
     const int kb = std::min(nb, n - k);
     double* Akk = A + k + (size_t)k * lda;
-    rocblas_status st = panel_factor(h, n, A, lda, k, kb, info++, cfg.own_diag, scratch, ws);
+    rocblas_status st = panel_factor(h, n, A, lda, k, kb, info++, cfg.own_diag, scratch, ws, ex);
     if (st != rocblas_status_success) return st;
     const int m = n - k - kb;
     if (m == 0) break;
@@ -1156,6 +1156,11 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
     if (!cfg.gemm_update) {
       st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, m, kb, &minus_one, Aik, lda, &one, T, lda);
       if (st != rocblas_status_success) return st;
+      if (ex > 0) {  // the extra rows below the trailing matrix
+        st = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, ex, m, kb, &minus_one, Aik + m, lda,
+                           Aik, lda, &one, T + m, lda);
+        if (st != rocblas_status_success) return st;
+      }
     } else {
       // the look-ahead's partition and GEMM solution (block column k+1, then
       // columns of width nb or 2 nb): both orders run the same GEMMs on the
@@ -1164,7 +1169,7 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
       for (int j = 0; j < m; j = j == 0 ? jb0 : j + cw) {
         const int jb = std::min(j == 0 ? jb0 : cw, m - j);
-        st = gemm_nt(h, m - j, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
+        st = gemm_nt(h, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
         if (st != rocblas_status_success) return st;
       }
     }
@@ -1180,11 +1185,11 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
 // diagonal factor behind the MFMA update.
 // own_diag 6: diagonal factor + panel solve in one panel_factor_kernel launch
 rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info,
-                                  CholWorkspace* ws) {
+                                  CholWorkspace* ws, int ex) {
   if (!ws || !ws->pf_ctrl || !ws->pf_linv || !ws->err || kb > 64 * kPfMaxTiles) return rocblas_status_invalid_pointer;
   hipStream_t s;
   if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
-  const int mrows = n - k;
+  const int mrows = n - k + ex;  // the extra rows below the matrix take the panel solve too
   const int nc = (kb + 63) / 64;
   const int nbelow = (mrows - kb + 63) / 64;
   const int nr = nc + nbelow;  // workgroups (tickets) of the launch: one per row tile
@@ -1213,12 +1218,12 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
 // diagonal block (rocBLAS dtrtri) instead of a dtrsm: the panel solve runs at
 // dgemm rate off a copy of the panel.
 rocblas_status panel_factor_inv(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info,
-                                double* scratch, CholWorkspace* ws) {
-  if (!ws || !ws->tinv || !ws->tbuf || kb > kTinv || n - k - kb > ws->tbuf_rows) return rocblas_status_invalid_pointer;
+                                double* scratch, CholWorkspace* ws, int ex) {
+  if (!ws || !ws->tinv || !ws->tbuf || kb > kTinv || n - k - kb + ex > ws->tbuf_rows) return rocblas_status_invalid_pointer;
   double* Akk = A + k + (size_t)k * lda;
   rocblas_status st = potrf_leaf(h, kb, Akk, lda, info, 2, scratch);
   if (st != rocblas_status_success) return st;
-  const int m = n - k - kb;
+  const int m = n - k - kb + ex;
   if (m == 0) return st;
   hipStream_t s;
   if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
@@ -1235,15 +1240,15 @@ rocblas_status panel_factor_inv(rocblas_handle h, int n, double* A, int lda, int
 #endif
 
 rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, int own,
-                            double* scratch, CholWorkspace* ws) {
-  if (own == 6) return panel_factor_fused(h, n, A, lda, k, kb, info, ws);
+                            double* scratch, CholWorkspace* ws, int ex) {
+  if (own == 6) return panel_factor_fused(h, n, A, lda, k, kb, info, ws, ex);
 #ifdef MI_BA_AB_VARIANTS
-  if (own == 7) return panel_factor_inv(h, n, A, lda, k, kb, info, scratch, ws);
+  if (own == 7) return panel_factor_inv(h, n, A, lda, k, kb, info, scratch, ws, ex);
 #endif
   double* Akk = A + k + (size_t)k * lda;
   rocblas_status st = potrf_leaf(h, kb, Akk, lda, info, own, scratch);
   if (st != rocblas_status_success) return st;
-  const int m = n - k - kb;
+  const int m = n - k - kb + ex;
   if (m == 0) return st;
   const double one = 1.0;
   return rocblas_dtrsm(h, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
@@ -1268,7 +1273,7 @@ rocblas_status gemm_nt(rocblas_handle h, int m, int n, int k, const double* P, i
 }
 
 rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
-                                CholWorkspace& ws) {
+                                CholWorkspace& ws, int ex) {
   [[maybe_unused]] const double minus_one = -1.0, one = 1.0;  // rest_update 1 / 2 (tools build)
   const int nb = cfg.panel;
   hipStream_t s1;
@@ -1276,7 +1281,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
   if (ws.ev.size() < 2 * (size_t)((n + nb - 1) / nb)) return rocblas_status_invalid_size;
   double* scratch_main = ws.scratch;
   double* scratch_side = ws.scratch + kSub * kSub;
-  rocblas_status st = panel_factor(h, n, A, lda, 0, std::min(nb, n), info, cfg.own_diag, scratch_main, &ws);
+  rocblas_status st = panel_factor(h, n, A, lda, 0, std::min(nb, n), info, cfg.own_diag, scratch_main, &ws, ex);
   if (st != rocblas_status_success) return st;
   // On a failure after the side stream got work, the caller's stream waits
   // for it (the caller may free A / info once its own stream is drained).
@@ -1294,22 +1299,22 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     double* T = Aik + (size_t)kb * lda;          // trailing matrix, lower triangle
     // block column k+1 first
     const int jb0 = std::min(nb, m);
-    st = gemm_nt(h, m, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
+    st = gemm_nt(h, m + ex, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
     if (st != rocblas_status_success) return fail(st);
     hipEvent_t upd = ws.ev[2 * kk], pan = ws.ev[2 * kk + 1];
     if (hipEventRecord(upd, s1) != hipSuccess || hipStreamWaitEvent(ws.side, upd, 0) != hipSuccess)
       return fail(rocblas_status_internal_error);
-    st = panel_factor(ws.side_h, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag, scratch_side, &ws);
+    st = panel_factor(ws.side_h, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag, scratch_side, &ws, ex);
     if (st != rocblas_status_success) return fail(st);
     if (hipEventRecord(pan, ws.side) != hipSuccess) return fail(rocblas_status_internal_error);
     // the rest of the trailing lower triangle (columns jb0 .. m)
     [[maybe_unused]] const int mr = m - jb0;
 #ifdef MI_BA_AB_VARIANTS
-    if (mr > 0 && cfg.rest_update == 1) {
+    if (mr > 0 && cfg.rest_update == 1 && ex == 0) {
       st = rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, mr, kb, &minus_one, Aik + jb0, lda, &one,
                          T + jb0 + (size_t)jb0 * lda, lda);
       if (st != rocblas_status_success) return fail(st);
-    } else if (mr > 0 && cfg.rest_update == 2) {
+    } else if (mr > 0 && cfg.rest_update == 2 && ex == 0) {
       st = rocblas_dgemmt(h, rocblas_fill_lower, rocblas_operation_none, rocblas_operation_transpose, mr, kb,
                           &minus_one, Aik + jb0, lda, Aik + jb0, lda, &one, T + jb0 + (size_t)jb0 * lda, lda);
       if (st != rocblas_status_success) return fail(st);
@@ -1320,7 +1325,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
       for (int j = jb0; j < m; j += cw) {
         const int jb = std::min(cw, m - j);
-        st = gemm_nt(h, m - j, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
+        st = gemm_nt(h, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
         if (st != rocblas_status_success) return fail(st);
       }
     }
@@ -1431,8 +1436,9 @@ void CholWorkspace::destroy() {
 }
 
 rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
-                           CholWorkspace* ws) {
+                           CholWorkspace* ws, int extra_rows) {
   if (n <= 0) return rocblas_status_success;
+  if (extra_rows < 0 || lda < n + extra_rows || (extra_rows > 0 && cfg.panel <= 0)) return rocblas_status_invalid_size;
   if (cfg.own_diag && (!ws || !ws->scratch)) return rocblas_status_invalid_pointer;
   // the one-launch panel factor needs panels of at most 8 tiles: other panel
   // widths (and the recursive split) take the two-kernel diagonal factor
@@ -1450,8 +1456,8 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   }
   double* scratch = ws ? ws->scratch : nullptr;
   if (c.panel > 0 && c.gemm_update && c.lookahead && ws && ws->side)
-    return factor_lookahead(h, n, A, lda, info, c, *ws);
-  if (c.panel > 0) return factor_blocked(h, n, A, lda, info, c, scratch, ws);
+    return factor_lookahead(h, n, A, lda, info, c, *ws, extra_rows);
+  if (c.panel > 0) return factor_blocked(h, n, A, lda, info, c, scratch, ws, extra_rows);
   return factor(h, n, A, lda, info, c.own_diag, scratch);
 }
 
@@ -1464,6 +1470,24 @@ hipError_t chol_error(CholWorkspace* ws, hipStream_t s, unsigned* word) {
   if (e == hipSuccess && h != 0) e = hipMemsetAsync(ws->err, 0, sizeof(unsigned), s);
   if (e == hipSuccess) *word = h;
   return e;
+}
+
+rocblas_status chol_solve_backward(rocblas_handle h, int n, const double* A, int lda, double* x, CholWorkspace* ws) {
+  if (n <= 0) return rocblas_status_success;
+  if (!ws || !ws->ctrl || !ws->err || n > ws->linv_rows) return rocblas_status_invalid_pointer;
+  hipStream_t s;
+  if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
+  if (ws->epoch > 0xfffffff0u) {
+    if (hipMemsetAsync(ws->ctrl, 0, sizeof(unsigned) * (2 + (size_t)ws->linv_rows / kTB), s) != hipSuccess)
+      return rocblas_status_internal_error;
+    ws->epoch = 0;
+  }
+  if (hipMemsetAsync(ws->ctrl + 1, 0, sizeof(unsigned), s) != hipSuccess) return rocblas_status_internal_error;
+  const unsigned e = ++ws->epoch;
+  const int nblk = (n + kTB - 1) / kTB;
+  hipLaunchKernelGGL(trsv_sweep_kernel<false>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e,
+                     ws->err, ws->spin_limit);
+  return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
 
 rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x, int variant,

@@ -123,8 +123,13 @@ struct CholWorkspace {
 // ws is required for own_diag and for look-ahead; every exit path leaves no
 // work of this call pending on the side stream that h's stream does not wait
 // for.
+// extra_rows > 0 (blocked factorisations only, lda >= n + extra_rows): the
+// rows n .. n + extra_rows - 1 below the matrix are carried through the
+// factorisation as rows of a trapezoid, so on return they hold B L^-T for the
+// B they held on entry — for B = b' the forward solve L y = b (y' in row n)
+// comes out of the panel solves and trailing updates at no extra pass.
 rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
-                           CholWorkspace* ws);
+                           CholWorkspace* ws, int extra_rows = 0);
 int chol_leaf_count(int n, const CholConfig& cfg = {});
 // x := (L L')^-1 x with the factor chol_factor left in A, on h's stream.
 // variant 2 (default): sync-free forward / backward sweeps, one launch each
@@ -133,6 +138,9 @@ int chol_leaf_count(int n, const CholConfig& cfg = {});
 // (ws unused).
 rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, double* x, int variant,
                           CholWorkspace* ws);
+// x := L'^-1 x (the backward sweep of chol_solve variant 2 alone), after a
+// factorisation whose extra row delivered the forward solve.
+rocblas_status chol_solve_backward(rocblas_handle h, int n, const double* A, int lda, double* x, CholWorkspace* ws);
 // Error word of the factorisations / solves issued on stream s since the last
 // call (synchronises s, then clears the word): 0, or kCholErr* bits.  A
 // nonzero word means a result of those calls is invalid; callers report it

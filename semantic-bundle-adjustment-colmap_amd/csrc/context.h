@@ -84,6 +84,8 @@ struct mi_ba_context {
   miba::DevArray<miba::DevPoint> vpoints;
   int64_t npv = 0;
   int64_t nb_const = 0;  // reduced blocks of constant points
+  miba::DevArray<uint32_t> pchunks;  // [npchunks + 1] point-chunk boundaries (backsub_chunk_kernel)
+  int npchunks = 0;
   bool lin_overlap = false;            // semantic kernel on lin_side beside the reprojection kernel
   int lin_order = 0;                   // 0 reprojection kernel first, 1 semantic pass first
   hipStream_t lin_side = nullptr;
@@ -119,6 +121,7 @@ struct mi_ba_context {
   int nptiles = 0;
   miba::DevArray<int32_t> info;
   miba::CholConfig chol;                   // factorisation variant (mi_ba_set_tuning)
+  bool fused_rhs = true;                   // forward solve carried through the factorisation (S's spare row)
   miba::CholWorkspace cholws;              // side stream / handle / events / scratch of this context
 
   double fixed_cost = 0.0;

@@ -61,6 +61,9 @@ struct DevProblem {
   int num_images, num_cameras;
   int64_t num_points;
   int64_t nf;          // f-vector length: 6*I + ct*C (+ 8 per GSBA cylinder: fixed slots, masked)
+  int64_t lds;         // leading dimension of the explicit S (row-major upper = column-major lower): nf + 1
+                       // rounded to 16 on the exact path, whose extra column-major row n carries the
+                       // right-hand side through the factorisation (forward solve fused), else nf
   int64_t cyl0;        // first GSBA cylinder slot (= 6*I + ct*C)
   int cyl_var;         // GSBA cylinders are parameters (refine_geometry)
   int loss_type;
@@ -68,6 +71,7 @@ struct DevProblem {
   int refine_mask;     // bit0 focal, bit1 principal point, bit2 extra params
   int jvariant;        // Jacobian store path (kernels.hip reproj_jacobian_kernel V)
   int svariant;        // explicit Schur pair kernel (kernels.hip launch_dense_schur)
+  int fvariant;        // exact-path fblock kernel: 0 per-lane rows (default), 1 LDS-staged MFMA (tools build)
   // inputs
   const double2* obs_xy;
   const uint32_t* obs_img;

@@ -533,10 +533,10 @@ __global__ void gsba_product_kernel(const GsbaBlock* __restrict__ blocks, int nb
   }
 }
 
-// S += J'J (upper triangle, row-major nf x nf).
+// S += J'J (upper triangle, row-major, leading dimension lds).
 __global__ void gsba_dense_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
                                   const uint32_t* __restrict__ img_flags, const double* __restrict__ J, int64_t cyl0,
-                                  int cyl_var, int cw, int64_t nf, double* __restrict__ S) {
+                                  int cyl_var, int cw, int64_t lds, double* __restrict__ S) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)nblocks * 196) return;
   const int k = (int)(t / 196), e = (int)(t % 196);
@@ -546,7 +546,7 @@ __global__ void gsba_dense_kernel(const GsbaBlock* __restrict__ blocks, int nblo
   const int64_t ra = gsba_slot(b, a, cyl0, cyl_var, pv, cw), rc = gsba_slot(b, c, cyl0, cyl_var, pv, cw);
   if (ra < 0 || rc < 0 || ra > rc) return;
   const double* Jr = J + 14 * (size_t)k;
-  atomicAdd(S + ra * nf + rc, Jr[a] * Jr[c]);
+  atomicAdd(S + ra * lds + rc, Jr[a] * Jr[c]);
 }
 
 // model cost change contribution -(e (r + e / 2)), e = J df
@@ -832,7 +832,7 @@ void gsba_add_dense(mi_ba_context* ctx, double* S) {
   if (!G->nblocks) return;
   const int64_t n = (int64_t)G->nblocks * 196;
   hipLaunchKernelGGL(gsba_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, G->blocks.ptr,
-                     G->nblocks, ctx->dev.img_flags, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw, ctx->dev.nf, S);
+                     G->nblocks, ctx->dev.img_flags, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw, ctx->dev.lds, S);
 }
 
 void gsba_model_cost(mi_ba_context* ctx, const double* df, double* d_out) {

@@ -90,6 +90,12 @@ void launch_backsub(const DevProblem& p, const DevPoint* vp, int64_t npv, const 
 // Back substitution + model cost change in one pass over the variable
 // points' blocks (per-wave partials into partial, count returned; the
 // blocks of constant points, const_blocks, atomically into partial[0]).
+// Back substitution + model cost change over point chunks (blocks
+// [chunk[c], chunk[c+1]) of whole points, <= 64 unless one point has more):
+// one partial per chunk into partial[0..nchunks), returns nchunks.
+int64_t launch_backsub_chunks(const DevProblem& p, const uint32_t* chunk, int nchunks, const double* J,
+                              const double2* r, const double* Vg, const double* Vinv, const double* df, double* dX,
+                              double* partial, hipStream_t s);
 int64_t launch_backsub_cost(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* J, const double2* r,
                             const double* Vg, const double* Vinv, const double* df, double* dX, double* partial,
                             bool const_blocks, hipStream_t s);

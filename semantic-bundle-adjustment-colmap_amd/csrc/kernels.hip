@@ -890,15 +890,120 @@ __global__ __launch_bounds__(kBlock) void fblock_dense_kernel(DevProblem p, cons
     if (!(va && vc)) return;
     const int64_t ra = fslot(p, img, cam, a), rc = fslot(p, img, cam, c);
     if (ra <= rc)
-      atomicAdd(S + ra * p.nf + rc, v);
+      atomicAdd(S + ra * p.lds + rc, v);
     else
-      atomicAdd(S + rc * p.nf + ra, v);
+      atomicAdd(S + rc * p.lds + ra, v);
     if (a == c) atomicAdd(udiag + ra, v);
   } else {
     const int m = k - NU;
     if (m < 6 ? pv : cv) atomicAdd(bvec + fslot(p, img, cam, m), v);
   }
 }
+
+// As fblock_dense_kernel, on the matrix cores (tools build, fblock_variant
+// 1: measured slower — the row gathers bind, and the 70 KB LDS slab halves
+// the waves in flight): with
+// X = [J_f | e] (two rows per block, F + 1 <= 16 columns, e = r - J_p q_p),
+// U and b are blocks of X'X, one v_mfma_f64_16x16x4f64 per two blocks: lane
+// (m, k) supplies X[4s + k][m] as both the A (X') and the B (X) operand.
+// Each wave gathers its 64 camera-major rows into an LDS slab with 16-B
+// loads spread over the rows (about 4 rows per wave-instruction, where a
+// lane walking its own row touches 64 lines per instruction), forms e there,
+// then runs the MFMA steps; the four waves' accumulators are summed in fixed
+// order and scattered as fblock_dense_kernel does.
+#ifdef MI_BA_AB_VARIANTS
+template <int CT>
+__global__ __launch_bounds__(kBlock) void fblock_mfma_kernel(DevProblem p, const DevTile* __restrict__ tiles,
+                                                              const uint32_t* __restrict__ cm_perm,
+                                                              const double2* __restrict__ rr,
+                                                              const double* __restrict__ J,
+                                                              const double* __restrict__ q,
+                                                              double* __restrict__ bvec,
+                                                              double* __restrict__ udiag, double* __restrict__ S) {
+  constexpr int F = 6 + CT, W = 9 + CT, W2 = 2 * W, H = W;  // H: 16-B pieces per J row
+  constexpr int LS = W2 + 4;                                // J row, e (2), pad: 16-B rows
+  static_assert(F + 1 <= 16, "X = [J_f | e] must fit the 16-wide MFMA tile");
+  typedef double dvec4 __attribute__((ext_vector_type(4)));
+  __shared__ double sl[kBlock / 64][64 * LS];
+  const DevTile tile = tiles[blockIdx.x];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double* slab = sl[wv];
+  const int m = lane & 15, kq = lane >> 4;
+  const int cm = m < 6 ? m : (m < F ? 3 + m : (m == F ? W2 : -1));  // X column m within a slab row (+ rw W)
+  dvec4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (uint32_t c0 = 64u * wv; c0 < tile.count; c0 += kBlock) {
+    const int live = (int)min(64u, tile.count - c0);
+    const uint32_t bl = lane < live ? cm_perm[tile.start + c0 + lane] : 0u;
+#pragma unroll
+    for (int it = 0; it < H; ++it) {
+      const int e = lane + 64 * it;
+      const int row = e / H, col = e - row * H;
+      const uint32_t b = (uint32_t)__shfl((int)bl, row < 64 ? row : 0);
+      if (row < live) {
+        const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(J + (size_t)b * W2) + col);
+        *reinterpret_cast<dvec2*>(slab + row * LS + 2 * col) = v;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (lane < live) {
+      const uint32_t pt = p.obs_pt[bl];
+      const double2 r = rr[bl];
+      double qp[3] = {0.0, 0.0, 0.0};
+      if (p.pt_var[pt]) {
+        qp[0] = q[3 * (size_t)pt];
+        qp[1] = q[3 * (size_t)pt + 1];
+        qp[2] = q[3 * (size_t)pt + 2];
+      }
+      double* row = slab + lane * LS;
+      row[W2] = r.x - (row[6] * qp[0] + row[7] * qp[1] + row[8] * qp[2]);
+      row[W2 + 1] = r.y - (row[W + 6] * qp[0] + row[W + 7] * qp[1] + row[W + 8] * qp[2]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int nsteps = (2 * live + 3) >> 2;
+    for (int st = 0; st < nsteps; ++st) {
+      const int R = 4 * st + kq, j = R >> 1, rw = R & 1;
+      double x = 0.0;
+      if (j < live && cm >= 0) x = slab[j * LS + (cm == W2 ? W2 + rw : rw * W + cm)];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, x, acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  // the four waves' tiles summed in wave order
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) slab[r * 64 + lane] = acc[r];
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r] = sl[0][r * 64 + lane] + sl[1][r * 64 + lane] + sl[2][r * 64 + lane] + sl[3][r * 64 + lane];
+  const uint32_t img = tile.image, cam = p.img_cam[img];
+  const bool pv = p.img_flags[img] & 1u, cv = p.cam_var[cam] != 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int a = 4 * r + kq, c = m;  // D[4r + l/16][l%16]
+    if (a >= F || c > F || (c < F && c < a)) continue;
+    const double v = acc[r];
+    const bool va = a < 6 ? pv : cv;
+    if (!va) continue;
+    const int64_t ra = fslot(p, img, cam, a);
+    if (c == F) {
+      atomicAdd(bvec + ra, v);
+      continue;
+    }
+    if (!(c < 6 ? pv : cv)) continue;
+    const int64_t rc = fslot(p, img, cam, c);
+    if (ra <= rc)
+      atomicAdd(S + ra * p.lds + rc, v);
+    else
+      atomicAdd(S + rc * p.lds + ra, v);
+    if (a == c) atomicAdd(udiag + ra, v);
+  }
+}
+
+#endif  // MI_BA_AB_VARIANTS
 
 // Damp, Jacobi-scale and invert the diagonal blocks (one thread per block).
 template <int N>
@@ -1314,6 +1419,112 @@ __global__ __launch_bounds__(kBlock) void backsub_cost_kernel(DevProblem p, cons
   if ((threadIdx.x & 63) == 0 && k < npv) partial[k >> 6] = s;
 }
 
+// Back substitution + model cost change over point chunks (the default):
+// chunk c = blocks [chunk[c], chunk[c+1]) of whole points (point-major), at
+// most 64 blocks unless one point has more.  One lane per block: the wave
+// stages 64 J rows in its LDS slab with coalesced loads (a lane walking its
+// own point's rows touches a different line per lane and instruction: the
+// per-point loop of backsub_cost_kernel ran 1.33 ms at C4), forms
+// e = J_f df, the block's share -(e.r + |e|^2/2) of the model cost change and
+// t_b = J_p' e; the first lane of each variable point sums its points' t_b in
+// lane order (deterministic), then dX_p = -V_p^-1 (g_p + t) and the point's
+// terms -(dX.g_p + dX.t + dX' V_p dX / 2).  Blocks of constant points only
+// add their share.  One cost partial per chunk.
+template <int CT>
+__global__ __launch_bounds__(kBlock) void backsub_chunk_kernel(DevProblem p, const uint32_t* __restrict__ chunk,
+                                                                int nchunks, const double* __restrict__ J,
+                                                                const double2* __restrict__ rr,
+                                                                const double* __restrict__ Vg,
+                                                                const double* __restrict__ Vinv,
+                                                                const double* __restrict__ df,
+                                                                double* __restrict__ dX,
+                                                                double* __restrict__ partial) {
+  constexpr int W = 9 + CT, W2 = 2 * W, LS = W2 | 1;
+  __shared__ double sl[(kBlock / 64) * 64 * LS];
+  __shared__ uint32_t spt[kBlock / 64][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double* slab = sl + wv * 64 * LS;
+  uint32_t* wpt = spt[wv];
+  const int c = blockIdx.x * (kBlock / 64) + wv;
+  if (c >= nchunks) return;  // wave-uniform
+  const uint32_t b0 = chunk[c], b1 = chunk[c + 1];
+  const bool multi = b1 - b0 > 64u;  // one point with more than 64 blocks
+  double model = 0.0;
+  double carry[3] = {0.0, 0.0, 0.0};
+  uint32_t carry_pt = 0;
+  bool carry_var = false;
+  auto finalize = [&](uint32_t pt, const double t[3]) {
+    const double* g = Vg + 9 * (size_t)pt;
+    const double* vi = Vinv + 6 * (size_t)pt;
+    const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
+    const double tt[3] = {g[6] + t[0], g[7] + t[1], g[8] + t[2]};
+    double o[3];
+    sym3_mul(Vi, tt, o);
+    const double x[3] = {-o[0], -o[1], -o[2]};
+#pragma unroll
+    for (int n = 0; n < 3; ++n) dX[3 * (size_t)pt + n] = x[n];
+    double Vx[3];
+    sym3_mul(g, x, Vx);  // g[0..5] = V_p packed (undamped)
+    model -= x[0] * g[6] + x[1] * g[7] + x[2] * g[8] + x[0] * t[0] + x[1] * t[1] + x[2] * t[2] +
+             (x[0] * Vx[0] + x[1] * Vx[1] + x[2] * Vx[2]) / 2.0;
+  };
+  for (uint32_t s0 = b0; s0 < b1; s0 += 64) {
+    const int live = (int)min(64u, b1 - s0);
+    wave_load_rows<W2, LS>(J + (size_t)s0 * W2, slab, live);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const bool on = lane < live;
+    const uint32_t b = s0 + (on ? lane : 0);
+    const uint32_t pt = p.obs_pt[b];
+    const bool var = on && p.pt_var[pt] != 0;
+    double te[3] = {0.0, 0.0, 0.0};
+    if (on) {
+      const double* row = slab + lane * LS;
+      double e[2];
+      load_jf_x<CT>(p, row, p.obs_img[b], df, e);
+      const double2 r = rr[b];
+      model -= e[0] * r.x + e[1] * r.y + (e[0] * e[0] + e[1] * e[1]) / 2.0;
+      if (var) {
+#pragma unroll
+        for (int n = 0; n < 3; ++n) te[n] = row[6 + n] * e[0] + row[W + 6 + n] * e[1];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // segmented sum: t_b and the point id per lane in the slab
+    double* tv = slab + lane * 4;
+    tv[0] = te[0];
+    tv[1] = te[1];
+    tv[2] = te[2];
+    wpt[lane] = on ? pt : 0xffffffffu;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const bool head = var && (lane == 0 || wpt[lane - 1] != pt);
+    if (head) {
+      double t[3] = {te[0], te[1], te[2]};
+      for (int l = lane + 1; l < live && wpt[l] == pt; ++l) {
+        t[0] += slab[l * 4];
+        t[1] += slab[l * 4 + 1];
+        t[2] += slab[l * 4 + 2];
+      }
+      if (multi) {
+        carry[0] += t[0];
+        carry[1] += t[1];
+        carry[2] += t[2];
+        carry_pt = pt;
+        carry_var = true;
+      } else {
+        finalize(pt, t);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  if (multi && carry_var) finalize(carry_pt, carry);  // lane 0
+  const double s = wave_sum(model);
+  if (lane == 0) partial[c] = s;
+}
+
 // Model cost change of the blocks of constant points (no point step).
 template <int CT>
 __global__ __launch_bounds__(kBlock) void model_cost_const_kernel(DevProblem p, const double2* __restrict__ rr,
@@ -1484,9 +1695,9 @@ __global__ __launch_bounds__(kBlock) void dense_u_kernel(DevProblem p, const Dev
       const double v = sred[k];
       // upper triangle (row <= col) only: rocSOLVER reads the column-major lower
       if (ra <= rc)
-        atomicAdd(S + ra * p.nf + rc, v);
+        atomicAdd(S + ra * p.lds + rc, v);
       else
-        atomicAdd(S + rc * p.nf + ra, v);
+        atomicAdd(S + rc * p.lds + ra, v);
     }
   }
 }
@@ -1622,13 +1833,13 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
     const int64_t ra = fslot(p, ia, ca, mrow), rb = fslot(p, ib, cb, ncol);
     const double v = acc[r];
     if (tl.self) {
-      if (ra <= rb) atomicAdd(S + ra * p.nf + rb, -v);
+      if (ra <= rb) atomicAdd(S + ra * p.lds + rb, -v);
     } else if (ra < rb) {
-      atomicAdd(S + ra * p.nf + rb, -v);
+      atomicAdd(S + ra * p.lds + rb, -v);
     } else if (ra > rb) {
-      atomicAdd(S + rb * p.nf + ra, -v);
+      atomicAdd(S + rb * p.lds + ra, -v);
     } else {
-      atomicAdd(S + ra * p.nf + ra, -2.0 * v);
+      atomicAdd(S + ra * p.lds + ra, -2.0 * v);
     }
   }
 }
@@ -1705,13 +1916,13 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_pipelined_kernel(DevProble
     const int64_t ra = fslot(p, ia, ca, mrow), rb = fslot(p, ib, cb, ncol);
     const double v = acc[r];
     if (tl.self) {
-      if (ra <= rb) atomicAdd(S + ra * p.nf + rb, -v);
+      if (ra <= rb) atomicAdd(S + ra * p.lds + rb, -v);
     } else if (ra < rb) {
-      atomicAdd(S + ra * p.nf + rb, -v);
+      atomicAdd(S + ra * p.lds + rb, -v);
     } else if (ra > rb) {
-      atomicAdd(S + rb * p.nf + ra, -v);
+      atomicAdd(S + rb * p.lds + ra, -v);
     } else {
-      atomicAdd(S + ra * p.nf + ra, -2.0 * v);
+      atomicAdd(S + ra * p.lds + ra, -2.0 * v);
     }
   }
 }
@@ -1729,9 +1940,9 @@ __global__ void dense_finalize_kernel(DevProblem p, const double* __restrict__ l
     var = p.cam_var[(k - 6 * (int64_t)p.num_images) / (p.ct > 0 ? p.ct : 1)] != 0;
   }
   if (var) {
-    S[k * p.nf + k] += lambda_f[k];
+    S[k * p.lds + k] += lambda_f[k];
   } else {
-    S[k * p.nf + k] = 1.0;
+    S[k * p.lds + k] = 1.0;
   }
 }
 
@@ -1954,6 +2165,13 @@ void launch_fblock_dense(const DevProblem& p, const DevTile* tiles, int ntiles, 
   if (ntiles == 0) return;
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
+#ifdef MI_BA_AB_VARIANTS
+    if (p.fvariant == 1) {  // LDS-staged rows + MFMA: 1.30 vs 1.23 ms at C4 (profiles/r3_ab_fblock_fused_rhs.jsonl)
+      hipLaunchKernelGGL(fblock_mfma_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, q, b,
+                         udiag, S);
+      return;
+    }
+#endif
     hipLaunchKernelGGL(fblock_dense_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, q, b,
                        udiag, S);
   });
@@ -2048,6 +2266,18 @@ void launch_backsub(const DevProblem& p, const DevPoint* vp, int64_t npv, const 
     hipLaunchKernelGGL(backsub_kernel<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, J, Vg,
                        Vinv, df, dX);
   });
+}
+
+int64_t launch_backsub_chunks(const DevProblem& p, const uint32_t* chunk, int nchunks, const double* J,
+                              const double2* r, const double* Vg, const double* Vinv, const double* df, double* dX,
+                              double* partial, hipStream_t s) {
+  if (nchunks <= 0) return 0;
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    hipLaunchKernelGGL(backsub_chunk_kernel<CT>, dim3(grid_for(nchunks, kBlock / 64)), dim3(kBlock), 0, s, p, chunk,
+                       nchunks, J, r, Vg, Vinv, df, dX, partial);
+  });
+  return nchunks;
 }
 
 int64_t launch_backsub_cost(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* J, const double2* r,

@@ -75,9 +75,27 @@ double host_block_cost(const mi_ba_options& o, const mi_ba_problem* p, const Hos
   return 0.5 * rho[0];
 }
 
-__global__ void identity_kernel(double* __restrict__ S, int64_t n) {
+__global__ void identity_kernel(double* __restrict__ S, int64_t n, int64_t ld) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < n) S[k * n + k] = 1.0;
+  if (k < n) S[k * ld + k] = 1.0;
+}
+
+// Spare column-major row n of S <-> a vector: to_row 1 writes v into it (the
+// rhs the factorisation carries), 0 reads the forward solution back.
+__global__ void rhs_row_kernel(double* __restrict__ S, int64_t n, int64_t ld, double* __restrict__ v, int to_row) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  if (to_row)
+    S[j * ld + n] = v[j];
+  else
+    v[j] = S[j * ld + n];
+}
+
+// The forward solve rides in the factorisation (spare row) when the blocked
+// factor and the sync-free backward sweep are in use ("cholesky_fused_rhs").
+bool fused_rhs(const mi_ba_context* ctx) {
+  const CholConfig& c = ctx->chol;
+  return ctx->fused_rhs && c.panel > 0 && c.gemm_update && c.solve == 2 && ctx->dev.lds > ctx->dev.nf;
 }
 
 mi_ba_status read_scalars(mi_ba_context* ctx, int first, int count) {
@@ -394,6 +412,26 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
     }
     ctx->npv = (int64_t)vp.size();
     ctx->nb_const = nb - nb_var;
+    // point chunks of the back substitution: whole points, <= 64 blocks
+    // (a point with more blocks is a chunk of its own)
+    std::vector<uint32_t> ch;
+    {
+      int64_t c0 = 0, q = 0;
+      while (q < nb) {
+        int64_t e = q;
+        while (e < nb && pt[e] == pt[q]) ++e;
+        if (e - c0 > 64 && q > c0) {
+          ch.push_back((uint32_t)c0);
+          c0 = q;
+        }
+        q = e;
+      }
+      if (nb > 0) ch.push_back((uint32_t)c0);
+      ch.push_back((uint32_t)nb);
+    }
+    ctx->npchunks = (int)ch.size() - 1;
+    if (ctx->pchunks.alloc(ch.size())) return fail(MI_BA_ERR_OUT_OF_MEMORY);
+    if (hipMemcpy(ctx->pchunks.ptr, ch.data(), ch.size() * 4, hipMemcpyHostToDevice)) return fail(MI_BA_ERR_HIP);
     if (ctx->vpoints.alloc(vp.size())) return fail(MI_BA_ERR_OUT_OF_MEMORY);
     if (!vp.empty() && hipMemcpy(ctx->vpoints.ptr, vp.data(), vp.size() * sizeof(DevPoint), hipMemcpyHostToDevice))
       return fail(MI_BA_ERR_HIP);
@@ -441,6 +479,7 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
   {
     const int slots = gsba ? gsba_cylinder_slots(*o, p, gsba) : 0;
     d.nf = d.cyl0 + slots;
+    d.lds = d.nf;  // the exact path widens it below
     d.cyl_var = slots > 0;
   }
   d.loss_type = o->loss_function_type;
@@ -449,6 +488,7 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
   // image-block tile order, dispatch-order mapping: schur_build 4.9 -> 3.4 ms
   // at C4 (profiles/r3_ab_schur_order.jsonl)
   d.svariant = 4;
+  d.fvariant = 0;
   d.refine_mask = (o->refine_focal_length ? 1 : 0) | (o->refine_principal_point ? 2 : 0) |
                   (o->refine_extra_params ? 4 : 0);
   d.obs_xy = ctx->obs_xy.ptr;
@@ -464,7 +504,7 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
   d.X = ctx->X.ptr;
   d.img_rec = ctx->img_rec.ptr;
   // linearization + LM buffers
-  ctx->npartial = std::max<int64_t>(1, reproj_grid(nb));
+  ctx->npartial = std::max<int64_t>({1, reproj_grid(nb), (int64_t)ctx->npchunks});
   const int64_t nf = d.nf;
   const int ncs = s.ct * (s.ct + 1) / 2;
   if (ctx->r.alloc(nb) || ctx->J.alloc((size_t)nb * 2 * d.W) || ctx->Vg.alloc(9 * P) ||
@@ -505,7 +545,10 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
       ctx->dense = ncfg <= 1000 && fits;
     }
     if (ctx->dense) {
-      if (ctx->S.alloc((size_t)d.nf * d.nf) ||
+      // S's leading dimension: one spare column-major row (the rhs carried
+      // through the factorisation), rounded to 16 doubles (128-B columns)
+      d.lds = (d.nf + 1 + 15) / 16 * 16;
+      if (ctx->S.alloc((size_t)d.nf * d.lds) ||
           ctx->info.alloc(std::max<int64_t>(chol_leaf_count((int)d.nf), d.nf / 64 + 1)))
         return fail(MI_BA_ERR_OUT_OF_MEMORY);
       st = build_pair_tiles(ctx);
@@ -531,11 +574,14 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
           hipMemsetAsync(ctx->cg_x.ptr, 0, nf * 8, ctx->stream) != hipSuccess)
         return fail(MI_BA_ERR_HIP);
       hipLaunchKernelGGL(identity_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, ctx->stream, ctx->S.ptr,
-                         nf);
+                         nf, d.lds);
       unsigned werr = 0;
-      if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr, ctx->chol, &ctx->cholws) !=
+      const int ex = fused_rhs(ctx) ? 1 : 0;
+      if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)d.lds, ctx->info.ptr, ctx->chol, &ctx->cholws, ex) !=
               rocblas_status_success ||
-          chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr, ctx->chol.solve, &ctx->cholws) != rocblas_status_success ||
+          (ex ? chol_solve_backward(ctx->blas, (int)nf, ctx->S.ptr, (int)d.lds, ctx->cg_x.ptr, &ctx->cholws)
+              : chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)d.lds, ctx->cg_x.ptr, ctx->chol.solve,
+                           &ctx->cholws)) != rocblas_status_success ||
           chol_error(&ctx->cholws, ctx->stream, &werr) != hipSuccess || werr != 0)
         return fail(MI_BA_ERR_HIP);
     }
@@ -759,21 +805,29 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
     // nf^2 (0.60 vs 1.15 GB over xGMI at nf = 12 000), and no pack kernels.
     Phase ph_(ctx, "s_allreduce");
     constexpr int64_t kBand = 512;
+    const int64_t ld = d.lds;
     for (int64_t r0 = 0; r0 < nf; r0 += kBand) {
       const int64_t r1 = std::min<int64_t>(nf, r0 + kBand);
-      mi_ba_status st = allreduce(ctx, ctx->S.ptr + r0 * nf + r0, r1 * nf - (r0 * nf + r0));
+      mi_ba_status st = allreduce(ctx, ctx->S.ptr + r0 * ld + r0, r1 * ld - (r0 * ld + r0));
       if (st != MI_BA_OK) return st;
     }
   }
   timer_begin(ctx, "schur_build", &stop);
   launch_dense_finalize(d, ctx->lambda_f.ptr, ctx->S.ptr, s);
   timer_end(ctx, stop);
-  MI_HIP(hipMemcpyAsync(ctx->cg_x.ptr, ctx->bvec.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
+  // fused: the rhs rides in S's spare row and leaves it as the forward
+  // solution y = L^-1 b (one backward sweep left); else the two sweeps on b
+  const bool fused = fused_rhs(ctx);
+  const unsigned gn = (unsigned)((nf + 255) / 256);
+  if (fused)
+    hipLaunchKernelGGL(rhs_row_kernel, dim3(gn), dim3(256), 0, s, ctx->S.ptr, nf, d.lds, ctx->bvec.ptr, 1);
+  else
+    MI_HIP(hipMemcpyAsync(ctx->cg_x.ptr, ctx->bvec.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
   timer_begin(ctx, "cholesky", &stop);
   // S holds the upper triangle row-major == the lower triangle column-major.
   const int leaves = chol_leaf_count((int)nf, ctx->chol);
-  if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->info.ptr, ctx->chol, &ctx->cholws) !=
-      rocblas_status_success)
+  if (chol_factor(ctx->blas, (int)nf, ctx->S.ptr, (int)d.lds, ctx->info.ptr, ctx->chol, &ctx->cholws,
+                  fused ? 1 : 0) != rocblas_status_success)
     return MI_BA_ERR_HIP;
   timer_end(ctx, stop);
   std::vector<int32_t> info(leaves, 0);
@@ -792,8 +846,15 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
   }
   {
     Phase ph_(ctx, "cholesky_solve");
-    if (chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)nf, ctx->cg_x.ptr, ctx->chol.solve, &ctx->cholws) != rocblas_status_success)
+    if (fused) {
+      hipLaunchKernelGGL(rhs_row_kernel, dim3(gn), dim3(256), 0, s, ctx->S.ptr, nf, d.lds, ctx->cg_x.ptr, 0);
+      if (chol_solve_backward(ctx->blas, (int)nf, ctx->S.ptr, (int)d.lds, ctx->cg_x.ptr, &ctx->cholws) !=
+          rocblas_status_success)
+        return MI_BA_ERR_HIP;
+    } else if (chol_solve(ctx->blas, (int)nf, ctx->S.ptr, (int)d.lds, ctx->cg_x.ptr, ctx->chol.solve, &ctx->cholws) !=
+               rocblas_status_success) {
       return MI_BA_ERR_HIP;
+    }
   }
   MI_HIP(chol_error(&ctx->cholws, s, &werr));
   return agree_on_error(ctx, werr != 0);
@@ -962,8 +1023,8 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     int64_t nmodel = 0;
     {
       Phase ph_(ctx, "backsub");
-      nmodel = launch_backsub_cost(d, ctx->vpoints.ptr, ctx->npv, ctx->J.ptr, ctx->r.ptr, ctx->Vg.ptr,
-                                   ctx->Vinv.ptr, ctx->cg_x.ptr, ctx->dX.ptr, ctx->partial.ptr, ctx->nb_const > 0, s);
+      nmodel = launch_backsub_chunks(d, ctx->pchunks.ptr, ctx->npchunks, ctx->J.ptr, ctx->r.ptr, ctx->Vg.ptr,
+                                     ctx->Vinv.ptr, ctx->cg_x.ptr, ctx->dX.ptr, ctx->partial.ptr, s);
     }
     MI_HIP(hipMemsetAsync(sc + kModelCost, 0, 8, s));
     MI_HIP(hipMemsetAsync(sc + kSemModel, 0, 8, s));
@@ -1542,6 +1603,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->dev.svariant = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "fblock_variant") == 0 && (value == 0 || value == 1) && ab_value(value, 0)) {
+    ctx->dev.fvariant = value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "schur_block_images") == 0 && value >= 1) {
     ctx->schur_block = value;
     return ctx->ptiles_host.empty() ? MI_BA_OK : order_block_tiles(ctx);
@@ -1577,6 +1642,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   }
   if (std::strcmp(key, "cholesky_write_through") == 0 && (value == 0 || value == 1) && ab_value(value, 1)) {
     ctx->chol.write_through = value != 0;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_fused_rhs") == 0 && (value == 0 || value == 1)) {
+    ctx->fused_rhs = value != 0;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_spin_log2") == 0 && value >= 0 && value <= 30) {

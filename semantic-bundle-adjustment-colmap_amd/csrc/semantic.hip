@@ -1439,9 +1439,10 @@ __global__ void semantic_product_kernel(const SemPair* __restrict__ pairs, int n
   }
 }
 
-// Pair blocks into the explicit reduced camera system (upper triangle).
+// Pair blocks into the explicit reduced camera system (upper triangle,
+// row-major with leading dimension lds).
 __global__ void semantic_dense_kernel(const SemPair* __restrict__ pairs, int npairs,
-                                      const double* __restrict__ pair_blk, int64_t nf, double* __restrict__ S) {
+                                      const double* __restrict__ pair_blk, int64_t lds, double* __restrict__ S) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)npairs * 144) return;
   const int k = (int)(t / 144), e = (int)(t % 144);
@@ -1452,7 +1453,7 @@ __global__ void semantic_dense_kernel(const SemPair* __restrict__ pairs, int npa
   const double v = pair_blk[(size_t)k * kPairStride + (a <= b ? sym12(a, b) : sym12(b, a))];
   const int64_t ra = 6 * (int64_t)(a < 6 ? pr.i : pr.j) + a % 6;
   const int64_t rb = 6 * (int64_t)(b < 6 ? pr.i : pr.j) + b % 6;
-  if (ra <= rb) atomicAdd(S + ra * nf + rb, v);
+  if (ra <= rb) atomicAdd(S + ra * lds + rb, v);
 }
 
 __global__ void semantic_model_kernel(const SemPair* __restrict__ pairs, int npairs,
@@ -1770,7 +1771,7 @@ void semantic_add_dense(mi_ba_context* ctx, double* S) {
   if (!S_->npairs) return;
   const int64_t n = (int64_t)S_->npairs * 144;
   hipLaunchKernelGGL(semantic_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
-                     S_->pairs.ptr, S_->npairs, S_->pair_blk.ptr, ctx->dev.nf, S);
+                     S_->pairs.ptr, S_->npairs, S_->pair_blk.ptr, ctx->dev.lds, S);
 }
 
 void semantic_model_cost(mi_ba_context* ctx, const double* df, double* d_out) {

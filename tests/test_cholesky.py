@@ -293,3 +293,23 @@ def test_lm_schur_pair_orders(gpu):
     for a in res[1:]:
         assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
         assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
+
+
+@pytest.mark.parametrize("images", [40, 200])
+def test_lm_fused_forward_solve(gpu, images):
+    """The forward solve L y = b carried through the factorisation in S's
+    spare row (cholesky_fused_rhs 1, the default: one backward sweep left)
+    drives the same LM as the two separate sweeps (0), at one panel (nf = 313)
+    and several (nf = 1593)."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, images, 100 * images, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=7)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for fused in (1, 0):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            ctx.set_tuning("cholesky_fused_rhs", fused)
+            res.append(ctx.solve())
+    a, b = res
+    assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
+    assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
+    assert a.final_cost < a.initial_cost

@@ -1,6 +1,5 @@
 #!/bin/bash
 # GPU checkpoint: full GPU suite + default bench line, counter list, in-step vs back-to-back Jacobian PMC
-# image-block Schur default; counter list; in-step vs back-to-back Jacobian PMC
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
