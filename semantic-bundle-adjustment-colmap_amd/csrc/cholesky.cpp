@@ -853,7 +853,7 @@ template <int FV, bool WT>
 __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ A, int lda, int kb, int mrows,
                                                            int* __restrict__ info, double* __restrict__ linv,
                                                            unsigned* ctrl, unsigned base, unsigned epoch,
-                                                           unsigned* err, unsigned limit,
+                                                           unsigned* err, unsigned limit, int below_groups = 0,
                                                            unsigned long long* dbg = nullptr) {
   __shared__ double T[64 * kPfLd];   // staging / factor tile (row-major padded)
   __shared__ double Li[64 * kPfLd];  // a diagonal tile's inverse (own, or workgroup c's)
@@ -895,8 +895,17 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
       }
   }
   if (!diag_row) {
-    // below the diagonal block: one 64-row tile per workgroup, left-looking
-    // over the panel's column tiles (L_ck staged with L_rk per update)
+    // below the diagonal block: left-looking over the panel's column tiles
+    // (L_ck staged with L_rk per update), one 64-row tile at a time.  With
+    // below_groups = G > 0 the launch has G below-diagonal workgroups, each
+    // taking row tiles r, r + G, ...: its first tile follows the diagonal
+    // chain, the later ones find every flag set.  Fewer resident workgroups
+    // leave the CUs to the concurrent trailing dgemm while the panel has
+    // slack (the look-ahead's dgemm-bound head).
+    const int nbelow = (mrows - kb + 63) / 64;
+    const int G = below_groups > 0 ? below_groups : nbelow;
+    for (int rr = r; rr < nc + nbelow; rr += G) {
+    const int r0 = pf_row0(rr, kb, nc), hr = pf_rows(rr, kb, nc, mrows);
     for (int c = 0; c < nc; ++c) {
       const int c0 = 64 * c, wc = min(64, kb - c0);
       pf_dvec4 acc[4];
@@ -944,6 +953,7 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
       }
       stamp(2 + 2 * c);
       __syncthreads();  // T and Li are restaged next step
+    }
     }
     return;
   }
@@ -1192,7 +1202,13 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   const int mrows = n - k + ex;  // the extra rows below the matrix take the panel solve too
   const int nc = (kb + 63) / 64;
   const int nbelow = (mrows - kb + 63) / 64;
-  const int nr = nc + nbelow;  // workgroups (tickets) of the launch: one per row tile
+  // below-diagonal workgroups: one per row tile, or (while the trailing
+  // update is long: rows below >= group_min_rows) one per rows_per_group
+  // row tiles
+  int groups = 0;
+  if (ws->rows_per_group > 1 && mrows - kb >= ws->group_min_rows && nbelow > 0)
+    groups = (nbelow + ws->rows_per_group - 1) / ws->rows_per_group;
+  const int nr = nc + (groups > 0 ? groups : nbelow);  // workgroups (tickets) of the launch
   if (ws->pf_base > 0x7fffffffu || ws->pf_epoch > 0xfffffff0u) {
     if (hipMemsetAsync(ws->pf_ctrl, 0, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles), s) != hipSuccess)
       return rocblas_status_internal_error;
@@ -1207,7 +1223,7 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   auto kern = panel_factor_kernel<2, true>;  // the tools build keeps tile_factor 1 / plain stores for A/B
 #endif
   hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, s, A + k + (size_t)k * lda, lda, kb, mrows, info, ws->pf_linv,
-                     ws->pf_ctrl, ws->pf_base, epoch, ws->err, ws->spin_limit, nullptr);
+                     ws->pf_ctrl, ws->pf_base, epoch, ws->err, ws->spin_limit, groups, nullptr);
   ws->pf_base += (unsigned)nr;
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
@@ -1453,6 +1469,8 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
     ws->tile_factor = c.tile_factor;
     ws->write_through = c.write_through;
     ws->spin_limit = c.spin_log2 <= 0 ? 0u : (1u << std::min(c.spin_log2, 30));
+    ws->rows_per_group = c.panel_rows_per_group;
+    ws->group_min_rows = c.panel_group_min_rows;
   }
   double* scratch = ws ? ws->scratch : nullptr;
   if (c.panel > 0 && c.gemm_update && c.lookahead && ws && ws->side)

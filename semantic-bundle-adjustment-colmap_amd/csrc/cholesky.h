@@ -73,6 +73,12 @@ struct CholConfig {
   // A wait that runs out records kCholErrWait in the workspace's error word
   // (chol_error) instead of returning a silently wrong factor or solution.
   int spin_log2 = 24;
+  // own_diag 6: below-diagonal row tiles per panel workgroup while the rows
+  // below the panel number at least panel_group_min_rows (1: one workgroup per
+  // row tile throughout).  The resident panel workgroups cost the concurrent
+  // trailing dgemm CU time; in the dgemm-bound head the panel has slack.
+  int panel_rows_per_group = 1;
+  int panel_group_min_rows = 6000;
 };
 
 // Error word bits (CholWorkspace::err, read by chol_error).
@@ -106,6 +112,8 @@ struct CholWorkspace {
   int tbuf_rows = 0;
   unsigned* err = nullptr;      // [4] error word (kCholErr* bits) of the in-launch flag waits
   unsigned spin_limit = 1u << 24;  // polls per flag wait (CholConfig::spin_log2)
+  int rows_per_group = 1;          // CholConfig::panel_rows_per_group
+  int group_min_rows = 6000;       // CholConfig::panel_group_min_rows
 
   // Creates the resources on `device` with events for up to `max_panels`
   // panels and diagonal-block inverses for matrices up to max_n; false on any

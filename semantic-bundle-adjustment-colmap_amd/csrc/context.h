@@ -86,6 +86,7 @@ struct mi_ba_context {
   int64_t nb_const = 0;  // reduced blocks of constant points
   miba::DevArray<uint32_t> pchunks;  // [npchunks + 1] point-chunk boundaries (backsub_chunk_kernel)
   int npchunks = 0;
+  miba::DevArray<double> sum_ws;      // [kSumScratch] stage + ticket of launch_sum's many-workgroup pass
   bool lin_overlap = false;            // semantic kernel on lin_side beside the reprojection kernel
   int lin_order = 0;                   // 0 reprojection kernel first, 1 semantic pass first
   hipStream_t lin_side = nullptr;
@@ -116,7 +117,8 @@ struct mi_ba_context {
   miba::DevArray<miba::DevPairTile> ptiles;
   miba::DevArray<miba::DevPairTile> ptiles_blk;  // the same tiles in image-block order (schur_pairs_variant 4, default)
   std::vector<miba::DevPairTile> ptiles_host;    // first-image order, kept to re-order on "schur_block_images"
-  int schur_block = 32;                           // images per block edge of ptiles_blk
+  int schur_block = 8;                            // images per block edge of ptiles_blk (8: schur_build 3.26 ms
+                                                  // vs 3.32 / 3.42 / 3.64 at 16 / 32 / 64, profiles/r3_ab_schur_block.jsonl)
   miba::DevArray<uint2> pairs;             // (a, b) block pairs bucketed by image pair
   int nptiles = 0;
   miba::DevArray<int32_t> info;

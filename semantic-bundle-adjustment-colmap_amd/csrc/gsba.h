@@ -42,6 +42,9 @@ struct GsbaState {
   DevArray<GsbaEval> evals;          // linearization: every evaluation
   DevArray<GsbaEval> centres;        // cost: one per block
   DevArray<uint8_t> masks;           // [slot][H][W]
+  DevArray<uint64_t> mask_bits;      // [slot][H][words] bit-packed masks (span kernel)
+  int words = 0;                     // 64-bit words per mask row
+  int iou_variant = 0;               // 0 row spans over mask_bits, 1 per-pixel predicate (tools build)
   DevArray<int64_t> sem_total;       // [slot]
   DevArray<double> cyl, cyl_c;       // [ncyl][9] q(4) t(3) radius height (by 2 points: t1(3) t2(3) radius 0 0):
                                      // current, candidate

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 
 #include "ba_math.h"
 #include "kernels.h"
@@ -249,9 +250,10 @@ struct GsbaArgs {
   const double* cam;       // [C][8]
   const uint32_t* img_cam;
   const double* cyl;       // [ncyl][9]
-  const uint8_t* masks;    // [slot][H][W]
+  const uint8_t* masks;    // [slot][H][W] (per-pixel kernel, tools build)
+  const uint64_t* mask_bits;  // [slot][H][words]: bit x % 64 of word x / 64 = mask pixel (y, x) != 0
   const int64_t* sem_total;
-  int H, W;
+  int H, W, words;
   double rel_step;
   int by2;                 // MI_BA_CYLINDER_BY_2_POINTS: cyl rows are t1(3) t2(3) r, 0, 0
 };
@@ -272,12 +274,18 @@ __device__ inline double step_of(double xj, double rel) {
   return fmax(sqrt(DBL_EPSILON), fabs(xj) * rel);
 }
 
-// One IoU evaluation per workgroup.
-__global__ __launch_bounds__(kTB) void gsba_iou_kernel(GsbaArgs a, const GsbaEval* __restrict__ evals,
-                                                       double* __restrict__ iou_out) {
-  __shared__ int64_t red[2][kTB / 64];
-  const GsbaEval ev = evals[blockIdx.x];
-  const GsbaBlock b = a.blocks[ev.block];
+// The projected quadrilateral of one IoU evaluation (the evaluation's
+// parameter perturbed): drawQuadrilateral's bounding box, the four edges'
+// boxes and directions, and the four corner rectangles it clears.
+struct QuadGeom {
+  bool ok;
+  double p[4][2];
+  double dy[4], dx[4];
+  Box box, eb[4], rb[4];
+};
+
+__device__ inline QuadGeom quad_geom(const GsbaArgs& a, const GsbaEval& ev, const GsbaBlock& b) {
+  QuadGeom g;
   double x[16];
   load_params(a, b, x);
   if (ev.param >= 0) {
@@ -293,77 +301,58 @@ __global__ __launch_bounds__(kTB) void gsba_iou_kernel(GsbaArgs a, const GsbaEva
 #pragma unroll
     for (int m = 0; m < 9; ++m) x[7 + m] = cyl[m];
   }
-  double p[4][2];
-  const bool ok = project_quad(x, K, p);
+  g.ok = project_quad(x, K, g.p);
+  g.box = Box{0, 0, 0, 0};
+  if (!g.ok) return g;
   const int H = a.H, W = a.W;
-  int64_t tp = 0, fp = 0;
-  if (ok) {
-    // drawQuadrilateral as a predicate over the shrunk bounding box
-    double min_x = p[0][0], min_y = p[0][1], max_x = p[0][0], max_y = p[0][1];
+  const double(&p)[4][2] = g.p;
+  // drawQuadrilateral as a predicate over the shrunk bounding box
+  double min_x = p[0][0], min_y = p[0][1], max_x = p[0][0], max_y = p[0][1];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      min_x = fmin(min_x, p[k][0]);
-      max_x = fmax(max_x, p[k][0]);
-      min_y = fmin(min_y, p[k][1]);
-      max_y = fmax(max_y, p[k][1]);
-    }
-    Box box;
-    box.x = cast_to_int_x86(floor(min_x));
-    box.y = cast_to_int_x86(floor(min_y));
-    box.w = cast_to_int_x86(ceil(max_x)) - box.x + 1;
-    box.h = cast_to_int_x86(ceil(max_y)) - box.y + 1;
-    box = shrink(box, W, H);
-    Box eb[4];
-    double dy[4], dx[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int n = (e + 1) & 3;
-      eb[e] = shrink(bound2(p[e][0], p[e][1], p[n][0], p[n][1]), W, H);
-      dy[e] = p[n][1] - p[e][1];
-      dx[e] = p[n][0] - p[e][0];
-    }
-    Box rb[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      rb[k] = Box{0, 0, 0, 0};
-      const double qx = p[k][0], qy = p[k][1];
-      if (qx - box.x < 1 || box.x_end() - qx < 1 || qy - box.y < 1 || box.y_end() - qy < 1) continue;
-      const int cx[4] = {box.x, box.x_end(), box.x_end(), box.x};
-      const int cy[4] = {box.y, box.y, box.y_end(), box.y_end()};
-      int best = 0;
-      double bd = 0.0;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const double ddx = qx - (double)cx[m], ddy = qy - (double)cy[m];
-        const double d = sqrt(ddx * ddx + ddy * ddy);
-        if (m == 0 || d < bd) { best = m; bd = d; }
-      }
-      rb[k] = shrink(bound2((double)cx[best], (double)cy[best], qx, qy), W, H);
-    }
-    const uint8_t* sem = a.masks + (size_t)b.slot * H * W;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int y = box.y + wave; y <= box.y_end(); y += kTB / 64) {
-      const uint8_t* srow = sem + (size_t)y * W;
-      for (int xx = box.x + lane; xx <= box.x_end(); xx += 64) {
-        bool m = true;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (xx >= eb[e].x && xx <= eb[e].x_end() && y >= eb[e].y && y <= eb[e].y_end()) {
-            const double cross = ((double)xx - p[e][0]) * dy[e] - ((double)y - p[e][1]) * dx[e];
-            if (cross > 0) m = false;
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (xx >= rb[k].x && xx <= rb[k].x_end() && y >= rb[k].y && y <= rb[k].y_end()) m = false;
-        if (m) {
-          if (srow[xx]) ++tp;
-          else ++fp;
-        }
-      }
-    }
+  for (int k = 0; k < 4; ++k) {
+    min_x = fmin(min_x, p[k][0]);
+    max_x = fmax(max_x, p[k][0]);
+    min_y = fmin(min_y, p[k][1]);
+    max_y = fmax(max_y, p[k][1]);
   }
-  // workgroup sums
+  Box box;
+  box.x = cast_to_int_x86(floor(min_x));
+  box.y = cast_to_int_x86(floor(min_y));
+  box.w = cast_to_int_x86(ceil(max_x)) - box.x + 1;
+  box.h = cast_to_int_x86(ceil(max_y)) - box.y + 1;
+  box = shrink(box, W, H);
+  g.box = box;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int n = (e + 1) & 3;
+    g.eb[e] = shrink(bound2(p[e][0], p[e][1], p[n][0], p[n][1]), W, H);
+    g.dy[e] = p[n][1] - p[e][1];
+    g.dx[e] = p[n][0] - p[e][0];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    g.rb[k] = Box{0, 0, 0, 0};
+    const double qx = p[k][0], qy = p[k][1];
+    if (qx - box.x < 1 || box.x_end() - qx < 1 || qy - box.y < 1 || box.y_end() - qy < 1) continue;
+    const int cx[4] = {box.x, box.x_end(), box.x_end(), box.x};
+    const int cy[4] = {box.y, box.y, box.y_end(), box.y_end()};
+    int best = 0;
+    double bd = 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const double ddx = qx - (double)cx[m], ddy = qy - (double)cy[m];
+      const double d = sqrt(ddx * ddx + ddy * ddy);
+      if (m == 0 || d < bd) { best = m; bd = d; }
+    }
+    g.rb[k] = shrink(bound2((double)cx[best], (double)cy[best], qx, qy), W, H);
+  }
+  return g;
+}
+
+// IoU = TP / (TP + FP + FN) from the workgroup's per-thread counts (thread 0
+// writes it; FN = the mask's pixel total - TP).
+__device__ inline void iou_reduce(int64_t tp, int64_t fp, bool ok, int64_t total, double* out) {
+  __shared__ int64_t red[2][kTB / 64];
   for (int off = 32; off > 0; off >>= 1) {
     tp += __shfl_xor(tp, off, 64);
     fp += __shfl_xor(fp, off, 64);
@@ -382,14 +371,139 @@ __global__ __launch_bounds__(kTB) void gsba_iou_kernel(GsbaArgs a, const GsbaEva
         T += red[0][w];
         F += red[1][w];
       }
-      const int64_t fn = a.sem_total[b.slot] - T;
+      const int64_t fn = total - T;
       double den = (double)T * 1.;
       den = den + (double)F;
       den = den + (double)fn;
       iou = (double)T / den;
     }
-    iou_out[blockIdx.x] = iou;
+    *out = iou;
   }
+}
+
+#ifdef MI_BA_AB_VARIANTS
+// One IoU evaluation per workgroup, a per-pixel predicate (tools build,
+// gsba_variant 1; the round-2 kernel): waves take rows of the box, lanes
+// consecutive pixels of the byte mask.
+__global__ __launch_bounds__(kTB) void gsba_iou_kernel(GsbaArgs a, const GsbaEval* __restrict__ evals,
+                                                       double* __restrict__ iou_out) {
+  const GsbaEval ev = evals[blockIdx.x];
+  const GsbaBlock b = a.blocks[ev.block];
+  const QuadGeom g = quad_geom(a, ev, b);
+  const int H = a.H, W = a.W;
+  int64_t tp = 0, fp = 0;
+  if (g.ok) {
+    const Box box = g.box;
+    const uint8_t* sem = a.masks + (size_t)b.slot * H * W;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int y = box.y + wave; y <= box.y_end(); y += kTB / 64) {
+      const uint8_t* srow = sem + (size_t)y * W;
+      for (int xx = box.x + lane; xx <= box.x_end(); xx += 64) {
+        bool m = true;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (xx >= g.eb[e].x && xx <= g.eb[e].x_end() && y >= g.eb[e].y && y <= g.eb[e].y_end()) {
+            const double cross = ((double)xx - g.p[e][0]) * g.dy[e] - ((double)y - g.p[e][1]) * g.dx[e];
+            if (cross > 0) m = false;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (xx >= g.rb[k].x && xx <= g.rb[k].x_end() && y >= g.rb[k].y && y <= g.rb[k].y_end()) m = false;
+        if (m) {
+          if (srow[xx]) ++tp;
+          else ++fp;
+        }
+      }
+    }
+  }
+  iou_reduce(tp, fp, g.ok, a.sem_total[b.slot], iou_out + blockIdx.x);
+}
+#endif
+
+// Bits lo..hi (0 <= lo, hi <= 63) of a word; 0 when lo > hi.
+__device__ inline uint64_t bit_range(int lo, int hi) {
+  lo = max(lo, 0);
+  hi = min(hi, 63);
+  if (lo > hi) return 0ull;
+  return (~0ull >> (63 - hi)) & (~0ull << lo);
+}
+
+// One IoU evaluation per workgroup by row spans over the bit-packed mask (the
+// default).  In row y the pixels drawQuadrilateral clears are <= 8 intervals:
+// per edge e, the pixels of its box with cross_e > 0, and the corner
+// rectangles.  The computed cross_e(x) = fl(fl(fl(x - p_e.x) dy_e) -
+// fl(fl(y - p_e.y) dx_e)) is monotone in x (every rounding step is monotone;
+// the sign of dy_e gives the direction), so {x : cross_e(x) > 0} is a half-line
+// and a binary search with the per-pixel predicate itself finds its end: the
+// spans are exactly the per-pixel kernel's pixels.  TP / FP are popcounts of
+// the kept bits of each 64-pixel word against the mask bits.  One thread per
+// row; per row about 4 x 11 predicate evaluations + 2 popcounts per word,
+// where the per-pixel kernel evaluated up to 4 predicates per pixel.
+__global__ __launch_bounds__(kTB) void gsba_iou_span_kernel(GsbaArgs a, const GsbaEval* __restrict__ evals,
+                                                            double* __restrict__ iou_out) {
+  const GsbaEval ev = evals[blockIdx.x];
+  const GsbaBlock b = a.blocks[ev.block];
+  const QuadGeom g = quad_geom(a, ev, b);
+  int64_t tp = 0, fp = 0;
+  if (g.ok && g.box.w > 0) {
+    const Box box = g.box;
+    const uint64_t* bits = a.mask_bits + (size_t)b.slot * a.H * a.words;
+    for (int y = box.y + (int)threadIdx.x; y <= box.y_end(); y += kTB) {
+      int lo[8], hi[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        lo[e] = 1;
+        hi[e] = 0;
+        const Box& eb = g.eb[e];
+        if (eb.w <= 0 || y < eb.y || y > eb.y_end()) continue;
+        const int l = max(eb.x, box.x), h = min(eb.x_end(), box.x_end());
+        if (l > h) continue;
+        const double px = g.p[e][0], dy = g.dy[e];
+        const double cy = ((double)y - g.p[e][1]) * g.dx[e];
+        auto clear = [&](int xx) { return ((double)xx - px) * dy - cy > 0; };
+        if (dy > 0) {  // cleared: [first x with cross > 0, h]
+          int u = l, v = h + 1;
+          while (u < v) {
+            const int mid = (u + v) >> 1;
+            if (clear(mid)) v = mid; else u = mid + 1;
+          }
+          lo[e] = u;
+          hi[e] = h;
+        } else if (dy < 0) {  // cleared: [l, last x with cross > 0]
+          int u = l - 1, v = h;
+          while (u < v) {
+            const int mid = (u + v + 1) >> 1;
+            if (clear(mid)) u = mid; else v = mid - 1;
+          }
+          lo[e] = l;
+          hi[e] = u;
+        } else if (clear(l)) {  // constant in x
+          lo[e] = l;
+          hi[e] = h;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const Box& rb = g.rb[k];
+        const bool in = rb.w > 0 && y >= rb.y && y <= rb.y_end();
+        lo[4 + k] = in ? rb.x : 1;
+        hi[4 + k] = in ? rb.x_end() : 0;
+      }
+      const uint64_t* row = bits + (size_t)y * a.words;
+      for (int w = box.x >> 6; w <= (box.x_end() >> 6); ++w) {
+        const int w0 = 64 * w;
+        uint64_t keep = bit_range(box.x - w0, box.x_end() - w0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (lo[i] <= hi[i]) keep &= ~bit_range(lo[i] - w0, hi[i] - w0);
+        const uint64_t mb = row[w];
+        tp += __popcll(keep & mb);
+        fp += __popcll(keep & ~mb);
+      }
+    }
+  }
+  iou_reduce(tp, fp, g.ok, a.sem_total[b.slot], iou_out + blockIdx.x);
 }
 
 // Ceres 2.1 QuaternionManifold::PlusJacobian (4 x 3 row-major)
@@ -617,6 +731,8 @@ GsbaArgs make_args(mi_ba_context* ctx, const double* qt, const double* cyl) {
   a.img_cam = ctx->dev.img_cam;
   a.cyl = cyl;
   a.masks = G->masks.ptr;
+  a.mask_bits = G->mask_bits.ptr;
+  a.words = G->words;
   a.sem_total = G->sem_total.ptr;
   a.H = G->H;
   a.W = G->W;
@@ -751,6 +867,26 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
     if (hipMemcpy(G->masks.ptr + k * plane, g->trunk_mask + (size_t)slot_images[k] * plane, plane,
                   hipMemcpyHostToDevice))
       return MI_BA_ERR_HIP;
+#ifdef MI_BA_AB_VARIANTS
+  // tools build: MI_BA_GSBA_VARIANT=1 selects the per-pixel kernel (the GSBA
+  // entry points create their contexts internally, out of mi_ba_set_tuning's reach)
+  if (const char* v = std::getenv("MI_BA_GSBA_VARIANT")) G->iou_variant = std::atoi(v) == 1 ? 1 : 0;
+#endif
+  // bit-packed masks (row-major, whole 64-bit words per row) for the span kernel
+  G->words = (G->W + 63) / 64;
+  {
+    const size_t wplane = (size_t)G->H * G->words;
+    if (G->mask_bits.alloc(wplane * std::max<size_t>(1, slot_images.size()))) return MI_BA_ERR_OUT_OF_MEMORY;
+    std::vector<uint64_t> wb(wplane);
+    for (size_t k = 0; k < slot_images.size(); ++k) {
+      const uint8_t* m = g->trunk_mask + (size_t)slot_images[k] * plane;
+      std::fill(wb.begin(), wb.end(), 0ull);
+      for (int y = 0; y < G->H; ++y)
+        for (int x = 0; x < G->W; ++x)
+          if (m[(size_t)y * G->W + x]) wb[(size_t)y * G->words + (x >> 6)] |= 1ull << (x & 63);
+      if (hipMemcpy(G->mask_bits.ptr + k * wplane, wb.data(), wplane * 8, hipMemcpyHostToDevice)) return MI_BA_ERR_HIP;
+    }
+  }
   // refresh image flags (poses made variable by the GSBA term)
   std::vector<uint32_t> fl(I);
   for (int i = 0; i < I; ++i) fl[i] = (s.img_var[i] ? 1u : 0u) | ((uint32_t)s.img_tvec_mask[i] << 1);
@@ -765,6 +901,22 @@ void gsba_destroy(mi_ba_context* ctx) {
 }
 
 namespace {
+// The IoU evaluations: row spans over the bit-packed masks (default), or the
+// per-pixel predicate over the byte masks (tools build, gsba_variant 1).
+void launch_iou(mi_ba_context* ctx, const GsbaArgs& a, const GsbaEval* evals, int64_t n, double* out,
+                hipStream_t s) {
+  if (n <= 0) return;
+#ifdef MI_BA_AB_VARIANTS
+  if (ctx->gsba->iou_variant == 1) {
+    hipLaunchKernelGGL(gsba_iou_kernel, dim3((unsigned)n), dim3(kTB), 0, s, a, evals, out);
+    return;
+  }
+#else
+  (void)ctx;
+#endif
+  hipLaunchKernelGGL(gsba_iou_span_kernel, dim3((unsigned)n), dim3(kTB), 0, s, a, evals, out);
+}
+
 mi_ba_status eval_blocks(mi_ba_context* ctx, double* d_cost, double* J16, double* r_raw) {
   GsbaState* G = ctx->gsba;
   if (!G->nblocks) return MI_BA_OK;
@@ -772,7 +924,7 @@ mi_ba_status eval_blocks(mi_ba_context* ctx, double* d_cost, double* J16, double
   GsbaArgs a = make_args(ctx, ctx->dev.qt, G->cyl.ptr);
   hipEvent_t stop;
   timer_begin(ctx, "gsba_iou", &stop);
-  hipLaunchKernelGGL(gsba_iou_kernel, dim3((unsigned)G->nevals), dim3(kTB), 0, s, a, G->evals.ptr, G->iou.ptr);
+  launch_iou(ctx, a, G->evals.ptr, G->nevals, G->iou.ptr, s);
   timer_end(ctx, stop);
   hipLaunchKernelGGL(gsba_block_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, s, a, G->nblocks, ctx->dev.img_flags,
                      G->iou.ptr, G->weight, G->r.ptr, G->J.ptr, J16, r_raw, G->partial.ptr);
@@ -788,7 +940,7 @@ void gsba_cost(mi_ba_context* ctx, const double* qt, const double* cyl, double* 
   if (!G->nblocks) return;
   hipStream_t s = ctx->stream;
   GsbaArgs a = make_args(ctx, qt, cyl);
-  hipLaunchKernelGGL(gsba_iou_kernel, dim3((unsigned)G->nblocks), dim3(kTB), 0, s, a, G->centres.ptr, G->iou.ptr);
+  launch_iou(ctx, a, G->centres.ptr, G->nblocks, G->iou.ptr, s);
   hipLaunchKernelGGL(gsba_cost_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, s, G->blocks.ptr, G->nblocks,
                      G->iou.ptr, G->weight, G->partial.ptr);
   launch_sum(G->partial.ptr, G->nblocks, d_cost, s);

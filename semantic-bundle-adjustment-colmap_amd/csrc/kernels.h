@@ -25,7 +25,11 @@ void launch_reproj_cost(const DevProblem& p, const double* qt, const double* cam
                         double* cost_partial, hipStream_t s);
 
 // Sum n partials into out[0] (single workgroup).
-void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s);
+// out[0] = sum of partial[0..n) in a fixed order.  scratch (kSumScratch
+// doubles, last slot a zeroed ticket) enables the many-workgroup pass for long
+// lists; launches sharing a scratch must be stream-ordered.
+constexpr int kSumScratch = 65;
+void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s, double* scratch = nullptr);
 
 // Point side: Jacobi scale (first), LM diagonal (when !reuse_diag) and the
 // damped inverse Vinv[P][6] of V_p + Lambda_p.

@@ -514,7 +514,8 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
       ctx->lambda_f.alloc(nf) || ctx->prec_pose.alloc(36 * (size_t)I) ||
       ctx->prec_cam.alloc((size_t)s.ct * s.ct * C + 1) || ctx->cg_x.alloc(nf) || ctx->cg_r.alloc(nf) ||
       ctx->cg_z.alloc(nf) || ctx->cg_p.alloc(nf) || ctx->cg_q.alloc(nf) || ctx->cg_w.alloc(3 * P) ||
-      ctx->dX.alloc(3 * P) || ctx->scalars.alloc(kNumScalars) || ctx->red.alloc(kReduceBlocks))
+      ctx->dX.alloc(3 * P) || ctx->scalars.alloc(kNumScalars) || ctx->red.alloc(kReduceBlocks) ||
+      ctx->sum_ws.alloc(kSumScratch))
     return fail(MI_BA_ERR_OUT_OF_MEMORY);
   if (!ctx->host_scalars &&
       hipHostMalloc(&ctx->host_scalars, sizeof(double) * kNumScalars, hipHostMallocDefault) != hipSuccess) {
@@ -522,7 +523,8 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
     return fail(MI_BA_ERR_OUT_OF_MEMORY);
   }
   // stream-ordered (see build_pair_tiles)
-  if (hipMemsetAsync(ctx->scalars.ptr, 0, sizeof(double) * kNumScalars, ctx->stream) != hipSuccess)
+  if (hipMemsetAsync(ctx->scalars.ptr, 0, sizeof(double) * kNumScalars, ctx->stream) != hipSuccess ||
+      hipMemsetAsync(ctx->sum_ws.ptr, 0, sizeof(double) * kSumScratch, ctx->stream) != hipSuccess)
     return fail(MI_BA_ERR_HIP);
   if (P && (hipMemsetAsync(ctx->dX.ptr, 0, 3 * P * 8, ctx->stream) ||
             hipMemsetAsync(ctx->Vinv.ptr, 0, 6 * P * 8, ctx->stream) ||
@@ -665,7 +667,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   timer_begin(ctx, "reproj_jacobian", &stop);
   launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->partial.ptr, s);
   timer_end(ctx, stop);
-  if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s);
+  if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s, ctx->sum_ws.ptr);
   if (overlap) {
     MI_HIP(hipStreamWaitEvent(s, ctx->lin_ev[1], 0));
   } else if (ctx->sem && !sem_first) {
@@ -1029,7 +1031,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     MI_HIP(hipMemsetAsync(sc + kModelCost, 0, 8, s));
     MI_HIP(hipMemsetAsync(sc + kSemModel, 0, 8, s));
     MI_HIP(hipMemsetAsync(sc + kGsModel, 0, 8, s));
-    if (d.nb) launch_sum(ctx->partial.ptr, nmodel, sc + kModelCost, s);
+    if (d.nb) launch_sum(ctx->partial.ptr, nmodel, sc + kModelCost, s, ctx->sum_ws.ptr);
     if (ctx->sem) semantic_model_cost(ctx, ctx->cg_x.ptr, sc + kSemModel);
     if (ctx->gsba) gsba_model_cost(ctx, ctx->cg_x.ptr, sc + kGsModel);
     // camera step counted once (rank 0), point steps on their own ranks
@@ -1071,7 +1073,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       Phase ph_(ctx, "trial_cost");
       launch_reproj_cost(d, ctx->qt_c.ptr, ctx->cam_c.ptr, ctx->X_c.ptr, ctx->partial.ptr, s);
     }
-    if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kCandCost, s);
+    if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kCandCost, s, ctx->sum_ws.ptr);
     if (ctx->sem) semantic_cost(ctx, ctx->qt_c.ptr, ctx->cam_c.ptr, sc + kSemCand);
     if (ctx->gsba) gsba_cost(ctx, ctx->qt_c.ptr, ctx->gsba->cyl_c.ptr, sc + kGsCand);
     if (ctx->world > 1) {
@@ -1505,7 +1507,7 @@ mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost) {
   MI_HIP(hipMemsetAsync(sc + kCandCost, 0, 8, s));
   MI_HIP(hipMemsetAsync(sc + kSemCand, 0, 8, s));
   launch_reproj_cost(ctx->dev, ctx->qt.ptr, ctx->cam.ptr, ctx->X.ptr, ctx->partial.ptr, s);
-  if (ctx->dev.nb) launch_sum(ctx->partial.ptr, reproj_grid(ctx->dev.nb), sc + kCandCost, s);
+  if (ctx->dev.nb) launch_sum(ctx->partial.ptr, reproj_grid(ctx->dev.nb), sc + kCandCost, s, ctx->sum_ws.ptr);
   if (ctx->sem) semantic_cost(ctx, ctx->qt.ptr, ctx->cam.ptr, sc + kSemCand);
   MI_HIP(hipMemsetAsync(sc + kGsCand, 0, 8, s));
   if (ctx->gsba) gsba_cost(ctx, ctx->qt.ptr, ctx->gsba->cyl.ptr, sc + kGsCand);
@@ -1642,6 +1644,16 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   }
   if (std::strcmp(key, "cholesky_write_through") == 0 && (value == 0 || value == 1) && ab_value(value, 1)) {
     ctx->chol.write_through = value != 0;
+    return MI_BA_OK;
+  }
+  // grouped below-diagonal panel rows: measured slower (Cholesky 15.6 -> 15.7 / 16.9 ms
+  // with 2 rows per group, 18-22 ms with 4; profiles/r3_ab_panel_groups.jsonl)
+  if (std::strcmp(key, "cholesky_panel_rows_per_group") == 0 && value >= 1 && value <= 64 && ab_value(value, 1)) {
+    ctx->chol.panel_rows_per_group = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_panel_group_min_rows") == 0 && value >= 0) {
+    ctx->chol.panel_group_min_rows = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_fused_rhs") == 0 && (value == 0 || value == 1)) {

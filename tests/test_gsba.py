@@ -298,3 +298,35 @@ def test_by2_facade_option(gpu, tmp_path):
     assert (int(ns), int(nu)) == (s.num_successful_steps, s.num_unsuccessful_steps)
     bad = subprocess.run(args + ["by_3_points"], capture_output=True, text=True)
     assert bad.returncode == 3 and "not a valid cylinder parametrization" in bad.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("by2", [0, 1])
+def test_gsba_span_kernel_tilted_wide(gpu, by2):
+    """The IoU by row spans over bit-packed masks (gsba_iou_span_kernel: per
+    edge a binary search with the per-pixel predicate) on wide rows (1000
+    pixels: 16 mask words per row) with tilted cylinders (slanted edges, every
+    edge search live) and a shift that pushes quadrilaterals over the image
+    borders: residuals and Jacobians against the oracle's per-pixel scan."""
+    h, w = 360, 1000
+    sc, cyl = mi_ba.gsba_scene(8, 4, h, w, seed=11)
+    masks = oracle.gsba_render(sc, cyl, h, w)
+    rng = np.random.default_rng(12)
+    init = cyl.copy()
+    init[:, 4:6] += rng.uniform(-0.3, 0.3, (4, 2))
+    init[:, 7] *= rng.uniform(0.7, 1.4, 4)
+    for c in range(4):
+        a = rng.uniform(-0.5, 0.5, 2)
+        q = np.array([1.0, a[0] / 2, a[1] / 2, 0.0])
+        init[c, :4] = q / np.linalg.norm(q)
+    sc = sc.gauge()
+    g = mi_ba.GsbaInput(masks, init)
+    if by2:
+        g.cylinder_parametrization = BY2
+    o = mi_ba.default_options()
+    ids_o, r_o, J_o = oracle.gsba_evaluate(o, sc, g)
+    ids_g, r_g, J_g = mi_ba.gsba_evaluate(o, sc, g)
+    assert np.array_equal(ids_g, ids_o)
+    same = np.concatenate([(r_g == r_o)[:, None], J_g == J_o], axis=1)
+    assert same.mean() >= 0.999, int((~same).sum())
+    assert np.abs(J_o).sum() > 0 and (r_o != 0).any()

@@ -59,7 +59,7 @@ int main(int argc, char** argv) {
     auto kern = fv == 2 ? (wt ? panel_factor_kernel<2, true> : panel_factor_kernel<2, false>)
                         : (wt ? panel_factor_kernel<1, true> : panel_factor_kernel<1, false>);
     hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, ws.side, A, n, kb, n, info, ws.pf_linv, ws.pf_ctrl, ws.pf_base, epoch,
-                       ws.err, ws.spin_limit, dbg);
+                       ws.err, ws.spin_limit, 0, dbg);
     hipEventRecord(e1, ws.side);
     hipEventSynchronize(e1);
     if (busy) {
