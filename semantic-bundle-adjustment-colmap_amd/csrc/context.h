@@ -87,7 +87,8 @@ struct mi_ba_context {
   miba::DevArray<uint32_t> pchunks;  // [npchunks + 1] point-chunk boundaries (backsub_chunk_kernel)
   int npchunks = 0;
   miba::DevArray<double> sum_ws;      // [kSumScratch] stage + ticket of launch_sum's many-workgroup pass
-  bool lin_overlap = false;            // semantic kernel on lin_side beside the reprojection kernel
+  int lin_overlap = 0;                 // 1 semantic kernels on lin_side beside the reprojection kernel,
+                                       // 2 flat pass first, deferred pass on lin_side beside it
   int lin_order = 0;                   // 0 reprojection kernel first, 1 semantic pass first
   hipStream_t lin_side = nullptr;
   hipEvent_t lin_ev[2] = {nullptr, nullptr};

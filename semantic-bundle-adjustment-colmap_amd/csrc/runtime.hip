@@ -637,18 +637,26 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   hipEvent_t stop;
   // image records + the scalar slots zeroed in one launch
   launch_pack_images(d, ctx->img_rec.ptr, s, ctx->scalars.ptr, kNumScalars);
-  // linearize_overlap: the semantic kernel (FP64/latency-bound) on a second
-  // stream beside the reprojection kernel (HBM-write-bound); joined below
-  const bool overlap = ctx->sem && ctx->lin_overlap;
-  if (overlap) {
-    if (!ctx->lin_side) {
-      if (hipStreamCreateWithFlags(&ctx->lin_side, hipStreamNonBlocking) != hipSuccess) {
-        ctx->lin_side = nullptr;
-        return MI_BA_ERR_HIP;
-      }
-      MI_HIP(hipEventCreateWithFlags(&ctx->lin_ev[0], hipEventDisableTiming));
-      MI_HIP(hipEventCreateWithFlags(&ctx->lin_ev[1], hipEventDisableTiming));
+  // linearize_overlap: 1 the semantic kernels on a second stream beside the
+  // reprojection kernel; 2 the semantic flat pass first, then its
+  // deferred-sample pass (latency-bound) on the second stream beside the
+  // reprojection kernel (HBM-write-bound); joined below
+  const bool overlap = ctx->sem && ctx->lin_overlap == 1;
+  const bool split = ctx->sem && ctx->lin_overlap == 2;
+  if ((overlap || split) && !ctx->lin_side) {
+    if (hipStreamCreateWithFlags(&ctx->lin_side, hipStreamNonBlocking) != hipSuccess) {
+      ctx->lin_side = nullptr;
+      return MI_BA_ERR_HIP;
     }
+    MI_HIP(hipEventCreateWithFlags(&ctx->lin_ev[0], hipEventDisableTiming));
+    MI_HIP(hipEventCreateWithFlags(&ctx->lin_ev[1], hipEventDisableTiming));
+  }
+  if (split) {
+    mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false, ctx->lin_side, ctx->lin_ev[0]);
+    if (st != MI_BA_OK) return st;
+    MI_HIP(hipEventRecord(ctx->lin_ev[1], ctx->lin_side));
+  }
+  if (overlap) {
     MI_HIP(hipEventRecord(ctx->lin_ev[0], s));
     MI_HIP(hipStreamWaitEvent(ctx->lin_side, ctx->lin_ev[0], 0));
     ctx->stream = ctx->lin_side;  // semantic_linearize launches (and times) on ctx->stream
@@ -659,7 +667,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   }
   // lin_order: 0 reprojection then semantic, 1 semantic first (A/B of the
   // reprojection kernel's in-step time after the semantic gathers)
-  const bool sem_first = ctx->sem && !overlap && ctx->lin_order == 1;
+  const bool sem_first = ctx->sem && !overlap && !split && ctx->lin_order == 1;
   if (sem_first) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
@@ -668,7 +676,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->partial.ptr, s);
   timer_end(ctx, stop);
   if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s, ctx->sum_ws.ptr);
-  if (overlap) {
+  if (overlap || split) {
     MI_HIP(hipStreamWaitEvent(s, ctx->lin_ev[1], 0));
   } else if (ctx->sem && !sem_first) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
@@ -1588,8 +1596,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->lin_order = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "linearize_overlap") == 0 && (value == 0 || value == 1)) {
-    ctx->lin_overlap = value != 0;
+  // stream layouts 1 / 2 measured slower (step 1.04 / 1.06-1.07 vs 1.01-1.03 ms
+  // at C4, profiles/r3_ab_linearize_overlap.jsonl)
+  if (std::strcmp(key, "linearize_overlap") == 0 && value >= 0 && value <= 2 && ab_value(value, 0)) {
+    ctx->lin_overlap = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "semantic_diag") == 0 && (value == 0 || value == 1)) {

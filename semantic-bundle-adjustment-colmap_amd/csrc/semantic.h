@@ -67,7 +67,10 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem);
 void semantic_destroy(mi_ba_context* ctx);
 // Evaluate residuals + numeric-diff Jacobians of every sample; store r/J and
 // reduce into per-pair blocks; cost (0.5 * w * sum rho) into *d_cost.
-mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples);
+// deferred_stream (nullable): run the two-pass route's deferred-sample pass
+// there, ordered after the flat pass by flat_done; the caller joins it.
+mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples,
+                                hipStream_t deferred_stream = nullptr, hipEvent_t flat_done = nullptr);
 // Cost only, at parameters qt (candidate evaluation).
 void semantic_cost(mi_ba_context* ctx, const double* qt, const double* cam, double* d_cost);
 // Fold the pair blocks into the Schur-Jacobi pose blocks, b and diag(U).

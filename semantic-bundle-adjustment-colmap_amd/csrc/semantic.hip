@@ -1675,7 +1675,11 @@ void semantic_destroy(mi_ba_context* ctx) {
   ctx->sem = nullptr;
 }
 
-mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples) {
+// deferred_stream: when given (two-pass route), the deferred-sample pass is
+// launched there instead (after an event on ctx->stream marks the flat pass
+// done), and the caller joins it; the cost is complete on ctx->stream.
+mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples, hipStream_t deferred_stream,
+                                hipEvent_t flat_done) {
   SemanticState* S = ctx->sem;
   hipStream_t s = ctx->stream;
   S->samples_valid = write_samples;
@@ -1690,21 +1694,36 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 1) / 2), dim3(64), 0, s, S->pairs.ptr, S->npairs,
                      a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs, S->pair_blk.ptr, kPairStride,
                      ctx->sem_variant == 6 ? S->pair_cnt.ptr : nullptr);
+  const bool split = deferred_stream != nullptr && ctx->sem_variant == 6;
   if (ctx->sem_variant == 6) {
     const int ws = write_samples ? 1 | (ctx->sem_diag ? 2 : 0) : 0;
+    auto deferred = [&](hipStream_t ds) {
+      for (int model = 0; model < kNumModels; ++model) {
+        const int c0 = S->model_chunks[model], nc = S->model_chunks[model + 1] - c0;
+        if (S->model_tiles[model + 1] == S->model_tiles[model] || nc == 0) continue;
+        dispatch_model(model, [&](auto m) {
+          constexpr int M = decltype(m)::value;
+          hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4>), dim3(nc), dim3(64), 0, ds, a, S->chunks.ptr + c0,
+                             pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
+        });
+      }
+    };
     for (int model = 0; model < kNumModels; ++model) {
       const int t0 = S->model_tiles[model], nt = S->model_tiles[model + 1] - t0;
-      const int c0 = S->model_chunks[model], nc = S->model_chunks[model + 1] - c0;
       if (nt == 0) continue;
       dispatch_model(model, [&](auto m) {
         constexpr int M = decltype(m)::value;
         hipLaunchKernelGGL((semantic_flat_kernel<M, true>), dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0, pcs,
                            S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr,
                            ws);
-        if (nc > 0)
-          hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4>), dim3(nc), dim3(64), 0, s, a, S->chunks.ptr + c0,
-                             pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
       });
+    }
+    if (split) {
+      if (hipEventRecord(flat_done, s) != hipSuccess || hipStreamWaitEvent(deferred_stream, flat_done, 0) != hipSuccess)
+        return MI_BA_ERR_HIP;
+      deferred(deferred_stream);
+    } else {
+      deferred(s);
     }
   }
 #ifdef MI_BA_AB_VARIANTS

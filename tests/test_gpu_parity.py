@@ -299,6 +299,18 @@ def test_combined_geometric_semantic_solve(gpu):
     assert_solve_parity(opts, sc, sem, rel=1e-6)
 
 
+@pytest.mark.parametrize("loss", [mi_ba.LOSS_SOFT_L1, mi_ba.LOSS_CAUCHY])
+def test_semantic_solve_parity_robust_loss(gpu, loss):
+    """Robust losses on the semantic residuals (ScaledLoss + the loss's
+    Corrector in the pair blocks, semantic.hip) as well as the reprojection
+    residuals: the LM against the oracle's."""
+    sc, sem = semantic_scene(mi_ba.SIMPLE_RADIAL, images=4, size=120, step=6, seed=4)
+    sc.camera_constant = None
+    opts = mi_ba.default_options(max_num_iterations=20, semantic_weight=0.05, eta=1e-12,
+                                 loss_function_type=loss, loss_function_scale=1.0)
+    assert_solve_parity(opts, sc, sem, rel=1e-6)
+
+
 # ---------------------------------------------------------------------------
 # Full-size properties (BASELINE configs) — size-independent checks
 # ---------------------------------------------------------------------------
@@ -356,3 +368,28 @@ def test_own_diagonal_cholesky_matches_rocsolver(gpu, images):
     assert a.num_unsuccessful_steps == b.num_unsuccessful_steps
     assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost, (a.final_cost, b.final_cost)
     assert a.final_cost < a.initial_cost
+
+
+def test_linearize_overlap_modes_agree(gpu):
+    """The linearization step's stream layouts — all on one stream (0), the
+    semantic kernels beside the reprojection kernel (1), the flat pass first
+    and the deferred-sample pass beside the reprojection kernel (2) — give the
+    same cost and drive the same LM (pair blocks are atomic sums: order-only
+    differences)."""
+    if not mi_ba.ab_build():
+        pytest.skip("stream layouts 1 / 2 (measured slower): tools build only (MI_BA_LIB=ab)")
+    sc, sem = semantic_scene(mi_ba.SIMPLE_RADIAL, images=6, size=160, step=3, seed=9)
+    sc.camera_constant = None
+    opts = mi_ba.default_options(max_num_iterations=10, semantic_weight=0.01, eta=1e-12)
+    res = []
+    for ov in (0, 1, 2):
+        with mi_ba.Context(opts, sc.copy(), sem) as ctx:
+            ctx.set_tuning("linearize_overlap", ov)
+            ctx.linearize()
+            res.append(ctx.solve())
+    for s in res[1:]:
+        assert abs(s.initial_cost - res[0].initial_cost) <= 1e-12 * res[0].initial_cost
+        assert (s.num_successful_steps, s.num_unsuccessful_steps) == (res[0].num_successful_steps,
+                                                                      res[0].num_unsuccessful_steps)
+        assert abs(s.final_cost - res[0].final_cost) <= 1e-9 * res[0].final_cost
+    assert res[0].final_cost < res[0].initial_cost

@@ -1,5 +1,5 @@
 """A/B of the LM-phase timings at C4 over Cholesky tuning keys (own_diag, lookahead, panel, solve).
-    python tools/ab_cholesky.py"""
+    python tools/ab_cholesky.py [comma list of variant indices; 0 = production]"""
 import sys, time, json
 import os as _os
 _os.environ.setdefault("MI_BA_LIB", "ab")  # A/B variants: the tools-only build (make ab)
@@ -11,7 +11,9 @@ sc = mi_ba.generate_scene(c).gauge()
 w = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.OPENCV, 30, 300, track_length=5, rotation_range=0.05, extra=(-0.1, 0.01, 1e-4, -1e-4))).gauge()
 with mi_ba.Context(mi_ba.default_options(max_num_iterations=2), w) as x: x.solve()
 import os
-variants = [dict(own=1, la=1, panel=512, solve=1), dict(own=2, la=1, panel=512, solve=1),
+# index 0: the production configuration (one-launch panel factor, sync-free sweeps)
+variants = [dict(own=6, la=1, panel=512, solve=2),
+            dict(own=1, la=1, panel=512, solve=1), dict(own=2, la=1, panel=512, solve=1),
             dict(own=2, la=1, panel=1024, solve=1), dict(own=3, la=1, panel=512, solve=1),
             dict(own=0, la=1, panel=512, solve=1), dict(own=4, la=1, panel=512, solve=1),
             dict(own=5, la=1, panel=512, solve=1),

@@ -20,7 +20,7 @@ sc, sem = bench.build_shard(cfg, 0, 1)
 ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
 nb, _, ns = ctx.dims()
 for rnd in range(2):
-    for ov in (0, 1):
+    for ov in (0, 2, 1):
         ctx.set_tuning("linearize_overlap", ov)
         for _ in range(3):
             ctx.linearize()
