@@ -80,6 +80,19 @@ __global__ void identity_kernel(double* __restrict__ S, int64_t n, int64_t ld) {
   if (k < n) S[k * ld + k] = 1.0;
 }
 
+// Row i of S (row-major view, leading dimension ld): zero columns
+// [i rounded down to 512, ld).
+__global__ __launch_bounds__(256) void zero_upper_kernel(double* __restrict__ S, int64_t n, int64_t ld) {
+  const int64_t i = blockIdx.x;
+  if (i >= n) return;
+  const int64_t c0 = i / 512 * 512;
+  double* row = S + i * ld;
+  typedef double zvec2 __attribute__((ext_vector_type(2)));
+  int64_t c = c0 + 2 * threadIdx.x;
+  for (; c + 1 < ld; c += 512) *reinterpret_cast<zvec2*>(row + c) = zvec2{0.0, 0.0};
+  if (c < ld) row[c] = 0.0;
+}
+
 // Spare column-major row n of S <-> a vector: to_row 1 writes v into it (the
 // rhs the factorisation carries), 0 reads the forward solution back.
 __global__ void rhs_row_kernel(double* __restrict__ S, int64_t n, int64_t ld, double* __restrict__ v, int to_row) {
@@ -977,7 +990,11 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     MI_HIP(hipMemsetAsync(ctx->udiag.ptr, 0, ctx->udiag.bytes(), s));
     if (ctx->dense) {
       Phase ph_(ctx, "s_zero");
-      MI_HIP(hipMemsetAsync(ctx->S.ptr, 0, ctx->S.bytes(), s));
+      // the part of S the LM writes and the factorisation reads: row i of the
+      // row-major upper triangle from the start of its 512-row diagonal block
+      // (the trailing dgemms also rewrite the diagonal blocks' other half),
+      // through the spare column — about half of S
+      hipLaunchKernelGGL(zero_upper_kernel, dim3((unsigned)d.nf), dim3(256), 0, s, ctx->S.ptr, d.nf, d.lds);
     }
     {
       Phase ph_(ctx, "fblock");
