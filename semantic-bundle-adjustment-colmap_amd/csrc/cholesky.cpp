@@ -534,6 +534,128 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
   if (lane == 0) __hip_atomic_store(flag + ib, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifdef MI_BA_AB_VARIANTS
+// Tools build (cholesky_bwd_pairs 1): measured slower, 1.50 vs 0.83 ms at
+// nf = 12 000 — with two waves per block each wave streams twice the
+// dependency blocks, and the streaming, not the hand-off, then paces the
+// deep blocks (profiles/r3_ab_bwd_pairs_schur_xcd.jsonl).
+// Backward sweep L'x = y over PAIRS of 64-row blocks (hi, lo = hi - 1): one
+// flag hand-off per 128 rows instead of per 64.  Waves 0-1 fold the
+// dependencies jb > hi into block hi, waves 2-3 the same jb into block lo;
+// wave 0 solves hi, wave 3 folds the local block L[hi][lo]' x_hi, wave 2
+// solves lo; both blocks are published under one epoch.  Same arithmetic per
+// block as trsv_sweep_kernel<false> except the order in which the dependency
+// products are summed (a ragged top block pairs with nothing).
+__global__ __launch_bounds__(256) void trsv_bwd_pair_kernel(const double* __restrict__ L, int lda, int n, double* x,
+                                                            unsigned* ctrl, unsigned epoch, unsigned* err,
+                                                            unsigned limit) {
+  __shared__ int s_t;
+  __shared__ double part[4][kTB];
+  __shared__ double xs[4][kTB];
+  __shared__ double xhi[kTB];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nblk = (n + kTB - 1) / kTB;
+  if (threadIdx.x == 0) s_t = (int)atomicAdd(ctrl + 1, 1u);
+  __syncthreads();
+  const int hi = nblk - 1 - 2 * s_t, lo = hi - 1;
+  unsigned* flag = ctrl + 2;
+  const bool mine_hi = wv < 2;
+  const int rb = mine_hi ? hi : lo;  // the block whose column this wave reads
+  if (rb < 0) {                      // hi == 0: no lo block; its waves only join the barriers
+    __syncthreads();
+    __syncthreads();
+    __syncthreads();
+    __syncthreads();
+    return;
+  }
+  const int r0 = rb * kTB, w = min(kTB, n - r0);
+  const int me = r0 + min(lane, w - 1);  // the lane's column, clamped
+  double acc = 0.0;
+  const int ndep = nblk - 1 - hi;  // blocks jb > hi
+  for (int q = (wv & 1); q < ndep; q += 2) {
+    const int jb = nblk - 1 - q;
+    const int c0 = jb * kTB, wj = min(kTB, n - c0);
+    double v[kTB];
+    const double* src = L + c0 + (size_t)me * lda;
+    if (wj == kTB && ((c0 | lda) & 1) == 0) {
+      const sweep_dvec2* s2 = reinterpret_cast<const sweep_dvec2*>(src);
+#pragma unroll
+      for (int r = 0; r < kTB / 2; ++r) {
+        const sweep_dvec2 pv = __builtin_nontemporal_load(s2 + r);
+        v[2 * r] = pv.x;
+        v[2 * r + 1] = pv.y;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kTB; ++r) v[r] = src[min(r, wj - 1)];
+    }
+    flag_wait(flag + jb, epoch, err, limit);
+    xs[wv][lane] = lane < wj ? x[c0 + lane] : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+    for (int c = 0; c < kTB; ++c) acc += v[c] * xs[wv][c];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  part[wv][lane] = acc;
+  // wave 0: block hi's diagonal; wave 3: the local block L[hi][lo] (column
+  // me of lo, rows of hi: contiguous); wave 2: block lo's diagonal
+  double u[kTB];
+  double dinv = 0.0;
+  if (wv == 0 || wv == 2) {
+    const double* src = L + r0 + (size_t)me * lda;
+#pragma unroll
+    for (int r = 0; r < kTB; ++r) u[r] = src[min(r, w - 1)];
+    dinv = 1.0 / L[(size_t)me * (lda + 1)];
+  } else if (wv == 3) {
+    const int h0 = hi * kTB, wh = min(kTB, n - h0);
+    const double* src = L + h0 + (size_t)me * lda;
+#pragma unroll
+    for (int r = 0; r < kTB; ++r) u[r] = src[min(r, wh - 1)];
+  }
+  __syncthreads();  // (1) dependency parts
+  auto solve = [&](double z) {
+    if (lane >= w) z = 0.0;
+#pragma unroll
+    for (int r = kTB - 1; r >= 0; --r) {
+      const double xr = readlane_f64(z, r) * readlane_f64(dinv, r);
+      const double zu = z - u[r] * xr;
+      z = lane == r ? xr : (lane < r ? zu : z);
+    }
+    return z;
+  };
+  if (wv == 0) {
+    double z = lane < w ? x[r0 + lane] : 0.0;
+    z -= part[0][lane] + part[1][lane];
+    z = solve(z);
+    if (lane < w) x[r0 + lane] = z;
+    xhi[lane] = lane < w ? z : 0.0;
+    __threadfence();
+  }
+  __syncthreads();  // (2) x_hi
+  if (wv == 3) {
+    double a = 0.0;
+#pragma unroll
+    for (int c = 0; c < kTB; ++c) a += u[c] * xhi[c];
+    part[3][lane] += a;
+  }
+  __syncthreads();  // (3) local fold
+  if (wv == 2) {
+    double z = lane < w ? x[r0 + lane] : 0.0;
+    z -= part[2][lane] + part[3][lane];
+    z = solve(z);
+    if (lane < w) x[r0 + lane] = z;
+    __threadfence();
+  }
+  __syncthreads();  // (4) both blocks stored
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(flag + hi, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (lo >= 0) __hip_atomic_store(flag + lo, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // Panel factor in ONE launch (own_diag 6): the diagonal block's Cholesky AND
 // the panel's triangular solve below it (replaces potrf_diag's 16 launches
@@ -1470,6 +1592,7 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
     ws->write_through = c.write_through;
     ws->spin_limit = c.spin_log2 <= 0 ? 0u : (1u << std::min(c.spin_log2, 30));
     ws->rows_per_group = c.panel_rows_per_group;
+    ws->bwd_pairs = c.bwd_pairs;
     ws->group_min_rows = c.panel_group_min_rows;
   }
   double* scratch = ws ? ws->scratch : nullptr;
@@ -1503,8 +1626,14 @@ rocblas_status chol_solve_backward(rocblas_handle h, int n, const double* A, int
   if (hipMemsetAsync(ws->ctrl + 1, 0, sizeof(unsigned), s) != hipSuccess) return rocblas_status_internal_error;
   const unsigned e = ++ws->epoch;
   const int nblk = (n + kTB - 1) / kTB;
-  hipLaunchKernelGGL(trsv_sweep_kernel<false>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e,
-                     ws->err, ws->spin_limit);
+#ifdef MI_BA_AB_VARIANTS
+  if (ws->bwd_pairs)
+    hipLaunchKernelGGL(trsv_bwd_pair_kernel, dim3((nblk + 1) / 2), dim3(256), 0, s, A, lda, n, x, ws->ctrl, e, ws->err,
+                       ws->spin_limit);
+  else
+#endif
+    hipLaunchKernelGGL(trsv_sweep_kernel<false>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e,
+                       ws->err, ws->spin_limit);
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
 

@@ -78,6 +78,9 @@ struct CholConfig {
   // row tile throughout).  The resident panel workgroups cost the concurrent
   // trailing dgemm CU time; in the dgemm-bound head the panel has slack.
   int panel_rows_per_group = 1;
+  // chol_solve_backward over pairs of 64-row blocks (tools build: measured
+  // slower), or per block (trsv_sweep_kernel<false>, the default)
+  bool bwd_pairs = false;
   int panel_group_min_rows = 6000;
 };
 
@@ -113,6 +116,7 @@ struct CholWorkspace {
   unsigned* err = nullptr;      // [4] error word (kCholErr* bits) of the in-launch flag waits
   unsigned spin_limit = 1u << 24;  // polls per flag wait (CholConfig::spin_log2)
   int rows_per_group = 1;          // CholConfig::panel_rows_per_group
+  bool bwd_pairs = false;          // CholConfig::bwd_pairs
   int group_min_rows = 6000;       // CholConfig::panel_group_min_rows
 
   // Creates the resources on `device` with events for up to `max_panels`

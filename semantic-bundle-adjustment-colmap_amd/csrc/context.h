@@ -56,6 +56,7 @@ struct GsbaState;      // gsba.h
 struct KernelTimer {
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> pool;
+  std::vector<hipEvent_t> borrowed;  // start events shared with the previous pending entry (pooled once)
   std::map<std::string, std::pair<double, int64_t>> totals;
 };
 
@@ -118,6 +119,8 @@ struct mi_ba_context {
   miba::DevArray<miba::DevPairTile> ptiles;
   miba::DevArray<miba::DevPairTile> ptiles_blk;  // the same tiles in image-block order (schur_pairs_variant 4, default)
   std::vector<miba::DevPairTile> ptiles_host;    // first-image order, kept to re-order on "schur_block_images"
+  miba::DevArray<miba::DevPairTile> ptiles_xcd;  // XCD-interleaved order (schur_pairs_variant 5), empty-tile padded
+  int nptiles_xcd = 0;
   int schur_block = 8;                            // images per block edge of ptiles_blk (8: schur_build 3.26 ms
                                                   // vs 3.32 / 3.42 / 3.64 at 16 / 32 / 64, profiles/r3_ab_schur_block.jsonl)
   miba::DevArray<uint2> pairs;             // (a, b) block pairs bucketed by image pair
@@ -125,6 +128,10 @@ struct mi_ba_context {
   miba::DevArray<int32_t> info;
   miba::CholConfig chol;                   // factorisation variant (mi_ba_set_tuning)
   bool fused_rhs = true;                   // forward solve carried through the factorisation (S's spare row)
+  bool schur_overlap = false;              // one rank: Schur terms on lm_side beside the camera-block pass
+                                           // (measured slower: BA iteration 28.5 vs 27.1 ms at C4; tools build)
+  hipStream_t lm_side = nullptr;
+  hipEvent_t lm_ev[2] = {nullptr, nullptr};
   miba::CholWorkspace cholws;              // side stream / handle / events / scratch of this context
 
   double fixed_cost = 0.0;
@@ -158,4 +165,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum);
 mi_ba_status context_writeback(mi_ba_context* ctx);
 void timer_begin(mi_ba_context* ctx, const char* name, hipEvent_t* stop_out);
 void timer_end(mi_ba_context* ctx, hipEvent_t stop);
+// As timer_begin, starting at an already recorded event (the previous
+// measurement's stop): one event record fewer between back-to-back phases.
+void timer_begin_after(mi_ba_context* ctx, const char* name, hipEvent_t start, hipEvent_t* stop_out);
 }  // namespace miba

@@ -28,8 +28,12 @@ void launch_reproj_cost(const DevProblem& p, const double* qt, const double* cam
 // out[0] = sum of partial[0..n) in a fixed order.  scratch (kSumScratch
 // doubles, last slot a zeroed ticket) enables the many-workgroup pass for long
 // lists; launches sharing a scratch must be stream-ordered.
-constexpr int kSumScratch = 65;
+constexpr int kSumScratch = 65 + 17;  // launch_sum: [64] stage + ticket; launch_sum2 adds [16] + ticket
 void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s, double* scratch = nullptr);
+// Both sums in one launch, each by a many-workgroup pass (64 and 16
+// workgroups; scratch1: kSumScratch doubles, zeroed tickets).
+void launch_sum2(const double* p1, int64_t n1, double* out1, double* scratch1, const double* p2, int64_t n2,
+                 double* out2, hipStream_t s);
 
 // Point side: Jacobi scale (first), LM diagonal (when !reuse_diag) and the
 // damped inverse Vinv[P][6] of V_p + Lambda_p.

@@ -621,6 +621,61 @@ __global__ __launch_bounds__(256) void sum_multi_kernel(const double* __restrict
   }
 }
 
+// Two partial lists in one launch: workgroups 0..kSumGroups-1 sum list 1,
+// the next kSumGroups2 list 2, each set as sum_multi_kernel does (its own
+// stage slots and ticket in the scratch).  Deterministic.
+constexpr int kSumGroups2 = 16;
+__device__ inline void group_sum(const double* __restrict__ p, int64_t n, double* __restrict__ out,
+                                 double* __restrict__ stage, unsigned* __restrict__ ticket, int G, int g,
+                                 double* sred, bool* last) {
+  const int64_t per = (n + G - 1) / G;
+  const int64_t b0 = (int64_t)g * per, b1 = min(n, b0 + per);
+  double v = 0.0;
+  int64_t k = b0 + threadIdx.x;
+  for (; k + 3 * 256 < b1; k += 4 * 256) {
+    const double x0 = p[k], x1 = p[k + 256], x2 = p[k + 512], x3 = p[k + 768];
+    v += x0;
+    v += x1;
+    v += x2;
+    v += x3;
+  }
+  for (; k < b1; k += 256) v += p[k];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    stage[g] = ((sred[0] + sred[1]) + sred[2]) + sred[3];
+    __threadfence();
+    *last = atomicAdd(ticket, 1u) == (unsigned)G - 1;
+  }
+  __syncthreads();
+  if (!*last) return;
+  __threadfence();
+  double w = (int)threadIdx.x < G ? __hip_atomic_load(stage + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0.0;
+  w = wave_sum(w);
+  if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[0] = ((sred[0] + sred[1]) + sred[2]) + sred[3];
+    *ticket = 0u;
+  }
+}
+
+__global__ __launch_bounds__(256) void sum2_kernel(const double* __restrict__ p1, int64_t n1, double* __restrict__ out1,
+                                                   double* __restrict__ scratch, const double* __restrict__ p2,
+                                                   int64_t n2, double* __restrict__ out2) {
+  __shared__ double sred[4];
+  __shared__ bool last;
+  if (blockIdx.x < kSumGroups)
+    group_sum(p1, n1, out1, scratch, reinterpret_cast<unsigned*>(scratch + kSumGroups), kSumGroups, blockIdx.x, sred,
+              &last);
+  else
+    group_sum(p2, n2, out2, scratch + kSumGroups + 1,
+              reinterpret_cast<unsigned*>(scratch + kSumGroups + 1 + kSumGroups2), kSumGroups2,
+              blockIdx.x - kSumGroups, sred, &last);
+}
+
 // ---------------------------------------------------------------------------
 // Point side
 // ---------------------------------------------------------------------------
@@ -1823,7 +1878,9 @@ __global__ __launch_bounds__(kBlock) void schur_z_kernel(DevProblem p, const dou
 // contiguous range of tiles (tiles sorted by first image, so one image's Z
 // rows stay in that XCD's L2 while its pairs stream by).  Else dispatch order
 // (image-block-ordered tiles: every XCD sweeps the same image block at once).
-template <int CT, bool XMAP = true>
+// NTB: second-image (b-side) rows loaded nontemporal, so the streaming b-side
+// does not evict the first image's rows an XCD keeps in its L2 (variant 5).
+template <int CT, bool XMAP = true, bool NTB = false>
 __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const DevPairTile* __restrict__ tiles,
                                                               int ntiles, const uint2* __restrict__ pairs,
                                                               const double* __restrict__ Z, double* __restrict__ S) {
@@ -1836,6 +1893,7 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
   const int t = lb * 4 + wv;
   if (lb >= G || t >= ntiles) return;
   const DevPairTile tl = tiles[t];
+  if (tl.count == 0) return;  // padding tile (variant 5)
   const int lane = threadIdx.x & 63;
   const int m = lane & 15, k = lane >> 4;
   const bool on = m < F && k < 3;
@@ -1853,7 +1911,10 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       va[u] = on ? Z[(size_t)pr[u].x * ZN + off] : 0.0;
-      vb[u] = on ? Z[(size_t)pr[u].y * ZN + off] : 0.0;
+      if constexpr (NTB)
+        vb[u] = on ? __builtin_nontemporal_load(Z + (size_t)pr[u].y * ZN + off) : 0.0;
+      else
+        vb[u] = on ? Z[(size_t)pr[u].y * ZN + off] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va[u], vb[u], acc, 0, 0, 0);
@@ -1861,7 +1922,11 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
   for (; n < cnt; ++n) {
     const uint2 pr = pl[n];
     const double va = on ? Z[(size_t)pr.x * ZN + off] : 0.0;
-    const double vb = on ? Z[(size_t)pr.y * ZN + off] : 0.0;
+    double vb = 0.0;
+    if constexpr (NTB)
+      vb = on ? __builtin_nontemporal_load(Z + (size_t)pr.y * ZN + off) : 0.0;
+    else
+      vb = on ? Z[(size_t)pr.y * ZN + off] : 0.0;
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, acc, 0, 0, 0);
   }
   const uint32_t ia = tl.ia, ib = tl.ib;
@@ -2183,6 +2248,12 @@ void launch_reproj_cost(const DevProblem& p, const double* qt, const double* cam
   });
 }
 
+void launch_sum2(const double* p1, int64_t n1, double* out1, double* scratch1, const double* p2, int64_t n2,
+                 double* out2, hipStream_t s) {
+  hipLaunchKernelGGL(sum2_kernel, dim3(kSumGroups + kSumGroups2), dim3(256), 0, s, p1, n1, out1, scratch1, p2, n2,
+                     out2);
+}
+
 void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s, double* scratch) {
   if (scratch && n >= 32768) {
     hipLaunchKernelGGL(sum_multi_kernel, dim3(kSumGroups), dim3(256), 0, s, partial, n, out, scratch,
@@ -2385,6 +2456,12 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
                            pairs, Z, S);
       else if (p.svariant == 3)
         hipLaunchKernelGGL((schur_pairs_pipelined_kernel<CT, 16>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles,
+                           pairs, Z, S);
+      else
+#endif
+#ifdef MI_BA_AB_VARIANTS
+      if (p.svariant == 5)
+        hipLaunchKernelGGL((schur_pairs_kernel<CT, false, true>), dim3(G), dim3(kBlock), 0, s, p, ptiles, nptiles,
                            pairs, Z, S);
       else
 #endif

@@ -160,6 +160,25 @@ void timer_end(mi_ba_context* ctx, hipEvent_t stop) {
   (void)hipEventRecord(stop, ctx->stream);
 }
 
+void timer_begin_after(mi_ba_context* ctx, const char* name, hipEvent_t start, hipEvent_t* stop_out) {
+  if (!start) {
+    timer_begin(ctx, name, stop_out);
+    return;
+  }
+  *stop_out = nullptr;
+  if (!ctx->timing) return;
+  hipEvent_t b;
+  if (!ctx->timer.pool.empty()) {
+    b = ctx->timer.pool.back();
+    ctx->timer.pool.pop_back();
+  } else {
+    (void)hipEventCreate(&b);
+  }
+  ctx->timer.pending.push_back({name, {start, b}});
+  ctx->timer.borrowed.push_back(start);
+  *stop_out = b;
+}
+
 // Scoped phase timer (HIP events on the context stream; no-op unless timing).
 struct Phase {
   mi_ba_context* ctx;
@@ -177,10 +196,12 @@ static void timer_collect(mi_ba_context* ctx) {
     auto& t = ctx->timer.totals[e.first];
     t.first += ms;
     t.second += 1;
-    ctx->timer.pool.push_back(e.second.first);
+    if (std::find(ctx->timer.borrowed.begin(), ctx->timer.borrowed.end(), e.second.first) == ctx->timer.borrowed.end())
+      ctx->timer.pool.push_back(e.second.first);
     ctx->timer.pool.push_back(e.second.second);
   }
   ctx->timer.pending.clear();
+  ctx->timer.borrowed.clear();
 }
 
 // Pair list of the explicit Schur build: every unordered pair {a, b} of
@@ -193,6 +214,47 @@ static void timer_collect(mi_ba_context* ctx) {
 // (2.9 MB of Z per image at C4), where the first-image order scatters the
 // second image's rows over every image.
 mi_ba_status order_block_tiles(mi_ba_context* ctx) {
+#ifdef MI_BA_AB_VARIANTS
+  // XCD-interleaved order (schur_pairs_variant 5, tools build: measured
+  // slower, 3.39 vs 3.26 ms per schur_build call): rows of 8 first images;
+  // within a row, image Ia + x's tiles in second-image order go to XCD x
+  // (workgroup b runs on XCD b % 8, four tiles per workgroup), so each XCD
+  // keeps ONE first image's Z rows (2.9 MB at C4) in its 4 MB L2 for the whole
+  // sweep over second images, while the eight XCDs stream the same second
+  // images through the MALL.  Empty tiles pad the shorter lists.
+  {
+    const std::vector<DevPairTile>& tl = ctx->ptiles_host;
+    constexpr int kX = 8, kW = kBlock / 64;
+    uint32_t nimg = 0;
+    for (const DevPairTile& t : tl) nimg = std::max(nimg, t.ia + 1);
+    std::vector<std::vector<uint32_t>> per(nimg);
+    for (uint32_t k = 0; k < (uint32_t)tl.size(); ++k) per[tl[k].ia].push_back(k);
+    std::vector<DevPairTile> tx;
+    DevPairTile empty{};
+    for (uint32_t i0 = 0; i0 < nimg; i0 += kX) {
+      std::vector<std::vector<uint32_t>*> lists;
+      size_t longest = 0;
+      for (int x = 0; x < kX; ++x) {
+        std::vector<uint32_t>* l = i0 + x < nimg ? &per[i0 + x] : nullptr;
+        if (l) std::stable_sort(l->begin(), l->end(), [&](uint32_t a, uint32_t b) { return tl[a].ib < tl[b].ib; });
+        lists.push_back(l);
+        if (l) longest = std::max(longest, l->size());
+      }
+      for (size_t k = 0; k < longest; k += kW)
+        for (int x = 0; x < kX; ++x)
+          for (int w = 0; w < kW; ++w) {
+            const std::vector<uint32_t>* l = lists[x];
+            tx.push_back(l && k + w < l->size() ? tl[(*l)[k + w]] : empty);
+          }
+    }
+    if (ctx->ptiles_xcd.alloc(std::max<size_t>(1, tx.size()))) return MI_BA_ERR_OUT_OF_MEMORY;
+    ctx->nptiles_xcd = (int)tx.size();
+    if (!tx.empty() && (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+                        hipMemcpy(ctx->ptiles_xcd.ptr, tx.data(), tx.size() * sizeof(DevPairTile),
+                                  hipMemcpyHostToDevice) != hipSuccess))
+      return MI_BA_ERR_HIP;
+  }
+#endif
   std::vector<DevPairTile> tb(ctx->ptiles_host);
   const uint32_t B = (uint32_t)std::max(1, ctx->schur_block);
   std::stable_sort(tb.begin(), tb.end(), [B](const DevPairTile& x, const DevPairTile& y) {
@@ -636,6 +698,12 @@ void context_destroy(mi_ba_context* ctx) {
     (void)hipStreamSynchronize(ctx->lin_side);
     (void)hipStreamDestroy(ctx->lin_side);
   }
+  if (ctx->lm_side) {
+    (void)hipStreamSynchronize(ctx->lm_side);
+    (void)hipStreamDestroy(ctx->lm_side);
+  }
+  if (ctx->lm_ev[0]) (void)hipEventDestroy(ctx->lm_ev[0]);
+  if (ctx->lm_ev[1]) (void)hipEventDestroy(ctx->lm_ev[1]);
   if (ctx->lin_ev[0]) (void)hipEventDestroy(ctx->lin_ev[0]);
   if (ctx->lin_ev[1]) (void)hipEventDestroy(ctx->lin_ev[1]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -688,13 +756,19 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   timer_begin(ctx, "reproj_jacobian", &stop);
   launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->partial.ptr, s);
   timer_end(ctx, stop);
-  if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s, ctx->sum_ws.ptr);
-  if (overlap || split) {
-    MI_HIP(hipStreamWaitEvent(s, ctx->lin_ev[1], 0));
-  } else if (ctx->sem && !sem_first) {
-    mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
+  // default layout: the semantic pass right behind the reprojection kernel
+  // (its timer starts at the reprojection kernel's stop event), then both
+  // cost sums in one launch
+  const bool sem_after = ctx->sem && !overlap && !split && !sem_first;
+  if (sem_after) {
+    mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false, nullptr, nullptr, stop,
+                                         d.nb ? ctx->partial.ptr : nullptr, reproj_grid(d.nb),
+                                         ctx->scalars.ptr + kCost, ctx->sum_ws.ptr);
     if (st != MI_BA_OK) return st;
+  } else if (d.nb) {
+    launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s, ctx->sum_ws.ptr);
   }
+  if (overlap || split) MI_HIP(hipStreamWaitEvent(s, ctx->lin_ev[1], 0));
   if (ctx->gsba) {
     mi_ba_status st = gsba_linearize(ctx, ctx->scalars.ptr + kGsCost);
     if (st != MI_BA_OK) return st;
@@ -804,22 +878,35 @@ mi_ba_status agree_on_error(mi_ba_context* ctx, bool failed) {
   return ctx->host_scalars[kXR] != 0.0 ? MI_BA_ERR_HIP : MI_BA_OK;
 }
 
+// The Schur terms of S on ctx->stream: - sum_p W_p V_p^-1 W_p' (Z factors,
+// then the image-pair tiles) and the semantic / GSBA blocks.
+void launch_schur_terms(mi_ba_context* ctx) {
+  const DevProblem& d = ctx->dev;
+  hipEvent_t stop;
+  timer_begin(ctx, "schur_build", &stop);
+  launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
+                     d.svariant == 5 ? ctx->ptiles_xcd.ptr : d.svariant == 4 ? ctx->ptiles_blk.ptr : ctx->ptiles.ptr,
+                     d.svariant == 5 ? ctx->nptiles_xcd : ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, false,
+                     ctx->stream);
+  if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
+  if (ctx->gsba) gsba_add_dense(ctx, ctx->S.ptr);
+  timer_end(ctx, stop);
+}
+
 // Exact solve of S df = -b with the explicit reduced camera system.
 // *ok = false when S is not positive definite (Ceres: invalid step).
-mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok) {
+// schur_launched: the Schur terms already run on lm_side (joined here).
+mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok, bool schur_launched) {
   const DevProblem& d = ctx->dev;
   hipStream_t s = ctx->stream;
   const int64_t nf = d.nf;
   *ok = true;
-  // S was zeroed and took U from launch_fblock_dense (context_solve)
   hipEvent_t stop;
-  timer_begin(ctx, "schur_build", &stop);
-  launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
-                     d.svariant == 4 ? ctx->ptiles_blk.ptr : ctx->ptiles.ptr, ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr,
-                     false, s);
-  if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
-  if (ctx->gsba) gsba_add_dense(ctx, ctx->S.ptr);
-  timer_end(ctx, stop);
+  // S was zeroed and took U from launch_fblock_dense (context_solve)
+  if (schur_launched)
+    MI_HIP(hipStreamWaitEvent(s, ctx->lm_ev[1], 0));
+  else
+    launch_schur_terms(ctx);
   if (ctx->world > 1) {
     // every rank holds the Schur contribution of its own points.  Only the
     // upper triangle (row <= col) is meaningful: one in-place all-reduce per
@@ -996,6 +1083,25 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       // through the spare column — about half of S
       hipLaunchKernelGGL(zero_upper_kernel, dim3((unsigned)d.nf), dim3(256), 0, s, ctx->S.ptr, d.nf, d.lds);
     }
+    // one rank: the Schur terms (fabric-bound pair gathers) on lm_side beside
+    // the camera-block pass (HBM-bound row gathers); both only add into S
+    const bool schur_side = ctx->dense && ctx->world == 1 && ctx->schur_overlap;
+    if (schur_side) {
+      if (!ctx->lm_side) {
+        if (hipStreamCreateWithFlags(&ctx->lm_side, hipStreamNonBlocking) != hipSuccess) {
+          ctx->lm_side = nullptr;
+          return MI_BA_ERR_HIP;
+        }
+        MI_HIP(hipEventCreateWithFlags(&ctx->lm_ev[0], hipEventDisableTiming));
+        MI_HIP(hipEventCreateWithFlags(&ctx->lm_ev[1], hipEventDisableTiming));
+      }
+      MI_HIP(hipEventRecord(ctx->lm_ev[0], s));
+      MI_HIP(hipStreamWaitEvent(ctx->lm_side, ctx->lm_ev[0], 0));
+      ctx->stream = ctx->lm_side;  // launch_schur_terms launches (and times) on ctx->stream
+      launch_schur_terms(ctx);
+      ctx->stream = s;
+      MI_HIP(hipEventRecord(ctx->lm_ev[1], ctx->lm_side));
+    }
     {
       Phase ph_(ctx, "fblock");
       if (ctx->dense)
@@ -1024,7 +1130,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     int cg_it = 0;
     bool solved_ok = true;
     if (ctx->dense) {
-      st = dense_solve(ctx, &solved_ok);
+      st = dense_solve(ctx, &solved_ok, schur_side);
       cg_it = 1;
     } else {
       hipEvent_t pstop;
@@ -1627,7 +1733,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->sem_variant = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 4 &&
+  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 5 &&
       (value == 0 || value == 4 || ab_value(value, 0))) {
     ctx->dev.svariant = value;
     return MI_BA_OK;
@@ -1681,6 +1787,14 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   }
   if (std::strcmp(key, "cholesky_panel_group_min_rows") == 0 && value >= 0) {
     ctx->chol.panel_group_min_rows = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_bwd_pairs") == 0 && (value == 0 || value == 1) && ab_value(value, 0)) {
+    ctx->chol.bwd_pairs = value != 0;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "schur_overlap") == 0 && (value == 0 || value == 1) && ab_value(value, 0)) {
+    ctx->schur_overlap = value != 0;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_fused_rhs") == 0 && (value == 0 || value == 1)) {

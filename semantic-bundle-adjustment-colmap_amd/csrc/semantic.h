@@ -69,8 +69,14 @@ void semantic_destroy(mi_ba_context* ctx);
 // reduce into per-pair blocks; cost (0.5 * w * sum rho) into *d_cost.
 // deferred_stream (nullable): run the two-pass route's deferred-sample pass
 // there, ordered after the flat pass by flat_done; the caller joins it.
+// timer_start: the semantic timer starts at this recorded event (the
+// previous phase's stop).  other_partial / other_n / other_out / other_scratch:
+// a second cost sum (the reprojection partials) launched together with the
+// semantic one.
 mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples,
-                                hipStream_t deferred_stream = nullptr, hipEvent_t flat_done = nullptr);
+                                hipStream_t deferred_stream = nullptr, hipEvent_t flat_done = nullptr,
+                                hipEvent_t timer_start = nullptr, const double* other_partial = nullptr,
+                                int64_t other_n = 0, double* other_out = nullptr, double* other_scratch = nullptr);
 // Cost only, at parameters qt (candidate evaluation).
 void semantic_cost(mi_ba_context* ctx, const double* qt, const double* cam, double* d_cost);
 // Fold the pair blocks into the Schur-Jacobi pose blocks, b and diag(U).

@@ -1679,18 +1679,20 @@ void semantic_destroy(mi_ba_context* ctx) {
 // launched there instead (after an event on ctx->stream marks the flat pass
 // done), and the caller joins it; the cost is complete on ctx->stream.
 mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples, hipStream_t deferred_stream,
-                                hipEvent_t flat_done) {
+                                hipEvent_t flat_done, hipEvent_t timer_start, const double* other_partial,
+                                int64_t other_n, double* other_out, double* other_scratch) {
   SemanticState* S = ctx->sem;
   hipStream_t s = ctx->stream;
   S->samples_valid = write_samples;
   if (S->ns == 0) {
     if (S->npairs && hipMemsetAsync(S->pair_blk.ptr, 0, S->pair_blk.bytes(), s) != hipSuccess) return MI_BA_ERR_HIP;
+    if (other_partial) launch_sum(other_partial, other_n, other_out, s, other_scratch);
     return MI_BA_OK;
   }
   SemArgs a = make_args(ctx, ctx->dev.qt, ctx->dev.cam);
   PairConst* pcs = reinterpret_cast<PairConst*>(S->pconst.ptr);
   hipEvent_t stop;
-  timer_begin(ctx, "semantic_jacobian", &stop);
+  timer_begin_after(ctx, "semantic_jacobian", timer_start, &stop);
   hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 1) / 2), dim3(64), 0, s, S->pairs.ptr, S->npairs,
                      a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs, S->pair_blk.ptr, kPairStride,
                      ctx->sem_variant == 6 ? S->pair_cnt.ptr : nullptr);
@@ -1750,7 +1752,10 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   }
 #endif
   timer_end(ctx, stop);
-  launch_sum(S->partial.ptr, S->ntiles, d_cost, s);
+  if (other_partial)
+    launch_sum2(other_partial, other_n, other_out, other_scratch, S->partial.ptr, S->ntiles, d_cost, s);
+  else
+    launch_sum(S->partial.ptr, S->ntiles, d_cost, s);
   if (hipGetLastError() != hipSuccess) return MI_BA_ERR_HIP;
   return MI_BA_OK;
 }
