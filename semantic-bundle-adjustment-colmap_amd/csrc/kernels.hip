@@ -1540,10 +1540,14 @@ __global__ __launch_bounds__(kBlock) void backsub_chunk_kernel(DevProblem p, con
                                                                 double* __restrict__ dX,
                                                                 double* __restrict__ partial) {
   constexpr int W = 9 + CT, W2 = 2 * W, LS = W2 | 1;
-  __shared__ double sl[(kBlock / 64) * 64 * LS];
+  // rows staged 32 at a time (7.9 KB per wave at OPENCV, 39 KB per
+  // workgroup: four workgroups per CU; a 64-row slab allowed two)
+  __shared__ double sl[(kBlock / 64) * 32 * LS];
+  __shared__ double stv[kBlock / 64][64 * 3];
   __shared__ uint32_t spt[kBlock / 64][64];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  double* slab = sl + wv * 64 * LS;
+  double* slab = sl + wv * 32 * LS;
+  double* tvs = stv[wv];
   uint32_t* wpt = spt[wv];
   const int c = blockIdx.x * (kBlock / 64) + wv;
   if (c >= nchunks) return;  // wave-uniform
@@ -1570,29 +1574,33 @@ __global__ __launch_bounds__(kBlock) void backsub_chunk_kernel(DevProblem p, con
   };
   for (uint32_t s0 = b0; s0 < b1; s0 += 64) {
     const int live = (int)min(64u, b1 - s0);
-    wave_load_rows<W2, LS>(J + (size_t)s0 * W2, slab, live);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const bool on = lane < live;
     const uint32_t b = s0 + (on ? lane : 0);
     const uint32_t pt = p.obs_pt[b];
     const bool var = on && p.pt_var[pt] != 0;
     double te[3] = {0.0, 0.0, 0.0};
-    if (on) {
-      const double* row = slab + lane * LS;
-      double e[2];
-      load_jf_x<CT>(p, row, p.obs_img[b], df, e);
-      const double2 r = rr[b];
-      model -= e[0] * r.x + e[1] * r.y + (e[0] * e[0] + e[1] * e[1]) / 2.0;
-      if (var) {
+    for (int h = 0; h < 2; ++h) {
+      const int live_h = min(32, live - 32 * h);
+      if (live_h <= 0) break;  // wave-uniform
+      wave_load_rows<W2, LS>(J + (size_t)(s0 + 32 * h) * W2, slab, live_h);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      if (on && (lane >> 5) == h) {
+        const double* row = slab + (lane - 32 * h) * LS;
+        double e[2];
+        load_jf_x<CT>(p, row, p.obs_img[b], df, e);
+        const double2 r = rr[b];
+        model -= e[0] * r.x + e[1] * r.y + (e[0] * e[0] + e[1] * e[1]) / 2.0;
+        if (var) {
 #pragma unroll
-        for (int n = 0; n < 3; ++n) te[n] = row[6 + n] * e[0] + row[W + 6 + n] * e[1];
+          for (int n = 0; n < 3; ++n) te[n] = row[6 + n] * e[0] + row[W + 6 + n] * e[1];
+        }
       }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // segmented sum: t_b and the point id per lane in the slab
-    double* tv = slab + lane * 4;
+    // segmented sum: t_b and the point id per lane
+    double* tv = tvs + lane * 3;
     tv[0] = te[0];
     tv[1] = te[1];
     tv[2] = te[2];
@@ -1603,9 +1611,9 @@ __global__ __launch_bounds__(kBlock) void backsub_chunk_kernel(DevProblem p, con
     if (head) {
       double t[3] = {te[0], te[1], te[2]};
       for (int l = lane + 1; l < live && wpt[l] == pt; ++l) {
-        t[0] += slab[l * 4];
-        t[1] += slab[l * 4 + 1];
-        t[2] += slab[l * 4 + 2];
+        t[0] += tvs[l * 3];
+        t[1] += tvs[l * 3 + 1];
+        t[2] += tvs[l * 3 + 2];
       }
       if (multi) {
         carry[0] += t[0];
