@@ -80,6 +80,7 @@ struct mi_ba_context {
   miba::DevArray<double> qt_c, cam_c, X_c; // candidate parameters
   miba::DevArray<double> img_rec;          // [I][16] packed image records
   miba::DevArray<uint32_t> cm_perm;
+  miba::DevArray<uint32_t> cm_ptv;  // [nb] camera-major: the block's point if variable, else 0xffffffff
   miba::DevArray<miba::DevTile> tiles;
   int ntiles = 0;
   miba::DevArray<miba::DevPoint> vpoints;
@@ -128,6 +129,7 @@ struct mi_ba_context {
   miba::DevArray<int32_t> info;
   miba::CholConfig chol;                   // factorisation variant (mi_ba_set_tuning)
   bool fused_rhs = true;                   // forward solve carried through the factorisation (S's spare row)
+  bool pp_chunks = true;                   // PCG Schur product's point pass on the point chunks (0: per point, tools build)
   bool schur_overlap = false;              // one rank: Schur terms on lm_side beside the camera-block pass
                                            // (measured slower: BA iteration 28.5 vs 27.1 ms at C4; tools build)
   hipStream_t lm_side = nullptr;

@@ -56,8 +56,8 @@ void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const 
 // blocks, b = g - sum W V^-1 g_p and diag(U), in one pass (no Schur-Jacobi
 // blocks, which only the PCG preconditioner uses).
 void launch_fblock_dense(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
-                         const double2* r, const double* J, const double* q, double* b, double* udiag, double* S,
-                         hipStream_t s);
+                         const uint32_t* cm_ptv, const double2* r, const double* J, const double* q, double* b,
+                         double* udiag, double* S, hipStream_t s);
 
 // Finalise: Jacobi scale (first), LM diagonal, damping Lambda_f, block-Jacobi
 // preconditioner (inverse of the damped diagonal blocks), rhs = -b.
@@ -68,9 +68,11 @@ void launch_fblock_finalize(const DevProblem& p, const double* pose_blk, const d
 
 // Implicit Schur product y = S x (without the semantic pair term); lambda_f
 // null leaves out the damping diagonal (multi-rank: added by rank 0 only).
+// chunks: the back substitution's point chunks (the point pass runs on them).
 void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles,
                           int ntiles, const uint32_t* cm_perm, const double* J, const double* Vinv,
-                          const double* lambda_f, const double* x, double* w, double* y, hipStream_t s);
+                          const double* lambda_f, const double* x, double* w, double* y, hipStream_t s,
+                          const uint32_t* chunks = nullptr, int nchunks = 0, const uint32_t* cm_ptv = nullptr);
 
 // Block-Jacobi preconditioner apply z = M^-1 r.
 void launch_precond(const DevProblem& p, const double* prec_pose, const double* prec_cam,

@@ -933,6 +933,7 @@ __device__ inline int64_t fslot(const DevProblem& p, uint32_t img, uint32_t cam,
 template <int CT>
 __global__ __launch_bounds__(kBlock) void fblock_dense_kernel(DevProblem p, const DevTile* __restrict__ tiles,
                                                                const uint32_t* __restrict__ cm_perm,
+                                                               const uint32_t* __restrict__ cm_ptv,
                                                                const double2* __restrict__ rr,
                                                                const double* __restrict__ J,
                                                                const double* __restrict__ q,
@@ -948,9 +949,9 @@ __global__ __launch_bounds__(kBlock) void fblock_dense_kernel(DevProblem p, cons
   for (uint32_t k = threadIdx.x; k < tile.count; k += kBlock) {
     const uint32_t b = cm_perm[tile.start + k];
     const double* Jb = J + (size_t)b * 2 * W;
-    const uint32_t pt = p.obs_pt[b];
+    const uint32_t pt = cm_ptv[tile.start + k];
     const double2 r = rr[b];
-    const bool ptv = p.pt_var[pt] != 0;
+    const bool ptv = pt != 0xffffffffu;
     double qp[3] = {0.0, 0.0, 0.0};
     if (ptv) {
       qp[0] = q[3 * (size_t)pt];
@@ -1325,6 +1326,7 @@ __global__ __launch_bounds__(kBlock) void schur_point_pass(DevProblem p, const D
 template <int CT>
 __global__ __launch_bounds__(kBlock) void schur_f_pass(DevProblem p, const DevTile* __restrict__ tiles,
                                                         const uint32_t* __restrict__ cm_perm,
+                                                        const uint32_t* __restrict__ cm_ptv,
                                                         const double* __restrict__ J,
                                                         const double* __restrict__ x,
                                                         const double* __restrict__ w,
@@ -1341,8 +1343,14 @@ __global__ __launch_bounds__(kBlock) void schur_f_pass(DevProblem p, const DevTi
     const double* Jb = J + (size_t)b * 2 * W;
     double e[2];
     load_jf_x<CT>(p, Jb, tile.image, x, e);
-    const uint32_t pt = p.obs_pt[b];
-    if (p.pt_var[pt]) {
+    uint32_t pt;
+    if (cm_ptv) {
+      pt = cm_ptv[tile.start + k];  // coalesced; 0xffffffff: constant point
+    } else {
+      pt = p.obs_pt[b];
+      if (!p.pt_var[pt]) pt = 0xffffffffu;
+    }
+    if (pt != 0xffffffffu) {
       const double wv[3] = {w[3 * (size_t)pt], w[3 * (size_t)pt + 1], w[3 * (size_t)pt + 2]};
 #pragma unroll
       for (int row = 0; row < 2; ++row)
@@ -1530,7 +1538,10 @@ __global__ __launch_bounds__(kBlock) void backsub_cost_kernel(DevProblem p, cons
 // lane order (deterministic), then dX_p = -V_p^-1 (g_p + t) and the point's
 // terms -(dX.g_p + dX.t + dX' V_p dX / 2).  Blocks of constant points only
 // add their share.  One cost partial per chunk.
-template <int CT>
+// PP: the implicit Schur product's point pass instead (x = the CG vector):
+// w_p = V_p^-1 sum_a J_p,a' (J_f,a x), no cost terms (schur_point_pass's
+// per-point loop, on chunks).
+template <int CT, bool PP = false>
 __global__ __launch_bounds__(kBlock) void backsub_chunk_kernel(DevProblem p, const uint32_t* __restrict__ chunk,
                                                                 int nchunks, const double* __restrict__ J,
                                                                 const double2* __restrict__ rr,
@@ -1558,8 +1569,16 @@ __global__ __launch_bounds__(kBlock) void backsub_chunk_kernel(DevProblem p, con
   uint32_t carry_pt = 0;
   bool carry_var = false;
   auto finalize = [&](uint32_t pt, const double t[3]) {
-    const double* g = Vg + 9 * (size_t)pt;
     const double* vi = Vinv + 6 * (size_t)pt;
+    if constexpr (PP) {
+      const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
+      double wv[3];
+      sym3_mul(Vi, t, wv);
+#pragma unroll
+      for (int n = 0; n < 3; ++n) dX[3 * (size_t)pt + n] = wv[n];
+      return;
+    }
+    const double* g = Vg + 9 * (size_t)pt;
     const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
     const double tt[3] = {g[6] + t[0], g[7] + t[1], g[8] + t[2]};
     double o[3];
@@ -1589,8 +1608,10 @@ __global__ __launch_bounds__(kBlock) void backsub_chunk_kernel(DevProblem p, con
         const double* row = slab + (lane - 32 * h) * LS;
         double e[2];
         load_jf_x<CT>(p, row, p.obs_img[b], df, e);
-        const double2 r = rr[b];
-        model -= e[0] * r.x + e[1] * r.y + (e[0] * e[0] + e[1] * e[1]) / 2.0;
+        if constexpr (!PP) {
+          const double2 r = rr[b];
+          model -= e[0] * r.x + e[1] * r.y + (e[0] * e[0] + e[1] * e[1]) / 2.0;
+        }
         if (var) {
 #pragma unroll
           for (int n = 0; n < 3; ++n) te[n] = row[6 + n] * e[0] + row[W + 6 + n] * e[1];
@@ -1629,8 +1650,10 @@ __global__ __launch_bounds__(kBlock) void backsub_chunk_kernel(DevProblem p, con
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   }
   if (multi && carry_var) finalize(carry_pt, carry);  // lane 0
-  const double s = wave_sum(model);
-  if (lane == 0) partial[c] = s;
+  if constexpr (!PP) {
+    const double s = wave_sum(model);
+    if (lane == 0) partial[c] = s;
+  }
 }
 
 // Model cost change of the blocks of constant points (no point step).
@@ -2289,8 +2312,8 @@ void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, 
 }
 
 void launch_fblock_dense(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
-                         const double2* r, const double* J, const double* q, double* b, double* udiag, double* S,
-                         hipStream_t s) {
+                         const uint32_t* cm_ptv, const double2* r, const double* J, const double* q, double* b,
+                         double* udiag, double* S, hipStream_t s) {
   if (ntiles == 0) return;
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
@@ -2301,8 +2324,8 @@ void launch_fblock_dense(const DevProblem& p, const DevTile* tiles, int ntiles, 
       return;
     }
 #endif
-    hipLaunchKernelGGL(fblock_dense_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, q, b,
-                       udiag, S);
+    hipLaunchKernelGGL(fblock_dense_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, cm_ptv, r, J, q,
+                       b, udiag, S);
   });
 }
 
@@ -2331,15 +2354,19 @@ void launch_fblock_finalize(const DevProblem& p, const double* pose_blk, const d
 
 void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles,
                           int ntiles, const uint32_t* cm_perm, const double* J, const double* Vinv,
-                          const double* lambda_f, const double* x, double* w, double* y, hipStream_t s) {
+                          const double* lambda_f, const double* x, double* w, double* y, hipStream_t s,
+                          const uint32_t* chunks, int nchunks, const uint32_t* cm_ptv) {
   (void)hipMemsetAsync(y, 0, sizeof(double) * p.nf, s);
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
-    if (npv > 0)
+    if (npv > 0 && chunks && nchunks > 0)
+      hipLaunchKernelGGL((backsub_chunk_kernel<CT, true>), dim3(grid_for(nchunks, kBlock / 64)), dim3(kBlock), 0, s,
+                         p, chunks, nchunks, J, nullptr, nullptr, Vinv, x, w, nullptr);
+    else if (npv > 0)
       hipLaunchKernelGGL(schur_point_pass<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, J,
                          Vinv, x, w);
     if (ntiles > 0)
-      hipLaunchKernelGGL(schur_f_pass<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, J, x, w, y);
+      hipLaunchKernelGGL(schur_f_pass<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, cm_ptv, J, x, w, y);
   });
   if (lambda_f)
     hipLaunchKernelGGL(add_diag_kernel, dim3(grid_for(p.nf, kBlock)), dim3(kBlock), 0, s, lambda_f, x, y, p.nf);

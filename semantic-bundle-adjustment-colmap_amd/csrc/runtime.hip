@@ -467,6 +467,18 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
     if (nb && (hipMemcpy(ctx->cm_perm.ptr, perm.data(), nb * 4, hipMemcpyHostToDevice) ||
                hipMemcpy(ctx->tiles.ptr, tl.data(), tl.size() * sizeof(DevTile), hipMemcpyHostToDevice)))
       return fail(MI_BA_ERR_HIP);
+    // camera-major point of each block, 0xffffffff for constant points: the
+    // camera-block pass reads it coalesced instead of gathering obs_pt and
+    // pt_var per block
+    {
+      std::vector<uint32_t> cp(nb);
+      for (int64_t k = 0; k < nb; ++k) {
+        const uint32_t q = pt[perm[k]];
+        cp[k] = s.pt_var[q] ? q : 0xffffffffu;
+      }
+      if (ctx->cm_ptv.alloc(std::max<int64_t>(1, nb))) return fail(MI_BA_ERR_OUT_OF_MEMORY);
+      if (nb && hipMemcpy(ctx->cm_ptv.ptr, cp.data(), nb * 4, hipMemcpyHostToDevice)) return fail(MI_BA_ERR_HIP);
+    }
     // variable points with their contiguous block ranges
     std::vector<DevPoint> vp;
     int64_t b = 0, nb_var = 0;
@@ -797,7 +809,9 @@ namespace {
 mi_ba_status schur_product(mi_ba_context* ctx, const double* x, double* y) {
   const DevProblem& d = ctx->dev;
   launch_schur_product(d, ctx->vpoints.ptr, ctx->npv, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr,
-                       ctx->Vinv.ptr, ctx->rank == 0 ? ctx->lambda_f.ptr : nullptr, x, ctx->cg_w.ptr, y, ctx->stream);
+                       ctx->Vinv.ptr, ctx->rank == 0 ? ctx->lambda_f.ptr : nullptr, x, ctx->cg_w.ptr, y, ctx->stream,
+                       ctx->pp_chunks ? ctx->pchunks.ptr : nullptr, ctx->npchunks,
+                       ctx->pp_chunks ? ctx->cm_ptv.ptr : nullptr);
   if (ctx->sem) semantic_schur_product(ctx, x, y);
   if (ctx->gsba) gsba_schur_product(ctx, x, y);
   return allreduce(ctx, y, d.nf);
@@ -1105,7 +1119,8 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     {
       Phase ph_(ctx, "fblock");
       if (ctx->dense)
-        launch_fblock_dense(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->cg_w.ptr,
+        launch_fblock_dense(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->cm_ptv.ptr, ctx->r.ptr, ctx->J.ptr,
+                            ctx->cg_w.ptr,
                             ctx->bvec.ptr, ctx->udiag.ptr, ctx->S.ptr, s);
       else
         launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr,
@@ -1787,6 +1802,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   }
   if (std::strcmp(key, "cholesky_panel_group_min_rows") == 0 && value >= 0) {
     ctx->chol.panel_group_min_rows = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "pcg_point_chunks") == 0 && (value == 0 || value == 1) && ab_value(value, 1)) {
+    ctx->pp_chunks = value != 0;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_bwd_pairs") == 0 && (value == 0 || value == 1) && ab_value(value, 0)) {

@@ -2,6 +2,7 @@
 LM per combination of the given keys.
     python tools/ab_schur.py schur_pairs_variant=0,1 cholesky_rest_update=0,1,2,3"""
 import json
+import os
 import sys
 
 import os as _os
@@ -21,14 +22,16 @@ grid = [[]]
 for arg in sys.argv[1:]:
     key, vals = arg.split("=")
     grid = [g + [(key, int(v))] for g in grid for v in vals.split(",")]
+# AB_SOLVER=iterative: the implicit-Schur PCG LM (the N > 1 default) instead of the exact one
+solver = mi_ba.SOLVER_ITERATIVE_SCHUR if os.environ.get("AB_SOLVER") == "iterative" else mi_ba.SOLVER_DENSE_SCHUR
 for tun in grid:
-    with mi_ba.Context(mi_ba.default_options(max_num_iterations=3), sc.copy()) as ctx:
+    with mi_ba.Context(mi_ba.default_options(max_num_iterations=3, linear_solver_type=solver), sc.copy()) as ctx:
         for key, val in tun:
             ctx.set_tuning(key, val)
         ctx.set_timing(True)
         s = ctx.solve()
         its = s.num_successful_steps + s.num_unsuccessful_steps
-        ph = {k: ctx.kernel_time(k) for k in ("cholesky", "cholesky_solve", "schur_build", "fblock", "backsub")}
+        ph = {k: ctx.kernel_time(k) for k in ("cholesky", "cholesky_solve", "schur_build", "fblock", "backsub", "pcg")}
         print(json.dumps(dict(tun, ba_ms=1e3 * s.total_time_in_seconds / its,
                               final=s.final_cost, steps=(s.num_successful_steps, s.num_unsuccessful_steps),
                               **{k: round(t[0] / max(1, t[1]), 3) for k, t in ph.items()})), flush=True)
