@@ -100,6 +100,8 @@ struct mi_ba_context {
   // linearization
   miba::DevArray<double2> r;
   miba::DevArray<double> J;
+  miba::DevArray<double> Jcm;  // PCG path: J's rows in camera-major (cm_perm) order
+  bool jcm_stale = true;       // J re-linearized since Jcm was built
   miba::DevArray<double> Vg;               // [P][9]
   miba::DevArray<double> partial;          // per-workgroup partial sums
   int64_t npartial = 0;
@@ -129,6 +131,7 @@ struct mi_ba_context {
   miba::DevArray<int32_t> info;
   miba::CholConfig chol;                   // factorisation variant (mi_ba_set_tuning)
   bool fused_rhs = true;                   // forward solve carried through the factorisation (S's spare row)
+  int pcg_jcm = 2;  // PCG camera-side passes on the camera-major J copy, f pass staged through LDS (1: per-lane rows, 0: row gathers; tools build)
   bool pp_chunks = true;                   // PCG Schur product's point pass on the point chunks (0: per point, tools build)
   bool schur_overlap = false;              // one rank: Schur terms on lm_side beside the camera-block pass
                                            // (measured slower: BA iteration 28.5 vs 27.1 ms at C4; tools build)

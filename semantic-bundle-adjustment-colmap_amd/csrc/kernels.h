@@ -48,9 +48,13 @@ void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, 
 
 // Camera-side tile pass: per image/camera tangent block S_ii = U_ii - sum W V^-1 W',
 // b = g - sum W V^-1 g_p and diag(U) (undamped column norms).
+// Jcm (nullable): J's rows in camera-major order (launch_permute_rows).
 void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
-                   const double2* r, const double* J, const double* Vg, const double* Vinv,
+                   const double2* r, const double* J, const double* Jcm, const double* Vg, const double* Vinv,
                    double* pose_blk, double* cam_blk, double* b, double* udiag, hipStream_t s);
+// Jcm[k] = J[cm_perm[k]] for k < n (2 (9 + ct) doubles per block).
+void launch_permute_rows(const DevProblem& p, const uint32_t* cm_perm, int64_t n, const double* J, double* Jcm,
+                         hipStream_t s);
 
 // Exact-solver variant of launch_fblock: U = sum J_f'J_f added into S's image
 // blocks, b = g - sum W V^-1 g_p and diag(U), in one pass (no Schur-Jacobi
@@ -69,10 +73,13 @@ void launch_fblock_finalize(const DevProblem& p, const double* pose_blk, const d
 // Implicit Schur product y = S x (without the semantic pair term); lambda_f
 // null leaves out the damping diagonal (multi-rank: added by rank 0 only).
 // chunks: the back substitution's point chunks (the point pass runs on them).
+// Jcm: J's rows in camera-major order (the f pass reads them contiguously;
+// staged: through LDS by coalesced loads, one residual row per lane).
 void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles,
                           int ntiles, const uint32_t* cm_perm, const double* J, const double* Vinv,
                           const double* lambda_f, const double* x, double* w, double* y, hipStream_t s,
-                          const uint32_t* chunks = nullptr, int nchunks = 0, const uint32_t* cm_ptv = nullptr);
+                          const uint32_t* chunks = nullptr, int nchunks = 0, const uint32_t* cm_ptv = nullptr,
+                          const double* Jcm = nullptr, bool staged = false);
 
 // Block-Jacobi preconditioner apply z = M^-1 r.
 void launch_precond(const DevProblem& p, const double* prec_pose, const double* prec_cam,

@@ -802,6 +802,7 @@ __global__ __launch_bounds__(kBlock) void fblock_kernel(DevProblem p, const DevT
                                                          const uint32_t* __restrict__ cm_perm,
                                                          const double2* __restrict__ rr,
                                                          const double* __restrict__ J,
+                                                         const double* __restrict__ Jcm,
                                                          const double* __restrict__ Vg,
                                                          const double* __restrict__ Vinv,
                                                          double* __restrict__ pose_blk,
@@ -818,7 +819,7 @@ __global__ __launch_bounds__(kBlock) void fblock_kernel(DevProblem p, const DevT
   for (int k = 0; k < NV; ++k) acc[k] = 0.0;
   for (uint32_t k = threadIdx.x; k < tile.count; k += kBlock) {
     const uint32_t b = cm_perm[tile.start + k];
-    const double* Jb = J + (size_t)b * 2 * W;
+    const double* Jb = Jcm ? Jcm + (size_t)(tile.start + k) * 2 * W : J + (size_t)b * 2 * W;
     const double2 r = rr[b];
     double jf[2][6 + CT], jx[2][3];
 #pragma unroll
@@ -1328,6 +1329,7 @@ __global__ __launch_bounds__(kBlock) void schur_f_pass(DevProblem p, const DevTi
                                                         const uint32_t* __restrict__ cm_perm,
                                                         const uint32_t* __restrict__ cm_ptv,
                                                         const double* __restrict__ J,
+                                                        const double* __restrict__ Jcm,
                                                         const double* __restrict__ x,
                                                         const double* __restrict__ w,
                                                         double* __restrict__ y) {
@@ -1339,15 +1341,15 @@ __global__ __launch_bounds__(kBlock) void schur_f_pass(DevProblem p, const DevTi
 #pragma unroll
   for (int m = 0; m < NV; ++m) acc[m] = 0.0;
   for (uint32_t k = threadIdx.x; k < tile.count; k += kBlock) {
-    const uint32_t b = cm_perm[tile.start + k];
-    const double* Jb = J + (size_t)b * 2 * W;
+    // Jcm: the rows in camera-major order (contiguous over the tile)
+    const double* Jb = Jcm ? Jcm + (size_t)(tile.start + k) * 2 * W : J + (size_t)cm_perm[tile.start + k] * 2 * W;
     double e[2];
     load_jf_x<CT>(p, Jb, tile.image, x, e);
     uint32_t pt;
     if (cm_ptv) {
       pt = cm_ptv[tile.start + k];  // coalesced; 0xffffffff: constant point
     } else {
-      pt = p.obs_pt[b];
+      pt = p.obs_pt[cm_perm[tile.start + k]];
       if (!p.pt_var[pt]) pt = 0xffffffffu;
     }
     if (pt != 0xffffffffu) {
@@ -1372,6 +1374,83 @@ __global__ __launch_bounds__(kBlock) void schur_f_pass(DevProblem p, const DevTi
       if (p.cam_var[cam]) atomicAdd(y + 6 * (size_t)p.num_images + (size_t)CT * cam + (k - 6), sred[k]);
     }
   }
+}
+
+// schur_f_pass on the camera-major copy, rows staged through the wave's LDS
+// slab by coalesced loads, 32 blocks per pass: lane l takes residual row
+// l / 32 of block l % 32 (y_f = sum over residual rows of J_f,row' e_row).
+template <int CT>
+__global__ __launch_bounds__(kBlock) void schur_f_rows_kernel(DevProblem p, const DevTile* __restrict__ tiles,
+                                                               const uint32_t* __restrict__ cm_ptv,
+                                                               const double* __restrict__ Jcm,
+                                                               const double* __restrict__ x,
+                                                               const double* __restrict__ w,
+                                                               double* __restrict__ y) {
+  constexpr int NV = 6 + CT, W = 9 + CT, W2 = 2 * W, LS = W2 | 1;
+  __shared__ double sl[(kBlock / 64) * 32 * LS];
+  __shared__ double sred[4 * NV];
+  const DevTile tile = tiles[blockIdx.x];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double* slab = sl + wv * 32 * LS;
+  const uint32_t img = tile.image, cam = p.img_cam[img];
+  double xv[NV];
+#pragma unroll
+  for (int m = 0; m < 6; ++m) xv[m] = x[6 * (size_t)img + m];
+#pragma unroll
+  for (int m = 0; m < CT; ++m) xv[6 + m] = x[6 * (size_t)p.num_images + (size_t)CT * cam + m];
+  double acc[NV];
+#pragma unroll
+  for (int m = 0; m < NV; ++m) acc[m] = 0.0;
+  const int bi = lane & 31, rw = lane >> 5;
+  for (uint32_t k0 = 32u * wv; k0 < tile.count; k0 += 32u * (kBlock / 64)) {
+    const int live = (int)min(32u, tile.count - k0);
+    wave_load_rows<W2, LS>(Jcm + (size_t)(tile.start + k0) * W2, slab, live);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (bi < live) {
+      const double* jr = slab + bi * LS + rw * W;
+      double e = 0.0;
+#pragma unroll
+      for (int m = 0; m < 6; ++m) e += jr[m] * xv[m];
+#pragma unroll
+      for (int m = 0; m < CT; ++m) e += jr[9 + m] * xv[6 + m];
+      const uint32_t pt = cm_ptv[tile.start + k0 + bi];
+      if (pt != 0xffffffffu)
+        e -= jr[6] * w[3 * (size_t)pt] + jr[7] * w[3 * (size_t)pt + 1] + jr[8] * w[3 * (size_t)pt + 2];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) acc[m] += jr[m] * e;
+#pragma unroll
+      for (int m = 0; m < CT; ++m) acc[6 + m] += jr[9 + m] * e;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  block_reduce<NV>(acc, sred);
+  const int k = threadIdx.x;
+  if (k < NV) {
+    if (k < 6) {
+      if (p.img_flags[img] & 1u) atomicAdd(y + 6 * (size_t)img + k, sred[k]);
+    } else if (p.cam_var[cam]) {
+      atomicAdd(y + 6 * (size_t)p.num_images + (size_t)CT * cam + (k - 6), sred[k]);
+    }
+  }
+}
+
+// Jcm[k] = J[cm_perm[k]]: the Jacobian rows in camera-major order, 16 B per
+// lane, consecutive lanes on consecutive destination pieces (coalesced
+// stores, row-contiguous gathers).  Built once per linearization for the PCG
+// path, whose camera-side passes then read rows contiguously.
+template <int CT>
+__global__ __launch_bounds__(kBlock) void permute_rows_kernel(const uint32_t* __restrict__ cm_perm, int64_t n,
+                                                               const double* __restrict__ J,
+                                                               double* __restrict__ Jcm) {
+  constexpr int H = 9 + CT;  // 16-B pieces per block (2 rows of 9 + CT doubles)
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n * H) return;
+  const int64_t k = e / H;
+  const int piece = (int)(e - k * H);
+  const dvec2 v = reinterpret_cast<const dvec2*>(J + (size_t)cm_perm[k] * 2 * H)[piece];
+  reinterpret_cast<dvec2*>(Jcm + (size_t)k * 2 * H)[piece] = v;
 }
 
 __global__ void add_diag_kernel(const double* __restrict__ lambda_f, const double* __restrict__ x,
@@ -2330,13 +2409,23 @@ void launch_fblock_dense(const DevProblem& p, const DevTile* tiles, int ntiles, 
 }
 
 void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
-                   const double2* r, const double* J, const double* Vg, const double* Vinv, double* pose_blk,
-                   double* cam_blk, double* b, double* udiag, hipStream_t s) {
+                   const double2* r, const double* J, const double* Jcm, const double* Vg, const double* Vinv,
+                   double* pose_blk, double* cam_blk, double* b, double* udiag, hipStream_t s) {
   if (ntiles == 0) return;
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
-    hipLaunchKernelGGL(fblock_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, Vg, Vinv,
+    hipLaunchKernelGGL(fblock_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, Jcm, Vg, Vinv,
                        pose_blk, cam_blk, b, udiag);
+  });
+}
+
+void launch_permute_rows(const DevProblem& p, const uint32_t* cm_perm, int64_t n, const double* J, double* Jcm,
+                         hipStream_t s) {
+  if (n == 0) return;
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    hipLaunchKernelGGL(permute_rows_kernel<CT>, dim3((unsigned)grid_for(n * (9 + CT), kBlock)), dim3(kBlock), 0, s,
+                       cm_perm, n, J, Jcm);
   });
 }
 
@@ -2355,7 +2444,8 @@ void launch_fblock_finalize(const DevProblem& p, const double* pose_blk, const d
 void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, const DevTile* tiles,
                           int ntiles, const uint32_t* cm_perm, const double* J, const double* Vinv,
                           const double* lambda_f, const double* x, double* w, double* y, hipStream_t s,
-                          const uint32_t* chunks, int nchunks, const uint32_t* cm_ptv) {
+                          const uint32_t* chunks, int nchunks, const uint32_t* cm_ptv, const double* Jcm,
+                          bool staged) {
   (void)hipMemsetAsync(y, 0, sizeof(double) * p.nf, s);
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
@@ -2365,8 +2455,11 @@ void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, 
     else if (npv > 0)
       hipLaunchKernelGGL(schur_point_pass<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, J,
                          Vinv, x, w);
-    if (ntiles > 0)
-      hipLaunchKernelGGL(schur_f_pass<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, cm_ptv, J, x, w, y);
+    if (ntiles > 0 && Jcm && cm_ptv && staged)
+      hipLaunchKernelGGL(schur_f_rows_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_ptv, Jcm, x, w, y);
+    else if (ntiles > 0)
+      hipLaunchKernelGGL(schur_f_pass<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, cm_ptv, J, Jcm, x, w,
+                         y);
   });
   if (lambda_f)
     hipLaunchKernelGGL(add_diag_kernel, dim3(grid_for(p.nf, kBlock)), dim3(kBlock), 0, s, lambda_f, x, y, p.nf);

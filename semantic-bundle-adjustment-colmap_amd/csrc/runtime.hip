@@ -724,10 +724,34 @@ void context_destroy(mi_ba_context* ctx) {
 
 // Residuals + Jacobians + point blocks at the current parameters; cost into
 // scalars[kCost] (geometric) + scalars[kSemCost] (semantic).
+// The PCG path's camera-major copy of J, rebuilt after each linearization
+// (one gather pass; the ~10-20 camera-side passes of an LM iteration then
+// read their rows contiguously instead of gathering them).  Null when the
+// key is off or the copy does not fit (the passes then gather from J).
+static const double* pcg_jcm(mi_ba_context* ctx) {
+  if (!ctx->pcg_jcm || ctx->dense) return nullptr;
+  const size_t nb = ctx->cm_perm.n;
+  if (!ctx->Jcm.ptr || ctx->Jcm.n != ctx->J.n) {
+    if (nb == 0 || ctx->Jcm.alloc(ctx->J.n) != hipSuccess) {
+      (void)hipGetLastError();
+      ctx->Jcm.release();
+      return nullptr;
+    }
+    ctx->jcm_stale = true;
+  }
+  if (ctx->jcm_stale) {
+    Phase ph_(ctx, "permute_rows");
+    launch_permute_rows(ctx->dev, ctx->cm_perm.ptr, (int64_t)nb, ctx->J.ptr, ctx->Jcm.ptr, ctx->stream);
+    ctx->jcm_stale = false;
+  }
+  return ctx->Jcm.ptr;
+}
+
 mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   hipStream_t s = ctx->stream;
   const DevProblem& d = ctx->dev;
   hipEvent_t stop;
+  ctx->jcm_stale = true;
   // image records + the scalar slots zeroed in one launch
   launch_pack_images(d, ctx->img_rec.ptr, s, ctx->scalars.ptr, kNumScalars);
   // linearize_overlap: 1 the semantic kernels on a second stream beside the
@@ -811,7 +835,8 @@ mi_ba_status schur_product(mi_ba_context* ctx, const double* x, double* y) {
   launch_schur_product(d, ctx->vpoints.ptr, ctx->npv, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr,
                        ctx->Vinv.ptr, ctx->rank == 0 ? ctx->lambda_f.ptr : nullptr, x, ctx->cg_w.ptr, y, ctx->stream,
                        ctx->pp_chunks ? ctx->pchunks.ptr : nullptr, ctx->npchunks,
-                       ctx->pp_chunks ? ctx->cm_ptv.ptr : nullptr);
+                       ctx->pp_chunks ? ctx->cm_ptv.ptr : nullptr, ctx->pcg_jcm && !ctx->jcm_stale ? ctx->Jcm.ptr : nullptr,
+                       ctx->pcg_jcm == 2);
   if (ctx->sem) semantic_schur_product(ctx, x, y);
   if (ctx->gsba) gsba_schur_product(ctx, x, y);
   return allreduce(ctx, y, d.nf);
@@ -1123,8 +1148,9 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
                             ctx->cg_w.ptr,
                             ctx->bvec.ptr, ctx->udiag.ptr, ctx->S.ptr, s);
       else
-        launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr,
-                      ctx->Vinv.ptr, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr, s);
+        launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, pcg_jcm(ctx),
+                      ctx->Vg.ptr, ctx->Vinv.ptr, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->bvec.ptr,
+                      ctx->udiag.ptr, s);
       if (ctx->sem) semantic_add_fblock(ctx);
       if (ctx->gsba) gsba_add_fblock(ctx);
     }
@@ -1802,6 +1828,11 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   }
   if (std::strcmp(key, "cholesky_panel_group_min_rows") == 0 && value >= 0) {
     ctx->chol.panel_group_min_rows = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "pcg_jcm") == 0 && value >= 0 && value <= 2 && ab_value(value, 2)) {
+    ctx->pcg_jcm = (int)value;
+    if (!ctx->pcg_jcm) ctx->Jcm.release();
     return MI_BA_OK;
   }
   if (std::strcmp(key, "pcg_point_chunks") == 0 && (value == 0 || value == 1) && ab_value(value, 1)) {
