@@ -71,7 +71,7 @@ struct DevProblem {
   int refine_mask;     // bit0 focal, bit1 principal point, bit2 extra params
   int jvariant;        // Jacobian store path (kernels.hip reproj_jacobian_kernel V)
   int svariant;        // explicit Schur pair kernel (kernels.hip launch_dense_schur)
-  int fvariant;        // exact-path fblock kernel: 0 per-lane rows (default), 1 LDS-staged MFMA (tools build)
+  int fvariant;        // fblock kernels: 0 default; 1 exact path LDS-staged MFMA, 2 PCG path one lane per block (tools build)
   // inputs
   const double2* obs_xy;
   const uint32_t* obs_img;

@@ -247,6 +247,31 @@ __device__ inline void wave_load_rows(const double* __restrict__ src, double* __
   }
 }
 
+// As wave_load_rows for at most NR rows, fully unrolled: every load of the
+// wave is issued before the first LDS write waits on one (the looped form
+// kept ~4 loads in flight per wave, too few to cover HBM latency at the
+// occupancy the slabs allow).
+template <int R, int LS, int NR>
+__device__ inline void wave_load_rows_u(const double* __restrict__ src, double* __restrict__ dst, int nrows) {
+  constexpr int T = (NR * R + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int total = nrows * R;
+  double v[T];
+#pragma unroll
+  for (int i = 0; i < T; ++i) {
+    const int e = lane + 64 * i;
+    v[i] = e < total ? __builtin_nontemporal_load(src + e) : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < T; ++i) {
+    const int e = lane + 64 * i;
+    if (e < total) {
+      const int row = e / R;
+      dst[row * LS + (e - row * R)] = v[i];
+    }
+  }
+}
+
 // One lane per reduced block, one wavefront per 64 consecutive blocks; the
 // kernel writes residuals, tangent Jacobian rows and a per-workgroup cost
 // partial, nothing else (the point/camera normal-equation blocks are reduced
@@ -920,6 +945,128 @@ __global__ __launch_bounds__(kBlock) void fblock_kernel(DevProblem p, const DevT
   }
 }
 
+// packed upper-triangle index of (a, c), a <= c < n
+__device__ inline int sym_index(int a, int c, int n) { return a * n - a * (a - 1) / 2 + (c - a); }
+
+// fblock_kernel with two lanes per block: the even lane takes the pose
+// columns, the odd lane the camera columns (their Schur-Jacobi diagonal
+// blocks, rhs and diag(U) are disjoint), so each lane holds half the
+// accumulators — 256 -> ~130 VGPRs, 1 -> 3 waves per SIMD for the row
+// gathers to overlap.  Same terms, summed per half in lane order by a
+// butterfly that skips the parity bit, then over the waves in order.
+template <int CT>
+__global__ __launch_bounds__(kBlock) void fblock_pair_kernel(DevProblem p, const DevTile* __restrict__ tiles,
+                                                              const uint32_t* __restrict__ cm_perm,
+                                                              const double2* __restrict__ rr,
+                                                              const double* __restrict__ J,
+                                                              const double* __restrict__ Jcm,
+                                                              const double* __restrict__ Vg,
+                                                              const double* __restrict__ Vinv,
+                                                              double* __restrict__ pose_blk,
+                                                              double* __restrict__ cam_blk,
+                                                              double* __restrict__ bvec,
+                                                              double* __restrict__ udiag) {
+  constexpr int NH = CT > 6 ? CT : 6;  // columns per half
+  constexpr int NS = sym_size(NH), NA = NS + 2 * NH;
+  __shared__ double sred[kBlock / 64][2][NA];
+  const DevTile tile = tiles[blockIdx.x];
+  const int W = 9 + CT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hf = lane & 1;
+  const int base = hf ? 9 : 0, nh = hf ? CT : 6;
+  double acc[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) acc[k] = 0.0;
+  for (uint32_t k = threadIdx.x >> 1; k < tile.count; k += kBlock / 2) {
+    const uint32_t b = cm_perm[tile.start + k];
+    const double* Jb = Jcm ? Jcm + (size_t)(tile.start + k) * 2 * W : J + (size_t)b * 2 * W;
+    const double2 r = rr[b];
+    double jf[2][NH], jx[2][3];
+#pragma unroll
+    for (int row = 0; row < 2; ++row) {
+#pragma unroll
+      for (int m = 0; m < NH; ++m) jf[row][m] = m < nh ? Jb[row * W + base + m] : 0.0;
+#pragma unroll
+      for (int m = 0; m < 3; ++m) jx[row][m] = Jb[row * W + 6 + m];
+    }
+    double gm[NH];
+#pragma unroll
+    for (int m = 0; m < NH; ++m) gm[m] = jf[0][m] * r.x + jf[1][m] * r.y;
+    const uint32_t pt = p.obs_pt[b];
+    if (p.pt_var[pt] != 0) {
+      // W_m = J_f,m' J_p (3 values) recomputed where used rather than held
+      // for all m: the registers go to the accumulators
+      const double* vi = Vinv + 6 * (size_t)pt;
+      const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
+      const double* gp = Vg + 9 * (size_t)pt + 6;
+      const double gpv[3] = {gp[0], gp[1], gp[2]};
+      int o = 0;
+#pragma unroll
+      for (int a = 0; a < NH; ++a) {
+        double Wa[3], Ya[3];
+#pragma unroll
+        for (int n = 0; n < 3; ++n) Wa[n] = jf[0][a] * jx[0][n] + jf[1][a] * jx[1][n];
+        sym3_mul(Vi, Wa, Ya);
+        gm[a] -= Ya[0] * gpv[0] + Ya[1] * gpv[1] + Ya[2] * gpv[2];
+#pragma unroll
+        for (int c = a; c < NH; ++c, ++o) {
+          double Wc[3];
+#pragma unroll
+          for (int n = 0; n < 3; ++n) Wc[n] = jf[0][c] * jx[0][n] + jf[1][c] * jx[1][n];
+          acc[o] += jf[0][a] * jf[0][c] + jf[1][a] * jf[1][c] - (Ya[0] * Wc[0] + Ya[1] * Wc[1] + Ya[2] * Wc[2]);
+        }
+      }
+    } else {
+      int o = 0;
+#pragma unroll
+      for (int a = 0; a < NH; ++a)
+#pragma unroll
+        for (int c = a; c < NH; ++c, ++o) acc[o] += jf[0][a] * jf[0][c] + jf[1][a] * jf[1][c];
+    }
+#pragma unroll
+    for (int m = 0; m < NH; ++m) {
+      acc[NS + m] += gm[m];
+      acc[NS + NH + m] += jf[0][m] * jf[0][m] + jf[1][m] * jf[1][m];
+    }
+  }
+  // per half: butterfly over the lanes of one parity, then the waves in order
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {
+    double v = acc[k];
+#pragma unroll
+    for (int off = 2; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+    acc[k] = v;
+  }
+  if (lane < 2) {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) sred[wv][lane][k] = acc[k];
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= 2 * NA) return;
+  const int h = t / NA, k = t - h * NA;
+  double v = sred[0][h][k];
+#pragma unroll
+  for (int w = 1; w < kBlock / 64; ++w) v += sred[w][h][k];
+  const uint32_t img = tile.image, cam = p.img_cam[img];
+  const int n = h ? CT : 6;
+  if (h == 0 ? !(p.img_flags[img] & 1u) : !p.cam_var[cam]) return;
+  if (k < NS) {
+    int a = 0, rem = k;
+    while (rem >= NH - a) { rem -= NH - a; ++a; }
+    const int c = a + rem;
+    if (c >= n) return;
+    if (h == 0)
+      atomicAdd(pose_blk + (size_t)img * kSymPose + sym_index(a, c, 6), v);
+    else
+      atomicAdd(cam_blk + (size_t)cam * sym_size(CT) + sym_index(a, c, CT), v);
+    return;
+  }
+  const int m = (k - NS) % NH;
+  if (m >= n) return;
+  double* dst = k < NS + NH ? bvec : udiag;
+  atomicAdd(dst + (h == 0 ? 6 * (size_t)img + m : 6 * (size_t)p.num_images + (size_t)CT * cam + m), v);
+}
+
 // f-vector slot of tangent column m (pose 0..5, camera 6..) of an image's block
 __device__ inline int64_t fslot(const DevProblem& p, uint32_t img, uint32_t cam, int m) {
   return m < 6 ? 6 * (int64_t)img + m : 6 * (int64_t)p.num_images + (int64_t)p.ct * cam + (m - 6);
@@ -1404,7 +1551,7 @@ __global__ __launch_bounds__(kBlock) void schur_f_rows_kernel(DevProblem p, cons
   const int bi = lane & 31, rw = lane >> 5;
   for (uint32_t k0 = 32u * wv; k0 < tile.count; k0 += 32u * (kBlock / 64)) {
     const int live = (int)min(32u, tile.count - k0);
-    wave_load_rows<W2, LS>(Jcm + (size_t)(tile.start + k0) * W2, slab, live);
+    wave_load_rows_u<W2, LS, 32>(Jcm + (size_t)(tile.start + k0) * W2, slab, live);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (bi < live) {
@@ -1677,28 +1824,43 @@ __global__ __launch_bounds__(kBlock) void backsub_chunk_kernel(DevProblem p, con
     const uint32_t pt = p.obs_pt[b];
     const bool var = on && p.pt_var[pt] != 0;
     double te[3] = {0.0, 0.0, 0.0};
+    // each half: lane l takes residual row l / 32 of block l % 32; the two
+    // rows' t terms meet by a cross-half swizzle at the block's own lane
+    const int bi = lane & 31, rw = lane >> 5;
     for (int h = 0; h < 2; ++h) {
       const int live_h = min(32, live - 32 * h);
       if (live_h <= 0) break;  // wave-uniform
-      wave_load_rows<W2, LS>(J + (size_t)(s0 + 32 * h) * W2, slab, live_h);
+      wave_load_rows_u<W2, LS, 32>(J + (size_t)(s0 + 32 * h) * W2, slab, live_h);
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      if (on && (lane >> 5) == h) {
-        const double* row = slab + (lane - 32 * h) * LS;
-        double e[2];
-        load_jf_x<CT>(p, row, p.obs_img[b], df, e);
-        if constexpr (!PP) {
-          const double2 r = rr[b];
-          model -= e[0] * r.x + e[1] * r.y + (e[0] * e[0] + e[1] * e[1]) / 2.0;
-        }
-        if (var) {
+      double tr[3] = {0.0, 0.0, 0.0};
+      if (bi < live_h) {
+        const uint32_t bb = s0 + 32 * h + bi;
+        const double* row = slab + bi * LS + rw * W;
+        const uint32_t img = p.obs_img[bb];
+        const double* xi = df + 6 * (size_t)img;
+        const double* xc = df + 6 * (size_t)p.num_images + (size_t)CT * p.img_cam[img];
+        double e = 0.0;
 #pragma unroll
-          for (int n = 0; n < 3; ++n) te[n] = row[6 + n] * e[0] + row[W + 6 + n] * e[1];
+        for (int m = 0; m < 6; ++m) e += row[m] * xi[m];
+#pragma unroll
+        for (int m = 0; m < CT; ++m) e += row[9 + m] * xc[m];
+        if constexpr (!PP) {
+          const double2 r = rr[bb];
+          model -= e * (rw ? r.y : r.x) + e * e / 2.0;
         }
+#pragma unroll
+        for (int n = 0; n < 3; ++n) tr[n] = row[6 + n] * e;
+      }
+#pragma unroll
+      for (int n = 0; n < 3; ++n) {
+        const double o = __shfl_xor(tr[n], 32);
+        if (rw == h) te[n] = tr[n] + o;  // row 0 + row 1
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
+    if (!var) te[0] = te[1] = te[2] = 0.0;
     // segmented sum: t_b and the point id per lane
     double* tv = tvs + lane * 3;
     tv[0] = te[0];
@@ -1938,7 +2100,7 @@ __global__ __launch_bounds__(kBlock) void schur_z_kernel(DevProblem p, const dou
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t wb0 = i - lane;
   const int live = wb0 >= p.nb ? 0 : (p.nb - wb0 < 64 ? (int)(p.nb - wb0) : 64);
-  wave_load_rows<W2, LS>(J + wb0 * W2, slab, live);
+  wave_load_rows_u<W2, LS, 64>(J + wb0 * W2, slab, live);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   double jf[2][F], jp[2][3];
@@ -2414,8 +2576,12 @@ void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const 
   if (ntiles == 0) return;
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
-    hipLaunchKernelGGL(fblock_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, Jcm, Vg, Vinv,
-                       pose_blk, cam_blk, b, udiag);
+    if (p.fvariant == 2)  // one lane per block (tools build)
+      hipLaunchKernelGGL(fblock_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, Jcm, Vg, Vinv,
+                         pose_blk, cam_blk, b, udiag);
+    else
+      hipLaunchKernelGGL(fblock_pair_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, Jcm, Vg,
+                         Vinv, pose_blk, cam_blk, b, udiag);
   });
 }
 

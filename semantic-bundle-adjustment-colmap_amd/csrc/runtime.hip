@@ -1779,7 +1779,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->dev.svariant = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "fblock_variant") == 0 && (value == 0 || value == 1) && ab_value(value, 0)) {
+  if (std::strcmp(key, "fblock_variant") == 0 && value >= 0 && value <= 2 && ab_value(value, 0)) {
     ctx->dev.fvariant = value;
     return MI_BA_OK;
   }
