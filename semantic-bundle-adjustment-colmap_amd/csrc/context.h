@@ -132,6 +132,7 @@ struct mi_ba_context {
   miba::CholConfig chol;                   // factorisation variant (mi_ba_set_tuning)
   bool fused_rhs = true;                   // forward solve carried through the factorisation (S's spare row)
   int pcg_jcm = 2;  // PCG camera-side passes on the camera-major J copy, f pass staged through LDS (1: per-lane rows, 0: row gathers; tools build)
+  bool pn_chunks = true;  // point blocks (V_p, g_p) on the point chunks (0: one lane per point, tools build)
   bool pp_chunks = true;                   // PCG Schur product's point pass on the point chunks (0: per point, tools build)
   bool schur_overlap = false;              // one rank: Schur terms on lm_side beside the camera-block pass
                                            // (measured slower: BA iteration 28.5 vs 27.1 ms at C4; tools build)

@@ -39,8 +39,9 @@ void launch_sum2(const double* p1, int64_t n1, double* out1, double* scratch1, c
 // damped inverse Vinv[P][6] of V_p + Lambda_p.
 // Point blocks Vg[P][9] = (V_p packed upper 6, g_p 3) of the variable points
 // from J and r (the solver's point-side normal equations).
+// chunks: the point chunks (one lane per block; else one lane per point)
 void launch_point_normal(const DevProblem& p, const DevPoint* vp, int64_t npv, const double2* r, const double* J,
-                         double* Vg, hipStream_t s);
+                         double* Vg, hipStream_t s, const uint32_t* chunks = nullptr, int nchunks = 0);
 void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg,
                           double* scale_p, double* diag_p, double* Vinv, double* Linv, double* q, int first,
                           int reuse_diag, double radius, hipStream_t s);

@@ -758,6 +758,81 @@ __global__ __launch_bounds__(kBlock) void point_normal_kernel(const DevPoint* __
   for (int m = 0; m < 9; ++m) out[m] = v[m];
 }
 
+// point_normal_kernel on the point chunks: one lane per block (its J_p
+// rows and r, no serial walk per lane), then the first lane of each
+// variable point sums its blocks' terms in lane order (the per-point loop's
+// order; a point of more than 64 blocks sums per 64-block pass).
+template <int CT>
+__global__ __launch_bounds__(kBlock) void point_normal_chunk_kernel(DevProblem p, const uint32_t* __restrict__ chunk,
+                                                                     int nchunks, const double2* __restrict__ rr,
+                                                                     const double* __restrict__ J,
+                                                                     double* __restrict__ Vg) {
+  constexpr int W = 9 + CT;
+  __shared__ double sv[kBlock / 64][64 * 9];
+  __shared__ uint32_t spt[kBlock / 64][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double* tvs = sv[wv];
+  uint32_t* wpt = spt[wv];
+  const int c = blockIdx.x * (kBlock / 64) + wv;
+  if (c >= nchunks) return;  // wave-uniform
+  const uint32_t b0 = chunk[c], b1 = chunk[c + 1];
+  const bool multi = b1 - b0 > 64u;  // one point with more than 64 blocks
+  double carry[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t carry_pt = 0;
+  bool carry_var = false;
+  for (uint32_t s0 = b0; s0 < b1; s0 += 64) {
+    const int live = (int)min(64u, b1 - s0);
+    const bool on = lane < live;
+    const uint32_t b = s0 + (on ? lane : 0);
+    const uint32_t pt = p.obs_pt[b];
+    const bool var = on && p.pt_var[pt] != 0;
+    double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (var) {
+      const double* Jb = J + (size_t)b * 2 * W;
+      const double2 r = rr[b];
+      const double a0 = Jb[6], a1 = Jb[7], a2 = Jb[8];
+      const double c0 = Jb[W + 6], c1 = Jb[W + 7], c2 = Jb[W + 8];
+      v[0] = a0 * a0 + c0 * c0;
+      v[1] = a0 * a1 + c0 * c1;
+      v[2] = a0 * a2 + c0 * c2;
+      v[3] = a1 * a1 + c1 * c1;
+      v[4] = a1 * a2 + c1 * c2;
+      v[5] = a2 * a2 + c2 * c2;
+      v[6] = a0 * r.x + c0 * r.y;
+      v[7] = a1 * r.x + c1 * r.y;
+      v[8] = a2 * r.x + c2 * r.y;
+    }
+#pragma unroll
+    for (int m = 0; m < 9; ++m) tvs[lane * 9 + m] = v[m];
+    wpt[lane] = on ? pt : 0xffffffffu;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const bool head = var && (lane == 0 || wpt[lane - 1] != pt);
+    if (head) {
+      for (int l = lane + 1; l < live && wpt[l] == pt; ++l)
+#pragma unroll
+        for (int m = 0; m < 9; ++m) v[m] += tvs[l * 9 + m];
+      if (multi) {
+#pragma unroll
+        for (int m = 0; m < 9; ++m) carry[m] += v[m];
+        carry_pt = pt;
+        carry_var = true;
+      } else {
+        double* out = Vg + 9 * (size_t)pt;
+#pragma unroll
+        for (int m = 0; m < 9; ++m) out[m] = v[m];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  if (multi && carry_var) {  // lane 0
+    double* out = Vg + 9 * (size_t)carry_pt;
+#pragma unroll
+    for (int m = 0; m < 9; ++m) out[m] = carry[m];
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void point_prepare_kernel(const DevPoint* __restrict__ vp, int64_t npv,
                                                                 const double* __restrict__ Vg,
                                                                 double* __restrict__ scale_p,
@@ -2536,11 +2611,15 @@ void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s, do
 }
 
 void launch_point_normal(const DevProblem& p, const DevPoint* vp, int64_t npv, const double2* r, const double* J,
-                         double* Vg, hipStream_t s) {
+                         double* Vg, hipStream_t s, const uint32_t* chunks, int nchunks) {
   if (npv == 0) return;
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
-    hipLaunchKernelGGL(point_normal_kernel<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, vp, npv, r, J, Vg);
+    if (chunks && nchunks > 0)
+      hipLaunchKernelGGL(point_normal_chunk_kernel<CT>, dim3(grid_for(nchunks, kBlock / 64)), dim3(kBlock), 0, s, p,
+                         chunks, nchunks, r, J, Vg);
+    else
+      hipLaunchKernelGGL(point_normal_kernel<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, vp, npv, r, J, Vg);
   });
 }
 

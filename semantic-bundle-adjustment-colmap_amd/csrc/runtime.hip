@@ -747,6 +747,9 @@ static const double* pcg_jcm(mi_ba_context* ctx) {
   return ctx->Jcm.ptr;
 }
 
+// point blocks on the point chunks unless the tools-build key says per point
+static const uint32_t* pn_chunks(mi_ba_context* ctx) { return ctx->pn_chunks ? ctx->pchunks.ptr : nullptr; }
+
 mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   hipStream_t s = ctx->stream;
   const DevProblem& d = ctx->dev;
@@ -1067,7 +1070,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
   double x_cost = 0.0;
   mi_ba_status st = context_linearize(ctx, &x_cost);
   if (st != MI_BA_OK) return st;
-  launch_point_normal(d, ctx->vpoints.ptr, ctx->npv, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr, s);
+  launch_point_normal(d, ctx->vpoints.ptr, ctx->npv, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr, s, pn_chunks(ctx), ctx->npchunks);
   sum->jacobian_evaluation_time_in_seconds += now_s() - tj;
   sum->num_jacobian_evaluations = 1;
   sum->initial_cost = x_cost + ctx->fixed_cost;
@@ -1297,7 +1300,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       tj = now_s();
       st = context_linearize(ctx, nullptr);
       if (st != MI_BA_OK) return st;
-      launch_point_normal(d, ctx->vpoints.ptr, ctx->npv, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr, s);
+      launch_point_normal(d, ctx->vpoints.ptr, ctx->npv, ctx->r.ptr, ctx->J.ptr, ctx->Vg.ptr, s, pn_chunks(ctx), ctx->npchunks);
       sum->num_jacobian_evaluations += 1;
       sum->jacobian_evaluation_time_in_seconds += now_s() - tj;
     } else {
@@ -1833,6 +1836,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   if (std::strcmp(key, "pcg_jcm") == 0 && value >= 0 && value <= 2 && ab_value(value, 2)) {
     ctx->pcg_jcm = (int)value;
     if (!ctx->pcg_jcm) ctx->Jcm.release();
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "point_normal_chunks") == 0 && (value == 0 || value == 1) && ab_value(value, 1)) {
+    ctx->pn_chunks = value != 0;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "pcg_point_chunks") == 0 && (value == 0 || value == 1) && ab_value(value, 1)) {
