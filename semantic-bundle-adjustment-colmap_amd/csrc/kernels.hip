@@ -1843,7 +1843,7 @@ __global__ __launch_bounds__(kBlock) void backsub_cost_kernel(DevProblem p, cons
 // w_p = V_p^-1 sum_a J_p,a' (J_f,a x), no cost terms (schur_point_pass's
 // per-point loop, on chunks).
 template <int CT, bool PP = false>
-__global__ __launch_bounds__(kBlock) void backsub_chunk_kernel(DevProblem p, const uint32_t* __restrict__ chunk,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void backsub_chunk_kernel(DevProblem p, const uint32_t* __restrict__ chunk,
                                                                 int nchunks, const double* __restrict__ J,
                                                                 const double2* __restrict__ rr,
                                                                 const double* __restrict__ Vg,
