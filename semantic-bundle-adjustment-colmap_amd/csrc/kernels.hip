@@ -897,6 +897,7 @@ __global__ __launch_bounds__(kBlock) void point_prepare_kernel(const DevPoint* _
 // ---------------------------------------------------------------------------
 // Camera side: tile pass building the Schur-Jacobi diagonal blocks and rhs.
 // ---------------------------------------------------------------------------
+#ifdef MI_BA_AB_VARIANTS  // one lane per block: fblock_variant 2 (tools build)
 template <int CT>
 __global__ __launch_bounds__(kBlock) void fblock_kernel(DevProblem p, const DevTile* __restrict__ tiles,
                                                          const uint32_t* __restrict__ cm_perm,
@@ -1019,6 +1020,7 @@ __global__ __launch_bounds__(kBlock) void fblock_kernel(DevProblem p, const DevT
     }
   }
 }
+#endif  // MI_BA_AB_VARIANTS
 
 // packed upper-triangle index of (a, c), a <= c < n
 __device__ inline int sym_index(int a, int c, int n) { return a * n - a * (a - 1) / 2 + (c - a); }
@@ -2655,11 +2657,14 @@ void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const 
   if (ntiles == 0) return;
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
-    if (p.fvariant == 2)  // one lane per block (tools build)
+#ifdef MI_BA_AB_VARIANTS
+    if (p.fvariant == 2) {  // one lane per block (tools build)
       hipLaunchKernelGGL(fblock_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, Jcm, Vg, Vinv,
                          pose_blk, cam_blk, b, udiag);
-    else
-      hipLaunchKernelGGL(fblock_pair_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, Jcm, Vg,
+      return;
+    }
+#endif
+    hipLaunchKernelGGL(fblock_pair_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, Jcm, Vg,
                          Vinv, pose_blk, cam_blk, b, udiag);
   });
 }

@@ -57,7 +57,8 @@ def test_product_library_ships_no_ab_variants():
     library: its code object holds none of their kernels."""
     prod = os.path.join(os.path.dirname(mi_ba.__file__), "libmi_ba.so")
     data = open(prod, "rb").read()
-    for name in (b"schur_pairs_pipelined_kernel", b"semantic_linearize_kernel", b"panel_factor_kernelILi1E"):
+    for name in (b"schur_pairs_pipelined_kernel", b"semantic_linearize_kernel", b"panel_factor_kernelILi1E",
+                 b"13fblock_kernelI"):
         assert name not in data, name
     assert b"semantic_flat_kernel" in data and b"schur_pairs_kernel" in data
 
