@@ -1496,6 +1496,7 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
     side = nullptr;
     return false;
   }
+  side_cus = 0;
   if (rocblas_create_handle(&side_h) != rocblas_status_success) { side_h = nullptr; return false; }
   if (rocblas_set_stream(side_h, side) != rocblas_status_success) return false;
   for (int k = 0; k < 2 * std::max(1, max_panels); ++k) {
@@ -1533,6 +1534,36 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
     epoch = 0;
     linv_rows = nblk * kTB;
   }
+  return true;
+}
+
+bool CholWorkspace::set_side_cus(int ncu) {
+  if (!side || !side_h) return false;
+  if (hipStreamSynchronize(side) != hipSuccess) return false;
+  hipStream_t ns = nullptr;
+  if (ncu > 0) {
+    int total = 0;
+    if (hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || total <= 0)
+      return false;
+    ncu = std::min(ncu, total);
+    std::vector<uint32_t> mask((total + 31) / 32, 0u);
+    for (int k = 0; k < ncu; ++k) {
+      const int cu = (int)((int64_t)k * total / ncu);
+      mask[cu / 32] |= 1u << (cu % 32);
+    }
+    if (hipExtStreamCreateWithCUMask(&ns, (uint32_t)mask.size(), mask.data()) != hipSuccess) return false;
+  } else {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = least = 0;
+    if (hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, greatest) != hipSuccess) return false;
+  }
+  if (rocblas_set_stream(side_h, ns) != rocblas_status_success) {
+    (void)hipStreamDestroy(ns);
+    return false;
+  }
+  (void)hipStreamDestroy(side);
+  side = ns;
+  side_cus = ncu;
   return true;
 }
 
@@ -1594,6 +1625,8 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
     ws->rows_per_group = c.panel_rows_per_group;
     ws->bwd_pairs = c.bwd_pairs;
     ws->group_min_rows = c.panel_group_min_rows;
+    if (ws->side && c.side_cus != ws->side_cus && !ws->set_side_cus(c.side_cus))
+      return rocblas_status_internal_error;
   }
   double* scratch = ws ? ws->scratch : nullptr;
   if (c.panel > 0 && c.gemm_update && c.lookahead && ws && ws->side)

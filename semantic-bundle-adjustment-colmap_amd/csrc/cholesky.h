@@ -24,6 +24,10 @@ namespace miba {
 // chol_variants.txt).
 struct CholConfig {
   int panel = 512;        // 0: recursive split; > 0: right-looking panel width
+  // look-ahead side stream confined to this many CUs (spread over the chip)
+  // so the panel factor's waiting workgroups leave the rest to the trailing
+  // dgemm; 0: all CUs at high priority (tools build: cholesky_panel_cus)
+  int side_cus = 0;
   bool gemm_update = true;
   // look-ahead: the trailing update after the next panel's block column,
   // 0 one dgemm per 512-wide block column, 1 one dsyrk, 2 one dgemmt,
@@ -118,6 +122,8 @@ struct CholWorkspace {
   int rows_per_group = 1;          // CholConfig::panel_rows_per_group
   bool bwd_pairs = false;          // CholConfig::bwd_pairs
   int group_min_rows = 6000;       // CholConfig::panel_group_min_rows
+  int side_cus = 0;                // CholConfig::side_cus of the current side stream
+  bool set_side_cus(int ncu);      // re-create the side stream with that CU mask
 
   // Creates the resources on `device` with events for up to `max_panels`
   // panels and diagonal-block inverses for matrices up to max_n; false on any

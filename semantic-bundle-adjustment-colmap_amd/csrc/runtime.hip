@@ -1829,6 +1829,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.panel_rows_per_group = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "cholesky_panel_cus") == 0 && value >= 0 && value <= 4096 && ab_value(value, 0)) {
+    ctx->chol.side_cus = (int)value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_panel_group_min_rows") == 0 && value >= 0) {
     ctx->chol.panel_group_min_rows = value;
     return MI_BA_OK;
