@@ -134,6 +134,42 @@ def test_iterative_schur_parity(gpu, case):
     assert abs(s_g.final_cost - s_o.final_cost) <= 1e-6 * s_o.final_cost, (s_g.final_cost, s_o.final_cost)
 
 
+@pytest.mark.parametrize("case", ["constants", "long_tracks"])
+def test_iterative_schur_parity_chunks(gpu, case):
+    """The PCG path's chunked point passes and camera-major J copy against the
+    oracle: constant points (camera-major slots without a point term),
+    constant cameras and poses (skipped f-slots), or every point observed by
+    70 images (each point chunk a single point of more than 64 blocks: the
+    carried multi-pass sums)."""
+    if case == "constants":
+        sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.OPENCV, 30, 2000, track_length=6, rotation_range=0.05,
+                                                     extra=(-0.1, 0.01, 1e-4, -1e-4), seed=11)).gauge()
+        rng = np.random.default_rng(3)
+        sc.point_config = np.where(rng.uniform(size=sc.num_points) < 0.3, 2, 1).astype(np.uint8)
+        sc.camera_constant = (np.arange(sc.num_cameras) % 3 == 0).astype(np.uint8)
+        sc.image_constant_pose[5] = 1
+    else:
+        sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 80, 300, track_length=70,
+                                                     rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=12)).gauge()
+    # 3 iterations: same accept/reject decisions; 8: converged to the same
+    # cost.  (Once converged, steps are decided at the rounding floor, where
+    # the oracle and even the exact GPU solve differ: 'constants' reaches
+    # 13157.18092343093 with (6, 2) oracle steps, (8, 0) exact GPU steps,
+    # (6, 1) PCG steps — tools/diag_pcg_constants.py.)
+    for iters in (3, 8):
+        ref = mi_ba.default_options(max_num_iterations=iters, eta=1e-12)
+        opts = mi_ba.default_options(max_num_iterations=iters, eta=1e-12, max_linear_solver_iterations=1000,
+                                     linear_solver_type=mi_ba.SOLVER_ITERATIVE_SCHUR)
+        a, b = sc.copy(), sc.copy()
+        s_o = oracle.solve(ref, a, None)
+        s_g = mi_ba.solve(opts, b, None)
+        assert s_g.num_linear_solver_iterations > s_g.num_successful_steps  # the CG path ran
+        if iters == 3:
+            assert (s_g.num_successful_steps, s_g.num_unsuccessful_steps) == \
+                (s_o.num_successful_steps, s_o.num_unsuccessful_steps)
+        assert abs(s_g.final_cost - s_o.final_cost) <= 1e-6 * s_o.final_cost, (iters, s_g.final_cost, s_o.final_cost)
+
+
 def test_c4_lm_first_iteration_matches_oracle(gpu):
     """The C4 exact-Schur LM the bench times (1000 OPENCV cameras, 1M points,
     10M observations + 5.0M semantic samples; nf = 11 993, dense S) against
