@@ -106,7 +106,43 @@ class Reconstruction {
   const Point3D& GetPoint3D(point3D_t id) const { return points3D.at(id); }
 
   void AddCamera(const Camera& c) { cameras[c.camera_id] = c; }
-  void AddImage(const Image& im) { images[im.image_id] = im; }
+  // A registered image joins the registration order (reg_image_ids_) when it
+  // is first added: the model readers add images in file order, as
+  // ReadImagesBinary / ReadImagesText register them (reconstruction.cc:
+  // 1599-1600,1826-1827).
+  void AddImage(const Image& im) {
+    const bool known = images.count(im.image_id) != 0;
+    images[im.image_id] = im;
+    if (im.registered && (!known || !InRegOrder(im.image_id))) reg_image_ids_.push_back(im.image_id);
+  }
+  // Reconstruction::RegisterImage / DeRegisterImage (reconstruction.cc:296-320)
+  void RegisterImage(image_t id) {
+    Image& im = images.at(id);
+    if (!im.registered || !InRegOrder(id)) {
+      im.registered = true;
+      if (!InRegOrder(id)) reg_image_ids_.push_back(id);
+    }
+  }
+  void DeRegisterImage(image_t id) {
+    Image& im = images.at(id);
+    for (point2D_t k = 0; k < (point2D_t)im.points2D.size(); ++k)
+      if (images.at(id).points2D[k].HasPoint3D()) DeleteObservation(id, k);
+    images.at(id).registered = false;
+    reg_image_ids_.erase(std::remove(reg_image_ids_.begin(), reg_image_ids_.end(), id), reg_image_ids_.end());
+  }
+  // Reconstruction::RegImageIds: registered images in registration order.
+  // Images whose `registered` flag was set directly (not through
+  // RegisterImage / AddImage) follow in image-id order; cleared flags drop out.
+  std::vector<image_t> RegImageIds() const {
+    std::vector<image_t> ids;
+    for (const image_t id : reg_image_ids_) {
+      auto it = images.find(id);
+      if (it != images.end() && it->second.registered) ids.push_back(id);
+    }
+    for (const auto& e : images)
+      if (e.second.registered && !InRegOrder(e.first)) ids.push_back(e.first);
+    return ids;
+  }
   point3D_t AddPoint3D(const double xyz[3]) {
     const point3D_t id = ++num_added_points3D_;  // 1-based like COLMAP
     Point3D p;
@@ -155,12 +191,17 @@ class Reconstruction {
   // Reconstruction::FilterObservationsWithNegativeDepth (reconstruction.cc:
   // 647-665): the depth test of every observation of the registered images
   // on the GPU (mi_ba_positive_depth), then the reference's deletions in
-  // image / point2D order (registered images in image-id order).  Returns the
+  // image / point2D order (registered images in registration order,
+  // RegImageIds).  Returns the
   // number of observations deleted.
   size_t FilterObservationsWithNegativeDepth(int device = 0);
 
  private:
+  bool InRegOrder(image_t id) const {
+    return std::find(reg_image_ids_.begin(), reg_image_ids_.end(), id) != reg_image_ids_.end();
+  }
   point3D_t num_added_points3D_ = 0;
+  std::vector<image_t> reg_image_ids_;
 };
 
 // ---------------------------------------------------------------------------
@@ -581,21 +622,25 @@ inline size_t Reconstruction::FilterObservationsWithNegativeDepth(int device) {
     pidx[p.first] = (int32_t)(xyz.size() / 3);
     xyz.insert(xyz.end(), p.second.xyz, p.second.xyz + 3);
   }
+  std::unordered_map<image_t, int32_t> iidx;
   for (const auto& im : images) {
-    const int32_t i = (int32_t)image_camera.size();
+    iidx[im.first] = (int32_t)image_camera.size();
     qv.insert(qv.end(), im.second.qvec, im.second.qvec + 4);
     tv.insert(tv.end(), im.second.tvec, im.second.tvec + 3);
     image_camera.push_back(cidx.at(im.second.camera_id));
     reg.push_back(im.second.IsRegistered() ? 1 : 0);
-    if (!im.second.IsRegistered()) continue;
-    for (point2D_t k = 0; k < (point2D_t)im.second.points2D.size(); ++k) {
-      const Point2D& p2 = im.second.points2D[k];
+  }
+  // reconstruction.cc:649: for (image_id : reg_image_ids_)
+  for (const image_t id : RegImageIds()) {
+    const Image& im = images.at(id);
+    for (point2D_t k = 0; k < (point2D_t)im.points2D.size(); ++k) {
+      const Point2D& p2 = im.points2D[k];
       if (!p2.HasPoint3D()) continue;
       obs_xy.push_back(p2.xy[0]);
       obs_xy.push_back(p2.xy[1]);
-      obs_image.push_back(i);
+      obs_image.push_back(iidx.at(id));
       obs_point.push_back(pidx.at(p2.point3D_id));
-      obs_ref.emplace_back(im.first, k);
+      obs_ref.emplace_back(id, k);
     }
   }
   if (obs_ref.empty()) return 0;

@@ -17,8 +17,9 @@
 // subclasses; here Run() is synchronous and Stop / Pause / Resume may be
 // called from any other thread while it runs (the util::Thread subset the
 // callbacks use: threading.h:99-145).  Registered images are taken in
-// image-id order (the facade's Reconstruction keeps no separate
-// registration order).
+// registration order (Reconstruction::RegImageIds: file order for a model
+// read from disk, as reconstruction_->RegImageIds() in the reference), so the
+// gauge fixes the same first pose and second tvec as the reference's.
 #pragma once
 
 #include <atomic>
@@ -83,12 +84,7 @@ class ControllerIterationCallback : public IterationCallback {
   ControllerThread* thread_;
 };
 
-inline std::vector<image_t> RegImageIds(const Reconstruction& r) {
-  std::vector<image_t> ids;
-  for (const auto& e : r.images)
-    if (e.second.IsRegistered()) ids.push_back(e.first);
-  return ids;
-}
+inline std::vector<image_t> RegImageIds(const Reconstruction& r) { return r.RegImageIds(); }
 }  // namespace internal
 
 class BundleAdjustmentController : public ControllerThread {

@@ -115,7 +115,8 @@ typedef struct mi_ba_iteration_summary {
   int32_t step_is_successful;
   int32_t linear_solver_iterations;
   double cost;                        /* at the current (accepted) point, fixed cost included */
-  double cost_change;                 /* decrease of this iteration's step (0 when not successful) */
+  double cost_change;                 /* cost - candidate cost of every valid step (negative when
+                                         rejected, as Ceres); 0 for an invalid step */
   double relative_decrease;
   double trust_region_radius;         /* after this iteration's update */
   double step_norm;
@@ -451,13 +452,25 @@ mi_ba_status mi_ba_context_cost(mi_ba_context* ctx, double* cost);
  * mi_ba_context_solve.  Per LM iteration the camera-side normal-equation
  * blocks, the explicit reduced camera system S and the cost scalars are
  * summed over ranks; every rank then factors the same S and back-substitutes
- * its own points.  Exact (dense Schur) solver only.
+ * its own points (exact Schur), or every Schur product of the implicit-Schur
+ * PCG is summed as one nf-vector (ITERATIVE_SCHUR, the N > 1 default).
+ * Sums go over the ranks whenever a reducer is installed, also at world 1
+ * (a 1-rank communicator runs the multi-rank code path; tests/test_comm.py).
+ *
+ * Failure: every RCCL call is polled with a deadline ("comm_timeout_ms",
+ * default 300 000): a collective or a communicator set-up that has not
+ * completed by then, or that reports an asynchronous error
+ * (ncclCommGetAsyncError), aborts the communicator (ncclCommAbort) and the
+ * call returns MI_BA_ERR_HIP — a dead or diverged peer ends the solve
+ * instead of hanging it.  After a failed set_comm the context remains a
+ * single-rank context; after a failed collective every later one fails.
  *
  * mi_ba_comm_unique_id: RCCL unique id (ncclGetUniqueId) to be created on
  * rank 0 and broadcast by the caller (e.g. torch.distributed). */
 #define MI_BA_COMM_ID_BYTES 128
 mi_ba_status mi_ba_comm_unique_id(char id[MI_BA_COMM_ID_BYTES]);
-/* Join rank `rank` of `world` over RCCL (xGMI on one node). */
+/* Join rank `rank` of `world` over RCCL (xGMI on one node); non-blocking
+ * set-up polled to the "comm_timeout_ms" deadline (set that key first). */
 mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t world,
                                     const char id[MI_BA_COMM_ID_BYTES]);
 /* Alternative reducer for hosts without one GPU per rank: sums `n` doubles of
@@ -469,8 +482,13 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
 
 /* Kernel-variant switches for in-process A/B measurement (key, value);
  * unknown keys return MI_BA_ERR_INVALID_ARGUMENT.  Keys:
+ *   "comm_timeout_ms"       deadline of one RCCL collective / of set_comm (default
+ *                           300000); a collective past it aborts the communicator
+ *   "comm_stall_ms"         test hook: a kernel holds the stream this long ahead of
+ *                           every RCCL collective (0 = off), as a missing peer would
  *   "jacobian_variant"      0 production; 1/4 row-staging passes, 9/10 no-store /
- *                           no-arithmetic roofline builds, 20-22 store variants,
+ *                           no-arithmetic roofline builds (11/12 the same of the
+ *                           one-pass production shape), 20-22 store variants,
  *                           30-35 occupancy study (tools/ab_jacobian.py)
  *   "cholesky_panel"        0 recursive split, 64..4096 right-looking panel width
  *   "cholesky_gemm_update"  0 dsyrk / 1 dgemm trailing update

@@ -1,10 +1,12 @@
 // cholesky.cpp — recursive blocked Cholesky over rocBLAS/rocSOLVER (see cholesky.h).
+#define ROCBLAS_BETA_FEATURES_API  // rocblas_gemm_ex_get_solutions
 #include "cholesky.h"
 
 #include <hip/hip_runtime.h>
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 namespace miba {
@@ -1397,9 +1399,38 @@ rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, 
 // rows' block column of C): rocBLAS dgemm, or rocblas_gemm_ex with an
 // explicit Tensile solution index (CholConfig::gemm_solution); an index the
 // library does not accept for the shape falls back to the default solution.
+// Whether this rocBLAS build offers Tensile solution `sol` for the update's
+// problem type (rocblas_gemm_ex_get_solutions), asked once per process per
+// index: an index from another rocBLAS build is then never tried again (no
+// failing rocblas_gemm_ex call, or log line, per trailing update).
+static bool gemm_solution_offered(rocblas_handle h, int m, int n, int k, const double* P, int ldp, double* C, int ldc,
+                                  int sol) {
+  static std::atomic<long long> cache{0};  // (sol << 2) | 1 offered, | 2 not offered; 0 unknown
+  const long long c = cache.load(std::memory_order_relaxed);
+  if (c != 0 && (c >> 2) == sol) return (c & 3) == 1;
+  const double minus_one = -1.0, one = 1.0;
+  rocblas_int size = 0;
+  bool offered = false;
+  if (rocblas_gemm_ex_get_solutions(h, rocblas_operation_none, rocblas_operation_transpose, m, n, k, &minus_one, P,
+                                    rocblas_datatype_f64_r, ldp, P, rocblas_datatype_f64_r, ldp, &one, C,
+                                    rocblas_datatype_f64_r, ldc, C, rocblas_datatype_f64_r, ldc, rocblas_datatype_f64_r,
+                                    rocblas_gemm_algo_solution_index, 0, nullptr, &size) == rocblas_status_success &&
+      size > 0) {
+    std::vector<rocblas_int> list(size);
+    if (rocblas_gemm_ex_get_solutions(h, rocblas_operation_none, rocblas_operation_transpose, m, n, k, &minus_one, P,
+                                      rocblas_datatype_f64_r, ldp, P, rocblas_datatype_f64_r, ldp, &one, C,
+                                      rocblas_datatype_f64_r, ldc, C, rocblas_datatype_f64_r, ldc,
+                                      rocblas_datatype_f64_r, rocblas_gemm_algo_solution_index, 0, list.data(),
+                                      &size) == rocblas_status_success)
+      offered = std::find(list.begin(), list.begin() + size, sol) != list.begin() + size;
+  }
+  cache.store(((long long)sol << 2) | (offered ? 1 : 2), std::memory_order_relaxed);
+  return offered;
+}
+
 rocblas_status gemm_nt(rocblas_handle h, int m, int n, int k, const double* P, int ldp, double* C, int ldc, int sol) {
   const double minus_one = -1.0, one = 1.0;
-  if (sol != 0) {
+  if (sol != 0 && gemm_solution_offered(h, m, n, k, P, ldp, C, ldc, sol)) {
     const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_transpose, m, n, k,
                                               &minus_one, P, rocblas_datatype_f64_r, ldp, P, rocblas_datatype_f64_r, ldp,
                                               &one, C, rocblas_datatype_f64_r, ldc, C, rocblas_datatype_f64_r, ldc,

@@ -150,10 +150,18 @@ struct mi_ba_context {
 
   // multi-rank LM (mi_ba_context_set_comm / _set_host_reducer)
   int rank = 0, world = 1;
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;       // non-blocking RCCL communicator (every call polled with a deadline)
+  bool comm_failed = false;        // the communicator was aborted: every later collective fails
+  int comm_timeout_ms = 300000;    // deadline of one collective / of the communicator set-up ("comm_timeout_ms")
+  int comm_stall_ms = 0;           // test hook ("comm_stall_ms"): a kernel that holds the stream this long
+                                   // ahead of every collective (a peer that never arrives, seen locally)
+  int* stall_flag = nullptr;       // pinned release flag of that kernel
   mi_ba_host_allreduce_fn host_reduce = nullptr;
   void* host_reduce_user = nullptr;
   std::vector<double> reduce_buf;
+  // Sums go over the ranks whenever a reducer is installed, a 1-rank RCCL
+  // communicator included (the multi-rank code path at world 1).
+  bool distributed() const { return world > 1 || comm != nullptr || comm_failed || host_reduce != nullptr; }
 };
 
 namespace miba {

@@ -2550,6 +2550,17 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, 2, kJacProduction | 2>), dim3(g), dim3(kBlock), 0, s, p, r, J,
                                  cost_partial);
               return;
+            // roofline decomposition of the production shape (one slab pass):
+            // 11 = store-only (obs read, r + J rows written, no arithmetic),
+            // 12 = no J store (everything but the J write)
+            case 11:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, kJacPasses, kJacProduction | 2>), dim3(g), dim3(kBlock),
+                                 0, s, p, r, J, cost_partial);
+              return;
+            case 12:
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, kJacPasses, kJacProduction | 1>), dim3(g), dim3(kBlock),
+                                 0, s, p, r, J, cost_partial);
+              return;
             default:
               break;
           }
@@ -2603,8 +2614,12 @@ void launch_sum2(const double* p1, int64_t n1, double* out1, double* scratch1, c
                      out2);
 }
 
+// With scratch the list is always summed by the 64-workgroup pass (the order
+// sum2_kernel gives the same list, so the initial, model and trial costs of
+// the reprojection partials are summed alike at every size); the single
+// workgroup only serves lists without scratch.
 void launch_sum(const double* partial, int64_t n, double* out, hipStream_t s, double* scratch) {
-  if (scratch && n >= 32768) {
+  if (scratch) {
     hipLaunchKernelGGL(sum_multi_kernel, dim3(kSumGroups), dim3(256), 0, s, partial, n, out, scratch,
                        reinterpret_cast<unsigned*>(scratch + kSumGroups));
     return;

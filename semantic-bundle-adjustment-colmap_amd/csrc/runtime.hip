@@ -120,14 +120,96 @@ mi_ba_status read_scalars(mi_ba_context* ctx, int first, int count) {
 
 }  // namespace
 
+namespace {
+
+// A peer that died or diverged must not hang the LM: the communicator is
+// aborted (its kernels leave their wait loops, the stream drains) and every
+// later collective of this context fails at once.
+mi_ba_status comm_fail(mi_ba_context* ctx) {
+  if (ctx->comm && ctx->stall_flag && ctx->stall_flag[0] == 0) {
+    // test hook: the stall was the only thing holding the stream; release it
+    // and let the (1-rank) collective behind it finish before the abort
+    __atomic_store_n(ctx->stall_flag, 1, __ATOMIC_RELEASE);
+    const double until = now_s() + 10.0;
+    while (hipStreamQuery(ctx->stream) == hipErrorNotReady && now_s() < until)
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+  if (ctx->comm) (void)ncclCommAbort(ctx->comm);
+  ctx->comm = nullptr;
+  ctx->comm_failed = true;
+  return MI_BA_ERR_HIP;
+}
+
+// Poll a non-blocking communicator until its pending call (set-up or the
+// enqueue of a collective) is done, an asynchronous error shows, or the
+// deadline passes.
+mi_ba_status comm_settle(mi_ba_context* ctx, double deadline) {
+  for (int spin = 0;; ++spin) {
+    ncclResult_t e = ncclSuccess;
+    if (ncclCommGetAsyncError(ctx->comm, &e) != ncclSuccess) return comm_fail(ctx);
+    if (e == ncclSuccess) return MI_BA_OK;
+    if (e != ncclInProgress || now_s() > deadline) return comm_fail(ctx);
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+// Wait for the context stream (a collective just enqueued on it) with the
+// same deadline, watching the communicator's asynchronous error state: a
+// collective whose peer never arrives is aborted instead of waited on.
+mi_ba_status comm_wait_stream(mi_ba_context* ctx, double deadline) {
+  for (int spin = 0;; ++spin) {
+    const hipError_t q = hipStreamQuery(ctx->stream);
+    if (q == hipSuccess) return MI_BA_OK;
+    if (q != hipErrorNotReady) return comm_fail(ctx);
+    ncclResult_t e = ncclSuccess;
+    if (ncclCommGetAsyncError(ctx->comm, &e) != ncclSuccess || (e != ncclSuccess && e != ncclInProgress) ||
+        now_s() > deadline)
+      return comm_fail(ctx);
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+// Test hook ("comm_stall_ms"): hold the stream, as a collective whose peer
+// never arrives would, until the host releases the flag or the stall time
+// has passed.  One wave; it always ends (a bound on the constant-rate wall
+// clock), so the grid drains by itself.
+__global__ void stall_kernel(const int* flag, uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 && wall_clock64() - t0 < ticks)
+    __builtin_amdgcn_s_sleep(64);
+}
+
+}  // namespace
+
 // Sum n doubles of a device buffer over the ranks of a multi-rank solve (RCCL
-// all-reduce on the context stream, or the host reducer); no-op on one rank.
+// all-reduce on the context stream, or the host reducer); no-op without a
+// reducer.  With RCCL the call returns once the sum is complete: every
+// collective is waited on with the context's deadline ("comm_timeout_ms"), and
+// a failed or timed-out collective aborts the communicator and returns
+// MI_BA_ERR_HIP (on every rank that sees it; a rank whose peer failed sees its
+// own collective time out).
 mi_ba_status allreduce(mi_ba_context* ctx, double* d, int64_t n) {
-  if (ctx->world <= 1 || n <= 0) return MI_BA_OK;
+  if (!ctx->distributed() || n <= 0) return MI_BA_OK;
+  if (ctx->comm_failed) return MI_BA_ERR_HIP;
   if (ctx->comm) {
-    if (ncclAllReduce(d, d, (size_t)n, ncclDouble, ncclSum, ctx->comm, ctx->stream) != ncclSuccess)
-      return MI_BA_ERR_HIP;
-    return MI_BA_OK;
+    const double deadline = now_s() + 1e-3 * ctx->comm_timeout_ms;
+    if (ctx->comm_stall_ms > 0) {
+      int khz = 0;
+      if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess || khz <= 0)
+        return MI_BA_ERR_HIP;
+      if (!ctx->stall_flag && hipHostMalloc(&ctx->stall_flag, sizeof(int), hipHostMallocCoherent) != hipSuccess) {
+        ctx->stall_flag = nullptr;
+        return MI_BA_ERR_HIP;
+      }
+      __atomic_store_n(ctx->stall_flag, 0, __ATOMIC_RELEASE);
+      hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->stall_flag,
+                         (uint64_t)khz * ctx->comm_stall_ms);
+    }
+    const ncclResult_t r = ncclAllReduce(d, d, (size_t)n, ncclDouble, ncclSum, ctx->comm, ctx->stream);
+    if (r != ncclSuccess && r != ncclInProgress) return comm_fail(ctx);
+    mi_ba_status st = comm_settle(ctx, deadline);
+    if (st != MI_BA_OK) return st;
+    return comm_wait_stream(ctx, deadline);
   }
   if (!ctx->host_reduce) return MI_BA_ERR_STATE;
   ctx->reduce_buf.resize(n);
@@ -397,7 +479,7 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
     return MI_BA_ERR_HIP;
   }
   mi_ba_context* ctx = nullptr;
-  const bool recycled = old && old->device == o->device && old->world <= 1 && old->timer.pending.empty();
+  const bool recycled = old && old->device == o->device && !old->distributed() && old->timer.pending.empty();
   if (recycled) {
     ctx = old;
     reset_problem_state(ctx);
@@ -704,8 +786,25 @@ void context_destroy(mi_ba_context* ctx) {
   for (auto e : ctx->timer.pool) (void)hipEventDestroy(e);
   ctx->cholws.destroy();
   if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas);
-  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  if (ctx->comm) {
+    // finalize (flushes the communicator's pending work; non-blocking, so
+    // polled with a bound), then destroy; a communicator that does not
+    // finalize cleanly is aborted
+    const ncclResult_t f = ncclCommFinalize(ctx->comm);
+    bool clean = f == ncclSuccess || f == ncclInProgress;
+    const double deadline = now_s() + 10.0;
+    while (clean) {
+      ncclResult_t e = ncclSuccess;
+      if (ncclCommGetAsyncError(ctx->comm, &e) != ncclSuccess) { clean = false; break; }
+      if (e == ncclSuccess) break;
+      if (e != ncclInProgress || now_s() > deadline) { clean = false; break; }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    (void)(clean ? ncclCommDestroy(ctx->comm) : ncclCommAbort(ctx->comm));
+    ctx->comm = nullptr;
+  }
   if (ctx->host_scalars) (void)hipHostFree(ctx->host_scalars);
+  if (ctx->stall_flag) (void)hipHostFree(ctx->stall_flag);
   if (ctx->lin_side) {
     (void)hipStreamSynchronize(ctx->lin_side);
     (void)hipStreamDestroy(ctx->lin_side);
@@ -813,7 +912,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     if (st != MI_BA_OK) return st;
   }
   MI_HIP(hipGetLastError());
-  if (ctx->world > 1 && cost_out) {
+  if (ctx->distributed() && cost_out) {
     mi_ba_status st = allreduce(ctx, ctx->scalars.ptr + kCost, 1);
     if (st == MI_BA_OK) st = allreduce(ctx, ctx->scalars.ptr + kSemCost, 1);
     if (st != MI_BA_OK) return st;
@@ -909,7 +1008,7 @@ mi_ba_status pcg(mi_ba_context* ctx, int* iterations) {
 // out) ends the solve with MI_BA_ERR_HIP on every rank: one 8-byte sum over
 // the ranks, so no rank stays behind in a later collective.
 mi_ba_status agree_on_error(mi_ba_context* ctx, bool failed) {
-  if (ctx->world <= 1) return failed ? MI_BA_ERR_HIP : MI_BA_OK;
+  if (!ctx->distributed()) return failed ? MI_BA_ERR_HIP : MI_BA_OK;
   double* slot = ctx->scalars.ptr + kXR;
   const double v = failed ? 1.0 : 0.0;
   MI_HIP(hipMemcpyAsync(slot, &v, 8, hipMemcpyHostToDevice, ctx->stream));
@@ -949,7 +1048,7 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok, bool schur_launched) {
     MI_HIP(hipStreamWaitEvent(s, ctx->lm_ev[1], 0));
   else
     launch_schur_terms(ctx);
-  if (ctx->world > 1) {
+  if (ctx->distributed()) {
     // every rank holds the Schur contribution of its own points.  Only the
     // upper triangle (row <= col) is meaningful: one in-place all-reduce per
     // 512-row band over the band's contiguous range from its first diagonal
@@ -1032,7 +1131,7 @@ mi_ba_status run_callbacks(mi_ba_context* ctx, const mi_ba_iteration_summary& it
     const int32_t v = o.iteration_callback(o.callback_user, &it);
     if (v == MI_BA_SOLVER_TERMINATE_SUCCESSFULLY || v == MI_BA_SOLVER_ABORT) d = v;
   }
-  if (ctx->world > 1) {
+  if (ctx->distributed()) {
     double* slot = ctx->scalars.ptr + kXB;  // kXB, kXR: PCG scratch, free between solves
     const double v[2] = {d == MI_BA_SOLVER_TERMINATE_SUCCESSFULLY ? 1.0 : 0.0, d == MI_BA_SOLVER_ABORT ? 1.0 : 0.0};
     MI_HIP(hipMemcpyAsync(slot, v, 16, hipMemcpyHostToDevice, ctx->stream));
@@ -1086,7 +1185,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
   its.step_is_valid = 1;
   its.step_is_successful = 1;
   double t_iter = t_start;
-  const bool callbacks = o.iteration_callback || o.stop_flag || ctx->world > 1;
+  const bool callbacks = o.iteration_callback || o.stop_flag || ctx->distributed();
   while (true) {
     if (callbacks) {
       its.iteration = iteration;
@@ -1127,7 +1226,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     }
     // one rank: the Schur terms (fabric-bound pair gathers) on lm_side beside
     // the camera-block pass (HBM-bound row gathers); both only add into S
-    const bool schur_side = ctx->dense && ctx->world == 1 && ctx->schur_overlap;
+    const bool schur_side = ctx->dense && !ctx->distributed() && ctx->schur_overlap;
     if (schur_side) {
       if (!ctx->lm_side) {
         if (hipStreamCreateWithFlags(&ctx->lm_side, hipStreamNonBlocking) != hipSuccess) {
@@ -1157,7 +1256,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       if (ctx->sem) semantic_add_fblock(ctx);
       if (ctx->gsba) gsba_add_fblock(ctx);
     }
-    if (ctx->world > 1) {
+    if (ctx->distributed()) {
       Phase ph_(ctx, "f_allreduce");
       st = allreduce(ctx, ctx->pose_blk.ptr, (int64_t)ctx->pose_blk.n);
       if (st == MI_BA_OK) st = allreduce(ctx, ctx->cam_blk.ptr, (int64_t)ctx->cam_blk.n);
@@ -1212,7 +1311,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     // camera step counted once (rank 0), point steps on their own ranks
     launch_sqnorm2(ctx->cg_x.ptr, ctx->rank == 0 ? nf : 0, ctx->dX.ptr, 3 * d.num_points, sc + kStepNorm,
                    ctx->red.ptr, s);
-    if (ctx->world > 1) {
+    if (ctx->distributed()) {
       st = allreduce(ctx, sc + kModelCost, 1);
       if (st == MI_BA_OK) st = allreduce(ctx, sc + kSemModel, 1);
       if (st == MI_BA_OK) st = allreduce(ctx, sc + kStepNorm, 1);
@@ -1251,7 +1350,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kCandCost, s, ctx->sum_ws.ptr);
     if (ctx->sem) semantic_cost(ctx, ctx->qt_c.ptr, ctx->cam_c.ptr, sc + kSemCand);
     if (ctx->gsba) gsba_cost(ctx, ctx->qt_c.ptr, ctx->gsba->cyl_c.ptr, sc + kGsCand);
-    if (ctx->world > 1) {
+    if (ctx->distributed()) {
       st = allreduce(ctx, sc + kCandCost, 1);
       if (st == MI_BA_OK) st = allreduce(ctx, sc + kSemCand, 1);
       if (st != MI_BA_OK) return st;
@@ -1281,10 +1380,10 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       break;
     }
     its.relative_decrease = relative_decrease;
+    its.cost_change = cost_change;  // every valid step, as Ceres (negative when rejected)
     if (success) {
       ++sum->num_successful_steps;
       its.step_is_successful = 1;
-      its.cost_change = cost_change;
       x_cost = candidate_cost;
       std::swap(ctx->qt.ptr, ctx->qt_c.ptr);
       std::swap(ctx->cam.ptr, ctx->cam_c.ptr);
@@ -1722,14 +1821,30 @@ mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t wo
   if (!ctx || !id || world < 1 || rank < 0 || rank >= world) return MI_BA_ERR_INVALID_ARGUMENT;
   if (ctx->comm || ctx->host_reduce || ctx->solved) return MI_BA_ERR_STATE;
   MI_HIP(hipSetDevice(ctx->device));
+  if (ctx->comm_failed) return MI_BA_ERR_STATE;
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
-  if (ncclCommInitRank(&ctx->comm, world, u, rank) != ncclSuccess) {
+  // non-blocking: a peer that never joins ends the set-up at the deadline
+  // (MI_BA_ERR_HIP) instead of blocking the caller forever
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  const double deadline = now_s() + 1e-3 * ctx->comm_timeout_ms;
+  const ncclResult_t r = ncclCommInitRankConfig(&ctx->comm, world, u, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (ctx->comm) (void)ncclCommAbort(ctx->comm);
     ctx->comm = nullptr;
     return MI_BA_ERR_HIP;
   }
   ctx->rank = rank;
   ctx->world = world;
+  mi_ba_status st = comm_settle(ctx, deadline);
+  if (st != MI_BA_OK) {
+    // the context stays usable as a single-rank context
+    ctx->comm_failed = false;
+    ctx->rank = 0;
+    ctx->world = 1;
+    return st;
+  }
   return reduce_fixed_cost(ctx);
 }
 
@@ -1757,6 +1872,17 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   if (!ctx || !key) return MI_BA_ERR_INVALID_ARGUMENT;
   if (std::strcmp(key, "jacobian_variant") == 0 && value >= 0 && value <= 63 && ab_value(value, 0)) {
     ctx->dev.jvariant = value;
+    return MI_BA_OK;
+  }
+  // multi-rank: deadline of one collective or of the communicator set-up
+  // (a timed-out collective aborts the communicator, MI_BA_ERR_HIP)
+  if (std::strcmp(key, "comm_timeout_ms") == 0 && value >= 1) {
+    ctx->comm_timeout_ms = value;
+    return MI_BA_OK;
+  }
+  // test hook: hold the stream ahead of every RCCL collective for `value` ms
+  if (std::strcmp(key, "comm_stall_ms") == 0 && value >= 0 && value <= 60000) {
+    ctx->comm_stall_ms = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "linearize_order") == 0 && (value == 0 || value == 1)) {

@@ -8,6 +8,9 @@
 // Known answers transcribed from the reference's tests:
 //   TestFilterObservationsWithNegativeDepth  src/base/reconstruction_test.cc:510-531
 //   TestFilterPoints3D (reprojection half)   src/base/reconstruction_test.cc:415-434
+// Registration order: ReadImagesText / ReadImagesBinary register images in
+// file order (reconstruction.cc:1599-1600,1826-1827); the controllers' gauge
+// takes RegImageIds()[0] / [1] (controllers/bundle_adjustment.cc:91-94).
 // Callback semantics: ceres::IterationCallback as the reference's controllers
 // use it (controllers/bundle_adjustment.cc:43-61,87-88) and the SBA snapshot
 // callback's update_state_every_iteration (semantic_bundle_adjustment.h:129,
@@ -23,6 +26,10 @@
 #include <vector>
 
 #include "colmap_amd/controllers.h"
+#include "colmap_amd/model_io.h"
+
+#include <cstdlib>
+#include <fstream>
 
 using namespace colmap_amd;
 
@@ -360,6 +367,65 @@ int main(int argc, char** argv) {
     CHECK_T(fc.Summary().num_successful_steps + fc.Summary().num_unsuccessful_steps == 3);
     CHECK_T(ms >= 60.0);
     CHECK_T(fc.IsStopped());
+  }});
+
+  // A model whose images.txt is not in image-id order: RegImageIds follows
+  // the file, RegisterImage / DeRegisterImage append / remove.
+  cases.push_back({"TestRegImageIdsFileOrder", false, [] {
+    char tmpl[] = "/tmp/reg_order_XXXXXX";
+    const char* dir = mkdtemp(tmpl);
+    CHECK_T(dir != nullptr);
+    if (!dir) return;
+    const std::string d(dir);
+    std::ofstream(d + "/cameras.txt") << "1 SIMPLE_RADIAL 100 100 100 50 50 0\n";
+    std::ofstream(d + "/images.txt") << "5 1 0 0 0 0 0 10 1 a.png\n10 20 1\n"
+                                        "2 1 0 0 0 0.5 0 10 1 b.png\n11 21 1\n"
+                                        "9 1 0 0 0 -0.5 0 10 1 c.png\n12 22 1\n";
+    std::ofstream(d + "/points3D.txt") << "1 0 0 0 0 0 0 -1 5 0 2 0 9 0\n";
+    Reconstruction rec;
+    ReadModelText(d, &rec);
+    CHECK_T((rec.RegImageIds() == std::vector<image_t>{5, 2, 9}));
+    rec.DeRegisterImage(2);
+    CHECK_T((rec.RegImageIds() == std::vector<image_t>{5, 9}));
+    CHECK_T(!rec.GetImage(2).IsRegistered() && rec.points3D.at(1).track.size() == 2);
+    rec.RegisterImage(2);
+    CHECK_T((rec.RegImageIds() == std::vector<image_t>{5, 9, 2}));
+    // the binary round trip keeps a registration order of the same images
+    WriteModelBinary(d, rec);
+    Reconstruction back;
+    ReadModelBinary(d, &back);
+    std::vector<image_t> ids = back.RegImageIds();
+    std::sort(ids.begin(), ids.end());
+    CHECK_T((ids == std::vector<image_t>{2, 5, 9}));
+    for (const char* f : {"cameras", "images", "points3D"}) {
+      std::remove((d + "/" + f + ".txt").c_str());
+      std::remove((d + "/" + f + ".bin").c_str());
+    }
+    rmdir(dir);
+  }});
+
+  // The controller's gauge follows the registration order: images registered
+  // as 2, 0, 3, 1 fix image 2's pose and image 0's tvec x.
+  cases.push_back({"TestControllerGaugeFollowsRegistrationOrder", true, [] {
+    const Reconstruction base = SolveScene(4, 80);
+    Reconstruction rec;
+    rec.cameras = base.cameras;
+    rec.points3D = base.points3D;
+    for (image_t id : {2u, 0u, 3u, 1u}) rec.AddImage(base.images.at(id));
+    CHECK_T((rec.RegImageIds() == std::vector<image_t>{2, 0, 3, 1}));
+    Image before2 = rec.GetImage(2), before0 = rec.GetImage(0), before1 = rec.GetImage(1);
+    BundleAdjustmentOptions o;
+    o.print_summary = false;
+    BundleAdjustmentController ctl(o, &rec);
+    ctl.Run();
+    CHECK_T(ctl.Solved());
+    const Image& a2 = rec.GetImage(2);
+    const Image& a0 = rec.GetImage(0);
+    const Image& a1 = rec.GetImage(1);
+    for (int m = 0; m < 3; ++m) CHECK_T(a2.tvec[m] == before2.tvec[m]);
+    CHECK_T(a0.tvec[0] == before0.tvec[0]);
+    CHECK_T(a0.tvec[1] != before0.tvec[1]);
+    CHECK_T(a1.tvec[0] != before1.tvec[0]);
   }});
 
   // Fewer than two registered images: the reference prints an error and returns.

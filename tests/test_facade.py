@@ -40,10 +40,10 @@ def test_facade_solve_gpu(gpu):
 
 def test_controllers_host():
     out = run("host", "controllers_test")
-    assert out.count("PASS") == 2
+    assert out.count("PASS") == 3
 
 
 @pytest.mark.gpu
 def test_controllers_gpu(gpu):
     out = run("gpu", "controllers_test")
-    assert out.count("PASS") == 9
+    assert out.count("PASS") == 11
