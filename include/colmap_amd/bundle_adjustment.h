@@ -21,8 +21,12 @@
 // residuals (bundle_adjustment.cc:267-269).
 #pragma once
 
+#include <sys/stat.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
+#include <fstream>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -36,173 +40,10 @@
 #include <vector>
 
 #include "../mi_ba.h"
+#include "model_io.h"
+#include "reconstruction.h"
 
 namespace colmap_amd {
-
-typedef uint32_t camera_t;
-typedef uint32_t image_t;
-typedef uint64_t point3D_t;
-typedef uint32_t point2D_t;
-const point3D_t kInvalidPoint3DId = std::numeric_limits<point3D_t>::max();
-
-// ---------------------------------------------------------------------------
-// Minimal Reconstruction (the parts BundleAdjuster touches).
-// ---------------------------------------------------------------------------
-struct Camera {
-  camera_t camera_id = 0;
-  int model_id = MI_BA_SIMPLE_RADIAL;
-  uint64_t width = 0, height = 0;
-  std::vector<double> params;
-  double* ParamsData() { return params.data(); }
-  int ModelId() const { return model_id; }
-  camera_t CameraId() const { return camera_id; }
-};
-
-struct Point2D {
-  double xy[2] = {0, 0};
-  point3D_t point3D_id = kInvalidPoint3DId;
-  bool HasPoint3D() const { return point3D_id != kInvalidPoint3DId; }
-};
-
-struct TrackElement {
-  image_t image_id;
-  point2D_t point2D_idx;
-};
-
-struct Image {
-  image_t image_id = 0;
-  camera_t camera_id = 0;
-  std::string name;
-  double qvec[4] = {1, 0, 0, 0};
-  double tvec[3] = {0, 0, 0};
-  std::vector<Point2D> points2D;
-  bool registered = true;
-  bool IsRegistered() const { return registered; }
-  image_t ImageId() const { return image_id; }
-  camera_t CameraId() const { return camera_id; }
-  const std::string& Name() const { return name; }
-  size_t NumPoints3D() const {
-    return (size_t)std::count_if(points2D.begin(), points2D.end(), [](const Point2D& p) { return p.HasPoint3D(); });
-  }
-};
-
-struct Point3D {
-  double xyz[3] = {0, 0, 0};
-  uint8_t color[3] = {0, 0, 0};
-  double error = -1.0;
-  std::vector<TrackElement> track;
-};
-
-class Reconstruction {
- public:
-  std::map<camera_t, Camera> cameras;
-  std::map<image_t, Image> images;
-  std::map<point3D_t, Point3D> points3D;
-
-  Camera& GetCamera(camera_t id) { return cameras.at(id); }
-  Image& GetImage(image_t id) { return images.at(id); }
-  Point3D& GetPoint3D(point3D_t id) { return points3D.at(id); }
-  const Image& GetImage(image_t id) const { return images.at(id); }
-  const Point3D& GetPoint3D(point3D_t id) const { return points3D.at(id); }
-
-  void AddCamera(const Camera& c) { cameras[c.camera_id] = c; }
-  // A registered image joins the registration order (reg_image_ids_) when it
-  // is first added: the model readers add images in file order, as
-  // ReadImagesBinary / ReadImagesText register them (reconstruction.cc:
-  // 1599-1600,1826-1827).
-  void AddImage(const Image& im) {
-    const bool known = images.count(im.image_id) != 0;
-    images[im.image_id] = im;
-    if (im.registered && (!known || !InRegOrder(im.image_id))) reg_image_ids_.push_back(im.image_id);
-  }
-  // Reconstruction::RegisterImage / DeRegisterImage (reconstruction.cc:296-320)
-  void RegisterImage(image_t id) {
-    Image& im = images.at(id);
-    if (!im.registered || !InRegOrder(id)) {
-      im.registered = true;
-      if (!InRegOrder(id)) reg_image_ids_.push_back(id);
-    }
-  }
-  void DeRegisterImage(image_t id) {
-    Image& im = images.at(id);
-    for (point2D_t k = 0; k < (point2D_t)im.points2D.size(); ++k)
-      if (images.at(id).points2D[k].HasPoint3D()) DeleteObservation(id, k);
-    images.at(id).registered = false;
-    reg_image_ids_.erase(std::remove(reg_image_ids_.begin(), reg_image_ids_.end(), id), reg_image_ids_.end());
-  }
-  // Reconstruction::RegImageIds: registered images in registration order.
-  // Images whose `registered` flag was set directly (not through
-  // RegisterImage / AddImage) follow in image-id order; cleared flags drop out.
-  std::vector<image_t> RegImageIds() const {
-    std::vector<image_t> ids;
-    for (const image_t id : reg_image_ids_) {
-      auto it = images.find(id);
-      if (it != images.end() && it->second.registered) ids.push_back(id);
-    }
-    for (const auto& e : images)
-      if (e.second.registered && !InRegOrder(e.first)) ids.push_back(e.first);
-    return ids;
-  }
-  point3D_t AddPoint3D(const double xyz[3]) {
-    const point3D_t id = ++num_added_points3D_;  // 1-based like COLMAP
-    Point3D p;
-    std::copy(xyz, xyz + 3, p.xyz);
-    points3D[id] = p;
-    return id;
-  }
-  // A point with a given id (model readers); later AddPoint3D ids continue after it.
-  void SetPoint3D(point3D_t id, const Point3D& p) {
-    points3D[id] = p;
-    num_added_points3D_ = std::max(num_added_points3D_, id);
-  }
-  void AddObservation(point3D_t point3D_id, const TrackElement& te) {
-    images.at(te.image_id).points2D.at(te.point2D_idx).point3D_id = point3D_id;
-    points3D.at(point3D_id).track.push_back(te);
-  }
-  // Reconstruction::DeleteObservation (reconstruction.cc:257-277): a track
-  // of length <= 2 takes its point with it.
-  void DeleteObservation(image_t image_id, point2D_t point2D_idx) {
-    Point2D& p2 = images.at(image_id).points2D.at(point2D_idx);
-    auto& tr = points3D.at(p2.point3D_id).track;
-    if (tr.size() <= 2) {
-      DeletePoint3D(p2.point3D_id);
-      return;
-    }
-    tr.erase(std::remove_if(tr.begin(), tr.end(),
-                            [&](const TrackElement& t) { return t.image_id == image_id && t.point2D_idx == point2D_idx; }),
-             tr.end());
-    p2.point3D_id = kInvalidPoint3DId;
-  }
-  void DeletePoint3D(point3D_t id) {
-    for (const TrackElement& te : points3D.at(id).track)
-      images.at(te.image_id).points2D.at(te.point2D_idx).point3D_id = kInvalidPoint3DId;
-    points3D.erase(id);
-  }
-
-  // Reconstruction::FilterPoints3DWithLargeReprojectionError
-  // (reconstruction.cc:1472-1525) on the GPU (mi_ba_filter_points3d): the
-  // given points' track elements are flattened in Track order, their errors
-  // evaluated and the decisions applied here.  Returns the number of
-  // observations filtered.
-  size_t FilterPoints3DWithLargeReprojectionError(double max_reproj_error,
-                                                  const std::unordered_set<point3D_t>& point3D_ids,
-                                                  int device = 0);
-
-  // Reconstruction::FilterObservationsWithNegativeDepth (reconstruction.cc:
-  // 647-665): the depth test of every observation of the registered images
-  // on the GPU (mi_ba_positive_depth), then the reference's deletions in
-  // image / point2D order (registered images in registration order,
-  // RegImageIds).  Returns the
-  // number of observations deleted.
-  size_t FilterObservationsWithNegativeDepth(int device = 0);
-
- private:
-  bool InRegOrder(image_t id) const {
-    return std::find(reg_image_ids_.begin(), reg_image_ids_.end(), id) != reg_image_ids_.end();
-  }
-  point3D_t num_added_points3D_ = 0;
-  std::vector<image_t> reg_image_ids_;
-};
 
 // ---------------------------------------------------------------------------
 // Options / config (bundle_adjustment.h:49-167)
@@ -358,14 +199,15 @@ struct SolverSummary {
 
 namespace internal {
 
-inline void ThrowStatus(mi_ba_status st, const char* what) {
-  const std::string msg = std::string(what) + ": " + mi_ba_status_string(st);
-  switch (st) {
-    case MI_BA_OK: return;
-    case MI_BA_ERR_INVALID_ARGUMENT: throw std::invalid_argument(msg);
-    case MI_BA_ERR_UNSUPPORTED: throw std::domain_error(msg);
-    case MI_BA_ERR_STATE: throw std::logic_error(msg);
-    default: throw std::runtime_error(msg);
+// mkdir -p (createFolder, util/utils.h:92-105, without emptying the folder)
+inline void MakeDirs(const std::string& path) {
+  std::string cur;
+  for (size_t k = 0; k <= path.size(); ++k) {
+    if (k == path.size() || path[k] == '/') {
+      if (!cur.empty() && ::mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST)
+        throw std::runtime_error("cannot create folder " + cur);
+    }
+    if (k < path.size()) cur += path[k];
   }
 }
 
@@ -537,144 +379,6 @@ inline SolverSummary ToSummary(const mi_ba_summary& s) {
 
 }  // namespace internal
 
-inline size_t Reconstruction::FilterPoints3DWithLargeReprojectionError(
-    double max_reproj_error, const std::unordered_set<point3D_t>& point3D_ids, int device) {
-  std::unordered_map<camera_t, int32_t> cidx;
-  std::unordered_map<image_t, int32_t> iidx;
-  std::vector<camera_t> cam_ids;
-  std::vector<image_t> img_ids;
-  std::vector<point3D_t> pt_ids;
-  std::vector<double> params, qv, tv, xyz, obs_xy;
-  std::vector<int32_t> models, image_camera, obs_image, obs_point;
-  std::vector<TrackElement> obs_te;
-  for (const auto& c : cameras) {
-    cidx[c.first] = (int32_t)cam_ids.size();
-    cam_ids.push_back(c.first);
-    models.push_back(c.second.model_id);
-    params.insert(params.end(), c.second.params.begin(), c.second.params.end());
-  }
-  for (const auto& im : images) {
-    iidx[im.first] = (int32_t)img_ids.size();
-    img_ids.push_back(im.first);
-    qv.insert(qv.end(), im.second.qvec, im.second.qvec + 4);
-    tv.insert(tv.end(), im.second.tvec, im.second.tvec + 3);
-    image_camera.push_back(cidx.at(im.second.camera_id));
-  }
-  for (const point3D_t id : point3D_ids) {
-    auto it = points3D.find(id);
-    if (it == points3D.end()) continue;  // ExistsPoint3D (:1481-1483)
-    const int32_t p = (int32_t)pt_ids.size();
-    pt_ids.push_back(id);
-    xyz.insert(xyz.end(), it->second.xyz, it->second.xyz + 3);
-    for (const TrackElement& te : it->second.track) {
-      const Point2D& p2 = images.at(te.image_id).points2D.at(te.point2D_idx);
-      obs_xy.push_back(p2.xy[0]);
-      obs_xy.push_back(p2.xy[1]);
-      obs_image.push_back(iidx.at(te.image_id));
-      obs_point.push_back(p);
-      obs_te.push_back(te);
-    }
-  }
-  mi_ba_problem pr{};
-  pr.camera_model = models.empty() ? MI_BA_SIMPLE_RADIAL : models[0];
-  pr.camera_model_ids = models.data();
-  pr.num_cameras = (int32_t)cam_ids.size();
-  pr.camera_params = params.data();
-  pr.num_images = (int32_t)img_ids.size();
-  pr.qvec = qv.data();
-  pr.tvec = tv.data();
-  pr.image_camera = image_camera.data();
-  pr.num_points = (int64_t)pt_ids.size();
-  pr.xyz = xyz.data();
-  pr.num_obs = (int64_t)obs_image.size();
-  pr.obs_xy = obs_xy.data();
-  pr.obs_image = obs_image.data();
-  pr.obs_point = obs_point.data();
-  std::vector<uint8_t> obs_keep(obs_image.size()), point_keep(pt_ids.size());
-  std::vector<double> err(pt_ids.size());
-  for (size_t p = 0; p < pt_ids.size(); ++p) err[p] = points3D.at(pt_ids[p]).error;
-  int64_t num_filtered = 0;
-  internal::ThrowStatus(mi_ba_filter_points3d(&pr, max_reproj_error, nullptr, device, obs_keep.data(),
-                                              point_keep.data(), err.data(), &num_filtered),
-                        "FilterPoints3DWithLargeReprojectionError");
-  for (size_t k = 0; k < obs_te.size(); ++k)
-    if (point_keep[obs_point[k]] && !obs_keep[k]) DeleteObservation(obs_te[k].image_id, obs_te[k].point2D_idx);
-  for (size_t p = 0; p < pt_ids.size(); ++p) {
-    if (!point_keep[p]) DeletePoint3D(pt_ids[p]);
-    else points3D.at(pt_ids[p]).error = err[p];
-  }
-  return (size_t)num_filtered;
-}
-
-inline size_t Reconstruction::FilterObservationsWithNegativeDepth(int device) {
-  std::unordered_map<camera_t, int32_t> cidx;
-  std::vector<double> params, qv, tv, xyz, obs_xy;
-  std::vector<int32_t> models, image_camera, obs_image, obs_point;
-  std::vector<uint8_t> reg;
-  std::vector<std::pair<image_t, point2D_t>> obs_ref;
-  std::unordered_map<point3D_t, int32_t> pidx;
-  for (const auto& c : cameras) {
-    cidx[c.first] = (int32_t)models.size();
-    models.push_back(c.second.model_id);
-    params.insert(params.end(), c.second.params.begin(), c.second.params.end());
-  }
-  for (const auto& p : points3D) {
-    pidx[p.first] = (int32_t)(xyz.size() / 3);
-    xyz.insert(xyz.end(), p.second.xyz, p.second.xyz + 3);
-  }
-  std::unordered_map<image_t, int32_t> iidx;
-  for (const auto& im : images) {
-    iidx[im.first] = (int32_t)image_camera.size();
-    qv.insert(qv.end(), im.second.qvec, im.second.qvec + 4);
-    tv.insert(tv.end(), im.second.tvec, im.second.tvec + 3);
-    image_camera.push_back(cidx.at(im.second.camera_id));
-    reg.push_back(im.second.IsRegistered() ? 1 : 0);
-  }
-  // reconstruction.cc:649: for (image_id : reg_image_ids_)
-  for (const image_t id : RegImageIds()) {
-    const Image& im = images.at(id);
-    for (point2D_t k = 0; k < (point2D_t)im.points2D.size(); ++k) {
-      const Point2D& p2 = im.points2D[k];
-      if (!p2.HasPoint3D()) continue;
-      obs_xy.push_back(p2.xy[0]);
-      obs_xy.push_back(p2.xy[1]);
-      obs_image.push_back(iidx.at(id));
-      obs_point.push_back(pidx.at(p2.point3D_id));
-      obs_ref.emplace_back(id, k);
-    }
-  }
-  if (obs_ref.empty()) return 0;
-  mi_ba_problem pr{};
-  pr.camera_model = models.empty() ? MI_BA_SIMPLE_RADIAL : models[0];
-  pr.camera_model_ids = models.data();
-  pr.num_cameras = (int32_t)models.size();
-  pr.camera_params = params.data();
-  pr.num_images = (int32_t)image_camera.size();
-  pr.qvec = qv.data();
-  pr.tvec = tv.data();
-  pr.image_camera = image_camera.data();
-  pr.num_points = (int64_t)(xyz.size() / 3);
-  pr.xyz = xyz.data();
-  pr.num_obs = (int64_t)obs_image.size();
-  pr.obs_xy = obs_xy.data();
-  pr.obs_image = obs_image.data();
-  pr.obs_point = obs_point.data();
-  std::vector<uint8_t> keep(obs_ref.size());
-  int64_t negative = 0;
-  internal::ThrowStatus(mi_ba_positive_depth(&pr, reg.data(), device, keep.data(), &negative),
-                        "FilterObservationsWithNegativeDepth");
-  // the reference's deletions, in order: an observation whose point an
-  // earlier deletion already removed is no longer counted (HasPoint3D)
-  size_t num_filtered = 0;
-  for (size_t k = 0; k < obs_ref.size(); ++k) {
-    if (keep[k]) continue;
-    if (!images.at(obs_ref[k].first).points2D.at(obs_ref[k].second).HasPoint3D()) continue;
-    DeleteObservation(obs_ref[k].first, obs_ref[k].second);
-    ++num_filtered;
-  }
-  return num_filtered;
-}
-
 // Device resources reused by consecutive solves of one host thread (the
 // mapper's repeated local BAs): pass the same arena to every Solve.
 class SolverArena {
@@ -742,6 +446,22 @@ class BundleAdjuster {
 // Semantic BA (semantic_bundle_adjustment.h:53-272)
 // ---------------------------------------------------------------------------
 struct SemanticBundleAdjustmentOptions : BundleAdjustmentOptions {
+  // Outputs (semantic_bundle_adjustment.h:60-73).  output_path: the refined
+  // reconstruction is written there (binary) and to output_path/text after
+  // the solve.  visualization_path ("{output_path}/run" resolves to
+  // output_path + "/run", as the controller does, controllers/
+  // semantic_bundle_adjustment.cc:92-94): every LM iteration k writes the
+  // current reconstruction to visualization_path/optim_steps/step_k (binary)
+  // and step_k/text (SBACallbackFunctor, semantic_bundle_adjustment.cc:
+  // 1086-1123), and with export_csv the semantic error of every grid pixel of
+  // every ordered pair of config images to step_k/vis_<image1>_to_<image2>.csv
+  // (ExportSemanticErrorToCSV, :908-1019; the rows come from the GPU,
+  // mi_ba_semantic_export).  Off by default (output_path empty).  Unlike the
+  // reference's createFolders (util/utils.h:101-104), existing folders are
+  // never emptied: files of the same names are overwritten, others are kept.
+  std::string output_path;
+  std::string visualization_path = "{output_path}/run";
+  bool export_csv = false;
   double depth_error_threshold = 2;
   int error_computation_pixel_step = 10;
   double numeric_relative_step_size = 1e-3;
@@ -750,6 +470,12 @@ struct SemanticBundleAdjustmentOptions : BundleAdjustmentOptions {
     solver_options.function_tolerance = 1e-8;
     solver_options.gradient_tolerance = 1e-8;
     solver_options.parameter_tolerance = 1e-8;
+    // the reference's SBA callbacks read the current point (semantic_bundle_adjustment.h:127-129)
+    solver_options.update_state_every_iteration = true;
+  }
+  std::string ResolvedVisualizationPath() const {
+    if (visualization_path == "{output_path}/run") return output_path.empty() ? std::string() : output_path + "/run";
+    return visualization_path;
   }
 };
 typedef BundleAdjustmentConfig SemanticBundleAdjustmentConfig;
@@ -817,18 +543,90 @@ class SemanticBundleAdjuster {
     sem.numeric_relative_step_size = options_.numeric_relative_step_size;
     mi_ba_options o = internal::ToOptions(options_);
     o.semantic_weight = options_.semantic_weight;
+    // the per-iteration snapshot writer runs after the caller's callbacks
+    // (Solve pushes the SBACallbackFunctor last, semantic_bundle_adjustment.cc:519-520)
+    const std::string steps = options_.ResolvedVisualizationPath();
+    SolverArena arena;  // the live context, for the CSV rows inside the callback
+    SemanticBundleAdjustmentOptions cb_options = options_;
+    struct StepWriter : IterationCallback {
+      SemanticBundleAdjuster* sba;
+      Reconstruction* rec;
+      const internal::Flat* flat;
+      SolverArena* arena;
+      std::string steps;
+      CallbackReturnType operator()(const IterationSummary& it) override {
+        std::printf("\nOptimization Iteration %d Update\n%-16s%.6g\n%-16s%.6g\n", it.iteration, "Cost: ", it.cost,
+                    "Cost change: ", it.cost_change);
+        sba->WriteStep(*rec, *flat, *arena->get(), steps + "/optim_steps/step_" + std::to_string(it.iteration));
+        return SOLVER_CONTINUE;
+      }
+    } writer;
+    writer.sba = this;
+    writer.rec = reconstruction;
+    writer.flat = &flat;
+    writer.arena = &arena;
+    writer.steps = steps;
+    if (!steps.empty()) {
+      cb_options.solver_options.callbacks.push_back(&writer);
+      cb_options.solver_options.update_state_every_iteration = true;
+    }
     internal::CallbackBridge bridge;
-    internal::InstallCallbacks(options_, &bridge, [&] { flat.WriteBack(reconstruction); }, &o);
+    internal::InstallCallbacks(cb_options, &bridge, [&] { flat.WriteBack(reconstruction); }, &o);
     mi_ba_summary s;
-    const mi_ba_status st = mi_ba_solve(&o, &flat.problem, &sem, &s);
+    const mi_ba_status st = mi_ba_solve_in(arena.get(), &o, &flat.problem, &sem, &s);
     if (st == MI_BA_ERR_NO_RESIDUALS) return false;
     internal::ThrowStatus(st, "SemanticBundleAdjuster::Solve");
     summary_ = internal::ToSummary(s);
     flat.WriteBack(reconstruction);
+    if (!options_.output_path.empty()) {  // :531-538
+      internal::MakeDirs(options_.output_path + "/text");
+      WriteModelBinary(options_.output_path, *reconstruction);
+      WriteModelText(options_.output_path + "/text", *reconstruction);
+    }
     return true;
   }
 
   const SolverSummary& Summary() const { return summary_; }
+
+  // One snapshot (SBACallbackFunctor::operator(), semantic_bundle_adjustment.cc:
+  // 1090-1123): the reconstruction's current state to dir (binary) and
+  // dir/text, and with export_csv every ordered pair of config images'
+  // ExportSemanticErrorToCSV file dir/vis_<name1>_to_<name2>.csv.
+  void WriteStep(const Reconstruction& rec, const internal::Flat& flat, mi_ba_context* ctx, const std::string& dir) {
+    internal::MakeDirs(dir + "/text");
+    if (options_.export_csv) {
+      std::vector<int32_t> pix, status;
+      std::vector<double> err, world;
+      for (size_t a = 0; a < flat.img_ids.size(); ++a) {
+        if (!flat.img_cfg[a]) continue;
+        for (size_t b = 0; b < flat.img_ids.size(); ++b) {
+          if (a == b || !flat.img_cfg[b]) continue;
+          int64_t n = 0;
+          internal::ThrowStatus(mi_ba_semantic_export(ctx, (int32_t)a, (int32_t)b, &n, nullptr, nullptr, nullptr, nullptr),
+                                "ExportSemanticErrorToCSV");
+          pix.resize(4 * n);
+          status.resize(n);
+          err.resize(n);
+          world.resize(3 * n);
+          internal::ThrowStatus(mi_ba_semantic_export(ctx, (int32_t)a, (int32_t)b, &n, pix.data(), status.data(),
+                                                      err.data(), world.data()),
+                                "ExportSemanticErrorToCSV");
+          const std::string path = dir + "/vis_" + rec.GetImage(flat.img_ids[a]).name + "_to_" +
+                                   rec.GetImage(flat.img_ids[b]).name + ".csv";
+          std::ofstream f(path);
+          if (!f.is_open()) throw std::runtime_error("cannot write " + path);
+          // :994-1007: default stream formatting, the error as float
+          f << "Type,SemanticError,X1,Y1,X2,Y2,X3D,Y3D,Z3D\n";
+          for (int64_t k = 0; k < n; ++k)
+            f << status[k] << "," << (float)err[k] << "," << pix[4 * k] << "," << pix[4 * k + 1] << ","
+              << pix[4 * k + 2] << "," << pix[4 * k + 3] << "," << world[3 * k] << "," << world[3 * k + 1] << ","
+              << world[3 * k + 2] << "\n";
+        }
+      }
+    }
+    WriteModelBinary(dir, rec);
+    WriteModelText(dir + "/text", rec);
+  }
 
  private:
   SemanticBundleAdjustmentOptions options_;

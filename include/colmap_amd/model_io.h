@@ -27,7 +27,7 @@
 #include <string>
 #include <vector>
 
-#include "bundle_adjustment.h"
+#include "reconstruction.h"
 
 namespace colmap_amd {
 

@@ -436,6 +436,22 @@ mi_ba_status mi_ba_download_jacobian(mi_ba_context* ctx, int64_t* block_obs,
 mi_ba_status mi_ba_download_semantic(mi_ba_context* ctx, int32_t* sample_pixel,
                                      int32_t* status, double* residuals,
                                      double* jacobian);
+/* The rows of SemanticBundleAdjuster::ExportSemanticErrorToCSV
+ * (semantic_bundle_adjustment.cc:908-1019) for the ordered image pair
+ * (image1, image2) — problem image indices — at the context's current
+ * parameters (inside an iteration callback: the current LM point): every
+ * pixel of image1's grid, y outer / x inner with the semantic pixel_step,
+ * zero-depth pixels included (the reference exports them; the problem's
+ * samples skip them), through compute_semantic_error
+ * (semantic_cost_functions.h:87-208).  *count = number of grid pixels;
+ * with pixels == NULL only the count is returned.  Rows:
+ *   pixels [n][4] (X1, Y1, X2, Y2: image1 pixel, rounded image2 pixel);
+ *   status [n] (MI_BA_VALID / _OUT_OF_BOUNDS / _INVALID_DEPTH);
+ *   error [n] (0 / 1); world [n][3] (the image1 pixel's point in world).
+ * MI_BA_ERR_UNSUPPORTED when either image's rasters are not resident (an
+ * image that is the second image of no configured pair). */
+mi_ba_status mi_ba_semantic_export(mi_ba_context* ctx, int32_t image1, int32_t image2, int64_t* count,
+                                   int32_t* pixels, int32_t* status, double* error, double* world);
 /* LM solve on a resident context (single use, like BundleAdjuster::Solve);
  * parameters stay on the device until mi_ba_context_writeback. */
 mi_ba_status mi_ba_context_solve(mi_ba_context* ctx, mi_ba_summary* summary);

@@ -360,16 +360,28 @@ void BuildSemSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& 
   }
 }
 
+// compute_semantic_error (semantic_cost_functions.h:87-208) against image j;
+// pw_out / pxy_out (nullable): return_point3D / return_point2D_2.
+double SemanticErrorTo(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, int j, const SemSample& smp,
+                       const double q1[4], const double t1[3], const double q2[4], const double t2[3], int* status,
+                       double* pw_out = nullptr, int* pxy_out = nullptr);
+
 double SemanticError(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, const SemSample& smp,
                      const double q1[4], const double t1[3], const double q2[4], const double t2[3],
                      int* status) {
-  const int j = sem->pairs[2 * smp.pair + 1];
+  return SemanticErrorTo(p, s, sem, sem->pairs[2 * smp.pair + 1], smp, q1, t1, q2, t2, status);
+}
+
+double SemanticErrorTo(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, int j, const SemSample& smp,
+                       const double q1[4], const double t1[3], const double q2[4], const double t2[3], int* status,
+                       double* pw_out, int* pxy_out) {
   const int cam2 = p->image_camera[j];
   const double* K2 = &p->camera_params[s.cam_poff[cam2]];
   double q1i[4], t1i[3];
   PoseInverse(q1, t1, q1i, t1i);                       // :121-125
   double pw[3];
   PoseTransformPoint(q1i, t1i, smp.pc1, pw);           // :127-128
+  if (pw_out) for (int m = 0; m < 3; ++m) pw_out[m] = pw[m];  // :131-133
   double pc2[3];
   PoseTransformPoint(q2, t2, pw, pc2);                 // :136-138
   const double u2 = pc2[0] / pc2[2];                   // :141-144
@@ -379,6 +391,10 @@ double SemanticError(const mi_ba_problem* p, const Setup& s, const mi_ba_semanti
   WorldToImage(s.cam_model[cam2], K2, u2, v2, &x2, &y2); // :149-151
   const int px = CastToIntX86(std::round(x2));         // :154-156
   const int py = CastToIntX86(std::round(y2));
+  if (pxy_out) {                                       // :159-160
+    pxy_out[0] = px;
+    pxy_out[1] = py;
+  }
   const int H = sem->height, W = sem->width;
   if (px < 0 || px >= W || py < 0 || py >= H) {        // :163-177
     *status = MI_BA_OUT_OF_BOUNDS;
@@ -1227,6 +1243,51 @@ int64_t oracle_semantic_eval(const mi_ba_options* o, mi_ba_problem* p, const mi_
     int stt;
     EvalSemantic(p, s, sem, ss, k, &stt, &residuals[k], &jacobian[12 * k]);
     status[k] = stt;
+  }
+  return n;
+}
+
+// SemanticBundleAdjuster::ExportSemanticErrorToCSV (semantic_bundle_adjustment.cc:
+// 908-1019): every pixel of image1's grid (y outer, x inner, zero-depth pixels
+// included) against image2 at the problem's parameters.  Returns the row
+// count (rows written when it fits capacity), or -status.
+int64_t oracle_semantic_export(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem, int32_t image1,
+                               int32_t image2, int32_t* pixels, int32_t* status, double* error, double* world,
+                               int64_t capacity) {
+  Setup s;
+  const int st = BuildSetup(o, p, &s);
+  if (st) return -st;
+  const int H = sem->height, W = sem->width, step = sem->pixel_step;
+  const int nx = (W + step - 1) / step, ny = (H + step - 1) / step;
+  const int64_t n = (int64_t)nx * ny;
+  if (n > capacity) return n;
+  const int cam1 = p->image_camera[image1];
+  const double* K1 = &p->camera_params[s.cam_poff[cam1]];
+  const double* q1 = p->qvec + 4 * image1;
+  const double* t1 = p->tvec + 3 * image1;
+  const double* q2 = p->qvec + 4 * image2;
+  const double* t2 = p->tvec + 3 * image2;
+  int64_t k = 0;
+  for (int y = 0; y < H; y += step) {       // :953-956
+    for (int x = 0; x < W; x += step, ++k) {
+      const int64_t off = (int64_t)image1 * H * W + (int64_t)y * W + x;
+      SemSample smp;
+      smp.pair = 0; smp.x = x; smp.y = y;
+      double u1, v1;
+      ImageToWorld(s.cam_model[cam1], K1, (double)x, (double)y, &u1, &v1);
+      const double depth = (double)sem->depth[off];
+      smp.pc1[0] = u1 * depth;
+      smp.pc1[1] = v1 * depth;
+      smp.pc1[2] = depth;
+      smp.label1 = sem->label[off];
+      int stt = 0, pxy[2] = {0, 0};
+      error[k] = SemanticErrorTo(p, s, sem, image2, smp, q1, t1, q2, t2, &stt, &world[3 * k], pxy);
+      status[k] = stt;
+      pixels[4 * k] = x;
+      pixels[4 * k + 1] = y;
+      pixels[4 * k + 2] = pxy[0];
+      pixels[4 * k + 3] = pxy[1];
+    }
   }
   return n;
 }

@@ -50,6 +50,10 @@ def load():
     lib.oracle_reproj_throughput.restype = C.c_double
     lib.oracle_reproj_throughput.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem), C.c_int64,
                                              C.c_int, C.c_int, _i64p]
+    lib.oracle_semantic_export.restype = C.c_int64
+    lib.oracle_semantic_export.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem),
+                                           C.POINTER(mi_ba.Semantic), C.c_int32, C.c_int32, _i32p, _i32p,
+                                           _dp, _dp, C.c_int64]
     lib.oracle_semantic_eval.restype = C.c_int64
     lib.oracle_semantic_eval.argtypes = [C.POINTER(mi_ba.Options), C.POINTER(mi_ba.Problem),
                                          C.POINTER(mi_ba.Semantic), _i32p, _i32p, _dp, _dp, C.c_int64]
@@ -292,6 +296,27 @@ def semantic_eval(options, scene, semantic):
     lib.oracle_semantic_eval(C.byref(options), C.byref(p), C.byref(s), px.ctypes.data_as(_i32p),
                              st.ctypes.data_as(_i32p), r.ctypes.data_as(_dp), J.ctypes.data_as(_dp), n)
     return px, st, r, J
+
+
+def semantic_export(options, scene, semantic, image1, image2):
+    """ExportSemanticErrorToCSV rows of (image1, image2) at the scene's
+    parameters: (pixels [n][4], status [n], error [n], world [n][3])."""
+    s = semantic.struct()
+    sc = scene.copy()
+    p = sc.problem()
+    lib = load()
+    n = lib.oracle_semantic_export(C.byref(options), C.byref(p), C.byref(s), image1, image2, None, None, None, None, 0)
+    if n < 0:
+        raise RuntimeError(f"oracle_semantic_export status {-n}")
+    pix = np.empty((n, 4), np.int32)
+    st = np.empty(n, np.int32)
+    err = np.empty(n)
+    world = np.empty((n, 3))
+    sc = scene.copy()
+    p = sc.problem()
+    lib.oracle_semantic_export(C.byref(options), C.byref(p), C.byref(s), image1, image2, pix.ctypes.data_as(_i32p),
+                               st.ctypes.data_as(_i32p), err.ctypes.data_as(_dp), world.ctypes.data_as(_dp), n)
+    return pix, st, err, world
 
 
 def semantic_flat_property(options, scene, semantic, bound_scale=1.0):

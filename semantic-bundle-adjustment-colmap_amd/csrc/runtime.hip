@@ -1762,6 +1762,12 @@ mi_ba_status mi_ba_download_semantic(mi_ba_context* ctx, int32_t* sample_pixel, 
   return MI_BA_OK;
 }
 
+mi_ba_status mi_ba_semantic_export(mi_ba_context* ctx, int32_t image1, int32_t image2, int64_t* count,
+                                   int32_t* pixels, int32_t* status, double* error, double* world) {
+  MI_BIND(ctx);
+  return semantic_export(ctx, image1, image2, count, pixels, status, error, world);
+}
+
 mi_ba_status mi_ba_context_solve(mi_ba_context* ctx, mi_ba_summary* summary) {
   if (!summary) return MI_BA_ERR_INVALID_ARGUMENT;
   MI_BIND(ctx);

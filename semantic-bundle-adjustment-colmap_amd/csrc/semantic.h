@@ -37,6 +37,8 @@ struct SemanticState {
   int H = 0, W = 0;
   double depth_threshold = 2.0;
   double rel_step = 1e-3;
+  int step = 1;          // pixel grid step (error_computation_pixel_step)
+  std::vector<uint8_t> has_raster;         // [I] image has a raster slot
   int64_t ns = 0;        // samples
   int npairs = 0;
   std::vector<SemPair> pairs_host;
@@ -77,6 +79,10 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
                                 hipStream_t deferred_stream = nullptr, hipEvent_t flat_done = nullptr,
                                 hipEvent_t timer_start = nullptr, const double* other_partial = nullptr,
                                 int64_t other_n = 0, double* other_out = nullptr, double* other_scratch = nullptr);
+// ExportSemanticErrorToCSV rows of the ordered image pair (image1, image2) at
+// the current parameters (mi_ba_semantic_export).
+mi_ba_status semantic_export(mi_ba_context* ctx, int32_t image1, int32_t image2, int64_t* count, int32_t* pixels,
+                             int32_t* status, double* error, double* world);
 // Cost only, at parameters qt (candidate evaluation).
 void semantic_cost(mi_ba_context* ctx, const double* qt, const double* cam, double* d_cost);
 // Fold the pair blocks into the Schur-Jacobi pose blocks, b and diag(U).

@@ -55,10 +55,13 @@ __device__ inline void quat_rotate_point(const double q[4], const double pt[3], 
 
 // compute_semantic_error (semantic_cost_functions.h:87-208), the reference's
 // operation sequence.
+// pw_out / pxy_out (nullable): the world point and the rounded pixel in image
+// 2 (compute_semantic_error's return_point3D / return_point2D_2).
 template <int M>
 __device__ inline double semantic_error(const SemArgs& a, const double pc1[3], float label1, const double* q1,
                                         const double* t1, const double* q2, const double* t2, const double* K2,
-                                        const float2* dl2, int* status) {
+                                        const float2* dl2, int* status, double* pw_out = nullptr,
+                                        int* pxy_out = nullptr) {
   // PoseInverse (rotation_extension.h:43-57)
   const double sc = 1.0 / sqrt(q1[0] * q1[0] + q1[1] * q1[1] + q1[2] * q1[2] + q1[3] * q1[3]);
   const double qi[4] = {sc * q1[0], -(sc * q1[1]), -(sc * q1[2]), -(sc * q1[3])};
@@ -82,6 +85,11 @@ __device__ inline double semantic_error(const SemArgs& a, const double pc1[3], f
   pw[0] += ti[0];
   pw[1] += ti[1];
   pw[2] += ti[2];
+  if (pw_out) {
+    pw_out[0] = pw[0];
+    pw_out[1] = pw[1];
+    pw_out[2] = pw[2];
+  }
   // PoseTransformPoint(q2, t2, P_w) -> camera 2
   double p2[3];
   quat_rotate_point(q2, pw, p2);
@@ -95,6 +103,10 @@ __device__ inline double semantic_error(const SemArgs& a, const double pc1[3], f
   world_to_image<M>(K2, u2, v2, &x2, &y2);
   const int px = cast_to_int_x86(round(x2));
   const int py = cast_to_int_x86(round(y2));
+  if (pxy_out) {
+    pxy_out[0] = px;
+    pxy_out[1] = py;
+  }
   if (px < 0 || px >= a.W || py < 0 || py >= a.H) {
     *status = MI_BA_OUT_OF_BOUNDS;
     return 0.0;
@@ -1482,6 +1494,52 @@ __global__ void semantic_model_kernel(const SemPair* __restrict__ pairs, int npa
   if ((threadIdx.x & 63) == 0) atomicAdd(out, v);
 }
 
+// ExportSemanticErrorToCSV (semantic_bundle_adjustment.cc:908-1019): every
+// pixel of image i's grid (y outer, x inner, step `step`; zero-depth pixels
+// included, unlike the problem's samples) evaluated against image j at the
+// current parameters by compute_semantic_error — status, error, the rounded
+// pixel in image j and the world point.  One lane per grid pixel.
+__global__ __launch_bounds__(kBlock) void semantic_export_kernel(SemArgs a, uint32_t i, uint32_t j, int step, int nx,
+                                                                  int64_t n, int32_t* __restrict__ pix,
+                                                                  int32_t* __restrict__ status,
+                                                                  double* __restrict__ err,
+                                                                  double* __restrict__ world) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= n) return;
+  const int x = (int)(k % nx) * step, y = (int)(k / nx) * step;
+  const uint32_t cam1 = a.img_cam[i], cam2 = a.img_cam[j];
+  const double* K1 = a.cam + 8 * (size_t)cam1;
+  const double* kc = a.cam + 8 * (size_t)cam2;
+  double K2[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) K2[m] = kc[m];
+  const float2 c1 = a.dl[(size_t)a.raster_slot[i] * a.H * a.W + (size_t)y * a.W + x];
+  double u1 = 0.0, v1 = 0.0;
+  image_to_world_any(a.cam_model[cam1], K1, (double)x, (double)y, &u1, &v1);
+  const double depth = (double)c1.x;
+  const double pc1[3] = {u1 * depth, v1 * depth, depth};
+  const double* qt1 = a.qt + 8 * (size_t)i;
+  const double* qt2 = a.qt + 8 * (size_t)j;
+  const double q1[4] = {qt1[0], qt1[1], qt1[2], qt1[3]}, t1[3] = {qt1[4], qt1[5], qt1[6]};
+  const double q2[4] = {qt2[0], qt2[1], qt2[2], qt2[3]}, t2[3] = {qt2[4], qt2[5], qt2[6]};
+  const float2* dl2 = a.dl + (size_t)a.raster_slot[j] * a.H * a.W;
+  int st = 0;
+  double r = 0.0, pw[3] = {0.0, 0.0, 0.0};
+  int pxy[2] = {0, 0};
+  switch_model(a.cam_model[cam2], [&](auto m) {
+    r = semantic_error<decltype(m)::value>(a, pc1, c1.y, q1, t1, q2, t2, K2, dl2, &st, pw, pxy);
+  });
+  pix[4 * k] = x;
+  pix[4 * k + 1] = y;
+  pix[4 * k + 2] = pxy[0];
+  pix[4 * k + 3] = pxy[1];
+  status[k] = st;
+  err[k] = r;
+  world[3 * k] = pw[0];
+  world[3 * k + 1] = pw[1];
+  world[3 * k + 2] = pw[2];
+}
+
 SemArgs make_args(mi_ba_context* ctx, const double* qt, const double* cam) {
   SemanticState* S = ctx->sem;
   SemArgs a;
@@ -1519,6 +1577,7 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
   S->W = sem->width;
   S->depth_threshold = sem->depth_error_threshold;
   S->rel_step = sem->numeric_relative_step_size;
+  S->step = sem->pixel_step;
   const int H = S->H, W = S->W, I = p->num_images;
   const HostSetup& hs = ctx->setup;
   auto const_pose = [&](int i) {
@@ -1610,6 +1669,8 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
   const size_t plane = (size_t)H * W;
   std::vector<uint32_t> slot_u(I, 0);
   for (int i = 0; i < I; ++i) slot_u[i] = slot[i] < 0 ? 0u : (uint32_t)slot[i];
+  S->has_raster.assign(I, 0);
+  for (int i = 0; i < I; ++i) S->has_raster[i] = slot[i] >= 0;
   // tiles grouped by the model of the pair's second camera (one launch per
   // model present; order within a model unchanged)
   {
@@ -1666,6 +1727,35 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
     if (hipMemcpy(S->dl.ptr + s * plane, buf.data(), plane * sizeof(float2), hipMemcpyHostToDevice))
       return MI_BA_ERR_HIP;
   }
+  return MI_BA_OK;
+}
+
+mi_ba_status semantic_export(mi_ba_context* ctx, int32_t image1, int32_t image2, int64_t* count, int32_t* pixels,
+                             int32_t* status, double* error, double* world) {
+  SemanticState* S = ctx->sem;
+  const int I = ctx->problem.num_images;
+  if (!S || !count || image1 < 0 || image1 >= I || image2 < 0 || image2 >= I || image1 == image2)
+    return MI_BA_ERR_INVALID_ARGUMENT;
+  const int nx = (S->W + S->step - 1) / S->step, ny = (S->H + S->step - 1) / S->step;
+  const int64_t n = (int64_t)nx * ny;
+  *count = n;
+  if (!pixels) return MI_BA_OK;
+  if (!status || !error || !world) return MI_BA_ERR_INVALID_ARGUMENT;
+  if (!S->has_raster[image1] || !S->has_raster[image2]) return MI_BA_ERR_UNSUPPORTED;
+  if (n == 0) return MI_BA_OK;
+  DevArray<int32_t> d_pix, d_st;
+  DevArray<double> d_err, d_w;
+  if (d_pix.alloc(4 * n) || d_st.alloc(n) || d_err.alloc(n) || d_w.alloc(3 * n)) return MI_BA_ERR_OUT_OF_MEMORY;
+  SemArgs a = make_args(ctx, ctx->dev.qt, ctx->dev.cam);
+  hipLaunchKernelGGL(semantic_export_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                     a, (uint32_t)image1, (uint32_t)image2, S->step, nx, n, d_pix.ptr, d_st.ptr, d_err.ptr, d_w.ptr);
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(pixels, d_pix.ptr, 16 * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      hipMemcpyAsync(status, d_st.ptr, 4 * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      hipMemcpyAsync(error, d_err.ptr, 8 * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      hipMemcpyAsync(world, d_w.ptr, 24 * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess)
+    return MI_BA_ERR_HIP;
   return MI_BA_OK;
 }
 

@@ -262,6 +262,7 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_context_dims.argtypes = [C.c_void_p, _i64p, _i32p, _i64p]
     lib.mi_ba_download_jacobian.argtypes = [C.c_void_p, _i64p, _dp, _dp]
     lib.mi_ba_download_semantic.argtypes = [C.c_void_p, _i32p, _i32p, _dp, _dp]
+    lib.mi_ba_semantic_export.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _i64p, _i32p, _i32p, _dp, _dp]
     lib.mi_ba_context_cost.argtypes = [C.c_void_p, _dp]
     lib.mi_ba_context_solve.argtypes = [C.c_void_p, C.POINTER(Summary)]
     lib.mi_ba_context_writeback.argtypes = [C.c_void_p]
@@ -819,6 +820,21 @@ class Context:
         check(self.lib.mi_ba_download_semantic(self.h, _ptr(px, _i32p), _ptr(st, _i32p), _ptr(r, _dp),
                                                _ptr(J, _dp)), "download_semantic")
         return px, st, r, J
+
+    def semantic_export(self, image1: int, image2: int):
+        """mi_ba_semantic_export: ExportSemanticErrorToCSV's rows of the ordered
+        image pair at the current parameters -> (pixels [n][4] (x1, y1, x2, y2),
+        status [n], error [n], world [n][3])."""
+        n = C.c_int64(0)
+        check(self.lib.mi_ba_semantic_export(self.h, image1, image2, C.byref(n), None, None, None, None),
+              "mi_ba_semantic_export")
+        pix = np.empty((n.value, 4), np.int32)
+        st = np.empty(n.value, np.int32)
+        err = np.empty(n.value, np.float64)
+        world = np.empty((n.value, 3), np.float64)
+        check(self.lib.mi_ba_semantic_export(self.h, image1, image2, C.byref(n), _ptr(pix, _i32p), _ptr(st, _i32p),
+                                             _ptr(err, _dp), _ptr(world, _dp)), "mi_ba_semantic_export")
+        return pix, st, err, world
 
     def solve(self) -> Summary:
         s = Summary()

@@ -8,6 +8,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
 #include <functional>
 #include <random>
 #include <string>
@@ -408,6 +411,110 @@ int main(int argc, char** argv) {
     CheckConstantImage(rec, orig, 0);
     for (camera_t c = 0; c < 3; ++c) CheckConstantCamera(rec, orig, c);
     for (auto& p : rec.points3D) CheckConstantPoint(rec, orig, p.first);
+  }});
+
+  // SBA outputs (SBACallbackFunctor, semantic_bundle_adjustment.cc:1086-1123;
+  // ExportSemanticErrorToCSV :908-1019; the final write :531-538): every
+  // iteration's step_k model equals the state the caller's callback saw at
+  // that iteration, the CSV files hold every grid pixel of every ordered pair
+  // and their errors sum to twice the iteration's cost (TRIVIAL loss, weight
+  // 1, no zero-depth pixel, every pair in the problem), the final model is
+  // written to output_path.
+  cases.push_back({"TestSemanticBundleAdjusterSnapshots", [](bool s) {
+    if (!s) return;
+    Reconstruction rec = GenerateReconstruction(3, 10);
+    const int H = 60, W = 60, step = 3;
+    SemanticMaps maps;
+    maps.height = H;
+    maps.width = W;
+    for (auto& e : rec.images) {
+      Image& im = e.second;
+      std::vector<float> depth((size_t)H * W), label((size_t)H * W);
+      for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+          const double d = im.tvec[2];
+          const double X = (x - 500.0 + 470.0) / 1200.0 * d - im.tvec[0];
+          const double Y = (y - 500.0 + 470.0) / 1200.0 * d - im.tvec[1];
+          depth[(size_t)y * W + x] = (float)d;
+          label[(size_t)y * W + x] = (float)((((int)std::floor(X / 0.05) + (int)std::floor(Y / 0.05)) % 2 + 2) % 2);
+        }
+      maps.depth[im.name] = depth;
+      maps.semantic[im.name] = label;
+      rec.GetCamera(im.camera_id).params = {1200, 30, 30, 0};
+      im.tvec[0] += 0.002 * (double)im.image_id;
+    }
+    char tmpl[] = "/tmp/sba_out_XXXXXX";
+    const char* dir = mkdtemp(tmpl);
+    CHECK_T(dir != nullptr);
+    if (!dir) return;
+    const std::string out(dir);
+    SemanticBundleAdjustmentOptions options;
+    options.print_summary = false;
+    options.error_computation_pixel_step = step;
+    options.output_path = out;
+    options.export_csv = true;
+    options.solver_options.max_num_iterations = 4;
+    SemanticBundleAdjustmentConfig config;
+    for (image_t i = 0; i < 3; ++i) config.AddImage(i);
+    config.SetConstantPose(0);
+    for (camera_t c = 0; c < 3; ++c) config.SetConstantCamera(c);
+    std::vector<Reconstruction> seen;
+    std::vector<double> costs;
+    struct Saver : IterationCallback {
+      std::function<void(const IterationSummary&)> fn;
+      CallbackReturnType operator()(const IterationSummary& it) override { fn(it); return SOLVER_CONTINUE; }
+    } saver;
+    saver.fn = [&](const IterationSummary& it) {
+      seen.push_back(rec);
+      costs.push_back(it.cost);
+    };
+    options.solver_options.callbacks.push_back(&saver);
+    SemanticBundleAdjuster sba(options, config, maps);
+    CHECK_T(sba.Solve(&rec));
+    CHECK_T(seen.size() >= 2);
+    const int grid = ((W + step - 1) / step) * ((H + step - 1) / step);
+    for (size_t k = 0; k < seen.size(); ++k) {
+      const std::string sd = out + "/run/optim_steps/step_" + std::to_string(k);
+      Reconstruction bin, txt;
+      ReadModelBinary(sd, &bin);
+      ReadModelText(sd + "/text", &txt);
+      for (const auto& e : seen[k].images) {
+        const Image& a = e.second;
+        const Image& b = bin.GetImage(e.first);
+        const Image& t = txt.GetImage(e.first);
+        for (int m = 0; m < 3; ++m) CHECK_T(b.tvec[m] == a.tvec[m] && t.tvec[m] == a.tvec[m]);
+        for (int m = 0; m < 4; ++m)
+          CHECK_T(std::fabs(b.qvec[m] - a.qvec[m]) <= 1e-15 && std::fabs(t.qvec[m] - a.qvec[m]) <= 1e-15);
+      }
+      long errors = 0;
+      for (image_t i = 0; i < 3; ++i)
+        for (image_t j = 0; j < 3; ++j) {
+          if (i == j) continue;
+          std::ifstream f(sd + "/vis_" + std::to_string(i) + "_to_" + std::to_string(j) + ".csv");
+          CHECK_T(f.is_open());
+          std::string line;
+          std::getline(f, line);
+          CHECK_T(line == "Type,SemanticError,X1,Y1,X2,Y2,X3D,Y3D,Z3D");
+          int rows = 0;
+          while (std::getline(f, line)) {
+            std::stringstream ls(line);
+            std::string type, err;
+            std::getline(ls, type, ',');
+            std::getline(ls, err, ',');
+            CHECK_T(type == "10" || type == "-1" || type == "-2");
+            CHECK_T(err == "0" || err == "1");
+            errors += err == "1";
+            ++rows;
+          }
+          CHECK_T(rows == grid);
+        }
+      CHECK_T(0.5 * (double)errors == costs[k]);
+    }
+    Reconstruction fin;
+    ReadModelBinary(out, &fin);
+    for (const auto& e : rec.images)
+      for (int m = 0; m < 3; ++m) CHECK_T(fin.GetImage(e.first).tvec[m] == e.second.tvec[m]);
+    if (std::system(("rm -rf '" + out + "'").c_str()) != 0) std::printf("  (could not remove %s)\n", out.c_str());
   }});
 
   // Reconstruction::FilterPoints3DWithLargeReprojectionError

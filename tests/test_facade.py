@@ -29,13 +29,13 @@ def run(mode, name="bundle_adjustment_test"):
 
 def test_facade_counts_cpu():
     out = run("counts")
-    assert out.count("PASS") == 15
+    assert out.count("PASS") == 16
 
 
 @pytest.mark.gpu
 def test_facade_solve_gpu(gpu):
     out = run("solve")
-    assert out.count("PASS") == 15
+    assert out.count("PASS") == 16
 
 
 def test_controllers_host():

@@ -4,7 +4,7 @@ set -o pipefail
 T=${1:-r4a}
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_comm.py > gpurun_out/$T/comm_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu ${TESTS:-tests/test_comm.py} > gpurun_out/$T/comm_tests.log 2>&1
 rc=$?; echo "comm tests rc $rc"
 tail -3 gpurun_out/$T/comm_tests.log
 # test failures (1) do not stop the session; a crash, abort or timeout does
