@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256) void trsv_bwd_pair_kernel(const double* __rest
 // Workgroups only ever wait for lower-numbered ones (flag = epoch of this
 // launch, release/acquire at agent scope, as the sweeps above).
 typedef double pf_dvec4 __attribute__((ext_vector_type(4)));
-constexpr int kPfMaxTiles = 8;  // column tiles per panel (panel <= 512)
+constexpr int kPfMaxTiles = 16;  // column tiles per panel (panel <= 1024)
 [[maybe_unused]] constexpr int kTinv = 512;  // own_diag 7: widest panel
 
 __device__ __forceinline__ int pf_row0(int r, int kb, int nc) { return r < nc ? 64 * r : kb + 64 * (r - nc); }
@@ -913,7 +913,7 @@ __device__ __forceinline__ int pf_chol_inv_fast(double* M, double* X, double* sc
 // 1 + 2c after step c's waits (diagonal step: after the factor), 2 + 2c at
 // step c's end; diagonal rows' last solve step (c = r - 1): 17 inverse staged,
 // 18 solve GEMM done, 19 SYRK done and published.
-constexpr int kPfDbgSlots = 20;
+constexpr int kPfDbgSlots = 36;
 
 // Tile staging global -> LDS S[i * kPfLd + j] with every load of the tile
 // in flight before the first LDS store (16 per thread, 256 threads): a
@@ -989,7 +989,7 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
   __syncthreads();
   const int r = s_r;
   const int nc = (kb + 63) / 64;
-  unsigned* flag = ctrl + 1;  // [8][8]: tile (r, c) of the diagonal block rows final in A
+  unsigned* flag = ctrl + 1;  // [16][16]: tile (r, c) of the diagonal block rows final in A
   auto stamp = [&](int slot) {
     if (dbg && threadIdx.x == 0) dbg[(size_t)r * kPfDbgSlots + slot] = wall_clock64();
   };
@@ -1278,8 +1278,9 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
                               double* scratch, CholWorkspace* ws, int ex) {
   const double one = 1.0, minus_one = -1.0;
   const int nb = cfg.panel;
-  for (int k = 0; k < n; k += nb) {
-    const int kb = std::min(nb, n - k);
+  const std::vector<int> ps = chol_panel_starts(n, cfg);
+  for (size_t pk = 0; pk + 1 < ps.size(); ++pk) {
+    const int k = ps[pk], kb = ps[pk + 1] - k;
     double* Akk = A + k + (size_t)k * lda;
     rocblas_status st = panel_factor(h, n, A, lda, k, kb, info++, cfg.own_diag, scratch, ws, ex);
     if (st != rocblas_status_success) return st;
@@ -1299,7 +1300,7 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
       // the look-ahead's partition and GEMM solution (block column k+1, then
       // columns of width nb or 2 nb): both orders run the same GEMMs on the
       // same shapes, so their factors are bitwise equal
-      const int jb0 = std::min(nb, m);
+      const int jb0 = ps[pk + 2] - ps[pk + 1];  // the next panel's width
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
       for (int j = 0; j < m; j = j == 0 ? jb0 : j + cw) {
         const int jb = std::min(j == 0 ? jb0 : cw, m - j);
@@ -1447,10 +1448,11 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
   const int nb = cfg.panel;
   hipStream_t s1;
   if (rocblas_get_stream(h, &s1) != rocblas_status_success) return rocblas_status_internal_error;
-  if (ws.ev.size() < 2 * (size_t)((n + nb - 1) / nb)) return rocblas_status_invalid_size;
+  const std::vector<int> ps = chol_panel_starts(n, cfg);
+  if (ws.ev.size() < 2 * (ps.size() - 1)) return rocblas_status_invalid_size;
   double* scratch_main = ws.scratch;
   double* scratch_side = ws.scratch + kSub * kSub;
-  rocblas_status st = panel_factor(h, n, A, lda, 0, std::min(nb, n), info, cfg.own_diag, scratch_main, &ws, ex);
+  rocblas_status st = panel_factor(h, n, A, lda, 0, ps[1], info, cfg.own_diag, scratch_main, &ws, ex);
   if (st != rocblas_status_success) return st;
   // On a failure after the side stream got work, the caller's stream waits
   // for it (the caller may free A / info once its own stream is drained).
@@ -1460,14 +1462,14 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       (void)hipStreamSynchronize(ws.side);
     return e;
   };
-  for (int k = 0, kk = 0; k < n; k += nb, ++kk) {
-    const int kb = std::min(nb, n - k);
+  for (int kk = 0; kk + 1 < (int)ps.size(); ++kk) {
+    const int k = ps[kk], kb = ps[kk + 1] - k;
     const int m = n - k - kb;
     if (m == 0) break;
     double* Aik = A + k + kb + (size_t)k * lda;  // panel k below its diagonal block
     double* T = Aik + (size_t)kb * lda;          // trailing matrix, lower triangle
-    // block column k+1 first
-    const int jb0 = std::min(nb, m);
+    // block column k+1 (the next panel) first
+    const int jb0 = ps[kk + 2] - ps[kk + 1];
     st = gemm_nt(h, m + ex, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
     if (st != rocblas_status_success) return fail(st);
     hipEvent_t upd = ws.ev[2 * kk], pan = ws.ev[2 * kk + 1];
@@ -1506,9 +1508,22 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
 
 }  // namespace
 
+std::vector<int> chol_panel_starts(int n, const CholConfig& cfg) {
+  std::vector<int> ps;
+  for (int k = 0; k < n;) {
+    ps.push_back(k);
+    int w = cfg.panel;
+    if (cfg.tail_panel > 0 && n - k <= cfg.tail_cols) w = cfg.tail_panel;
+    else if (cfg.head_panel > 0 && k < cfg.head_cols) w = cfg.head_panel;
+    k += std::min(std::max(w, 1), n - k);
+  }
+  ps.push_back(n);
+  return ps;
+}
+
 int chol_leaf_count(int n, const CholConfig& cfg) {
   if (n <= 0) return 1;
-  return cfg.panel > 0 ? (n + cfg.panel - 1) / cfg.panel : leaves(n);
+  return cfg.panel > 0 ? (int)chol_panel_starts(n, cfg).size() - 1 : leaves(n);
 }
 
 bool CholWorkspace::create(int dev, int max_panels, int max_n) {
@@ -1643,7 +1658,8 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   // the one-launch panel factor needs panels of at most 8 tiles: other panel
   // widths (and the recursive split) take the two-kernel diagonal factor
   CholConfig c = cfg;
-  if (c.own_diag == 6 && (c.panel <= 0 || c.panel > 64 * kPfMaxTiles)) c.own_diag = 2;
+  const int widest = std::max({c.panel, c.head_panel, c.tail_panel});
+  if (c.own_diag == 6 && (c.panel <= 0 || widest > 64 * kPfMaxTiles)) c.own_diag = 2;
 #ifdef MI_BA_AB_VARIANTS
   if (c.own_diag == 7 && (c.panel <= 0 || c.panel > kTinv)) c.own_diag = 2;
 #else

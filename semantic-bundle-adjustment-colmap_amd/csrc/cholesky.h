@@ -24,6 +24,11 @@ namespace miba {
 // chol_variants.txt).
 struct CholConfig {
   int panel = 512;        // 0: recursive split; > 0: right-looking panel width
+  // non-uniform panel schedule (chol_panel_starts): panels of head_panel
+  // columns while the panel starts before column head_cols, of tail_panel
+  // columns once at most tail_cols columns remain; 0 = off
+  int head_panel = 0, head_cols = 0;
+  int tail_panel = 0, tail_cols = 0;
   // look-ahead side stream confined to this many CUs (spread over the chip)
   // so the panel factor's waiting workgroups leave the rest to the trailing
   // dgemm; 0: all CUs at high priority (tools build: cholesky_panel_cus)
@@ -149,6 +154,8 @@ struct CholWorkspace {
 rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
                            CholWorkspace* ws, int extra_rows = 0);
 int chol_leaf_count(int n, const CholConfig& cfg = {});
+// First column of every panel of the right-looking factorisation, then n.
+std::vector<int> chol_panel_starts(int n, const CholConfig& cfg);
 // x := (L L')^-1 x with the factor chol_factor left in A, on h's stream.
 // variant 2 (default): sync-free forward / backward sweeps, one launch each
 // (per-block solution flags in ws); 1: one launch per 64-wide block column,

@@ -1905,6 +1905,12 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->sem_diag = value;
     return MI_BA_OK;
   }
+  // the flat pass decides samples from 3x3 window summaries of the rasters
+  // (16 B per raster pixel more HBM) before reading the raster
+  if (std::strcmp(key, "semantic_window_summary") == 0 && (value == 0 || value == 1)) {
+    if (!ctx->sem) return value ? MI_BA_ERR_STATE : MI_BA_OK;
+    return semantic_set_window_summary(ctx, value != 0);
+  }
   if (std::strcmp(key, "semantic_variant") == 0 && value >= 0 && value <= 6 && ab_value(value, 6)) {
     ctx->sem_variant = value;
     return MI_BA_OK;
@@ -1924,6 +1930,23 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   }
   if (std::strcmp(key, "cholesky_panel") == 0 && (value == 0 || (value >= 64 && value <= 4096))) {
     ctx->chol.panel = value;
+    return MI_BA_OK;
+  }
+  // non-uniform panel schedule (CholConfig::head_panel / tail_panel)
+  if (std::strcmp(key, "cholesky_head_panel") == 0 && (value == 0 || (value >= 64 && value <= 1024))) {
+    ctx->chol.head_panel = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_head_cols") == 0 && value >= 0) {
+    ctx->chol.head_cols = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_tail_panel") == 0 && (value == 0 || (value >= 64 && value <= 1024))) {
+    ctx->chol.tail_panel = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_tail_cols") == 0 && value >= 0) {
+    ctx->chol.tail_cols = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_lookahead") == 0 && (value == 0 || value == 1)) {

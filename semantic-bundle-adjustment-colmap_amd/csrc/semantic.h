@@ -46,6 +46,9 @@ struct SemanticState {
   DevArray<SemSample> samples;
   DevArray<SemPair> pairs;
   DevArray<float2> dl;                     // [slot][H][W] (depth, label) of images used as j
+  int nslots = 0;
+  DevArray<float4> wsum;                   // [slot][H][W] 3x3 window summaries ("semantic_window_summary")
+  bool use_wsum = false;
   DevArray<uint32_t> raster_slot;          // image -> raster slot
   DevArray<double> r;                      // [ns]
   DevArray<int32_t> status;                // [ns]
@@ -83,6 +86,9 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
 // the current parameters (mi_ba_semantic_export).
 mi_ba_status semantic_export(mi_ba_context* ctx, int32_t image1, int32_t image2, int64_t* count, int32_t* pixels,
                              int32_t* status, double* error, double* world);
+// Build (on) or drop (off) the rasters' 3x3 window summaries the flat pass
+// decides most samples from without reading the raster.
+mi_ba_status semantic_set_window_summary(mi_ba_context* ctx, bool on);
 // Cost only, at parameters qt (candidate evaluation).
 void semantic_cost(mi_ba_context* ctx, const double* qt, const double* cam, double* d_cost);
 // Fold the pair blocks into the Schur-Jacobi pose blocks, b and diag(U).

@@ -38,6 +38,7 @@ struct SemArgs {
   const uint32_t* img_flags;
   const uint32_t* raster_slot;
   const float2* dl;   // interleaved (depth, label) rasters [slot][H][W]
+  const float4* wsum; // 3x3 window summaries [slot][H][W] (window_summary_kernel) or null
   int H, W;
   double threshold;
   double rel_step;
@@ -1195,7 +1196,66 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
 // pair table), and reduces their J'J / J'r into the pair block — dense
 // waves, unlike in-tile compaction, which leaves most waves of a tile idle.
 // ---------------------------------------------------------------------------
-template <int M, bool FAST>
+// The 3x3 window summary of pixel p (window_summary_kernel): the window with
+// top-left corner p = (x, y), inside the raster, every label == the first
+// (not NaN): {min depth, max depth, label, 0}; any other window: dmin = NaN.
+// It decides a sample of the flat pass alone (no centre or box read) when the
+// window holding the sample's box lies on one side of the depth test with
+// the flat test's margin for every depth in it: then every box pixel, the
+// centre pixel among them, has the outcome the window's label (valid side)
+// or INVALID_DEPTH (invalid side) gives, exactly as flat_check and the centre
+// evaluation would find pixel by pixel (fabs(s - z) is monotone in s, and the
+// margin 1e-9 (1 + |s| + mag) in |s|).  Undecided samples read the raster.
+__device__ __forceinline__ bool window_decides(const SemArgs& a, const FlatBox& fb, const float4& w, double z,
+                                               double mag, float label1, int* st, double* r) {
+  const double dmin = (double)w.x, dmax = (double)w.y;
+  if (!(dmin <= dmax)) return false;  // NaN: a mixed-label or edge window
+  const double margin = fb.d + 1e-9 * (1.0 + fmax(fabs(dmin), fabs(dmax)) + mag);
+  const double far = fmax(fabs(dmax - z), fabs(dmin - z));
+  const double dzmax = far - a.threshold;
+  if (dzmax < 0.0 && -dzmax > margin) {
+    *st = MI_BA_VALID;
+    *r = (label1 == w.z) ? 0.0 : 1.0;
+    return true;
+  }
+  const double nearest = (z >= dmin && z <= dmax) ? 0.0 : fmin(fabs(dmin - z), fabs(dmax - z));
+  const double dzmin = nearest - a.threshold;
+  if (dzmin > 0.0 && dzmin > margin) {
+    *st = MI_BA_INVALID_DEPTH;
+    *r = 0.0;
+    return true;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void window_summary_kernel(const float2* __restrict__ dl, int H, int W,
+                                                             int64_t n, float4* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  const int64_t plane = (int64_t)H * W;
+  const int64_t slot = k / plane;
+  const int rem = (int)(k - slot * plane);
+  const int y = rem / W, x = rem - y * W;
+  float4 o = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
+  if (x + 2 < W && y + 2 < H) {
+    const float2* base = dl + slot * plane + (int64_t)y * W + x;
+    const float L = base[0].y;
+    float dmin = base[0].x, dmax = base[0].x;
+    bool uniform = true;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const float2 v = base[(q / 3) * W + q % 3];
+      uniform = uniform && (v.y == L);
+      dmin = fminf(dmin, v.x);
+      dmax = fmaxf(dmax, v.x);
+      if (v.x != v.x) uniform = false;  // NaN depth: the pixel test is left to the raster
+    }
+    if (uniform) o = make_float4(dmin, dmax, L, 0.f);
+  }
+  out[k] = o;
+}
+
+template <int M, bool FAST, bool WS = false>
 __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const SemTile* __restrict__ tiles,
                                                                const PairConst* __restrict__ pcs,
                                                                uint32_t* __restrict__ pair_cnt,
@@ -1243,23 +1303,33 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
     const bool cin = !(cpx < 0 || cpx >= a.W || cpy < 0 || cpy >= a.H);
     FlatBox fb;
     const bool cand = flat_box<M>(P, c, K2, fb);
-    // every raster read of the sample in one round trip: the centre pixel and the box
-    const float2 sc = dl2[cin ? cpy * a.W + cpx : 0];
-    float2 s[9];
-#pragma unroll
-    for (int q = 0; q < 9; ++q) s[q] = dl2[flat_index(a, fb, cand, q)];
-    // centre outcome (semantic_cost_functions.h:141-205)
-    if (!cin) {
-      c.st = MI_BA_OUT_OF_BOUNDS;
-      c.r = 0.0;
-    } else if (fabs((double)sc.x - c.p2[2]) > a.threshold) {
-      c.st = MI_BA_INVALID_DEPTH;
-      c.r = 0.0;
-    } else {
-      c.st = MI_BA_VALID;
-      c.r = (smp.label1 == sc.y) ? 0.0 : 1.0;
+    bool decided = false;
+    if constexpr (WS) {
+      // one 16-B read of the window holding the box (its top-left pixel)
+      if (cand && fb.x0 >= 0 && fb.y0 >= 0 && fb.x0 + 2 < a.W && fb.y0 + 2 < a.H) {
+        const float4 w = a.wsum[(size_t)P->slot * a.H * a.W + (size_t)fb.y0 * a.W + fb.x0];
+        decided = window_decides(a, fb, w, c.p2[2], c.mag, smp.label1, &c.st, &c.r);
+      }
     }
-    deferred = !(cand && flat_check(a, fb, s, c.p2[2], c.mag, smp.label1, c.r));
+    if (!decided) {
+      // every raster read of the sample in one round trip: the centre pixel and the box
+      const float2 sc = dl2[cin ? cpy * a.W + cpx : 0];
+      float2 s[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) s[q] = dl2[flat_index(a, fb, cand, q)];
+      // centre outcome (semantic_cost_functions.h:141-205)
+      if (!cin) {
+        c.st = MI_BA_OUT_OF_BOUNDS;
+        c.r = 0.0;
+      } else if (fabs((double)sc.x - c.p2[2]) > a.threshold) {
+        c.st = MI_BA_INVALID_DEPTH;
+        c.r = 0.0;
+      } else {
+        c.st = MI_BA_VALID;
+        c.r = (smp.label1 == sc.y) ? 0.0 : 1.0;
+      }
+      deferred = !(cand && flat_check(a, fb, s, c.p2[2], c.mag, smp.label1, c.r));
+    }
     double rho[3];
     loss_eval(a.loss_type, a.loss_scale, c.r * c.r, rho);
     cost = 0.5 * (a.weight * rho[0]);
@@ -1552,6 +1622,7 @@ SemArgs make_args(mi_ba_context* ctx, const double* qt, const double* cam) {
   a.img_flags = ctx->dev.img_flags;
   a.raster_slot = S->raster_slot.ptr;
   a.dl = S->dl.ptr;
+  a.wsum = S->use_wsum ? S->wsum.ptr : nullptr;
   a.H = S->H;
   a.W = S->W;
   a.threshold = S->depth_threshold;
@@ -1669,6 +1740,7 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
   const size_t plane = (size_t)H * W;
   std::vector<uint32_t> slot_u(I, 0);
   for (int i = 0; i < I; ++i) slot_u[i] = slot[i] < 0 ? 0u : (uint32_t)slot[i];
+  S->nslots = (int)slot_images.size();
   S->has_raster.assign(I, 0);
   for (int i = 0; i < I; ++i) S->has_raster[i] = slot[i] >= 0;
   // tiles grouped by the model of the pair's second camera (one launch per
@@ -1759,6 +1831,23 @@ mi_ba_status semantic_export(mi_ba_context* ctx, int32_t image1, int32_t image2,
   return MI_BA_OK;
 }
 
+mi_ba_status semantic_set_window_summary(mi_ba_context* ctx, bool on) {
+  SemanticState* S = ctx->sem;
+  if (!S) return MI_BA_ERR_STATE;
+  if (on && !S->wsum.ptr) {
+    const int64_t n = (int64_t)S->nslots * S->H * S->W;
+    if (n > 0) {
+      if (S->wsum.alloc((size_t)n)) return MI_BA_ERR_OUT_OF_MEMORY;
+      hipLaunchKernelGGL(window_summary_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, S->dl.ptr,
+                         S->H, S->W, n, S->wsum.ptr);
+      if (hipGetLastError() != hipSuccess) return MI_BA_ERR_HIP;
+    }
+  }
+  if (!on) S->wsum.release();
+  S->use_wsum = on && S->wsum.ptr != nullptr;
+  return MI_BA_OK;
+}
+
 void semantic_destroy(mi_ba_context* ctx) {
   if (!ctx->sem) return;
   delete ctx->sem;
@@ -1805,9 +1894,14 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
       if (nt == 0) continue;
       dispatch_model(model, [&](auto m) {
         constexpr int M = decltype(m)::value;
-        hipLaunchKernelGGL((semantic_flat_kernel<M, true>), dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0, pcs,
-                           S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr,
-                           ws);
+        if (a.wsum)
+          hipLaunchKernelGGL((semantic_flat_kernel<M, true, true>), dim3(nt), dim3(kBlock), 0, s, a,
+                             S->tiles.ptr + t0, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr,
+                             S->status.ptr, S->J.ptr, ws);
+        else
+          hipLaunchKernelGGL((semantic_flat_kernel<M, true>), dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0,
+                             pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr,
+                             S->J.ptr, ws);
       });
     }
     if (split) {

@@ -315,3 +315,26 @@ def test_lm_fused_forward_solve(gpu, images):
     assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
     assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
     assert a.final_cost < a.initial_cost
+
+
+@pytest.mark.parametrize("schedule", [dict(head_panel=1024, head_cols=1024), dict(tail_panel=256, tail_cols=768),
+                                      dict(head_panel=768, head_cols=700, tail_panel=128, tail_cols=300)])
+def test_lm_panel_schedule(gpu, schedule):
+    """Non-uniform panel schedules (cholesky_head_panel / _head_cols /
+    _tail_panel / _tail_cols: 1024-wide one-launch panels of 16 column tiles,
+    narrower ones at the end) drive the same LM as the uniform 512-wide
+    panels (nf = 1593), with and without the look-ahead (S itself differs
+    between runs in the order of the Schur build's float atomics)."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for keys in ({}, schedule, dict(schedule, lookahead=0)):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            for k, v in keys.items():
+                ctx.set_tuning("cholesky_" + k, v)
+            res.append(ctx.solve())
+    b = res[0]
+    for a in res[1:]:
+        assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
+        assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost

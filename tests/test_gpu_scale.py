@@ -221,3 +221,25 @@ def test_c4_lm_first_iteration_matches_oracle(gpu):
     for name, x0 in (("qvec", q0), ("tvec", sc.tvec), ("xyz", sc.xyz), ("camera_params", sc.camera_params)):
         dg, do = getattr(g, name) - x0, getattr(o, name) - x0
         assert np.abs(dg - do).max() <= 1e-6 * max(np.abs(do).max(), 1e-300), name
+
+
+def test_c3_window_summary_flat_pass_bitwise(gpu):
+    """The flat pass deciding samples from the rasters' 3x3 window summaries
+    (semantic_window_summary 1) against the raster-only flat pass at C3 size
+    (4.0M samples): status, residual and Jacobian of every sample bitwise,
+    and the same samples deferred to the full stencil."""
+    sc = c2_scene()
+    sem = semantic_input(sc, step=10, pairs_per_image=2)
+    sc.tvec[5:] += 0.002  # pose errors: some samples change label between pixels
+    out = []
+    with mi_ba.Context(mi_ba.default_options(), sc.copy(), sem) as ctx:
+        ctx.set_tuning("semantic_diag", 1)
+        for ws in (0, 1, 0):
+            ctx.set_tuning("semantic_window_summary", ws)
+            ctx.evaluate_semantic()
+            out.append(ctx.download_semantic())
+    for o in out[1:]:
+        for a, b in zip(out[0], o):
+            assert np.array_equal(a, b)
+    st = out[0][1]
+    assert (st & 0x1000).sum() > 0 and ((st & ~0x1000) == mi_ba.VALID).mean() > 0.5

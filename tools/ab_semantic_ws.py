@@ -1,0 +1,61 @@
+"""The flat pass with and without the rasters' 3x3 window summaries
+("semantic_window_summary") inside the C4 linearization step (as bench.py):
+semantic / reprojection kernel times (HIP events) and step wall time over
+interleaved rounds; samples checked bitwise against the raster-only route.
+    python tools/ab_semantic_ws.py [--rounds 6] [--reps 10]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "semantic-bundle-adjustment-colmap_amd"))
+sys.path.insert(0, ROOT)
+import mi_ba  # noqa: E402
+import bench  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rounds", type=int, default=6)
+ap.add_argument("--reps", type=int, default=10)
+args = ap.parse_args()
+sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
+ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
+ref = None
+for ws in (0, 1):
+    ctx.set_tuning("semantic_window_summary", ws)
+    ctx.set_tuning("semantic_diag", 1)
+    ctx.evaluate_semantic()
+    out = ctx.download_semantic()
+    ctx.set_tuning("semantic_diag", 0)
+    if ref is None:
+        ref = out
+    same = all(np.array_equal(a, b) for a, b in zip(ref[1:], out[1:]))
+    print(json.dumps({"window_summary": ws, "bitwise_equal_incl_deferral": bool(same),
+                      "deferred": int((out[1] >= 0x800).sum())}), flush=True)
+res = {0: [], 1: []}
+for rnd in range(args.rounds):
+    for ws in (0, 1):
+        ctx.set_tuning("semantic_window_summary", ws)
+        for _ in range(3):
+            ctx.linearize()
+        ctx.synchronize()
+        ctx.set_timing(True)
+        ctx.reset_kernel_times()
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            ctx.linearize()
+        ctx.synchronize()
+        wall = (time.perf_counter() - t0) / args.reps * 1e3
+        sj = ctx.kernel_time("semantic_jacobian")
+        rj = ctx.kernel_time("reproj_jacobian")
+        ctx.set_timing(False)
+        res[ws].append((sj[0] / sj[1], rj[0] / rj[1], wall))
+for ws in (0, 1):
+    a = np.array(res[ws])
+    print(json.dumps({"window_summary": ws, "semantic_ms_median": float(np.median(a[:, 0])),
+                      "reproj_ms_median": float(np.median(a[:, 1])), "step_wall_ms_median": float(np.median(a[:, 2])),
+                      "rounds": args.rounds, "reps": args.reps}), flush=True)
+ctx.close()
