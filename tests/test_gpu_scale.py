@@ -242,4 +242,5 @@ def test_c3_window_summary_flat_pass_bitwise(gpu):
         for a, b in zip(out[0], o):
             assert np.array_equal(a, b)
     st = out[0][1]
-    assert (st & 0x1000).sum() > 0 and ((st & ~0x1000) == mi_ba.VALID).mean() > 0.5
+    deferred = st >= 0x800  # semantic_diag: deferred samples' status offset by +0x1000
+    assert deferred.sum() > 0 and (np.where(deferred, st - 0x1000, st) == mi_ba.VALID).mean() > 0.5
