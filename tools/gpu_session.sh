@@ -1,15 +1,45 @@
 #!/bin/bash
-# One GPU session of measurements / tests; steps chained, each under its own limit.
+# One GPU session: the named stages in order, each under its own time limit;
+# a test failure (pytest rc 1) does not stop the session, any crash, abort or
+# timeout does.  Output under gpurun_out/<tag>/.
+#   bash tools/gpu_session.sh <tag> <stage> [<stage> ...]
+# stages: tests (TESTS="..." files, default the whole -m gpu suite), jac (the
+# reproj_jacobian roofline decomposition in-step and back-to-back), ws (flat
+# pass window summaries A/B), chol (panel schedules A/B; CHOL="k=v,k=v ..."),
+# trace (rocprofv3 kernel trace of the bench command), bench (the bench line),
+# smoke
 set -o pipefail
-T=${1:-r4a}
+T=${1:?tag}
+shift
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu ${TESTS:-tests/test_comm.py} > gpurun_out/$T/comm_tests.log 2>&1
-rc=$?; echo "comm tests rc $rc"
-tail -3 gpurun_out/$T/comm_tests.log
-# test failures (1) do not stop the session; a crash, abort or timeout does
-[ $rc -le 1 ] || exit 1
-timeout -k 10 300 python -u tools/ab_jacobian.py --step --variants 0,11,12 --rounds 5 --reps 5 > gpurun_out/$T/ab_step.jsonl 2> gpurun_out/$T/ab_step.err || exit 1
-timeout -k 10 300 python -u tools/ab_jacobian.py --variants 0,11,12 --rounds 5 --reps 5 > gpurun_out/$T/ab_b2b.jsonl 2> gpurun_out/$T/ab_b2b.err || exit 1
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/bench_trace -o run -- python3 bench.py --lm-iters 0 --no-cpu-baseline > gpurun_out/$T/bench_trace.log 2>&1 || exit 1
-echo done
+for stage in "$@"; do
+  echo "== $stage $(date +%T)"
+  case $stage in
+    tests)
+      timeout -k 10 ${TESTS_TIMEOUT:-900} python -u -m pytest -x -v --timeout 400 --timeout-method thread -m gpu ${TESTS:-tests} > gpurun_out/$T/tests.log 2>&1
+      rc=$?; echo "tests rc $rc"; tail -3 gpurun_out/$T/tests.log
+      [ $rc -le 1 ] || exit 1 ;;
+    jac)
+      timeout -k 10 300 python -u tools/ab_jacobian.py --step --variants 0,11,12 --rounds 5 --reps 5 > gpurun_out/$T/ab_jac_step.jsonl 2> gpurun_out/$T/ab_jac_step.err || exit 1
+      timeout -k 10 300 python -u tools/ab_jacobian.py --variants 0,11,12 --rounds 5 --reps 5 > gpurun_out/$T/ab_jac_b2b.jsonl 2> gpurun_out/$T/ab_jac_b2b.err || exit 1
+      cat gpurun_out/$T/ab_jac_step.jsonl ;;
+    ws)
+      timeout -k 10 300 python -u tools/ab_semantic_ws.py > gpurun_out/$T/ab_ws.jsonl 2> gpurun_out/$T/ab_ws.err || exit 1
+      cat gpurun_out/$T/ab_ws.jsonl ;;
+    chol)
+      timeout -k 10 600 python -u tools/ab_chol_keys.py "" $CHOL > gpurun_out/$T/ab_chol.jsonl 2> gpurun_out/$T/ab_chol.err || exit 1
+      cat gpurun_out/$T/ab_chol.jsonl ;;
+    trace)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/bench_trace -o run -- python3 bench.py --lm-iters 0 --no-cpu-baseline > gpurun_out/$T/bench_trace.log 2>&1 || exit 1
+      tail -c 300 gpurun_out/$T/bench_trace.log ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
+      tail -c 300 gpurun_out/$T/bench.json ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 || { tail -5 gpurun_out/$T/smoke.log; exit 1; }
+      tail -1 gpurun_out/$T/smoke.log ;;
+    *) echo "unknown stage $stage"; exit 2 ;;
+  esac
+done
+echo "session done $(date +%T)"
