@@ -131,6 +131,13 @@ struct mi_ba_context {
   miba::DevArray<int32_t> info;
   miba::CholConfig chol;                   // factorisation variant (mi_ba_set_tuning)
   bool fused_rhs = true;                   // forward solve carried through the factorisation (S's spare row)
+  // PCG product matrix-free ("pcg_matrix_free"): both passes recompute the
+  // blocks' Jacobian rows (no Jcm copy, no J read per product); Xcm / obs_cm
+  // the camera-major copies of the blocks' points / observations
+  bool pcg_mf = false;
+  miba::DevArray<double> Xcm;
+  miba::DevArray<double2> obs_cm;
+  bool xcm_stale = true;
   int pcg_jcm = 2;  // PCG camera-side passes on the camera-major J copy, f pass staged through LDS (1: per-lane rows, 0: row gathers; tools build)
   bool pn_chunks = true;  // point blocks (V_p, g_p) on the point chunks (0: one lane per point, tools build)
   bool pp_chunks = true;                   // PCG Schur product's point pass on the point chunks (0: per point, tools build)

@@ -80,7 +80,14 @@ void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, 
                           int ntiles, const uint32_t* cm_perm, const double* J, const double* Vinv,
                           const double* lambda_f, const double* x, double* w, double* y, hipStream_t s,
                           const uint32_t* chunks = nullptr, int nchunks = 0, const uint32_t* cm_ptv = nullptr,
-                          const double* Jcm = nullptr, bool staged = false);
+                          const double* Jcm = nullptr, bool staged = false, const double* Xcm = nullptr,
+                          const double2* obs_cm = nullptr);
+// Matrix-free product (Xcm non-null, with chunks and cm_ptv): both passes
+// recompute the blocks' Jacobian rows instead of reading J; Xcm / obs_cm are
+// the camera-major copies of the blocks' points / observations (obs_cm only
+// with a robust loss) built by launch_gather_cm.
+void launch_gather_cm(const DevProblem& p, const uint32_t* cm_perm, int64_t n, double* Xcm, double2* obs_cm,
+                      hipStream_t s);
 
 // Block-Jacobi preconditioner apply z = M^-1 r.
 void launch_precond(const DevProblem& p, const double* prec_pose, const double* prec_cam,

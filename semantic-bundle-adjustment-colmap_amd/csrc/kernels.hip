@@ -1660,6 +1660,267 @@ __global__ __launch_bounds__(kBlock) void schur_f_rows_kernel(DevProblem p, cons
   }
 }
 
+// ---------------------------------------------------------------------------
+// Matrix-free implicit Schur product (PCG path, "pcg_matrix_free").  The two
+// passes of y = S x recompute each block's tangent Jacobian rows from the
+// block's inputs — the point (24 B, point-major / camera-major copy), the
+// image record (L2-resident), the CG vector — instead of reading the 2 (9+c)
+// stored doubles (240 B at OPENCV) twice per product: the rows are the
+// production reproj_jacobian_kernel arithmetic (R X through the rotation
+// matrix, closed-form rotation columns for a unit q, Dq * PlusJacobian
+// otherwise, the Corrector's sqrt(rho') with a robust loss; the model and
+// its refined-intrinsics mask from the image record at run time).
+// ---------------------------------------------------------------------------
+template <int CT, int LOSS>
+__device__ inline void block_rows_mf(const DevProblem& p, const double* q, const double* t, const double* prm,
+                                     uint32_t meta, const double* X, bool ptv, double2 o, double (&Jr)[2][9 + CT]) {
+  const uint32_t flags = meta & 0xffu;
+  const bool pose_var = flags & 1u;
+  const bool cv = (meta >> 8) & 1u;
+  const int model = (int)((meta >> 16) & 0xffu);
+  double Rm[9];
+  unit_quat_matrix(q, Rm);
+  double P[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) P[c] = Rm[3 * c] * X[0] + Rm[3 * c + 1] * X[1] + Rm[3 * c + 2] * X[2];
+  const double a0 = P[0], a1 = P[1], a2 = P[2];  // R X
+  P[0] += t[0];
+  P[1] += t[1];
+  P[2] += t[2];
+  const double iz = 1.0 / P[2];
+  const double u = P[0] * iz, v = P[1] * iz;
+  double x, y, A[4], Jp[16];
+  world_to_image_jac_any(model, prm, u, v, &x, &y, A, Jp);
+  const unsigned cmask = cam_tangent_mask(model, p.refine_mask);
+  double sc = 1.0;
+  if constexpr (LOSS != 0) {
+    const double r0 = x - o.x, r1 = y - o.y;
+    double rho[3];
+    loss_eval(p.loss_type, p.loss_scale, r0 * r0 + r1 * r1, rho);
+    sc = sqrt(rho[1]);
+  }
+  double B[6] = {A[0] * iz, A[1] * iz, -(A[0] * u + A[1] * v) * iz,
+                 A[2] * iz, A[3] * iz, -(A[2] * u + A[3] * v) * iz};
+  if constexpr (LOSS != 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) B[k] *= sc;
+  }
+  double Mq[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const bool unit_q = fabs(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3] - 1.0) <= 1e-12;
+  if (pose_var && unit_q) {
+    Mq[1] = 2.0 * a2;  Mq[2] = -2.0 * a1;
+    Mq[3] = -2.0 * a2; Mq[5] = 2.0 * a0;
+    Mq[6] = 2.0 * a1;  Mq[7] = -2.0 * a0;
+  } else if (pose_var) {
+    double Dq[12], PJ[12];
+    unit_quat_rotate_dq(q, X, Dq);
+    quat_plus_jacobian(q, PJ);
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b)
+        Mq[a * 3 + b] = Dq[a * 4 + 0] * PJ[0 * 3 + b] + Dq[a * 4 + 1] * PJ[1 * 3 + b] + Dq[a * 4 + 2] * PJ[2 * 3 + b] +
+                        Dq[a * 4 + 3] * PJ[3 * 3 + b];
+  }
+  double jx[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  if (ptv) {
+#pragma unroll
+    for (int rw = 0; rw < 2; ++rw)
+#pragma unroll
+      for (int b = 0; b < 3; ++b)
+        jx[rw][b] = B[rw * 3 + 0] * Rm[b] + B[rw * 3 + 1] * Rm[3 + b] + B[rw * 3 + 2] * Rm[6 + b];
+  }
+#pragma unroll
+  for (int rw = 0; rw < 2; ++rw) emit_row_mixed<CT>(rw, Jr[rw], B, Mq, pose_var, flags, jx, Jp, sc, cv, cmask);
+}
+
+// The image record of img (q, t, meta, camera parameters) from img_rec.
+__device__ inline uint32_t load_image_record(const DevProblem& p, uint32_t img, double q[4], double t[3],
+                                             double prm[8]) {
+  const double2* rv = reinterpret_cast<const double2*>(p.img_rec + 16 * (size_t)img);
+  const double2 a0 = rv[0], a1 = rv[1], a2 = rv[2], a3 = rv[3];
+  q[0] = a0.x; q[1] = a0.y; q[2] = a1.x; q[3] = a1.y;
+  t[0] = a2.x; t[1] = a2.y; t[2] = a3.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double2 c = rv[4 + k];
+    prm[2 * k] = c.x;
+    prm[2 * k + 1] = c.y;
+  }
+  return (uint32_t)__double_as_longlong(a3.y);
+}
+
+// Point pass, matrix-free: w_p = V_p^-1 sum_a J_p,a' (J_f,a x) over the
+// point chunks (one wave per chunk, one lane per block, the points' sums
+// segmented in lane order as backsub_chunk_kernel's).
+template <int CT, int LOSS>
+__global__ __launch_bounds__(kBlock) void pcg_point_pass_mf(DevProblem p, const uint32_t* __restrict__ chunk,
+                                                             int nchunks, const double* __restrict__ Vinv,
+                                                             const double* __restrict__ x, double* __restrict__ w) {
+  __shared__ double stv[kBlock / 64][64 * 3];
+  __shared__ uint32_t spt[kBlock / 64][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double* tvs = stv[wv];
+  uint32_t* wpt = spt[wv];
+  const int c = blockIdx.x * (kBlock / 64) + wv;
+  if (c >= nchunks) return;  // wave-uniform
+  const uint32_t b0 = chunk[c], b1 = chunk[c + 1];
+  const bool multi = b1 - b0 > 64u;
+  double carry[3] = {0.0, 0.0, 0.0};
+  uint32_t carry_pt = 0;
+  bool carry_var = false;
+  auto finalize = [&](uint32_t pt, const double tt[3]) {
+    const double* vi = Vinv + 6 * (size_t)pt;
+    const double Vi[6] = {vi[0], vi[1], vi[2], vi[3], vi[4], vi[5]};
+    double o[3];
+    sym3_mul(Vi, tt, o);
+#pragma unroll
+    for (int n = 0; n < 3; ++n) w[3 * (size_t)pt + n] = o[n];
+  };
+  for (uint32_t s0 = b0; s0 < b1; s0 += 64) {
+    const int live = (int)min(64u, b1 - s0);
+    const bool on = lane < live;
+    const uint32_t b = s0 + (on ? lane : 0);
+    const uint32_t pt = p.obs_pt[b];
+    const bool var = on && p.pt_var[pt] != 0;
+    double te[3] = {0.0, 0.0, 0.0};
+    if (var) {
+      const uint32_t img = p.obs_img[b];
+      double q[4], t[3], prm[8];
+      const uint32_t meta = load_image_record(p, img, q, t, prm);
+      const double X[3] = {p.X[3 * (size_t)pt], p.X[3 * (size_t)pt + 1], p.X[3 * (size_t)pt + 2]};
+      const double2 o = LOSS != 0 ? p.obs_xy[b] : make_double2(0.0, 0.0);
+      double Jr[2][9 + CT];
+      block_rows_mf<CT, LOSS>(p, q, t, prm, meta, X, true, o, Jr);
+      const double* xi = x + 6 * (size_t)img;
+      const double* xc = x + 6 * (size_t)p.num_images + (size_t)CT * p.img_cam[img];
+      double xv[6 + CT];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) xv[m] = xi[m];
+#pragma unroll
+      for (int m = 0; m < CT; ++m) xv[6 + m] = xc[m];
+#pragma unroll
+      for (int rw = 0; rw < 2; ++rw) {
+        double e = 0.0;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) e += Jr[rw][m] * xv[m];
+#pragma unroll
+        for (int m = 0; m < CT; ++m) e += Jr[rw][9 + m] * xv[6 + m];
+#pragma unroll
+        for (int n = 0; n < 3; ++n) te[n] += Jr[rw][6 + n] * e;
+      }
+    }
+    double* tv = tvs + lane * 3;
+    tv[0] = te[0];
+    tv[1] = te[1];
+    tv[2] = te[2];
+    wpt[lane] = on ? pt : 0xffffffffu;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const bool head = var && (lane == 0 || wpt[lane - 1] != pt);
+    if (head) {
+      double tt[3] = {te[0], te[1], te[2]};
+      for (int l = lane + 1; l < live && wpt[l] == pt; ++l) {
+        tt[0] += tvs[l * 3];
+        tt[1] += tvs[l * 3 + 1];
+        tt[2] += tvs[l * 3 + 2];
+      }
+      if (multi) {
+        carry[0] += tt[0];
+        carry[1] += tt[1];
+        carry[2] += tt[2];
+        carry_pt = pt;
+        carry_var = true;
+      } else {
+        finalize(pt, tt);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  if (multi && carry_var) finalize(carry_pt, carry);
+}
+
+// Camera pass, matrix-free: y_f = sum over the tile's blocks of J_f'
+// (J_f x - J_p w_p), the image record tile-uniform, the blocks' points from
+// the camera-major copy Xcm (and the observations from obs_cm with a robust
+// loss), w_p gathered for variable points (cm_ptv).
+template <int CT, int LOSS>
+__global__ __launch_bounds__(kBlock) void pcg_camera_pass_mf(DevProblem p, const DevTile* __restrict__ tiles,
+                                                              const uint32_t* __restrict__ cm_ptv,
+                                                              const double* __restrict__ Xcm,
+                                                              const double2* __restrict__ obs_cm,
+                                                              const double* __restrict__ x,
+                                                              const double* __restrict__ w, double* __restrict__ y) {
+  constexpr int NV = 6 + CT;
+  __shared__ double sred[4 * NV];
+  const DevTile tile = tiles[blockIdx.x];
+  const uint32_t img = tile.image, cam = p.img_cam[img];
+  double q[4], t[3], prm[8];
+  const uint32_t meta = load_image_record(p, img, q, t, prm);
+  double xv[NV];
+#pragma unroll
+  for (int m = 0; m < 6; ++m) xv[m] = x[6 * (size_t)img + m];
+#pragma unroll
+  for (int m = 0; m < CT; ++m) xv[6 + m] = x[6 * (size_t)p.num_images + (size_t)CT * cam + m];
+  double acc[NV];
+#pragma unroll
+  for (int m = 0; m < NV; ++m) acc[m] = 0.0;
+  for (uint32_t k = threadIdx.x; k < tile.count; k += kBlock) {
+    const size_t kk = (size_t)tile.start + k;
+    const double X[3] = {Xcm[3 * kk], Xcm[3 * kk + 1], Xcm[3 * kk + 2]};
+    const uint32_t pt = cm_ptv[kk];
+    const bool ptv = pt != 0xffffffffu;
+    const double2 o = LOSS != 0 ? obs_cm[kk] : make_double2(0.0, 0.0);
+    double Jr[2][9 + CT];
+    block_rows_mf<CT, LOSS>(p, q, t, prm, meta, X, ptv, o, Jr);
+    double wv3[3] = {0.0, 0.0, 0.0};
+    if (ptv) {
+      wv3[0] = w[3 * (size_t)pt];
+      wv3[1] = w[3 * (size_t)pt + 1];
+      wv3[2] = w[3 * (size_t)pt + 2];
+    }
+#pragma unroll
+    for (int rw = 0; rw < 2; ++rw) {
+      double e = 0.0;
+#pragma unroll
+      for (int m = 0; m < 6; ++m) e += Jr[rw][m] * xv[m];
+#pragma unroll
+      for (int m = 0; m < CT; ++m) e += Jr[rw][9 + m] * xv[6 + m];
+      if (ptv) e -= Jr[rw][6] * wv3[0] + Jr[rw][7] * wv3[1] + Jr[rw][8] * wv3[2];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) acc[m] += Jr[rw][m] * e;
+#pragma unroll
+      for (int m = 0; m < CT; ++m) acc[6 + m] += Jr[rw][9 + m] * e;
+    }
+  }
+  block_reduce<NV>(acc, sred);
+  const int k = threadIdx.x;
+  if (k < NV) {
+    if (k < 6) {
+      if (p.img_flags[img] & 1u) atomicAdd(y + 6 * (size_t)img + k, sred[k]);
+    } else if (p.cam_var[cam]) {
+      atomicAdd(y + 6 * (size_t)p.num_images + (size_t)CT * cam + (k - 6), sred[k]);
+    }
+  }
+}
+
+// The camera-major copies the matrix-free camera pass reads: Xcm[k] =
+// X[obs_pt[cm_perm[k]]] (rebuilt whenever X changes) and, with a robust loss,
+// obs_cm[k] = obs_xy[cm_perm[k]] (static).
+__global__ __launch_bounds__(kBlock) void gather_cm_kernel(DevProblem p, const uint32_t* __restrict__ cm_perm,
+                                                           int64_t n, double* __restrict__ Xcm,
+                                                           double2* __restrict__ obs_cm) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t b = cm_perm[k];
+  const uint32_t pt = p.obs_pt[b];
+  Xcm[3 * k] = p.X[3 * (size_t)pt];
+  Xcm[3 * k + 1] = p.X[3 * (size_t)pt + 1];
+  Xcm[3 * k + 2] = p.X[3 * (size_t)pt + 2];
+  if (obs_cm) obs_cm[k] = p.obs_xy[b];
+}
+
 // Jcm[k] = J[cm_perm[k]]: the Jacobian rows in camera-major order, 16 B per
 // lane, consecutive lanes on consecutive destination pieces (coalesced
 // stores, row-contiguous gathers).  Built once per linearization for the PCG
@@ -2684,6 +2945,12 @@ void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const 
   });
 }
 
+void launch_gather_cm(const DevProblem& p, const uint32_t* cm_perm, int64_t n, double* Xcm, double2* obs_cm,
+                      hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_cm_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, p, cm_perm, n, Xcm, obs_cm);
+}
+
 void launch_permute_rows(const DevProblem& p, const uint32_t* cm_perm, int64_t n, const double* J, double* Jcm,
                          hipStream_t s) {
   if (n == 0) return;
@@ -2710,10 +2977,27 @@ void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, 
                           int ntiles, const uint32_t* cm_perm, const double* J, const double* Vinv,
                           const double* lambda_f, const double* x, double* w, double* y, hipStream_t s,
                           const uint32_t* chunks, int nchunks, const uint32_t* cm_ptv, const double* Jcm,
-                          bool staged) {
+                          bool staged, const double* Xcm, const double2* obs_cm) {
   (void)hipMemsetAsync(y, 0, sizeof(double) * p.nf, s);
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
+    if (Xcm && chunks && cm_ptv && (p.loss_type == 0 || obs_cm)) {
+      // matrix-free passes (no J read)
+      auto go = [&](auto loss) {
+        constexpr int LOSS = decltype(loss)::value;
+        if (npv > 0 && nchunks > 0)
+          hipLaunchKernelGGL((pcg_point_pass_mf<CT, LOSS>), dim3(grid_for(nchunks, kBlock / 64)), dim3(kBlock), 0, s,
+                             p, chunks, nchunks, Vinv, x, w);
+        if (ntiles > 0)
+          hipLaunchKernelGGL((pcg_camera_pass_mf<CT, LOSS>), dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_ptv, Xcm,
+                             obs_cm, x, w, y);
+      };
+      if (p.loss_type == 0)
+        go(std::integral_constant<int, 0>{});
+      else
+        go(std::integral_constant<int, 1>{});
+      return;
+    }
     if (npv > 0 && chunks && nchunks > 0)
       hipLaunchKernelGGL((backsub_chunk_kernel<CT, true>), dim3(grid_for(nchunks, kBlock / 64)), dim3(kBlock), 0, s,
                          p, chunks, nchunks, J, nullptr, nullptr, Vinv, x, w, nullptr);

@@ -828,7 +828,7 @@ void context_destroy(mi_ba_context* ctx) {
 // read their rows contiguously instead of gathering them).  Null when the
 // key is off or the copy does not fit (the passes then gather from J).
 static const double* pcg_jcm(mi_ba_context* ctx) {
-  if (!ctx->pcg_jcm || ctx->dense) return nullptr;
+  if (!ctx->pcg_jcm || ctx->dense || ctx->pcg_mf) return nullptr;
   const size_t nb = ctx->cm_perm.n;
   if (!ctx->Jcm.ptr || ctx->Jcm.n != ctx->J.n) {
     if (nb == 0 || ctx->Jcm.alloc(ctx->J.n) != hipSuccess) {
@@ -854,6 +854,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   const DevProblem& d = ctx->dev;
   hipEvent_t stop;
   ctx->jcm_stale = true;
+  ctx->xcm_stale = true;
   // image records + the scalar slots zeroed in one launch
   launch_pack_images(d, ctx->img_rec.ptr, s, ctx->scalars.ptr, kNumScalars);
   // linearize_overlap: 1 the semantic kernels on a second stream beside the
@@ -932,13 +933,39 @@ namespace {
 // pairs (the damping diagonal on rank 0 only) and the ranks sum y — one
 // nf-vector all-reduce per product, the x / r / z / p vectors stay
 // replicated (identical bits on every rank).
+// The matrix-free product's camera-major copies (null when off or they do
+// not fit: the product then reads J).
+static const double* pcg_xcm(mi_ba_context* ctx) {
+  if (!ctx->pcg_mf || ctx->dense || !ctx->pp_chunks) return nullptr;
+  const size_t nb = ctx->cm_perm.n;
+  const bool robust = ctx->dev.loss_type != MI_BA_LOSS_TRIVIAL;
+  if (nb == 0) return nullptr;
+  if (!ctx->Xcm.ptr || ctx->Xcm.n != 3 * nb || (robust && ctx->obs_cm.n != nb)) {
+    if (ctx->Xcm.alloc(3 * nb) != hipSuccess || (robust && ctx->obs_cm.alloc(nb) != hipSuccess)) {
+      (void)hipGetLastError();
+      ctx->Xcm.release();
+      ctx->obs_cm.release();
+      return nullptr;
+    }
+    ctx->xcm_stale = true;
+  }
+  if (ctx->xcm_stale) {
+    Phase ph_(ctx, "gather_cm");
+    launch_gather_cm(ctx->dev, ctx->cm_perm.ptr, (int64_t)nb, ctx->Xcm.ptr, robust ? ctx->obs_cm.ptr : nullptr,
+                     ctx->stream);
+    ctx->xcm_stale = false;
+  }
+  return ctx->Xcm.ptr;
+}
+
 mi_ba_status schur_product(mi_ba_context* ctx, const double* x, double* y) {
   const DevProblem& d = ctx->dev;
+  const double* xcm = pcg_xcm(ctx);
   launch_schur_product(d, ctx->vpoints.ptr, ctx->npv, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr,
                        ctx->Vinv.ptr, ctx->rank == 0 ? ctx->lambda_f.ptr : nullptr, x, ctx->cg_w.ptr, y, ctx->stream,
                        ctx->pp_chunks ? ctx->pchunks.ptr : nullptr, ctx->npchunks,
                        ctx->pp_chunks ? ctx->cm_ptv.ptr : nullptr, ctx->pcg_jcm && !ctx->jcm_stale ? ctx->Jcm.ptr : nullptr,
-                       ctx->pcg_jcm == 2);
+                       ctx->pcg_jcm == 2, xcm, xcm && ctx->obs_cm.ptr ? ctx->obs_cm.ptr : nullptr);
   if (ctx->sem) semantic_schur_product(ctx, x, y);
   if (ctx->gsba) gsba_schur_product(ctx, x, y);
   return allreduce(ctx, y, d.nf);
@@ -1990,6 +2017,16 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   }
   if (std::strcmp(key, "cholesky_panel_group_min_rows") == 0 && value >= 0) {
     ctx->chol.panel_group_min_rows = value;
+    return MI_BA_OK;
+  }
+  // PCG product without J reads (the passes recompute the Jacobian rows)
+  if (std::strcmp(key, "pcg_matrix_free") == 0 && (value == 0 || value == 1)) {
+    ctx->pcg_mf = value != 0;
+    if (ctx->pcg_mf) ctx->Jcm.release();
+    else {
+      ctx->Xcm.release();
+      ctx->obs_cm.release();
+    }
     return MI_BA_OK;
   }
   if (std::strcmp(key, "pcg_jcm") == 0 && value >= 0 && value <= 2 && ab_value(value, 2)) {

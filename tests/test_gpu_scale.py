@@ -118,8 +118,9 @@ def test_c4_semantic_sampled_pairs_bitwise(gpu):
     assert (st_o == mi_ba.VALID).mean() > 0.5 and (np.abs(J_o).sum(axis=1) > 0).sum() > 100
 
 
+@pytest.mark.parametrize("mf", [0, 1])
 @pytest.mark.parametrize("case", ["geo", "sem"])
-def test_iterative_schur_parity(gpu, case):
+def test_iterative_schur_parity(gpu, case, mf):
     sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 30, 2000, track_length=6,
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=9)).gauge()
     sem = None
@@ -131,7 +132,10 @@ def test_iterative_schur_parity(gpu, case):
     a, b = sc.copy(), sc.copy()
     s_o = oracle.solve(ref, a, sem)
     opts.linear_solver_type = mi_ba.SOLVER_ITERATIVE_SCHUR
-    s_g = mi_ba.solve(opts, b, sem)
+    with mi_ba.Context(opts, b, sem) as ctx:  # mf 1: the matrix-free Schur product
+        ctx.set_tuning("pcg_matrix_free", mf)
+        s_g = ctx.solve()
+        ctx.writeback()
     assert s_g.num_linear_solver_iterations > s_g.num_successful_steps  # the CG path ran
     assert (s_g.num_successful_steps, s_g.num_unsuccessful_steps) == \
         (s_o.num_successful_steps, s_o.num_unsuccessful_steps)
@@ -151,8 +155,9 @@ def test_c2_iterative_schur_default_eta_converges_to_oracle(gpu):
     assert np.abs(b.xyz - a.xyz).max() <= 1e-5
 
 
-@pytest.mark.parametrize("case", ["constants", "long_tracks"])
-def test_iterative_schur_parity_chunks(gpu, case):
+@pytest.mark.parametrize("mf", [0, 1])
+@pytest.mark.parametrize("case", ["constants", "long_tracks", "soft_l1"])
+def test_iterative_schur_parity_chunks(gpu, case, mf):
     """The PCG path's chunked point passes and camera-major J copy against the
     oracle: constant points (camera-major slots without a point term),
     constant cameras and poses (skipped f-slots), or every point observed by
@@ -165,21 +170,27 @@ def test_iterative_schur_parity_chunks(gpu, case):
         sc.point_config = np.where(rng.uniform(size=sc.num_points) < 0.3, 2, 1).astype(np.uint8)
         sc.camera_constant = (np.arange(sc.num_cameras) % 3 == 0).astype(np.uint8)
         sc.image_constant_pose[5] = 1
-    else:
+    elif case == "long_tracks":
         sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 80, 300, track_length=70,
                                                      rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=12)).gauge()
+    else:  # robust loss: the Corrector's sqrt(rho') on the recomputed rows
+        sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.OPENCV, 30, 2000, track_length=6, rotation_range=0.05,
+                                                     extra=(-0.1, 0.01, 1e-4, -1e-4), seed=13)).gauge()
+    loss = dict(loss_function_type=mi_ba.LOSS_SOFT_L1, loss_function_scale=1.0) if case == "soft_l1" else {}
     # 3 iterations: same accept/reject decisions; 8: converged to the same
     # cost.  (Once converged, steps are decided at the rounding floor, where
     # the oracle and even the exact GPU solve differ: 'constants' reaches
     # 13157.18092343093 with (6, 2) oracle steps, (8, 0) exact GPU steps,
     # (6, 1) PCG steps — tools/diag_pcg_constants.py.)
     for iters in (3, 8):
-        ref = mi_ba.default_options(max_num_iterations=iters, eta=1e-12)
+        ref = mi_ba.default_options(max_num_iterations=iters, eta=1e-12, **loss)
         opts = mi_ba.default_options(max_num_iterations=iters, eta=1e-12, max_linear_solver_iterations=1000,
-                                     linear_solver_type=mi_ba.SOLVER_ITERATIVE_SCHUR)
+                                     linear_solver_type=mi_ba.SOLVER_ITERATIVE_SCHUR, **loss)
         a, b = sc.copy(), sc.copy()
         s_o = oracle.solve(ref, a, None)
-        s_g = mi_ba.solve(opts, b, None)
+        with mi_ba.Context(opts, b) as ctx:
+            ctx.set_tuning("pcg_matrix_free", mf)
+            s_g = ctx.solve()
         assert s_g.num_linear_solver_iterations > s_g.num_successful_steps  # the CG path ran
         if iters == 3:
             assert (s_g.num_successful_steps, s_g.num_unsuccessful_steps) == \

@@ -7,6 +7,8 @@
 # reproj_jacobian roofline decomposition in-step and back-to-back), ws (flat
 # pass window summaries A/B), chol (panel schedules A/B; CHOL="k=v,k=v ..."),
 # trace (rocprofv3 kernel trace of the bench command), bench (the bench line),
+# jacsweep (in-step times of the tools-build Jacobian variants JACV), pcg
+# (matrix-free PCG product A/B),
 # smoke
 set -o pipefail
 T=${1:?tag}
@@ -17,13 +19,19 @@ for stage in "$@"; do
   echo "== $stage $(date +%T)"
   case $stage in
     tests)
-      timeout -k 10 ${TESTS_TIMEOUT:-900} python -u -m pytest -x -v --timeout 400 --timeout-method thread -m gpu ${TESTS:-tests} > gpurun_out/$T/tests.log 2>&1
+      timeout -k 10 ${TESTS_TIMEOUT:-900} python -u -m pytest ${PYTEST_X--x} -v --timeout 400 --timeout-method thread -m gpu ${TESTS:-tests} > gpurun_out/$T/tests.log 2>&1
       rc=$?; echo "tests rc $rc"; tail -3 gpurun_out/$T/tests.log
       [ $rc -le 1 ] || exit 1 ;;
     jac)
       timeout -k 10 300 python -u tools/ab_jacobian.py --step --variants 0,11,12 --rounds 5 --reps 5 > gpurun_out/$T/ab_jac_step.jsonl 2> gpurun_out/$T/ab_jac_step.err || exit 1
       timeout -k 10 300 python -u tools/ab_jacobian.py --variants 0,11,12 --rounds 5 --reps 5 > gpurun_out/$T/ab_jac_b2b.jsonl 2> gpurun_out/$T/ab_jac_b2b.err || exit 1
       cat gpurun_out/$T/ab_jac_step.jsonl ;;
+    jacsweep)
+      timeout -k 10 400 python -u tools/ab_jacobian.py --step --variants ${JACV:-0,1,2,4,30,31,32,35,39} --rounds 5 --reps 5 > gpurun_out/$T/ab_jac_sweep.jsonl 2> gpurun_out/$T/ab_jac_sweep.err || exit 1
+      cat gpurun_out/$T/ab_jac_sweep.jsonl ;;
+    pcg)
+      timeout -k 10 500 python -u tools/ab_pcg_mf.py > gpurun_out/$T/ab_pcg_mf.jsonl 2> gpurun_out/$T/ab_pcg_mf.err || exit 1
+      cat gpurun_out/$T/ab_pcg_mf.jsonl ;;
     ws)
       timeout -k 10 300 python -u tools/ab_semantic_ws.py > gpurun_out/$T/ab_ws.jsonl 2> gpurun_out/$T/ab_ws.err || exit 1
       cat gpurun_out/$T/ab_ws.jsonl ;;
