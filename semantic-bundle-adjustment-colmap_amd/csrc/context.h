@@ -78,7 +78,7 @@ struct mi_ba_context {
   miba::DevArray<uint8_t> cam_var, cam_model, pt_var;
   miba::DevArray<double> qt, cam, X;       // current parameters
   miba::DevArray<double> qt_c, cam_c, X_c; // candidate parameters
-  miba::DevArray<double> img_rec;          // [I][16] packed image records
+  miba::DevArray<double> img_rec;          // [I][kImgRec] packed image records
   miba::DevArray<uint32_t> cm_perm;
   miba::DevArray<uint32_t> cm_ptv;  // [nb] camera-major: the block's point if variable, else 0xffffffff
   miba::DevArray<miba::DevTile> tiles;

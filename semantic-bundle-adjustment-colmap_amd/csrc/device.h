@@ -12,8 +12,8 @@
 //   images     qt[I][8]        q(4) t(3) pad — one 64-B line per image
 //              img_flags u32[I] bit0 variable pose, bits1..3 constant tvec
 //   cameras    cam[C][8]       params, padded to 8
-//   img_rec    double[I][16]   q t meta cam: the Jacobian kernel's per-image
-//                              record (one 128-B line), packed per linearization;
+//   img_rec    double[I][kImgRec] q t meta cam R unit-q: the Jacobian kernel's per-image
+//                              record (two 128-B lines), packed per linearization;
 //                              meta = img_flags | cam_var << 8 | model << 16
 //   points     X[P][3]
 // Camera-side reductions run over cm_perm (blocks sorted by image) in tiles
@@ -50,6 +50,9 @@ struct DevPairTile {   // image-pair tile of the explicit Schur build
 };
 constexpr int kPairTile = 256;
 
+// doubles per packed image record (kernels.hip pack_images_kernel)
+constexpr int kImgRec = 32;
+
 struct DevProblem {
   int model;           // camera model of every camera, or kMixedModels (per-camera cam_model)
   int np;              // camera params per camera (largest)
@@ -85,7 +88,7 @@ struct DevProblem {
   double* qt;   // [I][8]
   double* cam;  // [C][8]
   double* X;    // [P][3]
-  double* img_rec;  // [I][16] q(4) t(3) meta cam(8): packed by launch_pack_images
+  double* img_rec;  // [I][kImgRec] q(4) t(3) meta cam(8) R(9) unit-q: packed by launch_pack_images
 };
 
 }  // namespace miba

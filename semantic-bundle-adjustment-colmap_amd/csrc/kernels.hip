@@ -315,7 +315,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   // even stride: W2 + 4 gives 2-way conflicts on the row writes
   constexpr int LS = (D & 32) ? W2 + 4 : (W2 | 1);
   constexpr int RP = 64 / NP;
-  constexpr int RS = 18;  // LDS stride of an image record (144 B: conflict-free ds_read_b128)
+  // LDS stride of an image record: 144 B (the first 128 B: conflict-free
+  // ds_read_b128), 272 B with the per-image rotation matrix (D & 2048)
+  constexpr int RS = (D & 2048) ? 34 : 18;
   // D & 64: image records fetched per lane (no LDS staging), slab = J rows only
   constexpr int SLAB = ((D & 64) || RP * LS > 64 * RS) ? RP * LS : 64 * RS;
   __shared__ double sJ[(TB / 64) * SLAB];
@@ -367,11 +369,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
     if constexpr ((D & 4) != 0) img &= 127u;  // diagnostic: L1-resident record working set
     double q[4], t[3], prm[np];
+    double Rrec[9];  // D & 2048: the image record's rotation matrix
+    bool unit_rec = false;
     uint32_t meta;
     if constexpr ((D & 64) != 0) {
       // per-lane record fetch: 16-B loads of the lane's own 128-B line (L1/L2
       // resident, 1000 images = 128 KB), no LDS and no wave barrier
-      const double2* rv = reinterpret_cast<const double2*>(p.img_rec + 16 * (size_t)img);
+      const double2* rv = reinterpret_cast<const double2*>(p.img_rec + kImgRec * (size_t)img);
       const double2 a0 = rv[0], a1 = rv[1], a2 = rv[2], a3 = rv[3];
       q[0] = a0.x; q[1] = a0.y; q[2] = a1.x; q[3] = a1.y;
       t[0] = a2.x; t[1] = a2.y; t[2] = a3.x;
@@ -387,8 +391,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       for (int j = 0; j < 8; ++j) {
         const int src = 8 * j + (lane >> 3);
         const uint32_t is = __shfl(img, src, 64);
-        const double2 v = reinterpret_cast<const double2*>(p.img_rec + 16 * (size_t)is)[lane & 7];
+        const double2* rv = reinterpret_cast<const double2*>(p.img_rec + kImgRec * (size_t)is);
+        const double2 v = rv[lane & 7];
         reinterpret_cast<double2*>(slab + src * RS)[lane & 7] = v;
+        if constexpr ((D & 2048) != 0) {
+          if ((lane & 7) < 5) reinterpret_cast<double2*>(slab + src * RS)[8 + (lane & 7)] = rv[8 + (lane & 7)];
+        }
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -398,6 +406,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       meta = (uint32_t)__double_as_longlong(rec[7]);
 #pragma unroll
       for (int k = 0; k < np; ++k) prm[k] = rec[8 + k];
+      if constexpr ((D & 2048) != 0) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Rrec[k] = rec[16 + k];
+        unit_rec = rec[25] != 0.0;
+      }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
@@ -428,7 +441,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       cv = (meta >> 8) & 1u;
       double P[3];
       double Rm[9];
-      if constexpr ((D & 1024) != 0) {
+      if constexpr ((D & 2048) != 0) {
+        // R X from the record's rotation matrix (computed once per image)
+#pragma unroll
+        for (int c = 0; c < 9; ++c) Rm[c] = Rrec[c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) P[c] = Rm[3 * c] * X[0] + Rm[3 * c + 1] * X[1] + Rm[3 * c + 2] * X[2];
+      } else if constexpr ((D & 1024) != 0) {
         // R X from the rotation matrix the point columns need anyway
         unit_quat_matrix(q, Rm);
 #pragma unroll
@@ -472,7 +491,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       // closed form, equal up to rounding for a unit q (the general product
       // serves a quaternion that is not normalised, as AutoDiff would)
       const bool unit_q =
-          (D & 512) && ((D & 4096) || fabs(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3] - 1.0) <= 1e-12);
+          (D & 512) && ((D & 4096) || ((D & 2048) ? unit_rec
+                                                  : fabs(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3] - 1.0) <= 1e-12));
       if (pose_var && unit_q) {
         Mq[0] = 0.0;       Mq[1] = 2.0 * a2;  Mq[2] = -2.0 * a1;
         Mq[3] = -2.0 * a2; Mq[4] = 0.0;       Mq[5] = 2.0 * a0;
@@ -490,7 +510,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
       if (ptv) {
         double R[9];
-        if constexpr ((D & 1024) != 0) {
+        if constexpr ((D & (1024 | 2048)) != 0) {
 #pragma unroll
           for (int c = 0; c < 9; ++c) R[c] = Rm[c];
         } else {
@@ -543,9 +563,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   if (lane == 0 && wb0 < p.nb) cost_partial[wb0 >> 6] = s;
 }
 
-// Image records img_rec[I][16] = q(4) t(3) meta camera-params(8), meta =
-// img_flags | cam_var << 8 (bit pattern in a double slot): one 128-B line per
-// image, rebuilt whenever poses or intrinsics change.
+// Image records img_rec[I][kImgRec] = q(4) t(3) meta camera-params(8)
+// R(9) unit-q(1) pad, meta = img_flags | cam_var << 8 | model << 16 (bit
+// pattern in a double slot), R = the rotation matrix of q and unit-q = 1.0
+// when |q|^2 is 1 within 1e-12 (the Jacobian kernels' closed-form test) —
+// both per image instead of per block: two 128-B lines per image, rebuilt
+// whenever poses or intrinsics change.
 // zero[0..nzero) is cleared too (the step's scalar slots: one launch fewer
 // than a separate memset ahead of it).
 __global__ void pack_images_kernel(DevProblem p, double* __restrict__ rec, double* __restrict__ zero, int nzero) {
@@ -553,13 +576,21 @@ __global__ void pack_images_kernel(DevProblem p, double* __restrict__ rec, doubl
   if (k < nzero) zero[k] = 0.0;
   if (k >= p.num_images) return;
   const uint32_t cam = p.img_cam[k];
-  double* o = rec + 16 * (size_t)k;
+  double* o = rec + kImgRec * (size_t)k;
 #pragma unroll
   for (int m = 0; m < 7; ++m) o[m] = p.qt[8 * (size_t)k + m];
   o[7] = __longlong_as_double(
       (long long)(p.img_flags[k] | ((p.cam_var[cam] != 0 ? 1u : 0u) << 8) | ((uint32_t)p.cam_model[cam] << 16)));
 #pragma unroll
   for (int m = 0; m < 8; ++m) o[8 + m] = p.cam[8 * (size_t)cam + m];
+  const double q[4] = {o[0], o[1], o[2], o[3]};
+  double R[9];
+  unit_quat_matrix(q, R);
+#pragma unroll
+  for (int m = 0; m < 9; ++m) o[16 + m] = R[m];
+  o[25] = fabs(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3] - 1.0) <= 1e-12 ? 1.0 : 0.0;
+#pragma unroll
+  for (int m = 26; m < kImgRec; ++m) o[m] = 0.0;
 }
 
 template <int M>
@@ -1737,7 +1768,7 @@ __device__ inline void block_rows_mf(const DevProblem& p, const double* q, const
 // The image record of img (q, t, meta, camera parameters) from img_rec.
 __device__ inline uint32_t load_image_record(const DevProblem& p, uint32_t img, double q[4], double t[3],
                                              double prm[8]) {
-  const double2* rv = reinterpret_cast<const double2*>(p.img_rec + 16 * (size_t)img);
+  const double2* rv = reinterpret_cast<const double2*>(p.img_rec + kImgRec * (size_t)img);
   const double2 a0 = rv[0], a1 = rv[1], a2 = rv[2], a3 = rv[3];
   q[0] = a0.x; q[1] = a0.y; q[2] = a1.x; q[3] = a1.y;
   t[0] = a2.x; t[1] = a2.y; t[2] = a3.x;
@@ -2821,6 +2852,10 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
             case 12:
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, kJacPasses, kJacProduction | 1>), dim3(g), dim3(kBlock),
                                  0, s, p, r, J, cost_partial);
+              return;
+            case 13:  // R and the unit-q test from the image record (per image, not per block)
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, kJacPasses, kJacProduction | 2048>), dim3(g),
+                                 dim3(kBlock), 0, s, p, r, J, cost_partial);
               return;
             default:
               break;

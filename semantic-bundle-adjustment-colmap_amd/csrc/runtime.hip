@@ -622,7 +622,7 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
     }
     if (ctx->qt.alloc(8 * I) || ctx->qt_c.alloc(8 * I) || ctx->cam.alloc(8 * C) || ctx->cam_c.alloc(8 * C) ||
         ctx->X.alloc(3 * P) || ctx->X_c.alloc(3 * P) || ctx->img_flags.alloc(I) || ctx->img_cam.alloc(I) ||
-        ctx->cam_var.alloc(C) || ctx->cam_model.alloc(C) || ctx->pt_var.alloc(P) || ctx->img_rec.alloc(16 * I))
+        ctx->cam_var.alloc(C) || ctx->cam_model.alloc(C) || ctx->pt_var.alloc(P) || ctx->img_rec.alloc(kImgRec * (size_t)I))
       return fail(MI_BA_ERR_OUT_OF_MEMORY);
     if ((I && (hipMemcpy(ctx->qt.ptr, qt.data(), qt.size() * 8, hipMemcpyHostToDevice) ||
                hipMemcpy(ctx->img_flags.ptr, fl.data(), I * 4, hipMemcpyHostToDevice) ||
