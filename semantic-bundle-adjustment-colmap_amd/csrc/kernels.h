@@ -54,6 +54,12 @@ void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const 
                    const double2* r, const double* J, const double* Jcm, const double* Vg, const double* Vinv,
                    double* pose_blk, double* cam_blk, double* b, double* udiag, hipStream_t s);
 // Jcm[k] = J[cm_perm[k]] for k < n (2 (9 + ct) doubles per block).
+// Doubles per block of the Schur build's per-block records (Z rows, or the
+// JG records of schur_pairs_variant 6).
+inline int64_t schur_record_width(int ct, int svariant) {
+  const int F = 6 + ct;
+  return svariant == 6 ? ((2 * F + 6 + 15) / 16) * 16 : 3 * F;
+}
 void launch_permute_rows(const DevProblem& p, const uint32_t* cm_perm, int64_t n, const double* J, double* Jcm,
                          hipStream_t s);
 

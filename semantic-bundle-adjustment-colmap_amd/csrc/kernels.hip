@@ -2595,6 +2595,137 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
   }
 }
 
+// schur_pairs_variant 6: per block the record JG_a = [J_f,a (2 x F, row-major),
+// G_a = Linv J_p,a' (3 x 2), zero pad] of jg_width(F) doubles (256 B at F <=
+// 13: two aligned 128-B lines, where a Z row of 3 F doubles spans three), so
+// that Z_a Z_b' = J_f,a' (G_a' G_b) J_f,b: a pair's two records cost four line
+// requests instead of six.
+__host__ __device__ constexpr int jg_width(int F) { return ((2 * F + 6 + 15) / 16) * 16; }
+
+template <int CT>
+__global__ __launch_bounds__(kBlock) void schur_jg_kernel(DevProblem p, const double* __restrict__ J,
+                                                           const double* __restrict__ Linv, double* __restrict__ JG) {
+  constexpr int F = 6 + CT, W = 9 + CT, W2 = 2 * W, LS = W2 | 1;
+  constexpr int RW = jg_width(F), RS = RW | 1;
+  constexpr int SL = (LS > RS ? LS : RS) * 64;
+  __shared__ double sl[(kBlock / 64) * SL];
+  double* slab = sl + (threadIdx.x >> 6) * SL;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t wb0 = i - lane;
+  const int live = wb0 >= p.nb ? 0 : (p.nb - wb0 < 64 ? (int)(p.nb - wb0) : 64);
+  wave_load_rows_u<W2, LS, 64>(J + wb0 * W2, slab, live);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  double jf[2][F], jp[2][3];
+  {
+    const double* row = slab + lane * LS;
+#pragma unroll
+    for (int rw = 0; rw < 2; ++rw) {
+#pragma unroll
+      for (int m = 0; m < 6; ++m) jf[rw][m] = row[rw * W + m];
+#pragma unroll
+      for (int m = 0; m < 3; ++m) jp[rw][m] = row[rw * W + 6 + m];
+#pragma unroll
+      for (int m = 0; m < CT; ++m) jf[rw][6 + m] = row[rw * W + 9 + m];
+    }
+  }
+  double L[6] = {0, 0, 0, 0, 0, 0};
+  if (i < p.nb) {
+    const uint32_t pt = p.obs_pt[i];
+    if (p.pt_var[pt]) {
+#pragma unroll
+      for (int m = 0; m < 6; ++m) L[m] = Linv[6 * (size_t)pt + m];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  double* o = slab + lane * RS;
+#pragma unroll
+  for (int rw = 0; rw < 2; ++rw)
+#pragma unroll
+    for (int m = 0; m < F; ++m) o[rw * F + m] = jf[rw][m];
+#pragma unroll
+  for (int rw = 0; rw < 2; ++rw) {
+    o[2 * F + rw] = L[0] * jp[rw][0];
+    o[2 * F + 2 + rw] = L[1] * jp[rw][0] + L[2] * jp[rw][1];
+    o[2 * F + 4 + rw] = L[3] * jp[rw][0] + L[4] * jp[rw][1] + L[5] * jp[rw][2];
+  }
+#pragma unroll
+  for (int m = 2 * F + 6; m < RW; ++m) o[m] = 0.0;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  wave_readout<RW, RS, RW>(slab, JG + wb0 * RW, live);
+}
+
+// Variant 6 of schur_pairs_kernel: two pairs per v_mfma_f64_16x16x4f64 (K
+// slots 0, 1 the first pair's two residual rows, 2, 3 the second's), per
+// pair acc += J_f,a' T with T = (G_a' G_b) J_f,b: lane (m, k) loads J_f,a[k
+// & 1][m] and J_f,b[0..1][m]; the pairs' G blocks are wave-uniform.
+template <int CT>
+__global__ __launch_bounds__(kBlock) void schur_pairs_jg_kernel(DevProblem p, const DevPairTile* __restrict__ tiles,
+                                                                 int ntiles, const uint2* __restrict__ pairs,
+                                                                 const double* __restrict__ JG,
+                                                                 double* __restrict__ S) {
+  constexpr int F = 6 + CT, RW = jg_width(F);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = blockIdx.x * 4 + wv;
+  if (t >= ntiles) return;
+  const DevPairTile tl = tiles[t];
+  if (tl.count == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int m = lane & 15, k = lane >> 4;
+  const int slot = k >> 1, r = k & 1;
+  const bool on = m < F;
+  const int mm = on ? m : 0;
+  typedef double dvec4 __attribute__((ext_vector_type(4)));
+  dvec4 acc = {0.0, 0.0, 0.0, 0.0};
+  const uint32_t cnt = tl.count;
+  const uint2* pl = pairs + tl.start;
+#pragma unroll 2
+  for (uint32_t n = 0; n < cnt; n += 2) {
+    const uint2 pa = pl[n];
+    const bool two = n + 1 < cnt;
+    const uint2 pb = two ? pl[n + 1] : pa;
+    // wave-uniform: both pairs' G blocks
+    const uint32_t a0 = __builtin_amdgcn_readfirstlane(pa.x), b0 = __builtin_amdgcn_readfirstlane(pa.y);
+    const uint32_t a1 = __builtin_amdgcn_readfirstlane(pb.x), b1 = __builtin_amdgcn_readfirstlane(pb.y);
+    const double* ga = JG + (size_t)(slot ? a1 : a0) * RW;
+    const double* gb = JG + (size_t)(slot ? b1 : b0) * RW;
+    // this lane's row r of M = G_a' G_b (2 x 2): M[r][s] = sum_c G_a[c][r] G_b[c][s]
+    const double g0 = ga[2 * F + r], g1 = ga[2 * F + 2 + r], g2 = ga[2 * F + 4 + r];
+    const double m0 = g0 * gb[2 * F] + g1 * gb[2 * F + 2] + g2 * gb[2 * F + 4];
+    const double m1 = g0 * gb[2 * F + 1] + g1 * gb[2 * F + 3] + g2 * gb[2 * F + 5];
+    const double va = ga[r * F + mm];
+    const double vb = m0 * gb[mm] + m1 * gb[F + mm];
+    const bool use = on && (slot == 0 || two);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(use ? va : 0.0, use ? vb : 0.0, acc, 0, 0, 0);
+  }
+  const uint32_t ia = tl.ia, ib = tl.ib;
+  const uint32_t ca = p.img_cam[ia], cb = p.img_cam[ib];
+  const bool pa_ = p.img_flags[ia] & 1u, pb_ = p.img_flags[ib] & 1u;
+  const bool cva = p.cam_var[ca] != 0, cvb = p.cam_var[cb] != 0;
+  const int ncol = lane & 15;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int mrow = 4 * q + (lane >> 4);  // v_mfma_f64_16x16x4f64 D layout: D[4q + l/16][l%16]
+    if (mrow >= F || ncol >= F) continue;
+    const bool va_ = mrow < 6 ? pa_ : cva, vb_ = ncol < 6 ? pb_ : cvb;
+    if (!va_ || !vb_) continue;
+    const int64_t ra = fslot(p, ia, ca, mrow), rb = fslot(p, ib, cb, ncol);
+    const double v = acc[q];
+    if (tl.self) {
+      if (ra <= rb) atomicAdd(S + ra * p.lds + rb, -v);
+    } else if (ra < rb) {
+      atomicAdd(S + ra * p.lds + rb, -v);
+    } else if (ra > rb) {
+      atomicAdd(S + rb * p.lds + ra, -v);
+    } else {
+      atomicAdd(S + ra * p.lds + ra, -2.0 * v);
+    }
+  }
+}
+
 // As schur_pairs_kernel, latency-hidden: the tile's pair list is staged once
 // in the wave's LDS slot (read back as broadcasts, no dependent global load
 // per pair), and the Z rows of U pairs are requested one step ahead, so the
@@ -3155,7 +3286,12 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
     constexpr int CT = decltype(c)::value;
     if (with_u && ntiles > 0)
       hipLaunchKernelGGL(dense_u_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, J, S);
-    if (nptiles > 0 && p.nb > 0) {
+    if (nptiles > 0 && p.nb > 0 && p.svariant == 6) {
+      // JG records + two pairs per MFMA, image-block tile order (dispatch order)
+      hipLaunchKernelGGL(schur_jg_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z);
+      hipLaunchKernelGGL(schur_pairs_jg_kernel<CT>, dim3((nptiles + 3) / 4), dim3(kBlock), 0, s, p, ptiles, nptiles,
+                         pairs, Z, S);
+    } else if (nptiles > 0 && p.nb > 0) {
       hipLaunchKernelGGL(schur_z_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z);
       const int G = (nptiles + 3) / 4;
       const int grid = ((G + 7) / 8) * 8;  // whole XCD stripes (extra workgroups exit)

@@ -421,7 +421,7 @@ mi_ba_status build_pair_tiles(mi_ba_context* ctx) {
   // (2.9 MB of Z per image at C4), where the first-image order scatters the
   // second image's rows over every image
   if (ctx->pairs.alloc(npairs) || ctx->ptiles.alloc(tl.size()) || ctx->ptiles_blk.alloc(tl.size()) ||
-      ctx->Linv.alloc(6 * (size_t)d.num_points) || ctx->Z.alloc((size_t)nb * 3 * (6 + d.ct)))
+      ctx->Linv.alloc(6 * (size_t)d.num_points) || ctx->Z.alloc((size_t)nb * std::max<int64_t>(schur_record_width(d.ct, 4), schur_record_width(d.ct, 6))))
     return MI_BA_ERR_OUT_OF_MEMORY;
   if ((npairs && hipMemcpy(ctx->pairs.ptr, pr.data(), npairs * sizeof(uint2), hipMemcpyHostToDevice)) ||
       (!tl.empty() && hipMemcpy(ctx->ptiles.ptr, tl.data(), tl.size() * sizeof(DevPairTile), hipMemcpyHostToDevice)))
@@ -1053,7 +1053,9 @@ void launch_schur_terms(mi_ba_context* ctx) {
   hipEvent_t stop;
   timer_begin(ctx, "schur_build", &stop);
   launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
-                     d.svariant == 5 ? ctx->ptiles_xcd.ptr : d.svariant == 4 ? ctx->ptiles_blk.ptr : ctx->ptiles.ptr,
+                     d.svariant == 5 ? ctx->ptiles_xcd.ptr
+                     : (d.svariant == 4 || d.svariant == 6) ? ctx->ptiles_blk.ptr
+                                                            : ctx->ptiles.ptr,
                      d.svariant == 5 ? ctx->nptiles_xcd : ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, false,
                      ctx->stream);
   if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
@@ -1938,12 +1940,16 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     if (!ctx->sem) return value ? MI_BA_ERR_STATE : MI_BA_OK;
     return semantic_set_window_summary(ctx, value != 0);
   }
+  if (std::strcmp(key, "semantic_deferred_box") == 0 && (value == 0 || value == 1)) {
+    ctx->sem_deferred_box = value != 0;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "semantic_variant") == 0 && value >= 0 && value <= 6 && ab_value(value, 6)) {
     ctx->sem_variant = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 5 &&
-      (value == 0 || value == 4 || ab_value(value, 0))) {
+  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 6 &&
+      (value == 0 || value == 4 || value == 6 || ab_value(value, 0))) {
     ctx->dev.svariant = value;
     return MI_BA_OK;
   }

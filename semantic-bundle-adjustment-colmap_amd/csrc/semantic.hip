@@ -656,11 +656,16 @@ __device__ __forceinline__ void stencil_rolled(const SemArgs& a, const PairConst
 // (stencil_rolled, which falls back to the reference sequence), so the
 // values stay the reference's bit for bit.
 // ---------------------------------------------------------------------------
+struct FlatBox {
+  int x0, y0, ncol, nrow;  // reachable pixels (x0 .. x0 + ncol - 1, y0 .. y0 + nrow - 1)
+  double d;                // bound of the depth change
+};
+
 // First half of resolve: 0 = inside a pixel margin (redo), 1 = out of bounds
-// (f = 0), 2 = raster test at *idx needed.
+// (f = 0), 2 = raster test at *idx (pixel *pxo, *pyo) needed.
 template <int M, bool FAST>
 __device__ __forceinline__ int probe_pixel(const SemArgs& a, const double p[3], double mag, const double* K2,
-                                           double exk, int* idx) {
+                                           double exk, int* idx, int* pxo = nullptr, int* pyo = nullptr) {
   double iz;
   if constexpr (FAST) {
     const double x0 = p[2];
@@ -691,6 +696,10 @@ __device__ __forceinline__ int probe_pixel(const SemArgs& a, const double p[3], 
   const int py = (int)fy + (ry > 0.5 ? 1 : 0);
   if (px < 0 || px >= a.W || py < 0 || py >= a.H) return 1;
   *idx = py * a.W + px;
+  if (pxo) {
+    *pxo = px;
+    *pyo = py;
+  }
   return 2;
 }
 
@@ -707,30 +716,41 @@ __device__ __forceinline__ bool probe_depth(const SemArgs& a, float2 s, double z
 // m0 + j for parameter k0 + j; fp / fm the + / - values.  cidx: a pixel the
 // lane has read already (the centre's), read again by points with no raster
 // test so that every read of the step issues unconditionally.
+// box (nullable): the sample's reachable 3 x 3 box of raster pixels (fb), read
+// once into the lane's LDS slot: every stencil point's pixel lies in it (the
+// flat test's bound), so the step takes its pixels from LDS instead of the
+// raster (a pixel outside it, which the bound rules out, is read from the
+// raster all the same).
 template <int M, bool FAST, int GRP, int NB>
 __device__ __forceinline__ bool stencil_step(const SemArgs& a, const PairConst* __restrict__ P, int m0, int k0, int n,
                                              const double w[3], const double pw[3], const double p2[3], double mag,
                                              float label1, const double* K2, const float2* __restrict__ dl2, int cidx,
-                                             double exk, double fp[NB], double fm[NB]) {
-  int code[2 * NB], idx[2 * NB];
+                                             double exk, double fp[NB], double fm[NB], const float2* box = nullptr,
+                                             const FlatBox* fb = nullptr) {
+  int code[2 * NB], idx[2 * NB], bq[2 * NB];
   double z[2 * NB];
 #pragma unroll
   for (int j = 0; j < 2 * NB; ++j) {
     code[j] = 1;
     idx[j] = cidx;
+    bq[j] = -1;
     z[j] = 0.0;
     if (k0 + j / 2 < n) {
       double pp[3];
       stencil_pp<FAST, GRP>(P, 2 * (m0 + j / 2) + (j & 1), k0 + j / 2, w, pw, p2, pp);
       z[j] = pp[2];
-      int ix = cidx;
-      code[j] = probe_pixel<M, FAST>(a, pp, mag, K2, exk, &ix);
+      int ix = cidx, px = 0, py = 0;
+      code[j] = probe_pixel<M, FAST>(a, pp, mag, K2, exk, &ix, &px, &py);
       idx[j] = code[j] == 2 ? ix : cidx;
+      if (box && code[j] == 2) {
+        const int dx = px - fb->x0, dy = py - fb->y0;
+        if (dx >= 0 && dx < fb->ncol && dy >= 0 && dy < fb->nrow) bq[j] = dy * 3 + dx;
+      }
     }
   }
   float2 s[2 * NB];
 #pragma unroll
-  for (int j = 0; j < 2 * NB; ++j) s[j] = dl2[idx[j]];
+  for (int j = 0; j < 2 * NB; ++j) s[j] = bq[j] >= 0 ? box[bq[j]] : dl2[idx[j]];
   bool ok = true;
 #pragma unroll
   for (int j = 0; j < 2 * NB; ++j) {
@@ -751,14 +771,16 @@ template <int M, bool FAST, int NB>
 __device__ __forceinline__ bool stencil_batched(const SemArgs& a, const PairConst* __restrict__ P, const double w[3],
                                                 const double pw[3], const double p2[3], double mag, float label1,
                                                 const double* K2, const float2* dl2, int cidx, double exk,
-                                                double Jt[12]) {
+                                                double Jt[12], const float2* box = nullptr,
+                                                const FlatBox* fb = nullptr) {
   double jq1[3] = {0.0, 0.0, 0.0}, jt1[3] = {0.0, 0.0, 0.0}, jq2[3] = {0.0, 0.0, 0.0}, jt2[3] = {0.0, 0.0, 0.0};
   bool ok = true;
   if (P->var1) {
 #pragma unroll 1
     for (int k = 0; k < 4; k += NB) {
       double fp[NB], fm[NB];
-      ok &= stencil_step<M, FAST, 0, NB>(a, P, k, k, 4, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm);
+      ok &= stencil_step<M, FAST, 0, NB>(a, P, k, k, 4, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm,
+                                                box, fb);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         if (k + j < 4) {
@@ -772,7 +794,8 @@ __device__ __forceinline__ bool stencil_batched(const SemArgs& a, const PairCons
 #pragma unroll 1
     for (int k = 0; k < 3; k += NB) {
       double fp[NB], fm[NB];
-      ok &= stencil_step<M, FAST, 1, NB>(a, P, 4 + k, k, 3, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm);
+      ok &= stencil_step<M, FAST, 1, NB>(a, P, 4 + k, k, 3, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm,
+                                                box, fb);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         if (k + j < 3) {
@@ -788,7 +811,8 @@ __device__ __forceinline__ bool stencil_batched(const SemArgs& a, const PairCons
 #pragma unroll 1
     for (int k = 0; k < 4; k += NB) {
       double fp[NB], fm[NB];
-      ok &= stencil_step<M, FAST, 2, NB>(a, P, 7 + k, k, 4, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm);
+      ok &= stencil_step<M, FAST, 2, NB>(a, P, 7 + k, k, 4, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm,
+                                                box, fb);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         if (k + j < 4) {
@@ -802,7 +826,8 @@ __device__ __forceinline__ bool stencil_batched(const SemArgs& a, const PairCons
 #pragma unroll 1
     for (int k = 0; k < 3; k += NB) {
       double fp[NB], fm[NB];
-      ok &= stencil_step<M, FAST, 3, NB>(a, P, 11 + k, k, 3, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm);
+      ok &= stencil_step<M, FAST, 3, NB>(a, P, 11 + k, k, 3, w, pw, p2, mag, label1, K2, dl2, cidx, exk, fp, fm,
+                                                box, fb);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         if (k + j < 3) {
@@ -880,10 +905,11 @@ __device__ __forceinline__ void centre_eval(const SemArgs& a, const PairConst* _
 template <int M, bool FAST, int NB>
 __device__ __forceinline__ void stencil_full(const SemArgs& a, const PairConst* __restrict__ P, const Centre& c,
                                              const SemSample& smp, const double* K2, const float2* dl2,
-                                             double Jt[12]) {
+                                             double Jt[12], const float2* box = nullptr,
+                                             const FlatBox* fb = nullptr) {
   if constexpr (NB > 0) {
     const int cidx = c.pc.valid ? c.pc.py * a.W + c.pc.px : 0;
-    if (!stencil_batched<M, FAST, NB>(a, P, c.w, c.pw, c.p2, c.mag, smp.label1, K2, dl2, cidx, c.exk, Jt))
+    if (!stencil_batched<M, FAST, NB>(a, P, c.w, c.pw, c.p2, c.mag, smp.label1, K2, dl2, cidx, c.exk, Jt, box, fb))
       stencil_rolled<M, FAST>(a, P, c.w, c.pw, c.p2, c.mag, smp.pc1, smp.label1, K2, dl2, c.pc, c.exk, Jt);
   } else {
     stencil_rolled<M, FAST>(a, P, c.w, c.pw, c.p2, c.mag, smp.pc1, smp.label1, K2, dl2, c.pc, c.exk, Jt);
@@ -916,10 +942,6 @@ __device__ __forceinline__ void stencil_full(const SemArgs& a, const PairConst* 
 // stencil.  tests/test_semantic_flat_property.py checks the oracle's
 // restatement of this test against the full stencil on >= 1e7 samples.
 // ---------------------------------------------------------------------------
-struct FlatBox {
-  int x0, y0, ncol, nrow;  // reachable pixels (x0 .. x0 + ncol - 1, y0 .. y0 + nrow - 1)
-  double d;                // bound of the depth change
-};
 
 // Bound H(rho) of every second derivative of the distortion map (u, v) ->
 // u + Du(u, v) (and v + Dv) over |(u, v)| <= rho, per unit focal length:
@@ -1368,7 +1390,7 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
 
 // Pass 2: chunk = 64 consecutive entries of one pair's deferred region
 // (chunks past the pair's count exit at once).
-template <int M, bool FAST, int NB>
+template <int M, bool FAST, int NB, bool BOX = false>
 __global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const uint2* __restrict__ chunks,
                                                               const PairConst* __restrict__ pcs,
                                                               const uint32_t* __restrict__ pair_cnt,
@@ -1376,6 +1398,7 @@ __global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const 
                                                               double* __restrict__ pair_blk,
                                                               double* __restrict__ J_out, int write_samples) {
   __shared__ double sJ[64 * kSemRow];
+  __shared__ float2 sbox[BOX ? 64 * 9 : 1];  // BOX: each lane's 3 x 3 box of raster pixels
   const uint2 ch = chunks[blockIdx.x];  // (pair, first entry)
   const uint32_t cnt = pair_cnt[ch.x];
   if (ch.y >= cnt) return;
@@ -1394,7 +1417,21 @@ __global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const 
     Centre c;
     centre_eval<M, FAST>(a, P, smp, K2, dl2, c);
     double Jt[12];
-    stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt);
+    if constexpr (BOX) {
+      // the reachable box (the flat test's bound), read in one round trip:
+      // the stencil's steps then take their pixels from LDS
+      FlatBox fb;
+      if (flat_box<M>(P, c, K2, fb)) {
+        float2* mine = sbox + 9 * lane;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) mine[q] = dl2[flat_index(a, fb, true, q)];
+        stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt, mine, &fb);
+      } else {
+        stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt);
+      }
+    } else {
+      stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt);
+    }
     if (write_samples) {
       double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
 #pragma unroll
@@ -1892,8 +1929,12 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
         if (S->model_tiles[model + 1] == S->model_tiles[model] || nc == 0) continue;
         dispatch_model(model, [&](auto m) {
           constexpr int M = decltype(m)::value;
-          hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4>), dim3(nc), dim3(64), 0, ds, a, S->chunks.ptr + c0,
-                             pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
+          if (ctx->sem_deferred_box)
+            hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4, true>), dim3(nc), dim3(64), 0, ds, a,
+                               S->chunks.ptr + c0, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
+          else
+            hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4>), dim3(nc), dim3(64), 0, ds, a, S->chunks.ptr + c0,
+                               pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
         });
       }
     };

@@ -236,17 +236,20 @@ def test_c4_lm_first_iteration_matches_oracle(gpu):
 
 def test_c3_window_summary_flat_pass_bitwise(gpu):
     """The flat pass deciding samples from the rasters' 3x3 window summaries
-    (semantic_window_summary 1) against the raster-only flat pass at C3 size
-    (4.0M samples): status, residual and Jacobian of every sample bitwise,
-    and the same samples deferred to the full stencil."""
+    (semantic_window_summary 1) and the deferred pass taking its stencil
+    pixels from the once-read 3x3 box (semantic_deferred_box 1) against the
+    raster-only passes at C3 size (4.0M samples): status, residual and
+    Jacobian of every sample bitwise, and the same samples deferred to the
+    full stencil."""
     sc = c2_scene()
     sem = semantic_input(sc, step=10, pairs_per_image=2)
     sc.tvec[5:] += 0.002  # pose errors: some samples change label between pixels
     out = []
     with mi_ba.Context(mi_ba.default_options(), sc.copy(), sem) as ctx:
         ctx.set_tuning("semantic_diag", 1)
-        for ws in (0, 1, 0):
+        for ws, box in ((0, 0), (1, 0), (1, 1), (0, 1)):
             ctx.set_tuning("semantic_window_summary", ws)
+            ctx.set_tuning("semantic_deferred_box", box)
             ctx.evaluate_semantic()
             out.append(ctx.download_semantic())
     for o in out[1:]:

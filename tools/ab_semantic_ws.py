@@ -1,5 +1,7 @@
 """The flat pass with and without the rasters' 3x3 window summaries
-("semantic_window_summary") inside the C4 linearization step (as bench.py):
+("semantic_window_summary"), and the deferred pass with and without the
+once-read 3x3 box ("semantic_deferred_box"), inside the C4 linearization
+step (as bench.py):
 semantic / reprojection kernel times (HIP events) and step wall time over
 interleaved rounds; samples checked bitwise against the raster-only route.
     python tools/ab_semantic_ws.py [--rounds 6] [--reps 10]"""
@@ -23,9 +25,17 @@ ap.add_argument("--reps", type=int, default=10)
 args = ap.parse_args()
 sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
 ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
+CONFIGS = [(0, 0), (1, 0), (1, 1)]
+
+
+def apply(cfg):
+    ctx.set_tuning("semantic_window_summary", cfg[0])
+    ctx.set_tuning("semantic_deferred_box", cfg[1])
+
+
 ref = None
-for ws in (0, 1):
-    ctx.set_tuning("semantic_window_summary", ws)
+for cfg in CONFIGS:
+    apply(cfg)
     ctx.set_tuning("semantic_diag", 1)
     ctx.evaluate_semantic()
     out = ctx.download_semantic()
@@ -33,12 +43,12 @@ for ws in (0, 1):
     if ref is None:
         ref = out
     same = all(np.array_equal(a, b) for a, b in zip(ref[1:], out[1:]))
-    print(json.dumps({"window_summary": ws, "bitwise_equal_incl_deferral": bool(same),
+    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "bitwise_equal_incl_deferral": bool(same),
                       "deferred": int((out[1] >= 0x800).sum())}), flush=True)
-res = {0: [], 1: []}
+res = {c: [] for c in CONFIGS}
 for rnd in range(args.rounds):
-    for ws in (0, 1):
-        ctx.set_tuning("semantic_window_summary", ws)
+    for cfg in CONFIGS:
+        apply(cfg)
         for _ in range(3):
             ctx.linearize()
         ctx.synchronize()
@@ -52,10 +62,10 @@ for rnd in range(args.rounds):
         sj = ctx.kernel_time("semantic_jacobian")
         rj = ctx.kernel_time("reproj_jacobian")
         ctx.set_timing(False)
-        res[ws].append((sj[0] / sj[1], rj[0] / rj[1], wall))
-for ws in (0, 1):
-    a = np.array(res[ws])
-    print(json.dumps({"window_summary": ws, "semantic_ms_median": float(np.median(a[:, 0])),
+        res[cfg].append((sj[0] / sj[1], rj[0] / rj[1], wall))
+for cfg in CONFIGS:
+    a = np.array(res[cfg])
+    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "semantic_ms_median": float(np.median(a[:, 0])),
                       "reproj_ms_median": float(np.median(a[:, 1])), "step_wall_ms_median": float(np.median(a[:, 2])),
                       "rounds": args.rounds, "reps": args.reps}), flush=True)
 ctx.close()

@@ -32,6 +32,9 @@ for stage in "$@"; do
     pcg)
       timeout -k 10 500 python -u tools/ab_pcg_mf.py > gpurun_out/$T/ab_pcg_mf.jsonl 2> gpurun_out/$T/ab_pcg_mf.err || exit 1
       cat gpurun_out/$T/ab_pcg_mf.jsonl ;;
+    lmkeys)
+      timeout -k 10 900 python -u tools/ab_lm_keys.py "" $LMKEYS > gpurun_out/$T/ab_lm_keys.jsonl 2> gpurun_out/$T/ab_lm_keys.err || exit 1
+      cat gpurun_out/$T/ab_lm_keys.jsonl ;;
     ws)
       timeout -k 10 300 python -u tools/ab_semantic_ws.py > gpurun_out/$T/ab_ws.jsonl 2> gpurun_out/$T/ab_ws.err || exit 1
       cat gpurun_out/$T/ab_ws.jsonl ;;
