@@ -529,11 +529,14 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *   "cholesky_solve"        2 sync-free triangular sweeps, one launch per direction
  *                           (default) / 1 hand-written blocked triangular sweeps /
  *                           0 recursive rocBLAS dtrsv + dgemv
- *   "cholesky_spin_log2"    bound of the in-launch flag waits, 2^value polls (default
- *                           24; 0: no polling, so a wait on a flag not already set runs
- *                           out at once — the hook of the timeout test).  A wait that
- *                           runs out makes the solve return MI_BA_ERR_HIP (never a
- *                           silently wrong factor) */
+ *   "cholesky_wait_ms"      bound of each in-launch flag wait of the factor and the
+ *                           triangular sweeps, in wall-clock milliseconds (default
+ *                           5000, at most 40000).  A wait that runs out makes the
+ *                           solve return MI_BA_ERR_HIP (a hard error, never a
+ *                           silently wrong factor)
+ *   "cholesky_spin_log2"    0: no polling, so a wait on a flag not already set runs
+ *                           out at once (the hook of the timeout test); any other
+ *                           value (default 24): the time bound above */
 mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value);
 
 /* Dense Cholesky of a symmetric positive-definite n x n matrix with the

@@ -411,20 +411,28 @@ __global__ __launch_bounds__(kTB) void trsv_bwd_step_kernel(const double* __rest
 // after the flag is seen: an acquire load in the loop would issue an
 // agent-scope cache invalidate (buffer_inv sc1) per poll, from every waiting
 // workgroup, flushing the XCD's cached tiles under the concurrent trailing
-// dgemm.  Bounded by `limit` polls: a lost flag must not leave waves that
-// never finish.  A wait that runs out — or that sees (every 256 polls) that
-// another wait of the call already ran out, so a broken chain drains fast —
-// sets kCholErrWait in the error word and returns; the host reads the word
-// (chol_error) and reports the factor / solution invalid instead of using it.
+// dgemm.  Bounded by elapsed time, `limit` ticks of the constant-rate wall
+// clock (CholWorkspace::wait_ticks, from CholConfig::wait_ms; a poll count
+// would drift with the shader clock): a lost flag must not leave waves that
+// never finish, and a producer held up for a while (a time-shared GPU, the
+// CU-masked side stream) must not fail a factorisation that would complete.
+// limit 0 is the no-polling test hook.  A wait that runs out — or that sees
+// (every 256 polls) that another wait of the call already ran out, so a broken
+// chain drains fast — sets kCholErrWait in the error word and returns; the
+// host reads the word (chol_error) and reports the factor / solution invalid
+// (a hard error: the solve ends with MI_BA_ERR_HIP) instead of using it.
 __device__ __forceinline__ void flag_wait(const unsigned* f, unsigned epoch, unsigned* err, unsigned limit) {
-  for (unsigned spin = 0;; ++spin) {
-    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
-    if (spin >= limit ||
-        ((spin & 255u) == 255u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-      __hip_atomic_fetch_or(err, kCholErrWait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
+  if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+    const uint64_t t0 = wall_clock64();
+    for (unsigned spin = 0;; ++spin) {
+      if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
+      if (limit == 0u || ((spin & 15u) == 15u && wall_clock64() - t0 >= limit) ||
+          ((spin & 255u) == 255u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+        __hip_atomic_fetch_or(err, kCholErrWait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_s_sleep(1);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
@@ -1530,6 +1538,8 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
   destroy();
   device = dev;
   if (hipSetDevice(dev) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&clock_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) clock_khz = 0;
+  spin_limit = wait_ticks(CholConfig{}.wait_ms);
   // The side stream carries the look-ahead's critical path (diagonal factor +
   // panel dtrsm).  A higher priority puts it on a hardware queue of its own:
   // with HIP's round-robin stream -> queue mapping (4 queues per process), a
@@ -1668,7 +1678,7 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   if (ws) {
     ws->tile_factor = c.tile_factor;
     ws->write_through = c.write_through;
-    ws->spin_limit = c.spin_log2 <= 0 ? 0u : (1u << std::min(c.spin_log2, 30));
+    ws->spin_limit = c.spin_log2 <= 0 ? 0u : ws->wait_ticks(c.wait_ms);
     ws->rows_per_group = c.panel_rows_per_group;
     ws->bwd_pairs = c.bwd_pairs;
     ws->group_min_rows = c.panel_group_min_rows;

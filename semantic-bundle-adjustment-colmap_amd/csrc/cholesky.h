@@ -77,11 +77,14 @@ struct CholConfig {
   // rocBLAS dtrsv / dgemv
   int solve = 2;
   // bound of every in-launch flag wait (panel factor, sync-free sweeps):
-  // 2^spin_log2 polls (~64 cycles each), 0 = no polling at all (a wait whose
-  // flag is not already set times out at once: the timeout test's hook).
-  // A wait that runs out records kCholErrWait in the workspace's error word
-  // (chol_error) instead of returning a silently wrong factor or solution.
+  // wait_ms of wall-clock time per wait; spin_log2 0 = no polling at all (a
+  // wait whose flag is not already set times out at once: the timeout test's
+  // hook), any other value = the time bound.  A wait that runs out records
+  // kCholErrWait in the workspace's error word (chol_error) instead of
+  // returning a silently wrong factor or solution; the solve reports it as a
+  // hard error.
   int spin_log2 = 24;
+  int wait_ms = 5000;
   // own_diag 6: below-diagonal row tiles per panel workgroup while the rows
   // below the panel number at least panel_group_min_rows (1: one workgroup per
   // row tile throughout).  The resident panel workgroups cost the concurrent
@@ -123,7 +126,12 @@ struct CholWorkspace {
   double* tbuf = nullptr;       // own_diag 7: [max_n * 512] copy of the panel below it
   int tbuf_rows = 0;
   unsigned* err = nullptr;      // [4] error word (kCholErr* bits) of the in-launch flag waits
-  unsigned spin_limit = 1u << 24;  // polls per flag wait (CholConfig::spin_log2)
+  unsigned spin_limit = 0;  // wall-clock ticks per flag wait (CholConfig::wait_ms; 0 = no polling)
+  int clock_khz = 0;        // wall-clock rate of the device (hipDeviceAttributeWallClockRate)
+  unsigned wait_ticks(int ms) const {
+    const uint64_t t = (uint64_t)(ms > 0 ? ms : 1) * (uint64_t)(clock_khz > 0 ? clock_khz : 100000);
+    return (unsigned)(t < 0xffffffffull ? t : 0xffffffffull);
+  }
   int rows_per_group = 1;          // CholConfig::panel_rows_per_group
   bool bwd_pairs = false;          // CholConfig::bwd_pairs
   int group_min_rows = 6000;       // CholConfig::panel_group_min_rows

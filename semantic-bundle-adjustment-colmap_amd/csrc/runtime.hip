@@ -2060,6 +2060,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->fused_rhs = value != 0;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "cholesky_wait_ms") == 0 && value >= 1 && value <= 40000) {
+    ctx->chol.wait_ms = value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_spin_log2") == 0 && value >= 0 && value <= 30) {
     ctx->chol.spin_log2 = value;
     return MI_BA_OK;
