@@ -9,6 +9,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -37,12 +38,14 @@ def main():
     with mi_ba.Context(opts, sc, sem) as ctx:
         if dist is not None:
             ctx.set_host_reducer(a.rank, a.world, mc.gloo_reducer())
+        t0 = time.perf_counter()
         s = ctx.solve()
+        solve_s = time.perf_counter() - t0
         ctx.writeback()
     with open(a.out, "w") as f:
         json.dump({"rank": a.rank, "world": a.world, "eta": opts.eta, "initial_cost": s.initial_cost,
                    "final_cost": s.final_cost, "successful": s.num_successful_steps,
-                   "unsuccessful": s.num_unsuccessful_steps, "cg_iterations": s.num_linear_solver_iterations,
+                   "unsuccessful": s.num_unsuccessful_steps, "cg_iterations": s.num_linear_solver_iterations, "solve_s": solve_s,
                    "qvec0": sc.qvec[:50].tolist(), "tvec0": sc.tvec[:50].tolist()}, f)
     if dist is not None:
         dist.destroy_process_group()

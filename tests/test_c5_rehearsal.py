@@ -53,3 +53,9 @@ def test_c5_two_rank_pcg_matches_one_rank(gpu, tmp_path):
         assert r["final_cost"] < r["initial_cost"]
     assert res[0]["qvec0"] == res[1]["qvec0"] and res[0]["tvec0"] == res[1]["tvec0"]
     assert res[0]["cg_iterations"] == res[1]["cg_iterations"]
+    out = os.environ.get("MI_BA_PROFILE_DIR")  # the GPU session's record of the comparison
+    if out:
+        with open(os.path.join(out, "c5_rehearsal.json"), "w") as f:
+            json.dump({"one_rank": {k: v for k, v in ref.items() if k not in ("qvec0", "tvec0")},
+                       "two_ranks": [{k: v for k, v in r.items() if k not in ("qvec0", "tvec0")} for r in res]}, f,
+                      indent=1)

@@ -15,6 +15,7 @@ T=${1:?tag}
 shift
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
+export MI_BA_PROFILE_DIR=$PWD/gpurun_out/$T
 for stage in "$@"; do
   echo "== $stage $(date +%T)"
   case $stage in
