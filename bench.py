@@ -250,6 +250,7 @@ def roofline_semantic(config, ns, avg_ms):
            "fp64_ops_per_launch": flops,
            "hbm_achieved_GBs": hbm / t / 1e9 if hbm else None, "hbm_frac": f_hbm if hbm else None,
            "traffic": hbm, "traffic_unit": "bytes/launch",
+           "traffic_bytes_per_sample": hbm / ns if hbm and ns else None,
            "algorithmic_bytes_per_sample_survey": 128, "algorithmic_bytes_per_sample_fused": 40,
            "algorithmic_GBs_survey": 128.0 * ns / t / 1e9, "algorithmic_GBs_fused": 40.0 * ns / t / 1e9,
            "samples_per_launch": ns, "avg_launch_ms": avg_ms, "pmc_source": src}

@@ -1930,7 +1930,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->lin_overlap = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "semantic_diag") == 0 && (value == 0 || value == 1)) {
+  if (std::strcmp(key, "semantic_diag") == 0 && value >= 0 && value <= 2) {
     ctx->sem_diag = value;
     return MI_BA_OK;
   }

@@ -1357,7 +1357,7 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
     cost = 0.5 * (a.weight * rho[0]);
     if (write_samples) {
       r_out[n] = c.r;
-      status_out[n] = c.st + ((write_samples & 2) && deferred ? 0x1000 : 0);
+      status_out[n] = c.st + ((write_samples & 2) && deferred ? 0x1000 : 0) + ((write_samples & 4) && decided ? 0x4000 : 0);
       if (!deferred) {
         double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
 #pragma unroll
@@ -1922,7 +1922,7 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
                      ctx->sem_variant == 6 ? S->pair_cnt.ptr : nullptr);
   const bool split = deferred_stream != nullptr && ctx->sem_variant == 6;
   if (ctx->sem_variant == 6) {
-    const int ws = write_samples ? 1 | (ctx->sem_diag ? 2 : 0) : 0;
+    const int ws = write_samples ? 1 | (ctx->sem_diag ? 2 : 0) | (ctx->sem_diag == 2 ? 4 : 0) : 0;
     auto deferred = [&](hipStream_t ds) {
       for (int model = 0; model < kNumModels; ++model) {
         const int c0 = S->model_chunks[model], nc = S->model_chunks[model + 1] - c0;
@@ -1971,7 +1971,7 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
       auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0, pcs, S->pair_blk.ptr,
                            S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr,
-                           write_samples ? 1 | (ctx->sem_diag ? 2 : 0) : 0);
+                           write_samples ? 1 | (ctx->sem_diag ? 2 : 0) | (ctx->sem_diag == 2 ? 4 : 0) : 0);
       };
       switch (ctx->sem_variant) {
         case 0: launch(semantic_linearize_kernel<M, false>); break;

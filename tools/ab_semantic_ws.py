@@ -33,18 +33,33 @@ def apply(cfg):
     ctx.set_tuning("semantic_deferred_box", cfg[1])
 
 
+def decode(st):
+    """semantic_diag 2 marks: +0x1000 deferred, +0x4000 decided by a window summary"""
+    ws = st >= 0x2800
+    st = np.where(ws, st - 0x4000, st)
+    d = st >= 0x800
+    return np.where(d, st - 0x1000, st), d, ws
+
+
 ref = None
 for cfg in CONFIGS:
     apply(cfg)
-    ctx.set_tuning("semantic_diag", 1)
+    ctx.set_tuning("semantic_diag", 2)
     ctx.evaluate_semantic()
     out = ctx.download_semantic()
     ctx.set_tuning("semantic_diag", 0)
+    st, d, ws = decode(out[1])
+    out = (out[0], st) + tuple(out[2:])
     if ref is None:
         ref = out
     same = all(np.array_equal(a, b) for a, b in zip(ref[1:], out[1:]))
-    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "bitwise_equal_incl_deferral": bool(same),
-                      "deferred": int((out[1] >= 0x800).sum())}), flush=True)
+    n = len(st)
+    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "bitwise_equal": bool(same),
+                      "samples": n, "deferred": int(d.sum()), "window_decided": int(ws.sum()),
+                      "window_decided_valid": int((ws & (st == mi_ba.VALID)).sum()),
+                      "status_valid": int((st == mi_ba.VALID).sum()),
+                      "status_invalid_depth": int((st == mi_ba.INVALID_DEPTH).sum()),
+                      "status_other": int(((st != mi_ba.VALID) & (st != mi_ba.INVALID_DEPTH)).sum())}), flush=True)
 res = {c: [] for c in CONFIGS}
 for rnd in range(args.rounds):
     for cfg in CONFIGS:

@@ -9,7 +9,7 @@
 # trace (rocprofv3 kernel trace of the bench command), bench (the bench line),
 # jacsweep (in-step times of the tools-build Jacobian variants JACV), pcg
 # (matrix-free PCG product A/B),
-# smoke
+# pmcs (semantic PMC passes + summary), smoke
 set -o pipefail
 T=${1:?tag}
 shift
@@ -42,6 +42,9 @@ for stage in "$@"; do
     chol)
       timeout -k 10 600 python -u tools/ab_chol_keys.py "" $CHOL > gpurun_out/$T/ab_chol.jsonl 2> gpurun_out/$T/ab_chol.err || exit 1
       cat gpurun_out/$T/ab_chol.jsonl ;;
+    pmcs)
+      timeout -k 10 900 bash tools/pmc_semantic.sh gpurun_out/$T/pmcs > gpurun_out/$T/pmcs.log 2>&1 || { tail -5 gpurun_out/$T/pmcs.log; exit 1; }
+      python tools/summarize_pmc_semantic.py gpurun_out/$T/pmcs gpurun_out/$T/c4_semantic_pmc.json && cat gpurun_out/$T/c4_semantic_pmc.json ;;
     trace)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/bench_trace -o run -- python3 bench.py --lm-iters 0 --no-cpu-baseline > gpurun_out/$T/bench_trace.log 2>&1 || exit 1
       tail -c 300 gpurun_out/$T/bench_trace.log ;;
