@@ -1940,6 +1940,12 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     if (!ctx->sem) return value ? MI_BA_ERR_STATE : MI_BA_OK;
     return semantic_set_window_summary(ctx, value != 0);
   }
+  // 1: the flat pass reads the label planes first (8-bit label indices + 8 x 8
+  // tile depth ranges; ~1.1 GB at C4), 0: not
+  if (std::strcmp(key, "semantic_label_planes") == 0 && (value == 0 || value == 1)) {
+    if (!ctx->sem) return value ? MI_BA_ERR_STATE : MI_BA_OK;
+    return semantic_set_label_planes(ctx, value != 0);
+  }
   if (std::strcmp(key, "semantic_deferred_box") == 0 && (value == 0 || value == 1)) {
     ctx->sem_deferred_box = value != 0;
     return MI_BA_OK;

@@ -49,6 +49,15 @@ struct SemanticState {
   int nslots = 0;
   DevArray<float4> wsum;                   // [slot][H][W] 3x3 window summaries ("semantic_window_summary")
   bool use_wsum = false;
+  // label planes ("semantic_label_planes"): the flat pass's first reads.
+  // lab8 = each raster pixel's label as an index into pal (the rasters'
+  // distinct label bit patterns, <= 256), dtile = (min, max) depth over each
+  // 8 x 8 pixel tile extended by 2 pixels right and down (every 3 x 3 box
+  // whose top-left pixel lies in the tile), NaN when a depth in it is NaN
+  DevArray<uint8_t> lab8;                  // [slot][H][W]
+  DevArray<float2> dtile;                  // [slot][ceil(H/8)][ceil(W/8)]
+  DevArray<float> pal;                     // [256]
+  bool use_lp = false;
   DevArray<uint32_t> raster_slot;          // image -> raster slot
   DevArray<double> r;                      // [ns]
   DevArray<int32_t> status;                // [ns]
@@ -89,6 +98,10 @@ mi_ba_status semantic_export(mi_ba_context* ctx, int32_t image1, int32_t image2,
 // Build (on) or drop (off) the rasters' 3x3 window summaries the flat pass
 // decides most samples from without reading the raster.
 mi_ba_status semantic_set_window_summary(mi_ba_context* ctx, bool on);
+// Build (on) or drop (off) the label planes (an 8-bit label index plane with
+// its palette, and 8 x 8 tile depth ranges) the flat pass reads first: on
+// with more than 256 distinct labels leaves them off (MI_BA_OK).
+mi_ba_status semantic_set_label_planes(mi_ba_context* ctx, bool on);
 // Cost only, at parameters qt (candidate evaluation).
 void semantic_cost(mi_ba_context* ctx, const double* qt, const double* cam, double* d_cost);
 // Fold the pair blocks into the Schur-Jacobi pose blocks, b and diag(U).

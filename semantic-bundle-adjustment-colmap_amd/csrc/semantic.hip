@@ -39,6 +39,10 @@ struct SemArgs {
   const uint32_t* raster_slot;
   const float2* dl;   // interleaved (depth, label) rasters [slot][H][W]
   const float4* wsum; // 3x3 window summaries [slot][H][W] (window_summary_kernel) or null
+  const uint8_t* lab8; // label planes (label_index_kernel) or null
+  const float2* dtile; // [slot][TH][TW] tile depth ranges (depth_tile_kernel)
+  const float* pal;    // [256] label values of the lab8 indices
+  int TH, TW;
   int H, W;
   double threshold;
   double rel_step;
@@ -1277,7 +1281,86 @@ __global__ __launch_bounds__(256) void window_summary_kernel(const float2* __res
   out[k] = o;
 }
 
-template <int M, bool FAST, bool WS = false>
+// Label planes.  The palette: every distinct label bit pattern of the
+// rasters in an open-addressed table of 256 keys (bit pattern | 1 << 32, 0 =
+// empty); more than 256 distinct labels sets *overflow and the planes are not
+// used.  Comparing the sample's label with pal[index] is the comparison with
+// the raster's label itself (the same bits), NaN and signed zeros included.
+__device__ __forceinline__ uint32_t pal_hash(uint32_t b) {
+  b ^= b >> 16;
+  b *= 0x7feb352du;
+  b ^= b >> 15;
+  return b & 255u;
+}
+
+__global__ __launch_bounds__(256) void label_palette_kernel(const float2* __restrict__ dl, int64_t n,
+                                                            unsigned long long* keys, unsigned* overflow) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t bits = __float_as_uint(dl[k].y);
+  const unsigned long long key = (unsigned long long)bits | (1ull << 32);
+  uint32_t h = pal_hash(bits);
+  for (int probe = 0; probe < 256; ++probe, h = (h + 1u) & 255u) {
+    const unsigned long long cur = __hip_atomic_load(keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) return;
+    if (cur == 0ull) {
+      const unsigned long long prev = atomicCAS(keys + h, 0ull, key);
+      if (prev == 0ull || prev == key) return;
+    }
+  }
+  atomicOr(overflow, 1u);
+}
+
+__global__ __launch_bounds__(256) void label_index_kernel(const float2* __restrict__ dl, int64_t n,
+                                                          const unsigned long long* __restrict__ keys,
+                                                          uint8_t* __restrict__ lab8) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t bits = __float_as_uint(dl[k].y);
+  const unsigned long long key = (unsigned long long)bits | (1ull << 32);
+  uint32_t h = pal_hash(bits);
+  for (int probe = 0; probe < 256 && keys[h] != key; ++probe) h = (h + 1u) & 255u;
+  lab8[k] = (uint8_t)h;
+}
+
+__global__ __launch_bounds__(256) void depth_tile_kernel(const float2* __restrict__ dl, int H, int W, int TH, int TW,
+                                                         int64_t n, float2* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  const int64_t per = (int64_t)TH * TW;
+  const int64_t slot = k / per;
+  const int rem = (int)(k - slot * per);
+  const int ty = rem / TW, tx = rem - ty * TW;
+  const float2* base = dl + slot * H * (int64_t)W;
+  float dmin = __builtin_inff(), dmax = -__builtin_inff();
+  bool nan = false;
+  const int y1 = min(8 * ty + 10, H), x1 = min(8 * tx + 10, W);
+  for (int y = 8 * ty; y < y1; ++y)
+    for (int x = 8 * tx; x < x1; ++x) {
+      const float d = base[(int64_t)y * W + x].x;
+      nan = nan || d != d;
+      dmin = fminf(dmin, d);
+      dmax = fmaxf(dmax, d);
+    }
+  out[k] = nan ? make_float2(__builtin_nanf(""), __builtin_nanf("")) : make_float2(dmin, dmax);
+}
+
+// The depth side of every pixel of a box in one tile: 1 when every depth in
+// [dmin, dmax] passes the depth test with the flat test's margin (|d - z| is
+// convex in d: its maximum over the range is at an end), 2 when every depth
+// fails it with the margin, 0 undecided (a NaN range included).
+__device__ __forceinline__ int tile_depth_side(const SemArgs& a, const FlatBox& fb, float2 dr, double z, double mag) {
+  const double dmin = (double)dr.x, dmax = (double)dr.y;
+  if (!(dmin <= dmax)) return 0;
+  const double margin = fb.d + 1e-9 * (1.0 + fmax(fabs(dmin), fabs(dmax)) + mag);
+  const double far = fmax(fabs(dmax - z), fabs(dmin - z));
+  if (a.threshold - far > margin) return 1;
+  const double nearest = (z >= dmin && z <= dmax) ? 0.0 : fmin(fabs(dmin - z), fabs(dmax - z));
+  if (nearest - a.threshold > margin) return 2;
+  return 0;
+}
+
+template <int M, bool FAST, bool WS = false, bool LP = false>
 __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const SemTile* __restrict__ tiles,
                                                                const PairConst* __restrict__ pcs,
                                                                uint32_t* __restrict__ pair_cnt,
@@ -1287,6 +1370,7 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
                                                                int32_t* __restrict__ status_out,
                                                                double* __restrict__ J_out, int write_samples) {
   __shared__ double sred[kBlock / 64];
+  __shared__ float spal[LP ? 256 : 1];
   const SemTile t = tiles[blockIdx.x];
   const PairConst* __restrict__ P = pcs + t.pair;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1296,6 +1380,11 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
   const double* K2 = P->K2;
   double cost = 0.0;
   bool deferred = false;
+  if constexpr (LP) {
+    static_assert(kBlock >= 256, "one palette entry per thread");
+    spal[tid] = a.pal[tid];
+    __syncthreads();
+  }
   if (active) {
     const SemSample smp = a.samples[n];
     // centre geometry (reference sequence, as centre_eval / project_centre)
@@ -1325,15 +1414,45 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
     const bool cin = !(cpx < 0 || cpx >= a.W || cpy < 0 || cpy >= a.H);
     FlatBox fb;
     const bool cand = flat_box<M>(P, c, K2, fb);
-    bool decided = false;
-    if constexpr (WS) {
-      // one 16-B read of the window holding the box (its top-left pixel)
-      if (cand && fb.x0 >= 0 && fb.y0 >= 0 && fb.x0 + 2 < a.W && fb.y0 + 2 < a.H) {
-        const float4 w = a.wsum[(size_t)P->slot * a.H * a.W + (size_t)fb.y0 * a.W + fb.x0];
-        decided = window_decides(a, fb, w, c.p2[2], c.mag, smp.label1, &c.st, &c.r);
+    bool decided = false;   // the centre outcome and the flat test are settled without the raster
+    bool resolved = false;  // the centre outcome is settled (the flat test may have failed)
+    if constexpr (LP) {
+      // label planes: one 8-B tile depth range (a line shared by the wave's
+      // neighbouring samples) settles the depth test of the whole box; on the
+      // valid side the box's labels come from the 1-B label plane
+      if (cand && fb.x0 >= 0 && fb.y0 >= 0 && fb.x0 + fb.ncol <= a.W && fb.y0 + fb.nrow <= a.H && cpx >= fb.x0 &&
+          cpx < fb.x0 + fb.ncol && cpy >= fb.y0 && cpy < fb.y0 + fb.nrow) {
+        const float2 dr = a.dtile[((size_t)P->slot * a.TH + (fb.y0 >> 3)) * a.TW + (fb.x0 >> 3)];
+        const int side = tile_depth_side(a, fb, dr, c.p2[2], c.mag);
+        if (side == 2) {
+          c.st = MI_BA_INVALID_DEPTH;
+          c.r = 0.0;
+          decided = resolved = true;
+        } else if (side == 1) {
+          const uint8_t* lp = a.lab8 + (size_t)P->slot * a.H * a.W + (size_t)fb.y0 * a.W + fb.x0;
+          const uint8_t lc = lp[(size_t)(cpy - fb.y0) * a.W + (cpx - fb.x0)];
+          uint8_t L[9];
+#pragma unroll
+          for (int q = 0; q < 9; ++q) L[q] = (q % 3 < fb.ncol && q / 3 < fb.nrow) ? lp[(size_t)(q / 3) * a.W + q % 3] : lc;
+          c.st = MI_BA_VALID;
+          c.r = (smp.label1 == spal[lc]) ? 0.0 : 1.0;
+          bool flat = true;
+#pragma unroll
+          for (int q = 0; q < 9; ++q) flat = flat && ((smp.label1 == spal[L[q]]) ? 0.0 : 1.0) == c.r;
+          resolved = true;
+          decided = flat;
+          deferred = !flat;
+        }
       }
     }
-    if (!decided) {
+    if constexpr (WS) {
+      // one 16-B read of the window holding the box (its top-left pixel)
+      if (!resolved && cand && fb.x0 >= 0 && fb.y0 >= 0 && fb.x0 + 2 < a.W && fb.y0 + 2 < a.H) {
+        const float4 w = a.wsum[(size_t)P->slot * a.H * a.W + (size_t)fb.y0 * a.W + fb.x0];
+        decided = resolved = window_decides(a, fb, w, c.p2[2], c.mag, smp.label1, &c.st, &c.r);
+      }
+    }
+    if (!resolved) {
       // every raster read of the sample in one round trip: the centre pixel and the box
       const float2 sc = dl2[cin ? cpy * a.W + cpx : 0];
       float2 s[9];
@@ -1660,6 +1779,11 @@ SemArgs make_args(mi_ba_context* ctx, const double* qt, const double* cam) {
   a.raster_slot = S->raster_slot.ptr;
   a.dl = S->dl.ptr;
   a.wsum = S->use_wsum ? S->wsum.ptr : nullptr;
+  a.lab8 = S->use_lp ? S->lab8.ptr : nullptr;
+  a.dtile = S->use_lp ? S->dtile.ptr : nullptr;
+  a.pal = S->use_lp ? S->pal.ptr : nullptr;
+  a.TH = (S->H + 7) / 8;
+  a.TW = (S->W + 7) / 8;
   a.H = S->H;
   a.W = S->W;
   a.threshold = S->depth_threshold;
@@ -1893,6 +2017,63 @@ mi_ba_status semantic_set_window_summary(mi_ba_context* ctx, bool on) {
   return MI_BA_OK;
 }
 
+mi_ba_status semantic_set_label_planes(mi_ba_context* ctx, bool on) {
+  SemanticState* S = ctx->sem;
+  if (!S) return MI_BA_ERR_STATE;
+  if (!on) {
+    S->lab8.release();
+    S->dtile.release();
+    S->pal.release();
+    S->use_lp = false;
+    return MI_BA_OK;
+  }
+  if (S->use_lp) return MI_BA_OK;
+  const int64_t n = (int64_t)S->nslots * S->H * S->W;
+  if (n <= 0) return MI_BA_OK;
+  const int TH = (S->H + 7) / 8, TW = (S->W + 7) / 8;
+  const int64_t nt = (int64_t)S->nslots * TH * TW;
+  DevArray<unsigned long long> keys;
+  DevArray<unsigned> overflow;
+  if (keys.alloc(256) || overflow.alloc(1) || S->lab8.alloc((size_t)n) || S->dtile.alloc((size_t)nt) ||
+      S->pal.alloc(256)) {
+    (void)hipGetLastError();
+    S->lab8.release();
+    S->dtile.release();
+    S->pal.release();
+    return MI_BA_ERR_OUT_OF_MEMORY;
+  }
+  hipStream_t s = ctx->stream;
+  const unsigned g = (unsigned)((n + 255) / 256);
+  if (hipMemsetAsync(keys.ptr, 0, keys.bytes(), s) != hipSuccess ||
+      hipMemsetAsync(overflow.ptr, 0, overflow.bytes(), s) != hipSuccess)
+    return MI_BA_ERR_HIP;
+  hipLaunchKernelGGL(label_palette_kernel, dim3(g), dim3(256), 0, s, S->dl.ptr, n, keys.ptr, overflow.ptr);
+  unsigned long long hk[256];
+  unsigned ov = 0;
+  if (hipGetLastError() != hipSuccess || hipMemcpyAsync(hk, keys.ptr, sizeof(hk), hipMemcpyDeviceToHost, s) ||
+      hipMemcpyAsync(&ov, overflow.ptr, sizeof(ov), hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
+    return MI_BA_ERR_HIP;
+  if (ov) {  // more than 256 distinct labels: the flat pass reads the rasters
+    S->lab8.release();
+    S->dtile.release();
+    S->pal.release();
+    return MI_BA_OK;
+  }
+  float hp[256];
+  for (int k = 0; k < 256; ++k) {
+    const uint32_t b = (uint32_t)(hk[k] & 0xffffffffull);
+    std::memcpy(&hp[k], &b, 4);
+  }
+  hipLaunchKernelGGL(label_index_kernel, dim3(g), dim3(256), 0, s, S->dl.ptr, n, keys.ptr, S->lab8.ptr);
+  hipLaunchKernelGGL(depth_tile_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, S->dl.ptr, S->H, S->W,
+                     TH, TW, nt, S->dtile.ptr);
+  if (hipGetLastError() != hipSuccess || hipMemcpyAsync(S->pal.ptr, hp, sizeof(hp), hipMemcpyHostToDevice, s) ||
+      hipStreamSynchronize(s))
+    return MI_BA_ERR_HIP;
+  S->use_lp = true;
+  return MI_BA_OK;
+}
+
 void semantic_destroy(mi_ba_context* ctx) {
   if (!ctx->sem) return;
   delete ctx->sem;
@@ -1943,7 +2124,11 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
       if (nt == 0) continue;
       dispatch_model(model, [&](auto m) {
         constexpr int M = decltype(m)::value;
-        if (a.wsum)
+        if (a.lab8)
+          hipLaunchKernelGGL((semantic_flat_kernel<M, true, false, true>), dim3(nt), dim3(kBlock), 0, s, a,
+                             S->tiles.ptr + t0, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr,
+                             S->status.ptr, S->J.ptr, ws);
+        else if (a.wsum)
           hipLaunchKernelGGL((semantic_flat_kernel<M, true, true>), dim3(nt), dim3(kBlock), 0, s, a,
                              S->tiles.ptr + t0, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr,
                              S->status.ptr, S->J.ptr, ws);

@@ -236,7 +236,8 @@ def test_c4_lm_first_iteration_matches_oracle(gpu):
 
 def test_c3_window_summary_flat_pass_bitwise(gpu):
     """The flat pass deciding samples from the rasters' 3x3 window summaries
-    (semantic_window_summary 1) and the deferred pass taking its stencil
+    (semantic_window_summary 1) or from the label planes (8-bit label indices
+    + tile depth ranges, semantic_label_planes 1) and the deferred pass taking its stencil
     pixels from the once-read 3x3 box (semantic_deferred_box 1) against the
     raster-only passes at C3 size (4.0M samples): status, residual and
     Jacobian of every sample bitwise, and the same samples deferred to the
@@ -247,9 +248,10 @@ def test_c3_window_summary_flat_pass_bitwise(gpu):
     out = []
     with mi_ba.Context(mi_ba.default_options(), sc.copy(), sem) as ctx:
         ctx.set_tuning("semantic_diag", 1)
-        for ws, box in ((0, 0), (1, 0), (1, 1), (0, 1)):
+        for ws, box, lp in ((0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 1, 0), (0, 0, 1), (1, 1, 1)):
             ctx.set_tuning("semantic_window_summary", ws)
             ctx.set_tuning("semantic_deferred_box", box)
+            ctx.set_tuning("semantic_label_planes", lp)
             ctx.evaluate_semantic()
             out.append(ctx.download_semantic())
     for o in out[1:]:

@@ -1,5 +1,5 @@
 """The flat pass with and without the rasters' 3x3 window summaries
-("semantic_window_summary"), and the deferred pass with and without the
+("semantic_window_summary") or the label planes ("semantic_label_planes"), and the deferred pass with and without the
 once-read 3x3 box ("semantic_deferred_box"), inside the C4 linearization
 step (as bench.py):
 semantic / reprojection kernel times (HIP events) and step wall time over
@@ -25,12 +25,13 @@ ap.add_argument("--reps", type=int, default=10)
 args = ap.parse_args()
 sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
 ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
-CONFIGS = [(0, 0), (1, 0), (1, 1)]
+CONFIGS = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 0, 1), (0, 1, 1)]
 
 
 def apply(cfg):
     ctx.set_tuning("semantic_window_summary", cfg[0])
     ctx.set_tuning("semantic_deferred_box", cfg[1])
+    ctx.set_tuning("semantic_label_planes", cfg[2])
 
 
 def decode(st):
@@ -54,7 +55,7 @@ for cfg in CONFIGS:
         ref = out
     same = all(np.array_equal(a, b) for a, b in zip(ref[1:], out[1:]))
     n = len(st)
-    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "bitwise_equal": bool(same),
+    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "label_planes": cfg[2], "bitwise_equal": bool(same),
                       "samples": n, "deferred": int(d.sum()), "window_decided": int(ws.sum()),
                       "window_decided_valid": int((ws & (st == mi_ba.VALID)).sum()),
                       "status_valid": int((st == mi_ba.VALID).sum()),
@@ -80,7 +81,7 @@ for rnd in range(args.rounds):
         res[cfg].append((sj[0] / sj[1], rj[0] / rj[1], wall))
 for cfg in CONFIGS:
     a = np.array(res[cfg])
-    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "semantic_ms_median": float(np.median(a[:, 0])),
+    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "label_planes": cfg[2], "semantic_ms_median": float(np.median(a[:, 0])),
                       "reproj_ms_median": float(np.median(a[:, 1])), "step_wall_ms_median": float(np.median(a[:, 2])),
                       "rounds": args.rounds, "reps": args.reps}), flush=True)
 ctx.close()
