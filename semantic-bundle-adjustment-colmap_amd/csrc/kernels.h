@@ -18,6 +18,7 @@ struct SemDevice;  // defined in semantic.h
 // also zeroes zero[0..nzero) when zero is given
 void launch_pack_images(const DevProblem& p, double* rec, hipStream_t s, double* zero = nullptr, int nzero = 0);
 void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s);
+void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s);
 int reproj_grid(int64_t nb);
 
 // Cost 0.5*sum(rho) of every reduced block at parameters (qt, cam, X).

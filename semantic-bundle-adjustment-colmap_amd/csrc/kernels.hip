@@ -2851,6 +2851,29 @@ inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 
 // cost partials of the reprojection kernels: one per 64 blocks
 int reproj_grid(int64_t nb) { return (int)grid_for(nb, 64); }
 
+// Reads a byte range (16 B per lane, grid-stride) and drops the values: a
+// warm-up of the reprojection kernel's streamed inputs in the memory-side
+// cache (A/B "jac_prefetch").  The sink is written only for an impossible sum.
+__global__ __launch_bounds__(256) void touch_kernel(const uint4* __restrict__ a, int64_t n16, unsigned* sink) {
+  unsigned acc = 0u;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n16; k += (int64_t)gridDim.x * 256) {
+    const uint4 v = a[k];  // a plain load: allocates in the caches
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9e3779b9u && n16 < 0) *sink = acc;
+}
+
+void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s) {
+  auto touch = [&](const void* ptr, int64_t bytes) {
+    if (!ptr || bytes < 16) return;
+    hipLaunchKernelGGL(touch_kernel, dim3(2048), dim3(256), 0, s, reinterpret_cast<const uint4*>(ptr), bytes / 16, sink);
+  };
+  touch(p.obs_xy, p.nb * 16);
+  touch(p.obs_img, p.nb * 4);
+  touch(p.obs_pt, p.nb * 4);
+  touch(p.X, p.num_points * 24);
+}
+
 void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s) {
   if (p.nb == 0) return;
   const unsigned g = grid_for(p.nb, kBlock);

@@ -15,6 +15,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <cmath>
 #include <cstdio>
@@ -892,6 +895,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
   }
+  if (ctx->jac_prefetch) launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), s);
   timer_begin(ctx, "reproj_jacobian", &stop);
   launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->partial.ptr, s);
   timer_end(ctx, stop);
@@ -1859,27 +1863,60 @@ mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t wo
   if (ctx->comm_failed) return MI_BA_ERR_STATE;
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
-  // non-blocking: a peer that never joins ends the set-up at the deadline
-  // (MI_BA_ERR_HIP) instead of blocking the caller forever
-  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  cfg.blocking = 0;
-  const double deadline = now_s() + 1e-3 * ctx->comm_timeout_ms;
-  const ncclResult_t r = ncclCommInitRankConfig(&ctx->comm, world, u, rank, &cfg);
-  if (r != ncclSuccess && r != ncclInProgress) {
-    if (ctx->comm) (void)ncclCommAbort(ctx->comm);
-    ctx->comm = nullptr;
-    return MI_BA_ERR_HIP;
+  // The set-up runs on a helper thread: RCCL's bootstrap can block inside the
+  // init call itself (and an abort of a half-initialised communicator can wait
+  // on it) while a peer has not joined, so the caller waits for the helper
+  // only until the deadline and then returns MI_BA_ERR_HIP with the context
+  // still single-rank.  An abandoned helper aborts the communicator it may
+  // still get (the process may also end with it blocked; it holds nothing of
+  // the context).  The communicator is non-blocking: its collectives are
+  // polled against the same deadline (comm_settle, comm_wait_stream).
+  struct InitJob {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclResult_t res = ncclInternalError;
+    ncclComm_t comm = nullptr;
+  };
+  auto job = std::make_shared<InitJob>();
+  const int dev = ctx->device;
+  std::thread([job, u, world, rank, dev]() {
+    ncclComm_t c = nullptr;
+    ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+    if (r == ncclSuccess) {
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      cfg.blocking = 0;
+      ncclUniqueId uu = u;
+      r = ncclCommInitRankConfig(&c, world, uu, rank, &cfg);
+      while (r == ncclInProgress || r == ncclSuccess) {
+        ncclResult_t e = ncclSuccess;
+        if (!c || ncclCommGetAsyncError(c, &e) != ncclSuccess) { r = ncclInternalError; break; }
+        if (e != ncclInProgress) { r = e; break; }
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+      }
+    }
+    bool abandoned;
+    {
+      std::lock_guard<std::mutex> g(job->m);
+      job->done = true;
+      job->res = r;
+      job->comm = c;
+      abandoned = job->abandoned;
+    }
+    job->cv.notify_all();
+    if ((abandoned || r != ncclSuccess) && c) (void)ncclCommAbort(c);
+  }).detach();
+  bool ok;
+  {
+    std::unique_lock<std::mutex> g(job->m);
+    job->cv.wait_for(g, std::chrono::milliseconds(std::max(1, ctx->comm_timeout_ms)), [&] { return job->done; });
+    ok = job->done && job->res == ncclSuccess && job->comm;
+    if (!job->done) job->abandoned = true;
+    if (ok) ctx->comm = job->comm;
   }
+  if (!ok) return MI_BA_ERR_HIP;  // the context stays usable as a single-rank context
   ctx->rank = rank;
   ctx->world = world;
-  mi_ba_status st = comm_settle(ctx, deadline);
-  if (st != MI_BA_OK) {
-    // the context stays usable as a single-rank context
-    ctx->comm_failed = false;
-    ctx->rank = 0;
-    ctx->world = 1;
-    return st;
-  }
   return reduce_fixed_cost(ctx);
 }
 
@@ -1918,6 +1955,11 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   // test hook: hold the stream ahead of every RCCL collective for `value` ms
   if (std::strcmp(key, "comm_stall_ms") == 0 && value >= 0 && value <= 60000) {
     ctx->comm_stall_ms = value;
+    return MI_BA_OK;
+  }
+  // diagnostic: read the reprojection kernel's streamed inputs right before it
+  if (std::strcmp(key, "jac_prefetch") == 0 && (value == 0 || value == 1)) {
+    ctx->jac_prefetch = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "linearize_order") == 0 && (value == 0 || value == 1)) {

@@ -58,11 +58,15 @@ def test_export_matches_oracle(gpu, model):
 
 def test_export_needs_resident_rasters(gpu):
     sc, sem = scene(mi_ba.SIMPLE_PINHOLE)
-    only = mi_ba.SemanticInput(sem.depth, sem.label, np.array([(0, 1)], np.int32), pixel_step=4)
+    # pairs (0, 1), (1, 2): images 1 and 2 are some pair's second image, so
+    # only their rasters are on the device; the export needs both images'
+    only = mi_ba.SemanticInput(sem.depth, sem.label, np.array([(0, 1), (1, 2)], np.int32), pixel_step=4)
     with mi_ba.Context(mi_ba.default_options(), sc.copy(), only) as ctx:
-        ctx.semantic_export(0, 1)
-        with pytest.raises(mi_ba.MiBaError) as e:
-            ctx.semantic_export(1, 0)  # image 0 is no pair's second image: no raster on the device
-        assert e.value.status == mi_ba.ERR_UNSUPPORTED
+        ctx.semantic_export(1, 2)
+        ctx.semantic_export(2, 1)
+        for i, j in ((0, 1), (1, 0)):
+            with pytest.raises(mi_ba.MiBaError) as e:
+                ctx.semantic_export(i, j)  # image 0 is no pair's second image: no raster on the device
+            assert e.value.status == mi_ba.ERR_UNSUPPORTED
         with pytest.raises(mi_ba.MiBaError):
             ctx.semantic_export(1, 1)

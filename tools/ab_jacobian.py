@@ -1,6 +1,8 @@
 """Times the reproj_jacobian kernel alone on a BASELINE config (HIP events on
 the context stream, interleaved rounds) and reports GB/s vs the 8 TB/s peak.
-    python tools/ab_jacobian.py [--config C4] [--rounds 5] [--reps 5]
+    python tools/ab_jacobian.py [--config C4] [--rounds 5] [--reps 5] [--variants 0,13,0:jac_prefetch=1]
+A variant is a jacobian_variant number, optionally with tuning keys set for
+it alone ("0:jac_prefetch=1:linearize_order=1"; reset to 0 afterwards).
 """
 import argparse
 import json
@@ -36,11 +38,22 @@ else:
     ctx = mi_ba.Context(mi_ba.default_options(), sc)
 nb, W, _ = ctx.dims()
 bpb = bench.bytes_per_block(cfg["model"], cfg["track"])
-variants = [int(v) for v in args.variants.split(",")]
+variants = args.variants.split(",")
+
+
+def apply(spec, on=True):
+    parts = spec.split(":")
+    if on:
+        ctx.set_tuning("jacobian_variant", int(parts[0]))
+    for kv in parts[1:]:
+        k, val = kv.split("=")
+        ctx.set_tuning(k, int(val) if on else 0)
+
+
 ref = None
 ok = {}
 for v in variants:
-    ctx.set_tuning("jacobian_variant", v)
+    apply(v)
     ctx.evaluate_jacobian()
     ctx.synchronize()
     _, r, J = ctx.download_jacobian()
@@ -48,11 +61,12 @@ for v in variants:
         ref = (r.copy(), J.copy())
     ok[v] = bool(np.array_equal(r, ref[0]) and np.array_equal(J, ref[1]))
     ok[v] = (ok[v], float(np.abs(J - ref[1]).max() / max(1.0, float(np.abs(ref[1]).max()))))
+    apply(v, False)
     del r, J
 res = {v: [] for v in variants}
 for rnd in range(args.rounds):
     for v in variants:
-        ctx.set_tuning("jacobian_variant", v)
+        apply(v)
         ctx.evaluate_jacobian()
         ctx.set_timing(True)
         ctx.reset_kernel_times()
@@ -60,6 +74,7 @@ for rnd in range(args.rounds):
             ctx.linearize() if args.step else ctx.evaluate_jacobian()
         ms, n = ctx.kernel_time("reproj_jacobian")
         ctx.set_timing(False)
+        apply(v, False)
         res[v].append(ms / n)
 for v in variants:
     med = float(np.median(res[v]))
