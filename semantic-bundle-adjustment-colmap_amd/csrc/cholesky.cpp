@@ -1464,7 +1464,16 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
   if (st != rocblas_status_success) return st;
   // On a failure after the side stream got work, the caller's stream waits
   // for it (the caller may free A / info once its own stream is drained).
+  // split head (CholConfig::split_cus): the panel factor and the trailing
+  // dgemm on disjoint CU sets while the panel starts before split_cols
+  const bool split_ok = cfg.split_cus > 0 && ws.split_n > 0 && ws.split_side_h && ws.split_main_h;
+  rocblas_handle hm = h, hs = ws.side_h;
+  hipStream_t sm = s1, ss = ws.side;
   auto fail = [&](rocblas_status e) {
+    if (split_ok) {
+      (void)hipStreamSynchronize(ws.split_side);
+      (void)hipStreamSynchronize(ws.split_main);
+    }
     hipEvent_t last = ws.ev.back();
     if (hipEventRecord(last, ws.side) != hipSuccess || hipStreamWaitEvent(s1, last, 0) != hipSuccess)
       (void)hipStreamSynchronize(ws.side);
@@ -1474,18 +1483,34 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     const int k = ps[kk], kb = ps[kk + 1] - k;
     const int m = n - k - kb;
     if (m == 0) break;
+    const bool want = split_ok && k < cfg.split_cols;
+    if (want && sm == s1) {  // into the split: the dgemm stream follows the caller's stream
+      if (hipEventRecord(ws.ev_split[0], s1) != hipSuccess || hipStreamWaitEvent(ws.split_main, ws.ev_split[0], 0))
+        return fail(rocblas_status_internal_error);
+      hm = ws.split_main_h;
+      hs = ws.split_side_h;
+      sm = ws.split_main;
+      ss = ws.split_side;
+    } else if (!want && sm != s1) {  // out of it: the caller's stream follows the dgemm stream
+      if (hipEventRecord(ws.ev_split[1], sm) != hipSuccess || hipStreamWaitEvent(s1, ws.ev_split[1], 0))
+        return fail(rocblas_status_internal_error);
+      hm = h;
+      hs = ws.side_h;
+      sm = s1;
+      ss = ws.side;
+    }
     double* Aik = A + k + kb + (size_t)k * lda;  // panel k below its diagonal block
     double* T = Aik + (size_t)kb * lda;          // trailing matrix, lower triangle
     // block column k+1 (the next panel) first
     const int jb0 = ps[kk + 2] - ps[kk + 1];
-    st = gemm_nt(h, m + ex, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
+    st = gemm_nt(hm, m + ex, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
     if (st != rocblas_status_success) return fail(st);
     hipEvent_t upd = ws.ev[2 * kk], pan = ws.ev[2 * kk + 1];
-    if (hipEventRecord(upd, s1) != hipSuccess || hipStreamWaitEvent(ws.side, upd, 0) != hipSuccess)
+    if (hipEventRecord(upd, sm) != hipSuccess || hipStreamWaitEvent(ss, upd, 0) != hipSuccess)
       return fail(rocblas_status_internal_error);
-    st = panel_factor(ws.side_h, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag, scratch_side, &ws, ex);
+    st = panel_factor(hs, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag, scratch_side, &ws, ex);
     if (st != rocblas_status_success) return fail(st);
-    if (hipEventRecord(pan, ws.side) != hipSuccess) return fail(rocblas_status_internal_error);
+    if (hipEventRecord(pan, ss) != hipSuccess) return fail(rocblas_status_internal_error);
     // the rest of the trailing lower triangle (columns jb0 .. m)
     [[maybe_unused]] const int mr = m - jb0;
 #ifdef MI_BA_AB_VARIANTS
@@ -1504,13 +1529,15 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
       for (int j = jb0; j < m; j += cw) {
         const int jb = std::min(cw, m - j);
-        st = gemm_nt(h, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
+        st = gemm_nt(hm, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
         if (st != rocblas_status_success) return fail(st);
       }
     }
     // panel k+1 is read by the next iteration's updates (and by the solve)
-    if (hipStreamWaitEvent(s1, pan, 0) != hipSuccess) return fail(rocblas_status_internal_error);
+    if (hipStreamWaitEvent(sm, pan, 0) != hipSuccess) return fail(rocblas_status_internal_error);
   }
+  if (sm != s1 && (hipEventRecord(ws.ev_split[2], sm) != hipSuccess || hipStreamWaitEvent(s1, ws.ev_split[2], 0)))
+    return fail(rocblas_status_internal_error);
   return rocblas_status_success;
 }
 
@@ -1629,9 +1656,57 @@ bool CholWorkspace::ensure(int dev, int max_panels, int max_n) {
   return create(dev, max_panels, max_n);
 }
 
+bool CholWorkspace::set_split_cus(int ncu) {
+  const int req = ncu;
+  if (split_side) (void)hipStreamSynchronize(split_side);
+  if (split_main) (void)hipStreamSynchronize(split_main);
+  if (split_side_h) (void)rocblas_destroy_handle(split_side_h);
+  if (split_main_h) (void)rocblas_destroy_handle(split_main_h);
+  if (split_side) (void)hipStreamDestroy(split_side);
+  if (split_main) (void)hipStreamDestroy(split_main);
+  for (hipEvent_t& e : ev_split) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+  }
+  split_side = split_main = nullptr;
+  split_side_h = split_main_h = nullptr;
+  split_n = 0;
+  if (ncu <= 0) return true;
+  if (hipSetDevice(device) != hipSuccess) return false;
+  int total = 0;
+  if (hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || total <= 1)
+    return false;
+  ncu = std::min(ncu, total - 1);
+  std::vector<uint32_t> ms((total + 31) / 32, 0u), mm((total + 31) / 32, 0u);
+  std::vector<char> in(total, 0);
+  for (int k = 0; k < ncu; ++k) in[(int)((int64_t)k * total / ncu)] = 1;
+  for (int cu = 0; cu < total; ++cu) (in[cu] ? ms : mm)[cu / 32] |= 1u << (cu % 32);
+  if (hipExtStreamCreateWithCUMask(&split_side, (uint32_t)ms.size(), ms.data()) != hipSuccess) {
+    split_side = nullptr;
+    return false;
+  }
+  if (hipExtStreamCreateWithCUMask(&split_main, (uint32_t)mm.size(), mm.data()) != hipSuccess) {
+    split_main = nullptr;
+    return false;
+  }
+  if (rocblas_create_handle(&split_side_h) != rocblas_status_success) { split_side_h = nullptr; return false; }
+  if (rocblas_create_handle(&split_main_h) != rocblas_status_success) { split_main_h = nullptr; return false; }
+  if (rocblas_set_stream(split_side_h, split_side) != rocblas_status_success ||
+      rocblas_set_stream(split_main_h, split_main) != rocblas_status_success)
+    return false;
+  for (hipEvent_t& e : ev_split)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      e = nullptr;
+      return false;
+    }
+  split_n = req;
+  return true;
+}
+
 void CholWorkspace::destroy() {
   if (device >= 0) (void)hipSetDevice(device);
   if (side) (void)hipStreamSynchronize(side);
+  if (split_n > 0 || split_side || split_main) (void)set_split_cus(0);
   for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   ev.clear();
   if (side_h) (void)rocblas_destroy_handle(side_h);
@@ -1683,6 +1758,8 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
     ws->bwd_pairs = c.bwd_pairs;
     ws->group_min_rows = c.panel_group_min_rows;
     if (ws->side && c.side_cus != ws->side_cus && !ws->set_side_cus(c.side_cus))
+      return rocblas_status_internal_error;
+    if (ws->side && c.split_cus != ws->split_n && !ws->set_split_cus(c.split_cus))
       return rocblas_status_internal_error;
   }
   double* scratch = ws ? ws->scratch : nullptr;

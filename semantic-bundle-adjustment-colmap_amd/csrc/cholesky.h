@@ -33,6 +33,12 @@ struct CholConfig {
   // so the panel factor's waiting workgroups leave the rest to the trailing
   // dgemm; 0: all CUs at high priority (tools build: cholesky_panel_cus)
   int side_cus = 0;
+  // split head: while the panel starts before column split_cols, the
+  // look-ahead's panel factor runs on split_cus CUs (spread over the chip) and
+  // the trailing dgemm on the complement, so the panel's resident workgroups
+  // (76 KB LDS, 342 VGPRs per lane) do not halve the dgemm's occupancy on the
+  // CUs they share; 0 = off
+  int split_cus = 0, split_cols = 0;
   bool gemm_update = true;
   // look-ahead: the trailing update after the next panel's block column,
   // 0 one dgemm per 512-wide block column, 1 one dsyrk, 2 one dgemmt,
@@ -137,6 +143,14 @@ struct CholWorkspace {
   int group_min_rows = 6000;       // CholConfig::panel_group_min_rows
   int side_cus = 0;                // CholConfig::side_cus of the current side stream
   bool set_side_cus(int ncu);      // re-create the side stream with that CU mask
+  // split head (CholConfig::split_cus): a panel stream on split_cus CUs and a
+  // dgemm stream on the others, each with its rocBLAS handle; ev_split orders
+  // them against the caller's and the side stream at the regime switches
+  hipStream_t split_side = nullptr, split_main = nullptr;
+  rocblas_handle split_side_h = nullptr, split_main_h = nullptr;
+  hipEvent_t ev_split[4] = {nullptr, nullptr, nullptr, nullptr};
+  int split_n = 0;                 // split_cus of the current split streams
+  bool set_split_cus(int ncu);
 
   // Creates the resources on `device` with events for up to `max_panels`
   // panels and diagonal-block inverses for matrices up to max_n; false on any

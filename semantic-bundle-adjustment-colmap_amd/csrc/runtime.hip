@@ -2065,6 +2065,16 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.panel_rows_per_group = value;
     return MI_BA_OK;
   }
+  // split head: panel factor on this many CUs, trailing dgemm on the rest,
+  // while the panel starts before column cholesky_split_cols
+  if (std::strcmp(key, "cholesky_split_cus") == 0 && value >= 0 && value <= 4096) {
+    ctx->chol.split_cus = (int)value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_split_cols") == 0 && value >= 0) {
+    ctx->chol.split_cols = (int)value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_panel_cus") == 0 && value >= 0 && value <= 4096 && ab_value(value, 0)) {
     ctx->chol.side_cus = (int)value;
     return MI_BA_OK;
