@@ -866,7 +866,15 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   // reprojection kernel (HBM-write-bound); joined below
   const bool overlap = ctx->sem && ctx->lin_overlap == 1;
   const bool split = ctx->sem && ctx->lin_overlap == 2;
-  if ((overlap || split) && !ctx->lin_side) {
+  // warm (default): the semantic pass first; while its compute-bound deferred
+  // pass runs, a read-only kernel on the side stream streams the reprojection
+  // kernel's inputs (observations, image / point ids, points: 264 MB at C4)
+  // into the memory-side cache, so the reprojection kernel's HBM traffic is its
+  // J / r write stream alone (in-step 0.552 -> 0.44 ms at C4,
+  // profiles/r4_ab_jacobian_warm_inputs.jsonl: read/write interleaving on HBM
+  // cost it more than its arithmetic)
+  const bool warm = ctx->sem && !overlap && !split && ctx->lin_warm && ctx->sem_variant == 6 && d.nb > 0;
+  if ((overlap || split || warm) && !ctx->lin_side) {
     if (hipStreamCreateWithFlags(&ctx->lin_side, hipStreamNonBlocking) != hipSuccess) {
       ctx->lin_side = nullptr;
       return MI_BA_ERR_HIP;
@@ -888,9 +896,22 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     if (st != MI_BA_OK) return st;
     MI_HIP(hipEventRecord(ctx->lin_ev[1], ctx->lin_side));
   }
+  if (warm) {
+    auto after_flat = [&]() -> mi_ba_status {
+      MI_HIP(hipEventRecord(ctx->lin_ev[0], s));
+      MI_HIP(hipStreamWaitEvent(ctx->lin_side, ctx->lin_ev[0], 0));
+      launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), ctx->lin_side);
+      MI_HIP(hipEventRecord(ctx->lin_ev[1], ctx->lin_side));
+      return MI_BA_OK;
+    };
+    mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false, nullptr, nullptr, nullptr, nullptr, 0,
+                                         nullptr, nullptr, after_flat);
+    if (st != MI_BA_OK) return st;
+    MI_HIP(hipStreamWaitEvent(s, ctx->lin_ev[1], 0));
+  }
   // lin_order: 0 reprojection then semantic, 1 semantic first (A/B of the
   // reprojection kernel's in-step time after the semantic gathers)
-  const bool sem_first = ctx->sem && !overlap && !split && ctx->lin_order == 1;
+  const bool sem_first = ctx->sem && !overlap && !split && !warm && ctx->lin_order == 1;
   if (sem_first) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
@@ -902,7 +923,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   // default layout: the semantic pass right behind the reprojection kernel
   // (its timer starts at the reprojection kernel's stop event), then both
   // cost sums in one launch
-  const bool sem_after = ctx->sem && !overlap && !split && !sem_first;
+  const bool sem_after = ctx->sem && !overlap && !split && !sem_first && !warm;
   if (sem_after) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false, nullptr, nullptr, stop,
                                          d.nb ? ctx->partial.ptr : nullptr, reproj_grid(d.nb),
@@ -1955,6 +1976,12 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   // test hook: hold the stream ahead of every RCCL collective for `value` ms
   if (std::strcmp(key, "comm_stall_ms") == 0 && value >= 0 && value <= 60000) {
     ctx->comm_stall_ms = value;
+    return MI_BA_OK;
+  }
+  // 1 (default): warm the reprojection kernel's inputs beside the semantic
+  // deferred pass (context_linearize); 0: reprojection kernel first
+  if (std::strcmp(key, "linearize_warm_inputs") == 0 && (value == 0 || value == 1)) {
+    ctx->lin_warm = value;
     return MI_BA_OK;
   }
   // diagnostic: read the reprojection kernel's streamed inputs right before it

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 
 #include "../../include/mi_ba.h"
 #include "ba_math.h"
@@ -86,11 +87,13 @@ void semantic_destroy(mi_ba_context* ctx);
 // timer_start: the semantic timer starts at this recorded event (the
 // previous phase's stop).  other_partial / other_n / other_out / other_scratch:
 // a second cost sum (the reprojection partials) launched together with the
-// semantic one.
+// semantic one.  after_flat (optional): called once the flat pass is
+// enqueued, before the deferred pass (the input warm-up's launch point).
 mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples,
                                 hipStream_t deferred_stream = nullptr, hipEvent_t flat_done = nullptr,
                                 hipEvent_t timer_start = nullptr, const double* other_partial = nullptr,
-                                int64_t other_n = 0, double* other_out = nullptr, double* other_scratch = nullptr);
+                                int64_t other_n = 0, double* other_out = nullptr, double* other_scratch = nullptr,
+                                const std::function<mi_ba_status()>& after_flat = nullptr);
 // ExportSemanticErrorToCSV rows of the ordered image pair (image1, image2) at
 // the current parameters (mi_ba_semantic_export).
 mi_ba_status semantic_export(mi_ba_context* ctx, int32_t image1, int32_t image2, int64_t* count, int32_t* pixels,

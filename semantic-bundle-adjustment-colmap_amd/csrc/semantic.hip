@@ -1960,10 +1960,14 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
     if (hipMemcpy(S->dl.ptr + s * plane, buf.data(), plane * sizeof(float2), hipMemcpyHostToDevice))
       return MI_BA_ERR_HIP;
   }
-  // the flat pass's 3x3 window summaries (semantic step 0.40 -> 0.38 ms at C4,
-  // profiles/r4_ab_semantic_window_summary.jsonl); without the memory for
-  // them the flat pass reads the rasters alone
-  if (semantic_set_window_summary(ctx, true) == MI_BA_ERR_HIP) return MI_BA_ERR_HIP;
+  // the flat pass's label planes (3.9M of 5.0M C4 samples settled without the
+  // float rasters, 1.1 GB), else (more than 256 distinct labels) the 3x3
+  // window summaries (2.8M, 16 B per raster pixel): semantic step 0.41 ->
+  // 0.39 ms at C4 either way (profiles/r4_ab_semantic_label_planes.jsonl);
+  // without the memory for them the flat pass reads the rasters alone
+  mi_ba_status st = semantic_set_label_planes(ctx, true);
+  if (st == MI_BA_ERR_HIP) return st;
+  if (!S->use_lp && semantic_set_window_summary(ctx, true) == MI_BA_ERR_HIP) return MI_BA_ERR_HIP;
   return MI_BA_OK;
 }
 
@@ -2085,7 +2089,8 @@ void semantic_destroy(mi_ba_context* ctx) {
 // done), and the caller joins it; the cost is complete on ctx->stream.
 mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples, hipStream_t deferred_stream,
                                 hipEvent_t flat_done, hipEvent_t timer_start, const double* other_partial,
-                                int64_t other_n, double* other_out, double* other_scratch) {
+                                int64_t other_n, double* other_out, double* other_scratch,
+                                const std::function<mi_ba_status()>& after_flat) {
   SemanticState* S = ctx->sem;
   hipStream_t s = ctx->stream;
   S->samples_valid = write_samples;
@@ -2137,6 +2142,10 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
                              pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr,
                              S->J.ptr, ws);
       });
+    }
+    if (after_flat) {
+      const mi_ba_status st = after_flat();
+      if (st != MI_BA_OK) return st;
     }
     if (split) {
       if (hipEventRecord(flat_done, s) != hipSuccess || hipStreamWaitEvent(deferred_stream, flat_done, 0) != hipSuccess)

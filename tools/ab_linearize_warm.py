@@ -1,0 +1,65 @@
+"""The C4 linearization step (as bench.py) with the reprojection kernel's
+inputs warmed beside the semantic deferred pass ("linearize_warm_inputs" 1,
+the default: semantic pass first, a read-only kernel on a side stream streams
+observations / ids / points into the memory-side cache) against the
+reprojection kernel first (0): step wall time and the two kernels' times
+(HIP events) over interleaved rounds; the step's cost checked equal.
+    python tools/ab_linearize_warm.py [--rounds 6] [--reps 10]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "semantic-bundle-adjustment-colmap_amd"))
+sys.path.insert(0, ROOT)
+import mi_ba  # noqa: E402
+import bench  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rounds", type=int, default=6)
+ap.add_argument("--reps", type=int, default=10)
+args = ap.parse_args()
+sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
+ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
+CONFIGS = [0, 1]
+costs, same = {}, {}
+ref = None
+for cfg in CONFIGS:
+    ctx.set_tuning("linearize_warm_inputs", cfg)
+    ctx.linearize()
+    costs[cfg] = ctx.cost()
+    _, r, J = ctx.download_jacobian()
+    if ref is None:
+        ref = (r, J)
+    same[cfg] = bool(np.array_equal(r, ref[0]) and np.array_equal(J, ref[1]))
+    del r, J
+ref = None
+res = {c: [] for c in CONFIGS}
+for rnd in range(args.rounds):
+    for cfg in CONFIGS:
+        ctx.set_tuning("linearize_warm_inputs", cfg)
+        for _ in range(3):
+            ctx.linearize()
+        ctx.synchronize()
+        ctx.set_timing(True)
+        ctx.reset_kernel_times()
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            ctx.linearize()
+        ctx.synchronize()
+        wall = (time.perf_counter() - t0) / args.reps * 1e3
+        sj = ctx.kernel_time("semantic_jacobian")
+        rj = ctx.kernel_time("reproj_jacobian")
+        ctx.set_timing(False)
+        res[cfg].append((sj[0] / sj[1], rj[0] / rj[1], wall))
+for cfg in CONFIGS:
+    a = np.array(res[cfg])
+    print(json.dumps({"linearize_warm_inputs": cfg, "cost": costs[cfg], "cost_equal": costs[cfg] == costs[0], "r_J_equal": same[cfg],
+                      "semantic_ms_median": float(np.median(a[:, 0])), "reproj_ms_median": float(np.median(a[:, 1])),
+                      "step_wall_ms_median": float(np.median(a[:, 2])), "rounds": args.rounds, "reps": args.reps}),
+          flush=True)
+ctx.close()

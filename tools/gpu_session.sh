@@ -9,7 +9,7 @@
 # trace (rocprofv3 kernel trace of the bench command), bench (the bench line),
 # jacsweep (in-step times of the tools-build Jacobian variants JACV), pcg
 # (matrix-free PCG product A/B),
-# pmcs (semantic PMC passes + summary), smoke
+# pmcs (semantic PMC passes + summary), warm (linearize_warm_inputs A/B), smoke
 set -o pipefail
 T=${1:?tag}
 shift
@@ -33,6 +33,9 @@ for stage in "$@"; do
     pcg)
       timeout -k 10 500 python -u tools/ab_pcg_mf.py > gpurun_out/$T/ab_pcg_mf.jsonl 2> gpurun_out/$T/ab_pcg_mf.err || exit 1
       cat gpurun_out/$T/ab_pcg_mf.jsonl ;;
+    warm)
+      timeout -k 10 300 python -u tools/ab_linearize_warm.py > gpurun_out/$T/ab_warm.jsonl 2> gpurun_out/$T/ab_warm.err || exit 1
+      cat gpurun_out/$T/ab_warm.jsonl ;;
     lmkeys)
       timeout -k 10 900 python -u tools/ab_lm_keys.py "" $LMKEYS > gpurun_out/$T/ab_lm_keys.jsonl 2> gpurun_out/$T/ab_lm_keys.err || exit 1
       cat gpurun_out/$T/ab_lm_keys.jsonl ;;
