@@ -888,6 +888,10 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     MI_HIP(hipEventRecord(ctx->lin_ev[1], ctx->lin_side));
   }
   if (overlap) {
+    // with linearize_warm_inputs: the inputs streamed in first, then the two
+    // passes side by side
+    if (ctx->lin_warm && d.nb > 0)
+      launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), s);
     MI_HIP(hipEventRecord(ctx->lin_ev[0], s));
     MI_HIP(hipStreamWaitEvent(ctx->lin_side, ctx->lin_ev[0], 0));
     ctx->stream = ctx->lin_side;  // semantic_linearize launches (and times) on ctx->stream

@@ -36,6 +36,8 @@ f64 = 64 * (avg.get("SQ_INSTS_VALU_ADD_F64", 0) + avg.get("SQ_INSTS_VALU_MUL_F64
 out = {"kernel": "+".join(sorted({f for per in vals.values() for f in per})),
        "launches_sampled": {k: {f: len(v) for f, v in per.items()} for k, per in vals.items()},
        "counters_avg_per_launch": avg,
+       "counters_avg_per_launch_by_kernel": {f: {k: sum(per[f]) / len(per[f]) for k, per in vals.items() if f in per}
+                                             for f in sorted({f for per in vals.values() for f in per})},
        "fp64_ops_per_launch": f64,
        "hbm_bytes_per_launch": 1024 * (2 * avg.get("FETCH_SIZE", 0) + avg.get("WRITE_SIZE", 0))
        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg else None,
