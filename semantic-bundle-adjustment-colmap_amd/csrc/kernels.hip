@@ -2851,27 +2851,49 @@ inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 
 // cost partials of the reprojection kernels: one per 64 blocks
 int reproj_grid(int64_t nb) { return (int)grid_for(nb, 64); }
 
-// Reads a byte range (16 B per lane, grid-stride) and drops the values: a
-// warm-up of the reprojection kernel's streamed inputs in the memory-side
-// cache (A/B "jac_prefetch").  The sink is written only for an impossible sum.
-__global__ __launch_bounds__(256) void touch_kernel(const uint4* __restrict__ a, int64_t n16, unsigned* sink) {
+// Reads the reprojection kernel's streamed inputs (observations, image /
+// point ids, points; 16 B per lane, grid-stride, four loads in flight per
+// lane) and drops the values: they land in the memory-side cache, so the
+// reprojection kernel behind it meets HBM with its write stream alone
+// (linearize_warm_inputs).  One launch of few workgroups (one per CU): it
+// runs beside the semantic deferred pass and should take as little of the
+// CUs' wave slots as it can.  The sink is written only for an impossible sum.
+struct TouchRanges {
+  const uint4* ptr[4];
+  int64_t n16[4];
+};
+
+__global__ __launch_bounds__(256) void touch_kernel(TouchRanges t, unsigned* sink) {
   unsigned acc = 0u;
-  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n16; k += (int64_t)gridDim.x * 256) {
-    const uint4 v = a[k];  // a plain load: allocates in the caches
-    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint4* a = t.ptr[q];
+    const int64_t n = t.n16[q];
+    int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; k + 3 * stride < n; k += 4 * stride) {
+      const uint4 v0 = a[k], v1 = a[k + stride], v2 = a[k + 2 * stride], v3 = a[k + 3 * stride];
+      acc ^= v0.x ^ v1.y ^ v2.z ^ v3.w;
+    }
+    for (; k < n; k += stride) acc ^= a[k].x;
   }
-  if (acc == 0x9e3779b9u && n16 < 0) *sink = acc;
+  if (acc == 0x9e3779b9u && t.n16[0] < 0) *sink = acc;
 }
 
 void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s) {
-  auto touch = [&](const void* ptr, int64_t bytes) {
-    if (!ptr || bytes < 16) return;
-    hipLaunchKernelGGL(touch_kernel, dim3(2048), dim3(256), 0, s, reinterpret_cast<const uint4*>(ptr), bytes / 16, sink);
-  };
-  touch(p.obs_xy, p.nb * 16);
-  touch(p.obs_img, p.nb * 4);
-  touch(p.obs_pt, p.nb * 4);
-  touch(p.X, p.num_points * 24);
+  TouchRanges t{};
+  const void* ptrs[4] = {p.obs_xy, p.obs_img, p.obs_pt, p.X};
+  const int64_t bytes[4] = {p.nb * 16, p.nb * 4, p.nb * 4, p.num_points * 24};
+  for (int q = 0; q < 4; ++q) {
+    t.ptr[q] = reinterpret_cast<const uint4*>(ptrs[q]);
+    t.n16[q] = ptrs[q] ? bytes[q] / 16 : 0;
+  }
+  int cus = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) ||
+      cus <= 0)
+    cus = 256;
+  hipLaunchKernelGGL(touch_kernel, dim3(cus), dim3(256), 0, s, t, sink);
 }
 
 void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s) {
