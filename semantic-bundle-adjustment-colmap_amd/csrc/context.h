@@ -91,8 +91,10 @@ struct mi_ba_context {
   miba::DevArray<double> sum_ws;      // [kSumScratch] stage + ticket of launch_sum's many-workgroup pass
   int lin_overlap = 0;                 // 1 semantic kernels on lin_side beside the reprojection kernel,
                                        // 2 flat pass first, deferred pass on lin_side beside it
-  int lin_warm = 1;                    // "linearize_warm_inputs": semantic first, reprojection inputs warmed beside its deferred pass
-  int jac_prefetch = 0;                // A/B: warm the reprojection kernel's inputs right before it
+  int lin_warm = 15;                   // "linearize_warm_inputs": semantic first, reprojection inputs warmed beside its deferred
+                                       // pass (range mask: 1 observations, 2 image ids, 4 point ids, 8 points; 0 off)
+  int jac_prefetch = 0;                // A/B: warm the reprojection kernel's inputs right before it (range mask, bits as lin_warm)
+  int warm_wgs = 2048;                 // workgroups of the warm-up kernel (0: one per CU)
   int lin_order = 0;                   // 0 reprojection kernel first, 1 semantic pass first
   hipStream_t lin_side = nullptr;
   hipEvent_t lin_ev[2] = {nullptr, nullptr};

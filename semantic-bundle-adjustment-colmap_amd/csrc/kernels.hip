@@ -2880,20 +2880,22 @@ __global__ __launch_bounds__(256) void touch_kernel(TouchRanges t, unsigned* sin
   if (acc == 0x9e3779b9u && t.n16[0] < 0) *sink = acc;
 }
 
-void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s) {
+void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s, int mask, int wgs) {
   TouchRanges t{};
   const void* ptrs[4] = {p.obs_xy, p.obs_img, p.obs_pt, p.X};
   const int64_t bytes[4] = {p.nb * 16, p.nb * 4, p.nb * 4, p.num_points * 24};
   for (int q = 0; q < 4; ++q) {
     t.ptr[q] = reinterpret_cast<const uint4*>(ptrs[q]);
-    t.n16[q] = ptrs[q] ? bytes[q] / 16 : 0;
+    t.n16[q] = ptrs[q] && ((mask >> q) & 1) ? bytes[q] / 16 : 0;
   }
-  int cus = 256;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) ||
-      cus <= 0)
-    cus = 256;
-  hipLaunchKernelGGL(touch_kernel, dim3(cus), dim3(256), 0, s, t, sink);
+  if (wgs <= 0) {  // one workgroup per CU
+    int dev = 0;
+    wgs = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&wgs, hipDeviceAttributeMultiprocessorCount, dev) ||
+        wgs <= 0)
+      wgs = 256;
+  }
+  hipLaunchKernelGGL(touch_kernel, dim3(wgs), dim3(256), 0, s, t, sink);
 }
 
 void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s) {

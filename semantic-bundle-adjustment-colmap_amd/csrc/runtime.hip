@@ -891,7 +891,8 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     // with linearize_warm_inputs: the inputs streamed in first, then the two
     // passes side by side
     if (ctx->lin_warm && d.nb > 0)
-      launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), s);
+      launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), s, ctx->lin_warm,
+                          ctx->warm_wgs);
     MI_HIP(hipEventRecord(ctx->lin_ev[0], s));
     MI_HIP(hipStreamWaitEvent(ctx->lin_side, ctx->lin_ev[0], 0));
     ctx->stream = ctx->lin_side;  // semantic_linearize launches (and times) on ctx->stream
@@ -904,7 +905,8 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     auto after_flat = [&]() -> mi_ba_status {
       MI_HIP(hipEventRecord(ctx->lin_ev[0], s));
       MI_HIP(hipStreamWaitEvent(ctx->lin_side, ctx->lin_ev[0], 0));
-      launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), ctx->lin_side);
+      launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), ctx->lin_side, ctx->lin_warm,
+                          ctx->warm_wgs);
       MI_HIP(hipEventRecord(ctx->lin_ev[1], ctx->lin_side));
       return MI_BA_OK;
     };
@@ -920,7 +922,9 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
   }
-  if (ctx->jac_prefetch) launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), s);
+  if (ctx->jac_prefetch)
+    launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), s, ctx->jac_prefetch,
+                        ctx->warm_wgs);
   timer_begin(ctx, "reproj_jacobian", &stop);
   launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->partial.ptr, s);
   timer_end(ctx, stop);
@@ -1984,13 +1988,17 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   }
   // 1 (default): warm the reprojection kernel's inputs beside the semantic
   // deferred pass (context_linearize); 0: reprojection kernel first
-  if (std::strcmp(key, "linearize_warm_inputs") == 0 && (value == 0 || value == 1)) {
-    ctx->lin_warm = value;
+  if (std::strcmp(key, "linearize_warm_inputs") == 0 && value >= 0 && value <= 15) {
+    ctx->lin_warm = value == 1 ? 15 : value;  // 1: every range
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "warm_workgroups") == 0 && value >= 0 && value <= 65536) {
+    ctx->warm_wgs = value;
     return MI_BA_OK;
   }
   // diagnostic: read the reprojection kernel's streamed inputs right before it
-  if (std::strcmp(key, "jac_prefetch") == 0 && (value == 0 || value == 1)) {
-    ctx->jac_prefetch = value;
+  if (std::strcmp(key, "jac_prefetch") == 0 && value >= 0 && value <= 15) {
+    ctx->jac_prefetch = value == 1 ? 15 : value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "linearize_order") == 0 && (value == 0 || value == 1)) {

@@ -13,7 +13,6 @@ import time
 
 import numpy as np
 
-os.environ.setdefault("MI_BA_LIB", "ab")  # linearize_overlap: the tools-only build (make ab)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "semantic-bundle-adjustment-colmap_amd"))
 sys.path.insert(0, ROOT)
@@ -26,14 +25,15 @@ ap.add_argument("--reps", type=int, default=10)
 args = ap.parse_args()
 sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
 ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
-# (linearize_warm_inputs, linearize_overlap): 1 the semantic pass on a second
-# stream beside the reprojection kernel, 2 only its deferred pass
-CONFIGS = [(0, 0), (1, 0), (1, 1), (1, 2)]
+# (linearize_warm_inputs range mask: 1 observations, 2 image ids, 4 point ids,
+#  8 points; warm_workgroups: 0 one per CU)
+CONFIGS = [(0, 2048), (15, 2048), (15, 0), (14, 2048), (1, 2048), (15, 8192)]
 
 
 def apply(cfg):
     ctx.set_tuning("linearize_warm_inputs", cfg[0])
-    ctx.set_tuning("linearize_overlap", cfg[1])
+    ctx.set_tuning("warm_workgroups", cfg[1])
+
 
 costs, same = {}, {}
 ref = None
@@ -67,7 +67,7 @@ for rnd in range(args.rounds):
         res[cfg].append((sj[0] / sj[1], rj[0] / rj[1], wall))
 for cfg in CONFIGS:
     a = np.array(res[cfg])
-    print(json.dumps({"linearize_warm_inputs": cfg[0], "linearize_overlap": cfg[1], "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
+    print(json.dumps({"linearize_warm_inputs": cfg[0], "warm_workgroups": cfg[1], "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
                       "semantic_ms_median": float(np.median(a[:, 0])), "reproj_ms_median": float(np.median(a[:, 1])),
                       "step_wall_ms_median": float(np.median(a[:, 2])), "rounds": args.rounds, "reps": args.reps}),
           flush=True)

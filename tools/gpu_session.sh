@@ -9,6 +9,7 @@
 # trace (rocprofv3 kernel trace of the bench command), bench (the bench line),
 # jacsweep (in-step times of the tools-build Jacobian variants JACV), pcg
 # (matrix-free PCG product A/B),
+# prof (trace + traffic PMC of the bench step, summarized), pmcj (reproj PMC b2b vs in-step),
 # pmcs (semantic PMC passes + summary), warm (linearize_warm_inputs A/B), smoke
 set -o pipefail
 T=${1:?tag}
@@ -45,6 +46,12 @@ for stage in "$@"; do
     chol)
       timeout -k 10 600 python -u tools/ab_chol_keys.py "" $CHOL > gpurun_out/$T/ab_chol.jsonl 2> gpurun_out/$T/ab_chol.err || exit 1
       cat gpurun_out/$T/ab_chol.jsonl ;;
+    prof)
+      timeout -k 10 1500 bash tools/profile.sh gpurun_out/$T/prof > gpurun_out/$T/prof.log 2>&1 || { tail -5 gpurun_out/$T/prof.log; exit 1; }
+      python tools/summarize_profile.py gpurun_out/$T/prof gpurun_out/$T/c4 && head -40 gpurun_out/$T/c4.md ;;
+    pmcj)
+      timeout -k 10 900 bash tools/pmc_jac_context.sh gpurun_out/$T/pmcctx > gpurun_out/$T/pmcctx.log 2>&1 || { tail -5 gpurun_out/$T/pmcctx.log; exit 1; }
+      tail -2 gpurun_out/$T/pmcctx.log ;;
     pmcs)
       timeout -k 10 900 bash tools/pmc_semantic.sh gpurun_out/$T/pmcs > gpurun_out/$T/pmcs.log 2>&1 || { tail -5 gpurun_out/$T/pmcs.log; exit 1; }
       python tools/summarize_pmc_semantic.py gpurun_out/$T/pmcs gpurun_out/$T/c4_semantic_pmc.json && cat gpurun_out/$T/c4_semantic_pmc.json ;;
