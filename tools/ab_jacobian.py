@@ -41,13 +41,17 @@ bpb = bench.bytes_per_block(cfg["model"], cfg["track"])
 variants = args.variants.split(",")
 
 
+# the product defaults the keys return to after a variant that set them
+DEFAULTS = {"jac_prefetch": 0, "linearize_order": 0, "linearize_warm_inputs": 15, "warm_workgroups": 2048}
+
+
 def apply(spec, on=True):
     parts = spec.split(":")
     if on:
         ctx.set_tuning("jacobian_variant", int(parts[0]))
     for kv in parts[1:]:
         k, val = kv.split("=")
-        ctx.set_tuning(k, int(val) if on else 0)
+        ctx.set_tuning(k, int(val) if on else DEFAULTS.get(k, 0))
 
 
 ref = None
