@@ -522,7 +522,18 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *                           1 per-point FMA route; 0 per-point uncontracted
  *                           (all bitwise equal)
  *   "semantic_diag"         1: downloaded status is offset by +0x1000 for samples
- *                           the flat test deferred (variants 5, 6; diagnostic)
+ *                           the flat test deferred (variants 5, 6; diagnostic); 2:
+ *                           also by +0x4000 for samples settled without the rasters
+ *   "semantic_label_planes" 1 (default): the flat pass reads an 8-bit label index
+ *                           plane and 8 x 8 tile depth ranges first (left off when the
+ *                           rasters hold more than 256 distinct labels); 0 off
+ *   "semantic_window_summary" 1: 3x3 window summaries of every raster pixel (the
+ *                           default when the label planes are off); 0 off
+ *   "linearize_warm_inputs" 15 / 1 (default): the semantic pass first, the
+ *                           reprojection kernel's inputs read into the memory-side
+ *                           cache beside its deferred pass; a mask of 1 observations,
+ *                           2 image ids, 4 point ids, 8 points; 0: reprojection first
+ *   "warm_workgroups"       workgroups of that read (default 2048; 0 one per CU)
  *   "linearize_overlap"     1 semantic kernel on a second stream beside the reprojection
  *                           kernel, 0 one stream (default)
  *   "cholesky_lookahead"    1 side-stream look-ahead (default) / 0 serial
