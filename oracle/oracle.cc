@@ -472,6 +472,10 @@ void EvalSemantic(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* 
 // Negative control of the property test (oracle_set_flat_bound_scale): the
 // pixel bound bx, by is multiplied by this factor (1 = the product's test).
 double g_flat_bound_scale = 1.0;
+// 1: the coarse form the product's flat pass uses (semantic_flat_coarse,
+// csrc/semantic.hip flat_box_coarse): the classes' bounds replaced by their
+// componentwise maxima (oracle_set_flat_coarse).
+int g_flat_coarse = 0;
 
 struct FlatBounds {
   double rho1 = 0, rho2 = 0, dt1[3] = {0, 0, 0}, dt2[3] = {0, 0, 0}, C[9] = {0};
@@ -558,6 +562,12 @@ bool FlatClears(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* se
     cls.push_back({B.dt2[0], 0.0, 0.0});
     cls.push_back({0.0, B.dt2[1], 0.0});
     cls.push_back({0.0, 0.0, B.dt2[2]});
+  }
+  if (g_flat_coarse && !cls.empty()) {  // one class: the componentwise maxima
+    std::array<double, 3> m = {0.0, 0.0, 0.0};
+    for (const auto& c : cls)
+      for (int k = 0; k < 3; ++k) m[k] = std::max(m[k], c[k]);
+    cls.assign(1, m);
   }
   double az = 0.0;
   for (const auto& c : cls) az = std::max(az, c[2]);
@@ -1391,6 +1401,7 @@ int oracle_semantic_flat_property(const mi_ba_options* o, mi_ba_problem* p, cons
 }
 
 void oracle_set_flat_bound_scale(double scale) { g_flat_bound_scale = scale; }
+void oracle_set_flat_coarse(int coarse) { g_flat_coarse = coarse; }
 
 // Registers (or clears, NULL) the dense factor the LM uses for its reduced
 // camera system.

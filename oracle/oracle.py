@@ -75,6 +75,8 @@ def load():
                                                   C.POINTER(mi_ba.Semantic), _i64p]
     lib.oracle_set_flat_bound_scale.argtypes = [C.c_double]
     lib.oracle_set_flat_bound_scale.restype = None
+    lib.oracle_set_flat_coarse.argtypes = [C.c_int]
+    lib.oracle_set_flat_coarse.restype = None
     lib.oracle_set_dense_factor.argtypes = [DENSE_FACTOR_FN]
     lib.oracle_set_dense_factor.restype = None
     _lib = lib
@@ -319,21 +321,24 @@ def semantic_export(options, scene, semantic, image1, image2):
     return pix, st, err, world
 
 
-def semantic_flat_property(options, scene, semantic, bound_scale=1.0):
+def semantic_flat_property(options, scene, semantic, bound_scale=1.0, coarse=False):
     """The product's semantic flat test (restated) vs the full CENTRAL
     stencil over every sample: dict(samples, cleared, cleared_not_flat,
     nonzero_jacobian, flat_deferred).  cleared_not_flat must be 0.
-    bound_scale < 1 shrinks the pixel bound (negative control)."""
+    bound_scale < 1 shrinks the pixel bound (negative control); coarse: the
+    form with the classes' componentwise maxima (semantic_flat_coarse)."""
     sc = scene.copy()
     p = sc.problem()
     s = semantic.struct()
     counts = np.zeros(5, np.int64)
     lib = load()
     lib.oracle_set_flat_bound_scale(bound_scale)
+    lib.oracle_set_flat_coarse(1 if coarse else 0)
     try:
         st = lib.oracle_semantic_flat_property(C.byref(options), C.byref(p), C.byref(s), counts.ctypes.data_as(_i64p))
     finally:
         lib.oracle_set_flat_bound_scale(1.0)
+        lib.oracle_set_flat_coarse(0)
     if st != 0:
         raise RuntimeError(f"oracle_semantic_flat_property status {st}")
     return dict(zip(("samples", "cleared", "cleared_not_flat", "nonzero_jacobian", "flat_deferred"),

@@ -866,14 +866,11 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   // reprojection kernel (HBM-write-bound); joined below
   const bool overlap = ctx->sem && ctx->lin_overlap == 1;
   const bool split = ctx->sem && ctx->lin_overlap == 2;
-  // warm (default): the semantic pass first; while its compute-bound deferred
-  // pass runs, a read-only kernel on the side stream streams the reprojection
-  // kernel's inputs (observations, image / point ids, points: 264 MB at C4)
-  // into the memory-side cache, so the reprojection kernel's HBM traffic is its
-  // J / r write stream alone (in-step 0.552 -> 0.44 ms at C4,
-  // profiles/r4_ab_jacobian_warm_inputs.jsonl: read/write interleaving on HBM
-  // cost it more than its arithmetic)
-  const bool warm = ctx->sem && !overlap && !split && ctx->lin_warm && ctx->sem_variant == 6 && d.nb > 0;
+  // warm_conc (tools build, linearize_warm_concurrent): the semantic pass
+  // first; while its deferred pass runs, touch_kernel streams the reprojection
+  // kernel's inputs on a side stream (measured: only the ids and points stay
+  // cached that way, profiles/r4_ab_linearize_warm_ranges.jsonl)
+  const bool warm = ctx->sem && !overlap && !split && ctx->lin_warm_conc && ctx->sem_variant == 6 && d.nb > 0;
   if ((overlap || split || warm) && !ctx->lin_side) {
     if (hipStreamCreateWithFlags(&ctx->lin_side, hipStreamNonBlocking) != hipSuccess) {
       ctx->lin_side = nullptr;
@@ -890,9 +887,6 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   if (overlap) {
     // with linearize_warm_inputs: the inputs streamed in first, then the two
     // passes side by side
-    if (ctx->lin_warm && d.nb > 0)
-      launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), s, ctx->lin_warm,
-                          ctx->warm_wgs);
     MI_HIP(hipEventRecord(ctx->lin_ev[0], s));
     MI_HIP(hipStreamWaitEvent(ctx->lin_side, ctx->lin_ev[0], 0));
     ctx->stream = ctx->lin_side;  // semantic_linearize launches (and times) on ctx->stream
@@ -905,8 +899,8 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     auto after_flat = [&]() -> mi_ba_status {
       MI_HIP(hipEventRecord(ctx->lin_ev[0], s));
       MI_HIP(hipStreamWaitEvent(ctx->lin_side, ctx->lin_ev[0], 0));
-      launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), ctx->lin_side, ctx->lin_warm,
-                          ctx->warm_wgs);
+      launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), ctx->lin_side,
+                          ctx->lin_warm_conc, ctx->warm_wgs);
       MI_HIP(hipEventRecord(ctx->lin_ev[1], ctx->lin_side));
       return MI_BA_OK;
     };
@@ -922,10 +916,20 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
   }
-  if (ctx->jac_prefetch)
-    launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), s, ctx->jac_prefetch,
+  // linearize_warm_inputs (default: the observations): the reprojection
+  // kernel's streamed inputs read right before it, so the memory-side cache
+  // serves its reads and HBM sees its J / r write stream alone (in-step 0.567
+  // -> 0.420 ms at C4 for a ~0.03 ms read of the 160 MB of observations,
+  // profiles/r4_ab_linearize_warm_ranges.jsonl).  Only after the semantic
+  // pass has used the cache; a geometric-only step finds them cached.
+  hipEvent_t wstop = nullptr;
+  if (ctx->sem && ctx->lin_warm && d.nb > 0) {
+    timer_begin(ctx, "input_warm", &wstop);
+    launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), s, ctx->lin_warm,
                         ctx->warm_wgs);
-  timer_begin(ctx, "reproj_jacobian", &stop);
+    timer_end(ctx, wstop);
+  }
+  timer_begin_after(ctx, "reproj_jacobian", wstop, &stop);  // starts at the warm-up's stop event
   launch_reproj_jacobian(d, ctx->r.ptr, ctx->J.ptr, ctx->partial.ptr, s);
   timer_end(ctx, stop);
   // default layout: the semantic pass right behind the reprojection kernel
@@ -1986,19 +1990,19 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->comm_stall_ms = value;
     return MI_BA_OK;
   }
-  // 1 (default): warm the reprojection kernel's inputs beside the semantic
-  // deferred pass (context_linearize); 0: reprojection kernel first
+  // range mask of the inputs read right before the reprojection kernel (1
+  // observations (default), 2 image ids, 4 point ids, 8 points; 0 off)
   if (std::strcmp(key, "linearize_warm_inputs") == 0 && value >= 0 && value <= 15) {
-    ctx->lin_warm = value == 1 ? 15 : value;  // 1: every range
+    ctx->lin_warm = value;
+    return MI_BA_OK;
+  }
+  // tools build: the same read beside the semantic deferred pass instead
+  if (std::strcmp(key, "linearize_warm_concurrent") == 0 && value >= 0 && value <= 15 && ab_value(value, 0)) {
+    ctx->lin_warm_conc = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "warm_workgroups") == 0 && value >= 0 && value <= 65536) {
     ctx->warm_wgs = value;
-    return MI_BA_OK;
-  }
-  // diagnostic: read the reprojection kernel's streamed inputs right before it
-  if (std::strcmp(key, "jac_prefetch") == 0 && value >= 0 && value <= 15) {
-    ctx->jac_prefetch = value == 1 ? 15 : value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "linearize_order") == 0 && (value == 0 || value == 1)) {
@@ -2009,6 +2013,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   // at C4, profiles/r3_ab_linearize_overlap.jsonl)
   if (std::strcmp(key, "linearize_overlap") == 0 && value >= 0 && value <= 2 && ab_value(value, 0)) {
     ctx->lin_overlap = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "semantic_flat_coarse") == 0 && (value == 0 || value == 1)) {
+    ctx->sem_coarse = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "semantic_diag") == 0 && value >= 0 && value <= 2) {

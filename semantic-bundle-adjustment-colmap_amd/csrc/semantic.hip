@@ -1035,6 +1035,63 @@ __device__ __forceinline__ bool flat_box(const PairConst* __restrict__ P, const 
   return fb.ncol <= 3 && fb.nrow <= 3;
 }
 
+// flat_box with the per-class displacement bounds replaced by their
+// componentwise maxima (ax, ay, az) over the classes: each class's pixel
+// bound is monotone in its (ax, ay, az) and in 1 / (z - az), so the one bound
+// covers every class — a box at most marginally wider, without the per-class
+// loops (about a quarter of the flat pass's FP64 instructions).  The depth
+// bound az is flat_box's.  Restated in the oracle (FlatClears, coarse form)
+// for tests/test_semantic_flat_property.py.
+template <int M>
+__device__ __forceinline__ bool flat_box_coarse(const PairConst* __restrict__ P, const Centre& c, const double* K2,
+                                                FlatBox& fb) {
+  const double z = c.p2[2];
+  if (!(z > 0.0)) return false;  // NaN-safe
+  const double iz = 1.0 / z;
+  const double u = c.p2[0] * iz, v = c.p2[1] * iz;
+  constexpr int np = Model<M>::kNumParams;
+  double x, y, A[4], Jp[2 * np];
+  world_to_image_jac<M>(K2, u, v, &x, &y, A, Jp);
+  if (!(fabs(x) < 1e8 && fabs(y) < 1e8 && fabs(u) < 1e6 && fabs(v) < 1e6)) return false;
+  double ax = 0.0, ay = 0.0, az = 0.0;
+  if (P->var1) {
+    const double dq1 = P->rho1 * sqrt(c.w[0] * c.w[0] + c.w[1] * c.w[1] + c.w[2] * c.w[2]) * (1.0 + 1e-12);
+    ax = fmax(dq1, fmax(P->dt1[0] * fabs(P->C[0]), fmax(P->dt1[1] * fabs(P->C[1]), P->dt1[2] * fabs(P->C[2]))));
+    ay = fmax(dq1, fmax(P->dt1[0] * fabs(P->C[3]), fmax(P->dt1[1] * fabs(P->C[4]), P->dt1[2] * fabs(P->C[5]))));
+    az = fmax(dq1, fmax(P->dt1[0] * fabs(P->C[6]), fmax(P->dt1[1] * fabs(P->C[7]), P->dt1[2] * fabs(P->C[8]))));
+  }
+  if (P->var2) {
+    const double dq2 = P->rho2 * sqrt(c.pw[0] * c.pw[0] + c.pw[1] * c.pw[1] + c.pw[2] * c.pw[2]) * (1.0 + 1e-12);
+    ax = fmax(ax, fmax(dq2, P->dt2[0]));
+    ay = fmax(ay, fmax(dq2, P->dt2[1]));
+    az = fmax(az, fmax(dq2, P->dt2[2]));
+  }
+  if (!(z - az > 0.5 * z)) return false;
+  const double iden = 1.0 / (z - az) * (1.0 + 1e-12);
+  const double cu = (ax + fabs(u) * az) * iden;
+  const double cv = (ay + fabs(v) * az) * iden;
+  const double gm = fmax(cu, cv);
+  if (!(gm < 0.1)) return false;  // a stencil this wide is never cleared (and keeps rho finite)
+  const double ru = fabs(u) + gm, rv = fabs(v) + gm;
+  const double H = second_derivative_bound<M>(K2, sqrt(ru * ru + rv * rv) * (1.0 + 1e-12));
+  const double fx = fabs(K2[0]);
+  const double fy = (M == kPinhole || M == kOpenCV) ? fabs(K2[1]) : fabs(K2[0]);
+  const double sk = cu + cv;
+  const double bxm = (fabs(A[0]) + fx * H * sk) * cu + (fabs(A[1]) + fx * H * sk) * cv;
+  const double bym = (fabs(A[2]) + fy * H * sk) * cu + (fabs(A[3]) + fy * H * sk) * cv;
+  const double gain = distortion_gain<M>(K2, u * u + v * v);
+  const double kscale = (fabs(K2[0]) + fabs(K2[1])) * gain * (1.0 + fabs(u) + fabs(v)) * (1.0 + c.mag * fabs(iz));
+  const double ex = 1e-6 + 1e-11 * (kscale + fabs(x) + fabs(y));
+  const double bx = bxm * (1.0 + 1e-12) + ex;
+  const double by = bym * (1.0 + 1e-12) + ex;
+  fb.x0 = (int)round(x - bx);
+  fb.y0 = (int)round(y - by);
+  fb.ncol = (int)round(x + bx) - fb.x0 + 1;
+  fb.nrow = (int)round(y + by) - fb.y0 + 1;
+  fb.d = az;
+  return fb.ncol <= 3 && fb.nrow <= 3;
+}
+
 // Box entry q (of 3 x 3): raster index to read (pixel 0 when q is outside the
 // box or the raster — read and ignored, so every read issues unconditionally).
 __device__ __forceinline__ int flat_index(const SemArgs& a, const FlatBox& fb, bool cand, int q) {
@@ -1360,7 +1417,7 @@ __device__ __forceinline__ int tile_depth_side(const SemArgs& a, const FlatBox& 
   return 0;
 }
 
-template <int M, bool FAST, bool WS = false, bool LP = false>
+template <int M, bool FAST, bool WS = false, bool LP = false, bool COARSE = false>
 __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const SemTile* __restrict__ tiles,
                                                                const PairConst* __restrict__ pcs,
                                                                uint32_t* __restrict__ pair_cnt,
@@ -1413,7 +1470,7 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
     const int cpy = cast_to_int_x86(round(y2));
     const bool cin = !(cpx < 0 || cpx >= a.W || cpy < 0 || cpy >= a.H);
     FlatBox fb;
-    const bool cand = flat_box<M>(P, c, K2, fb);
+    const bool cand = COARSE ? flat_box_coarse<M>(P, c, K2, fb) : flat_box<M>(P, c, K2, fb);
     bool decided = false;   // the centre outcome and the flat test are settled without the raster
     bool resolved = false;  // the centre outcome is settled (the flat test may have failed)
     if constexpr (LP) {
@@ -2129,7 +2186,11 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
       if (nt == 0) continue;
       dispatch_model(model, [&](auto m) {
         constexpr int M = decltype(m)::value;
-        if (a.lab8)
+        if (a.lab8 && ctx->sem_coarse)
+          hipLaunchKernelGGL((semantic_flat_kernel<M, true, false, true, true>), dim3(nt), dim3(kBlock), 0, s, a,
+                             S->tiles.ptr + t0, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr,
+                             S->status.ptr, S->J.ptr, ws);
+        else if (a.lab8)
           hipLaunchKernelGGL((semantic_flat_kernel<M, true, false, true>), dim3(nt), dim3(kBlock), 0, s, a,
                              S->tiles.ptr + t0, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr,
                              S->status.ptr, S->J.ptr, ws);

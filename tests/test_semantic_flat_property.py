@@ -17,6 +17,7 @@ tests then check that the product's flat pass clears exactly such samples:
 tests/test_gpu_parity.py test_semantic_flat_test_regimes.)
 """
 import numpy as np
+import pytest
 
 import mi_ba
 import oracle
@@ -61,12 +62,15 @@ CASES = [
 ]
 
 
-def test_flat_test_never_clears_a_non_flat_stencil():
+@pytest.mark.parametrize("coarse", [False, True])
+def test_flat_test_never_clears_a_non_flat_stencil(coarse):
+    """coarse: the form with the stencil classes' componentwise maxima
+    (semantic_flat_coarse, csrc/semantic.hip flat_box_coarse)."""
     total = cleared = nonzero = 0
     rows = []
     for model, extra, rel, seed, kw in CASES:
         sc, sem = scene(model, extra, rel, seed, **kw)
-        c = oracle.semantic_flat_property(mi_ba.default_options(), sc, sem)
+        c = oracle.semantic_flat_property(mi_ba.default_options(), sc, sem, coarse=coarse)
         rows.append((model, rel, seed, c))
         assert c["cleared_not_flat"] == 0, (model, extra, rel, seed, kw, c)
         total += c["samples"]
@@ -85,4 +89,6 @@ def test_property_check_catches_an_unsound_bound():
     clears samples whose stencil is not flat, and the check reports them."""
     sc, sem = scene(mi_ba.OPENCV, (-0.6, 0.3, 0.01, -0.01), 1e-2, 6)
     c = oracle.semantic_flat_property(mi_ba.default_options(), sc, sem, bound_scale=0.3)
+    assert c["cleared_not_flat"] > 0, c
+    c = oracle.semantic_flat_property(mi_ba.default_options(), sc, sem, bound_scale=0.3, coarse=True)
     assert c["cleared_not_flat"] > 0, c

@@ -1,9 +1,9 @@
 """The C4 linearization step (as bench.py) with the reprojection kernel's
-inputs warmed beside the semantic deferred pass ("linearize_warm_inputs" 1,
-the default: semantic pass first, a read-only kernel on a side stream streams
-observations / ids / points into the memory-side cache) against the
-reprojection kernel first (0): step wall time and the two kernels' times
-(HIP events) over interleaved rounds; the step's cost checked equal.
+inputs read into the memory-side cache right before it
+("linearize_warm_inputs": range mask, default 1 = the observations) and the
+flat pass's coarse box ("semantic_flat_coarse"): step wall time, the kernels'
+times (HIP events) and the warm-up's over interleaved rounds; the step's cost,
+r and J checked equal.
     python tools/ab_linearize_warm.py [--rounds 6] [--reps 10]"""
 import argparse
 import json
@@ -25,14 +25,15 @@ ap.add_argument("--reps", type=int, default=10)
 args = ap.parse_args()
 sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
 ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
-# (linearize_warm_inputs range mask: 1 observations, 2 image ids, 4 point ids,
-#  8 points; warm_workgroups: 0 one per CU)
-CONFIGS = [(0, 2048), (15, 2048), (15, 0), (14, 2048), (1, 2048), (15, 8192)]
+# (linearize_warm_inputs: range mask read right before the reprojection
+#  kernel, 1 observations, 2 image ids, 4 point ids, 8 points; 0 off;
+#  semantic_flat_coarse)
+CONFIGS = [(0, 0), (1, 0), (15, 0), (3, 0), (1, 1)]
 
 
 def apply(cfg):
     ctx.set_tuning("linearize_warm_inputs", cfg[0])
-    ctx.set_tuning("warm_workgroups", cfg[1])
+    ctx.set_tuning("semantic_flat_coarse", cfg[1])
 
 
 costs, same = {}, {}
@@ -63,12 +64,14 @@ for rnd in range(args.rounds):
         wall = (time.perf_counter() - t0) / args.reps * 1e3
         sj = ctx.kernel_time("semantic_jacobian")
         rj = ctx.kernel_time("reproj_jacobian")
+        wj = ctx.kernel_time("input_warm")
         ctx.set_timing(False)
-        res[cfg].append((sj[0] / sj[1], rj[0] / rj[1], wall))
+        res[cfg].append((sj[0] / sj[1], rj[0] / rj[1], wall, wj[0] / max(1, wj[1])))
 for cfg in CONFIGS:
     a = np.array(res[cfg])
-    print(json.dumps({"linearize_warm_inputs": cfg[0], "warm_workgroups": cfg[1], "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
+    print(json.dumps({"linearize_warm_inputs": cfg[0], "semantic_flat_coarse": cfg[1], "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
                       "semantic_ms_median": float(np.median(a[:, 0])), "reproj_ms_median": float(np.median(a[:, 1])),
-                      "step_wall_ms_median": float(np.median(a[:, 2])), "rounds": args.rounds, "reps": args.reps}),
+                      "step_wall_ms_median": float(np.median(a[:, 2])),
+                      "input_warm_ms_median": float(np.median(a[:, 3])), "rounds": args.rounds, "reps": args.reps}),
           flush=True)
 ctx.close()
