@@ -13,6 +13,8 @@ import time
 
 import numpy as np
 
+if "--overlap" in sys.argv:
+    os.environ.setdefault("MI_BA_LIB", "ab")  # linearize_overlap: the tools-only build (make ab)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "semantic-bundle-adjustment-colmap_amd"))
 sys.path.insert(0, ROOT)
@@ -22,18 +24,25 @@ import bench  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=6)
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--overlap", action="store_true",
+                help="the semantic pass on a second stream beside the reprojection kernel (1) or only its "
+                     "deferred pass (2), with the warm-up (tools build)")
 args = ap.parse_args()
 sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
 ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
 # (linearize_warm_inputs: range mask read right before the reprojection
 #  kernel, 1 observations, 2 image ids, 4 point ids, 8 points; 0 off;
 #  semantic_flat_coarse)
-CONFIGS = [(0, 0), (1, 0), (15, 0), (3, 0), (1, 1)]
+CONFIGS = [(0, 0, 0), (1, 0, 0), (15, 0, 0), (3, 0, 0), (1, 1, 0)]
+if args.overlap:
+    CONFIGS = [(1, 0, 0), (1, 0, 1), (1, 0, 2), (0, 0, 1)]
 
 
 def apply(cfg):
     ctx.set_tuning("linearize_warm_inputs", cfg[0])
     ctx.set_tuning("semantic_flat_coarse", cfg[1])
+    if args.overlap:
+        ctx.set_tuning("linearize_overlap", cfg[2])
 
 
 costs, same = {}, {}
@@ -69,7 +78,7 @@ for rnd in range(args.rounds):
         res[cfg].append((sj[0] / sj[1], rj[0] / rj[1], wall, wj[0] / max(1, wj[1])))
 for cfg in CONFIGS:
     a = np.array(res[cfg])
-    print(json.dumps({"linearize_warm_inputs": cfg[0], "semantic_flat_coarse": cfg[1], "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
+    print(json.dumps({"linearize_warm_inputs": cfg[0], "semantic_flat_coarse": cfg[1], "linearize_overlap": cfg[2], "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
                       "semantic_ms_median": float(np.median(a[:, 0])), "reproj_ms_median": float(np.median(a[:, 1])),
                       "step_wall_ms_median": float(np.median(a[:, 2])),
                       "input_warm_ms_median": float(np.median(a[:, 3])), "rounds": args.rounds, "reps": args.reps}),

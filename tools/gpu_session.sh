@@ -37,6 +37,9 @@ for stage in "$@"; do
     warm)
       timeout -k 10 300 python -u tools/ab_linearize_warm.py > gpurun_out/$T/ab_warm.jsonl 2> gpurun_out/$T/ab_warm.err || exit 1
       cat gpurun_out/$T/ab_warm.jsonl ;;
+    warmov)
+      timeout -k 10 300 python -u tools/ab_linearize_warm.py --overlap > gpurun_out/$T/ab_warm_overlap.jsonl 2> gpurun_out/$T/ab_warm_overlap.err || exit 1
+      cat gpurun_out/$T/ab_warm_overlap.jsonl ;;
     lmkeys)
       timeout -k 10 900 python -u tools/ab_lm_keys.py "" $LMKEYS > gpurun_out/$T/ab_lm_keys.jsonl 2> gpurun_out/$T/ab_lm_keys.err || exit 1
       cat gpurun_out/$T/ab_lm_keys.jsonl ;;
