@@ -529,10 +529,12 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *                           rasters hold more than 256 distinct labels); 0 off
  *   "semantic_window_summary" 1: 3x3 window summaries of every raster pixel (the
  *                           default when the label planes are off); 0 off
- *   "linearize_warm_inputs" 15 / 1 (default): the semantic pass first, the
- *                           reprojection kernel's inputs read into the memory-side
- *                           cache beside its deferred pass; a mask of 1 observations,
- *                           2 image ids, 4 point ids, 8 points; 0: reprojection first
+ *   "linearize_warm_inputs" range mask of the reprojection kernel's inputs read into
+ *                           the memory-side cache right before it (semantic contexts):
+ *                           1 observations, 2 image ids, 4 point ids, 8 points;
+ *                           default 15, 0 off
+ *   "semantic_flat_coarse"  1 (default): the flat pass's pixel box from the stencil
+ *                           classes' componentwise maximum displacement; 0 per class
  *   "warm_workgroups"       workgroups of that read (default 2048; 0 one per CU)
  *   "linearize_overlap"     1 semantic kernel on a second stream beside the reprojection
  *                           kernel, 0 one stream (default)

@@ -91,7 +91,7 @@ struct mi_ba_context {
   miba::DevArray<double> sum_ws;      // [kSumScratch] stage + ticket of launch_sum's many-workgroup pass
   int lin_overlap = 0;                 // 1 semantic kernels on lin_side beside the reprojection kernel,
                                        // 2 flat pass first, deferred pass on lin_side beside it
-  int lin_warm = 1;                    // "linearize_warm_inputs": range mask read right before the reprojection kernel
+  int lin_warm = 15;                   // "linearize_warm_inputs": range mask read right before the reprojection kernel
                                        // (1 observations, 2 image ids, 4 point ids, 8 points; 0 off)
   int lin_warm_conc = 0;               // "linearize_warm_concurrent" (tools): that read beside the semantic deferred pass
   int warm_wgs = 2048;                 // workgroups of the warm-up kernel (0: one per CU)
@@ -101,7 +101,8 @@ struct mi_ba_context {
   int sem_diag = 0;      // "semantic_diag" 1: downloaded status is offset by +0x1000 for samples the flat test
                          // deferred; 2: also by +0x4000 for samples a window summary decided
   bool sem_deferred_box = false;  // "semantic_deferred_box": the deferred pass reads each sample's 3x3 box once
-  int sem_coarse = 0;    // "semantic_flat_coarse": the flat pass's box from the classes' componentwise maxima
+  int sem_coarse = 1;    // "semantic_flat_coarse": the flat pass's box from the classes' componentwise maxima
+                         // (default; 0 the per-class bounds)
   int sem_variant = 6;   // semantic kernel ("semantic_variant"): 6 flat pass + deferred-sample pass (0.42 ms at C4), 5 flat test + in-tile gather, 4/3/2 batched stencil with 4/2/1 parameters per step (0.70 ms), 1 per-point FMA route (0.82 ms), 0 per-point uncontracted (0.92 ms); all bitwise equal
 
   // linearization

@@ -916,12 +916,12 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
   }
-  // linearize_warm_inputs (default: the observations): the reprojection
-  // kernel's streamed inputs read right before it, so the memory-side cache
-  // serves its reads and HBM sees its J / r write stream alone (in-step 0.567
-  // -> 0.420 ms at C4 for a ~0.03 ms read of the 160 MB of observations,
-  // profiles/r4_ab_linearize_warm_ranges.jsonl).  Only after the semantic
-  // pass has used the cache; a geometric-only step finds them cached.
+  // linearize_warm_inputs (default: every range): the reprojection kernel's
+  // streamed inputs (264 MB at C4) read right before it, so the memory-side
+  // cache serves its reads and HBM sees its J / r write stream alone (in-step
+  // 0.576 -> 0.431 ms at C4 for a 0.055 ms read; the observations or ids alone
+  // do not do it: profiles/r4_ab_linearize_warm_ranges.jsonl).  Only after the
+  // semantic pass has used the cache; a geometric-only step finds them cached.
   hipEvent_t wstop = nullptr;
   if (ctx->sem && ctx->lin_warm && d.nb > 0) {
     timer_begin(ctx, "input_warm", &wstop);
@@ -1991,7 +1991,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     return MI_BA_OK;
   }
   // range mask of the inputs read right before the reprojection kernel (1
-  // observations (default), 2 image ids, 4 point ids, 8 points; 0 off)
+  // observations, 2 image ids, 4 point ids, 8 points; default 15; 0 off)
   if (std::strcmp(key, "linearize_warm_inputs") == 0 && value >= 0 && value <= 15) {
     ctx->lin_warm = value;
     return MI_BA_OK;
