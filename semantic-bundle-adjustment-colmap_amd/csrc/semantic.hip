@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 
 #include "ba_math.h"
 #include "kernels.h"
@@ -2186,22 +2187,20 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
       if (nt == 0) continue;
       dispatch_model(model, [&](auto m) {
         constexpr int M = decltype(m)::value;
-        if (a.lab8 && ctx->sem_coarse)
-          hipLaunchKernelGGL((semantic_flat_kernel<M, true, false, true, true>), dim3(nt), dim3(kBlock), 0, s, a,
-                             S->tiles.ptr + t0, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr,
-                             S->status.ptr, S->J.ptr, ws);
-        else if (a.lab8)
-          hipLaunchKernelGGL((semantic_flat_kernel<M, true, false, true>), dim3(nt), dim3(kBlock), 0, s, a,
-                             S->tiles.ptr + t0, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr,
-                             S->status.ptr, S->J.ptr, ws);
+        auto launch = [&](auto ws_, auto lp_, auto coarse_) {
+          hipLaunchKernelGGL((semantic_flat_kernel<M, true, decltype(ws_)::value, decltype(lp_)::value,
+                                                   decltype(coarse_)::value>),
+                             dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0, pcs, S->pair_cnt.ptr, S->dlist.ptr,
+                             S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr, ws);
+        };
+        using T = std::true_type;
+        using F = std::false_type;
+        if (a.lab8)
+          ctx->sem_coarse ? launch(F{}, T{}, T{}) : launch(F{}, T{}, F{});
         else if (a.wsum)
-          hipLaunchKernelGGL((semantic_flat_kernel<M, true, true>), dim3(nt), dim3(kBlock), 0, s, a,
-                             S->tiles.ptr + t0, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr,
-                             S->status.ptr, S->J.ptr, ws);
+          ctx->sem_coarse ? launch(T{}, F{}, T{}) : launch(T{}, F{}, F{});
         else
-          hipLaunchKernelGGL((semantic_flat_kernel<M, true>), dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0,
-                             pcs, S->pair_cnt.ptr, S->dlist.ptr, S->partial.ptr + t0, S->r.ptr, S->status.ptr,
-                             S->J.ptr, ws);
+          ctx->sem_coarse ? launch(F{}, F{}, T{}) : launch(F{}, F{}, F{});
       });
     }
     if (after_flat) {
