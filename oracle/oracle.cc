@@ -512,6 +512,36 @@ double FlatDistortionGain(int model, const double* K, double r2) {
   return 1.0 + s * g * g * g;
 }
 
+// Upper bounds of |d(x, y) / d(u, v)| from the radius (semantic.hip
+// image_jac_bound; the coarse form)
+void FlatImageJacBound(int model, const double* K, double u, double v, double Ah[4]) {
+  const double r2 = u * u + v * v, r1 = std::fabs(u) + std::fabs(v);
+  if (model == MI_BA_SIMPLE_PINHOLE) {
+    Ah[0] = Ah[3] = std::fabs(K[0]);
+    Ah[1] = Ah[2] = 0.0;
+  } else if (model == MI_BA_PINHOLE) {
+    Ah[0] = std::fabs(K[0]);
+    Ah[3] = std::fabs(K[1]);
+    Ah[1] = Ah[2] = 0.0;
+  } else if (model == MI_BA_SIMPLE_RADIAL) {
+    const double k = std::fabs(K[3]);
+    Ah[0] = Ah[3] = std::fabs(K[0]) * (1.0 + 3.0 * k * r2);
+    Ah[1] = Ah[2] = std::fabs(K[0]) * (k * r2);
+  } else if (model == MI_BA_RADIAL) {
+    const double k1 = std::fabs(K[3]), k2 = std::fabs(K[4]);
+    Ah[0] = Ah[3] = std::fabs(K[0]) * (1.0 + 3.0 * k1 * r2 + 5.0 * k2 * r2 * r2);
+    Ah[1] = Ah[2] = std::fabs(K[0]) * (k1 * r2 + 2.0 * k2 * r2 * r2);
+  } else {
+    const double k1 = std::fabs(K[4]), k2 = std::fabs(K[5]), p1 = std::fabs(K[6]), p2 = std::fabs(K[7]);
+    const double rad = 3.0 * k1 * r2 + 5.0 * k2 * r2 * r2;
+    const double off = k1 * r2 + 2.0 * k2 * r2 * r2 + 2.0 * (p1 + p2) * r1;
+    Ah[0] = std::fabs(K[0]) * (1.0 + rad + (2.0 * p1 + 6.0 * p2) * r1);
+    Ah[1] = std::fabs(K[0]) * off;
+    Ah[2] = std::fabs(K[1]) * off;
+    Ah[3] = std::fabs(K[1]) * (1.0 + rad + (6.0 * p1 + 2.0 * p2) * r1);
+  }
+}
+
 // every second derivative of (u, v) -> u + Du over |(u, v)| <= rho
 double FlatSecondDerivativeBound(int model, const double* K, double rho) {
   if (model == MI_BA_SIMPLE_RADIAL) return 6.0 * std::fabs(K[3]) * rho;
@@ -541,13 +571,21 @@ bool FlatClears(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* se
   const double z = p2[2];
   if (!(z > 0.0)) return false;
   const double iz = 1.0 / z;
-  const double u = p2[0] * iz, v = p2[1] * iz;
+  double u = p2[0] * iz, v = p2[1] * iz;
   // x, y and A = d(x, y) / d(u, v) by dual numbers
   Jet<2> Kj[8], uj(u, 0), vj(v, 1), xj, yj;
   for (int m = 0; m < NumParams(model); ++m) Kj[m] = Jet<2>(K[m]);
   WorldToImage(model, Kj, uj, vj, &xj, &yj);
-  const double x = xj.a, y = yj.a;
-  const double A[4] = {xj.v[0], xj.v[1], yj.v[0], yj.v[1]};
+  double x = xj.a, y = yj.a;
+  double A[4] = {xj.v[0], xj.v[1], yj.v[0], yj.v[1]};
+  if (g_flat_coarse) {
+    // the coarse form expands about the reference's own centre pixel and
+    // bounds |A| from the radius (semantic.hip image_jac_bound)
+    u = p2[0] / p2[2];
+    v = p2[1] / p2[2];
+    WorldToImage(model, K, u, v, &x, &y);
+    FlatImageJacBound(model, K, u, v, A);
+  }
   if (!(std::fabs(x) < 1e8 && std::fabs(y) < 1e8 && std::fabs(u) < 1e6 && std::fabs(v) < 1e6)) return false;
   const double dq1 = var1 ? B.rho1 * std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]) * (1.0 + 1e-12) : 0.0;
   const double dq2 = var2 ? B.rho2 * std::sqrt(pw[0] * pw[0] + pw[1] * pw[1] + pw[2] * pw[2]) * (1.0 + 1e-12) : 0.0;

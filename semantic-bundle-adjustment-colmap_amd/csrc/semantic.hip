@@ -1036,23 +1036,54 @@ __device__ __forceinline__ bool flat_box(const PairConst* __restrict__ P, const 
   return fb.ncol <= 3 && fb.nrow <= 3;
 }
 
+// Upper bounds of |A| = |d(x, y) / d(u, v)| at (u, v) from the radius alone
+// (triangle inequality on the models' derivatives, 2 |u v| <= r^2, |u|, |v|
+// <= r <= |u| + |v|): radial u r^2 gives d/du <= 3 r^2, d/dv <= r^2; u r^4
+// gives 5 r^4, 2 r^4; the OPENCV tangential terms 2 p1 u v + p2 (r^2 + 2 u^2)
+// give (2 |p1| + 6 |p2|) r1 and 2 (|p1| + |p2|) r1 (v alike with p1, p2
+// swapped), r1 = |u| + |v|.
+template <int M>
+__device__ __forceinline__ void image_jac_bound(const double* K, double u, double v, double Ah[4]) {
+  const double r2 = u * u + v * v, r1 = fabs(u) + fabs(v);
+  if constexpr (M == kSimplePinhole) {
+    Ah[0] = Ah[3] = fabs(K[0]);
+    Ah[1] = Ah[2] = 0.0;
+  } else if constexpr (M == kPinhole) {
+    Ah[0] = fabs(K[0]);
+    Ah[3] = fabs(K[1]);
+    Ah[1] = Ah[2] = 0.0;
+  } else if constexpr (M == kSimpleRadial) {
+    const double k = fabs(K[3]);
+    Ah[0] = Ah[3] = fabs(K[0]) * (1.0 + 3.0 * k * r2);
+    Ah[1] = Ah[2] = fabs(K[0]) * (k * r2);
+  } else if constexpr (M == kRadial) {
+    const double k1 = fabs(K[3]), k2 = fabs(K[4]);
+    Ah[0] = Ah[3] = fabs(K[0]) * (1.0 + 3.0 * k1 * r2 + 5.0 * k2 * r2 * r2);
+    Ah[1] = Ah[2] = fabs(K[0]) * (k1 * r2 + 2.0 * k2 * r2 * r2);
+  } else {
+    const double k1 = fabs(K[4]), k2 = fabs(K[5]), p1 = fabs(K[6]), p2 = fabs(K[7]);
+    const double rad = 3.0 * k1 * r2 + 5.0 * k2 * r2 * r2, off = k1 * r2 + 2.0 * k2 * r2 * r2 + 2.0 * (p1 + p2) * r1;
+    Ah[0] = fabs(K[0]) * (1.0 + rad + (2.0 * p1 + 6.0 * p2) * r1);
+    Ah[1] = fabs(K[0]) * off;
+    Ah[2] = fabs(K[1]) * off;
+    Ah[3] = fabs(K[1]) * (1.0 + rad + (6.0 * p1 + 2.0 * p2) * r1);
+  }
+}
+
 // flat_box with the per-class displacement bounds replaced by their
 // componentwise maxima (ax, ay, az) over the classes: each class's pixel
 // bound is monotone in its (ax, ay, az) and in 1 / (z - az), so the one bound
 // covers every class — a box at most marginally wider, without the per-class
-// loops (about a quarter of the flat pass's FP64 instructions).  The depth
+// loops.  The centre's own (u, v) and pixel (x, y) (the reference sequence)
+// serve as the expansion point and |A| is bounded from the radius
+// (image_jac_bound), so no camera-model Jacobian is evaluated.  The depth
 // bound az is flat_box's.  Restated in the oracle (FlatClears, coarse form)
 // for tests/test_semantic_flat_property.py.
 template <int M>
 __device__ __forceinline__ bool flat_box_coarse(const PairConst* __restrict__ P, const Centre& c, const double* K2,
-                                                FlatBox& fb) {
+                                                double u, double v, double x, double y, FlatBox& fb) {
   const double z = c.p2[2];
   if (!(z > 0.0)) return false;  // NaN-safe
-  const double iz = 1.0 / z;
-  const double u = c.p2[0] * iz, v = c.p2[1] * iz;
-  constexpr int np = Model<M>::kNumParams;
-  double x, y, A[4], Jp[2 * np];
-  world_to_image_jac<M>(K2, u, v, &x, &y, A, Jp);
   if (!(fabs(x) < 1e8 && fabs(y) < 1e8 && fabs(u) < 1e6 && fabs(v) < 1e6)) return false;
   double ax = 0.0, ay = 0.0, az = 0.0;
   if (P->var1) {
@@ -1077,11 +1108,13 @@ __device__ __forceinline__ bool flat_box_coarse(const PairConst* __restrict__ P,
   const double H = second_derivative_bound<M>(K2, sqrt(ru * ru + rv * rv) * (1.0 + 1e-12));
   const double fx = fabs(K2[0]);
   const double fy = (M == kPinhole || M == kOpenCV) ? fabs(K2[1]) : fabs(K2[0]);
+  double Ah[4];
+  image_jac_bound<M>(K2, u, v, Ah);
   const double sk = cu + cv;
-  const double bxm = (fabs(A[0]) + fx * H * sk) * cu + (fabs(A[1]) + fx * H * sk) * cv;
-  const double bym = (fabs(A[2]) + fy * H * sk) * cu + (fabs(A[3]) + fy * H * sk) * cv;
+  const double bxm = (Ah[0] + fx * H * sk) * cu + (Ah[1] + fx * H * sk) * cv;
+  const double bym = (Ah[2] + fy * H * sk) * cu + (Ah[3] + fy * H * sk) * cv;
   const double gain = distortion_gain<M>(K2, u * u + v * v);
-  const double kscale = (fabs(K2[0]) + fabs(K2[1])) * gain * (1.0 + fabs(u) + fabs(v)) * (1.0 + c.mag * fabs(iz));
+  const double kscale = (fabs(K2[0]) + fabs(K2[1])) * gain * (1.0 + fabs(u) + fabs(v)) * (1.0 + c.mag * fabs(1.0 / z));
   const double ex = 1e-6 + 1e-11 * (kscale + fabs(x) + fabs(y));
   const double bx = bxm * (1.0 + 1e-12) + ex;
   const double by = bym * (1.0 + 1e-12) + ex;
@@ -1471,7 +1504,7 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
     const int cpy = cast_to_int_x86(round(y2));
     const bool cin = !(cpx < 0 || cpx >= a.W || cpy < 0 || cpy >= a.H);
     FlatBox fb;
-    const bool cand = COARSE ? flat_box_coarse<M>(P, c, K2, fb) : flat_box<M>(P, c, K2, fb);
+    const bool cand = COARSE ? flat_box_coarse<M>(P, c, K2, u2, v2, x2, y2, fb) : flat_box<M>(P, c, K2, fb);
     bool decided = false;   // the centre outcome and the flat test are settled without the raster
     bool resolved = false;  // the centre outcome is settled (the flat test may have failed)
     if constexpr (LP) {
