@@ -75,6 +75,9 @@ struct SemanticState {
   DevArray<uint32_t> pair_cnt;             // [npairs] deferred samples of the pair
   DevArray<uint32_t> dlist;                // [ns] deferred samples (offset in pair), pair regions
   DevArray<uint2> chunks;                  // (pair, first entry): 64-entry chunks of every pair region
+  DevArray<uint2> dchunks;                 // the chunks the flat pass filled (deferred_compact_kernel), same regions
+  DevArray<uint32_t> dcount;               // [model] their number
+  int n_cu = 256;                          // compute units (the deferred pass's resident grid)
   int model_chunks[kNumModels + 1] = {};   // chunk range of each camera model
 };
 

@@ -1602,6 +1602,7 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
 // (chunks past the pair's count exit at once).
 template <int M, bool FAST, int NB, bool BOX = false>
 __global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const uint2* __restrict__ chunks,
+                                                              const uint32_t* __restrict__ ccount,
                                                               const PairConst* __restrict__ pcs,
                                                               const uint32_t* __restrict__ pair_cnt,
                                                               const uint32_t* __restrict__ dlist,
@@ -1609,9 +1610,15 @@ __global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const 
                                                               double* __restrict__ J_out, int write_samples) {
   __shared__ double sJ[64 * kSemRow];
   __shared__ float2 sbox[BOX ? 64 * 9 : 1];  // BOX: each lane's 3 x 3 box of raster pixels
-  const uint2 ch = chunks[blockIdx.x];  // (pair, first entry)
+  // ccount (the compacted list's length, deferred_compact_kernel): a grid of
+  // resident workgroups loops over the non-empty chunks; null: one chunk per
+  // workgroup over the whole static list (empty chunks exit at once)
+  const uint32_t nch = ccount ? *ccount : blockIdx.x + 1;
+  const uint32_t stride = ccount ? gridDim.x : 1u;
+  for (uint32_t ci = blockIdx.x; ci < nch; ci += stride) {
+  const uint2 ch = chunks[ci];  // (pair, first entry)
   const uint32_t cnt = pair_cnt[ch.x];
-  if (ch.y >= cnt) return;
+  if (ch.y >= cnt) continue;  // workgroup-uniform
   const PairConst* __restrict__ P = pcs + ch.x;
   const int lane = threadIdx.x;
   const uint32_t k = ch.y + lane;
@@ -1676,6 +1683,49 @@ __global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const 
       for (int q = 0; q < rows; ++q) acc += sJ[q * kSemRow + ca] * sJ[q * kSemRow + cb];
       atomicAdd(pair_blk + (size_t)ch.x * kPairStride + e, acc);
     }
+  }
+  __syncthreads();  // sJ / sbox are rewritten by the next chunk
+  }
+}
+
+// The deferred pass's work list: the static list of every pair's possible
+// 64-entry chunks (grouped by model, model_chunks) filtered to the chunks the
+// flat pass filled (first entry < pair_cnt), per model into the same region
+// of `out`, counts in cnt[model] (zeroed before).  Launching one workgroup per
+// static chunk instead spent the deferred pass's time dispatching the ~92 %
+// that are empty (80k workgroups for 6.4k chunks at C4).  One atomic per wave
+// and model; the order within a model is the atomics' (the pair sums already
+// accumulate by atomics in any order).
+struct ModelRanges {
+  int b[kNumModels + 1];
+};
+
+__global__ __launch_bounds__(256) void deferred_compact_kernel(const uint2* __restrict__ chunks, int nchunks,
+                                                               const uint32_t* __restrict__ pair_cnt, ModelRanges mr,
+                                                               uint2* __restrict__ out, uint32_t* __restrict__ cnt) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool valid = i < nchunks;
+  uint2 ch = make_uint2(0u, 0u);
+  int m = 0;
+  bool live = false;
+  if (valid) {
+    ch = chunks[i];
+    live = ch.y < pair_cnt[ch.x];
+    while (m + 1 < kNumModels && i >= mr.b[m + 1]) ++m;
+  }
+  unsigned long long todo = __ballot(valid);
+  while (todo) {
+    const int leader = __ffsll((long long)todo) - 1;
+    const int mm = __shfl(m, leader, 64);
+    const unsigned long long grp = __ballot(valid && m == mm);
+    const unsigned long long sel = __ballot(valid && m == mm && live);
+    uint32_t base = 0;
+    if (lane == leader && sel) base = atomicAdd(cnt + mm, (uint32_t)__popcll(sel));
+    base = __shfl(base, leader, 64);
+    if (valid && m == mm && live)
+      out[mr.b[mm] + base + (uint32_t)__popcll(sel & ((1ull << lane) - 1ull))] = ch;
+    todo &= ~grp;
   }
 }
 
@@ -2022,8 +2072,16 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
     }
   }
   if (S->pair_cnt.alloc(std::max(1, S->npairs)) || S->dlist.alloc(std::max<int64_t>(1, S->ns)) ||
-      S->chunks.alloc(std::max<size_t>(1, chunks.size())))
+      S->chunks.alloc(std::max<size_t>(1, chunks.size())) || S->dchunks.alloc(std::max<size_t>(1, chunks.size())) ||
+      S->dcount.alloc(kNumModels))
     return MI_BA_ERR_OUT_OF_MEMORY;
+  {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) ||
+        ncu <= 0)
+      ncu = 256;
+    S->n_cu = ncu;
+  }
   if (!chunks.empty() && hipMemcpy(S->chunks.ptr, chunks.data(), chunks.size() * sizeof(uint2), hipMemcpyHostToDevice))
     return MI_BA_ERR_HIP;
   if (S->samples.alloc(S->ns) || S->pairs.alloc(S->npairs) || S->raster_slot.alloc(I) ||
@@ -2200,20 +2258,35 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   const bool split = deferred_stream != nullptr && ctx->sem_variant == 6;
   if (ctx->sem_variant == 6) {
     const int ws = write_samples ? 1 | (ctx->sem_diag ? 2 : 0) | (ctx->sem_diag == 2 ? 4 : 0) : 0;
-    auto deferred = [&](hipStream_t ds) {
+    auto deferred = [&](hipStream_t ds) -> mi_ba_status {
+      // the non-empty chunks, then a resident grid per model looping over them
+      const int nall = S->model_chunks[kNumModels];
+      const bool compact = ctx->sem_compact != 0;
+      if (nall > 0 && compact) {
+        ModelRanges mr;
+        for (int m = 0; m <= kNumModels; ++m) mr.b[m] = S->model_chunks[m];
+        if (hipMemsetAsync(S->dcount.ptr, 0, S->dcount.bytes(), ds) != hipSuccess) return MI_BA_ERR_HIP;
+        hipLaunchKernelGGL(deferred_compact_kernel, dim3((unsigned)((nall + 255) / 256)), dim3(256), 0, ds,
+                           S->chunks.ptr, nall, S->pair_cnt.ptr, mr, S->dchunks.ptr, S->dcount.ptr);
+      }
       for (int model = 0; model < kNumModels; ++model) {
         const int c0 = S->model_chunks[model], nc = S->model_chunks[model + 1] - c0;
         if (S->model_tiles[model + 1] == S->model_tiles[model] || nc == 0) continue;
+        // compact: 64-thread workgroups, 16 resident per CU; else one per static chunk
+        const int grid = compact ? std::min(nc, 16 * S->n_cu) : nc;
+        const uint2* list = (compact ? S->dchunks.ptr : S->chunks.ptr) + c0;
+        const uint32_t* count = compact ? S->dcount.ptr + model : nullptr;
         dispatch_model(model, [&](auto m) {
           constexpr int M = decltype(m)::value;
           if (ctx->sem_deferred_box)
-            hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4, true>), dim3(nc), dim3(64), 0, ds, a,
-                               S->chunks.ptr + c0, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
+            hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4, true>), dim3(grid), dim3(64), 0, ds, a, list,
+                               count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
           else
-            hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4>), dim3(nc), dim3(64), 0, ds, a, S->chunks.ptr + c0,
+            hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4>), dim3(grid), dim3(64), 0, ds, a, list, count,
                                pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
         });
       }
+      return MI_BA_OK;
     };
     for (int model = 0; model < kNumModels; ++model) {
       const int t0 = S->model_tiles[model], nt = S->model_tiles[model + 1] - t0;
@@ -2243,9 +2316,11 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
     if (split) {
       if (hipEventRecord(flat_done, s) != hipSuccess || hipStreamWaitEvent(deferred_stream, flat_done, 0) != hipSuccess)
         return MI_BA_ERR_HIP;
-      deferred(deferred_stream);
+      const mi_ba_status st = deferred(deferred_stream);
+      if (st != MI_BA_OK) return st;
     } else {
-      deferred(s);
+      const mi_ba_status st = deferred(s);
+      if (st != MI_BA_OK) return st;
     }
   }
 #ifdef MI_BA_AB_VARIANTS

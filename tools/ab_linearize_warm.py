@@ -33,7 +33,7 @@ ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
 # (linearize_warm_inputs: range mask read right before the reprojection
 #  kernel, 1 observations, 2 image ids, 4 point ids, 8 points; 0 off;
 #  semantic_flat_coarse)
-CONFIGS = [(0, 0, 0), (15, 1, 0), (15, 0, 0), (0, 1, 0)]
+CONFIGS = [(0, 0, 0), (15, 1, 0), (15, 0, 0), (0, 1, 0), (15, 1, 0, 0)]
 if args.overlap:
     CONFIGS = [(15, 1, 0), (15, 1, 1), (15, 1, 2), (0, 1, 1)]
 
@@ -41,6 +41,7 @@ if args.overlap:
 def apply(cfg):
     ctx.set_tuning("linearize_warm_inputs", cfg[0])
     ctx.set_tuning("semantic_flat_coarse", cfg[1])
+    ctx.set_tuning("semantic_deferred_compact", cfg[3] if len(cfg) > 3 else 1)
     if args.overlap:
         ctx.set_tuning("linearize_overlap", cfg[2])
 
@@ -78,7 +79,8 @@ for rnd in range(args.rounds):
         res[cfg].append((sj[0] / sj[1], rj[0] / rj[1], wall, wj[0] / max(1, wj[1])))
 for cfg in CONFIGS:
     a = np.array(res[cfg])
-    print(json.dumps({"linearize_warm_inputs": cfg[0], "semantic_flat_coarse": cfg[1], "linearize_overlap": cfg[2], "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
+    print(json.dumps({"linearize_warm_inputs": cfg[0], "semantic_flat_coarse": cfg[1], "linearize_overlap": cfg[2],
+                      "semantic_deferred_compact": cfg[3] if len(cfg) > 3 else 1, "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
                       "semantic_ms_median": float(np.median(a[:, 0])), "reproj_ms_median": float(np.median(a[:, 1])),
                       "step_wall_ms_median": float(np.median(a[:, 2])),
                       "input_warm_ms_median": float(np.median(a[:, 3])), "rounds": args.rounds, "reps": args.reps}),
