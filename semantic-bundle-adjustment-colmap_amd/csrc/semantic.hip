@@ -1513,18 +1513,20 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
       // valid side the box's labels come from the 1-B label plane
       if (cand && fb.x0 >= 0 && fb.y0 >= 0 && fb.x0 + fb.ncol <= a.W && fb.y0 + fb.nrow <= a.H && cpx >= fb.x0 &&
           cpx < fb.x0 + fb.ncol && cpy >= fb.y0 && cpy < fb.y0 + fb.nrow) {
+        // the tile range and the box's labels requested together (one round
+        // trip; the labels go unused when the depth test settles the box invalid)
         const float2 dr = a.dtile[((size_t)P->slot * a.TH + (fb.y0 >> 3)) * a.TW + (fb.x0 >> 3)];
+        const uint8_t* lp = a.lab8 + (size_t)P->slot * a.H * a.W + (size_t)fb.y0 * a.W + fb.x0;
+        const uint8_t lc = lp[(size_t)(cpy - fb.y0) * a.W + (cpx - fb.x0)];
+        uint8_t L[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) L[q] = (q % 3 < fb.ncol && q / 3 < fb.nrow) ? lp[(size_t)(q / 3) * a.W + q % 3] : lc;
         const int side = tile_depth_side(a, fb, dr, c.p2[2], c.mag);
         if (side == 2) {
           c.st = MI_BA_INVALID_DEPTH;
           c.r = 0.0;
           decided = resolved = true;
         } else if (side == 1) {
-          const uint8_t* lp = a.lab8 + (size_t)P->slot * a.H * a.W + (size_t)fb.y0 * a.W + fb.x0;
-          const uint8_t lc = lp[(size_t)(cpy - fb.y0) * a.W + (cpx - fb.x0)];
-          uint8_t L[9];
-#pragma unroll
-          for (int q = 0; q < 9; ++q) L[q] = (q % 3 < fb.ncol && q / 3 < fb.nrow) ? lp[(size_t)(q / 3) * a.W + q % 3] : lc;
           c.st = MI_BA_VALID;
           c.r = (smp.label1 == spal[lc]) ? 0.0 : 1.0;
           bool flat = true;
