@@ -10,7 +10,7 @@
 # jacsweep (in-step times of the tools-build Jacobian variants JACV), pcg
 # (matrix-free PCG product A/B),
 # prof (trace + traffic PMC of the bench step, summarized), pmcj (reproj PMC b2b vs in-step),
-# pmcs (semantic PMC passes + summary), warm (linearize_warm_inputs A/B), smoke
+# pmcs (semantic PMC passes + summary), warm (linearize_warm_inputs A/B), cpuba (oracle C4 BA iteration on the box's CPU share), smoke
 set -o pipefail
 T=${1:?tag}
 shift
@@ -37,6 +37,9 @@ for stage in "$@"; do
     warm)
       timeout -k 10 300 python -u tools/ab_linearize_warm.py > gpurun_out/$T/ab_warm.jsonl 2> gpurun_out/$T/ab_warm.err || exit 1
       cat gpurun_out/$T/ab_warm.jsonl ;;
+    cpuba)
+      timeout -k 10 600 python -u tools/cpu_ba_iteration.py --config C4 --iters 1 > gpurun_out/$T/cpu_ba_c4.json 2> gpurun_out/$T/cpu_ba_c4.err || exit 1
+      cat gpurun_out/$T/cpu_ba_c4.json ;;
     warmov)
       timeout -k 10 300 python -u tools/ab_linearize_warm.py --overlap > gpurun_out/$T/ab_warm_overlap.jsonl 2> gpurun_out/$T/ab_warm_overlap.err || exit 1
       cat gpurun_out/$T/ab_warm_overlap.jsonl ;;
