@@ -1460,7 +1460,8 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
   if (ws.ev.size() < 2 * (ps.size() - 1)) return rocblas_status_invalid_size;
   double* scratch_main = ws.scratch;
   double* scratch_side = ws.scratch + kSub * kSub;
-  rocblas_status st = panel_factor(h, n, A, lda, 0, ps[1], info, cfg.own_diag, scratch_main, &ws, ex);
+  auto own_for = [&](int k0) { return cfg.head_own > 0 && k0 < cfg.head_own_cols ? cfg.head_own : cfg.own_diag; };
+  rocblas_status st = panel_factor(h, n, A, lda, 0, ps[1], info, own_for(0), scratch_main, &ws, ex);
   if (st != rocblas_status_success) return st;
   // On a failure after the side stream got work, the caller's stream waits
   // for it (the caller may free A / info once its own stream is drained).
@@ -1508,7 +1509,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     hipEvent_t upd = ws.ev[2 * kk], pan = ws.ev[2 * kk + 1];
     if (hipEventRecord(upd, sm) != hipSuccess || hipStreamWaitEvent(ss, upd, 0) != hipSuccess)
       return fail(rocblas_status_internal_error);
-    st = panel_factor(hs, n, A, lda, k + kb, jb0, info + kk + 1, cfg.own_diag, scratch_side, &ws, ex);
+    st = panel_factor(hs, n, A, lda, k + kb, jb0, info + kk + 1, own_for(k + kb), scratch_side, &ws, ex);
     if (st != rocblas_status_success) return fail(st);
     if (hipEventRecord(pan, ss) != hipSuccess) return fail(rocblas_status_internal_error);
     // the rest of the trailing lower triangle (columns jb0 .. m)
@@ -1745,6 +1746,7 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   CholConfig c = cfg;
   const int widest = std::max({c.panel, c.head_panel, c.tail_panel});
   if (c.own_diag == 6 && (c.panel <= 0 || widest > 64 * kPfMaxTiles)) c.own_diag = 2;
+  if (c.head_own == 6 && (c.panel <= 0 || widest > 64 * kPfMaxTiles)) c.head_own = 2;
 #ifdef MI_BA_AB_VARIANTS
   if (c.own_diag == 7 && (c.panel <= 0 || c.panel > kTinv)) c.own_diag = 2;
 #else

@@ -39,6 +39,10 @@ struct CholConfig {
   // (76 KB LDS, 342 VGPRs per lane) do not halve the dgemm's occupancy on the
   // CUs they share; 0 = off
   int split_cus = 0, split_cols = 0;
+  // head panel kind: panels starting before column head_own_cols use own_diag
+  // head_own (e.g. 2: 64-wide diagonal kernels + rocBLAS dtrsm, no resident
+  // spin-waiting workgroups beside the trailing dgemm); 0 = off
+  int head_own = 0, head_own_cols = 0;
   bool gemm_update = true;
   // look-ahead: the trailing update after the next panel's block column,
   // 0 one dgemm per 512-wide block column, 1 one dsyrk, 2 one dgemmt,

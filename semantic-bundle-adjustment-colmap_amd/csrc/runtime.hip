@@ -2085,6 +2085,14 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.lookahead = value != 0;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "cholesky_head_own_diag") == 0 && (value == 0 || value == 2 || value == 6)) {
+    ctx->chol.head_own = (int)value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_head_own_cols") == 0 && value >= 0) {
+    ctx->chol.head_own_cols = (int)value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_own_diag") == 0 && value >= 0 && value <= 7 && (value != 7 || ab_value(value, 6))) {
     ctx->chol.own_diag = value;
     return MI_BA_OK;

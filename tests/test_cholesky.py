@@ -320,13 +320,16 @@ def test_lm_fused_forward_solve(gpu, images):
 
 @pytest.mark.parametrize("schedule", [dict(head_panel=1024, head_cols=1024), dict(tail_panel=256, tail_cols=768),
                                       dict(head_panel=768, head_cols=700, tail_panel=128, tail_cols=300),
-                                      dict(split_cus=32, split_cols=1024), dict(split_cus=200, split_cols=1593)])
+                                      dict(split_cus=32, split_cols=1024), dict(split_cus=200, split_cols=1593),
+                                      dict(head_own_diag=2, head_own_cols=1024)])
 def test_lm_panel_schedule(gpu, schedule):
     """Non-uniform panel schedules (cholesky_head_panel / _head_cols /
     _tail_panel / _tail_cols: 1024-wide one-launch panels of 16 column tiles,
     narrower ones at the end) drive the same LM as the uniform 512-wide
-    panels (nf = 1593), as does the split head (cholesky_split_cus / _cols:
-    the panel factor and the trailing dgemm on disjoint CU sets), with and
+    panels (nf = 1593), as do the split head (cholesky_split_cus / _cols:
+    the panel factor and the trailing dgemm on disjoint CU sets) and the
+    two-kernel diagonal factor + dtrsm for the head panels
+    (cholesky_head_own_diag / _cols), with and
     without the look-ahead (S itself differs
     between runs in the order of the Schur build's float atomics)."""
     if "split_cus" in schedule and not mi_ba.ab_build():
