@@ -907,17 +907,23 @@ __device__ __forceinline__ void centre_eval(const SemArgs& a, const PairConst* _
 // and the stencil point (perturbed value, 1/(2 delta), the perturbed rotation
 // folded into one 3x3 map, PlusJacobian rows) comes from the per-pair table
 // as wave-uniform scalar loads; a lane forms one mat-vec per point.
+// Returns true when the batched route had to be redone per point (a decision
+// inside a margin; semantic_diag 2 counts them).
 template <int M, bool FAST, int NB>
-__device__ __forceinline__ void stencil_full(const SemArgs& a, const PairConst* __restrict__ P, const Centre& c,
+__device__ __forceinline__ bool stencil_full(const SemArgs& a, const PairConst* __restrict__ P, const Centre& c,
                                              const SemSample& smp, const double* K2, const float2* dl2,
                                              double Jt[12], const float2* box = nullptr,
                                              const FlatBox* fb = nullptr) {
   if constexpr (NB > 0) {
     const int cidx = c.pc.valid ? c.pc.py * a.W + c.pc.px : 0;
-    if (!stencil_batched<M, FAST, NB>(a, P, c.w, c.pw, c.p2, c.mag, smp.label1, K2, dl2, cidx, c.exk, Jt, box, fb))
+    if (!stencil_batched<M, FAST, NB>(a, P, c.w, c.pw, c.p2, c.mag, smp.label1, K2, dl2, cidx, c.exk, Jt, box, fb)) {
       stencil_rolled<M, FAST>(a, P, c.w, c.pw, c.p2, c.mag, smp.pc1, smp.label1, K2, dl2, c.pc, c.exk, Jt);
+      return true;
+    }
+    return false;
   } else {
     stencil_rolled<M, FAST>(a, P, c.w, c.pw, c.p2, c.mag, smp.pc1, smp.label1, K2, dl2, c.pc, c.exk, Jt);
+    return true;
   }
 }
 
@@ -1609,7 +1615,8 @@ __global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const 
                                                               const uint32_t* __restrict__ pair_cnt,
                                                               const uint32_t* __restrict__ dlist,
                                                               double* __restrict__ pair_blk,
-                                                              double* __restrict__ J_out, int write_samples) {
+                                                              double* __restrict__ J_out, int write_samples,
+                                                              int32_t* __restrict__ status_out = nullptr) {
   __shared__ double sJ[64 * kSemRow];
   __shared__ float2 sbox[BOX ? 64 * 9 : 1];  // BOX: each lane's 3 x 3 box of raster pixels
   // ccount (the compacted list's length, deferred_compact_kernel): a grid of
@@ -1636,6 +1643,7 @@ __global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const 
     Centre c;
     centre_eval<M, FAST>(a, P, smp, K2, dl2, c);
     double Jt[12];
+    bool redone;
     if constexpr (BOX) {
       // the reachable box (the flat test's bound), read in one round trip:
       // the stencil's steps then take their pixels from LDS
@@ -1644,13 +1652,14 @@ __global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const 
         float2* mine = sbox + 9 * lane;
 #pragma unroll
         for (int q = 0; q < 9; ++q) mine[q] = dl2[flat_index(a, fb, true, q)];
-        stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt, mine, &fb);
+        redone = stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt, mine, &fb);
       } else {
-        stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt);
+        redone = stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt);
       }
     } else {
-      stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt);
+      redone = stencil_full<M, FAST, NB>(a, P, c, smp, K2, dl2, Jt);
     }
+    if ((write_samples & 4) && status_out && redone) status_out[n] += 0x10000;  // diagnostic
     if (write_samples) {
       double2* jo = reinterpret_cast<double2*>(J_out + 12 * n);
 #pragma unroll
@@ -2282,10 +2291,11 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
           constexpr int M = decltype(m)::value;
           if (ctx->sem_deferred_box)
             hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4, true>), dim3(grid), dim3(64), 0, ds, a, list,
-                               count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
+                               count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws,
+                               S->status.ptr);
           else
             hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4>), dim3(grid), dim3(64), 0, ds, a, list, count,
-                               pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws);
+                               pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws, S->status.ptr);
         });
       }
       return MI_BA_OK;

@@ -35,11 +35,14 @@ def apply(cfg):
 
 
 def decode(st):
-    """semantic_diag 2 marks: +0x1000 deferred, +0x4000 decided by a window summary"""
+    """semantic_diag 2 marks: +0x1000 deferred, +0x4000 settled without the
+    rasters, +0x10000 a deferred sample redone per point"""
+    redo = st >= 0xC000
+    st = np.where(redo, st - 0x10000, st)
     ws = st >= 0x2800
     st = np.where(ws, st - 0x4000, st)
     d = st >= 0x800
-    return np.where(d, st - 0x1000, st), d, ws
+    return np.where(d, st - 0x1000, st), d, ws, redo
 
 
 ref = None
@@ -49,14 +52,15 @@ for cfg in CONFIGS:
     ctx.evaluate_semantic()
     out = ctx.download_semantic()
     ctx.set_tuning("semantic_diag", 0)
-    st, d, ws = decode(out[1])
+    st, d, ws, redo = decode(out[1])
     out = (out[0], st) + tuple(out[2:])
     if ref is None:
         ref = out
     same = all(np.array_equal(a, b) for a, b in zip(ref[1:], out[1:]))
     n = len(st)
     print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "label_planes": cfg[2], "bitwise_equal": bool(same),
-                      "samples": n, "deferred": int(d.sum()), "window_decided": int(ws.sum()),
+                      "samples": n, "deferred": int(d.sum()), "deferred_redone_per_point": int(redo.sum()),
+                      "window_decided": int(ws.sum()),
                       "window_decided_valid": int((ws & (st == mi_ba.VALID)).sum()),
                       "status_valid": int((st == mi_ba.VALID).sum()),
                       "status_invalid_depth": int((st == mi_ba.INVALID_DEPTH).sum()),
