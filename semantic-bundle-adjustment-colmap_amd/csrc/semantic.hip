@@ -1704,8 +1704,8 @@ __global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const 
 // flat pass filled (first entry < pair_cnt), per model into the same region
 // of `out`, counts in cnt[model] (zeroed before).  Launching one workgroup per
 // static chunk instead spent the deferred pass's time dispatching the ~92 %
-// that are empty (80k workgroups for 6.4k chunks at C4).  One atomic per wave
-// and model; the order within a model is the atomics' (the pair sums already
+// that are empty (80k workgroups for 6.4k chunks at C4).  One atomic per
+// workgroup and model; the order within a model is the atomics' (the pair sums already
 // accumulate by atomics in any order).
 struct ModelRanges {
   int b[kNumModels + 1];
@@ -1714,8 +1714,12 @@ struct ModelRanges {
 __global__ __launch_bounds__(256) void deferred_compact_kernel(const uint2* __restrict__ chunks, int nchunks,
                                                                const uint32_t* __restrict__ pair_cnt, ModelRanges mr,
                                                                uint2* __restrict__ out, uint32_t* __restrict__ cnt) {
+  // one atomic per workgroup and model: per-wave counts through LDS, the
+  // workgroup's base per model, then each wave's offset inside it
+  __shared__ uint32_t swc[4][kNumModels];
+  __shared__ uint32_t sbase[kNumModels];
   const int i = blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool valid = i < nchunks;
   uint2 ch = make_uint2(0u, 0u);
   int m = 0;
@@ -1725,18 +1729,23 @@ __global__ __launch_bounds__(256) void deferred_compact_kernel(const uint2* __re
     live = ch.y < pair_cnt[ch.x];
     while (m + 1 < kNumModels && i >= mr.b[m + 1]) ++m;
   }
-  unsigned long long todo = __ballot(valid);
-  while (todo) {
-    const int leader = __ffsll((long long)todo) - 1;
-    const int mm = __shfl(m, leader, 64);
-    const unsigned long long grp = __ballot(valid && m == mm);
-    const unsigned long long sel = __ballot(valid && m == mm && live);
-    uint32_t base = 0;
-    if (lane == leader && sel) base = atomicAdd(cnt + mm, (uint32_t)__popcll(sel));
-    base = __shfl(base, leader, 64);
-    if (valid && m == mm && live)
-      out[mr.b[mm] + base + (uint32_t)__popcll(sel & ((1ull << lane) - 1ull))] = ch;
-    todo &= ~grp;
+  uint32_t rank = 0;  // the lane's rank among its wave's live chunks of its model
+#pragma unroll
+  for (int mm = 0; mm < kNumModels; ++mm) {
+    const unsigned long long sel = __ballot(live && m == mm);
+    if (lane == 0) swc[wv][mm] = (uint32_t)__popcll(sel);
+    if (live && m == mm) rank = (uint32_t)__popcll(sel & ((1ull << lane) - 1ull));
+  }
+  __syncthreads();
+  if (threadIdx.x < kNumModels) {
+    const uint32_t tot = swc[0][threadIdx.x] + swc[1][threadIdx.x] + swc[2][threadIdx.x] + swc[3][threadIdx.x];
+    sbase[threadIdx.x] = tot ? atomicAdd(cnt + threadIdx.x, tot) : 0u;
+  }
+  __syncthreads();
+  if (live) {
+    uint32_t off = sbase[m];
+    for (int w = 0; w < wv; ++w) off += swc[w][m];
+    out[mr.b[m] + off + rank] = ch;
   }
 }
 
