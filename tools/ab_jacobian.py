@@ -1,8 +1,9 @@
 """Times the reproj_jacobian kernel alone on a BASELINE config (HIP events on
 the context stream, interleaved rounds) and reports GB/s vs the 8 TB/s peak.
-    python tools/ab_jacobian.py [--config C4] [--rounds 5] [--reps 5] [--variants 0,13,0:jac_prefetch=1]
+    python tools/ab_jacobian.py [--config C4] [--rounds 5] [--reps 5] [--variants 0,13,0:linearize_warm_inputs=0]
 A variant is a jacobian_variant number, optionally with tuning keys set for
-it alone ("0:jac_prefetch=1:linearize_order=1"; reset to 0 afterwards).
+it alone ("0:linearize_warm_inputs=0:linearize_order=1"; reset to the product
+defaults afterwards).
 """
 import argparse
 import json
@@ -42,7 +43,7 @@ variants = args.variants.split(",")
 
 
 # the product defaults the keys return to after a variant that set them
-DEFAULTS = {"jac_prefetch": 0, "linearize_order": 0, "linearize_warm_inputs": 15, "warm_workgroups": 2048}
+DEFAULTS = {"linearize_order": 0, "linearize_warm_inputs": 15, "warm_workgroups": 2048}
 
 
 def apply(spec, on=True):
