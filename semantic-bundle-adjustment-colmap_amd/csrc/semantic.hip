@@ -442,9 +442,11 @@ __global__ void semantic_pair_prep_kernel(const SemPair* __restrict__ pairs, int
                                           const uint32_t* __restrict__ img_flags,
                                           const uint32_t* __restrict__ raster_slot, double rel_step,
                                           PairConst* __restrict__ out, double* __restrict__ pair_blk, int blk_stride,
-                                          uint32_t* __restrict__ pair_cnt) {
+                                          uint32_t* __restrict__ pair_cnt, uint32_t* __restrict__ zero_n = nullptr,
+                                          int nzero = 0) {
   const int k = blockIdx.x * 2 + (threadIdx.x >> 5);
   const int lane = threadIdx.x & 31;
+  if (zero_n && blockIdx.x == 0 && (int)threadIdx.x < nzero) zero_n[threadIdx.x] = 0u;  // the deferred pass's counts
   if (k >= npairs) return;
   for (int e = lane; e < blk_stride; e += 32) pair_blk[(size_t)k * blk_stride + e] = 0.0;
   if (pair_cnt && lane == 31) pair_cnt[k] = 0u;
@@ -2274,7 +2276,8 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   timer_begin_after(ctx, "semantic_jacobian", timer_start, &stop);
   hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 1) / 2), dim3(64), 0, s, S->pairs.ptr, S->npairs,
                      a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs, S->pair_blk.ptr, kPairStride,
-                     ctx->sem_variant == 6 ? S->pair_cnt.ptr : nullptr);
+                     ctx->sem_variant == 6 ? S->pair_cnt.ptr : nullptr, ctx->sem_variant == 6 ? S->dcount.ptr : nullptr,
+                     kNumModels);
   const bool split = deferred_stream != nullptr && ctx->sem_variant == 6;
   if (ctx->sem_variant == 6) {
     const int ws = write_samples ? 1 | (ctx->sem_diag ? 2 : 0) | (ctx->sem_diag == 2 ? 4 : 0) : 0;
@@ -2285,7 +2288,7 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
       if (nall > 0 && compact) {
         ModelRanges mr;
         for (int m = 0; m <= kNumModels; ++m) mr.b[m] = S->model_chunks[m];
-        if (hipMemsetAsync(S->dcount.ptr, 0, S->dcount.bytes(), ds) != hipSuccess) return MI_BA_ERR_HIP;
+        // dcount was zeroed by the pair prep kernel (ordered before the flat pass)
         hipLaunchKernelGGL(deferred_compact_kernel, dim3((unsigned)((nall + 255) / 256)), dim3(256), 0, ds,
                            S->chunks.ptr, nall, S->pair_cnt.ptr, mr, S->dchunks.ptr, S->dcount.ptr);
       }
