@@ -472,9 +472,12 @@ void EvalSemantic(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* 
 // Negative control of the property test (oracle_set_flat_bound_scale): the
 // pixel bound bx, by is multiplied by this factor (1 = the product's test).
 double g_flat_bound_scale = 1.0;
-// 1: the coarse form the product's flat pass uses (semantic_flat_coarse,
-// csrc/semantic.hip flat_box_coarse): the classes' bounds replaced by their
-// componentwise maxima (oracle_set_flat_coarse).
+// 1 / 2 / 3: the coarse forms of the product's flat pass
+// (semantic_flat_coarse, csrc/semantic.hip flat_box_coarse): the stencil
+// classes gathered into a rotation group and a translation group; 1 / 2
+// combine the groups' (du, dv) into one bound, |A| from the radius (1) or
+// exact (2); 3 bounds the groups apart, |A| from the radius
+// (oracle_set_flat_coarse).
 int g_flat_coarse = 0;
 
 struct FlatBounds {
@@ -578,9 +581,10 @@ bool FlatClears(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* se
   WorldToImage(model, Kj, uj, vj, &xj, &yj);
   double x = xj.a, y = yj.a;
   double A[4] = {xj.v[0], xj.v[1], yj.v[0], yj.v[1]};
-  if (g_flat_coarse) {
+  if (g_flat_coarse == 1 || g_flat_coarse == 3) {
     // the coarse form expands about the reference's own centre pixel and
-    // bounds |A| from the radius (semantic.hip image_jac_bound)
+    // bounds |A| from the radius (semantic.hip image_jac_bound; form 2 keeps
+    // the exact A)
     u = p2[0] / p2[2];
     v = p2[1] / p2[2];
     WorldToImage(model, K, u, v, &x, &y);
@@ -601,11 +605,17 @@ bool FlatClears(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* se
     cls.push_back({0.0, B.dt2[1], 0.0});
     cls.push_back({0.0, 0.0, B.dt2[2]});
   }
-  if (g_flat_coarse && !cls.empty()) {  // one class: the componentwise maxima
-    std::array<double, 3> m = {0.0, 0.0, 0.0};
-    for (const auto& c : cls)
-      for (int k = 0; k < 3; ++k) m[k] = std::max(m[k], c[k]);
-    cls.assign(1, m);
+  if (g_flat_coarse && !cls.empty()) {
+    // two groups: the rotation classes (isotropic dq) and the translation
+    // classes (componentwise maxima)
+    std::array<double, 3> rg = {0.0, 0.0, 0.0}, tg = {0.0, 0.0, 0.0};
+    for (const auto& c : cls) {
+      const bool rot = c[0] == c[1] && c[1] == c[2] && (c[0] == dq1 || c[0] == dq2) && c[0] > 0.0;
+      auto& g = rot ? rg : tg;
+      for (int k = 0; k < 3; ++k) g[k] = std::max(g[k], c[k]);
+    }
+    const double dq = std::max(rg[0], std::max(rg[1], rg[2]));
+    cls.assign({{dq, dq, dq}, tg});
   }
   double az = 0.0;
   for (const auto& c : cls) az = std::max(az, c[2]);
@@ -616,6 +626,11 @@ bool FlatClears(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* se
   for (const auto& c : cls) {
     d.push_back({(c[0] + std::fabs(u) * c[2]) * iden, (c[1] + std::fabs(v) * c[2]) * iden});
     gm = std::max(gm, std::max(d.back()[0], d.back()[1]));
+  }
+  if (g_flat_coarse == 1 || g_flat_coarse == 2) {  // the groups' (du, dv) combined (3 keeps them apart)
+    std::array<double, 2> e = {0.0, 0.0};
+    for (const auto& x : d) e = {std::max(e[0], x[0]), std::max(e[1], x[1])};
+    d.assign(1, e);
   }
   if (!(gm < 0.1)) return false;
   const double ru = std::fabs(u) + gm, rv = std::fabs(v) + gm;

@@ -325,15 +325,16 @@ def semantic_flat_property(options, scene, semantic, bound_scale=1.0, coarse=Fal
     """The product's semantic flat test (restated) vs the full CENTRAL
     stencil over every sample: dict(samples, cleared, cleared_not_flat,
     nonzero_jacobian, flat_deferred).  cleared_not_flat must be 0.
-    bound_scale < 1 shrinks the pixel bound (negative control); coarse: the
-    form with the classes' componentwise maxima (semantic_flat_coarse)."""
+    bound_scale < 1 shrinks the pixel bound (negative control); coarse 1 / 2:
+    the forms with the classes' componentwise maxima (semantic_flat_coarse;
+    1 bounds |A| from the radius, 2 keeps it exact)."""
     sc = scene.copy()
     p = sc.problem()
     s = semantic.struct()
     counts = np.zeros(5, np.int64)
     lib = load()
     lib.oracle_set_flat_bound_scale(bound_scale)
-    lib.oracle_set_flat_coarse(1 if coarse else 0)
+    lib.oracle_set_flat_coarse(int(coarse))
     try:
         st = lib.oracle_semantic_flat_property(C.byref(options), C.byref(p), C.byref(s), counts.ctypes.data_as(_i64p))
     finally:

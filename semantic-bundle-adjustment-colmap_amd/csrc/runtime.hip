@@ -2019,7 +2019,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->sem_compact = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "semantic_flat_coarse") == 0 && (value == 0 || value == 1)) {
+  if (std::strcmp(key, "semantic_flat_coarse") == 0 && value >= 0 && value <= 3) {
     ctx->sem_coarse = value;
     return MI_BA_OK;
   }

@@ -1087,29 +1087,40 @@ __device__ __forceinline__ void image_jac_bound(const double* K, double u, doubl
 // (image_jac_bound), so no camera-model Jacobian is evaluated.  The depth
 // bound az is flat_box's.  Restated in the oracle (FlatClears, coarse form)
 // for tests/test_semantic_flat_property.py.
-template <int M>
+template <int M, bool EXACT_A = false, bool GROUPS = false>
 __device__ __forceinline__ bool flat_box_coarse(const PairConst* __restrict__ P, const Centre& c, const double* K2,
                                                 double u, double v, double x, double y, FlatBox& fb) {
   const double z = c.p2[2];
   if (!(z > 0.0)) return false;  // NaN-safe
+  double Ae[4];
+  if constexpr (EXACT_A) {  // semantic_flat_coarse 2: A at the centre from the camera model's Jacobian
+    constexpr int np = Model<M>::kNumParams;
+    double Jp[2 * np];
+    world_to_image_jac<M>(K2, u, v, &x, &y, Ae, Jp);
+  }
   if (!(fabs(x) < 1e8 && fabs(y) < 1e8 && fabs(u) < 1e6 && fabs(v) < 1e6)) return false;
-  double ax = 0.0, ay = 0.0, az = 0.0;
+  // rotation classes (isotropic dq) and translation classes (componentwise
+  // maxima of the t1 / t2 steps); GROUPS: bounded separately, else together
+  double dq = 0.0, tx = 0.0, ty = 0.0, tz = 0.0;
   if (P->var1) {
-    const double dq1 = P->rho1 * sqrt(c.w[0] * c.w[0] + c.w[1] * c.w[1] + c.w[2] * c.w[2]) * (1.0 + 1e-12);
-    ax = fmax(dq1, fmax(P->dt1[0] * fabs(P->C[0]), fmax(P->dt1[1] * fabs(P->C[1]), P->dt1[2] * fabs(P->C[2]))));
-    ay = fmax(dq1, fmax(P->dt1[0] * fabs(P->C[3]), fmax(P->dt1[1] * fabs(P->C[4]), P->dt1[2] * fabs(P->C[5]))));
-    az = fmax(dq1, fmax(P->dt1[0] * fabs(P->C[6]), fmax(P->dt1[1] * fabs(P->C[7]), P->dt1[2] * fabs(P->C[8]))));
+    dq = P->rho1 * sqrt(c.w[0] * c.w[0] + c.w[1] * c.w[1] + c.w[2] * c.w[2]) * (1.0 + 1e-12);
+    tx = fmax(P->dt1[0] * fabs(P->C[0]), fmax(P->dt1[1] * fabs(P->C[1]), P->dt1[2] * fabs(P->C[2])));
+    ty = fmax(P->dt1[0] * fabs(P->C[3]), fmax(P->dt1[1] * fabs(P->C[4]), P->dt1[2] * fabs(P->C[5])));
+    tz = fmax(P->dt1[0] * fabs(P->C[6]), fmax(P->dt1[1] * fabs(P->C[7]), P->dt1[2] * fabs(P->C[8])));
   }
   if (P->var2) {
-    const double dq2 = P->rho2 * sqrt(c.pw[0] * c.pw[0] + c.pw[1] * c.pw[1] + c.pw[2] * c.pw[2]) * (1.0 + 1e-12);
-    ax = fmax(ax, fmax(dq2, P->dt2[0]));
-    ay = fmax(ay, fmax(dq2, P->dt2[1]));
-    az = fmax(az, fmax(dq2, P->dt2[2]));
+    dq = fmax(dq, P->rho2 * sqrt(c.pw[0] * c.pw[0] + c.pw[1] * c.pw[1] + c.pw[2] * c.pw[2]) * (1.0 + 1e-12));
+    tx = fmax(tx, P->dt2[0]);
+    ty = fmax(ty, P->dt2[1]);
+    tz = fmax(tz, P->dt2[2]);
   }
+  const double az = fmax(dq, tz);
   if (!(z - az > 0.5 * z)) return false;
   const double iden = 1.0 / (z - az) * (1.0 + 1e-12);
-  const double cu = (ax + fabs(u) * az) * iden;
-  const double cv = (ay + fabs(v) * az) * iden;
+  // (cu, cv) of the group(s): the rotation group's and the translation group's
+  const double cu_r = (dq + fabs(u) * dq) * iden, cv_r = (dq + fabs(v) * dq) * iden;
+  const double cu_t = (tx + fabs(u) * tz) * iden, cv_t = (ty + fabs(v) * tz) * iden;
+  const double cu = fmax(cu_r, cu_t), cv = fmax(cv_r, cv_t);
   const double gm = fmax(cu, cv);
   if (!(gm < 0.1)) return false;  // a stencil this wide is never cleared (and keeps rho finite)
   const double ru = fabs(u) + gm, rv = fabs(v) + gm;
@@ -1117,10 +1128,24 @@ __device__ __forceinline__ bool flat_box_coarse(const PairConst* __restrict__ P,
   const double fx = fabs(K2[0]);
   const double fy = (M == kPinhole || M == kOpenCV) ? fabs(K2[1]) : fabs(K2[0]);
   double Ah[4];
-  image_jac_bound<M>(K2, u, v, Ah);
-  const double sk = cu + cv;
-  const double bxm = (Ah[0] + fx * H * sk) * cu + (Ah[1] + fx * H * sk) * cv;
-  const double bym = (Ah[2] + fy * H * sk) * cu + (Ah[3] + fy * H * sk) * cv;
+  if constexpr (EXACT_A) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Ah[k] = fabs(Ae[k]);
+  } else {
+    image_jac_bound<M>(K2, u, v, Ah);
+  }
+  double bxm, bym;
+  if constexpr (GROUPS) {
+    const double sr = cu_r + cv_r, st = cu_t + cv_t;
+    bxm = fmax((Ah[0] + fx * H * sr) * cu_r + (Ah[1] + fx * H * sr) * cv_r,
+               (Ah[0] + fx * H * st) * cu_t + (Ah[1] + fx * H * st) * cv_t);
+    bym = fmax((Ah[2] + fy * H * sr) * cu_r + (Ah[3] + fy * H * sr) * cv_r,
+               (Ah[2] + fy * H * st) * cu_t + (Ah[3] + fy * H * st) * cv_t);
+  } else {
+    const double sk = cu + cv;
+    bxm = (Ah[0] + fx * H * sk) * cu + (Ah[1] + fx * H * sk) * cv;
+    bym = (Ah[2] + fy * H * sk) * cu + (Ah[3] + fy * H * sk) * cv;
+  }
   const double gain = distortion_gain<M>(K2, u * u + v * v);
   const double kscale = (fabs(K2[0]) + fabs(K2[1])) * gain * (1.0 + fabs(u) + fabs(v)) * (1.0 + c.mag * fabs(1.0 / z));
   const double ex = 1e-6 + 1e-11 * (kscale + fabs(x) + fabs(y));
@@ -1459,7 +1484,7 @@ __device__ __forceinline__ int tile_depth_side(const SemArgs& a, const FlatBox& 
   return 0;
 }
 
-template <int M, bool FAST, bool WS = false, bool LP = false, bool COARSE = false>
+template <int M, bool FAST, bool WS = false, bool LP = false, int COARSE = 0>
 __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const SemTile* __restrict__ tiles,
                                                                const PairConst* __restrict__ pcs,
                                                                uint32_t* __restrict__ pair_cnt,
@@ -1512,7 +1537,10 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
     const int cpy = cast_to_int_x86(round(y2));
     const bool cin = !(cpx < 0 || cpx >= a.W || cpy < 0 || cpy >= a.H);
     FlatBox fb;
-    const bool cand = COARSE ? flat_box_coarse<M>(P, c, K2, u2, v2, x2, y2, fb) : flat_box<M>(P, c, K2, fb);
+    const bool cand = COARSE == 3   ? flat_box_coarse<M, false, true>(P, c, K2, u2, v2, x2, y2, fb)
+                      : COARSE == 2 ? flat_box_coarse<M, true>(P, c, K2, u2, v2, x2, y2, fb)
+                      : COARSE == 1 ? flat_box_coarse<M>(P, c, K2, u2, v2, x2, y2, fb)
+                                    : flat_box<M>(P, c, K2, fb);
     bool decided = false;   // the centre outcome and the flat test are settled without the raster
     bool resolved = false;  // the centre outcome is settled (the flat test may have failed)
     if constexpr (LP) {
@@ -2325,12 +2353,22 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
         };
         using T = std::true_type;
         using F = std::false_type;
+        using C0 = std::integral_constant<int, 0>;
+        using C1 = std::integral_constant<int, 1>;
+        using C2 = std::integral_constant<int, 2>;
+        using C3 = std::integral_constant<int, 3>;
+        auto pick = [&](auto ws_, auto lp_) {
+          if (ctx->sem_coarse == 3) launch(ws_, lp_, C3{});
+          else if (ctx->sem_coarse == 2) launch(ws_, lp_, C2{});
+          else if (ctx->sem_coarse == 1) launch(ws_, lp_, C1{});
+          else launch(ws_, lp_, C0{});
+        };
         if (a.lab8)
-          ctx->sem_coarse ? launch(F{}, T{}, T{}) : launch(F{}, T{}, F{});
+          pick(F{}, T{});
         else if (a.wsum)
-          ctx->sem_coarse ? launch(T{}, F{}, T{}) : launch(T{}, F{}, F{});
+          pick(T{}, F{});
         else
-          ctx->sem_coarse ? launch(F{}, F{}, T{}) : launch(F{}, F{}, F{});
+          pick(F{}, F{});
       });
     }
     if (after_flat) {

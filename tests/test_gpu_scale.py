@@ -254,7 +254,7 @@ def test_c3_window_summary_flat_pass_bitwise(gpu):
     with mi_ba.Context(mi_ba.default_options(), sc.copy(), sem) as ctx:
         ctx.set_tuning("semantic_diag", 1)
         for ws, box, lp, coarse in ((0, 0, 0, 0), (1, 0, 0, 0), (1, 1, 0, 0), (0, 1, 0, 0), (0, 0, 1, 0), (1, 1, 1, 0),
-                                    (0, 0, 1, 1)):
+                                    (0, 0, 1, 1), (0, 0, 1, 2), (0, 0, 1, 3), (1, 0, 0, 1), (0, 0, 0, 1)):
             ctx.set_tuning("semantic_window_summary", ws)
             ctx.set_tuning("semantic_deferred_box", box)
             ctx.set_tuning("semantic_label_planes", lp)
@@ -263,7 +263,7 @@ def test_c3_window_summary_flat_pass_bitwise(gpu):
             out.append(ctx.download_semantic())
     for k, o in enumerate(out[1:]):
         for m, (a, b) in enumerate(zip(out[0], o)):
-            if k == len(out) - 2 and m == 1:  # the coarse box defers a few more samples: statuses sans the mark
+            if k >= 5 and m == 1:  # the coarse boxes defer a few more samples: statuses sans the mark
                 a, b = np.where(a >= 0x800, a - 0x1000, a), np.where(b >= 0x800, b - 0x1000, b)
             assert np.array_equal(a, b)
     st = out[0][1]

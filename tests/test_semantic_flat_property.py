@@ -62,10 +62,12 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("coarse", [False, True])
+@pytest.mark.parametrize("coarse", [0, 1, 2, 3])
 def test_flat_test_never_clears_a_non_flat_stencil(coarse):
-    """coarse: the form with the stencil classes' componentwise maxima
-    (semantic_flat_coarse, csrc/semantic.hip flat_box_coarse)."""
+    """coarse 1 / 2 / 3: the forms with the stencil classes gathered into a
+    rotation and a translation group (semantic_flat_coarse, csrc/semantic.hip
+    flat_box_coarse; 1 bounds |A| from the radius, 2 keeps the camera model's
+    exact A, 3 bounds the two groups apart)."""
     total = cleared = nonzero = 0
     rows = []
     for model, extra, rel, seed, kw in CASES:
@@ -90,5 +92,5 @@ def test_property_check_catches_an_unsound_bound():
     sc, sem = scene(mi_ba.OPENCV, (-0.6, 0.3, 0.01, -0.01), 1e-2, 6)
     c = oracle.semantic_flat_property(mi_ba.default_options(), sc, sem, bound_scale=0.3)
     assert c["cleared_not_flat"] > 0, c
-    c = oracle.semantic_flat_property(mi_ba.default_options(), sc, sem, bound_scale=0.3, coarse=True)
+    c = oracle.semantic_flat_property(mi_ba.default_options(), sc, sem, bound_scale=0.3, coarse=1)
     assert c["cleared_not_flat"] > 0, c

@@ -25,13 +25,15 @@ ap.add_argument("--reps", type=int, default=10)
 args = ap.parse_args()
 sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
 ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
-CONFIGS = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 0, 1), (0, 1, 1)]
+# (window summaries, deferred box, label planes, coarse flat box form)
+CONFIGS = [(0, 0, 0, 0), (0, 0, 1, 0), (0, 0, 1, 1), (0, 0, 1, 2), (0, 0, 1, 3)]
 
 
 def apply(cfg):
     ctx.set_tuning("semantic_window_summary", cfg[0])
     ctx.set_tuning("semantic_deferred_box", cfg[1])
     ctx.set_tuning("semantic_label_planes", cfg[2])
+    ctx.set_tuning("semantic_flat_coarse", cfg[3])
 
 
 def decode(st):
@@ -58,7 +60,8 @@ for cfg in CONFIGS:
         ref = out
     same = all(np.array_equal(a, b) for a, b in zip(ref[1:], out[1:]))
     n = len(st)
-    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "label_planes": cfg[2], "bitwise_equal": bool(same),
+    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "label_planes": cfg[2], "flat_coarse": cfg[3],
+                      "bitwise_equal": bool(same),
                       "samples": n, "deferred": int(d.sum()), "deferred_redone_per_point": int(redo.sum()),
                       "window_decided": int(ws.sum()),
                       "window_decided_valid": int((ws & (st == mi_ba.VALID)).sum()),
@@ -85,7 +88,7 @@ for rnd in range(args.rounds):
         res[cfg].append((sj[0] / sj[1], rj[0] / rj[1], wall))
 for cfg in CONFIGS:
     a = np.array(res[cfg])
-    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "label_planes": cfg[2], "semantic_ms_median": float(np.median(a[:, 0])),
+    print(json.dumps({"window_summary": cfg[0], "deferred_box": cfg[1], "label_planes": cfg[2], "flat_coarse": cfg[3], "semantic_ms_median": float(np.median(a[:, 0])),
                       "reproj_ms_median": float(np.median(a[:, 1])), "step_wall_ms_median": float(np.median(a[:, 2])),
                       "rounds": args.rounds, "reps": args.reps}), flush=True)
 ctx.close()
