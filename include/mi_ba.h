@@ -533,8 +533,10 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *                           the memory-side cache right before it (semantic contexts):
  *                           1 observations, 2 image ids, 4 point ids, 8 points;
  *                           default 15, 0 off
- *   "semantic_flat_coarse"  1 (default): the flat pass's pixel box from the stencil
- *                           classes' componentwise maximum displacement; 0 per class
+ *   "semantic_flat_coarse"  the flat pass's pixel box from a rotation and a translation
+ *                           group of the stencil classes: 2 (default) with the camera
+ *                           model's Jacobian at the centre, 1 with |A| bounded from the
+ *                           radius, 3 the groups bounded apart; 0 per class
  *   "warm_workgroups"       workgroups of that read (default 2048; 0 one per CU)
  *   "linearize_overlap"     1 semantic kernel on a second stream beside the reprojection
  *                           kernel, 0 one stream (default)

@@ -102,8 +102,9 @@ struct mi_ba_context {
                          // deferred; 2: also by +0x4000 for samples a window summary decided
   bool sem_deferred_box = false;  // "semantic_deferred_box": the deferred pass reads each sample's 3x3 box once
   int sem_compact = 1;   // "semantic_deferred_compact": the deferred pass over the filled chunks only (resident grid)
-  int sem_coarse = 1;    // "semantic_flat_coarse": the flat pass's box from the classes' componentwise maxima
-                         // (default; 0 the per-class bounds)
+  int sem_coarse = 2;    // "semantic_flat_coarse": the flat pass's box from a rotation and a translation group
+                         // of the stencil classes (2 default: exact A; 1 |A| from the radius; 3 groups
+                         // bounded apart; 0 the per-class bounds)
   int sem_variant = 6;   // semantic kernel ("semantic_variant"): 6 flat pass + deferred-sample pass (0.42 ms at C4), 5 flat test + in-tile gather, 4/3/2 batched stencil with 4/2/1 parameters per step (0.70 ms), 1 per-point FMA route (0.82 ms), 0 per-point uncontracted (0.92 ms); all bitwise equal
 
   // linearization
