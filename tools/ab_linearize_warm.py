@@ -33,9 +33,9 @@ ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
 # (linearize_warm_inputs: range mask read right before the reprojection
 #  kernel, 1 observations, 2 image ids, 4 point ids, 8 points; 0 off;
 #  semantic_flat_coarse)
-CONFIGS = [(0, 0, 0), (15, 1, 0), (15, 0, 0), (0, 1, 0), (15, 1, 0, 0)]
+CONFIGS = [(0, 0, 0), (15, 2, 0), (15, 0, 0), (0, 2, 0), (15, 2, 0, 0)]
 if args.overlap:
-    CONFIGS = [(15, 1, 0), (15, 1, 1), (15, 1, 2), (0, 1, 1)]
+    CONFIGS = [(15, 2, 0), (15, 2, 1), (15, 2, 2), (0, 2, 1)]
 
 
 def apply(cfg):
