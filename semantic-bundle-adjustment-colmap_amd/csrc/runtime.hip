@@ -2015,6 +2015,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->lin_overlap = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "semantic_deferred_grid") == 0 && value >= 1 && value <= 64) {
+    ctx->sem_dgrid = value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "semantic_deferred_compact") == 0 && (value == 0 || value == 1)) {
     ctx->sem_compact = value;
     return MI_BA_OK;

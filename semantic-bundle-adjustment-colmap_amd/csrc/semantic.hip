@@ -2323,8 +2323,9 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
       for (int model = 0; model < kNumModels; ++model) {
         const int c0 = S->model_chunks[model], nc = S->model_chunks[model + 1] - c0;
         if (S->model_tiles[model + 1] == S->model_tiles[model] || nc == 0) continue;
-        // compact: 64-thread workgroups, 16 resident per CU; else one per static chunk
-        const int grid = compact ? std::min(nc, 16 * S->n_cu) : nc;
+        // compact: a resident grid of 64-thread workgroups, semantic_deferred_grid per
+        // CU (LDS allows 24 at 6.6 KB each); else one per static chunk
+        const int grid = compact ? std::min(nc, std::max(1, ctx->sem_dgrid) * S->n_cu) : nc;
         const uint2* list = (compact ? S->dchunks.ptr : S->chunks.ptr) + c0;
         const uint32_t* count = compact ? S->dcount.ptr + model : nullptr;
         dispatch_model(model, [&](auto m) {

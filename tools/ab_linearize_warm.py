@@ -33,7 +33,9 @@ ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
 # (linearize_warm_inputs: range mask read right before the reprojection
 #  kernel, 1 observations, 2 image ids, 4 point ids, 8 points; 0 off;
 #  semantic_flat_coarse)
-CONFIGS = [(0, 0, 0), (15, 2, 0), (15, 0, 0), (0, 2, 0), (15, 2, 0, 0), (15, 2, 0, 1, 4096), (15, 2, 0, 1, 0)]
+# (..., semantic_deferred_compact, warm_workgroups, semantic_deferred_grid)
+CONFIGS = [(0, 0, 0), (15, 2, 0), (15, 2, 0, 1, 2048, 16), (15, 2, 0, 1, 2048, 32), (15, 2, 0, 1, 4096),
+           (15, 2, 0, 1, 0)]
 if args.overlap:
     CONFIGS = [(15, 2, 0), (15, 2, 1), (15, 2, 2), (0, 2, 1)]
 
@@ -43,6 +45,7 @@ def apply(cfg):
     ctx.set_tuning("semantic_flat_coarse", cfg[1])
     ctx.set_tuning("semantic_deferred_compact", cfg[3] if len(cfg) > 3 else 1)
     ctx.set_tuning("warm_workgroups", cfg[4] if len(cfg) > 4 else 2048)
+    ctx.set_tuning("semantic_deferred_grid", cfg[5] if len(cfg) > 5 else 24)
     if args.overlap:
         ctx.set_tuning("linearize_overlap", cfg[2])
 
@@ -82,7 +85,8 @@ for cfg in CONFIGS:
     a = np.array(res[cfg])
     print(json.dumps({"linearize_warm_inputs": cfg[0], "semantic_flat_coarse": cfg[1], "linearize_overlap": cfg[2],
                       "semantic_deferred_compact": cfg[3] if len(cfg) > 3 else 1,
-                      "warm_workgroups": cfg[4] if len(cfg) > 4 else 2048, "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
+                      "warm_workgroups": cfg[4] if len(cfg) > 4 else 2048,
+                      "semantic_deferred_grid": cfg[5] if len(cfg) > 5 else 24, "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
                       "semantic_ms_median": float(np.median(a[:, 0])), "reproj_ms_median": float(np.median(a[:, 1])),
                       "step_wall_ms_median": float(np.median(a[:, 2])),
                       "input_warm_ms_median": float(np.median(a[:, 3])), "rounds": args.rounds, "reps": args.reps}),
