@@ -922,6 +922,26 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   // 0.576 -> 0.431 ms at C4 for a 0.055 ms read; the observations or ids alone
   // do not do it: profiles/r4_ab_linearize_warm_ranges.jsonl).  Only after the
   // semantic pass has used the cache; a geometric-only step finds them cached.
+  // prep_early (default): the semantic pair tables formed on the side stream
+  // beside the warm-up and the reprojection kernel (they read the poses
+  // only), instead of on the critical path after it
+  hipEvent_t prep_ev = nullptr;
+  if (ctx->sem && ctx->sem_prep_early && !overlap && !split && !warm && !sem_first && ctx->sem_variant == 6) {
+    if (!ctx->lin_side) {
+      if (hipStreamCreateWithFlags(&ctx->lin_side, hipStreamNonBlocking) != hipSuccess) {
+        ctx->lin_side = nullptr;
+        return MI_BA_ERR_HIP;
+      }
+      MI_HIP(hipEventCreateWithFlags(&ctx->lin_ev[0], hipEventDisableTiming));
+      MI_HIP(hipEventCreateWithFlags(&ctx->lin_ev[1], hipEventDisableTiming));
+    }
+    MI_HIP(hipEventRecord(ctx->lin_ev[0], s));
+    MI_HIP(hipStreamWaitEvent(ctx->lin_side, ctx->lin_ev[0], 0));
+    mi_ba_status st = semantic_pair_prep(ctx, ctx->lin_side);
+    if (st != MI_BA_OK) return st;
+    MI_HIP(hipEventRecord(ctx->lin_ev[1], ctx->lin_side));
+    prep_ev = ctx->lin_ev[1];
+  }
   hipEvent_t wstop = nullptr;
   if (ctx->sem && ctx->lin_warm && d.nb > 0) {
     timer_begin(ctx, "input_warm", &wstop);
@@ -939,7 +959,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   if (sem_after) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false, nullptr, nullptr, stop,
                                          d.nb ? ctx->partial.ptr : nullptr, reproj_grid(d.nb),
-                                         ctx->scalars.ptr + kCost, ctx->sum_ws.ptr);
+                                         ctx->scalars.ptr + kCost, ctx->sum_ws.ptr, nullptr, prep_ev);
     if (st != MI_BA_OK) return st;
   } else if (d.nb) {
     launch_sum(ctx->partial.ptr, reproj_grid(d.nb), ctx->scalars.ptr + kCost, s, ctx->sum_ws.ptr);
@@ -2013,6 +2033,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   // at C4, profiles/r3_ab_linearize_overlap.jsonl)
   if (std::strcmp(key, "linearize_overlap") == 0 && value >= 0 && value <= 2 && ab_value(value, 0)) {
     ctx->lin_overlap = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "semantic_prep_early") == 0 && (value == 0 || value == 1)) {
+    ctx->sem_prep_early = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "semantic_deferred_grid") == 0 && value >= 1 && value <= 64) {

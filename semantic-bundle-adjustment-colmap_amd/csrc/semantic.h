@@ -96,7 +96,11 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
                                 hipStream_t deferred_stream = nullptr, hipEvent_t flat_done = nullptr,
                                 hipEvent_t timer_start = nullptr, const double* other_partial = nullptr,
                                 int64_t other_n = 0, double* other_out = nullptr, double* other_scratch = nullptr,
-                                const std::function<mi_ba_status()>& after_flat = nullptr);
+                                const std::function<mi_ba_status()>& after_flat = nullptr,
+                                hipEvent_t prep_done = nullptr);
+// The pair tables of one linearization on `stream` (semantic_linearize does
+// it itself unless given prep_done, the event after an earlier call).
+mi_ba_status semantic_pair_prep(mi_ba_context* ctx, hipStream_t stream);
 // ExportSemanticErrorToCSV rows of the ordered image pair (image1, image2) at
 // the current parameters (mi_ba_semantic_export).
 mi_ba_status semantic_export(mi_ba_context* ctx, int32_t image1, int32_t image2, int64_t* count, int32_t* pixels,

@@ -2283,13 +2283,27 @@ void semantic_destroy(mi_ba_context* ctx) {
   ctx->sem = nullptr;
 }
 
+// The per-pair stencil tables and the cleared accumulators of one
+// linearization (semantic_pair_prep_kernel) on `stream`.
+mi_ba_status semantic_pair_prep(mi_ba_context* ctx, hipStream_t stream) {
+  SemanticState* S = ctx->sem;
+  if (!S || S->ns == 0 || S->npairs == 0) return MI_BA_OK;
+  SemArgs a = make_args(ctx, ctx->dev.qt, ctx->dev.cam);
+  PairConst* pcs = reinterpret_cast<PairConst*>(S->pconst.ptr);
+  hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 1) / 2), dim3(64), 0, stream, S->pairs.ptr,
+                     S->npairs, a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs, S->pair_blk.ptr,
+                     kPairStride, ctx->sem_variant == 6 ? S->pair_cnt.ptr : nullptr,
+                     ctx->sem_variant == 6 ? S->dcount.ptr : nullptr, kNumModels);
+  return hipGetLastError() == hipSuccess ? MI_BA_OK : MI_BA_ERR_HIP;
+}
+
 // deferred_stream: when given (two-pass route), the deferred-sample pass is
 // launched there instead (after an event on ctx->stream marks the flat pass
 // done), and the caller joins it; the cost is complete on ctx->stream.
 mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_samples, hipStream_t deferred_stream,
                                 hipEvent_t flat_done, hipEvent_t timer_start, const double* other_partial,
                                 int64_t other_n, double* other_out, double* other_scratch,
-                                const std::function<mi_ba_status()>& after_flat) {
+                                const std::function<mi_ba_status()>& after_flat, hipEvent_t prep_done) {
   SemanticState* S = ctx->sem;
   hipStream_t s = ctx->stream;
   S->samples_valid = write_samples;
@@ -2302,10 +2316,14 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   PairConst* pcs = reinterpret_cast<PairConst*>(S->pconst.ptr);
   hipEvent_t stop;
   timer_begin_after(ctx, "semantic_jacobian", timer_start, &stop);
-  hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 1) / 2), dim3(64), 0, s, S->pairs.ptr, S->npairs,
-                     a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs, S->pair_blk.ptr, kPairStride,
-                     ctx->sem_variant == 6 ? S->pair_cnt.ptr : nullptr, ctx->sem_variant == 6 ? S->dcount.ptr : nullptr,
-                     kNumModels);
+  if (prep_done) {
+    // the pair tables were formed on a side stream beside the reprojection
+    // kernel (semantic_pair_prep)
+    if (hipStreamWaitEvent(s, prep_done, 0) != hipSuccess) return MI_BA_ERR_HIP;
+  } else {
+    const mi_ba_status st = semantic_pair_prep(ctx, s);
+    if (st != MI_BA_OK) return st;
+  }
   const bool split = deferred_stream != nullptr && ctx->sem_variant == 6;
   if (ctx->sem_variant == 6) {
     const int ws = write_samples ? 1 | (ctx->sem_diag ? 2 : 0) | (ctx->sem_diag == 2 ? 4 : 0) : 0;
