@@ -101,7 +101,8 @@ struct mi_ba_context {
   int sem_diag = 0;      // "semantic_diag" 1: downloaded status is offset by +0x1000 for samples the flat test
                          // deferred; 2: also by +0x4000 for samples a window summary decided
   bool sem_deferred_box = false;  // "semantic_deferred_box": the deferred pass reads each sample's 3x3 box once
-  int sem_prep_early = 1; // "semantic_prep_early": pair tables on the side stream beside the reprojection kernel
+  int sem_prep_early = 0; // "semantic_prep_early": pair tables on the side stream beside the reprojection kernel
+                          // (measured slower: 0.823 vs 0.808 ms per step, it slows the warm-up beside it)
   int sem_dgrid = 24;    // "semantic_deferred_grid": resident deferred-pass workgroups per CU
   int sem_compact = 1;   // "semantic_deferred_compact": the deferred pass over the filled chunks only (resident grid)
   int sem_coarse = 2;    // "semantic_flat_coarse": the flat pass's box from a rotation and a translation group

@@ -922,9 +922,10 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   // 0.576 -> 0.431 ms at C4 for a 0.055 ms read; the observations or ids alone
   // do not do it: profiles/r4_ab_linearize_warm_ranges.jsonl).  Only after the
   // semantic pass has used the cache; a geometric-only step finds them cached.
-  // prep_early (default): the semantic pair tables formed on the side stream
-  // beside the warm-up and the reprojection kernel (they read the poses
-  // only), instead of on the critical path after it
+  // prep_early (semantic_prep_early; measured slower, off): the semantic pair
+  // tables formed on the side stream beside the warm-up and the reprojection
+  // kernel (they read the poses only), instead of on the critical path after
+  // it — the warm-up beside it slows by more (profiles/r4q_ab_prep_early.jsonl)
   hipEvent_t prep_ev = nullptr;
   if (ctx->sem && ctx->sem_prep_early && !overlap && !split && !warm && !sem_first && ctx->sem_variant == 6) {
     if (!ctx->lin_side) {
