@@ -35,7 +35,7 @@ ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
 #  semantic_flat_coarse)
 # (..., semantic_deferred_compact, warm_workgroups, semantic_deferred_grid)
 # (..., semantic_deferred_compact, warm_workgroups, semantic_deferred_grid, semantic_prep_early)
-CONFIGS = [(0, 0, 0, 1, 2048, 24, 0), (15, 2, 0), (15, 2, 0, 1, 2048, 24, 0)]
+CONFIGS = [(0, 2, 0), (15, 2, 0), (13, 2, 0), (11, 2, 0), (7, 2, 0), (9, 2, 0)]
 if args.overlap:
     CONFIGS = [(15, 2, 0), (15, 2, 1), (15, 2, 2), (0, 2, 1)]
 
