@@ -46,7 +46,7 @@ def apply(cfg):
     ctx.set_tuning("semantic_deferred_compact", cfg[3] if len(cfg) > 3 else 1)
     ctx.set_tuning("warm_workgroups", cfg[4] if len(cfg) > 4 else 2048)
     ctx.set_tuning("semantic_deferred_grid", cfg[5] if len(cfg) > 5 else 24)
-    ctx.set_tuning("semantic_prep_early", cfg[6] if len(cfg) > 6 else 1)
+    ctx.set_tuning("semantic_prep_early", cfg[6] if len(cfg) > 6 else 0)
     if args.overlap:
         ctx.set_tuning("linearize_overlap", cfg[2])
 
@@ -88,7 +88,7 @@ for cfg in CONFIGS:
                       "semantic_deferred_compact": cfg[3] if len(cfg) > 3 else 1,
                       "warm_workgroups": cfg[4] if len(cfg) > 4 else 2048,
                       "semantic_deferred_grid": cfg[5] if len(cfg) > 5 else 24,
-                      "semantic_prep_early": cfg[6] if len(cfg) > 6 else 1, "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
+                      "semantic_prep_early": cfg[6] if len(cfg) > 6 else 0, "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
                       "semantic_ms_median": float(np.median(a[:, 0])), "reproj_ms_median": float(np.median(a[:, 1])),
                       "step_wall_ms_median": float(np.median(a[:, 2])),
                       "input_warm_ms_median": float(np.median(a[:, 3])), "rounds": args.rounds, "reps": args.reps}),
