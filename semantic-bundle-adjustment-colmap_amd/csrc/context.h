@@ -94,6 +94,7 @@ struct mi_ba_context {
   int lin_warm = 15;                   // "linearize_warm_inputs": range mask read right before the reprojection kernel
                                        // (1 observations, 2 image ids, 4 point ids, 8 points; 0 off)
   int lin_warm_conc = 0;               // "linearize_warm_concurrent" (tools): that read beside the semantic deferred pass
+  int warm_unroll = 4;                 // "warm_unroll": loads in flight per lane of the warm-up (4 or 8)
   int warm_wgs = 2048;                 // workgroups of the warm-up kernel (0: one per CU)
   int lin_order = 0;                   // 0 reprojection kernel first, 1 semantic pass first
   hipStream_t lin_side = nullptr;

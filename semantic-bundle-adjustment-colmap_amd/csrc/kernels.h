@@ -19,7 +19,8 @@ struct SemDevice;  // defined in semantic.h
 void launch_pack_images(const DevProblem& p, double* rec, hipStream_t s, double* zero = nullptr, int nzero = 0);
 void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s);
 // mask: bit 0 observations, 1 image ids, 2 point ids, 3 points; wgs <= 0: one workgroup per CU
-void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s, int mask = 15, int wgs = 0);
+void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s, int mask = 15, int wgs = 0,
+                         int unroll = 4);
 int reproj_grid(int64_t nb);
 
 // Cost 0.5*sum(rho) of every reduced block at parameters (qt, cam, X).

@@ -2863,6 +2863,7 @@ struct TouchRanges {
   int64_t n16[4];
 };
 
+template <int U>
 __global__ __launch_bounds__(256) void touch_kernel(TouchRanges t, unsigned* sink) {
   unsigned acc = 0u;
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -2871,16 +2872,19 @@ __global__ __launch_bounds__(256) void touch_kernel(TouchRanges t, unsigned* sin
     const uint4* a = t.ptr[q];
     const int64_t n = t.n16[q];
     int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    for (; k + 3 * stride < n; k += 4 * stride) {
-      const uint4 v0 = a[k], v1 = a[k + stride], v2 = a[k + 2 * stride], v3 = a[k + 3 * stride];
-      acc ^= v0.x ^ v1.y ^ v2.z ^ v3.w;
+    for (; k + (U - 1) * stride < n; k += U * stride) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = a[k + u * stride];  // U loads in flight per lane
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].w;
     }
     for (; k < n; k += stride) acc ^= a[k].x;
   }
   if (acc == 0x9e3779b9u && t.n16[0] < 0) *sink = acc;
 }
 
-void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s, int mask, int wgs) {
+void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s, int mask, int wgs, int unroll) {
   TouchRanges t{};
   const void* ptrs[4] = {p.obs_xy, p.obs_img, p.obs_pt, p.X};
   const int64_t bytes[4] = {p.nb * 16, p.nb * 4, p.nb * 4, p.num_points * 24};
@@ -2895,7 +2899,10 @@ void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s, int
         wgs <= 0)
       wgs = 256;
   }
-  hipLaunchKernelGGL(touch_kernel, dim3(wgs), dim3(256), 0, s, t, sink);
+  if (unroll >= 8)
+    hipLaunchKernelGGL(touch_kernel<8>, dim3(wgs), dim3(256), 0, s, t, sink);
+  else
+    hipLaunchKernelGGL(touch_kernel<4>, dim3(wgs), dim3(256), 0, s, t, sink);
 }
 
 void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* cost_partial, hipStream_t s) {

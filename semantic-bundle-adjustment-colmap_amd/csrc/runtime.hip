@@ -947,7 +947,7 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   if (ctx->sem && ctx->lin_warm && d.nb > 0) {
     timer_begin(ctx, "input_warm", &wstop);
     launch_touch_inputs(d, reinterpret_cast<unsigned*>(ctx->scalars.ptr + kNumScalars - 1), s, ctx->lin_warm,
-                        ctx->warm_wgs);
+                        ctx->warm_wgs, ctx->warm_unroll);
     timer_end(ctx, wstop);
   }
   timer_begin_after(ctx, "reproj_jacobian", wstop, &stop);  // starts at the warm-up's stop event
@@ -2020,6 +2020,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   // tools build: the same read beside the semantic deferred pass instead
   if (std::strcmp(key, "linearize_warm_concurrent") == 0 && value >= 0 && value <= 15 && ab_value(value, 0)) {
     ctx->lin_warm_conc = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "warm_unroll") == 0 && (value == 4 || value == 8)) {
+    ctx->warm_unroll = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "warm_workgroups") == 0 && value >= 0 && value <= 65536) {
