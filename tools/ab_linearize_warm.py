@@ -36,7 +36,9 @@ ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
 # (..., semantic_deferred_compact, warm_workgroups, semantic_deferred_grid)
 # (..., semantic_deferred_compact, warm_workgroups, semantic_deferred_grid, semantic_prep_early)
 # (..., linearize_order: 1 the semantic pass first)
-CONFIGS = [(0, 2, 0), (15, 2, 0), (15, 2, 0, 1, 2048, 24, 0, 1), (0, 2, 0, 1, 2048, 24, 0, 1)]
+# (..., warm_unroll)
+CONFIGS = [(15, 2, 0), (15, 2, 0, 1, 2048, 24, 0, 0, 8), (15, 2, 0, 1, 1024, 24, 0, 0, 8),
+           (15, 2, 0, 1, 4096, 24, 0, 0, 8)]
 if args.overlap:
     CONFIGS = [(15, 2, 0), (15, 2, 1), (15, 2, 2), (0, 2, 1)]
 
@@ -49,6 +51,7 @@ def apply(cfg):
     ctx.set_tuning("semantic_deferred_grid", cfg[5] if len(cfg) > 5 else 24)
     ctx.set_tuning("semantic_prep_early", cfg[6] if len(cfg) > 6 else 0)
     ctx.set_tuning("linearize_order", cfg[7] if len(cfg) > 7 else 0)
+    ctx.set_tuning("warm_unroll", cfg[8] if len(cfg) > 8 else 4)
     if args.overlap:
         ctx.set_tuning("linearize_overlap", cfg[2])
 
@@ -91,7 +94,8 @@ for cfg in CONFIGS:
                       "warm_workgroups": cfg[4] if len(cfg) > 4 else 2048,
                       "semantic_deferred_grid": cfg[5] if len(cfg) > 5 else 24,
                       "semantic_prep_early": cfg[6] if len(cfg) > 6 else 0,
-                      "linearize_order": cfg[7] if len(cfg) > 7 else 0, "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
+                      "linearize_order": cfg[7] if len(cfg) > 7 else 0,
+                      "warm_unroll": cfg[8] if len(cfg) > 8 else 4, "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
                       "semantic_ms_median": float(np.median(a[:, 0])), "reproj_ms_median": float(np.median(a[:, 1])),
                       "step_wall_ms_median": float(np.median(a[:, 2])),
                       "input_warm_ms_median": float(np.median(a[:, 3])), "rounds": args.rounds, "reps": args.reps}),
