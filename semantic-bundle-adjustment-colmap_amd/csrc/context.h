@@ -105,6 +105,7 @@ struct mi_ba_context {
   int sem_prep_early = 0; // "semantic_prep_early": pair tables on the side stream beside the reprojection kernel
                           // (measured slower: 0.823 vs 0.808 ms per step, it slows the warm-up beside it)
   int sem_dgrid = 24;    // "semantic_deferred_grid": resident deferred-pass workgroups per CU
+  int sem_dvar = 0;      // "semantic_deferred_variant" (tools build): stencil batch / occupancy variants
   int sem_compact = 1;   // "semantic_deferred_compact": the deferred pass over the filled chunks only (resident grid)
   int sem_coarse = 2;    // "semantic_flat_coarse": the flat pass's box from a rotation and a translation group
                          // of the stencil classes (2 default: exact A; 1 |A| from the radius; 3 groups

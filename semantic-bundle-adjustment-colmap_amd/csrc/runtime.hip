@@ -2044,6 +2044,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->sem_prep_early = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "semantic_deferred_variant") == 0 && value >= 0 && value <= 4 && ab_value(value, 0)) {
+    ctx->sem_dvar = value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "semantic_deferred_grid") == 0 && value >= 1 && value <= 64) {
     ctx->sem_dgrid = value;
     return MI_BA_OK;

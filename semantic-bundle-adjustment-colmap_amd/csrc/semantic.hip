@@ -1638,8 +1638,11 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
 
 // Pass 2: chunk = 64 consecutive entries of one pair's deferred region
 // (chunks past the pair's count exit at once).
-template <int M, bool FAST, int NB, bool BOX = false>
-__global__ __launch_bounds__(64) void semantic_deferred_kernel(SemArgs a, const uint2* __restrict__ chunks,
+// WPE: minimum waves per SIMD asked of the register allocator (tools-build
+// variants; the default build's 128 VGPRs give 4 waves per SIMD, 16 of these
+// 64-thread workgroups per CU)
+template <int M, bool FAST, int NB, bool BOX = false, int WPE = 1>
+__global__ __launch_bounds__(64, WPE) void semantic_deferred_kernel(SemArgs a, const uint2* __restrict__ chunks,
                                                               const uint32_t* __restrict__ ccount,
                                                               const PairConst* __restrict__ pcs,
                                                               const uint32_t* __restrict__ pair_cnt,
@@ -2341,8 +2344,10 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
       for (int model = 0; model < kNumModels; ++model) {
         const int c0 = S->model_chunks[model], nc = S->model_chunks[model + 1] - c0;
         if (S->model_tiles[model + 1] == S->model_tiles[model] || nc == 0) continue;
-        // compact: a resident grid of 64-thread workgroups, semantic_deferred_grid per
-        // CU (LDS allows 24 at 6.6 KB each); else one per static chunk
+        // compact: a grid of 64-thread workgroups, semantic_deferred_grid per CU
+        // (16 resident at 128 VGPRs, LDS would allow 24 at 6.6 KB each; 24
+        // measured 6 us faster than 16: the extra ones take the second round's
+        // chunks as the first finish); else one per static chunk
         const int grid = compact ? std::min(nc, std::max(1, ctx->sem_dgrid) * S->n_cu) : nc;
         const uint2* list = (compact ? S->dchunks.ptr : S->chunks.ptr) + c0;
         const uint32_t* count = compact ? S->dcount.ptr + model : nullptr;
@@ -2352,6 +2357,25 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
             hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4, true>), dim3(grid), dim3(64), 0, ds, a, list,
                                count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws,
                                S->status.ptr);
+#ifdef MI_BA_AB_VARIANTS
+          // semantic_deferred_variant: 1 NB 2; 2 NB 2 at >= 5 waves per SIMD;
+          // 3 NB 4 at >= 5; 4 NB 2 at >= 6 (register spills)
+          else if (ctx->sem_dvar == 1)
+            hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 2>), dim3(grid), dim3(64), 0, ds, a, list, count,
+                               pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws, S->status.ptr);
+          else if (ctx->sem_dvar == 2)
+            hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 2, false, 5>), dim3(grid), dim3(64), 0, ds, a,
+                               list, count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws,
+                               S->status.ptr);
+          else if (ctx->sem_dvar == 3)
+            hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4, false, 5>), dim3(grid), dim3(64), 0, ds, a,
+                               list, count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws,
+                               S->status.ptr);
+          else if (ctx->sem_dvar == 4)
+            hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 2, false, 6>), dim3(grid), dim3(64), 0, ds, a,
+                               list, count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws,
+                               S->status.ptr);
+#endif
           else
             hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4>), dim3(grid), dim3(64), 0, ds, a, list, count,
                                pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws, S->status.ptr);

@@ -13,7 +13,7 @@ import time
 
 import numpy as np
 
-if "--overlap" in sys.argv:
+if "--overlap" in sys.argv or "--ab" in sys.argv:
     os.environ.setdefault("MI_BA_LIB", "ab")  # linearize_overlap: the tools-only build (make ab)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "semantic-bundle-adjustment-colmap_amd"))
@@ -27,6 +27,7 @@ ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--overlap", action="store_true",
                 help="the semantic pass on a second stream beside the reprojection kernel (1) or only its "
                      "deferred pass (2), with the warm-up (tools build)")
+ap.add_argument("--ab", action="store_true", help="the tools build (semantic_deferred_variant)")
 args = ap.parse_args()
 sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
 ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
@@ -36,9 +37,9 @@ ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
 # (..., semantic_deferred_compact, warm_workgroups, semantic_deferred_grid)
 # (..., semantic_deferred_compact, warm_workgroups, semantic_deferred_grid, semantic_prep_early)
 # (..., linearize_order: 1 the semantic pass first)
-# (..., warm_unroll)
-CONFIGS = [(15, 2, 0), (15, 2, 0, 1, 2048, 24, 0, 0, 8), (15, 2, 0, 1, 1024, 24, 0, 0, 8),
-           (15, 2, 0, 1, 4096, 24, 0, 0, 8)]
+# (..., warm_unroll, semantic_deferred_variant)
+CONFIGS = [(15, 2, 0, 1, 2048, 24, 0, 0, 4, v) for v in range(5)] if args.ab else \
+    [(15, 2, 0), (15, 2, 0, 1, 2048, 24, 0, 0, 8)]
 if args.overlap:
     CONFIGS = [(15, 2, 0), (15, 2, 1), (15, 2, 2), (0, 2, 1)]
 
@@ -52,6 +53,8 @@ def apply(cfg):
     ctx.set_tuning("semantic_prep_early", cfg[6] if len(cfg) > 6 else 0)
     ctx.set_tuning("linearize_order", cfg[7] if len(cfg) > 7 else 0)
     ctx.set_tuning("warm_unroll", cfg[8] if len(cfg) > 8 else 4)
+    if len(cfg) > 9:
+        ctx.set_tuning("semantic_deferred_variant", cfg[9])
     if args.overlap:
         ctx.set_tuning("linearize_overlap", cfg[2])
 
@@ -63,10 +66,12 @@ for cfg in CONFIGS:
     ctx.linearize()
     costs[cfg] = ctx.cost()
     _, r, J = ctx.download_jacobian()
+    _, sst, sr, sJ = ctx.download_semantic()  # the samples re-evaluated with write_samples
     if ref is None:
-        ref = (r, J)
-    same[cfg] = bool(np.array_equal(r, ref[0]) and np.array_equal(J, ref[1]))
-    del r, J
+        ref = (r, J, sst, sr, sJ)
+    same[cfg] = bool(np.array_equal(r, ref[0]) and np.array_equal(J, ref[1]) and np.array_equal(sst, ref[2])
+                     and np.array_equal(sr, ref[3]) and np.array_equal(sJ, ref[4]))
+    del r, J, sst, sr, sJ
 ref = None
 res = {c: [] for c in CONFIGS}
 for rnd in range(args.rounds):
@@ -95,7 +100,8 @@ for cfg in CONFIGS:
                       "semantic_deferred_grid": cfg[5] if len(cfg) > 5 else 24,
                       "semantic_prep_early": cfg[6] if len(cfg) > 6 else 0,
                       "linearize_order": cfg[7] if len(cfg) > 7 else 0,
-                      "warm_unroll": cfg[8] if len(cfg) > 8 else 4, "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
+                      "warm_unroll": cfg[8] if len(cfg) > 8 else 4,
+                      "semantic_deferred_variant": cfg[9] if len(cfg) > 9 else 0, "cost": costs[cfg], "cost_equal": costs[cfg] == costs[CONFIGS[0]], "r_J_equal": same[cfg],
                       "semantic_ms_median": float(np.median(a[:, 0])), "reproj_ms_median": float(np.median(a[:, 1])),
                       "step_wall_ms_median": float(np.median(a[:, 2])),
                       "input_warm_ms_median": float(np.median(a[:, 3])), "rounds": args.rounds, "reps": args.reps}),

@@ -35,7 +35,7 @@ for stage in "$@"; do
       timeout -k 10 500 python -u tools/ab_pcg_mf.py > gpurun_out/$T/ab_pcg_mf.jsonl 2> gpurun_out/$T/ab_pcg_mf.err || exit 1
       cat gpurun_out/$T/ab_pcg_mf.jsonl ;;
     warm)
-      timeout -k 10 300 python -u tools/ab_linearize_warm.py > gpurun_out/$T/ab_warm.jsonl 2> gpurun_out/$T/ab_warm.err || exit 1
+      timeout -k 10 300 python -u tools/ab_linearize_warm.py $WARM_ARGS > gpurun_out/$T/ab_warm.jsonl 2> gpurun_out/$T/ab_warm.err || exit 1
       cat gpurun_out/$T/ab_warm.jsonl ;;
     cpuba)
       timeout -k 10 600 python -u tools/cpu_ba_iteration.py --config C4 --iters 1 > gpurun_out/$T/cpu_ba_c4.json 2> gpurun_out/$T/cpu_ba_c4.err || exit 1
