@@ -66,7 +66,8 @@ for cfg in CONFIGS:
     ctx.linearize()
     costs[cfg] = ctx.cost()
     _, r, J = ctx.download_jacobian()
-    _, sst, sr, sJ = ctx.download_semantic()  # the samples re-evaluated with write_samples
+    ctx.evaluate_semantic()  # the samples re-evaluated with write_samples
+    _, sst, sr, sJ = ctx.download_semantic()
     if ref is None:
         ref = (r, J, sst, sr, sJ)
     same[cfg] = bool(np.array_equal(r, ref[0]) and np.array_equal(J, ref[1]) and np.array_equal(sst, ref[2])
