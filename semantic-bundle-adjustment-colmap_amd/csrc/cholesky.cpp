@@ -1470,7 +1470,13 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
   const bool split_ok = cfg.split_cus > 0 && ws.split_n > 0 && ws.split_side_h && ws.split_main_h;
   rocblas_handle hm = h, hs = ws.side_h;
   hipStream_t sm = s1, ss = ws.side;
+  // rest_streams 2 (not inside the split head): block columns alternate
+  // between the dgemm stream and ws.rest_s, forked after the next panel's
+  // block column and joined before the next iteration
+  const bool rest2 = cfg.rest_streams == 2 && ws.rest_n == 2 && ws.rest_s && ws.rest_h &&
+                     ws.ev_rest.size() >= ws.ev.size();
   auto fail = [&](rocblas_status e) {
+    if (rest2) (void)hipStreamSynchronize(ws.rest_s);
     if (split_ok) {
       (void)hipStreamSynchronize(ws.split_side);
       (void)hipStreamSynchronize(ws.split_main);
@@ -1528,10 +1534,23 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     {
       // block columns of width nb (rest_update 0) or 2 nb (3)
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
-      for (int j = jb0; j < m; j += cw) {
+      const bool two = rest2 && sm == s1 && mr > cw;
+      if (two) {
+        if (hipEventRecord(ws.ev_rest[2 * kk], sm) != hipSuccess ||
+            hipStreamWaitEvent(ws.rest_s, ws.ev_rest[2 * kk], 0) != hipSuccess)
+          return fail(rocblas_status_internal_error);
+      }
+      int c = 0;
+      for (int j = jb0; j < m; j += cw, ++c) {
         const int jb = std::min(cw, m - j);
-        st = gemm_nt(hm, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
+        st = gemm_nt(two && (c & 1) ? ws.rest_h : hm, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda,
+                     cfg.gemm_solution);
         if (st != rocblas_status_success) return fail(st);
+      }
+      if (two) {
+        if (hipEventRecord(ws.ev_rest[2 * kk + 1], ws.rest_s) != hipSuccess ||
+            hipStreamWaitEvent(sm, ws.ev_rest[2 * kk + 1], 0) != hipSuccess)
+          return fail(rocblas_status_internal_error);
       }
     }
     // panel k+1 is read by the next iteration's updates (and by the solve)
@@ -1704,10 +1723,34 @@ bool CholWorkspace::set_split_cus(int ncu) {
   return true;
 }
 
+bool CholWorkspace::set_rest_streams(int k) {
+  if (rest_s) (void)hipStreamSynchronize(rest_s);
+  if (rest_h) (void)rocblas_destroy_handle(rest_h);
+  if (rest_s) (void)hipStreamDestroy(rest_s);
+  for (hipEvent_t e : ev_rest) (void)hipEventDestroy(e);
+  ev_rest.clear();
+  rest_s = nullptr;
+  rest_h = nullptr;
+  rest_n = 1;
+  if (k != 2) return true;
+  if (hipSetDevice(device) != hipSuccess) return false;
+  if (hipStreamCreateWithFlags(&rest_s, hipStreamNonBlocking) != hipSuccess) { rest_s = nullptr; return false; }
+  if (rocblas_create_handle(&rest_h) != rocblas_status_success) { rest_h = nullptr; return false; }
+  if (rocblas_set_stream(rest_h, rest_s) != rocblas_status_success) return false;
+  for (size_t i = 0; i < ev.size(); ++i) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+    ev_rest.push_back(e);
+  }
+  rest_n = 2;
+  return true;
+}
+
 void CholWorkspace::destroy() {
   if (device >= 0) (void)hipSetDevice(device);
   if (side) (void)hipStreamSynchronize(side);
   if (split_n > 0 || split_side || split_main) (void)set_split_cus(0);
+  if (rest_s || rest_n != 1) (void)set_rest_streams(1);
   for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   ev.clear();
   if (side_h) (void)rocblas_destroy_handle(side_h);
@@ -1762,6 +1805,11 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
     if (ws->side && c.side_cus != ws->side_cus && !ws->set_side_cus(c.side_cus))
       return rocblas_status_internal_error;
     if (ws->side && c.split_cus != ws->split_n && !ws->set_split_cus(c.split_cus))
+      return rocblas_status_internal_error;
+    if (ws->side && (c.rest_streams == 2 ? 2 : 1) != ws->rest_n && !ws->set_rest_streams(c.rest_streams))
+      return rocblas_status_internal_error;
+    // the events follow the panel count (create() may have re-made ev)
+    if (ws->rest_n == 2 && ws->ev_rest.size() < ws->ev.size() && !ws->set_rest_streams(2))
       return rocblas_status_internal_error;
   }
   double* scratch = ws ? ws->scratch : nullptr;

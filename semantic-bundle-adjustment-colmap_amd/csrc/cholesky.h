@@ -43,6 +43,10 @@ struct CholConfig {
   // head_own (e.g. 2: 64-wide diagonal kernels + rocBLAS dtrsm, no resident
   // spin-waiting workgroups beside the trailing dgemm); 0 = off
   int head_own = 0, head_own_cols = 0;
+  // trailing update's block columns (after the next panel's) alternated over
+  // the caller's stream and a second one, so one launch's last tiles overlap
+  // the next launch's first (tools build: cholesky_rest_streams 2); 1 = off
+  int rest_streams = 1;
   bool gemm_update = true;
   // look-ahead: the trailing update after the next panel's block column,
   // 0 one dgemm per 512-wide block column, 1 one dsyrk, 2 one dgemmt,
@@ -155,6 +159,13 @@ struct CholWorkspace {
   hipEvent_t ev_split[4] = {nullptr, nullptr, nullptr, nullptr};
   int split_n = 0;                 // split_cus of the current split streams
   bool set_split_cus(int ncu);
+  // CholConfig::rest_streams 2: the second trailing-update stream, its handle
+  // and a fork / join event pair per panel
+  hipStream_t rest_s = nullptr;
+  rocblas_handle rest_h = nullptr;
+  std::vector<hipEvent_t> ev_rest;
+  int rest_n = 1;
+  bool set_rest_streams(int k);
 
   // Creates the resources on `device` with events for up to `max_panels`
   // panels and diagonal-block inverses for matrices up to max_n; false on any

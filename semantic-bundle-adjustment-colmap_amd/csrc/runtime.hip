@@ -2166,6 +2166,11 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   // split head: panel factor on this many CUs, trailing dgemm on the rest,
   // while the panel starts before column cholesky_split_cols (tools build:
   // measured 22.5-27.5 vs 15.6 ms, profiles/r4_ab_cholesky_split_cus.jsonl)
+  // trailing-update block columns over two streams (tools build)
+  if (std::strcmp(key, "cholesky_rest_streams") == 0 && (value == 1 || value == 2) && ab_value(value, 1)) {
+    ctx->chol.rest_streams = (int)value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_split_cus") == 0 && value >= 0 && value <= 4096 && ab_value(value, 0)) {
     ctx->chol.split_cus = (int)value;
     return MI_BA_OK;
