@@ -1470,13 +1470,15 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
   const bool split_ok = cfg.split_cus > 0 && ws.split_n > 0 && ws.split_side_h && ws.split_main_h;
   rocblas_handle hm = h, hs = ws.side_h;
   hipStream_t sm = s1, ss = ws.side;
-  // rest_streams 2 (not inside the split head): block columns alternate
-  // between the dgemm stream and ws.rest_s, forked after the next panel's
-  // block column and joined before the next iteration
-  const bool rest2 = cfg.rest_streams == 2 && ws.rest_n == 2 && ws.rest_s && ws.rest_h &&
-                     ws.ev_rest.size() >= ws.ev.size();
+  // rest_streams k > 1 (not inside the split head): block columns dealt
+  // round-robin over the dgemm stream and ws.rest_s[0 .. k-2], forked after
+  // the next panel's block column and joined before the next iteration
+  const int nrest = cfg.rest_streams > 1 && ws.rest_n == cfg.rest_streams &&
+                            ws.ev_rest.size() >= (size_t)CholWorkspace::kMaxRest * (ws.ev.size() / 2)
+                        ? cfg.rest_streams
+                        : 1;
   auto fail = [&](rocblas_status e) {
-    if (rest2) (void)hipStreamSynchronize(ws.rest_s);
+    for (int r = 0; r + 1 < nrest; ++r) (void)hipStreamSynchronize(ws.rest_s[r]);
     if (split_ok) {
       (void)hipStreamSynchronize(ws.split_side);
       (void)hipStreamSynchronize(ws.split_main);
@@ -1534,24 +1536,25 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     {
       // block columns of width nb (rest_update 0) or 2 nb (3)
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
-      const bool two = rest2 && sm == s1 && mr > cw;
-      if (two) {
-        if (hipEventRecord(ws.ev_rest[2 * kk], sm) != hipSuccess ||
-            hipStreamWaitEvent(ws.rest_s, ws.ev_rest[2 * kk], 0) != hipSuccess)
-          return fail(rocblas_status_internal_error);
+      // streams used this panel: no more than its block columns
+      const int ns = sm == s1 ? std::min(nrest, (mr + cw - 1) / cw) : 1;
+      hipEvent_t* evr = ns > 1 ? ws.ev_rest.data() + (size_t)CholWorkspace::kMaxRest * kk : nullptr;
+      if (ns > 1) {
+        if (hipEventRecord(evr[0], sm) != hipSuccess) return fail(rocblas_status_internal_error);
+        for (int r = 0; r + 1 < ns; ++r)
+          if (hipStreamWaitEvent(ws.rest_s[r], evr[0], 0) != hipSuccess) return fail(rocblas_status_internal_error);
       }
       int c = 0;
       for (int j = jb0; j < m; j += cw, ++c) {
         const int jb = std::min(cw, m - j);
-        st = gemm_nt(two && (c & 1) ? ws.rest_h : hm, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda,
+        const int r = c % ns;
+        st = gemm_nt(r ? ws.rest_h[r - 1] : hm, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda,
                      cfg.gemm_solution);
         if (st != rocblas_status_success) return fail(st);
       }
-      if (two) {
-        if (hipEventRecord(ws.ev_rest[2 * kk + 1], ws.rest_s) != hipSuccess ||
-            hipStreamWaitEvent(sm, ws.ev_rest[2 * kk + 1], 0) != hipSuccess)
+      for (int r = 0; r + 1 < ns; ++r)
+        if (hipEventRecord(evr[1 + r], ws.rest_s[r]) != hipSuccess || hipStreamWaitEvent(sm, evr[1 + r], 0) != hipSuccess)
           return fail(rocblas_status_internal_error);
-      }
     }
     // panel k+1 is read by the next iteration's updates (and by the solve)
     if (hipStreamWaitEvent(sm, pan, 0) != hipSuccess) return fail(rocblas_status_internal_error);
@@ -1724,25 +1727,35 @@ bool CholWorkspace::set_split_cus(int ncu) {
 }
 
 bool CholWorkspace::set_rest_streams(int k) {
-  if (rest_s) (void)hipStreamSynchronize(rest_s);
-  if (rest_h) (void)rocblas_destroy_handle(rest_h);
-  if (rest_s) (void)hipStreamDestroy(rest_s);
+  for (int r = 0; r + 1 < kMaxRest; ++r) {
+    if (rest_s[r]) (void)hipStreamSynchronize(rest_s[r]);
+    if (rest_h[r]) (void)rocblas_destroy_handle(rest_h[r]);
+    if (rest_s[r]) (void)hipStreamDestroy(rest_s[r]);
+    rest_s[r] = nullptr;
+    rest_h[r] = nullptr;
+  }
   for (hipEvent_t e : ev_rest) (void)hipEventDestroy(e);
   ev_rest.clear();
-  rest_s = nullptr;
-  rest_h = nullptr;
   rest_n = 1;
-  if (k != 2) return true;
-  if (hipSetDevice(device) != hipSuccess) return false;
-  if (hipStreamCreateWithFlags(&rest_s, hipStreamNonBlocking) != hipSuccess) { rest_s = nullptr; return false; }
-  if (rocblas_create_handle(&rest_h) != rocblas_status_success) { rest_h = nullptr; return false; }
-  if (rocblas_set_stream(rest_h, rest_s) != rocblas_status_success) return false;
-  for (size_t i = 0; i < ev.size(); ++i) {
+  if (k <= 1) return true;
+  if (k > kMaxRest || hipSetDevice(device) != hipSuccess) return false;
+  for (int r = 0; r + 1 < k; ++r) {
+    if (hipStreamCreateWithFlags(&rest_s[r], hipStreamNonBlocking) != hipSuccess) {
+      rest_s[r] = nullptr;
+      return false;
+    }
+    if (rocblas_create_handle(&rest_h[r]) != rocblas_status_success) {
+      rest_h[r] = nullptr;
+      return false;
+    }
+    if (rocblas_set_stream(rest_h[r], rest_s[r]) != rocblas_status_success) return false;
+  }
+  for (size_t i = 0; i < (size_t)kMaxRest * (ev.size() / 2); ++i) {
     hipEvent_t e;
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
     ev_rest.push_back(e);
   }
-  rest_n = 2;
+  rest_n = k;
   return true;
 }
 
@@ -1750,7 +1763,7 @@ void CholWorkspace::destroy() {
   if (device >= 0) (void)hipSetDevice(device);
   if (side) (void)hipStreamSynchronize(side);
   if (split_n > 0 || split_side || split_main) (void)set_split_cus(0);
-  if (rest_s || rest_n != 1) (void)set_rest_streams(1);
+  if (rest_s[0] || rest_n != 1) (void)set_rest_streams(1);
   for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   ev.clear();
   if (side_h) (void)rocblas_destroy_handle(side_h);
@@ -1806,10 +1819,11 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
       return rocblas_status_internal_error;
     if (ws->side && c.split_cus != ws->split_n && !ws->set_split_cus(c.split_cus))
       return rocblas_status_internal_error;
-    if (ws->side && (c.rest_streams == 2 ? 2 : 1) != ws->rest_n && !ws->set_rest_streams(c.rest_streams))
-      return rocblas_status_internal_error;
-    // the events follow the panel count (create() may have re-made ev)
-    if (ws->rest_n == 2 && ws->ev_rest.size() < ws->ev.size() && !ws->set_rest_streams(2))
+    const int want_rest = std::min(std::max(c.rest_streams, 1), (int)CholWorkspace::kMaxRest);
+    // (re)made when the count changes or the panel events outgrew them (create() re-makes ev)
+    if (ws->side && (want_rest != ws->rest_n ||
+                     (want_rest > 1 && ws->ev_rest.size() < (size_t)CholWorkspace::kMaxRest * (ws->ev.size() / 2))) &&
+        !ws->set_rest_streams(want_rest))
       return rocblas_status_internal_error;
   }
   double* scratch = ws ? ws->scratch : nullptr;

@@ -43,9 +43,9 @@ struct CholConfig {
   // head_own (e.g. 2: 64-wide diagonal kernels + rocBLAS dtrsm, no resident
   // spin-waiting workgroups beside the trailing dgemm); 0 = off
   int head_own = 0, head_own_cols = 0;
-  // trailing update's block columns (after the next panel's) alternated over
-  // the caller's stream and a second one, so one launch's last tiles overlap
-  // the next launch's first (tools build: cholesky_rest_streams 2); 1 = off
+  // trailing update's block columns (after the next panel's) dealt round-robin
+  // over the caller's stream and rest_streams - 1 more (1..4), so one launch's
+  // last tiles overlap the next launches' first; 1 = one stream
   int rest_streams = 1;
   bool gemm_update = true;
   // look-ahead: the trailing update after the next panel's block column,
@@ -159,11 +159,12 @@ struct CholWorkspace {
   hipEvent_t ev_split[4] = {nullptr, nullptr, nullptr, nullptr};
   int split_n = 0;                 // split_cus of the current split streams
   bool set_split_cus(int ncu);
-  // CholConfig::rest_streams 2: the second trailing-update stream, its handle
-  // and a fork / join event pair per panel
-  hipStream_t rest_s = nullptr;
-  rocblas_handle rest_h = nullptr;
-  std::vector<hipEvent_t> ev_rest;
+  // CholConfig::rest_streams k > 1: the k - 1 further trailing-update
+  // streams with their handles, and per panel a fork event and k - 1 joins
+  static constexpr int kMaxRest = 4;
+  hipStream_t rest_s[kMaxRest - 1] = {nullptr, nullptr, nullptr};
+  rocblas_handle rest_h[kMaxRest - 1] = {nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> ev_rest;  // [panel][kMaxRest]
   int rest_n = 1;
   bool set_rest_streams(int k);
 

@@ -322,7 +322,8 @@ def test_lm_fused_forward_solve(gpu, images):
                                       dict(head_panel=768, head_cols=700, tail_panel=128, tail_cols=300),
                                       dict(split_cus=32, split_cols=1024), dict(split_cus=200, split_cols=1593),
                                       dict(head_own_diag=2, head_own_cols=1024),
-                                      dict(rest_streams=2, rest_update=0)])
+                                      dict(rest_streams=2, rest_update=0), dict(rest_streams=4, rest_update=0),
+                                      dict(rest_streams=3)])
 def test_lm_panel_schedule(gpu, schedule):
     """Non-uniform panel schedules (cholesky_head_panel / _head_cols /
     _tail_panel / _tail_cols: 1024-wide one-launch panels of 16 column tiles,
@@ -331,11 +332,11 @@ def test_lm_panel_schedule(gpu, schedule):
     the panel factor and the trailing dgemm on disjoint CU sets) and the
     two-kernel diagonal factor + dtrsm for the head panels
     (cholesky_head_own_diag / _cols) and the trailing update's block columns
-    over two streams (cholesky_rest_streams), with and
+    over several streams (cholesky_rest_streams), with and
     without the look-ahead (S itself differs
     between runs in the order of the Schur build's float atomics)."""
-    if any(k in schedule for k in ("split_cus", "head_own_diag", "rest_streams")) and not mi_ba.ab_build():
-        pytest.skip("split head / head panel kind / two update streams: tools build only (MI_BA_LIB=ab)")
+    if any(k in schedule for k in ("split_cus", "head_own_diag")) and not mi_ba.ab_build():
+        pytest.skip("split head / head panel kind: tools build only (MI_BA_LIB=ab)")
     sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
