@@ -45,8 +45,10 @@ struct CholConfig {
   int head_own = 0, head_own_cols = 0;
   // trailing update's block columns (after the next panel's) dealt round-robin
   // over the caller's stream and rest_streams - 1 more (1..4), so one launch's
-  // last tiles overlap the next launches' first; 1 = one stream
-  int rest_streams = 1;
+  // last tiles overlap the next launches' first; 1 = one stream.  Default 2:
+  // Cholesky 15.5 -> 14.7-15.1 ms at nf = 11 993; 3 / 4 streams 16.8-20.8 ms
+  // (profiles/r4w_ab_cholesky_rest_streams.jsonl, r4x_..._1to4.jsonl)
+  int rest_streams = 2;
   bool gemm_update = true;
   // look-ahead: the trailing update after the next panel's block column,
   // 0 one dgemm per 512-wide block column, 1 one dsyrk, 2 one dgemmt,
