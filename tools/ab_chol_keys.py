@@ -18,7 +18,19 @@ w = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.OPENCV, 30, 300, track_length=
                                             extra=(-0.1, 0.01, 1e-4, -1e-4))).gauge()
 with mi_ba.Context(mi_ba.default_options(max_num_iterations=2), w) as x:
     x.solve()
-for arg in sys.argv[1:] or [""]:
+# --bench-like: bench.py's linearization context (its streams and memory) alive
+# and stepped beside the LM contexts, as in the bench's BA-iteration leg
+argv = [a for a in sys.argv[1:] if a != "--bench-like"]
+lin = None
+if "--bench-like" in sys.argv:
+    sys.path.insert(0, ".")
+    import bench  # noqa: E402
+    bsc, bsem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
+    lin = mi_ba.Context(mi_ba.default_options(), bsc, bsem)
+    for _ in range(5):
+        lin.linearize()
+    lin.synchronize()
+for arg in argv or [""]:
     keys = dict(kv.split("=") for kv in arg.split(",") if kv)
     for rep in range(2):
         with mi_ba.Context(mi_ba.default_options(max_num_iterations=3), sc.copy()) as ctx:
