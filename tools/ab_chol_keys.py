@@ -20,9 +20,10 @@ with mi_ba.Context(mi_ba.default_options(max_num_iterations=2), w) as x:
     x.solve()
 # --bench-like: bench.py's linearization context (its streams and memory) alive
 # and stepped beside the LM contexts, as in the bench's BA-iteration leg
-argv = [a for a in sys.argv[1:] if a != "--bench-like"]
+# --bench-like-closed: the same context stepped and then closed before the LM runs
+argv = [a for a in sys.argv[1:] if a not in ("--bench-like", "--bench-like-closed")]
 lin = None
-if "--bench-like" in sys.argv:
+if "--bench-like" in sys.argv or "--bench-like-closed" in sys.argv:
     sys.path.insert(0, ".")
     import bench  # noqa: E402
     bsc, bsem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
@@ -30,6 +31,9 @@ if "--bench-like" in sys.argv:
     for _ in range(5):
         lin.linearize()
     lin.synchronize()
+    if "--bench-like-closed" in sys.argv:
+        lin.close()
+        lin = None
 for arg in argv or [""]:
     keys = dict(kv.split("=") for kv in arg.split(",") if kv)
     for rep in range(2):
