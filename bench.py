@@ -337,6 +337,10 @@ def main():
     s_ms, s_n = ctx.kernel_time("semantic_jacobian")
     w_ms, w_n = ctx.kernel_time("input_warm")
     ctx.set_timing(False)
+    # the linearization context is done: closed before the BA-iteration leg
+    # (its idle streams otherwise share the LM context's hardware queues:
+    # Cholesky 15.9 vs 14.7 ms, profiles/r4za_ab_cholesky_rest_streams_closed.jsonl)
+    ctx.close()
     total_blocks = allreduce_sum(float(nb + ns))
     value = total_blocks * args.steps / dt
 
@@ -450,7 +454,6 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -1726,7 +1726,7 @@ bool CholWorkspace::set_split_cus(int ncu) {
   return true;
 }
 
-bool CholWorkspace::set_rest_streams(int k) {
+bool CholWorkspace::set_rest_streams(int k, bool cumask) {
   for (int r = 0; r + 1 < kMaxRest; ++r) {
     if (rest_s[r]) (void)hipStreamSynchronize(rest_s[r]);
     if (rest_h[r]) (void)rocblas_destroy_handle(rest_h[r]);
@@ -1737,10 +1737,21 @@ bool CholWorkspace::set_rest_streams(int k) {
   for (hipEvent_t e : ev_rest) (void)hipEventDestroy(e);
   ev_rest.clear();
   rest_n = 1;
+  rest_cumask = false;
   if (k <= 1) return true;
   if (k > kMaxRest || hipSetDevice(device) != hipSuccess) return false;
+  std::vector<uint32_t> all;
+  if (cumask) {
+    int total = 0;
+    if (hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || total <= 0)
+      return false;
+    all.assign((total + 31) / 32, 0u);
+    for (int cu = 0; cu < total; ++cu) all[cu / 32] |= 1u << (cu % 32);
+  }
   for (int r = 0; r + 1 < k; ++r) {
-    if (hipStreamCreateWithFlags(&rest_s[r], hipStreamNonBlocking) != hipSuccess) {
+    const hipError_t e = cumask ? hipExtStreamCreateWithCUMask(&rest_s[r], (uint32_t)all.size(), all.data())
+                                : hipStreamCreateWithFlags(&rest_s[r], hipStreamNonBlocking);
+    if (e != hipSuccess) {
       rest_s[r] = nullptr;
       return false;
     }
@@ -1756,6 +1767,7 @@ bool CholWorkspace::set_rest_streams(int k) {
     ev_rest.push_back(e);
   }
   rest_n = k;
+  rest_cumask = cumask;
   return true;
 }
 
@@ -1821,9 +1833,9 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
       return rocblas_status_internal_error;
     const int want_rest = std::min(std::max(c.rest_streams, 1), (int)CholWorkspace::kMaxRest);
     // (re)made when the count changes or the panel events outgrew them (create() re-makes ev)
-    if (ws->side && (want_rest != ws->rest_n ||
+    if (ws->side && (want_rest != ws->rest_n || (want_rest > 1 && c.rest_cumask != ws->rest_cumask) ||
                      (want_rest > 1 && ws->ev_rest.size() < (size_t)CholWorkspace::kMaxRest * (ws->ev.size() / 2))) &&
-        !ws->set_rest_streams(want_rest))
+        !ws->set_rest_streams(want_rest, c.rest_cumask))
       return rocblas_status_internal_error;
   }
   double* scratch = ws ? ws->scratch : nullptr;

@@ -49,6 +49,9 @@ struct CholConfig {
   // Cholesky 15.5 -> 14.7-15.1 ms at nf = 11 993; 3 / 4 streams 16.8-20.8 ms
   // (profiles/r4w_ab_cholesky_rest_streams.jsonl, r4x_..._1to4.jsonl)
   int rest_streams = 2;
+  // the further update streams created with an all-CU mask (a hardware queue
+  // of their own instead of HIP's round-robin share of the process's queues)
+  bool rest_cumask = false;
   bool gemm_update = true;
   // look-ahead: the trailing update after the next panel's block column,
   // 0 one dgemm per 512-wide block column, 1 one dsyrk, 2 one dgemmt,
@@ -168,7 +171,8 @@ struct CholWorkspace {
   rocblas_handle rest_h[kMaxRest - 1] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> ev_rest;  // [panel][kMaxRest]
   int rest_n = 1;
-  bool set_rest_streams(int k);
+  bool rest_cumask = false;
+  bool set_rest_streams(int k, bool cumask = false);
 
   // Creates the resources on `device` with events for up to `max_panels`
   // panels and diagonal-block inverses for matrices up to max_n; false on any
