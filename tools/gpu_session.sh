@@ -64,6 +64,9 @@ for stage in "$@"; do
     trace)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/bench_trace -o run -- python3 bench.py --lm-iters 0 --no-cpu-baseline > gpurun_out/$T/bench_trace.log 2>&1 || exit 1
       tail -c 300 gpurun_out/$T/bench_trace.log ;;
+    tracelm)
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/lm_trace -o run -- python3 bench.py --no-cpu-baseline > gpurun_out/$T/lm_trace.log 2>&1 || exit 1
+      tail -c 300 gpurun_out/$T/lm_trace.log ;;
     bench)
       timeout -k 10 600 python -u bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
       tail -c 300 gpurun_out/$T/bench.json ;;
