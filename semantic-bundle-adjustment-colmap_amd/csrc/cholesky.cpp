@@ -1726,7 +1726,7 @@ bool CholWorkspace::set_split_cus(int ncu) {
   return true;
 }
 
-bool CholWorkspace::set_rest_streams(int k, bool cumask) {
+bool CholWorkspace::set_rest_streams(int k, bool cumask, bool priority) {
   for (int r = 0; r + 1 < kMaxRest; ++r) {
     if (rest_s[r]) (void)hipStreamSynchronize(rest_s[r]);
     if (rest_h[r]) (void)rocblas_destroy_handle(rest_h[r]);
@@ -1737,7 +1737,7 @@ bool CholWorkspace::set_rest_streams(int k, bool cumask) {
   for (hipEvent_t e : ev_rest) (void)hipEventDestroy(e);
   ev_rest.clear();
   rest_n = 1;
-  rest_cumask = false;
+  rest_cumask = rest_priority = false;
   if (k <= 1) return true;
   if (k > kMaxRest || hipSetDevice(device) != hipSuccess) return false;
   std::vector<uint32_t> all;
@@ -1749,8 +1749,11 @@ bool CholWorkspace::set_rest_streams(int k, bool cumask) {
     for (int cu = 0; cu < total; ++cu) all[cu / 32] |= 1u << (cu % 32);
   }
   for (int r = 0; r + 1 < k; ++r) {
-    const hipError_t e = cumask ? hipExtStreamCreateWithCUMask(&rest_s[r], (uint32_t)all.size(), all.data())
-                                : hipStreamCreateWithFlags(&rest_s[r], hipStreamNonBlocking);
+    int least = 0, greatest = 0;
+    if (priority && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    const hipError_t e = cumask     ? hipExtStreamCreateWithCUMask(&rest_s[r], (uint32_t)all.size(), all.data())
+                         : priority ? hipStreamCreateWithPriority(&rest_s[r], hipStreamNonBlocking, greatest)
+                                    : hipStreamCreateWithFlags(&rest_s[r], hipStreamNonBlocking);
     if (e != hipSuccess) {
       rest_s[r] = nullptr;
       return false;
@@ -1768,6 +1771,7 @@ bool CholWorkspace::set_rest_streams(int k, bool cumask) {
   }
   rest_n = k;
   rest_cumask = cumask;
+  rest_priority = priority;
   return true;
 }
 
@@ -1833,9 +1837,10 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
       return rocblas_status_internal_error;
     const int want_rest = std::min(std::max(c.rest_streams, 1), (int)CholWorkspace::kMaxRest);
     // (re)made when the count changes or the panel events outgrew them (create() re-makes ev)
-    if (ws->side && (want_rest != ws->rest_n || (want_rest > 1 && c.rest_cumask != ws->rest_cumask) ||
+    if (ws->side && (want_rest != ws->rest_n ||
+                     (want_rest > 1 && (c.rest_cumask != ws->rest_cumask || c.rest_priority != ws->rest_priority)) ||
                      (want_rest > 1 && ws->ev_rest.size() < (size_t)CholWorkspace::kMaxRest * (ws->ev.size() / 2))) &&
-        !ws->set_rest_streams(want_rest, c.rest_cumask))
+        !ws->set_rest_streams(want_rest, c.rest_cumask, c.rest_priority))
       return rocblas_status_internal_error;
   }
   double* scratch = ws ? ws->scratch : nullptr;

@@ -52,6 +52,9 @@ struct CholConfig {
   // the further update streams created with an all-CU mask (a hardware queue
   // of their own instead of HIP's round-robin share of the process's queues)
   bool rest_cumask = false;
+  // the further update streams at the highest stream priority (as the
+  // look-ahead side stream)
+  bool rest_priority = false;
   bool gemm_update = true;
   // look-ahead: the trailing update after the next panel's block column,
   // 0 one dgemm per 512-wide block column, 1 one dsyrk, 2 one dgemmt,
@@ -171,8 +174,8 @@ struct CholWorkspace {
   rocblas_handle rest_h[kMaxRest - 1] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> ev_rest;  // [panel][kMaxRest]
   int rest_n = 1;
-  bool rest_cumask = false;
-  bool set_rest_streams(int k, bool cumask = false);
+  bool rest_cumask = false, rest_priority = false;
+  bool set_rest_streams(int k, bool cumask = false, bool priority = false);
 
   // Creates the resources on `device` with events for up to `max_panels`
   // panels and diagonal-block inverses for matrices up to max_n; false on any

@@ -2167,6 +2167,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   // while the panel starts before column cholesky_split_cols (tools build:
   // measured 22.5-27.5 vs 15.6 ms, profiles/r4_ab_cholesky_split_cus.jsonl)
   // trailing-update block columns over this many streams (1..4)
+  if (std::strcmp(key, "cholesky_rest_priority") == 0 && (value == 0 || value == 1)) {
+    ctx->chol.rest_priority = value != 0;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_rest_cumask") == 0 && (value == 0 || value == 1)) {
     ctx->chol.rest_cumask = value != 0;
     return MI_BA_OK;
