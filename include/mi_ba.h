@@ -516,6 +516,9 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *                           1024-wide block column (default), 0 per 512, 1 dsyrk, 2 dgemmt
  *   "cholesky_rest_streams" those block columns dealt round-robin over this many
  *                           streams (1-4; default 2)
+ *   "cholesky_rest_cumask" / "cholesky_rest_priority"  1: the extra streams created
+ *                           with an all-CU mask / at the highest priority (measured
+ *                           slower; default 0)
  *   "schur_pairs_variant"   0 explicit Schur pair kernel (default), 1-3 pipelined variants
  *   "semantic_variant"      6 flat pass (samples whose stencil provably stays on
  *                           the centre's outcome: J = 0) + deferred-sample pass
