@@ -30,6 +30,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <exception>
 #include <functional>
 #include <limits>
 #include <map>
@@ -334,17 +335,30 @@ static_assert(sizeof(std::atomic<int32_t>) == sizeof(int32_t) && alignof(std::at
 // runs the caller's callbacks in order; `sync` (set when
 // update_state_every_iteration) copies the point the library has just
 // written into the flattened arrays back into the caller's objects first.
+// No exception crosses the C-ABI callback: one thrown by a callback (or by
+// the state copy) is kept, the solve is aborted (SOLVER_ABORT) and Solve
+// rethrows it once the library has returned (Rethrow), so it leaves Solve as
+// it would leave ceres::Solve.
 struct CallbackBridge {
   const std::vector<IterationCallback*>* callbacks = nullptr;
   std::function<void()> sync;
+  std::exception_ptr error;
   static int32_t Call(void* user, const mi_ba_iteration_summary* summary) {
     CallbackBridge* b = static_cast<CallbackBridge*>(user);
-    if (b->sync) b->sync();
-    for (IterationCallback* cb : *b->callbacks) {
-      const CallbackReturnType r = (*cb)(*summary);
-      if (r != SOLVER_CONTINUE) return r;
+    try {
+      if (b->sync) b->sync();
+      for (IterationCallback* cb : *b->callbacks) {
+        const CallbackReturnType r = (*cb)(*summary);
+        if (r != SOLVER_CONTINUE) return r;
+      }
+    } catch (...) {
+      b->error = std::current_exception();
+      return SOLVER_ABORT;
     }
     return SOLVER_CONTINUE;
+  }
+  void Rethrow() {
+    if (error) std::rethrow_exception(error);
   }
 };
 
@@ -416,6 +430,7 @@ class BundleAdjuster {
     mi_ba_summary s;
     const mi_ba_status st = arena ? mi_ba_solve_in(arena->get(), &o, &flat.problem, nullptr, &s)
                                   : mi_ba_solve(&o, &flat.problem, nullptr, &s);
+    bridge.Rethrow();
     if (st == MI_BA_ERR_NO_RESIDUALS) return false;
     internal::ThrowStatus(st, "BundleAdjuster::Solve");
     summary_ = internal::ToSummary(s);
@@ -438,200 +453,6 @@ class BundleAdjuster {
  private:
   BundleAdjustmentOptions options_;
   BundleAdjustmentConfig config_;
-  SolverSummary summary_;
-  bool used_ = false;
-};
-
-// ---------------------------------------------------------------------------
-// Semantic BA (semantic_bundle_adjustment.h:53-272)
-// ---------------------------------------------------------------------------
-struct SemanticBundleAdjustmentOptions : BundleAdjustmentOptions {
-  // Outputs (semantic_bundle_adjustment.h:60-73).  output_path: the refined
-  // reconstruction is written there (binary) and to output_path/text after
-  // the solve.  visualization_path ("{output_path}/run" resolves to
-  // output_path + "/run", as the controller does, controllers/
-  // semantic_bundle_adjustment.cc:92-94): every LM iteration k writes the
-  // current reconstruction to visualization_path/optim_steps/step_k (binary)
-  // and step_k/text (SBACallbackFunctor, semantic_bundle_adjustment.cc:
-  // 1086-1123), and with export_csv the semantic error of every grid pixel of
-  // every ordered pair of config images to step_k/vis_<image1>_to_<image2>.csv
-  // (ExportSemanticErrorToCSV, :908-1019; the rows come from the GPU,
-  // mi_ba_semantic_export).  Off by default (output_path empty).  Unlike the
-  // reference's createFolders (util/utils.h:101-104), existing folders are
-  // never emptied: files of the same names are overwritten, others are kept.
-  std::string output_path;
-  std::string visualization_path = "{output_path}/run";
-  bool export_csv = false;
-  double depth_error_threshold = 2;
-  int error_computation_pixel_step = 10;
-  double numeric_relative_step_size = 1e-3;
-  double semantic_weight = 1.0;  // build addition (ScaledLoss weight)
-  SemanticBundleAdjustmentOptions() {
-    solver_options.function_tolerance = 1e-8;
-    solver_options.gradient_tolerance = 1e-8;
-    solver_options.parameter_tolerance = 1e-8;
-    // the reference's SBA callbacks read the current point (semantic_bundle_adjustment.h:127-129)
-    solver_options.update_state_every_iteration = true;
-  }
-  std::string ResolvedVisualizationPath() const {
-    if (visualization_path == "{output_path}/run") return output_path.empty() ? std::string() : output_path + "/run";
-    return visualization_path;
-  }
-};
-typedef BundleAdjustmentConfig SemanticBundleAdjustmentConfig;
-
-// Depth / semantic maps per image name: row-major H x W float32 (the
-// matrixFromTiff matrices after their vertical flip, matrix_vis.h:130-176).
-struct SemanticMaps {
-  int height = 0, width = 0;
-  std::unordered_map<std::string, std::vector<float>> depth, semantic;
-};
-
-class SemanticBundleAdjuster {
- public:
-  SemanticBundleAdjuster(const SemanticBundleAdjustmentOptions& options, const SemanticBundleAdjustmentConfig& config,
-                         const SemanticMaps& maps)
-      : options_(options), config_(config), maps_(maps) {
-    options_.Check();
-  }
-
-  bool Solve(Reconstruction* reconstruction) {
-    if (!reconstruction) throw std::invalid_argument("reconstruction is null");
-    if (used_) throw std::logic_error("Cannot use the same BundleAdjuster multiple times");
-    used_ = true;
-    // SemanticBundleAdjuster::Assert (semantic_bundle_adjustment.cc:604-644)
-    if (!options_.refine_extrinsics) throw std::runtime_error("the argument 'refine_extrinsics' must be set to true.");
-    for (const image_t id : config_.Images()) {
-      const Image& im = reconstruction->GetImage(id);
-      if (!config_.IsConstantCamera(im.camera_id))
-        throw std::runtime_error("camera intrinsics of image '" + im.name + "' are not set to constant.");
-    }
-    internal::Flat flat;
-    flat.Build(*reconstruction, config_);
-    // The pose-only semantic problem: no reprojection blocks.
-    flat.problem.num_obs = 0;
-    const int H = maps_.height, W = maps_.width;
-    const size_t plane = (size_t)H * W;
-    std::vector<float> depth(plane * flat.img_ids.size(), 0.f), label(plane * flat.img_ids.size(), 0.f);
-    std::vector<int32_t> pairs;
-    for (size_t i = 0; i < flat.img_ids.size(); ++i) {
-      const Image& im = reconstruction->GetImage(flat.img_ids[i]);
-      auto d = maps_.depth.find(im.name), l = maps_.semantic.find(im.name);
-      if (d == maps_.depth.end() || l == maps_.semantic.end()) {
-        if (config_.HasImage(im.image_id)) throw std::runtime_error("missing depth/semantic map for " + im.name);
-        continue;
-      }
-      std::copy(d->second.begin(), d->second.end(), depth.begin() + i * plane);
-      std::copy(l->second.begin(), l->second.end(), label.begin() + i * plane);
-    }
-    // every ordered pair of config images (SetUp, semantic_bundle_adjustment.cc:656-661)
-    for (size_t i = 0; i < flat.img_ids.size(); ++i)
-      for (size_t j = 0; j < flat.img_ids.size(); ++j)
-        if (flat.img_cfg[i] && flat.img_cfg[j]) {
-          pairs.push_back((int32_t)i);
-          pairs.push_back((int32_t)j);
-        }
-    mi_ba_semantic sem;
-    sem.height = H;
-    sem.width = W;
-    sem.depth = depth.data();
-    sem.label = label.data();
-    sem.num_pairs = (int32_t)(pairs.size() / 2);
-    sem.pairs = pairs.data();
-    sem.pixel_step = options_.error_computation_pixel_step;
-    sem.depth_error_threshold = options_.depth_error_threshold;
-    sem.numeric_relative_step_size = options_.numeric_relative_step_size;
-    mi_ba_options o = internal::ToOptions(options_);
-    o.semantic_weight = options_.semantic_weight;
-    // the per-iteration snapshot writer runs after the caller's callbacks
-    // (Solve pushes the SBACallbackFunctor last, semantic_bundle_adjustment.cc:519-520)
-    const std::string steps = options_.ResolvedVisualizationPath();
-    SolverArena arena;  // the live context, for the CSV rows inside the callback
-    SemanticBundleAdjustmentOptions cb_options = options_;
-    struct StepWriter : IterationCallback {
-      SemanticBundleAdjuster* sba;
-      Reconstruction* rec;
-      const internal::Flat* flat;
-      SolverArena* arena;
-      std::string steps;
-      CallbackReturnType operator()(const IterationSummary& it) override {
-        std::printf("\nOptimization Iteration %d Update\n%-16s%.6g\n%-16s%.6g\n", it.iteration, "Cost: ", it.cost,
-                    "Cost change: ", it.cost_change);
-        sba->WriteStep(*rec, *flat, *arena->get(), steps + "/optim_steps/step_" + std::to_string(it.iteration));
-        return SOLVER_CONTINUE;
-      }
-    } writer;
-    writer.sba = this;
-    writer.rec = reconstruction;
-    writer.flat = &flat;
-    writer.arena = &arena;
-    writer.steps = steps;
-    if (!steps.empty()) {
-      cb_options.solver_options.callbacks.push_back(&writer);
-      cb_options.solver_options.update_state_every_iteration = true;
-    }
-    internal::CallbackBridge bridge;
-    internal::InstallCallbacks(cb_options, &bridge, [&] { flat.WriteBack(reconstruction); }, &o);
-    mi_ba_summary s;
-    const mi_ba_status st = mi_ba_solve_in(arena.get(), &o, &flat.problem, &sem, &s);
-    if (st == MI_BA_ERR_NO_RESIDUALS) return false;
-    internal::ThrowStatus(st, "SemanticBundleAdjuster::Solve");
-    summary_ = internal::ToSummary(s);
-    flat.WriteBack(reconstruction);
-    if (!options_.output_path.empty()) {  // :531-538
-      internal::MakeDirs(options_.output_path + "/text");
-      WriteModelBinary(options_.output_path, *reconstruction);
-      WriteModelText(options_.output_path + "/text", *reconstruction);
-    }
-    return true;
-  }
-
-  const SolverSummary& Summary() const { return summary_; }
-
-  // One snapshot (SBACallbackFunctor::operator(), semantic_bundle_adjustment.cc:
-  // 1090-1123): the reconstruction's current state to dir (binary) and
-  // dir/text, and with export_csv every ordered pair of config images'
-  // ExportSemanticErrorToCSV file dir/vis_<name1>_to_<name2>.csv.
-  void WriteStep(const Reconstruction& rec, const internal::Flat& flat, mi_ba_context* ctx, const std::string& dir) {
-    internal::MakeDirs(dir + "/text");
-    if (options_.export_csv) {
-      std::vector<int32_t> pix, status;
-      std::vector<double> err, world;
-      for (size_t a = 0; a < flat.img_ids.size(); ++a) {
-        if (!flat.img_cfg[a]) continue;
-        for (size_t b = 0; b < flat.img_ids.size(); ++b) {
-          if (a == b || !flat.img_cfg[b]) continue;
-          int64_t n = 0;
-          internal::ThrowStatus(mi_ba_semantic_export(ctx, (int32_t)a, (int32_t)b, &n, nullptr, nullptr, nullptr, nullptr),
-                                "ExportSemanticErrorToCSV");
-          pix.resize(4 * n);
-          status.resize(n);
-          err.resize(n);
-          world.resize(3 * n);
-          internal::ThrowStatus(mi_ba_semantic_export(ctx, (int32_t)a, (int32_t)b, &n, pix.data(), status.data(),
-                                                      err.data(), world.data()),
-                                "ExportSemanticErrorToCSV");
-          const std::string path = dir + "/vis_" + rec.GetImage(flat.img_ids[a]).name + "_to_" +
-                                   rec.GetImage(flat.img_ids[b]).name + ".csv";
-          std::ofstream f(path);
-          if (!f.is_open()) throw std::runtime_error("cannot write " + path);
-          // :994-1007: default stream formatting, the error as float
-          f << "Type,SemanticError,X1,Y1,X2,Y2,X3D,Y3D,Z3D\n";
-          for (int64_t k = 0; k < n; ++k)
-            f << status[k] << "," << (float)err[k] << "," << pix[4 * k] << "," << pix[4 * k + 1] << ","
-              << pix[4 * k + 2] << "," << pix[4 * k + 3] << "," << world[3 * k] << "," << world[3 * k + 1] << ","
-              << world[3 * k + 2] << "\n";
-        }
-      }
-    }
-    WriteModelBinary(dir, rec);
-    WriteModelText(dir + "/text", rec);
-  }
-
- private:
-  SemanticBundleAdjustmentOptions options_;
-  SemanticBundleAdjustmentConfig config_;
-  SemanticMaps maps_;
   SolverSummary summary_;
   bool used_ = false;
 };
@@ -778,3 +599,7 @@ inline void PrintSolverSummary(const SolverSummary& s) {
 }
 
 }  // namespace colmap_amd
+
+// SemanticBundleAdjuster and its options live in semantic_bundle_adjustment.h
+// (the reference's file split); included here so existing callers keep working.
+#include "semantic_bundle_adjustment.h"

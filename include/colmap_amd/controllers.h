@@ -127,8 +127,8 @@ class BundleAdjustmentController : public ControllerThread {
 
 class SemanticBundleAdjustmentController : public ControllerThread {
  public:
-  // data_path: the folder with depth_tiff/ and semantic_tiff/
-  // (SemanticBundleAdjustmentOptions::data_path)
+  // data_path (nonempty): the folder with depth_tiff/ and semantic_tiff/,
+  // overriding options.data_path (SemanticBundleAdjustmentOptions::data_path)
   SemanticBundleAdjustmentController(const SemanticBundleAdjustmentOptions& options, const std::string& data_path,
                                      Reconstruction* reconstruction)
       : options_(options), data_path_(data_path), reconstruction_(reconstruction) {}
@@ -150,8 +150,8 @@ class SemanticBundleAdjustmentController : public ControllerThread {
     config.SetConstantPose(reg[0]);
     config.SetConstantTvec(reg[1], {0});
     for (const image_t id : reg) config.SetConstantCamera(reconstruction_->GetImage(id).camera_id);
-    const SemanticMaps maps = LoadSemanticMaps(data_path_, *reconstruction_, config);
-    SemanticBundleAdjuster adjuster(ba_options, config, maps);
+    if (!data_path_.empty()) ba_options.data_path = data_path_;
+    SemanticBundleAdjuster adjuster(ba_options, config);  // the maps from ba_options.data_path
     solved_ = adjuster.Solve(reconstruction_);
     summary_ = adjuster.Summary();
   }

@@ -175,6 +175,7 @@ class GeometricSemanticBundleAdjuster {
     }, &o);
     mi_ba_summary s;
     const mi_ba_status st = mi_ba_gsba_solve(&o, &flat.problem, &g, &s);
+    bridge.Rethrow();
     if (st == MI_BA_ERR_NO_RESIDUALS) return false;
     internal::ThrowStatus(st, "GeometricSemanticBundleAdjuster::Solve");
     summary_ = internal::ToSummary(s);

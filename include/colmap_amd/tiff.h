@@ -2,8 +2,8 @@
 // (header-only, host code).
 //
 //   MatrixFromTiff  <- matrixFromTiff (src/util/matrix_vis.h:130-176)
-//   LoadSemanticMaps <- SemanticBundleAdjuster::ReadDepthAndSemanticMaps
-//                       (src/optim/semantic_bundle_adjustment.cc:1021-1068)
+//   LoadSemanticMaps (ReadDepthAndSemanticMaps, src/optim/semantic_bundle_adjustment.cc:
+//   1021-1068) is in semantic_bundle_adjustment.h.
 //
 // The reference loads through FreeImage, whose bitmaps are stored bottom-up,
 // and writes matrix(height - 1 - i, j) = scanline i: the Eigen matrix is the
@@ -31,7 +31,6 @@
 #include <unordered_map>
 #include <vector>
 
-#include "bundle_adjustment.h"
 
 #ifdef COLMAP_AMD_TIFF_ZLIB
 #include <zlib.h>
@@ -283,37 +282,8 @@ inline std::vector<float> MatrixFromTiff(const std::string& path, int* height, i
   return out;
 }
 
-// SemanticBundleAdjuster::ReadDepthAndSemanticMaps (semantic_bundle_adjustment.cc:
-// 1021-1068): <data_path>/depth_tiff/<stem>_depth.tiff and
-// <data_path>/semantic_tiff/<stem>_semantic.tiff of every config image, stem
-// = the image name up to its last '.'.  Every map must have one size (the
-// semantic term samples one H x W grid, mi_ba_semantic).
-inline SemanticMaps LoadSemanticMaps(const std::string& data_path, const Reconstruction& reconstruction,
-                                     const BundleAdjustmentConfig& config) {
-  SemanticMaps maps;
-  auto exists = [](const std::string& p) {
-    std::ifstream f(p, std::ios::binary);
-    return f.good();
-  };
-  for (const image_t id : config.Images()) {
-    const std::string& name = reconstruction.GetImage(id).name;
-    const std::string stem = name.substr(0, name.find_last_of('.'));
-    const std::string depth_path = data_path + "/depth_tiff/" + stem + "_depth.tiff";
-    const std::string semantic_path = data_path + "/semantic_tiff/" + stem + "_semantic.tiff";
-    if (!exists(depth_path)) throw std::runtime_error("ERROR: the depth file '" + depth_path + "' does not exist.");
-    if (!exists(semantic_path))
-      throw std::runtime_error("ERROR: the semantic file '" + semantic_path + "' does not exist.");
-    int h0, w0, h1, w1;
-    std::vector<float> d = MatrixFromTiff(depth_path, &h0, &w0);
-    std::vector<float> l = MatrixFromTiff(semantic_path, &h1, &w1);
-    if (h0 != h1 || w0 != w1 || (maps.height && (h0 != maps.height || w0 != maps.width)))
-      throw std::invalid_argument("depth / semantic maps of different sizes");
-    maps.height = h0;
-    maps.width = w0;
-    maps.depth[name] = std::move(d);
-    maps.semantic[name] = std::move(l);
-  }
-  return maps;
-}
-
 }  // namespace colmap_amd
+
+// LoadSemanticMaps (ReadDepthAndSemanticMaps) lives in semantic_bundle_adjustment.h;
+// included here so existing callers keep working.
+#include "semantic_bundle_adjustment.h"

@@ -489,6 +489,10 @@ mi_ba_status mi_ba_comm_unique_id(char id[MI_BA_COMM_ID_BYTES]);
  * set-up polled to the "comm_timeout_ms" deadline (set that key first). */
 mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t world,
                                     const char id[MI_BA_COMM_ID_BYTES]);
+/* Number of communicator set-ups still running on their helper threads (a
+ * failed or timed-out set_comm ends its helper by the same deadline: the
+ * helper stops polling, aborts the half-built communicator and exits). */
+int32_t mi_ba_comm_pending_setups(void);
 /* Alternative reducer for hosts without one GPU per rank: sums `n` doubles of
  * a host buffer in place across ranks (returns 0 on success).  Used by the
  * 1-GPU multi-rank rehearsal (gloo). */

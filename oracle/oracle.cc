@@ -908,6 +908,13 @@ int CholeskyBlocked(double* A, int n) {
 typedef int (*DenseFactorFn)(double* A, int n);
 DenseFactorFn g_dense_factor = nullptr;
 
+// Optional per-iteration trace of the LM (test infrastructure,
+// oracle_set_trace): per iteration k >= 1, entries [4k-4, 4k) = step valid,
+// step successful, linear solver iterations, termination marker (1 on the
+// iteration that ended the solve).
+int32_t* g_trace = nullptr;
+int g_trace_cap = 0;
+
 bool Cholesky(std::vector<double>& A, int n) {  // in place, lower
   if (g_dense_factor) return g_dense_factor(A.data(), n) == 0;
   return CholeskyBlocked(A.data(), n) == 0;
@@ -1175,6 +1182,91 @@ struct Solver {
       y.radius = std::max(y.radius + d[6], 0.0);
       y.height += d[7];
     }
+  }
+  // TrustRegionMinimizer's state vector x_: the reduced program's variable
+  // parameter blocks in ambient coordinates (qvec 4, tvec 3, the camera's
+  // params, X 3, the cylinder's blocks).  |x| and |x - candidate| give Ceres'
+  // ParameterToleranceReached (step_norm = |x - candidate_x|).
+  void State(std::vector<double>* x) const {
+    x->clear();
+    for (int i = 0; i < p->num_images; ++i) {
+      if (L.img_off[i] < 0) continue;
+      x->insert(x->end(), &p->qvec[i * 4], &p->qvec[i * 4] + 4);
+      x->insert(x->end(), &p->tvec[i * 3], &p->tvec[i * 3] + 3);
+    }
+    for (int c = 0; c < p->num_cameras; ++c)
+      if (L.cam_off[c] >= 0)
+        x->insert(x->end(), &p->camera_params[s.cam_poff[c]], &p->camera_params[s.cam_poff[c + 1]]);
+    for (int64_t pt = 0; pt < p->num_points; ++pt)
+      if (L.pt_off[pt] >= 0) x->insert(x->end(), &p->xyz[pt * 3], &p->xyz[pt * 3] + 3);
+    for (size_t c = 0; c < L.cyl_off.size(); ++c) {
+      if (L.cyl_off[c] < 0) continue;
+      if (gs.by2) {
+        x->insert(x->end(), &gs.by2p[7 * c], &gs.by2p[7 * c] + 7);
+      } else {
+        const mi_ba_cylinder& y = gs.g->cylinders[c];
+        x->insert(x->end(), y.qvec, y.qvec + 4);
+        x->insert(x->end(), y.tvec, y.tvec + 3);
+        x->push_back(y.radius);
+        x->push_back(y.height);
+      }
+    }
+  }
+  // |x - Plus(x, -g)|_inf with g = J'f the tangent gradient at the current
+  // point (TrustRegionMinimizer::EvaluateGradientAndJacobian: Ceres' gradient
+  // max norm, projected through each block's Plus and its bounds — the
+  // cylinder radius >= 0).
+  double GradientMaxNorm(const Linearization& lin) const {
+    constexpr int kF = Linearization::kF;
+    const int nf = L.nf;
+    std::vector<double> g(nf + L.ne, 0.0);
+    for (size_t R = 0; R < lin.rows(); ++R) {
+      for (int m = 0; m < lin.fn[R]; ++m) g[lin.fcol[R * kF + m]] += lin.fval[R * kF + m] * lin.r[R];
+      for (int m = 0; m < lin.en[R]; ++m) g[nf + lin.ecol[R * 3 + m]] += lin.eval[R * 3 + m] * lin.r[R];
+    }
+    double mx = 0.0;
+    auto euclid = [&](double x, double gc) { mx = std::max(mx, std::fabs(x - (x + -gc))); };
+    auto quat = [&](const double* q, const double* gq) {
+      const double d[3] = {-gq[0], -gq[1], -gq[2]};
+      double qn[4];
+      QuaternionPlus(q, d, qn);
+      for (int m = 0; m < 4; ++m) mx = std::max(mx, std::fabs(q[m] - qn[m]));
+    };
+    for (int i = 0; i < p->num_images; ++i) {
+      if (L.img_off[i] < 0) continue;
+      double gq[3];
+      for (int m = 0; m < 3; ++m) gq[m] = g[L.img_cols[(size_t)i * 6 + m]];
+      quat(&p->qvec[i * 4], gq);
+      for (int m = 3; m < 6; ++m) {
+        const int col = L.img_cols[(size_t)i * 6 + m];
+        if (col >= 0) euclid(p->tvec[i * 3 + m - 3], g[col]);
+      }
+    }
+    for (int c = 0; c < p->num_cameras; ++c) {
+      if (L.cam_off[c] < 0) continue;
+      for (size_t m = 0; m < s.cam_tangent[c].size(); ++m)
+        euclid(p->camera_params[s.cam_poff[c] + s.cam_tangent[c][m]], g[L.cam_off[c] + m]);
+    }
+    for (int64_t pt = 0; pt < p->num_points; ++pt) {
+      if (L.pt_off[pt] < 0) continue;
+      for (int m = 0; m < 3; ++m) euclid(p->xyz[pt * 3 + m], g[nf + L.pt_off[pt] + m]);
+    }
+    for (size_t c = 0; c < L.cyl_off.size(); ++c) {
+      if (L.cyl_off[c] < 0) continue;
+      const double* gc = &g[L.cyl_off[c]];
+      if (gs.by2) {
+        const double* y = &gs.by2p[7 * c];
+        for (int m = 0; m < 6; ++m) euclid(y[m], gc[m]);
+        mx = std::max(mx, std::fabs(y[6] - std::max(y[6] + -gc[6], 0.0)));
+      } else {
+        const mi_ba_cylinder& y = gs.g->cylinders[c];
+        quat(y.qvec, gc);
+        for (int m = 0; m < 3; ++m) euclid(y.tvec[m], gc[3 + m]);
+        mx = std::max(mx, std::fabs(y.radius - std::max(y.radius + -gc[6], 0.0)));
+        euclid(y.height, gc[7]);
+      }
+    }
+    return mx;
   }
 };
 
@@ -1460,11 +1552,319 @@ void oracle_set_flat_coarse(int coarse) { g_flat_coarse = coarse; }
 // camera system.
 void oracle_set_dense_factor(DenseFactorFn fn) { g_dense_factor = fn; }
 
+// Record the per-iteration LM trace of the next solves into buf (4 int32 per
+// iteration, at most cap iterations); null turns it off.
+void oracle_set_trace(int32_t* buf, int cap) {
+  g_trace = buf;
+  g_trace_cap = buf ? cap : 0;
+}
+
 }  // extern "C"
 
 namespace {
-// Full LM solve, dense Schur (Ceres 2.1 LM semantics, restated), with the
-// optional semantic (SBA) and GSBA terms.
+
+// ---------------------------------------------------------------------------
+// ITERATIVE_SCHUR + SCHUR_JACOBI, the solver BundleAdjuster::Solve selects
+// above 1000 images (bundle_adjustment.cc:276-286; SBA the same,
+// semantic_bundle_adjustment.cc:494-499).  Ceres 2.1 is third party and not
+// vendored; restated from its published sources:
+//   * ImplicitSchurComplement (implicit_schur_complement.cc) with A = J
+//     diag(scale) = [E | F] (points are the e blocks):
+//       S x  = D_f^2 x + F'(F x - E (E'E + D_e^2)^-1 E'F x)
+//       rhs  = F'(b - E (E'E + D_e^2)^-1 E'b)
+//       back substitution x_e = (E'E + D_e^2)^-1 E'(b - F x_f)
+//     every product through the rows (RightMultiplyF, LeftMultiplyE,
+//     RightMultiplyE, LeftMultiplyF), never forming S;
+//   * SchurJacobiPreconditioner (schur_jacobi_preconditioner.cc): the
+//     diagonal blocks of S, one per f parameter block — qvec (3 tangent),
+//     tvec (3, or fewer under a SubsetManifold), the camera's refined
+//     intrinsics, and for GSBA the cylinder's qvec / tvec / radius / height
+//     (by two points: tvec_1 / tvec_2 / radius) — each inverted through an LLT
+//     (BlockRandomAccessDiagonalMatrix::Invert);
+//   * ConjugateGradientsSolver (conjugate_gradients_solver.cc): x = 0, r = b;
+//     r_tolerance off (LevenbergMarquardtStrategy passes -1); per iteration
+//     z = M r, rho = r'z (FAILURE when 0 / inf), p = z or z + (rho / rho_prev)
+//     p (FAILURE when beta is 0 / inf), q = S p, pq = p'q (NO_CONVERGENCE when
+//     <= 0 / inf, before x moves), alpha = rho / pq (FAILURE when inf),
+//     x += alpha p, r = b - S x every residual_reset_period = 10 iterations
+//     else r -= alpha q, Q1 = -x'(b + r), stop when i (Q1 - Q0) / Q1 < eta,
+//     NO_CONVERGENCE at max_linear_solver_iterations.  A FAILURE is an invalid
+//     LM step (TrustRegionMinimizer::ComputeTrustRegionStep); NO_CONVERGENCE
+//     and SUCCESS steps are used.
+// ---------------------------------------------------------------------------
+enum CgTermination { kCgSuccess = 0, kCgNoConvergence = 1, kCgFailure = 2 };
+
+struct ImplicitSchur {
+  const Linearization* lin = nullptr;
+  const double* scale = nullptr;  // Jacobi scaling, f then e coordinates
+  const double* D2 = nullptr;     // LM diagonal D^2 (diag / radius), f then e
+  const double* Vinv = nullptr;   // [np3][9] (E'E + D_e^2)^-1
+  int nf = 0;
+  int64_t np3 = 0;
+  std::vector<int64_t> prow_off, prow;  // each point's rows, in row order
+  std::vector<int64_t> ft_off, ft_row;  // F transposed: each column's rows, in row order
+  std::vector<int> ft_slot;             // the row's f slot of that column
+  std::vector<double> rows, te, te2;
+
+  // structure (the rows of each point, the rows of each f column): once per
+  // linearization layout (constant over the solve)
+  void Structure(const Linearization& L, int nf_, int64_t np3_) {
+    lin = &L;
+    nf = nf_;
+    np3 = np3_;
+    constexpr int kF = Linearization::kF;
+    const size_t nr = L.rows();
+    prow_off.assign(np3 + 1, 0);
+    for (size_t R = 0; R < nr; ++R)
+      if (L.en[R]) ++prow_off[L.ecol[R * 3] / 3 + 1];
+    for (int64_t p = 0; p < np3; ++p) prow_off[p + 1] += prow_off[p];
+    prow.assign(prow_off[np3], 0);
+    {
+      std::vector<int64_t> pos(prow_off.begin(), prow_off.end() - 1);
+      for (size_t R = 0; R < nr; ++R)
+        if (L.en[R]) prow[pos[L.ecol[R * 3] / 3]++] = (int64_t)R;
+    }
+    ft_off.assign(nf + 1, 0);
+    for (size_t R = 0; R < nr; ++R)
+      for (int m = 0; m < L.fn[R]; ++m) ++ft_off[L.fcol[R * kF + m] + 1];
+    for (int c = 0; c < nf; ++c) ft_off[c + 1] += ft_off[c];
+    ft_row.assign(ft_off[nf], 0);
+    ft_slot.assign(ft_off[nf], 0);
+    std::vector<int64_t> pos(ft_off.begin(), ft_off.end() - 1);
+    for (size_t R = 0; R < nr; ++R)
+      for (int m = 0; m < L.fn[R]; ++m) {
+        const int64_t k = pos[L.fcol[R * kF + m]]++;
+        ft_row[k] = (int64_t)R;
+        ft_slot[k] = m;
+      }
+    rows.assign(nr, 0.0);
+    te.assign(3 * np3, 0.0);
+    te2.assign(3 * np3, 0.0);
+  }
+  // out[R] = (F x)[R]
+  void RightMultiplyF(const double* x, double* out) const {
+    constexpr int kF = Linearization::kF;
+    const int64_t nr = (int64_t)lin->rows();
+#pragma omp parallel for schedule(static)
+    for (int64_t R = 0; R < nr; ++R) {
+      double acc = 0.0;
+      for (int m = 0; m < lin->fn[R]; ++m) {
+        const int32_t c = lin->fcol[R * kF + m];
+        acc += (lin->fval[R * kF + m] * scale[c]) * x[c];
+      }
+      out[R] = acc;
+    }
+  }
+  // e = E' in (per point, its rows in order)
+  void LeftMultiplyE(const double* in, double* e) const {
+#pragma omp parallel for schedule(static)
+    for (int64_t p = 0; p < np3; ++p) {
+      double a[3] = {0.0, 0.0, 0.0};
+      for (int64_t k = prow_off[p]; k < prow_off[p + 1]; ++k) {
+        const int64_t R = prow[k];
+        for (int m = 0; m < 3; ++m) {
+          const int64_t c = lin->ecol[R * 3 + m];
+          a[c % 3] += (lin->eval[R * 3 + m] * scale[nf + c]) * in[R];
+        }
+      }
+      for (int m = 0; m < 3; ++m) e[3 * p + m] = a[m];
+    }
+  }
+  // out[R] += (E e)[R]
+  void RightMultiplyE(const double* e, double* out) const {
+    const int64_t nr = (int64_t)lin->rows();
+#pragma omp parallel for schedule(static)
+    for (int64_t R = 0; R < nr; ++R) {
+      if (!lin->en[R]) continue;
+      double acc = 0.0;
+      for (int m = 0; m < 3; ++m) {
+        const int64_t c = lin->ecol[R * 3 + m];
+        acc += (lin->eval[R * 3 + m] * scale[nf + c]) * e[c];
+      }
+      out[R] += acc;
+    }
+  }
+  // y += F' in (per column, its rows in order)
+  void LeftMultiplyF(const double* in, double* y) const {
+    constexpr int kF = Linearization::kF;
+#pragma omp parallel for schedule(static)
+    for (int c = 0; c < nf; ++c) {
+      double acc = 0.0;
+      for (int64_t k = ft_off[c]; k < ft_off[c + 1]; ++k) {
+        const int64_t R = ft_row[k];
+        acc += (lin->fval[R * kF + ft_slot[k]] * scale[c]) * in[R];
+      }
+      y[c] += acc;
+    }
+  }
+  void EtEInverse(const double* in, double* out) const {
+#pragma omp parallel for schedule(static)
+    for (int64_t p = 0; p < np3; ++p)
+      for (int a = 0; a < 3; ++a) {
+        double acc = 0.0;
+        for (int k = 0; k < 3; ++k) acc += Vinv[p * 9 + a * 3 + k] * in[3 * p + k];
+        out[3 * p + a] = acc;
+      }
+  }
+  // ImplicitSchurComplement::RightMultiply
+  void RightMultiply(const double* x, double* y) {
+    RightMultiplyF(x, rows.data());
+    LeftMultiplyE(rows.data(), te.data());
+    EtEInverse(te.data(), te2.data());
+    for (auto& v : te2) v = -v;
+    RightMultiplyE(te2.data(), rows.data());
+    for (int c = 0; c < nf; ++c) y[c] = D2[c] * x[c];
+    LeftMultiplyF(rows.data(), y);
+  }
+  // ImplicitSchurComplement::UpdateRhs (b = the residuals)
+  void Rhs(const double* b, double* rhs) {
+    LeftMultiplyE(b, te.data());
+    EtEInverse(te.data(), te2.data());
+    const int64_t nr = (int64_t)lin->rows();
+    std::fill(rows.begin(), rows.end(), 0.0);
+    RightMultiplyE(te2.data(), rows.data());
+    for (int64_t R = 0; R < nr; ++R) rows[R] = b[R] - rows[R];
+    std::fill(rhs, rhs + nf, 0.0);
+    LeftMultiplyF(rows.data(), rhs);
+  }
+  // ImplicitSchurComplement::BackSubstitute: x_e from x_f
+  void BackSubstitute(const double* b, const double* xf, double* xe) {
+    RightMultiplyF(xf, rows.data());
+    const int64_t nr = (int64_t)lin->rows();
+    for (int64_t R = 0; R < nr; ++R) rows[R] = b[R] - rows[R];
+    LeftMultiplyE(rows.data(), te.data());
+    EtEInverse(te.data(), xe);
+  }
+};
+
+// The f parameter blocks of the reduced camera system (Ceres column blocks
+// after the e blocks): (first column, size).
+std::vector<std::pair<int, int>> FBlocks(const Setup& s, const mi_ba_problem* p, const Layout& L,
+                                         const GsbaSetup& gs) {
+  std::vector<std::pair<int, int>> b;
+  for (int i = 0; i < p->num_images; ++i) {
+    if (L.img_off[i] < 0) continue;
+    b.push_back({L.img_cols[(size_t)i * 6], 3});
+    int nt = 0, t0 = -1;
+    for (int m = 3; m < 6; ++m)
+      if (L.img_cols[(size_t)i * 6 + m] >= 0) { if (t0 < 0) t0 = L.img_cols[(size_t)i * 6 + m]; ++nt; }
+    if (nt) b.push_back({t0, nt});
+  }
+  for (int c = 0; c < p->num_cameras; ++c)
+    if (L.cam_off[c] >= 0 && !s.cam_tangent[c].empty()) b.push_back({L.cam_off[c], (int)s.cam_tangent[c].size()});
+  for (size_t c = 0; c < L.cyl_off.size(); ++c) {
+    if (L.cyl_off[c] < 0) continue;
+    const int o = L.cyl_off[c];
+    b.push_back({o, 3});
+    b.push_back({o + 3, 3});
+    b.push_back({o + 6, 1});
+    if (!gs.by2) b.push_back({o + 7, 1});
+  }
+  return b;
+}
+
+// Inverse of a small SPD block through its LLT (Eigen llt().solve(I)); the
+// upper triangle is read, as selfadjointView<Upper>.
+void LltInverse(const std::vector<double>& M, int k, std::vector<double>* inv) {
+  std::vector<double> L((size_t)k * k, 0.0);
+  for (int j = 0; j < k; ++j) {
+    double d = M[(size_t)j * k + j];
+    for (int m = 0; m < j; ++m) d -= L[(size_t)j * k + m] * L[(size_t)j * k + m];
+    d = std::sqrt(d);
+    L[(size_t)j * k + j] = d;
+    for (int i = j + 1; i < k; ++i) {
+      double v = M[(size_t)j * k + i];  // upper: (j, i)
+      for (int m = 0; m < j; ++m) v -= L[(size_t)i * k + m] * L[(size_t)j * k + m];
+      L[(size_t)i * k + j] = v / d;
+    }
+  }
+  inv->assign((size_t)k * k, 0.0);
+  std::vector<double> y(k);
+  for (int c = 0; c < k; ++c) {
+    for (int i = 0; i < k; ++i) {
+      double v = i == c ? 1.0 : 0.0;
+      for (int m = 0; m < i; ++m) v -= L[(size_t)i * k + m] * y[m];
+      y[i] = v / L[(size_t)i * k + i];
+    }
+    for (int i = k - 1; i >= 0; --i) {
+      double v = y[i];
+      for (int m = i + 1; m < k; ++m) v -= L[(size_t)m * k + i] * y[m];
+      y[i] = v / L[(size_t)i * k + i];
+    }
+    for (int i = 0; i < k; ++i) (*inv)[(size_t)i * k + c] = y[i];
+  }
+}
+
+// ConjugateGradientsSolver::Solve on the implicit Schur complement with the
+// SCHUR_JACOBI blocks.  x (nf) out; returns the CgTermination.
+int SchurPcg(ImplicitSchur& A, const std::vector<std::pair<int, int>>& blocks,
+             const std::vector<std::vector<double>>& Minv, const double* b, int nf, double eta, int max_it,
+             double* x, int* iterations) {
+  std::fill(x, x + nf, 0.0);
+  *iterations = 0;
+  double norm_b = 0.0;
+  for (int i = 0; i < nf; ++i) norm_b += b[i] * b[i];
+  if (std::sqrt(norm_b) == 0.0) return kCgSuccess;  // "Convergence. |b| = 0."
+  std::vector<double> r(b, b + nf), p(nf, 0.0), z(nf), tmp(nf);
+  auto zero_or_inf = [](double v) { return v == 0.0 || std::isinf(v); };
+  double rho = 1.0;
+  double Q0 = 0.0;  // -x'(b + r) at x = 0
+  for (int it = 1;; ++it) {
+    *iterations = it;
+    for (size_t k = 0; k < blocks.size(); ++k) {  // z = M r
+      const int o = blocks[k].first, w = blocks[k].second;
+      for (int a = 0; a < w; ++a) {
+        double acc = 0.0;
+        for (int c = 0; c < w; ++c) acc += Minv[k][(size_t)a * w + c] * r[o + c];
+        z[o + a] = acc;
+      }
+    }
+    const double last_rho = rho;
+    rho = 0.0;
+    for (int i = 0; i < nf; ++i) rho += r[i] * z[i];
+    if (zero_or_inf(rho)) return kCgFailure;
+    if (it == 1) {
+      p = z;
+    } else {
+      const double beta = rho / last_rho;
+      if (zero_or_inf(beta)) return kCgFailure;
+      for (int i = 0; i < nf; ++i) p[i] = z[i] + beta * p[i];
+    }
+    std::vector<double>& q = z;
+    A.RightMultiply(p.data(), q.data());
+    double pq = 0.0;
+    for (int i = 0; i < nf; ++i) pq += p[i] * q[i];
+    if (pq <= 0.0 || std::isinf(pq)) return kCgNoConvergence;
+    const double alpha = rho / pq;
+    if (std::isinf(alpha)) return kCgFailure;
+    for (int i = 0; i < nf; ++i) x[i] = x[i] + alpha * p[i];
+    if (it % 10 == 0) {
+      A.RightMultiply(x, tmp.data());
+      for (int i = 0; i < nf; ++i) r[i] = b[i] - tmp[i];
+    } else {
+      for (int i = 0; i < nf; ++i) r[i] = r[i] - alpha * q[i];
+    }
+    double Q1 = 0.0;
+    for (int i = 0; i < nf; ++i) Q1 += x[i] * (b[i] + r[i]);
+    Q1 = -1.0 * Q1;
+    const double zeta = it * (Q1 - Q0) / Q1;
+    if (zeta < eta) return kCgSuccess;
+    Q0 = Q1;
+    if (it >= max_it) return kCgNoConvergence;
+  }
+}
+
+// Images in the configuration (bundle_adjustment.cc:276-286 counts
+// config.NumImages()).
+int64_t ConfigImages(const mi_ba_problem* p) {
+  int64_t n = 0;
+  for (int i = 0; i < p->num_images; ++i) n += p->image_in_config ? (p->image_in_config[i] != 0) : 1;
+  return n;
+}
+
+// Full LM solve (Ceres 2.1 LM semantics, restated) with the exact dense
+// Schur solve or ITERATIVE_SCHUR, and the optional semantic (SBA) and GSBA
+// terms.
 int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* sem, const mi_ba_gsba* gsba,
               mi_ba_summary* sum) {
   Solver S;
@@ -1525,9 +1925,35 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
   std::vector<std::vector<double>> W(np3);
   std::vector<std::vector<int>> Wcols(np3);
   std::vector<int> wslot;  // [row][kF] slot of f entry in its point's W
+  // linear solver (bundle_adjustment.cc:276-286): the exact Schur solve up
+  // to 1000 configured images, ITERATIVE_SCHUR + SCHUR_JACOBI above
+  const bool use_pcg = o->linear_solver_type == MI_BA_SOLVER_ITERATIVE_SCHUR ||
+                       (o->linear_solver_type == MI_BA_SOLVER_AUTO && ConfigImages(p) > 1000);
+  ImplicitSchur isc;
+  std::vector<std::pair<int, int>> fblocks;
+  if (use_pcg) {
+    isc.Structure(lin, nf, np3);
+    isc.scale = scale.data();
+    fblocks = FBlocks(S.s, p, S.L, S.gs);
+  }
+  // gradient max norm at the current point (Ceres evaluates it with every
+  // Jacobian: IterationZero and each successful step)
+  double gmax = S.GradientMaxNorm(lin);
+  bool last_successful = true;  // iteration 0 counts as successful
+  auto trace = [&](int it, int valid, int success, int cg, int end) {
+    if (!g_trace || it < 1 || it > g_trace_cap) return;
+    int32_t* t = g_trace + 4 * (size_t)(it - 1);
+    t[0] = valid; t[1] = success; t[2] = cg; t[3] = end;
+  };
+  if (g_trace) std::fill(g_trace, g_trace + 4 * (size_t)g_trace_cap, -1);
+  std::vector<double> x_state, c_state;
   while (true) {
+    // FinalizeIterationAndCheckIfMinimizerCanContinue: the iteration cap, the
+    // gradient tolerance (after a successful step or at iteration 0), the
+    // minimum trust-region radius
     if (iteration >= o->max_num_iterations) { sum->termination_type = MI_BA_NO_CONVERGENCE; break; }
-    if (radius < 1e-32) { sum->termination_type = MI_BA_CONVERGENCE; break; }
+    if (last_successful && gmax <= o->gradient_tolerance) { sum->termination_type = MI_BA_CONVERGENCE; break; }
+    if (radius <= 1e-32) { sum->termination_type = MI_BA_CONVERGENCE; break; }
     ++iteration;
     // scaled Jacobian column norms -> LM diagonal
     if (!reuse_diagonal) {
@@ -1621,10 +2047,6 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
       for (int m = 0; m < 3; ++m) V[pt * 9 + m * 4] += D2[nf + pt * 3 + m];
       if (!Inv3(&V[pt * 9], &Vinv[pt * 9])) ok = false;
     }
-    // S = U - sum W Vinv W^T ; rhs = g_f - sum W Vinv g_e.  Every element
-    // of S is updated in point order; threads own contiguous row ranges of S,
-    // so the arithmetic is that of the serial loop.
-    std::vector<double> Sm = U, rhs(g.begin(), g.begin() + nf);
     std::vector<std::vector<double>> WV(np3);
     if (ok) {
 #pragma omp parallel for schedule(static)
@@ -1638,6 +2060,59 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
             WV[pt][a * 3 + c2] = acc;
           }
       }
+    }
+    std::vector<double> step(n, 0.0);
+    int cg_its = 0;
+    if (use_pcg) {
+      if (ok) {
+        // SCHUR_JACOBI: the diagonal blocks of S = U - sum_p W_p V_p^-1 W_p'
+        // (U carries D_f^2), one per f parameter block, each inverted
+        std::vector<int> blk_of(nf, -1), blk_pos(nf, 0);
+        for (size_t k = 0; k < fblocks.size(); ++k)
+          for (int a = 0; a < fblocks[k].second; ++a) {
+            blk_of[fblocks[k].first + a] = (int)k;
+            blk_pos[fblocks[k].first + a] = a;
+          }
+        std::vector<std::vector<double>> M(fblocks.size()), Minv(fblocks.size());
+        for (size_t k = 0; k < fblocks.size(); ++k) {
+          const int o0 = fblocks[k].first, w = fblocks[k].second;
+          M[k].assign((size_t)w * w, 0.0);
+          for (int a = 0; a < w; ++a)
+            for (int c = 0; c < w; ++c) M[k][(size_t)a * w + c] = U[(size_t)(o0 + a) * nf + o0 + c];
+        }
+        for (int64_t pt = 0; pt < np3; ++pt) {
+          const auto& cols = Wcols[pt];
+          for (size_t a = 0; a < cols.size(); ++a)
+            for (size_t b2 = 0; b2 < cols.size(); ++b2) {
+              const int ka = blk_of[cols[a]];
+              if (ka < 0 || ka != blk_of[cols[b2]]) continue;
+              double acc = 0.0;
+              for (int k = 0; k < 3; ++k) acc += WV[pt][a * 3 + k] * W[pt][b2 * 3 + k];
+              M[ka][(size_t)blk_pos[cols[a]] * fblocks[ka].second + blk_pos[cols[b2]]] -= acc;
+            }
+        }
+        for (size_t k = 0; k < fblocks.size(); ++k) LltInverse(M[k], fblocks[k].second, &Minv[k]);
+        isc.D2 = D2.data();
+        isc.Vinv = Vinv.data();
+        std::vector<double> rhs(nf), xf(nf);
+        isc.Rhs(lin.r.data(), rhs.data());
+        const int term = SchurPcg(isc, fblocks, Minv, rhs.data(), nf, o->eta,
+                                  std::max(1, o->max_linear_solver_iterations), xf.data(), &cg_its);
+        if (term == kCgFailure) {
+          ok = false;
+        } else {
+          for (int i = 0; i < nf; ++i) step[i] = xf[i];
+          isc.BackSubstitute(lin.r.data(), xf.data(), step.data() + nf);
+          for (auto& v : step) v = -v;
+        }
+      }
+    } else {
+    // S = U - sum W Vinv W^T ; rhs = g_f - sum W Vinv g_e.  Every element
+    // of S is updated in point order; threads own contiguous row ranges of S,
+    // so the arithmetic is that of the serial loop.
+    std::vector<double> Sm = U, rhs(g.begin(), g.begin() + nf);
+    cg_its = 1;
+    if (ok) {
 #pragma omp parallel
       {
         const int nt = omp_get_num_threads(), tid = omp_get_thread_num();
@@ -1664,7 +2139,6 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
         }
       }
     }
-    std::vector<double> step(n, 0.0);
     if (ok && nf > 0) ok = Cholesky(Sm, nf);
     if (ok) {
       if (nf > 0) CholSolve(Sm, nf, rhs);
@@ -1684,6 +2158,7 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
       }
       for (auto& v : step) v = -v;  // Ceres solves (J'J+D'D)x = J'f, step = -x
     }
+    }  // exact Schur solve
     reuse_diagonal = true;
     double model_cost_change = 0.0;
     if (ok) {
@@ -1699,10 +2174,17 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
       for (double v : mc) model_cost_change += v;
       ok = model_cost_change > 0.0;
     }
+    sum->num_linear_solver_iterations += cg_its;
     if (!ok) {
       ++consecutive_invalid;
       ++sum->num_unsuccessful_steps;
-      if (consecutive_invalid > o->max_num_consecutive_invalid_steps) { sum->termination_type = MI_BA_FAILURE; break; }
+      last_successful = false;
+      if (consecutive_invalid > o->max_num_consecutive_invalid_steps) {
+        trace(iteration, 0, 0, cg_its, 1);
+        sum->termination_type = MI_BA_FAILURE;
+        break;
+      }
+      trace(iteration, 0, 0, cg_its, 0);
       radius = radius / decrease_factor;
       decrease_factor *= 2.0;
       continue;
@@ -1723,27 +2205,35 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
       if (gsba) std::copy(y0.begin(), y0.end(), gsba->cylinders);
       S.gs.by2p = by2_0;
     };
-    double x_norm2 = 0.0;
-    for (double v : q0) x_norm2 += v * v;
+    S.State(&x_state);
     S.Plus(delta);
+    S.State(&c_state);
     const double candidate_cost = S.Cost();
-    // ParameterToleranceReached / FunctionToleranceReached (tolerance 0 default)
-    double step_norm2 = 0.0;
-    for (int64_t i = 0; i < n; ++i) step_norm2 += delta[i] * delta[i];
+    // ParameterToleranceReached: step_norm = |x - candidate_x| <=
+    // parameter_tolerance (|x| + parameter_tolerance), x the ambient state;
+    // FunctionToleranceReached: |cost change| <= function_tolerance * cost.
+    // Both return before the candidate is accepted (x_ stays).
+    double x_norm2 = 0.0, step_norm2 = 0.0;
+    for (size_t i = 0; i < x_state.size(); ++i) {
+      x_norm2 += x_state[i] * x_state[i];
+      const double d = x_state[i] - c_state[i];
+      step_norm2 += d * d;
+    }
     const double cost_change = x_cost - candidate_cost;
     const double relative_decrease = cost_change / model_cost_change;
     const bool success = relative_decrease > o->min_relative_decrease;
-    // ParameterToleranceReached / FunctionToleranceReached return before the
-    // candidate is accepted (x_ stays).
     if (std::sqrt(step_norm2) <= o->parameter_tolerance * (std::sqrt(x_norm2) + o->parameter_tolerance) ||
         std::fabs(cost_change) <= o->function_tolerance * x_cost) {
       restore();
       sum->termination_type = MI_BA_CONVERGENCE;
       ++sum->num_unsuccessful_steps;
+      trace(iteration, 1, 0, cg_its, 1);
       break;
     }
+    trace(iteration, 1, success ? 1 : 0, cg_its, 0);
     if (success) {
       ++sum->num_successful_steps;
+      last_successful = true;
       x_cost = candidate_cost;
       radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * relative_decrease - 1.0, 3));
       radius = std::min(1e16, radius);
@@ -1753,10 +2243,14 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
       // after the last allowed one (counted as the solver does, which
       // evaluates it there too); saves a full C4 linearization in the
       // one-iteration parity test
-      if (iteration < o->max_num_iterations) S.Linearize(&lin);
+      if (iteration < o->max_num_iterations) {
+        S.Linearize(&lin);
+        gmax = S.GradientMaxNorm(lin);
+      }
       ++sum->num_jacobian_evaluations;
     } else {
       ++sum->num_unsuccessful_steps;
+      last_successful = false;
       restore();
       radius = radius / decrease_factor;
       decrease_factor *= 2.0;

@@ -79,6 +79,8 @@ def load():
     lib.oracle_set_flat_coarse.restype = None
     lib.oracle_set_dense_factor.argtypes = [DENSE_FACTOR_FN]
     lib.oracle_set_dense_factor.restype = None
+    lib.oracle_set_trace.argtypes = [_i32p, C.c_int]
+    lib.oracle_set_trace.restype = None
     _lib = lib
     return lib
 
@@ -363,6 +365,22 @@ def solve(options, scene, semantic=None):
     if st != 0:
         raise RuntimeError(f"oracle_solve status {st}")
     return s
+
+
+def solve_traced(options, scene, semantic=None):
+    """oracle.solve plus the per-iteration LM trace: an int32 array
+    [iterations][4] = (step valid, step successful, linear solver iterations,
+    1 on the iteration that ended the solve), rows of iterations that did not
+    run are -1."""
+    cap = max(1, int(options.max_num_iterations))
+    buf = np.full((cap, 4), -1, np.int32)
+    lib = load()
+    lib.oracle_set_trace(buf.ctypes.data_as(_i32p), cap)
+    try:
+        s = solve(options, scene, semantic)
+    finally:
+        lib.oracle_set_trace(None, 0)
+    return s, buf
 
 
 def reproj_throughput(options, scene, max_blocks, repeats=1, threads=1):

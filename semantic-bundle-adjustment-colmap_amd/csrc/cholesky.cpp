@@ -8,6 +8,9 @@
 #include <algorithm>
 #include <atomic>
 #include <vector>
+#include <array>
+#include <map>
+#include <mutex>
 
 namespace miba {
 
@@ -1409,14 +1412,23 @@ rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, 
 // explicit Tensile solution index (CholConfig::gemm_solution); an index the
 // library does not accept for the shape falls back to the default solution.
 // Whether this rocBLAS build offers Tensile solution `sol` for the update's
-// problem type (rocblas_gemm_ex_get_solutions), asked once per process per
-// index: an index from another rocBLAS build is then never tried again (no
-// failing rocblas_gemm_ex call, or log line, per trailing update).
+// problem (rocblas_gemm_ex_get_solutions), asked once per (device, solution,
+// shape): Tensile's offer depends on the problem size, so an index offered for
+// one trailing-update shape is not assumed for another, and an index from
+// another rocBLAS build is never tried twice for a shape (no failing
+// rocblas_gemm_ex call, or log line, per trailing update).
 static bool gemm_solution_offered(rocblas_handle h, int m, int n, int k, const double* P, int ldp, double* C, int ldc,
                                   int sol) {
-  static std::atomic<long long> cache{0};  // (sol << 2) | 1 offered, | 2 not offered; 0 unknown
-  const long long c = cache.load(std::memory_order_relaxed);
-  if (c != 0 && (c >> 2) == sol) return (c & 3) == 1;
+  static std::mutex mu;
+  static std::map<std::array<long long, 6>, bool> cache;
+  int dev = -1;
+  (void)hipGetDevice(&dev);
+  const std::array<long long, 6> key{dev, sol, m, n, k, (long long)ldp * 1000003LL + ldc};
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
   const double minus_one = -1.0, one = 1.0;
   rocblas_int size = 0;
   bool offered = false;
@@ -1433,7 +1445,8 @@ static bool gemm_solution_offered(rocblas_handle h, int m, int n, int k, const d
                                       &size) == rocblas_status_success)
       offered = std::find(list.begin(), list.begin() + size, sol) != list.begin() + size;
   }
-  cache.store(((long long)sol << 2) | (offered ? 1 : 2), std::memory_order_relaxed);
+  std::lock_guard<std::mutex> g(mu);
+  cache[key] = offered;
   return offered;
 }
 

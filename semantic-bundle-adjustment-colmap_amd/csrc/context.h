@@ -127,6 +127,7 @@ struct mi_ba_context {
   miba::DevArray<double> cg_x, cg_r, cg_z, cg_p, cg_q, cg_w, dX;
   miba::DevArray<double> scalars;          // device scalars
   miba::DevArray<double> red;              // per-workgroup partials of the multi-workgroup reductions
+  miba::DevArray<double> aux;              // [world + 2] gradient max norms: per-rank point part, camera part
   double* host_scalars = nullptr;          // pinned
 
   // explicit reduced camera system (exact Schur solve, rocSOLVER Cholesky)

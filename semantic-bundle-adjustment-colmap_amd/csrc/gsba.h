@@ -78,6 +78,12 @@ void gsba_model_cost(mi_ba_context* ctx, const double* df, double* d_out);
 // candidate cylinders from the step df (QuaternionManifold, radius >= 0)
 void gsba_plus(mi_ba_context* ctx, const double* df);
 void gsba_accept(mi_ba_context* ctx);
+// gradient tolerance: g += J'r of every block; |y - Plus(y, -g)|_inf of the
+// cylinders max-ed into *out (bit pattern, atomicMax)
+void gsba_add_gradient(mi_ba_context* ctx, double* g);
+void gsba_grad_max(mi_ba_context* ctx, const double* g, double* out);
+// parameter tolerance: |y|^2, |y - y_c|^2 of the cylinders added into out[0..1]
+void gsba_state_norms(mi_ba_context* ctx, double* out);
 mi_ba_status gsba_writeback(mi_ba_context* ctx);
 // every block's residual (1 - IoU) and ambient Jacobian [16] (mi_ba_gsba_evaluate)
 mi_ba_status gsba_download(mi_ba_context* ctx, int32_t* ids, double* residuals, double* jacobians);

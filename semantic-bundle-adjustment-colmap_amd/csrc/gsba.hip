@@ -722,6 +722,76 @@ __global__ void gsba_plus_by2_kernel(int ncyl, const double* __restrict__ cyl, c
   o[8] = 0.0;
 }
 
+// g += J'r over the block's slots (the raw gradient of the gradient
+// tolerance test).
+__global__ void gsba_gradient_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
+                                     const uint32_t* __restrict__ img_flags, const double* __restrict__ r,
+                                     const double* __restrict__ J, int64_t cyl0, int cyl_var, int cw,
+                                     double* __restrict__ g) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= nblocks) return;
+  const GsbaBlock b = blocks[k];
+  const double* Jr = J + 14 * (size_t)k;
+  const uint32_t pv = img_flags[b.img] & 1u;
+  for (int m = 0; m < 14; ++m) {
+    const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv, cw);
+    if (s >= 0) atomicAdd(g + s, Jr[m] * r[k]);
+  }
+}
+
+__device__ inline void gsba_atomic_max(double* out, double v) {
+  if (v > 0.0) atomicMax(reinterpret_cast<unsigned long long*>(out), (unsigned long long)__double_as_longlong(v));
+}
+
+// |y - Plus(y, -g)|_inf of every cylinder (qvec on the QuaternionManifold,
+// the radius projected onto its bound 0; by two points Euclidean + radius).
+__global__ void gsba_grad_max_kernel(int ncyl, int by2, const double* __restrict__ cyl, const double* __restrict__ g,
+                                     double* out) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= ncyl) return;
+  const double* y = cyl + 9 * (size_t)k;
+  double mx = 0.0;
+  if (by2) {
+    const double* gc = g + 7 * (size_t)k;
+    for (int m = 0; m < 6; ++m) mx = fmax(mx, fabs(y[m] - (y[m] + -gc[m])));
+    mx = fmax(mx, fabs(y[6] - fmax(y[6] + -gc[6], 0.0)));
+  } else {
+    const double* gc = g + 8 * (size_t)k;
+    const double q[4] = {y[0], y[1], y[2], y[3]};
+    const double d[3] = {-gc[0], -gc[1], -gc[2]};
+    double qn[4];
+    quat_plus(q, d, qn);
+    for (int m = 0; m < 4; ++m) mx = fmax(mx, fabs(q[m] - qn[m]));
+    for (int m = 0; m < 3; ++m) mx = fmax(mx, fabs(y[4 + m] - (y[4 + m] + -gc[3 + m])));
+    mx = fmax(mx, fabs(y[7] - fmax(y[7] + -gc[6], 0.0)));
+    mx = fmax(mx, fabs(y[8] - (y[8] + -gc[7])));
+  }
+  gsba_atomic_max(out, mx);
+}
+
+// |y|^2 and |y - y_c|^2 of the cylinders' ambient coordinates into out[0..1].
+__global__ void gsba_state_kernel(int ncyl, int by2, const double* __restrict__ cyl, const double* __restrict__ cyl_c,
+                                  double* out) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  double vx = 0.0, vd = 0.0;
+  if (k < ncyl) {
+    const int n = by2 ? 7 : 9;
+    for (int m = 0; m < n; ++m) {
+      const double a = cyl[9 * (size_t)k + m], d = a - cyl_c[9 * (size_t)k + m];
+      vx += a * a;
+      vd += d * d;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    vx += __shfl_xor(vx, off, 64);
+    vd += __shfl_xor(vd, off, 64);
+  }
+  if (threadIdx.x == 0) {
+    atomicAdd(out, vx);
+    atomicAdd(out + 1, vd);
+  }
+}
+
 GsbaArgs make_args(mi_ba_context* ctx, const double* qt, const double* cyl) {
   GsbaState* G = ctx->gsba;
   GsbaArgs a;
@@ -1008,6 +1078,27 @@ void gsba_plus(mi_ba_context* ctx, const double* df) {
   else
     hipLaunchKernelGGL(gsba_plus_kernel, dim3(grid64(G->ncyl)), dim3(64), 0, ctx->stream, G->ncyl, G->cyl.ptr,
                        df + ctx->dev.cyl0, G->cyl_c.ptr);
+}
+
+void gsba_add_gradient(mi_ba_context* ctx, double* g) {
+  GsbaState* G = ctx->gsba;
+  if (!G->nblocks) return;
+  hipLaunchKernelGGL(gsba_gradient_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, ctx->stream, G->blocks.ptr,
+                     G->nblocks, ctx->dev.img_flags, G->r.ptr, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw, g);
+}
+
+void gsba_grad_max(mi_ba_context* ctx, const double* g, double* out) {
+  GsbaState* G = ctx->gsba;
+  if (!ctx->dev.cyl_var || G->ncyl == 0) return;
+  hipLaunchKernelGGL(gsba_grad_max_kernel, dim3(grid64(G->ncyl)), dim3(64), 0, ctx->stream, G->ncyl, G->by2 ? 1 : 0,
+                     G->cyl.ptr, g + ctx->dev.cyl0, out);
+}
+
+void gsba_state_norms(mi_ba_context* ctx, double* out) {
+  GsbaState* G = ctx->gsba;
+  if (!ctx->dev.cyl_var || G->ncyl == 0) return;
+  hipLaunchKernelGGL(gsba_state_kernel, dim3(grid64(G->ncyl)), dim3(64), 0, ctx->stream, G->ncyl, G->by2 ? 1 : 0,
+                     G->cyl.ptr, G->cyl_c.ptr, out);
 }
 
 void gsba_accept(mi_ba_context* ctx) {

@@ -160,4 +160,27 @@ constexpr int kReduceBlocks = 256;
 void launch_sqnorm2(const double* a, int64_t na, const double* b, int64_t nb, double* out, double* scratch,
                     hipStream_t s);
 
+// One CG step x += alpha p (and r -= alpha q when update_r), alpha = rho /
+// pq, skipped where Ceres' ConjugateGradientsSolver stops before moving x
+// (rho or beta = rho / rho_prev 0 / inf, pq <= 0 / inf, alpha inf; rho_prev
+// nullable on the first iteration).
+void launch_cg_step(double* x, const double* p, double* r, const double* q, const double* rho,
+                    const double* rho_prev, const double* pq, bool update_r, int64_t n, hipStream_t s);
+
+// Gradient tolerance (TrustRegionMinimizer::EvaluateGradientAndJacobian):
+// g += sum J_f' r over the camera-major tiles (raw tangent gradient of the
+// image / camera slots); |x - Plus(x, -g)|_inf of the image and camera
+// blocks, and of the variable points (g_p from Vg), atomically max-ed into
+// out[0] (non-negative doubles, as bit patterns).
+void launch_grad_f(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm, const double2* r,
+                   const double* J, double* g, hipStream_t s);
+void launch_grad_max_f(const DevProblem& p, const double* g, double* out, hipStream_t s);
+void launch_grad_max_points(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg, double* out,
+                            hipStream_t s);
+// Ceres' ambient state norms for ParameterToleranceReached: out[0] = |x|^2,
+// out[1] = |x - x_c|^2 over the variable image / camera blocks (when with_f)
+// and variable points; scratch: kReduceBlocks doubles.
+void launch_state_norms(const DevProblem& p, const double* qt_c, const double* cam_c, const double* X_c, bool with_f,
+                        double* out, double* scratch, hipStream_t s);
+
 }  // namespace miba

@@ -1415,7 +1415,17 @@ __device__ inline void chol_inverse(double (&A)[N][N], double (&Ainv)[N][N]) {
     }
 }
 
-template <int N>
+// Parameter block of tangent slot a within an N-wide finalize block (the
+// SCHUR_JACOBI preconditioner has one diagonal block per Ceres parameter
+// block, SchurJacobiPreconditioner): KIND 0 one block (camera intrinsics),
+// 1 an image's qvec (3) | tvec (3), 2 a cylinder's qvec (3) | tvec (3) |
+// radius | height (by two points: tvec_1 (3) | tvec_2 (3) | radius).
+template <int KIND>
+__device__ constexpr int param_group(int a) {
+  return KIND == 0 ? 0 : KIND == 1 ? (a < 3 ? 0 : 1) : (a < 3 ? 0 : a < 6 ? 1 : a);
+}
+
+template <int N, int KIND = 0>
 __device__ void finalize_block(const double* __restrict__ blk, const double* __restrict__ udiag,
                                double* __restrict__ scale_f, double* __restrict__ diag_f,
                                double* __restrict__ lambda_f, double* __restrict__ prec, double* __restrict__ b,
@@ -1426,7 +1436,8 @@ __device__ void finalize_block(const double* __restrict__ blk, const double* __r
   for (int a = 0; a < N; ++a)
 #pragma unroll
     for (int c = a; c < N; ++c, ++o) {
-      A[a][c] = var ? blk[o] : 0.0;
+      // the preconditioner keeps the diagonal blocks of the parameter blocks
+      A[a][c] = var && param_group<KIND>(a) == param_group<KIND>(c) ? blk[o] : 0.0;
       A[c][a] = A[a][c];
     }
 #pragma unroll
@@ -1481,8 +1492,8 @@ __global__ __launch_bounds__(64) void fblock_finalize_kernel(DevProblem p, const
   if (k < I) {
     const bool var = p.img_flags[k] & 1u;
     const size_t o = 6 * (size_t)k;
-    finalize_block<6>(pose_blk + (size_t)k * kSymPose, udiag + o, scale_f + o, diag_f + o, lambda_f + o,
-                      prec_pose + 36 * (size_t)k, b + o, var, first, reuse_diag, radius);
+    finalize_block<6, 1>(pose_blk + (size_t)k * kSymPose, udiag + o, scale_f + o, diag_f + o, lambda_f + o,
+                         prec_pose + 36 * (size_t)k, b + o, var, first, reuse_diag, radius);
   } else if (CT > 0 && k < I + C) {
     const int c = k - I;
     const bool var = p.cam_var[c] != 0;
@@ -1504,8 +1515,8 @@ __global__ __launch_bounds__(64) void finalize_n_kernel(int n, const double* __r
   const int k = blockIdx.x * 64 + threadIdx.x;
   if (k >= n) return;
   const size_t o = N * (size_t)k;
-  finalize_block<N>(blk + (N * (N + 1) / 2) * (size_t)k, udiag + o, scale_f + o, diag_f + o, lambda_f + o,
-                    prec + N * N * (size_t)k, b + o, var != 0, first, reuse_diag, radius);
+  finalize_block<N, 2>(blk + (N * (N + 1) / 2) * (size_t)k, udiag + o, scale_f + o, diag_f + o, lambda_f + o,
+                       prec + N * N * (size_t)k, b + o, var != 0, first, reuse_diag, radius);
 }
 
 template <int N>
@@ -2036,6 +2047,178 @@ __global__ void xpby_kernel(double* __restrict__ pv, const double* __restrict__ 
                             const double* den, int64_t n) {
   const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (k < n) pv[k] = z[k] + (num[0] / den[0]) * pv[k];
+}
+
+// The CG step of ConjugateGradientsSolver (Ceres 2.1, restated): alpha =
+// rho / pq, x += alpha p and (update_r) r -= alpha q — taken only when the
+// iteration gets that far in Ceres: rho (and beta = rho / rho_prev, when
+// given) neither 0 nor inf, pq > 0 and finite, alpha finite.  Otherwise x
+// and r stay, and the host (which reads the same scalars) ends the solve
+// with FAILURE or NO_CONVERGENCE.
+__device__ inline bool cg_zero_or_inf(double v) { return v == 0.0 || isinf(v) || isnan(v); }
+__global__ void cg_step_kernel(double* __restrict__ x, const double* __restrict__ pv, double* __restrict__ r,
+                               const double* __restrict__ q, const double* rho, const double* rho_prev,
+                               const double* pq, int update_r, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= n) return;
+  const double rh = rho[0], d = pq[0];
+  if (cg_zero_or_inf(rh) || (rho_prev && cg_zero_or_inf(rh / rho_prev[0]))) return;
+  if (!(d > 0.0) || isinf(d)) return;
+  const double alpha = rh / d;
+  if (isinf(alpha)) return;
+  x[k] = x[k] + alpha * pv[k];
+  if (update_r) r[k] = r[k] - alpha * q[k];
+}
+
+// Raw camera-side gradient g_f += sum J_f' r (tangent, unscaled) of every
+// reduced block over the image-aligned camera-major tiles, one atomic flush
+// per tile (the gradient tolerance test: TrustRegionMinimizer::
+// EvaluateGradientAndJacobian).
+template <int CT>
+__global__ __launch_bounds__(kBlock) void grad_f_kernel(DevProblem p, const DevTile* __restrict__ tiles,
+                                                         const uint32_t* __restrict__ cm_perm,
+                                                         const double2* __restrict__ rr,
+                                                         const double* __restrict__ J, double* __restrict__ g) {
+  constexpr int F = 6 + CT, W = 9 + CT;
+  __shared__ double sred[4 * F];
+  const DevTile tile = tiles[blockIdx.x];
+  double acc[F];
+#pragma unroll
+  for (int m = 0; m < F; ++m) acc[m] = 0.0;
+  for (uint32_t k = threadIdx.x; k < tile.count; k += kBlock) {
+    const uint32_t b = cm_perm[tile.start + k];
+    const double* Jb = J + (size_t)b * 2 * W;
+    const double2 r = rr[b];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) acc[m] += Jb[m] * r.x + Jb[W + m] * r.y;
+#pragma unroll
+    for (int m = 0; m < CT; ++m) acc[6 + m] += Jb[9 + m] * r.x + Jb[W + 9 + m] * r.y;
+  }
+  block_reduce<F>(acc, sred);
+  const int k = threadIdx.x;
+  if (k >= F) return;
+  const uint32_t img = tile.image, cam = p.img_cam[img];
+  if (k < 6 ? !(p.img_flags[img] & 1u) : !p.cam_var[cam]) return;
+  atomicAdd(g + fslot(p, img, cam, k), sred[k]);
+}
+
+__device__ inline void atomic_max_nonneg(double* out, double v) {
+  atomicMax(reinterpret_cast<unsigned long long*>(out), (unsigned long long)__double_as_longlong(v));
+}
+
+// |x - Plus(x, -g)|_inf over the image and camera blocks (qvec on the
+// QuaternionManifold, tvec / intrinsics under their SubsetManifolds) into
+// out[0] (as the bit pattern of a non-negative double: atomicMax).
+__global__ void grad_max_f_kernel(DevProblem p, const double* __restrict__ g, double* out) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  double mx = 0.0;
+  if (k < p.num_images) {
+    const uint32_t fl = p.img_flags[k];
+    if (fl & 1u) {
+      const double* a = p.qt + 8 * (size_t)k;
+      const double* gk = g + 6 * (size_t)k;
+      const double q[4] = {a[0], a[1], a[2], a[3]};
+      const double d[3] = {-gk[0], -gk[1], -gk[2]};
+      double qn[4];
+      quat_plus(q, d, qn);
+      for (int m = 0; m < 4; ++m) mx = fmax(mx, fabs(q[m] - qn[m]));
+      for (int m = 0; m < 3; ++m)
+        if (!((fl >> (1 + m)) & 1u)) mx = fmax(mx, fabs(a[4 + m] - (a[4 + m] + -gk[3 + m])));
+    }
+  } else if (k < p.num_images + p.num_cameras) {
+    const int c = k - p.num_images;
+    if (p.cam_var[c]) {
+      const double* a = p.cam + 8 * (size_t)c;
+      const double* gc = g + 6 * (size_t)p.num_images + (size_t)p.ct * c;
+      const unsigned cm = cam_tangent_mask(p.cam_model[c], p.refine_mask);
+      int t = 0;
+      for (int m = 0; m < 8; ++m)
+        if ((cm >> m) & 1u) {
+          mx = fmax(mx, fabs(a[m] - (a[m] + -gc[t])));
+          ++t;
+        }
+    }
+  } else {
+    return;
+  }
+  if (mx > 0.0) atomic_max_nonneg(out, mx);
+}
+
+// The same over the variable points (g_p from the point blocks Vg).
+__global__ void grad_max_points_kernel(DevProblem p, const DevPoint* __restrict__ vp, int64_t npv,
+                                       const double* __restrict__ Vg, double* out) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double mx = 0.0;
+  if (k < npv) {
+    const uint32_t pt = vp[k].point;
+    const double* gp = Vg + 9 * (size_t)pt + 6;
+    const double* X = p.X + 3 * (size_t)pt;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) mx = fmax(mx, fabs(X[m] - (X[m] + -gp[m])));
+  }
+  // one atomic per wave
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
+  if ((threadIdx.x & 63) == 0 && mx > 0.0) atomic_max_nonneg(out, mx);
+}
+
+// Ceres' state vector over the variable blocks, ambient coordinates: |x|^2
+// and |x - x_c|^2 (ParameterToleranceReached's x_norm and step_norm).  Images
+// and cameras counted when with_f (rank 0 of a multi-rank solve), points
+// always (each rank its own).  Per-workgroup partials: out[b] (|x|^2) and
+// out[gridDim.x + b] (|x - x_c|^2), summed in a fixed order afterwards.
+__global__ __launch_bounds__(1024) void state_norms_kernel(DevProblem p, const double* __restrict__ qt_c,
+                                                           const double* __restrict__ cam_c,
+                                                           const double* __restrict__ X_c, int with_f,
+                                                           double* __restrict__ out) {
+  __shared__ double sred[2][16];
+  double vx = 0.0, vd = 0.0;
+  const int64_t nf_items = with_f ? (int64_t)p.num_images + p.num_cameras : 0;
+  const int64_t n = nf_items + p.num_points;
+  const int64_t stride = (int64_t)gridDim.x * 1024;
+  for (int64_t k = (int64_t)blockIdx.x * 1024 + threadIdx.x; k < n; k += stride) {
+    const double* a = nullptr;
+    const double* b = nullptr;
+    int cnt = 0;
+    if (k < p.num_images && with_f) {
+      if (p.img_flags[k] & 1u) {
+        a = p.qt + 8 * k;
+        b = qt_c + 8 * k;
+        cnt = 7;
+      }
+    } else if (k < nf_items) {
+      const int64_t c = k - p.num_images;
+      if (p.cam_var[c]) {
+        a = p.cam + 8 * c;
+        b = cam_c + 8 * c;
+        cnt = num_params(p.cam_model[c]);
+      }
+    } else {
+      const int64_t q = k - nf_items;
+      if (p.pt_var[q]) {
+        a = p.X + 3 * q;
+        b = X_c + 3 * q;
+        cnt = 3;
+      }
+    }
+    for (int m = 0; m < cnt; ++m) {
+      const double d = a[m] - b[m];
+      vx += a[m] * a[m];
+      vd += d * d;
+    }
+  }
+  vx = wave_sum(vx);
+  vd = wave_sum(vd);
+  if ((threadIdx.x & 63) == 0) {
+    sred[0][threadIdx.x >> 6] = vx;
+    sred[1][threadIdx.x >> 6] = vd;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double s = 0.0;
+    for (int k = 0; k < 16; ++k) s += sred[threadIdx.x][k];
+    out[threadIdx.x * gridDim.x + blockIdx.x] = s;
+  }
 }
 
 template <int CT>
@@ -3393,6 +3576,42 @@ void launch_sqnorm2(const double* a, int64_t na, const double* b, int64_t nb2, d
   const unsigned g = (unsigned)std::min<int64_t>(kReduceBlocks, (n + 4095) / 4096);
   hipLaunchKernelGGL(sqnorm2_kernel, dim3(g), dim3(1024), 0, s, a, na, b, nb2, scratch);
   hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, s, scratch, (int64_t)g, out);
+}
+
+void launch_cg_step(double* x, const double* pv, double* r, const double* q, const double* rho,
+                    const double* rho_prev, const double* pq, bool update_r, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(cg_step_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, x, pv, r, q, rho, rho_prev, pq,
+                     update_r ? 1 : 0, n);
+}
+
+void launch_grad_f(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm, const double2* r,
+                   const double* J, double* g, hipStream_t s) {
+  if (ntiles == 0) return;
+  dispatch_ct(p.ct, [&](auto c) {
+    constexpr int CT = decltype(c)::value;
+    hipLaunchKernelGGL(grad_f_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, g);
+  });
+}
+
+void launch_grad_max_f(const DevProblem& p, const double* g, double* out, hipStream_t s) {
+  const int n = p.num_images + p.num_cameras;
+  if (n > 0) hipLaunchKernelGGL(grad_max_f_kernel, dim3(grid_for(n, 64)), dim3(64), 0, s, p, g, out);
+}
+
+void launch_grad_max_points(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg, double* out,
+                            hipStream_t s) {
+  if (npv > 0)
+    hipLaunchKernelGGL(grad_max_points_kernel, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, Vg, out);
+}
+
+void launch_state_norms(const DevProblem& p, const double* qt_c, const double* cam_c, const double* X_c, bool with_f,
+                        double* out, double* scratch, hipStream_t s) {
+  const int64_t n = (with_f ? (int64_t)p.num_images + p.num_cameras : 0) + p.num_points;
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(kReduceBlocks / 2, (n + 4095) / 4096));
+  hipLaunchKernelGGL(state_norms_kernel, dim3(g), dim3(1024), 0, s, p, qt_c, cam_c, X_c, with_f ? 1 : 0, scratch);
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, s, scratch, (int64_t)g, out);
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, s, scratch + g, (int64_t)g, out + 1);
 }
 
 }  // namespace miba

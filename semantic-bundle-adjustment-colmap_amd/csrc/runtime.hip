@@ -1029,22 +1029,30 @@ mi_ba_status schur_product(mi_ba_context* ctx, const double* x, double* y) {
   return allreduce(ctx, y, d.nf);
 }
 
-// Preconditioned CG on the Schur complement, Ceres ConjugateGradientsSolver
-// semantics (restated): q-termination with tolerance eta, r_tolerance off,
-// residual recomputed every 10 iterations, stop on rho = 0/inf or pq <= 0.
-mi_ba_status pcg(mi_ba_context* ctx, int* iterations) {
+// Preconditioned CG on the Schur complement, Ceres 2.1
+// ConjugateGradientsSolver semantics (restated): x = 0, r = b; q-termination
+// i (Q1 - Q0) / Q1 < eta with Q = -x'(b + r); r_tolerance off
+// (LevenbergMarquardtStrategy passes -1); residual recomputed every 10
+// iterations; FAILURE on rho or beta = rho / rho_prev 0 / inf or alpha inf
+// (*failed: an invalid LM step, TrustRegionMinimizer::ComputeTrustRegionStep),
+// NO_CONVERGENCE on pq <= 0 / inf or the iteration cap (the step is used).
+// Where Ceres stops before x moves, the device step (launch_cg_step) leaves x
+// and r as they are.  One host round trip per iteration (the scalars).
+mi_ba_status pcg(mi_ba_context* ctx, int* iterations, bool* failed) {
   const DevProblem& d = ctx->dev;
   hipStream_t s = ctx->stream;
   const int64_t nf = d.nf;
   double* sc = ctx->scalars.ptr;
   double* hs = ctx->host_scalars;
+  *failed = false;
   MI_HIP(hipMemsetAsync(ctx->cg_x.ptr, 0, nf * 8, s));
   MI_HIP(hipMemcpyAsync(ctx->cg_r.ptr, ctx->bvec.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
   launch_dot(ctx->bvec.ptr, ctx->bvec.ptr, nf, sc + kXB, s);
   mi_ba_status st = read_scalars(ctx, kXB, 1);
   if (st != MI_BA_OK) return st;
   *iterations = 0;
-  if (hs[kXB] == 0.0) return MI_BA_OK;
+  if (hs[kXB] == 0.0) return MI_BA_OK;  // "Convergence. |b| = 0."
+  auto zero_or_inf = [](double v) { return v == 0.0 || std::isinf(v) || std::isnan(v); };
   double Q0 = 0.0;
   const int max_it = std::max(1, ctx->options.max_linear_solver_iterations);
   for (int it = 1; it <= max_it; ++it) {
@@ -1060,9 +1068,10 @@ mi_ba_status pcg(mi_ba_context* ctx, int* iterations) {
     st = schur_product(ctx, ctx->cg_p.ptr, ctx->cg_q.ptr);
     if (st != MI_BA_OK) return st;
     launch_dot(ctx->cg_p.ptr, ctx->cg_q.ptr, nf, sc + kPQ, s);
-    launch_axpy(ctx->cg_x.ptr, ctx->cg_p.ptr, sc + kRho, sc + kPQ, 1.0, nf, s);
+    const double* rho_prev = it > 1 ? sc + kRhoPrev : nullptr;
     if (it % 10 == 0) {
-      // r = b - S x
+      // x += alpha p, then r = b - S x
+      launch_cg_step(ctx->cg_x.ptr, ctx->cg_p.ptr, nullptr, nullptr, sc + kRho, rho_prev, sc + kPQ, false, nf, s);
       st = schur_product(ctx, ctx->cg_x.ptr, ctx->cg_q.ptr);
       if (st != MI_BA_OK) return st;
       MI_HIP(hipMemcpyAsync(ctx->cg_r.ptr, ctx->bvec.ptr, nf * 8, hipMemcpyDeviceToDevice, s));
@@ -1071,7 +1080,8 @@ mi_ba_status pcg(mi_ba_context* ctx, int* iterations) {
       MI_HIP(hipMemcpyAsync(sc + kStepNorm, &one, 8, hipMemcpyHostToDevice, s));
       launch_axpy(ctx->cg_r.ptr, ctx->cg_q.ptr, sc + kStepNorm, sc + kStepNorm, -1.0, nf, s);
     } else {
-      launch_axpy(ctx->cg_r.ptr, ctx->cg_q.ptr, sc + kRho, sc + kPQ, -1.0, nf, s);
+      launch_cg_step(ctx->cg_x.ptr, ctx->cg_p.ptr, ctx->cg_r.ptr, ctx->cg_q.ptr, sc + kRho, rho_prev, sc + kPQ, true,
+                     nf, s);
     }
     launch_dot(ctx->cg_x.ptr, ctx->bvec.ptr, nf, sc + kXB, s);
     launch_dot(ctx->cg_x.ptr, ctx->cg_r.ptr, nf, sc + kXR, s);
@@ -1079,13 +1089,65 @@ mi_ba_status pcg(mi_ba_context* ctx, int* iterations) {
     if (st != MI_BA_OK) return st;
     *iterations = it;
     const double rho = hs[kRho], pq = hs[kPQ];
-    if (rho == 0.0 || !std::isfinite(rho)) break;
-    if (!(pq > 0.0) || !std::isfinite(pq)) break;
-    const double Q1 = -1.0 * (hs[kXB] + hs[kXR]) / 2.0;
+    if (zero_or_inf(rho) || (it > 1 && zero_or_inf(rho / hs[kRhoPrev]))) {
+      *failed = true;  // LINEAR_SOLVER_FAILURE: rho or beta 0 / inf
+      break;
+    }
+    if (!(pq > 0.0) || std::isinf(pq)) break;  // NO_CONVERGENCE, x as it was
+    if (std::isinf(rho / pq)) {
+      *failed = true;  // alpha inf
+      break;
+    }
+    const double Q1 = -1.0 * (hs[kXB] + hs[kXR]);
     const double zeta = it * (Q1 - Q0) / Q1;
     if (zeta < ctx->options.eta) break;
     Q0 = Q1;
   }
+  return MI_BA_OK;
+}
+
+// Ceres' GradientToleranceReached at the current point (its Jacobian and the
+// point blocks Vg current): |x - Plus(x, -g)|_inf <= gradient_tolerance with
+// g = J'f, the raw tangent gradient (TrustRegionMinimizer::
+// EvaluateGradientAndJacobian).  The variable points' part comes from Vg
+// (one read of the point blocks); the image / camera / cylinder part needs a
+// pass over the camera-side rows and is evaluated only when the point part
+// alone does not already exceed the tolerance.  Multi-rank: each rank's
+// point part goes into its own slot of a world-long vector (one sum), the
+// camera-side gradient is summed like b.
+mi_ba_status gradient_reached(mi_ba_context* ctx, bool* reached) {
+  const DevProblem& d = ctx->dev;
+  hipStream_t s = ctx->stream;
+  const double tol = ctx->options.gradient_tolerance;
+  const int nw = ctx->world;
+  *reached = false;
+  if (ctx->aux.n < (size_t)nw + 2 && ctx->aux.alloc(nw + 2) != hipSuccess) return MI_BA_ERR_OUT_OF_MEMORY;
+  double* aux = ctx->aux.ptr;
+  MI_HIP(hipMemsetAsync(aux, 0, (nw + 2) * 8, s));
+  launch_grad_max_points(d, ctx->vpoints.ptr, ctx->npv, ctx->Vg.ptr, aux + ctx->rank, s);
+  mi_ba_status st = allreduce(ctx, aux, nw);
+  if (st != MI_BA_OK) return st;
+  std::vector<double> h(nw + 2, 0.0);
+  MI_HIP(hipMemcpyAsync(h.data(), aux, nw * 8, hipMemcpyDeviceToHost, s));
+  MI_HIP(hipStreamSynchronize(s));
+  double gmax = 0.0;
+  for (int k = 0; k < nw; ++k) gmax = std::max(gmax, h[k]);
+  if (gmax > tol) return MI_BA_OK;
+  // camera side: g_f = sum J_f' r (+ semantic pairs, GSBA blocks) into cg_z
+  // (PCG scratch, free between solves)
+  double* g = ctx->cg_z.ptr;
+  MI_HIP(hipMemsetAsync(g, 0, d.nf * 8, s));
+  launch_grad_f(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, g, s);
+  if (ctx->sem) semantic_add_gradient(ctx, g);
+  if (ctx->gsba) gsba_add_gradient(ctx, g);
+  st = allreduce(ctx, g, d.nf);
+  if (st != MI_BA_OK) return st;
+  launch_grad_max_f(d, g, aux + nw, s);
+  if (ctx->gsba) gsba_grad_max(ctx, g, aux + nw);
+  MI_HIP(hipMemcpyAsync(h.data() + nw, aux + nw, 8, hipMemcpyDeviceToHost, s));
+  MI_HIP(hipStreamSynchronize(s));
+  gmax = std::max(gmax, h[nw]);
+  *reached = gmax <= tol;
   return MI_BA_OK;
 }
 
@@ -1265,7 +1327,6 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
   bool reuse_diag = false, first = true;
   int consecutive_invalid = 0, iteration = 0;
   sum->termination_type = MI_BA_NO_CONVERGENCE;
-  const int64_t nf = d.nf;
   // the finished iteration handed to the callbacks (iteration 0: the initial
   // evaluation, valid and successful as in Ceres' IterationZero)
   mi_ba_iteration_summary its{};
@@ -1273,6 +1334,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
   its.step_is_successful = 1;
   double t_iter = t_start;
   const bool callbacks = o.iteration_callback || o.stop_flag || ctx->distributed();
+  bool last_successful = true;  // iteration 0 counts as successful (IterationZero)
   while (true) {
     if (callbacks) {
       its.iteration = iteration;
@@ -1286,8 +1348,18 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       if (decision == MI_BA_SOLVER_TERMINATE_SUCCESSFULLY) { sum->termination_type = MI_BA_USER_SUCCESS; break; }
       if (decision == MI_BA_SOLVER_ABORT) { sum->termination_type = MI_BA_USER_FAILURE; break; }
     }
+    // FinalizeIterationAndCheckIfMinimizerCanContinue: the iteration cap,
+    // the gradient tolerance (after a successful step or at iteration 0; with
+    // the default tolerance 0 only an exactly zero gradient stops), the
+    // minimum trust-region radius (1e-32)
     if (iteration >= o.max_num_iterations) { sum->termination_type = MI_BA_NO_CONVERGENCE; break; }
-    if (radius < 1e-32) { sum->termination_type = MI_BA_CONVERGENCE; break; }
+    if (last_successful) {
+      bool reached = false;
+      st = gradient_reached(ctx, &reached);
+      if (st != MI_BA_OK) return st;
+      if (reached) { sum->termination_type = MI_BA_CONVERGENCE; break; }
+    }
+    if (radius <= 1e-32) { sum->termination_type = MI_BA_CONVERGENCE; break; }
     ++iteration;
     t_iter = now_s();
     its = mi_ba_iteration_summary{};
@@ -1365,13 +1437,16 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     } else {
       hipEvent_t pstop;
       timer_begin(ctx, "pcg", &pstop);
-      st = pcg(ctx, &cg_it);
+      bool failed = false;
+      st = pcg(ctx, &cg_it, &failed);
+      solved_ok = !failed;
       timer_end(ctx, pstop);
     }
     if (st != MI_BA_OK) return st;
     sum->num_linear_solver_iterations += cg_it;
     its.linear_solver_iterations = cg_it;
     if (!solved_ok) {
+      last_successful = false;
       ++consecutive_invalid;
       ++sum->num_unsuccessful_steps;
       if (consecutive_invalid > o.max_num_consecutive_invalid_steps) {
@@ -1395,13 +1470,9 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     if (d.nb) launch_sum(ctx->partial.ptr, nmodel, sc + kModelCost, s, ctx->sum_ws.ptr);
     if (ctx->sem) semantic_model_cost(ctx, ctx->cg_x.ptr, sc + kSemModel);
     if (ctx->gsba) gsba_model_cost(ctx, ctx->cg_x.ptr, sc + kGsModel);
-    // camera step counted once (rank 0), point steps on their own ranks
-    launch_sqnorm2(ctx->cg_x.ptr, ctx->rank == 0 ? nf : 0, ctx->dX.ptr, 3 * d.num_points, sc + kStepNorm,
-                   ctx->red.ptr, s);
     if (ctx->distributed()) {
       st = allreduce(ctx, sc + kModelCost, 1);
       if (st == MI_BA_OK) st = allreduce(ctx, sc + kSemModel, 1);
-      if (st == MI_BA_OK) st = allreduce(ctx, sc + kStepNorm, 1);
       if (st != MI_BA_OK) return st;
     }
     st = read_scalars(ctx, 0, kNumScalars);
@@ -1409,6 +1480,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     const double model_cost_change = hs[kModelCost] + hs[kSemModel] + hs[kGsModel];
     const bool valid = std::isfinite(model_cost_change) && model_cost_change > 0.0;
     if (!valid) {
+      last_successful = false;
       ++consecutive_invalid;
       ++sum->num_unsuccessful_steps;
       if (consecutive_invalid > o.max_num_consecutive_invalid_steps) {
@@ -1420,9 +1492,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       continue;
     }
     consecutive_invalid = 0;
-    const double step_norm = std::sqrt(hs[kStepNorm]);
     its.step_is_valid = 1;
-    its.step_norm = step_norm;
     // candidate
     launch_plus(d, ctx->cg_x.ptr, ctx->dX.ptr, ctx->qt.ptr, ctx->cam.ptr, ctx->X.ptr, ctx->qt_c.ptr,
                 ctx->cam_c.ptr, ctx->X_c.ptr, s);
@@ -1437,9 +1507,15 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     if (d.nb) launch_sum(ctx->partial.ptr, reproj_grid(d.nb), sc + kCandCost, s, ctx->sum_ws.ptr);
     if (ctx->sem) semantic_cost(ctx, ctx->qt_c.ptr, ctx->cam_c.ptr, sc + kSemCand);
     if (ctx->gsba) gsba_cost(ctx, ctx->qt_c.ptr, ctx->gsba->cyl_c.ptr, sc + kGsCand);
+    // Ceres' |x|^2 and |x - candidate_x|^2 over the variable blocks, ambient
+    // coordinates (kXB, kXR: PCG scratch, free here); images, cameras and
+    // cylinders counted on rank 0, points on their own ranks
+    launch_state_norms(d, ctx->qt_c.ptr, ctx->cam_c.ptr, ctx->X_c.ptr, ctx->rank == 0, sc + kXB, ctx->red.ptr, s);
+    if (ctx->gsba && ctx->rank == 0) gsba_state_norms(ctx, sc + kXB);
     if (ctx->distributed()) {
       st = allreduce(ctx, sc + kCandCost, 1);
       if (st == MI_BA_OK) st = allreduce(ctx, sc + kSemCand, 1);
+      if (st == MI_BA_OK) st = allreduce(ctx, sc + kXB, 2);
       if (st != MI_BA_OK) return st;
     }
     st = read_scalars(ctx, 0, kNumScalars);
@@ -1448,18 +1524,13 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     const double cost_change = x_cost - candidate_cost;
     const double relative_decrease = cost_change / model_cost_change;
     const bool success = std::isfinite(candidate_cost) && relative_decrease > o.min_relative_decrease;
-    // ParameterToleranceReached / FunctionToleranceReached: Ceres returns
-    // before accepting the candidate (x stays at the current point).
-    double x_norm = 0.0;
-    if (o.parameter_tolerance > 0.0) {
-      launch_sqnorm2(ctx->qt.ptr, ctx->rank == 0 ? 8 * (int64_t)d.num_images : 0, ctx->X.ptr, 3 * d.num_points,
-                     sc + kStepNorm, ctx->red.ptr, s);
-      st = allreduce(ctx, sc + kStepNorm, 1);
-      if (st != MI_BA_OK) return st;
-      st = read_scalars(ctx, kStepNorm, 1);
-      if (st != MI_BA_OK) return st;
-      x_norm = std::sqrt(hs[kStepNorm]);
-    }
+    // ParameterToleranceReached (step_norm = |x - candidate_x| <= tol (|x| +
+    // tol); with tol 0: the candidate equals x bitwise) /
+    // FunctionToleranceReached: Ceres returns before accepting the candidate
+    // (x stays at the current point).
+    const double x_norm = std::sqrt(hs[kXB]);
+    const double step_norm = std::sqrt(hs[kXR]);
+    its.step_norm = step_norm;
     if (step_norm <= o.parameter_tolerance * (x_norm + o.parameter_tolerance) ||
         std::fabs(cost_change) <= o.function_tolerance * x_cost) {
       ++sum->num_unsuccessful_steps;
@@ -1468,6 +1539,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     }
     its.relative_decrease = relative_decrease;
     its.cost_change = cost_change;  // every valid step, as Ceres (negative when rejected)
+    last_successful = success;
     if (success) {
       ++sum->num_successful_steps;
       its.step_is_successful = 1;
@@ -1909,6 +1981,11 @@ mi_ba_status mi_ba_comm_unique_id(char id[MI_BA_COMM_ID_BYTES]) {
   return MI_BA_OK;
 }
 
+// set_comm helper threads still running (mi_ba_comm_pending_setups)
+static std::atomic<int32_t> g_setup_helpers{0};
+
+int32_t mi_ba_comm_pending_setups(void) { return g_setup_helpers.load(); }
+
 mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t world,
                                     const char id[MI_BA_COMM_ID_BYTES]) {
   if (!ctx || !id || world < 1 || rank < 0 || rank >= world) return MI_BA_ERR_INVALID_ARGUMENT;
@@ -1934,7 +2011,9 @@ mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t wo
   };
   auto job = std::make_shared<InitJob>();
   const int dev = ctx->device;
-  std::thread([job, u, world, rank, dev]() {
+  const double deadline = now_s() + 1e-3 * std::max(1, ctx->comm_timeout_ms);
+  g_setup_helpers.fetch_add(1);
+  std::thread([job, u, world, rank, dev, deadline]() {
     ncclComm_t c = nullptr;
     ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
     if (r == ncclSuccess) {
@@ -1942,10 +2021,20 @@ mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t wo
       cfg.blocking = 0;
       ncclUniqueId uu = u;
       r = ncclCommInitRankConfig(&c, world, uu, rank, &cfg);
+      // poll the non-blocking set-up until it completes, fails, the caller
+      // gave up on it (abandoned) or the deadline passes: the last two end
+      // the helper too (the communicator is aborted below), so a peer that
+      // never joins leaves no polling thread behind
       while (r == ncclInProgress || r == ncclSuccess) {
         ncclResult_t e = ncclSuccess;
         if (!c || ncclCommGetAsyncError(c, &e) != ncclSuccess) { r = ncclInternalError; break; }
         if (e != ncclInProgress) { r = e; break; }
+        bool gave_up;
+        {
+          std::lock_guard<std::mutex> g(job->m);
+          gave_up = job->abandoned;
+        }
+        if (gave_up || now_s() > deadline) { r = ncclInternalError; break; }
         std::this_thread::sleep_for(std::chrono::microseconds(100));
       }
     }
@@ -1959,6 +2048,7 @@ mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t wo
     }
     job->cv.notify_all();
     if ((abandoned || r != ncclSuccess) && c) (void)ncclCommAbort(c);
+    g_setup_helpers.fetch_sub(1);
   }).detach();
   bool ok;
   {
@@ -2163,10 +2253,6 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.panel_rows_per_group = value;
     return MI_BA_OK;
   }
-  // split head: panel factor on this many CUs, trailing dgemm on the rest,
-  // while the panel starts before column cholesky_split_cols (tools build:
-  // measured 22.5-27.5 vs 15.6 ms, profiles/r4_ab_cholesky_split_cus.jsonl)
-  // trailing-update block columns over this many streams (1..4)
   if (std::strcmp(key, "cholesky_rest_priority") == 0 && (value == 0 || value == 1)) {
     ctx->chol.rest_priority = value != 0;
     return MI_BA_OK;
@@ -2175,10 +2261,14 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.rest_cumask = value != 0;
     return MI_BA_OK;
   }
+  // trailing-update block columns over this many streams (1..4)
   if (std::strcmp(key, "cholesky_rest_streams") == 0 && value >= 1 && value <= 4) {
     ctx->chol.rest_streams = (int)value;
     return MI_BA_OK;
   }
+  // split head: panel factor on this many CUs, trailing dgemm on the rest,
+  // while the panel starts before column cholesky_split_cols (tools build:
+  // measured 22.5-27.5 vs 15.6 ms, profiles/r4_ab_cholesky_split_cus.jsonl)
   if (std::strcmp(key, "cholesky_split_cus") == 0 && value >= 0 && value <= 4096 && ab_value(value, 0)) {
     ctx->chol.split_cus = (int)value;
     return MI_BA_OK;

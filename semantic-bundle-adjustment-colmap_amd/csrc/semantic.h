@@ -116,6 +116,8 @@ mi_ba_status semantic_set_label_planes(mi_ba_context* ctx, bool on);
 void semantic_cost(mi_ba_context* ctx, const double* qt, const double* cam, double* d_cost);
 // Fold the pair blocks into the Schur-Jacobi pose blocks, b and diag(U).
 void semantic_add_fblock(mi_ba_context* ctx);
+// g += the pair blocks' J'r on their poses (gradient tolerance test).
+void semantic_add_gradient(mi_ba_context* ctx, double* g);
 // y += M_pair x (implicit Schur product).
 void semantic_schur_product(mi_ba_context* ctx, const double* x, double* y);
 // Add the pair blocks M into the explicit reduced camera system S.

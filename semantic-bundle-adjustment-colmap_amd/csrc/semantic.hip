@@ -1849,6 +1849,21 @@ __global__ void semantic_fblock_kernel(const SemPair* __restrict__ pairs, int np
   }
 }
 
+// g += J'r of the pair's samples (its block's g part) on its two poses: the
+// raw gradient of the gradient tolerance test.
+__global__ void semantic_gradient_kernel(const SemPair* __restrict__ pairs, int npairs,
+                                         const double* __restrict__ pair_blk, double* __restrict__ g) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= npairs) return;
+  const SemPair pr = pairs[k];
+  const double* B = pair_blk + (size_t)k * kPairStride;
+  for (int side = 0; side < 2; ++side) {
+    if (!(side == 0 ? pr.var1 : pr.var2)) continue;
+    const uint32_t img = side == 0 ? pr.i : pr.j;
+    for (int a = 0; a < 6; ++a) atomicAdd(g + 6 * (size_t)img + a, B[78 + side * 6 + a]);
+  }
+}
+
 // y += M x over the pair's two poses.
 __global__ void semantic_product_kernel(const SemPair* __restrict__ pairs, int npairs,
                                         const double* __restrict__ pair_blk, const double* __restrict__ x,
@@ -2481,6 +2496,13 @@ void semantic_add_fblock(mi_ba_context* ctx) {
   if (!S->npairs) return;
   hipLaunchKernelGGL(semantic_fblock_kernel, dim3((S->npairs + 63) / 64), dim3(64), 0, ctx->stream, S->pairs.ptr,
                      S->npairs, S->pair_blk.ptr, ctx->pose_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr);
+}
+
+void semantic_add_gradient(mi_ba_context* ctx, double* g) {
+  SemanticState* S = ctx->sem;
+  if (!S->npairs) return;
+  hipLaunchKernelGGL(semantic_gradient_kernel, dim3((S->npairs + 63) / 64), dim3(64), 0, ctx->stream, S->pairs.ptr,
+                     S->npairs, S->pair_blk.ptr, g);
 }
 
 void semantic_schur_product(mi_ba_context* ctx, const double* x, double* y) {

@@ -271,6 +271,8 @@ def load(path: str = LIB_PATH):
     lib.mi_ba_kernel_time.argtypes = [C.c_void_p, C.c_char_p, _dp, _i64p]
     lib.mi_ba_comm_unique_id.argtypes = [C.c_char_p]
     lib.mi_ba_context_set_comm.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
+    lib.mi_ba_comm_pending_setups.argtypes = []
+    lib.mi_ba_comm_pending_setups.restype = C.c_int32
     lib.mi_ba_context_set_host_reducer.argtypes = [C.c_void_p, C.c_int32, C.c_int32, HOST_ALLREDUCE_FN, C.c_void_p]
     lib.mi_ba_dense_cholesky.argtypes = [C.c_int32, C.c_int32, _dp, _dp, C.c_int32, C.c_int32, C.c_int32, _i32p]
     lib.mi_ba_dense_cholesky_ex.argtypes = [C.c_int32, C.c_int32, _dp, _dp, C.c_int32, C.c_int32, C.c_int32,
@@ -457,6 +459,11 @@ class SemanticInput:
         s.depth_error_threshold = self.depth_error_threshold
         s.numeric_relative_step_size = self.numeric_relative_step_size
         return s
+
+
+def comm_pending_setups() -> int:
+    """Communicator set-ups still running on their helper threads."""
+    return int(load().mi_ba_comm_pending_setups())
 
 
 def comm_unique_id() -> bytes:

@@ -25,10 +25,20 @@ with mi_ba.Context(mi_ba.default_options(max_num_iterations=3), sc.copy()) as ct
         print(f"missing peer: {name} after {dt:.2f} s", flush=True)
         if e.status != mi_ba.ERR_HIP or dt > 30:
             sys.exit(1)
+    # the abandoned set-up's helper stops at the same deadline (it aborts the
+    # half-built communicator and exits): none left running shortly after
+    t1 = time.perf_counter()
+    while mi_ba.comm_pending_setups() and time.perf_counter() - t1 < 20:
+        time.sleep(0.05)
+    pending = mi_ba.comm_pending_setups()
+    print(f"set-up helpers still running: {pending}", flush=True)
+    if pending:
+        sys.stdout.flush()
+        os._exit(1)
     s = ctx.solve()
     print(f"single-rank solve after the failed set-up: {s.num_successful_steps} steps", flush=True)
     ok = s.num_successful_steps >= 1
-# the abandoned set-up's helper thread may still sit in RCCL's bootstrap: end
-# the process without waiting for it
+# RCCL's own bootstrap threads may outlive the aborted communicator: end the
+# process without waiting for them
 sys.stdout.flush()
 os._exit(0 if ok else 1)

@@ -1,0 +1,280 @@
+// sba_reference_test.cc — SemanticBundleAdjuster through the facade with the
+// reference's own construction (src/optim/semantic_bundle_adjustment.h:
+// 219-225): options.data_path names the folder of depth_tiff/ and
+// semantic_tiff/ maps, the adjuster is built from (options, config) and Solve
+// reads the maps (ReadDepthAndSemanticMaps, semantic_bundle_adjustment.cc:
+// 1021-1068).  The solve block below is the reference controller's
+// (controllers/semantic_bundle_adjustment.cc:100-119) with the facade's
+// Reconstruction accessor (GetImage) for Reconstruction::Image.
+//
+//   ./sba_reference_test host   TIFF maps written and read back, a missing
+//                               file reported as the reference does (no GPU)
+//   ./sba_reference_test gpu    + the solve from the files, equal to the solve
+//                               with the same maps in memory
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "colmap_amd/semantic_bundle_adjustment.h"
+
+using namespace colmap_amd;
+
+static int g_failures = 0;
+#define CHECK_T(cond)                                                        \
+  do {                                                                       \
+    if (!(cond)) {                                                           \
+      std::printf("  FAILED %s:%d: %s\n", __FILE__, __LINE__, #cond);        \
+      ++g_failures;                                                          \
+    }                                                                        \
+  } while (0)
+
+// Little-endian baseline TIFF, one strip, uncompressed, 32-bit IEEE float
+// samples (SampleFormat 3): the layout matrixFromTiff reads (matrix_vis.h:
+// 130-176); rows in file order = raster rows y = 0..H-1.
+static void WriteFloatTiff(const std::string& path, int H, int W, const std::vector<float>& data) {
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot write " + path);
+  auto u16 = [&](uint16_t v) { f.write(reinterpret_cast<const char*>(&v), 2); };
+  auto u32 = [&](uint32_t v) { f.write(reinterpret_cast<const char*>(&v), 4); };
+  const uint32_t bytes = (uint32_t)H * W * 4;
+  const uint16_t n = 10;
+  const uint32_t ifd = 8, data_off = ifd + 2 + 12 * n + 4;
+  f.write("II", 2);
+  u16(42);
+  u32(ifd);
+  u16(n);
+  auto entry = [&](uint16_t tag, uint16_t type, uint32_t value) {
+    u16(tag);
+    u16(type);
+    u32(1);
+    if (type == 3) {
+      u16((uint16_t)value);
+      u16(0);
+    } else {
+      u32(value);
+    }
+  };
+  entry(256, 4, (uint32_t)W);  // ImageWidth
+  entry(257, 4, (uint32_t)H);  // ImageLength
+  entry(258, 3, 32);           // BitsPerSample
+  entry(259, 3, 1);            // Compression: none
+  entry(262, 3, 1);            // PhotometricInterpretation: BlackIsZero
+  entry(273, 4, data_off);     // StripOffsets
+  entry(277, 3, 1);            // SamplesPerPixel
+  entry(278, 4, (uint32_t)H);  // RowsPerStrip
+  entry(279, 4, bytes);        // StripByteCounts
+  entry(339, 3, 3);            // SampleFormat: IEEE float
+  u32(0);
+  f.write(reinterpret_cast<const char*>(data.data()), bytes);
+}
+
+// Three cameras looking at a labelled plane (the facade SBA test's scene,
+// tests/cpp/bundle_adjustment_test.cc TestSemanticBundleAdjuster), image
+// names with an extension so the map stems are exercised.
+static Reconstruction Scene(SemanticMaps* maps) {
+  std::mt19937 prng(0);
+  auto U = [&](double a, double b) { return std::uniform_real_distribution<double>(a, b)(prng); };
+  Reconstruction rec;
+  std::vector<point3D_t> ids;
+  for (int i = 0; i < 10; ++i) {
+    double xyz[3] = {U(-1, 1), U(-1, 1), U(-1, 1)};
+    ids.push_back(rec.AddPoint3D(xyz));
+  }
+  const int H = 60, W = 60;
+  maps->height = H;
+  maps->width = W;
+  for (int i = 0; i < 3; ++i) {
+    Camera cam;
+    cam.camera_id = (camera_t)i;
+    cam.model_id = MI_BA_SIMPLE_RADIAL;
+    cam.params = {1200, 30, 30, 0};
+    rec.AddCamera(cam);
+    Image im;
+    im.image_id = (image_t)i;
+    im.camera_id = (camera_t)i;
+    im.name = "frame_" + std::to_string(i) + ".v1.jpg";
+    im.tvec[0] = U(-1.0, 1.0);
+    im.tvec[1] = U(-1.0, 1.0);
+    im.tvec[2] = 10;
+    for (point3D_t id : ids) {
+      const double* X = rec.GetPoint3D(id).xyz;
+      Point2D p2;
+      p2.xy[0] = 1200 * (X[0] + im.tvec[0]) / (X[2] + 10) + 30;
+      p2.xy[1] = 1200 * (X[1] + im.tvec[1]) / (X[2] + 10) + 30;
+      im.points2D.push_back(p2);
+    }
+    std::vector<float> depth((size_t)H * W), label((size_t)H * W);
+    for (int y = 0; y < H; ++y)
+      for (int x = 0; x < W; ++x) {
+        const double d = im.tvec[2];
+        const double X = (x - 500.0 + 470.0) / 1200.0 * d - im.tvec[0];
+        const double Y = (y - 500.0 + 470.0) / 1200.0 * d - im.tvec[1];
+        depth[(size_t)y * W + x] = (float)(d + 0.01 * y);  // rows differ: a flip would show
+        label[(size_t)y * W + x] = (float)((((int)std::floor(X / 0.05) + (int)std::floor(Y / 0.05)) % 2 + 2) % 2);
+      }
+    maps->depth[im.name] = depth;
+    maps->semantic[im.name] = label;
+    im.tvec[0] += 0.002 * i;  // pose error for the semantic term to pull on
+    rec.AddImage(im);
+  }
+  for (int i = 0; i < 3; ++i) {
+    point2D_t idx = 0;
+    for (point3D_t id : ids) rec.AddObservation(id, TrackElement{(image_t)i, idx++});
+  }
+  for (int i = 0; i < 3; ++i) rec.RegisterImage((image_t)i);
+  return rec;
+}
+
+static void WriteMaps(const std::string& dir, const Reconstruction& rec, const SemanticMaps& maps) {
+  internal::MakeDirs(dir + "/depth_tiff");
+  internal::MakeDirs(dir + "/semantic_tiff");
+  for (const auto& e : rec.images) {
+    const std::string& name = e.second.name;
+    const std::string stem = name.substr(0, name.find_last_of('.'));
+    WriteFloatTiff(dir + "/depth_tiff/" + stem + "_depth.tiff", maps.height, maps.width, maps.depth.at(name));
+    WriteFloatTiff(dir + "/semantic_tiff/" + stem + "_semantic.tiff", maps.height, maps.width,
+                   maps.semantic.at(name));
+  }
+}
+
+// controllers/semantic_bundle_adjustment.cc:100-119 (the configuration and
+// the two calls), on `reconstruction_`.
+static SolverSummary ReferenceSolve(const SemanticBundleAdjustmentOptions& options, Reconstruction* reconstruction_,
+                                    bool* solved) {
+  const std::vector<image_t> reg_image_ids = reconstruction_->RegImageIds();
+  SemanticBundleAdjustmentOptions ba_options = options;
+
+  // Configure bundle adjustment.
+  SemanticBundleAdjustmentConfig ba_config;
+  for (const image_t image_id : reg_image_ids) {
+    ba_config.AddImage(image_id);
+  }
+
+  // Set first pose and second translation vector to constant
+  ba_config.SetConstantPose(reg_image_ids[0]);
+  ba_config.SetConstantTvec(reg_image_ids[1], {0});
+
+  // Set all camera intrinsics to constant
+  for (const image_t image_id : reg_image_ids) {
+    camera_t camera_id = reconstruction_->GetImage(image_id).CameraId();
+    ba_config.SetConstantCamera(camera_id);
+  }
+
+  // Run bundle adjustment.
+  SemanticBundleAdjuster bundle_adjuster(ba_options, ba_config);
+  *solved = bundle_adjuster.Solve(reconstruction_);
+  return bundle_adjuster.Summary();
+}
+
+int main(int argc, char** argv) {
+  const std::string mode = argc > 1 ? argv[1] : "host";
+  char tmpl[] = "/tmp/sba_ref_XXXXXX";
+  const char* d = mkdtemp(tmpl);
+  if (!d) {
+    std::printf("mkdtemp failed\n1 failure(s)\n");
+    return 1;
+  }
+  const std::string dir(d);
+  SemanticMaps maps;
+  const Reconstruction scene = Scene(&maps);
+  WriteMaps(dir, scene, maps);
+
+  struct Case {
+    std::string name;
+    std::function<void()> run;
+  };
+  std::vector<Case> cases;
+  // the maps read back from the files equal the rasters written (row order,
+  // float bits), for every config image
+  cases.push_back({"TestMapsFromDataPath", [&] {
+    BundleAdjustmentConfig config;
+    for (image_t i = 0; i < 3; ++i) config.AddImage(i);
+    const SemanticMaps back = LoadSemanticMaps(dir, scene, config);
+    CHECK_T(back.height == maps.height && back.width == maps.width);
+    for (const auto& e : scene.images) {
+      const std::string& n = e.second.name;
+      CHECK_T(back.depth.at(n).size() == maps.depth.at(n).size());
+      CHECK_T(std::memcmp(back.depth.at(n).data(), maps.depth.at(n).data(), 4 * maps.depth.at(n).size()) == 0);
+      CHECK_T(std::memcmp(back.semantic.at(n).data(), maps.semantic.at(n).data(), 4 * maps.semantic.at(n).size()) ==
+              0);
+    }
+  }});
+  // ReadDepthAndSemanticMaps (:1037-1048): a missing map file is a
+  // std::runtime_error naming the file, raised by Solve before any solve
+  cases.push_back({"TestMissingMapFile", [&] {
+    const std::string other = dir + "_missing";
+    internal::MakeDirs(other + "/depth_tiff");
+    internal::MakeDirs(other + "/semantic_tiff");
+    SemanticBundleAdjustmentOptions options;
+    options.print_summary = false;
+    options.data_path = other;
+    Reconstruction rec = scene;
+    bool threw = false, solved = false;
+    try {
+      ReferenceSolve(options, &rec, &solved);
+    } catch (const std::runtime_error& e) {
+      threw = std::string(e.what()).find("does not exist") != std::string::npos;
+    }
+    CHECK_T(threw);
+    if (std::system(("rm -rf '" + other + "'").c_str()) != 0) std::printf("  (could not remove %s)\n", other.c_str());
+  }});
+  if (mode == "gpu") {
+    // the reference construction solving from the files takes exactly the
+    // steps of the in-memory form
+    cases.push_back({"TestSolveFromDataPath", [&] {
+      SemanticBundleAdjustmentOptions options;
+      options.print_summary = false;
+      options.error_computation_pixel_step = 3;
+      options.data_path = dir;
+      Reconstruction a = scene, b = scene;
+      bool solved = false;
+      const SolverSummary sa = ReferenceSolve(options, &a, &solved);
+      CHECK_T(solved);
+      CHECK_T(sa.num_residuals_reduced > 0);
+      CHECK_T(sa.final_cost <= sa.initial_cost);
+      SemanticBundleAdjustmentConfig config;
+      for (const image_t id : b.RegImageIds()) config.AddImage(id);
+      config.SetConstantPose(0);
+      config.SetConstantTvec(1, {0});
+      for (camera_t c = 0; c < 3; ++c) config.SetConstantCamera(c);
+      SemanticBundleAdjuster mem(options, config, maps);
+      CHECK_T(mem.Solve(&b));
+      const SolverSummary& sb = mem.Summary();
+      CHECK_T(sa.num_residuals_reduced == sb.num_residuals_reduced);
+      CHECK_T(sa.initial_cost == sb.initial_cost && sa.final_cost == sb.final_cost);
+      CHECK_T(sa.num_successful_steps == sb.num_successful_steps &&
+              sa.num_unsuccessful_steps == sb.num_unsuccessful_steps);
+      CHECK_T(sa.termination_type == sb.termination_type);
+      for (const auto& e : a.images) {
+        const Image& x = e.second;
+        const Image& y = b.GetImage(e.first);
+        CHECK_T(std::memcmp(x.qvec, y.qvec, sizeof(x.qvec)) == 0 && std::memcmp(x.tvec, y.tvec, sizeof(x.tvec)) == 0);
+      }
+      // image 0 constant, image 1's tvec[0] constant (the controller's gauge)
+      const Image& i0 = a.GetImage(0);
+      const Image& s0 = scene.GetImage(0);
+      CHECK_T(std::memcmp(i0.tvec, s0.tvec, sizeof(i0.tvec)) == 0);
+      CHECK_T(a.GetImage(1).tvec[0] == scene.GetImage(1).tvec[0]);
+    }});
+  }
+  for (auto& c : cases) {
+    const int before = g_failures;
+    try {
+      c.run();
+    } catch (const std::exception& e) {
+      std::printf("  EXCEPTION %s\n", e.what());
+      ++g_failures;
+    }
+    std::printf("%s %s\n", g_failures == before ? "PASS" : "FAIL", c.name.c_str());
+  }
+  if (std::system(("rm -rf '" + dir + "'").c_str()) != 0) std::printf("  (could not remove %s)\n", dir.c_str());
+  std::printf("%d failure(s)\n", g_failures);
+  return g_failures == 0 ? 0 : 1;
+}

@@ -323,7 +323,7 @@ def test_lm_fused_forward_solve(gpu, images):
                                       dict(split_cus=32, split_cols=1024), dict(split_cus=200, split_cols=1593),
                                       dict(head_own_diag=2, head_own_cols=1024),
                                       dict(rest_streams=2, rest_update=0), dict(rest_streams=4, rest_update=0),
-                                      dict(rest_streams=3)])
+                                      dict(rest_streams=3), dict(rest_streams=2)])
 def test_lm_panel_schedule(gpu, schedule):
     """Non-uniform panel schedules (cholesky_head_panel / _head_cols /
     _tail_panel / _tail_cols: 1024-wide one-launch panels of 16 column tiles,
@@ -334,14 +334,16 @@ def test_lm_panel_schedule(gpu, schedule):
     (cholesky_head_own_diag / _cols) and the trailing update's block columns
     over several streams (cholesky_rest_streams), with and
     without the look-ahead (S itself differs
-    between runs in the order of the Schur build's float atomics)."""
+    between runs in the order of the Schur build's float atomics).  The
+    baseline is the single-stream trailing update (rest_streams 1), so the
+    default two-stream update is compared with it too."""
     if any(k in schedule for k in ("split_cus", "head_own_diag")) and not mi_ba.ab_build():
         pytest.skip("split head / head panel kind: tools build only (MI_BA_LIB=ab)")
     sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
     res = []
-    for keys in ({}, schedule, dict(schedule, lookahead=0)):
+    for keys in (dict(rest_streams=1), schedule, dict(schedule, lookahead=0)):
         with mi_ba.Context(opts, sc.copy()) as ctx:
             for k, v in keys.items():
                 ctx.set_tuning("cholesky_" + k, v)

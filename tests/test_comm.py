@@ -101,3 +101,4 @@ def test_missing_peer_at_setup_returns_error(gpu):
                        timeout=180)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "missing peer: ERR_HIP" in p.stdout, p.stdout
+    assert "set-up helpers still running: 0" in p.stdout, p.stdout

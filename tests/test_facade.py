@@ -47,3 +47,20 @@ def test_controllers_host():
 def test_controllers_gpu(gpu):
     out = run("gpu", "controllers_test")
     assert out.count("PASS") == 11
+
+
+def test_sba_reference_signature_host():
+    """SemanticBundleAdjuster(options, config) with options.data_path
+    (semantic_bundle_adjustment.h:219-225): the TIFF maps read back bitwise,
+    a missing map file raised as ReadDepthAndSemanticMaps does."""
+    out = run("host", "sba_reference_test")
+    assert out.count("PASS") == 2
+
+
+@pytest.mark.gpu
+def test_sba_reference_signature_gpu(gpu):
+    """The reference controller's construction + Solve
+    (controllers/semantic_bundle_adjustment.cc:100-119) from TIFF files equals
+    the in-memory-maps solve bitwise."""
+    out = run("gpu", "sba_reference_test")
+    assert out.count("PASS") == 3

@@ -19,8 +19,10 @@
     final cost within 1e-6 relative, same step counts.
   * ITERATIVE_SCHUR at the settings bench.py uses at N > 1 (default eta 0.1,
     200 CG iterations per solve), C2 size, run to the 100-iteration cap
-    against the oracle's exact LM: the inexact steps take another path, so
-    only the converged cost (1e-6 relative) and the points (1e-5) are compared.
+    against the oracle's exact LM: the inexact steps take another path; the
+    converged cost (1e-6 relative) is compared, and the parameter difference
+    is shown to lie along the problem's near-null direction (tests/valley.py).
+    Step-for-step against the oracle's own PCG: tests/test_lm_semantics.py.
 """
 import numpy as np
 import pytest
@@ -143,6 +145,18 @@ def test_iterative_schur_parity(gpu, case, mf):
 
 
 def test_c2_iterative_schur_default_eta_converges_to_oracle(gpu):
+    """ITERATIVE_SCHUR at bench.py's N > 1 settings (eta 0.1, 200 CG
+    iterations per solve) run to the 100-iteration cap against the oracle's
+    exact-Schur LM: the converged cost within 1e-6 relative, and the
+    parameters checked against the problem's flat valley (round 4 deleted
+    that check after a 3.5e-4 point difference; the step-for-step PCG parity
+    is tests/test_lm_semantics.py).  At the exact solution the Jacobi-scaled
+    reduced camera system has a near-null direction (focal length against
+    point depth); the camera-side difference of the two solutions must lie
+    along it: >= 99 % of its energy in the three smallest-eigenvalue
+    eigenvectors, whose eigenvalues are < 1e-4 of the median
+    (tests/valley.py)."""
+    import valley
     sc = c2_scene()
     ref = mi_ba.default_options(max_num_iterations=100)
     opts = mi_ba.default_options(max_num_iterations=100, linear_solver_type=mi_ba.SOLVER_ITERATIVE_SCHUR)
@@ -152,10 +166,11 @@ def test_c2_iterative_schur_default_eta_converges_to_oracle(gpu):
     s_g = mi_ba.solve(opts, b)
     assert s_g.num_linear_solver_iterations > s_g.num_successful_steps  # the CG path ran
     assert abs(s_g.final_cost - s_o.final_cost) <= 1e-6 * s_o.final_cost, (s_g.final_cost, s_o.final_cost)
-    # no parameter-level check: the minimum has a near-flat valley (focal
-    # length against point depth; measured: the inexact CG stops up to 3e-4
-    # along it, run to run, at the same cost to 1e-6), so only the cost is a
-    # property of the converged solve
+    rep = valley.valley_report(mi_ba.default_options(), a, b)
+    print("valley: lambda", rep["lam"][:4], "median", np.median(rep["lam"]), "energy", rep["energy"][:4],
+          "|d|", rep["norm"], "xyz diff", np.abs(a.xyz - b.xyz).max())
+    assert rep["lam"][2] < 1e-4 * np.median(rep["lam"])
+    assert rep["energy"][2] >= 0.99, rep["energy"][:4]
 
 
 @pytest.mark.parametrize("mf", [0, 1])
