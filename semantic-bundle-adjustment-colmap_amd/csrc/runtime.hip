@@ -860,6 +860,8 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
   ctx->xcm_stale = true;
   // image records + the scalar slots zeroed in one launch
   launch_pack_images(d, ctx->img_rec.ptr, s, ctx->scalars.ptr, kNumScalars);
+#ifdef MI_BA_AB_VARIANTS
+  // Step layouts measured slower than the default (tools build only):
   // linearize_overlap: 1 the semantic kernels on a second stream beside the
   // reprojection kernel; 2 the semantic flat pass first, then its
   // deferred-sample pass (latency-bound) on the second stream beside the
@@ -916,12 +918,6 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     mi_ba_status st = semantic_linearize(ctx, ctx->scalars.ptr + kSemCost, false);
     if (st != MI_BA_OK) return st;
   }
-  // linearize_warm_inputs (default: every range): the reprojection kernel's
-  // streamed inputs (264 MB at C4) read right before it, so the memory-side
-  // cache serves its reads and HBM sees its J / r write stream alone (in-step
-  // 0.576 -> 0.431 ms at C4 for a 0.055 ms read; the observations or ids alone
-  // do not do it: profiles/r4_ab_linearize_warm_ranges.jsonl).  Only after the
-  // semantic pass has used the cache; a geometric-only step finds them cached.
   // prep_early (semantic_prep_early; measured slower, off): the semantic pair
   // tables formed on the side stream beside the warm-up and the reprojection
   // kernel (they read the poses only), instead of on the critical path after
@@ -943,6 +939,17 @@ mi_ba_status context_linearize(mi_ba_context* ctx, double* cost_out) {
     MI_HIP(hipEventRecord(ctx->lin_ev[1], ctx->lin_side));
     prep_ev = ctx->lin_ev[1];
   }
+#else
+  // the product's one layout: input warm-up, reprojection kernel, semantic pass
+  constexpr bool overlap = false, split = false, warm = false, sem_first = false;
+  hipEvent_t prep_ev = nullptr;
+#endif
+  // linearize_warm_inputs (default: every range): the reprojection kernel's
+  // streamed inputs (264 MB at C4) read right before it, so the memory-side
+  // cache serves its reads and HBM sees its J / r write stream alone (in-step
+  // 0.576 -> 0.431 ms at C4 for a 0.055 ms read; the observations or ids alone
+  // do not do it: profiles/r4_ab_linearize_warm_ranges.jsonl).  Only after the
+  // semantic pass has used the cache; a geometric-only step finds them cached.
   hipEvent_t wstop = nullptr;
   if (ctx->sem && ctx->lin_warm && d.nb > 0) {
     timer_begin(ctx, "input_warm", &wstop);
@@ -2112,7 +2119,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->lin_warm_conc = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "warm_unroll") == 0 && (value == 4 || value == 8)) {
+  if (std::strcmp(key, "warm_unroll") == 0 && (value == 4 || value == 8) && ab_value(value, 4)) {
     ctx->warm_unroll = value;
     return MI_BA_OK;
   }
@@ -2120,7 +2127,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->warm_wgs = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "linearize_order") == 0 && (value == 0 || value == 1)) {
+  if (std::strcmp(key, "linearize_order") == 0 && (value == 0 || value == 1) && ab_value(value, 0)) {
     ctx->lin_order = value;
     return MI_BA_OK;
   }
@@ -2130,7 +2137,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->lin_overlap = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "semantic_prep_early") == 0 && (value == 0 || value == 1)) {
+  if (std::strcmp(key, "semantic_prep_early") == 0 && (value == 0 || value == 1) && ab_value(value, 0)) {
     ctx->sem_prep_early = value;
     return MI_BA_OK;
   }
