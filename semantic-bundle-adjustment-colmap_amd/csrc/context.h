@@ -83,6 +83,13 @@ struct mi_ba_context {
   miba::DevArray<uint32_t> cm_ptv;  // [nb] camera-major: the block's point if variable, else 0xffffffff
   miba::DevArray<miba::DevTile> tiles;
   int ntiles = 0;
+  // deterministic camera-side sums (owner_flush_kernel): the tiles of each
+  // image and camera, and the per-tile partials
+  miba::DevArray<uint32_t> img_tile_off, cam_tile_off, cam_tiles;
+  miba::DevArray<double> tpart;            // [ntiles][kTilePartStride]
+  bool det_sums = true;                    // "deterministic_sums" (0: float-atomic flushes)
+  const miba::TileOwners* owners() const { return det_sums && tpart.ptr ? &owners_ : nullptr; }
+  miba::TileOwners owners_{};
   miba::DevArray<miba::DevPoint> vpoints;
   int64_t npv = 0;
   int64_t nb_const = 0;  // reduced blocks of constant points
@@ -142,6 +149,13 @@ struct mi_ba_context {
   int nptiles_xcd = 0;
   int schur_block = 8;                            // images per block edge of ptiles_blk (8: schur_build 3.26 ms
                                                   // vs 3.32 / 3.42 / 3.64 at 16 / 32 / 64, profiles/r3_ab_schur_block.jsonl)
+  // deterministic Schur pair sums (PairFlush; cameras not shared between images)
+  miba::DevArray<int32_t> pslot;           // [nptiles] of ptiles_blk: partial slot or -1
+  miba::DevArray<double> spart;            // [nslots][256]
+  miba::DevArray<uint4> pdest;             // [ndest] (ia, ib, first slot, slots)
+  miba::DevArray<uint8_t> pself;           // [nslots]
+  int npdest = 0;
+  bool pflush_ok = false;
   miba::DevArray<uint2> pairs;             // (a, b) block pairs bucketed by image pair
   int nptiles = 0;
   miba::DevArray<int32_t> info;

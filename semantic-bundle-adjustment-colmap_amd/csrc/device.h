@@ -17,8 +17,11 @@
 //                              meta = img_flags | cam_var << 8 | model << 16
 //   points     X[P][3]
 // Camera-side reductions run over cm_perm (blocks sorted by image) in tiles
-// that never straddle an image, so each tile folds into one atomic flush.
+// that never straddle an image; each tile's sums are flushed per image /
+// camera in a fixed order (TileOwners, deterministic).
 #pragma once
+
+#include <hip/hip_runtime.h>
 
 #include <cstdint>
 
@@ -52,6 +55,35 @@ constexpr int kPairTile = 256;
 
 // doubles per packed image record (kernels.hip pack_images_kernel)
 constexpr int kImgRec = 32;
+
+// Owners of the camera-side tile sums (the deterministic flush,
+// kernels.hip owner_flush_kernel): the tiles of image i are
+// [img_tile_off[i], img_tile_off[i + 1]) (tiles are image-sorted); the tiles
+// of camera c are cam_tiles[cam_tile_off[c] .. cam_tile_off[c + 1]) in image
+// then tile order.  part: per-tile block sums, [tile][stride].
+struct TileOwners {
+  const uint32_t* img_tile_off;
+  const uint32_t* cam_tile_off;
+  const uint32_t* cam_tiles;
+  double* part;
+  int stride;  // capacity per tile (kTilePartStride)
+};
+constexpr int kTilePartStride = 120;  // >= the widest per-tile flush (fblock_dense at 8 intrinsics: 105 + 14)
+
+// Deterministic Schur pair sums (kernels.hip schur_pairs_kernel with pslot):
+// a pair tile whose S block no other tile writes (an off-diagonal image
+// pair's only tile, cameras not shared between images) subtracts its block
+// from S directly; every other tile (a diagonal block's self / same-image
+// tiles, an image pair of more than one tile) writes its 16 x 16 accumulator
+// to part[pslot[t]] and schur_pairs_flush_kernel sums each such block's
+// tiles in list order.  pslot null: float-atomic flushes.
+struct PairFlush {
+  const int32_t* pslot;  // [ntiles] partial slot, -1: direct
+  double* part;          // [nslots][256]
+  const uint4* dest;     // [ndest] (ia, ib, first slot, slot count)
+  const uint8_t* self;   // [nslots] the slot's tile holds self pairs (a == b)
+  int ndest;
+};
 
 struct DevProblem {
   int model;           // camera model of every camera, or kMixedModels (per-camera cam_model)

@@ -53,9 +53,13 @@ void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, 
 // Camera-side tile pass: per image/camera tangent block S_ii = U_ii - sum W V^-1 W',
 // b = g - sum W V^-1 g_p and diag(U) (undamped column norms).
 // Jcm (nullable): J's rows in camera-major order (launch_permute_rows).
+// own (nullable): the deterministic flush (per-tile partials summed per image /
+// camera in a fixed order, owner_flush_kernel) instead of float atomics; the
+// same for every camera-side tile pass below.
 void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
                    const double2* r, const double* J, const double* Jcm, const double* Vg, const double* Vinv,
-                   double* pose_blk, double* cam_blk, double* b, double* udiag, hipStream_t s);
+                   double* pose_blk, double* cam_blk, double* b, double* udiag, hipStream_t s,
+                   const TileOwners* own = nullptr);
 // Jcm[k] = J[cm_perm[k]] for k < n (2 (9 + ct) doubles per block).
 // Doubles per block of the Schur build's per-block records (Z rows, or the
 // JG records of schur_pairs_variant 6).
@@ -71,7 +75,7 @@ void launch_permute_rows(const DevProblem& p, const uint32_t* cm_perm, int64_t n
 // blocks, which only the PCG preconditioner uses).
 void launch_fblock_dense(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
                          const uint32_t* cm_ptv, const double2* r, const double* J, const double* q, double* b,
-                         double* udiag, double* S, hipStream_t s);
+                         double* udiag, double* S, hipStream_t s, const TileOwners* own = nullptr);
 
 // Finalise: Jacobi scale (first), LM diagonal, damping Lambda_f, block-Jacobi
 // preconditioner (inverse of the damped diagonal blocks), rhs = -b.
@@ -90,7 +94,7 @@ void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, 
                           const double* lambda_f, const double* x, double* w, double* y, hipStream_t s,
                           const uint32_t* chunks = nullptr, int nchunks = 0, const uint32_t* cm_ptv = nullptr,
                           const double* Jcm = nullptr, bool staged = false, const double* Xcm = nullptr,
-                          const double2* obs_cm = nullptr);
+                          const double2* obs_cm = nullptr, const TileOwners* own = nullptr);
 // Matrix-free product (Xcm non-null, with chunks and cm_ptv): both passes
 // recompute the blocks' Jacobian rows instead of reading J; Xcm / obs_cm are
 // the camera-major copies of the blocks' points / observations (obs_cm only
@@ -149,7 +153,7 @@ void launch_plus(const DevProblem& p, const double* df, const double* dX, const 
 // image-pair tiles).
 void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
                         const double* J, const double* Linv, double* Z, const DevPairTile* ptiles, int nptiles,
-                        const uint2* pairs, double* S, bool with_u, hipStream_t s);
+                        const uint2* pairs, double* S, bool with_u, hipStream_t s, const PairFlush* pflush = nullptr);
 // S_kk += Lambda_k on parameter slots, S_kk = 1 on non-parameter slots.
 void launch_dense_finalize(const DevProblem& p, const double* lambda_f, double* S, hipStream_t s);
 
@@ -173,7 +177,7 @@ void launch_cg_step(double* x, const double* p, double* r, const double* q, cons
 // blocks, and of the variable points (g_p from Vg), atomically max-ed into
 // out[0] (non-negative doubles, as bit patterns).
 void launch_grad_f(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm, const double2* r,
-                   const double* J, double* g, hipStream_t s);
+                   const double* J, double* g, hipStream_t s, const TileOwners* own = nullptr);
 void launch_grad_max_f(const DevProblem& p, const double* g, double* out, hipStream_t s);
 void launch_grad_max_points(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg, double* out,
                             hipStream_t s);

@@ -1073,7 +1073,8 @@ __global__ __launch_bounds__(kBlock) void fblock_pair_kernel(DevProblem p, const
                                                               double* __restrict__ pose_blk,
                                                               double* __restrict__ cam_blk,
                                                               double* __restrict__ bvec,
-                                                              double* __restrict__ udiag) {
+                                                              double* __restrict__ udiag,
+                                                              double* __restrict__ part) {
   constexpr int NH = CT > 6 ? CT : 6;  // columns per half
   constexpr int NS = sym_size(NH), NA = NS + 2 * NH;
   __shared__ double sred[kBlock / 64][2][NA];
@@ -1155,6 +1156,10 @@ __global__ __launch_bounds__(kBlock) void fblock_pair_kernel(DevProblem p, const
   double v = sred[0][h][k];
 #pragma unroll
   for (int w = 1; w < kBlock / 64; ++w) v += sred[w][h][k];
+  if (part) {  // deterministic flush (owner_flush_kernel, FlushPair)
+    part[(size_t)blockIdx.x * kTilePartStride + t] = v;
+    return;
+  }
   const uint32_t img = tile.image, cam = p.img_cam[img];
   const int n = h ? CT : 6;
   if (h == 0 ? !(p.img_flags[img] & 1u) : !p.cam_var[cam]) return;
@@ -1180,6 +1185,130 @@ __device__ inline int64_t fslot(const DevProblem& p, uint32_t img, uint32_t cam,
   return m < 6 ? 6 * (int64_t)img + m : 6 * (int64_t)p.num_images + (int64_t)p.ct * cam + (m - 6);
 }
 
+// ---------------------------------------------------------------------------
+// Deterministic camera-side flush.  The tile kernels (one workgroup per
+// image-aligned tile of camera-major blocks) write their block-reduced sums
+// to TileOwners::part[tile][k] instead of adding them atomically into the
+// shared image / camera slots; owner_flush_kernel then sums each value over
+// its owner's tiles — an image's tiles, or the tiles of every image of a
+// camera — in one fixed order (lane-strided partial sums, then the wave's
+// butterfly) and adds the total to its destination, which no other workgroup
+// writes.  The LM's camera-side sums (S's image blocks, b, diag(U), the
+// Schur-Jacobi blocks, every Schur product) are then bitwise reproducible
+// run to run.  D: has(cam, k) whether value k belongs to an image (cam =
+// false) or a camera owner; put(cam, owner, k, v) its destination.
+// ---------------------------------------------------------------------------
+template <class D>
+__global__ __launch_bounds__(64) void owner_flush_kernel(D d, TileOwners o, int stride, int nimg) {
+  const int ow = blockIdx.x, lane = threadIdx.x;
+  const bool cam = ow >= nimg;
+  const uint32_t id = cam ? (uint32_t)(ow - nimg) : (uint32_t)ow;
+  const uint32_t t0 = cam ? o.cam_tile_off[id] : o.img_tile_off[id];
+  const uint32_t t1 = cam ? o.cam_tile_off[id + 1] : o.img_tile_off[id + 1];
+  if (t0 == t1) return;
+  for (int k = 0; k < stride; ++k) {
+    if (!d.has(cam, k)) continue;
+    double v = 0.0;
+    for (uint32_t t = t0 + lane; t < t1; t += 64) {
+      const uint32_t tile = cam ? o.cam_tiles[t] : t;
+      v += o.part[(size_t)tile * o.stride + k];
+    }
+    v = wave_sum(v);
+    if (lane == 0) d.put(cam, id, k, v);
+  }
+}
+
+template <class D>
+void launch_owner_flush(const D& d, const TileOwners& o, int stride, const DevProblem& p, hipStream_t s) {
+  const int n = p.num_images + p.num_cameras;
+  if (n > 0) hipLaunchKernelGGL(owner_flush_kernel<D>, dim3(n), dim3(64), 0, s, d, o, stride, p.num_images);
+}
+
+// y[f-slot] += v: F = 6 + CT values per tile (pose 0..5, camera 6..)
+struct FlushFVec {
+  DevProblem p;
+  double* y;
+  __device__ bool has(bool cam, int k) const { return cam ? k >= 6 : k < 6; }
+  __device__ void put(bool cam, uint32_t id, int k, double v) const {
+    if (!cam) {
+      if (p.img_flags[id] & 1u) y[6 * (size_t)id + k] += v;
+    } else if (p.cam_var[id]) {
+      y[6 * (size_t)p.num_images + (size_t)p.ct * id + (k - 6)] += v;
+    }
+  }
+};
+
+// fblock_dense_kernel's NU + F values: U's packed upper triangle over the
+// image's tangent columns (pose 0..5, camera 6..), then b.  Pose-pose and
+// pose-camera entries belong to the image, camera-camera ones to the camera.
+struct FlushDense {
+  DevProblem p;
+  double* S;
+  double* bvec;
+  double* udiag;
+  int F, NU;
+  __device__ void pair(int k, int* a, int* c) const {
+    int aa = 0, rem = k;
+    while (rem >= F - aa) { rem -= F - aa; ++aa; }
+    *a = aa;
+    *c = aa + rem;
+  }
+  __device__ bool has(bool cam, int k) const {
+    if (k >= NU + F) return false;
+    if (k >= NU) return cam ? k - NU >= 6 : k - NU < 6;
+    int a, c;
+    pair(k, &a, &c);
+    return cam ? a >= 6 : a < 6;
+  }
+  __device__ void put(bool cam, uint32_t id, int k, double v) const {
+    // camera owner: the camera's own slots only (a, c >= 6)
+    const uint32_t img = cam ? 0u : id, cm = cam ? id : p.img_cam[id];
+    const bool pv = !cam && (p.img_flags[img] & 1u), cv = p.cam_var[cm] != 0;
+    if (k >= NU) {
+      const int m = k - NU;
+      if (m < 6 ? pv : cv) bvec[fslot(p, img, cm, m)] += v;
+      return;
+    }
+    int a, c;
+    pair(k, &a, &c);
+    if (!((a < 6 ? pv : cv) && (c < 6 ? pv : cv))) return;
+    const int64_t ra = fslot(p, img, cm, a), rc = fslot(p, img, cm, c);
+    S[(ra <= rc ? ra * p.lds + rc : rc * p.lds + ra)] += v;
+    if (a == c) udiag[ra] += v;
+  }
+};
+
+// fblock_pair_kernel's 2 NA values: per half h (0 pose, 1 camera) the packed
+// upper Schur-Jacobi block over NH columns, then NH of b and NH of diag(U).
+struct FlushPair {
+  DevProblem p;
+  double* pose_blk;
+  double* cam_blk;
+  double* bvec;
+  double* udiag;
+  int NH, NS, NA;
+  __device__ bool has(bool cam, int t) const { return t < 2 * NA && (cam ? t >= NA : t < NA); }
+  __device__ void put(bool cam, uint32_t id, int t, double v) const {
+    const int h = cam ? 1 : 0, k = t - h * NA, n = h ? p.ct : 6;
+    if (h == 0 ? !(p.img_flags[id] & 1u) : !p.cam_var[id]) return;
+    if (k < NS) {
+      int a = 0, rem = k;
+      while (rem >= NH - a) { rem -= NH - a; ++a; }
+      const int c = a + rem;
+      if (c >= n) return;
+      if (h == 0)
+        pose_blk[(size_t)id * kSymPose + sym_index(a, c, 6)] += v;
+      else
+        cam_blk[(size_t)id * sym_size(p.ct) + sym_index(a, c, p.ct)] += v;
+      return;
+    }
+    const int m = (k - NS) % NH;
+    if (m >= n) return;
+    double* dst = k < NS + NH ? bvec : udiag;
+    dst[h == 0 ? 6 * (size_t)id + m : 6 * (size_t)p.num_images + (size_t)p.ct * id + m] += v;
+  }
+};
+
 // Exact (explicit S) path: one pass over an image tile's J rows giving
 //   U = sum J_f'J_f into S's image block (upper triangle, as dense_u_kernel),
 //   b = g - sum W V^-1 g_p = sum J_f'(r - J_p q_p), q_p = V_p^-1 g_p (point_prepare),
@@ -1194,7 +1323,8 @@ __global__ __launch_bounds__(kBlock) void fblock_dense_kernel(DevProblem p, cons
                                                                const double* __restrict__ J,
                                                                const double* __restrict__ q,
                                                                double* __restrict__ bvec,
-                                                               double* __restrict__ udiag, double* __restrict__ S) {
+                                                               double* __restrict__ udiag, double* __restrict__ S,
+                                                               double* __restrict__ part) {
   constexpr int F = 6 + CT, W = 9 + CT;
   constexpr int NU = F * (F + 1) / 2, NV = NU + F;
   __shared__ double sred[4 * NV];
@@ -1236,6 +1366,10 @@ __global__ __launch_bounds__(kBlock) void fblock_dense_kernel(DevProblem p, cons
   block_reduce<NV>(acc, sred);
   const int k = threadIdx.x;
   if (k >= NV) return;
+  if (part) {  // deterministic flush (owner_flush_kernel, FlushDense)
+    part[(size_t)blockIdx.x * kTilePartStride + k] = sred[k];
+    return;
+  }
   const uint32_t img = tile.image, cam = p.img_cam[img];
   const bool pv = p.img_flags[img] & 1u, cv = p.cam_var[cam] != 0;
   const double v = sred[k];
@@ -1598,7 +1732,7 @@ __global__ __launch_bounds__(kBlock) void schur_f_pass(DevProblem p, const DevTi
                                                         const double* __restrict__ Jcm,
                                                         const double* __restrict__ x,
                                                         const double* __restrict__ w,
-                                                        double* __restrict__ y) {
+                                                        double* __restrict__ y, double* __restrict__ part) {
   constexpr int NV = 6 + CT;
   __shared__ double sred[4 * NV];
   const DevTile tile = tiles[blockIdx.x];
@@ -1631,7 +1765,9 @@ __global__ __launch_bounds__(kBlock) void schur_f_pass(DevProblem p, const DevTi
   }
   block_reduce<NV>(acc, sred);
   const int k = threadIdx.x;
-  if (k < NV) {
+  if (k < NV && part) {
+    part[(size_t)blockIdx.x * kTilePartStride + k] = sred[k];
+  } else if (k < NV) {
     const uint32_t img = tile.image;
     if (k < 6) {
       if (p.img_flags[img] & 1u) atomicAdd(y + 6 * (size_t)img + k, sred[k]);
@@ -1651,7 +1787,7 @@ __global__ __launch_bounds__(kBlock) void schur_f_rows_kernel(DevProblem p, cons
                                                                const double* __restrict__ Jcm,
                                                                const double* __restrict__ x,
                                                                const double* __restrict__ w,
-                                                               double* __restrict__ y) {
+                                                               double* __restrict__ y, double* __restrict__ part) {
   constexpr int NV = 6 + CT, W = 9 + CT, W2 = 2 * W, LS = W2 | 1;
   __shared__ double sl[(kBlock / 64) * 32 * LS];
   __shared__ double sred[4 * NV];
@@ -1693,7 +1829,9 @@ __global__ __launch_bounds__(kBlock) void schur_f_rows_kernel(DevProblem p, cons
   }
   block_reduce<NV>(acc, sred);
   const int k = threadIdx.x;
-  if (k < NV) {
+  if (k < NV && part) {
+    part[(size_t)blockIdx.x * kTilePartStride + k] = sred[k];
+  } else if (k < NV) {
     if (k < 6) {
       if (p.img_flags[img] & 1u) atomicAdd(y + 6 * (size_t)img + k, sred[k]);
     } else if (p.cam_var[cam]) {
@@ -1893,7 +2031,8 @@ __global__ __launch_bounds__(kBlock) void pcg_camera_pass_mf(DevProblem p, const
                                                               const double* __restrict__ Xcm,
                                                               const double2* __restrict__ obs_cm,
                                                               const double* __restrict__ x,
-                                                              const double* __restrict__ w, double* __restrict__ y) {
+                                                              const double* __restrict__ w, double* __restrict__ y,
+                                                              double* __restrict__ part) {
   constexpr int NV = 6 + CT;
   __shared__ double sred[4 * NV];
   const DevTile tile = tiles[blockIdx.x];
@@ -1938,7 +2077,9 @@ __global__ __launch_bounds__(kBlock) void pcg_camera_pass_mf(DevProblem p, const
   }
   block_reduce<NV>(acc, sred);
   const int k = threadIdx.x;
-  if (k < NV) {
+  if (k < NV && part) {
+    part[(size_t)blockIdx.x * kTilePartStride + k] = sred[k];
+  } else if (k < NV) {
     if (k < 6) {
       if (p.img_flags[img] & 1u) atomicAdd(y + 6 * (size_t)img + k, sred[k]);
     } else if (p.cam_var[cam]) {
@@ -2078,7 +2219,8 @@ template <int CT>
 __global__ __launch_bounds__(kBlock) void grad_f_kernel(DevProblem p, const DevTile* __restrict__ tiles,
                                                          const uint32_t* __restrict__ cm_perm,
                                                          const double2* __restrict__ rr,
-                                                         const double* __restrict__ J, double* __restrict__ g) {
+                                                         const double* __restrict__ J, double* __restrict__ g,
+                                                         double* __restrict__ part) {
   constexpr int F = 6 + CT, W = 9 + CT;
   __shared__ double sred[4 * F];
   const DevTile tile = tiles[blockIdx.x];
@@ -2097,6 +2239,10 @@ __global__ __launch_bounds__(kBlock) void grad_f_kernel(DevProblem p, const DevT
   block_reduce<F>(acc, sred);
   const int k = threadIdx.x;
   if (k >= F) return;
+  if (part) {
+    part[(size_t)blockIdx.x * kTilePartStride + k] = sred[k];
+    return;
+  }
   const uint32_t img = tile.image, cam = p.img_cam[img];
   if (k < 6 ? !(p.img_flags[img] & 1u) : !p.cam_var[cam]) return;
   atomicAdd(g + fslot(p, img, cam, k), sred[k]);
@@ -2707,7 +2853,8 @@ __global__ __launch_bounds__(kBlock) void schur_z_kernel(DevProblem p, const dou
 template <int CT, bool XMAP = true, bool NTB = false>
 __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const DevPairTile* __restrict__ tiles,
                                                               int ntiles, const uint2* __restrict__ pairs,
-                                                              const double* __restrict__ Z, double* __restrict__ S) {
+                                                              const double* __restrict__ Z, double* __restrict__ S,
+                                                              PairFlush pf) {
   constexpr int F = 6 + CT, ZN = 3 * F;
   const int G = (ntiles + 3) / 4;
   const int per = (G + 7) / 8;
@@ -2753,6 +2900,14 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
       vb = on ? Z[(size_t)pr.y * ZN + off] : 0.0;
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, acc, 0, 0, 0);
   }
+  if (pf.pslot) {
+    const int32_t ps = pf.pslot[t];
+    if (ps >= 0) {  // summed with the block's other tiles (schur_pairs_flush_kernel)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pf.part[(size_t)ps * 256 + r * 64 + lane] = acc[r];
+      return;
+    }
+  }
   const uint32_t ia = tl.ia, ib = tl.ib;
   const uint32_t ca = p.img_cam[ia], cb = p.img_cam[ib];
   const bool pa = p.img_flags[ia] & 1u, pb = p.img_flags[ib] & 1u;
@@ -2766,6 +2921,11 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
     if (!va || !vb) continue;
     const int64_t ra = fslot(p, ia, ca, mrow), rb = fslot(p, ib, cb, ncol);
     const double v = acc[r];
+    if (pf.pslot) {  // the block's only tile (ia != ib, cameras not shared): ra != rb, one writer
+      double* e = S + (ra < rb ? ra * p.lds + rb : rb * p.lds + ra);
+      *e -= v;
+      continue;
+    }
     if (tl.self) {
       if (ra <= rb) atomicAdd(S + ra * p.lds + rb, -v);
     } else if (ra < rb) {
@@ -2776,6 +2936,36 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
       atomicAdd(S + ra * p.lds + ra, -2.0 * v);
     }
   }
+}
+
+// The pair tiles' partial blocks summed per S block in list order and
+// subtracted (one workgroup per block, thread (m, n) of the 16 x 16 tile).
+// Diagonal blocks (ia == ib) take the upper triangle: a self tile's Z_a Z_a'
+// as is, a same-image tile's Z_a Z_b' + its transpose (a pair a != b of one
+// image lands on both (m, n) and (n, m)).  Cameras are not shared (the
+// condition of the deterministic route), so every (m, n) of an off-diagonal
+// block is a distinct S element.
+__device__ inline int mfma_d_index(int m, int n) { return (m >> 2) * 64 + ((m & 3) << 4) + n; }
+
+template <int CT>
+__global__ __launch_bounds__(256) void schur_pairs_flush_kernel(DevProblem p, PairFlush pf, double* __restrict__ S) {
+  constexpr int F = 6 + CT;
+  const uint4 d = pf.dest[blockIdx.x];
+  const int m = threadIdx.x >> 4, n = threadIdx.x & 15;
+  if (m >= F || n >= F) return;
+  const uint32_t ia = d.x, ib = d.y;
+  if (ia == ib && m > n) return;
+  double v = 0.0;
+  for (uint32_t k = 0; k < d.w; ++k) {
+    const double* a = pf.part + (size_t)(d.z + k) * 256;
+    v += (ia == ib && !pf.self[d.z + k]) ? a[mfma_d_index(m, n)] + a[mfma_d_index(n, m)] : a[mfma_d_index(m, n)];
+  }
+  const uint32_t ca = p.img_cam[ia], cb = p.img_cam[ib];
+  const bool va = m < 6 ? (p.img_flags[ia] & 1u) : p.cam_var[ca] != 0;
+  const bool vb = n < 6 ? (p.img_flags[ib] & 1u) : p.cam_var[cb] != 0;
+  if (!va || !vb) return;
+  const int64_t ra = fslot(p, ia, ca, m), rb = fslot(p, ib, cb, n);
+  S[ra <= rb ? ra * p.lds + rb : rb * p.lds + ra] -= v;
 }
 
 // schur_pairs_variant 6: per block the record JG_a = [J_f,a (2 x F, row-major),
@@ -3314,7 +3504,7 @@ void launch_point_prepare(const DevProblem& p, const DevPoint* vp, int64_t npv, 
 
 void launch_fblock_dense(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
                          const uint32_t* cm_ptv, const double2* r, const double* J, const double* q, double* b,
-                         double* udiag, double* S, hipStream_t s) {
+                         double* udiag, double* S, hipStream_t s, const TileOwners* own) {
   if (ntiles == 0) return;
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
@@ -3326,13 +3516,18 @@ void launch_fblock_dense(const DevProblem& p, const DevTile* tiles, int ntiles, 
     }
 #endif
     hipLaunchKernelGGL(fblock_dense_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, cm_ptv, r, J, q,
-                       b, udiag, S);
+                       b, udiag, S, own ? own->part : nullptr);
+    if (own) {
+      constexpr int F = 6 + CT, NU = F * (F + 1) / 2;
+      static_assert(NU + F <= kTilePartStride, "tile partial stride");
+      launch_owner_flush(FlushDense{p, S, b, udiag, F, NU}, *own, NU + F, p, s);
+    }
   });
 }
 
 void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
                    const double2* r, const double* J, const double* Jcm, const double* Vg, const double* Vinv,
-                   double* pose_blk, double* cam_blk, double* b, double* udiag, hipStream_t s) {
+                   double* pose_blk, double* cam_blk, double* b, double* udiag, hipStream_t s, const TileOwners* own) {
   if (ntiles == 0) return;
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
@@ -3344,7 +3539,12 @@ void launch_fblock(const DevProblem& p, const DevTile* tiles, int ntiles, const 
     }
 #endif
     hipLaunchKernelGGL(fblock_pair_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, Jcm, Vg,
-                         Vinv, pose_blk, cam_blk, b, udiag);
+                         Vinv, pose_blk, cam_blk, b, udiag, own ? own->part : nullptr);
+    if (own) {
+      constexpr int NH = CT > 6 ? CT : 6, NS = sym_size(NH), NA = NS + 2 * NH;
+      static_assert(2 * NA <= kTilePartStride, "tile partial stride");
+      launch_owner_flush(FlushPair{p, pose_blk, cam_blk, b, udiag, NH, NS, NA}, *own, 2 * NA, p, s);
+    }
   });
 }
 
@@ -3380,8 +3580,9 @@ void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, 
                           int ntiles, const uint32_t* cm_perm, const double* J, const double* Vinv,
                           const double* lambda_f, const double* x, double* w, double* y, hipStream_t s,
                           const uint32_t* chunks, int nchunks, const uint32_t* cm_ptv, const double* Jcm,
-                          bool staged, const double* Xcm, const double2* obs_cm) {
+                          bool staged, const double* Xcm, const double2* obs_cm, const TileOwners* own) {
   (void)hipMemsetAsync(y, 0, sizeof(double) * p.nf, s);
+  double* part = own ? own->part : nullptr;
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
     if (Xcm && chunks && cm_ptv && (p.loss_type == 0 || obs_cm)) {
@@ -3393,12 +3594,13 @@ void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, 
                              p, chunks, nchunks, Vinv, x, w);
         if (ntiles > 0)
           hipLaunchKernelGGL((pcg_camera_pass_mf<CT, LOSS>), dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_ptv, Xcm,
-                             obs_cm, x, w, y);
+                             obs_cm, x, w, y, part);
       };
       if (p.loss_type == 0)
         go(std::integral_constant<int, 0>{});
       else
         go(std::integral_constant<int, 1>{});
+      if (own && ntiles > 0) launch_owner_flush(FlushFVec{p, y}, *own, 6 + CT, p, s);
       return;
     }
     if (npv > 0 && chunks && nchunks > 0)
@@ -3408,10 +3610,12 @@ void launch_schur_product(const DevProblem& p, const DevPoint* vp, int64_t npv, 
       hipLaunchKernelGGL(schur_point_pass<CT>, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, J,
                          Vinv, x, w);
     if (ntiles > 0 && Jcm && cm_ptv && staged)
-      hipLaunchKernelGGL(schur_f_rows_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_ptv, Jcm, x, w, y);
+      hipLaunchKernelGGL(schur_f_rows_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_ptv, Jcm, x, w, y,
+                         part);
     else if (ntiles > 0)
       hipLaunchKernelGGL(schur_f_pass<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, cm_ptv, J, Jcm, x, w,
-                         y);
+                         y, part);
+    if (own && ntiles > 0) launch_owner_flush(FlushFVec{p, y}, *own, 6 + CT, p, s);
   });
   if (lambda_f)
     hipLaunchKernelGGL(add_diag_kernel, dim3(grid_for(p.nf, kBlock)), dim3(kBlock), 0, s, lambda_f, x, y, p.nf);
@@ -3518,7 +3722,8 @@ void launch_plus(const DevProblem& p, const double* df, const double* dX, const 
 
 void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
                         const double* J, const double* Linv, double* Z, const DevPairTile* ptiles, int nptiles,
-                        const uint2* pairs, double* S, bool with_u, hipStream_t s) {
+                        const uint2* pairs, double* S, bool with_u, hipStream_t s, const PairFlush* pflush) {
+  const PairFlush nof{nullptr, nullptr, nullptr, nullptr, 0};
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
     if (with_u && ntiles > 0)
@@ -3547,14 +3752,20 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
 #ifdef MI_BA_AB_VARIANTS
       if (p.svariant == 5)
         hipLaunchKernelGGL((schur_pairs_kernel<CT, false, true>), dim3(G), dim3(kBlock), 0, s, p, ptiles, nptiles,
-                           pairs, Z, S);
+                           pairs, Z, S, nof);
       else
 #endif
-      if (p.svariant == 4)
+      if (p.svariant == 4) {
+        // pflush: the image-block tile order's deterministic route
+        const PairFlush& pf = pflush ? *pflush : nof;
         hipLaunchKernelGGL((schur_pairs_kernel<CT, false>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs,
-                           Z, S);
-      else
-        hipLaunchKernelGGL(schur_pairs_kernel<CT>, dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs, Z, S);
+                           Z, S, pf);
+        if (pf.pslot && pf.ndest > 0)
+          hipLaunchKernelGGL(schur_pairs_flush_kernel<CT>, dim3(pf.ndest), dim3(256), 0, s, p, pf, S);
+      } else {
+        hipLaunchKernelGGL(schur_pairs_kernel<CT>, dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs, Z, S,
+                           nof);
+      }
     }
   });
 }
@@ -3586,11 +3797,13 @@ void launch_cg_step(double* x, const double* pv, double* r, const double* q, con
 }
 
 void launch_grad_f(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm, const double2* r,
-                   const double* J, double* g, hipStream_t s) {
+                   const double* J, double* g, hipStream_t s, const TileOwners* own) {
   if (ntiles == 0) return;
   dispatch_ct(p.ct, [&](auto c) {
     constexpr int CT = decltype(c)::value;
-    hipLaunchKernelGGL(grad_f_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, g);
+    hipLaunchKernelGGL(grad_f_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, r, J, g,
+                       own ? own->part : nullptr);
+    if (own) launch_owner_flush(FlushFVec{p, g}, *own, 6 + CT, p, s);
   });
 }
 

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <numeric>
+#include <unordered_map>
 
 #include "../../include/mi_ba.h"
 #include "ba_math.h"
@@ -351,6 +352,53 @@ mi_ba_status order_block_tiles(mi_ba_context* ctx) {
   if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
       hipMemcpy(ctx->ptiles_blk.ptr, tb.data(), tb.size() * sizeof(DevPairTile), hipMemcpyHostToDevice) != hipSuccess)
     return MI_BA_ERR_HIP;
+  // The deterministic route (PairFlush): each S block written by one tile is
+  // written directly, every other block (diagonal blocks, image pairs of
+  // several tiles) summed from per-tile partials in tile order.  Needs every
+  // camera on at most one image: a shared camera's columns gather many image
+  // pairs' tiles, which stay on float atomics.
+  ctx->pflush_ok = false;
+  {
+    const mi_ba_problem* p = &ctx->problem;
+    std::vector<int> per_cam(p->num_cameras, 0);
+    bool distinct = true;
+    for (int i = 0; i < p->num_images && distinct; ++i) distinct = ++per_cam[p->image_camera[i]] <= 1;
+    if (!distinct) return MI_BA_OK;
+  }
+  std::unordered_map<uint64_t, uint32_t> didx;
+  std::vector<std::vector<uint32_t>> dtiles;
+  std::vector<uint2> dkey;
+  for (uint32_t k = 0; k < (uint32_t)tb.size(); ++k) {
+    const uint64_t key = (uint64_t)tb[k].ia << 32 | tb[k].ib;
+    auto it = didx.find(key);
+    if (it == didx.end()) {
+      it = didx.emplace(key, (uint32_t)dtiles.size()).first;
+      dtiles.emplace_back();
+      dkey.push_back(make_uint2(tb[k].ia, tb[k].ib));
+    }
+    dtiles[it->second].push_back(k);
+  }
+  std::vector<int32_t> ps(tb.size(), -1);
+  std::vector<uint4> dest;
+  std::vector<uint8_t> self;
+  for (size_t d = 0; d < dtiles.size(); ++d) {
+    if (dkey[d].x != dkey[d].y && dtiles[d].size() == 1) continue;  // direct
+    dest.push_back(make_uint4(dkey[d].x, dkey[d].y, (uint32_t)self.size(), (uint32_t)dtiles[d].size()));
+    for (uint32_t k : dtiles[d]) {
+      ps[k] = (int32_t)self.size();
+      self.push_back(tb[k].self ? 1 : 0);
+    }
+  }
+  if (ctx->pslot.alloc(ps.size()) || ctx->spart.alloc(std::max<size_t>(1, self.size()) * 256) ||
+      ctx->pdest.alloc(std::max<size_t>(1, dest.size())) || ctx->pself.alloc(std::max<size_t>(1, self.size())))
+    return MI_BA_ERR_OUT_OF_MEMORY;
+  if (hipMemcpy(ctx->pslot.ptr, ps.data(), ps.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      (!dest.empty() && hipMemcpy(ctx->pdest.ptr, dest.data(), dest.size() * sizeof(uint4), hipMemcpyHostToDevice) !=
+                            hipSuccess) ||
+      (!self.empty() && hipMemcpy(ctx->pself.ptr, self.data(), self.size(), hipMemcpyHostToDevice) != hipSuccess))
+    return MI_BA_ERR_HIP;
+  ctx->npdest = (int)dest.size();
+  ctx->pflush_ok = true;
   return MI_BA_OK;
 }
 
@@ -552,6 +600,29 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
     if (nb && (hipMemcpy(ctx->cm_perm.ptr, perm.data(), nb * 4, hipMemcpyHostToDevice) ||
                hipMemcpy(ctx->tiles.ptr, tl.data(), tl.size() * sizeof(DevTile), hipMemcpyHostToDevice)))
       return fail(MI_BA_ERR_HIP);
+    // owners of the tile sums (deterministic flush): each image's tiles (a
+    // contiguous, image-sorted range) and each camera's, image then tile order
+    {
+      std::vector<uint32_t> ito(I + 1, 0), cto(C + 1, 0), ct;
+      for (const DevTile& x : tl) ++ito[x.image + 1];
+      for (int i = 0; i < I; ++i) ito[i + 1] += ito[i];
+      for (int i = 0; i < I; ++i) cto[p->image_camera[i] + 1] += ito[i + 1] - ito[i];
+      for (int c = 0; c < C; ++c) cto[c + 1] += cto[c];
+      ct.resize(tl.size());
+      std::vector<uint32_t> pos(cto.begin(), cto.end() - 1);
+      for (int i = 0; i < I; ++i)
+        for (uint32_t k = ito[i]; k < ito[i + 1]; ++k) ct[pos[p->image_camera[i]]++] = k;
+      if (ctx->img_tile_off.alloc(I + 1) || ctx->cam_tile_off.alloc(C + 1) ||
+          ctx->cam_tiles.alloc(std::max<size_t>(1, ct.size())) ||
+          ctx->tpart.alloc(std::max<size_t>(1, tl.size()) * kTilePartStride))
+        return fail(MI_BA_ERR_OUT_OF_MEMORY);
+      if (hipMemcpy(ctx->img_tile_off.ptr, ito.data(), ito.size() * 4, hipMemcpyHostToDevice) ||
+          hipMemcpy(ctx->cam_tile_off.ptr, cto.data(), cto.size() * 4, hipMemcpyHostToDevice) ||
+          (!ct.empty() && hipMemcpy(ctx->cam_tiles.ptr, ct.data(), ct.size() * 4, hipMemcpyHostToDevice)))
+        return fail(MI_BA_ERR_HIP);
+      ctx->owners_ = TileOwners{ctx->img_tile_off.ptr, ctx->cam_tile_off.ptr, ctx->cam_tiles.ptr, ctx->tpart.ptr,
+                                kTilePartStride};
+    }
     // camera-major point of each block, 0xffffffff for constant points: the
     // camera-block pass reads it coalesced instead of gathering obs_pt and
     // pt_var per block
@@ -1030,7 +1101,7 @@ mi_ba_status schur_product(mi_ba_context* ctx, const double* x, double* y) {
                        ctx->Vinv.ptr, ctx->rank == 0 ? ctx->lambda_f.ptr : nullptr, x, ctx->cg_w.ptr, y, ctx->stream,
                        ctx->pp_chunks ? ctx->pchunks.ptr : nullptr, ctx->npchunks,
                        ctx->pp_chunks ? ctx->cm_ptv.ptr : nullptr, ctx->pcg_jcm && !ctx->jcm_stale ? ctx->Jcm.ptr : nullptr,
-                       ctx->pcg_jcm == 2, xcm, xcm && ctx->obs_cm.ptr ? ctx->obs_cm.ptr : nullptr);
+                       ctx->pcg_jcm == 2, xcm, xcm && ctx->obs_cm.ptr ? ctx->obs_cm.ptr : nullptr, ctx->owners());
   if (ctx->sem) semantic_schur_product(ctx, x, y);
   if (ctx->gsba) gsba_schur_product(ctx, x, y);
   return allreduce(ctx, y, d.nf);
@@ -1144,7 +1215,7 @@ mi_ba_status gradient_reached(mi_ba_context* ctx, bool* reached) {
   // (PCG scratch, free between solves)
   double* g = ctx->cg_z.ptr;
   MI_HIP(hipMemsetAsync(g, 0, d.nf * 8, s));
-  launch_grad_f(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, g, s);
+  launch_grad_f(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, g, s, ctx->owners());
   if (ctx->sem) semantic_add_gradient(ctx, g);
   if (ctx->gsba) gsba_add_gradient(ctx, g);
   st = allreduce(ctx, g, d.nf);
@@ -1179,12 +1250,13 @@ void launch_schur_terms(mi_ba_context* ctx) {
   const DevProblem& d = ctx->dev;
   hipEvent_t stop;
   timer_begin(ctx, "schur_build", &stop);
+  const PairFlush pf{ctx->pslot.ptr, ctx->spart.ptr, ctx->pdest.ptr, ctx->pself.ptr, ctx->npdest};
   launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
                      d.svariant == 5 ? ctx->ptiles_xcd.ptr
                      : (d.svariant == 4 || d.svariant == 6) ? ctx->ptiles_blk.ptr
                                                             : ctx->ptiles.ptr,
                      d.svariant == 5 ? ctx->nptiles_xcd : ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, false,
-                     ctx->stream);
+                     ctx->stream, ctx->det_sums && ctx->pflush_ok ? &pf : nullptr);
   if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
   if (ctx->gsba) gsba_add_dense(ctx, ctx->S.ptr);
   timer_end(ctx, stop);
@@ -1413,12 +1485,11 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
       Phase ph_(ctx, "fblock");
       if (ctx->dense)
         launch_fblock_dense(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->cm_ptv.ptr, ctx->r.ptr, ctx->J.ptr,
-                            ctx->cg_w.ptr,
-                            ctx->bvec.ptr, ctx->udiag.ptr, ctx->S.ptr, s);
+                            ctx->cg_w.ptr, ctx->bvec.ptr, ctx->udiag.ptr, ctx->S.ptr, s, ctx->owners());
       else
         launch_fblock(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->r.ptr, ctx->J.ptr, pcg_jcm(ctx),
                       ctx->Vg.ptr, ctx->Vinv.ptr, ctx->pose_blk.ptr, ctx->cam_blk.ptr, ctx->bvec.ptr,
-                      ctx->udiag.ptr, s);
+                      ctx->udiag.ptr, s, ctx->owners());
       if (ctx->sem) semantic_add_fblock(ctx);
       if (ctx->gsba) gsba_add_fblock(ctx);
     }
@@ -2333,6 +2404,12 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   }
   if (std::strcmp(key, "cholesky_spin_log2") == 0 && value >= 0 && value <= 30) {
     ctx->chol.spin_log2 = value;
+    return MI_BA_OK;
+  }
+  // 1 (default): camera-side sums flushed per image / camera in a fixed order
+  // (bitwise reproducible LM); 0: float-atomic flushes
+  if (std::strcmp(key, "deterministic_sums") == 0 && (value == 0 || value == 1)) {
+    ctx->det_sums = value != 0;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_gemm_update") == 0 && (value == 0 || value == 1)) {

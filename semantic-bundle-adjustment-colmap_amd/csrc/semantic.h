@@ -79,6 +79,18 @@ struct SemanticState {
   DevArray<uint32_t> dcount;               // [model] their number
   int n_cu = 256;                          // compute units (the deferred pass's resident grid)
   int model_chunks[kNumModels + 1] = {};   // chunk range of each camera model
+  // deterministic sums: the flat pass's deferral masks ([tile][4] words),
+  // each pair's first tile and first static chunk, the deferred pass's chunk
+  // partials; the pairs of each image ((pair << 1) | side, pair order) and
+  // the pair-block contributions to each explicit S block
+  DevArray<unsigned long long> dmask;
+  DevArray<uint32_t> pair_tile0, pair_chunk0;
+  DevArray<double> cpart;                  // [static chunk][kPairVals]
+  DevArray<uint32_t> img_pairs_off, img_pairs;
+  DevArray<uint2> sblk;                    // S blocks (i <= j) the pairs touch
+  DevArray<uint32_t> sblk_off, sblk_ent;   // their contributions ((pair << 1) | i-is-second)
+  int nsblk = 0;
+  DevArray<double> mpart;                  // per-wave partials of the model cost change
 };
 
 mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem);

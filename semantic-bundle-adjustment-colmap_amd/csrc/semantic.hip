@@ -14,6 +14,8 @@
 // flush per tile).
 #include <hip/hip_runtime.h>
 
+#include <map>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -1487,8 +1489,7 @@ __device__ __forceinline__ int tile_depth_side(const SemArgs& a, const FlatBox& 
 template <int M, bool FAST, bool WS = false, bool LP = false, int COARSE = 0>
 __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const SemTile* __restrict__ tiles,
                                                                const PairConst* __restrict__ pcs,
-                                                               uint32_t* __restrict__ pair_cnt,
-                                                               uint32_t* __restrict__ dlist,
+                                                               unsigned long long* __restrict__ dmask,
                                                                double* __restrict__ cost_partial,
                                                                double* __restrict__ r_out,
                                                                int32_t* __restrict__ status_out,
@@ -1613,17 +1614,10 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
       }
     }
   }
-  // append the wave's deferred samples to the pair's region
+  // the wave's deferred samples as one mask word (tile-major, 4 words per
+  // tile): deferred_order_kernel lists them per pair in sample order
   const unsigned long long bal = __ballot(deferred);
-  if (bal) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(pair_cnt + t.pair, (uint32_t)__popcll(bal));
-    base = __shfl(base, 0, 64);
-    if (deferred) {
-      const uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-      dlist[a.pairs[t.pair].start + slot] = (uint32_t)(n - a.pairs[t.pair].start);
-    }
-  }
+  if (lane == 0) dmask[(size_t)blockIdx.x * (kBlock / 64) + (tid >> 6)] = bal;
   double v = cost;
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   if (lane == 0) sred[tid >> 6] = v;
@@ -1647,7 +1641,8 @@ __global__ __launch_bounds__(64, WPE) void semantic_deferred_kernel(SemArgs a, c
                                                               const PairConst* __restrict__ pcs,
                                                               const uint32_t* __restrict__ pair_cnt,
                                                               const uint32_t* __restrict__ dlist,
-                                                              double* __restrict__ pair_blk,
+                                                              const uint32_t* __restrict__ pair_chunk0,
+                                                              double* __restrict__ cpart,
                                                               double* __restrict__ J_out, int write_samples,
                                                               int32_t* __restrict__ status_out = nullptr) {
   __shared__ double sJ[64 * kSemRow];
@@ -1725,11 +1720,65 @@ __global__ __launch_bounds__(64, WPE) void semantic_deferred_kernel(SemArgs a, c
       }
       double acc = 0.0;
       for (int q = 0; q < rows; ++q) acc += sJ[q * kSemRow + ca] * sJ[q * kSemRow + cb];
-      atomicAdd(pair_blk + (size_t)ch.x * kPairStride + e, acc);
+      // the chunk's J'J / J'r, summed per pair in chunk order (pair_reduce_kernel)
+      cpart[((size_t)pair_chunk0[ch.x] + ch.y / 64) * kPairVals + e] = acc;
     }
   }
   __syncthreads();  // sJ / sbox are rewritten by the next chunk
   }
+}
+
+// The pair's deferred samples in sample order from the flat pass's wave masks
+// (one workgroup per pair; a pair's tiles are consecutive, 256 samples each
+// from the pair's start, so mask word w covers samples 64 w .. 64 w + 63):
+// popcounts, a workgroup scan, each set bit's offset.  pair_cnt = their
+// number.  Sample order makes every chunk of the deferred pass, hence every
+// pair block sum, the same run to run.
+__global__ __launch_bounds__(256) void deferred_order_kernel(const unsigned long long* __restrict__ dmask,
+                                                             const uint32_t* __restrict__ pair_tile0,
+                                                             const SemPair* __restrict__ pairs,
+                                                             uint32_t* __restrict__ pair_cnt,
+                                                             uint32_t* __restrict__ dlist) {
+  __shared__ uint32_t sc[256];
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const SemPair pr = pairs[p];
+  const uint32_t words = (pr.count + 63) / 64;
+  const unsigned long long* mk = dmask + (size_t)pair_tile0[p] * (kBlock / 64);
+  uint32_t base = 0;
+  for (uint32_t w0 = 0; w0 < words; w0 += 256) {
+    const uint32_t w = w0 + tid;
+    const unsigned long long m = w < words ? mk[w] : 0ull;
+    const uint32_t c = (uint32_t)__popcll(m);
+    sc[tid] = c;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {  // inclusive scan (Hillis-Steele)
+      const uint32_t v = tid >= off ? sc[tid - off] : 0u;
+      __syncthreads();
+      sc[tid] += v;
+      __syncthreads();
+    }
+    uint32_t o = base + sc[tid] - c;
+    for (unsigned long long r = m; r; r &= r - 1) dlist[pr.start + o++] = 64 * w + (uint32_t)__ffsll((long long)r) - 1;
+    base += sc[255];
+    __syncthreads();
+  }
+  if (tid == 0) pair_cnt[p] = base;
+}
+
+// Pair blocks from the deferred pass's chunk partials, summed in chunk order
+// (one workgroup per pair; a pair without deferred samples gets zeros: its
+// cleared samples have J = 0).
+__global__ __launch_bounds__(128) void pair_reduce_kernel(const uint32_t* __restrict__ pair_cnt,
+                                                          const uint32_t* __restrict__ pair_chunk0,
+                                                          const double* __restrict__ cpart,
+                                                          double* __restrict__ pair_blk) {
+  const int p = blockIdx.x, e = threadIdx.x;
+  if (e >= kPairVals) return;
+  const uint32_t nch = (pair_cnt[p] + 63) / 64;
+  const double* c = cpart + (size_t)pair_chunk0[p] * kPairVals + e;
+  double v = 0.0;
+  for (uint32_t j = 0; j < nch; ++j) v += c[(size_t)j * kPairVals];
+  pair_blk[(size_t)p * kPairStride + e] = v;
 }
 
 // The deferred pass's work list: the static list of every pair's possible
@@ -1828,84 +1877,141 @@ __device__ inline int sym12(int a, int b) {  // a <= b
 }
 
 // Fold pair blocks into the per-image Schur-Jacobi blocks, b, diag(U).
-__global__ void semantic_fblock_kernel(const SemPair* __restrict__ pairs, int npairs,
-                                       const double* __restrict__ pair_blk, double* __restrict__ pose_blk,
-                                       double* __restrict__ bvec, double* __restrict__ udiag) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= npairs) return;
-  const SemPair pr = pairs[k];
-  const double* B = pair_blk + (size_t)k * kPairStride;
-  for (int side = 0; side < 2; ++side) {
-    if (!(side == 0 ? pr.var1 : pr.var2)) continue;
-    const uint32_t img = side == 0 ? pr.i : pr.j;
-    const int base = side * 6;
-    int o = 0;
-    for (int a = 0; a < 6; ++a)
-      for (int b = a; b < 6; ++b, ++o) atomicAdd(pose_blk + 21 * (size_t)img + o, B[sym12(base + a, base + b)]);
-    for (int a = 0; a < 6; ++a) {
-      atomicAdd(bvec + 6 * (size_t)img + a, B[78 + base + a]);
-      atomicAdd(udiag + 6 * (size_t)img + a, B[sym12(base + a, base + a)]);
-    }
+// The pair blocks folded into their images' slots deterministically: each
+// image (or S block) sums its pairs in pair order (img_pairs / sblk_ent,
+// built once), no float atomics.  Entry (pair << 1) | side: the image is the
+// pair's first (side 0) or second (1) pose; a pose that is not variable takes
+// nothing.
+
+// Schur-Jacobi pose block (21), b (6) and diag(U) (6) of every image: one
+// 64-thread workgroup per image, thread e one of the 33 values.
+__global__ void semantic_fblock_kernel(const SemPair* __restrict__ pairs, const uint32_t* __restrict__ img_pairs_off,
+                                       const uint32_t* __restrict__ img_pairs, const double* __restrict__ pair_blk,
+                                       double* __restrict__ pose_blk, double* __restrict__ bvec,
+                                       double* __restrict__ udiag) {
+  const uint32_t img = blockIdx.x;
+  const int e = threadIdx.x;
+  if (e >= 33) return;
+  int a = 0, b = 0;
+  if (e < 21) {
+    int rem = e;
+    while (rem >= 6 - a) { rem -= 6 - a; ++a; }
+    b = a + rem;
+  } else {
+    a = b = (e - 21) % 6;
   }
+  double v = 0.0;
+  bool any = false;
+  for (uint32_t q = img_pairs_off[img]; q < img_pairs_off[img + 1]; ++q) {
+    const uint32_t k = img_pairs[q] >> 1, side = img_pairs[q] & 1u;
+    const SemPair pr = pairs[k];
+    if (!(side ? pr.var2 : pr.var1)) continue;
+    const double* B = pair_blk + (size_t)k * kPairStride;
+    const int base = 6 * (int)side;
+    v += e < 21 || e >= 27 ? B[sym12(base + a, base + b)] : B[78 + base + a];
+    any = true;
+  }
+  if (!any) return;
+  if (e < 21)
+    pose_blk[21 * (size_t)img + e] += v;
+  else if (e < 27)
+    bvec[6 * (size_t)img + a] += v;
+  else
+    udiag[6 * (size_t)img + a] += v;
 }
 
-// g += J'r of the pair's samples (its block's g part) on its two poses: the
-// raw gradient of the gradient tolerance test.
-__global__ void semantic_gradient_kernel(const SemPair* __restrict__ pairs, int npairs,
-                                         const double* __restrict__ pair_blk, double* __restrict__ g) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= npairs) return;
-  const SemPair pr = pairs[k];
-  const double* B = pair_blk + (size_t)k * kPairStride;
-  for (int side = 0; side < 2; ++side) {
-    if (!(side == 0 ? pr.var1 : pr.var2)) continue;
-    const uint32_t img = side == 0 ? pr.i : pr.j;
-    for (int a = 0; a < 6; ++a) atomicAdd(g + 6 * (size_t)img + a, B[78 + side * 6 + a]);
+// g += J'r of the pair blocks on the image's pose (the raw gradient of the
+// gradient tolerance test).
+__global__ void semantic_gradient_kernel(const SemPair* __restrict__ pairs, const uint32_t* __restrict__ img_pairs_off,
+                                         const uint32_t* __restrict__ img_pairs, const double* __restrict__ pair_blk,
+                                         double* __restrict__ g) {
+  const uint32_t img = blockIdx.x;
+  const int a = threadIdx.x;
+  if (a >= 6) return;
+  double v = 0.0;
+  for (uint32_t q = img_pairs_off[img]; q < img_pairs_off[img + 1]; ++q) {
+    const uint32_t k = img_pairs[q] >> 1, side = img_pairs[q] & 1u;
+    const SemPair pr = pairs[k];
+    if (!(side ? pr.var2 : pr.var1)) continue;
+    v += pair_blk[(size_t)k * kPairStride + 78 + 6 * side + a];
   }
+  g[6 * (size_t)img + a] += v;
 }
 
-// y += M x over the pair's two poses.
-__global__ void semantic_product_kernel(const SemPair* __restrict__ pairs, int npairs,
-                                        const double* __restrict__ pair_blk, const double* __restrict__ x,
-                                        double* __restrict__ y) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= npairs) return;
-  const SemPair pr = pairs[k];
-  const double* B = pair_blk + (size_t)k * kPairStride;
-  double xv[12];
-  for (int m = 0; m < 6; ++m) {
-    xv[m] = pr.var1 ? x[6 * (size_t)pr.i + m] : 0.0;
-    xv[6 + m] = pr.var2 ? x[6 * (size_t)pr.j + m] : 0.0;
-  }
-  for (int a = 0; a < 12; ++a) {
-    if (!(a < 6 ? pr.var1 : pr.var2)) continue;
+// y += M x on the image's pose rows: row (6 side + a) of each pair's M times
+// the pair's two poses of x.
+__global__ void semantic_product_kernel(const SemPair* __restrict__ pairs, const uint32_t* __restrict__ img_pairs_off,
+                                        const uint32_t* __restrict__ img_pairs, const double* __restrict__ pair_blk,
+                                        const double* __restrict__ x, double* __restrict__ y) {
+  const uint32_t img = blockIdx.x;
+  const int a = threadIdx.x;
+  if (a >= 6) return;
+  double v = 0.0;
+  bool any = false;
+  for (uint32_t q = img_pairs_off[img]; q < img_pairs_off[img + 1]; ++q) {
+    const uint32_t k = img_pairs[q] >> 1, side = img_pairs[q] & 1u;
+    const SemPair pr = pairs[k];
+    if (!(side ? pr.var2 : pr.var1)) continue;
+    const double* B = pair_blk + (size_t)k * kPairStride;
+    const int r = 6 * (int)side + a;
     double s = 0.0;
-    for (int b = 0; b < 12; ++b) s += B[a <= b ? sym12(a, b) : sym12(b, a)] * xv[b];
-    const uint32_t img = a < 6 ? pr.i : pr.j;
-    atomicAdd(y + 6 * (size_t)img + (a % 6), s);
+    for (int c = 0; c < 12; ++c) {
+      const bool vc = c < 6 ? pr.var1 : pr.var2;
+      const double xc = vc ? x[6 * (size_t)(c < 6 ? pr.i : pr.j) + c % 6] : 0.0;
+      s += B[r <= c ? sym12(r, c) : sym12(c, r)] * xc;
+    }
+    v += s;
+    any = true;
   }
+  if (any) y[6 * (size_t)img + a] += v;
 }
 
 // Pair blocks into the explicit reduced camera system (upper triangle,
-// row-major with leading dimension lds).
-__global__ void semantic_dense_kernel(const SemPair* __restrict__ pairs, int npairs,
+// row-major with leading dimension lds): one workgroup per 6 x 6 S block (i,
+// j), i <= j, thread (a, b); the block's contributions in pair order.  Entry
+// flag: diagonal block — image i is the pair's first (M11) or second (M22)
+// pose; off-diagonal — rows i are the pair's first pose (M[a][6 + b]) or its
+// second (M[6 + a][b]).
+__global__ void semantic_dense_kernel(const SemPair* __restrict__ pairs, const uint2* __restrict__ sblk,
+                                      const uint32_t* __restrict__ sblk_off, const uint32_t* __restrict__ sblk_ent,
                                       const double* __restrict__ pair_blk, int64_t lds, double* __restrict__ S) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)npairs * 144) return;
-  const int k = (int)(t / 144), e = (int)(t % 144);
-  const int a = e / 12, b = e % 12;
-  const SemPair pr = pairs[k];
-  const bool va = a < 6 ? pr.var1 : pr.var2, vb = b < 6 ? pr.var1 : pr.var2;
-  if (!va || !vb) return;
-  const double v = pair_blk[(size_t)k * kPairStride + (a <= b ? sym12(a, b) : sym12(b, a))];
-  const int64_t ra = 6 * (int64_t)(a < 6 ? pr.i : pr.j) + a % 6;
-  const int64_t rb = 6 * (int64_t)(b < 6 ? pr.i : pr.j) + b % 6;
-  if (ra <= rb) atomicAdd(S + ra * lds + rb, v);
+  const uint2 bl = sblk[blockIdx.x];
+  const int a = threadIdx.x / 6, b = threadIdx.x % 6;
+  if (threadIdx.x >= 36 || (bl.x == bl.y && a > b)) return;
+  double v = 0.0;
+  bool any = false;
+  for (uint32_t q = sblk_off[blockIdx.x]; q < sblk_off[blockIdx.x + 1]; ++q) {
+    const uint32_t k = sblk_ent[q] >> 1, f = sblk_ent[q] & 1u;
+    const SemPair pr = pairs[k];
+    int A, B;
+    bool va, vb;
+    if (bl.x == bl.y) {
+      A = 6 * (int)f + a;
+      B = 6 * (int)f + b;
+      va = vb = f ? pr.var2 : pr.var1;
+    } else if (!f) {
+      A = a;
+      B = 6 + b;
+      va = pr.var1;
+      vb = pr.var2;
+    } else {
+      A = 6 + a;
+      B = b;
+      va = pr.var2;
+      vb = pr.var1;
+    }
+    if (!va || !vb) continue;
+    v += pair_blk[(size_t)k * kPairStride + (A <= B ? sym12(A, B) : sym12(B, A))];
+    any = true;
+  }
+  if (any) S[(6 * (int64_t)bl.x + a) * lds + 6 * (int64_t)bl.y + b] += v;
 }
 
+// model cost change -(g'd + d'Md/2) per pair, one partial per wave (summed
+// by launch_sum in a fixed order)
 __global__ void semantic_model_kernel(const SemPair* __restrict__ pairs, int npairs,
                                       const double* __restrict__ pair_blk, const double* __restrict__ df,
-                                      double* __restrict__ out) {
+                                      double* __restrict__ partial) {
   const int k = blockIdx.x * 64 + threadIdx.x;
   double v = 0.0;
   if (k < npairs) {
@@ -1926,7 +2032,7 @@ __global__ void semantic_model_kernel(const SemPair* __restrict__ pairs, int npa
     v = -(gd + 0.5 * dMd);
   }
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  if ((threadIdx.x & 63) == 0) atomicAdd(out, v);
+  if (threadIdx.x == 0) partial[blockIdx.x] = v;
 }
 
 // ExportSemanticErrorToCSV (semantic_bundle_adjustment.cc:908-1019): every
@@ -2143,6 +2249,72 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
       S->chunks.alloc(std::max<size_t>(1, chunks.size())) || S->dchunks.alloc(std::max<size_t>(1, chunks.size())) ||
       S->dcount.alloc(kNumModels))
     return MI_BA_ERR_OUT_OF_MEMORY;
+  // deterministic sums (see SemanticState)
+  {
+    const int np = S->npairs;
+    std::vector<uint32_t> tile0(std::max(1, np), 0), chunk0(std::max(1, np), 0);
+    for (size_t k = tiles.size(); k-- > 0;) tile0[tiles[k].pair] = (uint32_t)k;  // first tile of each pair
+    std::vector<uint32_t> nchk(std::max(1, np), 0);
+    for (const uint2& c : chunks) ++nchk[c.x];
+    for (size_t k = chunks.size(); k-- > 0;) chunk0[chunks[k].x] = (uint32_t)k;
+    // a pair's tiles and chunks are consecutive (grouped by model, pair order inside)
+    for (int k = 0; k < np; ++k) {
+      const SemPair& pr = S->pairs_host[k];
+      const uint32_t nt = (pr.count + kBlock - 1) / kBlock;
+      for (uint32_t j = 0; j < nt; ++j)
+        if (tiles[tile0[k] + j].pair != (uint32_t)k || tiles[tile0[k] + j].start != pr.start + j * kBlock)
+          return MI_BA_ERR_HIP;
+      for (uint32_t j = 0; j < nchk[k]; ++j)
+        if (chunks[chunk0[k] + j].x != (uint32_t)k || chunks[chunk0[k] + j].y != 64 * j) return MI_BA_ERR_HIP;
+    }
+    // the pairs of each image, and the S blocks' contributions
+    std::vector<uint32_t> ipo(I + 1, 0), ip;
+    for (int k = 0; k < np; ++k) {
+      ++ipo[S->pairs_host[k].i + 1];
+      ++ipo[S->pairs_host[k].j + 1];
+    }
+    for (int i = 0; i < I; ++i) ipo[i + 1] += ipo[i];
+    ip.resize(ipo[I]);
+    {
+      std::vector<uint32_t> pos(ipo.begin(), ipo.end() - 1);
+      for (int k = 0; k < np; ++k) {
+        ip[pos[S->pairs_host[k].i]++] = (uint32_t)k << 1;
+        ip[pos[S->pairs_host[k].j]++] = (uint32_t)k << 1 | 1u;
+      }
+    }
+    std::map<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>> blocks;
+    for (int k = 0; k < np; ++k) {
+      const SemPair& pr = S->pairs_host[k];
+      blocks[{pr.i, pr.i}].push_back((uint32_t)k << 1);       // M11 on image i's diagonal block
+      blocks[{pr.j, pr.j}].push_back((uint32_t)k << 1 | 1u);  // M22 on image j's
+      if (pr.i < pr.j)
+        blocks[{pr.i, pr.j}].push_back((uint32_t)k << 1);      // rows i (first), columns j
+      else
+        blocks[{pr.j, pr.i}].push_back((uint32_t)k << 1 | 1u); // rows j (second), columns i
+    }
+    std::vector<uint2> sb;
+    std::vector<uint32_t> so(1, 0), se;
+    for (auto& b : blocks) {
+      sb.push_back(make_uint2(b.first.first, b.first.second));
+      se.insert(se.end(), b.second.begin(), b.second.end());
+      so.push_back((uint32_t)se.size());
+    }
+    S->nsblk = (int)sb.size();
+    if (S->dmask.alloc(std::max<size_t>(1, tiles.size()) * (kBlock / 64)) || S->pair_tile0.alloc(tile0.size()) ||
+        S->pair_chunk0.alloc(chunk0.size()) || S->cpart.alloc(std::max<size_t>(1, chunks.size()) * kPairVals) ||
+        S->img_pairs_off.alloc(ipo.size()) || S->img_pairs.alloc(std::max<size_t>(1, ip.size())) ||
+        S->sblk.alloc(std::max<size_t>(1, sb.size())) || S->sblk_off.alloc(so.size()) ||
+        S->sblk_ent.alloc(std::max<size_t>(1, se.size())) || S->mpart.alloc((std::max(1, np) + 63) / 64))
+      return MI_BA_ERR_OUT_OF_MEMORY;
+    if (hipMemcpy(S->pair_tile0.ptr, tile0.data(), tile0.size() * 4, hipMemcpyHostToDevice) ||
+        hipMemcpy(S->pair_chunk0.ptr, chunk0.data(), chunk0.size() * 4, hipMemcpyHostToDevice) ||
+        hipMemcpy(S->img_pairs_off.ptr, ipo.data(), ipo.size() * 4, hipMemcpyHostToDevice) ||
+        (!ip.empty() && hipMemcpy(S->img_pairs.ptr, ip.data(), ip.size() * 4, hipMemcpyHostToDevice)) ||
+        (!sb.empty() && hipMemcpy(S->sblk.ptr, sb.data(), sb.size() * sizeof(uint2), hipMemcpyHostToDevice)) ||
+        hipMemcpy(S->sblk_off.ptr, so.data(), so.size() * 4, hipMemcpyHostToDevice) ||
+        (!se.empty() && hipMemcpy(S->sblk_ent.ptr, se.data(), se.size() * 4, hipMemcpyHostToDevice)))
+      return MI_BA_ERR_HIP;
+  }
   {
     int dev = 0, ncu = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) ||
@@ -2346,6 +2518,9 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
   if (ctx->sem_variant == 6) {
     const int ws = write_samples ? 1 | (ctx->sem_diag ? 2 : 0) | (ctx->sem_diag == 2 ? 4 : 0) : 0;
     auto deferred = [&](hipStream_t ds) -> mi_ba_status {
+      // each pair's deferred samples in sample order (pair_cnt, dlist)
+      hipLaunchKernelGGL(deferred_order_kernel, dim3(S->npairs), dim3(256), 0, ds, S->dmask.ptr, S->pair_tile0.ptr,
+                         S->pairs.ptr, S->pair_cnt.ptr, S->dlist.ptr);
       // the non-empty chunks, then a resident grid per model looping over them
       const int nall = S->model_chunks[kNumModels];
       const bool compact = ctx->sem_compact != 0;
@@ -2370,32 +2545,37 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
           constexpr int M = decltype(m)::value;
           if (ctx->sem_deferred_box)
             hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4, true>), dim3(grid), dim3(64), 0, ds, a, list,
-                               count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws,
-                               S->status.ptr);
+                               count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_chunk0.ptr, S->cpart.ptr, S->J.ptr,
+                               ws, S->status.ptr);
 #ifdef MI_BA_AB_VARIANTS
           // semantic_deferred_variant: 1 NB 2; 2 NB 2 at >= 5 waves per SIMD;
           // 3 NB 4 at >= 5; 4 NB 2 at >= 6 (register spills)
           else if (ctx->sem_dvar == 1)
             hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 2>), dim3(grid), dim3(64), 0, ds, a, list, count,
-                               pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws, S->status.ptr);
+                               pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_chunk0.ptr, S->cpart.ptr, S->J.ptr, ws,
+                               S->status.ptr);
           else if (ctx->sem_dvar == 2)
             hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 2, false, 5>), dim3(grid), dim3(64), 0, ds, a,
-                               list, count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws,
-                               S->status.ptr);
+                               list, count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_chunk0.ptr, S->cpart.ptr, S->J.ptr,
+                               ws, S->status.ptr);
           else if (ctx->sem_dvar == 3)
             hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4, false, 5>), dim3(grid), dim3(64), 0, ds, a,
-                               list, count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws,
-                               S->status.ptr);
+                               list, count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_chunk0.ptr, S->cpart.ptr, S->J.ptr,
+                               ws, S->status.ptr);
           else if (ctx->sem_dvar == 4)
             hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 2, false, 6>), dim3(grid), dim3(64), 0, ds, a,
-                               list, count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws,
-                               S->status.ptr);
+                               list, count, pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_chunk0.ptr, S->cpart.ptr, S->J.ptr,
+                               ws, S->status.ptr);
 #endif
           else
             hipLaunchKernelGGL((semantic_deferred_kernel<M, true, 4>), dim3(grid), dim3(64), 0, ds, a, list, count,
-                               pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_blk.ptr, S->J.ptr, ws, S->status.ptr);
+                               pcs, S->pair_cnt.ptr, S->dlist.ptr, S->pair_chunk0.ptr, S->cpart.ptr, S->J.ptr, ws,
+                               S->status.ptr);
         });
       }
+      // pair blocks from the chunk partials, in chunk order
+      hipLaunchKernelGGL(pair_reduce_kernel, dim3(S->npairs), dim3(128), 0, ds, S->pair_cnt.ptr, S->pair_chunk0.ptr,
+                         S->cpart.ptr, S->pair_blk.ptr);
       return MI_BA_OK;
     };
     for (int model = 0; model < kNumModels; ++model) {
@@ -2406,8 +2586,9 @@ mi_ba_status semantic_linearize(mi_ba_context* ctx, double* d_cost, bool write_s
         auto launch = [&](auto ws_, auto lp_, auto coarse_) {
           hipLaunchKernelGGL((semantic_flat_kernel<M, true, decltype(ws_)::value, decltype(lp_)::value,
                                                    decltype(coarse_)::value>),
-                             dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0, pcs, S->pair_cnt.ptr, S->dlist.ptr,
-                             S->partial.ptr + t0, S->r.ptr, S->status.ptr, S->J.ptr, ws);
+                             dim3(nt), dim3(kBlock), 0, s, a, S->tiles.ptr + t0, pcs,
+                             S->dmask.ptr + (size_t)t0 * (kBlock / 64), S->partial.ptr + t0, S->r.ptr, S->status.ptr,
+                             S->J.ptr, ws);
         };
         using T = std::true_type;
         using F = std::false_type;
@@ -2493,38 +2674,42 @@ void semantic_cost(mi_ba_context* ctx, const double* qt, const double* cam, doub
 
 void semantic_add_fblock(mi_ba_context* ctx) {
   SemanticState* S = ctx->sem;
-  if (!S->npairs) return;
-  hipLaunchKernelGGL(semantic_fblock_kernel, dim3((S->npairs + 63) / 64), dim3(64), 0, ctx->stream, S->pairs.ptr,
-                     S->npairs, S->pair_blk.ptr, ctx->pose_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr);
+  const int I = ctx->dev.num_images;
+  if (!S->npairs || I == 0) return;
+  hipLaunchKernelGGL(semantic_fblock_kernel, dim3(I), dim3(64), 0, ctx->stream, S->pairs.ptr, S->img_pairs_off.ptr,
+                     S->img_pairs.ptr, S->pair_blk.ptr, ctx->pose_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr);
 }
 
 void semantic_add_gradient(mi_ba_context* ctx, double* g) {
   SemanticState* S = ctx->sem;
-  if (!S->npairs) return;
-  hipLaunchKernelGGL(semantic_gradient_kernel, dim3((S->npairs + 63) / 64), dim3(64), 0, ctx->stream, S->pairs.ptr,
-                     S->npairs, S->pair_blk.ptr, g);
+  const int I = ctx->dev.num_images;
+  if (!S->npairs || I == 0) return;
+  hipLaunchKernelGGL(semantic_gradient_kernel, dim3(I), dim3(64), 0, ctx->stream, S->pairs.ptr, S->img_pairs_off.ptr,
+                     S->img_pairs.ptr, S->pair_blk.ptr, g);
 }
 
 void semantic_schur_product(mi_ba_context* ctx, const double* x, double* y) {
   SemanticState* S = ctx->sem;
-  if (!S->npairs) return;
-  hipLaunchKernelGGL(semantic_product_kernel, dim3((S->npairs + 63) / 64), dim3(64), 0, ctx->stream, S->pairs.ptr,
-                     S->npairs, S->pair_blk.ptr, x, y);
+  const int I = ctx->dev.num_images;
+  if (!S->npairs || I == 0) return;
+  hipLaunchKernelGGL(semantic_product_kernel, dim3(I), dim3(64), 0, ctx->stream, S->pairs.ptr, S->img_pairs_off.ptr,
+                     S->img_pairs.ptr, S->pair_blk.ptr, x, y);
 }
 
 void semantic_add_dense(mi_ba_context* ctx, double* S) {
   SemanticState* S_ = ctx->sem;
-  if (!S_->npairs) return;
-  const int64_t n = (int64_t)S_->npairs * 144;
-  hipLaunchKernelGGL(semantic_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
-                     S_->pairs.ptr, S_->npairs, S_->pair_blk.ptr, ctx->dev.lds, S);
+  if (!S_->npairs || S_->nsblk == 0) return;
+  hipLaunchKernelGGL(semantic_dense_kernel, dim3(S_->nsblk), dim3(64), 0, ctx->stream, S_->pairs.ptr, S_->sblk.ptr,
+                     S_->sblk_off.ptr, S_->sblk_ent.ptr, S_->pair_blk.ptr, ctx->dev.lds, S);
 }
 
 void semantic_model_cost(mi_ba_context* ctx, const double* df, double* d_out) {
   SemanticState* S = ctx->sem;
   if (!S->npairs) return;
-  hipLaunchKernelGGL(semantic_model_kernel, dim3((S->npairs + 63) / 64), dim3(64), 0, ctx->stream, S->pairs.ptr,
-                     S->npairs, S->pair_blk.ptr, df, d_out);
+  const int nw = (S->npairs + 63) / 64;
+  hipLaunchKernelGGL(semantic_model_kernel, dim3(nw), dim3(64), 0, ctx->stream, S->pairs.ptr, S->npairs,
+                     S->pair_blk.ptr, df, S->mpart.ptr);
+  launch_sum(S->mpart.ptr, nw, d_out, ctx->stream);
 }
 
 }  // namespace miba

@@ -1,0 +1,71 @@
+"""Bitwise run-to-run reproducibility of the GPU LM.
+
+Every camera-side sum of the solver is flushed in a fixed order instead of by
+float atomics: the tile passes' per-tile partials summed per image / camera
+(kernels.hip owner_flush_kernel: S's image blocks, b, diag(U), the
+Schur-Jacobi blocks, every implicit Schur product, the gradient), the
+explicit Schur pair tiles written once or summed per S block in tile order
+(schur_pairs_flush_kernel; cameras not shared between images), the semantic
+term's deferred samples listed in sample order and its pair blocks summed in
+chunk order, then per image / S block in pair order (semantic.hip
+deferred_order_kernel, pair_reduce_kernel and the owner kernels).  So two
+solves of one problem take the same steps with the same bits, on the exact
+(DENSE_SCHUR) and the iterative (ITERATIVE_SCHUR) path, with and without the
+semantic term.  "deterministic_sums" 0 restores the atomic flushes (same
+steps, costs equal to rounding).
+"""
+import numpy as np
+import pytest
+
+import mi_ba
+
+pytestmark = pytest.mark.gpu
+
+
+def scene(seed=5):
+    return mi_ba.generate_scene(mi_ba.synth_config(mi_ba.OPENCV, 60, 8000, track_length=8, rotation_range=0.05,
+                                                   extra=(-0.1, 0.01, 1e-4, -1e-4), seed=seed)).gauge()
+
+
+def semantic(sc):
+    depth, label = mi_ba.render_semantic(sc, 200, 200, plane_z=1.0, cell=0.2)
+    I = sc.num_images
+    pairs = np.array([(i, (i + d) % I) for i in range(I) for d in (1, 2)], np.int32)
+    return mi_ba.SemanticInput(depth, label, pairs, pixel_step=5)
+
+
+def run(sc, sem, solver, det=1):
+    opts = mi_ba.default_options(max_num_iterations=6, linear_solver_type=solver, semantic_weight=0.1)
+    b = sc.copy()
+    with mi_ba.Context(opts, b, sem) as ctx:
+        ctx.set_tuning("deterministic_sums", det)
+        s = ctx.solve()
+        ctx.writeback()
+    return s, b
+
+
+@pytest.mark.parametrize("solver", [mi_ba.SOLVER_DENSE_SCHUR, mi_ba.SOLVER_ITERATIVE_SCHUR])
+@pytest.mark.parametrize("case", ["geo", "sem"])
+def test_lm_bitwise_reproducible(gpu, case, solver):
+    sc = scene()
+    sem = semantic(sc) if case == "sem" else None
+    s0, a = run(sc, sem, solver)
+    s1, b = run(sc, sem, solver)
+    assert s0.num_successful_steps >= 3
+    assert (s1.num_successful_steps, s1.num_unsuccessful_steps, s1.num_linear_solver_iterations) == \
+        (s0.num_successful_steps, s0.num_unsuccessful_steps, s0.num_linear_solver_iterations)
+    assert s1.initial_cost == s0.initial_cost and s1.final_cost == s0.final_cost
+    for key in ("qvec", "tvec", "xyz", "camera_params"):
+        assert np.array_equal(getattr(a, key), getattr(b, key)), key
+
+
+@pytest.mark.parametrize("solver", [mi_ba.SOLVER_DENSE_SCHUR, mi_ba.SOLVER_ITERATIVE_SCHUR])
+def test_atomic_flush_takes_the_same_steps(gpu, solver):
+    """The float-atomic flushes (deterministic_sums 0) sum the same terms in
+    another order: the same steps, costs equal to rounding."""
+    sc = scene(seed=6)
+    sem = semantic(sc)
+    s0, _ = run(sc, sem, solver, det=1)
+    s1, _ = run(sc, sem, solver, det=0)
+    assert (s1.num_successful_steps, s1.num_unsuccessful_steps) == (s0.num_successful_steps, s0.num_unsuccessful_steps)
+    assert abs(s1.final_cost - s0.final_cost) <= 1e-10 * s0.final_cost
