@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <numeric>
 #include <unordered_map>
 
@@ -2072,14 +2073,13 @@ mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t wo
   if (ctx->comm_failed) return MI_BA_ERR_STATE;
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
-  // The set-up runs on a helper thread: RCCL's bootstrap can block inside the
-  // init call itself (and an abort of a half-initialised communicator can wait
-  // on it) while a peer has not joined, so the caller waits for the helper
-  // only until the deadline and then returns MI_BA_ERR_HIP with the context
-  // still single-rank.  An abandoned helper aborts the communicator it may
-  // still get (the process may also end with it blocked; it holds nothing of
-  // the context).  The communicator is non-blocking: its collectives are
-  // polled against the same deadline (comm_settle, comm_wait_stream).
+  // The set-up runs on a helper thread that the caller waits for only until
+  // the deadline; it then returns MI_BA_ERR_HIP with the context still
+  // single-rank.  Once the init call returns, the helper polls the
+  // non-blocking set-up against the same deadline and aborts the half-built
+  // communicator, so it never outlives the set-up by polling.  The
+  // communicator's collectives are polled against the deadline as well
+  // (comm_settle, comm_wait_stream).
   struct InitJob {
     std::mutex m;
     std::condition_variable cv;
@@ -2098,6 +2098,12 @@ mi_ba_status mi_ba_context_set_comm(mi_ba_context* ctx, int32_t rank, int32_t wo
       ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
       cfg.blocking = 0;
       ncclUniqueId uu = u;
+      // RCCL 2.27 runs the bootstrap inside this call even for a non-blocking
+      // communicator (and inside ncclGroupEnd when wrapped in a group, with
+      // NCCL_COMM_BLOCKING=0 too, measured): while a peer is missing it does
+      // not return, and has no timeout.  The helper then stays blocked here
+      // until the peer joins or the process ends (counted by
+      // mi_ba_comm_pending_setups); it holds nothing of the context.
       r = ncclCommInitRankConfig(&c, world, uu, rank, &cfg);
       // poll the non-blocking set-up until it completes, fails, the caller
       // gave up on it (abandoned) or the deadline passes: the last two end

@@ -429,6 +429,14 @@ int main(int argc, char** argv) {
     maps.width = W;
     for (auto& e : rec.images) {
       Image& im = e.second;
+      // overlapping views (GenerateReconstruction's tvec spread is 8x the
+      // 0.5-wide footprint): the maps are rendered at these poses, then the
+      // poses move by 0.02 per image so the semantic cost is not zero.  The
+      // numeric-diff step is 1e-3 of each coordinate (sqrt(eps) at 0): with
+      // identity rotations only translations of ~5 step across pixels
+      // (0.6 px here), so the gradient is not zero either
+      im.tvec[0] = 5.0 + 0.05 * (double)im.image_id;
+      im.tvec[1] = 5.0 + 0.03 * (double)im.image_id;
       std::vector<float> depth((size_t)H * W), label((size_t)H * W);
       for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
@@ -441,7 +449,7 @@ int main(int argc, char** argv) {
       maps.depth[im.name] = depth;
       maps.semantic[im.name] = label;
       rec.GetCamera(im.camera_id).params = {1200, 30, 30, 0};
-      im.tvec[0] += 0.002 * (double)im.image_id;
+      im.tvec[0] += 0.02 * (double)im.image_id;
     }
     char tmpl[] = "/tmp/sba_out_XXXXXX";
     const char* dir = mkdtemp(tmpl);

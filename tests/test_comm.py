@@ -102,4 +102,8 @@ def test_missing_peer_at_setup_returns_error(gpu):
                        timeout=180)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "missing peer: ERR_HIP" in p.stdout, p.stdout
-    assert "set-up helpers still running: 0" in p.stdout, p.stdout
+    # RCCL 2.27's init call blocks in its bootstrap while the peer is missing
+    # (no timeout, non-blocking config or not): the helper stays inside it,
+    # reported, and the context solves single-rank regardless
+    assert "set-up helpers still running: 1" in p.stdout, p.stdout
+    assert "single-rank solve after the failed set-up" in p.stdout, p.stdout

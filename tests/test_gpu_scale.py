@@ -153,9 +153,10 @@ def test_c2_iterative_schur_default_eta_converges_to_oracle(gpu):
     is tests/test_lm_semantics.py).  At the exact solution the Jacobi-scaled
     reduced camera system has a near-null direction (focal length against
     point depth); the camera-side difference of the two solutions must lie
-    along it: >= 99 % of its energy in the three smallest-eigenvalue
-    eigenvectors, whose eigenvalues are < 1e-4 of the median
-    (tests/valley.py)."""
+    along it: >= 99.9 % of its energy in the two smallest-eigenvalue
+    eigenvectors, whose eigenvalues are < 1e-5 of the median (measured:
+    lambda 7.6e-7 and 5.2e-6 against a median of 0.81; 99.45 % of the energy
+    on the first, 99.9995 % on the two; tests/valley.py)."""
     import valley
     sc = c2_scene()
     ref = mi_ba.default_options(max_num_iterations=100)
@@ -169,8 +170,8 @@ def test_c2_iterative_schur_default_eta_converges_to_oracle(gpu):
     rep = valley.valley_report(mi_ba.default_options(), a, b)
     print("valley: lambda", rep["lam"][:4], "median", np.median(rep["lam"]), "energy", rep["energy"][:4],
           "|d|", rep["norm"], "xyz diff", np.abs(a.xyz - b.xyz).max())
-    assert rep["lam"][2] < 1e-4 * np.median(rep["lam"])
-    assert rep["energy"][2] >= 0.99, rep["energy"][:4]
+    assert rep["lam"][1] < 1e-5 * np.median(rep["lam"])
+    assert rep["energy"][1] >= 0.999, rep["energy"][:4]
 
 
 @pytest.mark.parametrize("mf", [0, 1])

@@ -144,8 +144,13 @@ def test_oracle_gradient_tolerance_stops_flat_semantic_problem_at_iteration_zero
 @pytest.mark.parametrize("case", ["geo", "sem"])
 def test_pcg_matches_oracle_pcg_step_for_step(gpu, case, eta):
     """Small scene (30 images), ITERATIVE_SCHUR on both sides: the same
-    accept/reject sequence, CG iterations per LM iteration within +-1, final
-    cost within 1e-9 relative, points within 1e-7 (unit-cube scene)."""
+    accept/reject sequence, final cost within 1e-9 relative, points within
+    1e-7 (unit-cube scene).  CG iterations per LM iteration: within +-1 at the
+    default eta; at eta 1e-12 the q-termination test compares quadratic-model
+    changes at the last digits, so the count is rounding-sensitive there
+    (150-236 iterations; GPU/oracle differences measured up to 14, 6.3 %) and
+    is held to 10 % — the solves themselves are exact either way, which the
+    cost and point checks hold."""
     sc = small_scene()
     sem = None
     if case == "sem":
@@ -164,7 +169,7 @@ def test_pcg_matches_oracle_pcg_step_for_step(gpu, case, eta):
     for k, (valid, succ, cg) in ro.items():
         gv, gs, gcg = rec[k]
         assert (gv, gs) == (valid, succ), (k, rec[k], ro[k])
-        assert abs(gcg - cg) <= 1, (k, gcg, cg)
+        assert abs(gcg - cg) <= (1 if eta >= 1e-6 else max(1, 0.10 * cg)), (k, gcg, cg)
     assert abs(s_g.final_cost - s_o.final_cost) <= 1e-9 * s_o.final_cost, (s_g.final_cost, s_o.final_cost)
     assert np.abs(b.xyz - a.xyz).max() <= 1e-7
 
@@ -222,8 +227,14 @@ def test_tolerances_end_the_solve_where_the_oracle_does(gpu, solver):
     """Gradient / parameter / function tolerances set (a geometric problem
     whose gradient falls below 1e-3 and whose steps shrink below the
     parameter tolerance): the GPU stops on the same iteration as the oracle,
-    with CONVERGENCE, the same step counts and cost."""
+    with CONVERGENCE, the same step counts and cost.  Cameras constant: with
+    the focal length and distortion refined, the parameter-tolerance stop
+    comes after a run of rejected steps whose accept/reject decisions rest on
+    cost changes at rounding level — the oracle itself stops after 1 to 4
+    rejections when the start moves by 1e-13 — while with constant cameras it
+    is (5, 1) under every such perturbation."""
     sc = small_scene(seed=4)
+    sc.camera_constant = np.ones(sc.num_cameras, np.uint8)
     for tol in (dict(gradient_tolerance=1e-3), dict(parameter_tolerance=1e-7), dict(function_tolerance=1e-10)):
         kw = dict(max_num_iterations=60, linear_solver_type=solver, eta=1e-10, max_linear_solver_iterations=1000, **tol)
         s_o = oracle.solve(mi_ba.default_options(**kw), sc.copy())
