@@ -1463,6 +1463,67 @@ rocblas_status gemm_nt(rocblas_handle h, int m, int n, int k, const double* P, i
                        &one, C, ldc);
 }
 
+// rest_update 4: the tile pointer tables of every panel's trailing update
+// after the next panel's block column (CholWorkspace::bgroups / bptr), made
+// once per (A, n, lda, ex, tile, panel schedule) and kept for the context's
+// later factorisations.
+static bool batch_tables(CholWorkspace& ws, const std::vector<int>& ps, int n, double* A, int lda, int ex, int tile,
+                         hipStream_t s) {
+  std::vector<long long> key{(long long)(uintptr_t)A, n, lda, ex, tile};
+  key.insert(key.end(), ps.begin(), ps.end());
+  if (key == ws.bkey && ws.bptr) return true;
+  std::vector<double*> host;
+  std::vector<CholWorkspace::TileGroup> groups;
+  const int np = (int)ps.size() - 1;
+  for (int kk = 0; kk < np; ++kk) {
+    const int k = ps[kk], kb = ps[kk + 1] - k, m = n - k - kb;
+    const int jb0 = kk + 2 < (int)ps.size() ? ps[kk + 2] - ps[kk + 1] : 0;
+    double* Aik = A + k + kb + (size_t)k * lda;
+    double* T = Aik + (size_t)kb * lda;
+    const int R = m - jb0;
+    const int nt = R > 0 ? (R + tile - 1) / tile : 0;
+    const int last = nt > 0 ? R - (nt - 1) * tile : 0;
+    // full tiles: every (ti >= tj) when the last tile is full, else those above the last tile row
+    const int nfull_rows = last == tile ? nt : nt - 1;
+    auto add = [&](int m_, int n_, const std::vector<std::pair<int, int>>& tiles) {
+      CholWorkspace::TileGroup g{(int)host.size(), (int)tiles.size(), m_, n_};
+      for (auto& ij : tiles) host.push_back(Aik + jb0 + (size_t)ij.first * tile);
+      for (auto& ij : tiles) host.push_back(Aik + jb0 + (size_t)ij.second * tile);
+      for (auto& ij : tiles)
+        host.push_back(T + jb0 + (size_t)ij.first * tile + (size_t)(jb0 + (size_t)ij.second * tile) * lda);
+      groups.push_back(g);
+    };
+    std::vector<std::pair<int, int>> full, row, corner;
+    for (int tj = 0; tj < nt; ++tj)
+      for (int ti = tj; ti < nt; ++ti) {
+        if (ti < nfull_rows) full.push_back({ti, tj});
+        else if (tj < nt - 1) row.push_back({ti, tj});
+        else corner.push_back({ti, tj});
+      }
+    add(tile, tile, full);
+    add(last, tile, row);
+    add(last, last, corner);
+  }
+  if (host.size() > ws.bptr_cap) {
+    if (ws.bptr) (void)hipFree(ws.bptr);
+    ws.bptr = nullptr;
+    ws.bptr_cap = 0;
+    if (hipMalloc(&ws.bptr, host.size() * sizeof(double*)) != hipSuccess) {
+      ws.bptr = nullptr;
+      return false;
+    }
+    ws.bptr_cap = host.size();
+  }
+  // (pageable source: wait for the copy before the vector goes)
+  if (!host.empty() && (hipMemcpyAsync(ws.bptr, host.data(), host.size() * sizeof(double*), hipMemcpyHostToDevice, s) !=
+                            hipSuccess ||
+                        hipStreamSynchronize(s) != hipSuccess))
+    return false;
+  ws.bgroups = std::move(groups);
+  ws.bkey = std::move(key);
+  return true;
+}
+
 rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
                                 CholWorkspace& ws, int ex) {
   [[maybe_unused]] const double minus_one = -1.0, one = 1.0;  // rest_update 1 / 2 (tools build)
@@ -1474,6 +1535,8 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
   double* scratch_main = ws.scratch;
   double* scratch_side = ws.scratch + kSub * kSub;
   auto own_for = [&](int k0) { return cfg.head_own > 0 && k0 < cfg.head_own_cols ? cfg.head_own : cfg.own_diag; };
+  const bool batched = cfg.rest_update == 4 && cfg.batch_tile > 0;
+  if (batched && !batch_tables(ws, ps, n, A, lda, ex, cfg.batch_tile, s1)) return rocblas_status_internal_error;
   rocblas_status st = panel_factor(h, n, A, lda, 0, ps[1], info, own_for(0), scratch_main, &ws, ex);
   if (st != rocblas_status_success) return st;
   // On a failure after the side stream got work, the caller's stream waits
@@ -1546,7 +1609,22 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       if (st != rocblas_status_success) return fail(st);
     } else
 #endif
-    {
+    if (batched && sm == s1) {
+      for (int g = 0; g < 3; ++g) {
+        const CholWorkspace::TileGroup& tg = ws.bgroups[3 * (size_t)kk + g];
+        if (tg.count == 0) continue;
+        double** pa = ws.bptr + tg.off;
+        st = rocblas_dgemm_batched(hm, rocblas_operation_none, rocblas_operation_transpose, tg.m, tg.n, kb, &minus_one,
+                                   pa, lda, pa + tg.count, lda, &one, pa + 2 * tg.count, lda, tg.count);
+        if (st != rocblas_status_success) return fail(st);
+      }
+      // the carried rows below the matrix (the forward solve's row n)
+      if (ex > 0 && mr > 0) {
+        st = rocblas_dgemm(hm, rocblas_operation_none, rocblas_operation_transpose, ex, mr, kb, &minus_one, Aik + m, lda,
+                           Aik + jb0, lda, &one, T + m + (size_t)jb0 * lda, lda);
+        if (st != rocblas_status_success) return fail(st);
+      }
+    } else {
       // block columns of width nb (rest_update 0) or 2 nb (3)
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
       // streams used this panel: no more than its block columns
@@ -1817,6 +1895,11 @@ void CholWorkspace::destroy() {
   tbuf = nullptr;
   if (err) (void)hipFree(err);
   err = nullptr;
+  if (bptr) (void)hipFree(bptr);
+  bptr = nullptr;
+  bptr_cap = 0;
+  bkey.clear();
+  bgroups.clear();
   tbuf_rows = 0;
   linv_rows = 0;
 }

@@ -61,6 +61,11 @@ struct CholConfig {
   // 3 one dgemm per 1024-wide block column (default: 25.7 -> 25.2 ms at nf =
   // 12 000; dsyrk 38.6 ms, dgemmt 519 ms — profiles/r2_ab_rest_update.jsonl)
   int rest_update = 3;
+  // rest_update 4: the trailing update after the next panel's block column as
+  // square batch_tile x batch_tile tiles of the lower triangle, one
+  // rocblas_dgemm_batched launch per tile shape (full, bottom row, corner):
+  // one stream, no launch staircase whose tails need a second stream
+  int batch_tile = 1024;
   // trailing-update dgemm: 0 rocBLAS's default solution, else a Tensile
   // solution index for rocblas_gemm_ex (rocblas_gemm_ex_get_solutions; an
   // index the shape does not accept falls back to the default).  Default: the
@@ -176,6 +181,16 @@ struct CholWorkspace {
   int rest_n = 1;
   bool rest_cumask = false, rest_priority = false;
   bool set_rest_streams(int k, bool cumask = false, bool priority = false);
+  // rest_update 4: per panel up to three tile groups (full, bottom row,
+  // corner), each A[count], B[count], C[count] pointer arrays at off in bptr
+  // (device), made for one (A, n, lda, extra rows, tile, panel schedule)
+  struct TileGroup {
+    int off, count, m, n;
+  };
+  std::vector<TileGroup> bgroups;  // [panel][3]
+  double** bptr = nullptr;
+  size_t bptr_cap = 0;
+  std::vector<long long> bkey;
 
   // Creates the resources on `device` with events for up to `max_panels`
   // panels and diagonal-block inverses for matrices up to max_n; false on any

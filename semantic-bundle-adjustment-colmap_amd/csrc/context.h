@@ -74,6 +74,7 @@ struct mi_ba_context {
   std::vector<int64_t> block_obs;          // host: observation index per device block
   miba::DevArray<double2> obs_xy;
   miba::DevArray<uint32_t> obs_img, obs_pt;
+  miba::DevArray<uint32_t> obs_ids, wave_pt0;  // packed ids (device.h DevProblem::obs_ids)
   miba::DevArray<uint32_t> img_flags, img_cam;
   miba::DevArray<uint8_t> cam_var, cam_model, pt_var;
   miba::DevArray<double> qt, cam, X;       // current parameters

@@ -6,6 +6,8 @@
 //     obs_xy   double2[nb]     observed pixel (Point2D::XY)
 //     obs_img  u32[nb]         image index
 //     obs_pt   u32[nb]         point index
+//     obs_ids  u32[nb], wave_pt0 u32[nb/64]: the same ids packed (the
+//                              reprojection kernel's reads)
 //     r        double2[nb]     corrected residual
 //     J        double[nb][2][W] corrected tangent Jacobian, W = 9 + c,
 //                              columns rot(3) trans(3) point(3) cam(c)
@@ -111,6 +113,13 @@ struct DevProblem {
   const double2* obs_xy;
   const uint32_t* obs_img;
   const uint32_t* obs_pt;
+  // packed ids of the reprojection kernel (reproj_jacobian_kernel D & 8192):
+  // obs_ids[b] = image | (point - wave_pt0[b / 64]) << 16, one 4-B read per
+  // block instead of two (point-major order keeps a wave's points within a
+  // few of each other); null (the kernel reads obs_img / obs_pt) above 65536
+  // images or when a wave's points span more than 65535
+  const uint32_t* obs_ids;
+  const uint32_t* wave_pt0;
   const uint32_t* img_flags;
   const uint32_t* img_cam;
   const uint8_t* cam_var;

@@ -291,7 +291,7 @@ __device__ inline void wave_load_rows_u(const double* __restrict__ src, double* 
 // loads and r stores, 32 16-B J stores, 128 per-block loads issued up front;
 // 1 and 2 are the diagnostic builds; 512 closed-form rotation columns, 1024
 // R X through the rotation matrix.
-constexpr int kJacProduction = 8 | 16 | 32 | 128 | 512 | 1024;  // 0.583 -> 0.543 ms at C4 with 512 | 1024
+constexpr int kJacProduction = 8 | 16 | 32 | 128 | 512 | 1024 | 8192;  // 0.583 -> 0.543 ms at C4 with 512 | 1024
 // J rows staged in one slab pass (64 rows, 17 KB of LDS per wave at OPENCV: 2
 // waves per SIMD, each store burst 15 KB): 0.554 (2 passes) -> 0.454 ms at C4
 // once the arithmetic was cut by the closed-form rotation columns
@@ -355,10 +355,24 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     double2 o_e = make_double2(0.0, 0.0);
     double X_e[3] = {0.0, 0.0, 0.0};
     bool ptv_e = false;
-    if (live) img = (D & 16) ? __builtin_nontemporal_load(p.obs_img + i) : p.obs_img[i];
+    bool packed = false;
+    if constexpr ((D & 8192) != 0) {
+      // packed ids (device.h obs_ids): image and the point's offset from the
+      // wave's first point in one 4-B read
+      packed = p.obs_ids != nullptr;
+      if (packed) {
+        const uint32_t w0 = wb0 < p.nb ? p.wave_pt0[__builtin_amdgcn_readfirstlane((int)(wb0 >> 6))] : 0u;
+        if (live) {
+          const uint32_t v = __builtin_nontemporal_load(p.obs_ids + i);
+          img = v & 0xffffu;
+          pt_e = w0 + (v >> 16);
+        }
+      }
+    }
+    if (!packed && live) img = (D & 16) ? __builtin_nontemporal_load(p.obs_img + i) : p.obs_img[i];
     if constexpr ((D & 128) != 0) {
       if (live) {
-        pt_e = __builtin_nontemporal_load(p.obs_pt + i);
+        if (!packed) pt_e = __builtin_nontemporal_load(p.obs_pt + i);
         const dvec2 ov = __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(p.obs_xy) + i);
         o_e = make_double2(ov.x, ov.y);
         X_e[0] = p.X[3 * (size_t)pt_e];
@@ -3232,8 +3246,8 @@ int reproj_grid(int64_t nb) { return (int)grid_for(nb, 64); }
 // runs beside the semantic deferred pass and should take as little of the
 // CUs' wave slots as it can.  The sink is written only for an impossible sum.
 struct TouchRanges {
-  const uint4* ptr[4];
-  int64_t n16[4];
+  const uint4* ptr[5];
+  int64_t n16[5];
 };
 
 template <int U>
@@ -3241,7 +3255,7 @@ __global__ __launch_bounds__(256) void touch_kernel(TouchRanges t, unsigned* sin
   unsigned acc = 0u;
   const int64_t stride = (int64_t)gridDim.x * 256;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < 5; ++q) {
     const uint4* a = t.ptr[q];
     const int64_t n = t.n16[q];
     int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -3258,12 +3272,18 @@ __global__ __launch_bounds__(256) void touch_kernel(TouchRanges t, unsigned* sin
 }
 
 void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s, int mask, int wgs, int unroll) {
+  // mask bits: 1 observations, 2 image ids, 4 point ids, 8 points; the ids
+  // in the layout the kernel reads (packed: both in obs_ids + wave_pt0)
   TouchRanges t{};
-  const void* ptrs[4] = {p.obs_xy, p.obs_img, p.obs_pt, p.X};
-  const int64_t bytes[4] = {p.nb * 16, p.nb * 4, p.nb * 4, p.num_points * 24};
-  for (int q = 0; q < 4; ++q) {
+  const bool packed = (kJacProduction & 8192) != 0 && p.obs_ids;
+  const int64_t nw = (p.nb + 63) / 64;
+  const void* ptrs[5] = {p.obs_xy, packed ? (const void*)p.obs_ids : (const void*)p.obs_img,
+                         packed ? (const void*)p.wave_pt0 : (const void*)p.obs_pt, nullptr, p.X};
+  const int64_t bytes[5] = {p.nb * 16, p.nb * 4, packed ? nw * 4 : p.nb * 4, 0, p.num_points * 24};
+  const int bit[5] = {1, 2, 4, 4, 8};
+  for (int q = 0; q < 5; ++q) {
     t.ptr[q] = reinterpret_cast<const uint4*>(ptrs[q]);
-    t.n16[q] = ptrs[q] && ((mask >> q) & 1) ? bytes[q] / 16 : 0;
+    t.n16[q] = ptrs[q] && (mask & bit[q]) ? bytes[q] / 16 : 0;
   }
   if (wgs <= 0) {  // one workgroup per CU
     int dev = 0;
@@ -3410,6 +3430,10 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
             case 12:
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, kJacPasses, kJacProduction | 1>), dim3(g), dim3(kBlock),
                                  0, s, p, r, J, cost_partial);
+              return;
+            case 43:  // ids from obs_img + obs_pt (before the packed ids)
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, kJacPasses, kJacProduction & ~8192>), dim3(g),
+                                 dim3(kBlock), 0, s, p, r, J, cost_partial);
               return;
             case 13:  // R and the unit-q test from the image record (per image, not per block)
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, kJacPasses, kJacProduction | 2048>), dim3(g),

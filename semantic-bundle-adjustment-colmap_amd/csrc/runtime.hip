@@ -575,6 +575,25 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
           hipMemcpy(ctx->obs_img.ptr, im.data(), nb * 4, hipMemcpyHostToDevice) ||
           hipMemcpy(ctx->obs_pt.ptr, pt.data(), nb * 4, hipMemcpyHostToDevice))
         return fail(MI_BA_ERR_HIP);
+      // packed ids of the reprojection kernel (device.h obs_ids)
+      const int64_t nw = (nb + 63) / 64;
+      std::vector<uint32_t> ids(nb), w0(nw);
+      bool packed = I <= 65536;
+      for (int64_t b = 0; b < nb && packed; ++b) {
+        if ((b & 63) == 0) w0[b >> 6] = pt[b];
+        const uint32_t base = w0[b >> 6];
+        packed = pt[b] >= base && pt[b] - base <= 65535u;
+        ids[b] = im[b] | (pt[b] - base) << 16;
+      }
+      if (!packed) {
+        ctx->obs_ids.release();
+        ctx->wave_pt0.release();
+      } else {
+        if (ctx->obs_ids.alloc(nb) || ctx->wave_pt0.alloc(nw)) return fail(MI_BA_ERR_OUT_OF_MEMORY);
+        if (hipMemcpy(ctx->obs_ids.ptr, ids.data(), nb * 4, hipMemcpyHostToDevice) ||
+            hipMemcpy(ctx->wave_pt0.ptr, w0.data(), nw * 4, hipMemcpyHostToDevice))
+          return fail(MI_BA_ERR_HIP);
+      }
     }
     // camera-major permutation and image-aligned tiles
     std::vector<uint32_t> perm(nb);
@@ -738,6 +757,8 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
   d.obs_xy = ctx->obs_xy.ptr;
   d.obs_img = ctx->obs_img.ptr;
   d.obs_pt = ctx->obs_pt.ptr;
+  d.obs_ids = ctx->obs_ids.ptr;
+  d.wave_pt0 = ctx->wave_pt0.ptr;
   d.img_flags = ctx->img_flags.ptr;
   d.img_cam = ctx->img_cam.ptr;
   d.cam_var = ctx->cam_var.ptr;
@@ -2318,9 +2339,13 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.gemm_solution = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 3 &&
-      (value == 0 || value == 3 || ab_value(value, 3))) {
+  if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 4 &&
+      (value == 0 || value == 3 || value == 4 || ab_value(value, 3))) {
     ctx->chol.rest_update = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_batch_tile") == 0 && value >= 64 && value % 64 == 0) {
+    ctx->chol.batch_tile = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_tile_factor") == 0 && (value == 1 || value == 2) && ab_value(value, 2)) {
