@@ -1463,7 +1463,10 @@ rocblas_status gemm_nt(rocblas_handle h, int m, int n, int k, const double* P, i
                        &one, C, ldc);
 }
 
-// rest_update 4: the tile pointer tables of every panel's trailing update
+#ifdef MI_BA_AB_VARIANTS
+// rest_update 4 (tools build: measured slower, 16.5-18.2 vs 15.1 ms with two
+// update streams at nf = 11 993, profiles/r5g_ab_cholesky_batched_tiles.jsonl):
+// the tile pointer tables of every panel's trailing update
 // after the next panel's block column (CholWorkspace::bgroups / bptr), made
 // once per (A, n, lda, ex, tile, panel schedule) and kept for the context's
 // later factorisations.
@@ -1523,6 +1526,7 @@ static bool batch_tables(CholWorkspace& ws, const std::vector<int>& ps, int n, d
   ws.bkey = std::move(key);
   return true;
 }
+#endif
 
 rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
                                 CholWorkspace& ws, int ex) {
@@ -1535,8 +1539,10 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
   double* scratch_main = ws.scratch;
   double* scratch_side = ws.scratch + kSub * kSub;
   auto own_for = [&](int k0) { return cfg.head_own > 0 && k0 < cfg.head_own_cols ? cfg.head_own : cfg.own_diag; };
+#ifdef MI_BA_AB_VARIANTS
   const bool batched = cfg.rest_update == 4 && cfg.batch_tile > 0;
   if (batched && !batch_tables(ws, ps, n, A, lda, ex, cfg.batch_tile, s1)) return rocblas_status_internal_error;
+#endif
   rocblas_status st = panel_factor(h, n, A, lda, 0, ps[1], info, own_for(0), scratch_main, &ws, ex);
   if (st != rocblas_status_success) return st;
   // On a failure after the side stream got work, the caller's stream waits
@@ -1607,9 +1613,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       st = rocblas_dgemmt(h, rocblas_fill_lower, rocblas_operation_none, rocblas_operation_transpose, mr, kb,
                           &minus_one, Aik + jb0, lda, Aik + jb0, lda, &one, T + jb0 + (size_t)jb0 * lda, lda);
       if (st != rocblas_status_success) return fail(st);
-    } else
-#endif
-    if (batched && sm == s1) {
+    } else if (batched && sm == s1) {
       for (int g = 0; g < 3; ++g) {
         const CholWorkspace::TileGroup& tg = ws.bgroups[3 * (size_t)kk + g];
         if (tg.count == 0) continue;
@@ -1624,7 +1628,9 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
                            Aik + jb0, lda, &one, T + m + (size_t)jb0 * lda, lda);
         if (st != rocblas_status_success) return fail(st);
       }
-    } else {
+    } else
+#endif
+    {
       // block columns of width nb (rest_update 0) or 2 nb (3)
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
       // streams used this panel: no more than its block columns
@@ -1817,7 +1823,7 @@ bool CholWorkspace::set_split_cus(int ncu) {
   return true;
 }
 
-bool CholWorkspace::set_rest_streams(int k, bool cumask, bool priority) {
+bool CholWorkspace::set_rest_streams(int k, bool cumask, int priority) {
   for (int r = 0; r + 1 < kMaxRest; ++r) {
     if (rest_s[r]) (void)hipStreamSynchronize(rest_s[r]);
     if (rest_h[r]) (void)rocblas_destroy_handle(rest_h[r]);
@@ -1828,7 +1834,8 @@ bool CholWorkspace::set_rest_streams(int k, bool cumask, bool priority) {
   for (hipEvent_t e : ev_rest) (void)hipEventDestroy(e);
   ev_rest.clear();
   rest_n = 1;
-  rest_cumask = rest_priority = false;
+  rest_cumask = false;
+  rest_priority = 0;
   if (k <= 1) return true;
   if (k > kMaxRest || hipSetDevice(device) != hipSuccess) return false;
   std::vector<uint32_t> all;
@@ -1841,10 +1848,11 @@ bool CholWorkspace::set_rest_streams(int k, bool cumask, bool priority) {
   }
   for (int r = 0; r + 1 < k; ++r) {
     int least = 0, greatest = 0;
-    if (priority && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
-    const hipError_t e = cumask     ? hipExtStreamCreateWithCUMask(&rest_s[r], (uint32_t)all.size(), all.data())
-                         : priority ? hipStreamCreateWithPriority(&rest_s[r], hipStreamNonBlocking, greatest)
-                                    : hipStreamCreateWithFlags(&rest_s[r], hipStreamNonBlocking);
+    if (priority && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = least = 0;
+    const hipError_t e =
+        cumask     ? hipExtStreamCreateWithCUMask(&rest_s[r], (uint32_t)all.size(), all.data())
+        : priority ? hipStreamCreateWithPriority(&rest_s[r], hipStreamNonBlocking, priority == 1 ? greatest : least)
+                   : hipStreamCreateWithFlags(&rest_s[r], hipStreamNonBlocking);
     if (e != hipSuccess) {
       rest_s[r] = nullptr;
       return false;

@@ -52,19 +52,20 @@ struct CholConfig {
   // the further update streams created with an all-CU mask (a hardware queue
   // of their own instead of HIP's round-robin share of the process's queues)
   bool rest_cumask = false;
-  // the further update streams at the highest stream priority (as the
-  // look-ahead side stream)
-  bool rest_priority = false;
+  // the further update streams' priority: 0 normal, 1 the highest (as the
+  // look-ahead side stream), 2 the lowest (HIP keeps a queue pool per
+  // priority: a low-priority stream never shares the caller's normal-priority
+  // hardware queue, whatever other streams the process holds)
+  int rest_priority = 0;
   bool gemm_update = true;
   // look-ahead: the trailing update after the next panel's block column,
   // 0 one dgemm per 512-wide block column, 1 one dsyrk, 2 one dgemmt,
   // 3 one dgemm per 1024-wide block column (default: 25.7 -> 25.2 ms at nf =
   // 12 000; dsyrk 38.6 ms, dgemmt 519 ms — profiles/r2_ab_rest_update.jsonl)
   int rest_update = 3;
-  // rest_update 4: the trailing update after the next panel's block column as
-  // square batch_tile x batch_tile tiles of the lower triangle, one
-  // rocblas_dgemm_batched launch per tile shape (full, bottom row, corner):
-  // one stream, no launch staircase whose tails need a second stream
+  // rest_update 4 (tools build, measured slower): the trailing update after
+  // the next panel's block column as square batch_tile x batch_tile tiles of
+  // the lower triangle, one rocblas_dgemm_batched launch per tile shape
   int batch_tile = 1024;
   // trailing-update dgemm: 0 rocBLAS's default solution, else a Tensile
   // solution index for rocblas_gemm_ex (rocblas_gemm_ex_get_solutions; an
@@ -179,8 +180,9 @@ struct CholWorkspace {
   rocblas_handle rest_h[kMaxRest - 1] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> ev_rest;  // [panel][kMaxRest]
   int rest_n = 1;
-  bool rest_cumask = false, rest_priority = false;
-  bool set_rest_streams(int k, bool cumask = false, bool priority = false);
+  bool rest_cumask = false;
+  int rest_priority = 0;
+  bool set_rest_streams(int k, bool cumask = false, int priority = 0);
   // rest_update 4: per panel up to three tile groups (full, bottom row,
   // corner), each A[count], B[count], C[count] pointer arrays at off in bptr
   // (device), made for one (A, n, lda, extra rows, tile, panel schedule)

@@ -116,9 +116,22 @@ bool fused_rhs(const mi_ba_context* ctx) {
   return ctx->fused_rhs && c.panel > 0 && c.gemm_update && c.solve == 2 && ctx->dev.lds > ctx->dev.nf;
 }
 
+mi_ba_status comm_drain(mi_ba_context* ctx);
+
+// A host wait on stream s of the context: pending collectives first
+// (comm_drain, deadline-bounded), then the synchronisation.
+#define MI_HIP_DRAIN(ctx_, s_)                          \
+  do {                                                  \
+    const mi_ba_status ds_ = comm_drain(ctx_);          \
+    if (ds_ != MI_BA_OK) return ds_;                    \
+    MI_HIP(hipStreamSynchronize(s_));                   \
+  } while (0)
+
 mi_ba_status read_scalars(mi_ba_context* ctx, int first, int count) {
   MI_HIP(hipMemcpyAsync(ctx->host_scalars + first, ctx->scalars.ptr + first, sizeof(double) * count,
                         hipMemcpyDeviceToHost, ctx->stream));
+  mi_ba_status st = comm_drain(ctx);
+  if (st != MI_BA_OK) return st;
   MI_HIP(hipStreamSynchronize(ctx->stream));
   return MI_BA_OK;
 }
@@ -174,6 +187,17 @@ mi_ba_status comm_wait_stream(mi_ba_context* ctx, double deadline) {
   }
 }
 
+// Collectives are enqueued without a host wait (allreduce); the next host
+// wait on the context stream goes through here first, bounded by their
+// deadline and watching the communicator's error state, so a dead peer ends
+// the wait instead of hanging it.  No pending collective: nothing to do.
+mi_ba_status comm_drain(mi_ba_context* ctx) {
+  if (!ctx->comm || ctx->comm_due <= 0.0) return MI_BA_OK;
+  const double due = ctx->comm_due;
+  ctx->comm_due = 0.0;
+  return comm_wait_stream(ctx, due);
+}
+
 // Test hook ("comm_stall_ms"): hold the stream, as a collective whose peer
 // never arrives would, until the host releases the flag or the stall time
 // has passed.  One wave; it always ends (a bound on the constant-rate wall
@@ -188,11 +212,13 @@ __global__ void stall_kernel(const int* flag, uint64_t ticks) {
 
 // Sum n doubles of a device buffer over the ranks of a multi-rank solve (RCCL
 // all-reduce on the context stream, or the host reducer); no-op without a
-// reducer.  With RCCL the call returns once the sum is complete: every
-// collective is waited on with the context's deadline ("comm_timeout_ms"), and
-// a failed or timed-out collective aborts the communicator and returns
-// MI_BA_ERR_HIP (on every rank that sees it; a rank whose peer failed sees its
-// own collective time out).
+// reducer.  With RCCL the call returns once the collective is enqueued (the
+// stream orders the kernels that read the sum behind it; back-to-back sums
+// pipeline with no host round trip between them); the next host wait
+// (comm_drain) bounds its completion by the context's deadline
+// ("comm_timeout_ms").  A failed or timed-out collective aborts the
+// communicator and returns MI_BA_ERR_HIP (on every rank that sees it; a rank
+// whose peer failed sees its own collective time out).
 mi_ba_status allreduce(mi_ba_context* ctx, double* d, int64_t n) {
   if (!ctx->distributed() || n <= 0) return MI_BA_OK;
   if (ctx->comm_failed) return MI_BA_ERR_HIP;
@@ -214,15 +240,16 @@ mi_ba_status allreduce(mi_ba_context* ctx, double* d, int64_t n) {
     if (r != ncclSuccess && r != ncclInProgress) return comm_fail(ctx);
     mi_ba_status st = comm_settle(ctx, deadline);
     if (st != MI_BA_OK) return st;
-    return comm_wait_stream(ctx, deadline);
+    ctx->comm_due = std::max(ctx->comm_due, deadline);
+    return MI_BA_OK;
   }
   if (!ctx->host_reduce) return MI_BA_ERR_STATE;
   ctx->reduce_buf.resize(n);
   MI_HIP(hipMemcpyAsync(ctx->reduce_buf.data(), d, n * 8, hipMemcpyDeviceToHost, ctx->stream));
-  MI_HIP(hipStreamSynchronize(ctx->stream));
+  MI_HIP_DRAIN(ctx, ctx->stream);
   if (ctx->host_reduce(ctx->reduce_buf.data(), n, ctx->host_reduce_user) != 0) return MI_BA_ERR_HIP;
   MI_HIP(hipMemcpyAsync(d, ctx->reduce_buf.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
-  MI_HIP(hipStreamSynchronize(ctx->stream));
+  MI_HIP_DRAIN(ctx, ctx->stream);
   return MI_BA_OK;
 }
 
@@ -1229,7 +1256,7 @@ mi_ba_status gradient_reached(mi_ba_context* ctx, bool* reached) {
   if (st != MI_BA_OK) return st;
   std::vector<double> h(nw + 2, 0.0);
   MI_HIP(hipMemcpyAsync(h.data(), aux, nw * 8, hipMemcpyDeviceToHost, s));
-  MI_HIP(hipStreamSynchronize(s));
+  MI_HIP_DRAIN(ctx, s);
   double gmax = 0.0;
   for (int k = 0; k < nw; ++k) gmax = std::max(gmax, h[k]);
   if (gmax > tol) return MI_BA_OK;
@@ -1245,7 +1272,7 @@ mi_ba_status gradient_reached(mi_ba_context* ctx, bool* reached) {
   launch_grad_max_f(d, g, aux + nw, s);
   if (ctx->gsba) gsba_grad_max(ctx, g, aux + nw);
   MI_HIP(hipMemcpyAsync(h.data() + nw, aux + nw, 8, hipMemcpyDeviceToHost, s));
-  MI_HIP(hipStreamSynchronize(s));
+  MI_HIP_DRAIN(ctx, s);
   gmax = std::max(gmax, h[nw]);
   *reached = gmax <= tol;
   return MI_BA_OK;
@@ -1334,6 +1361,10 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok, bool schur_launched) {
   std::vector<int32_t> info(leaves, 0);
   MI_HIP(hipMemcpyAsync(info.data(), ctx->info.ptr, 4 * (size_t)leaves, hipMemcpyDeviceToHost, s));
   unsigned werr = 0;
+  {
+    mi_ba_status ds = comm_drain(ctx);  // the S bands' sums
+    if (ds != MI_BA_OK) return ds;
+  }
   MI_HIP(chol_error(&ctx->cholws, s, &werr));  // synchronises s
   // a flag wait of the factorisation ran out: the factor is invalid (every
   // rank learns it, so no rank takes a step the others do not)
@@ -1356,6 +1387,10 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok, bool schur_launched) {
                rocblas_status_success) {
       return MI_BA_ERR_HIP;
     }
+  }
+  {
+    mi_ba_status ds = comm_drain(ctx);
+    if (ds != MI_BA_OK) return ds;
   }
   MI_HIP(chol_error(&ctx->cholws, s, &werr));
   return agree_on_error(ctx, werr != 0);
@@ -1668,7 +1703,7 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     }
   }
   sum->final_cost = x_cost + ctx->fixed_cost;
-  MI_HIP(hipStreamSynchronize(s));
+  MI_HIP_DRAIN(ctx, s);
   sum->total_time_in_seconds = now_s() - t_start;
   return MI_BA_OK;
 }
@@ -1679,7 +1714,7 @@ mi_ba_status context_writeback(mi_ba_context* ctx) {
   const int I = p->num_images, C = p->num_cameras;
   const int64_t P = p->num_points;
   std::vector<double> qt(8 * (size_t)I), cm(8 * (size_t)C), X(3 * (size_t)P);
-  MI_HIP(hipStreamSynchronize(ctx->stream));
+  MI_HIP_DRAIN(ctx, ctx->stream);
   if (I) MI_HIP(hipMemcpy(qt.data(), ctx->qt.ptr, qt.size() * 8, hipMemcpyDeviceToHost));
   if (C) MI_HIP(hipMemcpy(cm.data(), ctx->cam.ptr, cm.size() * 8, hipMemcpyDeviceToHost));
   if (P) MI_HIP(hipMemcpy(X.data(), ctx->X.ptr, X.size() * 8, hipMemcpyDeviceToHost));
@@ -1982,7 +2017,7 @@ mi_ba_status mi_ba_evaluate_semantic(mi_ba_context* ctx) {
 
 mi_ba_status mi_ba_synchronize(mi_ba_context* ctx) {
   MI_BIND(ctx);
-  MI_HIP(hipStreamSynchronize(ctx->stream));
+  MI_HIP_DRAIN(ctx, ctx->stream);
   return MI_BA_OK;
 }
 
@@ -1997,7 +2032,7 @@ mi_ba_status mi_ba_context_dims(const mi_ba_context* ctx, int64_t* nb, int32_t* 
 mi_ba_status mi_ba_download_jacobian(mi_ba_context* ctx, int64_t* block_obs, double* residuals, double* jacobian) {
   MI_BIND(ctx);
   const int64_t nb = ctx->dev.nb;
-  MI_HIP(hipStreamSynchronize(ctx->stream));
+  MI_HIP_DRAIN(ctx, ctx->stream);
   if (block_obs) std::memcpy(block_obs, ctx->block_obs.data(), nb * sizeof(int64_t));
   if (residuals && nb) MI_HIP(hipMemcpy(residuals, ctx->r.ptr, nb * sizeof(double2), hipMemcpyDeviceToHost));
   if (jacobian && nb)
@@ -2010,7 +2045,7 @@ mi_ba_status mi_ba_download_semantic(mi_ba_context* ctx, int32_t* sample_pixel, 
   MI_BIND(ctx);
   if (!ctx->sem) return MI_BA_ERR_INVALID_ARGUMENT;
   SemanticState* S = ctx->sem;
-  MI_HIP(hipStreamSynchronize(ctx->stream));
+  MI_HIP_DRAIN(ctx, ctx->stream);
   if (!S->samples_valid) return MI_BA_ERR_STATE;  // mi_ba_evaluate_semantic first
   const int64_t n = S->ns;
   if (sample_pixel) std::memcpy(sample_pixel, S->sample_pixel_host.data(), 3 * n * sizeof(int32_t));
@@ -2067,7 +2102,7 @@ static mi_ba_status reduce_fixed_cost(mi_ba_context* ctx) {
   mi_ba_status st = allreduce(ctx, slot, 1);
   if (st != MI_BA_OK) return st;
   MI_HIP(hipMemcpyAsync(&ctx->fixed_cost, slot, 8, hipMemcpyDeviceToHost, ctx->stream));
-  MI_HIP(hipStreamSynchronize(ctx->stream));
+  MI_HIP_DRAIN(ctx, ctx->stream);
   return MI_BA_OK;
 }
 
@@ -2340,7 +2375,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_rest_update") == 0 && value >= 0 && value <= 4 &&
-      (value == 0 || value == 3 || value == 4 || ab_value(value, 3))) {
+      (value == 0 || value == 3 || ab_value(value, 3))) {
     ctx->chol.rest_update = value;
     return MI_BA_OK;
   }
@@ -2362,8 +2397,8 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.panel_rows_per_group = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_rest_priority") == 0 && (value == 0 || value == 1)) {
-    ctx->chol.rest_priority = value != 0;
+  if (std::strcmp(key, "cholesky_rest_priority") == 0 && value >= 0 && value <= 2) {
+    ctx->chol.rest_priority = value;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_rest_cumask") == 0 && (value == 0 || value == 1)) {
