@@ -2305,21 +2305,31 @@ __global__ void grad_max_f_kernel(DevProblem p, const double* __restrict__ g, do
 }
 
 // The same over the variable points (g_p from the point blocks Vg).
-__global__ void grad_max_points_kernel(DevProblem p, const DevPoint* __restrict__ vp, int64_t npv,
-                                       const double* __restrict__ Vg, double* out) {
-  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+// Grid-stride over the variable points (a few workgroups per CU), one
+// atomic max per workgroup: one per wave over 1M points serialised ~16k
+// atomics on one address (185 us at C4).
+__global__ __launch_bounds__(kBlock) void grad_max_points_kernel(DevProblem p, const DevPoint* __restrict__ vp,
+                                                                 int64_t npv, const double* __restrict__ Vg,
+                                                                 double* out) {
+  __shared__ double smax[kBlock / 64];
   double mx = 0.0;
-  if (k < npv) {
+  for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < npv; k += (int64_t)gridDim.x * kBlock) {
     const uint32_t pt = vp[k].point;
     const double* gp = Vg + 9 * (size_t)pt + 6;
     const double* X = p.X + 3 * (size_t)pt;
 #pragma unroll
     for (int m = 0; m < 3; ++m) mx = fmax(mx, fabs(X[m] - (X[m] + -gp[m])));
   }
-  // one atomic per wave
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
-  if ((threadIdx.x & 63) == 0 && mx > 0.0) atomic_max_nonneg(out, mx);
+  if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = smax[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) m = fmax(m, smax[w]);
+    if (m > 0.0) atomic_max_nonneg(out, m);
+  }
 }
 
 // Ceres' state vector over the variable blocks, ambient coordinates: |x|^2
@@ -2853,6 +2863,50 @@ __global__ __launch_bounds__(kBlock) void schur_z_kernel(DevProblem p, const dou
   wave_readout<ZN, ZS, ZN>(slab, Z + wb0 * ZN, live);
 }
 
+// Store one pair tile's 16 x 16 accumulator (the v_mfma_f64_16x16x4f64 D
+// layout) into S: through the deterministic route's partial slot, as the S
+// block's only writer, or by float atomics (pf.pslot null).
+template <int F>
+__device__ __forceinline__ void pair_tile_store(const DevProblem& p, const DevPairTile& tl, int t, int lane,
+                                                const double (&acc)[4], double* __restrict__ S, const PairFlush& pf) {
+  if (pf.pslot) {
+    const int32_t ps = pf.pslot[t];
+    if (ps >= 0) {  // summed with the block's other tiles (schur_pairs_flush_kernel)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pf.part[(size_t)ps * 256 + r * 64 + lane] = acc[r];
+      return;
+    }
+  }
+  const uint32_t ia = tl.ia, ib = tl.ib;
+  const uint32_t ca = p.img_cam[ia], cb = p.img_cam[ib];
+  const bool pa = p.img_flags[ia] & 1u, pb = p.img_flags[ib] & 1u;
+  const bool cva = p.cam_var[ca] != 0, cvb = p.cam_var[cb] != 0;
+  const int ncol = lane & 15;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int mrow = 4 * r + (lane >> 4);  // v_mfma_f64_16x16x4f64 D layout (measured): D[4r + l/16][l%16]
+    if (mrow >= F || ncol >= F) continue;
+    const bool va = mrow < 6 ? pa : cva, vb = ncol < 6 ? pb : cvb;
+    if (!va || !vb) continue;
+    const int64_t ra = fslot(p, ia, ca, mrow), rb = fslot(p, ib, cb, ncol);
+    const double v = acc[r];
+    if (pf.pslot) {  // the block's only tile (ia != ib, cameras not shared): ra != rb, one writer
+      double* e = S + (ra < rb ? ra * p.lds + rb : rb * p.lds + ra);
+      *e -= v;
+      continue;
+    }
+    if (tl.self) {
+      if (ra <= rb) atomicAdd(S + ra * p.lds + rb, -v);
+    } else if (ra < rb) {
+      atomicAdd(S + ra * p.lds + rb, -v);
+    } else if (ra > rb) {
+      atomicAdd(S + rb * p.lds + ra, -v);
+    } else {
+      atomicAdd(S + ra * p.lds + ra, -2.0 * v);
+    }
+  }
+}
+
 // One wavefront per image-pair tile: acc = sum over the tile's pairs of
 // Z_a Z_b' (16x16 f64 MFMA accumulator), then -acc into the upper triangle
 // (row <= col, row-major = rocSOLVER's column-major lower) of S.
@@ -2914,42 +2968,90 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
       vb = on ? Z[(size_t)pr.y * ZN + off] : 0.0;
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, acc, 0, 0, 0);
   }
-  if (pf.pslot) {
-    const int32_t ps = pf.pslot[t];
-    if (ps >= 0) {  // summed with the block's other tiles (schur_pairs_flush_kernel)
+  const double accv[4] = {acc[0], acc[1], acc[2], acc[3]};
+  pair_tile_store<F>(p, tl, t, lane, accv, S, pf);
+}
+
+// Z_a's entry (k, m) formed from block a's J row and its point's Linv, with
+// schur_z_kernel's operation sequence: W_a = J_f,a' J_p,a (column m of the
+// camera side: pose 0..5 at J columns 0..5, intrinsics at 9..), Z_a = W_a
+// Linv'.  row: the block's 2 x W J rows; L: the packed lower Linv (zero for a
+// constant point).
+template <int W>
+__device__ __forceinline__ double z_from_j(const double* __restrict__ row, int col, int k, const double (&L)[6]) {
+  const double a0 = row[col], a1 = row[W + col];
+  const double w0 = a0 * row[6] + a1 * row[W + 6];
+  if (k == 0) return w0 * L[0];
+  const double w1 = a0 * row[7] + a1 * row[W + 7];
+  if (k == 1) return w0 * L[1] + w1 * L[2];
+  const double w2 = a0 * row[8] + a1 * row[W + 8];
+  return w0 * L[3] + w1 * L[4] + w2 * L[5];
+}
+
+// schur_pairs_variant 7: schur_pairs_kernel without the Z pass — each pair's
+// two Z rows are formed in registers from the blocks' J rows (240 B each at
+// OPENCV instead of Z's 288 B) and the point's Linv (48 B, shared by the
+// pair), so neither Z's 2.9 GB write nor schur_z_kernel's J read happens.
+// Dispatch-order tiles (the image-block order of svariant 4).
+template <int CT>
+__global__ __launch_bounds__(kBlock) void schur_pairs_j_kernel(DevProblem p, const DevPairTile* __restrict__ tiles,
+                                                                int ntiles, const uint2* __restrict__ pairs,
+                                                                const double* __restrict__ J,
+                                                                const double* __restrict__ Linv,
+                                                                double* __restrict__ S, PairFlush pf) {
+  constexpr int F = 6 + CT, W = 9 + CT, W2 = 2 * W;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = blockIdx.x * 4 + wv;
+  if (t >= ntiles) return;
+  const DevPairTile tl = tiles[t];
+  if (tl.count == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int m = lane & 15, k = lane >> 4;
+  const bool on = m < F && k < 3;
+  const int col = m < 6 ? m : 3 + m;  // J column of camera-side tangent m (pose 0..5, intrinsics 9..)
+  typedef double dvec4 __attribute__((ext_vector_type(4)));
+  dvec4 acc = {0.0, 0.0, 0.0, 0.0};
+  const uint32_t cnt = tl.count;
+  const uint2* pl = pairs + tl.start;
+  constexpr int U = 2;
+  uint32_t n = 0;
+  for (; n + U <= cnt; n += U) {
+    uint2 pr[U];
+    uint32_t pt[U];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) pf.part[(size_t)ps * 256 + r * 64 + lane] = acc[r];
-      return;
+    for (int u = 0; u < U; ++u) {
+      pr[u] = pl[n + u];
+      pt[u] = p.obs_pt[pr[u].x];
     }
-  }
-  const uint32_t ia = tl.ia, ib = tl.ib;
-  const uint32_t ca = p.img_cam[ia], cb = p.img_cam[ib];
-  const bool pa = p.img_flags[ia] & 1u, pb = p.img_flags[ib] & 1u;
-  const bool cva = p.cam_var[ca] != 0, cvb = p.cam_var[cb] != 0;
-  const int ncol = lane & 15;
+    double L[U][6];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int mrow = 4 * r + (lane >> 4);  // v_mfma_f64_16x16x4f64 D layout (measured): D[4r + l/16][l%16]
-    if (mrow >= F || ncol >= F) continue;
-    const bool va = mrow < 6 ? pa : cva, vb = ncol < 6 ? pb : cvb;
-    if (!va || !vb) continue;
-    const int64_t ra = fslot(p, ia, ca, mrow), rb = fslot(p, ib, cb, ncol);
-    const double v = acc[r];
-    if (pf.pslot) {  // the block's only tile (ia != ib, cameras not shared): ra != rb, one writer
-      double* e = S + (ra < rb ? ra * p.lds + rb : rb * p.lds + ra);
-      *e -= v;
-      continue;
+    for (int u = 0; u < U; ++u) {
+      const bool v = p.pt_var[pt[u]] != 0;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) L[u][q] = v ? Linv[6 * (size_t)pt[u] + q] : 0.0;
     }
-    if (tl.self) {
-      if (ra <= rb) atomicAdd(S + ra * p.lds + rb, -v);
-    } else if (ra < rb) {
-      atomicAdd(S + ra * p.lds + rb, -v);
-    } else if (ra > rb) {
-      atomicAdd(S + rb * p.lds + ra, -v);
-    } else {
-      atomicAdd(S + ra * p.lds + ra, -2.0 * v);
+    double va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      va[u] = on ? z_from_j<W>(J + (size_t)pr[u].x * W2, col, k, L[u]) : 0.0;
+      vb[u] = on ? z_from_j<W>(J + (size_t)pr[u].y * W2, col, k, L[u]) : 0.0;
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va[u], vb[u], acc, 0, 0, 0);
   }
+  for (; n < cnt; ++n) {
+    const uint2 pr = pl[n];
+    const uint32_t pt = p.obs_pt[pr.x];
+    double L[6];
+    const bool v = p.pt_var[pt] != 0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) L[q] = v ? Linv[6 * (size_t)pt + q] : 0.0;
+    const double va = on ? z_from_j<W>(J + (size_t)pr.x * W2, col, k, L) : 0.0;
+    const double vb = on ? z_from_j<W>(J + (size_t)pr.y * W2, col, k, L) : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, acc, 0, 0, 0);
+  }
+  const double accv[4] = {acc[0], acc[1], acc[2], acc[3]};
+  pair_tile_store<F>(p, tl, t, lane, accv, S, pf);
 }
 
 // The pair tiles' partial blocks summed per S block in list order and
@@ -3758,7 +3860,8 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
       hipLaunchKernelGGL(schur_pairs_jg_kernel<CT>, dim3((nptiles + 3) / 4), dim3(kBlock), 0, s, p, ptiles, nptiles,
                          pairs, Z, S);
     } else if (nptiles > 0 && p.nb > 0) {
-      hipLaunchKernelGGL(schur_z_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z);
+      if (p.svariant != 7)
+        hipLaunchKernelGGL(schur_z_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z);
       const int G = (nptiles + 3) / 4;
       const int grid = ((G + 7) / 8) * 8;  // whole XCD stripes (extra workgroups exit)
 #ifdef MI_BA_AB_VARIANTS
@@ -3774,7 +3877,14 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
       else
 #endif
 #ifdef MI_BA_AB_VARIANTS
-      if (p.svariant == 5)
+      if (p.svariant == 7) {
+        // Z formed in the pair kernel from J + Linv (no schur_z pass)
+        const PairFlush& pf = pflush ? *pflush : nof;
+        hipLaunchKernelGGL((schur_pairs_j_kernel<CT>), dim3(G), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs, J, Linv,
+                           S, pf);
+        if (pf.pslot && pf.ndest > 0)
+          hipLaunchKernelGGL(schur_pairs_flush_kernel<CT>, dim3(pf.ndest), dim3(256), 0, s, p, pf, S);
+      } else if (p.svariant == 5)
         hipLaunchKernelGGL((schur_pairs_kernel<CT, false, true>), dim3(G), dim3(kBlock), 0, s, p, ptiles, nptiles,
                            pairs, Z, S, nof);
       else
@@ -3839,7 +3949,8 @@ void launch_grad_max_f(const DevProblem& p, const double* g, double* out, hipStr
 void launch_grad_max_points(const DevProblem& p, const DevPoint* vp, int64_t npv, const double* Vg, double* out,
                             hipStream_t s) {
   if (npv > 0)
-    hipLaunchKernelGGL(grad_max_points_kernel, dim3(grid_for(npv, kBlock)), dim3(kBlock), 0, s, p, vp, npv, Vg, out);
+    hipLaunchKernelGGL(grad_max_points_kernel, dim3((unsigned)std::min<int64_t>(grid_for(npv, kBlock), 1024)),
+                       dim3(kBlock), 0, s, p, vp, npv, Vg, out);
 }
 
 void launch_state_norms(const DevProblem& p, const double* qt_c, const double* cam_c, const double* X_c, bool with_f,

@@ -280,13 +280,14 @@ def test_lm_schur_pair_orders(gpu):
     XCD-striped mapping (schur_pairs_variant 0), in image-block order with
     dispatch-order mapping (4, blocks of 8 and 64 images), the JG records
     with two pairs per MFMA (6: Z_a Z_b' = J_f,a' (G_a' G_b) J_f,b) and
-    XCD-interleaved by first image with padding tiles (5) drive the same LM:
+    XCD-interleaved by first image with padding tiles (5) and the Z rows
+    formed in the pair kernel from J and Linv (7) drive the same LM:
     the same S up to the order of the float atomics (nf = 1593)."""
     sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
     res = []
-    orders = ((0, 32), (4, 8), (4, 64), (6, 8)) + (((5, 8),) if mi_ba.ab_build() else ())
+    orders = ((0, 32), (4, 8), (4, 64), (6, 8)) + (((5, 8), (7, 8)) if mi_ba.ab_build() else ())
     for var, blk in orders:
         with mi_ba.Context(opts, sc.copy()) as ctx:
             ctx.set_tuning("schur_pairs_variant", var)
