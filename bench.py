@@ -401,6 +401,7 @@ def main():
         bpb = bytes_per_block(cfg["model"], cfg["track"])
         achieved = bpb * nb / (avg_j * 1e-3) / 1e9 if avg_j > 0 else 0.0
         traffic, traffic_src = pmc_traffic(args.config, "reproj_jacobian_kernel") if world == 1 else (None, None)
+        warm_traffic, _ = pmc_traffic(args.config, "touch_kernel") if world == 1 else (None, None)
         out = {
             "metric": METRIC,
             "value": value,
@@ -431,7 +432,10 @@ def main():
                          # kernel (linearize_warm_inputs): the kernel's rate with that read's time added
                          "input_warm_ms": w_ms / w_n if w_n else 0.0,
                          "frac_incl_input_warm": (bpb * nb / ((avg_j + (w_ms / w_n if w_n else 0.0)) * 1e-3) / 1e9
-                                                  / HBM_PEAK_GBS) if avg_j > 0 else None},
+                                                  / HBM_PEAK_GBS) if avg_j > 0 else None,
+                         # the warm-up's own HBM bytes (same PMC summary), and the pair's
+                         "traffic_input_warm": warm_traffic,
+                         "traffic_incl_input_warm": (traffic + warm_traffic) if traffic and warm_traffic else None},
             "kernels_ms": {"reproj_jacobian": avg_j, "semantic_jacobian": s_ms / max(1, s_n),
                            "input_warm": w_ms / w_n if w_n else 0.0},
             "roofline_semantic": roofline_semantic(args.config, ns, s_ms / max(1, s_n)) if ns and world == 1 else None,
