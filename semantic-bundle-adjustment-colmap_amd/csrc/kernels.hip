@@ -3215,6 +3215,71 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_jg_kernel(DevProblem p, co
   }
 }
 
+// schur_pairs_variant 8: the JG records of variant 6 (one 256-B record per
+// block at F <= 13: J_f (2 x F) and G = Linv J_p' (3 x 2)), one pair per
+// v_mfma_f64_16x16x4f64 with K = 2 (the residual rows; K slots 2, 3 zero):
+// acc += J_f,a' (M J_f,b), M = G_a' G_b (2 x 2).  The pair's G blocks are
+// wave-uniform (scalar loads, M formed on every lane); per lane a pair costs
+// three vector loads (J_f,a[r][m], J_f,b[0..1][n]) from two records — four
+// 128-B lines per pair where Z rows take six.
+template <int CT, int U>
+__global__ __launch_bounds__(kBlock) void schur_pairs_jg1_kernel(DevProblem p, const DevPairTile* __restrict__ tiles,
+                                                                  int ntiles, const uint2* __restrict__ pairs,
+                                                                  const double* __restrict__ JG,
+                                                                  double* __restrict__ S, PairFlush pf) {
+  constexpr int F = 6 + CT, RW = jg_width(F);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = blockIdx.x * 4 + wv;
+  if (t >= ntiles) return;
+  const DevPairTile tl = tiles[t];
+  if (tl.count == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int m = lane & 15, k = lane >> 4;
+  const bool on = m < F && k < 2;
+  const int mm = m < F ? m : 0;
+  const int r = k & 1;
+  typedef double dvec4 __attribute__((ext_vector_type(4)));
+  dvec4 acc = {0.0, 0.0, 0.0, 0.0};
+  const uint32_t cnt = tl.count;
+  const uint2* pl = pairs + tl.start;
+  auto step = [&](const uint2 pr) {
+    const double* ga = JG + (size_t)pr.x * RW;
+    const double* gb = JG + (size_t)pr.y * RW;
+    // M[r][s] = sum_c G_a[c][r] G_b[c][s] (G[c][s] at 2F + 2c + s)
+    const double m0 = ga[2 * F + r] * gb[2 * F] + ga[2 * F + 2 + r] * gb[2 * F + 2] + ga[2 * F + 4 + r] * gb[2 * F + 4];
+    const double m1 =
+        ga[2 * F + r] * gb[2 * F + 1] + ga[2 * F + 2 + r] * gb[2 * F + 3] + ga[2 * F + 4 + r] * gb[2 * F + 5];
+    const double va = ga[r * F + mm];
+    const double vb = m0 * gb[mm] + m1 * gb[F + mm];
+    return std::pair<double, double>(on ? va : 0.0, on ? vb : 0.0);
+  };
+  uint32_t n = 0;
+  for (; n + U <= cnt; n += U) {
+    uint2 pr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint2 q = pl[n + u];
+      pr[u] = make_uint2(__builtin_amdgcn_readfirstlane(q.x), __builtin_amdgcn_readfirstlane(q.y));
+    }
+    double va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const auto v = step(pr[u]);
+      va[u] = v.first;
+      vb[u] = v.second;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va[u], vb[u], acc, 0, 0, 0);
+  }
+  for (; n < cnt; ++n) {
+    const uint2 q = pl[n];
+    const auto v = step(make_uint2(__builtin_amdgcn_readfirstlane(q.x), __builtin_amdgcn_readfirstlane(q.y)));
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v.first, v.second, acc, 0, 0, 0);
+  }
+  const double accv[4] = {acc[0], acc[1], acc[2], acc[3]};
+  pair_tile_store<F>(p, tl, t, lane, accv, S, pf);
+}
+
 // As schur_pairs_kernel, latency-hidden: the tile's pair list is staged once
 // in the wave's LDS slot (read back as broadcasts, no dependent global load
 // per pair), and the Z rows of U pairs are requested one step ahead, so the
@@ -3854,6 +3919,22 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
     constexpr int CT = decltype(c)::value;
     if (with_u && ntiles > 0)
       hipLaunchKernelGGL(dense_u_kernel<CT>, dim3(ntiles), dim3(kBlock), 0, s, p, tiles, cm_perm, J, S);
+#ifdef MI_BA_AB_VARIANTS
+    if (nptiles > 0 && p.nb > 0 && (p.svariant == 8 || p.svariant == 9)) {
+      // JG records, one pair per MFMA (K = 2), image-block tile order
+      const PairFlush& pf = pflush ? *pflush : nof;
+      hipLaunchKernelGGL(schur_jg_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z);
+      if (p.svariant == 8)
+        hipLaunchKernelGGL((schur_pairs_jg1_kernel<CT, 4>), dim3((nptiles + 3) / 4), dim3(kBlock), 0, s, p, ptiles,
+                           nptiles, pairs, Z, S, pf);
+      else
+        hipLaunchKernelGGL((schur_pairs_jg1_kernel<CT, 8>), dim3((nptiles + 3) / 4), dim3(kBlock), 0, s, p, ptiles,
+                           nptiles, pairs, Z, S, pf);
+      if (pf.pslot && pf.ndest > 0)
+        hipLaunchKernelGGL(schur_pairs_flush_kernel<CT>, dim3(pf.ndest), dim3(256), 0, s, p, pf, S);
+      return;
+    }
+#endif
     if (nptiles > 0 && p.nb > 0 && p.svariant == 6) {
       // JG records + two pairs per MFMA, image-block tile order (dispatch order)
       hipLaunchKernelGGL(schur_jg_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z);

@@ -1302,7 +1302,7 @@ void launch_schur_terms(mi_ba_context* ctx) {
   const PairFlush pf{ctx->pslot.ptr, ctx->spart.ptr, ctx->pdest.ptr, ctx->pself.ptr, ctx->npdest};
   launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
                      d.svariant == 5 ? ctx->ptiles_xcd.ptr
-                     : (d.svariant == 4 || d.svariant == 6 || d.svariant == 7) ? ctx->ptiles_blk.ptr
+                     : (d.svariant == 4 || d.svariant >= 6) ? ctx->ptiles_blk.ptr
                                                             : ctx->ptiles.ptr,
                      d.svariant == 5 ? ctx->nptiles_xcd : ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, false,
                      ctx->stream, ctx->det_sums && ctx->pflush_ok ? &pf : nullptr);
@@ -2314,7 +2314,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->sem_variant = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 7 &&
+  if (std::strcmp(key, "schur_pairs_variant") == 0 && value >= 0 && value <= 9 &&
       (value == 0 || value == 4 || value == 6 || ab_value(value, 0))) {
     ctx->dev.svariant = value;
     return MI_BA_OK;

@@ -287,7 +287,7 @@ def test_lm_schur_pair_orders(gpu):
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
     res = []
-    orders = ((0, 32), (4, 8), (4, 64), (6, 8)) + (((5, 8), (7, 8)) if mi_ba.ab_build() else ())
+    orders = ((0, 32), (4, 8), (4, 64), (6, 8)) + (((5, 8), (7, 8), (8, 8), (9, 8)) if mi_ba.ab_build() else ())
     for var, blk in orders:
         with mi_ba.Context(opts, sc.copy()) as ctx:
             ctx.set_tuning("schur_pairs_variant", var)
