@@ -1582,6 +1582,15 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
         decided = resolved = window_decides(a, fb, w, c.p2[2], c.mag, smp.label1, &c.st, &c.r);
       }
     }
+    if (!resolved && cand &&
+        (fb.x0 + fb.ncol <= 0 || fb.x0 >= a.W || fb.y0 + fb.nrow <= 0 || fb.y0 >= a.H)) {
+      // every reachable pixel (the centre's among them) lies outside the
+      // raster: the centre and every stencil point are OUT_OF_BOUNDS (f = 0),
+      // the flat test's outcome without a raster read (14 % of C4's samples)
+      c.st = MI_BA_OUT_OF_BOUNDS;
+      c.r = 0.0;
+      decided = resolved = true;
+    }
     if (!resolved) {
       // every raster read of the sample in one round trip: the centre pixel and the box
       const float2 sc = dl2[cin ? cpy * a.W + cpx : 0];

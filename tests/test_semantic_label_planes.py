@@ -59,10 +59,15 @@ def test_label_planes_bitwise(gpu, labels):
         if k != 1:  # the status is compared below, without the diagnostic mark
             assert np.array_equal(x, y)
     st_a, st_b = a[1], b[1]
-    settled_b = decode(st_b).sum()
     plain = lambda st: np.where(decode(st), st - 0x4000, st) % 0x10000  # noqa: E731
     assert np.array_equal(plain(st_a), plain(st_b))
-    assert decode(st_a).sum() == 0  # neither summary in use
+    # a box wholly outside the raster is decided without it in every mode
+    # (every stencil point OUT_OF_BOUNDS); the planes decide the rest
+    outside_a = decode(st_a) & (plain(st_a) == 0xFFFF)
+    assert outside_a.sum() > 0
+    assert np.array_equal(outside_a, decode(st_b) & (plain(st_b) == 0xFFFF))
+    settled_b = (decode(st_b) & ~outside_a).sum()
+    assert (decode(st_a) & ~outside_a).sum() == 0  # neither summary in use
     if labels == "many":
         assert settled_b == 0  # > 256 labels: no planes
     else:
