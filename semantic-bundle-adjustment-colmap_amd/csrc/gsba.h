@@ -54,6 +54,12 @@ struct GsbaState {
   DevArray<double> cyl_blk;          // [ncyl][cw (cw + 1) / 2] cylinder Schur-Jacobi blocks (packed upper)
   DevArray<double> prec_cyl;         // [ncyl][64]
   DevArray<double> partial;          // per-block cost
+  // deterministic sums: blocks are image-major with every cylinder once per
+  // image (block = image rank * ncyl + cylinder), so an image's blocks are
+  // contiguous and a cylinder's are strided; the per-owner kernels sum them
+  // in block order (no float atomics)
+  DevArray<double> ework;            // [nblocks] per-block scalar (J x, residual, model term)
+  DevArray<double> cstate;           // [2][ncyl] per-cylinder |y|^2, |y - y_c|^2
 };
 
 // Number of cylinder parameter slots the context must reserve (8 per

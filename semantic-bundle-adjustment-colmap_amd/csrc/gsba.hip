@@ -597,93 +597,9 @@ __device__ inline int sym6(int a, int c) { return a * 6 - (a * (a - 1)) / 2 + (c
 // packed upper index of (a, c), a <= c < n
 __device__ inline int symn(int n, int a, int c) { return a * n - (a * (a - 1)) / 2 + (c - a); }
 
-__global__ void gsba_fblock_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
-                                   const uint32_t* __restrict__ img_flags, const double* __restrict__ r,
-                                   const double* __restrict__ J, int64_t cyl0, int cyl_var, int cw,
-                                   double* __restrict__ pose_blk, double* __restrict__ cyl_blk,
-                                   double* __restrict__ bvec, double* __restrict__ udiag) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= nblocks) return;
-  const GsbaBlock b = blocks[k];
-  const double* Jr = J + 14 * (size_t)k;
-  const double rr = r[k];
-  const uint32_t pv = img_flags[b.img] & 1u;
-  if (gsba_slot(b, 0, cyl0, cyl_var, pv, cw) >= 0) {
-    for (int a = 0; a < 6; ++a) {
-      for (int c = a; c < 6; ++c) atomicAdd(pose_blk + 21 * (size_t)b.img + sym6(a, c), Jr[a] * Jr[c]);
-      atomicAdd(bvec + 6 * (size_t)b.img + a, Jr[a] * rr);
-      atomicAdd(udiag + 6 * (size_t)b.img + a, Jr[a] * Jr[a]);
-    }
-  }
-  if (gsba_slot(b, 6, cyl0, cyl_var, pv, cw) >= 0) {
-    const int64_t o = cyl0 + cw * (int64_t)b.cyl;
-    const int ps = cw * (cw + 1) / 2;
-    for (int a = 0; a < cw; ++a) {
-      for (int c = a; c < cw; ++c) atomicAdd(cyl_blk + ps * (size_t)b.cyl + symn(cw, a, c), Jr[6 + a] * Jr[6 + c]);
-      atomicAdd(bvec + o + a, Jr[6 + a] * rr);
-      atomicAdd(udiag + o + a, Jr[6 + a] * Jr[6 + a]);
-    }
-  }
-}
 
-// y += J'(J x) over the block's slots.
-__global__ void gsba_product_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
-                                    const uint32_t* __restrict__ img_flags, const double* __restrict__ J,
-                                    int64_t cyl0, int cyl_var, int cw, const double* __restrict__ x,
-                                    double* __restrict__ y) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= nblocks) return;
-  const GsbaBlock b = blocks[k];
-  const double* Jr = J + 14 * (size_t)k;
-  const uint32_t pv = img_flags[b.img] & 1u;
-  double e = 0.0;
-  for (int m = 0; m < 14; ++m) {
-    const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv, cw);
-    if (s >= 0) e += Jr[m] * x[s];
-  }
-  for (int m = 0; m < 14; ++m) {
-    const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv, cw);
-    if (s >= 0) atomicAdd(y + s, Jr[m] * e);
-  }
-}
 
-// S += J'J (upper triangle, row-major, leading dimension lds).
-__global__ void gsba_dense_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
-                                  const uint32_t* __restrict__ img_flags, const double* __restrict__ J, int64_t cyl0,
-                                  int cyl_var, int cw, int64_t lds, double* __restrict__ S) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)nblocks * 196) return;
-  const int k = (int)(t / 196), e = (int)(t % 196);
-  const int a = e / 14, c = e % 14;
-  const GsbaBlock b = blocks[k];
-  const uint32_t pv = img_flags[b.img] & 1u;
-  const int64_t ra = gsba_slot(b, a, cyl0, cyl_var, pv, cw), rc = gsba_slot(b, c, cyl0, cyl_var, pv, cw);
-  if (ra < 0 || rc < 0 || ra > rc) return;
-  const double* Jr = J + 14 * (size_t)k;
-  atomicAdd(S + ra * lds + rc, Jr[a] * Jr[c]);
-}
 
-// model cost change contribution -(e (r + e / 2)), e = J df
-__global__ void gsba_model_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
-                                  const uint32_t* __restrict__ img_flags, const double* __restrict__ r,
-                                  const double* __restrict__ J, int64_t cyl0, int cyl_var, int cw,
-                                  const double* __restrict__ df, double* __restrict__ out) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  double v = 0.0;
-  if (k < nblocks) {
-    const GsbaBlock b = blocks[k];
-    const double* Jr = J + 14 * (size_t)k;
-    const uint32_t pv = img_flags[b.img] & 1u;
-    double e = 0.0;
-    for (int m = 0; m < 14; ++m) {
-      const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv, cw);
-      if (s >= 0) e += Jr[m] * df[s];
-    }
-    v = -(e * (r[k] + e / 2.0));
-  }
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  if ((threadIdx.x & 63) == 0) atomicAdd(out, v);
-}
 
 // Ceres 2.1 QuaternionManifold::Plus on the cylinder qvec, Euclidean t, r,
 // h; the radius is projected onto its lower bound 0 (ParameterBlock::Plus).
@@ -722,22 +638,6 @@ __global__ void gsba_plus_by2_kernel(int ncyl, const double* __restrict__ cyl, c
   o[8] = 0.0;
 }
 
-// g += J'r over the block's slots (the raw gradient of the gradient
-// tolerance test).
-__global__ void gsba_gradient_kernel(const GsbaBlock* __restrict__ blocks, int nblocks,
-                                     const uint32_t* __restrict__ img_flags, const double* __restrict__ r,
-                                     const double* __restrict__ J, int64_t cyl0, int cyl_var, int cw,
-                                     double* __restrict__ g) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= nblocks) return;
-  const GsbaBlock b = blocks[k];
-  const double* Jr = J + 14 * (size_t)k;
-  const uint32_t pv = img_flags[b.img] & 1u;
-  for (int m = 0; m < 14; ++m) {
-    const int64_t s = gsba_slot(b, m, cyl0, cyl_var, pv, cw);
-    if (s >= 0) atomicAdd(g + s, Jr[m] * r[k]);
-  }
-}
 
 __device__ inline void gsba_atomic_max(double* out, double v) {
   if (v > 0.0) atomicMax(reinterpret_cast<unsigned long long*>(out), (unsigned long long)__double_as_longlong(v));
@@ -769,26 +669,205 @@ __global__ void gsba_grad_max_kernel(int ncyl, int by2, const double* __restrict
   gsba_atomic_max(out, mx);
 }
 
-// |y|^2 and |y - y_c|^2 of the cylinders' ambient coordinates into out[0..1].
-__global__ void gsba_state_kernel(int ncyl, int by2, const double* __restrict__ cyl, const double* __restrict__ cyl_c,
-                                  double* out) {
+
+// ---------------------------------------------------------------------------
+// Deterministic per-owner sums.  Blocks are image-major, one per (image,
+// cylinder): image rank r owns blocks [r ncyl, (r + 1) ncyl), cylinder c owns
+// blocks c, c + ncyl, ...  One workgroup per owner (images first, then
+// cylinders), one thread per output value, the owner's blocks summed in block
+// order; each output is added once.
+// ---------------------------------------------------------------------------
+__device__ inline void sym_pair(int n, int k, int* a, int* c) {
+  int aa = 0, rem = k;
+  while (rem >= n - aa) { rem -= n - aa; ++aa; }
+  *a = aa;
+  *c = aa + rem;
+}
+
+struct GsbaOwn {
+  const GsbaBlock* blocks;
+  const uint32_t* img_flags;
+  const double* J;
+  int nblocks, ncyl, nimg;  // nimg: images with blocks (nblocks / ncyl)
+  int64_t cyl0;
+  int cyl_var, cw;
+  __device__ int first(int o) const { return o < nimg ? o * ncyl : o - nimg; }
+  __device__ int step(int o) const { return o < nimg ? 1 : ncyl; }
+  __device__ int count(int o) const { return o < nimg ? ncyl : nimg; }
+  __device__ bool valid(int k, bool cyl_side) const {
+    const GsbaBlock b = blocks[k];
+    return gsba_slot(b, cyl_side ? 6 : 0, cyl0, cyl_var, img_flags[b.img] & 1u, cw) >= 0;
+  }
+};
+
+// f-blocks: the image's pose Schur-Jacobi block (21), b (6), diag U (6); the
+// cylinder's block (cw (cw + 1) / 2), b (cw), diag U (cw).
+__global__ void gsba_fblock_owner_kernel(GsbaOwn w, const double* __restrict__ r, double* __restrict__ pose_blk,
+                                         double* __restrict__ cyl_blk, double* __restrict__ bvec,
+                                         double* __restrict__ udiag) {
+  const int o = blockIdx.x;
+  const bool cs = o >= w.nimg;
+  const int n = cs ? w.cw : 6, ns = n * (n + 1) / 2;
+  const int v = threadIdx.x;
+  if (v >= ns + 2 * n) return;
+  const int off = cs ? 6 : 0;
+  int a = 0, c = 0, kind = 0;  // 0 block entry (a, c), 1 b[a], 2 diag[a]
+  if (v < ns) {
+    sym_pair(n, v, &a, &c);
+  } else {
+    kind = v < ns + n ? 1 : 2;
+    a = v - ns - (kind == 1 ? 0 : n);
+  }
+  double acc = 0.0;
+  bool any = false;
+  const int k0 = w.first(o), st = w.step(o), cnt = w.count(o);
+  for (int q = 0; q < cnt; ++q) {
+    const int k = k0 + q * st;
+    if (!w.valid(k, cs)) continue;
+    any = true;
+    const double* Jr = w.J + 14 * (size_t)k;
+    const double ja = Jr[off + a];
+    acc += kind == 0 ? ja * Jr[off + c] : (kind == 1 ? ja * r[k] : ja * ja);
+  }
+  if (!any) return;
+  if (!cs) {
+    const int img = w.blocks[k0].img;
+    if (kind == 0) pose_blk[21 * (size_t)img + sym6(a, c)] += acc;
+    else if (kind == 1) bvec[6 * (size_t)img + a] += acc;
+    else udiag[6 * (size_t)img + a] += acc;
+  } else {
+    const int cyl = o - w.nimg;
+    const int64_t s0 = w.cyl0 + w.cw * (int64_t)cyl;
+    if (kind == 0) cyl_blk[ns * (size_t)cyl + symn(n, a, c)] += acc;
+    else if (kind == 1) bvec[s0 + a] += acc;
+    else udiag[s0 + a] += acc;
+  }
+}
+
+// e_k = J_k x over the block's slots (the product's first half).
+__global__ void gsba_jx_kernel(GsbaOwn w, const double* __restrict__ x, double* __restrict__ e) {
   const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= w.nblocks) return;
+  const GsbaBlock b = w.blocks[k];
+  const double* Jr = w.J + 14 * (size_t)k;
+  const uint32_t pv = w.img_flags[b.img] & 1u;
+  double s = 0.0;
+  for (int m = 0; m < 14; ++m) {
+    const int64_t sl = gsba_slot(b, m, w.cyl0, w.cyl_var, pv, w.cw);
+    if (sl >= 0) s += Jr[m] * x[sl];
+  }
+  e[k] = s;
+}
+
+// y[slot] += sum over the owner's blocks of J_k[m] e_k (J'(J x) with e = J x,
+// the gradient J'r with e = r).
+__global__ void gsba_jte_owner_kernel(GsbaOwn w, const double* __restrict__ e, double* __restrict__ y) {
+  const int o = blockIdx.x;
+  const bool cs = o >= w.nimg;
+  const int m = threadIdx.x;
+  if (m >= (cs ? w.cw : 6)) return;
+  const int off = cs ? 6 : 0;
+  double acc = 0.0;
+  bool any = false;
+  const int k0 = w.first(o), st = w.step(o), cnt = w.count(o);
+  for (int q = 0; q < cnt; ++q) {
+    const int k = k0 + q * st;
+    if (!w.valid(k, cs)) continue;
+    any = true;
+    acc += w.J[14 * (size_t)k + off + m] * e[k];
+  }
+  if (!any) return;
+  if (!cs) y[6 * (size_t)w.blocks[k0].img + m] += acc;
+  else y[w.cyl0 + w.cw * (int64_t)(o - w.nimg) + m] += acc;
+}
+
+// S += J'J: the owners' diagonal blocks (upper triangle), then one thread per
+// (block, pose column, cylinder column) for the pose-cylinder entries (each
+// block is the only one of its (image, cylinder) pair: one writer each).
+__global__ void gsba_dense_owner_kernel(GsbaOwn w, int64_t lds, double* __restrict__ S) {
+  const int o = blockIdx.x;
+  const bool cs = o >= w.nimg;
+  const int n = cs ? w.cw : 6, ns = n * (n + 1) / 2;
+  const int v = threadIdx.x;
+  if (v >= ns) return;
+  int a, c;
+  sym_pair(n, v, &a, &c);
+  const int off = cs ? 6 : 0;
+  double acc = 0.0;
+  bool any = false;
+  const int k0 = w.first(o), st = w.step(o), cnt = w.count(o);
+  for (int q = 0; q < cnt; ++q) {
+    const int k = k0 + q * st;
+    if (!w.valid(k, cs)) continue;
+    any = true;
+    const double* Jr = w.J + 14 * (size_t)k;
+    acc += Jr[off + a] * Jr[off + c];
+  }
+  if (!any) return;
+  const int64_t s0 = cs ? w.cyl0 + w.cw * (int64_t)(o - w.nimg) : 6 * (int64_t)w.blocks[k0].img;
+  S[(s0 + a) * lds + (s0 + c)] += acc;
+}
+
+__global__ void gsba_dense_cross_kernel(GsbaOwn w, int64_t lds, double* __restrict__ S) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)w.nblocks * 6 * w.cw) return;
+  const int k = (int)(t / (6 * w.cw)), e = (int)(t % (6 * w.cw));
+  const int a = e / w.cw, c = e % w.cw;
+  const GsbaBlock b = w.blocks[k];
+  const uint32_t pv = w.img_flags[b.img] & 1u;
+  const int64_t ra = gsba_slot(b, a, w.cyl0, w.cyl_var, pv, w.cw), rc = gsba_slot(b, 6 + c, w.cyl0, w.cyl_var, pv, w.cw);
+  if (ra < 0 || rc < 0) return;
+  const double* Jr = w.J + 14 * (size_t)k;
+  S[ra * lds + rc] += Jr[a] * Jr[6 + c];
+}
+
+// per-block model term -(e (r + e / 2)), e = J df
+__global__ void gsba_model_terms_kernel(GsbaOwn w, const double* __restrict__ r, const double* __restrict__ df,
+                                        double* __restrict__ out) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= w.nblocks) return;
+  const GsbaBlock b = w.blocks[k];
+  const double* Jr = w.J + 14 * (size_t)k;
+  const uint32_t pv = w.img_flags[b.img] & 1u;
+  double e = 0.0;
+  for (int m = 0; m < 14; ++m) {
+    const int64_t s = gsba_slot(b, m, w.cyl0, w.cyl_var, pv, w.cw);
+    if (s >= 0) e += Jr[m] * df[s];
+  }
+  out[k] = -(e * (r[k] + e / 2.0));
+}
+
+// per-cylinder |y|^2 and |y - y_c|^2 into part[k], part[ncyl + k]
+__global__ void gsba_state_terms_kernel(int ncyl, int by2, const double* __restrict__ cyl,
+                                        const double* __restrict__ cyl_c, double* __restrict__ part) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= ncyl) return;
+  const int n = by2 ? 7 : 9;
   double vx = 0.0, vd = 0.0;
-  if (k < ncyl) {
-    const int n = by2 ? 7 : 9;
-    for (int m = 0; m < n; ++m) {
-      const double a = cyl[9 * (size_t)k + m], d = a - cyl_c[9 * (size_t)k + m];
-      vx += a * a;
-      vd += d * d;
+  for (int m = 0; m < n; ++m) {
+    const double a = cyl[9 * (size_t)k + m], d = a - cyl_c[9 * (size_t)k + m];
+    vx += a * a;
+    vd += d * d;
+  }
+  part[k] = vx;
+  part[ncyl + k] = vd;
+}
+
+// out[j] += the n values of part + j n summed in index order (one workgroup)
+__global__ __launch_bounds__(256) void gsba_ordered_add_kernel(const double* __restrict__ part, int n, int nout,
+                                                               double* __restrict__ out) {
+  __shared__ double s[256];
+  for (int j = 0; j < nout; ++j) {
+    double v = 0.0;
+    for (int k = threadIdx.x; k < n; k += 256) v += part[(size_t)j * n + k];
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+      if ((int)threadIdx.x < h) s[threadIdx.x] += s[threadIdx.x + h];
+      __syncthreads();
     }
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    vx += __shfl_xor(vx, off, 64);
-    vd += __shfl_xor(vd, off, 64);
-  }
-  if (threadIdx.x == 0) {
-    atomicAdd(out, vx);
-    atomicAdd(out + 1, vd);
+    if (threadIdx.x == 0) out[j] += s[0];
+    __syncthreads();
   }
 }
 
@@ -812,6 +891,21 @@ GsbaArgs make_args(mi_ba_context* ctx, const double* qt, const double* cyl) {
 }
 
 unsigned grid64(int64_t n) { return (unsigned)((n + 63) / 64); }
+
+GsbaOwn owners(mi_ba_context* ctx) {
+  const GsbaState* G = ctx->gsba;
+  GsbaOwn w;
+  w.blocks = G->blocks.ptr;
+  w.img_flags = ctx->dev.img_flags;
+  w.J = G->J.ptr;
+  w.nblocks = G->nblocks;
+  w.ncyl = G->ncyl;
+  w.nimg = G->ncyl > 0 ? G->nblocks / G->ncyl : 0;
+  w.cyl0 = ctx->dev.cyl0;
+  w.cyl_var = ctx->dev.cyl_var;
+  w.cw = G->cw;
+  return w;
+}
 
 }  // namespace
 
@@ -923,7 +1017,8 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
       G->sem_total.alloc(std::max<size_t>(1, slot_images.size())) || G->cyl.alloc(cyl.size()) ||
       G->cyl_c.alloc(cyl.size()) || G->iou.alloc(std::max<int64_t>(1, G->nevals)) || G->r.alloc(nb) ||
       G->J.alloc(14 * (size_t)nb) || G->cyl_blk.alloc(36 * (size_t)std::max(1, G->ncyl)) ||
-      G->prec_cyl.alloc(64 * (size_t)std::max(1, G->ncyl)) || G->partial.alloc(nb))
+      G->prec_cyl.alloc(64 * (size_t)std::max(1, G->ncyl)) || G->partial.alloc(nb) || G->ework.alloc(nb) ||
+      G->cstate.alloc(2 * (size_t)std::max(1, G->ncyl)))
     return MI_BA_ERR_OUT_OF_MEMORY;
   if ((G->nblocks &&
        (hipMemcpy(G->blocks.ptr, G->blocks_host.data(), G->nblocks * sizeof(GsbaBlock), hipMemcpyHostToDevice) ||
@@ -1021,9 +1116,9 @@ void gsba_add_fblock(mi_ba_context* ctx) {
   hipStream_t s = ctx->stream;
   (void)hipMemsetAsync(G->cyl_blk.ptr, 0, G->cyl_blk.bytes(), s);
   if (!G->nblocks) return;
-  hipLaunchKernelGGL(gsba_fblock_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, s, G->blocks.ptr, G->nblocks,
-                     ctx->dev.img_flags, G->r.ptr, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw,
-                     ctx->pose_blk.ptr, G->cyl_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr);
+  const GsbaOwn w = owners(ctx);
+  hipLaunchKernelGGL(gsba_fblock_owner_kernel, dim3(w.nimg + w.ncyl), dim3(64), 0, s, w, G->r.ptr, ctx->pose_blk.ptr,
+                     G->cyl_blk.ptr, ctx->bvec.ptr, ctx->udiag.ptr);
 }
 
 void gsba_finalize(mi_ba_context* ctx, int first, int reuse_diag, double radius) {
@@ -1038,8 +1133,9 @@ void gsba_finalize(mi_ba_context* ctx, int first, int reuse_diag, double radius)
 void gsba_schur_product(mi_ba_context* ctx, const double* x, double* y) {
   GsbaState* G = ctx->gsba;
   if (!G->nblocks) return;
-  hipLaunchKernelGGL(gsba_product_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, ctx->stream, G->blocks.ptr,
-                     G->nblocks, ctx->dev.img_flags, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw, x, y);
+  const GsbaOwn w = owners(ctx);
+  hipLaunchKernelGGL(gsba_jx_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, ctx->stream, w, x, G->ework.ptr);
+  hipLaunchKernelGGL(gsba_jte_owner_kernel, dim3(w.nimg + w.ncyl), dim3(64), 0, ctx->stream, w, G->ework.ptr, y);
 }
 
 void gsba_precond(mi_ba_context* ctx, const double* r, double* z) {
@@ -1052,17 +1148,20 @@ void gsba_precond(mi_ba_context* ctx, const double* r, double* z) {
 void gsba_add_dense(mi_ba_context* ctx, double* S) {
   GsbaState* G = ctx->gsba;
   if (!G->nblocks) return;
-  const int64_t n = (int64_t)G->nblocks * 196;
-  hipLaunchKernelGGL(gsba_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, G->blocks.ptr,
-                     G->nblocks, ctx->dev.img_flags, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw, ctx->dev.lds, S);
+  const GsbaOwn w = owners(ctx);
+  hipLaunchKernelGGL(gsba_dense_owner_kernel, dim3(w.nimg + w.ncyl), dim3(64), 0, ctx->stream, w, ctx->dev.lds, S);
+  const int64_t n = (int64_t)G->nblocks * 6 * G->cw;
+  hipLaunchKernelGGL(gsba_dense_cross_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, w,
+                     ctx->dev.lds, S);
 }
 
 void gsba_model_cost(mi_ba_context* ctx, const double* df, double* d_out) {
   GsbaState* G = ctx->gsba;
   if (!G->nblocks) return;
-  hipLaunchKernelGGL(gsba_model_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, ctx->stream, G->blocks.ptr,
-                     G->nblocks, ctx->dev.img_flags, G->r.ptr, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw, df,
-                     d_out);
+  const GsbaOwn w = owners(ctx);
+  hipLaunchKernelGGL(gsba_model_terms_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, ctx->stream, w, G->r.ptr, df,
+                     G->ework.ptr);
+  hipLaunchKernelGGL(gsba_ordered_add_kernel, dim3(1), dim3(256), 0, ctx->stream, G->ework.ptr, G->nblocks, 1, d_out);
 }
 
 void gsba_plus(mi_ba_context* ctx, const double* df) {
@@ -1083,8 +1182,8 @@ void gsba_plus(mi_ba_context* ctx, const double* df) {
 void gsba_add_gradient(mi_ba_context* ctx, double* g) {
   GsbaState* G = ctx->gsba;
   if (!G->nblocks) return;
-  hipLaunchKernelGGL(gsba_gradient_kernel, dim3(grid64(G->nblocks)), dim3(64), 0, ctx->stream, G->blocks.ptr,
-                     G->nblocks, ctx->dev.img_flags, G->r.ptr, G->J.ptr, ctx->dev.cyl0, ctx->dev.cyl_var, G->cw, g);
+  const GsbaOwn w = owners(ctx);
+  hipLaunchKernelGGL(gsba_jte_owner_kernel, dim3(w.nimg + w.ncyl), dim3(64), 0, ctx->stream, w, G->r.ptr, g);
 }
 
 void gsba_grad_max(mi_ba_context* ctx, const double* g, double* out) {
@@ -1097,8 +1196,9 @@ void gsba_grad_max(mi_ba_context* ctx, const double* g, double* out) {
 void gsba_state_norms(mi_ba_context* ctx, double* out) {
   GsbaState* G = ctx->gsba;
   if (!ctx->dev.cyl_var || G->ncyl == 0) return;
-  hipLaunchKernelGGL(gsba_state_kernel, dim3(grid64(G->ncyl)), dim3(64), 0, ctx->stream, G->ncyl, G->by2 ? 1 : 0,
-                     G->cyl.ptr, G->cyl_c.ptr, out);
+  hipLaunchKernelGGL(gsba_state_terms_kernel, dim3(grid64(G->ncyl)), dim3(64), 0, ctx->stream, G->ncyl, G->by2 ? 1 : 0,
+                     G->cyl.ptr, G->cyl_c.ptr, G->cstate.ptr);
+  hipLaunchKernelGGL(gsba_ordered_add_kernel, dim3(1), dim3(256), 0, ctx->stream, G->cstate.ptr, G->ncyl, 2, out);
 }
 
 void gsba_accept(mi_ba_context* ctx) {
