@@ -157,6 +157,10 @@ struct mi_ba_context {
   miba::DevArray<uint8_t> pself;           // [nslots]
   int npdest = 0;
   bool pflush_ok = false;
+  miba::DevArray<uint4> podest, pochunk;   // shared cameras: owner pairs, their entry runs (PairFlush)
+  miba::DevArray<uint32_t> poent;
+  miba::DevArray<double> popart;           // [nochunk][64]
+  int npodest = 0, npochunk = 0;
   miba::DevArray<uint2> pairs;             // (a, b) block pairs bucketed by image pair
   int nptiles = 0;
   miba::DevArray<int32_t> info;

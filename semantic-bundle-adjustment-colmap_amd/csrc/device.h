@@ -85,7 +85,22 @@ struct PairFlush {
   const uint4* dest;     // [ndest] (ia, ib, first slot, slot count)
   const uint8_t* self;   // [nslots] the slot's tile holds self pairs (a == b)
   int ndest;
+  // Shared cameras (several images per camera): every tile's accumulator
+  // goes to part[tile] and the S blocks are summed per owner pair instead
+  // (schur_owner_chunk_kernel + schur_owner_flush_kernel).  An owner is a
+  // pose (image i: kOwnerPose | i) or a camera (kOwnerCam | c); a tile (ia,
+  // ib) holds the four owner-pair quadrants (pose ia | cam of ia) x (pose ib
+  // | cam of ib).  oent: (tile << 4 | quadrant << 2 | swapped << 1 | self),
+  // tile order per owner pair; ochunk: (owner pair, first entry, entries) in
+  // runs of <= 256, summed into opart[chunk][64]; odest: (X, Y, first chunk,
+  // chunks), X before Y in S's slot order.  odest null: the route above.
+  const uint4* odest;
+  const uint4* ochunk;
+  const uint32_t* oent;
+  double* opart;
+  int nodest, nochunk;
 };
+constexpr uint32_t kOwnerCam = 1u << 31;
 
 struct DevProblem {
   int model;           // camera model of every camera, or kMixedModels (per-camera cam_model)

@@ -3084,6 +3084,55 @@ __global__ __launch_bounds__(256) void schur_pairs_flush_kernel(DevProblem p, Pa
   S[ra <= rb ? ra * p.lds + rb : rb * p.lds + ra] -= v;
 }
 
+// Shared cameras (PairFlush::odest): one workgroup per run of an owner
+// pair's entries, thread (i, j) = element (X_i, Y_j) of the owner-pair block
+// (X_i the owner's i-th slot: pose 0..5 or camera 0..ct-1): the run's tile
+// partials summed in entry order into opart[run][8 i + j].  A quadrant whose
+// owners were swapped contributes its transposed element; an owner paired
+// with itself takes the upper triangle, a tile of a != b pairs contributing
+// both mirrored entries (twice on the diagonal), a self tile its upper one.
+__device__ inline double owner_quadrant_value(const double* __restrict__ g, uint32_t e, int i, int j, bool same) {
+  const int q = (e >> 2) & 3;
+  const int ro = (q & 2) ? 6 : 0, co = (q & 1) ? 6 : 0;
+  const bool sw = (e >> 1) & 1, self = e & 1;
+  if (!same) return sw ? g[mfma_d_index(ro + j, co + i)] : g[mfma_d_index(ro + i, co + j)];
+  if (self) return g[mfma_d_index(ro + i, co + j)];
+  return i == j ? 2.0 * g[mfma_d_index(ro + i, co + i)] : g[mfma_d_index(ro + i, co + j)] + g[mfma_d_index(ro + j, co + i)];
+}
+
+__global__ __launch_bounds__(64) void schur_owner_chunk_kernel(DevProblem p, PairFlush pf) {
+  const uint4 c = pf.ochunk[blockIdx.x];
+  const uint4 d = pf.odest[c.x];
+  const int i = threadIdx.x >> 3, j = threadIdx.x & 7;
+  const int nx = (d.x & kOwnerCam) ? p.ct : 6, ny = (d.y & kOwnerCam) ? p.ct : 6;
+  const bool same = d.x == d.y;
+  double v = 0.0;
+  if (i < nx && j < ny && !(same && i > j)) {
+    for (uint32_t k = 0; k < c.z; ++k) {
+      const uint32_t e = pf.oent[c.y + k];
+      v += owner_quadrant_value(pf.part + (size_t)(e >> 4) * 256, e, i, j, same);
+    }
+  }
+  pf.opart[(size_t)blockIdx.x * 64 + threadIdx.x] = v;
+}
+
+// The owner pair's runs added in run order and subtracted from S once
+// (variable owners only: a constant pose or camera has no S slots in use).
+__global__ __launch_bounds__(64) void schur_owner_flush_kernel(DevProblem p, PairFlush pf, double* __restrict__ S) {
+  const uint4 d = pf.odest[blockIdx.x];
+  const int i = threadIdx.x >> 3, j = threadIdx.x & 7;
+  const bool xc = d.x & kOwnerCam, yc = d.y & kOwnerCam;
+  const uint32_t xi = d.x & ~kOwnerCam, yi = d.y & ~kOwnerCam;
+  const int nx = xc ? p.ct : 6, ny = yc ? p.ct : 6;
+  if (i >= nx || j >= ny || (d.x == d.y && i > j)) return;
+  if (!(xc ? p.cam_var[xi] != 0 : (p.img_flags[xi] & 1u)) || !(yc ? p.cam_var[yi] != 0 : (p.img_flags[yi] & 1u))) return;
+  double v = 0.0;
+  for (uint32_t k = 0; k < d.w; ++k) v += pf.opart[(size_t)(d.z + k) * 64 + threadIdx.x];
+  const int64_t ra = xc ? fslot(p, 0, xi, 6 + i) : fslot(p, xi, 0, i);
+  const int64_t rb = yc ? fslot(p, 0, yi, 6 + j) : fslot(p, yi, 0, j);
+  S[ra <= rb ? ra * p.lds + rb : rb * p.lds + ra] -= v;
+}
+
 // schur_pairs_variant 6: per block the record JG_a = [J_f,a (2 x F, row-major),
 // G_a = Linv J_p,a' (3 x 2), zero pad] of jg_width(F) doubles (256 B at F <=
 // 13: two aligned 128-B lines, where a Z row of 3 F doubles spans three), so
@@ -3975,8 +4024,14 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
         const PairFlush& pf = pflush ? *pflush : nof;
         hipLaunchKernelGGL((schur_pairs_kernel<CT, false>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs,
                            Z, S, pf);
-        if (pf.pslot && pf.ndest > 0)
+        if (pf.pslot && pf.odest) {
+          if (pf.nochunk > 0) {
+            hipLaunchKernelGGL(schur_owner_chunk_kernel, dim3(pf.nochunk), dim3(64), 0, s, p, pf);
+            hipLaunchKernelGGL(schur_owner_flush_kernel, dim3(pf.nodest), dim3(64), 0, s, p, pf, S);
+          }
+        } else if (pf.pslot && pf.ndest > 0) {
           hipLaunchKernelGGL(schur_pairs_flush_kernel<CT>, dim3(pf.ndest), dim3(256), 0, s, p, pf, S);
+        }
       } else {
         hipLaunchKernelGGL(schur_pairs_kernel<CT>, dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs, Z, S,
                            nof);

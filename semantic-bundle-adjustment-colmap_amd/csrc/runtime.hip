@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <map>
 #include <numeric>
 #include <unordered_map>
 
@@ -327,6 +328,62 @@ static void timer_collect(mi_ba_context* ctx) {
 // gather the Z rows of ~2B images only — a working set the 256 MB MALL holds
 // (2.9 MB of Z per image at C4), where the first-image order scatters the
 // second image's rows over every image.
+// The deterministic route with shared cameras (PairFlush::odest): every
+// tile of the image-block order writes its accumulator to its own partial;
+// the S blocks are summed per owner pair (pose / camera of the tile's two
+// images) from those partials in tile order, long owner-pair lists (a
+// camera shared by many images) in runs of 256 entries whose sums are then
+// added in run order.
+mi_ba_status order_owner_flush(mi_ba_context* ctx, const std::vector<DevPairTile>& tb) {
+  const mi_ba_problem* p = &ctx->problem;
+  std::map<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>> lists;
+  for (uint32_t k = 0; k < (uint32_t)tb.size(); ++k) {
+    const DevPairTile& tl = tb[k];
+    const uint32_t ca = (uint32_t)p->image_camera[tl.ia], cb = (uint32_t)p->image_camera[tl.ib];
+    for (uint32_t q = 0; q < 4; ++q) {
+      if (tl.self && q == 2) continue;  // a self tile's (camera, pose) quadrant is the mirror of (pose, camera)
+      uint32_t x = (q & 2) ? kOwnerCam | ca : tl.ia, y = (q & 1) ? kOwnerCam | cb : tl.ib;
+      uint32_t sw = 0;
+      if (x > y) {
+        std::swap(x, y);
+        sw = 1;
+      }
+      lists[{x, y}].push_back(k << 4 | q << 2 | sw << 1 | (tl.self ? 1u : 0u));
+    }
+  }
+  if (tb.size() >= (1u << 27)) return MI_BA_ERR_INVALID_ARGUMENT;
+  std::vector<uint4> dest, chunk;
+  std::vector<uint32_t> ent;
+  constexpr uint32_t kRun = 256;
+  for (auto& kv : lists) {
+    const std::vector<uint32_t>& l = kv.second;
+    const uint32_t c0 = (uint32_t)chunk.size();
+    for (uint32_t f = 0; f < l.size(); f += kRun)
+      chunk.push_back(make_uint4((uint32_t)dest.size(), (uint32_t)ent.size() + f,
+                                 std::min<uint32_t>(kRun, (uint32_t)l.size() - f), 0u));
+    dest.push_back(make_uint4(kv.first.first, kv.first.second, c0, (uint32_t)chunk.size() - c0));
+    ent.insert(ent.end(), l.begin(), l.end());
+  }
+  std::vector<int32_t> ps(tb.size());
+  for (size_t k = 0; k < tb.size(); ++k) ps[k] = (int32_t)k;
+  if (ctx->pslot.alloc(std::max<size_t>(1, ps.size())) || ctx->spart.alloc(std::max<size_t>(1, tb.size()) * 256) ||
+      ctx->podest.alloc(std::max<size_t>(1, dest.size())) || ctx->pochunk.alloc(std::max<size_t>(1, chunk.size())) ||
+      ctx->poent.alloc(std::max<size_t>(1, ent.size())) || ctx->popart.alloc(std::max<size_t>(1, chunk.size()) * 64))
+    return MI_BA_ERR_OUT_OF_MEMORY;
+  if ((!ps.empty() && hipMemcpy(ctx->pslot.ptr, ps.data(), ps.size() * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+      (!dest.empty() && hipMemcpy(ctx->podest.ptr, dest.data(), dest.size() * sizeof(uint4), hipMemcpyHostToDevice) !=
+                            hipSuccess) ||
+      (!chunk.empty() &&
+       hipMemcpy(ctx->pochunk.ptr, chunk.data(), chunk.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess) ||
+      (!ent.empty() && hipMemcpy(ctx->poent.ptr, ent.data(), ent.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+    return MI_BA_ERR_HIP;
+  ctx->npdest = 0;
+  ctx->npodest = (int)dest.size();
+  ctx->npochunk = (int)chunk.size();
+  ctx->pflush_ok = true;
+  return MI_BA_OK;
+}
+
 mi_ba_status order_block_tiles(mi_ba_context* ctx) {
 #ifdef MI_BA_AB_VARIANTS
   // XCD-interleaved order (schur_pairs_variant 5, tools build: measured
@@ -386,12 +443,13 @@ mi_ba_status order_block_tiles(mi_ba_context* ctx) {
   // camera on at most one image: a shared camera's columns gather many image
   // pairs' tiles, which stay on float atomics.
   ctx->pflush_ok = false;
+  ctx->npodest = ctx->npochunk = 0;
   {
     const mi_ba_problem* p = &ctx->problem;
     std::vector<int> per_cam(p->num_cameras, 0);
     bool distinct = true;
     for (int i = 0; i < p->num_images && distinct; ++i) distinct = ++per_cam[p->image_camera[i]] <= 1;
-    if (!distinct) return MI_BA_OK;
+    if (!distinct) return order_owner_flush(ctx, tb);
   }
   std::unordered_map<uint64_t, uint32_t> didx;
   std::vector<std::vector<uint32_t>> dtiles;
@@ -1299,7 +1357,17 @@ void launch_schur_terms(mi_ba_context* ctx) {
   const DevProblem& d = ctx->dev;
   hipEvent_t stop;
   timer_begin(ctx, "schur_build", &stop);
-  const PairFlush pf{ctx->pslot.ptr, ctx->spart.ptr, ctx->pdest.ptr, ctx->pself.ptr, ctx->npdest};
+  const PairFlush pf{ctx->pslot.ptr,
+                     ctx->spart.ptr,
+                     ctx->pdest.ptr,
+                     ctx->pself.ptr,
+                     ctx->npdest,
+                     ctx->npodest ? ctx->podest.ptr : nullptr,
+                     ctx->pochunk.ptr,
+                     ctx->poent.ptr,
+                     ctx->popart.ptr,
+                     ctx->npodest,
+                     ctx->npochunk};
   launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
                      d.svariant == 5 ? ctx->ptiles_xcd.ptr
                      : (d.svariant == 4 || d.svariant >= 6) ? ctx->ptiles_blk.ptr

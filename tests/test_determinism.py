@@ -5,7 +5,8 @@ float atomics: the tile passes' per-tile partials summed per image / camera
 (kernels.hip owner_flush_kernel: S's image blocks, b, diag(U), the
 Schur-Jacobi blocks, every implicit Schur product, the gradient), the
 explicit Schur pair tiles written once or summed per S block in tile order
-(schur_pairs_flush_kernel; cameras not shared between images), the semantic
+(schur_pairs_flush_kernel when no camera is shared between images, else
+per (pose | camera) owner pair from every tile's partial), the semantic
 term's deferred samples listed in sample order and its pair blocks summed in
 chunk order, then per image / S block in pair order (semantic.hip
 deferred_order_kernel, pair_reduce_kernel and the owner kernels).  So two
@@ -27,6 +28,17 @@ def scene(seed=5):
                                                    extra=(-0.1, 0.01, 1e-4, -1e-4), seed=seed)).gauge()
 
 
+def shared(sc, ncam):
+    """The same scene with image i on camera i % ncam (the generator gives
+    every camera the same intrinsics, so the observations stay consistent)."""
+    sc = sc.copy()
+    sc.image_camera = (np.arange(sc.num_images) % ncam).astype(np.int32)
+    sc.camera_params = sc.camera_params[:ncam].copy()
+    if sc.camera_constant is not None:
+        sc.camera_constant = sc.camera_constant[:ncam].copy()
+    return sc
+
+
 def semantic(sc):
     depth, label = mi_ba.render_semantic(sc, 200, 200, plane_z=1.0, cell=0.2)
     I = sc.num_images
@@ -45,9 +57,14 @@ def run(sc, sem, solver, det=1):
 
 
 @pytest.mark.parametrize("solver", [mi_ba.SOLVER_DENSE_SCHUR, mi_ba.SOLVER_ITERATIVE_SCHUR])
-@pytest.mark.parametrize("case", ["geo", "sem"])
+@pytest.mark.parametrize("case", ["geo", "sem", "shared4", "shared1"])
 def test_lm_bitwise_reproducible(gpu, case, solver):
+    """shared4 / shared1: cameras shared by several images (4 cameras, one
+    camera): the Schur pair blocks are summed per (pose | camera) owner pair
+    from every tile's partial (schur_owner_chunk / schur_owner_flush)."""
     sc = scene()
+    if case.startswith("shared"):
+        sc = shared(sc, int(case[-1]))
     sem = semantic(sc) if case == "sem" else None
     s0, a = run(sc, sem, solver)
     s1, b = run(sc, sem, solver)
@@ -60,12 +77,29 @@ def test_lm_bitwise_reproducible(gpu, case, solver):
 
 
 @pytest.mark.parametrize("solver", [mi_ba.SOLVER_DENSE_SCHUR, mi_ba.SOLVER_ITERATIVE_SCHUR])
-def test_atomic_flush_takes_the_same_steps(gpu, solver):
+@pytest.mark.parametrize("ncam", [0, 4, 1])
+def test_atomic_flush_takes_the_same_steps(gpu, solver, ncam):
     """The float-atomic flushes (deterministic_sums 0) sum the same terms in
-    another order: the same steps, costs equal to rounding."""
+    another order: the same steps, costs equal to rounding (one camera per
+    image, or ncam cameras shared by the images)."""
     sc = scene(seed=6)
+    if ncam:
+        sc = shared(sc, ncam)
     sem = semantic(sc)
     s0, _ = run(sc, sem, solver, det=1)
     s1, _ = run(sc, sem, solver, det=0)
     assert (s1.num_successful_steps, s1.num_unsuccessful_steps) == (s0.num_successful_steps, s0.num_unsuccessful_steps)
     assert abs(s1.final_cost - s0.final_cost) <= 1e-10 * s0.final_cost
+
+
+@pytest.mark.parametrize("ncam", [4, 1])
+def test_shared_camera_lm_matches_oracle(gpu, ncam):
+    """The owner-pair flush builds the same S as the oracle's dense Schur
+    solve: shared cameras, exact LM, the oracle's steps and cost."""
+    import oracle
+    sc = shared(scene(seed=7), ncam)
+    opts = mi_ba.default_options(max_num_iterations=6)
+    s_o = oracle.solve(opts, sc.copy())
+    s_g, _ = run(sc, None, mi_ba.SOLVER_DENSE_SCHUR)
+    assert (s_g.num_successful_steps, s_g.num_unsuccessful_steps) == (s_o.num_successful_steps, s_o.num_unsuccessful_steps)
+    assert abs(s_g.final_cost - s_o.final_cost) <= 1e-9 * s_o.final_cost
