@@ -13,7 +13,7 @@ import time
 
 import numpy as np
 
-if "--overlap" in sys.argv or "--ab" in sys.argv:
+if "--overlap" in sys.argv or "--ab" in sys.argv or "--conc" in sys.argv:
     os.environ.setdefault("MI_BA_LIB", "ab")  # linearize_overlap: the tools-only build (make ab)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "semantic-bundle-adjustment-colmap_amd"))
@@ -28,6 +28,9 @@ ap.add_argument("--overlap", action="store_true",
                 help="the semantic pass on a second stream beside the reprojection kernel (1) or only its "
                      "deferred pass (2), with the warm-up (tools build)")
 ap.add_argument("--ab", action="store_true", help="the tools build (semantic_deferred_variant)")
+ap.add_argument("--conc", action="store_true",
+                help="the warm-up on a side stream beside the semantic deferred pass (linearize_warm_concurrent "
+                     "range mask, tools build) instead of serially before the reprojection kernel")
 args = ap.parse_args()
 sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
 ctx = mi_ba.Context(mi_ba.default_options(), sc, sem)
@@ -42,6 +45,8 @@ CONFIGS = [(15, 2, 0, 1, 2048, 24, 0, 0, 4, v) for v in range(5)] if args.ab els
     [(15, 2, 0), (15, 2, 0, 1, 2048, 24, 0, 0, 8)]
 if args.overlap:
     CONFIGS = [(15, 2, 0), (15, 2, 1), (15, 2, 2), (0, 2, 1)]
+if args.conc:  # cfg[2] is the concurrent range mask here
+    CONFIGS = [(15, 2, 0), (0, 2, 15), (0, 2, 1), (14, 2, 1), (0, 2, 7)]
 
 
 def apply(cfg):
@@ -57,6 +62,8 @@ def apply(cfg):
         ctx.set_tuning("semantic_deferred_variant", cfg[9])
     if args.overlap:
         ctx.set_tuning("linearize_overlap", cfg[2])
+    if args.conc:
+        ctx.set_tuning("linearize_warm_concurrent", cfg[2])
 
 
 costs, same = {}, {}
