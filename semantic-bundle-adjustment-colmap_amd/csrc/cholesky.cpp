@@ -440,6 +440,34 @@ __device__ __forceinline__ void flag_wait(const unsigned* f, unsigned epoch, uns
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
+// flag_wait without the acquire: for consumers whose every load of the
+// handed-off bytes is an sc1 load of bytes the producer stored sc1 and
+// drained before the flag (MI355X_MICROARCH.md §visibility, table row 1)
+__device__ __forceinline__ void flag_poll(const unsigned* f, unsigned epoch, unsigned* err, unsigned limit) {
+  if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) return;
+  const uint64_t t0 = wall_clock64();
+  for (unsigned spin = 0;; ++spin) {
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) return;
+    if (limit == 0u || ((spin & 15u) == 15u && wall_clock64() - t0 >= limit) ||
+        ((spin & 255u) == 255u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+      __hip_atomic_fetch_or(err, kCholErrWait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// 8-byte global sc1 load / store (relaxed agent-scope atomics on the global
+// address space: global_load/store_dwordx2 sc1)
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(
+      (const __attribute__((address_space(1))) unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)p,
+                     (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int kSweepWaves = 4;
 typedef double sweep_dvec2 __attribute__((ext_vector_type(2)));
 
@@ -450,7 +478,10 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
-template <bool FWD>
+// SC1: the block results x handed over as sc1 stores drained before a
+// relaxed flag, read by sc1 loads after a relaxed poll (no release /
+// acquire fences); one workgroup per CU (its u / v registers)
+template <bool FWD, bool SC1 = false>
 __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const double* __restrict__ L, int lda, int n,
                                                                       double* x, unsigned* ctrl, unsigned epoch,
                                                                       unsigned* err, unsigned limit) {
@@ -510,8 +541,13 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
         for (int r = 0; r < kTB; ++r) v[r] = src[min(r, wj - 1)];
       }
     }
-    flag_wait(flag + jb, epoch, err, limit);
-    xs[wv][lane] = lane < wj ? x[c0 + lane] : 0.0;
+    if (SC1) {
+      flag_poll(flag + jb, epoch, err, limit);
+      xs[wv][lane] = lane < wj ? ld_sc1(x + c0 + lane) : 0.0;
+    } else {
+      flag_wait(flag + jb, epoch, err, limit);
+      xs[wv][lane] = lane < wj ? x[c0 + lane] : 0.0;
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
@@ -541,6 +577,12 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
       const double zu = z - u[r] * xr;
       z = lane == r ? xr : (lane < r ? zu : z);
     }
+  }
+  if (SC1) {
+    if (lane < w) st_sc1(x + r0 + lane, z);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(flag + ib, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
   }
   if (lane < w) x[r0 + lane] = z;
   __threadfence();
@@ -696,8 +738,28 @@ __device__ __forceinline__ int pf_rows(int r, int kb, int nc, int mrows) {
   return r < nc ? min(64, kb - 64 * r) : min(64, mrows - kb - 64 * (r - nc));
 }
 
+// WM (wait mode): 0 every wave polls and takes the agent acquire; 1 one wave
+// polls and takes the acquire for the workgroup (the acquire invalidates the
+// CU's L1 for all its waves), its s_waitcnt holding the barrier until the
+// invalidate has completed (MI355X_MICROARCH.md §visibility, consumer form);
+// 2 one wave polls, no acquire: every load of the handed-off tiles is an sc1
+// load (PfStage<true>) of bytes stored sc1 and drained before the flag, one
+// workgroup per CU (the kernel's registers allow one) — the guide's table row
+// 1.  Called in workgroup-uniform control flow.
+template <int WM>
 __device__ __forceinline__ void pf_wait(const unsigned* f, unsigned epoch, unsigned* err, unsigned limit) {
-  flag_wait(f, epoch, err, limit);
+  if constexpr (WM == 1) {
+    if (threadIdx.x < 64) {
+      flag_wait(f, epoch, err, limit);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  } else if constexpr (WM == 2) {
+    if (threadIdx.x < 64) flag_poll(f, epoch, err, limit);
+    __syncthreads();
+  } else {
+    flag_wait(f, epoch, err, limit);
+  }
 }
 
 // acc (wave w: rows 16w..16w+15 of the 64x64 tile, column tiles t = 0..3,
@@ -852,6 +914,33 @@ __device__ __forceinline__ void pf_diag_inv16(const double* M, const double* din
   }
 }
 
+// pf_diag_inv16 with the operand loads ahead of the arithmetic: the 16
+// reciprocal pivots up front and row i + 1's multipliers loaded while row i's
+// substitution runs (the same operations in the same order: bitwise equal).
+__device__ __forceinline__ void pf_diag_inv16_pipe(const double* M, const double* dinv, double* X, int b, int lane) {
+  const int j = lane & 15, o = 16 * b;
+  double x[16], di[16], cur[16], nxt[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) di[i] = dinv[o + i];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i + 1 < 16) {
+#pragma unroll
+      for (int m2 = 0; m2 < i + 1; ++m2) nxt[m2] = M[(o + i + 1) * kPfLd + o + m2];
+    }
+    double v = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+    for (int m2 = 0; m2 < i; ++m2) v -= cur[m2] * x[m2];
+    x[i] = v * di[i];
+#pragma unroll
+    for (int m2 = 0; m2 < 16; ++m2) cur[m2] = nxt[m2];
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) X[(o + i) * kPfLd + o + j] = x[i];
+  }
+}
+
 // Factor + inverse of the 64x64 tile M (row-major padded, lower valid): the
 // four block-column sweeps by wave 0 (pf_col16), the trailing lower blocks
 // by all waves (MFMA); while wave 0 sweeps block column kb, wave
@@ -861,7 +950,11 @@ __device__ __forceinline__ void pf_diag_inv16(const double* M, const double* din
 // are: every consumer reads X as lower triangular, pf_gemm_nt_lt).
 // stamps (nullable, probes only): clock64() by thread 0 after each block
 // column's sweep and trailing update (8), the last diagonal inverse, the end.
-template <bool RSQ>
+// OVL (tools build): the last diagonal inverse (wave 3) overlapped with the
+// off-diagonal blocks that do not need it — only X_3k = -X_33 (sum) waits for
+// it, every other block of X depends on its own wave's earlier blocks; PIPE:
+// the diagonal inverses by pf_diag_inv16_pipe.  Bitwise equal to the default.
+template <bool RSQ, bool OVL = false, bool PIPE = false>
 __device__ __forceinline__ int pf_chol_inv_fast(double* M, double* X, double* scr, double* dinv, int lane, int wv,
                                                 long long* stamps = nullptr) {
   int bad = 0;
@@ -876,7 +969,10 @@ __device__ __forceinline__ int pf_chol_inv_fast(double* M, double* X, double* sc
       // bad lives in wave 0; every thread returns it
       if (kb == 3 && lane == 0) reinterpret_cast<int*>(scr)[4 * 16 * 17 * 2] = bad;
     } else if (kb >= 1 && wv == 1 + (kb - 1) % 3) {
-      pf_diag_inv16(M, dinv, X, kb - 1, lane);
+      if (PIPE)
+        pf_diag_inv16_pipe(M, dinv, X, kb - 1, lane);
+      else
+        pf_diag_inv16(M, dinv, X, kb - 1, lane);
     }
     __syncthreads();
     stamp(2 * kb);
@@ -894,12 +990,54 @@ __device__ __forceinline__ int pf_chol_inv_fast(double* M, double* X, double* sc
     if (kb < 3) __syncthreads();
     stamp(2 * kb + 1);
   }
-  if (wv == 3) pf_diag_inv16(M, dinv, X, 3, lane);
+  double* T = scr + wv * 16 * 17;
+  if constexpr (OVL) {
+    // wave 3: X_33; wave k < 3: X_ik for i = k + 1 .. 2, then the sum of
+    // X_3k (kept in its scratch) — the blocks it reads are its own or final
+    if (wv == 3) {
+      if (PIPE)
+        pf_diag_inv16_pipe(M, dinv, X, 3, lane);
+      else
+        pf_diag_inv16(M, dinv, X, 3, lane);
+    } else {
+      const int k = wv;
+      for (int i = k + 1; i < 4; ++i) {
+        pf_dvec4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int m2 = k; m2 < i; ++m2)
+          blk16_mma<false>(acc, 1.0, M + 16 * i * kPfLd + 16 * m2, kPfLd, X + 16 * m2 * kPfLd + 16 * k, kPfLd, lane);
+        blk16_store(acc, T, 17, lane);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        if (i == 3) break;
+        pf_dvec4 out = {0.0, 0.0, 0.0, 0.0};
+        blk16_mma<false>(out, -1.0, X + 16 * i * kPfLd + 16 * i, kPfLd, T, 17, lane);
+        blk16_store(out, X + 16 * i * kPfLd + 16 * k, kPfLd, lane);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      }
+    }
+    __syncthreads();
+    stamp(8);
+    bad = reinterpret_cast<const int*>(scr)[4 * 16 * 17 * 2];
+    if (wv < 3) {
+      pf_dvec4 out = {0.0, 0.0, 0.0, 0.0};
+      blk16_mma<false>(out, -1.0, X + 48 * kPfLd + 48, kPfLd, T, 17, lane);
+      blk16_store(out, X + 48 * kPfLd + 16 * wv, kPfLd, lane);
+    }
+    __syncthreads();
+    stamp(9);
+    return bad;
+  }
+  if (wv == 3) {
+    if (PIPE)
+      pf_diag_inv16_pipe(M, dinv, X, 3, lane);
+    else
+      pf_diag_inv16(M, dinv, X, 3, lane);
+  }
   __syncthreads();
   stamp(8);
   bad = reinterpret_cast<const int*>(scr)[4 * 16 * 17 * 2];
   // off-diagonal blocks by block diagonals d: X_ik = -X_ii (sum_{m=k}^{i-1} L_im X_mk)
-  double* T = scr + wv * 16 * 17;
   for (int d = 1; d < 4; ++d) {
     const int k = wv;
     const int i = k + d;
@@ -933,11 +1071,14 @@ constexpr int kPfDbgSlots = 36;
 // (i, j) at src[j * ld + i], rows clamped to h and columns to w, zero outside.
 struct PfStage {
   double v[16];
+  // SC: sc1 loads (pf_wait mode 2)
+  template <bool SC = false>
   __device__ __forceinline__ void load_cm(const double* __restrict__ src, size_t ld, int h, int w) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = threadIdx.x + 256 * q, i = e & 63, j = e >> 6;
-      v[q] = src[(size_t)min(j, w - 1) * ld + min(i, h - 1)];
+      const double* a = src + (size_t)min(j, w - 1) * ld + min(i, h - 1);
+      v[q] = SC ? ld_sc1(a) : *a;
     }
   }
   __device__ __forceinline__ void store_cm(double* S, int h, int w) const {
@@ -948,9 +1089,10 @@ struct PfStage {
     }
   }
   // row-major source with leading dimension 64 (the published inverses)
+  template <bool SC = false>
   __device__ __forceinline__ void load_rm(const double* __restrict__ src) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = src[threadIdx.x + 256 * q];
+    for (int q = 0; q < 16; ++q) v[q] = SC ? ld_sc1(src + threadIdx.x + 256 * q) : src[threadIdx.x + 256 * q];
   }
   __device__ __forceinline__ void store_rm(double* S) const {
 #pragma unroll
@@ -983,8 +1125,9 @@ __device__ __forceinline__ void pf_drain() {
 }
 
 // FV: 64x64 tile factor pf_chol_inv_fast, 1 sqrt + divide pivots, 2 rsq
-// pivots; WT: pf_st
-template <int FV, bool WT>
+// pivots, 3 / 4 / 5 rsq with the overlapped last inverse and / or the
+// pipelined diagonal inverses (tools build); WT: pf_st
+template <int FV, bool WT, int WM>
 __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ A, int lda, int kb, int mrows,
                                                            int* __restrict__ info, double* __restrict__ linv,
                                                            unsigned* ctrl, unsigned base, unsigned epoch,
@@ -1053,11 +1196,11 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
           acc[t][q] = (i < hr && jj < wc) ? v : 0.0;
         }
       for (int k = 0; k < c; ++k) {
-        pf_wait(flag + c * kPfMaxTiles + k, epoch, err, limit);
+        pf_wait<WM>(flag + c * kPfMaxTiles + k, epoch, err, limit);
         {
           PfStage sc, sr;
-          sc.load_cm(A + (size_t)64 * k * lda + c0, lda, wc, 64);
-          sr.load_cm(A + (size_t)64 * k * lda + r0, lda, hr, 64);
+          sc.template load_cm<WM == 2>(A + (size_t)64 * k * lda + c0, lda, wc, 64);
+          sr.template load_cm<WM == 2>(A + (size_t)64 * k * lda + r0, lda, hr, 64);
           sc.store_cm(Li, wc, 64);
           sr.store_cm(T, hr, 64);
         }
@@ -1065,11 +1208,11 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
         pf_gemm_nt(acc, -1.0, ltile(T), ltile(Li), wv, lane);
         __syncthreads();
       }
-      pf_wait(flag + c * kPfMaxTiles + c, epoch, err, limit);
+      pf_wait<WM>(flag + c * kPfMaxTiles + c, epoch, err, limit);
       stamp(1 + 2 * c);
       {
         PfStage sl;
-        sl.load_rm(linv + (size_t)c * 64 * 64);
+        sl.template load_rm<WM == 2>(linv + (size_t)c * 64 * 64);
         sl.store_rm(Li);
       }
       pf_acc_to_lds(acc, T, wv, lane);
@@ -1105,12 +1248,12 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
           acc[t][q] = (i < hr && j < wc) ? v : 0.0;
         }
       for (int k = 0; k < c; ++k) {
-        pf_wait(flag + c * kPfMaxTiles + k, epoch, err, limit);
+        pf_wait<WM>(flag + c * kPfMaxTiles + k, epoch, err, limit);
         // L_rk and L_ck staged together (all loads in flight), LDS GEMM
         {
           PfStage sr, sc;
-          sr.load_cm(A + (size_t)64 * k * lda + r0, lda, hr, 64);
-          sc.load_cm(A + (size_t)64 * k * lda + c0, lda, wc, 64);
+          sr.template load_cm<WM == 2>(A + (size_t)64 * k * lda + r0, lda, hr, 64);
+          sc.template load_cm<WM == 2>(A + (size_t)64 * k * lda + c0, lda, wc, 64);
           sr.store_cm(T, hr, 64);
           sc.store_cm(Li, wc, 64);
         }
@@ -1118,13 +1261,13 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
         pf_gemm_nt(acc, -1.0, ltile(T), ltile(Li), wv, lane);
         __syncthreads();
       }
-      pf_wait(flag + c * kPfMaxTiles + c, epoch, err, limit);
+      pf_wait<WM>(flag + c * kPfMaxTiles + c, epoch, err, limit);
       stamp(1 + 2 * c);
       // L_rc = T Linv_cc' (Linv_cc row-major in linv, staged in LDS)
       pf_acc_to_lds(acc, T, wv, lane);
       {
         PfStage sl;
-        sl.load_rm(linv + (size_t)c * 64 * 64);
+        sl.template load_rm<WM == 2>(linv + (size_t)c * 64 * 64);
         sl.store_rm(Li);
       }
       __syncthreads();
@@ -1158,8 +1301,11 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
     pf_acc_to_lds(dacc, T, wv, lane);
     __syncthreads();
     // factor + inverse by 16x16 blocks (Lc: pivot columns + per-wave scratch)
-    const int bad = FV == 2 ? pf_chol_inv_fast<true>(T, Li, Lc, dinv, lane, wv)
-                            : pf_chol_inv_fast<false>(T, Li, Lc, dinv, lane, wv);
+    const int bad = FV == 3   ? pf_chol_inv_fast<true, true, true>(T, Li, Lc, dinv, lane, wv)
+                    : FV == 4 ? pf_chol_inv_fast<true, true, false>(T, Li, Lc, dinv, lane, wv)
+                    : FV == 5 ? pf_chol_inv_fast<true, false, true>(T, Li, Lc, dinv, lane, wv)
+                    : FV == 2 ? pf_chol_inv_fast<true>(T, Li, Lc, dinv, lane, wv)
+                              : pf_chol_inv_fast<false>(T, Li, Lc, dinv, lane, wv);
     stamp(1 + 2 * c);
     // publish the inverse's lower blocks (row-major, ld 64: the only part
     // its consumers read); the factor tile itself is read by no workgroup of
@@ -1353,10 +1499,21 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   }
   const unsigned epoch = ++ws->pf_epoch;
 #ifdef MI_BA_AB_VARIANTS
-  auto kern = ws->tile_factor == 2 ? (ws->write_through ? panel_factor_kernel<2, true> : panel_factor_kernel<2, false>)
-                                   : (ws->write_through ? panel_factor_kernel<1, true> : panel_factor_kernel<1, false>);
+  auto pick = [&](auto wm) {
+    constexpr int W = decltype(wm)::value;
+    return ws->tile_factor == 3   ? panel_factor_kernel<3, true, W>
+           : ws->tile_factor == 4 ? panel_factor_kernel<4, true, W>
+           : ws->tile_factor == 5 ? panel_factor_kernel<5, true, W>
+           : ws->tile_factor == 2 ? (ws->write_through ? panel_factor_kernel<2, true, W> : panel_factor_kernel<2, false, W>)
+                                  : (ws->write_through ? panel_factor_kernel<1, true, W> : panel_factor_kernel<1, false, W>);
+  };
+  auto kern = ws->panel_wait == 2   ? pick(std::integral_constant<int, 2>{})
+              : ws->panel_wait == 1 ? pick(std::integral_constant<int, 1>{})
+                                    : pick(std::integral_constant<int, 0>{});
 #else
-  auto kern = panel_factor_kernel<2, true>;  // the tools build keeps tile_factor 1 / plain stores for A/B
+  // the tools build keeps the other tile factors / plain stores / wait modes for A/B
+  constexpr CholConfig kDef{};
+  auto kern = panel_factor_kernel<kDef.tile_factor, true, kDef.panel_wait>;
 #endif
   hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, s, A + k + (size_t)k * lda, lda, kb, mrows, info, ws->pf_linv,
                      ws->pf_ctrl, ws->pf_base, epoch, ws->err, ws->spin_limit, groups, nullptr);
@@ -1931,6 +2088,8 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   if (ws) {
     ws->tile_factor = c.tile_factor;
     ws->write_through = c.write_through;
+    ws->panel_wait = c.panel_wait;
+    ws->solve_sc1 = c.solve_sc1;
     ws->spin_limit = c.spin_log2 <= 0 ? 0u : ws->wait_ticks(c.wait_ms);
     ws->rows_per_group = c.panel_rows_per_group;
     ws->bwd_pairs = c.bwd_pairs;
@@ -1984,8 +2143,8 @@ rocblas_status chol_solve_backward(rocblas_handle h, int n, const double* A, int
                        ws->spin_limit);
   else
 #endif
-    hipLaunchKernelGGL(trsv_sweep_kernel<false>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e,
-                       ws->err, ws->spin_limit);
+    hipLaunchKernelGGL((ws->solve_sc1 ? trsv_sweep_kernel<false, true> : trsv_sweep_kernel<false, false>), dim3(nblk),
+                       dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e, ws->err, ws->spin_limit);
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
 
@@ -2012,10 +2171,10 @@ rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, dou
     const unsigned e = ++ws->epoch;
     const unsigned e2 = ++ws->epoch;
     const int nblk = (n + kTB - 1) / kTB;
-    hipLaunchKernelGGL(trsv_sweep_kernel<true>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e,
-                       ws->err, ws->spin_limit);
-    hipLaunchKernelGGL(trsv_sweep_kernel<false>, dim3(nblk), dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e2,
-                       ws->err, ws->spin_limit);
+    hipLaunchKernelGGL((ws->solve_sc1 ? trsv_sweep_kernel<true, true> : trsv_sweep_kernel<true, false>), dim3(nblk),
+                       dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e, ws->err, ws->spin_limit);
+    hipLaunchKernelGGL((ws->solve_sc1 ? trsv_sweep_kernel<false, true> : trsv_sweep_kernel<false, false>), dim3(nblk),
+                       dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e2, ws->err, ws->spin_limit);
     return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
   }
   // inverses of the diagonal blocks (full blocks in one batched call, the

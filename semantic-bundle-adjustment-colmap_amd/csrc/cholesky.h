@@ -93,13 +93,26 @@ struct CholConfig {
   int own_diag = 6;
   // own_diag 6: the diagonal tiles' 64x64 factor + inverse (block columns by
   // register sweeps, pf_chol_inv_fast): 2 pivots by rsq + two Goldschmidt
-  // steps (~1 ulp), 1 correctly rounded sqrt + divide.  2 (default): Cholesky
-  // 17.3 vs 17.7 ms at nf = 12 000; the previous per-pivot LDS-exchange
-  // factor (36 us per tile, 22 ms) is gone (profiles/r3_tile_probe.txt).
-  int tile_factor = 2;
+  // steps (~1 ulp), 1 correctly rounded sqrt + divide.  2: Cholesky 17.3 vs
+  // 17.7 ms at nf = 12 000; the previous per-pivot LDS-exchange factor (36 us
+  // per tile, 22 ms) is gone (profiles/r3_tile_probe.txt).  3 (default): 2
+  // with the diagonal 16x16 inverses' operands loaded ahead of their
+  // substitution and the last one overlapped with the inverse's other blocks
+  // (bitwise equal to 2; 14.3 vs 15.5 us per tile, profiles/r5x_tile_probe.txt);
+  // 4 / 5 the overlap / the loads alone (tools build).
+  int tile_factor = 3;
   // own_diag 6: published tiles stored write-through (sc1) and drained before
   // the flag, instead of plain stores + __threadfence()
   bool write_through = true;
+  // own_diag 6, panel hand-off waits: 0 every wave polls and acquires, 1 one
+  // wave polls and acquires for the workgroup, 2 (default) one wave polls and
+  // the handed-off tiles are read by sc1 loads (no acquire).  Panel alone
+  // 320 -> 262 (1) -> 230-245 us (2) at nf = 12 000 (profiles/r5y_*).
+  int panel_wait = 2;
+  // chol_solve variant 2 / the backward sweep: block results handed over as
+  // sc1 stores + relaxed flag, read by sc1 loads (no fences); default
+  // (0.82 -> 0.75 ms per solve at C4)
+  bool solve_sc1 = true;
   // chol_solve variant: 2 sync-free sweeps (one launch per direction), 1 one
   // launch per 64-wide block column with diagonal-block inverses, 0 recursive
   // rocBLAS dtrsv / dgemv
@@ -147,8 +160,10 @@ struct CholWorkspace {
   double* pf_linv = nullptr;    // [8][64*64] inverses of the panel's diagonal tiles
   unsigned pf_base = 0;         // tickets handed out so far
   unsigned pf_epoch = 0;        // flag value of the last panel launch
-  int tile_factor = 2;          // CholConfig::tile_factor
+  int tile_factor = 3;          // CholConfig::tile_factor
   bool write_through = false;   // CholConfig::write_through
+  int panel_wait = 2;           // CholConfig::panel_wait
+  bool solve_sc1 = true;        // CholConfig::solve_sc1
   int linv_rows = 0;
   double* tinv = nullptr;       // own_diag 7: [512*512] inverse of the panel's diagonal block
   double* tbuf = nullptr;       // own_diag 7: [max_n * 512] copy of the panel below it

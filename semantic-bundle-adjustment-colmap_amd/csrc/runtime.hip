@@ -2451,8 +2451,18 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.batch_tile = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_tile_factor") == 0 && (value == 1 || value == 2) && ab_value(value, 2)) {
+  if (std::strcmp(key, "cholesky_tile_factor") == 0 && value >= 1 && value <= 5 && ab_value(value, CholConfig{}.tile_factor)) {
     ctx->chol.tile_factor = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_panel_wait") == 0 && value >= 0 && value <= 2 &&
+      ab_value(value, CholConfig{}.panel_wait)) {
+    ctx->chol.panel_wait = value;
+    return MI_BA_OK;
+  }
+  if (std::strcmp(key, "cholesky_solve_sc1") == 0 && (value == 0 || value == 1) &&
+      ab_value(value, CholConfig{}.solve_sc1 ? 1 : 0)) {
+    ctx->chol.solve_sc1 = value != 0;
     return MI_BA_OK;
   }
   if (std::strcmp(key, "cholesky_write_through") == 0 && (value == 0 || value == 1) && ab_value(value, 1)) {

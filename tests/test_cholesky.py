@@ -243,8 +243,8 @@ def test_lm_tile_factor_and_publish(gpu):
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
     res = []
-    for tf in (2, 1):
-        for wt in (1, 0):
+    for tf in (2, 1, 3, 4, 5):
+        for wt in ((1, 0) if tf <= 2 else (1,)):
             with mi_ba.Context(opts, sc.copy()) as ctx:
                 ctx.set_tuning("cholesky_tile_factor", tf)
                 ctx.set_tuning("cholesky_write_through", wt)
@@ -254,6 +254,31 @@ def test_lm_tile_factor_and_publish(gpu):
         assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
         assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
 
+
+def test_lm_handoff_variants_bitwise(gpu):
+    """The panel factor's hand-off waits (every wave acquires / one wave
+    acquires for the workgroup / one wave polls and the tiles are read by sc1
+    loads) and the sweeps' sc1 hand-offs (no fences) change only
+    synchronisation: the same LM bit for bit (deterministic sums; nf = 1593,
+    4 panels, ragged last sweep block).  Non-default combinations: tools-only
+    A/B build."""
+    if not mi_ba.ab_build():
+        pytest.skip("hand-off variants: tools build only (MI_BA_LIB=ab)")
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for wm, sc1 in ((0, 0), (1, 0), (2, 0), (0, 1), (2, 1)):
+        b = sc.copy()
+        with mi_ba.Context(opts, b) as ctx:
+            ctx.set_tuning("cholesky_panel_wait", wm)
+            ctx.set_tuning("cholesky_solve_sc1", sc1)
+            s = ctx.solve()
+            ctx.writeback()
+        res.append((s.num_successful_steps, s.num_unsuccessful_steps, s.final_cost,
+                    b.qvec.tobytes(), b.tvec.tobytes(), b.xyz.tobytes(), b.camera_params.tobytes()))
+    for r in res[1:]:
+        assert r == res[0]
 
 
 def test_lm_gemm_solution(gpu):

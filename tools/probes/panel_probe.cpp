@@ -2,7 +2,7 @@
 // own_diag 6) on the first 512-wide panel of an nf = 12 000 SPD matrix:
 // wall_clock64() stamps per row tile (kernel's dbg buffer).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/panel_probe.cpp -lrocsolver -lrocblas -o tools/probes/panel_probe.bin
-//   tools/probes/panel_probe.bin [n] [tile_factor] [write_through] [concurrent dgemms]
+//   tools/probes/panel_probe.bin [n] [tile_factor] [write_through] [concurrent dgemms] [panel wait mode]
 #include "../../semantic-bundle-adjustment-colmap_amd/csrc/cholesky.cpp"
 
 #include <cstdio>
@@ -23,10 +23,11 @@ int main(int argc, char** argv) {
   unsigned long long* dbg;
   hipMalloc(&A, 8ull * n * n);
   hipMalloc(&info, 64);
-  const int fv = argc > 2 ? atoi(argv[2]) : 2;  // tile factor: 2 rsq, 1 sqrt pivots
+  const int fv = argc > 2 ? atoi(argv[2]) : 2;  // tile factor: 2 rsq, 1 sqrt pivots, 3-5 tools-build variants
   const int wt = argc > 3 ? atoi(argv[3]) : 1;  // write-through publish
   const int busy = argc > 4 ? atoi(argv[4]) : 0;  // 1: trailing-update dgemms on a second stream meanwhile
-  printf("n %d, tile_factor %d, write_through %d, concurrent dgemms %d\n", n, fv, wt, busy);
+  const int ow = argc > 5 ? atoi(argv[5]) : 0;  // panel wait mode (CholConfig::panel_wait)
+  printf("n %d, tile_factor %d, write_through %d, concurrent dgemms %d, panel wait %d\n", n, fv, wt, busy, ow);
   const int nr = 8 + (n - kb + 63) / 64;
   hipMalloc(&dbg, 8ull * nr * kPfDbgSlots);
   CholWorkspace ws;
@@ -56,8 +57,16 @@ int main(int argc, char** argv) {
                         rocblas_gemm_algo_solution_index, CholConfig{}.gemm_solution, 0);
     }
     hipEventRecord(e0, ws.side);
-    auto kern = fv == 2 ? (wt ? panel_factor_kernel<2, true> : panel_factor_kernel<2, false>)
-                        : (wt ? panel_factor_kernel<1, true> : panel_factor_kernel<1, false>);
+    auto pick = [&](auto wm) {
+      constexpr int W = decltype(wm)::value;
+      return fv == 3   ? panel_factor_kernel<3, true, W>
+             : fv == 4 ? panel_factor_kernel<4, true, W>
+             : fv == 5 ? panel_factor_kernel<5, true, W>
+             : fv == 2 ? (wt ? panel_factor_kernel<2, true, W> : panel_factor_kernel<2, false, W>)
+                       : (wt ? panel_factor_kernel<1, true, W> : panel_factor_kernel<1, false, W>);
+    };
+    auto kern = ow == 2 ? pick(std::integral_constant<int, 2>{})
+                : ow == 1 ? pick(std::integral_constant<int, 1>{}) : pick(std::integral_constant<int, 0>{});
     hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, ws.side, A, n, kb, n, info, ws.pf_linv, ws.pf_ctrl, ws.pf_base, epoch,
                        ws.err, ws.spin_limit, 0, dbg);
     hipEventRecord(e1, ws.side);

@@ -48,8 +48,12 @@ __global__ __launch_bounds__(256) void tile_probe_kernel(double* __restrict__ A,
     w[1] = wall_clock64(); c[1] = clock64();
     // 1: factor + inverse in LDS
     long long* sub = (long long*)(st + (size_t)kReps * kPhases * 2) + rep * 10;
-    const int bad = V == 1 ? pf_chol_inv_fast<false>(T, Li, Lc, dinv, lane, wv, blockIdx.x == 0 ? sub : nullptr)
-                           : pf_chol_inv_fast<true>(T, Li, Lc, dinv, lane, wv, blockIdx.x == 0 ? sub : nullptr);
+    long long* sp = blockIdx.x == 0 ? sub : nullptr;
+    const int bad = V == 1   ? pf_chol_inv_fast<false>(T, Li, Lc, dinv, lane, wv, sp)
+                    : V == 3 ? pf_chol_inv_fast<true, true, true>(T, Li, Lc, dinv, lane, wv, sp)
+                    : V == 4 ? pf_chol_inv_fast<true, true, false>(T, Li, Lc, dinv, lane, wv, sp)
+                    : V == 5 ? pf_chol_inv_fast<true, false, true>(T, Li, Lc, dinv, lane, wv, sp)
+                             : pf_chol_inv_fast<true>(T, Li, Lc, dinv, lane, wv, sp);
     __syncthreads();
     if (rep == kReps - 1 && blockIdx.x == 0)
       for (int e = threadIdx.x; e < 4096; e += 256) {
@@ -154,24 +158,32 @@ int main() {
   hipMalloc(&out, 8ull * 2 * 4096 * 64);
   hipMalloc(&st, 8ull * kReps * kPhases * 2 + 8ull * kReps * 10);
   double* res;
-  hipMalloc(&res, 8ull * 4 * 2 * 4096);
+  hipMalloc(&res, 8ull * 6 * 2 * 4096);
   hipMemcpy(A, h.data(), 8ull * n * n, hipMemcpyHostToDevice);
   const char* names[kPhases] = {"load tile -> LDS", "chol+inv", "gemm LDS operands",
                                 "gemm global operands", "publish 32KB plain + threadfence",
                                 "publish 32KB sc1 + vmcnt", "stage 32KB global -> LDS",
                                 "stage 32KB 16B loads in flight", "gemm global operands, cold tiles",
                                 "stage 2 cold tiles (16B) + LDS gemm"};
-  for (int cfg = 2; cfg < 6; ++cfg) {
+  const char* vname[6] = {"", "pf_chol_inv_fast<sqrt>", "pf_chol_inv_fast<rsq>", "pf_chol_inv_fast<rsq, ovl, pipe>",
+                          "pf_chol_inv_fast<rsq, ovl>", "pf_chol_inv_fast<rsq, pipe>"};
+  for (int cfg = 2; cfg < 12; ++cfg) {
     const int grid = cfg & 1 ? 8 : 1, V = cfg >> 1;
+    double* rv = res + (size_t)V * 8192;
     if (V == 1)
-      hipLaunchKernelGGL(tile_probe_kernel<1>, dim3(grid), dim3(256), 0, 0, A, n, out, st, res + 8192);
+      hipLaunchKernelGGL(tile_probe_kernel<1>, dim3(grid), dim3(256), 0, 0, A, n, out, st, rv);
+    else if (V == 2)
+      hipLaunchKernelGGL(tile_probe_kernel<2>, dim3(grid), dim3(256), 0, 0, A, n, out, st, rv);
+    else if (V == 3)
+      hipLaunchKernelGGL(tile_probe_kernel<3>, dim3(grid), dim3(256), 0, 0, A, n, out, st, rv);
+    else if (V == 4)
+      hipLaunchKernelGGL(tile_probe_kernel<4>, dim3(grid), dim3(256), 0, 0, A, n, out, st, rv);
     else
-      hipLaunchKernelGGL(tile_probe_kernel<2>, dim3(grid), dim3(256), 0, 0, A, n, out, st, res + 16384);
+      hipLaunchKernelGGL(tile_probe_kernel<5>, dim3(grid), dim3(256), 0, 0, A, n, out, st, rv);
     hipDeviceSynchronize();
     std::vector<unsigned long long> s((size_t)kReps * kPhases * 2);
     hipMemcpy(s.data(), st, 8 * s.size(), hipMemcpyDeviceToHost);
-    printf("%s, grid %d (workgroup 0), per phase: min / median over %d reps  [us, cycles]\n",
-           V == 1 ? "pf_chol_inv_fast<sqrt>" : "pf_chol_inv_fast<rsq>", grid, kReps);
+    printf("%s, grid %d (workgroup 0), per phase: min / median over %d reps  [us, cycles]\n", vname[V], grid, kReps);
     for (int k = 0; k < kPhases; ++k) {
       std::vector<double> us, cy;
       for (int r = 1; r < kReps; ++r) {
@@ -193,7 +205,7 @@ int main() {
     }
   }
   // L and X of both variants vs a host Cholesky of the same tile
-  std::vector<double> r(8 * 4096);
+  std::vector<double> r(12 * 4096);
   hipMemcpy(r.data(), res, 8ull * r.size(), hipMemcpyDeviceToHost);
   std::vector<double> L(4096, 0.0);
   for (int j = 0; j < 64; ++j) {
@@ -206,7 +218,16 @@ int main() {
       L[i * 64 + j] = v / L[j * 64 + j];
     }
   }
-  for (int V = 1; V < 3; ++V) {
+  for (int V = 3; V < 6; ++V) {  // the tools-build variants against rsq (same operations: bitwise)
+    bool same = true;
+    for (int i = 0; i < 64; ++i)
+      for (int j = 0; j < 64; ++j) {
+        if (j <= i && r[V * 8192 + i * 64 + j] != r[2 * 8192 + i * 64 + j]) same = false;
+        if ((j >> 4) <= (i >> 4) && r[V * 8192 + 4096 + i * 64 + j] != r[2 * 8192 + 4096 + i * 64 + j]) same = false;
+      }
+    printf("variant %d: L and X bitwise equal to variant 2: %s\n", V, same ? "yes" : "NO");
+  }
+  for (int V = 1; V < 6; ++V) {
     double el = 0.0, ex = 0.0;
     for (int i = 0; i < 64; ++i)
       for (int j = 0; j < 64; ++j) {
