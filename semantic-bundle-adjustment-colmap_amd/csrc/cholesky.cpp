@@ -745,7 +745,9 @@ __device__ __forceinline__ int pf_rows(int r, int kb, int nc, int mrows) {
 // 2 one wave polls, no acquire: every load of the handed-off tiles is an sc1
 // load (PfStage<true>) of bytes stored sc1 and drained before the flag, one
 // workgroup per CU (the kernel's registers allow one) — the guide's table row
-// 1.  Called in workgroup-uniform control flow.
+// 1; 3 as 2 with the next stage's tiles loaded during the current stage's
+// GEMM when its flag is already set (pf_stages).  Called in
+// workgroup-uniform control flow.
 template <int WM>
 __device__ __forceinline__ void pf_wait(const unsigned* f, unsigned epoch, unsigned* err, unsigned limit) {
   if constexpr (WM == 1) {
@@ -754,7 +756,7 @@ __device__ __forceinline__ void pf_wait(const unsigned* f, unsigned epoch, unsig
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-  } else if constexpr (WM == 2) {
+  } else if constexpr (WM >= 2) {
     if (threadIdx.x < 64) flag_poll(f, epoch, err, limit);
     __syncthreads();
   } else {
@@ -1124,6 +1126,60 @@ __device__ __forceinline__ void pf_drain() {
     __threadfence();
 }
 
+// The left-looking updates of one tile: acc -= sum_{k < c} L_rk L_ck' (row
+// tile r0 / hr, column tile c0 / wc; flags fc[k] = tile (c, k) final), L_rk
+// staged in T and L_ck in Li.  WM 3: the tiles of stage k + 1 are loaded
+// while stage k's GEMM runs if flag k + 1 is already set (one wave polls,
+// the workgroup's barrier follows: sc1 loads, pf_wait mode 2), else after it;
+// the same GEMMs in the same order (bitwise equal).
+template <int WM>
+__device__ __forceinline__ void pf_stages(pf_dvec4 (&acc)[4], const double* A, int lda, int r0, int hr, int c0, int wc,
+                                          int c, const unsigned* fc, unsigned epoch, unsigned* err, unsigned limit,
+                                          double* T, double* Li, int* s_ready, int wv, int lane) {
+  auto ltile = [&](const double* S) { return [=](int i, int j) { return S[i * kPfLd + j]; }; };
+  if constexpr (WM == 3) {
+    PfStage sr, sc;
+    if (c > 0) {
+      pf_wait<WM>(fc, epoch, err, limit);
+      sr.template load_cm<true>(A + r0, lda, hr, 64);
+      sc.template load_cm<true>(A + c0, lda, wc, 64);
+    }
+    for (int k = 0; k < c; ++k) {
+      sr.store_cm(T, hr, 64);
+      sc.store_cm(Li, wc, 64);
+      if (threadIdx.x < 64)
+        *s_ready = k + 1 < c && __hip_atomic_load(fc + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      __syncthreads();
+      const bool ready = *s_ready != 0;
+      if (ready) {
+        sr.template load_cm<true>(A + (size_t)64 * (k + 1) * lda + r0, lda, hr, 64);
+        sc.template load_cm<true>(A + (size_t)64 * (k + 1) * lda + c0, lda, wc, 64);
+      }
+      pf_gemm_nt(acc, -1.0, ltile(T), ltile(Li), wv, lane);
+      __syncthreads();
+      if (k + 1 < c && !ready) {
+        pf_wait<WM>(fc + k + 1, epoch, err, limit);
+        sr.template load_cm<true>(A + (size_t)64 * (k + 1) * lda + r0, lda, hr, 64);
+        sc.template load_cm<true>(A + (size_t)64 * (k + 1) * lda + c0, lda, wc, 64);
+      }
+    }
+  } else {
+    for (int k = 0; k < c; ++k) {
+      pf_wait<WM>(fc + k, epoch, err, limit);
+      {
+        PfStage sr, sc;
+        sr.template load_cm<WM == 2>(A + (size_t)64 * k * lda + r0, lda, hr, 64);
+        sc.template load_cm<WM == 2>(A + (size_t)64 * k * lda + c0, lda, wc, 64);
+        sr.store_cm(T, hr, 64);
+        sc.store_cm(Li, wc, 64);
+      }
+      __syncthreads();
+      pf_gemm_nt(acc, -1.0, ltile(T), ltile(Li), wv, lane);
+      __syncthreads();
+    }
+  }
+}
+
 // FV: 64x64 tile factor pf_chol_inv_fast, 1 sqrt + divide pivots, 2 rsq
 // pivots, 3 / 4 / 5 rsq with the overlapped last inverse and / or the
 // pipelined diagonal inverses (tools build); WT: pf_st
@@ -1137,7 +1193,7 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
   __shared__ double Li[64 * kPfLd];  // a diagonal tile's inverse (own, or workgroup c's)
   __shared__ double Lc[1152];        // pf_chol_inv_fast scratch: per-wave 16x16 tiles + the pivot status
   __shared__ double dinv[64];
-  __shared__ int s_r;
+  __shared__ int s_r, s_ready;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_r = (int)(atomicAdd(ctrl, 1u) - base);
   __syncthreads();
@@ -1195,24 +1251,13 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
           const double v = A[(size_t)(c0 + min(jj, wc - 1)) * lda + r0 + min(i, hr - 1)];
           acc[t][q] = (i < hr && jj < wc) ? v : 0.0;
         }
-      for (int k = 0; k < c; ++k) {
-        pf_wait<WM>(flag + c * kPfMaxTiles + k, epoch, err, limit);
-        {
-          PfStage sc, sr;
-          sc.template load_cm<WM == 2>(A + (size_t)64 * k * lda + c0, lda, wc, 64);
-          sr.template load_cm<WM == 2>(A + (size_t)64 * k * lda + r0, lda, hr, 64);
-          sc.store_cm(Li, wc, 64);
-          sr.store_cm(T, hr, 64);
-        }
-        __syncthreads();
-        pf_gemm_nt(acc, -1.0, ltile(T), ltile(Li), wv, lane);
-        __syncthreads();
-      }
+      pf_stages<WM>(acc, A, lda, r0, hr, c0, wc, c, flag + c * kPfMaxTiles, epoch, err, limit, T, Li, &s_ready, wv,
+                    lane);
       pf_wait<WM>(flag + c * kPfMaxTiles + c, epoch, err, limit);
       stamp(1 + 2 * c);
       {
         PfStage sl;
-        sl.template load_rm<WM == 2>(linv + (size_t)c * 64 * 64);
+        sl.template load_rm<WM >= 2>(linv + (size_t)c * 64 * 64);
         sl.store_rm(Li);
       }
       pf_acc_to_lds(acc, T, wv, lane);
@@ -1247,27 +1292,15 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
           const double v = A[(size_t)(c0 + min(j, wc - 1)) * lda + r0 + min(i, hr - 1)];
           acc[t][q] = (i < hr && j < wc) ? v : 0.0;
         }
-      for (int k = 0; k < c; ++k) {
-        pf_wait<WM>(flag + c * kPfMaxTiles + k, epoch, err, limit);
-        // L_rk and L_ck staged together (all loads in flight), LDS GEMM
-        {
-          PfStage sr, sc;
-          sr.template load_cm<WM == 2>(A + (size_t)64 * k * lda + r0, lda, hr, 64);
-          sc.template load_cm<WM == 2>(A + (size_t)64 * k * lda + c0, lda, wc, 64);
-          sr.store_cm(T, hr, 64);
-          sc.store_cm(Li, wc, 64);
-        }
-        __syncthreads();
-        pf_gemm_nt(acc, -1.0, ltile(T), ltile(Li), wv, lane);
-        __syncthreads();
-      }
+      pf_stages<WM>(acc, A, lda, r0, hr, c0, wc, c, flag + c * kPfMaxTiles, epoch, err, limit, T, Li, &s_ready, wv,
+                    lane);
       pf_wait<WM>(flag + c * kPfMaxTiles + c, epoch, err, limit);
       stamp(1 + 2 * c);
       // L_rc = T Linv_cc' (Linv_cc row-major in linv, staged in LDS)
       pf_acc_to_lds(acc, T, wv, lane);
       {
         PfStage sl;
-        sl.template load_rm<WM == 2>(linv + (size_t)c * 64 * 64);
+        sl.template load_rm<WM >= 2>(linv + (size_t)c * 64 * 64);
         sl.store_rm(Li);
       }
       __syncthreads();
@@ -1507,7 +1540,8 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
            : ws->tile_factor == 2 ? (ws->write_through ? panel_factor_kernel<2, true, W> : panel_factor_kernel<2, false, W>)
                                   : (ws->write_through ? panel_factor_kernel<1, true, W> : panel_factor_kernel<1, false, W>);
   };
-  auto kern = ws->panel_wait == 2   ? pick(std::integral_constant<int, 2>{})
+  auto kern = ws->panel_wait == 3   ? pick(std::integral_constant<int, 3>{})
+              : ws->panel_wait == 2 ? pick(std::integral_constant<int, 2>{})
               : ws->panel_wait == 1 ? pick(std::integral_constant<int, 1>{})
                                     : pick(std::integral_constant<int, 0>{});
 #else

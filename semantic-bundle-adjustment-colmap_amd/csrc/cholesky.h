@@ -106,7 +106,8 @@ struct CholConfig {
   bool write_through = true;
   // own_diag 6, panel hand-off waits: 0 every wave polls and acquires, 1 one
   // wave polls and acquires for the workgroup, 2 (default) one wave polls and
-  // the handed-off tiles are read by sc1 loads (no acquire).  Panel alone
+  // the handed-off tiles are read by sc1 loads (no acquire), 3 as 2 with the
+  // next stage's tiles loaded during the current GEMM (tools build).  Panel alone
   // 320 -> 262 (1) -> 230-245 us (2) at nf = 12 000 (profiles/r5y_*).
   int panel_wait = 2;
   // chol_solve variant 2 / the backward sweep: block results handed over as

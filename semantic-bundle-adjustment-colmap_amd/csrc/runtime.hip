@@ -2455,7 +2455,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.tile_factor = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_panel_wait") == 0 && value >= 0 && value <= 2 &&
+  if (std::strcmp(key, "cholesky_panel_wait") == 0 && value >= 0 && value <= 3 &&
       ab_value(value, CholConfig{}.panel_wait)) {
     ctx->chol.panel_wait = value;
     return MI_BA_OK;

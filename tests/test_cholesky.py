@@ -258,7 +258,8 @@ def test_lm_tile_factor_and_publish(gpu):
 def test_lm_handoff_variants_bitwise(gpu):
     """The panel factor's hand-off waits (every wave acquires / one wave
     acquires for the workgroup / one wave polls and the tiles are read by sc1
-    loads) and the sweeps' sc1 hand-offs (no fences) change only
+    loads, with or without the next stage's tiles loaded during the current
+    GEMM) and the sweeps' sc1 hand-offs (no fences) change only
     synchronisation: the same LM bit for bit (deterministic sums; nf = 1593,
     4 panels, ragged last sweep block).  Non-default combinations: tools-only
     A/B build."""
@@ -268,7 +269,7 @@ def test_lm_handoff_variants_bitwise(gpu):
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
     res = []
-    for wm, sc1 in ((0, 0), (1, 0), (2, 0), (0, 1), (2, 1)):
+    for wm, sc1 in ((2, 1), (0, 0), (1, 0), (2, 0), (3, 1)):
         b = sc.copy()
         with mi_ba.Context(opts, b) as ctx:
             ctx.set_tuning("cholesky_panel_wait", wm)

@@ -65,7 +65,8 @@ int main(int argc, char** argv) {
              : fv == 2 ? (wt ? panel_factor_kernel<2, true, W> : panel_factor_kernel<2, false, W>)
                        : (wt ? panel_factor_kernel<1, true, W> : panel_factor_kernel<1, false, W>);
     };
-    auto kern = ow == 2 ? pick(std::integral_constant<int, 2>{})
+    auto kern = ow == 3 ? pick(std::integral_constant<int, 3>{})
+                : ow == 2 ? pick(std::integral_constant<int, 2>{})
                 : ow == 1 ? pick(std::integral_constant<int, 1>{}) : pick(std::integral_constant<int, 0>{});
     hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, ws.side, A, n, kb, n, info, ws.pf_linv, ws.pf_ctrl, ws.pf_base, epoch,
                        ws.err, ws.spin_limit, 0, dbg);
