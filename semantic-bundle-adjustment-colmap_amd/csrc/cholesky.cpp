@@ -543,6 +543,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
     }
     if (SC1) {
       flag_poll(flag + jb, epoch, err, limit);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
       xs[wv][lane] = lane < wj ? ld_sc1(x + c0 + lane) : 0.0;
     } else {
       flag_wait(flag + jb, epoch, err, limit);
@@ -757,7 +758,10 @@ __device__ __forceinline__ void pf_wait(const unsigned* f, unsigned epoch, unsig
     }
     __syncthreads();
   } else if constexpr (WM >= 2) {
-    if (threadIdx.x < 64) flag_poll(f, epoch, err, limit);
+    if (threadIdx.x < 64) {
+      flag_poll(f, epoch, err, limit);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
+    }
     __syncthreads();
   } else {
     flag_wait(f, epoch, err, limit);
@@ -1135,7 +1139,13 @@ __device__ __forceinline__ void pf_drain() {
 template <int WM>
 __device__ __forceinline__ void pf_stages(pf_dvec4 (&acc)[4], const double* A, int lda, int r0, int hr, int c0, int wc,
                                           int c, const unsigned* fc, unsigned epoch, unsigned* err, unsigned limit,
-                                          double* T, double* Li, int* s_ready, int wv, int lane) {
+                                          double* T, double* Li, int* s_ready, int wv, int lane,
+                                          unsigned long long* st = nullptr) {
+  // st (probes only): wall_clock64() after each phase of each stage, 3 per
+  // stage (tiles loaded and staged, GEMM done) — slots 3k, 3k + 1, 3k + 2
+  auto stamp = [&](int slot) {
+    if (st && threadIdx.x == 0 && slot < 16) st[slot] = wall_clock64();
+  };
   auto ltile = [&](const double* S) { return [=](int i, int j) { return S[i * kPfLd + j]; }; };
   if constexpr (WM == 3) {
     PfStage sr, sc;
@@ -1166,6 +1176,7 @@ __device__ __forceinline__ void pf_stages(pf_dvec4 (&acc)[4], const double* A, i
   } else {
     for (int k = 0; k < c; ++k) {
       pf_wait<WM>(fc + k, epoch, err, limit);
+      stamp(3 * k);
       {
         PfStage sr, sc;
         sr.template load_cm<WM == 2>(A + (size_t)64 * k * lda + r0, lda, hr, 64);
@@ -1174,8 +1185,10 @@ __device__ __forceinline__ void pf_stages(pf_dvec4 (&acc)[4], const double* A, i
         sc.store_cm(Li, wc, 64);
       }
       __syncthreads();
+      stamp(3 * k + 1);
       pf_gemm_nt(acc, -1.0, ltile(T), ltile(Li), wv, lane);
       __syncthreads();
+      stamp(3 * k + 2);
     }
   }
 }
@@ -1293,7 +1306,7 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
           acc[t][q] = (i < hr && j < wc) ? v : 0.0;
         }
       pf_stages<WM>(acc, A, lda, r0, hr, c0, wc, c, flag + c * kPfMaxTiles, epoch, err, limit, T, Li, &s_ready, wv,
-                    lane);
+                    lane, dbg && c == r - 1 && r == nc - 1 ? dbg + (size_t)r * kPfDbgSlots + 20 : nullptr);
       pf_wait<WM>(flag + c * kPfMaxTiles + c, epoch, err, limit);
       stamp(1 + 2 * c);
       // L_rc = T Linv_cc' (Linv_cc row-major in linv, staged in LDS)

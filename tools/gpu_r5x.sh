@@ -1,4 +1,5 @@
 set -o pipefail
-mkdir -p gpurun_out/r5ab
-export MI_BA_LIB=ab
-timeout -k 10 900 python -u tools/ab_chol_keys.py "" "panel_rows_per_group=2,panel_group_min_rows=6000" "panel_rows_per_group=2" "head_panel=1024,head_cols=4096" "tail_panel=256,tail_cols=4096" "" "panel_rows_per_group=2,panel_group_min_rows=6000" "head_panel=1024,head_cols=4096" > gpurun_out/r5ab/ab.jsonl 2> gpurun_out/r5ab/ab.err
+mkdir -p gpurun_out/r5ac
+timeout -k 10 60 tools/probes/panel_probe.bin 12000 3 1 0 2 > gpurun_out/r5ac/probe_fv3_wm2.txt 2>&1 &&
+timeout -k 10 60 tools/probes/panel_probe.bin 12000 3 1 0 0 > gpurun_out/r5ac/probe_fv3_wm0.txt 2>&1 &&
+MI_BA_LIB=ab timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_cholesky.py > gpurun_out/r5ac/tests_chol_ab.log 2>&1
