@@ -291,7 +291,9 @@ __device__ inline void wave_load_rows_u(const double* __restrict__ src, double* 
 // loads and r stores, 32 16-B J stores, 128 per-block loads issued up front;
 // 1 and 2 are the diagnostic builds; 512 closed-form rotation columns, 1024
 // R X through the rotation matrix.
-constexpr int kJacProduction = 8 | 16 | 32 | 128 | 512 | 1024 | 8192;  // 0.583 -> 0.543 ms at C4 with 512 | 1024
+// (8192, the packed ids, is a tools-build variant: 0.496 vs 0.460 ms in the
+// bench step on one box, profiles/r5ae_bench_packed_ids_vs_r4.jsonl)
+constexpr int kJacProduction = 8 | 16 | 32 | 128 | 512 | 1024;  // 0.583 -> 0.543 ms at C4 with 512 | 1024
 // J rows staged in one slab pass (64 rows, 17 KB of LDS per wave at OPENCV: 2
 // waves per SIMD, each store burst 15 KB): 0.554 (2 passes) -> 0.454 ms at C4
 // once the arithmetic was cut by the closed-form rotation columns
@@ -3491,7 +3493,11 @@ void launch_touch_inputs(const DevProblem& p, unsigned* sink, hipStream_t s, int
   // mask bits: 1 observations, 2 image ids, 4 point ids, 8 points; the ids
   // in the layout the kernel reads (packed: both in obs_ids + wave_pt0)
   TouchRanges t{};
+#ifdef MI_BA_AB_VARIANTS
+  const bool packed = ((kJacProduction & 8192) != 0 || p.jvariant == 43) && p.obs_ids;
+#else
   const bool packed = (kJacProduction & 8192) != 0 && p.obs_ids;
+#endif
   const int64_t nw = (p.nb + 63) / 64;
   const void* ptrs[5] = {p.obs_xy, packed ? (const void*)p.obs_ids : (const void*)p.obs_img,
                          packed ? (const void*)p.wave_pt0 : (const void*)p.obs_pt, nullptr, p.X};
@@ -3647,8 +3653,8 @@ void launch_reproj_jacobian(const DevProblem& p, double2* r, double* J, double* 
               hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, kJacPasses, kJacProduction | 1>), dim3(g), dim3(kBlock),
                                  0, s, p, r, J, cost_partial);
               return;
-            case 43:  // ids from obs_img + obs_pt (before the packed ids)
-              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, kJacPasses, kJacProduction & ~8192>), dim3(g),
+            case 43:  // packed ids (obs_ids + wave_pt0; slower in the bench step)
+              hipLaunchKernelGGL((reproj_jacobian_kernel<M, RF, 0, kJacPasses, kJacProduction | 8192>), dim3(g),
                                  dim3(kBlock), 0, s, p, r, J, cost_partial);
               return;
             case 13:  // R and the unit-q test from the image record (per image, not per block)

@@ -660,7 +660,9 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
           hipMemcpy(ctx->obs_img.ptr, im.data(), nb * 4, hipMemcpyHostToDevice) ||
           hipMemcpy(ctx->obs_pt.ptr, pt.data(), nb * 4, hipMemcpyHostToDevice))
         return fail(MI_BA_ERR_HIP);
-      // packed ids of the reprojection kernel (device.h obs_ids)
+#ifdef MI_BA_AB_VARIANTS
+      // packed ids of the reprojection kernel (device.h obs_ids; tools build,
+      // jacobian_variant 43)
       const int64_t nw = (nb + 63) / 64;
       std::vector<uint32_t> ids(nb), w0(nw);
       bool packed = I <= 65536;
@@ -679,6 +681,7 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
             hipMemcpy(ctx->wave_pt0.ptr, w0.data(), nw * 4, hipMemcpyHostToDevice))
           return fail(MI_BA_ERR_HIP);
       }
+#endif
     }
     // camera-major permutation and image-aligned tiles
     std::vector<uint32_t> perm(nb);
