@@ -1201,14 +1201,17 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
                                                            int* __restrict__ info, double* __restrict__ linv,
                                                            unsigned* ctrl, unsigned base, unsigned epoch,
                                                            unsigned* err, unsigned limit, int below_groups = 0,
-                                                           unsigned long long* dbg = nullptr) {
+                                                           unsigned long long* dbg = nullptr, int r_off = 0,
+                                                           unsigned* tick = nullptr) {
   __shared__ double T[64 * kPfLd];   // staging / factor tile (row-major padded)
   __shared__ double Li[64 * kPfLd];  // a diagonal tile's inverse (own, or workgroup c's)
   __shared__ double Lc[1152];        // pf_chol_inv_fast scratch: per-wave 16x16 tiles + the pivot status
   __shared__ double dinv[64];
   __shared__ int s_r, s_ready;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_r = (int)(atomicAdd(ctrl, 1u) - base);
+  // row tile from the launch's ticket (tick: a second counter, r_off: the
+  // first row tile of a below-rows launch of the split tail)
+  if (threadIdx.x == 0) s_r = (int)(atomicAdd(tick ? tick : ctrl, 1u) - base) + r_off;
   __syncthreads();
   const int r = s_r;
   const int nc = (kb + 63) / 64;
@@ -1475,7 +1478,23 @@ rocblas_status backward(rocblas_handle h, int n, const double* A, int lda, doubl
 // updated by dsyrk (or by dgemm per block column of width `panel`).
 rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, int own,
                             double* scratch, CholWorkspace* ws, int ex);
+rocblas_status panel_factor_fused(hipStream_t s, int n, double* A, int lda, int k, int kb, int* info,
+                                  CholWorkspace* ws, int ex, int part);
 rocblas_status gemm_nt(rocblas_handle h, int m, int n, int k, const double* P, int ldp, double* C, int ldc, int sol);
+rocblas_status gemm_nt2(rocblas_handle h, int m, int n, int k, const double* Pa, const double* Pb, int ldp, double* C,
+                        int ldc, int sol);
+// split tail (CholConfig::split_tail_cols): does panel kk + 1 (start ps[kk + 1])
+// get its block column in two dgemms?
+// Tools build only: measured slower (Cholesky 16.2-16.6 vs 14.2 ms — the
+// fourth stream shares a hardware queue, profiles/r5ag_ab_cholesky_split_tail.jsonl).
+static bool split_tail(const CholConfig& cfg, const std::vector<int>& ps, int kk, int n, int ex) {
+#ifndef MI_BA_AB_VARIANTS
+  if (cfg.split_tail_cols >= 0) return false;
+#endif
+  if (cfg.split_tail_cols <= 0 || cfg.own_diag != 6 || kk + 2 >= (int)ps.size()) return false;
+  const int k1 = ps[kk + 1], jb0 = ps[kk + 2] - k1;
+  return n - k1 <= cfg.split_tail_cols && n - k1 + ex > jb0;
+}
 
 rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* info, const CholConfig& cfg,
                               double* scratch, CholWorkspace* ws, int ex) {
@@ -1507,7 +1526,13 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
       for (int j = 0; j < m; j = j == 0 ? jb0 : j + cw) {
         const int jb = std::min(j == 0 ? jb0 : cw, m - j);
-        st = gemm_nt(h, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
+        if (j == 0 && split_tail(cfg, ps, (int)pk, n, ex)) {  // the look-ahead's two dgemms (split tail)
+          st = gemm_nt(h, jb0, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
+          if (st == rocblas_status_success)
+            st = gemm_nt2(h, m + ex - jb0, jb0, kb, Aik + jb0, Aik, lda, T + jb0, lda, cfg.gemm_solution);
+        } else {
+          st = gemm_nt(h, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda, cfg.gemm_solution);
+        }
         if (st != rocblas_status_success) return st;
       }
     }
@@ -1522,11 +1547,12 @@ rocblas_status factor_blocked(rocblas_handle h, int n, double* A, int lda, int* 
 // iteration's dgemm waits on the side stream's event.  Hides the latency-bound
 // diagonal factor behind the MFMA update.
 // own_diag 6: diagonal factor + panel solve in one panel_factor_kernel launch
-rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info,
-                                  CholWorkspace* ws, int ex) {
+// part: 0 the whole panel, 1 its diagonal-block rows, 2 the rows below them
+// (split tail: the same epoch as the part-1 launch before it, tickets from
+// the second counter, row tiles from nc)
+rocblas_status panel_factor_fused(hipStream_t s, int n, double* A, int lda, int k, int kb, int* info,
+                                  CholWorkspace* ws, int ex, int part) {
   if (!ws || !ws->pf_ctrl || !ws->pf_linv || !ws->err || kb > 64 * kPfMaxTiles) return rocblas_status_invalid_pointer;
-  hipStream_t s;
-  if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
   const int mrows = n - k + ex;  // the extra rows below the matrix take the panel solve too
   const int nc = (kb + 63) / 64;
   const int nbelow = (mrows - kb + 63) / 64;
@@ -1536,14 +1562,19 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   int groups = 0;
   if (ws->rows_per_group > 1 && mrows - kb >= ws->group_min_rows && nbelow > 0)
     groups = (nbelow + ws->rows_per_group - 1) / ws->rows_per_group;
-  const int nr = nc + (groups > 0 ? groups : nbelow);  // workgroups (tickets) of the launch
-  if (ws->pf_base > 0x7fffffffu || ws->pf_epoch > 0xfffffff0u) {
-    if (hipMemsetAsync(ws->pf_ctrl, 0, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles), s) != hipSuccess)
+  const int nbg = groups > 0 ? groups : nbelow;
+  const int nr = part == 1 ? nc : part == 2 ? nbg : nc + nbg;  // workgroups (tickets) of the launch
+  if (nr == 0) return rocblas_status_success;
+  if (part != 2 && (ws->pf_base > 0x7fffffffu || ws->pf_base2 > 0x7fffffffu || ws->pf_epoch > 0xfffffff0u)) {
+    if (hipMemsetAsync(ws->pf_ctrl, 0, sizeof(unsigned) * (2 + kPfMaxTiles * kPfMaxTiles), s) != hipSuccess)
       return rocblas_status_internal_error;
     ws->pf_base = 0;
+    ws->pf_base2 = 0;
     ws->pf_epoch = 0;
   }
-  const unsigned epoch = ++ws->pf_epoch;
+  const unsigned epoch = part == 2 ? ws->pf_epoch : ++ws->pf_epoch;
+  unsigned* tick = part == 2 ? ws->pf_ctrl + 1 + kPfMaxTiles * kPfMaxTiles : nullptr;
+  const unsigned base = part == 2 ? ws->pf_base2 : ws->pf_base;
 #ifdef MI_BA_AB_VARIANTS
   auto pick = [&](auto wm) {
     constexpr int W = decltype(wm)::value;
@@ -1563,8 +1594,8 @@ rocblas_status panel_factor_fused(rocblas_handle h, int n, double* A, int lda, i
   auto kern = panel_factor_kernel<kDef.tile_factor, true, kDef.panel_wait>;
 #endif
   hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, s, A + k + (size_t)k * lda, lda, kb, mrows, info, ws->pf_linv,
-                     ws->pf_ctrl, ws->pf_base, epoch, ws->err, ws->spin_limit, groups, nullptr);
-  ws->pf_base += (unsigned)nr;
+                     ws->pf_ctrl, base, epoch, ws->err, ws->spin_limit, groups, nullptr, part == 2 ? nc : 0, tick);
+  (part == 2 ? ws->pf_base2 : ws->pf_base) += (unsigned)nr;
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
 
@@ -1597,7 +1628,11 @@ rocblas_status panel_factor_inv(rocblas_handle h, int n, double* A, int lda, int
 
 rocblas_status panel_factor(rocblas_handle h, int n, double* A, int lda, int k, int kb, int* info, int own,
                             double* scratch, CholWorkspace* ws, int ex) {
-  if (own == 6) return panel_factor_fused(h, n, A, lda, k, kb, info, ws, ex);
+  if (own == 6) {
+    hipStream_t s;
+    if (rocblas_get_stream(h, &s) != rocblas_status_success) return rocblas_status_internal_error;
+    return panel_factor_fused(s, n, A, lda, k, kb, info, ws, ex, 0);
+  }
 #ifdef MI_BA_AB_VARIANTS
   if (own == 7) return panel_factor_inv(h, n, A, lda, k, kb, info, scratch, ws, ex);
 #endif
@@ -1655,15 +1690,22 @@ static bool gemm_solution_offered(rocblas_handle h, int m, int n, int k, const d
 }
 
 rocblas_status gemm_nt(rocblas_handle h, int m, int n, int k, const double* P, int ldp, double* C, int ldc, int sol) {
+  return gemm_nt2(h, m, n, k, P, P, ldp, C, ldc, sol);
+}
+
+// C -= Pa Pb' (m x n, K = k): the rows below a block column's diagonal block
+// (split tail), Pa those rows of the panel, Pb the block column's rows of it
+rocblas_status gemm_nt2(rocblas_handle h, int m, int n, int k, const double* Pa, const double* Pb, int ldp, double* C,
+                        int ldc, int sol) {
   const double minus_one = -1.0, one = 1.0;
-  if (sol != 0 && gemm_solution_offered(h, m, n, k, P, ldp, C, ldc, sol)) {
+  if (sol != 0 && gemm_solution_offered(h, m, n, k, Pa, ldp, C, ldc, sol)) {
     const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_transpose, m, n, k,
-                                              &minus_one, P, rocblas_datatype_f64_r, ldp, P, rocblas_datatype_f64_r, ldp,
-                                              &one, C, rocblas_datatype_f64_r, ldc, C, rocblas_datatype_f64_r, ldc,
+                                              &minus_one, Pa, rocblas_datatype_f64_r, ldp, Pb, rocblas_datatype_f64_r,
+                                              ldp, &one, C, rocblas_datatype_f64_r, ldc, C, rocblas_datatype_f64_r, ldc,
                                               rocblas_datatype_f64_r, rocblas_gemm_algo_solution_index, sol, 0);
     if (st == rocblas_status_success) return st;
   }
-  return rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, n, k, &minus_one, P, ldp, P, ldp,
+  return rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, n, k, &minus_one, Pa, ldp, Pb, ldp,
                        &one, C, ldc);
 }
 
@@ -1765,6 +1807,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
                         : 1;
   auto fail = [&](rocblas_status e) {
     for (int r = 0; r + 1 < nrest; ++r) (void)hipStreamSynchronize(ws.rest_s[r]);
+    if (ws.side2) (void)hipStreamSynchronize(ws.side2);
     if (split_ok) {
       (void)hipStreamSynchronize(ws.split_side);
       (void)hipStreamSynchronize(ws.split_main);
@@ -1798,14 +1841,38 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     double* T = Aik + (size_t)kb * lda;          // trailing matrix, lower triangle
     // block column k+1 (the next panel) first
     const int jb0 = ps[kk + 2] - ps[kk + 1];
-    st = gemm_nt(hm, m + ex, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
-    if (st != rocblas_status_success) return fail(st);
     hipEvent_t upd = ws.ev[2 * kk], pan = ws.ev[2 * kk + 1];
-    if (hipEventRecord(upd, sm) != hipSuccess || hipStreamWaitEvent(ss, upd, 0) != hipSuccess)
-      return fail(rocblas_status_internal_error);
-    st = panel_factor(hs, n, A, lda, k + kb, jb0, info + kk + 1, own_for(k + kb), scratch_side, &ws, ex);
-    if (st != rocblas_status_success) return fail(st);
-    if (hipEventRecord(pan, ss) != hipSuccess) return fail(rocblas_status_internal_error);
+    // split tail: the diagonal block's rows of block column k+1, the panel's
+    // diagonal-block rows on the side stream, then the rows below and the
+    // panel's below-diagonal rows on side2 (factor_blocked: the same dgemms)
+    const bool split = split_tail(cfg, ps, kk, n, ex) && sm == s1 && own_for(k + kb) == 6 && ws.side2 &&
+                       ws.ev2.size() >= 2 * (size_t)(kk + 1);
+    if (split) {
+      st = gemm_nt(hm, jb0, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
+      if (st != rocblas_status_success) return fail(st);
+      if (hipEventRecord(upd, sm) != hipSuccess || hipStreamWaitEvent(ss, upd, 0) != hipSuccess)
+        return fail(rocblas_status_internal_error);
+      st = panel_factor_fused(ss, n, A, lda, k + kb, jb0, info + kk + 1, &ws, ex, 1);
+      if (st != rocblas_status_success) return fail(st);
+      st = gemm_nt2(hm, m + ex - jb0, jb0, kb, Aik + jb0, Aik, lda, T + jb0, lda, cfg.gemm_solution);
+      if (st != rocblas_status_success) return fail(st);
+      hipEvent_t upd2 = ws.ev2[2 * kk], pan2 = ws.ev2[2 * kk + 1];
+      if (hipEventRecord(upd2, sm) != hipSuccess || hipStreamWaitEvent(ws.side2, upd2, 0) != hipSuccess)
+        return fail(rocblas_status_internal_error);
+      st = panel_factor_fused(ws.side2, n, A, lda, k + kb, jb0, info + kk + 1, &ws, ex, 2);
+      if (st != rocblas_status_success) return fail(st);
+      if (hipEventRecord(pan2, ws.side2) != hipSuccess || hipStreamWaitEvent(ss, pan2, 0) != hipSuccess)
+        return fail(rocblas_status_internal_error);
+      if (hipEventRecord(pan, ss) != hipSuccess) return fail(rocblas_status_internal_error);
+    } else {
+      st = gemm_nt(hm, m + ex, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
+      if (st != rocblas_status_success) return fail(st);
+      if (hipEventRecord(upd, sm) != hipSuccess || hipStreamWaitEvent(ss, upd, 0) != hipSuccess)
+        return fail(rocblas_status_internal_error);
+      st = panel_factor(hs, n, A, lda, k + kb, jb0, info + kk + 1, own_for(k + kb), scratch_side, &ws, ex);
+      if (st != rocblas_status_success) return fail(st);
+      if (hipEventRecord(pan, ss) != hipSuccess) return fail(rocblas_status_internal_error);
+    }
     // the rest of the trailing lower triangle (columns jb0 .. m)
     [[maybe_unused]] const int mr = m - jb0;
 #ifdef MI_BA_AB_VARIANTS
@@ -1920,14 +1987,15 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
     // null-stream memset is not ordered against the non-blocking streams)
     if (hipMemsetAsync(linv, 0, sizeof(double) * kTB * kTB * (size_t)nblk, side) != hipSuccess) return false;
     if (hipMalloc(&ctrl, sizeof(unsigned) * (2 + (size_t)nblk)) != hipSuccess) { ctrl = nullptr; return false; }
-    if (hipMalloc(&pf_ctrl, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles)) != hipSuccess) {
+    if (hipMalloc(&pf_ctrl, sizeof(unsigned) * (2 + kPfMaxTiles * kPfMaxTiles)) != hipSuccess) {
       pf_ctrl = nullptr;
       return false;
     }
-    if (hipMemsetAsync(pf_ctrl, 0, sizeof(unsigned) * (1 + kPfMaxTiles * kPfMaxTiles), side) != hipSuccess)
+    if (hipMemsetAsync(pf_ctrl, 0, sizeof(unsigned) * (2 + kPfMaxTiles * kPfMaxTiles), side) != hipSuccess)
       return false;
     if (hipMalloc(&pf_linv, sizeof(double) * 64 * 64 * kPfMaxTiles) != hipSuccess) { pf_linv = nullptr; return false; }
     pf_base = 0;
+    pf_base2 = 0;
     pf_epoch = 0;
     if (hipMemsetAsync(ctrl, 0, sizeof(unsigned) * (2 + (size_t)nblk), side) != hipSuccess) return false;
     if (hipMalloc(&err, 4 * sizeof(unsigned)) != hipSuccess) { err = nullptr; return false; }
@@ -2078,9 +2146,33 @@ bool CholWorkspace::set_rest_streams(int k, bool cumask, int priority) {
   return true;
 }
 
+// split tail: the below-rows stream (the side stream's priority: a hardware
+// queue of its own) and its events, made on first use
+bool CholWorkspace::ensure_side2(int max_panels) {
+  if (!side2) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = least = 0;
+    if (hipStreamCreateWithPriority(&side2, hipStreamNonBlocking, greatest) != hipSuccess) {
+      side2 = nullptr;
+      return false;
+    }
+  }
+  while (ev2.size() < 2 * (size_t)std::max(1, max_panels)) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+    ev2.push_back(e);
+  }
+  return true;
+}
+
 void CholWorkspace::destroy() {
   if (device >= 0) (void)hipSetDevice(device);
   if (side) (void)hipStreamSynchronize(side);
+  if (side2) (void)hipStreamSynchronize(side2);
+  for (hipEvent_t e : ev2) (void)hipEventDestroy(e);
+  ev2.clear();
+  if (side2) (void)hipStreamDestroy(side2);
+  side2 = nullptr;
   if (split_n > 0 || split_side || split_main) (void)set_split_cus(0);
   if (rest_s[0] || rest_n != 1) (void)set_rest_streams(1);
   for (hipEvent_t e : ev) (void)hipEventDestroy(e);
@@ -2133,6 +2225,11 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   if (c.own_diag == 7) c.own_diag = 2;  // own_diag 7 is in the tools build only
 #endif
   if (ws) {
+#ifdef MI_BA_AB_VARIANTS
+    if (c.split_tail_cols > 0 && c.own_diag == 6 && c.lookahead &&
+        !ws->ensure_side2((int)chol_panel_starts(n, c).size()))
+      return rocblas_status_internal_error;
+#endif
     ws->tile_factor = c.tile_factor;
     ws->write_through = c.write_through;
     ws->panel_wait = c.panel_wait;

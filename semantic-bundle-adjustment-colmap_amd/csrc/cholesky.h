@@ -39,6 +39,15 @@ struct CholConfig {
   // (76 KB LDS, 342 VGPRs per lane) do not halve the dgemm's occupancy on the
   // CUs they share; 0 = off
   int split_cus = 0, split_cols = 0;
+  // split tail (own_diag 6, look-ahead): for the panels starting within the
+  // last split_tail_cols columns, the next panel's block column is updated in
+  // two dgemms — its diagonal block's rows first, so the diagonal-block rows of
+  // the panel factor start on the side stream, the rows below second — and the
+  // panel's below-diagonal rows run as a second launch on a second side stream
+  // once they are updated; factor_blocked makes the same two dgemms (bitwise
+  // equal factors); 0 = off.  Tools build: measured slower, the second side
+  // stream takes a fourth hardware queue (profiles/r5ag_ab_cholesky_split_tail.jsonl)
+  int split_tail_cols = 0;
   // head panel kind: panels starting before column head_own_cols use own_diag
   // head_own (e.g. 2: 64-wide diagonal kernels + rocBLAS dtrsm, no resident
   // spin-waiting workgroups beside the trailing dgemm); 0 = off
@@ -157,9 +166,13 @@ struct CholWorkspace {
   double* ybuf = nullptr;     // [n] intermediate vector of chol_solve (L y = b)
   unsigned* ctrl = nullptr;   // [2 + n/64] sync-free sweeps: two tickets + per-block solution flags
   unsigned epoch = 0;         // last flag value published (two per chol_solve)
-  unsigned* pf_ctrl = nullptr;  // one-launch panel factor: ticket + [8][8] tile flags
+  unsigned* pf_ctrl = nullptr;  // one-launch panel factor: ticket + [16][16] tile flags + second ticket
   double* pf_linv = nullptr;    // [8][64*64] inverses of the panel's diagonal tiles
   unsigned pf_base = 0;         // tickets handed out so far
+  unsigned pf_base2 = 0;        // tickets of the below-rows launches (split tail), second counter
+  hipStream_t side2 = nullptr;  // split tail: the below-rows launches
+  std::vector<hipEvent_t> ev2;  // split tail: [panel][2] below rows updated / factored
+  bool ensure_side2(int max_panels);
   unsigned pf_epoch = 0;        // flag value of the last panel launch
   int tile_factor = 3;          // CholConfig::tile_factor
   bool write_through = false;   // CholConfig::write_through

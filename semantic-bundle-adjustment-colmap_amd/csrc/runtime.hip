@@ -2458,6 +2458,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.tile_factor = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "cholesky_split_tail_cols") == 0 && value >= 0 && ab_value(value, CholConfig{}.split_tail_cols)) {
+    ctx->chol.split_tail_cols = value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_panel_wait") == 0 && value >= 0 && value <= 3 &&
       ab_value(value, CholConfig{}.panel_wait)) {
     ctx->chol.panel_wait = value;

@@ -282,6 +282,30 @@ def test_lm_handoff_variants_bitwise(gpu):
         assert r == res[0]
 
 
+def test_lm_split_tail(gpu):
+    """Split tail (cholesky_split_tail_cols, tools build): the next panel's
+    block column updated in two dgemms and the panel's below-diagonal rows as
+    a second launch on a second side stream, over the last 1024 / all columns
+    (nf = 1593: 4 panels): the same LM steps as the one-launch panels, final
+    cost within 1e-9 (different dgemm shapes sum in a different order), and
+    bit for bit repeatable."""
+    if not mi_ba.ab_build():
+        pytest.skip("split tail: tools build only (MI_BA_LIB=ab)")
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for cols in (0, 1024, 100000, 100000):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            ctx.set_tuning("cholesky_split_tail_cols", cols)
+            res.append(ctx.solve())
+    b = res[0]
+    for a in res[1:]:
+        assert (a.num_successful_steps, a.num_unsuccessful_steps) == (b.num_successful_steps, b.num_unsuccessful_steps)
+        assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
+    assert res[2].final_cost == res[3].final_cost
+
+
 def test_lm_gemm_solution(gpu):
     """The trailing update through rocblas_gemm_ex with an explicit Tensile
     solution index (cholesky_gemm_solution; an index the shape does not accept
