@@ -1845,7 +1845,8 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     // split tail: the diagonal block's rows of block column k+1, the panel's
     // diagonal-block rows on the side stream, then the rows below and the
     // panel's below-diagonal rows on side2 (factor_blocked: the same dgemms)
-    const bool split = split_tail(cfg, ps, kk, n, ex) && sm == s1 && own_for(k + kb) == 6 && ws.side2 &&
+    hipStream_t s2 = cfg.split_tail_rest ? (nrest > 1 ? ws.rest_s[0] : nullptr) : ws.side2;
+    const bool split = split_tail(cfg, ps, kk, n, ex) && sm == s1 && own_for(k + kb) == 6 && s2 &&
                        ws.ev2.size() >= 2 * (size_t)(kk + 1);
     if (split) {
       st = gemm_nt(hm, jb0, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
@@ -1857,11 +1858,11 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       st = gemm_nt2(hm, m + ex - jb0, jb0, kb, Aik + jb0, Aik, lda, T + jb0, lda, cfg.gemm_solution);
       if (st != rocblas_status_success) return fail(st);
       hipEvent_t upd2 = ws.ev2[2 * kk], pan2 = ws.ev2[2 * kk + 1];
-      if (hipEventRecord(upd2, sm) != hipSuccess || hipStreamWaitEvent(ws.side2, upd2, 0) != hipSuccess)
+      if (hipEventRecord(upd2, sm) != hipSuccess || hipStreamWaitEvent(s2, upd2, 0) != hipSuccess)
         return fail(rocblas_status_internal_error);
-      st = panel_factor_fused(ws.side2, n, A, lda, k + kb, jb0, info + kk + 1, &ws, ex, 2);
+      st = panel_factor_fused(s2, n, A, lda, k + kb, jb0, info + kk + 1, &ws, ex, 2);
       if (st != rocblas_status_success) return fail(st);
-      if (hipEventRecord(pan2, ws.side2) != hipSuccess || hipStreamWaitEvent(ss, pan2, 0) != hipSuccess)
+      if (hipEventRecord(pan2, s2) != hipSuccess || hipStreamWaitEvent(ss, pan2, 0) != hipSuccess)
         return fail(rocblas_status_internal_error);
       if (hipEventRecord(pan, ss) != hipSuccess) return fail(rocblas_status_internal_error);
     } else {
@@ -1905,7 +1906,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       // block columns of width nb (rest_update 0) or 2 nb (3)
       const int cw = cfg.rest_update == 3 ? 2 * nb : nb;
       // streams used this panel: no more than its block columns
-      const int ns = sm == s1 ? std::min(nrest, (mr + cw - 1) / cw) : 1;
+      const int ns = sm == s1 && !(split && cfg.split_tail_rest) ? std::min(nrest, (mr + cw - 1) / cw) : 1;
       hipEvent_t* evr = ns > 1 ? ws.ev_rest.data() + (size_t)CholWorkspace::kMaxRest * kk : nullptr;
       if (ns > 1) {
         if (hipEventRecord(evr[0], sm) != hipSuccess) return fail(rocblas_status_internal_error);
@@ -2148,8 +2149,8 @@ bool CholWorkspace::set_rest_streams(int k, bool cumask, int priority) {
 
 // split tail: the below-rows stream (the side stream's priority: a hardware
 // queue of its own) and its events, made on first use
-bool CholWorkspace::ensure_side2(int max_panels) {
-  if (!side2) {
+bool CholWorkspace::ensure_side2(int max_panels, bool stream) {
+  if (stream && !side2) {
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = least = 0;
     if (hipStreamCreateWithPriority(&side2, hipStreamNonBlocking, greatest) != hipSuccess) {
@@ -2227,7 +2228,7 @@ rocblas_status chol_factor(rocblas_handle h, int n, double* A, int lda, int* inf
   if (ws) {
 #ifdef MI_BA_AB_VARIANTS
     if (c.split_tail_cols > 0 && c.own_diag == 6 && c.lookahead &&
-        !ws->ensure_side2((int)chol_panel_starts(n, c).size()))
+        !ws->ensure_side2((int)chol_panel_starts(n, c).size(), !c.split_tail_rest))
       return rocblas_status_internal_error;
 #endif
     ws->tile_factor = c.tile_factor;

@@ -48,6 +48,10 @@ struct CholConfig {
   // equal factors); 0 = off.  Tools build: measured slower, the second side
   // stream takes a fourth hardware queue (profiles/r5ag_ab_cholesky_split_tail.jsonl)
   int split_tail_cols = 0;
+  // split tail: the below-rows launch on the second trailing-update stream
+  // (rest_streams >= 2; that panel's whole trailing update then on the
+  // caller's stream) instead of a fourth stream
+  bool split_tail_rest = false;
   // head panel kind: panels starting before column head_own_cols use own_diag
   // head_own (e.g. 2: 64-wide diagonal kernels + rocBLAS dtrsm, no resident
   // spin-waiting workgroups beside the trailing dgemm); 0 = off
@@ -172,7 +176,7 @@ struct CholWorkspace {
   unsigned pf_base2 = 0;        // tickets of the below-rows launches (split tail), second counter
   hipStream_t side2 = nullptr;  // split tail: the below-rows launches
   std::vector<hipEvent_t> ev2;  // split tail: [panel][2] below rows updated / factored
-  bool ensure_side2(int max_panels);
+  bool ensure_side2(int max_panels, bool stream = true);
   unsigned pf_epoch = 0;        // flag value of the last panel launch
   int tile_factor = 3;          // CholConfig::tile_factor
   bool write_through = false;   // CholConfig::write_through

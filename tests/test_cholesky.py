@@ -285,7 +285,8 @@ def test_lm_handoff_variants_bitwise(gpu):
 def test_lm_split_tail(gpu):
     """Split tail (cholesky_split_tail_cols, tools build): the next panel's
     block column updated in two dgemms and the panel's below-diagonal rows as
-    a second launch on a second side stream, over the last 1024 / all columns
+    a second launch on a second side stream (or on the second trailing-update
+    stream, cholesky_split_tail_rest), over the last 1024 / all columns
     (nf = 1593: 4 panels): the same LM steps as the one-launch panels, final
     cost within 1e-9 (different dgemm shapes sum in a different order), and
     bit for bit repeatable."""
@@ -295,9 +296,10 @@ def test_lm_split_tail(gpu):
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
     res = []
-    for cols in (0, 1024, 100000, 100000):
+    for cols, rest in ((0, 0), (1024, 0), (100000, 0), (100000, 0), (100000, 1)):
         with mi_ba.Context(opts, sc.copy()) as ctx:
             ctx.set_tuning("cholesky_split_tail_cols", cols)
+            ctx.set_tuning("cholesky_split_tail_rest", rest)
             res.append(ctx.solve())
     b = res[0]
     for a in res[1:]:
