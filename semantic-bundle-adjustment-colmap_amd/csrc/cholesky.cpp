@@ -1868,11 +1868,22 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     } else {
       st = gemm_nt(hm, m + ex, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
       if (st != rocblas_status_success) return fail(st);
+    }
+    auto launch_panel = [&]() -> rocblas_status {
       if (hipEventRecord(upd, sm) != hipSuccess || hipStreamWaitEvent(ss, upd, 0) != hipSuccess)
-        return fail(rocblas_status_internal_error);
-      st = panel_factor(hs, n, A, lda, k + kb, jb0, info + kk + 1, own_for(k + kb), scratch_side, &ws, ex);
+        return rocblas_status_internal_error;
+      rocblas_status ps_ = panel_factor(hs, n, A, lda, k + kb, jb0, info + kk + 1, own_for(k + kb), scratch_side, &ws, ex);
+      if (ps_ != rocblas_status_success) return ps_;
+      return hipEventRecord(pan, ss) == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
+    };
+#ifdef MI_BA_AB_VARIANTS
+    const bool serial = !split && cfg.serial_head_cols > 0 && k + kb < cfg.serial_head_cols;
+#else
+    constexpr bool serial = false;
+#endif
+    if (!split && !serial) {
+      st = launch_panel();
       if (st != rocblas_status_success) return fail(st);
-      if (hipEventRecord(pan, ss) != hipSuccess) return fail(rocblas_status_internal_error);
     }
     // the rest of the trailing lower triangle (columns jb0 .. m)
     [[maybe_unused]] const int mr = m - jb0;
@@ -1924,6 +1935,10 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       for (int r = 0; r + 1 < ns; ++r)
         if (hipEventRecord(evr[1 + r], ws.rest_s[r]) != hipSuccess || hipStreamWaitEvent(sm, evr[1 + r], 0) != hipSuccess)
           return fail(rocblas_status_internal_error);
+    }
+    if (serial) {  // after the whole trailing update (joined into sm above)
+      st = launch_panel();
+      if (st != rocblas_status_success) return fail(st);
     }
     // panel k+1 is read by the next iteration's updates (and by the solve)
     if (hipStreamWaitEvent(sm, pan, 0) != hipSuccess) return fail(rocblas_status_internal_error);

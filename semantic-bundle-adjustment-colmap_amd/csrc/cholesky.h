@@ -48,6 +48,11 @@ struct CholConfig {
   // equal factors); 0 = off.  Tools build: measured slower, the second side
   // stream takes a fourth hardware queue (profiles/r5ag_ab_cholesky_split_tail.jsonl)
   int split_tail_cols = 0;
+  // serial head (tools build): the panels starting before serial_head_cols
+  // are factored after the previous panel's whole trailing update instead of
+  // beside it (the panel's resident workgroups then never share CUs with the
+  // dgemm); 0 = off
+  int serial_head_cols = 0;
   // split tail: the below-rows launch on the second trailing-update stream
   // (rest_streams >= 2; that panel's whole trailing update then on the
   // caller's stream) instead of a fourth stream

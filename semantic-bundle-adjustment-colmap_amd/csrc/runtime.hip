@@ -2462,6 +2462,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.split_tail_cols = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "cholesky_serial_head_cols") == 0 && value >= 0 && ab_value(value, 0)) {
+    ctx->chol.serial_head_cols = value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_split_tail_rest") == 0 && (value == 0 || value == 1) && ab_value(value, 0)) {
     ctx->chol.split_tail_rest = value != 0;
     return MI_BA_OK;
