@@ -440,6 +440,13 @@ __device__ __forceinline__ void flag_wait(const unsigned* f, unsigned epoch, uns
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
+// Resident workgroups per CU the runtime admits for kern (-1 if unknown): the
+// sc1 hand-offs without an acquire are used only where this is 1.
+static int blocks_per_cu(const void* kern, int threads) {
+  int nb = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, threads, 0) == hipSuccess ? nb : -1;
+}
+
 // flag_wait without the acquire: for consumers whose every load of the
 // handed-off bytes is an sc1 load of bytes the producer stored sc1 and
 // drained before the flag (MI355X_MICROARCH.md §visibility, table row 1)
@@ -588,6 +595,15 @@ __global__ __launch_bounds__(64 * kSweepWaves) void trsv_sweep_kernel(const doub
   if (lane < w) x[r0 + lane] = z;
   __threadfence();
   if (lane == 0) __hip_atomic_store(flag + ib, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The sweeps' sc1 hand-offs (no fences) only where one workgroup per CU is
+// resident (their registers give one; MI355X_MICROARCH.md §visibility).
+static bool sweep_sc1_ok() {
+  static const bool ok =
+      blocks_per_cu(reinterpret_cast<const void*>(&trsv_sweep_kernel<true, true>), 64 * kSweepWaves) == 1 &&
+      blocks_per_cu(reinterpret_cast<const void*>(&trsv_sweep_kernel<false, true>), 64 * kSweepWaves) == 1;
+  return ok;
 }
 
 #ifdef MI_BA_AB_VARIANTS
@@ -1589,9 +1605,16 @@ rocblas_status panel_factor_fused(hipStream_t s, int n, double* A, int lda, int 
               : ws->panel_wait == 1 ? pick(std::integral_constant<int, 1>{})
                                     : pick(std::integral_constant<int, 0>{});
 #else
-  // the tools build keeps the other tile factors / plain stores / wait modes for A/B
+  // the tools build keeps the other tile factors / plain stores / wait modes for A/B.
+  // Wait mode 2 (sc1 loads, no acquire) is the hand-off form measured for one
+  // workgroup per CU (MI355X_MICROARCH.md §visibility): the kernel's registers
+  // give one; should a build ever admit more, the acquire form (mode 1) runs.
   constexpr CholConfig kDef{};
-  auto kern = panel_factor_kernel<kDef.tile_factor, true, kDef.panel_wait>;
+  static const bool one_per_cu = blocks_per_cu(reinterpret_cast<const void*>(
+                                                   &panel_factor_kernel<kDef.tile_factor, true, kDef.panel_wait>),
+                                               256) == 1;
+  auto kern = one_per_cu ? panel_factor_kernel<kDef.tile_factor, true, kDef.panel_wait>
+                         : panel_factor_kernel<kDef.tile_factor, true, 1>;
 #endif
   hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, s, A + k + (size_t)k * lda, lda, kb, mrows, info, ws->pf_linv,
                      ws->pf_ctrl, base, epoch, ws->err, ws->spin_limit, groups, nullptr, part == 2 ? nc : 0, tick);
@@ -2303,7 +2326,7 @@ rocblas_status chol_solve_backward(rocblas_handle h, int n, const double* A, int
                        ws->spin_limit);
   else
 #endif
-    hipLaunchKernelGGL((ws->solve_sc1 ? trsv_sweep_kernel<false, true> : trsv_sweep_kernel<false, false>), dim3(nblk),
+    hipLaunchKernelGGL((ws->solve_sc1 && sweep_sc1_ok() ? trsv_sweep_kernel<false, true> : trsv_sweep_kernel<false, false>), dim3(nblk),
                        dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e, ws->err, ws->spin_limit);
   return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
 }
@@ -2331,9 +2354,9 @@ rocblas_status chol_solve(rocblas_handle h, int n, const double* A, int lda, dou
     const unsigned e = ++ws->epoch;
     const unsigned e2 = ++ws->epoch;
     const int nblk = (n + kTB - 1) / kTB;
-    hipLaunchKernelGGL((ws->solve_sc1 ? trsv_sweep_kernel<true, true> : trsv_sweep_kernel<true, false>), dim3(nblk),
+    hipLaunchKernelGGL((ws->solve_sc1 && sweep_sc1_ok() ? trsv_sweep_kernel<true, true> : trsv_sweep_kernel<true, false>), dim3(nblk),
                        dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e, ws->err, ws->spin_limit);
-    hipLaunchKernelGGL((ws->solve_sc1 ? trsv_sweep_kernel<false, true> : trsv_sweep_kernel<false, false>), dim3(nblk),
+    hipLaunchKernelGGL((ws->solve_sc1 && sweep_sc1_ok() ? trsv_sweep_kernel<false, true> : trsv_sweep_kernel<false, false>), dim3(nblk),
                        dim3(64 * kSweepWaves), 0, s, A, lda, n, x, ws->ctrl, e2, ws->err, ws->spin_limit);
     return hipGetLastError() == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
   }
