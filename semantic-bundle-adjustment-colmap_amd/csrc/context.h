@@ -137,6 +137,10 @@ struct mi_ba_context {
   miba::DevArray<double> red;              // per-workgroup partials of the multi-workgroup reductions
   miba::DevArray<double> aux;              // [world + 2] gradient max norms: per-rank point part, camera part
   double* host_scalars = nullptr;          // pinned
+  int32_t* host_info = nullptr;            // pinned: the factor's per-block info + the flag-wait error word
+  int host_info_cap = 0;
+  bool chol_pending = false;               // host_info enqueued, not yet checked (dense_solve, single rank)
+  int chol_leaves = 0;
 
   // explicit reduced camera system (exact Schur solve, rocSOLVER Cholesky)
   bool dense = false;

@@ -988,6 +988,7 @@ void context_destroy(mi_ba_context* ctx) {
     ctx->comm = nullptr;
   }
   if (ctx->host_scalars) (void)hipHostFree(ctx->host_scalars);
+  if (ctx->host_info) (void)hipHostFree(ctx->host_info);
   if (ctx->stall_flag) (void)hipHostFree(ctx->stall_flag);
   if (ctx->lin_side) {
     (void)hipStreamSynchronize(ctx->lin_side);
@@ -1385,6 +1386,23 @@ void launch_schur_terms(mi_ba_context* ctx) {
 // Exact solve of S df = -b with the explicit reduced camera system.
 // *ok = false when S is not positive definite (Ceres: invalid step).
 // schur_launched: the Schur terms already run on lm_side (joined here).
+// Single rank: the factor's info and the flag-wait word are only enqueued
+// (ctx->chol_pending); the LM checks them at its next host wait, the model
+// cost's, and treats a failed factorisation as the invalid step it is.
+mi_ba_status chol_check_pending(mi_ba_context* ctx, bool* ok) {
+  *ok = true;
+  if (!ctx->chol_pending) return MI_BA_OK;
+  ctx->chol_pending = false;
+  const int leaves = ctx->chol_leaves;
+  const unsigned werr = (unsigned)ctx->host_info[leaves];
+  if (werr != 0) MI_HIP(hipMemsetAsync(ctx->cholws.err, 0, 4, ctx->stream));
+  mi_ba_status st = agree_on_error(ctx, werr != 0);
+  if (st != MI_BA_OK) return st;
+  for (int k = 0; k < leaves; ++k)
+    if (ctx->host_info[k] != 0) *ok = false;
+  return MI_BA_OK;
+}
+
 mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok, bool schur_launched) {
   const DevProblem& d = ctx->dev;
   hipStream_t s = ctx->stream;
@@ -1429,23 +1447,19 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok, bool schur_launched) {
                   fused ? 1 : 0) != rocblas_status_success)
     return MI_BA_ERR_HIP;
   timer_end(ctx, stop);
-  std::vector<int32_t> info(leaves, 0);
-  MI_HIP(hipMemcpyAsync(info.data(), ctx->info.ptr, 4 * (size_t)leaves, hipMemcpyDeviceToHost, s));
-  unsigned werr = 0;
-  {
-    mi_ba_status ds = comm_drain(ctx);  // the S bands' sums
-    if (ds != MI_BA_OK) return ds;
-  }
-  MI_HIP(chol_error(&ctx->cholws, s, &werr));  // synchronises s
-  // a flag wait of the factorisation ran out: the factor is invalid (every
-  // rank learns it, so no rank takes a step the others do not)
-  mi_ba_status st = agree_on_error(ctx, werr != 0);
-  if (st != MI_BA_OK) return st;
-  for (int32_t v : info) {
-    if (v != 0) {
-      *ok = false;
-      return MI_BA_OK;
+  // The backward sweep goes right behind the factorisation; its result is
+  // used only when every diagonal block was positive definite and no flag
+  // wait ran out, checked once after it (one host wait per solve instead of
+  // two: the factor's info and the error word land in pinned memory).
+  if (ctx->host_info_cap < leaves + 1) {
+    if (ctx->host_info) (void)hipHostFree(ctx->host_info);
+    ctx->host_info = nullptr;
+    ctx->host_info_cap = 0;
+    if (hipHostMalloc(&ctx->host_info, sizeof(int32_t) * (leaves + 1), hipHostMallocDefault) != hipSuccess) {
+      ctx->host_info = nullptr;
+      return MI_BA_ERR_OUT_OF_MEMORY;
     }
+    ctx->host_info_cap = leaves + 1;
   }
   {
     Phase ph_(ctx, "cholesky_solve");
@@ -1459,12 +1473,16 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok, bool schur_launched) {
       return MI_BA_ERR_HIP;
     }
   }
-  {
-    mi_ba_status ds = comm_drain(ctx);
-    if (ds != MI_BA_OK) return ds;
-  }
-  MI_HIP(chol_error(&ctx->cholws, s, &werr));
-  return agree_on_error(ctx, werr != 0);
+  MI_HIP(hipMemcpyAsync(ctx->host_info, ctx->info.ptr, 4 * (size_t)leaves, hipMemcpyDeviceToHost, s));
+  MI_HIP(hipMemcpyAsync(ctx->host_info + leaves, ctx->cholws.err, 4, hipMemcpyDeviceToHost, s));
+  ctx->chol_pending = true;
+  ctx->chol_leaves = leaves;
+  if (!ctx->distributed()) return MI_BA_OK;  // checked at the LM's next host wait
+  // multi-rank: checked here, agreed over the ranks (a flag wait of the
+  // factorisation or the sweep that ran out makes the step invalid on every
+  // rank, so no rank takes a step the others do not)
+  MI_HIP_DRAIN(ctx, s);  // the S bands' sums, then the factorisation and the sweep
+  return chol_check_pending(ctx, ok);
 }
 
 // Ceres RunCallbacks for one finished iteration: the stop flag, then the
@@ -1508,6 +1526,7 @@ mi_ba_status run_callbacks(mi_ba_context* ctx, const mi_ba_iteration_summary& it
 mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
   if (ctx->solved) return MI_BA_ERR_STATE;
   ctx->solved = true;
+  ctx->chol_pending = false;
   const double t_start = now_s();
   const mi_ba_options& o = ctx->options;
   const DevProblem& d = ctx->dev;
@@ -1683,8 +1702,12 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     }
     st = read_scalars(ctx, 0, kNumScalars);
     if (st != MI_BA_OK) return st;
+    // single rank: the factorisation's check, its copies landed with the scalars
+    bool factored = true;
+    st = chol_check_pending(ctx, &factored);
+    if (st != MI_BA_OK) return st;
     const double model_cost_change = hs[kModelCost] + hs[kSemModel] + hs[kGsModel];
-    const bool valid = std::isfinite(model_cost_change) && model_cost_change > 0.0;
+    const bool valid = factored && std::isfinite(model_cost_change) && model_cost_change > 0.0;
     if (!valid) {
       last_successful = false;
       ++consecutive_invalid;
