@@ -200,6 +200,8 @@ struct mi_ba_context {
   bool comm_failed = false;        // the communicator was aborted: every later collective fails
   int comm_timeout_ms = 300000;    // deadline of one collective / of the communicator set-up ("comm_timeout_ms")
   double comm_due = 0.0;           // collectives enqueued since the last host wait: their latest deadline (0: none)
+  int fail_factorizations = 0;     // test hook ("test_fail_factorizations"): the next n factorisations report a
+                                   // non-positive pivot (the LM's invalid-step path)
   int comm_stall_ms = 0;           // test hook ("comm_stall_ms"): a kernel that holds the stream this long
                                    // ahead of every collective (a peer that never arrives, seen locally)
   int* stall_flag = nullptr;       // pinned release flag of that kernel

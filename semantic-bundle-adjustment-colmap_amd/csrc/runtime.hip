@@ -1473,6 +1473,10 @@ mi_ba_status dense_solve(mi_ba_context* ctx, bool* ok, bool schur_launched) {
       return MI_BA_ERR_HIP;
     }
   }
+  if (ctx->fail_factorizations > 0) {  // test hook
+    --ctx->fail_factorizations;
+    MI_HIP(hipMemsetAsync(ctx->info.ptr, 0x01, 4, s));
+  }
   MI_HIP(hipMemcpyAsync(ctx->host_info, ctx->info.ptr, 4 * (size_t)leaves, hipMemcpyDeviceToHost, s));
   MI_HIP(hipMemcpyAsync(ctx->host_info + leaves, ctx->cholws.err, 4, hipMemcpyDeviceToHost, s));
   ctx->chol_pending = true;
@@ -2328,6 +2332,12 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
   // (a timed-out collective aborts the communicator, MI_BA_ERR_HIP)
   if (std::strcmp(key, "comm_timeout_ms") == 0 && value >= 1) {
     ctx->comm_timeout_ms = value;
+    return MI_BA_OK;
+  }
+  // test hook: the next `value` factorisations of the exact solve report a
+  // non-positive pivot in their first diagonal block
+  if (std::strcmp(key, "test_fail_factorizations") == 0 && value >= 0 && value <= 1000) {
+    ctx->fail_factorizations = value;
     return MI_BA_OK;
   }
   // test hook: hold the stream ahead of every RCCL collective for `value` ms

@@ -266,3 +266,30 @@ def test_c3_with_sba_tolerances_matches_oracle(gpu):
     assert (s_g.num_successful_steps, s_g.num_unsuccessful_steps) == (s_o.num_successful_steps, s_o.num_unsuccessful_steps)
     assert s_g.termination_type == s_o.termination_type
     assert abs(s_g.final_cost - s_o.final_cost) <= 1e-6 * s_o.final_cost
+
+
+@pytest.mark.gpu
+def test_failed_factorisation_is_an_invalid_step(gpu):
+    """A factorisation that reports a non-positive pivot makes the step
+    invalid, as Ceres' dense Schur solver failing does: the radius shrinks
+    and the LM goes on (checked at the model cost's host wait on one rank).
+    Test hook `test_fail_factorizations` n: the next n factorisations report
+    one.  Two of them: two more unsuccessful steps, then the same minimum;
+    eleven (> max_num_consecutive_invalid_steps 10): FAILURE at the initial
+    point."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 60, 3000, track_length=6,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=9)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=30, linear_solver_type=mi_ba.SOLVER_DENSE_SCHUR)
+    res = {}
+    for n in (0, 2, 11):
+        with mi_ba.Context(opts, sc.copy()) as ctx:
+            ctx.set_tuning("test_fail_factorizations", n)
+            res[n] = ctx.solve()
+    s0, s2, s11 = res[0], res[2], res[11]
+    assert s0.termination_type != mi_ba.FAILURE and s0.final_cost < s0.initial_cost
+    assert s2.termination_type != mi_ba.FAILURE
+    assert s2.num_unsuccessful_steps >= 2 and s2.initial_cost == s0.initial_cost
+    assert abs(s2.final_cost - s0.final_cost) <= 1e-6 * s0.final_cost
+    assert s11.termination_type == mi_ba.FAILURE
+    assert (s11.num_successful_steps, s11.num_unsuccessful_steps) == (0, 11)
+    assert s11.final_cost == s11.initial_cost
