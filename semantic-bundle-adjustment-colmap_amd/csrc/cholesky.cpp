@@ -917,6 +917,51 @@ __device__ __forceinline__ int pf_col16(double* M, double* dinv, int o, int lane
   return bad;
 }
 
+// pf_col16 with the next pivot formed from broadcast values: the
+// multipliers of column k are (a[k] at lane o + c) * isd — taken by readlane
+// of a[k] before the pivot is known — and the next pivot is (a[k + 1] at lane
+// o + k + 1) - m * m, so the pivot chain runs rsq -> refinement -> one mul ->
+// one fma without the per-lane select and the two readlanes of each column
+// (the same operations on the same values: bitwise equal; tools build).
+template <bool RSQ>
+__device__ __forceinline__ int pf_col16_fp(double* M, double* dinv, int o, int lane) {
+  double a[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) a[c] = M[lane * kPfLd + o + c];
+  int bad = 0;
+  double my_isd = 0.0;  // lane o + k keeps pivot k's reciprocal
+  double d = readlane_f64(a[0], o);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (!(d > 0.0) && bad == 0) bad = o + k + 1;
+    double x[16];
+#pragma unroll
+    for (int c = k + 1; c < 16; ++c) x[c] = readlane_f64(a[k], o + c);
+    const double y = k + 1 < 16 ? readlane_f64(a[k + 1], o + k + 1) : 0.0;
+    double sd, isd;
+    pf_pivot<RSQ>(d, sd, isd);
+    const bool piv = lane == o + k;
+    const double l = piv ? sd : a[k] * isd;
+    my_isd = piv ? isd : my_isd;
+    a[k] = l;
+#pragma unroll
+    for (int c = k + 1; c < 16; ++c) {
+      const double m = x[c] * isd;
+      a[c] -= l * m;
+    }
+    if (k + 1 < 16) {
+      const double m1 = x[k + 1] * isd;
+      d = y - m1 * m1;
+    }
+  }
+  if (lane >= o) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) M[lane * kPfLd + o + c] = lane >= o + c ? a[c] : 0.0;
+    if (lane < o + 16) dinv[lane] = my_isd;
+  }
+  return bad;
+}
+
 // Diagonal block b's inverse X_bb = L_bb^-1 by one wave: lane = column j
 // (lanes 16.. repeat lanes 0..15 and store nothing), forward substitution
 // over the block's rows with L broadcast from LDS.
@@ -976,7 +1021,7 @@ __device__ __forceinline__ void pf_diag_inv16_pipe(const double* M, const double
 // off-diagonal blocks that do not need it — only X_3k = -X_33 (sum) waits for
 // it, every other block of X depends on its own wave's earlier blocks; PIPE:
 // the diagonal inverses by pf_diag_inv16_pipe.  Bitwise equal to the default.
-template <bool RSQ, bool OVL = false, bool PIPE = false>
+template <bool RSQ, bool OVL = false, bool PIPE = false, bool FP = false>
 __device__ __forceinline__ int pf_chol_inv_fast(double* M, double* X, double* scr, double* dinv, int lane, int wv,
                                                 long long* stamps = nullptr) {
   int bad = 0;
@@ -986,7 +1031,7 @@ __device__ __forceinline__ int pf_chol_inv_fast(double* M, double* X, double* sc
   for (int kb = 0; kb < 4; ++kb) {
     const int o = 16 * kb;
     if (wv == 0) {
-      const int b = pf_col16<RSQ>(M, dinv, o, lane);
+      const int b = FP ? pf_col16_fp<RSQ>(M, dinv, o, lane) : pf_col16<RSQ>(M, dinv, o, lane);
       if (bad == 0) bad = b;
       // bad lives in wave 0; every thread returns it
       if (kb == 3 && lane == 0) reinterpret_cast<int*>(scr)[4 * 16 * 17 * 2] = bad;
@@ -1366,7 +1411,8 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
     pf_acc_to_lds(dacc, T, wv, lane);
     __syncthreads();
     // factor + inverse by 16x16 blocks (Lc: pivot columns + per-wave scratch)
-    const int bad = FV == 3   ? pf_chol_inv_fast<true, true, true>(T, Li, Lc, dinv, lane, wv)
+    const int bad = FV == 6   ? pf_chol_inv_fast<true, true, true, true>(T, Li, Lc, dinv, lane, wv)
+                    : FV == 3 ? pf_chol_inv_fast<true, true, true>(T, Li, Lc, dinv, lane, wv)
                     : FV == 4 ? pf_chol_inv_fast<true, true, false>(T, Li, Lc, dinv, lane, wv)
                     : FV == 5 ? pf_chol_inv_fast<true, false, true>(T, Li, Lc, dinv, lane, wv)
                     : FV == 2 ? pf_chol_inv_fast<true>(T, Li, Lc, dinv, lane, wv)
@@ -1594,7 +1640,8 @@ rocblas_status panel_factor_fused(hipStream_t s, int n, double* A, int lda, int 
 #ifdef MI_BA_AB_VARIANTS
   auto pick = [&](auto wm) {
     constexpr int W = decltype(wm)::value;
-    return ws->tile_factor == 3   ? panel_factor_kernel<3, true, W>
+    return ws->tile_factor == 6   ? panel_factor_kernel<6, true, W>
+           : ws->tile_factor == 3 ? panel_factor_kernel<3, true, W>
            : ws->tile_factor == 4 ? panel_factor_kernel<4, true, W>
            : ws->tile_factor == 5 ? panel_factor_kernel<5, true, W>
            : ws->tile_factor == 2 ? (ws->write_through ? panel_factor_kernel<2, true, W> : panel_factor_kernel<2, false, W>)

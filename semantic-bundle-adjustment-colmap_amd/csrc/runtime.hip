@@ -2487,7 +2487,7 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.batch_tile = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_tile_factor") == 0 && value >= 1 && value <= 5 && ab_value(value, CholConfig{}.tile_factor)) {
+  if (std::strcmp(key, "cholesky_tile_factor") == 0 && value >= 1 && value <= 6 && ab_value(value, CholConfig{}.tile_factor)) {
     ctx->chol.tile_factor = value;
     return MI_BA_OK;
   }

@@ -243,7 +243,7 @@ def test_lm_tile_factor_and_publish(gpu):
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
     res = []
-    for tf in (2, 1, 3, 4, 5):
+    for tf in (2, 1, 3, 4, 5, 6):
         for wt in ((1, 0) if tf <= 2 else (1,)):
             with mi_ba.Context(opts, sc.copy()) as ctx:
                 ctx.set_tuning("cholesky_tile_factor", tf)

@@ -59,7 +59,8 @@ int main(int argc, char** argv) {
     hipEventRecord(e0, ws.side);
     auto pick = [&](auto wm) {
       constexpr int W = decltype(wm)::value;
-      return fv == 3   ? panel_factor_kernel<3, true, W>
+      return fv == 6   ? panel_factor_kernel<6, true, W>
+             : fv == 3 ? panel_factor_kernel<3, true, W>
              : fv == 4 ? panel_factor_kernel<4, true, W>
              : fv == 5 ? panel_factor_kernel<5, true, W>
              : fv == 2 ? (wt ? panel_factor_kernel<2, true, W> : panel_factor_kernel<2, false, W>)
@@ -69,7 +70,7 @@ int main(int argc, char** argv) {
                 : ow == 2 ? pick(std::integral_constant<int, 2>{})
                 : ow == 1 ? pick(std::integral_constant<int, 1>{}) : pick(std::integral_constant<int, 0>{});
     hipLaunchKernelGGL(kern, dim3(nr), dim3(256), 0, ws.side, A, n, kb, n, info, ws.pf_linv, ws.pf_ctrl, ws.pf_base, epoch,
-                       ws.err, ws.spin_limit, 0, dbg);
+                       ws.err, ws.spin_limit, 0, dbg, 0, nullptr);
     hipEventRecord(e1, ws.side);
     hipEventSynchronize(e1);
     if (busy) {

@@ -53,6 +53,7 @@ __global__ __launch_bounds__(256) void tile_probe_kernel(double* __restrict__ A,
                     : V == 3 ? pf_chol_inv_fast<true, true, true>(T, Li, Lc, dinv, lane, wv, sp)
                     : V == 4 ? pf_chol_inv_fast<true, true, false>(T, Li, Lc, dinv, lane, wv, sp)
                     : V == 5 ? pf_chol_inv_fast<true, false, true>(T, Li, Lc, dinv, lane, wv, sp)
+                    : V == 6 ? pf_chol_inv_fast<true, true, true, true>(T, Li, Lc, dinv, lane, wv, sp)
                              : pf_chol_inv_fast<true>(T, Li, Lc, dinv, lane, wv, sp);
     __syncthreads();
     if (rep == kReps - 1 && blockIdx.x == 0)
@@ -158,16 +159,16 @@ int main() {
   hipMalloc(&out, 8ull * 2 * 4096 * 64);
   hipMalloc(&st, 8ull * kReps * kPhases * 2 + 8ull * kReps * 10);
   double* res;
-  hipMalloc(&res, 8ull * 6 * 2 * 4096);
+  hipMalloc(&res, 8ull * 7 * 2 * 4096);
   hipMemcpy(A, h.data(), 8ull * n * n, hipMemcpyHostToDevice);
   const char* names[kPhases] = {"load tile -> LDS", "chol+inv", "gemm LDS operands",
                                 "gemm global operands", "publish 32KB plain + threadfence",
                                 "publish 32KB sc1 + vmcnt", "stage 32KB global -> LDS",
                                 "stage 32KB 16B loads in flight", "gemm global operands, cold tiles",
                                 "stage 2 cold tiles (16B) + LDS gemm"};
-  const char* vname[6] = {"", "pf_chol_inv_fast<sqrt>", "pf_chol_inv_fast<rsq>", "pf_chol_inv_fast<rsq, ovl, pipe>",
-                          "pf_chol_inv_fast<rsq, ovl>", "pf_chol_inv_fast<rsq, pipe>"};
-  for (int cfg = 2; cfg < 12; ++cfg) {
+  const char* vname[7] = {"", "pf_chol_inv_fast<sqrt>", "pf_chol_inv_fast<rsq>", "pf_chol_inv_fast<rsq, ovl, pipe>",
+                          "pf_chol_inv_fast<rsq, ovl>", "pf_chol_inv_fast<rsq, pipe>", "pf_chol_inv_fast<rsq, ovl, pipe, fast pivots>"};
+  for (int cfg = 2; cfg < 14; ++cfg) {
     const int grid = cfg & 1 ? 8 : 1, V = cfg >> 1;
     double* rv = res + (size_t)V * 8192;
     if (V == 1)
@@ -178,8 +179,10 @@ int main() {
       hipLaunchKernelGGL(tile_probe_kernel<3>, dim3(grid), dim3(256), 0, 0, A, n, out, st, rv);
     else if (V == 4)
       hipLaunchKernelGGL(tile_probe_kernel<4>, dim3(grid), dim3(256), 0, 0, A, n, out, st, rv);
-    else
+    else if (V == 5)
       hipLaunchKernelGGL(tile_probe_kernel<5>, dim3(grid), dim3(256), 0, 0, A, n, out, st, rv);
+    else
+      hipLaunchKernelGGL(tile_probe_kernel<6>, dim3(grid), dim3(256), 0, 0, A, n, out, st, rv);
     hipDeviceSynchronize();
     std::vector<unsigned long long> s((size_t)kReps * kPhases * 2);
     hipMemcpy(s.data(), st, 8 * s.size(), hipMemcpyDeviceToHost);
@@ -205,7 +208,7 @@ int main() {
     }
   }
   // L and X of both variants vs a host Cholesky of the same tile
-  std::vector<double> r(12 * 4096);
+  std::vector<double> r(14 * 4096);
   hipMemcpy(r.data(), res, 8ull * r.size(), hipMemcpyDeviceToHost);
   std::vector<double> L(4096, 0.0);
   for (int j = 0; j < 64; ++j) {
@@ -218,7 +221,7 @@ int main() {
       L[i * 64 + j] = v / L[j * 64 + j];
     }
   }
-  for (int V = 3; V < 6; ++V) {  // the tools-build variants against rsq (same operations: bitwise)
+  for (int V = 3; V < 7; ++V) {  // the tools-build variants against rsq (same operations: bitwise)
     bool same = true;
     for (int i = 0; i < 64; ++i)
       for (int j = 0; j < 64; ++j) {
@@ -227,7 +230,7 @@ int main() {
       }
     printf("variant %d: L and X bitwise equal to variant 2: %s\n", V, same ? "yes" : "NO");
   }
-  for (int V = 1; V < 6; ++V) {
+  for (int V = 1; V < 7; ++V) {
     double el = 0.0, ex = 0.0;
     for (int i = 0; i < 64; ++i)
       for (int j = 0; j < 64; ++j) {
