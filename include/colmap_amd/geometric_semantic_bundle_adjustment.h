@@ -135,16 +135,21 @@ class GeometricSemanticBundleAdjuster {
     internal::Flat flat;
     flat.Build(*reconstruction, config_);
     // trunk masks of the config images (ReadDepthAndSemanticMaps, :1298-1336)
+    // each on its own map's size (the IoU is rasterised on that size,
+    // :1530-1531), planes back to back (ABI 4)
     const SemanticMaps maps = LoadSemanticMaps(options_.data_path, *reconstruction, config_);
-    const size_t plane = (size_t)maps.height * maps.width;
-    std::vector<uint8_t> masks(plane * flat.img_ids.size(), 0);
+    std::vector<int32_t> mask_h(flat.img_ids.size(), 0), mask_w(flat.img_ids.size(), 0);
+    std::vector<uint8_t> masks;
     for (size_t i = 0; i < flat.img_ids.size(); ++i) {
       const Image& im = reconstruction->GetImage(flat.img_ids[i]);
       auto it = maps.semantic.find(im.name);
       if (it == maps.semantic.end()) continue;  // not a config image
-      for (size_t k = 0; k < plane; ++k)
-        masks[i * plane + k] = (double)it->second[k] == options_.trunk_semantic_class ? 1 : 0;
+      const std::pair<int, int> hw = maps.Size(im.name);
+      mask_h[i] = hw.first;
+      mask_w[i] = hw.second;
+      for (const float v : it->second) masks.push_back((double)v == options_.trunk_semantic_class ? 1 : 0);
     }
+    if (masks.empty()) masks.push_back(0);  // a non-null plane pointer
     std::vector<mi_ba_cylinder> cyl(cylinders->size());
     for (size_t c = 0; c < cyl.size(); ++c) {
       const Cylinder& y = (*cylinders)[c];
@@ -155,8 +160,8 @@ class GeometricSemanticBundleAdjuster {
     }
     mi_ba_gsba g;
     mi_ba_default_gsba(&g);
-    g.height = maps.height;
-    g.width = maps.width;
+    g.image_height = mask_h.data();
+    g.image_width = mask_w.data();
     g.trunk_mask = masks.data();
     g.num_cylinders = (int32_t)cyl.size();
     g.cylinders = cyl.data();

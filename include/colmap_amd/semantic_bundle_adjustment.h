@@ -14,8 +14,11 @@
 // form is kept, next to an overload taking the maps in memory.
 #pragma once
 
+#include <algorithm>
 #include <cstdio>
 #include <exception>
+#include <iomanip>
+#include <iostream>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -55,6 +58,13 @@ struct SemanticBundleAdjustmentOptions : BundleAdjustmentOptions {
   int error_computation_pixel_step = 10;
   double numeric_relative_step_size = 1e-3;
   double semantic_weight = 1.0;  // build addition (ScaledLoss weight)
+  // Build extension, off by default: the reference accepts SIMPLE_PINHOLE
+  // cameras only and throws std::runtime_error for any other model
+  // (SemanticBundleAdjuster::Assert, semantic_bundle_adjustment.cc:619-631),
+  // as Solve does here unless this is set; with it, PINHOLE, SIMPLE_RADIAL,
+  // RADIAL and OPENCV cameras take the same residual through their own
+  // ImageToWorld / WorldToImage.
+  bool allow_any_camera_model = false;
   SemanticBundleAdjustmentOptions() {
     solver_options.function_tolerance = 1e-8;
     solver_options.gradient_tolerance = 1e-8;
@@ -69,18 +79,58 @@ struct SemanticBundleAdjustmentOptions : BundleAdjustmentOptions {
 };
 typedef BundleAdjustmentConfig SemanticBundleAdjustmentConfig;
 
-// Depth / semantic maps per image name: row-major H x W float32 (the
+// Depth / semantic maps per image name: row-major float32 (the
 // matrixFromTiff matrices after their vertical flip, matrix_vis.h:130-176).
+// Each image's two maps share one size: sizes[name] = (rows, cols), or, for
+// an image without an entry, height x width.  Images may differ in size, as
+// in the reference (image 1 sampled on its own grid, the reprojected pixel
+// bounds-checked against image 2's own size: semantic_bundle_adjustment.cc:
+// 792-799, semantic_cost_functions.h:163).
 struct SemanticMaps {
   int height = 0, width = 0;
+  std::unordered_map<std::string, std::pair<int, int>> sizes;
   std::unordered_map<std::string, std::vector<float>> depth, semantic;
+  std::pair<int, int> Size(const std::string& name) const {
+    auto it = sizes.find(name);
+    return it == sizes.end() ? std::make_pair(height, width) : it->second;
+  }
 };
+
+// PrintSemanticSolverSummary (semantic_bundle_adjustment.cc:546-598): the raw
+// costs (not RMS pixels as PrintSolverSummary), labels right-aligned in 16
+// columns, costs with precision 6.
+inline void PrintSemanticSolverSummary(const SolverSummary& s, std::ostream& out = std::cout) {
+  const char* term = s.termination_type == SolverSummary::CONVERGENCE      ? "Convergence"
+                     : s.termination_type == SolverSummary::NO_CONVERGENCE ? "No convergence"
+                     : s.termination_type == SolverSummary::FAILURE        ? "Failure"
+                     : s.termination_type == SolverSummary::USER_SUCCESS   ? "User success"
+                     : s.termination_type == SolverSummary::USER_FAILURE   ? "User failure"
+                                                                           : "Unknown";
+  out << std::right << std::setw(16) << "Residuals : " << std::left << s.num_residuals_reduced << std::endl;
+  out << std::right << std::setw(16) << "Parameters : " << std::left << s.num_effective_parameters_reduced
+      << std::endl;
+  out << std::right << std::setw(16) << "Iterations : " << std::left
+      << s.num_successful_steps + s.num_unsuccessful_steps << std::endl;
+  out << std::right << std::setw(16) << "Time : " << std::left << s.total_time_in_seconds << " [s]" << std::endl;
+  out << std::right << std::setw(16) << "Initial cost : " << std::right << std::setprecision(6) << s.initial_cost
+      << " " << std::endl;
+  out << std::right << std::setw(16) << "Final cost : " << std::right << std::setprecision(6) << s.final_cost << " "
+      << std::endl;
+  out << std::right << std::setw(16) << "Termination : " << std::right << term << std::endl;
+  out << std::endl;
+}
+
+// PrintHeading2 (util/misc.cc:197-200)
+inline void PrintHeading2(const std::string& heading, std::ostream& out = std::cout) {
+  out << std::endl << heading << std::endl;
+  out << std::string(std::min<size_t>(heading.size(), 78), '-') << std::endl;
+}
 
 // SemanticBundleAdjuster::ReadDepthAndSemanticMaps (semantic_bundle_adjustment.cc:
 // 1021-1068): <data_path>/depth_tiff/<stem>_depth.tiff and
 // <data_path>/semantic_tiff/<stem>_semantic.tiff of every config image, stem
-// = the image name up to its last '.'.  Every map must have one size (the
-// semantic term samples one H x W grid, mi_ba_semantic).
+// = the image name up to its last '.'.  Each image keeps its maps' own size;
+// an image's depth and semantic maps must agree (std::invalid_argument).
 inline SemanticMaps LoadSemanticMaps(const std::string& data_path, const Reconstruction& reconstruction,
                                      const BundleAdjustmentConfig& config) {
   SemanticMaps maps;
@@ -99,15 +149,66 @@ inline SemanticMaps LoadSemanticMaps(const std::string& data_path, const Reconst
     int h0, w0, h1, w1;
     std::vector<float> d = MatrixFromTiff(depth_path, &h0, &w0);
     std::vector<float> l = MatrixFromTiff(semantic_path, &h1, &w1);
-    if (h0 != h1 || w0 != w1 || (maps.height && (h0 != maps.height || w0 != maps.width)))
-      throw std::invalid_argument("depth / semantic maps of different sizes");
-    maps.height = h0;
-    maps.width = w0;
+    if (h0 != h1 || w0 != w1)
+      throw std::invalid_argument("the depth and semantic maps of '" + name + "' differ in size");
+    maps.sizes[name] = std::make_pair(h0, w0);
     maps.depth[name] = std::move(d);
     maps.semantic[name] = std::move(l);
   }
   return maps;
 }
+
+namespace internal {
+// The semantic term of a flattened reconstruction (SemanticBundleAdjuster::
+// SetUp, semantic_bundle_adjustment.cc:646-668): every image's maps on their
+// own size, planes back to back in flat image order (ABI 4; an image without
+// maps, outside the config, gets an empty plane), and every ordered pair of
+// config images (:656-661).  `sem` points into the owned vectors.
+struct SemanticInputs {
+  std::vector<int32_t> img_h, img_w, pairs;
+  std::vector<float> depth, label;
+  mi_ba_semantic sem{};
+
+  void Build(const Flat& flat, const Reconstruction& rec, const BundleAdjustmentConfig& config,
+             const SemanticMaps& maps, const SemanticBundleAdjustmentOptions& options) {
+    img_h.assign(flat.img_ids.size(), 0);
+    img_w.assign(flat.img_ids.size(), 0);
+    for (size_t i = 0; i < flat.img_ids.size(); ++i) {
+      const Image& im = rec.GetImage(flat.img_ids[i]);
+      auto d = maps.depth.find(im.name), l = maps.semantic.find(im.name);
+      if (d == maps.depth.end() || l == maps.semantic.end()) {
+        if (config.HasImage(im.image_id)) throw std::runtime_error("missing depth/semantic map for " + im.name);
+        continue;
+      }
+      const std::pair<int, int> hw = maps.Size(im.name);
+      if (hw.first <= 0 || hw.second <= 0 || d->second.size() != (size_t)hw.first * hw.second ||
+          l->second.size() != d->second.size())
+        throw std::invalid_argument("the depth / semantic maps of '" + im.name + "' do not match their size");
+      img_h[i] = hw.first;
+      img_w[i] = hw.second;
+      depth.insert(depth.end(), d->second.begin(), d->second.end());
+      label.insert(label.end(), l->second.begin(), l->second.end());
+    }
+    for (size_t i = 0; i < flat.img_ids.size(); ++i)
+      for (size_t j = 0; j < flat.img_ids.size(); ++j)
+        if (flat.img_cfg[i] && flat.img_cfg[j]) {
+          pairs.push_back((int32_t)i);
+          pairs.push_back((int32_t)j);
+        }
+    static const float kNoMaps = 0.f;  // no image with maps: the library still takes a non-null plane pointer
+    sem = mi_ba_semantic{};
+    sem.image_height = img_h.data();
+    sem.image_width = img_w.data();
+    sem.depth = depth.empty() ? &kNoMaps : depth.data();
+    sem.label = label.empty() ? &kNoMaps : label.data();
+    sem.num_pairs = (int32_t)(pairs.size() / 2);
+    sem.pairs = pairs.data();
+    sem.pixel_step = options.error_computation_pixel_step;
+    sem.depth_error_threshold = options.depth_error_threshold;
+    sem.numeric_relative_step_size = options.numeric_relative_step_size;
+  }
+};
+}  // namespace internal
 
 class SemanticBundleAdjuster {
  public:
@@ -128,13 +229,22 @@ class SemanticBundleAdjuster {
     if (!reconstruction) throw std::invalid_argument("reconstruction is null");
     if (used_) throw std::logic_error("Cannot use the same BundleAdjuster multiple times");
     used_ = true;
-    // SemanticBundleAdjuster::Assert (semantic_bundle_adjustment.cc:604-644)
-    if (!options_.refine_extrinsics) throw std::runtime_error("the argument 'refine_extrinsics' must be set to true.");
+    // SemanticBundleAdjuster::Assert (semantic_bundle_adjustment.cc:604-644),
+    // in its order and with its messages
     for (const image_t id : config_.Images()) {
       const Image& im = reconstruction->GetImage(id);
       if (!config_.IsConstantCamera(im.camera_id))
-        throw std::runtime_error("camera intrinsics of image '" + im.name + "' are not set to constant.");
+        throw std::runtime_error("ERROR: camera intrinsics of image '" + im.name +
+                                 "' are not set to constant. This is not supported.");
     }
+    if (!options_.allow_any_camera_model)
+      for (const image_t id : config_.Images()) {
+        const Image& im = reconstruction->GetImage(id);
+        if (reconstruction->GetCamera(im.camera_id).model_id != MI_BA_SIMPLE_PINHOLE)
+          throw std::runtime_error("ERROR: the only supported camera model is SimplePinholeCameraModel.");
+      }
+    if (!options_.refine_extrinsics)
+      throw std::runtime_error("ERROR: the argument 'refine_extrinsics' must be set to true.");
     // SetUp -> ReadDepthAndSemanticMaps (:1021-1068)
     if (!have_maps_) {
       maps_ = LoadSemanticMaps(options_.data_path, *reconstruction, config_);
@@ -144,39 +254,12 @@ class SemanticBundleAdjuster {
     flat.Build(*reconstruction, config_);
     // The pose-only semantic problem: no reprojection blocks.
     flat.problem.num_obs = 0;
-    const int H = maps_.height, W = maps_.width;
-    const size_t plane = (size_t)H * W;
-    std::vector<float> depth(plane * flat.img_ids.size(), 0.f), label(plane * flat.img_ids.size(), 0.f);
-    std::vector<int32_t> pairs;
-    for (size_t i = 0; i < flat.img_ids.size(); ++i) {
-      const Image& im = reconstruction->GetImage(flat.img_ids[i]);
-      auto d = maps_.depth.find(im.name), l = maps_.semantic.find(im.name);
-      if (d == maps_.depth.end() || l == maps_.semantic.end()) {
-        if (config_.HasImage(im.image_id)) throw std::runtime_error("missing depth/semantic map for " + im.name);
-        continue;
-      }
-      std::copy(d->second.begin(), d->second.end(), depth.begin() + i * plane);
-      std::copy(l->second.begin(), l->second.end(), label.begin() + i * plane);
-    }
-    // every ordered pair of config images (SetUp, semantic_bundle_adjustment.cc:656-661)
-    for (size_t i = 0; i < flat.img_ids.size(); ++i)
-      for (size_t j = 0; j < flat.img_ids.size(); ++j)
-        if (flat.img_cfg[i] && flat.img_cfg[j]) {
-          pairs.push_back((int32_t)i);
-          pairs.push_back((int32_t)j);
-        }
-    mi_ba_semantic sem;
-    sem.height = H;
-    sem.width = W;
-    sem.depth = depth.data();
-    sem.label = label.data();
-    sem.num_pairs = (int32_t)(pairs.size() / 2);
-    sem.pairs = pairs.data();
-    sem.pixel_step = options_.error_computation_pixel_step;
-    sem.depth_error_threshold = options_.depth_error_threshold;
-    sem.numeric_relative_step_size = options_.numeric_relative_step_size;
+    internal::SemanticInputs in;
+    in.Build(flat, *reconstruction, config_, maps_, options_);
+    const mi_ba_semantic& sem = in.sem;
     mi_ba_options o = internal::ToOptions(options_);
     o.semantic_weight = options_.semantic_weight;
+    o.print_summary = 0;  // the SBA prints its own report (PrintSemanticSolverSummary, below)
     // the per-iteration snapshot writer runs after the caller's callbacks
     // (Solve pushes the SBACallbackFunctor last, semantic_bundle_adjustment.cc:519-520)
     const std::string steps = options_.ResolvedVisualizationPath();
@@ -219,6 +302,10 @@ class SemanticBundleAdjuster {
     if (st == MI_BA_ERR_NO_RESIDUALS) return false;
     internal::ThrowStatus(st, "SemanticBundleAdjuster::Solve");
     summary_ = internal::ToSummary(s);
+    if (options_.print_summary) {  // :526-529
+      PrintHeading2("Semantic Bundle Adjustment Report");
+      PrintSemanticSolverSummary(summary_);
+    }
     flat.WriteBack(reconstruction);
     if (!options_.output_path.empty()) {  // :531-538
       internal::MakeDirs(options_.output_path + "/text");

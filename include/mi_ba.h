@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define MI_BA_ABI_VERSION 3
+#define MI_BA_ABI_VERSION 4
 
 typedef enum mi_ba_status {
   MI_BA_OK = 0,
@@ -204,19 +204,30 @@ typedef struct mi_ba_problem {
   const int32_t* camera_model_ids;   /* nullable; [num_cameras] MI_BA_* model id per camera (ABI 2) */
 } mi_ba_problem;
 
-/* Semantic term (SBA).  Rasters are row-major [image][H][W] float32, i.e. the
+/* Semantic term (SBA).  Rasters are row-major float32, i.e. the
  * Eigen::MatrixXf (row=y, col=x) of matrixFromTiff after its vertical flip
- * (matrix_vis.h:130-176); every image shares H and W. */
+ * (matrix_vis.h:130-176).  An image's depth and semantic maps share one size.
+ * Sizes (ABI 4): with image_height / image_width NULL every image is
+ * height x width and depth / label are [num_images][height][width]; else
+ * image i is image_height[i] x image_width[i] (height / width are ignored)
+ * and depth / label hold the images' planes back to back in image order
+ * (plane i starts at sum_{k<i} H_k W_k).  As the reference
+ * (semantic_bundle_adjustment.cc:792-799, semantic_cost_functions.h:163),
+ * image i of a pair is sampled on its own H_i x W_i grid and the reprojected
+ * pixel is bounds-checked against image j's own H_j x W_j.  Every image of a
+ * pair needs H, W > 0 (MI_BA_ERR_INVALID_ARGUMENT otherwise). */
 typedef struct mi_ba_semantic {
   int32_t height;
   int32_t width;
-  const float* depth;                /* [num_images][H][W] */
-  const float* label;                /* [num_images][H][W] */
+  const float* depth;                /* image planes, see above */
+  const float* label;                /* image planes, see above */
   int32_t num_pairs;                 /* ordered pairs (i, j); reference uses all i != j */
   const int32_t* pairs;              /* [num_pairs][2] */
   int32_t pixel_step;                /* error_computation_pixel_step, default 10 */
   double depth_error_threshold;      /* default 2 */
   double numeric_relative_step_size; /* default 1e-3 */
+  const int32_t* image_height;       /* nullable [num_images] (ABI 4) */
+  const int32_t* image_width;        /* nullable [num_images] (ABI 4) */
 } mi_ba_semantic;
 
 /* Geometric-semantic BA (GSBA): one cylinder IoU residual per (config image,
@@ -248,10 +259,11 @@ typedef struct mi_ba_cylinder {
 enum { MI_BA_CYLINDER_DEFAULT = 0, MI_BA_CYLINDER_BY_2_POINTS = 1 };
 
 typedef struct mi_ba_gsba {
-  int32_t height;                    /* trunk mask size, every image */
+  int32_t height;                    /* trunk mask size of every image (image_height NULL) */
   int32_t width;
-  const uint8_t* trunk_mask;         /* [num_images][H][W] row-major, 1 where the semantic map
-                                        == trunk_semantic_class (:1328-1333), images in problem order */
+  const uint8_t* trunk_mask;         /* row-major, 1 where the semantic map == trunk_semantic_class
+                                        (:1328-1333), images in problem order: [num_images][H][W], or
+                                        with image_height / image_width the planes back to back */
   int32_t num_cylinders;
   mi_ba_cylinder* cylinders;         /* (in/out) */
   int32_t refine_geometry;           /* default 1 */
@@ -259,6 +271,12 @@ typedef struct mi_ba_gsba {
   int32_t include_landmark_error;    /* default 0: the problem's observations are not used */
   double landmark_error_weight;      /* default 1: reprojection blocks get ScaledLoss(w / #config 2D features) */
   int32_t cylinder_parametrization;  /* MI_BA_CYLINDER_*, default MI_BA_CYLINDER_DEFAULT (ABI 3) */
+  /* nullable [num_images] per-image mask sizes (ABI 4): each image's IoU is
+   * rasterised on its own semantic map's size (Cylinder::ComputeSemanticIoU
+   * takes the map's rows / cols, cylinder.h:496-504;
+   * geometric_semantic_bundle_adjustment.cc:1530-1531) */
+  const int32_t* image_height;
+  const int32_t* image_width;
 } mi_ba_gsba;
 
 /* Mirrors the ceres::Solver::Summary fields COLMAP reads

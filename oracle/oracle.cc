@@ -318,16 +318,43 @@ struct SemSample {
   float label1;
 };
 
+// One image's depth / semantic map (the depth_maps_ / semantic_maps_ entry,
+// semantic_bundle_adjustment.cc:1021-1068): its own rows x cols.
+struct SemRaster {
+  const float* depth;
+  const float* label;
+  int H, W;
+};
+
+// Every image's raster (mi_ba_semantic: one size for all, or per-image sizes
+// with the planes back to back in image order).
+struct SemPlanes {
+  std::vector<SemRaster> img;
+  void build(const mi_ba_semantic* sem, int I) {
+    img.assign(I, SemRaster{nullptr, nullptr, 0, 0});
+    int64_t off = 0;
+    for (int i = 0; i < I; ++i) {
+      const int H = sem->image_height ? sem->image_height[i] : sem->height;
+      const int W = sem->image_width ? sem->image_width[i] : sem->width;
+      img[i] = SemRaster{sem->depth + off, sem->label + off, H, W};
+      off += (int64_t)H * W;
+    }
+  }
+};
+
 struct SemSetup {
   std::vector<SemSample> samples;
   std::vector<uint8_t> pair_var1, pair_var2;  // pose i / pose j variable
+  SemPlanes planes;
 };
 
 // semantic_bundle_adjustment.cc:699-906 (AddImagePairToProblem): pixel grid
-// y outer, x inner, step s, skip depth < 1e-4, skip both-constant pairs.
+// of image 1's own size (:792-799), y outer, x inner, step s, skip depth <
+// 1e-4, skip both-constant pairs.
 void BuildSemSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& s,
                    const mi_ba_semantic* sem, SemSetup* ss) {
-  const int H = sem->height, W = sem->width, step = sem->pixel_step;
+  const int step = sem->pixel_step;
+  ss->planes.build(sem, p->num_images);
   ss->pair_var1.assign(sem->num_pairs, 0);
   ss->pair_var2.assign(sem->num_pairs, 0);
   for (int k = 0; k < sem->num_pairs; ++k) {
@@ -340,8 +367,10 @@ void BuildSemSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& 
     ss->pair_var2[k] = !c2;
     const int cam1 = p->image_camera[i];
     const double* K1 = &p->camera_params[s.cam_poff[cam1]];
-    const float* depth1 = sem->depth + (int64_t)i * H * W;
-    const float* label1 = sem->label + (int64_t)i * H * W;
+    const SemRaster& r1 = ss->planes.img[i];
+    const int H = r1.H, W = r1.W;
+    const float* depth1 = r1.depth;
+    const float* label1 = r1.label;
     for (int y = 0; y < H; y += step) {
       for (int x = 0; x < W; x += step) {
         const float depth = depth1[(int64_t)y * W + x];
@@ -360,21 +389,23 @@ void BuildSemSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& 
   }
 }
 
-// compute_semantic_error (semantic_cost_functions.h:87-208) against image j;
-// pw_out / pxy_out (nullable): return_point3D / return_point2D_2.
-double SemanticErrorTo(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, int j, const SemSample& smp,
-                       const double q1[4], const double t1[3], const double q2[4], const double t2[3], int* status,
-                       double* pw_out = nullptr, int* pxy_out = nullptr);
+// compute_semantic_error (semantic_cost_functions.h:87-208) against image j
+// (raster r2 = image j's maps); pw_out / pxy_out (nullable): return_point3D /
+// return_point2D_2.
+double SemanticErrorTo(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, int j, const SemRaster& r2,
+                       const SemSample& smp, const double q1[4], const double t1[3], const double q2[4],
+                       const double t2[3], int* status, double* pw_out = nullptr, int* pxy_out = nullptr);
 
-double SemanticError(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, const SemSample& smp,
-                     const double q1[4], const double t1[3], const double q2[4], const double t2[3],
-                     int* status) {
-  return SemanticErrorTo(p, s, sem, sem->pairs[2 * smp.pair + 1], smp, q1, t1, q2, t2, status);
+double SemanticError(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, const SemSetup& ss,
+                     const SemSample& smp, const double q1[4], const double t1[3], const double q2[4],
+                     const double t2[3], int* status) {
+  const int j = sem->pairs[2 * smp.pair + 1];
+  return SemanticErrorTo(p, s, sem, j, ss.planes.img[j], smp, q1, t1, q2, t2, status);
 }
 
-double SemanticErrorTo(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, int j, const SemSample& smp,
-                       const double q1[4], const double t1[3], const double q2[4], const double t2[3], int* status,
-                       double* pw_out, int* pxy_out) {
+double SemanticErrorTo(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, int j, const SemRaster& r2,
+                       const SemSample& smp, const double q1[4], const double t1[3], const double q2[4],
+                       const double t2[3], int* status, double* pw_out, int* pxy_out) {
   const int cam2 = p->image_camera[j];
   const double* K2 = &p->camera_params[s.cam_poff[cam2]];
   double q1i[4], t1i[3];
@@ -387,7 +418,7 @@ double SemanticErrorTo(const mi_ba_problem* p, const Setup& s, const mi_ba_seman
   const double u2 = pc2[0] / pc2[2];                   // :141-144
   const double v2 = pc2[1] / pc2[2];
   const double measured_depth_2 = pc2[2];
-  double x2, y2;
+  double x2 = 0.0, y2 = 0.0;
   WorldToImage(s.cam_model[cam2], K2, u2, v2, &x2, &y2); // :149-151
   const int px = CastToIntX86(std::round(x2));         // :154-156
   const int py = CastToIntX86(std::round(y2));
@@ -395,19 +426,19 @@ double SemanticErrorTo(const mi_ba_problem* p, const Setup& s, const mi_ba_seman
     pxy_out[0] = px;
     pxy_out[1] = py;
   }
-  const int H = sem->height, W = sem->width;
+  const int H = r2.H, W = r2.W;                        // depth_map_2_ rows / cols (:163)
   if (px < 0 || px >= W || py < 0 || py >= H) {        // :163-177
     *status = MI_BA_OUT_OF_BOUNDS;
     return 0.0;
   }
-  const int64_t off = (int64_t)j * H * W + (int64_t)py * W + px;
-  const double depth_2 = (double)sem->depth[off];
+  const int64_t off = (int64_t)py * W + px;
+  const double depth_2 = (double)r2.depth[off];
   if (std::fabs(depth_2 - measured_depth_2) > sem->depth_error_threshold) {  // :180-196
     *status = MI_BA_INVALID_DEPTH;
     return 0.0;
   }
   *status = MI_BA_VALID;                               // :199-205
-  return (smp.label1 == sem->label[off]) ? 0.0 : 1.0;
+  return (smp.label1 == r2.label[off]) ? 0.0 : 1.0;
 }
 
 // Ceres 2.1 NumericDiffCostFunction<..., CENTRAL, 1, 4,3[,4,3]> (restated):
@@ -424,7 +455,7 @@ void EvalSemantic(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* 
   for (int m = 0; m < 4; ++m) x[7 + m] = p->qvec[j * 4 + m];
   for (int m = 0; m < 3; ++m) x[11 + m] = p->tvec[j * 3 + m];
   int st;
-  *r = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], status);
+  *r = SemanticError(p, s, sem, ss, smp, &x[0], &x[4], &x[7], &x[11], status);
   double Jamb[14] = {0};
   const bool var[2] = {ss.pair_var1[smp.pair] != 0, ss.pair_var2[smp.pair] != 0};
   const double min_step = std::sqrt(std::numeric_limits<double>::epsilon());
@@ -435,9 +466,9 @@ void EvalSemantic(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* 
       const double orig = x[idx];
       const double delta = std::max(min_step, std::fabs(orig) * sem->numeric_relative_step_size);
       x[idx] = orig + delta;
-      const double fp = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], &st);
+      const double fp = SemanticError(p, s, sem, ss, smp, &x[0], &x[4], &x[7], &x[11], &st);
       x[idx] = orig - delta;
-      const double fm = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], &st);
+      const double fm = SemanticError(p, s, sem, ss, smp, &x[0], &x[4], &x[7], &x[11], &st);
       x[idx] = orig;
       double one_over_delta = 1.0 / delta;
       one_over_delta /= 2;
@@ -555,7 +586,7 @@ double FlatSecondDerivativeBound(int model, const double* K, double rho) {
   return 0.0;
 }
 
-bool FlatClears(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, const SemSample& smp,
+bool FlatClears(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* sem, const SemSetup& ss, const SemSample& smp,
                 const FlatBounds& B, bool var1, bool var2, double r_centre) {
   const int i = sem->pairs[2 * smp.pair], j = sem->pairs[2 * smp.pair + 1];
   const double* q1 = &p->qvec[i * 4];
@@ -652,16 +683,17 @@ bool FlatClears(const mi_ba_problem* p, const Setup& s, const mi_ba_semantic* se
   const int x0 = (int)std::round(x - bx), y0 = (int)std::round(y - by);
   const int ncol = (int)std::round(x + bx) - x0 + 1, nrow = (int)std::round(y + by) - y0 + 1;
   if (ncol > 3 || nrow > 3) return false;
-  const int H_ = sem->height, W_ = sem->width;
+  const SemRaster& r2 = ss.planes.img[j];
+  const int H_ = r2.H, W_ = r2.W;
   for (int py = y0; py < y0 + nrow; ++py)
     for (int px = x0; px < x0 + ncol; ++px) {
       double f = 0.0;
       if (px >= 0 && px < W_ && py >= 0 && py < H_) {
-        const int64_t off = (int64_t)j * H_ * W_ + (int64_t)py * W_ + px;
-        const double sd = (double)sem->depth[off];
+        const int64_t off = (int64_t)py * W_ + px;
+        const double sd = (double)r2.depth[off];
         const double dz = std::fabs(sd - z) - sem->depth_error_threshold;
         if (!(std::fabs(dz) > az + 1e-9 * (1.0 + std::fabs(sd) + mag))) return false;
-        f = dz > 0.0 ? 0.0 : (smp.label1 == sem->label[off] ? 0.0 : 1.0);
+        f = dz > 0.0 ? 0.0 : (smp.label1 == r2.label[off] ? 0.0 : 1.0);
       }
       if (f != r_centre) return false;
     }
@@ -682,6 +714,8 @@ struct GsbaSetup {
   const mi_ba_gsba* g = nullptr;
   std::vector<GsbaBlock> blocks;
   std::vector<int64_t> sem_total;  // per image: count of the trunk mask
+  std::vector<int64_t> mask_off;   // per image: its trunk mask plane (own size, image_height / image_width)
+  std::vector<int> mask_h, mask_w;
   double weight = 1.0;             // ScaledLoss(1 / #config images), :721-722
   bool by2 = false;                // MI_BA_CYLINDER_BY_2_POINTS
   std::vector<double> by2p;        // by2: [ncyl][7] tvec_1, tvec_2, radius (the LM's parameters)
@@ -715,12 +749,20 @@ int BuildGsbaSetup(const mi_ba_options* o, const mi_ba_problem* p, const Setup& 
       GsbaCylinderToBy2(y.qvec, y.tvec, y.radius, y.height, &gs->by2p[7 * (size_t)c]);
     }
   }
-  const int64_t plane = (int64_t)g->height * g->width;
   gs->sem_total.assign(I, 0);
+  gs->mask_off.assign(I, 0);
+  gs->mask_h.assign(I, 0);
+  gs->mask_w.assign(I, 0);
+  int64_t off = 0;
   for (int i = 0; i < I; ++i) {
+    gs->mask_h[i] = g->image_height ? g->image_height[i] : g->height;
+    gs->mask_w[i] = g->image_width ? g->image_width[i] : g->width;
+    gs->mask_off[i] = off;
+    const int64_t plane = (int64_t)gs->mask_h[i] * gs->mask_w[i];
     int64_t c = 0;
-    for (int64_t k = 0; k < plane; ++k) c += g->trunk_mask[i * plane + k] != 0;
+    for (int64_t k = 0; k < plane; ++k) c += g->trunk_mask[off + k] != 0;
     gs->sem_total[i] = c;
+    off += plane;
   }
   for (int i = 0; i < I; ++i) {
     if (!in_cfg(i)) continue;
@@ -753,14 +795,13 @@ double GsbaResidual(const mi_ba_problem* p, const Setup& s, const GsbaSetup& gs,
   const mi_ba_gsba* g = gs.g;
   const mi_ba_cylinder& y = g->cylinders[b.cyl];
   const double* K = &p->camera_params[s.cam_poff[p->image_camera[b.img]]];
-  const int64_t plane = (int64_t)g->height * g->width;
+  const uint8_t* mask = g->trunk_mask + gs.mask_off[b.img];
+  const int H = gs.mask_h[b.img], W = gs.mask_w[b.img];
   if (gs.by2)
     return GsbaEvalBlock(b.variant, &p->qvec[b.img * 4], &p->tvec[b.img * 3], K, nullptr, &gs.by2p[7 * (size_t)b.cyl],
-                         0.0, 0.0, g->trunk_mask + b.img * plane, g->height, g->width, gs.sem_total[b.img],
-                         g->numeric_relative_step_size, J16);
+                         0.0, 0.0, mask, H, W, gs.sem_total[b.img], g->numeric_relative_step_size, J16);
   return GsbaEvalBlock(b.variant, &p->qvec[b.img * 4], &p->tvec[b.img * 3], K, y.qvec, y.tvec, y.radius, y.height,
-                       g->trunk_mask + b.img * plane, g->height, g->width, gs.sem_total[b.img],
-                       g->numeric_relative_step_size, J16);
+                       mask, H, W, gs.sem_total[b.img], g->numeric_relative_step_size, J16);
 }
 
 struct Layout {
@@ -995,7 +1036,7 @@ struct Solver {
     const SemSample& smp = ss.samples[n];
     const int i = sem->pairs[2 * smp.pair], j = sem->pairs[2 * smp.pair + 1];
     int st;
-    const double r = SemanticError(p, s, sem, smp, &p->qvec[i * 4], &p->tvec[i * 3], &p->qvec[j * 4], &p->tvec[j * 3], &st);
+    const double r = SemanticError(p, s, sem, ss, smp, &p->qvec[i * 4], &p->tvec[i * 3], &p->qvec[j * 4], &p->tvec[j * 3], &st);
     double rho[3];
     LossEvaluate(o->loss_function_type, o->loss_function_scale, r * r, rho);
     return 0.5 * (o->semantic_weight * rho[0]);  // ScaledLoss(w)
@@ -1412,7 +1453,10 @@ int64_t oracle_semantic_export(const mi_ba_options* o, mi_ba_problem* p, const m
   Setup s;
   const int st = BuildSetup(o, p, &s);
   if (st) return -st;
-  const int H = sem->height, W = sem->width, step = sem->pixel_step;
+  SemPlanes planes;
+  planes.build(sem, p->num_images);
+  const SemRaster& r1 = planes.img[image1];
+  const int H = r1.H, W = r1.W, step = sem->pixel_step;
   const int nx = (W + step - 1) / step, ny = (H + step - 1) / step;
   const int64_t n = (int64_t)nx * ny;
   if (n > capacity) return n;
@@ -1425,18 +1469,18 @@ int64_t oracle_semantic_export(const mi_ba_options* o, mi_ba_problem* p, const m
   int64_t k = 0;
   for (int y = 0; y < H; y += step) {       // :953-956
     for (int x = 0; x < W; x += step, ++k) {
-      const int64_t off = (int64_t)image1 * H * W + (int64_t)y * W + x;
+      const int64_t off = (int64_t)y * W + x;
       SemSample smp;
       smp.pair = 0; smp.x = x; smp.y = y;
       double u1, v1;
       ImageToWorld(s.cam_model[cam1], K1, (double)x, (double)y, &u1, &v1);
-      const double depth = (double)sem->depth[off];
+      const double depth = (double)r1.depth[off];
       smp.pc1[0] = u1 * depth;
       smp.pc1[1] = v1 * depth;
       smp.pc1[2] = depth;
-      smp.label1 = sem->label[off];
+      smp.label1 = r1.label[off];
       int stt = 0, pxy[2] = {0, 0};
-      error[k] = SemanticErrorTo(p, s, sem, image2, smp, q1, t1, q2, t2, &stt, &world[3 * k], pxy);
+      error[k] = SemanticErrorTo(p, s, sem, image2, planes.img[image2], smp, q1, t1, q2, t2, &stt, &world[3 * k], pxy);
       status[k] = stt;
       pixels[4 * k] = x;
       pixels[4 * k + 1] = y;
@@ -1512,7 +1556,7 @@ int oracle_semantic_flat_property(const mi_ba_options* o, mi_ba_problem* p, cons
     for (int m = 0; m < 4; ++m) x[7 + m] = p->qvec[j * 4 + m];
     for (int m = 0; m < 3; ++m) x[11 + m] = p->tvec[j * 3 + m];
     int stt;
-    const double r = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], &stt);
+    const double r = SemanticError(p, s, sem, ss, smp, &x[0], &x[4], &x[7], &x[11], &stt);
     const bool var[2] = {ss.pair_var1[smp.pair] != 0, ss.pair_var2[smp.pair] != 0};
     const double min_step = std::sqrt(std::numeric_limits<double>::epsilon());
     bool flat = true, jz = true;
@@ -1523,15 +1567,15 @@ int oracle_semantic_flat_property(const mi_ba_options* o, mi_ba_problem* p, cons
         const double orig = x[idx];
         const double delta = std::max(min_step, std::fabs(orig) * sem->numeric_relative_step_size);
         x[idx] = orig + delta;
-        const double fp = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], &stt);
+        const double fp = SemanticError(p, s, sem, ss, smp, &x[0], &x[4], &x[7], &x[11], &stt);
         x[idx] = orig - delta;
-        const double fm = SemanticError(p, s, sem, smp, &x[0], &x[4], &x[7], &x[11], &stt);
+        const double fm = SemanticError(p, s, sem, ss, smp, &x[0], &x[4], &x[7], &x[11], &stt);
         x[idx] = orig;
         if (fp != r || fm != r) flat = false;
         if (fp != fm) jz = false;
       }
     }
-    const bool clears = FlatClears(p, s, sem, smp, pb[smp.pair], var[0], var[1], r);
+    const bool clears = FlatClears(p, s, sem, ss, smp, pb[smp.pair], var[0], var[1], r);
     cleared += clears;
     bad += clears && !flat;
     nonzero += !jz;

@@ -23,6 +23,12 @@ struct GsbaBlock {     // device block descriptor
   int32_t img, cyl, variant, slot;   // slot: trunk mask of the image
   int32_t eval0, nevals, pad0, pad1; // evaluations [eval0, eval0 + nevals)
 };
+// One image's trunk mask (its own size, ABI 4): its plane in the byte masks
+// (moff) and in the bit-packed masks (boff, words per row).
+struct GsbaSlot {
+  uint64_t moff, boff;
+  int32_t H, W, words, pad;
+};
 struct GsbaEval {      // one IoU evaluation: block, perturbed parameter (-1 = none), sign
   int32_t block;
   int16_t param;
@@ -31,7 +37,7 @@ struct GsbaEval {      // one IoU evaluation: block, perturbed parameter (-1 = n
 
 struct GsbaState {
   const mi_ba_gsba* host = nullptr;  // caller's struct (cylinders written back)
-  int H = 0, W = 0, ncyl = 0, nblocks = 0;
+  int ncyl = 0, nblocks = 0;
   int64_t nevals = 0;
   double rel_step = 1e-3;
   double weight = 1.0;               // ScaledLoss(1 / #config images)
@@ -41,9 +47,10 @@ struct GsbaState {
   DevArray<GsbaBlock> blocks;
   DevArray<GsbaEval> evals;          // linearization: every evaluation
   DevArray<GsbaEval> centres;        // cost: one per block
-  DevArray<uint8_t> masks;           // [slot][H][W]
-  DevArray<uint64_t> mask_bits;      // [slot][H][words] bit-packed masks (span kernel)
-  int words = 0;                     // 64-bit words per mask row
+  std::vector<GsbaSlot> slots_host;  // [slot] the masks' planes and sizes
+  DevArray<GsbaSlot> slots;
+  DevArray<uint8_t> masks;           // slot planes [H_s][W_s]
+  DevArray<uint64_t> mask_bits;      // slot planes [H_s][words_s] bit-packed masks (span kernel)
   int iou_variant = 0;               // 0 row spans over mask_bits, 1 per-pixel predicate (tools build)
   DevArray<int64_t> sem_total;       // [slot]
   DevArray<double> cyl, cyl_c;       // [ncyl][9] q(4) t(3) radius height (by 2 points: t1(3) t2(3) radius 0 0):

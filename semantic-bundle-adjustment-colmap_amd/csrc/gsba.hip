@@ -250,10 +250,10 @@ struct GsbaArgs {
   const double* cam;       // [C][8]
   const uint32_t* img_cam;
   const double* cyl;       // [ncyl][9]
-  const uint8_t* masks;    // [slot][H][W] (per-pixel kernel, tools build)
-  const uint64_t* mask_bits;  // [slot][H][words]: bit x % 64 of word x / 64 = mask pixel (y, x) != 0
+  const GsbaSlot* slots;   // [slot] each mask's plane offsets and size
+  const uint8_t* masks;    // slot planes [H][W] (per-pixel kernel, tools build)
+  const uint64_t* mask_bits;  // slot planes [H][words]: bit x % 64 of word x / 64 = mask pixel (y, x) != 0
   const int64_t* sem_total;
-  int H, W, words;
   double rel_step;
   int by2;                 // MI_BA_CYLINDER_BY_2_POINTS: cyl rows are t1(3) t2(3) r, 0, 0
 };
@@ -304,7 +304,7 @@ __device__ inline QuadGeom quad_geom(const GsbaArgs& a, const GsbaEval& ev, cons
   g.ok = project_quad(x, K, g.p);
   g.box = Box{0, 0, 0, 0};
   if (!g.ok) return g;
-  const int H = a.H, W = a.W;
+  const int H = a.slots[b.slot].H, W = a.slots[b.slot].W;  // the image's own semantic map size
   const double(&p)[4][2] = g.p;
   // drawQuadrilateral as a predicate over the shrunk bounding box
   double min_x = p[0][0], min_y = p[0][1], max_x = p[0][0], max_y = p[0][1];
@@ -390,11 +390,11 @@ __global__ __launch_bounds__(kTB) void gsba_iou_kernel(GsbaArgs a, const GsbaEva
   const GsbaEval ev = evals[blockIdx.x];
   const GsbaBlock b = a.blocks[ev.block];
   const QuadGeom g = quad_geom(a, ev, b);
-  const int H = a.H, W = a.W;
+  const int W = a.slots[b.slot].W;
   int64_t tp = 0, fp = 0;
   if (g.ok) {
     const Box box = g.box;
-    const uint8_t* sem = a.masks + (size_t)b.slot * H * W;
+    const uint8_t* sem = a.masks + a.slots[b.slot].moff;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int y = box.y + wave; y <= box.y_end(); y += kTB / 64) {
       const uint8_t* srow = sem + (size_t)y * W;
@@ -448,7 +448,8 @@ __global__ __launch_bounds__(kTB) void gsba_iou_span_kernel(GsbaArgs a, const Gs
   int64_t tp = 0, fp = 0;
   if (g.ok && g.box.w > 0) {
     const Box box = g.box;
-    const uint64_t* bits = a.mask_bits + (size_t)b.slot * a.H * a.words;
+    const GsbaSlot si = a.slots[b.slot];
+    const uint64_t* bits = a.mask_bits + si.boff;
     for (int y = box.y + (int)threadIdx.x; y <= box.y_end(); y += kTB) {
       int lo[8], hi[8];
 #pragma unroll
@@ -490,7 +491,7 @@ __global__ __launch_bounds__(kTB) void gsba_iou_span_kernel(GsbaArgs a, const Gs
         lo[4 + k] = in ? rb.x : 1;
         hi[4 + k] = in ? rb.x_end() : 0;
       }
-      const uint64_t* row = bits + (size_t)y * a.words;
+      const uint64_t* row = bits + (size_t)y * si.words;
       for (int w = box.x >> 6; w <= (box.x_end() >> 6); ++w) {
         const int w0 = 64 * w;
         uint64_t keep = bit_range(box.x - w0, box.x_end() - w0);
@@ -879,12 +880,10 @@ GsbaArgs make_args(mi_ba_context* ctx, const double* qt, const double* cyl) {
   a.cam = ctx->dev.cam;
   a.img_cam = ctx->dev.img_cam;
   a.cyl = cyl;
+  a.slots = G->slots.ptr;
   a.masks = G->masks.ptr;
   a.mask_bits = G->mask_bits.ptr;
-  a.words = G->words;
   a.sem_total = G->sem_total.ptr;
-  a.H = G->H;
-  a.W = G->W;
   a.rel_step = G->rel_step;
   a.by2 = G->by2 ? 1 : 0;
   return a;
@@ -921,7 +920,9 @@ int gsba_cylinder_slots(const mi_ba_options& o, const mi_ba_problem* p, const mi
 mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
   const mi_ba_problem* p = &ctx->problem;
   const mi_ba_options& o = ctx->options;
-  if (g->height <= 0 || g->width <= 0 || !g->trunk_mask || g->num_cylinders < 0 ||
+  const bool per_image = g->image_height || g->image_width;
+  if ((per_image && !(g->image_height && g->image_width)) || (!per_image && (g->height <= 0 || g->width <= 0)) ||
+      !g->trunk_mask || g->num_cylinders < 0 ||
       (g->num_cylinders > 0 && !g->cylinders) || !(g->numeric_relative_step_size > 0) ||
       (g->cylinder_parametrization != MI_BA_CYLINDER_DEFAULT &&
        g->cylinder_parametrization != MI_BA_CYLINDER_BY_2_POINTS))
@@ -929,6 +930,20 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
   HostSetup& s = ctx->setup;
   const int I = p->num_images;
   auto in_cfg = [&](int i) { return p->image_in_config ? p->image_in_config[i] != 0 : true; };
+  // each image's mask size and plane (ABI 4: per-image sizes, planes back to back)
+  std::vector<int32_t> img_h(I), img_w(I);
+  std::vector<size_t> img_off(I);
+  {
+    size_t off = 0;
+    for (int i = 0; i < I; ++i) {
+      img_h[i] = per_image ? g->image_height[i] : g->height;
+      img_w[i] = per_image ? g->image_width[i] : g->width;
+      if (img_h[i] < 0 || img_w[i] < 0 || (in_cfg(i) && (img_h[i] == 0 || img_w[i] == 0)))
+        return MI_BA_ERR_INVALID_ARGUMENT;
+      img_off[i] = off;
+      off += (size_t)img_h[i] * img_w[i];
+    }
+  }
   // GeometricSemanticBundleAdjuster::Assert (:664-712)
   int ncfg = 0;
   for (int i = 0; i < I; ++i) {
@@ -941,8 +956,6 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
   auto* G = new GsbaState();
   ctx->gsba = G;
   G->host = g;
-  G->H = g->height;
-  G->W = g->width;
   G->ncyl = g->num_cylinders;
   G->rel_step = g->numeric_relative_step_size;
   G->weight = ncfg > 0 ? 1. / (double)ncfg : 1.0;
@@ -991,10 +1004,22 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
   G->nblocks = (int)G->blocks_host.size();
   G->nevals = (int64_t)evals.size();
   if (ctx->dev.cyl_var) s.num_effective_parameters_reduced += G->cw * (int64_t)G->ncyl;
-  const size_t plane = (size_t)G->H * G->W;
   std::vector<int64_t> totals(slot_images.size(), 0);
+  G->slots_host.resize(slot_images.size());
+  size_t mtot = 0, btot = 0;
   for (size_t k = 0; k < slot_images.size(); ++k) {
-    const uint8_t* m = g->trunk_mask + (size_t)slot_images[k] * plane;
+    const int i = slot_images[k];
+    GsbaSlot& si = G->slots_host[k];
+    si.H = img_h[i];
+    si.W = img_w[i];
+    si.words = (si.W + 63) / 64;
+    si.pad = 0;
+    si.moff = mtot;
+    si.boff = btot;
+    const size_t plane = (size_t)si.H * si.W;
+    mtot += plane;
+    btot += (size_t)si.H * si.words;
+    const uint8_t* m = g->trunk_mask + img_off[i];
     int64_t t = 0;
     for (size_t q = 0; q < plane; ++q) t += m[q] != 0;
     totals[k] = t;
@@ -1013,7 +1038,7 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
   }
   const int nb = std::max(1, G->nblocks);
   if (G->blocks.alloc(nb) || G->evals.alloc(std::max<int64_t>(1, G->nevals)) || G->centres.alloc(nb) ||
-      G->masks.alloc(plane * std::max<size_t>(1, slot_images.size())) ||
+      G->masks.alloc(std::max<size_t>(1, mtot)) || G->slots.alloc(std::max<size_t>(1, slot_images.size())) ||
       G->sem_total.alloc(std::max<size_t>(1, slot_images.size())) || G->cyl.alloc(cyl.size()) ||
       G->cyl_c.alloc(cyl.size()) || G->iou.alloc(std::max<int64_t>(1, G->nevals)) || G->r.alloc(nb) ||
       G->J.alloc(14 * (size_t)nb) || G->cyl_blk.alloc(36 * (size_t)std::max(1, G->ncyl)) ||
@@ -1026,30 +1051,34 @@ mi_ba_status gsba_create(mi_ba_context* ctx, const mi_ba_gsba* g) {
         hipMemcpy(G->centres.ptr, centres.data(), centres.size() * sizeof(GsbaEval), hipMemcpyHostToDevice))) ||
       hipMemcpy(G->cyl.ptr, cyl.data(), cyl.size() * 8, hipMemcpyHostToDevice) ||
       (!slot_images.empty() &&
-       hipMemcpy(G->sem_total.ptr, totals.data(), totals.size() * 8, hipMemcpyHostToDevice)))
+       (hipMemcpy(G->sem_total.ptr, totals.data(), totals.size() * 8, hipMemcpyHostToDevice) ||
+        hipMemcpy(G->slots.ptr, G->slots_host.data(), G->slots_host.size() * sizeof(GsbaSlot),
+                  hipMemcpyHostToDevice))))
     return MI_BA_ERR_HIP;
-  for (size_t k = 0; k < slot_images.size(); ++k)
-    if (hipMemcpy(G->masks.ptr + k * plane, g->trunk_mask + (size_t)slot_images[k] * plane, plane,
+  for (size_t k = 0; k < slot_images.size(); ++k) {
+    const GsbaSlot& si = G->slots_host[k];
+    if (hipMemcpy(G->masks.ptr + si.moff, g->trunk_mask + img_off[slot_images[k]], (size_t)si.H * si.W,
                   hipMemcpyHostToDevice))
       return MI_BA_ERR_HIP;
+  }
 #ifdef MI_BA_AB_VARIANTS
   // tools build: MI_BA_GSBA_VARIANT=1 selects the per-pixel kernel (the GSBA
   // entry points create their contexts internally, out of mi_ba_set_tuning's reach)
   if (const char* v = std::getenv("MI_BA_GSBA_VARIANT")) G->iou_variant = std::atoi(v) == 1 ? 1 : 0;
 #endif
   // bit-packed masks (row-major, whole 64-bit words per row) for the span kernel
-  G->words = (G->W + 63) / 64;
   {
-    const size_t wplane = (size_t)G->H * G->words;
-    if (G->mask_bits.alloc(wplane * std::max<size_t>(1, slot_images.size()))) return MI_BA_ERR_OUT_OF_MEMORY;
-    std::vector<uint64_t> wb(wplane);
+    if (G->mask_bits.alloc(std::max<size_t>(1, btot))) return MI_BA_ERR_OUT_OF_MEMORY;
+    std::vector<uint64_t> wb;
     for (size_t k = 0; k < slot_images.size(); ++k) {
-      const uint8_t* m = g->trunk_mask + (size_t)slot_images[k] * plane;
-      std::fill(wb.begin(), wb.end(), 0ull);
-      for (int y = 0; y < G->H; ++y)
-        for (int x = 0; x < G->W; ++x)
-          if (m[(size_t)y * G->W + x]) wb[(size_t)y * G->words + (x >> 6)] |= 1ull << (x & 63);
-      if (hipMemcpy(G->mask_bits.ptr + k * wplane, wb.data(), wplane * 8, hipMemcpyHostToDevice)) return MI_BA_ERR_HIP;
+      const GsbaSlot& si = G->slots_host[k];
+      const size_t wplane = (size_t)si.H * si.words;
+      const uint8_t* m = g->trunk_mask + img_off[slot_images[k]];
+      wb.assign(wplane, 0ull);
+      for (int y = 0; y < si.H; ++y)
+        for (int x = 0; x < si.W; ++x)
+          if (m[(size_t)y * si.W + x]) wb[(size_t)y * si.words + (x >> 6)] |= 1ull << (x & 63);
+      if (hipMemcpy(G->mask_bits.ptr + si.boff, wb.data(), wplane * 8, hipMemcpyHostToDevice)) return MI_BA_ERR_HIP;
     }
   }
   // refresh image flags (poses made variable by the GSBA term)

@@ -34,8 +34,23 @@ struct SemPair {
   uint32_t start, count;
 };
 
+// One raster slot (an image used as the second image of a pair): its plane
+// in the rasters / label plane / window summaries (off, pixels) and in the
+// tile depth ranges (toff, 8 x 8 tiles), its own size (ABI 4: every image
+// has its own H x W, semantic_bundle_adjustment.cc:792-793,
+// semantic_cost_functions.h:163) and tiles per row.
+struct SlotInfo {
+  uint64_t off, toff;
+  int32_t H, W, TW, pad;
+};
+
 struct SemanticState {
-  int H = 0, W = 0;
+  std::vector<int32_t> img_h, img_w;       // [I] each image's raster size
+  std::vector<SlotInfo> slots_host;        // [nslots]
+  DevArray<SlotInfo> slots;
+  int64_t npix = 0;                        // pixels of every slot's plane
+  int64_t ntile = 0;                       // 8 x 8 tiles of every slot
+  int max_plane = 0, max_tiles = 0;        // largest slot plane / tile grid
   double depth_threshold = 2.0;
   double rel_step = 1e-3;
   int step = 1;          // pixel grid step (error_computation_pixel_step)
@@ -46,17 +61,17 @@ struct SemanticState {
   std::vector<int32_t> sample_pixel_host;  // [ns][3]
   DevArray<SemSample> samples;
   DevArray<SemPair> pairs;
-  DevArray<float2> dl;                     // [slot][H][W] (depth, label) of images used as j
+  DevArray<float2> dl;                     // slot planes [H_s][W_s] (depth, label) of images used as j
   int nslots = 0;
-  DevArray<float4> wsum;                   // [slot][H][W] 3x3 window summaries ("semantic_window_summary")
+  DevArray<float4> wsum;                   // slot planes: 3x3 window summaries ("semantic_window_summary")
   bool use_wsum = false;
   // label planes ("semantic_label_planes"): the flat pass's first reads.
   // lab8 = each raster pixel's label as an index into pal (the rasters'
   // distinct label bit patterns, <= 256), dtile = (min, max) depth over each
   // 8 x 8 pixel tile extended by 2 pixels right and down (every 3 x 3 box
   // whose top-left pixel lies in the tile), NaN when a depth in it is NaN
-  DevArray<uint8_t> lab8;                  // [slot][H][W]
-  DevArray<float2> dtile;                  // [slot][ceil(H/8)][ceil(W/8)]
+  DevArray<uint8_t> lab8;                  // slot planes [H_s][W_s]
+  DevArray<float2> dtile;                  // slot tile planes [ceil(H_s/8)][ceil(W_s/8)]
   DevArray<float> pal;                     // [256]
   bool use_lp = false;
   DevArray<uint32_t> raster_slot;          // image -> raster slot

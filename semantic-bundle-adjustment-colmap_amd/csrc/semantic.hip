@@ -40,12 +40,15 @@ struct SemArgs {
   const uint8_t* cam_model;  // [C] model id per camera (mixed-model cost kernel)
   const uint32_t* img_flags;
   const uint32_t* raster_slot;
-  const float2* dl;   // interleaved (depth, label) rasters [slot][H][W]
-  const float4* wsum; // 3x3 window summaries [slot][H][W] (window_summary_kernel) or null
-  const uint8_t* lab8; // label planes (label_index_kernel) or null
-  const float2* dtile; // [slot][TH][TW] tile depth ranges (depth_tile_kernel)
+  const SlotInfo* slots;  // [slot] plane offsets and size of each raster slot
+  const float2* dl;   // interleaved (depth, label) rasters, one plane per slot (SlotInfo::off)
+  const float4* wsum; // 3x3 window summaries, the rasters' layout (window_summary_kernel) or null
+  const uint8_t* lab8; // label planes, the rasters' layout (label_index_kernel) or null
+  const float2* dtile; // tile depth ranges, one plane per slot (SlotInfo::toff; depth_tile_kernel)
   const float* pal;    // [256] label values of the lab8 indices
-  int TH, TW;
+  // the raster of the current pair's second image (per pair: with_pair); 0 in
+  // the kernel arguments
+  int TW;
   int H, W;
   double threshold;
   double rel_step;
@@ -357,7 +360,8 @@ struct PairConst {
   double C[9];                        // R2 R: d P_2 / d t1 = -C (stencil)
   double K2[8];                       // camera of image j
   uint32_t var1, var2, mask1, mask2;  // variable poses, constant-tvec masks
-  uint32_t slot, pad0, pad1, pad2;
+  uint32_t slot, H2, W2, TW2;        // image j's raster slot, its size, its tiles per row
+  uint64_t roff, toff;                // its plane in the rasters / label planes, in the tiles
   // stencil tables, e = 2 m + minus over the 14 ambient parameters
   double pert[28];                    // perturbed parameter value
   double ood[14];                     // (1 / delta) / 2, Ceres CENTRAL
@@ -368,6 +372,16 @@ struct PairConst {
   // t1 point k moves it by dt1[k] C[:, k], t2 point k by dt2[k] e_k
   double rho1, rho2, dt1[3], dt2[3];
 };
+
+// The kernel arguments with the pair's second-image raster size (image j's own
+// H x W: the bounds test of semantic_cost_functions.h:163).
+__device__ __forceinline__ SemArgs with_pair(const SemArgs& ak, const PairConst* __restrict__ P) {
+  SemArgs a = ak;
+  a.H = (int)P->H2;
+  a.W = (int)P->W2;
+  a.TW = (int)P->TW2;
+  return a;
+}
 
 // Bounds of one pose's stencil (the flat test): a perturbed quaternion q' =
 // q + d e_k rotates by ||R(q') - R(q)|| = 2 sin(angle(q, q')) <= 2 d_perp /
@@ -442,7 +456,8 @@ __device__ inline void stencil_prep(const double* q1, const double* t1, const do
 __global__ void semantic_pair_prep_kernel(const SemPair* __restrict__ pairs, int npairs, const double* __restrict__ qt,
                                           const double* __restrict__ cam, const uint32_t* __restrict__ img_cam,
                                           const uint32_t* __restrict__ img_flags,
-                                          const uint32_t* __restrict__ raster_slot, double rel_step,
+                                          const uint32_t* __restrict__ raster_slot,
+                                          const SlotInfo* __restrict__ slots, double rel_step,
                                           PairConst* __restrict__ out, double* __restrict__ pair_blk, int blk_stride,
                                           uint32_t* __restrict__ pair_cnt, uint32_t* __restrict__ zero_n = nullptr,
                                           int nzero = 0) {
@@ -494,7 +509,12 @@ __global__ void semantic_pair_prep_kernel(const SemPair* __restrict__ pairs, int
   P.mask1 = (img_flags[pr.i] >> 1) & 7u;
   P.mask2 = (img_flags[pr.j] >> 1) & 7u;
   P.slot = raster_slot[pr.j];
-  P.pad0 = P.pad1 = P.pad2 = 0;
+  const SlotInfo si = slots[P.slot];
+  P.H2 = (uint32_t)si.H;
+  P.W2 = (uint32_t)si.W;
+  P.TW2 = (uint32_t)si.TW;
+  P.roff = si.off;
+  P.toff = si.toff;
   stencil_bounds(P.q1, P.t1, rel_step, &P.rho1, P.dt1);
   stencil_bounds(P.q2, P.t2, rel_step, &P.rho2, P.dt2);
 }
@@ -1207,7 +1227,7 @@ __device__ __forceinline__ bool stencil_flat(const SemArgs& a, const PairConst* 
 // lanes (one sample per lane) and only those evaluate the stencil, so a
 // workgroup with few of them keeps most of its waves free.
 template <int M, bool FAST = false, int NB = 0, bool FLAT = false>
-__global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, const SemTile* __restrict__ tiles,
+__global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs ak, const SemTile* __restrict__ tiles,
                                                                      const PairConst* __restrict__ pcs,
                                                                      double* __restrict__ pair_blk,
                                                                      double* __restrict__ cost_partial,
@@ -1226,10 +1246,11 @@ __global__ __launch_bounds__(kBlock) void semantic_linearize_kernel(SemArgs a, c
   double* sJ = sbuf;
   const SemTile t = tiles[blockIdx.x];
   const PairConst* __restrict__ P = pcs + t.pair;
+  const SemArgs a = with_pair(ak, P);
   const int tid = threadIdx.x;
   const bool active = tid < (int)t.count;
   const int64_t n = (int64_t)t.start + tid;
-  const float2* dl2 = a.dl + (size_t)P->slot * a.H * a.W;
+  const float2* dl2 = a.dl + P->roff;
   const double* K2 = P->K2;
   double cost = 0.0;
   double rowv[kSemRow];
@@ -1380,17 +1401,19 @@ __device__ __forceinline__ bool window_decides(const SemArgs& a, const FlatBox& 
   return false;
 }
 
-__global__ __launch_bounds__(256) void window_summary_kernel(const float2* __restrict__ dl, int H, int W,
-                                                             int64_t n, float4* __restrict__ out) {
-  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= n) return;
-  const int64_t plane = (int64_t)H * W;
-  const int64_t slot = k / plane;
-  const int rem = (int)(k - slot * plane);
-  const int y = rem / W, x = rem - y * W;
+// grid (pixel blocks of the largest plane, slots)
+__global__ __launch_bounds__(256) void window_summary_kernel(const float2* __restrict__ dl,
+                                                             const SlotInfo* __restrict__ slots,
+                                                             float4* __restrict__ out) {
+  const SlotInfo si = slots[blockIdx.y];
+  const int H = si.H, W = si.W;
+  const int64_t rem = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (rem >= (int64_t)H * W) return;
+  const int64_t k = (int64_t)si.off + rem;
+  const int y = (int)(rem / W), x = (int)(rem - (int64_t)y * W);
   float4 o = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
   if (x + 2 < W && y + 2 < H) {
-    const float2* base = dl + slot * plane + (int64_t)y * W + x;
+    const float2* base = dl + k;
     const float L = base[0].y;
     float dmin = base[0].x, dmax = base[0].x;
     bool uniform = true;
@@ -1449,15 +1472,16 @@ __global__ __launch_bounds__(256) void label_index_kernel(const float2* __restri
   lab8[k] = (uint8_t)h;
 }
 
-__global__ __launch_bounds__(256) void depth_tile_kernel(const float2* __restrict__ dl, int H, int W, int TH, int TW,
-                                                         int64_t n, float2* __restrict__ out) {
-  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= n) return;
-  const int64_t per = (int64_t)TH * TW;
-  const int64_t slot = k / per;
-  const int rem = (int)(k - slot * per);
+// grid (tile blocks of the largest tile plane, slots)
+__global__ __launch_bounds__(256) void depth_tile_kernel(const float2* __restrict__ dl,
+                                                         const SlotInfo* __restrict__ slots, float2* __restrict__ out) {
+  const SlotInfo si = slots[blockIdx.y];
+  const int H = si.H, W = si.W, TW = si.TW, TH = (H + 7) / 8;
+  const int rem = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (rem >= TH * TW) return;
+  const int64_t k = (int64_t)si.toff + rem;
   const int ty = rem / TW, tx = rem - ty * TW;
-  const float2* base = dl + slot * H * (int64_t)W;
+  const float2* base = dl + si.off;
   float dmin = __builtin_inff(), dmax = -__builtin_inff();
   bool nan = false;
   const int y1 = min(8 * ty + 10, H), x1 = min(8 * tx + 10, W);
@@ -1487,7 +1511,7 @@ __device__ __forceinline__ int tile_depth_side(const SemArgs& a, const FlatBox& 
 }
 
 template <int M, bool FAST, bool WS = false, bool LP = false, int COARSE = 0>
-__global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const SemTile* __restrict__ tiles,
+__global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs ak, const SemTile* __restrict__ tiles,
                                                                const PairConst* __restrict__ pcs,
                                                                unsigned long long* __restrict__ dmask,
                                                                double* __restrict__ cost_partial,
@@ -1498,10 +1522,11 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
   __shared__ float spal[LP ? 256 : 1];
   const SemTile t = tiles[blockIdx.x];
   const PairConst* __restrict__ P = pcs + t.pair;
+  const SemArgs a = with_pair(ak, P);
   const int tid = threadIdx.x, lane = tid & 63;
   const bool active = tid < (int)t.count;
   const int64_t n = (int64_t)t.start + tid;
-  const float2* dl2 = a.dl + (size_t)P->slot * a.H * a.W;
+  const float2* dl2 = a.dl + P->roff;
   const double* K2 = P->K2;
   double cost = 0.0;
   bool deferred = false;
@@ -1552,8 +1577,8 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
           cpx < fb.x0 + fb.ncol && cpy >= fb.y0 && cpy < fb.y0 + fb.nrow) {
         // the tile range and the box's labels requested together (one round
         // trip; the labels go unused when the depth test settles the box invalid)
-        const float2 dr = a.dtile[((size_t)P->slot * a.TH + (fb.y0 >> 3)) * a.TW + (fb.x0 >> 3)];
-        const uint8_t* lp = a.lab8 + (size_t)P->slot * a.H * a.W + (size_t)fb.y0 * a.W + fb.x0;
+        const float2 dr = a.dtile[P->toff + (size_t)(fb.y0 >> 3) * a.TW + (fb.x0 >> 3)];
+        const uint8_t* lp = a.lab8 + P->roff + (size_t)fb.y0 * a.W + fb.x0;
         const uint8_t lc = lp[(size_t)(cpy - fb.y0) * a.W + (cpx - fb.x0)];
         uint8_t L[9];
 #pragma unroll
@@ -1578,7 +1603,7 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
     if constexpr (WS) {
       // one 16-B read of the window holding the box (its top-left pixel)
       if (!resolved && cand && fb.x0 >= 0 && fb.y0 >= 0 && fb.x0 + 2 < a.W && fb.y0 + 2 < a.H) {
-        const float4 w = a.wsum[(size_t)P->slot * a.H * a.W + (size_t)fb.y0 * a.W + fb.x0];
+        const float4 w = a.wsum[P->roff + (size_t)fb.y0 * a.W + fb.x0];
         decided = resolved = window_decides(a, fb, w, c.p2[2], c.mag, smp.label1, &c.st, &c.r);
       }
     }
@@ -1645,7 +1670,7 @@ __global__ __launch_bounds__(kBlock) void semantic_flat_kernel(SemArgs a, const 
 // variants; the default build's 128 VGPRs give 4 waves per SIMD, 16 of these
 // 64-thread workgroups per CU)
 template <int M, bool FAST, int NB, bool BOX = false, int WPE = 1>
-__global__ __launch_bounds__(64, WPE) void semantic_deferred_kernel(SemArgs a, const uint2* __restrict__ chunks,
+__global__ __launch_bounds__(64, WPE) void semantic_deferred_kernel(SemArgs ak, const uint2* __restrict__ chunks,
                                                               const uint32_t* __restrict__ ccount,
                                                               const PairConst* __restrict__ pcs,
                                                               const uint32_t* __restrict__ pair_cnt,
@@ -1666,10 +1691,11 @@ __global__ __launch_bounds__(64, WPE) void semantic_deferred_kernel(SemArgs a, c
   const uint32_t cnt = pair_cnt[ch.x];
   if (ch.y >= cnt) continue;  // workgroup-uniform
   const PairConst* __restrict__ P = pcs + ch.x;
+  const SemArgs a = with_pair(ak, P);
   const int lane = threadIdx.x;
   const uint32_t k = ch.y + lane;
   const uint32_t pstart = a.pairs[ch.x].start;
-  const float2* dl2 = a.dl + (size_t)P->slot * a.H * a.W;
+  const float2* dl2 = a.dl + P->roff;
   const double* K2 = P->K2;
   double rowv[kSemRow];
 #pragma unroll
@@ -1858,16 +1884,18 @@ __global__ __launch_bounds__(kBlock) void semantic_cost_kernel(SemArgs a, double
     const double* kc = a.cam + 8 * (size_t)cam2;
 #pragma unroll
     for (int m = 0; m < np; ++m) K2[m] = kc[m];
-    const size_t slot = a.raster_slot[pr.j];
+    const SlotInfo si = a.slots[a.raster_slot[pr.j]];
+    SemArgs aj = a;  // image j's raster size
+    aj.H = si.H;
+    aj.W = si.W;
     int st;
     double r;
     if constexpr (M == kMixedModels) {
       switch_model(a.cam_model[cam2], [&](auto m) {
-        r = semantic_error<decltype(m)::value>(a, smp.pc1, smp.label1, q1, t1, q2, t2, K2, a.dl + slot * a.H * a.W,
-                                               &st);
+        r = semantic_error<decltype(m)::value>(aj, smp.pc1, smp.label1, q1, t1, q2, t2, K2, a.dl + si.off, &st);
       });
     } else {
-      r = semantic_error<M>(a, smp.pc1, smp.label1, q1, t1, q2, t2, K2, a.dl + slot * a.H * a.W, &st);
+      r = semantic_error<M>(aj, smp.pc1, smp.label1, q1, t1, q2, t2, K2, a.dl + si.off, &st);
     }
     double rho[3];
     loss_eval(a.loss_type, a.loss_scale, r * r, rho);
@@ -2063,7 +2091,8 @@ __global__ __launch_bounds__(kBlock) void semantic_export_kernel(SemArgs a, uint
   double K2[8];
 #pragma unroll
   for (int m = 0; m < 8; ++m) K2[m] = kc[m];
-  const float2 c1 = a.dl[(size_t)a.raster_slot[i] * a.H * a.W + (size_t)y * a.W + x];
+  const SlotInfo s1 = a.slots[a.raster_slot[i]], s2 = a.slots[a.raster_slot[j]];
+  const float2 c1 = a.dl[s1.off + (size_t)y * s1.W + x];
   double u1 = 0.0, v1 = 0.0;
   image_to_world_any(a.cam_model[cam1], K1, (double)x, (double)y, &u1, &v1);
   const double depth = (double)c1.x;
@@ -2072,12 +2101,15 @@ __global__ __launch_bounds__(kBlock) void semantic_export_kernel(SemArgs a, uint
   const double* qt2 = a.qt + 8 * (size_t)j;
   const double q1[4] = {qt1[0], qt1[1], qt1[2], qt1[3]}, t1[3] = {qt1[4], qt1[5], qt1[6]};
   const double q2[4] = {qt2[0], qt2[1], qt2[2], qt2[3]}, t2[3] = {qt2[4], qt2[5], qt2[6]};
-  const float2* dl2 = a.dl + (size_t)a.raster_slot[j] * a.H * a.W;
+  const float2* dl2 = a.dl + s2.off;
+  SemArgs aj = a;  // image j's raster size
+  aj.H = s2.H;
+  aj.W = s2.W;
   int st = 0;
   double r = 0.0, pw[3] = {0.0, 0.0, 0.0};
   int pxy[2] = {0, 0};
   switch_model(a.cam_model[cam2], [&](auto m) {
-    r = semantic_error<decltype(m)::value>(a, pc1, c1.y, q1, t1, q2, t2, K2, dl2, &st, pw, pxy);
+    r = semantic_error<decltype(m)::value>(aj, pc1, c1.y, q1, t1, q2, t2, K2, dl2, &st, pw, pxy);
   });
   pix[4 * k] = x;
   pix[4 * k + 1] = y;
@@ -2101,15 +2133,15 @@ SemArgs make_args(mi_ba_context* ctx, const double* qt, const double* cam) {
   a.cam_model = ctx->dev.cam_model;
   a.img_flags = ctx->dev.img_flags;
   a.raster_slot = S->raster_slot.ptr;
+  a.slots = S->slots.ptr;
   a.dl = S->dl.ptr;
   a.wsum = S->use_wsum ? S->wsum.ptr : nullptr;
   a.lab8 = S->use_lp ? S->lab8.ptr : nullptr;
   a.dtile = S->use_lp ? S->dtile.ptr : nullptr;
   a.pal = S->use_lp ? S->pal.ptr : nullptr;
-  a.TH = (S->H + 7) / 8;
-  a.TW = (S->W + 7) / 8;
-  a.H = S->H;
-  a.W = S->W;
+  a.TW = 0;  // per pair (with_pair)
+  a.H = 0;
+  a.W = 0;
   a.threshold = S->depth_threshold;
   a.rel_step = S->rel_step;
   a.ns = S->ns;
@@ -2124,17 +2156,39 @@ SemArgs make_args(mi_ba_context* ctx, const double* qt, const double* cam) {
 mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
   const mi_ba_problem* p = &ctx->problem;
   const mi_ba_options& o = ctx->options;
-  if (sem->height <= 0 || sem->width <= 0 || !sem->depth || !sem->label || sem->num_pairs < 0 ||
+  const bool per_image = sem->image_height || sem->image_width;
+  if ((per_image && !(sem->image_height && sem->image_width)) ||
+      (!per_image && (sem->height <= 0 || sem->width <= 0)) || !sem->depth || !sem->label || sem->num_pairs < 0 ||
       (sem->num_pairs > 0 && !sem->pairs) || sem->pixel_step <= 0)
     return MI_BA_ERR_INVALID_ARGUMENT;
+  const int I = p->num_images;
+  // each image's raster size and plane (ABI 4: per-image sizes, planes back to
+  // back in image order)
+  std::vector<int32_t> img_h(I), img_w(I);
+  std::vector<size_t> img_off(I);
+  {
+    size_t off = 0;
+    for (int i = 0; i < I; ++i) {
+      img_h[i] = per_image ? sem->image_height[i] : sem->height;
+      img_w[i] = per_image ? sem->image_width[i] : sem->width;
+      if (img_h[i] < 0 || img_w[i] < 0) return MI_BA_ERR_INVALID_ARGUMENT;
+      img_off[i] = off;
+      off += (size_t)img_h[i] * img_w[i];
+    }
+  }
+  for (int k = 0; k < sem->num_pairs; ++k) {
+    const int i = sem->pairs[2 * k], j = sem->pairs[2 * k + 1];
+    if (i < 0 || i >= I || j < 0 || j >= I) return MI_BA_ERR_INVALID_ARGUMENT;
+    if (i != j && (img_h[i] <= 0 || img_w[i] <= 0 || img_h[j] <= 0 || img_w[j] <= 0))
+      return MI_BA_ERR_INVALID_ARGUMENT;
+  }
   auto* S = new SemanticState();
   ctx->sem = S;
-  S->H = sem->height;
-  S->W = sem->width;
+  S->img_h = img_h;
+  S->img_w = img_w;
   S->depth_threshold = sem->depth_error_threshold;
   S->rel_step = sem->numeric_relative_step_size;
   S->step = sem->pixel_step;
-  const int H = S->H, W = S->W, I = p->num_images;
   const HostSetup& hs = ctx->setup;
   auto const_pose = [&](int i) {
     return !o.refine_extrinsics || (p->image_constant_pose && p->image_constant_pose[i]);
@@ -2158,8 +2212,9 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
     pr.start = (uint32_t)samples.size();
     const double* K1 = p->camera_params + hs.cam_off[p->image_camera[i]];
     const int model1 = hs.cam_model[p->image_camera[i]];
-    const float* d1 = sem->depth + (size_t)i * H * W;
-    const float* l1 = sem->label + (size_t)i * H * W;
+    const float* d1 = sem->depth + img_off[i];
+    const float* l1 = sem->label + img_off[i];
+    const int H = img_h[i], W = img_w[i];  // image 1's own size (:792-793)
     const uint32_t pair_idx = (uint32_t)S->pairs_host.size();
     // pixel grid: y outer, x inner (:796-799); skip depth < 1e-4 (:806-814)
     for (int y = 0; y < H; y += sem->pixel_step) {
@@ -2222,7 +2277,29 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
       return MI_BA_ERR_HIP;
     }
   }
-  const size_t plane = (size_t)H * W;
+  // the slots' planes (rasters / label planes / window summaries) and tile planes
+  S->slots_host.resize(slot_images.size());
+  {
+    uint64_t off = 0, toff = 0;
+    for (size_t k = 0; k < slot_images.size(); ++k) {
+      const int j = slot_images[k];
+      SlotInfo& si = S->slots_host[k];
+      si.H = img_h[j];
+      si.W = img_w[j];
+      si.TW = (si.W + 7) / 8;
+      si.pad = 0;
+      si.off = off;
+      si.toff = toff;
+      const int64_t plane = (int64_t)si.H * si.W, tiles = (int64_t)((si.H + 7) / 8) * si.TW;
+      if (plane > INT32_MAX - 256) return MI_BA_ERR_INVALID_ARGUMENT;  // per-slot kernels index a plane in int
+      off += (uint64_t)plane;
+      toff += (uint64_t)tiles;
+      S->max_plane = std::max<int>(S->max_plane, (int)plane);
+      S->max_tiles = std::max<int>(S->max_tiles, (int)tiles);
+    }
+    S->npix = (int64_t)off;
+    S->ntile = (int64_t)toff;
+  }
   std::vector<uint32_t> slot_u(I, 0);
   for (int i = 0; i < I; ++i) slot_u[i] = slot[i] < 0 ? 0u : (uint32_t)slot[i];
   S->nslots = (int)slot_images.size();
@@ -2334,7 +2411,8 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
   if (!chunks.empty() && hipMemcpy(S->chunks.ptr, chunks.data(), chunks.size() * sizeof(uint2), hipMemcpyHostToDevice))
     return MI_BA_ERR_HIP;
   if (S->samples.alloc(S->ns) || S->pairs.alloc(S->npairs) || S->raster_slot.alloc(I) ||
-      S->dl.alloc(plane * std::max<size_t>(1, slot_images.size())) || S->r.alloc(S->ns) ||
+      S->slots.alloc(std::max<size_t>(1, S->slots_host.size())) ||
+      S->dl.alloc(std::max<size_t>(1, (size_t)S->npix)) || S->r.alloc(S->ns) ||
       S->status.alloc(S->ns) || S->J.alloc(12 * S->ns) ||
       S->pair_blk.alloc((size_t)kPairStride * std::max(1, S->npairs)) || S->tiles.alloc(tiles.size()) ||
       S->pconst.alloc(sizeof(PairConst) / sizeof(double) * std::max(1, S->npairs)))
@@ -2345,17 +2423,20 @@ mi_ba_status semantic_create(mi_ba_context* ctx, const mi_ba_semantic* sem) {
       (S->npairs &&
        hipMemcpy(S->pairs.ptr, S->pairs_host.data(), S->npairs * sizeof(SemPair), hipMemcpyHostToDevice)) ||
       (I && hipMemcpy(S->raster_slot.ptr, slot_u.data(), I * 4, hipMemcpyHostToDevice)) ||
+      (!S->slots_host.empty() && hipMemcpy(S->slots.ptr, S->slots_host.data(), S->slots_host.size() * sizeof(SlotInfo),
+                                           hipMemcpyHostToDevice)) ||
       (!tiles.empty() &&
        hipMemcpy(S->tiles.ptr, tiles.data(), tiles.size() * sizeof(SemTile), hipMemcpyHostToDevice)))
     return MI_BA_ERR_HIP;
   // rasters interleaved (depth, label): one 8-B gather per pixel test
-  std::vector<float2> buf(plane);
+  std::vector<float2> buf((size_t)S->max_plane);
   for (size_t s = 0; s < slot_images.size(); ++s) {
     const int j = slot_images[s];
-    const float* d = sem->depth + (size_t)j * plane;
-    const float* l = sem->label + (size_t)j * plane;
+    const size_t plane = (size_t)img_h[j] * img_w[j];
+    const float* d = sem->depth + img_off[j];
+    const float* l = sem->label + img_off[j];
     for (size_t k = 0; k < plane; ++k) buf[k] = make_float2(d[k], l[k]);
-    if (hipMemcpy(S->dl.ptr + s * plane, buf.data(), plane * sizeof(float2), hipMemcpyHostToDevice))
+    if (hipMemcpy(S->dl.ptr + S->slots_host[s].off, buf.data(), plane * sizeof(float2), hipMemcpyHostToDevice))
       return MI_BA_ERR_HIP;
   }
   // the flat pass's label planes (3.9M of 5.0M C4 samples settled without the
@@ -2375,7 +2456,9 @@ mi_ba_status semantic_export(mi_ba_context* ctx, int32_t image1, int32_t image2,
   const int I = ctx->problem.num_images;
   if (!S || !count || image1 < 0 || image1 >= I || image2 < 0 || image2 >= I || image1 == image2)
     return MI_BA_ERR_INVALID_ARGUMENT;
-  const int nx = (S->W + S->step - 1) / S->step, ny = (S->H + S->step - 1) / S->step;
+  // image 1's own grid (ExportSemanticErrorToCSV loops over image 1's map, :953-956)
+  const int H1 = S->img_h[image1], W1 = S->img_w[image1];
+  const int nx = (W1 + S->step - 1) / S->step, ny = (H1 + S->step - 1) / S->step;
   const int64_t n = (int64_t)nx * ny;
   *count = n;
   if (!pixels) return MI_BA_OK;
@@ -2402,15 +2485,15 @@ mi_ba_status semantic_set_window_summary(mi_ba_context* ctx, bool on) {
   SemanticState* S = ctx->sem;
   if (!S) return MI_BA_ERR_STATE;
   if (on && !S->wsum.ptr) {
-    const int64_t n = (int64_t)S->nslots * S->H * S->W;
+    const int64_t n = S->npix;
     if (n > 0) {
       if (S->wsum.alloc((size_t)n)) {
         (void)hipGetLastError();
         S->use_wsum = false;
         return MI_BA_ERR_OUT_OF_MEMORY;
       }
-      hipLaunchKernelGGL(window_summary_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, S->dl.ptr,
-                         S->H, S->W, n, S->wsum.ptr);
+      hipLaunchKernelGGL(window_summary_kernel, dim3((unsigned)((S->max_plane + 255) / 256), (unsigned)S->nslots),
+                         dim3(256), 0, ctx->stream, S->dl.ptr, S->slots.ptr, S->wsum.ptr);
       if (hipGetLastError() != hipSuccess) return MI_BA_ERR_HIP;
     }
   }
@@ -2430,10 +2513,9 @@ mi_ba_status semantic_set_label_planes(mi_ba_context* ctx, bool on) {
     return MI_BA_OK;
   }
   if (S->use_lp) return MI_BA_OK;
-  const int64_t n = (int64_t)S->nslots * S->H * S->W;
+  const int64_t n = S->npix;
   if (n <= 0) return MI_BA_OK;
-  const int TH = (S->H + 7) / 8, TW = (S->W + 7) / 8;
-  const int64_t nt = (int64_t)S->nslots * TH * TW;
+  const int64_t nt = S->ntile;
   DevArray<unsigned long long> keys;
   DevArray<unsigned> overflow;
   if (keys.alloc(256) || overflow.alloc(1) || S->lab8.alloc((size_t)n) || S->dtile.alloc((size_t)nt) ||
@@ -2467,8 +2549,8 @@ mi_ba_status semantic_set_label_planes(mi_ba_context* ctx, bool on) {
     std::memcpy(&hp[k], &b, 4);
   }
   hipLaunchKernelGGL(label_index_kernel, dim3(g), dim3(256), 0, s, S->dl.ptr, n, keys.ptr, S->lab8.ptr);
-  hipLaunchKernelGGL(depth_tile_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, S->dl.ptr, S->H, S->W,
-                     TH, TW, nt, S->dtile.ptr);
+  hipLaunchKernelGGL(depth_tile_kernel, dim3((unsigned)((S->max_tiles + 255) / 256), (unsigned)S->nslots), dim3(256),
+                     0, s, S->dl.ptr, S->slots.ptr, S->dtile.ptr);
   if (hipGetLastError() != hipSuccess || hipMemcpyAsync(S->pal.ptr, hp, sizeof(hp), hipMemcpyHostToDevice, s) ||
       hipStreamSynchronize(s))
     return MI_BA_ERR_HIP;
@@ -2490,7 +2572,8 @@ mi_ba_status semantic_pair_prep(mi_ba_context* ctx, hipStream_t stream) {
   SemArgs a = make_args(ctx, ctx->dev.qt, ctx->dev.cam);
   PairConst* pcs = reinterpret_cast<PairConst*>(S->pconst.ptr);
   hipLaunchKernelGGL(semantic_pair_prep_kernel, dim3((S->npairs + 1) / 2), dim3(64), 0, stream, S->pairs.ptr,
-                     S->npairs, a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.rel_step, pcs, S->pair_blk.ptr,
+                     S->npairs, a.qt, a.cam, a.img_cam, a.img_flags, a.raster_slot, a.slots, a.rel_step, pcs,
+                     S->pair_blk.ptr,
                      kPairStride, ctx->sem_variant == 6 ? S->pair_cnt.ptr : nullptr,
                      ctx->sem_variant == 6 ? S->dcount.ptr : nullptr, kNumModels);
   return hipGetLastError() == hipSuccess ? MI_BA_OK : MI_BA_ERR_HIP;

@@ -157,6 +157,8 @@ class Gsba(C.Structure):
         ("include_landmark_error", C.c_int32),
         ("landmark_error_weight", C.c_double),
         ("cylinder_parametrization", C.c_int32),
+        ("image_height", _i32p),
+        ("image_width", _i32p),
     ]
 
 
@@ -171,7 +173,21 @@ class Semantic(C.Structure):
         ("pixel_step", C.c_int32),
         ("depth_error_threshold", C.c_double),
         ("numeric_relative_step_size", C.c_double),
+        ("image_height", _i32p),
+        ("image_width", _i32p),
     ]
+
+
+def _planes(maps, dtype):
+    """[I][H][W] array -> (it, None, None); list of per-image [H_i][W_i]
+    arrays (ABI 4: each image its own size) -> (planes back to back, heights,
+    widths)."""
+    if isinstance(maps, np.ndarray):
+        return np.ascontiguousarray(maps, dtype), None, None
+    hs = np.array([np.shape(m)[0] if np.ndim(m) == 2 else 0 for m in maps], np.int32)
+    ws = np.array([np.shape(m)[1] if np.ndim(m) == 2 else 0 for m in maps], np.int32)
+    flat = [np.ascontiguousarray(m, dtype).ravel() for m in maps]
+    return (np.concatenate(flat) if flat else np.zeros(0, dtype)), hs, ws
 
 
 class Summary(C.Structure):
@@ -437,22 +453,30 @@ class Scene:
 
 @dataclass
 class SemanticInput:
-    depth: np.ndarray          # [I][H][W] f32
-    label: np.ndarray          # [I][H][W] f32
+    depth: object              # [I][H][W] f32, or a list of per-image [H_i][W_i] maps
+    label: object              # as depth
     pairs: np.ndarray          # [K][2] i32
     pixel_step: int = 10
     depth_error_threshold: float = 2.0
     numeric_relative_step_size: float = 1e-3
 
     def struct(self) -> Semantic:
-        self.depth = np.ascontiguousarray(self.depth, np.float32)
-        self.label = np.ascontiguousarray(self.label, np.float32)
+        self._depth, self._h, self._w = _planes(self.depth, np.float32)
+        self._label, hl, wl = _planes(self.label, np.float32)
+        if (self._h is None) != (hl is None) or (self._h is not None and
+                                                  (not np.array_equal(self._h, hl) or not np.array_equal(self._w, wl))):
+            raise ValueError("depth and label maps differ in size")
         self.pairs = np.ascontiguousarray(self.pairs, np.int32).reshape(-1, 2)
         s = Semantic()
-        s.height = self.depth.shape[1]
-        s.width = self.depth.shape[2]
-        s.depth = _ptr(self.depth, _fp)
-        s.label = _ptr(self.label, _fp)
+        if self._h is None:
+            s.height = self._depth.shape[1]
+            s.width = self._depth.shape[2]
+        else:
+            s.height = s.width = 0
+            s.image_height = _ptr(self._h, _i32p)
+            s.image_width = _ptr(self._w, _i32p)
+        s.depth = _ptr(self._depth, _fp)
+        s.label = _ptr(self._label, _fp)
         s.num_pairs = self.pairs.shape[0]
         s.pairs = _ptr(self.pairs, _i32p)
         s.pixel_step = self.pixel_step
@@ -521,7 +545,7 @@ class GsbaInput:
                          self.include_landmark_error, self.landmark_error_weight, self.cylinder_parametrization)
 
     def struct(self):
-        self.masks = np.ascontiguousarray(self.masks, np.uint8)
+        self._masks, self._h, self._w = _planes(self.masks, np.uint8)
         n = len(self.cylinders)
         arr = (Cylinder * max(1, n))()
         for k in range(n):
@@ -531,8 +555,13 @@ class GsbaInput:
             arr[k].radius = float(c[7])
             arr[k].height = float(c[8])
         g = Gsba()
-        g.height, g.width = int(self.masks.shape[1]), int(self.masks.shape[2])
-        g.trunk_mask = _ptr(self.masks, _u8p)
+        if self._h is None:
+            g.height, g.width = int(self._masks.shape[1]), int(self._masks.shape[2])
+        else:
+            g.height = g.width = 0
+            g.image_height = _ptr(self._h, _i32p)
+            g.image_width = _ptr(self._w, _i32p)
+        g.trunk_mask = _ptr(self._masks, _u8p)
         g.num_cylinders = n
         g.cylinders = C.cast(arr, C.POINTER(Cylinder))
         g.refine_geometry = self.refine_geometry

@@ -385,7 +385,8 @@ int main(int argc, char** argv) {
         }
       maps.depth[im.name] = depth;
       maps.semantic[im.name] = label;
-      // a principal point near the raster so the pairs overlap inside it
+      // a principal point near the raster so the pairs overlap inside it; the
+      // SIMPLE_RADIAL model first (the reference's Assert rejects it)
       rec.GetCamera(im.camera_id).params = {1200, 30, 30, 0};
       im.tvec[0] += 0.002 * (double)im.image_id;  // pose error for the semantic term to pull on
     }
@@ -402,6 +403,44 @@ int main(int argc, char** argv) {
       CHECK_T(threw);
     }
     for (camera_t c = 0; c < 3; ++c) config.SetConstantCamera(c);
+    {
+      // not SIMPLE_PINHOLE: Assert throws (cc:619-631) unless the extension is asked for
+      SemanticBundleAdjuster bad(options, config, maps);
+      std::string what;
+      try { bad.Solve(&rec); } catch (const std::runtime_error& e) { what = e.what(); }
+      CHECK_T(what == "ERROR: the only supported camera model is SimplePinholeCameraModel.");
+    }
+    {
+      SemanticBundleAdjustmentOptions o2 = options;
+      o2.refine_extrinsics = false;  // (with SIMPLE_PINHOLE cameras) the third check
+      Reconstruction pin = rec;
+      for (auto& c : pin.cameras) {
+        c.second.model_id = MI_BA_SIMPLE_PINHOLE;
+        c.second.params = {1200, 30, 30};
+      }
+      SemanticBundleAdjuster bad(o2, config, maps);
+      std::string what;
+      try { bad.Solve(&pin); } catch (const std::runtime_error& e) { what = e.what(); }
+      CHECK_T(what == "ERROR: the argument 'refine_extrinsics' must be set to true.");
+    }
+    if (s) {
+      // the extension: a SIMPLE_RADIAL (k = 0) solve equals the SIMPLE_PINHOLE one
+      SemanticBundleAdjustmentOptions o2 = options;
+      o2.allow_any_camera_model = true;
+      Reconstruction rad = rec, pin = rec;
+      for (auto& c : pin.cameras) {
+        c.second.model_id = MI_BA_SIMPLE_PINHOLE;
+        c.second.params = {1200, 30, 30};
+      }
+      SemanticBundleAdjuster a(o2, config, maps), b(options, config, maps);
+      CHECK_T(a.Solve(&rad));
+      CHECK_T(b.Solve(&pin));
+      CHECK_T(a.Summary().final_cost == b.Summary().final_cost);
+    }
+    for (auto& c : rec.cameras) {
+      c.second.model_id = MI_BA_SIMPLE_PINHOLE;
+      c.second.params = {1200, 30, 30};
+    }
     if (!s) return;
     const Reconstruction orig = rec;
     SemanticBundleAdjuster sba(options, config, maps);
@@ -448,7 +487,9 @@ int main(int argc, char** argv) {
         }
       maps.depth[im.name] = depth;
       maps.semantic[im.name] = label;
-      rec.GetCamera(im.camera_id).params = {1200, 30, 30, 0};
+      Camera& cam = rec.GetCamera(im.camera_id);
+      cam.model_id = MI_BA_SIMPLE_PINHOLE;
+      cam.params = {1200, 30, 30};
       im.tvec[0] += 0.02 * (double)im.image_id;
     }
     char tmpl[] = "/tmp/sba_out_XXXXXX";

@@ -101,7 +101,17 @@ int main(int argc, char** argv) {
       BundleAdjustmentConfig cfg;
       for (const auto& e : r.images) cfg.AddImage(e.first);
       const SemanticMaps maps = LoadSemanticMaps(argv[2], r, cfg);
-      std::printf("%d %d %zu %zu\n", maps.height, maps.width, maps.depth.size(), maps.semantic.size());
+      // the maps' size when every image shares it, else -1 -1 (each image keeps its own)
+      int h = -2, w = -2;
+      for (const auto& e : maps.sizes) {
+        if (h == -2) {
+          h = e.second.first;
+          w = e.second.second;
+        } else if (h != e.second.first || w != e.second.second) {
+          h = w = -1;
+        }
+      }
+      std::printf("%d %d %zu %zu\n", h, w, maps.depth.size(), maps.semantic.size());
     } else if (mode == "ba" && argc >= 4) {
       Reconstruction r;
       ReadModel(argv[2], &r);

@@ -11,6 +11,17 @@
 //                               file reported as the reference does (no GPU)
 //   ./sba_reference_test gpu    + the solve from the files, equal to the solve
 //                               with the same maps in memory
+//   ./sba_reference_test export DIR
+//                               the solve from the files, plus the flattened
+//                               problem it solved (the facade's own
+//                               internal::Flat / SemanticInputs) and its result
+//                               as raw arrays in DIR, for the oracle comparison
+//                               (tests/test_facade.py)
+//
+// The three images have different map sizes (60 x 60, 48 x 72, 66 x 54): the
+// reference samples each image on its own grid and bounds-checks against the
+// second image's own size (semantic_bundle_adjustment.cc:792-799,
+// semantic_cost_functions.h:163).
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -75,9 +86,12 @@ static void WriteFloatTiff(const std::string& path, int H, int W, const std::vec
   f.write(reinterpret_cast<const char*>(data.data()), bytes);
 }
 
-// Three cameras looking at a labelled plane (the facade SBA test's scene,
+// Three SIMPLE_PINHOLE cameras (the only model the reference's SBA accepts)
+// looking at a labelled plane (the facade SBA test's scene,
 // tests/cpp/bundle_adjustment_test.cc TestSemanticBundleAdjuster), image
-// names with an extension so the map stems are exercised.
+// names with an extension so the map stems are exercised, maps of three sizes.
+static const int kH[3] = {60, 48, 66}, kW[3] = {60, 72, 54};
+
 static Reconstruction Scene(SemanticMaps* maps) {
   std::mt19937 prng(0);
   auto U = [&](double a, double b) { return std::uniform_real_distribution<double>(a, b)(prng); };
@@ -87,14 +101,12 @@ static Reconstruction Scene(SemanticMaps* maps) {
     double xyz[3] = {U(-1, 1), U(-1, 1), U(-1, 1)};
     ids.push_back(rec.AddPoint3D(xyz));
   }
-  const int H = 60, W = 60;
-  maps->height = H;
-  maps->width = W;
   for (int i = 0; i < 3; ++i) {
+    const int H = kH[i], W = kW[i];
     Camera cam;
     cam.camera_id = (camera_t)i;
-    cam.model_id = MI_BA_SIMPLE_RADIAL;
-    cam.params = {1200, 30, 30, 0};
+    cam.model_id = MI_BA_SIMPLE_PINHOLE;
+    cam.params = {1200, 30, 30};
     rec.AddCamera(cam);
     Image im;
     im.image_id = (image_t)i;
@@ -121,6 +133,7 @@ static Reconstruction Scene(SemanticMaps* maps) {
       }
     maps->depth[im.name] = depth;
     maps->semantic[im.name] = label;
+    maps->sizes[im.name] = std::make_pair(H, W);
     im.tvec[0] += 0.002 * i;  // pose error for the semantic term to pull on
     rec.AddImage(im);
   }
@@ -138,9 +151,9 @@ static void WriteMaps(const std::string& dir, const Reconstruction& rec, const S
   for (const auto& e : rec.images) {
     const std::string& name = e.second.name;
     const std::string stem = name.substr(0, name.find_last_of('.'));
-    WriteFloatTiff(dir + "/depth_tiff/" + stem + "_depth.tiff", maps.height, maps.width, maps.depth.at(name));
-    WriteFloatTiff(dir + "/semantic_tiff/" + stem + "_semantic.tiff", maps.height, maps.width,
-                   maps.semantic.at(name));
+    const std::pair<int, int> hw = maps.Size(name);
+    WriteFloatTiff(dir + "/depth_tiff/" + stem + "_depth.tiff", hw.first, hw.second, maps.depth.at(name));
+    WriteFloatTiff(dir + "/semantic_tiff/" + stem + "_semantic.tiff", hw.first, hw.second, maps.semantic.at(name));
   }
 }
 
@@ -197,9 +210,9 @@ int main(int argc, char** argv) {
     BundleAdjustmentConfig config;
     for (image_t i = 0; i < 3; ++i) config.AddImage(i);
     const SemanticMaps back = LoadSemanticMaps(dir, scene, config);
-    CHECK_T(back.height == maps.height && back.width == maps.width);
     for (const auto& e : scene.images) {
       const std::string& n = e.second.name;
+      CHECK_T(back.Size(n) == maps.Size(n));
       CHECK_T(back.depth.at(n).size() == maps.depth.at(n).size());
       CHECK_T(std::memcmp(back.depth.at(n).data(), maps.depth.at(n).data(), 4 * maps.depth.at(n).size()) == 0);
       CHECK_T(std::memcmp(back.semantic.at(n).data(), maps.semantic.at(n).data(), 4 * maps.semantic.at(n).size()) ==
@@ -225,6 +238,87 @@ int main(int argc, char** argv) {
     CHECK_T(threw);
     if (std::system(("rm -rf '" + other + "'").c_str()) != 0) std::printf("  (could not remove %s)\n", other.c_str());
   }});
+  // Assert (cc:619-631): a camera other than SIMPLE_PINHOLE is refused with
+  // the reference's message unless allow_any_camera_model is set
+  cases.push_back({"TestCameraModelPrecondition", [&] {
+    SemanticBundleAdjustmentOptions options;
+    options.print_summary = false;
+    options.data_path = dir;
+    Reconstruction rec = scene;
+    Camera& c = rec.GetCamera(1);
+    c.model_id = MI_BA_SIMPLE_RADIAL;
+    c.params = {1200, 30, 30, 0};
+    bool solved = false;
+    std::string what;
+    try {
+      ReferenceSolve(options, &rec, &solved);
+    } catch (const std::runtime_error& e) {
+      what = e.what();
+    }
+    CHECK_T(what == "ERROR: the only supported camera model is SimplePinholeCameraModel.");
+  }});
+  if (mode == "export") {
+    // the facade's TIFF solve and the flattened problem it solved, for the
+    // oracle (tests/test_facade.py::test_sba_mixed_sizes_match_oracle)
+    cases.push_back({"TestExportForOracle", [&] {
+      if (argc < 3) throw std::runtime_error("export needs a directory");
+      const std::string out = argv[2];
+      SemanticBundleAdjustmentOptions options;
+      options.print_summary = false;
+      options.error_computation_pixel_step = 3;
+      options.data_path = dir;
+      Reconstruction a = scene;
+      bool solved = false;
+      const SolverSummary sa = ReferenceSolve(options, &a, &solved);
+      CHECK_T(solved);
+      // the problem Solve flattened (its config is the controller's, above)
+      SemanticBundleAdjustmentConfig config;
+      const std::vector<image_t> reg = scene.RegImageIds();
+      for (const image_t id : reg) config.AddImage(id);
+      config.SetConstantPose(reg[0]);
+      config.SetConstantTvec(reg[1], {0});
+      for (const image_t id : reg) config.SetConstantCamera(scene.GetImage(id).CameraId());
+      internal::Flat flat;
+      flat.Build(scene, config);
+      internal::SemanticInputs in;
+      in.Build(flat, scene, config, LoadSemanticMaps(dir, scene, config), options);
+      internal::Flat fin;
+      fin.Build(a, config);
+      auto put = [&](const std::string& name, const void* data, size_t bytes) {
+        std::ofstream f(out + "/" + name, std::ios::binary);
+        f.write(reinterpret_cast<const char*>(data), (std::streamsize)bytes);
+      };
+      put("camera_params.f64", flat.cam_params.data(), 8 * flat.cam_params.size());
+      put("camera_models.i32", flat.cam_models.data(), 4 * flat.cam_models.size());
+      put("camera_constant.u8", flat.cam_const.data(), flat.cam_const.size());
+      put("qvec.f64", flat.qvec.data(), 8 * flat.qvec.size());
+      put("tvec.f64", flat.tvec.data(), 8 * flat.tvec.size());
+      put("image_camera.i32", flat.image_camera.data(), 4 * flat.image_camera.size());
+      put("image_in_config.u8", flat.img_cfg.data(), flat.img_cfg.size());
+      put("image_constant_pose.u8", flat.img_cpose.data(), flat.img_cpose.size());
+      put("image_constant_tvec.u8", flat.img_ctvec.data(), flat.img_ctvec.size());
+      put("image_height.i32", in.img_h.data(), 4 * in.img_h.size());
+      put("image_width.i32", in.img_w.data(), 4 * in.img_w.size());
+      put("pairs.i32", in.pairs.data(), 4 * in.pairs.size());
+      put("depth.f32", in.depth.data(), 4 * in.depth.size());
+      put("label.f32", in.label.data(), 4 * in.label.size());
+      put("final_qvec.f64", fin.qvec.data(), 8 * fin.qvec.size());
+      put("final_tvec.f64", fin.tvec.data(), 8 * fin.tvec.size());
+      std::ofstream m(out + "/summary.txt");
+      char buf[512];
+      std::snprintf(buf, sizeof(buf),
+                    "pixel_step %d\ndepth_error_threshold %.17g\nnumeric_relative_step_size %.17g\n"
+                    "max_num_iterations %d\nfunction_tolerance %.17g\ngradient_tolerance %.17g\n"
+                    "parameter_tolerance %.17g\nnum_residuals_reduced %lld\ninitial_cost %.17g\nfinal_cost %.17g\n"
+                    "num_successful_steps %d\nnum_unsuccessful_steps %d\ntermination_type %d\n",
+                    options.error_computation_pixel_step, options.depth_error_threshold,
+                    options.numeric_relative_step_size, options.solver_options.max_num_iterations,
+                    options.solver_options.function_tolerance, options.solver_options.gradient_tolerance,
+                    options.solver_options.parameter_tolerance, (long long)sa.num_residuals_reduced, sa.initial_cost,
+                    sa.final_cost, sa.num_successful_steps, sa.num_unsuccessful_steps, (int)sa.termination_type);
+      m << buf;
+    }});
+  }
   if (mode == "gpu") {
     // the reference construction solving from the files takes exactly the
     // steps of the in-memory form

@@ -76,7 +76,7 @@ def test_default_options_match_reference():
 
 def test_abi_version_and_params():
     lib = mi_ba.load()
-    assert lib.mi_ba_abi_version() == 3
+    assert lib.mi_ba_abi_version() == 4
     for m, n in mi_ba.NUM_PARAMS.items():
         assert lib.mi_ba_num_params(m) == n
     assert lib.mi_ba_num_params(99) == -1
