@@ -222,39 +222,39 @@ def cpu_baseline(opts, sc, sem, cfg, nb, ns):
 
 def roofline_semantic(config, ns, avg_ms):
     """The semantic linearization (two-pass route: flat pass + deferred-sample
-    pass, timed together) against both roofs: FP64 from PMC operation counts,
-    HBM from PMC traffic, per linearization, over the time measured here (HIP
-    events on the context stream).  SURVEY 8d expected it FP64-bound; since
-    the flat test skips the stencil of most samples the raster gathers bind
-    it.  `bound` names the roof with the larger fraction and `achieved` /
-    `peak` / `unit` / `frac` are that roof's.
-    Algorithmic bytes: SURVEY 8d's 128 B per sample (16 sample in, 8
-    compulsory raster gather, 8 residual + 96 tangent-Jacobian row out) is the
-    J-materialising definition; the product reduces the rows into the per-pair
-    J'J / J'r blocks instead of writing them, so its own algorithmic traffic is
-    32 (sample record) + 8 (raster gather) = 40 B per sample.  Both are
-    reported; the HBM fraction uses the measured (PMC) traffic."""
+    pass, timed together; HIP events on the context stream) against both
+    roofs, on ALGORITHMIC work:
+      * HBM: SURVEY 8d's 128 B per sample (16 sample in, 8 compulsory raster
+        gather, 8 residual + 96 tangent-Jacobian row out — the J-materialising
+        definition, kept although the product reduces the rows into per-pair
+        J'J / J'r blocks instead of writing them) x samples / time;
+      * FP64: the PMC FP64 operation count per linearization (ADD/MUL/TRANS 1,
+        FMA 2, x 64 lanes) / time, against 78.6 TF/s.
+    `bound` names the roof with the larger fraction; `achieved` / `peak` /
+    `unit` / `frac` are that roof's.  The measured (PMC) HBM traffic is
+    `traffic` only: it is not the numerator of any fraction (a kernel that
+    re-reads would otherwise score higher)."""
     flops, hbm, src = semantic_pmc(config)
-    if avg_ms <= 0:
+    if avg_ms <= 0 or not ns:
         return None
     t = avg_ms * 1e-3
+    alg = 128.0 * ns
+    f_hbm = alg / t / 1e9 / HBM_PEAK_GBS
     f_fp64 = flops / t / 1e12 / FP64_PEAK_TFS if flops else 0.0
-    f_hbm = hbm / t / 1e9 / HBM_PEAK_GBS if hbm else 0.0
-    hbm_bound = f_hbm > f_fp64
-    out = {"kernel": "semantic_flat+semantic_deferred", "bound": "hbm" if hbm_bound else "fp64",
-           "unit": "GB/s" if hbm_bound else "TFLOP/s",
-           "peak": HBM_PEAK_GBS if hbm_bound else FP64_PEAK_TFS,
-           "achieved": (hbm / t / 1e9 if hbm_bound else flops / t / 1e12) if (hbm or flops) else None,
-           "frac": (f_hbm if hbm_bound else f_fp64) if (hbm or flops) else None,
-           "fp64_achieved_TFs": flops / t / 1e12 if flops else None, "fp64_frac": f_fp64 if flops else None,
-           "fp64_ops_per_launch": flops,
-           "hbm_achieved_GBs": hbm / t / 1e9 if hbm else None, "hbm_frac": f_hbm if hbm else None,
-           "traffic": hbm, "traffic_unit": "bytes/launch",
-           "traffic_bytes_per_sample": hbm / ns if hbm and ns else None,
-           "algorithmic_bytes_per_sample_survey": 128, "algorithmic_bytes_per_sample_fused": 40,
-           "algorithmic_GBs_survey": 128.0 * ns / t / 1e9, "algorithmic_GBs_fused": 40.0 * ns / t / 1e9,
-           "samples_per_launch": ns, "avg_launch_ms": avg_ms, "pmc_source": src}
-    return out
+    hbm_bound = f_hbm >= f_fp64
+    return {"kernel": "semantic_flat+semantic_deferred", "bound": "hbm" if hbm_bound else "fp64",
+            "unit": "GB/s" if hbm_bound else "TFLOP/s",
+            "peak": HBM_PEAK_GBS if hbm_bound else FP64_PEAK_TFS,
+            "achieved": alg / t / 1e9 if hbm_bound else flops / t / 1e12,
+            "frac": f_hbm if hbm_bound else f_fp64,
+            "algorithmic_bytes_per_sample": 128, "algorithmic_bytes_per_launch": alg,
+            "hbm_algorithmic_GBs": alg / t / 1e9, "hbm_algorithmic_frac": f_hbm,
+            "fp64_achieved_TFs": flops / t / 1e12 if flops else None, "fp64_frac": f_fp64 if flops else None,
+            "fp64_ops_per_launch": flops,
+            "traffic": hbm, "traffic_unit": "bytes/launch (PMC FETCH_SIZE x 2 + WRITE_SIZE; not a numerator)",
+            "traffic_bytes_per_sample": hbm / ns if hbm else None,
+            "traffic_GBs": hbm / t / 1e9 if hbm else None,
+            "samples_per_launch": ns, "avg_launch_ms": avg_ms, "pmc_source": src}
 
 
 def main():

@@ -955,6 +955,10 @@ DenseFactorFn g_dense_factor = nullptr;
 // iteration that ended the solve).
 int32_t* g_trace = nullptr;
 int g_trace_cap = 0;
+// ... and its values (oracle_set_trace_values): per iteration k >= 1 with a
+// valid step, entries [4k-4, 4k) = step_norm (ambient |x - candidate_x|), the
+// parameter tolerance's bound tol (|x| + tol), cost change, model cost change
+double* g_trace_v = nullptr;
 
 bool Cholesky(std::vector<double>& A, int n) {  // in place, lower
   if (g_dense_factor) return g_dense_factor(A.data(), n) == 0;
@@ -1602,6 +1606,9 @@ void oracle_set_trace(int32_t* buf, int cap) {
   g_trace = buf;
   g_trace_cap = buf ? cap : 0;
 }
+// With a trace set: also record the step values into vbuf (4 doubles per
+// iteration, the same cap); null turns it off.
+void oracle_set_trace_values(double* vbuf) { g_trace_v = vbuf; }
 
 }  // extern "C"
 
@@ -2266,6 +2273,13 @@ int SolveImpl(const mi_ba_options* o, mi_ba_problem* p, const mi_ba_semantic* se
     const double cost_change = x_cost - candidate_cost;
     const double relative_decrease = cost_change / model_cost_change;
     const bool success = relative_decrease > o->min_relative_decrease;
+    if (g_trace_v && iteration >= 1 && iteration <= g_trace_cap) {
+      double* v = g_trace_v + 4 * (size_t)(iteration - 1);
+      v[0] = std::sqrt(step_norm2);
+      v[1] = o->parameter_tolerance * (std::sqrt(x_norm2) + o->parameter_tolerance);
+      v[2] = cost_change;
+      v[3] = model_cost_change;
+    }
     if (std::sqrt(step_norm2) <= o->parameter_tolerance * (std::sqrt(x_norm2) + o->parameter_tolerance) ||
         std::fabs(cost_change) <= o->function_tolerance * x_cost) {
       restore();

@@ -81,6 +81,8 @@ def load():
     lib.oracle_set_dense_factor.restype = None
     lib.oracle_set_trace.argtypes = [_i32p, C.c_int]
     lib.oracle_set_trace.restype = None
+    lib.oracle_set_trace_values.argtypes = [_dp]
+    lib.oracle_set_trace_values.restype = None
     _lib = lib
     return lib
 
@@ -367,19 +369,26 @@ def solve(options, scene, semantic=None):
     return s
 
 
-def solve_traced(options, scene, semantic=None):
+def solve_traced(options, scene, semantic=None, return_values=False):
     """oracle.solve plus the per-iteration LM trace: an int32 array
     [iterations][4] = (step valid, step successful, linear solver iterations,
     1 on the iteration that ended the solve), rows of iterations that did not
-    run are -1."""
+    run are -1; with return_values also a float array [iterations][4] =
+    (step norm, the parameter tolerance's bound, cost change, model cost
+    change) of each valid step (NaN elsewhere)."""
     cap = max(1, int(options.max_num_iterations))
     buf = np.full((cap, 4), -1, np.int32)
+    vals = np.full((cap, 4), np.nan)
     lib = load()
     lib.oracle_set_trace(buf.ctypes.data_as(_i32p), cap)
+    lib.oracle_set_trace_values(vals.ctypes.data_as(_dp))
     try:
         s = solve(options, scene, semantic)
     finally:
         lib.oracle_set_trace(None, 0)
+        lib.oracle_set_trace_values(None)
+    if return_values:
+        return s, buf, vals
     return s, buf
 
 

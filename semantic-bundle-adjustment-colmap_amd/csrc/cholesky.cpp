@@ -1347,10 +1347,17 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(double* __restrict__ 
       // through T: each wave stores whole 512-byte column segments
       pf_acc_to_lds(out, T, wv, lane);
       __syncthreads();
+      // L_rc is read back by this workgroup's next column steps (pf_stages
+      // stages L_rk with sc1 loads under panel_wait 2): stored the hand-off
+      // way — write-through, drained by every storing wave before the
+      // barrier — so that no later load of another wave can overtake a store
+      // still in flight (the invariant of the sc1 hand-off: every handed-off
+      // byte stored sc1 and drained, then read by sc1 loads)
       for (int e = threadIdx.x; e < 64 * 64; e += 256) {
         const int i = e & 63, jj = e >> 6;
-        if (i < hr && jj < wc) A[(size_t)(c0 + jj) * lda + r0 + i] = T[i * kPfLd + jj];
+        if (i < hr && jj < wc) pf_st<WT>(A + (size_t)(c0 + jj) * lda + r0 + i, T[i * kPfLd + jj]);
       }
+      pf_drain<WT>();
       stamp(2 + 2 * c);
       __syncthreads();  // T and Li are restaged next step
     }

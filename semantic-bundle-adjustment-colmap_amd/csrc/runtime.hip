@@ -960,6 +960,10 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
 void context_destroy(mi_ba_context* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  // collectives still pending (a solve that returned on another error after
+  // enqueuing them): waited on against their deadline first, a dead peer
+  // aborting the communicator, so that the stream sync below cannot hang
+  if (ctx->comm && ctx->comm_due > 0.0) (void)comm_drain(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   semantic_destroy(ctx);
   gsba_destroy(ctx);
@@ -1615,7 +1619,11 @@ mi_ba_status context_solve(mi_ba_context* ctx, mi_ba_summary* sum) {
     }
     // one rank: the Schur terms (fabric-bound pair gathers) on lm_side beside
     // the camera-block pass (HBM-bound row gathers); both only add into S
-    const bool schur_side = ctx->dense && !ctx->distributed() && ctx->schur_overlap;
+    // the side stream only with float-atomic flushes: the deterministic
+    // flushes (det_sums) update S's diagonal blocks by plain read-modify-write
+    // in FlushDense and in the Schur pair / owner flushes, which must not run
+    // concurrently
+    const bool schur_side = ctx->dense && !ctx->distributed() && ctx->schur_overlap && !ctx->det_sums;
     if (schur_side) {
       if (!ctx->lm_side) {
         if (hipStreamCreateWithFlags(&ctx->lm_side, hipStreamNonBlocking) != hipSuccess) {

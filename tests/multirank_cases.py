@@ -31,6 +31,22 @@ def make_case(name):
         rng = np.random.default_rng(2)
         sc.tvec[2:] += rng.uniform(-0.02, 0.02, sc.tvec[2:].shape)
         return sc, sem, mi_ba.default_options(max_num_iterations=10, semantic_weight=0.01, eta=1e-12)
+    if name in ("c2", "c2_pcg"):
+        # C2 (200 SIMPLE_RADIAL cameras, 50k points, 500k observations) with a
+        # semantic term: pairs (i, i + 1), (i, i + 2) sampled every 25 pixels
+        # of the 1000 x 1000 maps (640k samples), 5 LM iterations; exact Schur
+        # (nf = 1593, S summed in bands) or ITERATIVE_SCHUR at the bench's
+        # N > 1 settings (eta 0.1)
+        I = 200
+        sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, I, 50_000, track_length=10,
+                                                     rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=0)).gauge()
+        depth, label = mi_ba.render_semantic(sc, 1000, 1000, plane_z=1.0, cell=0.1)
+        pairs = np.array([(i, (i + d) % I) for i in range(I) for d in (1, 2)], np.int32)
+        sem = mi_ba.SemanticInput(depth, label, pairs, pixel_step=25)
+        opts = mi_ba.default_options(max_num_iterations=5)
+        if name == "c2_pcg":
+            opts.linear_solver_type = mi_ba.SOLVER_ITERATIVE_SCHUR
+        return sc, sem, opts
     if name in ("geo_pcg", "sem_pcg"):
         # ITERATIVE_SCHUR: one nf-vector all-reduce per Schur product; eta small
         # so the linear solves are exact to rounding

@@ -23,7 +23,12 @@
     converged cost (1e-6 relative) is compared, and the parameter difference
     is shown to lie along the problem's near-null direction (tests/valley.py).
     Step-for-step against the oracle's own PCG: tests/test_lm_semantics.py.
+  * C4 LM: the first iteration against the oracle live; the bench's three
+    iterations against the oracle's committed trajectory
+    (tests/golden/c4_lm3.json).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -31,6 +36,7 @@ import mi_ba
 import oracle
 
 pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 OPENCV_EXTRA = (-0.1, 0.01, 1e-4, -1e-4)
 
@@ -251,6 +257,46 @@ def test_c4_lm_first_iteration_matches_oracle(gpu):
     for name, x0 in (("qvec", q0), ("tvec", sc.tvec), ("xyz", sc.xyz), ("camera_params", sc.camera_params)):
         dg, do = getattr(g, name) - x0, getattr(o, name) - x0
         assert np.abs(dg - do).max() <= 1e-6 * max(np.abs(do).max(), 1e-300), name
+
+
+def test_c4_lm_three_iterations_match_fixture(gpu):
+    """The bench's BA-iteration leg itself — 3 exact-Schur LM iterations on
+    C4 with the 5.0M-sample semantic term — against the oracle's trajectory
+    on the same scene, committed as tests/golden/c4_lm3.json (written in the
+    container by tests/golden/make_c4_lm_fixture.py; the oracle's C4 LM takes
+    minutes of host time per iteration, too long for a GPU test).  Pass: the
+    same accept / reject sequence, initial cost within 1e-12, final cost
+    within 1e-6 relative (north-star tolerance), per parameter block type the
+    largest change within 1e-6 relative and every sampled parameter's change
+    within 1e-6 of that block type's largest change."""
+    import json
+    import bench
+    fx = json.load(open(os.path.join(HERE, "golden", "c4_lm3.json")))
+    sc, sem = bench.build_shard(bench.CONFIGS["C4"], 0, 1)
+    rec = {}
+    opts = mi_ba.default_options(max_num_iterations=fx["options"]["max_num_iterations"])
+    opts.set_callback(lambda it: rec.__setitem__(it.iteration, (it.step_is_valid, it.step_is_successful)))
+    g = sc.copy()
+    with mi_ba.Context(opts, g, sem) as ctx:
+        s = ctx.solve()
+        ctx.writeback()
+    assert s.num_residuals_reduced == fx["num_residuals_reduced"]
+    assert s.num_semantic_residuals == fx["num_semantic_residuals"]
+    assert (s.num_successful_steps, s.num_unsuccessful_steps) == \
+        (fx["num_successful_steps"], fx["num_unsuccessful_steps"])
+    for k, (valid, succ, _) in enumerate(fx["trace"], start=1):
+        assert rec[k] == (valid, succ), (k, rec[k])
+    assert abs(s.initial_cost - fx["initial_cost"]) <= 1e-12 * fx["initial_cost"]
+    assert abs(s.final_cost - fx["final_cost"]) <= 1e-6 * fx["final_cost"], (s.final_cost, fx["final_cost"])
+    q0 = sc.qvec / np.linalg.norm(sc.qvec, axis=1, keepdims=True)
+    d = {"qvec": g.qvec - q0, "tvec": g.tvec - sc.tvec, "xyz": g.xyz - sc.xyz,
+         "camera_params": g.camera_params - sc.camera_params}
+    smp = fx["sample"]
+    idx = {"qvec": smp["images"], "tvec": smp["images"], "xyz": smp["points"], "camera_params": smp["cameras"]}
+    for name, v in d.items():
+        m = fx["max_change"][name]
+        assert abs(np.abs(v).max() - m) <= 1e-6 * m, (name, np.abs(v).max(), m)
+        assert np.abs(v[idx[name]] - np.asarray(smp[name])).max() <= 1e-6 * m, name
 
 
 def test_c3_window_summary_flat_pass_bitwise(gpu):

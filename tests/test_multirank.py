@@ -1,13 +1,16 @@
 """Multi-rank LM (point-sharded).
 
-CPU (gloo, world 2): the shard partition and the host reducer.
+CPU (gloo, world 2): the shard partition (worlds 2, 3, 4, 8) and the host
+reducer.
 GPU: two ranks on the one visible MI355X, sums through gloo
 (exact Schur: S summed in 512-row bands of its upper triangle; ITERATIVE_SCHUR:
 one nf-vector sum per Schur product)
 (mi_ba_context_set_host_reducer), against the single-process solve of the
 same scene — final cost within 1e-6 relative (north-star tolerance; the two
 runs sum in different orders), cameras/poses bitwise equal across ranks,
-points within 1e-5.  The RCCL path (mi_ba_context_set_comm) needs one GPU per
+points within 1e-5; and C5's shape at C2 size over 4 and 8 ranks
+(exact and PCG, with semantics) against the single-rank solve and the
+oracle.  The RCCL path (mi_ba_context_set_comm) needs one GPU per
 rank and runs on multi-GPU nodes only.
 """
 import json
@@ -56,7 +59,7 @@ def test_gloo_host_reducer_world2():
         assert out[r] == (np.arange(5) * 3.0).tolist()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_shard_partition(world):
     sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 5, 101, track_length=3))
     depth = np.zeros((5, 8, 8), np.float32)
@@ -74,6 +77,58 @@ def test_shard_partition(world):
         pairs += [tuple(x) for x in ss.pairs]
     assert np.all(seen == 1)
     assert sorted(pairs) == sorted(tuple(x) for x in sem.pairs)
+
+
+def run_ranks(world, case, tmp_path, timeout=300):
+    port = _free_port()
+    outs = [tmp_path / f"r{r}.json" for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "multirank_worker.py"), "--rank", str(r),
+                               "--world", str(world), "--port", str(port), "--case", case, "--out", str(outs[r])])
+             for r in range(world)]
+    try:
+        for p in procs:
+            assert p.wait(timeout=timeout) == 0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return [json.load(open(o)) for o in outs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["c2", "c2_pcg"])
+@pytest.mark.parametrize("world", [4, 8])
+def test_c2_multi_rank_matches_single_and_oracle(gpu, world, case, tmp_path):
+    """C5's shape at C2 size: the scene point-sharded over 4 or 8 ranks (gloo
+    host reducer, every rank a context on the one card; uneven point and pair
+    shards, S or the Schur products summed from 4 / 8 partial contributions),
+    exact Schur and ITERATIVE_SCHUR at eta 0.1, with a semantic term.  Each
+    rank's result against the single-rank solve and the oracle's LM (the same
+    solver: its dense Schur, or its restatement of Ceres' PCG) on the
+    unsharded scene: the same step counts, final cost within 1e-6 relative
+    (north-star tolerance), cameras and poses bitwise equal across ranks and
+    within 1e-6 of the single-rank solve's, each rank's points within 1e-5."""
+    import oracle
+    res = run_ranks(world, case, tmp_path, timeout=600)
+    sc, sem, opts = mc.make_case(case)
+    full = sc.copy()
+    s1 = mi_ba.solve(opts, full, sem)
+    s_o = oracle.solve(mc.make_case(case)[2], sc.copy(), sem)  # the oracle's LM, same solver (its restated Ceres PCG)
+    for r in res:
+        assert abs(r["initial_cost"] - s_o.initial_cost) <= 1e-12 * s_o.initial_cost
+        assert (r["successful"], r["unsuccessful"]) == (s1.num_successful_steps, s1.num_unsuccessful_steps)
+        assert abs(r["final_cost"] - s1.final_cost) <= 1e-6 * s1.final_cost, (r["final_cost"], s1.final_cost)
+        assert abs(r["final_cost"] - s_o.final_cost) <= 1e-6 * s_o.final_cost, (r["final_cost"], s_o.final_cost)
+    assert (res[0]["successful"], res[0]["unsuccessful"]) == (s_o.num_successful_steps, s_o.num_unsuccessful_steps)
+    for r in res[1:]:
+        for key in ("qvec", "tvec", "camera_params"):
+            assert r[key] == res[0][key], key
+    assert np.abs(np.array(res[0]["qvec"]) - full.qvec).max() <= 1e-6
+    assert np.abs(np.array(res[0]["camera_params"]) - full.camera_params).max() <= 1e-6 * np.abs(full.camera_params).max()
+    for r in res:
+        p0, p1 = r["points"]
+        assert p1 > p0
+        assert np.abs(np.array(r["xyz"]).reshape(-1, 3) - full.xyz[p0:p1]).max() <= 1e-5
 
 
 @pytest.mark.gpu
