@@ -1949,7 +1949,16 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
     auto launch_panel = [&]() -> rocblas_status {
       if (hipEventRecord(upd, sm) != hipSuccess || hipStreamWaitEvent(ss, upd, 0) != hipSuccess)
         return rocblas_status_internal_error;
-      rocblas_status ps_ = panel_factor(hs, n, A, lda, k + kb, jb0, info + kk + 1, own_for(k + kb), scratch_side, &ws, ex);
+      rocblas_status ps_;
+      if (cfg.split_panel_cols > 0 && k + kb < cfg.split_panel_cols && own_for(k + kb) == 6) {
+        // split panel (CholConfig::split_panel_cols): the diagonal block's row
+        // tiles, then the rows below them, one launch after the other on the
+        // side stream (the same kernel and flags: bitwise the one-launch factor)
+        ps_ = panel_factor_fused(ss, n, A, lda, k + kb, jb0, info + kk + 1, &ws, ex, 1);
+        if (ps_ == rocblas_status_success) ps_ = panel_factor_fused(ss, n, A, lda, k + kb, jb0, info + kk + 1, &ws, ex, 2);
+      } else {
+        ps_ = panel_factor(hs, n, A, lda, k + kb, jb0, info + kk + 1, own_for(k + kb), scratch_side, &ws, ex);
+      }
       if (ps_ != rocblas_status_success) return ps_;
       return hipEventRecord(pan, ss) == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
     };

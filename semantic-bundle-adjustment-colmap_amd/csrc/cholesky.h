@@ -53,6 +53,13 @@ struct CholConfig {
   // beside it (the panel's resident workgroups then never share CUs with the
   // dgemm); 0 = off
   int serial_head_cols = 0;
+  // split panel: the panels starting before split_panel_cols are factored in
+  // two launches on the look-ahead side stream — the diagonal block's row
+  // tiles (the serial chain of 64x64 tile factors: kb / 64 workgroups), then,
+  // with every flag already set, the rows below it — so that while the chain
+  // runs only kb / 64 CUs are held instead of one per row tile of the panel
+  // (the trailing dgemm beside it gets the others).  0: one launch
+  int split_panel_cols = 0;
   // split tail: the below-rows launch on the second trailing-update stream
   // (rest_streams >= 2; that panel's whole trailing update then on the
   // caller's stream) instead of a fourth stream

@@ -2503,6 +2503,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.split_tail_cols = value;
     return MI_BA_OK;
   }
+  if (std::strcmp(key, "cholesky_split_panel_cols") == 0 && value >= 0) {
+    ctx->chol.split_panel_cols = value;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_serial_head_cols") == 0 && value >= 0 && ab_value(value, 0)) {
     ctx->chol.serial_head_cols = value;
     return MI_BA_OK;

@@ -282,6 +282,28 @@ def test_lm_handoff_variants_bitwise(gpu):
         assert r == res[0]
 
 
+def test_lm_split_panel_bitwise(gpu):
+    """Split panel (cholesky_split_panel_cols): the diagonal block's row tiles
+    and the rows below it in two launches, one after the other, on the
+    look-ahead stream (the same kernel, flags and GEMMs) — the LM bit for bit
+    the one-launch panel's (nf = 1593, 4 panels; split for the first 1024
+    columns and for all of them)."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for cols in (0, 1024, 100000):
+        b = sc.copy()
+        with mi_ba.Context(opts, b) as ctx:
+            ctx.set_tuning("cholesky_split_panel_cols", cols)
+            s = ctx.solve()
+            ctx.writeback()
+        res.append((s.num_successful_steps, s.num_unsuccessful_steps, s.final_cost,
+                    b.qvec.tobytes(), b.tvec.tobytes(), b.xyz.tobytes(), b.camera_params.tobytes()))
+    for r in res[1:]:
+        assert r == res[0]
+
+
 def test_lm_split_tail(gpu):
     """Split tail (cholesky_split_tail_cols, tools build): the next panel's
     block column updated in two dgemms and the panel's below-diagonal rows as

@@ -47,8 +47,11 @@ out = {"workload": f"{args.config}: {c['desc']}" + (" (geometric part)" if sem i
        "cpu_setup_s": t_setup, "cpu_final_cost": s.final_cost,
        "num_semantic_residuals": int(s.num_semantic_residuals)}
 if not args.no_gpu:
-    with mi_ba.Context(opts, sc.copy(), sem) as ctx:
-        g = ctx.solve()
+    # the GPU solve twice, the second reported: the first pays the lazy
+    # code-object loads of every LM kernel (bench.py warms them on a small scene)
+    for _ in range(2):
+        with mi_ba.Context(opts, sc.copy(), sem) as ctx:
+            g = ctx.solve()
     out.update({"gpu_ms_per_iteration": 1e3 * g.total_time_in_seconds / max(1, g.num_successful_steps +
                                                                              g.num_unsuccessful_steps),
                 "gpu_final_cost": g.final_cost})
