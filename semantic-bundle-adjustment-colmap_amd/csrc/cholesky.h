@@ -58,7 +58,12 @@ struct CholConfig {
   // tiles (the serial chain of 64x64 tile factors: kb / 64 workgroups), then,
   // with every flag already set, the rows below it — so that while the chain
   // runs only kb / 64 CUs are held instead of one per row tile of the panel
-  // (the trailing dgemm beside it gets the others).  0: one launch
+  // (the trailing dgemm beside it gets the others).  0: one launch.  Tools
+  // build only: slower at every width — Cholesky 14.40 / 14.77-14.93 / 15.76
+  // / 16.92 ms splitting the panels before 4096 / 6144 / 8192 / all columns
+  // vs 13.95-14.08 ms (profiles/r6c_ab_cholesky_split_panel.jsonl): the
+  // panel's latency stays on the critical path, the freed CUs do not make
+  // the dgemm beside it faster by as much
   int split_panel_cols = 0;
   // split tail: the below-rows launch on the second trailing-update stream
   // (rest_streams >= 2; that panel's whole trailing update then on the

@@ -2503,7 +2503,8 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     ctx->chol.split_tail_cols = value;
     return MI_BA_OK;
   }
-  if (std::strcmp(key, "cholesky_split_panel_cols") == 0 && value >= 0) {
+  // tools build: measured slower at every width (profiles/r6c_ab_cholesky_split_panel.jsonl)
+  if (std::strcmp(key, "cholesky_split_panel_cols") == 0 && value >= 0 && ab_value(value, 0)) {
     ctx->chol.split_panel_cols = value;
     return MI_BA_OK;
   }

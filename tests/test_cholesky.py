@@ -287,7 +287,9 @@ def test_lm_split_panel_bitwise(gpu):
     and the rows below it in two launches, one after the other, on the
     look-ahead stream (the same kernel, flags and GEMMs) — the LM bit for bit
     the one-launch panel's (nf = 1593, 4 panels; split for the first 1024
-    columns and for all of them)."""
+    columns and for all of them).  Tools build (measured slower)."""
+    if not mi_ba.ab_build():
+        pytest.skip("split panel: tools build only (MI_BA_LIB=ab)")
     sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
