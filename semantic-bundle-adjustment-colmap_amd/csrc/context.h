@@ -166,6 +166,7 @@ struct mi_ba_context {
   miba::DevArray<double> popart;           // [nochunk][64]
   int npodest = 0, npochunk = 0;
   miba::DevArray<uint2> pairs;             // (a, b) block pairs bucketed by image pair
+  miba::DevArray<uint2> pairs_pos;         // the same pairs as camera-major positions (Z rows of zorder 1)
   int nptiles = 0;
   miba::DevArray<int32_t> info;
   miba::CholConfig chol;                   // factorisation variant (mi_ba_set_tuning)

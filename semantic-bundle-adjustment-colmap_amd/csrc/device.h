@@ -124,6 +124,8 @@ struct DevProblem {
   int jvariant;        // Jacobian store path (kernels.hip reproj_jacobian_kernel V)
   int svariant;        // explicit Schur pair kernel (kernels.hip launch_dense_schur)
   int fvariant;        // fblock kernels: 0 default; 1 exact path LDS-staged MFMA, 2 PCG path one lane per block (tools build)
+  int sself1;          // schur_pairs_kernel: self tiles with one Z load per pair (1) or two (0)
+  int zorder;          // Schur factors Z: 0 rows in block order, 1 in image (cm_perm) order with pairs in positions
   // inputs
   const double2* obs_xy;
   const uint32_t* obs_img;

@@ -152,7 +152,7 @@ void launch_plus(const DevProblem& p, const double* df, const double* dX, const 
 // launch_fblock_dense added it) - sum_p W_p V_p^-1 W_p' (Z factors, then MFMA
 // image-pair tiles).
 void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
-                        const double* J, const double* Linv, double* Z, const DevPairTile* ptiles, int nptiles,
+                        const uint32_t* cm_ptv, const double* J, const double* Linv, double* Z, const DevPairTile* ptiles, int nptiles,
                         const uint2* pairs, double* S, bool with_u, hipStream_t s, const PairFlush* pflush = nullptr);
 // S_kk += Lambda_k on parameter slots, S_kk = 1 on non-parameter slots.
 void launch_dense_finalize(const DevProblem& p, const double* lambda_f, double* S, hipStream_t s);

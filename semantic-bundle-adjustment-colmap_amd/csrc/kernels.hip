@@ -272,6 +272,33 @@ __device__ inline void wave_load_rows_u(const double* __restrict__ src, double* 
   }
 }
 
+// As wave_load_rows_u for the rows idx[0..nrows) of src (idx: the wave's 64
+// row indices, one per lane; a lane's element finds its row's index by
+// ds_bpermute).
+template <int R, int LS, int NR>
+__device__ inline void wave_gather_rows_u(const double* __restrict__ src, uint32_t idx, double* __restrict__ dst,
+                                          int nrows) {
+  constexpr int T = (NR * R + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int total = nrows * R;
+  double v[T];
+#pragma unroll
+  for (int i = 0; i < T; ++i) {
+    const int e = lane + 64 * i;
+    const int row = e / R;
+    const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((row & 63) << 2, (int)idx);
+    v[i] = e < total ? __builtin_nontemporal_load(src + (size_t)r * R + (e - row * R)) : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < T; ++i) {
+    const int e = lane + 64 * i;
+    if (e < total) {
+      const int row = e / R;
+      dst[row * LS + (e - row * R)] = v[i];
+    }
+  }
+}
+
 // One lane per reduced block, one wavefront per 64 consecutive blocks; the
 // kernel writes residuals, tangent Jacobian rows and a per-workgroup cost
 // partial, nothing else (the point/camera normal-equation blocks are reduced
@@ -2812,9 +2839,14 @@ __global__ __launch_bounds__(kBlock) void dense_u_kernel(DevProblem p, const Dev
 // Z_a (k-major: Z[b][k*F + m]) of every block of a variable point; zero for
 // blocks of constant points.  J rows are read and Z rows written through the
 // wave's LDS slab (coalesced 8-B-per-lane transfers).
-template <int CT>
+// PERM (zorder 1): Z's row i is the block at camera-major position i
+// (cm_perm[i]; its J row gathered), so one image's Z rows are one contiguous
+// range and a pair tile's gathers stay inside two such ranges.
+template <int CT, bool PERM = false>
 __global__ __launch_bounds__(kBlock) void schur_z_kernel(DevProblem p, const double* __restrict__ J,
-                                                          const double* __restrict__ Linv, double* __restrict__ Z) {
+                                                          const double* __restrict__ Linv, double* __restrict__ Z,
+                                                          const uint32_t* __restrict__ cm_perm = nullptr,
+                                                          const uint32_t* __restrict__ cm_ptv = nullptr) {
   constexpr int F = 6 + CT, W = 9 + CT, W2 = 2 * W, LS = W2 | 1;
   constexpr int ZN = 3 * F, ZS = ZN | 1;
   constexpr int SL = (LS > ZS ? LS : ZS) * 64;
@@ -2824,7 +2856,10 @@ __global__ __launch_bounds__(kBlock) void schur_z_kernel(DevProblem p, const dou
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t wb0 = i - lane;
   const int live = wb0 >= p.nb ? 0 : (p.nb - wb0 < 64 ? (int)(p.nb - wb0) : 64);
-  wave_load_rows_u<W2, LS, 64>(J + wb0 * W2, slab, live);
+  if constexpr (PERM)
+    wave_gather_rows_u<W2, LS, 64>(J, i < p.nb ? cm_perm[i] : 0u, slab, live);
+  else
+    wave_load_rows_u<W2, LS, 64>(J + wb0 * W2, slab, live);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   double jf[2][F], jp[2][3];
@@ -2842,10 +2877,18 @@ __global__ __launch_bounds__(kBlock) void schur_z_kernel(DevProblem p, const dou
   }
   double L[6] = {0, 0, 0, 0, 0, 0};
   if (i < p.nb) {
-    const uint32_t pt = p.obs_pt[i];
-    if (p.pt_var[pt]) {
+    if constexpr (PERM) {
+      const uint32_t pt = cm_ptv[i];
+      if (pt != 0xffffffffu) {
 #pragma unroll
-      for (int m = 0; m < 6; ++m) L[m] = Linv[6 * (size_t)pt + m];
+        for (int m = 0; m < 6; ++m) L[m] = Linv[6 * (size_t)pt + m];
+      }
+    } else {
+      const uint32_t pt = p.obs_pt[i];
+      if (p.pt_var[pt]) {
+#pragma unroll
+        for (int m = 0; m < 6; ++m) L[m] = Linv[6 * (size_t)pt + m];
+      }
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -2920,7 +2963,7 @@ __device__ __forceinline__ void pair_tile_store(const DevProblem& p, const DevPa
 // (image-block-ordered tiles: every XCD sweeps the same image block at once).
 // NTB: second-image (b-side) rows loaded nontemporal, so the streaming b-side
 // does not evict the first image's rows an XCD keeps in its L2 (variant 5).
-template <int CT, bool XMAP = true, bool NTB = false>
+template <int CT, bool XMAP = true, bool NTB = false, bool SELF1 = false>
 __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const DevPairTile* __restrict__ tiles,
                                                               int ntiles, const uint2* __restrict__ pairs,
                                                               const double* __restrict__ Z, double* __restrict__ S,
@@ -2944,6 +2987,21 @@ __global__ __launch_bounds__(kBlock) void schur_pairs_kernel(DevProblem p, const
   const uint32_t cnt = tl.count;
   const uint2* pl = pairs + tl.start;
   uint32_t n = 0;
+  if (tl.self && SELF1) {
+    // self tile: a == b, one load per pair (a branch-free form of these
+    // loops, 8 pairs' loads issued behind one scalar load of their indices,
+    // measured the same: 5.15 ms, profiles/r6i_ab_schur_pairs_self_flat.log)
+    for (; n + 4 <= cnt; n += 4) {
+      uint32_t pa[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) pa[u] = pl[n + u].x;
+      double va[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) va[u] = on ? Z[(size_t)pa[u] * ZN + off] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va[u], va[u], acc, 0, 0, 0);
+    }
+  }
   for (; n + 4 <= cnt; n += 4) {
     uint2 pr[4];
 #pragma unroll
@@ -3967,7 +4025,7 @@ void launch_plus(const DevProblem& p, const double* df, const double* dX, const 
 }
 
 void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, const uint32_t* cm_perm,
-                        const double* J, const double* Linv, double* Z, const DevPairTile* ptiles, int nptiles,
+                        const uint32_t* cm_ptv, const double* J, const double* Linv, double* Z, const DevPairTile* ptiles, int nptiles,
                         const uint2* pairs, double* S, bool with_u, hipStream_t s, const PairFlush* pflush) {
   const PairFlush nof{nullptr, nullptr, nullptr, nullptr, 0};
   dispatch_ct(p.ct, [&](auto c) {
@@ -3996,8 +4054,18 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
       hipLaunchKernelGGL(schur_pairs_jg_kernel<CT>, dim3((nptiles + 3) / 4), dim3(kBlock), 0, s, p, ptiles, nptiles,
                          pairs, Z, S);
     } else if (nptiles > 0 && p.nb > 0) {
+#ifdef MI_BA_AB_VARIANTS
+      // Z rows in image order (zorder 1, tools build): schur_pairs 5.76 vs
+      // 5.64 ms and schur_z 1.28 vs 1.01 ms per C4 launch (the J rows
+      // gathered), profiles/r6g_ab_schur_z_image_order.md
+      if (p.svariant != 7 && p.zorder)
+        hipLaunchKernelGGL((schur_z_kernel<CT, true>), dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z,
+                           cm_perm, cm_ptv);
+      else
+#endif
       if (p.svariant != 7)
-        hipLaunchKernelGGL(schur_z_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z);
+        hipLaunchKernelGGL(schur_z_kernel<CT>, dim3(grid_for(p.nb, kBlock)), dim3(kBlock), 0, s, p, J, Linv, Z,
+                           nullptr, nullptr);
       const int G = (nptiles + 3) / 4;
       const int grid = ((G + 7) / 8) * 8;  // whole XCD stripes (extra workgroups exit)
 #ifdef MI_BA_AB_VARIANTS
@@ -4028,8 +4096,15 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
       if (p.svariant == 4) {
         // pflush: the image-block tile order's deterministic route
         const PairFlush& pf = pflush ? *pflush : nof;
-        hipLaunchKernelGGL((schur_pairs_kernel<CT, false>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs,
-                           Z, S, pf);
+        // self tiles with one Z load per pair: 5.11-5.15 vs 5.38 ms per C4
+        // launch (profiles/r6i_ab_schur_pairs_self_flat.log); the duplicate
+        // load of a self pair's row was an L2 request of its own
+        if (p.sself1)
+          hipLaunchKernelGGL((schur_pairs_kernel<CT, false, false, true>), dim3(grid), dim3(kBlock), 0, s, p, ptiles,
+                             nptiles, pairs, Z, S, pf);
+        else
+          hipLaunchKernelGGL((schur_pairs_kernel<CT, false>), dim3(grid), dim3(kBlock), 0, s, p, ptiles, nptiles, pairs,
+                             Z, S, pf);
         if (pf.pslot && pf.odest) {
           if (pf.nochunk > 0) {
             hipLaunchKernelGGL(schur_owner_chunk_kernel, dim3(pf.nochunk), dim3(64), 0, s, p, pf);

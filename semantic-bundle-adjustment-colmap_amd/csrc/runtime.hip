@@ -488,6 +488,31 @@ mi_ba_status order_block_tiles(mi_ba_context* ctx) {
   return MI_BA_OK;
 }
 
+// The pair list in camera-major positions (zorder 1: Z row k is the block
+// cm_perm[k]); pr: the block pairs (read back from the device when null).
+mi_ba_status build_pairs_pos(mi_ba_context* ctx, const std::vector<uint2>* pr) {
+  const int64_t nb = ctx->dev.nb;
+  const size_t np = ctx->pairs.n;
+  std::vector<uint2> host;
+  if (!pr) {
+    host.resize(np);
+    if (np && hipMemcpy(host.data(), ctx->pairs.ptr, np * sizeof(uint2), hipMemcpyDeviceToHost) != hipSuccess)
+      return MI_BA_ERR_HIP;
+    pr = &host;
+  }
+  std::vector<uint32_t> perm(nb), inv(nb);
+  if (nb && hipMemcpy(perm.data(), ctx->cm_perm.ptr, nb * 4, hipMemcpyDeviceToHost) != hipSuccess) return MI_BA_ERR_HIP;
+  for (int64_t k = 0; k < nb; ++k) inv[perm[k]] = (uint32_t)k;
+  std::vector<uint2> pos(np);
+  for (size_t e = 0; e < np; ++e) pos[e] = make_uint2(inv[(*pr)[e].x], inv[(*pr)[e].y]);
+  if (ctx->pairs_pos.alloc(std::max<size_t>(1, np))) return MI_BA_ERR_OUT_OF_MEMORY;
+  // kernels of an earlier solve may still read the old list
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+      (np && hipMemcpy(ctx->pairs_pos.ptr, pos.data(), np * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess))
+    return MI_BA_ERR_HIP;
+  return MI_BA_OK;
+}
+
 mi_ba_status build_pair_tiles(mi_ba_context* ctx) {
   const DevProblem& d = ctx->dev;
   const int I = d.num_images;
@@ -566,6 +591,12 @@ mi_ba_status build_pair_tiles(mi_ba_context* ctx) {
   ctx->ptiles_host = std::move(tl);
   mi_ba_status st = order_block_tiles(ctx);
   if (st != MI_BA_OK) return st;
+  if (d.zorder) {
+    st = build_pairs_pos(ctx, &pr);
+    if (st != MI_BA_OK) return st;
+  } else {
+    ctx->pairs_pos.release();
+  }
   // stream-ordered: a null-stream memset is not ordered against the context's
   // non-blocking stream (the LM's kernels could overtake it)
   if (d.num_points && hipMemsetAsync(ctx->Linv.ptr, 0, 6 * (size_t)d.num_points * 8, ctx->stream)) return MI_BA_ERR_HIP;
@@ -840,6 +871,8 @@ mi_ba_status context_recycle(mi_ba_context* old, const mi_ba_options* o, const m
   // at C4 (profiles/r3_ab_schur_order.jsonl)
   d.svariant = 4;
   d.fvariant = 0;
+  d.zorder = 0;
+  d.sself1 = 1;
   d.refine_mask = (o->refine_focal_length ? 1 : 0) | (o->refine_principal_point ? 2 : 0) |
                   (o->refine_extra_params ? 4 : 0);
   d.obs_xy = ctx->obs_xy.ptr;
@@ -1376,12 +1409,17 @@ void launch_schur_terms(mi_ba_context* ctx) {
                      ctx->popart.ptr,
                      ctx->npodest,
                      ctx->npochunk};
-  launch_dense_schur(d, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->J.ptr, ctx->Linv.ptr, ctx->Z.ptr,
+  // image-ordered Z rows (zorder 1) with the Z-row pair kernels only; the JG
+  // record / pair-from-J variants index blocks
+  DevProblem dz = d;
+  dz.zorder = d.zorder && d.svariant <= 5 && ctx->pairs_pos.ptr ? 1 : 0;
+  launch_dense_schur(dz, ctx->tiles.ptr, ctx->ntiles, ctx->cm_perm.ptr, ctx->cm_ptv.ptr, ctx->J.ptr, ctx->Linv.ptr,
+                     ctx->Z.ptr,
                      d.svariant == 5 ? ctx->ptiles_xcd.ptr
                      : (d.svariant == 4 || d.svariant >= 6) ? ctx->ptiles_blk.ptr
                                                             : ctx->ptiles.ptr,
-                     d.svariant == 5 ? ctx->nptiles_xcd : ctx->nptiles, ctx->pairs.ptr, ctx->S.ptr, false,
-                     ctx->stream, ctx->det_sums && ctx->pflush_ok ? &pf : nullptr);
+                     d.svariant == 5 ? ctx->nptiles_xcd : ctx->nptiles, dz.zorder ? ctx->pairs_pos.ptr : ctx->pairs.ptr,
+                     ctx->S.ptr, false, ctx->stream, ctx->det_sums && ctx->pflush_ok ? &pf : nullptr);
   if (ctx->sem) semantic_add_dense(ctx, ctx->S.ptr);
   if (ctx->gsba) gsba_add_dense(ctx, ctx->S.ptr);
   timer_end(ctx, stop);
@@ -2430,6 +2468,22 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
       (value == 0 || value == 4 || value == 6 || ab_value(value, 0))) {
     ctx->dev.svariant = value;
     return MI_BA_OK;
+  }
+  // 1: the pair kernel's self tiles load each Z row once (a == b), 0: twice
+  if (std::strcmp(key, "schur_self_one_load") == 0 && (value == 0 || value == 1) && ab_value(value, 1)) {
+    ctx->dev.sself1 = value;
+    return MI_BA_OK;
+  }
+  // 1: the Schur factors Z in image order (camera-major positions), the pair
+  // list in positions; 0: Z in block order
+  // (tools build: slower, kernels.hip launch_dense_schur)
+  if (std::strcmp(key, "schur_z_image_order") == 0 && (value == 0 || value == 1) && ab_value(value, 0)) {
+    ctx->dev.zorder = value;
+    if (!value) {
+      ctx->pairs_pos.release();
+      return MI_BA_OK;
+    }
+    return ctx->pairs.n ? build_pairs_pos(ctx, nullptr) : MI_BA_OK;
   }
   if (std::strcmp(key, "fblock_variant") == 0 && value >= 0 && value <= 2 && ab_value(value, 0)) {
     ctx->dev.fvariant = value;

@@ -103,3 +103,38 @@ def test_shared_camera_lm_matches_oracle(gpu, ncam):
     s_g, _ = run(sc, None, mi_ba.SOLVER_DENSE_SCHUR)
     assert (s_g.num_successful_steps, s_g.num_unsuccessful_steps) == (s_o.num_successful_steps, s_o.num_unsuccessful_steps)
     assert abs(s_g.final_cost - s_o.final_cost) <= 1e-9 * s_o.final_cost
+
+
+@pytest.mark.parametrize("key,default", [("schur_z_image_order", 0), ("schur_self_one_load", 1)])
+@pytest.mark.parametrize("case", ["sem", "shared4", "const"])
+def test_schur_build_variants_bitwise(gpu, case, key, default):
+    """Two forms of the explicit Schur build that take the same products in
+    the same order drive a bitwise equal exact LM: the Schur factors Z in
+    image order (schur_z_image_order 1: row k is the block at camera-major
+    position k, the pair list in positions) or block order (0, default); the
+    pair kernel's self tiles with one Z load per pair (schur_self_one_load 1,
+    default) or two (0).  const: every fourth point held constant (zero Z
+    rows).  Tools build only (the non-default values measured slower)."""
+    if not mi_ba.ab_build():
+        pytest.skip(key + " != default: tools build (MI_BA_LIB=ab)")
+    sc = scene(seed=8)
+    if case == "shared4":
+        sc = shared(sc, 4)
+    if case == "const":
+        sc.point_config = np.where(np.arange(sc.num_points) % 4 == 0, 2, 1).astype(np.uint8)
+    sem = semantic(sc) if case == "sem" else None
+    out = []
+    for v in (default, 1 - default):
+        opts = mi_ba.default_options(max_num_iterations=6, semantic_weight=0.1)
+        b = sc.copy()
+        with mi_ba.Context(opts, b, sem) as ctx:
+            ctx.set_tuning(key, v)
+            s = ctx.solve()
+            ctx.writeback()
+        out.append((s, b))
+    (s0, a), (s1, b) = out
+    assert s0.num_successful_steps >= 2
+    assert (s1.num_successful_steps, s1.num_unsuccessful_steps) == (s0.num_successful_steps, s0.num_unsuccessful_steps)
+    assert s1.final_cost == s0.final_cost
+    for key_ in ("qvec", "tvec", "xyz", "camera_params"):
+        assert np.array_equal(getattr(a, key_), getattr(b, key_)), key_
