@@ -4098,7 +4098,9 @@ void launch_dense_schur(const DevProblem& p, const DevTile* tiles, int ntiles, c
         const PairFlush& pf = pflush ? *pflush : nof;
         // self tiles with one Z load per pair: 5.11-5.15 vs 5.38 ms per C4
         // launch (profiles/r6i_ab_schur_pairs_self_flat.log); the duplicate
-        // load of a self pair's row was an L2 request of its own
+        // load of a self pair's row was an L2 request of its own.  Z rows
+        // padded to 64-B multiples measured slower (pairs 5.26 vs 5.12 ms, Z
+        // pass 1.61 vs 0.96 ms, profiles/r6j_ab_schur_z_align.log)
         if (p.sself1)
           hipLaunchKernelGGL((schur_pairs_kernel<CT, false, false, true>), dim3(grid), dim3(kBlock), 0, s, p, ptiles,
                              nptiles, pairs, Z, S, pf);
