@@ -1868,6 +1868,7 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
 #endif
   rocblas_status st = panel_factor(h, n, A, lda, 0, ps[1], info, own_for(0), scratch_main, &ws, ex);
   if (st != rocblas_status_success) return st;
+  ws.col_rec = -1;
   // On a failure after the side stream got work, the caller's stream waits
   // for it (the caller may free A / info once its own stream is drained).
   // split head (CholConfig::split_cus): the panel factor and the trailing
@@ -1942,12 +1943,26 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       if (hipEventRecord(pan2, s2) != hipSuccess || hipStreamWaitEvent(ss, pan2, 0) != hipSuccess)
         return fail(rocblas_status_internal_error);
       if (hipEventRecord(pan, ss) != hipSuccess) return fail(rocblas_status_internal_error);
-    } else {
-      st = gemm_nt(hm, m + ex, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
+    }
+#ifdef MI_BA_AB_VARIANTS
+    const bool serial = !split && cfg.serial_head_cols > 0 && k + kb < cfg.serial_head_cols;
+#else
+    constexpr bool serial = false;
+#endif
+    // look-ahead dgemm on the side stream (CholConfig::la_side_from): after
+    // panel k there (stream order) and the previous iteration's first
+    // block-column dgemm (ev_col), which brought block column k+1 up to date
+    const bool la_side = cfg.la_side_from >= 0 && kk >= 1 && k >= cfg.la_side_from && sm == s1 && !split &&
+                         !serial && ws.ev_col.size() > (size_t)kk && ws.col_rec == kk - 1 &&
+                         jb0 <= (cfg.rest_update == 3 ? 2 * nb : nb);
+    if (!split) {
+      if (la_side && hipStreamWaitEvent(ss, ws.ev_col[kk - 1], 0) != hipSuccess)
+        return fail(rocblas_status_internal_error);
+      st = gemm_nt(la_side ? hs : hm, m + ex, jb0, kb, Aik, lda, T, lda, cfg.gemm_solution);
       if (st != rocblas_status_success) return fail(st);
     }
     auto launch_panel = [&]() -> rocblas_status {
-      if (hipEventRecord(upd, sm) != hipSuccess || hipStreamWaitEvent(ss, upd, 0) != hipSuccess)
+      if (!la_side && (hipEventRecord(upd, sm) != hipSuccess || hipStreamWaitEvent(ss, upd, 0) != hipSuccess))
         return rocblas_status_internal_error;
       rocblas_status ps_;
       if (cfg.split_panel_cols > 0 && k + kb < cfg.split_panel_cols && own_for(k + kb) == 6) {
@@ -1962,11 +1977,6 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
       if (ps_ != rocblas_status_success) return ps_;
       return hipEventRecord(pan, ss) == hipSuccess ? rocblas_status_success : rocblas_status_internal_error;
     };
-#ifdef MI_BA_AB_VARIANTS
-    const bool serial = !split && cfg.serial_head_cols > 0 && k + kb < cfg.serial_head_cols;
-#else
-    constexpr bool serial = false;
-#endif
     if (!split && !serial) {
       st = launch_panel();
       if (st != rocblas_status_success) return fail(st);
@@ -2017,6 +2027,11 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
         st = gemm_nt(r ? ws.rest_h[r - 1] : hm, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda,
                      cfg.gemm_solution);
         if (st != rocblas_status_success) return fail(st);
+        // the next panel's block column is this first dgemm's (la_side_from)
+        if (c == 0 && cfg.la_side_from >= 0 && sm == s1 && ws.ev_col.size() > (size_t)kk) {
+          if (hipEventRecord(ws.ev_col[kk], sm) != hipSuccess) return fail(rocblas_status_internal_error);
+          ws.col_rec = kk;
+        }
       }
       for (int r = 0; r + 1 < ns; ++r)
         if (hipEventRecord(evr[1 + r], ws.rest_s[r]) != hipSuccess || hipStreamWaitEvent(sm, evr[1 + r], 0) != hipSuccess)
@@ -2079,6 +2094,11 @@ bool CholWorkspace::create(int dev, int max_panels, int max_n) {
     hipEvent_t e;
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
     ev.push_back(e);
+  }
+  for (int k = 0; k < std::max(1, max_panels); ++k) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+    ev_col.push_back(e);
   }
   if (hipMalloc(&scratch, 2 * sizeof(double) * kSub * kSub) != hipSuccess) { scratch = nullptr; return false; }
   const int nblk = (std::max(0, max_n) + kTB - 1) / kTB;
@@ -2279,6 +2299,8 @@ void CholWorkspace::destroy() {
   if (rest_s[0] || rest_n != 1) (void)set_rest_streams(1);
   for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   ev.clear();
+  for (hipEvent_t e : ev_col) (void)hipEventDestroy(e);
+  ev_col.clear();
   if (side_h) (void)rocblas_destroy_handle(side_h);
   side_h = nullptr;
   if (side) (void)hipStreamDestroy(side);

@@ -65,6 +65,17 @@ struct CholConfig {
   // panel's latency stays on the critical path, the freed CUs do not make
   // the dgemm beside it faster by as much
   int split_panel_cols = 0;
+  // look-ahead dgemm on the side stream: for the panels after the first
+  // starting at column >= la_side_from, the next panel's block column is
+  // updated on the look-ahead side stream right before the panel factor
+  // there (after the previous update's first block-column dgemm, which covers
+  // that column), so panel k -> update of k+1 -> panel k+1 chain on one
+  // hardware queue without two cross-queue waits per panel, and the update
+  // of k+1 no longer queues behind the rest of the previous trailing update;
+  // -1 = off (the update on the caller's stream).  Default 0: Cholesky 14.12-
+  // 14.31 -> 13.76-13.79 ms in the C4 LM, bitwise equal (from column 2048:
+  // 13.75, from 4096: 14.06; profiles/r6l_ab_cholesky_la_side.jsonl)
+  int la_side_from = 0;
   // split tail: the below-rows launch on the second trailing-update stream
   // (rest_streams >= 2; that panel's whole trailing update then on the
   // caller's stream) instead of a fourth stream
@@ -182,6 +193,8 @@ struct CholWorkspace {
   hipStream_t side = nullptr;
   rocblas_handle side_h = nullptr;
   std::vector<hipEvent_t> ev;
+  std::vector<hipEvent_t> ev_col;  // [panel] the trailing update's first block-column dgemm done (la_side_from)
+  int col_rec = -1;                // the panel whose ev_col this factorisation recorded last
   double* scratch = nullptr;  // [2][64*64]: [0] caller's stream, [1] side stream
   double* linv = nullptr;     // [n/64][64*64] inverses of the factor's 64x64 diagonal blocks (chol_solve)
   double* ybuf = nullptr;     // [n] intermediate vector of chol_solve (L y = b)

@@ -255,19 +255,20 @@ def test_lm_tile_factor_and_publish(gpu):
         assert abs(a.final_cost - b.final_cost) <= 1e-9 * b.final_cost
 
 
-def test_lm_handoff_variants_bitwise(gpu):
+@pytest.mark.parametrize("images", [200, 1000])
+def test_lm_handoff_variants_bitwise(gpu, images):
     """The panel factor's hand-off waits (every wave acquires / one wave
     acquires for the workgroup / one wave polls and the tiles are read by sc1
     loads, with or without the next stage's tiles loaded during the current
     GEMM) and the sweeps' sc1 hand-offs (no fences) change only
     synchronisation: the same LM bit for bit (deterministic sums; nf = 1593,
-    4 panels, ragged last sweep block).  Non-default combinations: tools-only
-    A/B build."""
+    4 panels, ragged last sweep block; nf = 7993, 16 panels, at C4's panel
+    count order).  Non-default combinations: tools-only A/B build."""
     if not mi_ba.ab_build():
         pytest.skip("hand-off variants: tools build only (MI_BA_LIB=ab)")
-    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, 200, 20000, track_length=8,
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, images, 100 * images, track_length=8,
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
-    opts = mi_ba.default_options(max_num_iterations=10)
+    opts = mi_ba.default_options(max_num_iterations=10 if images <= 200 else 4)
     res = []
     for wm, sc1 in ((2, 1), (0, 0), (1, 0), (2, 0), (3, 1)):
         b = sc.copy()
@@ -302,6 +303,31 @@ def test_lm_split_panel_bitwise(gpu):
             ctx.writeback()
         res.append((s.num_successful_steps, s.num_unsuccessful_steps, s.final_cost,
                     b.qvec.tobytes(), b.tvec.tobytes(), b.xyz.tobytes(), b.camera_params.tobytes()))
+    for r in res[1:]:
+        assert r == res[0]
+
+
+@pytest.mark.parametrize("images", [40, 120, 200])
+def test_lm_look_ahead_on_side_stream_bitwise(gpu, images):
+    """The look-ahead dgemm on the panel's side stream
+    (cholesky_la_side_from 0: from the second panel on; 1024: from column
+    1024) instead of the caller's stream (-1): the same GEMMs on the same
+    operands, ordered by the side stream and the previous update's first
+    block-column event — the LM bit for bit the default's (nf = 313: one
+    panel, 953: two, 1593: four)."""
+    sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, images, 100 * images, track_length=8,
+                                                 rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
+    opts = mi_ba.default_options(max_num_iterations=10)
+    res = []
+    for frm in (-1, 0, 1024, 0):
+        b = sc.copy()
+        with mi_ba.Context(opts, b) as ctx:
+            ctx.set_tuning("cholesky_la_side_from", frm)
+            s = ctx.solve()
+            ctx.writeback()
+        res.append((s.num_successful_steps, s.num_unsuccessful_steps, s.final_cost,
+                    b.qvec.tobytes(), b.tvec.tobytes(), b.xyz.tobytes(), b.camera_params.tobytes()))
+    assert res[0][0] >= 2
     for r in res[1:]:
         assert r == res[0]
 
