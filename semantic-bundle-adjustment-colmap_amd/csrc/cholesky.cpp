@@ -2020,9 +2020,12 @@ rocblas_status factor_lookahead(rocblas_handle h, int n, double* A, int lda, int
         for (int r = 0; r + 1 < ns; ++r)
           if (hipStreamWaitEvent(ws.rest_s[r], evr[0], 0) != hipSuccess) return fail(rocblas_status_internal_error);
       }
+      // the first block column as wide as the panel after next
+      // (CholConfig::rest_first_panel): the one the next look-ahead waits for
+      const int fw = cfg.rest_first_panel && kk + 3 < (int)ps.size() ? ps[kk + 3] - ps[kk + 2] : cw;
       int c = 0;
-      for (int j = jb0; j < m; j += cw, ++c) {
-        const int jb = std::min(cw, m - j);
+      for (int j = jb0; j < m; j += c == 0 ? fw : cw, ++c) {
+        const int jb = std::min(c == 0 ? fw : cw, m - j);
         const int r = c % ns;
         st = gemm_nt(r ? ws.rest_h[r - 1] : hm, m - j + ex, jb, kb, Aik + j, lda, T + j + (size_t)j * lda, lda,
                      cfg.gemm_solution);

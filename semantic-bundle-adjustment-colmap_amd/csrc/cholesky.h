@@ -76,6 +76,12 @@ struct CholConfig {
   // 14.31 -> 13.76-13.79 ms in the C4 LM, bitwise equal (from column 2048:
   // 13.75, from 4096: 14.06; profiles/r6l_ab_cholesky_la_side.jsonl)
   int la_side_from = 0;
+  // the trailing update's first block column only as wide as the panel after
+  // next (the columns the next look-ahead dgemm waits for), the others
+  // rest_update-wide; false: all rest_update-wide.  Tools build: within
+  // noise (13.67 / 13.77 vs 13.79 / 13.82 ms at C4, bitwise equal,
+  // profiles/r6o_ab_cholesky_rest_first_panel.jsonl)
+  bool rest_first_panel = false;
   // split tail: the below-rows launch on the second trailing-update stream
   // (rest_streams >= 2; that panel's whole trailing update then on the
   // caller's stream) instead of a fourth stream

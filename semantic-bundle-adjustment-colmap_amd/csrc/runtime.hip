@@ -2558,6 +2558,10 @@ mi_ba_status mi_ba_set_tuning(mi_ba_context* ctx, const char* key, int32_t value
     return MI_BA_OK;
   }
   // tools build: measured slower at every width (profiles/r6c_ab_cholesky_split_panel.jsonl)
+  if (std::strcmp(key, "cholesky_rest_first_panel") == 0 && (value == 0 || value == 1) && ab_value(value, 0)) {
+    ctx->chol.rest_first_panel = value != 0;
+    return MI_BA_OK;
+  }
   if (std::strcmp(key, "cholesky_la_side_from") == 0 && value >= -1) {
     ctx->chol.la_side_from = value;
     return MI_BA_OK;

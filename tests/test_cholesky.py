@@ -314,15 +314,20 @@ def test_lm_look_ahead_on_side_stream_bitwise(gpu, images):
     1024) instead of the caller's stream (-1): the same GEMMs on the same
     operands, ordered by the side stream and the previous update's first
     block-column event — the LM bit for bit the default's (nf = 313: one
-    panel, 953: two, 1593: four)."""
+    panel, 953: two, 1593: four).  With the trailing update's first block
+    column only one panel wide (cholesky_rest_first_panel 1) the dgemms
+    cover the same entries in other column ranges: bitwise as well (tools
+    build)."""
     sc = mi_ba.generate_scene(mi_ba.synth_config(mi_ba.SIMPLE_RADIAL, images, 100 * images, track_length=8,
                                                  rotation_range=0.05, extra=(0.05, 0, 0, 0), seed=6)).gauge()
     opts = mi_ba.default_options(max_num_iterations=10)
     res = []
-    for frm in (-1, 0, 1024, 0):
+    firsts = (0, 1) if mi_ba.ab_build() else (0,)  # rest_first_panel 1: tools build
+    for frm, first in [(f, x) for x in firsts for f in (-1, 0, 1024, 0)]:
         b = sc.copy()
         with mi_ba.Context(opts, b) as ctx:
             ctx.set_tuning("cholesky_la_side_from", frm)
+            ctx.set_tuning("cholesky_rest_first_panel", first)
             s = ctx.solve()
             ctx.writeback()
         res.append((s.num_successful_steps, s.num_unsuccessful_steps, s.final_cost,
