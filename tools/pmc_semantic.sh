@@ -4,6 +4,8 @@
 # Usage: bash tools/pmc_semantic.sh <outdir>
 OUT=${1:-gpurun_out/pmcs}
 export TMPDIR=/tmp
+# variant 6 is the product default: the product library (no A/B build needed)
+export MI_BA_LIB=product
 mkdir -p "$OUT"
 ARGS="tools/ab_semantic.py --rounds 1 --reps 2 --variants 6"
 run() { timeout -s KILL 180 rocprofv3 --kernel-include-regex 'semantic_(linearize|flat|deferred)' --pmc $2 --output-format csv -d "$OUT/$1" -o run -- python3 $ARGS > "$OUT/$1.log" 2>&1; }
