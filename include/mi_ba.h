@@ -568,6 +568,12 @@ mi_ba_status mi_ba_context_set_host_reducer(mi_ba_context* ctx, int32_t rank, in
  *   "linearize_overlap"     1 semantic kernel on a second stream beside the reprojection
  *                           kernel, 0 one stream (default)
  *   "cholesky_lookahead"    1 side-stream look-ahead (default) / 0 serial
+ *   "cholesky_la_side_from" the look-ahead's dgemm (the next panel's block column)
+ *                           on the side stream for panels starting at or after this
+ *                           column (default 0: all but the first); -1: on the
+ *                           caller's stream (bitwise equal)
+ *   "schur_self_one_load"   1 (default): the Schur pair kernel's self tiles load each
+ *                           Z row once; 0 twice (tools build; bitwise equal)
  *   "cholesky_solve"        2 sync-free triangular sweeps, one launch per direction
  *                           (default) / 1 hand-written blocked triangular sweeps /
  *                           0 recursive rocBLAS dtrsv + dgemv
