@@ -257,7 +257,9 @@ mi_ba_status allreduce(mi_ba_context* ctx, double* d, int64_t n) {
 // Phase timer events: timing only (timer_collect synchronises the stream
 // before reading them), so recorded without the system-scope fence — a
 // default event's record writes back and invalidates the caches, which the
-// next kernel then pays for (the C4 step 0.83 vs 0.78 ms with default events)
+// next kernel then pays for (C4 step with timing on / off: 0.799-0.802 /
+// 0.788-0.790 ms with default events, 0.790-0.792 / 0.787 ms with these,
+// profiles/r6z_step_timing_events.txt)
 static hipError_t timer_event(hipEvent_t* e) { return hipEventCreateWithFlags(e, hipEventDisableSystemFence); }
 
 void timer_begin(mi_ba_context* ctx, const char* name, hipEvent_t* stop_out) {
